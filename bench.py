@@ -1,0 +1,356 @@
+#!/usr/bin/env python3
+"""Benchmark of the BASELINE.json hot path on MI355X.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    (N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N)
+
+Headline (`value`): quorum-commit updates/s at BASELINE config 3 per GPU -- 1M RaftGroups x 5
+peers, 10% in joint consensus (old+new) -- weak-scaled: each rank owns the groups whose
+RaftGroupId hash maps to it (RaftId.java:119-122), 1M per GPU, no inter-GPU traffic on the
+hot path.  A step = one fused commit launch (LeaderStateImpl.updateCommit +
+RaftLogBase.updateCommitIndex for every group) over one 1M-group batch already resident in HBM.
+Steps rotate over 8 distinct batches (615 MB > the 256 MiB Infinity Cache) so every step reads
+HBM, not a cache.  Also reported in the same JSON line:
+  * crc32c: SegmentedRaftLog frame verification GB/s (config 5: 256 x 32 MiB segments of 4 KiB
+    frames = 8 GiB per GPU), its roofline and CPU baseline;
+  * pcie: host-buffer-inclusive rates for both paths;
+  * cpu_baseline: the oracle (a scalar C port of the reference's Java arithmetic) timed on this
+    host on a bounded sample, rank 0 at N = 1 only.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+METRIC = "quorum commit updates/sec @1M groups×5 peers; log CRC32C GB/s; % HBM peak"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--groups-per-gpu", type=int, default=1_000_000)
+    p.add_argument("--rotate", type=int, default=8)
+    p.add_argument("--gap", type=int, default=-1)
+    p.add_argument("--crc-segments", type=int, default=256, help="32 MiB segments per GPU (0 = skip CRC)")
+    p.add_argument("--crc-steps", type=int, default=20)
+    p.add_argument("--crc-variant", type=int, default=None)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-pcie", action="store_true")
+    p.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    return p.parse_args()
+
+
+def load_pmc(path):
+    try:
+        return json.load(open(path))
+    except Exception:
+        return {}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from ratis_amd import _lib, engine, shard, workload
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    n_gpus = world
+    dev = torch.device("cuda", local)
+    ctx = engine.Context(local)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    def max_over_ranks(x: float) -> float:
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def sum_over_ranks(x: int) -> int:
+        if world == 1:
+            return x
+        t = torch.tensor([x], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return int(t.item())
+
+    # ------------------------------------------------------------------ commit workload
+    # RaftGroupIds for the whole job (1M per GPU); this rank keeps floorMod(UUID.hashCode(), N).
+    msb, lsb = shard.random_group_ids(args.groups_per_gpu * n_gpus, seed=workload.SEED)
+    mine = shard.shard_of(msb, lsb, n_gpus) == rank
+    n_mine = int(mine.sum())
+    host = workload.commit_snapshot(n_mine, joint_frac=0.10, peers=5, seed=workload.SEED + 1000 * rank)
+    alg_bytes = sum(h.algorithmic_bytes() for h in host)      # per launch (per batch)
+    base = [workload.to_device(h, device=dev, gap_threshold=args.gap) for h in host]
+    # R rotating batches: batch r = batch 0 translated by r * 2^44 (every index column and the
+    # term start).  The commit arithmetic is translation-equivariant, so batch r's results are
+    # batch 0's + r * 2^44 (INT64_MIN stays for empty groups) -- checked after the timed loop.
+    SHIFT = 1 << 44
+    batches = []
+    for r in range(args.rotate):
+        tiers = []
+        for b in base:
+            def sh(x):
+                return x + r * SHIFT
+            t = engine.CommitTier(follower_index=sh(b.follower_index).contiguous(), self_index=sh(b.self_index),
+                                  conf=b.conf.clone(), commit_in=sh(b.commit_in), term_start=sh(b.term_start),
+                                  gap_threshold=args.gap)
+            t.alloc_outputs(mode=_lib.RH_MODE_COMMIT)
+            tiers.append(t)
+        batches.append(tiers)
+    del base
+    torch.cuda.synchronize()
+
+    stream = torch.cuda.current_stream()
+    for i in range(args.warmup):
+        engine.commit_launch(ctx, batches[i % args.rotate], stream=stream)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    barrier()
+    t0 = torch.cuda.Event(enable_timing=True)
+    t1 = torch.cuda.Event(enable_timing=True)
+    wall0 = time.perf_counter()
+    t0.record(stream)
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        engine.commit_launch(ctx, batches[i % args.rotate], stream=stream)
+        ev[i][1].record(stream)
+    t1.record(stream)
+    barrier()
+    wall = time.perf_counter() - wall0
+    elapsed_ms = max_over_ranks(t0.elapsed_time(t1))
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    kern_ms_max = max_over_ranks(kern_ms)
+    total_groups = sum_over_ranks(n_mine)
+    value = total_groups * args.steps / (elapsed_ms / 1e3)
+
+    # ---- correctness of the timed outputs: batch 0 vs the oracle, batch r by equivariance
+    from oracle import oracle as orc
+    check_ok = True
+    ref0 = []
+    for h in host:
+        ref0.append(orc.commit_soa(h.follower, h.flush, h.conf, mode=0, gap=args.gap, commit_in=h.commit,
+                                   term_start=h.term_start))
+    for r, tiers in enumerate(batches[: min(args.rotate, args.steps)]):
+        for h, t, ref in zip(host, tiers, ref0):
+            got_c = t.commit_out.cpu().numpy()
+            got_m = t.min_out.cpu().numpy()
+            want_m = np.where(ref["min"] == np.iinfo(np.int64).min, ref["min"], ref["min"] + r * SHIFT)
+            check_ok &= bool(np.array_equal(got_c, ref["commit"] + r * SHIFT) and np.array_equal(got_m, want_m))
+    advanced = 0
+    for h, t in zip(host, batches[0]):
+        advanced += int(np.unpackbits(t.advanced_bits.cpu().numpy().view(np.uint8))[: h.n].sum())
+
+    pmc = load_pmc(args.pmc_json)
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBPS, 4),
+                "traffic": pmc.get("commit_bytes_per_launch"),
+                "kernel": "commit_kernel<1,7> (fused stable F=4 + joint F=6 tiers)",
+                "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": round(kern_ms, 5)}
+
+    # ------------------------------------------------------------------ PCIe-inclusive commit
+    pcie = {}
+    if not args.no_pcie:
+        hb = []
+        for h in host:
+            hb.append({k: torch.from_numpy(np.ascontiguousarray(v)).pin_memory()
+                       for k, v in (("f", h.follower), ("s", h.flush), ("c", h.commit), ("t", h.term_start),
+                                    ("w", h.conf.view(np.int32)))})
+        outs = [torch.empty(h.n, dtype=torch.int64).pin_memory() for h in host]
+        tiers = batches[0]
+        reps = 5
+        torch.cuda.synchronize()
+        pa = torch.cuda.Event(enable_timing=True)
+        pb = torch.cuda.Event(enable_timing=True)
+        pa.record(stream)
+        for _ in range(reps):
+            for t, b in zip(tiers, hb):
+                t.follower_index.copy_(b["f"], non_blocking=True)
+                t.self_index.copy_(b["s"], non_blocking=True)
+                t.commit_in.copy_(b["c"], non_blocking=True)
+                t.term_start.copy_(b["t"], non_blocking=True)
+                t.conf.copy_(b["w"], non_blocking=True)
+            engine.commit_launch(ctx, tiers, stream=stream)
+            for t, o in zip(tiers, outs):
+                o.copy_(t.commit_out, non_blocking=True)
+        pb.record(stream)
+        torch.cuda.synchronize()
+        ms = pa.elapsed_time(pb) / reps
+        pcie["commit_updates_per_s_incl_pcie"] = round(n_mine / (ms * 1e-3), 1)
+        pcie["commit_ms_incl_pcie_full_snapshot"] = round(ms, 4)
+        pcie["note"] = "full snapshot H2D (pinned) + kernel + commit D2H per batch; delta streaming moves less"
+
+    # ------------------------------------------------------------------ CRC32C (config 5)
+    crc = {}
+    frames_verified = bytes_verified = mismatches = 0
+    if args.crc_segments > 0:
+        ss = workload.synth_segments(ctx, n_segments=args.crc_segments, seed=workload.SEED + 77 * rank,
+                                     device=dev)
+        fb = ss.batch
+        for i in range(2):
+            engine.crc32c_frames(ctx, fb, flags=_lib.RH_CRC_VERIFY, variant=args.crc_variant, stream=stream)
+        cev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.crc_steps)]
+        barrier()
+        c0 = torch.cuda.Event(enable_timing=True)
+        c1 = torch.cuda.Event(enable_timing=True)
+        c0.record(stream)
+        for i in range(args.crc_steps):
+            cev[i][0].record(stream)
+            engine.crc32c_frames(ctx, fb, flags=_lib.RH_CRC_VERIFY, variant=args.crc_variant, stream=stream)
+            cev[i][1].record(stream)
+        c1.record(stream)
+        barrier()
+        crc_ms = max_over_ranks(c0.elapsed_time(c1) / args.crc_steps)
+        crc_kern_ms = float(np.mean([a.elapsed_time(b) for a, b in cev]))
+        fb.n_bad.zero_()
+        fb.bad_bits.zero_()
+        engine.crc32c_frames(ctx, fb, flags=_lib.RH_CRC_VERIFY, variant=args.crc_variant, stream=stream)
+        torch.cuda.synchronize()
+        bad = np.nonzero(np.unpackbits(fb.bad_bits.cpu().numpy().view(np.uint8), bitorder="little")[: fb.n])[0]
+        crc_ok = bool(np.array_equal(bad, ss.corrupted))
+        frames_verified = fb.n * (args.crc_steps + 3)
+        bytes_verified = frames_verified * ss.frame_size
+        mismatches = int(bad.size)
+        # oracle spot check of 64 frames
+        idx = np.linspace(0, fb.n - 1, 64).astype(np.int64)
+        offs = fb.frame_off.cpu().numpy()
+        got = fb.crc_out.cpu().numpy().view(np.uint32)
+        for i in idx:
+            fr = fb.buf[int(offs[i]): int(offs[i]) + ss.frame_size - 4].cpu().numpy().tobytes()
+            crc_ok &= orc.crc32c(fr) == int(got[i])
+        frame_bytes = ss.frame_bytes
+        meta_bytes = fb.n * (8 + 4 + 4)   # offset + length read, crc written (bits negligible)
+        crc_alg = frame_bytes + meta_bytes
+        total_frame_bytes = sum_over_ranks(frame_bytes)
+        crc_gbps = total_frame_bytes / (crc_ms * 1e-3) / 1e9
+        crc_ach = crc_alg / (crc_kern_ms * 1e-3) / 1e9
+        crc = {"GBps": round(crc_gbps, 1), "unit": "GB/s (frame bytes, whole job)",
+               "workload": f"config5: {args.crc_segments} x 32 MiB segments/GPU, 4 KiB frames "
+                           f"({fb.n} frames/GPU, {ss.corrupted.size} corrupted)",
+               "ms_per_pass": round(crc_ms, 4), "mismatches_found": int(bad.size), "parity_ok": crc_ok,
+               "variant": args.crc_variant if args.crc_variant is not None else 0,
+               "roofline": {"bound": "hbm", "achieved": round(crc_ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                            "frac": round(crc_ach / HBM_PEAK_GBPS, 4),
+                            "traffic": pmc.get("crc_bytes_per_launch"),
+                            "kernel": "crc_frames_kernel<64,64,true>",
+                            "algorithmic_bytes_per_launch": crc_alg, "avg_launch_ms": round(crc_kern_ms, 4)}}
+        if not args.no_pcie:
+            # host image of 8 segments (256 MiB) -> H2D pinned + verify
+            nseg = min(8, args.crc_segments)
+            hsz = nseg * ss.segment_size
+            himg = fb.buf[:hsz].cpu().pin_memory()
+            nfr = nseg * ss.frames_per_segment
+            sub = engine.FrameBatch(buf=torch.empty(hsz, dtype=torch.uint8, device=dev),
+                                    frame_off=fb.frame_off[:nfr].clone(), frame_len=fb.frame_len[:nfr].clone())
+            sub.alloc_outputs()
+            hcrc = torch.empty(nfr, dtype=torch.int32).pin_memory()
+            torch.cuda.synchronize()
+            pa = torch.cuda.Event(enable_timing=True)
+            pb = torch.cuda.Event(enable_timing=True)
+            pa.record(stream)
+            for _ in range(3):
+                sub.buf.copy_(himg, non_blocking=True)
+                engine.crc32c_frames(ctx, sub, flags=_lib.RH_CRC_VERIFY, stream=stream)
+                hcrc.copy_(sub.crc_out, non_blocking=True)
+            pb.record(stream)
+            torch.cuda.synchronize()
+            ms = pa.elapsed_time(pb) / 3
+            pcie["crc32c_GBps_incl_pcie"] = round(nfr * ss.frame_size / (ms * 1e-3) / 1e9, 2)
+        del ss, fb
+        torch.cuda.empty_cache()
+
+    # ------------------------------------------------------------------ CPU baseline (rank 0, N = 1)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        h = host[0]
+        reps = 0
+        tc = time.perf_counter()
+        while time.perf_counter() - tc < 5.0:
+            orc.commit_soa(h.follower, h.flush, h.conf, mode=0, gap=args.gap, commit_in=h.commit,
+                           term_start=h.term_start)
+            reps += 1
+        cdt = time.perf_counter() - tc
+        cpu = {"value": round(h.n * reps / cdt, 1), "unit": "updates/s", "cores": 1, "kind": "port",
+               "sample": f"{reps} passes of orc_commit_soa over the {h.n}-group stable tier of the same "
+                         f"snapshot ({cdt:.1f} s, scalar C restatement of LeaderStateImpl/RaftLogBase, 1 thread)"}
+        if args.crc_segments > 0:
+            rng = np.random.default_rng(5)
+            nseg = 8
+            fps = (32 << 20) // 4096 - 1
+            sample = rng.integers(0, 256, size=nseg * (32 << 20), dtype=np.uint8)
+            offs = (np.repeat(np.arange(nseg) * (32 << 20), fps) + 8
+                    + np.tile(np.arange(fps) * 4096, nseg)).astype(np.uint64)
+            lens = np.full(offs.size, 4096, dtype=np.uint32)
+            reps = 0
+            tc = time.perf_counter()
+            while time.perf_counter() - tc < 5.0:
+                orc.crc32c_frames(sample, offs, lens)
+                reps += 1
+            cdt = time.perf_counter() - tc
+            cpu_crc = {"value": round(reps * offs.size * 4096 / cdt / 1e9, 3), "unit": "GB/s", "cores": 1,
+                       "kind": "port",
+                       "sample": f"{reps} passes over 8 x 32 MiB segment images ({offs.size} 4 KiB frames), "
+                                 "PureJavaCrc32C slicing-by-8 restatement, 1 thread"}
+            crc["cpu_baseline"] = cpu_crc
+
+    stats = shard.allreduce_stats({"groups_evaluated": n_mine * args.steps, "commits_advanced": advanced,
+                                   "frames_verified": frames_verified, "bytes_verified": bytes_verified,
+                                   "crc_mismatches": mismatches}, device=dev)
+
+    line = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "updates/s",
+        "n_gpus": n_gpus,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed_ms / args.steps, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int64",
+        "data": "synthetic",
+        "config": {"workload": "config3: 1M RaftGroups x 5 peers per GPU, 10% joint consensus (old+new conf), "
+                               "updateCommit + updateCommitIndex per group",
+                   "groups_per_gpu": args.groups_per_gpu, "groups_this_job": total_groups, "peers": 5,
+                   "joint_fraction": 0.10, "gap_threshold": args.gap, "rotating_batches": args.rotate,
+                   "sharding": f"RaftGroupId UUID.hashCode() floorMod {n_gpus}"},
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+        "crc32c": crc,
+        "pcie": pcie,
+        "parity_ok": check_ok,
+        "advanced_groups_batch0_rank0": advanced,
+        "stats": stats,
+        "wall_s_timed_region": round(wall, 4),
+    }
+    if rank == 0:
+        print(json.dumps(line))
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,230 @@
+/*
+ * ratis_hip.h -- C ABI of libratis_hip, the MI355X (gfx950) leader-bookkeeping engine for
+ * Apache Ratis (OneSizeFitsQuorum/ratis).
+ *
+ * Two hot paths of the reference are served, each as a batched HIP kernel over HBM-resident
+ * struct-of-arrays data:
+ *
+ *   1. Quorum commit -- LeaderStateImpl.updateCommit() / getMajorityMin() / MinMajorityMax and
+ *      RaftLogBase.updateCommitIndex(), including joint-consensus (old+new) confs and the
+ *      current-term check, evaluated for millions of RaftGroups per launch.
+ *   2. Log-entry CRC32C -- PureJavaCrc32C as used by SegmentedRaftLogOutputStream.write (frame
+ *      trailer) and SegmentedRaftLogReader.decodeEntry (frame verification).
+ *
+ * Reference paths cited below are relative to the ratis tree:
+ *   LSI = ratis-server/src/main/java/org/apache/ratis/server/impl/LeaderStateImpl.java
+ *   RLB = ratis-server/src/main/java/org/apache/ratis/server/raftlog/RaftLogBase.java
+ *   RCI = ratis-server/src/main/java/org/apache/ratis/server/impl/RaftConfigurationImpl.java
+ *   FII = ratis-server/src/main/java/org/apache/ratis/server/impl/FollowerInfoImpl.java
+ *   PJC = ratis-common/src/main/java/org/apache/ratis/util/PureJavaCrc32C.java
+ *   OUT = ratis-server/.../raftlog/segmented/SegmentedRaftLogOutputStream.java
+ *   RDR = ratis-server/.../raftlog/segmented/SegmentedRaftLogReader.java
+ *
+ * Conventions (all entry points):
+ *   - Plain C types only; no exception crosses the ABI.  Every int-returning function returns
+ *     RH_OK (0) or a negative RH_E_* code; rh_last_error() then holds a message for the calling
+ *     thread (the Java binding maps RH_E_INVAL to IllegalArgumentException, others to
+ *     IOException -- see INTEGRATION.md).
+ *   - "_launch" functions take DEVICE pointers, enqueue work on `stream` (a hipStream_t; NULL =
+ *     the context's own stream) and return without synchronising.
+ *   - All log indices are signed 64-bit (Java long); INVALID_LOG_INDEX = -1 is a legal value.
+ */
+#ifndef RATIS_HIP_H
+#define RATIS_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RH_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------------------- */
+#define RH_OK        0
+#define RH_E_INVAL  -1  /* bad argument (null pointer, size out of range, ...)               */
+#define RH_E_RANGE  -2  /* value outside what the engine supports (e.g. > 14 follower slots) */
+#define RH_E_DEVICE -3  /* HIP runtime failure (message carries hipGetErrorString)           */
+#define RH_E_NOMEM  -4  /* device or pinned host allocation failed                          */
+#define RH_E_STATE  -5  /* object used after destroy / on the wrong device                   */
+
+typedef struct rh_ctx rh_ctx;       /* one per (process, GPU): device, stream, constant tables */
+typedef struct rh_groups rh_groups; /* a resident table of leader divisions on one GPU       */
+
+int rh_abi_version(void);
+/* Message describing the last failure on the calling thread ("" if none). */
+const char* rh_last_error(void);
+/* Number of visible GPUs. */
+int rh_device_count(int* out);
+/* Binds device `device`, creates the context stream and uploads the CRC tables. */
+int rh_init(int device, rh_ctx** out);
+int rh_shutdown(rh_ctx* ctx);
+/* Waits for all work enqueued on the context stream. */
+int rh_synchronize(rh_ctx* ctx);
+/* The context's hipStream_t, for callers that order their own work against it. */
+void* rh_ctx_stream(rh_ctx* ctx);
+
+/* ===================================================================================== */
+/* 1. Quorum commit                                                                      */
+/* ===================================================================================== */
+
+/* Per-group membership word (one uint32 per group), host-built from RaftConfigurationImpl on
+ * every conf or leadership change (RCI:142-195, PeerConfiguration.java:96-128):
+ *   bits  0..13  follower slot k is a voter of conf (new/current) AND has a FollowerInfo
+ *                (LSI:274-293 getFollowerInfos: peers.streamPeerIds().map(map::get).filter(nonNull))
+ *   bit   14     includeSelf          = conf.containsInConf(selfId)          (LSI:963)
+ *   bit   15     transitional         = conf.isTransitional() (oldConf != null, RCI:142-144)
+ *   bits 16..29  follower slot k is a voter of oldConf with a FollowerInfo
+ *   bit   30     includeSelfInOldConf = conf.containsInOldConf(selfId)       (LSI:975)
+ *   bit   31     active: this division is LEADER and should be evaluated (inactive => no result)
+ * Listeners are never voters (PeerConfiguration keeps them in a separate map). */
+#define RH_MAX_FOLLOWERS    14u
+#define RH_CONF_SELF        (1u << 14)
+#define RH_CONF_TRANSITIONAL (1u << 15)
+#define RH_CONF_OLD_SHIFT   16u
+#define RH_CONF_SELF_OLD    (1u << 30)
+#define RH_CONF_ACTIVE      (1u << 31)
+
+static inline uint32_t rh_conf_pack(uint32_t new_mask, int include_self, int transitional,
+                                    uint32_t old_mask, int include_self_old, int active) {
+    return (new_mask & 0x3FFFu) | (include_self ? RH_CONF_SELF : 0u) |
+           (transitional ? RH_CONF_TRANSITIONAL : 0u) | ((old_mask & 0x3FFFu) << RH_CONF_OLD_SHIFT) |
+           (include_self_old ? RH_CONF_SELF_OLD : 0u) | (active ? RH_CONF_ACTIVE : 0u);
+}
+
+/* Which reference computation a launch performs. */
+#define RH_MODE_COMMIT 0 /* LSI:946-950 updateCommit(): getMajorityMin(matchIndex, flushIndex, gap)
+                            -> LSI:1015-1026 updateCommit(majority, min) -> RLB:121-142        */
+#define RH_MODE_WATCH  1 /* LSI:612-622 commitIndexChanged(): getMajorityMin(commitIndex,
+                            lastCommittedIndex) with gap -1 -> {min, majority, max} levels     */
+
+/* One struct-of-arrays table ("tier") of G groups with F follower slots each.  All pointers are
+ * device pointers.  Groups whose voter union needs more slots live in a wider tier; a launch
+ * takes up to RH_MAX_TIERS tiers and runs them in one kernel.  Per group, reads
+ * 8*(F+1) + 8 + 8 + 4 bytes and writes 16 bytes (COMMIT) -- the "8P+36 B" of SURVEY 8(d). */
+typedef struct rh_commit_soa {
+    uint64_t n;                    /* groups in this tier                                       */
+    uint32_t n_followers;          /* F, 1..RH_MAX_FOLLOWERS                                    */
+    int32_t  mode;                 /* RH_MODE_COMMIT or RH_MODE_WATCH                           */
+    int64_t  gap_threshold;        /* followerMaxGapThreshold (LSI:390-401), -1 = off; COMMIT only */
+    const int64_t* follower_index; /* [F][col_stride], column k = follower slot k:
+                                      FollowerInfo.getMatchIndex (COMMIT) or getCommitIndex
+                                      (WATCH) -- FII:87-105                                     */
+    uint64_t col_stride;           /* elements between follower columns; 0 means n             */
+    const int64_t* self_index;     /* [n] COMMIT: raftLog.getFlushIndex(); WATCH: getLastCommittedIndex() */
+    const int64_t* commit_in;      /* [n] raftLog.getLastCommittedIndex()  (COMMIT only)          */
+    const int64_t* term_start;     /* [n] first log index of the leader's current term (the
+                                      StartupLogEntry index, LSI:296-301); termAt(i)==currentTerm
+                                      <=> i >= term_start for i <= flushIndex (COMMIT only)       */
+    const uint32_t* conf;          /* [n] membership words (above)                               */
+    int64_t* commit_out;           /* [n] new commit index (COMMIT); may alias commit_in          */
+    int64_t* min_out;              /* [n] optional: min (watch ALL / ALL_COMMITTED level)         */
+    int64_t* maj_out;              /* [n] optional: majority (MAJORITY_COMMITTED level)           */
+    int64_t* max_out;              /* [n] optional: max (MAJORITY level)                          */
+    uint64_t* valid_bits;          /* [ceil(n/64)] optional: bit g = getMajorityMin was present  */
+    uint64_t* advanced_bits;       /* [ceil(n/64)] optional: bit g = updateCommitIndex stored     */
+    /* optional compacted list of advanced groups (COMMIT): entries appended in unspecified
+     * order; *adv_count must be zeroed by the caller (rh_groups does it). */
+    uint64_t* adv_rows;            /* [cap] row index within this tier                          */
+    int64_t*  adv_commit;          /* [cap] new commit index                                    */
+    unsigned long long* adv_count; /* single counter, shared by all tiers of a launch OK        */
+    uint64_t adv_cap;
+    uint64_t adv_row_base;         /* added to each row written to adv_rows (tier slot offset)   */
+} rh_commit_soa;
+
+#define RH_MAX_TIERS 4
+
+/* Evaluates every group of every tier (one kernel launch).  Invalid groups (inactive or
+ * Optional.empty()) keep commit_out = commit_in and get INT64_MIN in min/maj/max_out. */
+int rh_commit_soa_launch(rh_ctx* ctx, const rh_commit_soa* tiers, int n_tiers, void* stream);
+
+/* ---- resident group table (the object the Java ratis-hip module holds) ------------------ */
+
+/* Column ids for deltas (FollowerInfo / RaftLog producers of the indices). */
+#define RH_COL_MATCH(k)   ((uint32_t)(k))        /* follower k matchIndex: updateToMax (FII:93-95)  */
+#define RH_COL_FCOMMIT(k) (16u + (uint32_t)(k))  /* follower k commitIndex: updateToMax (FII:103-105)*/
+#define RH_COL_FLUSH      32u                    /* leader flushIndex: increasing                   */
+#define RH_COL_COMMITTED  33u                    /* leader commitIndex raised outside the kernel
+                                                    (RLB:155-166 updateSnapshotIndex): to-max       */
+typedef struct rh_delta {
+    uint64_t slot;    /* group slot in the table                                             */
+    uint32_t column;  /* RH_COL_*                                                            */
+    uint32_t reserved;
+    int64_t  value;
+} rh_delta;
+
+/* Creates a table of `capacity` group slots with `n_followers` follower slots each; all slots
+ * start inactive with every index = -1. */
+int rh_groups_create(rh_ctx* ctx, uint64_t capacity, uint32_t n_followers, int64_t gap_threshold,
+                     rh_groups** out);
+int rh_groups_destroy(rh_groups* g);
+/* Sets the conf word and the leader-side indices of one slot (conf change / leader start). */
+int rh_group_set(rh_groups* g, uint64_t slot, uint32_t conf, int64_t flush_index,
+                 int64_t commit_index, int64_t term_start);
+/* Bulk host->device load of rows [first, first+n).  Host arrays are column-major like the
+ * device SoA: match/fcommit are [F][n].  Any pointer may be NULL to leave that column. */
+int rh_groups_load(rh_groups* g, uint64_t first, uint64_t n, const int64_t* match,
+                   const int64_t* fcommit, const int64_t* flush, const int64_t* commit,
+                   const int64_t* term_start, const uint32_t* conf);
+/* Copies deltas through a pinned staging ring and applies them on the device (monotone max,
+ * exactly RaftLogIndex.updateToMax).  Thread-safe. */
+int rh_push_deltas(rh_groups* g, const rh_delta* deltas, size_t n);
+/* RH_MODE_COMMIT: runs updateCommit for every active group, stores advanced commit indices in
+ * the table, and returns (slot, new commit) of the groups that advanced, up to `cap`.
+ * out_min (optional, host [capacity]) receives the watch-ALL level of every group.
+ * Blocks until results are in the caller's buffers. */
+int rh_commit_batch(rh_groups* g, uint64_t* out_slots, int64_t* out_commit, size_t cap, size_t* out_n,
+                    int64_t* out_min);
+/* RH_MODE_WATCH over the follower commitIndex column: dense host outputs [capacity] (any may be
+ * NULL) plus valid bits [ceil(capacity/64)]. */
+int rh_watch_levels(rh_groups* g, int64_t* out_min, int64_t* out_maj, int64_t* out_max,
+                    uint64_t* out_valid_bits);
+/* Reads back the resident commit index column (debug / checkpoint). */
+int rh_groups_read_commit(rh_groups* g, uint64_t first, uint64_t n, int64_t* out);
+
+/* ===================================================================================== */
+/* 2. CRC32C (PureJavaCrc32C) over SegmentedRaftLog frames                               */
+/* ===================================================================================== */
+
+/* Frame = varint32(n) || LogEntryProto (n bytes) || big-endian u32 CRC32C(varint||proto)
+ * (OUT:86-110).  Flags: */
+#define RH_CRC_VERIFY 1u /* compare with the stored trailer, set bad bit on mismatch (RDR:327-336) */
+#define RH_CRC_STAMP  2u /* write the computed CRC into the trailer, big-endian (OUT:100-107)      */
+/* With neither flag, frame_len is a plain span length and only crc_out is produced. */
+
+typedef struct rh_frames {
+    uint8_t* buf;                 /* device pointer to segment bytes (read-only unless STAMP)   */
+    uint64_t buf_len;
+    const uint64_t* frame_off;    /* [n] offset of each frame's first varint byte               */
+    const uint32_t* frame_len;    /* [n] whole frame length = varint + proto + 4 (VERIFY/STAMP) */
+    uint64_t n;
+    uint32_t init_state;          /* PureJavaCrc32C state before update(): 0xFFFFFFFF = reset() */
+    uint32_t reserved;
+    uint32_t* crc_out;            /* [n] optional: getValue() after update(frame bytes)          */
+    uint64_t* bad_bits;           /* [ceil(n/64)] optional (VERIFY): stored != computed         */
+    unsigned long long* n_bad;    /* optional (VERIFY): mismatches are atomically added here    */
+} rh_frames;
+
+/* CRC of every frame (one launch).  Frames must lie inside [0, buf_len); lengths <= 2^31.
+ * Spans shorter than 4 bytes are supported. */
+int rh_crc32c_frames_launch(rh_ctx* ctx, const rh_frames* frames, uint32_t flags, void* stream);
+
+/* Host-buffer convenience (PCIe-inclusive): copies the segment image and frame table to the
+ * device, verifies every frame, copies results back.  Returns RH_OK; *n_bad = mismatches. */
+int rh_crc32c_verify_host(rh_ctx* ctx, const uint8_t* seg, uint64_t seg_len, const uint64_t* frame_off,
+                          const uint32_t* frame_len, uint64_t n, uint32_t* crc_out, uint64_t* bad_bits,
+                          uint64_t* n_bad);
+
+/* ---- tuning hooks (bench / A-B experiments; results are identical for every variant) ---- */
+/* CRC kernel variants: 0 = 64 lanes x 64 B per 4 KiB window (default), 1 = 16 x 256 B,
+ * 2 = 8 x 512 B, 3 = variant 0 with shared (non-replicated, bank-conflicting) tables. */
+int rh_crc32c_num_variants(void);
+int rh_crc32c_set_variant(int variant);
+int rh_crc32c_frames_launch_variant(rh_ctx* ctx, const rh_frames* frames, uint32_t flags, int variant,
+                                    void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RATIS_HIP_H */

@@ -1,0 +1,177 @@
+"""ctypes binding of libratis_hip.so (include/ratis_hip.h).
+
+The product path is the HIP library: if ``ratis_amd/lib/libratis_hip.so`` is missing this module
+raises on import of any compute entry point -- there is no CPU fallback anywhere in
+``ratis_amd``.  Structures below mirror the C structs field by field (checked against the
+header by ``tests/test_abi.py``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_int, c_int32, c_int64, c_size_t, c_uint32, c_uint64, c_void_p
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libratis_hip.so")
+
+RH_OK = 0
+RH_E_INVAL = -1
+RH_E_RANGE = -2
+RH_E_DEVICE = -3
+RH_E_NOMEM = -4
+RH_E_STATE = -5
+
+RH_MAX_FOLLOWERS = 14
+RH_CONF_SELF = 1 << 14
+RH_CONF_TRANSITIONAL = 1 << 15
+RH_CONF_OLD_SHIFT = 16
+RH_CONF_SELF_OLD = 1 << 30
+RH_CONF_ACTIVE = 1 << 31
+RH_MODE_COMMIT = 0
+RH_MODE_WATCH = 1
+RH_MAX_TIERS = 4
+
+RH_COL_FLUSH = 32
+RH_COL_COMMITTED = 33
+
+RH_CRC_VERIFY = 1
+RH_CRC_STAMP = 2
+
+
+def rh_col_match(k: int) -> int:
+    return k
+
+
+def rh_col_fcommit(k: int) -> int:
+    return 16 + k
+
+
+def conf_pack(new_mask: int, include_self: bool, transitional: bool, old_mask: int,
+              include_self_old: bool, active: bool = True) -> int:
+    """Python twin of ``rh_conf_pack`` (ratis_hip.h)."""
+    return ((new_mask & 0x3FFF) | (RH_CONF_SELF if include_self else 0)
+            | (RH_CONF_TRANSITIONAL if transitional else 0)
+            | ((old_mask & 0x3FFF) << RH_CONF_OLD_SHIFT)
+            | (RH_CONF_SELF_OLD if include_self_old else 0)
+            | (RH_CONF_ACTIVE if active else 0))
+
+
+class RhCommitSoa(ctypes.Structure):
+    _fields_ = [
+        ("n", c_uint64),
+        ("n_followers", c_uint32),
+        ("mode", c_int32),
+        ("gap_threshold", c_int64),
+        ("follower_index", c_void_p),
+        ("col_stride", c_uint64),
+        ("self_index", c_void_p),
+        ("commit_in", c_void_p),
+        ("term_start", c_void_p),
+        ("conf", c_void_p),
+        ("commit_out", c_void_p),
+        ("min_out", c_void_p),
+        ("maj_out", c_void_p),
+        ("max_out", c_void_p),
+        ("valid_bits", c_void_p),
+        ("advanced_bits", c_void_p),
+        ("adv_rows", c_void_p),
+        ("adv_commit", c_void_p),
+        ("adv_count", c_void_p),
+        ("adv_cap", c_uint64),
+        ("adv_row_base", c_uint64),
+    ]
+
+
+class RhDelta(ctypes.Structure):
+    _fields_ = [("slot", c_uint64), ("column", c_uint32), ("reserved", c_uint32), ("value", c_int64)]
+
+
+class RhFrames(ctypes.Structure):
+    _fields_ = [
+        ("buf", c_void_p),
+        ("buf_len", c_uint64),
+        ("frame_off", c_void_p),
+        ("frame_len", c_void_p),
+        ("n", c_uint64),
+        ("init_state", c_uint32),
+        ("reserved", c_uint32),
+        ("crc_out", c_void_p),
+        ("bad_bits", c_void_p),
+        ("n_bad", c_void_p),
+    ]
+
+
+# name -> (restype, argtypes); every function declared in include/ratis_hip.h
+_SIGNATURES = {
+    "rh_abi_version": (c_int, []),
+    "rh_last_error": (c_char_p, []),
+    "rh_device_count": (c_int, [POINTER(c_int)]),
+    "rh_init": (c_int, [c_int, POINTER(c_void_p)]),
+    "rh_shutdown": (c_int, [c_void_p]),
+    "rh_synchronize": (c_int, [c_void_p]),
+    "rh_ctx_stream": (c_void_p, [c_void_p]),
+    "rh_commit_soa_launch": (c_int, [c_void_p, POINTER(RhCommitSoa), c_int, c_void_p]),
+    "rh_groups_create": (c_int, [c_void_p, c_uint64, c_uint32, c_int64, POINTER(c_void_p)]),
+    "rh_groups_destroy": (c_int, [c_void_p]),
+    "rh_group_set": (c_int, [c_void_p, c_uint64, c_uint32, c_int64, c_int64, c_int64]),
+    "rh_groups_load": (c_int, [c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p,
+                               c_void_p, c_void_p]),
+    "rh_push_deltas": (c_int, [c_void_p, POINTER(RhDelta), c_size_t]),
+    "rh_commit_batch": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, POINTER(c_size_t), c_void_p]),
+    "rh_watch_levels": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "rh_groups_read_commit": (c_int, [c_void_p, c_uint64, c_uint64, c_void_p]),
+    "rh_crc32c_frames_launch": (c_int, [c_void_p, POINTER(RhFrames), c_uint32, c_void_p]),
+    "rh_crc32c_verify_host": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_uint64, c_void_p,
+                                      c_void_p, POINTER(c_uint64)]),
+    "rh_crc32c_num_variants": (c_int, []),
+    "rh_crc32c_set_variant": (c_int, [c_int]),
+    "rh_crc32c_frames_launch_variant": (c_int, [c_void_p, POINTER(RhFrames), c_uint32, c_int, c_void_p]),
+}
+
+
+class RatisHipError(RuntimeError):
+    """A libratis_hip call returned a negative RH_E_* status."""
+
+    def __init__(self, code: int, message: str):
+        super().__init__(f"[{code}] {message}")
+        self.code = code
+
+
+class IllegalArgumentError(RatisHipError, ValueError):
+    """RH_E_INVAL / RH_E_RANGE: the Java binding maps these to IllegalArgumentException."""
+
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Loads libratis_hip.so (once).  Raises if the native library has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"libratis_hip.so not found at {LIB_PATH}: build it with "
+            "`python -c 'import __graft_entry__ as g; g.build()'` (or make -C ratis_amd/csrc). "
+            "ratis_amd has no CPU fallback.")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in _SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int) -> int:
+    if rc >= 0:
+        return rc
+    msg = load().rh_last_error()
+    msg = msg.decode() if msg else ""
+    if rc in (RH_E_INVAL, RH_E_RANGE):
+        raise IllegalArgumentError(rc, msg)
+    raise RatisHipError(rc, msg)
+
+
+def exported_symbols() -> list[str]:
+    return sorted(_SIGNATURES)

@@ -1,0 +1,428 @@
+// Batched quorum commit for gfx950 (MI355X).
+//
+// Restates, per RaftGroup, the leader's commit decision of the reference:
+//   LeaderStateImpl.getMajorityMin        LeaderStateImpl.java:956-984
+//   LeaderStateImpl.getSorted             LeaderStateImpl.java:1076-1095
+//   MinMajorityMax.valueOf / combine      LeaderStateImpl.java:904-944
+//   LeaderStateImpl.updateCommit(maj,min) LeaderStateImpl.java:1015-1026
+//   RaftLogBase.updateCommitIndex         RaftLogBase.java:121-142
+// and, in WATCH mode, LeaderStateImpl.commitIndexChanged (LeaderStateImpl.java:612-622).
+//
+// Layout: one struct-of-arrays "tier" per follower-slot count F.  Every column is a contiguous
+// int64 array over the tier's groups, so a wave's loads of one column are one coalesced
+// 1 KiB request (2 groups per lane, 16 B per lane).  The k-th order statistic over <= F+1
+// voters is a Batcher merge-exchange network in registers with non-voters padded to
+// INT64_MAX -- integer compare/select work, no MFMA (this is not a contraction).  The kernel
+// is HBM-bound: 8(F+1)+20 bytes read and 16 bytes written per group.
+#include "rh_internal.h"
+
+#include <climits>
+
+namespace {
+
+constexpr int kBlock = 256;            // 4 waves
+constexpr int kGroupsPerLane = 2;      // 16-byte loads per column per lane
+constexpr int kTile = kBlock * kGroupsPerLane;  // groups per workgroup
+
+// ---- Batcher merge-exchange sorting network (Knuth, TAOCP 5.2.2, Algorithm M) ------------
+struct Net {
+    int n = 0;
+    int a[128] = {};
+    int b[128] = {};
+};
+
+constexpr Net make_net(int N) {
+    Net net{};
+    if (N < 2) return net;
+    int t = 0;
+    while ((1 << t) < N) ++t;
+    int p = 1 << (t - 1);
+    while (p > 0) {
+        int q = 1 << (t - 1), r = 0, d = p;
+        while (true) {
+            for (int i = 0; i < N - d; ++i)
+                if ((i & p) == r) {
+                    net.a[net.n] = i;
+                    net.b[net.n] = i + d;
+                    ++net.n;
+                }
+            if (q == p) break;
+            d = q - p;
+            q >>= 1;
+            r = p;
+        }
+        p >>= 1;
+    }
+    return net;
+}
+
+template <int N>
+constexpr Net kNet = make_net(N);
+
+template <int N, int I = 0>
+__device__ __forceinline__ void sort_net(int64_t (&v)[N]) {
+    if constexpr (I < kNet<N>.n) {
+        constexpr int a = kNet<N>.a[I];
+        constexpr int b = kNet<N>.b[I];
+        const int64_t x = v[a], y = v[b];
+        const bool lt = x < y;
+        v[a] = lt ? x : y;
+        v[b] = lt ? y : x;
+        sort_net<N, I + 1>(v);
+    }
+}
+
+// Order statistics of the voters selected by `member` (bit i = slot i, bit N-1 = self):
+// getSorted (LSI:1076-1095) + MinMajorityMax.valueOf(sorted, gap) (LSI:926-943).
+// Non-members sort to the end as INT64_MAX; k < n so they are never selected.
+template <int N>
+__device__ __forceinline__ void order_stats(const int64_t (&vals)[N], uint32_t member, int64_t gap,
+                                            int64_t& mn, int64_t& mj, int64_t& mx) {
+    int64_t s[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) s[i] = ((member >> i) & 1u) ? vals[i] : INT64_MAX;
+    sort_net<N>(s);
+    const int n = __builtin_popcount(member);
+    const int k = (n - 1) >> 1;  // getMajority: sorted[(length - 1) / 2]
+    mn = s[0];
+    mj = s[0];
+    mx = s[0];
+#pragma unroll
+    for (int j = 1; j < N; ++j) {
+        mj = (j == k) ? s[j] : mj;
+        mx = (j == n - 1) ? s[j] : mx;
+    }
+    // gapThreshold clamp; Java long subtraction wraps (LSI:929-933).
+    if (gap != -1 && (int64_t)((uint64_t)mj - (uint64_t)mn) > gap) mj = mn;
+}
+
+struct TierArgs {
+    rh_commit_soa t;
+    uint64_t stride;        // elements between follower columns
+    uint32_t block_begin;   // first block of this tier in the launch
+    uint32_t n_blocks;
+    bool vec_ok;            // every column 16-byte aligned: full tiles use 16-byte loads
+};
+
+struct LaunchArgs {
+    TierArgs tier[RH_MAX_TIERS];
+    int n_tiers;
+};
+
+__device__ __forceinline__ uint64_t spread32(uint64_t x) {
+    x &= 0xFFFFFFFFull;
+    x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
+    x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
+    x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
+    x = (x | (x << 2)) & 0x3333333333333333ull;
+    x = (x | (x << 1)) & 0x5555555555555555ull;
+    return x;
+}
+
+typedef int64_t v2i64 __attribute__((ext_vector_type(2)));
+typedef uint32_t v2u32 __attribute__((ext_vector_type(2)));
+
+// One workgroup tile of one tier.  Lane l of wave w handles rows base + 2l and base + 2l + 1
+// with base = tile*kTile + 128*w, so the wave's valid/advanced bits form two whole words.
+template <int F, bool VEC>
+__device__ __forceinline__ void commit_tile(const TierArgs& ta, uint64_t tile) {
+    constexpr int N = F + 1;
+    const rh_commit_soa& t = ta.t;
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const uint64_t wbase = tile * kTile + (uint64_t)wave * 128;
+    const uint64_t r0 = wbase + 2 * (uint64_t)lane;
+    const bool commit_mode = t.mode == RH_MODE_COMMIT;
+
+    // ---- loads (all issued before any compute) ----
+    int64_t fv[2][F];
+    int64_t self[2], cin[2], tstart[2];
+    uint32_t w[2];
+    if (VEC) {
+#pragma unroll
+        for (int k = 0; k < F; ++k) {
+            const v2i64 x = *reinterpret_cast<const v2i64*>(t.follower_index + (uint64_t)k * ta.stride + r0);
+            fv[0][k] = x.x;
+            fv[1][k] = x.y;
+        }
+        const v2i64 s = *reinterpret_cast<const v2i64*>(t.self_index + r0);
+        self[0] = s.x;
+        self[1] = s.y;
+        const v2u32 c = *reinterpret_cast<const v2u32*>(t.conf + r0);
+        w[0] = c.x;
+        w[1] = c.y;
+        if (commit_mode) {
+            const v2i64 ci = *reinterpret_cast<const v2i64*>(t.commit_in + r0);
+            const v2i64 ts = *reinterpret_cast<const v2i64*>(t.term_start + r0);
+            cin[0] = ci.x;
+            cin[1] = ci.y;
+            tstart[0] = ts.x;
+            tstart[1] = ts.y;
+        } else {
+            cin[0] = cin[1] = tstart[0] = tstart[1] = 0;
+        }
+    } else {
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            const uint64_t r = r0 + g;
+            const bool in = r < t.n;
+#pragma unroll
+            for (int k = 0; k < F; ++k) fv[g][k] = in ? t.follower_index[(uint64_t)k * ta.stride + r] : 0;
+            self[g] = in ? t.self_index[r] : 0;
+            w[g] = in ? t.conf[r] : 0u;  // inactive padding
+            cin[g] = (in && commit_mode) ? t.commit_in[r] : 0;
+            tstart[g] = (in && commit_mode) ? t.term_start[r] : 0;
+        }
+    }
+
+    // ---- getMajorityMin (LSI:956-984) ----
+    const int64_t gap = commit_mode ? t.gap_threshold : -1;  // 2-arg overload passes -1 (LSI:952-954)
+    bool valid[2], adv[2];
+    int64_t mn[2], mj[2], mx[2], cout[2];
+    const uint32_t fmask = (1u << F) - 1u;
+    bool trans[2];
+#pragma unroll
+    for (int g = 0; g < 2; ++g) trans[g] = (w[g] & RH_CONF_ACTIVE) && (w[g] & RH_CONF_TRANSITIONAL);
+    const bool any_trans = __any(trans[0] || trans[1]);
+
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+        int64_t vals[N];
+#pragma unroll
+        for (int k = 0; k < F; ++k) vals[k] = fv[g][k];
+        vals[F] = self[g];
+        const uint32_t mnew = (w[g] & fmask) | (((w[g] >> 14) & 1u) << F);
+        const uint32_t mold = ((w[g] >> RH_CONF_OLD_SHIFT) & fmask) | (((w[g] >> 30) & 1u) << F);
+        // followers.isEmpty() && !includeSelf -> Optional.empty()  (LSI:964-966, 976-978)
+        bool v = (w[g] & RH_CONF_ACTIVE) && mnew != 0 && (!trans[g] || mold != 0);
+        int64_t a0, a1, a2;
+        order_stats<N>(vals, mnew ? mnew : 1u, gap, a0, a1, a2);
+        if (any_trans) {
+            if (trans[g]) {  // combine(): element-wise min (LSI:915-920)
+                int64_t b0, b1, b2;
+                order_stats<N>(vals, mold ? mold : 1u, gap, b0, b1, b2);
+                a0 = b0 < a0 ? b0 : a0;
+                a1 = b1 < a1 ? b1 : a1;
+                a2 = b2 < a2 ? b2 : a2;
+            }
+        }
+        valid[g] = v;
+        mn[g] = v ? a0 : INT64_MIN;
+        mj[g] = v ? a1 : INT64_MIN;
+        mx[g] = v ? a2 : INT64_MIN;
+        // ---- updateCommit(majority, min) (LSI:1015-1026) -> RaftLogBase.updateCommitIndex ----
+        // old = lastCommitted; if (majority > old) { newCommit = min(majority, flushIndex);
+        //   if (old < newCommit && termAt(newCommit) == currentTerm) commit = newCommit; }
+        const int64_t old = cin[g];
+        const int64_t flush = self[g];
+        const int64_t nc = a1 < flush ? a1 : flush;
+        const bool a = commit_mode && v && a1 > old && old < nc && nc >= tstart[g];
+        adv[g] = a;
+        cout[g] = a ? nc : old;
+    }
+
+    // ---- stores ----
+    if (VEC) {
+        if (commit_mode) {
+            v2i64 c;
+            c.x = cout[0];
+            c.y = cout[1];
+            *reinterpret_cast<v2i64*>(t.commit_out + r0) = c;
+        }
+        if (t.min_out) {
+            v2i64 m;
+            m.x = mn[0];
+            m.y = mn[1];
+            *reinterpret_cast<v2i64*>(t.min_out + r0) = m;
+        }
+        if (t.maj_out) {
+            v2i64 m;
+            m.x = mj[0];
+            m.y = mj[1];
+            *reinterpret_cast<v2i64*>(t.maj_out + r0) = m;
+        }
+        if (t.max_out) {
+            v2i64 m;
+            m.x = mx[0];
+            m.y = mx[1];
+            *reinterpret_cast<v2i64*>(t.max_out + r0) = m;
+        }
+    } else {
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            const uint64_t r = r0 + g;
+            if (r < t.n) {
+                if (commit_mode) t.commit_out[r] = cout[g];
+                if (t.min_out) t.min_out[r] = mn[g];
+                if (t.maj_out) t.maj_out[r] = mj[g];
+                if (t.max_out) t.max_out[r] = mx[g];
+            }
+        }
+    }
+
+    // ---- per-wave bit words: bit j of word (wbase/64 + h) is row wbase + 64h + j ----
+    const uint64_t ve = __ballot(valid[0]), vo = __ballot(valid[1]);
+    const uint64_t ae = __ballot(adv[0]), ao = __ballot(adv[1]);
+    if (wbase < t.n) {
+        const uint64_t word = wbase >> 6;
+        const uint64_t nwords = (t.n + 63) >> 6;
+        if (t.valid_bits && lane < 2 && word + lane < nwords) {
+            const uint64_t e = lane ? (ve >> 32) : ve, o = lane ? (vo >> 32) : vo;
+            t.valid_bits[word + lane] = spread32(e) | (spread32(o) << 1);
+        }
+        if (t.advanced_bits && lane < 2 && word + lane < nwords) {
+            const uint64_t e = lane ? (ae >> 32) : ae, o = lane ? (ao >> 32) : ao;
+            t.advanced_bits[word + lane] = spread32(e) | (spread32(o) << 1);
+        }
+    }
+
+    // ---- compacted advanced list: one atomic per wave ----
+    if (t.adv_rows && (ae | ao)) {
+        const uint32_t cnt = __popcll(ae) + __popcll(ao);
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(t.adv_count, (unsigned long long)cnt);
+        base = __shfl(base, 0);
+        const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+        uint64_t pos = base + __popcll(ae & lt) + __popcll(ao & lt);
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            if (adv[g]) {
+                if (pos < t.adv_cap) {
+                    t.adv_rows[pos] = t.adv_row_base + r0 + g;
+                    t.adv_commit[pos] = cout[g];
+                }
+                ++pos;
+            }
+        }
+    }
+}
+
+template <int F>
+__device__ __forceinline__ void run_tile(const TierArgs& ta, uint64_t tile) {
+    const bool full = (tile + 1) * kTile <= ta.t.n && ta.vec_ok;
+    if (full)
+        commit_tile<F, true>(ta, tile);
+    else
+        commit_tile<F, false>(ta, tile);
+}
+
+}  // namespace
+
+namespace {
+
+template <int F, int FHI>
+__device__ __forceinline__ void dispatch_f(const TierArgs& ta, uint64_t tile) {
+    if (ta.t.n_followers == F)
+        run_tile<F>(ta, tile);
+    else if constexpr (F < FHI)
+        dispatch_f<F + 1, FHI>(ta, tile);
+}
+
+// One launch evaluates every tier whose F lies in [FLO, FHI]; blocks are assigned to tiers
+// in order.  The F switch is block-uniform, so it costs no divergence.
+template <int FLO, int FHI>
+__global__ __launch_bounds__(kBlock) void commit_kernel(const LaunchArgs args) {
+    const uint32_t b = blockIdx.x;
+    int ti = 0;
+#pragma unroll
+    for (int i = 1; i < RH_MAX_TIERS; ++i)
+        if (i < args.n_tiers && b >= args.tier[i].block_begin) ti = i;
+    const TierArgs& ta = args.tier[ti];
+    dispatch_f<FLO, FHI>(ta, (uint64_t)(b - ta.block_begin));
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+int launch_class(const rh_commit_soa* tiers, int n_tiers, int flo, int fhi, hipStream_t stream) {
+    LaunchArgs args{};
+    uint64_t blocks = 0;
+    for (int i = 0; i < n_tiers; ++i) {
+        const rh_commit_soa& t = tiers[i];
+        if ((int)t.n_followers < flo || (int)t.n_followers > fhi || t.n == 0) continue;
+        TierArgs& ta = args.tier[args.n_tiers++];
+        ta.t = t;
+        ta.stride = t.col_stride ? t.col_stride : t.n;
+        ta.block_begin = (uint32_t)blocks;
+        ta.n_blocks = (uint32_t)((t.n + kTile - 1) / kTile);
+        const bool cm = t.mode == RH_MODE_COMMIT;
+        ta.vec_ok = aligned16(t.follower_index) && (ta.stride % 2 == 0) && aligned16(t.self_index) &&
+                    (reinterpret_cast<uintptr_t>(t.conf) & 7u) == 0 &&
+                    (!cm || (aligned16(t.commit_in) && aligned16(t.term_start) && aligned16(t.commit_out))) &&
+                    (!t.min_out || aligned16(t.min_out)) && (!t.maj_out || aligned16(t.maj_out)) &&
+                    (!t.max_out || aligned16(t.max_out));
+        blocks += ta.n_blocks;
+    }
+    if (args.n_tiers == 0) return RH_OK;
+    if (blocks > 0x7FFFFFFFull) return rh::fail(RH_E_RANGE, "commit launch: too many groups");
+    if (fhi <= 7)
+        hipLaunchKernelGGL((commit_kernel<1, 7>), dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
+    else
+        hipLaunchKernelGGL((commit_kernel<8, 14>), dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
+    RH_HIP(hipGetLastError());
+    return RH_OK;
+}
+
+}  // namespace
+
+int rh_commit_launch_impl(rh_ctx* ctx, const rh_commit_soa* tiers, int n_tiers, hipStream_t stream) {
+    (void)ctx;
+    if (!tiers || n_tiers < 1 || n_tiers > RH_MAX_TIERS)
+        return rh::fail(RH_E_INVAL, "rh_commit_soa_launch: n_tiers must be in [1, RH_MAX_TIERS]");
+    for (int i = 0; i < n_tiers; ++i) {
+        const rh_commit_soa& t = tiers[i];
+        if (t.n_followers < 1 || t.n_followers > RH_MAX_FOLLOWERS)
+            return rh::fail(RH_E_RANGE, "rh_commit_soa_launch: n_followers must be in [1, 14]");
+        if (t.mode != RH_MODE_COMMIT && t.mode != RH_MODE_WATCH)
+            return rh::fail(RH_E_INVAL, "rh_commit_soa_launch: unknown mode");
+        if (t.n == 0) continue;
+        if (!t.follower_index || !t.self_index || !t.conf)
+            return rh::fail(RH_E_INVAL, "rh_commit_soa_launch: follower_index/self_index/conf required");
+        if (t.col_stride != 0 && t.col_stride < t.n)
+            return rh::fail(RH_E_INVAL, "rh_commit_soa_launch: col_stride < n");
+        if (t.mode == RH_MODE_COMMIT && (!t.commit_in || !t.term_start || !t.commit_out))
+            return rh::fail(RH_E_INVAL, "rh_commit_soa_launch: COMMIT needs commit_in, term_start, commit_out");
+        if (t.mode == RH_MODE_COMMIT && t.gap_threshold < -1)
+            return rh::fail(RH_E_INVAL, "rh_commit_soa_launch: gap_threshold must be -1 or >= 0");
+        if (t.adv_rows && (!t.adv_commit || !t.adv_count))
+            return rh::fail(RH_E_INVAL, "rh_commit_soa_launch: adv_rows needs adv_commit and adv_count");
+    }
+    int rc = launch_class(tiers, n_tiers, 1, 7, stream);
+    if (rc != RH_OK) return rc;
+    return launch_class(tiers, n_tiers, 8, 14, stream);
+}
+
+// ---- delta application: RaftLogIndex.updateToMax per (slot, column) ----------------------
+namespace {
+
+__global__ __launch_bounds__(256) void apply_deltas_kernel(const rh_delta* __restrict__ d, uint64_t n,
+                                                           uint64_t capacity, uint64_t stride,
+                                                           uint32_t nf, int64_t* match, int64_t* fcommit,
+                                                           int64_t* flush, int64_t* commit) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const rh_delta x = d[i];
+    if (x.slot >= capacity) return;  // validated on the host; never trust the ring blindly
+    int64_t* p = nullptr;
+    if (x.column < nf)
+        p = match + (uint64_t)x.column * stride + x.slot;
+    else if (x.column >= 16 && x.column < 16 + nf)
+        p = fcommit + (uint64_t)(x.column - 16) * stride + x.slot;
+    else if (x.column == RH_COL_FLUSH)
+        p = flush + x.slot;
+    else if (x.column == RH_COL_COMMITTED)
+        p = commit + x.slot;
+    if (p) atomicMax(reinterpret_cast<long long*>(p), (long long)x.value);
+}
+
+}  // namespace
+
+int rh_apply_deltas_impl(hipStream_t stream, const rh_delta* d_deltas, uint64_t n, uint64_t capacity,
+                         uint64_t stride, uint32_t n_followers, int64_t* match, int64_t* fcommit,
+                         int64_t* flush, int64_t* commit) {
+    if (n == 0) return RH_OK;
+    const uint64_t blocks = (n + 255) / 256;
+    hipLaunchKernelGGL(apply_deltas_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream, d_deltas, n,
+                       capacity, stride, n_followers, match, fcommit, flush, commit);
+    RH_HIP(hipGetLastError());
+    return RH_OK;
+}

@@ -1,0 +1,411 @@
+// CRC32C (PureJavaCrc32C) over SegmentedRaftLog frames, for gfx950 (MI355X).
+//
+// Reference semantics:
+//   PureJavaCrc32C.update/getValue/reset    PureJavaCrc32C.java:43-152 (tables :158-688)
+//   frame CRC = CRC32C(varint || proto), big-endian trailer
+//                                            SegmentedRaftLogOutputStream.java:86-110
+//   verification                             SegmentedRaftLogReader.java:327-336
+//
+// Structure.  A frame's CRC-covered span is cut into end-anchored windows of W = Q*S bytes;
+// each window is handled by Q consecutive lanes of a wave, lane i taking the contiguous chunk
+// [end - (Q-i)*S, end - (Q-i-1)*S) of the window.  Every lane folds its chunk into a CRC
+// register that starts at zero (slicing-by-4, 4 byte-tables), and the Q partial registers are
+// combined with a log2(Q)-level tree: left' = Z_d(left) ^ right, where Z_d advances a register
+// over d zero bytes (a 4x256 byte-table per power-of-two d).  CRC linearity makes this exact:
+// bytes before the frame start contribute nothing to a zero register, and the initial state
+// I (0xFFFFFFFF after reset()) is injected by XOR-ing it into the first 4 message bytes.
+//
+// LDS.  The 4 slicing tables are replicated 32 times and interleaved so that lane l always
+// reads bank (l & 31): the data-dependent lookups are bank-conflict free (a random byte index
+// into a shared table would cost ~3.4 LDS cycles per 32-lane group instead of 1).  128 KiB of
+// tables + 4 KiB per tree level => one 1024-thread workgroup per CU, persistent over frames.
+//
+// No MFMA: CRC is table/XOR integer work and the kernel is HBM-bound.
+#include "rh_internal.h"
+
+#include <vector>
+
+namespace {
+
+constexpr int kMaxLevels = 8;  // tree levels (log2 Q) + 1 window level
+
+// ---- host: zero-advance linear maps ------------------------------------------------------
+struct Map32 {
+    uint32_t col[32];  // image of bit i
+};
+
+uint32_t apply(const Map32& m, uint32_t x) {
+    uint32_t r = 0;
+    for (int i = 0; i < 32; ++i)
+        if (x >> i & 1u) r ^= m.col[i];
+    return r;
+}
+
+Map32 compose(const Map32& a, const Map32& b) {  // a o b
+    Map32 r{};
+    for (int i = 0; i < 32; ++i) r.col[i] = apply(a, b.col[i]);
+    return r;
+}
+
+}  // namespace
+
+namespace rh {
+
+void build_crc_slice_tables(CrcTables* t) {
+    for (uint32_t i = 0; i < 256; ++i) {
+        uint32_t c = i;
+        for (int k = 0; k < 8; ++k) c = (c >> 1) ^ ((c & 1u) ? 0x82F63B78u : 0u);
+        t->slice[0][i] = c;
+    }
+    for (int k = 1; k < 4; ++k)
+        for (int i = 0; i < 256; ++i)
+            t->slice[k][i] = (t->slice[k - 1][i] >> 8) ^ t->slice[0][t->slice[k - 1][i] & 0xffu];
+}
+
+void build_crc_shift_table(uint64_t nbytes, uint32_t out[4][256]) {
+    CrcTables st;
+    build_crc_slice_tables(&st);
+    Map32 one{};  // advance over one zero byte: r -> (r >> 8) ^ T0[r & 0xff]
+    for (int i = 0; i < 32; ++i) {
+        const uint32_t x = 1u << i;
+        one.col[i] = (x >> 8) ^ st.slice[0][x & 0xffu];
+    }
+    Map32 acc{};
+    for (int i = 0; i < 32; ++i) acc.col[i] = 1u << i;  // identity
+    Map32 p = one;
+    for (uint64_t n = nbytes; n; n >>= 1) {
+        if (n & 1u) acc = compose(p, acc);
+        p = compose(p, p);
+    }
+    for (int k = 0; k < 4; ++k)
+        for (int b = 0; b < 256; ++b) out[k][b] = apply(acc, (uint32_t)b << (8 * k));
+}
+
+}  // namespace rh
+
+namespace {
+
+struct FrameArgs {
+    const uint8_t* buf;
+    uint8_t* wbuf;
+    int64_t buf_len;
+    const uint64_t* off;
+    const uint32_t* len;
+    uint64_t n;
+    uint32_t init;
+    uint32_t flags;
+    uint32_t* crc_out;
+    uint64_t* bad_bits;
+    unsigned long long* n_bad;
+    const uint32_t* slice;   // [4][256] global
+    const uint32_t* shift;   // [levels][4][256] global: level j advances S*2^j, last = W
+};
+
+template <bool REPL>
+__device__ __forceinline__ uint32_t slice_lookup(const uint32_t* lds, int k, uint32_t e, uint32_t c) {
+    if (REPL) return lds[(k << 13) | (e << 5) | c];
+    return lds[(k << 8) | e];
+}
+
+template <bool REPL>
+__device__ __forceinline__ uint32_t fold_word(const uint32_t* lds, uint32_t r, uint32_t w, uint32_t c) {
+    const uint32_t x = r ^ w;
+    return slice_lookup<REPL>(lds, 3, x & 0xffu, c) ^ slice_lookup<REPL>(lds, 2, (x >> 8) & 0xffu, c) ^
+           slice_lookup<REPL>(lds, 1, (x >> 16) & 0xffu, c) ^ slice_lookup<REPL>(lds, 0, x >> 24, c);
+}
+
+template <bool REPL>
+__device__ __forceinline__ uint32_t fold_byte(const uint32_t* lds, uint32_t r, uint32_t b, uint32_t c) {
+    return (r >> 8) ^ slice_lookup<REPL>(lds, 0, (r ^ b) & 0xffu, c);
+}
+
+__device__ __forceinline__ uint32_t zshift(const uint32_t* tab, uint32_t r) {
+    return tab[r & 0xffu] ^ tab[256 + ((r >> 8) & 0xffu)] ^ tab[512 + ((r >> 16) & 0xffu)] ^ tab[768 + (r >> 24)];
+}
+
+// One little-endian dword at byte offset p (4-aligned) of a buffer of `lim` bytes; bytes at or
+// past `lim` read as zero and are never touched.
+__device__ __forceinline__ uint32_t load_dword_clamped(const uint8_t* buf, int64_t p, int64_t lim) {
+    if (p + 4 <= lim) return *reinterpret_cast<const uint32_t*>(buf + p);
+    uint32_t v = 0;
+    for (int i = 0; i < 4; ++i)
+        if (p + i < lim) v |= (uint32_t)buf[p + i] << (8 * i);
+    return v;
+}
+
+struct __attribute__((aligned(4))) u32x4a {
+    uint32_t x, y, z, w;
+};
+
+// Dwords [16*blk, 16*blk+16) after the 4-aligned byte offset b0; dwords >= need read as 0.
+__device__ __forceinline__ void load_block(uint32_t (&d)[16], const uint8_t* buf, int64_t b0, int blk,
+                                           int need, int64_t lim) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int idx = 16 * blk + 4 * q;
+        const int64_t p = b0 + 4 * (int64_t)idx;
+        if (idx < need && p + 16 <= lim) {
+            const u32x4a v = *reinterpret_cast<const u32x4a*>(buf + p);
+            d[4 * q] = v.x;
+            d[4 * q + 1] = v.y;
+            d[4 * q + 2] = v.z;
+            d[4 * q + 3] = v.w;
+        } else if (idx < need) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) d[4 * q + i] = load_dword_clamped(buf, p + 4 * i, lim);
+        } else {
+            d[4 * q] = d[4 * q + 1] = d[4 * q + 2] = d[4 * q + 3] = 0;
+        }
+    }
+}
+
+// Q lanes per frame window, S bytes per lane (multiple of 16), REPL = replicated tables.
+template <int Q, int S, bool REPL>
+__global__ __launch_bounds__(1024) void crc_frames_kernel(const FrameArgs a) {
+    constexpr int W = Q * S;
+    constexpr int LOGQ = __builtin_ctz(Q);
+    constexpr int NB = S / 64;                    // 64-byte blocks per full chunk
+    static_assert(S % 64 == 0, "chunk must be a multiple of 64 bytes");
+    constexpr int kSliceWords = REPL ? 4 * 256 * 32 : 4 * 256;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    uint32_t* lslice = lds;
+    uint32_t* lshift = lds + kSliceWords;  // [LOGQ + 1][1024]
+
+    // ---- stage tables into LDS ----
+    for (int i = threadIdx.x; i < kSliceWords; i += blockDim.x) {
+        if (REPL) {
+            const int k = i >> 13, e = (i >> 5) & 255;
+            lslice[i] = a.slice[(k << 8) | e];
+        } else {
+            lslice[i] = a.slice[i];
+        }
+    }
+    for (int i = threadIdx.x; i < (LOGQ + 1) * 1024; i += blockDim.x) lshift[i] = a.shift[i];
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63;
+    const uint32_t c = lane & 31;
+    const int gl = lane & (Q - 1);            // position inside the window group
+    const int gid = lane / Q;                 // group inside the wave
+    constexpr int kGroupsPerWave = 64 / Q;
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const bool trailer = (a.flags & (RH_CRC_VERIFY | RH_CRC_STAMP)) != 0;
+
+    for (uint64_t f0 = wave * kGroupsPerWave; f0 < a.n; f0 += nwaves * kGroupsPerWave) {
+        const uint64_t f = f0 + gid;
+        const bool active = f < a.n;
+        uint64_t o = 0;
+        int64_t Lc = 0;
+        bool malformed = false;  // frame outside the buffer, or shorter than its trailer
+        if (active) {
+            o = a.off[f];
+            const int64_t L = (int64_t)a.len[f];
+            malformed = o > (uint64_t)a.buf_len || L > a.buf_len - (int64_t)o || (trailer && L < 4);
+            Lc = malformed ? 0 : L - (trailer ? 4 : 0);
+        }
+        const int64_t E = (int64_t)o + Lc;              // end of the CRC-covered span
+        const int64_t nw = (Lc + W - 1) / W;            // windows of this frame (0 if empty)
+        const uint32_t sh = (uint32_t)(E & 3);          // byte misalignment of every word
+
+        // Wave-uniform trip count: the largest window count among the wave's groups.
+        int64_t nw_max = nw;
+        if (kGroupsPerWave > 1) {
+#pragma unroll
+            for (int d = Q; d < 64; d <<= 1) {
+                const int64_t other = __shfl_xor(nw_max, d);
+                nw_max = other > nw_max ? other : nw_max;
+            }
+        }
+
+        uint32_t R = 0;  // running register of the frame (meaningful in the group leader)
+        for (int64_t wi = 0; wi < nw_max; ++wi) {
+            const bool win_active = wi < nw;
+            // chunk [cs, be) of this lane
+            const int64_t be = E - (nw - 1 - wi) * (int64_t)W - (int64_t)(Q - 1 - gl) * S;
+            const int64_t cs = be - S;
+            const int64_t bs = cs > (int64_t)o ? cs : (int64_t)o;  // bytes before o are zero
+            int64_t cnt = be - bs;
+            if (!win_active || cnt < 0) cnt = 0;
+            const int h = (int)(cnt & 3);                          // head bytes (straddling lane)
+            const int nwords = (int)(cnt >> 2);
+            const int64_t A = bs + h;                              // first word's address
+            uint32_t r = 0;
+            // message position of the chunk's first byte (init injection at positions 0..3)
+            const bool has_start = cnt > 0 && bs == (int64_t)o;
+
+            // head bytes (at most 3, only the lane that holds the frame start)
+            if (h) {
+#pragma unroll
+                for (int i = 0; i < 3; ++i)
+                    if (i < h) {
+                        uint32_t b = a.buf[bs + i];
+                        if (has_start) b ^= (a.init >> (8 * i)) & 0xffu;
+                        r = fold_byte<REPL>(lslice, r, b, c);
+                    }
+            }
+            // words: 64-byte blocks loaded as 16-byte pieces from the 4-aligned base b0,
+            // realigned by `sh`; block blk+1 is in flight while block blk is folded.  Loads
+            // never touch [buf_len, ...): pieces crossing it are read per dword / per byte.
+            if (nwords > 0) {
+                const int64_t b0 = A - sh;                 // 4-aligned
+                const int need = nwords + (sh ? 1 : 0);    // dwords needed from b0
+                uint32_t cur[16], nxt[16];
+                load_block(cur, a.buf, b0, 0, need, a.buf_len);
+#pragma unroll
+                for (int blk = 0; blk < NB; ++blk) {
+                    if (blk + 1 < NB) {
+                        load_block(nxt, a.buf, b0, blk + 1, need, a.buf_len);
+                    } else {
+                        nxt[0] = (16 * NB < need) ? load_dword_clamped(a.buf, b0 + 64 * NB, a.buf_len) : 0u;
+                    }
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) {
+                        if (16 * blk + j < nwords) {
+                            const uint32_t hi = (j < 15) ? cur[j + 1] : nxt[0];
+                            uint32_t w = sh ? __builtin_amdgcn_alignbyte(hi, cur[j], sh) : cur[j];
+                            if (blk == 0 && j == 0 && has_start) w ^= a.init >> (8 * h);
+                            r = fold_word<REPL>(lslice, r, w, c);
+                        }
+                    }
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) cur[j] = nxt[j];
+                }
+            }
+            // init bytes that fall beyond a sub-4-byte message are handled after the loop
+            // ---- tree combine across the Q lanes of the window ----
+#pragma unroll
+            for (int j = 0; j < LOGQ; ++j) {
+                const uint32_t t = zshift(lshift + j * 1024, r);
+                const uint32_t p = __shfl_down(r, 1 << j);
+                r = t ^ p;
+            }
+            if (win_active) R = zshift(lshift + LOGQ * 1024, R) ^ r;
+        }
+
+        if (active && gl == 0) {
+            uint32_t state = R;
+            if (Lc < 4) state ^= (uint32_t)((uint64_t)a.init >> (8 * Lc));
+            const uint32_t value = ~state;  // getValue()
+            if (a.crc_out) a.crc_out[f] = malformed ? 0u : value;
+            if (malformed) {
+                if (a.bad_bits) atomicOr(reinterpret_cast<unsigned long long*>(a.bad_bits + (f >> 6)), 1ull << (f & 63));
+                if (a.n_bad) atomicAdd(a.n_bad, 1ull);
+            } else if (a.flags & RH_CRC_STAMP) {
+                a.wbuf[E + 0] = (uint8_t)(value >> 24);
+                a.wbuf[E + 1] = (uint8_t)(value >> 16);
+                a.wbuf[E + 2] = (uint8_t)(value >> 8);
+                a.wbuf[E + 3] = (uint8_t)value;
+            } else if (a.flags & RH_CRC_VERIFY) {
+                const uint32_t stored = ((uint32_t)a.buf[E] << 24) | ((uint32_t)a.buf[E + 1] << 16) |
+                                        ((uint32_t)a.buf[E + 2] << 8) | (uint32_t)a.buf[E + 3];
+                if (stored != value) {
+                    if (a.bad_bits) atomicOr(reinterpret_cast<unsigned long long*>(a.bad_bits + (f >> 6)),
+                                             1ull << (f & 63));
+                    if (a.n_bad) atomicAdd(a.n_bad, 1ull);
+                }
+            }
+        }
+    }
+}
+
+struct Variant {
+    int q, s;
+    bool repl;
+};
+
+constexpr Variant kVariants[] = {
+    {64, 64, true},    // 0: one wave per 4 KiB window (default)
+    {16, 256, true},   // 1: four 4 KiB windows per wave
+    {8, 512, true},    // 2: eight 4 KiB windows per wave
+    {64, 64, false},   // 3: shared (non-replicated) tables, for the bank-conflict A/B
+};
+constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
+
+int g_default_variant = 0;
+
+template <int Q, int S, bool REPL>
+int launch_variant(rh_ctx* ctx, const FrameArgs& fa, hipStream_t stream) {
+    constexpr int LOGQ = __builtin_ctz(Q);
+    constexpr size_t lds = (REPL ? 4 * 256 * 32 * 4 : 4 * 256 * 4) + (size_t)(LOGQ + 1) * 4096;
+    static_assert(lds <= 160 * 1024, "LDS budget");
+    const int block = REPL ? 1024 : 256;
+    const int per_cu = REPL ? 1 : 4;
+    auto kern = crc_frames_kernel<Q, S, REPL>;
+    static bool attr_set = false;
+    if (!attr_set) {
+        RH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        attr_set = true;
+    }
+    const uint64_t groups = (fa.n + (64 / Q) - 1) / (64 / Q);   // wave-iterations needed
+    uint64_t grid = (uint64_t)ctx->num_cus * per_cu;
+    const uint64_t need = (groups + (block / 64) - 1) / (block / 64);
+    if (need < grid) grid = need ? need : 1;
+    FrameArgs a = fa;
+    // per-level shift tables: S*2^j for j < LOGQ, then W
+    a.shift = ctx->d_shift + (size_t)__builtin_ctz(S) * 1024;
+    hipLaunchKernelGGL(kern, dim3((uint32_t)grid), dim3(block), lds, stream, a);
+    RH_HIP(hipGetLastError());
+    return RH_OK;
+}
+
+}  // namespace
+
+int rh_crc_upload_tables(rh_ctx* ctx) {
+    rh::CrcTables t;
+    rh::build_crc_slice_tables(&t);
+    RH_HIP(hipMalloc(&ctx->d_slice, sizeof(t.slice)));
+    RH_HIP(hipMemcpy(ctx->d_slice, t.slice, sizeof(t.slice), hipMemcpyHostToDevice));
+    // zero-advance maps for every power of two 2^0 .. 2^40 bytes
+    constexpr int kPow = 41;
+    std::vector<uint32_t> sh((size_t)kPow * 1024);
+    for (int m = 0; m < kPow; ++m)
+        rh::build_crc_shift_table(1ull << m, reinterpret_cast<uint32_t(*)[256]>(sh.data() + (size_t)m * 1024));
+    RH_HIP(hipMalloc(&ctx->d_shift, sh.size() * 4));
+    RH_HIP(hipMemcpy(ctx->d_shift, sh.data(), sh.size() * 4, hipMemcpyHostToDevice));
+    return RH_OK;
+}
+
+int rh_crc_launch_variant(rh_ctx* ctx, const rh_frames* f, uint32_t flags, int variant, hipStream_t stream) {
+    if (!f) return rh::fail(RH_E_INVAL, "rh_crc32c_frames_launch: frames == NULL");
+    if ((flags & ~(RH_CRC_VERIFY | RH_CRC_STAMP)) || flags == (RH_CRC_VERIFY | RH_CRC_STAMP))
+        return rh::fail(RH_E_INVAL, "rh_crc32c_frames_launch: flags must be 0, VERIFY or STAMP");
+    if (f->n == 0) return RH_OK;
+    if (!f->buf || !f->frame_off || !f->frame_len)
+        return rh::fail(RH_E_INVAL, "rh_crc32c_frames_launch: buf, frame_off, frame_len required");
+    if (variant < 0 || variant >= kNumVariants) return rh::fail(RH_E_INVAL, "unknown CRC kernel variant");
+    FrameArgs a{};
+    a.buf = f->buf;
+    a.wbuf = f->buf;
+    if (f->buf_len > (uint64_t)INT64_MAX) return rh::fail(RH_E_RANGE, "rh_crc32c_frames_launch: buf_len too large");
+    a.buf_len = (int64_t)f->buf_len;
+    a.off = f->frame_off;
+    a.len = f->frame_len;
+    a.n = f->n;
+    a.init = f->init_state;
+    a.flags = flags;
+    a.crc_out = f->crc_out;
+    a.bad_bits = f->bad_bits;
+    a.n_bad = f->n_bad;
+    a.slice = ctx->d_slice;
+    switch (variant) {
+        case 0: return launch_variant<64, 64, true>(ctx, a, stream);
+        case 1: return launch_variant<16, 256, true>(ctx, a, stream);
+        case 2: return launch_variant<8, 512, true>(ctx, a, stream);
+        case 3: return launch_variant<64, 64, false>(ctx, a, stream);
+    }
+    return rh::fail(RH_E_INVAL, "unknown CRC kernel variant");
+}
+
+int rh_crc_launch_impl(rh_ctx* ctx, const rh_frames* f, uint32_t flags, hipStream_t stream) {
+    return rh_crc_launch_variant(ctx, f, flags, g_default_variant, stream);
+}
+
+int rh_crc_set_default_variant(int v) {
+    if (v < 0 || v >= kNumVariants) return rh::fail(RH_E_INVAL, "unknown CRC kernel variant");
+    g_default_variant = v;
+    return RH_OK;
+}
+
+int rh_crc_num_variants() { return kNumVariants; }

@@ -1,0 +1,264 @@
+"""Device-side host API: contexts, commit tiers and frame batches over torch-owned HBM.
+
+PyTorch is used only as plumbing here -- device memory (``torch.empty(..., device='cuda')``)
+and streams (``torch.cuda.current_stream()``).  Every computation is a libratis_hip kernel
+reached through the C ABI in ``include/ratis_hip.h``.
+
+Reference mapping (paths relative to the ratis tree):
+  * :func:`commit_launch` with ``mode=COMMIT`` = ``LeaderStateImpl.updateCommit()``
+    (LeaderStateImpl.java:946-950, 956-984, 1015-1026) + ``RaftLogBase.updateCommitIndex``
+    (RaftLogBase.java:121-142), for every group of every tier.
+  * ``mode=WATCH`` = ``LeaderStateImpl.commitIndexChanged()`` (LeaderStateImpl.java:612-622).
+  * :func:`crc32c_frames` = ``PureJavaCrc32C`` (PureJavaCrc32C.java:43-152) over
+    ``SegmentedRaftLogOutputStream.write`` frames (:86-110), verified as in
+    ``SegmentedRaftLogReader.decodeEntry`` (:327-336) or stamped as in the writer.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass, field
+from typing import Optional, Sequence
+
+import torch
+
+from . import _lib
+from ._lib import RH_MODE_COMMIT, RH_MODE_WATCH, RhCommitSoa, RhFrames, check
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise ValueError("expected a CUDA (HIP) tensor")
+    if not t.is_contiguous():
+        raise ValueError("expected a contiguous tensor")
+    return t.data_ptr()
+
+
+def _stream_ptr(stream: Optional[torch.cuda.Stream]) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+class Context:
+    """One ``rh_ctx`` per (process, GPU)."""
+
+    def __init__(self, device: int = 0):
+        lib = _lib.load()
+        if not torch.cuda.is_available():
+            raise RuntimeError("ratis_amd.Context needs a GPU (MI355X/gfx950); there is no CPU fallback")
+        self.device = device
+        torch.cuda.set_device(device)
+        h = ctypes.c_void_p()
+        check(lib.rh_init(device, ctypes.byref(h)))
+        self._h = h
+
+    @property
+    def handle(self) -> ctypes.c_void_p:
+        if self._h is None:
+            raise _lib.RatisHipError(_lib.RH_E_STATE, "context closed")
+        return self._h
+
+    def close(self) -> None:
+        if self._h is not None:
+            check(_lib.load().rh_shutdown(self._h))
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+# ------------------------------------------------------------------------------------------
+# Quorum commit
+# ------------------------------------------------------------------------------------------
+@dataclass
+class CommitTier:
+    """One struct-of-arrays tier on the device (all tensors CUDA, contiguous).
+
+    ``follower_index`` is ``[F, n]`` int64 (row k = follower slot k), ``conf`` is int32 holding
+    the uint32 membership words of ``ratis_hip.h``.
+    """
+
+    follower_index: torch.Tensor
+    self_index: torch.Tensor
+    conf: torch.Tensor
+    commit_in: Optional[torch.Tensor] = None
+    term_start: Optional[torch.Tensor] = None
+    commit_out: Optional[torch.Tensor] = None
+    min_out: Optional[torch.Tensor] = None
+    maj_out: Optional[torch.Tensor] = None
+    max_out: Optional[torch.Tensor] = None
+    valid_bits: Optional[torch.Tensor] = None
+    advanced_bits: Optional[torch.Tensor] = None
+    gap_threshold: int = -1
+    adv_rows: Optional[torch.Tensor] = None
+    adv_commit: Optional[torch.Tensor] = None
+    adv_count: Optional[torch.Tensor] = None
+    adv_row_base: int = 0
+
+    @property
+    def n(self) -> int:
+        return int(self.self_index.numel())
+
+    @property
+    def n_followers(self) -> int:
+        return int(self.follower_index.shape[0])
+
+    def alloc_outputs(self, mode: int = RH_MODE_COMMIT, levels: bool = False, bits: bool = True) -> "CommitTier":
+        dev = self.self_index.device
+        n = self.n
+        nw = (n + 63) // 64
+        if mode == RH_MODE_COMMIT and self.commit_out is None:
+            self.commit_out = torch.empty(n, dtype=torch.int64, device=dev)
+        if self.min_out is None:
+            self.min_out = torch.empty(n, dtype=torch.int64, device=dev)
+        if levels or mode == RH_MODE_WATCH:
+            if self.maj_out is None:
+                self.maj_out = torch.empty(n, dtype=torch.int64, device=dev)
+            if self.max_out is None:
+                self.max_out = torch.empty(n, dtype=torch.int64, device=dev)
+        if bits:
+            if self.valid_bits is None:
+                self.valid_bits = torch.zeros(nw, dtype=torch.int64, device=dev)
+            if mode == RH_MODE_COMMIT and self.advanced_bits is None:
+                self.advanced_bits = torch.zeros(nw, dtype=torch.int64, device=dev)
+        return self
+
+    def to_struct(self, mode: int) -> RhCommitSoa:
+        fi = self.follower_index
+        if fi.dim() != 2 or fi.dtype != torch.int64:
+            raise ValueError("follower_index must be an int64 [F, n] tensor")
+        n = self.n
+        for name in ("self_index", "commit_in", "term_start", "commit_out", "min_out", "maj_out", "max_out"):
+            t = getattr(self, name)
+            if t is not None and (t.dtype != torch.int64 or t.numel() != n):
+                raise ValueError(f"{name} must be int64 with {n} elements")
+        if self.conf.dtype != torch.int32 or self.conf.numel() != n:
+            raise ValueError("conf must be int32 (uint32 bit patterns) with n elements")
+        s = RhCommitSoa()
+        s.n = n
+        s.n_followers = fi.shape[0]
+        s.mode = mode
+        s.gap_threshold = self.gap_threshold if mode == RH_MODE_COMMIT else -1
+        if not fi.is_cuda or fi.stride(1) != 1 or fi.stride(0) < n:
+            raise ValueError("follower_index must be a CUDA [F, n] view with unit row stride")
+        s.follower_index = fi.data_ptr()
+        s.col_stride = fi.stride(0)
+        s.self_index = _ptr(self.self_index)
+        s.commit_in = _ptr(self.commit_in)
+        s.term_start = _ptr(self.term_start)
+        s.conf = _ptr(self.conf)
+        s.commit_out = _ptr(self.commit_out)
+        s.min_out = _ptr(self.min_out)
+        s.maj_out = _ptr(self.maj_out)
+        s.max_out = _ptr(self.max_out)
+        s.valid_bits = _ptr(self.valid_bits)
+        s.advanced_bits = _ptr(self.advanced_bits) if mode == RH_MODE_COMMIT else None
+        if self.adv_rows is not None:
+            s.adv_rows = _ptr(self.adv_rows)
+            s.adv_commit = _ptr(self.adv_commit)
+            s.adv_count = _ptr(self.adv_count)
+            s.adv_cap = self.adv_rows.numel()
+            s.adv_row_base = self.adv_row_base
+        return s
+
+
+def commit_launch(ctx: Context, tiers: Sequence[CommitTier], mode: int = RH_MODE_COMMIT,
+                  stream: Optional[torch.cuda.Stream] = None) -> None:
+    """Enqueues one fused commit kernel over up to RH_MAX_TIERS tiers (asynchronous)."""
+    if not 1 <= len(tiers) <= _lib.RH_MAX_TIERS:
+        raise ValueError("1..4 tiers per launch")
+    arr = (RhCommitSoa * len(tiers))(*[t.to_struct(mode) for t in tiers])
+    check(_lib.load().rh_commit_soa_launch(ctx.handle, arr, len(tiers), _stream_ptr(stream)))
+
+
+def unpack_bits(words: torch.Tensor, n: int) -> torch.Tensor:
+    """Bit g of word g//64 -> bool tensor [n] (on the words' device)."""
+    w = words.view(torch.int64)
+    shifts = torch.arange(64, device=w.device, dtype=torch.int64)
+    bits = (w.unsqueeze(1) >> shifts) & 1
+    return bits.reshape(-1)[:n].bool()
+
+
+# ------------------------------------------------------------------------------------------
+# CRC32C over frames
+# ------------------------------------------------------------------------------------------
+@dataclass
+class FrameBatch:
+    """A segment image in HBM plus its frame table."""
+
+    buf: torch.Tensor          # uint8 [buf_len]
+    frame_off: torch.Tensor    # int64 [n]: offset of each frame's first varint byte
+    frame_len: torch.Tensor    # int32 [n]: varint + proto + 4
+    crc_out: Optional[torch.Tensor] = None   # int32 [n] (uint32 bit patterns)
+    bad_bits: Optional[torch.Tensor] = None  # int64 [ceil(n/64)]
+    n_bad: Optional[torch.Tensor] = None     # int64 [1]
+
+    @property
+    def n(self) -> int:
+        return int(self.frame_off.numel())
+
+    def alloc_outputs(self) -> "FrameBatch":
+        dev = self.buf.device
+        if self.crc_out is None:
+            self.crc_out = torch.empty(self.n, dtype=torch.int32, device=dev)
+        if self.bad_bits is None:
+            self.bad_bits = torch.zeros((self.n + 63) // 64, dtype=torch.int64, device=dev)
+        if self.n_bad is None:
+            self.n_bad = torch.zeros(1, dtype=torch.int64, device=dev)
+        return self
+
+    def to_struct(self, init_state: int) -> RhFrames:
+        if self.buf.dtype != torch.uint8:
+            raise ValueError("buf must be uint8")
+        if self.frame_off.dtype != torch.int64 or self.frame_len.dtype != torch.int32:
+            raise ValueError("frame_off must be int64 and frame_len int32")
+        if self.frame_len.numel() != self.n:
+            raise ValueError("frame_off and frame_len lengths differ")
+        f = RhFrames()
+        f.buf = _ptr(self.buf)
+        f.buf_len = self.buf.numel()
+        f.frame_off = _ptr(self.frame_off)
+        f.frame_len = _ptr(self.frame_len)
+        f.n = self.n
+        f.init_state = init_state & 0xFFFFFFFF
+        f.crc_out = _ptr(self.crc_out)
+        f.bad_bits = _ptr(self.bad_bits)
+        f.n_bad = _ptr(self.n_bad)
+        return f
+
+
+def crc32c_frames(ctx: Context, batch: FrameBatch, flags: int = _lib.RH_CRC_VERIFY,
+                  init_state: int = 0xFFFFFFFF, variant: Optional[int] = None,
+                  stream: Optional[torch.cuda.Stream] = None) -> None:
+    """Enqueues the frame CRC kernel (asynchronous).  ``flags``: 0, RH_CRC_VERIFY or RH_CRC_STAMP."""
+    f = batch.to_struct(init_state)
+    lib = _lib.load()
+    if variant is None:
+        check(lib.rh_crc32c_frames_launch(ctx.handle, ctypes.byref(f), flags, _stream_ptr(stream)))
+    else:
+        check(lib.rh_crc32c_frames_launch_variant(ctx.handle, ctypes.byref(f), flags, variant, _stream_ptr(stream)))
+
+
+def crc32c_num_variants() -> int:
+    return _lib.load().rh_crc32c_num_variants()
+
+
+def crc32c_bytes(ctx: Context, data: torch.Tensor, init_state: int = 0xFFFFFFFF) -> int:
+    """``PureJavaCrc32C`` state after ``update(data)`` from ``init_state``, as getValue() (uint32).
+
+    One span, computed by the frame kernel with no trailer (flags = 0)."""
+    if data.dtype != torch.uint8 or not data.is_cuda:
+        raise ValueError("data must be a CUDA uint8 tensor")
+    n = data.numel()
+    buf = data if n else torch.zeros(1, dtype=torch.uint8, device=data.device)
+    fb = FrameBatch(buf=buf,
+                    frame_off=torch.zeros(1, dtype=torch.int64, device=data.device),
+                    frame_len=torch.full((1,), n, dtype=torch.int32, device=data.device))
+    fb.alloc_outputs()
+    crc32c_frames(ctx, fb, flags=0, init_state=init_state)
+    torch.cuda.synchronize()
+    return int(fb.crc_out.item()) & 0xFFFFFFFF

@@ -1,0 +1,97 @@
+"""CPU tests of the C-ABI boundary: the library loads, exports every function include/ratis_hip.h
+declares, and the ctypes mirrors of the C structs have the C layout (no compute calls)."""
+import ctypes
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "ratis_hip.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\**\s+\**\s*(rh_[a-z0-9_]+)\s*\(", src, flags=re.M)
+    inline = set(re.findall(r"static\s+inline\s+\w+\s+(rh_[a-z0-9_]+)\s*\(", src))
+    return sorted(set(names) - inline)
+
+
+def test_header_parses_into_function_list():
+    names = declared_functions()
+    for must in ("rh_init", "rh_commit_soa_launch", "rh_crc32c_frames_launch", "rh_push_deltas",
+                 "rh_commit_batch", "rh_crc32c_verify_host"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol():
+    from ratis_amd import _lib
+    lib = _lib.load()
+    missing = [n for n in declared_functions() if not hasattr(lib, n)]
+    assert not missing, missing
+    # and the ctypes table covers exactly the declared surface
+    assert sorted(_lib.exported_symbols()) == declared_functions()
+
+
+def test_abi_version_and_error_slot():
+    from ratis_amd import _lib
+    lib = _lib.load()
+    assert lib.rh_abi_version() == 1
+    assert isinstance(lib.rh_last_error(), bytes)
+
+
+def test_invalid_arguments_fail_without_gpu():
+    """Argument validation happens before any device call (no GPU needed)."""
+    from ratis_amd import _lib
+    lib = _lib.load()
+    assert lib.rh_commit_soa_launch(None, None, 1, None) == _lib.RH_E_INVAL
+    assert b"ctx" in lib.rh_last_error()
+    assert lib.rh_groups_create(None, 10, 4, -1, None) == _lib.RH_E_INVAL
+    assert lib.rh_crc32c_set_variant(99) == _lib.RH_E_INVAL
+    with pytest.raises(_lib.IllegalArgumentError):
+        _lib.check(lib.rh_crc32c_set_variant(-1))
+    assert lib.rh_crc32c_set_variant(0) == _lib.RH_OK
+
+
+C_LAYOUT = r"""
+#include <stdio.h>
+#include <stddef.h>
+#include "ratis_hip.h"
+#define F(T, f) printf(#T "." #f " %zu\n", offsetof(T, f));
+int main(void) {
+  printf("rh_commit_soa %zu\n", sizeof(rh_commit_soa));
+  printf("rh_frames %zu\n", sizeof(rh_frames));
+  printf("rh_delta %zu\n", sizeof(rh_delta));
+  F(rh_commit_soa, n) F(rh_commit_soa, n_followers) F(rh_commit_soa, mode) F(rh_commit_soa, gap_threshold)
+  F(rh_commit_soa, follower_index) F(rh_commit_soa, col_stride) F(rh_commit_soa, self_index)
+  F(rh_commit_soa, commit_in) F(rh_commit_soa, term_start) F(rh_commit_soa, conf) F(rh_commit_soa, commit_out)
+  F(rh_commit_soa, min_out) F(rh_commit_soa, maj_out) F(rh_commit_soa, max_out) F(rh_commit_soa, valid_bits)
+  F(rh_commit_soa, advanced_bits) F(rh_commit_soa, adv_rows) F(rh_commit_soa, adv_commit)
+  F(rh_commit_soa, adv_count) F(rh_commit_soa, adv_cap) F(rh_commit_soa, adv_row_base)
+  F(rh_frames, buf) F(rh_frames, buf_len) F(rh_frames, frame_off) F(rh_frames, frame_len) F(rh_frames, n)
+  F(rh_frames, init_state) F(rh_frames, reserved) F(rh_frames, crc_out) F(rh_frames, bad_bits) F(rh_frames, n_bad)
+  F(rh_delta, slot) F(rh_delta, column) F(rh_delta, reserved) F(rh_delta, value)
+  printf("conf %u\n", rh_conf_pack(0x5, 1, 1, 0x3, 1, 1));
+  return 0;
+}
+"""
+
+
+def test_struct_layouts_match_header(tmp_path):
+    from ratis_amd import _lib
+    src = tmp_path / "layout.c"
+    src.write_text(C_LAYOUT)
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout
+    vals = dict(line.rsplit(" ", 1) for line in out.strip().splitlines())
+    assert int(vals["rh_commit_soa"]) == ctypes.sizeof(_lib.RhCommitSoa)
+    assert int(vals["rh_frames"]) == ctypes.sizeof(_lib.RhFrames)
+    assert int(vals["rh_delta"]) == ctypes.sizeof(_lib.RhDelta)
+    for cname, cls in (("rh_commit_soa", _lib.RhCommitSoa), ("rh_frames", _lib.RhFrames), ("rh_delta", _lib.RhDelta)):
+        for fname, _ in cls._fields_:
+            assert int(vals[f"{cname}.{fname}"]) == getattr(cls, fname).offset, (cname, fname)
+    assert int(vals["conf"]) == _lib.conf_pack(0x5, True, True, 0x3, True, True)

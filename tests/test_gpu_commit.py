@@ -1,0 +1,267 @@
+"""GPU parity of the batched quorum-commit kernel against the CPU oracle (bit-exact).
+
+Every launch goes through the C ABI (rh_commit_soa_launch / rh_groups_*).  The oracle is
+oracle/ratis_oracle.c (orc_commit_soa), itself pinned in tests/test_oracle.py."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _bits(words, n):
+    w = np.asarray(words).view(np.uint64)
+    return np.unpackbits(w.view(np.uint8), bitorder="little")[:n].astype(bool)
+
+
+def _run_gpu(ctx, follower, flush, conf, commit, ts, mode=0, gap=-1, levels=True, col_stride=None):
+    import torch
+
+    from ratis_amd import engine
+    F, n = follower.shape
+    dev = "cuda"
+    if col_stride is not None and col_stride != n:
+        big = torch.full((F, col_stride), -7, dtype=torch.int64, device=dev)
+        big[:, :n] = torch.from_numpy(follower).to(dev)
+        fi = big[:, :n]          # strided view: col_stride passes through the ABI
+    else:
+        fi = torch.from_numpy(np.ascontiguousarray(follower)).to(dev)
+    t = engine.CommitTier(follower_index=fi, self_index=torch.from_numpy(flush).to(dev),
+                          conf=torch.from_numpy(conf.astype(np.uint32).view(np.int32)).to(dev),
+                          commit_in=torch.from_numpy(commit).to(dev), term_start=torch.from_numpy(ts).to(dev),
+                          gap_threshold=gap)
+    t.alloc_outputs(mode=mode, levels=levels)
+    engine.commit_launch(ctx, [t], mode=mode)
+    torch.cuda.synchronize()
+    out = {"min": t.min_out.cpu().numpy(), "valid": _bits(t.valid_bits.cpu().numpy(), n)}
+    if mode == 0:
+        out["commit"] = t.commit_out.cpu().numpy()
+        out["adv"] = _bits(t.advanced_bits.cpu().numpy(), n)
+    if levels or mode == 1:
+        out["maj"] = t.maj_out.cpu().numpy()
+        out["max"] = t.max_out.cpu().numpy()
+    return out
+
+
+def _check(ctx, orc, follower, flush, conf, commit, ts, mode=0, gap=-1, col_stride=None):
+    got = _run_gpu(ctx, follower, flush, conf, commit, ts, mode=mode, gap=gap, col_stride=col_stride)
+    ref = orc.commit_soa(follower, flush, conf, mode=mode, gap=gap,
+                         commit_in=commit if mode == 0 else None, term_start=ts if mode == 0 else None)
+    n = flush.size
+    v_ref = _bits(ref["valid_bits"], n)
+    assert np.array_equal(got["valid"], v_ref)
+    assert np.array_equal(got["min"], ref["min"])
+    assert np.array_equal(got["maj"], ref["maj"])
+    assert np.array_equal(got["max"], ref["max"])
+    if mode == 0:
+        assert np.array_equal(got["commit"], ref["commit"])
+        assert np.array_equal(got["adv"], _bits(ref["advanced_bits"], n))
+    return got
+
+
+def _random_case(rng, F, n, lo=-1, hi=60, full_masks=False):
+    follower = rng.integers(lo, hi, size=(F, n)).astype(np.int64)
+    flush = rng.integers(lo, hi, size=n).astype(np.int64)
+    commit = rng.integers(lo, hi, size=n).astype(np.int64)
+    ts = rng.integers(0, hi, size=n).astype(np.int64)
+    fm = (1 << F) - 1
+    newm = rng.integers(0, 1 << F, size=n).astype(np.uint32)
+    oldm = rng.integers(0, 1 << F, size=n).astype(np.uint32)
+    flags = rng.integers(0, 16, size=n).astype(np.uint32)
+    if full_masks:
+        newm[:] = fm
+    conf = ((newm & fm) | ((flags & 1) << 14) | (((flags >> 1) & 1) << 15) | ((oldm & fm) << 16)
+            | (((flags >> 2) & 1) << 30) | (np.uint32(1) << 31)).astype(np.uint32)
+    inactive = rng.random(n) < 0.05
+    conf[inactive] &= np.uint32(0x7FFFFFFF)
+    return follower, flush, conf, commit, ts
+
+
+@pytest.mark.parametrize("F", list(range(1, 15)))
+def test_every_follower_width(ctx, orc, F):
+    rng = np.random.default_rng(100 + F)
+    n = 3001  # ragged: not a multiple of the 512-group tile
+    for gap in (-1, 0, 9):
+        _check(ctx, orc, *_random_case(rng, F, n), mode=0, gap=gap)
+    _check(ctx, orc, *_random_case(rng, F, n), mode=1)
+
+
+def test_golden_cases_on_gpu(ctx, orc):
+    cases = json.load(open(os.path.join(HERE, "golden", "commit_cases.json")))["cases"]
+    F = 4
+    n = len(cases)
+    follower = np.full((F, n), -1, dtype=np.int64)
+    flush = np.zeros(n, dtype=np.int64)
+    commit = np.zeros(n, dtype=np.int64)
+    ts = np.zeros(n, dtype=np.int64)
+    conf = np.zeros(n, dtype=np.uint32)
+    gaps = set(c["gap"] for c in cases)
+    for gap in gaps:
+        idx = [i for i, c in enumerate(cases) if c["gap"] == gap]
+        for j, i in enumerate(idx):
+            c = cases[i]
+            k = len(c["followers"])
+            follower[:k, i] = c["followers"]
+            flush[i] = c["self_index"]
+            commit[i] = c["last_committed"]
+            ts[i] = c["term_start"]
+            nm = sum(b << q for q, b in enumerate(c["in_new"]))
+            om = sum(b << q for q, b in enumerate(c["in_old"]))
+            conf[i] = nm | (c["include_self"] << 14) | (c["transitional"] << 15) | (om << 16) | (
+                c["include_self_old"] << 30) | (1 << 31)
+        got = _run_gpu(ctx, follower[:, idx], flush[idx], conf[idx], commit[idx], ts[idx], mode=0, gap=gap)
+        for j, i in enumerate(idx):
+            c = cases[i]
+            exp = c["expected"]
+            assert got["valid"][j] == (exp is not None), c["name"]
+            if exp is not None:
+                assert (got["min"][j], got["maj"][j], got["max"][j]) == (exp["min"], exp["majority"], exp["max"]), c["name"]
+            assert got["commit"][j] == c["expected_commit"], c["name"]
+
+
+def test_extreme_values_and_ties(ctx, orc):
+    rng = np.random.default_rng(11)
+    F, n = 6, 4096
+    pool = np.array([-(1 << 63), -2, -1, 0, 1, 2, (1 << 62), (1 << 63) - 1], dtype=np.int64)
+    follower = pool[rng.integers(0, pool.size, size=(F, n))]
+    flush = pool[rng.integers(0, pool.size, size=n)]
+    commit = pool[rng.integers(0, pool.size, size=n)]
+    ts = pool[rng.integers(0, pool.size, size=n)]
+    _, _, conf, _, _ = _random_case(rng, F, n)
+    for gap in (-1, 0, 1, (1 << 63) - 1):
+        _check(ctx, orc, follower, flush, conf, commit, ts, mode=0, gap=gap)
+
+
+def test_padded_column_stride_scalar_path(ctx, orc):
+    rng = np.random.default_rng(12)
+    F, n = 4, 1000
+    _check(ctx, orc, *_random_case(rng, F, n), mode=0, gap=3, col_stride=1027)  # odd stride: no 16-B loads
+
+
+def test_fused_multi_tier_launch_and_compaction(ctx, orc):
+    import torch
+
+    from ratis_amd import engine, workload
+    tiers_h = workload.commit_snapshot(200_000, joint_frac=0.1, peers=5, seed=77)
+    tiers_h.append(workload.stable_tier(50_000, seed=78, peers=3))
+    tiers_h.append(workload.stable_tier(7_777, seed=79, peers=9))   # F=8: second kernel class
+    tiers = []
+    total = sum(t.n for t in tiers_h)
+    adv_rows = torch.empty(total, dtype=torch.int64, device="cuda")
+    adv_commit = torch.empty(total, dtype=torch.int64, device="cuda")
+    adv_count = torch.zeros(1, dtype=torch.int64, device="cuda")
+    base = 0
+    for h in tiers_h:
+        t = workload.to_device(h, gap_threshold=2048).alloc_outputs(mode=0, levels=True)
+        t.adv_rows, t.adv_commit, t.adv_count, t.adv_row_base = adv_rows, adv_commit, adv_count, base
+        base += h.n
+        tiers.append(t)
+    engine.commit_launch(ctx, tiers, mode=0)
+    torch.cuda.synchronize()
+    all_adv = []
+    base = 0
+    for h, t in zip(tiers_h, tiers):
+        ref = orc.commit_soa(h.follower, h.flush, h.conf, mode=0, gap=2048, commit_in=h.commit, term_start=h.term_start)
+        assert np.array_equal(t.commit_out.cpu().numpy(), ref["commit"])
+        assert np.array_equal(t.min_out.cpu().numpy(), ref["min"])
+        assert np.array_equal(t.maj_out.cpu().numpy(), ref["maj"])
+        assert np.array_equal(t.max_out.cpu().numpy(), ref["max"])
+        adv = _bits(ref["advanced_bits"], h.n)
+        assert np.array_equal(_bits(t.advanced_bits.cpu().numpy(), h.n), adv)
+        assert np.array_equal(_bits(t.valid_bits.cpu().numpy(), h.n), _bits(ref["valid_bits"], h.n))
+        all_adv.append(np.nonzero(adv)[0] + base)
+        base += h.n
+    k = int(adv_count.item())
+    exp_rows = np.concatenate(all_adv)
+    assert k == exp_rows.size and k > 0
+    rows = adv_rows[:k].cpu().numpy()
+    order = np.argsort(rows)
+    assert np.array_equal(rows[order], exp_rows)
+    commits = np.concatenate([t.commit_out.cpu().numpy() for t in tiers])
+    assert np.array_equal(adv_commit[:k].cpu().numpy()[order], commits[exp_rows])
+
+
+def test_full_size_config3_parity(ctx, orc):
+    """BASELINE config 3 at full size: 1M groups x 5 peers, 10% joint, both gap settings."""
+    import torch
+
+    from ratis_amd import engine, workload
+    tiers_h = workload.commit_snapshot(1_000_000, joint_frac=0.1, peers=5)
+    for gap in (-1, 2048):
+        tiers = [workload.to_device(h, gap_threshold=gap).alloc_outputs(mode=0) for h in tiers_h]
+        engine.commit_launch(ctx, tiers, mode=0)
+        torch.cuda.synchronize()
+        for h, t in zip(tiers_h, tiers):
+            ref = orc.commit_soa(h.follower, h.flush, h.conf, mode=0, gap=gap, commit_in=h.commit,
+                                 term_start=h.term_start)
+            assert np.array_equal(t.commit_out.cpu().numpy(), ref["commit"])
+            assert np.array_equal(t.min_out.cpu().numpy(), ref["min"])
+            adv = _bits(ref["advanced_bits"], h.n)
+            assert np.array_equal(_bits(t.advanced_bits.cpu().numpy(), h.n), adv)
+            assert 0.05 < adv.mean() < 0.95   # both branches of the commit decision are exercised
+
+
+def test_group_table_api_with_deltas(ctx, orc):
+    """RaftGroupTable (rh_groups_*): bulk load, delta streaming (updateToMax), batched
+    updateCommit and commitIndexChanged, against the oracle replaying the same host state."""
+    from ratis_amd import groups, workload
+    rng = np.random.default_rng(21)
+    h = workload.stable_tier(10_000, seed=5, peers=5)
+    F, n = h.follower.shape
+    tab = groups.RaftGroupTable(ctx, capacity=n, n_followers=F, gap_threshold=-1)
+    try:
+        fcommit = h.follower - rng.integers(0, 100, size=h.follower.shape)
+        tab.load(0, n, match=h.follower, fcommit=fcommit, flush=h.flush, commit=h.commit, term_start=h.term_start,
+                 conf=h.conf)
+        match = h.follower.copy()
+        flush = h.flush.copy()
+        commit = h.commit.copy()
+        for rnd in range(3):
+            # followers ack: some go forward, some stale (updateToMax keeps the max)
+            k = 5000
+            slots = rng.integers(0, n, size=k)
+            col = rng.integers(0, F, size=k)
+            val = match[col, slots] + rng.integers(-50, 3000, size=k)
+            tab.push_deltas(slots, col, val)
+            np.maximum.at(match, (col, slots), val)
+            fs = rng.integers(0, n, size=1000)
+            fv = flush[fs] + rng.integers(0, 500, size=1000)
+            tab.update_flush_index(fs, fv)
+            np.maximum.at(flush, fs, fv)
+            got_slots, got_commit, got_min = tab.update_commit(want_min=True)
+            ref = orc.commit_soa(match, flush, h.conf, mode=0, gap=-1, commit_in=commit, term_start=h.term_start)
+            adv = np.nonzero(_bits(ref["advanced_bits"], n))[0]
+            assert np.array_equal(got_slots.astype(np.int64), adv)
+            assert np.array_equal(got_commit, ref["commit"][adv])
+            assert np.array_equal(got_min, ref["min"])
+            commit = ref["commit"]
+            assert np.array_equal(tab.read_commit(), commit)
+        mn, mj, mx, valid = tab.commit_index_changed()
+        ref = orc.commit_soa(fcommit, commit, h.conf, mode=1)
+        assert np.array_equal(valid, _bits(ref["valid_bits"], n))
+        assert np.array_equal(mn, ref["min"]) and np.array_equal(mj, ref["maj"]) and np.array_equal(mx, ref["max"])
+    finally:
+        tab.close()
+
+
+def test_group_table_rejects_bad_input(ctx):
+    from ratis_amd import _lib, groups
+    tab = groups.RaftGroupTable(ctx, capacity=100, n_followers=2)
+    try:
+        with pytest.raises(_lib.IllegalArgumentError):
+            tab.set_group(5, _lib.conf_pack(0b100, True, False, 0, False), 1, 1, 1)   # slot 2 >= F
+        with pytest.raises(_lib.IllegalArgumentError):
+            tab.push_deltas([100], [0], [1])                                        # slot out of range
+        with pytest.raises(_lib.IllegalArgumentError):
+            tab.push_deltas([1], [7], [1])                                          # column >= F
+        tab.set_group(5, _lib.conf_pack(0b11, True, False, 0, False), 10, 2, 0)
+        tab.update_match_index([5], 0, [9])
+        tab.update_match_index([5], 1, [8])
+        slots, commits, _ = tab.update_commit()
+        assert list(slots) == [5] and list(commits) == [9]   # sorted [8,9,10] -> majority 9
+    finally:
+        tab.close()

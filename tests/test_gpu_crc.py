@@ -1,0 +1,211 @@
+"""GPU parity of the CRC32C frame kernel against the CPU oracle (bit-exact), through the C ABI.
+
+Covers PureJavaCrc32C semantics (RFC 3720 answers, every span length/alignment, continuation
+from a non-reset state = TestPureJavaCrc32C's split invariance), the SegmentedRaftLog frame
+writer/verifier (TestRaftLogReadWrite scenario and corruption), every kernel variant, frames
+ending at the very end of the buffer, malformed frame tables, and the config-5 synthetic
+segments (a reduced segment count; the full 8 GiB run is checked in bench.py)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _dev(a, dt=None):
+    import torch
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if dt is not None:
+        t = t.to(dt)
+    return t.to("cuda")
+
+
+def _batch(img, offs, lens):
+    import torch
+
+    from ratis_amd import engine
+    return engine.FrameBatch(buf=_dev(img.astype(np.uint8)), frame_off=_dev(offs.astype(np.int64)),
+                             frame_len=_dev(lens.astype(np.int32))).alloc_outputs()
+
+
+def _bits(words, n):
+    return np.unpackbits(np.asarray(words).view(np.uint64).view(np.uint8), bitorder="little")[:n].astype(bool)
+
+
+def test_rfc3720_known_answers(ctx):
+    from ratis_amd import engine
+    ref = json.load(open(os.path.join(HERE, "golden", "crc_reference.json")))
+    for v in ref["rfc3720"]:
+        data = np.frombuffer(bytes.fromhex(v["hex"]), dtype=np.uint8)
+        assert engine.crc32c_bytes(ctx, _dev(data)) == int(v["crc"], 16), v["name"]
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+def test_every_length_and_alignment(ctx, orc, variant):
+    """Spans of every length 0..700 at every start alignment 0..15 (plain spans, flags=0)."""
+    import torch
+
+    from ratis_amd import engine
+    rng = np.random.default_rng(variant)
+    buf = rng.integers(0, 256, size=1 << 20, dtype=np.uint8)
+    offs, lens = [], []
+    pos = 0
+    for L in range(0, 701):
+        a = L % 16
+        pos = (pos + 15) // 16 * 16 + a
+        offs.append(pos)
+        lens.append(L)
+        pos += L + 1
+    offs = np.array(offs, dtype=np.int64)
+    lens = np.array(lens, dtype=np.int32)
+    fb = _batch(buf, offs, lens)
+    engine.crc32c_frames(ctx, fb, flags=0, variant=variant)
+    torch.cuda.synchronize()
+    got = fb.crc_out.cpu().numpy().view(np.uint32)
+    want = np.array([orc.crc32c(buf[o:o + l].tobytes()) for o, l in zip(offs, lens)], dtype=np.uint32)
+    assert np.array_equal(got, want)
+
+
+def test_long_spans_multiwindow(ctx, orc):
+    import torch
+
+    from ratis_amd import engine
+    rng = np.random.default_rng(3)
+    buf = rng.integers(0, 256, size=3 << 20, dtype=np.uint8)
+    lens = np.array([4095, 4096, 4097, 8191, 65536 + 13, 1 << 20, (1 << 20) + 7], dtype=np.int32)
+    offs = np.array([1, 8, 5000, 20000, 40001, 200003, 1 << 21], dtype=np.int64)
+    for v in range(engine.crc32c_num_variants()):
+        fb = _batch(buf, offs, lens)
+        engine.crc32c_frames(ctx, fb, flags=0, variant=v)
+        torch.cuda.synchronize()
+        got = fb.crc_out.cpu().numpy().view(np.uint32)
+        want = np.array([orc.crc32c(buf[o:o + l].tobytes()) for o, l in zip(offs, lens)], dtype=np.uint32)
+        assert np.array_equal(got, want), v
+
+
+def test_continuation_state_split_invariance(ctx, orc):
+    """update(a) then update(b) == update(a||b): the kernel continues from any PureJavaCrc32C state
+    (init_state) -- TestPureJavaCrc32C.java:31-58 split invariance."""
+    import torch
+
+    from ratis_amd import engine
+    rng = np.random.default_rng(9)
+    data = rng.integers(0, 256, size=20000, dtype=np.uint8)
+    for split in (0, 1, 2, 3, 4, 5, 63, 64, 65, 4095, 4096, 12345, 20000):
+        s1 = orc.crc32c_update(0xFFFFFFFF, data[:split].tobytes())
+        v = engine.crc32c_bytes(ctx, _dev(data[split:]), init_state=s1)
+        assert v == orc.crc32c(data.tobytes()), split
+    for n in range(0, 9):   # sub-4-byte messages from an arbitrary state
+        st = 0x12345678
+        d = data[:n].tobytes()
+        assert engine.crc32c_bytes(ctx, _dev(data[:n]), init_state=st) == (~orc.crc32c_update(st, d)) & 0xFFFFFFFF
+
+
+def test_raftlog_readwrite_segment_stamp_and_verify(ctx, orc):
+    """TestRaftLogReadWrite scenario: the GPU writer stamps the same CRCs the oracle writer does;
+    the verifier accepts the segment, then flags the frame holding byte 100 after corruption."""
+    import torch
+
+    from ratis_amd import _lib, engine, segment
+    z = np.load(os.path.join(HERE, "golden", "raftlog_rw.npz"))
+    protos = segment.simple_operation_entries(100, term=0)
+    img, offs, lens = segment.build_segment(protos, preallocate_to=int(z["expected_size"]) + 4096)
+    fb = _batch(img, offs, lens)
+    engine.crc32c_frames(ctx, fb, flags=_lib.RH_CRC_STAMP)
+    torch.cuda.synchronize()
+    stamped = fb.buf.cpu().numpy()
+    assert np.array_equal(stamped[: z["image"].size], z["image"])          # byte-identical segment
+    assert np.array_equal(fb.crc_out.cpu().numpy().view(np.uint32), z["crc"])
+    fb.n_bad.zero_()
+    engine.crc32c_frames(ctx, fb, flags=_lib.RH_CRC_VERIFY)
+    torch.cuda.synchronize()
+    assert int(fb.n_bad.item()) == 0
+    # corrupt byte 100 (TestRaftLogReadWrite.java:251-257)
+    fb.buf[100] = (fb.buf[100].to(torch.int32) + 1).to(torch.uint8)
+    fb.n_bad.zero_()
+    fb.bad_bits.zero_()
+    engine.crc32c_frames(ctx, fb, flags=_lib.RH_CRC_VERIFY)
+    torch.cuda.synchronize()
+    bad = np.nonzero(_bits(fb.bad_bits.cpu().numpy(), fb.n))[0]
+    holder = np.nonzero((offs <= 100) & (100 < offs + lens))[0]
+    assert list(bad) == list(holder) and int(fb.n_bad.item()) == 1
+    # the oracle reader stops with a ChecksumException at the same frame
+    _, _, _, st, stop = orc.segment_scan(fb.buf.cpu().numpy())
+    assert st == orc.ORC_E_CHECKSUM and stop == offs[holder[0]]
+
+
+def test_verify_host_roundtrip_matches_oracle(ctx, orc):
+    import ctypes
+
+    from ratis_amd import _lib, segment
+    protos = [segment.log_entry(3, i + 1, segment.state_machine_log_entry(bytes([i % 251]) * (i * 37 % 5000)))
+              for i in range(300)]
+    frames = [orc.frame_write(p) for p in protos]
+    img = np.frombuffer(segment.HEADER + b"".join(frames), dtype=np.uint8).copy()
+    lens = np.array([len(f) for f in frames], dtype=np.uint32)
+    offs = (8 + np.concatenate([[0], np.cumsum(lens)[:-1]])).astype(np.uint64)
+    img[offs[17] + 3] ^= 0x40
+    crc = np.zeros(300, dtype=np.uint32)
+    bits = np.zeros(5, dtype=np.uint64)
+    nbad = ctypes.c_uint64()
+    _lib.check(_lib.load().rh_crc32c_verify_host(ctx.handle, img.ctypes.data, img.size, offs.ctypes.data,
+                                                 lens.ctypes.data, 300, crc.ctypes.data, bits.ctypes.data,
+                                                 ctypes.byref(nbad)))
+    want, nb = orc.crc32c_frames(img, offs, lens)
+    assert np.array_equal(crc, want) and nbad.value == nb == 1
+    assert np.nonzero(_bits(bits, 300))[0].tolist() == [17]
+
+
+def test_frames_at_buffer_end_and_malformed(ctx, orc):
+    """A frame ending exactly at buf_len (odd length) reads nothing past the buffer; frames that
+    overflow the buffer or are shorter than their trailer are reported bad, not read."""
+    import torch
+
+    from ratis_amd import _lib, engine
+    rng = np.random.default_rng(4)
+    for total in (4099, 4101, 77, 1000003):
+        buf = rng.integers(0, 256, size=total, dtype=np.uint8)
+        L = min(total - 3, 70000)
+        o = total - L
+        c = orc.crc32c(buf[o:o + L - 4].tobytes())
+        buf[o + L - 4:o + L] = np.frombuffer(c.to_bytes(4, "big"), dtype=np.uint8)
+        offs = np.array([o, 0, total - 2, 5], dtype=np.int64)
+        lens = np.array([L, total + 1, 4, 3], dtype=np.int32)
+        fb = _batch(buf, offs, lens)
+        engine.crc32c_frames(ctx, fb, flags=_lib.RH_CRC_VERIFY)
+        torch.cuda.synchronize()
+        bad = _bits(fb.bad_bits.cpu().numpy(), 4)
+        assert list(bad) == [False, True, True, True]
+        assert int(fb.crc_out[0].item()) & 0xFFFFFFFF == c
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 3])
+def test_config5_segments_reduced(ctx, orc, variant):
+    """BASELINE config 5 shape (32 MiB segments, 4 KiB frames), 6 segments: every frame verifies
+    except the planted corruptions; the segment parses as a valid Ratis segment in the oracle."""
+    import torch
+
+    from ratis_amd import _lib, engine, workload
+    ss = workload.synth_segments(ctx, n_segments=6, corrupt_rate=2e-4, seed=31 + variant)
+    fb = ss.batch
+    fb.n_bad.zero_()
+    fb.bad_bits.zero_()
+    engine.crc32c_frames(ctx, fb, flags=_lib.RH_CRC_VERIFY, variant=variant)
+    torch.cuda.synchronize()
+    bad = np.nonzero(_bits(fb.bad_bits.cpu().numpy(), fb.n))[0]
+    assert np.array_equal(bad, ss.corrupted) and ss.corrupted.size > 0
+    assert int(fb.n_bad.item()) == ss.corrupted.size
+    seg0 = fb.buf[: ss.segment_size].cpu().numpy()
+    offs, lens, crcs, st, stop = orc.segment_scan(seg0)
+    n0 = ss.frames_per_segment
+    first_bad = ss.corrupted[0] if ss.corrupted[0] < n0 else None
+    if first_bad is None:
+        assert st == orc.ORC_END and offs.size == n0
+        assert np.all(lens == ss.frame_size)
+        assert np.array_equal(crcs, fb.crc_out[:n0].cpu().numpy().view(np.uint32))
+    else:
+        assert st == orc.ORC_E_CHECKSUM and offs.size == first_bad

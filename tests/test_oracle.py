@@ -1,0 +1,245 @@
+"""CPU tests of the parity oracle against the reference's pins (no GPU).
+
+The oracle must be trusted before it judges the HIP path:
+  * CRC32C: table identity with PureJavaCrc32C.java:167-688 (hash fixture; direct text compare
+    when /root/reference is mounted), RFC 3720 known answers, TestPureJavaCrc32C's
+    array == ByteBuffer split invariance (TestPureJavaCrc32C.java:31-58).
+  * Commit: hand-derived golden cases, two independent restatements agreeing exhaustively on
+    small confs, and TestPeerConfiguration's majority-count rule (TestPeerConfiguration.java:45-70).
+  * Frames: TestRaftLogReadWrite's size formula, corruption and padding behaviour
+    (TestRaftLogReadWrite.java:98-121, 161-268).
+"""
+import hashlib
+import itertools
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+from ratis_amd import segment
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = os.path.join(HERE, "golden")
+PJC = "/root/reference/ratis-common/src/main/java/org/apache/ratis/util/PureJavaCrc32C.java"
+
+
+# ---------------------------------------------------------------------------------------------
+# CRC32C
+# ---------------------------------------------------------------------------------------------
+def test_crc_table_matches_reference_hash(orc):
+    ref = json.load(open(os.path.join(GOLD, "crc_reference.json")))
+    t = orc.crc32c_tables()
+    assert hashlib.sha256(t.astype("<u4").tobytes()).hexdigest() == ref["table_sha256"]
+
+
+@pytest.mark.skipif(not os.path.exists(PJC), reason="reference tree not mounted")
+def test_crc_table_matches_reference_text(orc):
+    import re
+    src = open(PJC).read()
+    body = src[src.index("private static final int[] T = new int[] {"):]
+    body = body[:body.index("};")]
+    vals = np.array([int(x, 16) for x in re.findall(r"0x([0-9A-Fa-f]{8})", body)], dtype=np.uint32)
+    assert np.array_equal(vals, orc.crc32c_tables())
+
+
+def test_crc_rfc3720(orc):
+    ref = json.load(open(os.path.join(GOLD, "crc_reference.json")))
+    for v in ref["rfc3720"]:
+        data = bytes.fromhex(v["hex"])
+        assert orc.crc32c(data) == int(v["crc"], 16), v["name"]
+        assert orc.crc32c_py(data) == int(v["crc"], 16), v["name"]
+
+
+def test_crc_empty_and_small(orc):
+    assert orc.crc32c(b"") == 0
+    for n in range(0, 40):
+        d = bytes((7 * i + 3) & 0xFF for i in range(n))
+        assert orc.crc32c(d) == orc.crc32c_py(d)
+
+
+def test_crc_array_equals_bytebuffer_split_invariance(orc):
+    """TestPureJavaCrc32C.runTestByteBuffer: random lengths around powers of 4, random splits."""
+    rng = random.Random(1234)
+    length = 1
+    while length < 1 << 16:
+        for L in (length - 1, length, length + 1):
+            data = bytes(rng.getrandbits(8) for _ in range(L))
+            sa = sb = 0xFFFFFFFF
+            off = 0
+            while off < L:
+                k = rng.randrange(L - off) + 1
+                sa = orc.crc32c_update(sa, data[off:off + k])
+                sb = orc.crc32c_update(sb, data[off:off + k], bytebuffer=True)
+                assert sa == sb
+                off += k
+            assert (~sa) & 0xFFFFFFFF == orc.crc32c(data)
+        length <<= 2
+
+
+# ---------------------------------------------------------------------------------------------
+# Commit arithmetic
+# ---------------------------------------------------------------------------------------------
+def test_commit_golden_cases(orc):
+    cases = json.load(open(os.path.join(GOLD, "commit_cases.json")))["cases"]
+    assert len(cases) >= 15
+    for c in cases:
+        args = (c["followers"], c["in_new"], c["in_old"], c["include_self"], c["transitional"],
+                c["include_self_old"], c["self_index"], c["gap"])
+        exp = c["expected"]
+        exp = None if exp is None else (exp["min"], exp["majority"], exp["max"])
+        assert orc.get_majority_min(*args) == exp, c["name"]
+        assert orc.py_get_majority_min(*args) == exp, c["name"]
+
+
+def test_commit_two_restatements_agree_exhaustive(orc):
+    """Every new/old mask and self flag for 3 follower slots, values with ties and -1."""
+    rng = random.Random(7)
+    pool = [-1, -1, 0, 3, 3, 7, 100]
+    for _ in range(6):
+        vals = [rng.choice(pool) for _ in range(3)]
+        self_v = rng.choice(pool)
+        for bits in range(1 << 9):
+            a = [(bits >> i) & 1 for i in range(3)]
+            b = [(bits >> (3 + i)) & 1 for i in range(3)]
+            inc, tr, inco = (bits >> 6) & 1, (bits >> 7) & 1, (bits >> 8) & 1
+            for gap in (-1, 0, 4):
+                args = (vals, a, b, inc, tr, inco, self_v, gap)
+                assert orc.get_majority_min(*args) == orc.py_get_majority_min(*args), args
+
+
+def test_majority_is_the_quorum_order_statistic(orc):
+    """PeerConfiguration.hasMajority counts num > size/2 (PeerConfiguration.java:152-169,
+    pinned by TestPeerConfiguration odd/even quorum tests): the chosen majority index m must be
+    reached by a majority of voters, and no larger value is."""
+    rng = random.Random(99)
+    for _ in range(2000):
+        n = rng.randint(1, 7)
+        vals = [rng.randint(-1, 20) for _ in range(n)]
+        r = orc.get_majority_min(vals[:-1], [1] * (n - 1), [0] * (n - 1), 1, 0, 0, vals[-1], -1)
+        m = r[1]
+        acked = sum(1 for v in vals if v >= m)
+        assert acked > n // 2
+        bigger = [v for v in vals if v > m]
+        if bigger:
+            m2 = min(bigger)
+            assert not sum(1 for v in vals if v >= m2) > n // 2
+
+
+def test_literal_term_lookup_equals_term_start_rule(orc):
+    """RaftLogBase.updateCommitIndex's termAt(newCommit)==currentTerm over a monotone-term log
+    equals `newCommit >= termStart` (the rule the kernel evaluates)."""
+    rng = random.Random(5)
+    for _ in range(3000):
+        log_start = rng.randint(0, 20)
+        n_terms = rng.randint(1, 40)
+        cur = 5
+        ts = log_start + rng.randint(0, n_terms)  # first index of the current term (maybe none)
+        terms = [cur if log_start + i >= ts else rng.randint(1, cur - 1) for i in range(n_terms)]
+        terms_sorted = sorted(terms[: ts - log_start]) + terms[ts - log_start:]
+        flush = log_start + n_terms - 1
+        lc = rng.randint(-1, flush + 2)
+        maj = rng.randint(-1, flush + 5)
+        commit, adv, _ = orc.update_commit(lc, maj, 0, flush, cur, log_start, terms_sorted)
+        nc = min(maj, flush)
+        rule = maj > lc and lc < nc and log_start <= nc <= flush and nc >= ts
+        assert adv == rule
+        assert commit == (nc if rule else lc)
+
+
+def test_commit_soa_matches_per_group(orc):
+    rng = np.random.default_rng(3)
+    F, n = 4, 500
+    follower = rng.integers(-1, 50, size=(F, n))
+    flush = rng.integers(-1, 60, size=n)
+    commit = rng.integers(-1, 40, size=n)
+    ts = rng.integers(0, 60, size=n)
+    conf = rng.integers(0, 1 << 32, size=n, dtype=np.uint64).astype(np.uint32)
+    conf &= np.uint32(0xFFFF_FFFF) & ~np.uint32(((0x3FFF & ~0xF) | ((0x3FFF & ~0xF) << 16)))
+    out = orc.commit_soa(follower, flush, conf, mode=0, gap=7, commit_in=commit, term_start=ts)
+    for g in range(n):
+        w = int(conf[g])
+        a = [(w >> i) & 1 for i in range(F)]
+        b = [(w >> (16 + i)) & 1 for i in range(F)]
+        r = None
+        if w >> 31 & 1:
+            r = orc.py_get_majority_min(list(follower[:, g]), a, b, (w >> 14) & 1, (w >> 15) & 1, (w >> 30) & 1,
+                                        int(flush[g]), 7)
+        valid = bool(out["valid_bits"][g // 64] >> np.uint64(g % 64) & np.uint64(1))
+        assert valid == (r is not None)
+        c = int(commit[g])
+        if r is not None:
+            assert (out["min"][g], out["maj"][g], out["max"][g]) == r
+            nc = min(r[1], int(flush[g]))
+            if r[1] > c and c < nc and nc >= ts[g]:
+                c = nc
+        assert out["commit"][g] == c
+
+
+# ---------------------------------------------------------------------------------------------
+# Frames (TestRaftLogReadWrite)
+# ---------------------------------------------------------------------------------------------
+def _rw_fixture():
+    return np.load(os.path.join(GOLD, "raftlog_rw.npz"))
+
+
+def test_frame_size_formula_and_writer(orc):
+    z = _rw_fixture()
+    protos = segment.simple_operation_entries(100, term=0)
+    img, offs, lens = segment.build_segment(protos)
+    assert img.size == int(z["expected_size"])               # TestRaftLogReadWrite.java:98,121
+    assert np.array_equal(offs, z["frame_off"]) and np.array_equal(lens, z["frame_len"])
+    # frame writer restatement == layout + CRC trailer
+    for p, o, l, c in zip(protos, offs, lens, z["crc"]):
+        fb = orc.frame_write(p)
+        assert len(fb) == l and fb[-4:] == int(c).to_bytes(4, "big")
+        assert bytes(z["image"][o:o + l]) == fb
+
+
+def test_reader_accepts_segment_and_zero_padding(orc):
+    z = _rw_fixture()
+    img = np.concatenate([z["image"], np.zeros(4096, np.uint8)])   # preallocated zero fill
+    offs, lens, crcs, st, _ = orc.segment_scan(img)
+    assert st == orc.ORC_END and len(offs) == 100
+    assert np.array_equal(crcs, z["crc"])
+
+
+def test_reader_detects_entry_corruption(orc):
+    """TestRaftLogReadWrite.testReadWithEntryCorruption: byte 100 += 1 -> ChecksumException."""
+    z = _rw_fixture()
+    img = z["image"].copy()
+    img[100] = (int(img[100]) + 1) & 0xFF
+    offs, lens, crcs, st, stop = orc.segment_scan(img)
+    assert st == orc.ORC_E_CHECKSUM
+    assert offs.size < 100 and stop <= 100 < stop + lens.max() + 8
+
+
+def test_reader_rejects_corrupt_padding(orc):
+    """TestRaftLogReadWrite.testReadWithCorruptPadding: non-zero bytes after the terminator."""
+    z = _rw_fixture()
+    img = np.concatenate([z["image"], np.zeros(4096, np.uint8)])
+    img[-10] = 0xFF
+    img[-9] = 1
+    offs, _, _, st, _ = orc.segment_scan(img)
+    assert st == orc.ORC_E_PADDING and offs.size == 100
+
+
+def test_reader_partial_last_entry(orc):
+    """A truncated last entry is ignored (readEntry returns null on EOFException)."""
+    z = _rw_fixture()
+    img = z["image"][: int(z["frame_off"][-1]) + 5]
+    offs, _, _, st, _ = orc.segment_scan(img)
+    assert st == orc.ORC_PARTIAL and offs.size == 99
+
+
+def test_reader_oversize_entry(orc):
+    img = np.frombuffer(segment.HEADER + segment.varint(5 << 20) + b"x" * 16, dtype=np.uint8)
+    _, _, _, st, _ = orc.segment_scan(img, max_op=4 << 20)
+    assert st == orc.ORC_E_OVERSIZE
+
+
+def test_reader_header_states(orc):
+    assert orc.load().orc_verify_header(np.frombuffer(b"RaftLog1", np.uint8).ctypes.data, 8) == 1
+    assert orc.load().orc_verify_header(np.frombuffer(b"Raft\0\0\0\0", np.uint8).ctypes.data, 8) == 0
+    assert orc.load().orc_verify_header(np.frombuffer(b"RaftLog2", np.uint8).ctypes.data, 8) == orc.ORC_E_HEADER
