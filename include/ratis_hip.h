@@ -25,8 +25,9 @@
  *     RH_OK (0) or a negative RH_E_* code; rh_last_error() then holds a message for the calling
  *     thread (the Java binding maps RH_E_INVAL to IllegalArgumentException, others to
  *     IOException -- see INTEGRATION.md).
- *   - "_launch" functions take DEVICE pointers, enqueue work on `stream` (a hipStream_t; NULL =
- *     the context's own stream) and return without synchronising.
+ *   - "_launch" functions take DEVICE pointers, enqueue work on `stream` (a hipStream_t, used
+ *     as given: NULL is the HIP null stream; rh_ctx_stream() returns the context's own stream)
+ *     and return without synchronising.
  *   - All log indices are signed 64-bit (Java long); INVALID_LOG_INDEX = -1 is a legal value.
  */
 #ifndef RATIS_HIP_H

@@ -231,8 +231,10 @@ __global__ __launch_bounds__(1024) void crc_frames_kernel(const FrameArgs a) {
             const int nwords = (int)(cnt >> 2);
             const int64_t A = bs + h;                              // first word's address
             uint32_t r = 0;
-            // message position of the chunk's first byte (init injection at positions 0..3)
-            const bool has_start = cnt > 0 && bs == (int64_t)o;
+            // The initial state I is XOR-ed into message positions 0..3 (byte k of I at position
+            // k).  Those positions can be split over two lanes when the first lane holds < 4
+            // bytes, so the injection is by position: p0 = message position of this chunk.
+            const int64_t p0 = bs - (int64_t)o;
 
             // head bytes (at most 3, only the lane that holds the frame start)
             if (h) {
@@ -240,7 +242,7 @@ __global__ __launch_bounds__(1024) void crc_frames_kernel(const FrameArgs a) {
                 for (int i = 0; i < 3; ++i)
                     if (i < h) {
                         uint32_t b = a.buf[bs + i];
-                        if (has_start) b ^= (a.init >> (8 * i)) & 0xffu;
+                        if (p0 + i < 4) b ^= (a.init >> (8 * (p0 + i))) & 0xffu;
                         r = fold_byte<REPL>(lslice, r, b, c);
                     }
             }
@@ -264,7 +266,7 @@ __global__ __launch_bounds__(1024) void crc_frames_kernel(const FrameArgs a) {
                         if (16 * blk + j < nwords) {
                             const uint32_t hi = (j < 15) ? cur[j + 1] : nxt[0];
                             uint32_t w = sh ? __builtin_amdgcn_alignbyte(hi, cur[j], sh) : cur[j];
-                            if (blk == 0 && j == 0 && has_start) w ^= a.init >> (8 * h);
+                            if (blk == 0 && j == 0 && p0 + h < 4) w ^= a.init >> (8 * (p0 + h));
                             r = fold_word<REPL>(lslice, r, w, c);
                         }
                     }

@@ -42,7 +42,9 @@ struct DeviceGuard {
     }
 };
 
-hipStream_t pick_stream(rh_ctx* ctx, void* s) { return s ? reinterpret_cast<hipStream_t>(s) : ctx->stream; }
+// The stream is used exactly as given (NULL = the HIP null stream, which is also what a
+// PyTorch default stream reports); the context stream is only used by the rh_groups calls.
+hipStream_t pick_stream(rh_ctx*, void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 }  // namespace
 

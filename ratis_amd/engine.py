@@ -143,7 +143,7 @@ class CommitTier:
         s.n_followers = fi.shape[0]
         s.mode = mode
         s.gap_threshold = self.gap_threshold if mode == RH_MODE_COMMIT else -1
-        if not fi.is_cuda or fi.stride(1) != 1 or fi.stride(0) < n:
+        if not fi.is_cuda or (fi.stride(1) != 1 and n > 1) or fi.stride(0) < n:
             raise ValueError("follower_index must be a CUDA [F, n] view with unit row stride")
         s.follower_index = fi.data_ptr()
         s.col_stride = fi.stride(0)

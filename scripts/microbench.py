@@ -1,0 +1,49 @@
+"""A/B timing of kernel variants in ONE process (interleaved rounds), for tuning.
+
+    python scripts/microbench.py [--segments 32] [--rounds 5]
+Prints one JSON line per variant: median/min GB/s of frame bytes over the rounds."""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--segments", type=int, default=32)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=10)
+    a = ap.parse_args()
+    import torch
+
+    from ratis_amd import _lib, engine, workload
+    ctx = engine.Context(0)
+    ss = workload.synth_segments(ctx, n_segments=a.segments, corrupt_rate=0)
+    fb = ss.batch
+    nv = engine.crc32c_num_variants()
+    res = {v: [] for v in range(nv)}
+    for r in range(a.rounds):
+        for v in range(nv):
+            engine.crc32c_frames(ctx, fb, flags=_lib.RH_CRC_VERIFY, variant=v)
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.iters):
+                engine.crc32c_frames(ctx, fb, flags=_lib.RH_CRC_VERIFY, variant=v)
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / a.iters
+            res[v].append(ss.frame_bytes / (ms * 1e-3) / 1e9)
+            assert int(fb.n_bad.item()) == 0
+    for v in range(nv):
+        x = np.array(res[v])
+        print(json.dumps({"kernel": "crc32c", "variant": v, "median_GBps": round(float(np.median(x)), 1),
+                          "min_GBps": round(float(x.min()), 1), "max_GBps": round(float(x.max()), 1)}))
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -67,7 +67,8 @@ def test_every_length_and_alignment(ctx, orc, variant):
     torch.cuda.synchronize()
     got = fb.crc_out.cpu().numpy().view(np.uint32)
     want = np.array([orc.crc32c(buf[o:o + l].tobytes()) for o, l in zip(offs, lens)], dtype=np.uint32)
-    assert np.array_equal(got, want)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(int(offs[i]), int(lens[i])) for i in bad[:10]]
 
 
 def test_long_spans_multiwindow(ctx, orc):
@@ -75,7 +76,7 @@ def test_long_spans_multiwindow(ctx, orc):
 
     from ratis_amd import engine
     rng = np.random.default_rng(3)
-    buf = rng.integers(0, 256, size=3 << 20, dtype=np.uint8)
+    buf = rng.integers(0, 256, size=4 << 20, dtype=np.uint8)
     lens = np.array([4095, 4096, 4097, 8191, 65536 + 13, 1 << 20, (1 << 20) + 7], dtype=np.int32)
     offs = np.array([1, 8, 5000, 20000, 40001, 200003, 1 << 21], dtype=np.int64)
     for v in range(engine.crc32c_num_variants()):
