@@ -220,6 +220,9 @@ int rh_crc32c_verify_host(rh_ctx* ctx, const uint8_t* seg, uint64_t seg_len, con
 /* ---- tuning hooks (bench / A-B experiments; results are identical for every variant) ---- */
 /* CRC kernel variants: 0 = 64 lanes x 64 B per 4 KiB window (default), 1 = 16 x 256 B,
  * 2 = 8 x 512 B, 3 = variant 0 with shared (non-replicated, bank-conflicting) tables. */
+/* Commit kernel variants: sub-tiles of 128 groups per wave, 0 = 1, 1 = 2 (default), 2 = 4. */
+int rh_commit_num_variants(void);
+int rh_commit_set_variant(int variant);
 int rh_crc32c_num_variants(void);
 int rh_crc32c_set_variant(int variant);
 int rh_crc32c_frames_launch_variant(rh_ctx* ctx, const rh_frames* frames, uint32_t flags, int variant,

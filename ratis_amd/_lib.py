@@ -124,6 +124,8 @@ _SIGNATURES = {
     "rh_crc32c_verify_host": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_uint64, c_void_p,
                                       c_void_p, POINTER(c_uint64)]),
     "rh_crc32c_num_variants": (c_int, []),
+    "rh_commit_num_variants": (c_int, []),
+    "rh_commit_set_variant": (c_int, [c_int]),
     "rh_crc32c_set_variant": (c_int, [c_int]),
     "rh_crc32c_frames_launch_variant": (c_int, [c_void_p, POINTER(RhFrames), c_uint32, c_int, c_void_p]),
 }

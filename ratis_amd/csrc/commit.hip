@@ -22,7 +22,11 @@ namespace {
 
 constexpr int kBlock = 256;            // 4 waves
 constexpr int kGroupsPerLane = 2;      // 16-byte loads per column per lane
-constexpr int kTile = kBlock * kGroupsPerLane;  // groups per workgroup
+// Sub-tiles (of 128 groups) per wave: the launch variant.  Default 2 => a workgroup covers
+// 1024 groups and a 1M-group batch is ~980 workgroups, one resident round on 256 CUs.
+int g_commit_variant = 1;
+constexpr int kVariantT[] = {1, 2, 4};
+constexpr int kNumCommitVariants = 3;
 
 // ---- Batcher merge-exchange sorting network (Knuth, TAOCP 5.2.2, Algorithm M) ------------
 struct Net {
@@ -122,44 +126,39 @@ __device__ __forceinline__ uint64_t spread32(uint64_t x) {
 typedef int64_t v2i64 __attribute__((ext_vector_type(2)));
 typedef uint32_t v2u32 __attribute__((ext_vector_type(2)));
 
-// One workgroup tile of one tier.  Lane l of wave w handles rows base + 2l and base + 2l + 1
-// with base = tile*kTile + 128*w, so the wave's valid/advanced bits form two whole words.
-template <int F, bool VEC>
-__device__ __forceinline__ void commit_tile(const TierArgs& ta, uint64_t tile) {
-    constexpr int N = F + 1;
-    const rh_commit_soa& t = ta.t;
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const uint64_t wbase = tile * kTile + (uint64_t)wave * 128;
-    const uint64_t r0 = wbase + 2 * (uint64_t)lane;
-    const bool commit_mode = t.mode == RH_MODE_COMMIT;
-
-    // ---- loads (all issued before any compute) ----
+// A 128-group sub-tile of one wave: lane l holds rows r0 = base + 2l and r0 + 1.
+template <int F>
+struct SubTile {
     int64_t fv[2][F];
     int64_t self[2], cin[2], tstart[2];
     uint32_t w[2];
+};
+
+template <int F, bool VEC>
+__device__ __forceinline__ void load_sub(const TierArgs& ta, uint64_t r0, bool commit_mode, SubTile<F>& st) {
+    const rh_commit_soa& t = ta.t;
     if (VEC) {
 #pragma unroll
         for (int k = 0; k < F; ++k) {
             const v2i64 x = *reinterpret_cast<const v2i64*>(t.follower_index + (uint64_t)k * ta.stride + r0);
-            fv[0][k] = x.x;
-            fv[1][k] = x.y;
+            st.fv[0][k] = x.x;
+            st.fv[1][k] = x.y;
         }
         const v2i64 s = *reinterpret_cast<const v2i64*>(t.self_index + r0);
-        self[0] = s.x;
-        self[1] = s.y;
+        st.self[0] = s.x;
+        st.self[1] = s.y;
         const v2u32 c = *reinterpret_cast<const v2u32*>(t.conf + r0);
-        w[0] = c.x;
-        w[1] = c.y;
+        st.w[0] = c.x;
+        st.w[1] = c.y;
         if (commit_mode) {
             const v2i64 ci = *reinterpret_cast<const v2i64*>(t.commit_in + r0);
             const v2i64 ts = *reinterpret_cast<const v2i64*>(t.term_start + r0);
-            cin[0] = ci.x;
-            cin[1] = ci.y;
-            tstart[0] = ts.x;
-            tstart[1] = ts.y;
+            st.cin[0] = ci.x;
+            st.cin[1] = ci.y;
+            st.tstart[0] = ts.x;
+            st.tstart[1] = ts.y;
         } else {
-            cin[0] = cin[1] = tstart[0] = tstart[1] = 0;
+            st.cin[0] = st.cin[1] = st.tstart[0] = st.tstart[1] = 0;
         }
     } else {
 #pragma unroll
@@ -167,13 +166,22 @@ __device__ __forceinline__ void commit_tile(const TierArgs& ta, uint64_t tile) {
             const uint64_t r = r0 + g;
             const bool in = r < t.n;
 #pragma unroll
-            for (int k = 0; k < F; ++k) fv[g][k] = in ? t.follower_index[(uint64_t)k * ta.stride + r] : 0;
-            self[g] = in ? t.self_index[r] : 0;
-            w[g] = in ? t.conf[r] : 0u;  // inactive padding
-            cin[g] = (in && commit_mode) ? t.commit_in[r] : 0;
-            tstart[g] = (in && commit_mode) ? t.term_start[r] : 0;
+            for (int k = 0; k < F; ++k) st.fv[g][k] = in ? t.follower_index[(uint64_t)k * ta.stride + r] : 0;
+            st.self[g] = in ? t.self_index[r] : 0;
+            st.w[g] = in ? t.conf[r] : 0u;  // rows past n: inactive padding
+            st.cin[g] = (in && commit_mode) ? t.commit_in[r] : 0;
+            st.tstart[g] = (in && commit_mode) ? t.term_start[r] : 0;
         }
     }
+}
+
+template <int F, bool VEC>
+__device__ __forceinline__ void compute_store_sub(const TierArgs& ta, uint64_t wbase, bool commit_mode,
+                                                  const SubTile<F>& st) {
+    constexpr int N = F + 1;
+    const rh_commit_soa& t = ta.t;
+    const int lane = threadIdx.x & 63;
+    const uint64_t r0 = wbase + 2 * (uint64_t)lane;
 
     // ---- getMajorityMin (LSI:956-984) ----
     const int64_t gap = commit_mode ? t.gap_threshold : -1;  // 2-arg overload passes -1 (LSI:952-954)
@@ -182,19 +190,20 @@ __device__ __forceinline__ void commit_tile(const TierArgs& ta, uint64_t tile) {
     const uint32_t fmask = (1u << F) - 1u;
     bool trans[2];
 #pragma unroll
-    for (int g = 0; g < 2; ++g) trans[g] = (w[g] & RH_CONF_ACTIVE) && (w[g] & RH_CONF_TRANSITIONAL);
+    for (int g = 0; g < 2; ++g) trans[g] = (st.w[g] & RH_CONF_ACTIVE) && (st.w[g] & RH_CONF_TRANSITIONAL);
     const bool any_trans = __any(trans[0] || trans[1]);
 
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
+        const uint32_t w = st.w[g];
         int64_t vals[N];
 #pragma unroll
-        for (int k = 0; k < F; ++k) vals[k] = fv[g][k];
-        vals[F] = self[g];
-        const uint32_t mnew = (w[g] & fmask) | (((w[g] >> 14) & 1u) << F);
-        const uint32_t mold = ((w[g] >> RH_CONF_OLD_SHIFT) & fmask) | (((w[g] >> 30) & 1u) << F);
+        for (int k = 0; k < F; ++k) vals[k] = st.fv[g][k];
+        vals[F] = st.self[g];
+        const uint32_t mnew = (w & fmask) | (((w >> 14) & 1u) << F);
+        const uint32_t mold = ((w >> RH_CONF_OLD_SHIFT) & fmask) | (((w >> 30) & 1u) << F);
         // followers.isEmpty() && !includeSelf -> Optional.empty()  (LSI:964-966, 976-978)
-        bool v = (w[g] & RH_CONF_ACTIVE) && mnew != 0 && (!trans[g] || mold != 0);
+        const bool v = (w & RH_CONF_ACTIVE) && mnew != 0 && (!trans[g] || mold != 0);
         int64_t a0, a1, a2;
         order_stats<N>(vals, mnew ? mnew : 1u, gap, a0, a1, a2);
         if (any_trans) {
@@ -213,10 +222,10 @@ __device__ __forceinline__ void commit_tile(const TierArgs& ta, uint64_t tile) {
         // ---- updateCommit(majority, min) (LSI:1015-1026) -> RaftLogBase.updateCommitIndex ----
         // old = lastCommitted; if (majority > old) { newCommit = min(majority, flushIndex);
         //   if (old < newCommit && termAt(newCommit) == currentTerm) commit = newCommit; }
-        const int64_t old = cin[g];
-        const int64_t flush = self[g];
+        const int64_t old = st.cin[g];
+        const int64_t flush = st.self[g];
         const int64_t nc = a1 < flush ? a1 : flush;
-        const bool a = commit_mode && v && a1 > old && old < nc && nc >= tstart[g];
+        const bool a = commit_mode && v && a1 > old && old < nc && nc >= st.tstart[g];
         adv[g] = a;
         cout[g] = a ? nc : old;
     }
@@ -297,30 +306,47 @@ __device__ __forceinline__ void commit_tile(const TierArgs& ta, uint64_t tile) {
     }
 }
 
-template <int F>
+// One workgroup tile = 4 waves x T sub-tiles of 128 groups.  All T sub-tiles' loads are
+// issued before any compute, so a wave keeps T x (F+3) x 1 KiB in flight.
+template <int F, int T>
 __device__ __forceinline__ void run_tile(const TierArgs& ta, uint64_t tile) {
-    const bool full = (tile + 1) * kTile <= ta.t.n && ta.vec_ok;
-    if (full)
-        commit_tile<F, true>(ta, tile);
-    else
-        commit_tile<F, false>(ta, tile);
+    constexpr uint64_t kWaveGroups = 128ull * T;
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const uint64_t wchunk = tile * (kWaveGroups * (kBlock / 64)) + (uint64_t)wave * kWaveGroups;
+    const bool commit_mode = ta.t.mode == RH_MODE_COMMIT;
+    if (wchunk >= ta.t.n) return;
+    const bool full = wchunk + kWaveGroups <= ta.t.n && ta.vec_ok;
+    SubTile<F> st[T];
+    if (full) {
+#pragma unroll
+        for (int s = 0; s < T; ++s) load_sub<F, true>(ta, wchunk + 128 * s + 2 * lane, commit_mode, st[s]);
+#pragma unroll
+        for (int s = 0; s < T; ++s) compute_store_sub<F, true>(ta, wchunk + 128 * s, commit_mode, st[s]);
+    } else {
+#pragma unroll
+        for (int s = 0; s < T; ++s) {
+            load_sub<F, false>(ta, wchunk + 128 * s + 2 * lane, commit_mode, st[s]);
+            compute_store_sub<F, false>(ta, wchunk + 128 * s, commit_mode, st[s]);
+        }
+    }
 }
 
 }  // namespace
 
 namespace {
 
-template <int F, int FHI>
+template <int F, int FHI, int T>
 __device__ __forceinline__ void dispatch_f(const TierArgs& ta, uint64_t tile) {
     if (ta.t.n_followers == F)
-        run_tile<F>(ta, tile);
+        run_tile<F, T>(ta, tile);
     else if constexpr (F < FHI)
-        dispatch_f<F + 1, FHI>(ta, tile);
+        dispatch_f<F + 1, FHI, T>(ta, tile);
 }
 
 // One launch evaluates every tier whose F lies in [FLO, FHI]; blocks are assigned to tiers
 // in order.  The F switch is block-uniform, so it costs no divergence.
-template <int FLO, int FHI>
+template <int FLO, int FHI, int T>
 __global__ __launch_bounds__(kBlock) void commit_kernel(const LaunchArgs args) {
     const uint32_t b = blockIdx.x;
     int ti = 0;
@@ -328,12 +354,23 @@ __global__ __launch_bounds__(kBlock) void commit_kernel(const LaunchArgs args) {
     for (int i = 1; i < RH_MAX_TIERS; ++i)
         if (i < args.n_tiers && b >= args.tier[i].block_begin) ti = i;
     const TierArgs& ta = args.tier[ti];
-    dispatch_f<FLO, FHI>(ta, (uint64_t)(b - ta.block_begin));
+    dispatch_f<FLO, FHI, T>(ta, (uint64_t)(b - ta.block_begin));
 }
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
-int launch_class(const rh_commit_soa* tiers, int n_tiers, int flo, int fhi, hipStream_t stream) {
+template <int FLO, int FHI>
+void launch_t(int T, uint32_t blocks, const LaunchArgs& args, hipStream_t stream) {
+    switch (T) {
+        case 1: hipLaunchKernelGGL((commit_kernel<FLO, FHI, 1>), dim3(blocks), dim3(kBlock), 0, stream, args); break;
+        case 2: hipLaunchKernelGGL((commit_kernel<FLO, FHI, 2>), dim3(blocks), dim3(kBlock), 0, stream, args); break;
+        default: hipLaunchKernelGGL((commit_kernel<FLO, FHI, 4>), dim3(blocks), dim3(kBlock), 0, stream, args); break;
+    }
+}
+
+int launch_class(const rh_commit_soa* tiers, int n_tiers, int flo, int fhi, int variant, hipStream_t stream) {
+    const int T = kVariantT[variant];
+    const uint64_t kTile = (uint64_t)kBlock * kGroupsPerLane * T;  // groups per workgroup
     LaunchArgs args{};
     uint64_t blocks = 0;
     for (int i = 0; i < n_tiers; ++i) {
@@ -355,17 +392,26 @@ int launch_class(const rh_commit_soa* tiers, int n_tiers, int flo, int fhi, hipS
     if (args.n_tiers == 0) return RH_OK;
     if (blocks > 0x7FFFFFFFull) return rh::fail(RH_E_RANGE, "commit launch: too many groups");
     if (fhi <= 7)
-        hipLaunchKernelGGL((commit_kernel<1, 7>), dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
+        launch_t<1, 7>(T, (uint32_t)blocks, args, stream);
     else
-        hipLaunchKernelGGL((commit_kernel<8, 14>), dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
+        launch_t<8, 14>(T, (uint32_t)blocks, args, stream);
     RH_HIP(hipGetLastError());
     return RH_OK;
 }
 
 }  // namespace
 
+int rh_commit_set_variant_impl(int v) {
+    if (v < 0 || v >= kNumCommitVariants) return rh::fail(RH_E_INVAL, "unknown commit kernel variant");
+    g_commit_variant = v;
+    return RH_OK;
+}
+
+int rh_commit_num_variants_impl() { return kNumCommitVariants; }
+
 int rh_commit_launch_impl(rh_ctx* ctx, const rh_commit_soa* tiers, int n_tiers, hipStream_t stream) {
     (void)ctx;
+    const int variant = g_commit_variant;
     if (!tiers || n_tiers < 1 || n_tiers > RH_MAX_TIERS)
         return rh::fail(RH_E_INVAL, "rh_commit_soa_launch: n_tiers must be in [1, RH_MAX_TIERS]");
     for (int i = 0; i < n_tiers; ++i) {
@@ -386,9 +432,9 @@ int rh_commit_launch_impl(rh_ctx* ctx, const rh_commit_soa* tiers, int n_tiers, 
         if (t.adv_rows && (!t.adv_commit || !t.adv_count))
             return rh::fail(RH_E_INVAL, "rh_commit_soa_launch: adv_rows needs adv_commit and adv_count");
     }
-    int rc = launch_class(tiers, n_tiers, 1, 7, stream);
+    int rc = launch_class(tiers, n_tiers, 1, 7, variant, stream);
     if (rc != RH_OK) return rc;
-    return launch_class(tiers, n_tiers, 8, 14, stream);
+    return launch_class(tiers, n_tiers, 8, 14, variant, stream);
 }
 
 // ---- delta application: RaftLogIndex.updateToMax per (slot, column) ----------------------

@@ -27,8 +27,6 @@
 
 namespace {
 
-constexpr int kMaxLevels = 8;  // tree levels (log2 Q) + 1 window level
-
 // ---- host: zero-advance linear maps ------------------------------------------------------
 struct Map32 {
     uint32_t col[32];  // image of bit i
@@ -161,7 +159,7 @@ __device__ __forceinline__ void load_block(uint32_t (&d)[16], const uint8_t* buf
 
 // Q lanes per frame window, S bytes per lane (multiple of 16), REPL = replicated tables.
 template <int Q, int S, bool REPL>
-__global__ __launch_bounds__(1024) void crc_frames_kernel(const FrameArgs a) {
+__global__ __launch_bounds__(1024) void crc_frames_kernel(FrameArgs a) {
     constexpr int W = Q * S;
     constexpr int LOGQ = __builtin_ctz(Q);
     constexpr int NB = S / 64;                    // 64-byte blocks per full chunk
@@ -311,6 +309,198 @@ __global__ __launch_bounds__(1024) void crc_frames_kernel(const FrameArgs a) {
     }
 }
 
+// ---- v2: flattened (frame, window) cursor per lane group, one window of data in flight ------
+// Each Q-lane group walks its frames window by window; the chunk of the NEXT window (possibly
+// of the next frame) is loaded before the current one is folded, so HBM latency overlaps the
+// table work.  Chunk = 64 bytes per lane (S = 64): 17 dwords in registers per window.
+struct Cursor {
+    uint64_t f;        // frame index (>= n: exhausted)
+    int64_t o, Lc, E;  // frame start, CRC-covered length, end
+    int64_t nw, wi;    // windows of the frame, current window
+    uint32_t sh;       // E & 3
+    bool malformed;
+};
+
+__device__ __forceinline__ void cursor_frame(const FrameArgs& a, bool trailer, int64_t W, Cursor& c) {
+    c.wi = 0;
+    c.malformed = false;
+    c.o = c.Lc = c.E = c.nw = 0;
+    c.sh = 0;
+    if (c.f >= a.n) return;
+    const uint64_t o = a.off[c.f];
+    const int64_t L = (int64_t)a.len[c.f];
+    c.malformed = o > (uint64_t)a.buf_len || L > a.buf_len - (int64_t)o || (trailer && L < 4);
+    c.o = (int64_t)o;
+    c.Lc = c.malformed ? 0 : L - (trailer ? 4 : 0);
+    c.E = c.o + c.Lc;
+    c.nw = (c.Lc + W - 1) / W;
+    c.sh = (uint32_t)(c.E & 3);
+}
+
+// Chunk geometry of lane `gl` in window `wi` of the cursor's frame.
+struct Chunk {
+    int64_t bs, A, p0;
+    int cnt, h, nwords;
+};
+
+template <int Q, int S>
+__device__ __forceinline__ Chunk chunk_of(const Cursor& c, int gl) {
+    constexpr int64_t W = (int64_t)Q * S;
+    Chunk k;
+    const int64_t be = c.E - (c.nw - 1 - c.wi) * W - (int64_t)(Q - 1 - gl) * S;
+    const int64_t cs = be - S;
+    k.bs = cs > c.o ? cs : c.o;
+    int64_t cnt = be - k.bs;
+    if (c.wi >= c.nw || cnt < 0) cnt = 0;
+    k.cnt = (int)cnt;
+    k.h = k.cnt & 3;
+    k.nwords = k.cnt >> 2;
+    k.A = k.bs + k.h;
+    k.p0 = k.bs - c.o;
+    return k;
+}
+
+template <int Q, int S, bool REPL>
+__global__ __launch_bounds__(REPL ? 1024 : 256) void crc_frames_kernel2(FrameArgs a) {
+    static_assert(S == 64, "v2 keeps one 64-byte chunk per lane in registers");
+    constexpr int64_t W = (int64_t)Q * S;
+    constexpr int LOGQ = __builtin_ctz(Q);
+    constexpr int kSliceWords = REPL ? 4 * 256 * 32 : 4 * 256;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    uint32_t* lslice = lds;
+    uint32_t* lshift = lds + kSliceWords;
+    for (int i = threadIdx.x; i < kSliceWords; i += blockDim.x) {
+        if (REPL) {
+            const int k = i >> 13, e = (i >> 5) & 255;
+            lslice[i] = a.slice[(k << 8) | e];
+        } else {
+            lslice[i] = a.slice[i];
+        }
+    }
+    for (int i = threadIdx.x; i < (LOGQ + 1) * 1024; i += blockDim.x) lshift[i] = a.shift[i];
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63;
+    const uint32_t c = lane & 31;
+    const int gl = lane & (Q - 1);
+    const int gid = lane / Q;
+    constexpr int kGroupsPerWave = 64 / Q;
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint64_t fstride = nwaves * kGroupsPerWave;
+    const bool trailer = (a.flags & (RH_CRC_VERIFY | RH_CRC_STAMP)) != 0;
+
+    Cursor cur;
+    cur.f = wave * kGroupsPerWave + gid;
+    cursor_frame(a, trailer, W, cur);
+    // skip frames with no window (empty / malformed) after finalising them
+    uint32_t d[17];
+    auto load_chunk = [&](const Cursor& cc, uint32_t (&dd)[17]) {
+        const Chunk k = chunk_of<Q, S>(cc, gl);
+        const int need = k.nwords + (cc.sh ? 1 : 0);
+        const int64_t b0 = k.A - cc.sh;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int idx = 4 * q;
+            const int64_t p = b0 + 16 * q;
+            if (idx < need && p + 16 <= a.buf_len) {
+                const u32x4a v = *reinterpret_cast<const u32x4a*>(a.buf + p);
+                dd[idx] = v.x;
+                dd[idx + 1] = v.y;
+                dd[idx + 2] = v.z;
+                dd[idx + 3] = v.w;
+            } else if (idx < need) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) dd[idx + i] = load_dword_clamped(a.buf, p + 4 * i, a.buf_len);
+            } else {
+                dd[idx] = dd[idx + 1] = dd[idx + 2] = dd[idx + 3] = 0;
+            }
+        }
+        dd[16] = (16 < need) ? load_dword_clamped(a.buf, b0 + 64, a.buf_len) : 0u;
+    };
+    if (cur.f < a.n) load_chunk(cur, d);
+    uint32_t R = 0;
+    while (__any(cur.f < a.n)) {
+        // next cursor + its data, issued before folding the current window
+        Cursor nxt = cur;
+        if (cur.f < a.n) {
+            if (cur.wi + 1 < cur.nw) {
+                nxt.wi = cur.wi + 1;
+            } else {
+                nxt.f = cur.f + fstride;
+                cursor_frame(a, trailer, W, nxt);
+            }
+        }
+        uint32_t dn[17];
+        if (nxt.f < a.n) load_chunk(nxt, dn);
+
+        // fold the current window's chunk
+        uint32_t r = 0;
+        if (cur.f < a.n && cur.wi < cur.nw) {
+            const Chunk k = chunk_of<Q, S>(cur, gl);
+            if (k.h) {
+#pragma unroll
+                for (int i = 0; i < 3; ++i)
+                    if (i < k.h) {
+                        uint32_t b = a.buf[k.bs + i];
+                        if (k.p0 + i < 4) b ^= (a.init >> (8 * (k.p0 + i))) & 0xffu;
+                        r = fold_byte<REPL>(lslice, r, b, c);
+                    }
+            }
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                if (j < k.nwords) {
+                    uint32_t w = cur.sh ? __builtin_amdgcn_alignbyte(d[j + 1], d[j], cur.sh) : d[j];
+                    if (j == 0 && k.p0 + k.h < 4) w ^= a.init >> (8 * (k.p0 + k.h));
+                    r = fold_word<REPL>(lslice, r, w, c);
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < LOGQ; ++j) {
+            const uint32_t t = zshift(lshift + j * 1024, r);
+            const uint32_t p = __shfl_down(r, 1 << j);
+            r = t ^ p;
+        }
+        if (cur.f < a.n) {
+            if (cur.wi < cur.nw) R = zshift(lshift + LOGQ * 1024, R) ^ r;
+            if (cur.wi + 1 >= cur.nw) {  // frame complete: finalise in the group leader
+                if (gl == 0) {
+                    const uint64_t f = cur.f;
+                    uint32_t state = R;
+                    if (cur.Lc < 4) state ^= (uint32_t)((uint64_t)a.init >> (8 * cur.Lc));
+                    const uint32_t value = ~state;
+                    const int64_t E = cur.E;
+                    if (a.crc_out) a.crc_out[f] = cur.malformed ? 0u : value;
+                    if (cur.malformed) {
+                        if (a.bad_bits)
+                            atomicOr(reinterpret_cast<unsigned long long*>(a.bad_bits + (f >> 6)), 1ull << (f & 63));
+                        if (a.n_bad) atomicAdd(a.n_bad, 1ull);
+                    } else if (a.flags & RH_CRC_STAMP) {
+                        a.wbuf[E + 0] = (uint8_t)(value >> 24);
+                        a.wbuf[E + 1] = (uint8_t)(value >> 16);
+                        a.wbuf[E + 2] = (uint8_t)(value >> 8);
+                        a.wbuf[E + 3] = (uint8_t)value;
+                    } else if (a.flags & RH_CRC_VERIFY) {
+                        const uint32_t stored = ((uint32_t)a.buf[E] << 24) | ((uint32_t)a.buf[E + 1] << 16) |
+                                                ((uint32_t)a.buf[E + 2] << 8) | (uint32_t)a.buf[E + 3];
+                        if (stored != value) {
+                            if (a.bad_bits)
+                                atomicOr(reinterpret_cast<unsigned long long*>(a.bad_bits + (f >> 6)),
+                                         1ull << (f & 63));
+                            if (a.n_bad) atomicAdd(a.n_bad, 1ull);
+                        }
+                    }
+                }
+                R = 0;
+            }
+        }
+        cur = nxt;
+#pragma unroll
+        for (int j = 0; j < 17; ++j) d[j] = dn[j];
+    }
+}
+
 struct Variant {
     int q, s;
     bool repl;
@@ -321,19 +511,26 @@ constexpr Variant kVariants[] = {
     {16, 256, true},   // 1: four 4 KiB windows per wave
     {8, 512, true},    // 2: eight 4 KiB windows per wave
     {64, 64, false},   // 3: shared (non-replicated) tables, for the bank-conflict A/B
+    {64, 64, true},    // 4: v2 (window prefetch), replicated tables
+    {64, 64, false},   // 5: v2, shared tables, 4 workgroups per CU
+    {16, 64, true},    // 6: v2, 16 lanes x 64 B = 1 KiB windows
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
 int g_default_variant = 0;
 
-template <int Q, int S, bool REPL>
+template <int Q, int S, bool REPL, bool V2 = false>
 int launch_variant(rh_ctx* ctx, const FrameArgs& fa, hipStream_t stream) {
     constexpr int LOGQ = __builtin_ctz(Q);
     constexpr size_t lds = (REPL ? 4 * 256 * 32 * 4 : 4 * 256 * 4) + (size_t)(LOGQ + 1) * 4096;
     static_assert(lds <= 160 * 1024, "LDS budget");
     const int block = REPL ? 1024 : 256;
     const int per_cu = REPL ? 1 : 4;
-    auto kern = crc_frames_kernel<Q, S, REPL>;
+    void (*kern)(FrameArgs);
+    if constexpr (V2)
+        kern = crc_frames_kernel2<Q, S, REPL>;
+    else
+        kern = crc_frames_kernel<Q, S, REPL>;
     static bool attr_set = false;
     if (!attr_set) {
         RH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(kern),
@@ -396,6 +593,9 @@ int rh_crc_launch_variant(rh_ctx* ctx, const rh_frames* f, uint32_t flags, int v
         case 1: return launch_variant<16, 256, true>(ctx, a, stream);
         case 2: return launch_variant<8, 512, true>(ctx, a, stream);
         case 3: return launch_variant<64, 64, false>(ctx, a, stream);
+        case 4: return launch_variant<64, 64, true, true>(ctx, a, stream);
+        case 5: return launch_variant<64, 64, false, true>(ctx, a, stream);
+        case 6: return launch_variant<16, 64, true, true>(ctx, a, stream);
     }
     return rh::fail(RH_E_INVAL, "unknown CRC kernel variant");
 }

@@ -428,6 +428,10 @@ RH_EXPORT int rh_crc32c_frames_launch(rh_ctx* ctx, const rh_frames* frames, uint
 
 RH_EXPORT int rh_crc32c_num_variants(void) { return rh_crc_num_variants(); }
 
+RH_EXPORT int rh_commit_num_variants(void) { return rh_commit_num_variants_impl(); }
+
+RH_EXPORT int rh_commit_set_variant(int variant) { return rh_commit_set_variant_impl(variant); }
+
 RH_EXPORT int rh_crc32c_set_variant(int variant) { return rh_crc_set_default_variant(variant); }
 
 RH_EXPORT int rh_crc32c_frames_launch_variant(rh_ctx* ctx, const rh_frames* frames, uint32_t flags, int variant,

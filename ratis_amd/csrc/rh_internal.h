@@ -59,3 +59,5 @@ int rh_crc_upload_tables(rh_ctx* ctx);
 int rh_crc_launch_variant(rh_ctx* ctx, const rh_frames* f, uint32_t flags, int variant, hipStream_t stream);
 int rh_crc_set_default_variant(int v);
 int rh_crc_num_variants();
+int rh_commit_set_variant_impl(int v);
+int rh_commit_num_variants_impl();

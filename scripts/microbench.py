@@ -42,6 +42,43 @@ def main():
         x = np.array(res[v])
         print(json.dumps({"kernel": "crc32c", "variant": v, "median_GBps": round(float(np.median(x)), 1),
                           "min_GBps": round(float(x.min()), 1), "max_GBps": round(float(x.max()), 1)}))
+    del ss, fb
+    # commit kernel variants over 8 rotating 1M-group batches (config 3)
+    host = workload.commit_snapshot(1_000_000)
+    alg = sum(h.algorithmic_bytes() for h in host)
+    batches = []
+    for r in range(8):
+        tiers = []
+        for h in host:
+            t = workload.to_device(h)
+            t.follower_index += r << 44
+            t.self_index += r << 44
+            t.commit_in += r << 44
+            t.term_start += r << 44
+            tiers.append(t.alloc_outputs())
+        batches.append(tiers)
+    lib = _lib.load()
+    ncv = lib.rh_commit_num_variants()
+    cres = {v: [] for v in range(ncv)}
+    for r in range(a.rounds):
+        for v in range(ncv):
+            _lib.check(lib.rh_commit_set_variant(v))
+            for i in range(8):
+                engine.commit_launch(ctx, batches[i])
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for i in range(40):
+                engine.commit_launch(ctx, batches[i % 8])
+            e1.record()
+            torch.cuda.synchronize()
+            ms = e0.elapsed_time(e1) / 40
+            cres[v].append(alg / (ms * 1e-3) / 1e9)
+    _lib.check(lib.rh_commit_set_variant(1))
+    for v in range(ncv):
+        x = np.array(cres[v])
+        print(json.dumps({"kernel": "commit", "variant": v, "median_GBps": round(float(np.median(x)), 1),
+                          "min_GBps": round(float(x.min()), 1), "max_GBps": round(float(x.max()), 1),
+                          "median_Gupd_s": round(float(np.median(x)) * 1e9 / alg * 1e6 / 1e9, 2)}))
     ctx.close()
 
 
