@@ -97,6 +97,7 @@ struct FrameArgs {
     unsigned long long* n_bad;
     const uint32_t* slice;   // [4][256] global
     const uint32_t* shift;   // [levels][4][256] global: level j advances S*2^j, last = W
+    const uint32_t* shift32; // [4][256]: advance over 32 zero bytes (v3, ILP = 2)
 };
 
 template <bool REPL>
@@ -128,6 +129,14 @@ __device__ __forceinline__ uint32_t load_dword_clamped(const uint8_t* buf, int64
     uint32_t v = 0;
     for (int i = 0; i < 4; ++i)
         if (p + i < lim) v |= (uint32_t)buf[p + i] << (8 * i);
+    return v;
+}
+
+// Same as load_dword_clamped for the rare dword that crosses the buffer end (out of line).
+__device__ __noinline__ uint32_t load_dword_clamped_slow(const uint8_t* buf, int64_t p, int64_t lim) {
+    uint32_t v = 0;
+    for (int i = 0; i < 4; ++i)
+        if (p + i >= 0 && p + i < lim) v |= (uint32_t)buf[p + i] << (8 * i);
     return v;
 }
 
@@ -501,6 +510,178 @@ __global__ __launch_bounds__(REPL ? 1024 : 256) void crc_frames_kernel2(FrameArg
     }
 }
 
+// ---- v3: branch-free fold ----------------------------------------------------------------
+// Every lane folds exactly 16 words (its end-anchored 64-byte chunk).  Bytes of the chunk that
+// lie before the frame start are zeroed once after the load (a zero register absorbing leading
+// zero bytes stays zero, so this equals folding only the real bytes), and the initial state is
+// XOR-ed into the dwords that hold message positions 0..3.  Only the (at most one per window)
+// lane whose chunk crosses the frame start, or whose loads would cross a buffer edge, takes
+// the guarded load path.  ILP = 2 folds the two 32-byte halves as independent chains and joins
+// them with one 32-byte zero-advance: the serial LDS-latency chain per window halves.
+template <int Q, int ILP, bool REPL>
+__global__ __launch_bounds__(REPL ? 1024 : 256) void crc_frames_kernel3(FrameArgs a) {
+    constexpr int S = 64;
+    constexpr int64_t W = (int64_t)Q * S;
+    constexpr int LOGQ = __builtin_ctz(Q);
+    constexpr int kSliceWords = REPL ? 4 * 256 * 32 : 4 * 256;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    uint32_t* lslice = lds;
+    uint32_t* lshift = lds + kSliceWords;          // [LOGQ + 1] levels, S*2^j then W
+    uint32_t* lhalf = lshift + (LOGQ + 1) * 1024;  // 32-byte zero-advance (ILP = 2)
+    for (int i = threadIdx.x; i < kSliceWords; i += blockDim.x) {
+        if (REPL) {
+            const int k = i >> 13, e = (i >> 5) & 255;
+            lslice[i] = a.slice[(k << 8) | e];
+        } else {
+            lslice[i] = a.slice[i];
+        }
+    }
+    for (int i = threadIdx.x; i < (LOGQ + 1) * 1024; i += blockDim.x) lshift[i] = a.shift[i];
+    if (ILP == 2)
+        for (int i = threadIdx.x; i < 1024; i += blockDim.x) lhalf[i] = a.shift32[i];
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63;
+    const uint32_t c = lane & 31;
+    const int gl = lane & (Q - 1);
+    const int gid = lane / Q;
+    constexpr int kGroupsPerWave = 64 / Q;
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint64_t fstride = nwaves * kGroupsPerWave;
+    const bool trailer = (a.flags & (RH_CRC_VERIFY | RH_CRC_STAMP)) != 0;
+
+    // loads the 17 dwords of this lane's chunk in window `cc.wi`, pre-masked and init-injected
+    auto load_chunk = [&](const Cursor& cc, uint32_t (&dd)[17]) {
+        const int64_t be = cc.E - (cc.nw - 1 - cc.wi) * W - (int64_t)(Q - 1 - gl) * S;
+        const int64_t cs = be - S;
+        const int64_t b0 = cs - cc.sh;  // 4-aligned
+        const bool fast = cs >= cc.o && b0 + 68 <= a.buf_len;
+        if (fast) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const u32x4a v = *reinterpret_cast<const u32x4a*>(a.buf + b0 + 16 * q);
+                dd[4 * q] = v.x;
+                dd[4 * q + 1] = v.y;
+                dd[4 * q + 2] = v.z;
+                dd[4 * q + 3] = v.w;
+            }
+            dd[16] = cc.sh ? *reinterpret_cast<const uint32_t*>(a.buf + b0 + 64) : 0u;
+        } else {
+            // guarded path: only dwords overlapping [o, be) are read; none outside the buffer
+#pragma unroll
+            for (int i = 0; i < 17; ++i) {
+                const int64_t p = b0 + 4 * i;  // 4-aligned
+                uint32_t v = 0;
+                if (p + 4 > cc.o && p < be) {
+                    if (p >= 0 && p + 4 <= a.buf_len)
+                        v = *reinterpret_cast<const uint32_t*>(a.buf + p);
+                    else
+                        v = load_dword_clamped_slow(a.buf, p, a.buf_len);
+                    const int64_t lead = cc.o - p;  // bytes of this dword before the frame start
+                    if (lead > 0) v &= 0xFFFFFFFFu << (8 * (uint32_t)lead);
+                }
+                dd[i] = v;
+            }
+        }
+        // initial state at message positions 0..3: dword i covers positions q0+4i .. q0+4i+3
+        const int64_t q0l = b0 - cc.o;
+        if (q0l < 4 && q0l > -72) {
+            const int q0 = (int)q0l;
+#pragma unroll
+            for (int i = 0; i < 17; ++i) {
+                const int q = q0 + 4 * i;
+                const uint32_t up = (q >= 0 && q < 4) ? (a.init >> (8 * q)) : 0u;
+                const uint32_t dn = (q < 0 && q > -4) ? (a.init << (8 * -q)) : 0u;
+                dd[i] ^= up | dn;
+            }
+        }
+    };
+    auto fold16 = [&](const uint32_t (&dd)[17], uint32_t sh) -> uint32_t {
+        if (ILP == 2) {
+            uint32_t ra = 0, rb = 0;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const uint32_t wa = __builtin_amdgcn_alignbyte(dd[j + 1], dd[j], sh);
+                const uint32_t wb = __builtin_amdgcn_alignbyte(dd[j + 9], dd[j + 8], sh);
+                ra = fold_word<REPL>(lslice, ra, wa, c);
+                rb = fold_word<REPL>(lslice, rb, wb, c);
+            }
+            return zshift(lhalf, ra) ^ rb;
+        } else {
+            uint32_t r = 0;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) r = fold_word<REPL>(lslice, r, __builtin_amdgcn_alignbyte(dd[j + 1], dd[j], sh), c);
+            return r;
+        }
+    };
+
+    Cursor cur;
+    cur.f = wave * kGroupsPerWave + gid;
+    cursor_frame(a, trailer, W, cur);
+    uint32_t d[17];
+    if (cur.f < a.n && cur.wi < cur.nw) load_chunk(cur, d);
+    uint32_t R = 0;
+    while (__any(cur.f < a.n)) {
+        Cursor nxt = cur;
+        if (cur.f < a.n) {
+            if (cur.wi + 1 < cur.nw) {
+                nxt.wi = cur.wi + 1;
+            } else {
+                nxt.f = cur.f + fstride;
+                cursor_frame(a, trailer, W, nxt);
+            }
+        }
+        uint32_t dn[17];
+        if (nxt.f < a.n && nxt.wi < nxt.nw) load_chunk(nxt, dn);
+
+        uint32_t r = 0;
+        if (cur.f < a.n && cur.wi < cur.nw) r = fold16(d, cur.sh);
+#pragma unroll
+        for (int j = 0; j < LOGQ; ++j) {
+            const uint32_t t = zshift(lshift + j * 1024, r);
+            const uint32_t p = __shfl_down(r, 1 << j);
+            r = t ^ p;
+        }
+        if (cur.f < a.n) {
+            if (cur.wi < cur.nw) R = zshift(lshift + LOGQ * 1024, R) ^ r;
+            if (cur.wi + 1 >= cur.nw) {
+                if (gl == 0) {
+                    const uint64_t f = cur.f;
+                    uint32_t state = R;
+                    if (cur.Lc < 4) state ^= (uint32_t)((uint64_t)a.init >> (8 * cur.Lc));
+                    const uint32_t value = ~state;
+                    const int64_t E = cur.E;
+                    if (a.crc_out) a.crc_out[f] = cur.malformed ? 0u : value;
+                    if (cur.malformed) {
+                        if (a.bad_bits)
+                            atomicOr(reinterpret_cast<unsigned long long*>(a.bad_bits + (f >> 6)), 1ull << (f & 63));
+                        if (a.n_bad) atomicAdd(a.n_bad, 1ull);
+                    } else if (a.flags & RH_CRC_STAMP) {
+                        a.wbuf[E + 0] = (uint8_t)(value >> 24);
+                        a.wbuf[E + 1] = (uint8_t)(value >> 16);
+                        a.wbuf[E + 2] = (uint8_t)(value >> 8);
+                        a.wbuf[E + 3] = (uint8_t)value;
+                    } else if (a.flags & RH_CRC_VERIFY) {
+                        const uint32_t stored = ((uint32_t)a.buf[E] << 24) | ((uint32_t)a.buf[E + 1] << 16) |
+                                                ((uint32_t)a.buf[E + 2] << 8) | (uint32_t)a.buf[E + 3];
+                        if (stored != value) {
+                            if (a.bad_bits)
+                                atomicOr(reinterpret_cast<unsigned long long*>(a.bad_bits + (f >> 6)),
+                                         1ull << (f & 63));
+                            if (a.n_bad) atomicAdd(a.n_bad, 1ull);
+                        }
+                    }
+                }
+                R = 0;
+            }
+        }
+        cur = nxt;
+#pragma unroll
+        for (int j = 0; j < 17; ++j) d[j] = dn[j];
+    }
+}
+
 struct Variant {
     int q, s;
     bool repl;
@@ -514,20 +695,26 @@ constexpr Variant kVariants[] = {
     {64, 64, true},    // 4: v2 (window prefetch), replicated tables
     {64, 64, false},   // 5: v2, shared tables, 4 workgroups per CU
     {16, 64, true},    // 6: v2, 16 lanes x 64 B = 1 KiB windows
+    {64, 64, true},    // 7: v3 branch-free fold, ILP 1
+    {64, 64, true},    // 8: v3, ILP 2
+    {16, 64, true},    // 9: v3, 16 lanes, ILP 2
+    {64, 64, false},   // 10: v3, shared tables, ILP 2, 4 workgroups per CU
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
 int g_default_variant = 0;
 
-template <int Q, int S, bool REPL, bool V2 = false>
+template <int Q, int S, bool REPL, int V = 1, int ILP = 1>
 int launch_variant(rh_ctx* ctx, const FrameArgs& fa, hipStream_t stream) {
     constexpr int LOGQ = __builtin_ctz(Q);
-    constexpr size_t lds = (REPL ? 4 * 256 * 32 * 4 : 4 * 256 * 4) + (size_t)(LOGQ + 1) * 4096;
+    constexpr size_t lds = (REPL ? 4 * 256 * 32 * 4 : 4 * 256 * 4) + (size_t)(LOGQ + 1) * 4096 + (ILP == 2 ? 4096 : 0);
     static_assert(lds <= 160 * 1024, "LDS budget");
     const int block = REPL ? 1024 : 256;
     const int per_cu = REPL ? 1 : 4;
     void (*kern)(FrameArgs);
-    if constexpr (V2)
+    if constexpr (V == 3)
+        kern = crc_frames_kernel3<Q, ILP, REPL>;
+    else if constexpr (V == 2)
         kern = crc_frames_kernel2<Q, S, REPL>;
     else
         kern = crc_frames_kernel<Q, S, REPL>;
@@ -544,6 +731,7 @@ int launch_variant(rh_ctx* ctx, const FrameArgs& fa, hipStream_t stream) {
     FrameArgs a = fa;
     // per-level shift tables: S*2^j for j < LOGQ, then W
     a.shift = ctx->d_shift + (size_t)__builtin_ctz(S) * 1024;
+    a.shift32 = ctx->d_shift + (size_t)5 * 1024;
     hipLaunchKernelGGL(kern, dim3((uint32_t)grid), dim3(block), lds, stream, a);
     RH_HIP(hipGetLastError());
     return RH_OK;
@@ -593,9 +781,13 @@ int rh_crc_launch_variant(rh_ctx* ctx, const rh_frames* f, uint32_t flags, int v
         case 1: return launch_variant<16, 256, true>(ctx, a, stream);
         case 2: return launch_variant<8, 512, true>(ctx, a, stream);
         case 3: return launch_variant<64, 64, false>(ctx, a, stream);
-        case 4: return launch_variant<64, 64, true, true>(ctx, a, stream);
-        case 5: return launch_variant<64, 64, false, true>(ctx, a, stream);
-        case 6: return launch_variant<16, 64, true, true>(ctx, a, stream);
+        case 4: return launch_variant<64, 64, true, 2>(ctx, a, stream);
+        case 5: return launch_variant<64, 64, false, 2>(ctx, a, stream);
+        case 6: return launch_variant<16, 64, true, 2>(ctx, a, stream);
+        case 7: return launch_variant<64, 64, true, 3, 1>(ctx, a, stream);
+        case 8: return launch_variant<64, 64, true, 3, 2>(ctx, a, stream);
+        case 9: return launch_variant<16, 64, true, 3, 2>(ctx, a, stream);
+        case 10: return launch_variant<64, 64, false, 3, 2>(ctx, a, stream);
     }
     return rh::fail(RH_E_INVAL, "unknown CRC kernel variant");
 }

@@ -22,6 +22,20 @@ def main():
 
     from ratis_amd import _lib, engine, workload
     ctx = engine.Context(0)
+    # calibration: what plain torch streaming kernels reach on this device
+    x = torch.empty(1 << 27, dtype=torch.int64, device="cuda").random_()
+    y = torch.empty_like(x)
+    for name, fn, nbytes in (("copy_1GiB", lambda: y.copy_(x), 2 * x.numel() * 8),
+                             ("sum_1GiB", lambda: x.sum(), x.numel() * 8)):
+        fn()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        print(json.dumps({"kernel": "calibration:" + name, "GBps": round(nbytes / (e0.elapsed_time(e1) / 10 * 1e-3) / 1e9, 1)}))
+    del x, y
     ss = workload.synth_segments(ctx, n_segments=a.segments, corrupt_rate=0)
     fb = ss.batch
     nv = engine.crc32c_num_variants()
