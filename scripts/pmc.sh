@@ -1,0 +1,29 @@
+#!/bin/bash
+# PMC passes (separate rocprofv3 runs, kernel-trace only, no sys/runtime trace) for the two
+# hot kernels.  Output under gpurun_out/$RUN_TAG/pmc/<name>/.
+set -u
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R"
+OUT=$R/gpurun_out/${RUN_TAG:-pmc}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
+run() {  # name "counters" driver-args...
+  local name=$1 ctrs=$2; shift 2
+  timeout -k 10 300 rocprofv3 --kernel-trace --pmc $ctrs -d "$OUT/pmc/$name" -o run --output-format csv -- python3 "$R/scripts/prof_kernels.py" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "$name rc=$rc"
+  if [ $rc -ge 124 ]; then exit $rc; fi
+}
+for V in ${CRC_VARIANTS:-0 6}; do
+  run crc${V}_a "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS" --what crc --variant $V
+  run crc${V}_b "FETCH_SIZE GRBM_GUI_ACTIVE" --what crc --variant $V
+  run crc${V}_c "SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VMEM" --what crc --variant $V
+done
+for V in ${COMMIT_VARIANTS:-0}; do
+  run commit${V}_a "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD" --what commit --variant $V
+  run commit${V}_b "FETCH_SIZE GRBM_GUI_ACTIVE" --what commit --variant $V
+  run commit${V}_w "WRITE_SIZE" --what commit --variant $V
+done
+run crc0_w "WRITE_SIZE" --what crc --variant 0
+echo PMCDONE
