@@ -79,6 +79,38 @@ void build_crc_shift_table(uint64_t nbytes, uint32_t out[4][256]) {
         for (int b = 0; b < 256; ++b) out[k][b] = apply(acc, (uint32_t)b << (8 * k));
 }
 
+// Lane-distance tables for the v4 kernel: lane g of a Q-lane window advances its chunk CRC over
+// 64*(Q-1-g) zero bytes with 8 nibble lookups.  Layout [Q/32 halves][8 nibbles][16][32 copies]:
+// copy c (= lane & 31) holds the map of lane position (half*32 + c) mod Q, so every lane reads
+// LDS bank (lane & 31) -- conflict free.
+std::vector<uint32_t> build_crc_lane_tables(int Q, int S) {
+    const int halves = Q > 32 ? Q / 32 : 1;
+    std::vector<uint32_t> out((size_t)halves * 8 * 16 * 32);
+    CrcTables st;
+    build_crc_slice_tables(&st);
+    Map32 one{};
+    for (int i = 0; i < 32; ++i) {
+        const uint32_t x = 1u << i;
+        one.col[i] = (x >> 8) ^ st.slice[0][x & 0xffu];
+    }
+    for (int h = 0; h < halves; ++h)
+        for (int c = 0; c < 32; ++c) {
+            const int g = (h * 32 + c) % Q;
+            const uint64_t nbytes = (uint64_t)S * (uint64_t)(Q - 1 - g);
+            Map32 acc{};
+            for (int i = 0; i < 32; ++i) acc.col[i] = 1u << i;
+            Map32 p = one;
+            for (uint64_t n = nbytes; n; n >>= 1) {
+                if (n & 1u) acc = compose(p, acc);
+                p = compose(p, p);
+            }
+            for (int k = 0; k < 8; ++k)
+                for (int nib = 0; nib < 16; ++nib)
+                    out[(((size_t)h * 8 + k) * 16 + nib) * 32 + c] = apply(acc, (uint32_t)nib << (4 * k));
+        }
+    return out;
+}
+
 }  // namespace rh
 
 namespace {
@@ -97,7 +129,9 @@ struct FrameArgs {
     unsigned long long* n_bad;
     const uint32_t* slice;   // [4][256] global
     const uint32_t* shift;   // [levels][4][256] global: level j advances S*2^j, last = W
-    const uint32_t* shift32; // [4][256]: advance over 32 zero bytes (v3, ILP = 2)
+    const uint32_t* shift32; // [4][256]: advance over 32 zero bytes (v3/v4, ILP = 2)
+    const uint32_t* lanetab; // v4: lane-distance nibble tables (build_crc_lane_tables)
+    const uint32_t* zwin;    // v4: [4][256] advance over one window (Q*64 bytes)
 };
 
 template <bool REPL>
@@ -682,6 +716,199 @@ __global__ __launch_bounds__(REPL ? 1024 : 256) void crc_frames_kernel3(FrameArg
     }
 }
 
+// ---- v4: per-lane zero-advance instead of a tree ------------------------------------------
+// A window is Q lanes x 64 bytes.  Each lane folds its 16 words (slicing-by-4, replicated
+// tables), advances the partial register over the 64*(Q-1-g) bytes that follow its chunk in the
+// window with 8 conflict-free nibble lookups into lane-specific tables, and the group XOR-reduces
+// (log2 Q shuffles).  Frame-start masking and initial-state injection run only on windows that
+// contain a frame start (wave-uniform test); a frame's windows are chained by its leader lane
+// with one window-length zero-advance.
+template <int Q, int ILP, bool REPL>
+__global__ __launch_bounds__(1024) void crc_frames_kernel4(FrameArgs a) {
+    constexpr int S = 64;
+    constexpr int64_t W = (int64_t)Q * S;
+    constexpr int kSliceWords = REPL ? 4 * 256 * 32 : 4 * 256;
+    constexpr int kLaneWords = (Q > 32 ? Q / 32 : 1) * 8 * 16 * 32;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    uint32_t* lslice = lds;
+    uint32_t* llane = lslice + kSliceWords;
+    uint32_t* lzw = llane + kLaneWords;
+    uint32_t* lhalf = lzw + 1024;
+    for (int i = threadIdx.x; i < kSliceWords; i += blockDim.x) {
+        if (REPL) {
+            const int k = i >> 13, e = (i >> 5) & 255;
+            lslice[i] = a.slice[(k << 8) | e];
+        } else {
+            lslice[i] = a.slice[i];
+        }
+    }
+    for (int i = threadIdx.x; i < kLaneWords; i += blockDim.x) llane[i] = a.lanetab[i];
+    for (int i = threadIdx.x; i < 1024; i += blockDim.x) {
+        lzw[i] = a.zwin[i];
+        if (ILP == 2) lhalf[i] = a.shift32[i];
+    }
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63;
+    const uint32_t c = lane & 31;
+    const uint32_t lbase = (Q > 32 ? (uint32_t)(lane >> 5) * (8 * 16 * 32) : 0u) + c;
+    const int gl = lane & (Q - 1);
+    const int gid = lane / Q;
+    constexpr int kGroupsPerWave = 64 / Q;
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint64_t fstride = nwaves * kGroupsPerWave;
+    const bool trailer = (a.flags & (RH_CRC_VERIFY | RH_CRC_STAMP)) != 0;
+
+    auto load_chunk = [&](const Cursor& cc, uint32_t (&dd)[17]) {
+        const bool act = cc.f < a.n && cc.wi < cc.nw;
+        const int64_t be = cc.E - (cc.nw - 1 - cc.wi) * W - (int64_t)(Q - 1 - gl) * S;
+        const int64_t b0 = be - S - cc.sh;  // 4-aligned
+        const bool safe = !act || (b0 >= 0 && b0 + 68 <= a.buf_len);
+        if (__all(safe)) {
+            if (act) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const u32x4a v = *reinterpret_cast<const u32x4a*>(a.buf + b0 + 16 * q);
+                    dd[4 * q] = v.x;
+                    dd[4 * q + 1] = v.y;
+                    dd[4 * q + 2] = v.z;
+                    dd[4 * q + 3] = v.w;
+                }
+                dd[16] = *reinterpret_cast<const uint32_t*>(a.buf + b0 + 64);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 17; ++i) dd[i] = 0;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 17; ++i) {
+                const int64_t p = b0 + 4 * i;
+                uint32_t v = 0;
+                if (act && p + 4 > cc.o && p < be) {
+                    if (p >= 0 && p + 4 <= a.buf_len)
+                        v = *reinterpret_cast<const uint32_t*>(a.buf + p);
+                    else
+                        v = load_dword_clamped_slow(a.buf, p, a.buf_len);
+                }
+                dd[i] = v;
+            }
+        }
+    };
+
+    Cursor cur;
+    cur.f = wave * kGroupsPerWave + gid;
+    cursor_frame(a, trailer, W, cur);
+    uint32_t d[17];
+    load_chunk(cur, d);
+    uint32_t R = 0;
+    while (__any(cur.f < a.n)) {
+        Cursor nxt = cur;
+        if (cur.f < a.n) {
+            if (cur.wi + 1 < cur.nw) {
+                nxt.wi = cur.wi + 1;
+            } else {
+                nxt.f = cur.f + fstride;
+                cursor_frame(a, trailer, W, nxt);
+            }
+        }
+        uint32_t dn[17];
+        load_chunk(nxt, dn);
+
+        const bool act = cur.f < a.n && cur.wi < cur.nw;
+        // message position of dword 0 of this lane's chunk
+        const int64_t q0l = cur.E - (cur.nw - 1 - cur.wi) * W - (int64_t)(Q - gl) * S - cur.sh - cur.o;
+        const bool special = act && q0l < 4;
+        if (__any(special)) {
+            // zero bytes before the frame start; XOR the initial state into positions 0..3
+            const int64_t qc = q0l < -80 ? -80 : (q0l > 4 ? 4 : q0l);
+            const int q0 = (int)qc;
+#pragma unroll
+            for (int i = 0; i < 17; ++i) {
+                const int q = q0 + 4 * i;
+                uint32_t v = act ? d[i] : 0u;
+                v = (q <= -4) ? 0u : (q < 0 ? (v & (0xFFFFFFFFu << (8 * -q))) : v);
+                const uint32_t up = (q >= 0 && q < 4) ? (a.init >> (8 * q)) : 0u;
+                const uint32_t dn2 = (q < 0 && q > -4) ? (a.init << (8 * -q)) : 0u;
+                d[i] = (act && special) ? (v ^ up ^ dn2) : d[i];
+            }
+        }
+        // fold 16 words
+        uint32_t r;
+        const uint32_t sh = cur.sh;
+        if (ILP == 2) {
+            uint32_t ra = 0, rb = 0;
+            if (__all(sh == 0 || !act)) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    ra = fold_word<REPL>(lslice, ra, d[j], c);
+                    rb = fold_word<REPL>(lslice, rb, d[j + 8], c);
+                }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    ra = fold_word<REPL>(lslice, ra, __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh), c);
+                    rb = fold_word<REPL>(lslice, rb, __builtin_amdgcn_alignbyte(d[j + 9], d[j + 8], sh), c);
+                }
+            }
+            r = zshift(lhalf, ra) ^ rb;
+        } else {
+            r = 0;
+            if (__all(sh == 0 || !act)) {
+#pragma unroll
+                for (int j = 0; j < 16; ++j) r = fold_word<REPL>(lslice, r, d[j], c);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 16; ++j)
+                    r = fold_word<REPL>(lslice, r, __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh), c);
+            }
+        }
+        // advance over the rest of the window: 8 nibble lookups, lane-specific map, bank = lane&31
+        uint32_t z = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) z ^= llane[lbase + ((uint32_t)(k * 16) + ((r >> (4 * k)) & 15u)) * 32u];
+        r = act ? z : 0u;
+#pragma unroll
+        for (int dlt = 1; dlt < Q; dlt <<= 1) r ^= __shfl_xor(r, dlt);
+        if (cur.f < a.n) {
+            if (act) R = zshift(lzw, R) ^ r;
+            if (cur.wi + 1 >= cur.nw) {
+                if (gl == 0) {
+                    const uint64_t f = cur.f;
+                    uint32_t state = R;
+                    if (cur.Lc < 4) state ^= (uint32_t)((uint64_t)a.init >> (8 * cur.Lc));
+                    const uint32_t value = ~state;
+                    const int64_t E = cur.E;
+                    if (a.crc_out) a.crc_out[f] = cur.malformed ? 0u : value;
+                    if (cur.malformed) {
+                        if (a.bad_bits)
+                            atomicOr(reinterpret_cast<unsigned long long*>(a.bad_bits + (f >> 6)), 1ull << (f & 63));
+                        if (a.n_bad) atomicAdd(a.n_bad, 1ull);
+                    } else if (a.flags & RH_CRC_STAMP) {
+                        a.wbuf[E + 0] = (uint8_t)(value >> 24);
+                        a.wbuf[E + 1] = (uint8_t)(value >> 16);
+                        a.wbuf[E + 2] = (uint8_t)(value >> 8);
+                        a.wbuf[E + 3] = (uint8_t)value;
+                    } else if (a.flags & RH_CRC_VERIFY) {
+                        const uint32_t stored = ((uint32_t)a.buf[E] << 24) | ((uint32_t)a.buf[E + 1] << 16) |
+                                                ((uint32_t)a.buf[E + 2] << 8) | (uint32_t)a.buf[E + 3];
+                        if (stored != value) {
+                            if (a.bad_bits)
+                                atomicOr(reinterpret_cast<unsigned long long*>(a.bad_bits + (f >> 6)),
+                                         1ull << (f & 63));
+                            if (a.n_bad) atomicAdd(a.n_bad, 1ull);
+                        }
+                    }
+                }
+                R = 0;
+            }
+        }
+        cur = nxt;
+#pragma unroll
+        for (int j = 0; j < 17; ++j) d[j] = dn[j];
+    }
+}
+
 struct Variant {
     int q, s;
     bool repl;
@@ -699,6 +926,9 @@ constexpr Variant kVariants[] = {
     {64, 64, true},    // 8: v3, ILP 2
     {16, 64, true},    // 9: v3, 16 lanes, ILP 2
     {64, 64, false},   // 10: v3, shared tables, ILP 2, 4 workgroups per CU
+    {16, 64, true},    // 11: v4, 16 lanes x 64 B windows, ILP 1
+    {16, 64, true},    // 12: v4, ILP 2
+    {32, 64, true},    // 13: v4, 32 lanes, ILP 2
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
@@ -707,12 +937,16 @@ int g_default_variant = 0;
 template <int Q, int S, bool REPL, int V = 1, int ILP = 1>
 int launch_variant(rh_ctx* ctx, const FrameArgs& fa, hipStream_t stream) {
     constexpr int LOGQ = __builtin_ctz(Q);
-    constexpr size_t lds = (REPL ? 4 * 256 * 32 * 4 : 4 * 256 * 4) + (size_t)(LOGQ + 1) * 4096 + (ILP == 2 ? 4096 : 0);
+    constexpr size_t lds = V == 4 ? (REPL ? 4 * 256 * 32 * 4 : 4 * 256 * 4) + (size_t)(Q > 32 ? Q / 32 : 1) * 16384 + 4096 +
+                                        (ILP == 2 ? 4096 : 0)
+                                  : (REPL ? 4 * 256 * 32 * 4 : 4 * 256 * 4) + (size_t)(LOGQ + 1) * 4096 + (ILP == 2 ? 4096 : 0);
     static_assert(lds <= 160 * 1024, "LDS budget");
     const int block = REPL ? 1024 : 256;
     const int per_cu = REPL ? 1 : 4;
     void (*kern)(FrameArgs);
-    if constexpr (V == 3)
+    if constexpr (V == 4)
+        kern = crc_frames_kernel4<Q, ILP, REPL>;
+    else if constexpr (V == 3)
         kern = crc_frames_kernel3<Q, ILP, REPL>;
     else if constexpr (V == 2)
         kern = crc_frames_kernel2<Q, S, REPL>;
@@ -732,6 +966,8 @@ int launch_variant(rh_ctx* ctx, const FrameArgs& fa, hipStream_t stream) {
     // per-level shift tables: S*2^j for j < LOGQ, then W
     a.shift = ctx->d_shift + (size_t)__builtin_ctz(S) * 1024;
     a.shift32 = ctx->d_shift + (size_t)5 * 1024;
+    a.zwin = ctx->d_shift + (size_t)__builtin_ctz(Q * S) * 1024;
+    a.lanetab = Q == 16 ? ctx->d_lane16 : (Q == 32 ? ctx->d_lane32 : ctx->d_lane64);
     hipLaunchKernelGGL(kern, dim3((uint32_t)grid), dim3(block), lds, stream, a);
     RH_HIP(hipGetLastError());
     return RH_OK;
@@ -751,6 +987,13 @@ int rh_crc_upload_tables(rh_ctx* ctx) {
         rh::build_crc_shift_table(1ull << m, reinterpret_cast<uint32_t(*)[256]>(sh.data() + (size_t)m * 1024));
     RH_HIP(hipMalloc(&ctx->d_shift, sh.size() * 4));
     RH_HIP(hipMemcpy(ctx->d_shift, sh.data(), sh.size() * 4, hipMemcpyHostToDevice));
+    uint32_t** dst[3] = {&ctx->d_lane16, &ctx->d_lane32, &ctx->d_lane64};
+    const int qs[3] = {16, 32, 64};
+    for (int i = 0; i < 3; ++i) {
+        std::vector<uint32_t> lt = rh::build_crc_lane_tables(qs[i], 64);
+        RH_HIP(hipMalloc(dst[i], lt.size() * 4));
+        RH_HIP(hipMemcpy(*dst[i], lt.data(), lt.size() * 4, hipMemcpyHostToDevice));
+    }
     return RH_OK;
 }
 
@@ -788,6 +1031,9 @@ int rh_crc_launch_variant(rh_ctx* ctx, const rh_frames* f, uint32_t flags, int v
         case 8: return launch_variant<64, 64, true, 3, 2>(ctx, a, stream);
         case 9: return launch_variant<16, 64, true, 3, 2>(ctx, a, stream);
         case 10: return launch_variant<64, 64, false, 3, 2>(ctx, a, stream);
+        case 11: return launch_variant<16, 64, true, 4, 1>(ctx, a, stream);
+        case 12: return launch_variant<16, 64, true, 4, 2>(ctx, a, stream);
+        case 13: return launch_variant<32, 64, true, 4, 2>(ctx, a, stream);
     }
     return rh::fail(RH_E_INVAL, "unknown CRC kernel variant");
 }

@@ -126,6 +126,9 @@ RH_EXPORT int rh_shutdown(rh_ctx* ctx) {
     (void)hipStreamSynchronize(ctx->stream);
     (void)hipFree(ctx->d_slice);
     (void)hipFree(ctx->d_shift);
+    (void)hipFree(ctx->d_lane16);
+    (void)hipFree(ctx->d_lane32);
+    (void)hipFree(ctx->d_lane64);
     (void)hipFree(ctx->d_scratch);
     if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
     (void)hipStreamDestroy(ctx->stream);

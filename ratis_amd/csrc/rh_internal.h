@@ -6,6 +6,7 @@
 #include <cstdint>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "../../include/ratis_hip.h"
 
@@ -31,6 +32,7 @@ struct CrcTables {
 void build_crc_slice_tables(CrcTables* t);
 // Zero-advance map for `nbytes` zero bytes, as 4 byte-indexed tables (out[4][256]).
 void build_crc_shift_table(uint64_t nbytes, uint32_t out[4][256]);
+std::vector<uint32_t> build_crc_lane_tables(int Q, int S);
 
 }  // namespace rh
 
@@ -40,7 +42,10 @@ struct rh_ctx {
     int num_cus = 0;
     // device copies of the CRC tables
     uint32_t* d_slice = nullptr;   // [4][256]
-    uint32_t* d_shift = nullptr;   // [RH_CRC_SHIFT_LEVELS][4][256], per-level zero-advance maps
+    uint32_t* d_shift = nullptr;   // [41][4][256]: zero-advance maps over 2^m bytes, m = 0..40
+    uint32_t* d_lane16 = nullptr;  // lane-distance nibble tables for 16/32/64-lane windows
+    uint32_t* d_lane32 = nullptr;
+    uint32_t* d_lane64 = nullptr;
     // scratch for host-buffer convenience calls
     std::mutex mu;
     void* d_scratch = nullptr;
