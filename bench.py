@@ -165,7 +165,7 @@ def main():
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": pmc.get("commit_bytes_per_launch"),
-                "kernel": "commit_kernel<1,7> (fused stable F=4 + joint F=6 tiers)",
+                "kernel": "commit_kernel<1,7,1> (fused stable F=4 + joint F=6 tiers)",
                 "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": round(kern_ms, 5)}
 
     # ------------------------------------------------------------------ PCIe-inclusive commit
@@ -249,11 +249,11 @@ def main():
                "workload": f"config5: {args.crc_segments} x 32 MiB segments/GPU, 4 KiB frames "
                            f"({fb.n} frames/GPU, {ss.corrupted.size} corrupted)",
                "ms_per_pass": round(crc_ms, 4), "mismatches_found": int(bad.size), "parity_ok": crc_ok,
-               "variant": args.crc_variant if args.crc_variant is not None else 0,
+               "variant": args.crc_variant if args.crc_variant is not None else 15,
                "roofline": {"bound": "hbm", "achieved": round(crc_ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                             "frac": round(crc_ach / HBM_PEAK_GBPS, 4),
                             "traffic": pmc.get("crc_bytes_per_launch"),
-                            "kernel": "crc_frames_kernel<64,64,true>",
+                            "kernel": "crc_frames_kernel5<16,2> (variant 15)",
                             "algorithmic_bytes_per_launch": crc_alg, "avg_launch_ms": round(crc_kern_ms, 4)}}
         if not args.no_pcie:
             # host image of 8 segments (256 MiB) -> H2D pinned + verify

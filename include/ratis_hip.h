@@ -218,9 +218,14 @@ int rh_crc32c_verify_host(rh_ctx* ctx, const uint8_t* seg, uint64_t seg_len, con
                           uint64_t* n_bad);
 
 /* ---- tuning hooks (bench / A-B experiments; results are identical for every variant) ---- */
-/* CRC kernel variants: 0 = 64 lanes x 64 B per 4 KiB window (default), 1 = 16 x 256 B,
- * 2 = 8 x 512 B, 3 = variant 0 with shared (non-replicated, bank-conflicting) tables. */
-/* Commit kernel variants: sub-tiles of 128 groups per wave, 0 = 1, 1 = 2 (default), 2 = 4. */
+/* CRC kernel variants (identical results; see DESIGN.md "CRC kernel history"):
+ *   0-3   v1: Q lanes x S bytes per window + log-tree combine (0: 64x64, 1: 16x256, 2: 8x512,
+ *         3: 64x64 with shared bank-conflicting tables)
+ *   4-6   v2: + one window prefetched;  7-10 v3: branch-free fold with guarded slow path
+ *   11-13 v4: per-lane zero-advance (lane-distance nibble tables) instead of the tree
+ *   14-17 v5: v4 + one-v_perm table addressing; 14: 1 window in flight, 15: 2 (DEFAULT), 16: 3,
+ *         17: 32-lane windows, 2 in flight */
+/* Commit kernel variants: sub-tiles of 128 groups per wave, 0 = 1 (default), 1 = 2, 2 = 4. */
 int rh_commit_num_variants(void);
 int rh_commit_set_variant(int variant);
 int rh_crc32c_num_variants(void);

@@ -22,9 +22,9 @@ namespace {
 
 constexpr int kBlock = 256;            // 4 waves
 constexpr int kGroupsPerLane = 2;      // 16-byte loads per column per lane
-// Sub-tiles (of 128 groups) per wave: the launch variant.  Default 2 => a workgroup covers
-// 1024 groups and a 1M-group batch is ~980 workgroups, one resident round on 256 CUs.
-int g_commit_variant = 1;
+// Sub-tiles (of 128 groups) per wave: the launch variant.  Default T = 1 (measured fastest:
+// lowest VGPR count, highest occupancy; scripts/microbench.py).
+int g_commit_variant = 0;
 constexpr int kVariantT[] = {1, 2, 4};
 constexpr int kNumCommitVariants = 3;
 

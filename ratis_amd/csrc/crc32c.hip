@@ -1135,7 +1135,7 @@ constexpr Variant kVariants[] = {
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
-int g_default_variant = 0;
+int g_default_variant = 15;  // v5, 16-lane 1 KiB windows, 2 windows in flight (fastest measured)
 
 template <int Q, int S, bool REPL, int V = 1, int ILP = 1>
 int launch_variant(rh_ctx* ctx, const FrameArgs& fa, hipStream_t stream) {
