@@ -20,11 +20,11 @@ step() {  # name timeout cmd...
 rocminfo 2>/dev/null | grep -m1 -o "gfx9[0-9a-z]*" > "$OUT/arch.txt" || true
 step pytest_gpu 900 python -m pytest tests -m gpu -q --timeout 300 ${PYTEST_ARGS:-}
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step bench 900 python bench.py ${BENCH_ARGS:---steps 50 --crc-segments 32}
+step bench 900 python bench.py ${BENCH_ARGS:-}
 if [ "${MICRO:-1}" = "1" ]; then step micro 600 python scripts/microbench.py --segments 32; fi
 if [ "${PROFILE:-1}" = "1" ]; then
   export TMPDIR=/tmp
-  step rocprof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 "$R/bench.py" --steps 20 --crc-segments 32 --crc-steps 10 --no-cpu-baseline --no-pcie
+  step rocprof 900 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 "$R/bench.py" ${BENCH_ARGS:-}
 fi
 if [ "${PMC:-0}" = "1" ]; then step pmc 900 bash scripts/pmc.sh; fi
 echo ALLDONE
