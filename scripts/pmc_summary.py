@@ -39,6 +39,19 @@ def main():
         out[f"{name}_write_bytes_per_launch"] = round(write)
         out[f"{name}_bytes_per_launch"] = round(fetch + write)
         out[f"{name}_counters"] = {k: round(v) for k, v in {**s, **f, **w}.items()}
+        # units per launch, from the driver's log line (scripts/prof_kernels.py)
+        log = os.path.join(os.path.dirname(a.pmc_dir.rstrip("/")), f"{tag}_b.log")
+        units = None
+        if os.path.exists(log):
+            for line in open(log):
+                parts = line.split()
+                if parts[:1] == ["frame_bytes"] and len(parts) >= 4:
+                    units = int(parts[3])
+                if parts[:1] == ["alg_bytes"] and len(parts) >= 4:
+                    units = int(parts[3])
+        if units:
+            out[f"{name}_units_per_launch"] = units
+            out[f"{name}_bytes_per_unit"] = round((fetch + write) / units, 2)
     txt = json.dumps(out, indent=1)
     print(txt)
     if a.out:

@@ -45,7 +45,7 @@ def main():
         for i in range(a.iters):
             engine.commit_launch(ctx, batches[i % 8])
         torch.cuda.synchronize()
-        print("alg_bytes", sum(h.algorithmic_bytes() for h in host))
+        print("alg_bytes", sum(h.algorithmic_bytes() for h in host), "groups", sum(h.n for h in host))
     ctx.close()
 
 
