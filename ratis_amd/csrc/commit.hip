@@ -26,7 +26,11 @@ constexpr int kGroupsPerLane = 2;      // 16-byte loads per column per lane
 // lowest VGPR count, highest occupancy; scripts/microbench.py).
 int g_commit_variant = 0;
 constexpr int kVariantT[] = {1, 2, 4};
-constexpr int kNumCommitVariants = 3;
+// 0-2: v1 with T = 1, 2, 4 sub-tiles per wave (F classes [1,7] and [8,14])
+// 3:   v1, T = 1, F classes [1,4], [5,7], [8,14] (narrower register allocation)
+// 4-6: v2 persistent + prefetch, F classes [1,4], [5,7], [8,14]; 3/4/5 waves per SIMD
+// 7:   v2, F classes [1,7], [8,14], 4 waves per SIMD
+constexpr int kNumCommitVariants = 8;
 
 // ---- Batcher merge-exchange sorting network (Knuth, TAOCP 5.2.2, Algorithm M) ------------
 struct Net {
@@ -273,15 +277,18 @@ __device__ __forceinline__ void compute_store_sub(const TierArgs& ta, uint64_t w
     const uint64_t ve = __ballot(valid[0]), vo = __ballot(valid[1]);
     const uint64_t ae = __ballot(adv[0]), ao = __ballot(adv[1]);
     if (wbase < t.n) {
+        // ballots are wave-uniform: interleave them on the scalar unit, then lanes 0/1 store
         const uint64_t word = wbase >> 6;
         const uint64_t nwords = (t.n + 63) >> 6;
-        if (t.valid_bits && lane < 2 && word + lane < nwords) {
-            const uint64_t e = lane ? (ve >> 32) : ve, o = lane ? (vo >> 32) : vo;
-            t.valid_bits[word + lane] = spread32(e) | (spread32(o) << 1);
+        if (t.valid_bits) {
+            const uint64_t w0 = spread32(ve) | (spread32(vo) << 1);
+            const uint64_t w1 = spread32(ve >> 32) | (spread32(vo >> 32) << 1);
+            if (lane < 2 && word + lane < nwords) t.valid_bits[word + lane] = lane ? w1 : w0;
         }
-        if (t.advanced_bits && lane < 2 && word + lane < nwords) {
-            const uint64_t e = lane ? (ae >> 32) : ae, o = lane ? (ao >> 32) : ao;
-            t.advanced_bits[word + lane] = spread32(e) | (spread32(o) << 1);
+        if (t.advanced_bits) {
+            const uint64_t w0 = spread32(ae) | (spread32(ao) << 1);
+            const uint64_t w1 = spread32(ae >> 32) | (spread32(ao >> 32) << 1);
+            if (lane < 2 && word + lane < nwords) t.advanced_bits[word + lane] = lane ? w1 : w0;
         }
     }
 
@@ -332,6 +339,108 @@ __device__ __forceinline__ void run_tile(const TierArgs& ta, uint64_t tile) {
     }
 }
 
+
+// ---- v2: persistent waves, software-pipelined over 128-group units -------------------------
+// Each wave walks units u = wave, wave + nwaves, ... over all tiers of the launch and issues the
+// loads of its next unit before computing the current one, so the HBM stream of the next unit
+// overlaps the sorting-network work of this one (v1 runs ~1.5 "rounds" of waves with no such
+// overlap).  A unit never crosses a tier, so F is wave-uniform per unit.
+template <int F>
+__device__ __forceinline__ void unit_load(const TierArgs& ta, uint64_t ubase, bool commit_mode, bool full,
+                                          SubTile<F>& st) {
+    const uint64_t r0 = ubase + 2 * (uint64_t)(threadIdx.x & 63);
+    if (full)
+        load_sub<F, true>(ta, r0, commit_mode, st);
+    else
+        load_sub<F, false>(ta, r0, commit_mode, st);
+}
+
+template <int F>
+__device__ __forceinline__ void unit_compute(const TierArgs& ta, uint64_t ubase, bool commit_mode, bool full,
+                                             const SubTile<F>& st) {
+    if (full)
+        compute_store_sub<F, true>(ta, ubase, commit_mode, st);
+    else
+        compute_store_sub<F, false>(ta, ubase, commit_mode, st);
+}
+
+struct UnitRef {
+    int tier;
+    uint64_t base;  // first row of the unit in its tier
+    bool valid;
+};
+
+__device__ __forceinline__ UnitRef unit_ref(const LaunchArgs& args, uint64_t u) {
+    UnitRef r{0, 0, false};
+#pragma unroll
+    for (int i = 0; i < RH_MAX_TIERS; ++i) {
+        if (i < args.n_tiers) {
+            const uint64_t nu = (uint64_t)args.tier[i].n_blocks;  // here: units (128 groups) of tier i
+            if (!r.valid && u < nu) {
+                r.tier = i;
+                r.base = u * 128;
+                r.valid = true;
+            }
+            if (!r.valid) u -= nu;
+        }
+    }
+    return r;
+}
+
+template <int F>
+__device__ __forceinline__ void run_units(const LaunchArgs& args, uint64_t u0, uint64_t stride, uint64_t n_units) {
+    // all units of this wave have the same F only if the launch holds one F; otherwise units of
+    // other widths are skipped here and handled by their own dispatch_f2 instantiation.
+    SubTile<F> cur, nxt;
+    uint64_t u = u0;
+    // find first unit of width F
+    auto next_of_width = [&](uint64_t from) -> uint64_t {
+        for (uint64_t v = from; v < n_units; v += stride) {
+            const UnitRef r = unit_ref(args, v);
+            if ((int)args.tier[r.tier].t.n_followers == F) return v;
+        }
+        return n_units;
+    };
+    u = next_of_width(u);
+    if (u >= n_units) return;
+    UnitRef rc = unit_ref(args, u);
+    bool cfull = rc.base + 128 <= args.tier[rc.tier].t.n && args.tier[rc.tier].vec_ok;
+    bool ccm = args.tier[rc.tier].t.mode == RH_MODE_COMMIT;
+    unit_load<F>(args.tier[rc.tier], rc.base, ccm, cfull, cur);
+    while (true) {
+        const uint64_t un = next_of_width(u + stride);
+        UnitRef rn{0, 0, false};
+        bool nfull = false, ncm = false;
+        if (un < n_units) {
+            rn = unit_ref(args, un);
+            nfull = rn.base + 128 <= args.tier[rn.tier].t.n && args.tier[rn.tier].vec_ok;
+            ncm = args.tier[rn.tier].t.mode == RH_MODE_COMMIT;
+            unit_load<F>(args.tier[rn.tier], rn.base, ncm, nfull, nxt);
+        }
+        unit_compute<F>(args.tier[rc.tier], rc.base, ccm, cfull, cur);
+        if (un >= n_units) break;
+        u = un;
+        rc = rn;
+        cfull = nfull;
+        ccm = ncm;
+        cur = nxt;
+    }
+}
+
+template <int F, int FHI>
+__device__ __forceinline__ void dispatch_f2(const LaunchArgs& args, uint32_t fmask, uint64_t u0, uint64_t stride,
+                                            uint64_t n_units) {
+    if (fmask & (1u << F)) run_units<F>(args, u0, stride, n_units);
+    if constexpr (F < FHI) dispatch_f2<F + 1, FHI>(args, fmask, u0, stride, n_units);
+}
+
+template <int FLO, int FHI>
+__global__ __launch_bounds__(kBlock) void commit_kernel_v2(const LaunchArgs args, uint32_t fmask, uint64_t n_units) {
+    const uint64_t wave = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const uint64_t stride = (uint64_t)gridDim.x * (kBlock / 64);
+    dispatch_f2<FLO, FHI>(args, fmask, wave, stride, n_units);
+}
+
 }  // namespace
 
 namespace {
@@ -368,8 +477,49 @@ void launch_t(int T, uint32_t blocks, const LaunchArgs& args, hipStream_t stream
     }
 }
 
+int g_num_cus = 256;
+
+// v2 launch over the tiers whose F lies in [flo, fhi]: n_blocks holds units of 128 groups.
+int launch_class_v2(const rh_commit_soa* tiers, int n_tiers, int flo, int fhi, int waves_per_simd,
+                    hipStream_t stream) {
+    LaunchArgs args{};
+    uint64_t units = 0;
+    uint32_t fmask = 0;
+    for (int i = 0; i < n_tiers; ++i) {
+        const rh_commit_soa& t = tiers[i];
+        if ((int)t.n_followers < flo || (int)t.n_followers > fhi || t.n == 0) continue;
+        TierArgs& ta = args.tier[args.n_tiers++];
+        ta.t = t;
+        ta.stride = t.col_stride ? t.col_stride : t.n;
+        ta.block_begin = 0;
+        ta.n_blocks = (uint32_t)((t.n + 127) / 128);
+        const bool cm = t.mode == RH_MODE_COMMIT;
+        ta.vec_ok = aligned16(t.follower_index) && (ta.stride % 2 == 0) && aligned16(t.self_index) &&
+                    (reinterpret_cast<uintptr_t>(t.conf) & 7u) == 0 &&
+                    (!cm || (aligned16(t.commit_in) && aligned16(t.term_start) && aligned16(t.commit_out))) &&
+                    (!t.min_out || aligned16(t.min_out)) && (!t.maj_out || aligned16(t.maj_out)) &&
+                    (!t.max_out || aligned16(t.max_out));
+        units += ta.n_blocks;
+        fmask |= 1u << t.n_followers;
+    }
+    if (args.n_tiers == 0) return RH_OK;
+    uint64_t waves = (uint64_t)g_num_cus * 4 * waves_per_simd;
+    if (waves > units) waves = units;
+    const uint32_t blocks = (uint32_t)((waves + 3) / 4);
+    if (flo == 1 && fhi == 4)
+        hipLaunchKernelGGL((commit_kernel_v2<1, 4>), dim3(blocks), dim3(kBlock), 0, stream, args, fmask, units);
+    else if (flo == 5 && fhi == 7)
+        hipLaunchKernelGGL((commit_kernel_v2<5, 7>), dim3(blocks), dim3(kBlock), 0, stream, args, fmask, units);
+    else if (flo == 1 && fhi == 7)
+        hipLaunchKernelGGL((commit_kernel_v2<1, 7>), dim3(blocks), dim3(kBlock), 0, stream, args, fmask, units);
+    else
+        hipLaunchKernelGGL((commit_kernel_v2<8, 14>), dim3(blocks), dim3(kBlock), 0, stream, args, fmask, units);
+    RH_HIP(hipGetLastError());
+    return RH_OK;
+}
+
 int launch_class(const rh_commit_soa* tiers, int n_tiers, int flo, int fhi, int variant, hipStream_t stream) {
-    const int T = kVariantT[variant];
+    const int T = kVariantT[variant < 3 ? variant : 0];
     const uint64_t kTile = (uint64_t)kBlock * kGroupsPerLane * T;  // groups per workgroup
     LaunchArgs args{};
     uint64_t blocks = 0;
@@ -391,7 +541,11 @@ int launch_class(const rh_commit_soa* tiers, int n_tiers, int flo, int fhi, int 
     }
     if (args.n_tiers == 0) return RH_OK;
     if (blocks > 0x7FFFFFFFull) return rh::fail(RH_E_RANGE, "commit launch: too many groups");
-    if (fhi <= 7)
+    if (flo == 1 && fhi == 4)
+        launch_t<1, 4>(T, (uint32_t)blocks, args, stream);
+    else if (flo == 5 && fhi == 7)
+        launch_t<5, 7>(T, (uint32_t)blocks, args, stream);
+    else if (fhi <= 7)
         launch_t<1, 7>(T, (uint32_t)blocks, args, stream);
     else
         launch_t<8, 14>(T, (uint32_t)blocks, args, stream);
@@ -410,7 +564,7 @@ int rh_commit_set_variant_impl(int v) {
 int rh_commit_num_variants_impl() { return kNumCommitVariants; }
 
 int rh_commit_launch_impl(rh_ctx* ctx, const rh_commit_soa* tiers, int n_tiers, hipStream_t stream) {
-    (void)ctx;
+    if (ctx && ctx->num_cus > 0) g_num_cus = ctx->num_cus;
     const int variant = g_commit_variant;
     if (!tiers || n_tiers < 1 || n_tiers > RH_MAX_TIERS)
         return rh::fail(RH_E_INVAL, "rh_commit_soa_launch: n_tiers must be in [1, RH_MAX_TIERS]");
@@ -432,9 +586,21 @@ int rh_commit_launch_impl(rh_ctx* ctx, const rh_commit_soa* tiers, int n_tiers, 
         if (t.adv_rows && (!t.adv_commit || !t.adv_count))
             return rh::fail(RH_E_INVAL, "rh_commit_soa_launch: adv_rows needs adv_commit and adv_count");
     }
-    int rc = launch_class(tiers, n_tiers, 1, 7, variant, stream);
+    int rc = RH_OK;
+    if (variant <= 2) {
+        rc = launch_class(tiers, n_tiers, 1, 7, variant, stream);
+    } else if (variant == 3) {
+        rc = launch_class(tiers, n_tiers, 1, 4, variant, stream);
+        if (rc == RH_OK) rc = launch_class(tiers, n_tiers, 5, 7, variant, stream);
+    } else if (variant <= 6) {
+        rc = launch_class_v2(tiers, n_tiers, 1, 4, variant - 1, stream);
+        if (rc == RH_OK) rc = launch_class_v2(tiers, n_tiers, 5, 7, variant - 1, stream);
+    } else {
+        rc = launch_class_v2(tiers, n_tiers, 1, 7, 4, stream);
+    }
     if (rc != RH_OK) return rc;
-    return launch_class(tiers, n_tiers, 8, 14, variant, stream);
+    if (variant <= 3) return launch_class(tiers, n_tiers, 8, 14, variant, stream);
+    return launch_class_v2(tiers, n_tiers, 8, 14, 4, stream);
 }
 
 // ---- delta application: RaftLogIndex.updateToMax per (slot, column) ----------------------

@@ -81,8 +81,9 @@ def _random_case(rng, F, n, lo=-1, hi=60, full_masks=False):
     return follower, flush, conf, commit, ts
 
 
+@pytest.mark.parametrize("commit_variant", [0, 3, 4], indirect=True)
 @pytest.mark.parametrize("F", list(range(1, 15)))
-def test_every_follower_width(ctx, orc, F):
+def test_every_follower_width(ctx, orc, F, commit_variant):
     rng = np.random.default_rng(100 + F)
     n = 3001  # ragged: not a multiple of the 512-group tile
     for gap in (-1, 0, 9):
@@ -142,7 +143,23 @@ def test_padded_column_stride_scalar_path(ctx, orc):
     _check(ctx, orc, *_random_case(rng, F, n), mode=0, gap=3, col_stride=1027)  # odd stride: no 16-B loads
 
 
-def test_fused_multi_tier_launch_and_compaction(ctx, orc):
+@pytest.fixture
+def commit_variant(request):
+    from ratis_amd import _lib
+    lib = _lib.load()
+    v = getattr(request, "param", None)
+    old = None
+    if v is not None:
+        _lib.check(lib.rh_commit_set_variant(v))
+    yield v
+    _lib.check(lib.rh_commit_set_variant(DEFAULT_COMMIT_VARIANT))
+
+
+DEFAULT_COMMIT_VARIANT = 0
+
+
+@pytest.mark.parametrize("commit_variant", list(range(8)), indirect=True)
+def test_fused_multi_tier_launch_and_compaction(ctx, orc, commit_variant):
     import torch
 
     from ratis_amd import engine, workload
