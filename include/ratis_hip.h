@@ -217,6 +217,43 @@ int rh_crc32c_verify_host(rh_ctx* ctx, const uint8_t* seg, uint64_t seg_len, con
                           const uint32_t* frame_len, uint64_t n, uint32_t* crc_out, uint64_t* bad_bits,
                           uint64_t* n_bad);
 
+/* ---- segment framing (SegmentedRaftLogReader.verifyHeader / decodeEntry / verifyTerminator) --
+ * Walks each segment image: header "RaftLog1" (RDR:179-205), then frames varint32(n) || n bytes ||
+ * 4-byte CRC while the first byte is non-zero (RDR:291-323), then checks that the terminator
+ * padding is all zero (RDR:251-280).  The walk applies decodeEntry's size rules (maxOpSize, the
+ * LimitedInputStream limit) and EOF rules; it does NOT check CRCs -- feed the produced frame table
+ * to rh_crc32c_frames_launch(RH_CRC_VERIFY), exactly as readSegmentFile would verify each entry.
+ * One wave per segment; the serial varint chain is walked out of LDS windows. */
+#define RH_SEG_END          1   /* clean end: EOF at an entry boundary or zero padding to EOF  */
+#define RH_SEG_PARTIAL      2   /* last entry truncated (readEntry returns null, RDR:221-229)  */
+#define RH_SEG_E_OVERSIZE  -1   /* entry larger than maxOpSize (RDR:314-317, limit checks)      */
+#define RH_SEG_E_PADDING   -3   /* non-zero byte after the terminator (RDR:251-280)            */
+#define RH_SEG_E_VARINT    -4   /* malformed / truncated varint (CodedInputStream)             */
+#define RH_SEG_E_HEADER    -5   /* corrupted header (CorruptedFileException, RDR:201-204)       */
+#define RH_SEG_E_CAPACITY  -6   /* more frames than frames_per_seg_cap                          */
+
+typedef struct rh_segments {
+    const uint8_t* buf;           /* device: segment images                                     */
+    uint64_t buf_len;
+    const uint64_t* seg_off;      /* [n_seg] start of each segment image in buf                 */
+    const uint64_t* seg_len;      /* [n_seg] file length of each segment                        */
+    uint64_t n_seg;
+    uint32_t max_op;              /* raft.server.log.appender.buffer.byte-limit (default 4 MiB) */
+    uint32_t frames_per_seg_cap;  /* capacity of each segment's slot in the scratch table      */
+    uint64_t* scratch_off;        /* [n_seg * cap] per-segment slotted frame offsets           */
+    uint32_t* scratch_len;        /* [n_seg * cap]                                              */
+    uint64_t* frame_off;          /* [frame_cap] dense output: absolute offset in buf           */
+    uint32_t* frame_len;          /* [frame_cap] whole frame length (varint + proto + 4)        */
+    uint64_t frame_cap;
+    uint64_t* seg_first;          /* [n_seg] index of the segment's first frame in the output   */
+    uint32_t* seg_nframes;        /* [n_seg] frames found before the walk stopped               */
+    int32_t* seg_status;          /* [n_seg] RH_SEG_*                                           */
+    uint64_t* seg_stop;           /* [n_seg] offset (within the segment) where the walk stopped */
+    unsigned long long* total_frames; /* single counter (sum of seg_nframes)                    */
+} rh_segments;
+
+int rh_segments_scan_launch(rh_ctx* ctx, const rh_segments* segs, void* stream);
+
 /* ---- tuning hooks (bench / A-B experiments; results are identical for every variant) ---- */
 /* CRC kernel variants (identical results; see DESIGN.md "CRC kernel history"):
  *   0-3   v1: Q lanes x S bytes per window + log-tree combine (0: 64x64, 1: 16x256, 2: 8x512,

@@ -101,6 +101,37 @@ class RhFrames(ctypes.Structure):
     ]
 
 
+RH_SEG_END = 1
+RH_SEG_PARTIAL = 2
+RH_SEG_E_OVERSIZE = -1
+RH_SEG_E_PADDING = -3
+RH_SEG_E_VARINT = -4
+RH_SEG_E_HEADER = -5
+RH_SEG_E_CAPACITY = -6
+
+
+class RhSegments(ctypes.Structure):
+    _fields_ = [
+        ("buf", c_void_p),
+        ("buf_len", c_uint64),
+        ("seg_off", c_void_p),
+        ("seg_len", c_void_p),
+        ("n_seg", c_uint64),
+        ("max_op", c_uint32),
+        ("frames_per_seg_cap", c_uint32),
+        ("scratch_off", c_void_p),
+        ("scratch_len", c_void_p),
+        ("frame_off", c_void_p),
+        ("frame_len", c_void_p),
+        ("frame_cap", c_uint64),
+        ("seg_first", c_void_p),
+        ("seg_nframes", c_void_p),
+        ("seg_status", c_void_p),
+        ("seg_stop", c_void_p),
+        ("total_frames", c_void_p),
+    ]
+
+
 # name -> (restype, argtypes); every function declared in include/ratis_hip.h
 _SIGNATURES = {
     "rh_abi_version": (c_int, []),
@@ -123,6 +154,7 @@ _SIGNATURES = {
     "rh_crc32c_frames_launch": (c_int, [c_void_p, POINTER(RhFrames), c_uint32, c_void_p]),
     "rh_crc32c_verify_host": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_uint64, c_void_p,
                                       c_void_p, POINTER(c_uint64)]),
+    "rh_segments_scan_launch": (c_int, [c_void_p, POINTER(RhSegments), c_void_p]),
     "rh_crc32c_num_variants": (c_int, []),
     "rh_commit_num_variants": (c_int, []),
     "rh_commit_set_variant": (c_int, [c_int]),

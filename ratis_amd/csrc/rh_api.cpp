@@ -429,6 +429,13 @@ RH_EXPORT int rh_crc32c_frames_launch(rh_ctx* ctx, const rh_frames* frames, uint
     return rh_crc_launch_impl(ctx, frames, flags, pick_stream(ctx, stream));
 }
 
+// ---- segment framing -------------------------------------------------------------------------
+RH_EXPORT int rh_segments_scan_launch(rh_ctx* ctx, const rh_segments* segs, void* stream) {
+    if (!ctx) return rh::fail(RH_E_INVAL, "rh_segments_scan_launch: ctx == NULL");
+    DeviceGuard g(ctx->device);
+    return rh_segments_launch_impl(ctx, segs, pick_stream(ctx, stream));
+}
+
 RH_EXPORT int rh_crc32c_num_variants(void) { return rh_crc_num_variants(); }
 
 RH_EXPORT int rh_commit_num_variants(void) { return rh_commit_num_variants_impl(); }

@@ -1,0 +1,326 @@
+// SegmentedRaftLog segment framing on gfx950: the reader's varint walk, batched over segments.
+//
+// Reference semantics (ratis-server/.../raftlog/segmented/):
+//   SegmentedRaftLogReader.verifyHeader     SegmentedRaftLogReader.java:179-205
+//   SegmentedRaftLogReader.decodeEntry      SegmentedRaftLogReader.java:291-341 (size/EOF rules;
+//                                           the CRC itself is rh_crc32c_frames_launch's job)
+//   SegmentedRaftLogReader.verifyTerminator SegmentedRaftLogReader.java:251-280
+//   LimitedInputStream.checkLimit           SegmentedRaftLogReader.java:66-82
+//   SegmentedRaftLogFormat header/terminator SegmentedRaftLogFormat.java:30-80
+//
+// The walk is a serial chain (each frame's length is a varint at its start), so the parallelism
+// is across segments: one wave per segment.  The wave stages a 16 KiB window of the segment in
+// LDS with wide coalesced loads; lane 0 walks every frame header inside the window out of LDS,
+// and the wave reloads at the walk position when it runs out.  Terminator padding is checked
+// by the whole wave.  Frames are written to a per-segment slotted table, then compacted.
+#include "rh_internal.h"
+
+namespace {
+
+constexpr int kWin = 16384;     // LDS window bytes
+constexpr int kScanThreads = 1024;
+
+struct SegArgs {
+    const uint8_t* buf;
+    int64_t buf_len;
+    const uint64_t* seg_off;
+    const uint64_t* seg_len;
+    uint64_t n_seg;
+    uint32_t max_op;
+    uint32_t cap;
+    uint64_t* scratch_off;
+    uint32_t* scratch_len;
+    uint32_t* seg_nframes;
+    int32_t* seg_status;
+    uint64_t* seg_stop;
+};
+
+constexpr int kWalking = 0;
+constexpr int kTermPending = 100;
+
+__device__ __forceinline__ int varint32_size(uint32_t v) {
+    if ((v & (~0u << 7)) == 0) return 1;
+    if ((v & (~0u << 14)) == 0) return 2;
+    if ((v & (~0u << 21)) == 0) return 3;
+    if ((v & (~0u << 28)) == 0) return 4;
+    return 5;
+}
+
+struct __attribute__((aligned(4))) u32x4s {
+    uint32_t x, y, z, w;
+};
+
+__global__ __launch_bounds__(64) void segment_walk_kernel(SegArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t win[kWin + 16];
+    const int lane = threadIdx.x;
+    for (uint64_t s = blockIdx.x; s < a.n_seg; s += gridDim.x) {
+        const int64_t base = (int64_t)a.seg_off[s];
+        int64_t L = (int64_t)a.seg_len[s];
+        if (base > a.buf_len) L = 0;
+        else if (L > a.buf_len - base) L = a.buf_len - base;   // never read past the buffer
+        const uint8_t* seg = a.buf + base;
+        int status = kWalking;
+        int64_t pos = 0;
+        uint32_t nfr = 0;
+        // ---- verifyHeader (RDR:179-205) ----
+        {
+            const char H[8] = {'R', 'a', 'f', 't', 'L', 'o', 'g', '1'};
+            const int64_t rl = L < 8 ? L : 8;
+            int match = 0;
+            int bad = 0;
+            for (int i = 0; i < rl; ++i) {
+                const uint8_t b = seg[i];
+                if (match == i && b == (uint8_t)H[i]) match = i + 1;
+                else if (b != 0) bad = 1;   // a non-terminator byte after the matched prefix
+            }
+            if (rl == 8 && match == 8) {
+                pos = 8;
+            } else {
+                status = bad ? RH_SEG_E_HEADER : RH_SEG_END;  // partially written header => empty
+                pos = 0;
+            }
+        }
+        int64_t wbase = -(int64_t)kWin * 4;  // no window yet
+        while (status == kWalking) {
+            if (pos >= L) {
+                status = RH_SEG_END;
+                break;
+            }
+            // window must hold the (up to 10) varint bytes at pos, or reach the segment end
+            if (!(pos >= wbase && (pos + 16 <= wbase + kWin || wbase + kWin >= L))) {
+                wbase = ((base + pos) & ~(int64_t)15) - base;  // 16-B aligned in the buffer
+                __syncthreads();
+#pragma unroll 4
+                for (int i = 0; i < kWin / (64 * 16); ++i) {
+                    const int off = (i * 64 + lane) * 16;
+                    const int64_t p = wbase + off;
+                    u32x4s v{0, 0, 0, 0};
+                    if (p >= 0 && p + 16 <= L) {
+                        v = *reinterpret_cast<const u32x4s*>(seg + p);
+                    } else if (p < L) {
+                        uint32_t w[4] = {0, 0, 0, 0};
+                        for (int k = p < 0 ? (int)-p : 0; k < 16 && p + k < L; ++k)
+                            w[k >> 2] |= (uint32_t)seg[p + k] << (8 * (k & 3));
+                        v = {w[0], w[1], w[2], w[3]};
+                    }
+                    *reinterpret_cast<u32x4s*>(win + off) = v;
+                }
+                __syncthreads();
+            }
+            // lane 0 walks every frame header available in the window
+            if (lane == 0) {
+                while (status == kWalking) {
+                    if (pos >= L) {
+                        status = RH_SEG_END;
+                        break;
+                    }
+                    if (!(pos + 16 <= wbase + kWin || wbase + kWin >= L)) break;  // reload
+                    const uint8_t* w = win + (pos - wbase);
+                    if (w[0] == 0) {  // terminator (SegmentedRaftLogFormat.isTerminator)
+                        status = kTermPending;
+                        break;
+                    }
+                    // CodedInputStream.readRawVarint32(firstByte, in); EOF -> truncatedMessage
+                    uint32_t result = 0;
+                    bool done = false, trunc = false;
+                    for (int i = 0; i < 5; ++i) {
+                        if (pos + i >= L) {
+                            trunc = true;
+                            break;
+                        }
+                        const uint8_t b = w[i];
+                        result |= (uint32_t)(b & 0x7f) << (7 * i);
+                        if ((b & 0x80) == 0) {
+                            done = true;
+                            break;
+                        }
+                    }
+                    if (!done && !trunc) {
+                        for (int i = 5; i < 10; ++i) {
+                            if (pos + i >= L) {
+                                trunc = true;
+                                break;
+                            }
+                            if ((w[i] & 0x80) == 0) {
+                                done = true;
+                                break;
+                            }
+                        }
+                    }
+                    if (!done) {
+                        status = RH_SEG_E_VARINT;
+                        break;
+                    }
+                    const int32_t n = (int32_t)result;
+                    if (n > (int32_t)a.max_op) {
+                        status = RH_SEG_E_OVERSIZE;
+                        break;
+                    }
+                    if (n < 0) {
+                        status = RH_SEG_E_VARINT;
+                        break;
+                    }
+                    const int64_t total = (int64_t)varint32_size((uint32_t)n) + n;
+                    if (total > (int64_t)a.max_op) {  // checkBufferSize assertion
+                        status = RH_SEG_E_OVERSIZE;
+                        break;
+                    }
+                    if (pos + total > L) {  // readFully EOF
+                        status = RH_SEG_PARTIAL;
+                        break;
+                    }
+                    bool stop = false;
+                    for (int k = 1; k <= 4; ++k) {  // readInt: checkLimit(1) before each read
+                        if (total + k > (int64_t)a.max_op) {
+                            status = RH_SEG_E_OVERSIZE;
+                            stop = true;
+                            break;
+                        }
+                        if (pos + total + k > L) {
+                            status = RH_SEG_PARTIAL;
+                            stop = true;
+                            break;
+                        }
+                    }
+                    if (stop) break;
+                    if (nfr >= a.cap) {
+                        status = RH_SEG_E_CAPACITY;
+                        break;
+                    }
+                    a.scratch_off[s * (uint64_t)a.cap + nfr] = (uint64_t)(base + pos);
+                    a.scratch_len[s * (uint64_t)a.cap + nfr] = (uint32_t)(total + 4);
+                    ++nfr;
+                    pos += total + 4;
+                }
+            }
+            status = __shfl(status, 0);
+            pos = __shfl(pos, 0);
+            nfr = __shfl(nfr, 0);
+        }
+        if (status == kTermPending) {
+            // verifyTerminator: every byte from pos to EOF must be zero; report the first that is not
+            int64_t first_bad = L;
+            for (int64_t p0 = pos; p0 < L; p0 += 64 * 16) {
+                const int64_t p = p0 + lane * 16;
+                int64_t my_bad = L;
+                if (p < L) {
+                    if (p + 16 <= L && ((base + p) & 3) == 0) {
+                        const u32x4s v = *reinterpret_cast<const u32x4s*>(seg + p);
+                        if (v.x | v.y | v.z | v.w)
+                            for (int k = 0; k < 16; ++k)
+                                if (seg[p + k]) {
+                                    my_bad = p + k;
+                                    break;
+                                }
+                    } else {
+                        for (int k = 0; k < 16 && p + k < L; ++k)
+                            if (seg[p + k]) {
+                                my_bad = p + k;
+                                break;
+                            }
+                    }
+                }
+                // wave min
+                for (int d = 32; d >= 1; d >>= 1) {
+                    const int64_t o = __shfl_xor(my_bad, d);
+                    my_bad = o < my_bad ? o : my_bad;
+                }
+                if (my_bad < L) {
+                    first_bad = my_bad;
+                    break;
+                }
+            }
+            if (first_bad < L) {
+                status = RH_SEG_E_PADDING;
+                pos = first_bad;
+            } else {
+                status = RH_SEG_END;  // stop stays at the terminator (the segment's logical end)
+            }
+        }
+        if (lane == 0) {
+            a.seg_nframes[s] = nfr;
+            a.seg_status[s] = status;
+            a.seg_stop[s] = (uint64_t)pos;
+        }
+    }
+}
+
+// Exclusive scan of seg_nframes (capped at cap) -> seg_first, total_frames.  One block.
+__global__ __launch_bounds__(kScanThreads) void segment_scan_kernel(const uint32_t* nframes, uint64_t n_seg,
+                                                                    uint32_t cap, uint64_t* seg_first,
+                                                                    unsigned long long* total) {
+    __shared__ uint64_t part[kScanThreads];
+    const int t = threadIdx.x;
+    const uint64_t per = (n_seg + kScanThreads - 1) / kScanThreads;
+    const uint64_t lo = t * per, hi = lo + per < n_seg ? lo + per : n_seg;
+    uint64_t sum = 0;
+    for (uint64_t i = lo; i < hi; ++i) sum += nframes[i] < cap ? nframes[i] : cap;
+    part[t] = sum;
+    __syncthreads();
+    for (int d = 1; d < kScanThreads; d <<= 1) {  // Hillis-Steele inclusive scan
+        const uint64_t v = t >= d ? part[t - d] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint64_t run = t ? part[t - 1] : 0;
+    for (uint64_t i = lo; i < hi; ++i) {
+        seg_first[i] = run;
+        run += nframes[i] < cap ? nframes[i] : cap;
+    }
+    if (t == kScanThreads - 1) *total = part[t];
+}
+
+__global__ __launch_bounds__(256) void segment_compact_kernel(const uint64_t* scratch_off, const uint32_t* scratch_len,
+                                                              const uint32_t* nframes, const uint64_t* seg_first,
+                                                              uint64_t n_seg, uint32_t cap, uint64_t* frame_off,
+                                                              uint32_t* frame_len, uint64_t frame_cap) {
+    for (uint64_t s = blockIdx.x; s < n_seg; s += gridDim.x) {
+        const uint32_t n = nframes[s] < cap ? nframes[s] : cap;
+        const uint64_t first = seg_first[s];
+        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+            if (first + i < frame_cap) {
+                frame_off[first + i] = scratch_off[s * (uint64_t)cap + i];
+                frame_len[first + i] = scratch_len[s * (uint64_t)cap + i];
+            }
+        }
+    }
+}
+
+}  // namespace
+
+int rh_segments_launch_impl(rh_ctx* ctx, const rh_segments* g, hipStream_t stream) {
+    if (!g) return rh::fail(RH_E_INVAL, "rh_segments_scan_launch: segs == NULL");
+    if (g->n_seg == 0) return RH_OK;
+    if (!g->buf || !g->seg_off || !g->seg_len || !g->scratch_off || !g->scratch_len || !g->frame_off ||
+        !g->frame_len || !g->seg_first || !g->seg_nframes || !g->seg_status || !g->seg_stop || !g->total_frames)
+        return rh::fail(RH_E_INVAL, "rh_segments_scan_launch: every array is required");
+    if (g->frames_per_seg_cap == 0) return rh::fail(RH_E_INVAL, "rh_segments_scan_launch: frames_per_seg_cap == 0");
+    if (g->max_op == 0 || g->max_op > 0x7FFFFFFFu) return rh::fail(RH_E_INVAL, "rh_segments_scan_launch: bad max_op");
+    if (g->buf_len > (uint64_t)INT64_MAX) return rh::fail(RH_E_RANGE, "rh_segments_scan_launch: buf_len too large");
+    SegArgs a{};
+    a.buf = g->buf;
+    a.buf_len = (int64_t)g->buf_len;
+    a.seg_off = g->seg_off;
+    a.seg_len = g->seg_len;
+    a.n_seg = g->n_seg;
+    a.max_op = g->max_op;
+    a.cap = g->frames_per_seg_cap;
+    a.scratch_off = g->scratch_off;
+    a.scratch_len = g->scratch_len;
+    a.seg_nframes = g->seg_nframes;
+    a.seg_status = g->seg_status;
+    a.seg_stop = g->seg_stop;
+    const int cus = ctx && ctx->num_cus > 0 ? ctx->num_cus : 256;
+    uint64_t grid = g->n_seg < (uint64_t)cus * 8 ? g->n_seg : (uint64_t)cus * 8;
+    hipLaunchKernelGGL(segment_walk_kernel, dim3((uint32_t)grid), dim3(64), 0, stream, a);
+    RH_HIP(hipGetLastError());
+    hipLaunchKernelGGL(segment_scan_kernel, dim3(1), dim3(kScanThreads), 0, stream, g->seg_nframes, g->n_seg,
+                       g->frames_per_seg_cap, g->seg_first, g->total_frames);
+    RH_HIP(hipGetLastError());
+    hipLaunchKernelGGL(segment_compact_kernel, dim3((uint32_t)grid), dim3(256), 0, stream, g->scratch_off,
+                       g->scratch_len, g->seg_nframes, g->seg_first, g->n_seg, g->frames_per_seg_cap, g->frame_off,
+                       g->frame_len, g->frame_cap);
+    RH_HIP(hipGetLastError());
+    return RH_OK;
+}

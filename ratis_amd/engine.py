@@ -12,6 +12,10 @@ Reference mapping (paths relative to the ratis tree):
   * :func:`crc32c_frames` = ``PureJavaCrc32C`` (PureJavaCrc32C.java:43-152) over
     ``SegmentedRaftLogOutputStream.write`` frames (:86-110), verified as in
     ``SegmentedRaftLogReader.decodeEntry`` (:327-336) or stamped as in the writer.
+  * :func:`segments_scan` = the reader's framing walk (``verifyHeader`` :179-205, ``decodeEntry``
+    :291-323, ``verifyTerminator`` :251-280) over many segment images at once, and
+    :func:`read_segments` = framing + CRC verify, i.e. ``LogSegment.readSegmentFile``
+    (LogSegment.java:166-196) minus the proto parse.
 """
 from __future__ import annotations
 
@@ -22,7 +26,7 @@ from typing import Optional, Sequence
 import torch
 
 from . import _lib
-from ._lib import RH_MODE_COMMIT, RH_MODE_WATCH, RhCommitSoa, RhFrames, check
+from ._lib import RH_MODE_COMMIT, RH_MODE_WATCH, RhCommitSoa, RhFrames, RhSegments, check
 
 
 def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
@@ -262,3 +266,132 @@ def crc32c_bytes(ctx: Context, data: torch.Tensor, init_state: int = 0xFFFFFFFF)
     crc32c_frames(ctx, fb, flags=0, init_state=init_state)
     torch.cuda.synchronize()
     return int(fb.crc_out.item()) & 0xFFFFFFFF
+
+
+# ---- segment framing ---------------------------------------------------------------------------
+RH_SEG_E_CHECKSUM = -2   # read_segments only: the first frame whose CRC does not verify
+
+
+@dataclass
+class SegmentBatch:
+    """Many segment images in one HBM buffer, plus the framing outputs."""
+
+    buf: torch.Tensor          # uint8 [buf_len]
+    seg_off: torch.Tensor      # int64 [n_seg]
+    seg_len: torch.Tensor      # int64 [n_seg]
+    max_op: int = 4 * 1024 * 1024
+    frames_per_seg_cap: int = 4096
+    frame_cap: Optional[int] = None
+    scratch_off: Optional[torch.Tensor] = None
+    scratch_len: Optional[torch.Tensor] = None
+    frame_off: Optional[torch.Tensor] = None   # int64 [frame_cap]
+    frame_len: Optional[torch.Tensor] = None   # int32 [frame_cap]
+    seg_first: Optional[torch.Tensor] = None   # int64 [n_seg]
+    seg_nframes: Optional[torch.Tensor] = None  # int32 [n_seg]
+    seg_status: Optional[torch.Tensor] = None  # int32 [n_seg]
+    seg_stop: Optional[torch.Tensor] = None    # int64 [n_seg]
+    total_frames: Optional[torch.Tensor] = None  # int64 [1]
+
+    @property
+    def n_seg(self) -> int:
+        return int(self.seg_off.numel())
+
+    def alloc_outputs(self) -> "SegmentBatch":
+        dev, n, cap = self.buf.device, self.n_seg, self.frames_per_seg_cap
+        if self.frame_cap is None:
+            self.frame_cap = max(1, n * cap)
+        e = lambda k, dt: torch.empty(k, dtype=dt, device=dev)  # noqa: E731
+        if self.scratch_off is None:
+            self.scratch_off = e(max(1, n * cap), torch.int64)
+            self.scratch_len = e(max(1, n * cap), torch.int32)
+        if self.frame_off is None:
+            self.frame_off = e(self.frame_cap, torch.int64)
+            self.frame_len = e(self.frame_cap, torch.int32)
+        if self.seg_first is None:
+            self.seg_first = e(max(1, n), torch.int64)
+            self.seg_nframes = e(max(1, n), torch.int32)
+            self.seg_status = e(max(1, n), torch.int32)
+            self.seg_stop = e(max(1, n), torch.int64)
+            self.total_frames = torch.zeros(1, dtype=torch.int64, device=dev)
+        return self
+
+    def to_struct(self) -> RhSegments:
+        if self.buf.dtype != torch.uint8:
+            raise ValueError("buf must be uint8")
+        if self.seg_off.dtype != torch.int64 or self.seg_len.dtype != torch.int64:
+            raise ValueError("seg_off and seg_len must be int64")
+        if self.seg_len.numel() != self.n_seg:
+            raise ValueError("seg_off and seg_len lengths differ")
+        if self.scratch_off is None or self.scratch_off.numel() < self.n_seg * self.frames_per_seg_cap:
+            raise ValueError("scratch too small for n_seg * frames_per_seg_cap (call alloc_outputs)")
+        if self.frame_off.numel() < self.frame_cap or self.frame_len.numel() < self.frame_cap:
+            raise ValueError("frame table smaller than frame_cap")
+        g = RhSegments()
+        g.buf = _ptr(self.buf)
+        g.buf_len = self.buf.numel()
+        g.seg_off = _ptr(self.seg_off)
+        g.seg_len = _ptr(self.seg_len)
+        g.n_seg = self.n_seg
+        g.max_op = self.max_op
+        g.frames_per_seg_cap = self.frames_per_seg_cap
+        g.scratch_off = _ptr(self.scratch_off)
+        g.scratch_len = _ptr(self.scratch_len)
+        g.frame_off = _ptr(self.frame_off)
+        g.frame_len = _ptr(self.frame_len)
+        g.frame_cap = self.frame_cap
+        g.seg_first = _ptr(self.seg_first)
+        g.seg_nframes = _ptr(self.seg_nframes)
+        g.seg_status = _ptr(self.seg_status)
+        g.seg_stop = _ptr(self.seg_stop)
+        g.total_frames = _ptr(self.total_frames)
+        return g
+
+
+def segments_scan(ctx: Context, batch: SegmentBatch, stream: Optional[torch.cuda.Stream] = None) -> None:
+    """Enqueues the framing walk (asynchronous): fills the dense frame table and per-segment status."""
+    batch.alloc_outputs()
+    g = batch.to_struct()
+    check(_lib.load().rh_segments_scan_launch(ctx.handle, ctypes.byref(g), _stream_ptr(stream)))
+
+
+def read_segments(ctx: Context, batch: SegmentBatch, stream: Optional[torch.cuda.Stream] = None) -> dict:
+    """``LogSegment.readSegmentFile`` over every segment: framing, then CRC32C verify of every frame,
+    then each segment truncated at its first bad frame (``decodeEntry`` throws ChecksumException
+    there, RDR:330-336).  Returns device tensors ``n_ok``, ``status``, ``stop`` per segment plus the
+    frame table and CRC results.  All work stays on the device stream; tensor ops are glue only."""
+    segments_scan(ctx, batch, stream)
+    (stream or torch.cuda.current_stream()).synchronize()
+    n_total = min(int(batch.total_frames.item()), batch.frame_cap)
+    dev = batch.buf.device
+    fb = FrameBatch(buf=batch.buf, frame_off=batch.frame_off[:n_total],
+                    frame_len=batch.frame_len[:n_total]).alloc_outputs()
+    if n_total:
+        crc32c_frames(ctx, fb, flags=_lib.RH_CRC_VERIFY, stream=stream)
+    with torch.cuda.stream(stream) if stream is not None else _nullctx():
+        nseg = batch.n_seg
+        n_found = batch.seg_nframes[:nseg].to(torch.int64).clamp(max=batch.frames_per_seg_cap)
+        first = batch.seg_first[:nseg]
+        idx = torch.arange(n_total, device=dev)
+        bad = ((fb.bad_bits.view(-1, 1) >> torch.arange(64, device=dev)) & 1).view(-1)[:n_total].bool()
+        seg_of = torch.searchsorted(first, idx, right=True) - 1
+        big = torch.iinfo(torch.int64).max
+        first_bad = torch.full((nseg,), big, dtype=torch.int64, device=dev)
+        first_bad.scatter_reduce_(0, seg_of[bad], idx[bad], reduce="amin")
+        has_bad = first_bad < first + n_found
+        n_ok = torch.where(has_bad, first_bad - first, n_found)
+        status = torch.where(has_bad, torch.full_like(batch.seg_status[:nseg], RH_SEG_E_CHECKSUM),
+                             batch.seg_status[:nseg])
+        if n_total:
+            stop_abs = batch.frame_off[first_bad.clamp(max=n_total - 1)]
+            stop = torch.where(has_bad, stop_abs - batch.seg_off, batch.seg_stop[:nseg])
+        else:
+            stop = batch.seg_stop[:nseg].clone()
+    return {"n_ok": n_ok, "status": status, "stop": stop, "frames": fb, "total_frames": batch.total_frames}
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        return False

@@ -65,6 +65,7 @@ int main(void) {
   printf("rh_commit_soa %zu\n", sizeof(rh_commit_soa));
   printf("rh_frames %zu\n", sizeof(rh_frames));
   printf("rh_delta %zu\n", sizeof(rh_delta));
+  printf("rh_segments %zu\n", sizeof(rh_segments));
   F(rh_commit_soa, n) F(rh_commit_soa, n_followers) F(rh_commit_soa, mode) F(rh_commit_soa, gap_threshold)
   F(rh_commit_soa, follower_index) F(rh_commit_soa, col_stride) F(rh_commit_soa, self_index)
   F(rh_commit_soa, commit_in) F(rh_commit_soa, term_start) F(rh_commit_soa, conf) F(rh_commit_soa, commit_out)
@@ -74,6 +75,11 @@ int main(void) {
   F(rh_frames, buf) F(rh_frames, buf_len) F(rh_frames, frame_off) F(rh_frames, frame_len) F(rh_frames, n)
   F(rh_frames, init_state) F(rh_frames, reserved) F(rh_frames, crc_out) F(rh_frames, bad_bits) F(rh_frames, n_bad)
   F(rh_delta, slot) F(rh_delta, column) F(rh_delta, reserved) F(rh_delta, value)
+  F(rh_segments, buf) F(rh_segments, buf_len) F(rh_segments, seg_off) F(rh_segments, seg_len)
+  F(rh_segments, n_seg) F(rh_segments, max_op) F(rh_segments, frames_per_seg_cap) F(rh_segments, scratch_off)
+  F(rh_segments, scratch_len) F(rh_segments, frame_off) F(rh_segments, frame_len) F(rh_segments, frame_cap)
+  F(rh_segments, seg_first) F(rh_segments, seg_nframes) F(rh_segments, seg_status) F(rh_segments, seg_stop)
+  F(rh_segments, total_frames)
   printf("conf %u\n", rh_conf_pack(0x5, 1, 1, 0x3, 1, 1));
   return 0;
 }
@@ -91,7 +97,9 @@ def test_struct_layouts_match_header(tmp_path):
     assert int(vals["rh_commit_soa"]) == ctypes.sizeof(_lib.RhCommitSoa)
     assert int(vals["rh_frames"]) == ctypes.sizeof(_lib.RhFrames)
     assert int(vals["rh_delta"]) == ctypes.sizeof(_lib.RhDelta)
-    for cname, cls in (("rh_commit_soa", _lib.RhCommitSoa), ("rh_frames", _lib.RhFrames), ("rh_delta", _lib.RhDelta)):
+    assert int(vals["rh_segments"]) == ctypes.sizeof(_lib.RhSegments)
+    for cname, cls in (("rh_commit_soa", _lib.RhCommitSoa), ("rh_frames", _lib.RhFrames), ("rh_delta", _lib.RhDelta),
+                       ("rh_segments", _lib.RhSegments)):
         for fname, _ in cls._fields_:
             assert int(vals[f"{cname}.{fname}"]) == getattr(cls, fname).offset, (cname, fname)
     assert int(vals["conf"]) == _lib.conf_pack(0x5, True, True, 0x3, True, True)

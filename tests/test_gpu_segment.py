@@ -1,0 +1,230 @@
+"""GPU parity of the segment framing walk (rh_segments_scan_launch) and of read_segments
+(framing + CRC verify = LogSegment.readSegmentFile, LogSegment.java:166-196) against the oracle's
+orc_segment_scan (SegmentedRaftLogReader verifyHeader/decodeEntry/verifyTerminator).
+
+Segments are built on the host with the oracle's frame writer, then damaged the ways the reader
+distinguishes: partially written header, corrupt header, truncated entry / varint / trailer,
+garbage in the terminator padding, oversize and negative lengths, malformed varints, flipped
+payload bits.  Many segments share one buffer at arbitrary (unaligned) offsets."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HEADER = b"RaftLog1"
+KINDS = ["clean_pad", "clean_exact", "empty", "short_header", "zero_header", "bad_header", "truncate",
+         "truncate_varint", "pad_garbage", "crc_flip", "varint_bad", "oversize", "negative", "tiny"]
+
+
+def _protos(rng, n, big):
+    sizes = rng.integers(1, 300, n)
+    if big:
+        k = max(1, n // 8)
+        sizes[rng.choice(n, k, replace=False)] = rng.integers(3000, 40000, k)
+    return [rng.integers(0, 256, int(s), dtype=np.uint8).tobytes() for s in sizes]
+
+
+def make_segment(orc, rng, kind, big=False):
+    """Returns (image bytes, crc_corrupted flag)."""
+    n = int(rng.integers(1, 120))
+    frames = [orc.frame_write(p) for p in _protos(rng, n, big)]
+    body = HEADER + b"".join(frames)
+    bounds = np.cumsum([len(HEADER)] + [len(f) for f in frames])   # frame starts + end
+    pad = int(rng.integers(1, 5000))
+    if kind == "clean_pad":
+        return body + bytes(pad), False
+    if kind == "clean_exact":
+        return body, False
+    if kind == "empty":
+        return b"", False
+    if kind == "short_header":
+        return HEADER[: int(rng.integers(1, 8))] + bytes(int(rng.integers(0, 8))), False
+    if kind == "zero_header":
+        return bytes(int(rng.integers(1, 300))), False
+    if kind == "bad_header":
+        b = bytearray(body)
+        b[int(rng.integers(0, 8))] ^= 0x20
+        return bytes(b), False
+    if kind == "truncate":
+        return body[: int(rng.integers(9, len(body)))], False
+    if kind == "truncate_varint":
+        f = orc.frame_write(bytes(300))           # 2-byte varint; cut after its first byte
+        return body + f[:1], False
+    if kind == "pad_garbage":
+        p = bytearray(pad)
+        p[int(rng.integers(0, pad))] = int(rng.integers(1, 256))
+        return body + bytes(p), False
+    if kind == "crc_flip":
+        b = bytearray(body + bytes(pad))
+        i = int(rng.integers(0, n))
+        lo, hi = int(bounds[i]), int(bounds[i + 1])
+        b[int(rng.integers(lo + 3, hi))] ^= 1 << int(rng.integers(0, 8))
+        return bytes(b), True
+    if kind == "varint_bad":
+        i = int(rng.integers(0, n + 1))
+        return body[: bounds[i]] + b"\xff" * 10 + body[bounds[i]:], False
+    if kind == "oversize":
+        from ratis_amd import segment
+        return body + segment.varint(5 << 20) + bytes(64), False   # length 5 MiB > maxOpSize
+    if kind == "negative":
+        return body + b"\xff\xff\xff\xff\x0f" + bytes(32), False
+    if kind == "tiny":   # frames of 1..3 byte protos, back to back
+        fr = [orc.frame_write(bytes([1 + j % 200]) * (1 + j % 3)) for j in range(int(rng.integers(1, 3000)))]
+        return HEADER + b"".join(fr) + bytes(pad), False
+    raise AssertionError(kind)
+
+
+def pack(images, rng, align_random=True):
+    offs, parts, pos = [], [], 0
+    for img in images:
+        gap = int(rng.integers(0, 40)) if align_random else (-pos) % 16
+        parts.append(bytes(rng.integers(0, 256, gap, dtype=np.uint8)))   # junk between segments
+        pos += gap
+        offs.append(pos)
+        parts.append(img)
+        pos += len(img)
+    parts.append(bytes(rng.integers(0, 256, 64, dtype=np.uint8)))
+    return np.frombuffer(b"".join(parts), dtype=np.uint8).copy(), np.asarray(offs, np.int64), \
+        np.asarray([len(i) for i in images], np.int64)
+
+
+def run_scan(ctx, buf, offs, lens, max_op=4 << 20, cap=4096):
+    import torch
+
+    from ratis_amd import engine
+    dev = torch.device("cuda")
+    b = engine.SegmentBatch(buf=torch.from_numpy(buf).to(dev), seg_off=torch.from_numpy(offs).to(dev),
+                            seg_len=torch.from_numpy(lens).to(dev), max_op=max_op, frames_per_seg_cap=cap)
+    engine.segments_scan(ctx, b)
+    torch.cuda.synchronize()
+    return b
+
+
+def check_against_oracle(orc, b, buf, offs, lens, max_op=4 << 20, skip_crc=None):
+    first = b.seg_first.cpu().numpy()
+    nfr = b.seg_nframes.cpu().numpy()
+    st = b.seg_status.cpu().numpy()
+    stop = b.seg_stop.cpu().numpy()
+    total = int(b.total_frames.item())
+    fo = b.frame_off[:total].cpu().numpy()
+    fl = b.frame_len[:total].cpu().numpy()
+    assert total == int(nfr.sum())
+    for s in range(len(offs)):
+        if skip_crc is not None and skip_crc[s]:
+            continue
+        img = buf[offs[s]: offs[s] + lens[s]]
+        ro, rl, _, rst, rstop = orc.segment_scan(img, max_op=max_op)
+        assert (st[s], stop[s], nfr[s]) == (rst, rstop, len(ro)), s
+        k = first[s]
+        assert np.array_equal(fo[k: k + nfr[s]] - offs[s], ro), s
+        assert np.array_equal(fl[k: k + nfr[s]], rl), s
+
+
+@pytest.mark.parametrize("big", [False, True])
+def test_framing_matches_oracle_every_kind(ctx, orc, big):
+    rng = np.random.default_rng(7 + big)
+    kinds = [KINDS[i % len(KINDS)] for i in range(len(KINDS) * 6)]
+    made = [make_segment(orc, rng, k, big) for k in kinds]
+    buf, offs, lens = pack([m[0] for m in made], rng)
+    b = run_scan(ctx, buf, offs, lens)
+    # CRC-flipped segments frame identically to their clean selves; the oracle stops at the CRC.
+    check_against_oracle(orc, b, buf, offs, lens, skip_crc=[m[1] for m in made])
+    st = b.seg_status.cpu().numpy()
+    seen = set(st.tolist())
+    from ratis_amd import _lib
+    for code in (_lib.RH_SEG_END, _lib.RH_SEG_PARTIAL, _lib.RH_SEG_E_OVERSIZE, _lib.RH_SEG_E_PADDING,
+                 _lib.RH_SEG_E_VARINT, _lib.RH_SEG_E_HEADER):
+        assert code in seen, code
+
+
+def test_read_segments_matches_oracle_including_crc(ctx, orc):
+    from ratis_amd import engine
+    rng = np.random.default_rng(99)
+    kinds = [KINDS[i % len(KINDS)] for i in range(len(KINDS) * 5)]
+    made = [make_segment(orc, rng, k, big=bool(i % 2)) for i, k in enumerate(kinds)]
+    buf, offs, lens = pack([m[0] for m in made], rng)
+    import torch
+    dev = torch.device("cuda")
+    b = engine.SegmentBatch(buf=torch.from_numpy(buf).to(dev), seg_off=torch.from_numpy(offs).to(dev),
+                            seg_len=torch.from_numpy(lens).to(dev))
+    r = engine.read_segments(ctx, b)
+    torch.cuda.synchronize()
+    n_ok, st, stop = r["n_ok"].cpu().numpy(), r["status"].cpu().numpy(), r["stop"].cpu().numpy()
+    assert (st == engine.RH_SEG_E_CHECKSUM).sum() == sum(m[1] for m in made)
+    for s in range(len(offs)):
+        ro, _, _, rst, rstop = orc.segment_scan(buf[offs[s]: offs[s] + lens[s]])
+        assert (st[s], stop[s], n_ok[s]) == (rst, rstop, len(ro)), (s, kinds[s])
+
+
+def test_small_max_op_limits(ctx, orc):
+    """maxOpSize small enough that the LimitedInputStream checks on the varint, the body and the
+    4 trailer reads (RDR:66-82, 314-317, 343-352) each decide some frame."""
+    rng = np.random.default_rng(5)
+    images = []
+    for n in range(1, 40):
+        images.append(HEADER + orc.frame_write(bytes(rng.integers(1, 256, n, dtype=np.uint8))) + bytes(8))
+    buf, offs, lens = pack(images, rng)
+    for max_op in (8, 16, 20, 21, 22, 23, 24, 25, 40):
+        b = run_scan(ctx, buf, offs, lens, max_op=max_op)
+        check_against_oracle(orc, b, buf, offs, lens, max_op=max_op)
+
+
+def test_frame_capacity_reports_and_truncates(ctx, orc):
+    from ratis_amd import _lib
+    rng = np.random.default_rng(3)
+    img = HEADER + b"".join(orc.frame_write(bytes([7]) * 5) for _ in range(100)) + bytes(100)
+    buf, offs, lens = pack([img, img], rng)
+    b = run_scan(ctx, buf, offs, lens, cap=64)
+    st = b.seg_status.cpu().numpy()
+    assert list(st) == [_lib.RH_SEG_E_CAPACITY] * 2
+    assert list(b.seg_nframes.cpu().numpy()) == [64, 64]
+    ro, rl, _, _, _ = orc.segment_scan(img)
+    fo = b.frame_off[:128].cpu().numpy()
+    assert np.array_equal(fo[:64] - offs[0], ro[:64]) and np.array_equal(fo[64:] - offs[1], ro[:64])
+
+
+def test_raftlog_readwrite_segment_golden(ctx, orc):
+    """The segment TestRaftLogReadWrite.testReadWriteLog writes (100 SimpleOperation entries,
+    tests/golden/raftlog_rw.npz) frames to exactly the frames the writer laid out."""
+    import os
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "raftlog_rw.npz"))
+    img = np.asarray(z["image"], dtype=np.uint8)
+    rng = np.random.default_rng(0)
+    buf, offs, lens = pack([img.tobytes(), img.tobytes() + bytes(4096)], rng)
+    b = run_scan(ctx, buf, offs, lens)
+    check_against_oracle(orc, b, buf, offs, lens)
+    assert list(b.seg_nframes.cpu().numpy()) == [100, 100]
+
+
+def test_config5_shape_many_segments(ctx, orc):
+    """32 MiB segments of 4 KiB frames, 4 segments from the synthetic
+    generator: 8190 frames each, clean end at the zero padding; compared with the oracle walk."""
+    import torch
+
+    from ratis_amd import engine, workload
+    ss = workload.synth_segments(ctx, n_segments=4, corrupt_rate=0.0, seed=17)
+    n = ss.n_segments
+    seg_off = torch.arange(n, dtype=torch.int64, device="cuda") * ss.segment_size
+    seg_len = torch.full((n,), ss.segment_size, dtype=torch.int64, device="cuda")
+    b = engine.SegmentBatch(buf=ss.batch.buf, seg_off=seg_off, seg_len=seg_len,
+                            frames_per_seg_cap=ss.frames_per_segment + 16)
+    engine.segments_scan(ctx, b)
+    torch.cuda.synchronize()
+    assert int(b.total_frames.item()) == n * ss.frames_per_segment
+    assert torch.equal(b.frame_off[: n * ss.frames_per_segment], ss.batch.frame_off)
+    assert torch.equal(b.frame_len[: n * ss.frames_per_segment], ss.batch.frame_len)
+    seg0 = ss.batch.buf[: ss.segment_size].cpu().numpy()
+    _, _, _, rst, rstop = orc.segment_scan(seg0)
+    assert (int(b.seg_status[0]), int(b.seg_stop[0])) == (rst, rstop)
+
+
+def test_bad_arguments(ctx):
+    import torch
+
+    from ratis_amd import _lib, engine
+    dev = torch.device("cuda")
+    b = engine.SegmentBatch(buf=torch.zeros(16, dtype=torch.uint8, device=dev),
+                            seg_off=torch.zeros(1, dtype=torch.int64, device=dev),
+                            seg_len=torch.full((1,), 16, dtype=torch.int64, device=dev), frames_per_seg_cap=0)
+    with pytest.raises(_lib.IllegalArgumentError):
+        engine.segments_scan(ctx, b)
