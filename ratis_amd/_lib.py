@@ -155,6 +155,7 @@ _SIGNATURES = {
     "rh_crc32c_verify_host": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_uint64, c_void_p,
                                       c_void_p, POINTER(c_uint64)]),
     "rh_segments_scan_launch": (c_int, [c_void_p, POINTER(RhSegments), c_void_p]),
+    "rh_segments_set_variant": (c_int, [c_int]),
     "rh_crc32c_num_variants": (c_int, []),
     "rh_commit_num_variants": (c_int, []),
     "rh_commit_set_variant": (c_int, [c_int]),

@@ -436,6 +436,8 @@ RH_EXPORT int rh_segments_scan_launch(rh_ctx* ctx, const rh_segments* segs, void
     return rh_segments_launch_impl(ctx, segs, pick_stream(ctx, stream));
 }
 
+RH_EXPORT int rh_segments_set_variant(int variant) { return rh_segments_set_variant_impl(variant); }
+
 RH_EXPORT int rh_crc32c_num_variants(void) { return rh_crc_num_variants(); }
 
 RH_EXPORT int rh_commit_num_variants(void) { return rh_commit_num_variants_impl(); }

@@ -67,3 +67,4 @@ int rh_crc_num_variants();
 int rh_commit_set_variant_impl(int v);
 int rh_commit_num_variants_impl();
 int rh_segments_launch_impl(rh_ctx* ctx, const rh_segments* segs, hipStream_t stream);
+int rh_segments_set_variant_impl(int v);

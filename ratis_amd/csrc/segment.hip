@@ -245,6 +245,227 @@ __global__ __launch_bounds__(64) void segment_walk_kernel(SegArgs a) {
     }
 }
 
+// ---- v2: one 256-thread block per segment, double-buffered windows ---------------------------
+// The segment is cut into W-byte windows on a 16-B aligned grid.  Two windows live in an LDS ring
+// (2W bytes); while the walker (thread 0) walks the frames that START in window k, the block's
+// loads of window k+2 are in flight in registers, so HBM latency overlaps the serial walk.  Ring
+// index of segment byte p = (p - A) & (2W - 1), A = the grid origin (-15..0).  A frame whose
+// length jumps past window k+1 restarts the pipeline at the window holding the new position.
+constexpr int kBlock2 = 256;
+
+template <int W>
+struct Win {
+    static constexpr int PER = W / (kBlock2 * 16);  // 16-B loads per thread per window
+    u32x4s r[PER];
+
+    __device__ __forceinline__ void load(const uint8_t* seg, int64_t L, int64_t wstart, int t) {
+#pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int64_t p = wstart + (int64_t)(i * kBlock2 + t) * 16;
+            u32x4s v{0, 0, 0, 0};
+            if (p >= 0 && p + 16 <= L) {
+                v = *reinterpret_cast<const u32x4s*>(seg + p);
+            } else if (p < L && p + 16 > 0) {
+                uint32_t w[4] = {0, 0, 0, 0};
+                for (int k = p < 0 ? (int)-p : 0; k < 16 && p + k < L; ++k)
+                    w[k >> 2] |= (uint32_t)seg[p + k] << (8 * (k & 3));
+                v = {w[0], w[1], w[2], w[3]};
+            }
+            r[i] = v;
+        }
+    }
+    __device__ __forceinline__ void store(uint8_t* ring, int slot, int t) const {
+#pragma unroll
+        for (int i = 0; i < PER; ++i)
+            *reinterpret_cast<u32x4s*>(ring + slot * W + (i * kBlock2 + t) * 16) = r[i];
+    }
+};
+
+template <int W>
+__global__ __launch_bounds__(kBlock2) void segment_walk_kernel2(SegArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t ring[];  // [2W]
+    __shared__ int sh_status;
+    __shared__ long long sh_pos;
+    __shared__ uint32_t sh_nfr;
+    __shared__ unsigned long long sh_min;
+    constexpr int64_t MASK = 2 * W - 1;
+    const int t = threadIdx.x;
+    for (uint64_t s = blockIdx.x; s < a.n_seg; s += gridDim.x) {
+        const int64_t base = (int64_t)a.seg_off[s];
+        int64_t L = (int64_t)a.seg_len[s];
+        if (base > a.buf_len) L = 0;
+        else if (L > a.buf_len - base) L = a.buf_len - base;
+        const uint8_t* seg = a.buf + base;
+        const int64_t A = (base & ~(int64_t)15) - base;
+        if (t == 0) {  // verifyHeader (RDR:179-205)
+            const char H[8] = {'R', 'a', 'f', 't', 'L', 'o', 'g', '1'};
+            const int64_t rl = L < 8 ? L : 8;
+            int match = 0, bad = 0;
+            for (int i = 0; i < rl; ++i) {
+                const uint8_t b = seg[i];
+                if (match == i && b == (uint8_t)H[i]) match = i + 1;
+                else if (b != 0) bad = 1;
+            }
+            const bool ok = rl == 8 && match == 8;
+            sh_status = ok ? (8 >= L ? RH_SEG_END : kWalking) : (bad ? RH_SEG_E_HEADER : RH_SEG_END);
+            sh_pos = ok ? 8 : 0;
+            sh_nfr = 0;
+        }
+        __syncthreads();
+        int status = sh_status;
+        int64_t pos = sh_pos;
+        Win<W> nxt;
+        while (status == kWalking) {
+            // (re)start the pipeline at the window holding pos
+            int64_t k = (pos - A) / W;
+            {
+                Win<W> cur;
+                cur.load(seg, L, A + k * W, t);
+                cur.store(ring, (int)(k & 1), t);
+            }
+            nxt.load(seg, L, A + (k + 1) * W, t);
+            for (;;) {
+                nxt.store(ring, (int)((k + 1) & 1), t);   // ring now holds windows k, k+1
+                __syncthreads();
+                nxt.load(seg, L, A + (k + 2) * W, t);       // in flight during the walk
+                if (t == 0) {
+                    const int64_t wend = A + (k + 1) * W;
+                    uint32_t nfr = sh_nfr;
+                    int st = kWalking;
+                    int64_t p = pos;
+                    while (p < wend) {
+                        if (p >= L) {
+                            st = RH_SEG_END;
+                            break;
+                        }
+                        uint32_t b[5];
+#pragma unroll
+                        for (int i = 0; i < 5; ++i) b[i] = ring[(p + i - A) & MASK];
+                        if (b[0] == 0) {  // terminator (SegmentedRaftLogFormat.isTerminator)
+                            st = kTermPending;
+                            break;
+                        }
+                        // CodedInputStream.readRawVarint32(firstByte, in); EOF -> truncatedMessage
+                        const int64_t avail = L - p;
+                        uint32_t result = 0;
+                        bool done = false, trunc = false;
+#pragma unroll
+                        for (int i = 0; i < 5; ++i) {
+                            if (!done && !trunc) {
+                                if (i >= avail) {
+                                    trunc = true;
+                                } else {
+                                    result |= (b[i] & 0x7f) << (7 * i);
+                                    done = (b[i] & 0x80) == 0;
+                                }
+                            }
+                        }
+                        if (!done && !trunc) {  // discard up to 5 more bytes of a 64-bit varint
+                            for (int i = 5; i < 10; ++i) {
+                                if (i >= avail) {
+                                    trunc = true;
+                                    break;
+                                }
+                                if ((ring[(p + i - A) & MASK] & 0x80) == 0) {
+                                    done = true;
+                                    break;
+                                }
+                            }
+                        }
+                        if (!done) {
+                            st = RH_SEG_E_VARINT;
+                            break;
+                        }
+                        const int32_t n = (int32_t)result;
+                        if (n > (int32_t)a.max_op) {
+                            st = RH_SEG_E_OVERSIZE;
+                            break;
+                        }
+                        if (n < 0) {
+                            st = RH_SEG_E_VARINT;
+                            break;
+                        }
+                        const int64_t total = (int64_t)varint32_size((uint32_t)n) + n;
+                        if (total > (int64_t)a.max_op) {
+                            st = RH_SEG_E_OVERSIZE;
+                            break;
+                        }
+                        if (p + total > L) {
+                            st = RH_SEG_PARTIAL;
+                            break;
+                        }
+                        // readInt: checkLimit(1) before each of the 4 reads (RDR:66-82)
+                        const int64_t lim_room = (int64_t)a.max_op - total;  // reads allowed by the limit
+                        const int64_t eof_room = L - p - total;             // bytes before EOF
+                        if (lim_room < 4 || eof_room < 4) {
+                            st = lim_room <= eof_room ? RH_SEG_E_OVERSIZE : RH_SEG_PARTIAL;
+                            break;
+                        }
+                        if (nfr >= a.cap) {
+                            st = RH_SEG_E_CAPACITY;
+                            break;
+                        }
+                        a.scratch_off[s * (uint64_t)a.cap + nfr] = (uint64_t)(base + p);
+                        a.scratch_len[s * (uint64_t)a.cap + nfr] = (uint32_t)(total + 4);
+                        ++nfr;
+                        p += total + 4;
+                    }
+                    sh_status = st;
+                    sh_pos = p;
+                    sh_nfr = nfr;
+                }
+                __syncthreads();
+                status = sh_status;
+                pos = sh_pos;
+                if (status != kWalking) break;
+                if (pos >= A + (k + 2) * W) break;  // jumped past the ring: restart there
+                ++k;
+            }
+        }
+        if (status == kTermPending) {
+            // verifyTerminator (RDR:251-280): the first non-zero byte in [pos, L), block-wide
+            if (t == 0) sh_min = (unsigned long long)L;
+            __syncthreads();
+            const int64_t q0 = ((base + pos) & ~(int64_t)15) - base;
+            bool found = false;
+            for (int64_t q = q0; q < L && !found; q += (int64_t)W) {
+                Win<W> c;
+                c.load(seg, L, q, t);
+                unsigned long long my = (unsigned long long)L;
+#pragma unroll
+                for (int i = 0; i < Win<W>::PER; ++i) {
+                    const uint32_t ww[4] = {c.r[i].x, c.r[i].y, c.r[i].z, c.r[i].w};
+                    const int64_t p = q + (int64_t)(i * kBlock2 + t) * 16;
+                    for (int j = 0; j < 4; ++j) {
+                        if (ww[j] == 0) continue;
+                        for (int b = 0; b < 4; ++b) {
+                            const int64_t pb = p + 4 * j + b;
+                            if (((ww[j] >> (8 * b)) & 0xff) && pb >= pos && pb < L && (unsigned long long)pb < my)
+                                my = (unsigned long long)pb;
+                        }
+                    }
+                }
+                if (my < (unsigned long long)L) atomicMin(&sh_min, my);
+                __syncthreads();
+                found = sh_min < (unsigned long long)L;
+                __syncthreads();
+            }
+            if (found) {
+                status = RH_SEG_E_PADDING;
+                pos = (int64_t)sh_min;
+            } else {
+                status = RH_SEG_END;
+            }
+        }
+        if (t == 0) {
+            a.seg_nframes[s] = sh_nfr;
+            a.seg_status[s] = status;
+            a.seg_stop[s] = (uint64_t)pos;
+        }
+        __syncthreads();
+    }
+}
+
 // Exclusive scan of seg_nframes (capped at cap) -> seg_first, total_frames.  One block.
 __global__ __launch_bounds__(kScanThreads) void segment_scan_kernel(const uint32_t* nframes, uint64_t n_seg,
                                                                     uint32_t cap, uint64_t* seg_first,
@@ -287,7 +508,31 @@ __global__ __launch_bounds__(256) void segment_compact_kernel(const uint64_t* sc
     }
 }
 
+int g_seg_variant = 2;
+
+template <int W>
+hipError_t launch_walk2(const SegArgs& a, int cus, hipStream_t stream) {
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(segment_walk_kernel2<W>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 2 * W);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    const int per_cu = 2 * W <= 65536 ? 2 : 1;
+    const uint64_t cap = (uint64_t)cus * per_cu;
+    const uint64_t grid = a.n_seg < cap ? a.n_seg : cap;
+    hipLaunchKernelGGL(segment_walk_kernel2<W>, dim3((uint32_t)grid), dim3(kBlock2), 2 * W, stream, a);
+    return hipGetLastError();
+}
+
 }  // namespace
+
+int rh_segments_set_variant_impl(int v) {
+    if (v < 0 || v > 2) return rh::fail(RH_E_RANGE, "rh_segments_set_variant: variant out of range [0, 2]");
+    g_seg_variant = v;
+    return RH_OK;
+}
 
 int rh_segments_launch_impl(rh_ctx* ctx, const rh_segments* g, hipStream_t stream) {
     if (!g) return rh::fail(RH_E_INVAL, "rh_segments_scan_launch: segs == NULL");
@@ -313,7 +558,14 @@ int rh_segments_launch_impl(rh_ctx* ctx, const rh_segments* g, hipStream_t strea
     a.seg_stop = g->seg_stop;
     const int cus = ctx && ctx->num_cus > 0 ? ctx->num_cus : 256;
     uint64_t grid = g->n_seg < (uint64_t)cus * 8 ? g->n_seg : (uint64_t)cus * 8;
-    hipLaunchKernelGGL(segment_walk_kernel, dim3((uint32_t)grid), dim3(64), 0, stream, a);
+    const int v = g_seg_variant;
+    if (v == 0) {
+        hipLaunchKernelGGL(segment_walk_kernel, dim3((uint32_t)grid), dim3(64), 0, stream, a);
+    } else if (v == 1) {
+        RH_HIP(launch_walk2<32768>(a, cus, stream));
+    } else {
+        RH_HIP(launch_walk2<65536>(a, cus, stream));
+    }
     RH_HIP(hipGetLastError());
     hipLaunchKernelGGL(segment_scan_kernel, dim3(1), dim3(kScanThreads), 0, stream, g->seg_nframes, g->n_seg,
                        g->frames_per_seg_cap, g->seg_first, g->total_frames);

@@ -56,7 +56,26 @@ def main():
         x = np.array(res[v])
         print(json.dumps({"kernel": "crc32c", "variant": v, "median_GBps": round(float(np.median(x)), 1),
                           "min_GBps": round(float(x.min()), 1), "max_GBps": round(float(x.max()), 1)}))
-    del ss, fb
+    # segment framing walk over the same segment images
+    n = ss.n_segments
+    sb = engine.SegmentBatch(buf=fb.buf, seg_off=torch.arange(n, device="cuda", dtype=torch.int64) * ss.segment_size,
+                             seg_len=torch.full((n,), ss.segment_size, device="cuda", dtype=torch.int64),
+                             frames_per_seg_cap=ss.frames_per_segment + 16)
+    fr = []
+    for r in range(a.rounds):
+        engine.segments_scan(ctx, sb)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.iters):
+            engine.segments_scan(ctx, sb)
+        e1.record()
+        torch.cuda.synchronize()
+        fr.append(n * ss.segment_size / (e0.elapsed_time(e1) / a.iters * 1e-3) / 1e9)
+        assert int(sb.total_frames.item()) == n * ss.frames_per_segment
+    x = np.array(fr)
+    print(json.dumps({"kernel": "segments_scan", "segments": n, "median_GBps": round(float(np.median(x)), 1),
+                      "min_GBps": round(float(x.min()), 1), "max_GBps": round(float(x.max()), 1)}))
+    del ss, fb, sb
     # commit kernel variants over 8 rotating 1M-group batches (config 3)
     host = workload.commit_snapshot(1_000_000)
     alg = sum(h.algorithmic_bytes() for h in host)
@@ -87,7 +106,7 @@ def main():
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / 40
             cres[v].append(alg / (ms * 1e-3) / 1e9)
-    _lib.check(lib.rh_commit_set_variant(1))
+    _lib.check(lib.rh_commit_set_variant(0))
     for v in range(ncv):
         x = np.array(cres[v])
         print(json.dumps({"kernel": "commit", "variant": v, "median_GBps": round(float(np.median(x)), 1),

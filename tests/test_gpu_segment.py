@@ -120,9 +120,18 @@ def check_against_oracle(orc, b, buf, offs, lens, max_op=4 << 20, skip_crc=None)
         assert np.array_equal(fl[k: k + nfr[s]], rl), s
 
 
+@pytest.fixture(params=[0, 1, 2])
+def seg_variant(request):
+    from ratis_amd import _lib
+    lib = _lib.load()
+    _lib.check(lib.rh_segments_set_variant(request.param))
+    yield request.param
+    _lib.check(lib.rh_segments_set_variant(2))
+
+
 @pytest.mark.parametrize("big", [False, True])
-def test_framing_matches_oracle_every_kind(ctx, orc, big):
-    rng = np.random.default_rng(7 + big)
+def test_framing_matches_oracle_every_kind(ctx, orc, big, seg_variant):
+    rng = np.random.default_rng(7 + big + 10 * seg_variant)
     kinds = [KINDS[i % len(KINDS)] for i in range(len(KINDS) * 6)]
     made = [make_segment(orc, rng, k, big) for k in kinds]
     buf, offs, lens = pack([m[0] for m in made], rng)
@@ -156,7 +165,7 @@ def test_read_segments_matches_oracle_including_crc(ctx, orc):
         assert (st[s], stop[s], n_ok[s]) == (rst, rstop, len(ro)), (s, kinds[s])
 
 
-def test_small_max_op_limits(ctx, orc):
+def test_small_max_op_limits(ctx, orc, seg_variant):
     """maxOpSize small enough that the LimitedInputStream checks on the varint, the body and the
     4 trailer reads (RDR:66-82, 314-317, 343-352) each decide some frame."""
     rng = np.random.default_rng(5)
@@ -169,7 +178,7 @@ def test_small_max_op_limits(ctx, orc):
         check_against_oracle(orc, b, buf, offs, lens, max_op=max_op)
 
 
-def test_frame_capacity_reports_and_truncates(ctx, orc):
+def test_frame_capacity_reports_and_truncates(ctx, orc, seg_variant):
     from ratis_amd import _lib
     rng = np.random.default_rng(3)
     img = HEADER + b"".join(orc.frame_write(bytes([7]) * 5) for _ in range(100)) + bytes(100)
@@ -196,7 +205,7 @@ def test_raftlog_readwrite_segment_golden(ctx, orc):
     assert list(b.seg_nframes.cpu().numpy()) == [100, 100]
 
 
-def test_config5_shape_many_segments(ctx, orc):
+def test_config5_shape_many_segments(ctx, orc, seg_variant):
     """32 MiB segments of 4 KiB frames, 4 segments from the synthetic
     generator: 8190 frames each, clean end at the zero padding; compared with the oracle walk."""
     import torch
