@@ -217,6 +217,32 @@ int rh_crc32c_verify_host(rh_ctx* ctx, const uint8_t* seg, uint64_t seg_len, con
                           const uint32_t* frame_len, uint64_t n, uint32_t* crc_out, uint64_t* bad_bits,
                           uint64_t* n_bad);
 
+/* ---- leader lease (LeaderStateImpl.hasLease LSI:1229-1249; LeaderLease LL:60-103) ------------
+ * One tier = groups with the same follower-slot count F (0..14), same conf word as the commit
+ * path.  For every active group whose lease is enabled: if the lease is not valid and the conf is
+ * not a singleton, try LeaderLease.extend from the followers' lastRespondedAppendEntriesSendTime
+ * (majority of the peers responded within the timeout -> lease = earliest majority-ack time of the
+ * current and old confs); report hasLease (isRunning()/isReady() stay the caller's).  Times are
+ * System.nanoTime() values frozen at now_nanos; elapsed ms truncate like Java long division.
+ * Exact for |now - t| < 2^62 ns, where Timestamp.compareTo is a total order. */
+typedef struct rh_lease_soa {
+    uint64_t n;
+    uint32_t n_followers;          /* F, 0..14                                                    */
+    uint32_t reserved;
+    int64_t now_nanos;
+    int64_t timeout_ms;            /* leaseTimeoutMs = rpc.timeout.min x read.leader.lease.timeout.ratio */
+    const int64_t* follower_ts;    /* [F][col_stride]: lastRespondedAppendEntriesSendTime (nanos)  */
+    uint64_t col_stride;           /* elements between columns, >= n                              */
+    const uint32_t* conf;          /* [n] membership word (RH_CONF_*)                             */
+    const int64_t* lease_in;       /* [n] current lease timestamp (nanos)                         */
+    const uint64_t* enabled_bits;  /* optional [ceil(n/64)] LeaderLease.isEnabled; NULL = enabled */
+    int64_t* lease_out;            /* [n] lease after extension; may alias lease_in               */
+    uint64_t* has_lease_bits;      /* [ceil(n/64)] hasLease()                                     */
+    uint64_t* extended_bits;       /* optional [ceil(n/64)]: the lease was set by extend()        */
+} rh_lease_soa;
+
+int rh_lease_soa_launch(rh_ctx* ctx, const rh_lease_soa* tiers, int n_tiers, void* stream);
+
 /* ---- segment framing (SegmentedRaftLogReader.verifyHeader / decodeEntry / verifyTerminator) --
  * Walks each segment image: header "RaftLog1" (RDR:179-205), then frames varint32(n) || n bytes ||
  * 4-byte CRC while the first byte is non-zero (RDR:291-323), then checks that the terminator

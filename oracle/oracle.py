@@ -74,6 +74,11 @@ def load() -> ctypes.CDLL:
     L.orc_segment_scan.restype = c_uint64
     L.orc_segment_scan.argtypes = [c_void_p, c_uint64, c_uint32, c_uint64, c_void_p, c_void_p, c_void_p,
                                    POINTER(c_int), POINTER(c_uint64)]
+    L.orc_has_lease.restype = c_int
+    L.orc_has_lease.argtypes = [c_int, c_int64, c_int64, c_void_p, c_int, c_int, c_void_p, c_int, c_int, c_int,
+                                c_int64, POINTER(c_int64), POINTER(c_int)]
+    L.orc_lease_soa.restype = None
+    L.orc_lease_soa.argtypes = [c_uint64, c_uint32, c_int64, c_int64] + [c_void_p] * 7
     _lib = L
     return L
 
@@ -201,6 +206,80 @@ def commit_soa(follower: np.ndarray, self_index: np.ndarray, conf: np.ndarray, m
     out["valid_bits"] = vb
     out["advanced_bits"] = ab
     return out
+
+
+# ---- leader lease ----------------------------------------------------------------------------
+def has_lease(enabled: bool, now: int, timeout_ms: int, cur_ts, self_in_cur: bool, old_ts, self_in_old: bool,
+              transitional: bool, lease_in: int):
+    """orc_has_lease: LeaderStateImpl.hasLease for one group -> (has_lease, lease_out, extended)."""
+    cur = np.ascontiguousarray(cur_ts if len(cur_ts) else [0], dtype=np.int64)
+    old = np.ascontiguousarray(old_ts if len(old_ts) else [0], dtype=np.int64)
+    lo, ext = c_int64(), c_int()
+    r = load().orc_has_lease(int(enabled), now, timeout_ms, _p(cur), len(cur_ts), int(self_in_cur), _p(old),
+                             len(old_ts), int(self_in_old), int(transitional), lease_in, ctypes.byref(lo),
+                             ctypes.byref(ext))
+    return bool(r), lo.value, bool(ext.value)
+
+
+def py_has_lease(enabled, now, timeout_ms, cur_ts, self_in_cur, old_ts, self_in_old, transitional, lease_in):
+    """Pure-Python restatement of LeaderStateImpl.hasLease (LSI:1229-1249) / LeaderLease (LL:60-103)
+    with Java long semantics, written independently of the C one to cross-check it."""
+    import functools
+
+    def wrap(x):
+        x &= (1 << 64) - 1
+        return x - (1 << 64) if x >> 63 else x
+
+    def cmp(a, b):                       # Timestamp.compareTo
+        d = wrap(a - b)
+        return (d > 0) - (d < 0)
+
+    def elapsed_ms(t):                   # Timestamp.elapsedTimeMs, truncating division
+        d = wrap(now - t)
+        return abs(d) // 1000000 * (1 if d >= 0 else -1)
+
+    def has_majority(active, include_self):   # PeerConfiguration.hasMajority
+        if not active and not include_self:
+            return True
+        return (int(include_self) + sum(active)) > (len(active) + int(include_self)) // 2
+
+    def max_ts(ts):                      # LeaderLease.getMaxTimestampWithMajorityAck
+        if not ts:
+            return now
+        return sorted(ts, key=functools.cmp_to_key(cmp))[len(ts) // 2]
+
+    if not enabled:
+        return False, lease_in, False
+    singleton = len(cur_ts) + int(self_in_cur) == 1 and \
+        ((len(old_ts) + int(self_in_old)) if transitional else 0) <= 1
+    if singleton or elapsed_ms(lease_in) < timeout_ms:
+        return True, lease_in, False
+    ok = has_majority([elapsed_ms(t) < timeout_ms for t in cur_ts], self_in_cur)
+    if transitional:
+        ok = ok and has_majority([elapsed_ms(t) < timeout_ms for t in old_ts], self_in_old)
+    lease, ext = lease_in, False
+    if ok:
+        a = max_ts(list(cur_ts))
+        b = max_ts(list(old_ts)) if transitional else now
+        lease, ext = (b if cmp(a, b) > 0 else a), True
+    return bool(singleton or elapsed_ms(lease) < timeout_ms), lease, ext
+
+
+def lease_soa(follower_ts: np.ndarray, conf: np.ndarray, lease_in: np.ndarray, now: int, timeout_ms: int,
+              enabled_bits: Optional[np.ndarray] = None):
+    """Batched restatement with the argument layout of rh_lease_soa.  Returns a dict."""
+    F, n = follower_ts.shape
+    follower_ts = np.ascontiguousarray(follower_ts, dtype=np.int64)
+    conf = np.ascontiguousarray(conf).astype(np.uint32)
+    lease_in = np.ascontiguousarray(lease_in, dtype=np.int64)
+    en = None if enabled_bits is None else np.ascontiguousarray(enabled_bits, dtype=np.uint64)
+    lease_out = np.zeros(n, dtype=np.int64)
+    nw = (n + 63) // 64
+    hb = np.zeros(max(nw, 1), dtype=np.uint64)
+    eb = np.zeros(max(nw, 1), dtype=np.uint64)
+    load().orc_lease_soa(n, F, now, timeout_ms, _p(follower_ts), _p(conf), _p(lease_in), _p(en), _p(lease_out),
+                         _p(hb), _p(eb))
+    return {"lease": lease_out, "has_lease_bits": hb[:nw], "extended_bits": eb[:nw]}
 
 
 # ---- frames ----------------------------------------------------------------------------------

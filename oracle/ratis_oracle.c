@@ -334,6 +334,108 @@ ORC_API void orc_commit_soa(uint64_t n, uint32_t nf, int mode, int64_t gap,
 }
 
 /* ===================================================================================== */
+/* Leader lease -- LeaderStateImpl.hasLease (LSI:1229-1249), LeaderLease (LL:60-103),     */
+/* RaftConfigurationImpl.hasMajority/isSingleton (RCI:265-298), PeerConfiguration (PC:    */
+/* 152-169), Timestamp (TS:51-56, 87-112).  Literal list form; the GPU kernel works on    */
+/* elapsed times and order statistics instead, and tests check the two agree.             */
+/* ===================================================================================== */
+
+/* Timestamp.compareTo (TS:109-112): sign of the wrapped difference. */
+static int ts_compare(int64_t a, int64_t b) {
+    const int64_t d = (int64_t)((uint64_t)a - (uint64_t)b);
+    return d > 0 ? 1 : d == 0 ? 0 : -1;
+}
+
+/* Timestamp.elapsedTimeMs (TS:87-90) at a frozen System.nanoTime() == now. */
+static int64_t ts_elapsed_ms(int64_t now, int64_t t) {
+    const int64_t d = (int64_t)((uint64_t)now - (uint64_t)t);
+    return d / 1000000;   /* Java long division truncates toward zero, as C does */
+}
+
+/* PeerConfiguration.hasMajority(Predicate, includeSelf) (PC:157-169); `peers` = the conf's
+ * followers (size n) plus self when include_self. */
+static int pc_has_majority(const uint8_t* active, int n, int include_self) {
+    if (n == 0 && !include_self) return 1;
+    int num = include_self ? 1 : 0;
+    for (int i = 0; i < n; i++) num += active[i] ? 1 : 0;
+    return num > (n + (include_self ? 1 : 0)) / 2;
+}
+
+/* LeaderLease.getMaxTimestampWithMajorityAck (LL:90-103): sort ascending, element size/2;
+ * empty list -> currentTime(). */
+static int64_t ll_max_ts_with_majority_ack(const int64_t* ts, int n, int64_t now) {
+    if (n == 0) return now;
+    int64_t a[32];
+    for (int i = 0; i < n; i++) a[i] = ts[i];
+    for (int i = 1; i < n; i++) {                 /* stable insertion sort by compareTo */
+        const int64_t x = a[i];
+        int j = i - 1;
+        while (j >= 0 && ts_compare(a[j], x) > 0) { a[j + 1] = a[j]; j--; }
+        a[j + 1] = x;
+    }
+    return a[n / 2];
+}
+
+/* LeaderStateImpl.hasLease() for one group, isRunning() && isReady() taken as true.
+ * cur_ts / old_ts: lastRespondedAppendEntriesSendTime of the followers of the current / old
+ * conf (self excluded, as FollowerInfoMap.getFollowerInfos yields them, LSI:291-293); old_ts is
+ * used only when transitional.  Returns hasLease; *lease_out = the lease after any extension. */
+ORC_API int orc_has_lease(int enabled, int64_t now, int64_t timeout_ms, const int64_t* cur_ts, int n_cur,
+                          int self_in_cur, const int64_t* old_ts, int n_old, int self_in_old, int transitional,
+                          int64_t lease_in, int64_t* lease_out, int* extended) {
+    *lease_out = lease_in;
+    *extended = 0;
+    if (!enabled) return 0;                                                  /* LSI:1230-1232 */
+    /* RCI:296-298 isSingleton: getCurrentPeers().size()==1 && getPreviousPeers().size()<=1 */
+    const int singleton = (n_cur + self_in_cur) == 1 && (transitional ? n_old + self_in_old : 0) <= 1;
+    /* checkLeaderLease (LSI:1246-1249) with LeaderLease.isValid (LL:60-62) */
+    if (singleton || ts_elapsed_ms(now, lease_in) < timeout_ms) return 1;
+    /* LeaderLease.extend (LL:68-85): active peers of current ++ old, by last response time */
+    uint8_t act_cur[32], act_old[32];
+    for (int i = 0; i < n_cur; i++) act_cur[i] = ts_elapsed_ms(now, cur_ts[i]) < timeout_ms;
+    for (int i = 0; i < n_old; i++) act_old[i] = ts_elapsed_ms(now, old_ts[i]) < timeout_ms;
+    /* conf.hasMajority(peers, selfId) (RCI:265-269 -> PC:152-155) */
+    int maj = pc_has_majority(act_cur, n_cur, self_in_cur);
+    if (transitional) maj = maj && pc_has_majority(act_old, n_old, self_in_old);
+    if (maj) {
+        const int64_t a = ll_max_ts_with_majority_ack(cur_ts, n_cur, now);
+        const int64_t b = transitional ? ll_max_ts_with_majority_ack(old_ts, n_old, now) : now;  /* old==null */
+        *lease_out = ts_compare(a, b) > 0 ? b : a;                           /* Timestamp.earliest */
+        *extended = 1;
+    }
+    return singleton || ts_elapsed_ms(now, *lease_out) < timeout_ms;
+}
+
+/* Batched form over the SoA layout (same conf word as orc_commit_soa). */
+ORC_API void orc_lease_soa(uint64_t n, uint32_t nf, int64_t now, int64_t timeout_ms,
+                           const int64_t* follower_ts, /* [nf][n] */
+                           const uint32_t* conf, const int64_t* lease_in, const uint64_t* enabled_bits,
+                           int64_t* lease_out, uint64_t* has_lease_bits, uint64_t* extended_bits) {
+    const uint64_t nwords = (n + 63) / 64;
+    memset(has_lease_bits, 0, nwords * 8);
+    if (extended_bits) memset(extended_bits, 0, nwords * 8);
+    for (uint64_t g = 0; g < n; g++) {
+        const uint32_t w = conf[g];
+        if (!ORC_CONF_ACTIVE(w)) { lease_out[g] = lease_in[g]; continue; }
+        int64_t cur[16], old[16];
+        int nc = 0, no = 0;
+        for (uint32_t i = 0; i < nf; i++) {
+            const int64_t t = follower_ts[(uint64_t)i * n + g];
+            if ((ORC_CONF_NEW_MASK(w) >> i) & 1u) cur[nc++] = t;
+            if ((ORC_CONF_OLD_MASK(w) >> i) & 1u) old[no++] = t;
+        }
+        const int en = enabled_bits ? (int)((enabled_bits[g / 64] >> (g % 64)) & 1u) : 1;
+        int ext = 0;
+        int64_t lo = 0;
+        const int has = orc_has_lease(en, now, timeout_ms, cur, nc, (int)ORC_CONF_SELF(w), old, no,
+                                      (int)ORC_CONF_SELF_OLD(w), (int)ORC_CONF_TRANSITIONAL(w), lease_in[g], &lo, &ext);
+        lease_out[g] = lo;
+        if (has) has_lease_bits[g / 64] |= 1ull << (g % 64);
+        if (ext && extended_bits) extended_bits[g / 64] |= 1ull << (g % 64);
+    }
+}
+
+/* ===================================================================================== */
 /* SegmentedRaftLog frames -- writer OUT:86-110, reader RDR:179-341, format FMT:30-80     */
 /* ===================================================================================== */
 

@@ -101,6 +101,24 @@ class RhFrames(ctypes.Structure):
     ]
 
 
+class RhLeaseSoa(ctypes.Structure):
+    _fields_ = [
+        ("n", c_uint64),
+        ("n_followers", c_uint32),
+        ("reserved", c_uint32),
+        ("now_nanos", c_int64),
+        ("timeout_ms", c_int64),
+        ("follower_ts", c_void_p),
+        ("col_stride", c_uint64),
+        ("conf", c_void_p),
+        ("lease_in", c_void_p),
+        ("enabled_bits", c_void_p),
+        ("lease_out", c_void_p),
+        ("has_lease_bits", c_void_p),
+        ("extended_bits", c_void_p),
+    ]
+
+
 RH_SEG_END = 1
 RH_SEG_PARTIAL = 2
 RH_SEG_E_OVERSIZE = -1
@@ -154,6 +172,7 @@ _SIGNATURES = {
     "rh_crc32c_frames_launch": (c_int, [c_void_p, POINTER(RhFrames), c_uint32, c_void_p]),
     "rh_crc32c_verify_host": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_uint64, c_void_p,
                                       c_void_p, POINTER(c_uint64)]),
+    "rh_lease_soa_launch": (c_int, [c_void_p, POINTER(RhLeaseSoa), c_int, c_void_p]),
     "rh_segments_scan_launch": (c_int, [c_void_p, POINTER(RhSegments), c_void_p]),
     "rh_segments_set_variant": (c_int, [c_int]),
     "rh_crc32c_num_variants": (c_int, []),

@@ -15,6 +15,7 @@
 // INT64_MAX -- integer compare/select work, no MFMA (this is not a contraction).  The kernel
 // is HBM-bound: 8(F+1)+20 bytes read and 16 bytes written per group.
 #include "rh_internal.h"
+#include "sortnet.h"
 
 #include <climits>
 
@@ -32,54 +33,6 @@ constexpr int kVariantT[] = {1, 2, 4};
 // 7:   v2, F classes [1,7], [8,14], 4 waves per SIMD
 constexpr int kNumCommitVariants = 8;
 
-// ---- Batcher merge-exchange sorting network (Knuth, TAOCP 5.2.2, Algorithm M) ------------
-struct Net {
-    int n = 0;
-    int a[128] = {};
-    int b[128] = {};
-};
-
-constexpr Net make_net(int N) {
-    Net net{};
-    if (N < 2) return net;
-    int t = 0;
-    while ((1 << t) < N) ++t;
-    int p = 1 << (t - 1);
-    while (p > 0) {
-        int q = 1 << (t - 1), r = 0, d = p;
-        while (true) {
-            for (int i = 0; i < N - d; ++i)
-                if ((i & p) == r) {
-                    net.a[net.n] = i;
-                    net.b[net.n] = i + d;
-                    ++net.n;
-                }
-            if (q == p) break;
-            d = q - p;
-            q >>= 1;
-            r = p;
-        }
-        p >>= 1;
-    }
-    return net;
-}
-
-template <int N>
-constexpr Net kNet = make_net(N);
-
-template <int N, int I = 0>
-__device__ __forceinline__ void sort_net(int64_t (&v)[N]) {
-    if constexpr (I < kNet<N>.n) {
-        constexpr int a = kNet<N>.a[I];
-        constexpr int b = kNet<N>.b[I];
-        const int64_t x = v[a], y = v[b];
-        const bool lt = x < y;
-        v[a] = lt ? x : y;
-        v[b] = lt ? y : x;
-        sort_net<N, I + 1>(v);
-    }
-}
-
 // Order statistics of the voters selected by `member` (bit i = slot i, bit N-1 = self):
 // getSorted (LSI:1076-1095) + MinMajorityMax.valueOf(sorted, gap) (LSI:926-943).
 // Non-members sort to the end as INT64_MAX; k < n so they are never selected.
@@ -89,7 +42,7 @@ __device__ __forceinline__ void order_stats(const int64_t (&vals)[N], uint32_t m
     int64_t s[N];
 #pragma unroll
     for (int i = 0; i < N; ++i) s[i] = ((member >> i) & 1u) ? vals[i] : INT64_MAX;
-    sort_net<N>(s);
+    rh_sort::sort_net<N>(s);
     const int n = __builtin_popcount(member);
     const int k = (n - 1) >> 1;  // getMajority: sorted[(length - 1) / 2]
     mn = s[0];

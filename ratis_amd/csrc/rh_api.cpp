@@ -429,6 +429,13 @@ RH_EXPORT int rh_crc32c_frames_launch(rh_ctx* ctx, const rh_frames* frames, uint
     return rh_crc_launch_impl(ctx, frames, flags, pick_stream(ctx, stream));
 }
 
+// ---- leader lease ----------------------------------------------------------------------------
+RH_EXPORT int rh_lease_soa_launch(rh_ctx* ctx, const rh_lease_soa* tiers, int n_tiers, void* stream) {
+    if (!ctx) return rh::fail(RH_E_INVAL, "rh_lease_soa_launch: ctx == NULL");
+    DeviceGuard g(ctx->device);
+    return rh_lease_launch_impl(ctx, tiers, n_tiers, pick_stream(ctx, stream));
+}
+
 // ---- segment framing -------------------------------------------------------------------------
 RH_EXPORT int rh_segments_scan_launch(rh_ctx* ctx, const rh_segments* segs, void* stream) {
     if (!ctx) return rh::fail(RH_E_INVAL, "rh_segments_scan_launch: ctx == NULL");

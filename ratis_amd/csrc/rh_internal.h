@@ -68,3 +68,4 @@ int rh_commit_set_variant_impl(int v);
 int rh_commit_num_variants_impl();
 int rh_segments_launch_impl(rh_ctx* ctx, const rh_segments* segs, hipStream_t stream);
 int rh_segments_set_variant_impl(int v);
+int rh_lease_launch_impl(rh_ctx* ctx, const rh_lease_soa* tiers, int n_tiers, hipStream_t stream);

@@ -12,6 +12,8 @@ Reference mapping (paths relative to the ratis tree):
   * :func:`crc32c_frames` = ``PureJavaCrc32C`` (PureJavaCrc32C.java:43-152) over
     ``SegmentedRaftLogOutputStream.write`` frames (:86-110), verified as in
     ``SegmentedRaftLogReader.decodeEntry`` (:327-336) or stamped as in the writer.
+  * :func:`lease_launch` = ``LeaderStateImpl.hasLease()`` (LeaderStateImpl.java:1229-1249) with
+    ``LeaderLease.extend`` (LeaderLease.java:68-103) for every group of every tier.
   * :func:`segments_scan` = the reader's framing walk (``verifyHeader`` :179-205, ``decodeEntry``
     :291-323, ``verifyTerminator`` :251-280) over many segment images at once, and
     :func:`read_segments` = framing + CRC verify, i.e. ``LogSegment.readSegmentFile``
@@ -26,7 +28,7 @@ from typing import Optional, Sequence
 import torch
 
 from . import _lib
-from ._lib import RH_MODE_COMMIT, RH_MODE_WATCH, RhCommitSoa, RhFrames, RhSegments, check
+from ._lib import RH_MODE_COMMIT, RH_MODE_WATCH, RhCommitSoa, RhFrames, RhLeaseSoa, RhSegments, check
 
 
 def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
@@ -395,3 +397,61 @@ class _nullctx:
 
     def __exit__(self, *exc):
         return False
+
+
+# ---- leader lease ------------------------------------------------------------------------------
+@dataclass
+class LeaseTier:
+    """Groups with the same follower-slot count F (0..14) for rh_lease_soa_launch."""
+
+    follower_ts: torch.Tensor        # int64 [F, >=n] (column k = follower slot k), nanoTime values
+    conf: torch.Tensor               # int32 [n] membership words
+    lease_in: torch.Tensor           # int64 [n]
+    enabled_bits: Optional[torch.Tensor] = None   # int64 [ceil(n/64)] or None (all enabled)
+    lease_out: Optional[torch.Tensor] = None      # int64 [n]; may be lease_in itself
+    has_lease_bits: Optional[torch.Tensor] = None  # int64 [ceil(n/64)]
+    extended_bits: Optional[torch.Tensor] = None   # int64 [ceil(n/64)]
+
+    @property
+    def n(self) -> int:
+        return int(self.conf.numel())
+
+    def alloc_outputs(self, extended: bool = True) -> "LeaseTier":
+        dev, nw = self.conf.device, (self.n + 63) // 64
+        if self.lease_out is None:
+            self.lease_out = torch.empty(self.n, dtype=torch.int64, device=dev)
+        if self.has_lease_bits is None:
+            self.has_lease_bits = torch.zeros(max(nw, 1), dtype=torch.int64, device=dev)
+        if extended and self.extended_bits is None:
+            self.extended_bits = torch.zeros(max(nw, 1), dtype=torch.int64, device=dev)
+        return self
+
+    def to_struct(self, now_nanos: int, timeout_ms: int) -> RhLeaseSoa:
+        F = int(self.follower_ts.shape[0]) if self.follower_ts.dim() == 2 else 0
+        if self.follower_ts.dtype != torch.int64 or self.lease_in.dtype != torch.int64:
+            raise ValueError("follower_ts and lease_in must be int64")
+        if F and self.follower_ts.stride(1) != 1 and self.n > 1:
+            raise ValueError("follower_ts rows must be contiguous")
+        if self.lease_in.numel() != self.n:
+            raise ValueError("lease_in and conf lengths differ")
+        t = RhLeaseSoa()
+        t.n = self.n
+        t.n_followers = F
+        t.now_nanos = now_nanos
+        t.timeout_ms = timeout_ms
+        t.follower_ts = _ptr(self.follower_ts) if F else None
+        t.col_stride = int(self.follower_ts.stride(0)) if F else self.n
+        t.conf = _ptr(self.conf)
+        t.lease_in = _ptr(self.lease_in)
+        t.enabled_bits = _ptr(self.enabled_bits)
+        t.lease_out = _ptr(self.lease_out)
+        t.has_lease_bits = _ptr(self.has_lease_bits)
+        t.extended_bits = _ptr(self.extended_bits)
+        return t
+
+
+def lease_launch(ctx: Context, tiers: Sequence[LeaseTier], now_nanos: int, timeout_ms: int,
+                 stream: Optional[torch.cuda.Stream] = None) -> None:
+    """Enqueues the lease kernel for every tier (asynchronous)."""
+    arr = (RhLeaseSoa * len(tiers))(*[t.to_struct(now_nanos, timeout_ms) for t in tiers])
+    check(_lib.load().rh_lease_soa_launch(ctx.handle, arr, len(tiers), _stream_ptr(stream)))

@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--segments", type=int, default=32)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--only", default="crc,framing,commit", help="comma list of sections to run")
     a = ap.parse_args()
     import torch
 
@@ -38,7 +39,8 @@ def main():
     del x, y
     ss = workload.synth_segments(ctx, n_segments=a.segments, corrupt_rate=0)
     fb = ss.batch
-    nv = engine.crc32c_num_variants()
+    only = set(a.only.split(","))
+    nv = engine.crc32c_num_variants() if "crc" in only else 0
     res = {v: [] for v in range(nv)}
     for r in range(a.rounds):
         for v in range(nv):
@@ -56,26 +58,49 @@ def main():
         x = np.array(res[v])
         print(json.dumps({"kernel": "crc32c", "variant": v, "median_GBps": round(float(np.median(x)), 1),
                           "min_GBps": round(float(x.min()), 1), "max_GBps": round(float(x.max()), 1)}))
-    # segment framing walk over the same segment images
-    n = ss.n_segments
-    sb = engine.SegmentBatch(buf=fb.buf, seg_off=torch.arange(n, device="cuda", dtype=torch.int64) * ss.segment_size,
-                             seg_len=torch.full((n,), ss.segment_size, device="cuda", dtype=torch.int64),
-                             frames_per_seg_cap=ss.frames_per_segment + 16)
-    fr = []
-    for r in range(a.rounds):
-        engine.segments_scan(ctx, sb)
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(a.iters):
-            engine.segments_scan(ctx, sb)
-        e1.record()
-        torch.cuda.synchronize()
-        fr.append(n * ss.segment_size / (e0.elapsed_time(e1) / a.iters * 1e-3) / 1e9)
-        assert int(sb.total_frames.item()) == n * ss.frames_per_segment
-    x = np.array(fr)
-    print(json.dumps({"kernel": "segments_scan", "segments": n, "median_GBps": round(float(np.median(x)), 1),
-                      "min_GBps": round(float(x.min()), 1), "max_GBps": round(float(x.max()), 1)}))
-    del ss, fb, sb
+    # segment framing walk: variants x segment shapes (same 8 GiB footprint)
+    del fb
+    lib = _lib.load()
+
+    def framing(ss, tag):
+        n = ss.n_segments
+        sb = engine.SegmentBatch(buf=ss.batch.buf,
+                                 seg_off=torch.arange(n, device="cuda", dtype=torch.int64) * ss.segment_size,
+                                 seg_len=torch.full((n,), ss.segment_size, device="cuda", dtype=torch.int64),
+                                 frames_per_seg_cap=ss.frames_per_segment + 16)
+        for v in range(3):
+            _lib.check(lib.rh_segments_set_variant(v))
+            fr = []
+            for r in range(a.rounds):
+                engine.segments_scan(ctx, sb)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(a.iters):
+                    engine.segments_scan(ctx, sb)
+                e1.record()
+                torch.cuda.synchronize()
+                fr.append(n * ss.segment_size / (e0.elapsed_time(e1) / a.iters * 1e-3) / 1e9)
+                assert int(sb.total_frames.item()) == n * ss.frames_per_segment
+            x = np.array(fr)
+            print(json.dumps({"kernel": "segments_scan", "variant": v, "shape": tag, "segments": n,
+                              "median_GBps": round(float(np.median(x)), 1), "min_GBps": round(float(x.min()), 1),
+                              "max_GBps": round(float(x.max()), 1)}), flush=True)
+        _lib.check(lib.rh_segments_set_variant(2))
+
+    if "framing" not in only:
+        ss = None
+    else:
+        framing(ss, "32MiBx4KiB")
+        total = ss.n_segments * ss.segment_size
+        del ss
+        torch.cuda.empty_cache()
+        ss = workload.synth_segments(ctx, n_segments=total // (4 << 20), segment_size=4 << 20, corrupt_rate=0)
+        framing(ss, "4MiBx4KiB")
+        del ss
+        torch.cuda.empty_cache()
+        ss = workload.synth_segments(ctx, n_segments=a.segments, frame_size=512, corrupt_rate=0)
+        framing(ss, "32MiBx512B")
+    del ss
     # commit kernel variants over 8 rotating 1M-group batches (config 3)
     host = workload.commit_snapshot(1_000_000)
     alg = sum(h.algorithmic_bytes() for h in host)
@@ -91,7 +116,7 @@ def main():
             tiers.append(t.alloc_outputs())
         batches.append(tiers)
     lib = _lib.load()
-    ncv = lib.rh_commit_num_variants()
+    ncv = lib.rh_commit_num_variants() if "commit" in only else 0
     cres = {v: [] for v in range(ncv)}
     for r in range(a.rounds):
         for v in range(ncv):

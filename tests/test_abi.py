@@ -66,6 +66,7 @@ int main(void) {
   printf("rh_frames %zu\n", sizeof(rh_frames));
   printf("rh_delta %zu\n", sizeof(rh_delta));
   printf("rh_segments %zu\n", sizeof(rh_segments));
+  printf("rh_lease_soa %zu\n", sizeof(rh_lease_soa));
   F(rh_commit_soa, n) F(rh_commit_soa, n_followers) F(rh_commit_soa, mode) F(rh_commit_soa, gap_threshold)
   F(rh_commit_soa, follower_index) F(rh_commit_soa, col_stride) F(rh_commit_soa, self_index)
   F(rh_commit_soa, commit_in) F(rh_commit_soa, term_start) F(rh_commit_soa, conf) F(rh_commit_soa, commit_out)
@@ -80,6 +81,10 @@ int main(void) {
   F(rh_segments, scratch_len) F(rh_segments, frame_off) F(rh_segments, frame_len) F(rh_segments, frame_cap)
   F(rh_segments, seg_first) F(rh_segments, seg_nframes) F(rh_segments, seg_status) F(rh_segments, seg_stop)
   F(rh_segments, total_frames)
+  F(rh_lease_soa, n) F(rh_lease_soa, n_followers) F(rh_lease_soa, reserved) F(rh_lease_soa, now_nanos)
+  F(rh_lease_soa, timeout_ms) F(rh_lease_soa, follower_ts) F(rh_lease_soa, col_stride) F(rh_lease_soa, conf)
+  F(rh_lease_soa, lease_in) F(rh_lease_soa, enabled_bits) F(rh_lease_soa, lease_out)
+  F(rh_lease_soa, has_lease_bits) F(rh_lease_soa, extended_bits)
   printf("conf %u\n", rh_conf_pack(0x5, 1, 1, 0x3, 1, 1));
   return 0;
 }
@@ -98,8 +103,9 @@ def test_struct_layouts_match_header(tmp_path):
     assert int(vals["rh_frames"]) == ctypes.sizeof(_lib.RhFrames)
     assert int(vals["rh_delta"]) == ctypes.sizeof(_lib.RhDelta)
     assert int(vals["rh_segments"]) == ctypes.sizeof(_lib.RhSegments)
+    assert int(vals["rh_lease_soa"]) == ctypes.sizeof(_lib.RhLeaseSoa)
     for cname, cls in (("rh_commit_soa", _lib.RhCommitSoa), ("rh_frames", _lib.RhFrames), ("rh_delta", _lib.RhDelta),
-                       ("rh_segments", _lib.RhSegments)):
+                       ("rh_segments", _lib.RhSegments), ("rh_lease_soa", _lib.RhLeaseSoa)):
         for fname, _ in cls._fields_:
             assert int(vals[f"{cname}.{fname}"]) == getattr(cls, fname).offset, (cname, fname)
     assert int(vals["conf"]) == _lib.conf_pack(0x5, True, True, 0x3, True, True)

@@ -1,0 +1,120 @@
+"""GPU parity of the batched leader-lease kernel (rh_lease_soa_launch) against the oracle's literal
+LeaderStateImpl.hasLease / LeaderLease.extend restatement (orc_lease_soa, cross-checked against
+an independent Python restatement in tests/test_oracle.py).  Bit-exact: lease timestamps,
+hasLease bits and extended bits."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+MS = 1_000_000
+NOW = 1_700_000_000_000_000_000
+
+
+def random_lease_tier(rng, n, F, timeout_ms=100, joint_rate=0.2, boundary_rate=0.05):
+    ts = NOW - rng.integers(-5 * MS, 3 * timeout_ms * MS, size=(F, n), dtype=np.int64)
+    if F:   # exact millisecond boundaries of the activity test
+        m = rng.random((F, n)) < boundary_rate
+        ts[m] = NOW - timeout_ms * MS + rng.integers(-1, 2, int(m.sum()))
+    full = (1 << F) - 1
+    new = rng.integers(0, full + 1, n) if F else np.zeros(n, np.int64)
+    old = rng.integers(0, full + 1, n) if F else np.zeros(n, np.int64)
+    self_new = rng.random(n) < 0.9
+    trans = rng.random(n) < joint_rate
+    self_old = rng.random(n) < 0.8
+    active = rng.random(n) < 0.97
+    conf = (new | (self_new.astype(np.int64) << 14) | (trans.astype(np.int64) << 15) | (old << 16)
+            | (self_old.astype(np.int64) << 30) | (active.astype(np.int64) << 31)).astype(np.uint32)
+    lease_in = NOW - rng.integers(0, 2 * timeout_ms * MS, n, dtype=np.int64)
+    return ts, conf, lease_in
+
+
+def run_gpu(ctx, ts, conf, lease_in, timeout_ms, enabled=None, alias=False, pad=0):
+    import torch
+
+    from ratis_amd import engine
+    dev = torch.device("cuda")
+    F, n = ts.shape
+    tsd = torch.zeros((F, n + pad), dtype=torch.int64, device=dev)
+    tsd[:, :n] = torch.from_numpy(ts)
+    t = engine.LeaseTier(follower_ts=tsd, conf=torch.from_numpy(conf.view(np.int32)).to(dev),
+                         lease_in=torch.from_numpy(lease_in).to(dev),
+                         enabled_bits=None if enabled is None else torch.from_numpy(enabled.view(np.int64)).to(dev))
+    if alias:
+        t.lease_out = t.lease_in
+    t.alloc_outputs()
+    engine.lease_launch(ctx, [t], NOW, timeout_ms)
+    torch.cuda.synchronize()
+    nw = (n + 63) // 64
+    return (t.lease_out.cpu().numpy(), t.has_lease_bits[:nw].cpu().numpy().view(np.uint64),
+            t.extended_bits[:nw].cpu().numpy().view(np.uint64))
+
+
+def assert_same(ref, got):
+    lease, has, ext = got
+    assert np.array_equal(lease, ref["lease"])
+    assert np.array_equal(has, ref["has_lease_bits"])
+    assert np.array_equal(ext, ref["extended_bits"])
+
+
+@pytest.mark.parametrize("F", list(range(0, 15)))
+def test_lease_every_follower_count(ctx, orc, F):
+    rng = np.random.default_rng(1000 + F)
+    n = 20_000 + F * 37          # not a multiple of 64
+    ts, conf, lease_in = random_lease_tier(rng, n, F)
+    en = rng.integers(0, 1 << 63, (n + 63) // 64, dtype=np.int64).astype(np.uint64) | np.uint64(0xF0F0F0F0F0F0F0F0)
+    ref = orc.lease_soa(ts, conf, lease_in, NOW, 100, en)
+    assert_same(ref, run_gpu(ctx, ts, conf, lease_in, 100, enabled=en))
+    ref = orc.lease_soa(ts, conf, lease_in, NOW, 100)
+    assert_same(ref, run_gpu(ctx, ts, conf, lease_in, 100, alias=True, pad=45))
+
+
+@pytest.mark.parametrize("timeout_ms", [0, 1, 100, 5000])
+def test_lease_timeouts_and_extremes(ctx, orc, timeout_ms):
+    rng = np.random.default_rng(timeout_ms)
+    n, F = 5000, 4
+    ts, conf, lease_in = random_lease_tier(rng, n, F, timeout_ms=max(timeout_ms, 1), joint_rate=0.5)
+    # far-past and slightly-future timestamps (|now - t| well below 2^62)
+    ts[0, ::11] = NOW - (1 << 61)
+    ts[1, ::13] = NOW + 3 * MS
+    lease_in[::17] = NOW + 2 * MS
+    lease_in[::19] = NOW - (1 << 60)
+    ref = orc.lease_soa(ts, conf, lease_in, NOW, timeout_ms)
+    assert_same(ref, run_gpu(ctx, ts, conf, lease_in, timeout_ms))
+
+
+def test_lease_multi_tier_and_counts(ctx, orc):
+    import torch
+
+    from ratis_amd import engine
+    rng = np.random.default_rng(77)
+    tiers, refs = [], []
+    for F, n in ((2, 70_001), (4, 900_000), (6, 100_000)):
+        ts, conf, lease_in = random_lease_tier(rng, n, F)
+        refs.append(orc.lease_soa(ts, conf, lease_in, NOW, 150))
+        t = engine.LeaseTier(follower_ts=torch.from_numpy(ts).cuda(), conf=torch.from_numpy(conf.view(np.int32)).cuda(),
+                             lease_in=torch.from_numpy(lease_in).cuda()).alloc_outputs()
+        tiers.append(t)
+    engine.lease_launch(ctx, tiers, NOW, 150)
+    torch.cuda.synchronize()
+    for t, ref in zip(tiers, refs):
+        nw = (t.n + 63) // 64
+        assert np.array_equal(t.lease_out.cpu().numpy(), ref["lease"])
+        assert np.array_equal(t.has_lease_bits[:nw].cpu().numpy().view(np.uint64), ref["has_lease_bits"])
+        assert np.array_equal(t.extended_bits[:nw].cpu().numpy().view(np.uint64), ref["extended_bits"])
+
+
+def test_lease_bad_arguments(ctx):
+    import torch
+
+    from ratis_amd import _lib, engine
+    t = engine.LeaseTier(follower_ts=torch.zeros((15, 8), dtype=torch.int64, device="cuda"),
+                         conf=torch.zeros(8, dtype=torch.int32, device="cuda"),
+                         lease_in=torch.zeros(8, dtype=torch.int64, device="cuda")).alloc_outputs()
+    with pytest.raises(_lib.IllegalArgumentError):
+        engine.lease_launch(ctx, [t], NOW, 100)
+    t2 = engine.LeaseTier(follower_ts=torch.zeros((2, 8), dtype=torch.int64, device="cuda"),
+                          conf=torch.zeros(8, dtype=torch.int32, device="cuda"),
+                          lease_in=torch.zeros(8, dtype=torch.int64, device="cuda")).alloc_outputs()
+    with pytest.raises(_lib.IllegalArgumentError):
+        engine.lease_launch(ctx, [t2], NOW, -1)

@@ -187,7 +187,7 @@ def test_frame_capacity_reports_and_truncates(ctx, orc, seg_variant):
     st = b.seg_status.cpu().numpy()
     assert list(st) == [_lib.RH_SEG_E_CAPACITY] * 2
     assert list(b.seg_nframes.cpu().numpy()) == [64, 64]
-    ro, rl, _, _, _ = orc.segment_scan(img)
+    ro, rl, _, _, _ = orc.segment_scan(np.frombuffer(img, np.uint8))
     fo = b.frame_off[:128].cpu().numpy()
     assert np.array_equal(fo[:64] - offs[0], ro[:64]) and np.array_equal(fo[64:] - offs[1], ro[:64])
 
@@ -237,3 +237,23 @@ def test_bad_arguments(ctx):
                             seg_len=torch.full((1,), 16, dtype=torch.int64, device=dev), frames_per_seg_cap=0)
     with pytest.raises(_lib.IllegalArgumentError):
         engine.segments_scan(ctx, b)
+
+
+def test_long_padding_tails(ctx, orc, seg_variant):
+    """Preallocated segments (mostly zero tail, as an open segment's file is): the terminator
+    check must scan megabytes and report the exact first non-zero byte, or a clean end."""
+    rng = np.random.default_rng(21)
+    images = []
+    for i in range(12):
+        frames = b"".join(orc.frame_write(bytes(rng.integers(1, 256, int(rng.integers(1, 900)), dtype=np.uint8)))
+                          for _ in range(int(rng.integers(0, 50))))
+        tail = bytearray(int(rng.integers(1, 3 << 20)))
+        if i % 3 != 0:
+            for _ in range(i % 3):
+                tail[int(rng.integers(0, len(tail)))] = int(rng.integers(1, 256))
+        if i == 4:
+            tail[-1] = 9
+        images.append(HEADER + frames + bytes(tail))
+    buf, offs, lens = pack(images, rng)
+    b = run_scan(ctx, buf, offs, lens)
+    check_against_oracle(orc, b, buf, offs, lens)

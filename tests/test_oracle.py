@@ -243,3 +243,79 @@ def test_reader_header_states(orc):
     assert orc.load().orc_verify_header(np.frombuffer(b"RaftLog1", np.uint8).ctypes.data, 8) == 1
     assert orc.load().orc_verify_header(np.frombuffer(b"Raft\0\0\0\0", np.uint8).ctypes.data, 8) == 0
     assert orc.load().orc_verify_header(np.frombuffer(b"RaftLog2", np.uint8).ctypes.data, 8) == orc.ORC_E_HEADER
+
+
+# ---- leader lease (LeaderStateImpl.hasLease LSI:1229-1249, LeaderLease LL:60-103) -------------
+MS = 1_000_000
+NOW = 1_700_000_000_000_000_000
+
+
+def test_lease_hand_derived_cases(orc):
+    ts = [NOW - 10 * MS, NOW - 20 * MS, NOW - 150 * MS, NOW - 200 * MS]
+    expired = NOW - 1000 * MS
+    # 5 peers: self + 4 followers, 2 followers fresh -> 3 of 5 -> extend to the 2nd newest (now-20ms)
+    assert orc.has_lease(True, NOW, 100, ts, True, [], False, False, expired) == (True, NOW - 20 * MS, True)
+    # only one fresh follower -> no majority -> lease stays expired
+    ts1 = [NOW - 10 * MS, NOW - 120 * MS, NOW - 150 * MS, NOW - 200 * MS]
+    assert orc.has_lease(True, NOW, 100, ts1, True, [], False, False, expired) == (False, expired, False)
+    # still-valid lease: no extension attempted
+    assert orc.has_lease(True, NOW, 100, ts1, True, [], False, False, NOW - 50 * MS) == (True, NOW - 50 * MS, False)
+    # disabled lease
+    assert orc.has_lease(False, NOW, 100, ts, True, [], False, False, NOW) == (False, NOW, False)
+    # singleton conf (self only): always has the lease, lease untouched
+    assert orc.has_lease(True, NOW, 100, [], True, [], False, False, expired) == (True, expired, False)
+    # boundary: elapsed exactly 100 ms is not active (100 < 100 is false); 100ms - 1ns truncates to 99
+    edge = [NOW - 100 * MS, NOW - 100 * MS + 1]
+    assert orc.has_lease(True, NOW, 100, edge, True, [], False, False, expired) == (True, NOW - 100 * MS + 1, True)
+    assert orc.has_lease(True, NOW, 100, [NOW - 100 * MS, NOW - 100 * MS], True, [], False, False, expired)[0] is False
+    # a single follower 99 ms + 1 ns ago: active (elapsed truncates to 99), the extended lease is valid
+    assert orc.has_lease(True, NOW, 100, [NOW - 99 * MS - 1], True, [], False, False, expired) == \
+        (True, NOW - 99 * MS - 1, True)
+    # joint: new conf fine, old conf lacks majority -> no extension
+    assert orc.has_lease(True, NOW, 100, ts, True, [NOW - 500 * MS, NOW - 600 * MS], True, True, expired)[2] is False
+    # joint: both fine -> earliest of the two majority timestamps
+    r = orc.has_lease(True, NOW, 100, ts, True, [NOW - 5 * MS, NOW - 60 * MS], True, True, expired)
+    assert r == (True, NOW - 20 * MS, True)          # old: sorted [-60,-5] idx 1 = -5ms; earliest = -20ms
+
+
+def test_lease_c_matches_python_random(orc):
+    rng = np.random.default_rng(404)
+    for it in range(4000):
+        nc = int(rng.integers(0, 9))
+        no = int(rng.integers(0, 9))
+        timeout = int(rng.integers(1, 300))
+        spread = int(rng.choice([3 * MS, 100 * MS, 400 * MS, 10_000 * MS]))
+        cur = [NOW - int(rng.integers(-spread // 10, spread)) for _ in range(nc)]
+        old = [NOW - int(rng.integers(-spread // 10, spread)) for _ in range(no)]
+        if rng.random() < 0.2 and nc:                     # exact millisecond boundaries
+            cur[0] = NOW - timeout * MS + int(rng.integers(-1, 2))
+        args = (bool(rng.random() < 0.9), NOW, timeout, cur, bool(rng.random() < 0.8), old,
+                bool(rng.random() < 0.7), bool(rng.random() < 0.3), NOW - int(rng.integers(0, 2 * timeout * MS)))
+        assert orc.has_lease(*args) == orc.py_has_lease(*args), (it, args)
+
+
+def test_lease_soa_matches_per_group(orc):
+    rng = np.random.default_rng(5)
+    n, F = 3000, 6
+    ts = NOW - rng.integers(-5 * MS, 300 * MS, size=(F, n), dtype=np.int64)
+    new = rng.integers(0, 1 << F, n)
+    old = rng.integers(0, 1 << F, n)
+    conf = np.array([(int(new[g]) | (int(rng.random() < 0.9) << 14) | (int(rng.random() < 0.2) << 15)
+                      | (int(old[g]) << 16) | (int(rng.random() < 0.8) << 30) | (int(rng.random() < 0.95) << 31))
+                     for g in range(n)], dtype=np.uint32)
+    lease_in = NOW - rng.integers(0, 200 * MS, n, dtype=np.int64)
+    en = rng.integers(0, 1 << 63, (n + 63) // 64, dtype=np.int64).astype(np.uint64) | np.uint64(0x00FF00FF00FF00FF)
+    out = orc.lease_soa(ts, conf, lease_in, NOW, 100, en)
+    has = np.unpackbits(out["has_lease_bits"].view(np.uint8), bitorder="little")[:n]
+    ext = np.unpackbits(out["extended_bits"].view(np.uint8), bitorder="little")[:n]
+    for g in range(0, n, 7):
+        w = int(conf[g])
+        if not w >> 31:
+            assert out["lease"][g] == lease_in[g] and not has[g]
+            continue
+        cur = [int(ts[k, g]) for k in range(F) if (w >> k) & 1]
+        od = [int(ts[k, g]) for k in range(F) if (w >> (16 + k)) & 1]
+        e = bool((int(en[g // 64]) >> (g % 64)) & 1)
+        want = orc.py_has_lease(e, NOW, 100, cur, bool(w >> 14 & 1), od, bool(w >> 30 & 1), bool(w >> 15 & 1),
+                                int(lease_in[g]))
+        assert (bool(has[g]), int(out["lease"][g]), bool(ext[g])) == want, g
