@@ -90,6 +90,15 @@ __global__ __launch_bounds__(64) void segment_walk_kernel(SegArgs a) {
             if (!(pos >= wbase && (pos + 16 <= wbase + kWin || wbase + kWin >= L))) {
                 wbase = ((base + pos) & ~(int64_t)15) - base;  // 16-B aligned in the buffer
                 __syncthreads();
+                if (wbase >= 0 && wbase + kWin <= L) {
+                    u32x4s v[kWin / (64 * 16)];
+#pragma unroll
+                    for (int i = 0; i < kWin / (64 * 16); ++i)
+                        v[i] = *reinterpret_cast<const u32x4s*>(seg + wbase + (i * 64 + lane) * 16);
+#pragma unroll
+                    for (int i = 0; i < kWin / (64 * 16); ++i)
+                        *reinterpret_cast<u32x4s*>(win + (i * 64 + lane) * 16) = v[i];
+                } else
 #pragma unroll 4
                 for (int i = 0; i < kWin / (64 * 16); ++i) {
                     const int off = (i * 64 + lane) * 16;
@@ -259,6 +268,14 @@ struct Win {
     u32x4s r[PER];
 
     __device__ __forceinline__ void load(const uint8_t* seg, int64_t L, int64_t wstart, int t) {
+        if (wstart >= 0 && wstart + W <= L) {
+            // whole window inside the segment (block-uniform branch): PER independent 16-B loads
+            // in flight together -- no per-chunk guard, so no s_waitcnt between them
+#pragma unroll
+            for (int i = 0; i < PER; ++i)
+                r[i] = *reinterpret_cast<const u32x4s*>(seg + wstart + (int64_t)(i * kBlock2 + t) * 16);
+            return;
+        }
 #pragma unroll
         for (int i = 0; i < PER; ++i) {
             const int64_t p = wstart + (int64_t)(i * kBlock2 + t) * 16;
@@ -338,43 +355,40 @@ __global__ __launch_bounds__(kBlock2) void segment_walk_kernel2(SegArgs a) {
                             st = RH_SEG_END;
                             break;
                         }
-                        uint32_t b[5];
-#pragma unroll
-                        for (int i = 0; i < 5; ++i) b[i] = ring[(p + i - A) & MASK];
-                        if (b[0] == 0) {  // terminator (SegmentedRaftLogFormat.isTerminator)
+                        // bytes p..p+4 from two aligned LDS dwords (one round trip)
+                        const uint32_t q = (uint32_t)((p - A) & MASK);
+                        const uint32_t q0 = q & ~3u;
+                        const uint32_t lo = *reinterpret_cast<const uint32_t*>(ring + q0);
+                        const uint32_t hi = *reinterpret_cast<const uint32_t*>(ring + ((q0 + 4) & MASK));
+                        const uint64_t x = ((uint64_t)hi << 32 | lo) >> (8 * (q & 3));
+                        if ((x & 0xff) == 0) {  // terminator (SegmentedRaftLogFormat.isTerminator)
                             st = kTermPending;
                             break;
                         }
-                        // CodedInputStream.readRawVarint32(firstByte, in); EOF -> truncatedMessage
+                        // CodedInputStream.readRawVarint32(firstByte, in): 7 bits per byte, int
+                        // arithmetic (bits past 31 dropped); EOF inside the varint -> truncatedMessage
+                        const uint64_t stop = ~x & 0x8080808080ull;
+                        const int vlen = stop ? (__builtin_ctzll(stop) >> 3) + 1 : 6;
                         const int64_t avail = L - p;
-                        uint32_t result = 0;
-                        bool done = false, trunc = false;
-#pragma unroll
-                        for (int i = 0; i < 5; ++i) {
-                            if (!done && !trunc) {
-                                if (i >= avail) {
-                                    trunc = true;
-                                } else {
-                                    result |= (b[i] & 0x7f) << (7 * i);
-                                    done = (b[i] & 0x80) == 0;
-                                }
-                            }
+                        uint32_t result = (uint32_t)((x & 0x7f) | ((x >> 1) & 0x3f80) | ((x >> 2) & 0x1fc000) |
+                                                     ((x >> 3) & 0xfe00000) | ((x >> 4) & 0x7f0000000ull));
+                        if (vlen < 5) result &= (1u << (7 * vlen)) - 1u;
+                        if (avail < (vlen < 5 ? vlen : 5)) {
+                            st = RH_SEG_E_VARINT;
+                            break;
                         }
-                        if (!done && !trunc) {  // discard up to 5 more bytes of a 64-bit varint
-                            for (int i = 5; i < 10; ++i) {
-                                if (i >= avail) {
-                                    trunc = true;
-                                    break;
-                                }
+                        if (vlen == 6) {  // discard up to 5 more bytes of a 64-bit varint
+                            bool done = false;
+                            for (int i = 5; i < 10 && i < avail; ++i) {
                                 if ((ring[(p + i - A) & MASK] & 0x80) == 0) {
                                     done = true;
                                     break;
                                 }
                             }
-                        }
-                        if (!done) {
-                            st = RH_SEG_E_VARINT;
-                            break;
+                            if (!done) {
+                                st = RH_SEG_E_VARINT;
+                                break;
+                            }
                         }
                         const int32_t n = (int32_t)result;
                         if (n > (int32_t)a.max_op) {
