@@ -361,6 +361,29 @@ __global__ __launch_bounds__(kBlock2) void segment_walk_kernel2(SegArgs a) {
                         const uint32_t lo = *reinterpret_cast<const uint32_t*>(ring + q0);
                         const uint32_t hi = *reinterpret_cast<const uint32_t*>(ring + ((q0 + 4) & MASK));
                         const uint64_t x = ((uint64_t)hi << 32 | lo) >> (8 * (q & 3));
+                        {
+                            // Common case, all checks folded into one predicate: a non-zero first
+                            // byte, a varint of <= 4 bytes wholly before EOF, a frame within
+                            // maxOpSize and EOF, and scratch room.  Everything else takes the
+                            // full rule-by-rule path below (same results, more branches).
+                            const uint32_t stop4 = ~(uint32_t)x & 0x80808080u;
+                            const int vl = (__builtin_ctz(stop4 | 0x80000000u) >> 3) + 1;
+                            const uint32_t v = (uint32_t)x;
+                            const uint32_t nn = ((v & 0x7fu) | ((v >> 1) & 0x3f80u) | ((v >> 2) & 0x1fc000u) |
+                                                 ((v >> 3) & 0xfe00000u)) &
+                                                (0xffffffffu >> (32 - 7 * vl));
+                            const uint32_t vs = nn < (1u << 7) ? 1u : nn < (1u << 14) ? 2u : nn < (1u << 21) ? 3u : 4u;
+                            const int64_t total = (int64_t)vs + nn;
+                            const bool fast = (v & 0xffu) != 0 && stop4 != 0 && p + 8 <= L &&
+                                              total + 4 <= (int64_t)a.max_op && p + total + 4 <= L && nfr < a.cap;
+                            if (fast) {
+                                a.scratch_off[s * (uint64_t)a.cap + nfr] = (uint64_t)(base + p);
+                                a.scratch_len[s * (uint64_t)a.cap + nfr] = (uint32_t)(total + 4);
+                                ++nfr;
+                                p += total + 4;
+                                continue;
+                            }
+                        }
                         if ((x & 0xff) == 0) {  // terminator (SegmentedRaftLogFormat.isTerminator)
                             st = kTermPending;
                             break;
