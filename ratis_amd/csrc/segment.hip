@@ -351,39 +351,51 @@ __global__ __launch_bounds__(kBlock2) void segment_walk_kernel2(SegArgs a) {
                     int st = kWalking;
                     int64_t p = pos;
                     while (p < wend) {
+                        {
+                            // Fast loop for the common case, every check folded into two
+                            // predicates: a non-zero first byte and a varint of <= 4 bytes wholly
+                            // before EOF (p < pend), and a frame within maxOpSize and EOF.
+                            // Anything else drops to the rule-by-rule step below (same results).
+                            const int64_t pend = wend < L - 8 ? wend : L - 8;
+                            const uint32_t room = a.cap - nfr;
+                            uint64_t* so = a.scratch_off + s * (uint64_t)a.cap + nfr;
+                            uint32_t* sl = a.scratch_len + s * (uint64_t)a.cap + nfr;
+                            const int64_t maxop = (int64_t)a.max_op;
+                            uint32_t k = 0;
+                            while (p < pend && k < room) {
+                                const uint32_t q = (uint32_t)((p - A) & MASK);
+                                const uint32_t q0 = q & ~3u;
+                                const uint32_t lo = *reinterpret_cast<const uint32_t*>(ring + q0);
+                                const uint32_t hi = *reinterpret_cast<const uint32_t*>(ring + ((q0 + 4) & MASK));
+                                const uint32_t v = (uint32_t)(((uint64_t)hi << 32 | lo) >> (8 * (q & 3)));
+                                const uint32_t stop4 = ~v & 0x80808080u;
+                                if ((v & 0xffu) == 0 || stop4 == 0) break;
+                                const int vl = (__builtin_ctz(stop4) >> 3) + 1;
+                                const uint32_t nn = ((v & 0x7fu) | ((v >> 1) & 0x3f80u) | ((v >> 2) & 0x1fc000u) |
+                                                     ((v >> 3) & 0xfe00000u)) &
+                                                    (0xffffffffu >> (32 - 7 * vl));
+                                const uint32_t vs = nn < (1u << 7) ? 1u : nn < (1u << 14) ? 2u : nn < (1u << 21) ? 3u : 4u;
+                                const int64_t fl = (int64_t)(vs + nn) + 4;
+                                const int64_t lim = L - p < maxop ? L - p : maxop;
+                                if (fl > lim) break;
+                                so[k] = (uint64_t)(base + p);
+                                sl[k] = (uint32_t)fl;
+                                ++k;
+                                p += fl;
+                            }
+                            nfr += k;
+                        }
+                        if (p >= wend) break;
                         if (p >= L) {
                             st = RH_SEG_END;
                             break;
                         }
-                        // bytes p..p+4 from two aligned LDS dwords (one round trip)
+                        // general step: bytes p..p+4 from two aligned LDS dwords
                         const uint32_t q = (uint32_t)((p - A) & MASK);
                         const uint32_t q0 = q & ~3u;
                         const uint32_t lo = *reinterpret_cast<const uint32_t*>(ring + q0);
                         const uint32_t hi = *reinterpret_cast<const uint32_t*>(ring + ((q0 + 4) & MASK));
                         const uint64_t x = ((uint64_t)hi << 32 | lo) >> (8 * (q & 3));
-                        {
-                            // Common case, all checks folded into one predicate: a non-zero first
-                            // byte, a varint of <= 4 bytes wholly before EOF, a frame within
-                            // maxOpSize and EOF, and scratch room.  Everything else takes the
-                            // full rule-by-rule path below (same results, more branches).
-                            const uint32_t stop4 = ~(uint32_t)x & 0x80808080u;
-                            const int vl = (__builtin_ctz(stop4 | 0x80000000u) >> 3) + 1;
-                            const uint32_t v = (uint32_t)x;
-                            const uint32_t nn = ((v & 0x7fu) | ((v >> 1) & 0x3f80u) | ((v >> 2) & 0x1fc000u) |
-                                                 ((v >> 3) & 0xfe00000u)) &
-                                                (0xffffffffu >> (32 - 7 * vl));
-                            const uint32_t vs = nn < (1u << 7) ? 1u : nn < (1u << 14) ? 2u : nn < (1u << 21) ? 3u : 4u;
-                            const int64_t total = (int64_t)vs + nn;
-                            const bool fast = (v & 0xffu) != 0 && stop4 != 0 && p + 8 <= L &&
-                                              total + 4 <= (int64_t)a.max_op && p + total + 4 <= L && nfr < a.cap;
-                            if (fast) {
-                                a.scratch_off[s * (uint64_t)a.cap + nfr] = (uint64_t)(base + p);
-                                a.scratch_len[s * (uint64_t)a.cap + nfr] = (uint32_t)(total + 4);
-                                ++nfr;
-                                p += total + 4;
-                                continue;
-                            }
-                        }
                         if ((x & 0xff) == 0) {  // terminator (SegmentedRaftLogFormat.isTerminator)
                             st = kTermPending;
                             break;
