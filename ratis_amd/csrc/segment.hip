@@ -262,6 +262,13 @@ __global__ __launch_bounds__(64) void segment_walk_kernel(SegArgs a) {
 // length jumps past window k+1 restarts the pipeline at the window holding the new position.
 constexpr int kBlock2 = 256;
 
+// Block-uniform 64-bit value, pinned to SGPRs (keeps the walker's compares scalar).
+__device__ __forceinline__ int64_t uniform64(int64_t v) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
 template <int W>
 struct Win {
     static constexpr int PER = W / (kBlock2 * 16);  // 16-B loads per thread per window
@@ -295,12 +302,15 @@ struct Win {
 #pragma unroll
         for (int i = 0; i < PER; ++i)
             *reinterpret_cast<u32x4s*>(ring + slot * W + (i * kBlock2 + t) * 16) = r[i];
+        // mirror of the ring's first 16 bytes past its end: an 8-byte read at any q0 <= 2W-4
+        // needs no wrap-around
+        if (slot == 0 && t == 0) *reinterpret_cast<u32x4s*>(ring + 2 * W) = r[0];
     }
 };
 
 template <int W>
 __global__ __launch_bounds__(kBlock2) void segment_walk_kernel2(SegArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t ring[];  // [2W]
+    extern __shared__ __attribute__((aligned(16))) uint8_t ring[];  // [2W + 16]: 2 windows + mirror
     __shared__ int sh_status;
     __shared__ long long sh_pos;
     __shared__ uint32_t sh_nfr;
@@ -308,10 +318,11 @@ __global__ __launch_bounds__(kBlock2) void segment_walk_kernel2(SegArgs a) {
     constexpr int64_t MASK = 2 * W - 1;
     const int t = threadIdx.x;
     for (uint64_t s = blockIdx.x; s < a.n_seg; s += gridDim.x) {
-        const int64_t base = (int64_t)a.seg_off[s];
+        const int64_t base = uniform64((int64_t)a.seg_off[s]);
         int64_t L = (int64_t)a.seg_len[s];
         if (base > a.buf_len) L = 0;
         else if (L > a.buf_len - base) L = a.buf_len - base;
+        L = uniform64(L);
         const uint8_t* seg = a.buf + base;
         const int64_t A = (base & ~(int64_t)15) - base;
         if (t == 0) {  // verifyHeader (RDR:179-205)
@@ -360,28 +371,34 @@ __global__ __launch_bounds__(kBlock2) void segment_walk_kernel2(SegArgs a) {
                             const uint32_t room = a.cap - nfr;
                             uint64_t* so = a.scratch_off + s * (uint64_t)a.cap + nfr;
                             uint32_t* sl = a.scratch_len + s * (uint64_t)a.cap + nfr;
-                            const int64_t maxop = (int64_t)a.max_op;
                             uint32_t k = 0;
-                            while (p < pend && k < room) {
-                                const uint32_t q = (uint32_t)((p - A) & MASK);
-                                const uint32_t q0 = q & ~3u;
-                                const uint32_t lo = *reinterpret_cast<const uint32_t*>(ring + q0);
-                                const uint32_t hi = *reinterpret_cast<const uint32_t*>(ring + ((q0 + 4) & MASK));
-                                const uint32_t v = (uint32_t)(((uint64_t)hi << 32 | lo) >> (8 * (q & 3)));
-                                const uint32_t stop4 = ~v & 0x80808080u;
-                                if ((v & 0xffu) == 0 || stop4 == 0) break;
-                                const int vl = (__builtin_ctz(stop4) >> 3) + 1;
-                                const uint32_t nn = ((v & 0x7fu) | ((v >> 1) & 0x3f80u) | ((v >> 2) & 0x1fc000u) |
-                                                     ((v >> 3) & 0xfe00000u)) &
-                                                    (0xffffffffu >> (32 - 7 * vl));
-                                const uint32_t vs = nn < (1u << 7) ? 1u : nn < (1u << 14) ? 2u : nn < (1u << 21) ? 3u : 4u;
-                                const int64_t fl = (int64_t)(vs + nn) + 4;
-                                const int64_t lim = L - p < maxop ? L - p : maxop;
-                                if (fl > lim) break;
-                                so[k] = (uint64_t)(base + p);
-                                sl[k] = (uint32_t)fl;
-                                ++k;
-                                p += fl;
+                            if (L <= 0x7fffffff && pend > p) {  // 32-bit offsets: all-scalar compares
+                                uint32_t p32 = (uint32_t)p;
+                                const uint32_t pend32 = (uint32_t)pend, L32 = (uint32_t)L, mo = a.max_op;
+                                uint32_t q = (uint32_t)((p - A) & MASK);
+                                while (p32 < pend32 && k < room) {
+                                    const uint32_t q0 = q & ~3u;
+                                    const uint32_t lo = *reinterpret_cast<const uint32_t*>(ring + q0);
+                                    const uint32_t hi = *reinterpret_cast<const uint32_t*>(ring + q0 + 4);  // mirror
+                                    const uint32_t v = (uint32_t)(((uint64_t)hi << 32 | lo) >> (8 * (q & 3)));
+                                    const uint32_t stop4 = ~v & 0x80808080u;
+                                    if ((v & 0xffu) == 0 || stop4 == 0) break;
+                                    const int vl = (__builtin_ctz(stop4) >> 3) + 1;
+                                    const uint32_t nn = ((v & 0x7fu) | ((v >> 1) & 0x3f80u) | ((v >> 2) & 0x1fc000u) |
+                                                         ((v >> 3) & 0xfe00000u)) &
+                                                        (0xffffffffu >> (32 - 7 * vl));
+                                    const uint32_t vs =
+                                        nn < (1u << 7) ? 1u : nn < (1u << 14) ? 2u : nn < (1u << 21) ? 3u : 4u;
+                                    const uint32_t fl = vs + nn + 4;  // nn < 2^28: no overflow
+                                    const uint32_t left = L32 - p32;
+                                    if (fl > (left < mo ? left : mo)) break;
+                                    so[k] = (uint64_t)base + p32;
+                                    sl[k] = fl;
+                                    ++k;
+                                    p32 += fl;
+                                    q = (q + fl) & (uint32_t)MASK;
+                                }
+                                p = p32;
                             }
                             nfr += k;
                         }
@@ -564,14 +581,14 @@ hipError_t launch_walk2(const SegArgs& a, int cus, hipStream_t stream) {
     static bool attr_set = false;
     if (!attr_set) {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(segment_walk_kernel2<W>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 2 * W);
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, 2 * W + 16);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
     const int per_cu = 2 * W <= 65536 ? 2 : 1;
     const uint64_t cap = (uint64_t)cus * per_cu;
     const uint64_t grid = a.n_seg < cap ? a.n_seg : cap;
-    hipLaunchKernelGGL(segment_walk_kernel2<W>, dim3((uint32_t)grid), dim3(kBlock2), 2 * W, stream, a);
+    hipLaunchKernelGGL(segment_walk_kernel2<W>, dim3((uint32_t)grid), dim3(kBlock2), 2 * W + 16, stream, a);
     return hipGetLastError();
 }
 
