@@ -280,7 +280,7 @@ typedef struct rh_segments {
 
 int rh_segments_scan_launch(rh_ctx* ctx, const rh_segments* segs, void* stream);
 /* Framing kernel variant (identical results): 0 = one wave per segment, 16 KiB LDS window;
- * 1 / 2 = one 256-thread block per segment, double-buffered 32 / 64 KiB windows (default 2). */
+ * 1 / 2 = one 256-thread block per segment, double-buffered 32 / 64 KiB windows (default 1). */
 int rh_segments_set_variant(int variant);
 
 /* ---- tuning hooks (bench / A-B experiments; results are identical for every variant) ---- */

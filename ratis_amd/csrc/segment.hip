@@ -574,7 +574,7 @@ __global__ __launch_bounds__(256) void segment_compact_kernel(const uint64_t* sc
     }
 }
 
-int g_seg_variant = 2;
+int g_seg_variant = 1;
 
 template <int W>
 hipError_t launch_walk2(const SegArgs& a, int cus, hipStream_t stream) {

@@ -85,7 +85,7 @@ def main():
             print(json.dumps({"kernel": "segments_scan", "variant": v, "shape": tag, "segments": n,
                               "median_GBps": round(float(np.median(x)), 1), "min_GBps": round(float(x.min()), 1),
                               "max_GBps": round(float(x.max()), 1)}), flush=True)
-        _lib.check(lib.rh_segments_set_variant(2))
+        _lib.check(lib.rh_segments_set_variant(1))
 
     if "framing" not in only:
         ss = None

@@ -126,7 +126,7 @@ def seg_variant(request):
     lib = _lib.load()
     _lib.check(lib.rh_segments_set_variant(request.param))
     yield request.param
-    _lib.check(lib.rh_segments_set_variant(2))
+    _lib.check(lib.rh_segments_set_variant(1))
 
 
 @pytest.mark.parametrize("big", [False, True])
