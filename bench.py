@@ -13,6 +13,9 @@ Steps rotate over 8 distinct batches (615 MB > the 256 MiB Infinity Cache) so ev
 HBM, not a cache.  Also reported in the same JSON line:
   * crc32c: SegmentedRaftLog frame verification GB/s (config 5: 256 x 32 MiB segments of 4 KiB
     frames = 8 GiB per GPU), its roofline and CPU baseline;
+  * read_path: segment framing (SegmentedRaftLogReader walk) and framing + CRC verify
+    (LogSegment.readSegmentFile) GB/s over the same config-5 segments;
+  * lease: batched LeaderStateImpl.hasLease / LeaderLease.extend checks/s over the same 1M groups;
   * pcie: host-buffer-inclusive rates for both paths;
   * cpu_baseline: the oracle (a scalar C port of the reference's Java arithmetic) timed on this
     host on a bounded sample, rank 0 at N = 1 only.
@@ -45,6 +48,7 @@ def parse():
     p.add_argument("--crc-segments", type=int, default=256, help="32 MiB segments per GPU (0 = skip CRC)")
     p.add_argument("--crc-steps", type=int, default=20)
     p.add_argument("--crc-variant", type=int, default=None)
+    p.add_argument("--no-lease", action="store_true")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-pcie", action="store_true")
     p.add_argument("--pmc-json", default=None, help="default: the newest profiles/r*/pmc_traffic.json")
@@ -261,6 +265,49 @@ def main():
                             "traffic_source": pmc.get("_path"),
                             "kernel": "crc_frames_kernel5<16,2> (variant 15)",
                             "algorithmic_bytes_per_launch": crc_alg, "avg_launch_ms": round(crc_kern_ms, 4)}}
+        # ---- read path: framing walk, then framing + verify, over the same segment images
+        n_seg = args.crc_segments
+        sb = engine.SegmentBatch(buf=fb.buf,
+                                 seg_off=torch.arange(n_seg, dtype=torch.int64, device=dev) * ss.segment_size,
+                                 seg_len=torch.full((n_seg,), ss.segment_size, dtype=torch.int64, device=dev),
+                                 frames_per_seg_cap=ss.frames_per_segment + 16)
+        for _ in range(2):
+            engine.segments_scan(ctx, sb, stream=stream)
+        barrier()
+        f0, f1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        f0.record(stream)
+        for _ in range(args.crc_steps):
+            engine.segments_scan(ctx, sb, stream=stream)
+        f1.record(stream)
+        barrier()
+        scan_ms = f0.elapsed_time(f1) / args.crc_steps
+        nfr_found = int(sb.total_frames.item())
+        frame_ok = (nfr_found == fb.n and torch.equal(sb.frame_off[:fb.n], fb.frame_off)
+                    and torch.equal(sb.frame_len[:fb.n], fb.frame_len)
+                    and bool((sb.seg_status[:n_seg] == _lib.RH_SEG_END).all()))
+        rb = engine.FrameBatch(buf=fb.buf, frame_off=sb.frame_off[:fb.n], frame_len=sb.frame_len[:fb.n])
+        rb.alloc_outputs()
+        barrier()
+        f0.record(stream)
+        for _ in range(args.crc_steps):
+            engine.segments_scan(ctx, sb, stream=stream)
+            engine.crc32c_frames(ctx, rb, flags=_lib.RH_CRC_VERIFY, stream=stream)
+        f1.record(stream)
+        barrier()
+        read_ms = f0.elapsed_time(f1) / args.crc_steps
+        seg_bytes = n_seg * ss.segment_size
+        tot_seg_bytes = sum_over_ranks(seg_bytes)
+        scan_ach = seg_bytes / (scan_ms * 1e-3) / 1e9
+        crc["read_path"] = {
+            "framing_GBps": round(tot_seg_bytes / (max_over_ranks(scan_ms) * 1e-3) / 1e9, 1),
+            "framing_plus_verify_GBps": round(tot_seg_bytes / (max_over_ranks(read_ms) * 1e-3) / 1e9, 1),
+            "unit": "GB/s (segment bytes, whole job)", "frames_found": nfr_found, "parity_ok": bool(frame_ok),
+            "ms_framing": round(scan_ms, 4), "ms_framing_plus_verify": round(read_ms, 4),
+            "roofline": {"bound": "hbm", "achieved": round(scan_ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(scan_ach / HBM_PEAK_GBPS, 4),
+                         "kernel": "segment_walk_kernel2<32768> + scan + compact",
+                         "algorithmic_bytes_per_launch": seg_bytes}}
+        del sb, rb
         if not args.no_pcie:
             # host image of 8 segments (256 MiB) -> H2D pinned + verify
             nseg = min(8, args.crc_segments)
@@ -285,6 +332,58 @@ def main():
             pcie["crc32c_GBps_incl_pcie"] = round(nfr * ss.frame_size / (ms * 1e-3) / 1e9, 2)
         del ss, fb
         torch.cuda.empty_cache()
+
+    # ------------------------------------------------------------------ leader lease (same groups)
+    lease = {}
+    lease_inputs = []
+    if not args.no_lease:
+        NOW = 1 << 60
+        MS = 1_000_000
+        TIMEOUT_MS = 100
+        rng = np.random.default_rng(workload.SEED + 5 + rank)
+        for h in host:
+            ts = NOW - rng.integers(-MS, 3 * TIMEOUT_MS * MS, size=h.follower.shape, dtype=np.int64)
+            lin = NOW - rng.integers(0, 2 * TIMEOUT_MS * MS, size=h.n, dtype=np.int64)
+            lease_inputs.append((ts, h.conf, lin))
+        lbatches = []
+        for r in range(args.rotate):
+            tiers = []
+            for ts, conf, lin in lease_inputs:
+                t = engine.LeaseTier(follower_ts=torch.from_numpy(ts + r * SHIFT).to(dev),
+                                     conf=torch.from_numpy(conf.view(np.int32)).to(dev),
+                                     lease_in=torch.from_numpy(lin + r * SHIFT).to(dev))
+                tiers.append(t.alloc_outputs())
+            lbatches.append(tiers)
+        for i in range(args.warmup):
+            engine.lease_launch(ctx, lbatches[i % args.rotate], NOW + (i % args.rotate) * SHIFT, TIMEOUT_MS,
+                                stream=stream)
+        barrier()
+        l0, l1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        l0.record(stream)
+        for i in range(args.steps):
+            engine.lease_launch(ctx, lbatches[i % args.rotate], NOW + (i % args.rotate) * SHIFT, TIMEOUT_MS,
+                                stream=stream)
+        l1.record(stream)
+        barrier()
+        lease_kern_ms = l0.elapsed_time(l1) / args.steps
+        lease_ms = max_over_ranks(lease_kern_ms)
+        lease_ok = True
+        for r, tiers in enumerate(lbatches[: min(args.rotate, args.steps)]):
+            for (ts, conf, lin), t in zip(lease_inputs, tiers):
+                ref = orc.lease_soa(ts, conf, lin, NOW, TIMEOUT_MS)
+                nw = (t.n + 63) // 64
+                lease_ok &= bool(np.array_equal(t.lease_out.cpu().numpy(), ref["lease"] + r * SHIFT)
+                                 and np.array_equal(t.has_lease_bits[:nw].cpu().numpy().view(np.uint64),
+                                                    ref["has_lease_bits"]))
+        lease_alg = sum(ts.size * 8 + conf.size * 4 + lin.size * 16 + 2 * ((lin.size + 63) // 64) * 8
+                        for ts, conf, lin in lease_inputs)
+        lease_ach = lease_alg / (lease_kern_ms * 1e-3) / 1e9
+        lease = {"checks_per_s": round(total_groups / (lease_ms * 1e-3), 1), "unit": "hasLease checks/s (whole job)",
+                 "ms_per_pass": round(lease_ms, 5), "parity_ok": lease_ok, "timeout_ms": TIMEOUT_MS,
+                 "roofline": {"bound": "hbm", "achieved": round(lease_ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                              "frac": round(lease_ach / HBM_PEAK_GBPS, 4), "kernel": "lease_kernel<F> (F=4, 6)",
+                              "algorithmic_bytes_per_launch": lease_alg}}
+        del lbatches
 
     # ------------------------------------------------------------------ CPU baseline (rank 0, N = 1)
     cpu = None
@@ -319,6 +418,18 @@ def main():
                        "sample": f"{reps} passes over 8 x 32 MiB segment images ({offs.size} 4 KiB frames), "
                                  "PureJavaCrc32C slicing-by-8 restatement, 1 thread"}
             crc["cpu_baseline"] = cpu_crc
+        if lease_inputs:
+            ts, conf, lin = lease_inputs[0]
+            reps = 0
+            tc = time.perf_counter()
+            while time.perf_counter() - tc < 3.0:
+                orc.lease_soa(ts, conf, lin, 1 << 60, 100)
+                reps += 1
+            cdt = time.perf_counter() - tc
+            lease["cpu_baseline"] = {"value": round(conf.size * reps / cdt, 1), "unit": "checks/s", "cores": 1,
+                                     "kind": "port",
+                                     "sample": f"{reps} passes of orc_lease_soa over the {conf.size}-group stable "
+                                               f"tier ({cdt:.1f} s, literal LeaderLease restatement, 1 thread)"}
 
     stats = shard.allreduce_stats({"groups_evaluated": n_mine * args.steps, "commits_advanced": advanced,
                                    "frames_verified": frames_verified, "bytes_verified": bytes_verified,
@@ -345,6 +456,7 @@ def main():
         "roofline": roofline,
         "cpu_baseline": cpu,
         "crc32c": crc,
+        "lease": lease,
         "pcie": pcie,
         "parity_ok": check_ok,
         "advanced_groups_batch0_rank0": advanced,
