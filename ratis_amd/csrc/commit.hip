@@ -70,15 +70,7 @@ struct LaunchArgs {
     int n_tiers;
 };
 
-__device__ __forceinline__ uint64_t spread32(uint64_t x) {
-    x &= 0xFFFFFFFFull;
-    x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
-    x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
-    x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
-    x = (x | (x << 2)) & 0x3333333333333333ull;
-    x = (x | (x << 1)) & 0x5555555555555555ull;
-    return x;
-}
+using rh_bits::spread32;
 
 typedef int64_t v2i64 __attribute__((ext_vector_type(2)));
 typedef uint32_t v2u32 __attribute__((ext_vector_type(2)));

@@ -11,8 +11,9 @@
 // Work is done on elapsed times d = now - t (wrapping int64).  For |d| < 2^62 (every realistic
 // nanoTime) Timestamp.compareTo(a, b) == sign(d_b - d_a), so "sort ascending by timestamp, take
 // element size/2" is "take the ((size-1)/2)-th smallest elapsed time" -- the same order statistic
-// the commit kernel takes, here over the followers only (self has no FollowerInfo).  One group
-// per lane, column loads coalesced across the wave, hasLease/extended bits by wave ballot.
+// the commit kernel takes, here over the followers only (self has no FollowerInfo).  Two groups
+// per lane with 16-byte column loads, all tiers of a follower-count class in one launch,
+// hasLease/extended bits by wave ballot.
 #include "rh_internal.h"
 #include "sortnet.h"
 
@@ -20,9 +21,9 @@ namespace {
 
 constexpr int kLeaseBlock = 256;
 
-struct LeaseArgs {
-    rh_lease_soa t;
-};
+typedef int64_t v2i64 __attribute__((ext_vector_type(2)));
+typedef uint32_t v2u32 __attribute__((ext_vector_type(2)));
+using rh_bits::spread32;
 
 __device__ __forceinline__ int64_t elapsed_ms(int64_t d) { return d / 1000000; }  // truncating, as Java
 
@@ -52,21 +53,16 @@ __device__ __forceinline__ bool has_majority(uint32_t mask, uint32_t active, boo
     return num > (__builtin_popcount(mask) + (self ? 1 : 0)) / 2;
 }
 
+// hasLease() for one group (see the file header for the elapsed-time form).
 template <int F>
-__global__ __launch_bounds__(kLeaseBlock) void lease_kernel(LeaseArgs a) {
-    const rh_lease_soa& t = a.t;
-    const uint64_t i = (uint64_t)blockIdx.x * kLeaseBlock + threadIdx.x;
-    const bool in = i < t.n;
-    const uint32_t w = in ? t.conf[i] : 0u;
-    const int64_t lin = in ? t.lease_in[i] : 0;
-    const bool en = t.enabled_bits ? ((t.enabled_bits[i >> 6] >> (i & 63)) & 1ull) : true;
+__device__ __forceinline__ void lease_one(const rh_lease_soa& t, const int64_t (&ts)[F > 0 ? F : 1], uint32_t w,
+                                          int64_t lin, bool en, bool in, int64_t& lout, bool& has, bool& ext) {
     const int64_t now = t.now_nanos;
     int64_t d[F > 0 ? F : 1];
     uint32_t act = 0;
 #pragma unroll
     for (int k = 0; k < F; ++k) {
-        const int64_t ts = in ? t.follower_ts[(uint64_t)k * t.col_stride + i] : now;
-        d[k] = (int64_t)((uint64_t)now - (uint64_t)ts);
+        d[k] = (int64_t)((uint64_t)now - (uint64_t)ts[k]);
         act |= (elapsed_ms(d[k]) < t.timeout_ms ? 1u : 0u) << k;
     }
     const uint32_t nm = w & 0x3FFFu, om = (w >> 16) & 0x3FFFu;
@@ -78,10 +74,10 @@ __global__ __launch_bounds__(kLeaseBlock) void lease_kernel(LeaseArgs a) {
     const bool singleton = cur_size == 1 && prev_size <= 1;
     const bool valid_in = singleton || elapsed_ms((int64_t)((uint64_t)now - (uint64_t)lin)) < t.timeout_ms;
     const bool maj = has_majority(nm, act, self) && (!trans || has_majority(om, act, self_old));
-    const bool extend = in && active && en && !valid_in && maj;
-    int64_t lout = lin;
-    bool has = in && active && en && valid_in;
-    if (extend) {
+    ext = in && active && en && !valid_in && maj;
+    lout = lin;
+    has = in && active && en && valid_in;
+    if (ext) {
         const int64_t dc = majority_ack_elapsed<F>(d, nm);
         const int64_t dold = trans ? majority_ack_elapsed<F>(d, om) : 0;  // old == null -> currentTime()
         // Timestamp.earliest(a, b) = a.compareTo(b) > 0 ? b : a, with a - b == dold - dc (wrapping)
@@ -89,30 +85,132 @@ __global__ __launch_bounds__(kLeaseBlock) void lease_kernel(LeaseArgs a) {
         lout = (int64_t)((uint64_t)now - (uint64_t)dn);
         has = singleton || elapsed_ms(dn) < t.timeout_ms;
     }
-    if (in) t.lease_out[i] = lout;
-    const uint64_t hb = __ballot(has);
-    const uint64_t xb = __ballot(extend);
+}
+
+// One wave = 128 groups, lane l holds groups 2l and 2l+1: every column is one 16-byte load per
+// lane (VEC; needs an even col_stride and 16-byte aligned columns) and the two ballots of the
+// wave interleave into its two bit words.
+template <int F, bool VEC>
+__device__ __forceinline__ void lease_wave(const rh_lease_soa& t, uint64_t wbase) {
     const int lane = threadIdx.x & 63;
-    const uint64_t word = i >> 6;
-    if (lane == 0 && (word << 6) < t.n) {
-        t.has_lease_bits[word] = hb;
-        if (t.extended_bits) t.extended_bits[word] = xb;
+    const uint64_t r0 = wbase + 2 * (uint64_t)lane;
+    const bool in0 = r0 < t.n, in1 = r0 + 1 < t.n;
+    int64_t ts0[F > 0 ? F : 1], ts1[F > 0 ? F : 1];
+    uint32_t w0 = 0, w1 = 0;
+    int64_t l0 = 0, l1 = 0;
+    if (VEC && in1) {
+#pragma unroll
+        for (int k = 0; k < F; ++k) {
+            const v2i64 x = *reinterpret_cast<const v2i64*>(t.follower_ts + (uint64_t)k * t.col_stride + r0);
+            ts0[k] = x.x;
+            ts1[k] = x.y;
+        }
+        const v2u32 c = *reinterpret_cast<const v2u32*>(t.conf + r0);
+        const v2i64 li = *reinterpret_cast<const v2i64*>(t.lease_in + r0);
+        w0 = c.x;
+        w1 = c.y;
+        l0 = li.x;
+        l1 = li.y;
+    } else {
+#pragma unroll
+        for (int k = 0; k < F; ++k) {
+            ts0[k] = in0 ? t.follower_ts[(uint64_t)k * t.col_stride + r0] : t.now_nanos;
+            ts1[k] = in1 ? t.follower_ts[(uint64_t)k * t.col_stride + r0 + 1] : t.now_nanos;
+        }
+        w0 = in0 ? t.conf[r0] : 0u;
+        w1 = in1 ? t.conf[r0 + 1] : 0u;
+        l0 = in0 ? t.lease_in[r0] : 0;
+        l1 = in1 ? t.lease_in[r0 + 1] : 0;
+    }
+    // r0 is even, so both groups' bits live in the same enabled word
+    const uint64_t ew = (t.enabled_bits && in0) ? t.enabled_bits[r0 >> 6] : ~0ull;
+    const bool e0 = (ew >> (r0 & 63)) & 1ull;
+    const bool e1 = (ew >> ((r0 + 1) & 63)) & 1ull;
+    int64_t o0, o1;
+    bool h0, h1, x0, x1;
+    lease_one<F>(t, ts0, w0, l0, e0, in0, o0, h0, x0);
+    lease_one<F>(t, ts1, w1, l1, e1, in1, o1, h1, x1);
+    if (VEC && in1) {
+        *reinterpret_cast<v2i64*>(t.lease_out + r0) = v2i64{o0, o1};
+    } else {
+        if (in0) t.lease_out[r0] = o0;
+        if (in1) t.lease_out[r0 + 1] = o1;
+    }
+    const uint64_t he = __ballot(h0), ho = __ballot(h1);
+    const uint64_t xe = __ballot(x0), xo = __ballot(x1);
+    const uint64_t word = wbase >> 6;
+    const uint64_t nwords = (t.n + 63) >> 6;
+    if (lane < 2 && word + lane < nwords) {
+        const uint64_t hw = lane ? (spread32(he >> 32) | (spread32(ho >> 32) << 1))
+                                 : (spread32(he) | (spread32(ho) << 1));
+        t.has_lease_bits[word + lane] = hw;
+        if (t.extended_bits) {
+            const uint64_t xw = lane ? (spread32(xe >> 32) | (spread32(xo >> 32) << 1))
+                                     : (spread32(xe) | (spread32(xo) << 1));
+            t.extended_bits[word + lane] = xw;
+        }
     }
 }
 
-template <int F>
-void launch_f(const rh_lease_soa& t, hipStream_t stream) {
-    LeaseArgs a{t};
-    const uint64_t blocks = (t.n + kLeaseBlock - 1) / kLeaseBlock;
-    hipLaunchKernelGGL(lease_kernel<F>, dim3((uint32_t)blocks), dim3(kLeaseBlock), 0, stream, a);
+// All tiers of a follower-count class in one launch: block b belongs to the tier whose block
+// range holds it (block-uniform), then a block-uniform switch on F.
+struct LeaseLaunch {
+    rh_lease_soa t[RH_MAX_TIERS];
+    uint64_t first_block[RH_MAX_TIERS + 1];
+    uint32_t vec_mask;
+    int n_tiers;
+};
+
+template <int F, int FHI>
+__device__ __forceinline__ void lease_dispatch(const rh_lease_soa& t, bool vec, uint64_t wbase) {
+    if constexpr (F <= FHI) {
+        if ((int)t.n_followers == F) {
+            if (vec) lease_wave<F, true>(t, wbase);
+            else lease_wave<F, false>(t, wbase);
+        } else {
+            lease_dispatch<F + 1, FHI>(t, vec, wbase);
+        }
+    }
 }
 
-template <int F = 0>
-void dispatch(const rh_lease_soa& t, hipStream_t stream) {
-    if constexpr (F <= 14) {
-        if ((int)t.n_followers == F) launch_f<F>(t, stream);
-        else dispatch<F + 1>(t, stream);
+template <int FLO, int FHI>
+__global__ __launch_bounds__(kLeaseBlock) void lease_kernel(LeaseLaunch a) {
+    const uint64_t b = blockIdx.x;
+    int k = 0;
+#pragma unroll
+    for (int i = 1; i < RH_MAX_TIERS; ++i)
+        if (i < a.n_tiers && b >= a.first_block[i]) k = i;
+    const rh_lease_soa& t = a.t[k];
+    const uint64_t wbase = ((b - a.first_block[k]) * kLeaseBlock / 64 + (threadIdx.x >> 6)) * 128;
+    if (wbase >= t.n) return;
+    lease_dispatch<FLO, FHI>(t, (a.vec_mask >> k) & 1u, wbase);
+}
+
+constexpr uint64_t kGroupsPerBlock = kLeaseBlock / 64 * 128;
+
+int launch_class(const rh_lease_soa* tiers, int n_tiers, int flo, int fhi, hipStream_t stream) {
+    LeaseLaunch a{};
+    uint64_t blocks = 0;
+    for (int i = 0; i < n_tiers; ++i) {
+        const rh_lease_soa& t = tiers[i];
+        if (t.n == 0 || (int)t.n_followers < flo || (int)t.n_followers > fhi) continue;
+        const bool vec = (t.n_followers == 0 || t.col_stride % 2 == 0) &&
+                         (t.n_followers == 0 || ((uintptr_t)t.follower_ts & 15) == 0) &&
+                         ((uintptr_t)t.conf & 7) == 0 && ((uintptr_t)t.lease_in & 15) == 0 &&
+                         ((uintptr_t)t.lease_out & 15) == 0;
+        a.t[a.n_tiers] = t;
+        a.first_block[a.n_tiers] = blocks;
+        a.vec_mask |= (vec ? 1u : 0u) << a.n_tiers;
+        ++a.n_tiers;
+        blocks += (t.n + kGroupsPerBlock - 1) / kGroupsPerBlock;
     }
+    if (a.n_tiers == 0) return RH_OK;
+    a.first_block[a.n_tiers] = blocks;
+    if (blocks > 0x7fffffffull) return rh::fail(RH_E_RANGE, "rh_lease_soa_launch: too many groups");
+    if (flo == 0) hipLaunchKernelGGL((lease_kernel<0, 7>), dim3((uint32_t)blocks), dim3(kLeaseBlock), 0, stream, a);
+    else hipLaunchKernelGGL((lease_kernel<8, 14>), dim3((uint32_t)blocks), dim3(kLeaseBlock), 0, stream, a);
+    RH_HIP(hipGetLastError());
+    return RH_OK;
 }
 
 }  // namespace
@@ -131,10 +229,8 @@ int rh_lease_launch_impl(rh_ctx* ctx, const rh_lease_soa* tiers, int n_tiers, hi
         if (t.timeout_ms < 0) return rh::fail(RH_E_INVAL, "rh_lease_soa_launch: timeout_ms < 0");
         if (t.n > (uint64_t)UINT32_MAX * kLeaseBlock) return rh::fail(RH_E_RANGE, "rh_lease_soa_launch: n too large");
     }
-    for (int k = 0; k < n_tiers; ++k) {
-        if (tiers[k].n == 0) continue;
-        dispatch(tiers[k], stream);
-        RH_HIP(hipGetLastError());
-    }
+    int rc = launch_class(tiers, n_tiers, 0, 7, stream);
+    if (rc != RH_OK) return rc;
+    return launch_class(tiers, n_tiers, 8, 14, stream);
     return RH_OK;
 }

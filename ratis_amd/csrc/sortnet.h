@@ -1,6 +1,6 @@
 // Batcher merge-exchange sorting network on int64 registers, generated at compile time.
 // Shared by the commit (order statistics of match indices) and lease (order statistics of
-// follower response times) kernels.
+// follower response times) kernels, with the ballot bit-word helper both use.
 #pragma once
 #include <cstdint>
 
@@ -55,3 +55,19 @@ __device__ __forceinline__ void sort_net(int64_t (&v)[N]) {
 }
 
 }  // namespace rh_sort
+
+namespace rh_bits {
+
+// Interleave the low 32 bits of x with zeros (bit i -> bit 2i): two per-lane ballots of a wave
+// that holds 2 groups per lane become the group-ordered bit words.
+__device__ __forceinline__ uint64_t spread32(uint64_t x) {
+    x &= 0xFFFFFFFFull;
+    x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
+    x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
+    x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
+    x = (x | (x << 2)) & 0x3333333333333333ull;
+    x = (x | (x << 1)) & 0x5555555555555555ull;
+    return x;
+}
+
+}  // namespace rh_bits

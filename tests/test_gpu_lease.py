@@ -89,7 +89,7 @@ def test_lease_multi_tier_and_counts(ctx, orc):
     from ratis_amd import engine
     rng = np.random.default_rng(77)
     tiers, refs = [], []
-    for F, n in ((2, 70_001), (4, 900_000), (6, 100_000)):
+    for F, n in ((2, 70_001), (4, 900_000), (9, 3_333), (6, 100_000)):
         ts, conf, lease_in = random_lease_tier(rng, n, F)
         refs.append(orc.lease_soa(ts, conf, lease_in, NOW, 150))
         t = engine.LeaseTier(follower_ts=torch.from_numpy(ts).cuda(), conf=torch.from_numpy(conf.view(np.int32)).cuda(),
