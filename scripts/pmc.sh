@@ -26,4 +26,14 @@ for V in ${COMMIT_VARIANTS:-0}; do
   run commit${V}_b "FETCH_SIZE GRBM_GUI_ACTIVE" --what commit --variant $V
   run commit${V}_w "WRITE_SIZE" --what commit --variant $V
 done
+if [ "${FRAMING:-1}" = "1" ]; then
+  run framing_a "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_VMEM_RD" --what framing --segments 64
+  run framing_b "FETCH_SIZE GRBM_GUI_ACTIVE" --what framing --segments 64
+  run framing_w "WRITE_SIZE" --what framing --segments 64
+fi
+if [ "${LEASE:-1}" = "1" ]; then
+  run lease_a "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD" --what lease --iters 8
+  run lease_b "FETCH_SIZE GRBM_GUI_ACTIVE" --what lease --iters 8
+  run lease_w "WRITE_SIZE" --what lease --iters 8
+fi
 echo PMCDONE

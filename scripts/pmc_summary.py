@@ -29,7 +29,10 @@ def main():
     ap.add_argument("--commit", default="commit0")
     a = ap.parse_args()
     out = {"source": a.pmc_dir, "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), WRITE_SIZE x1, KiB x1024"}
-    for name, key, tag in (("crc", "crc_frames_kernel", a.crc), ("commit", "commit_kernel", a.commit)):
+    for name, key, tag in (("crc", "crc_frames_kernel", a.crc), ("commit", "commit_kernel", a.commit),
+                           ("framing", "segment_walk_kernel2", "framing"), ("lease", "lease_kernel", "lease")):
+        if not os.path.exists(os.path.join(a.pmc_dir, f"{tag}_b", "run_counter_collection.csv")):
+            continue
         f = per_kernel(os.path.join(a.pmc_dir, f"{tag}_b", "run_counter_collection.csv"), key)
         w = per_kernel(os.path.join(a.pmc_dir, f"{tag}_w", "run_counter_collection.csv"), key)
         s = per_kernel(os.path.join(a.pmc_dir, f"{tag}_a", "run_counter_collection.csv"), key)
@@ -47,7 +50,7 @@ def main():
                 parts = line.split()
                 if parts[:1] == ["frame_bytes"] and len(parts) >= 4:
                     units = int(parts[3])
-                if parts[:1] == ["alg_bytes"] and len(parts) >= 4:
+                if parts[:1] in (["alg_bytes"], ["seg_bytes"], ["lease_bytes"]) and len(parts) >= 4:
                     units = int(parts[3])
         if units:
             out[f"{name}_units_per_launch"] = units

@@ -12,7 +12,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--what", choices=["crc", "commit"], default="crc")
+    ap.add_argument("--what", choices=["crc", "commit", "framing", "lease"], default="crc")
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--segments", type=int, default=32)
     ap.add_argument("--iters", type=int, default=5)
@@ -21,7 +21,39 @@ def main():
 
     from ratis_amd import _lib, engine, workload
     ctx = engine.Context(0)
-    if a.what == "crc":
+    if a.what == "framing":
+        ss = workload.synth_segments(ctx, n_segments=a.segments, corrupt_rate=0)
+        n = ss.n_segments
+        sb = engine.SegmentBatch(buf=ss.batch.buf,
+                                 seg_off=torch.arange(n, device="cuda", dtype=torch.int64) * ss.segment_size,
+                                 seg_len=torch.full((n,), ss.segment_size, device="cuda", dtype=torch.int64),
+                                 frames_per_seg_cap=ss.frames_per_segment + 16)
+        for _ in range(a.iters):
+            engine.segments_scan(ctx, sb)
+        torch.cuda.synchronize()
+        print("seg_bytes", n * ss.segment_size, "segments", n)
+    elif a.what == "lease":
+        import numpy as np
+        host = workload.commit_snapshot(1_000_000)
+        rng = np.random.default_rng(3)
+        now = 1 << 60
+        batches = []
+        for r in range(8):
+            tiers = []
+            for h in host:
+                ts = now - rng.integers(0, 300_000_000, size=h.follower.shape, dtype=np.int64)
+                lin = now - rng.integers(0, 200_000_000, size=h.n, dtype=np.int64)
+                tiers.append(engine.LeaseTier(follower_ts=torch.from_numpy(ts).cuda(),
+                                              conf=torch.from_numpy(h.conf.view(np.int32)).cuda(),
+                                              lease_in=torch.from_numpy(lin).cuda()).alloc_outputs())
+            batches.append(tiers)
+        torch.cuda.synchronize()
+        for i in range(a.iters):
+            engine.lease_launch(ctx, batches[i % 8], now, 100)
+        torch.cuda.synchronize()
+        alg = sum(h.follower.size * 8 + h.n * 20 + 2 * ((h.n + 63) // 64) * 8 for h in host)
+        print("lease_bytes", alg, "groups", sum(h.n for h in host))
+    elif a.what == "crc":
         ss = workload.synth_segments(ctx, n_segments=a.segments, corrupt_rate=0)
         for _ in range(a.iters):
             engine.crc32c_frames(ctx, ss.batch, flags=_lib.RH_CRC_VERIFY, variant=a.variant)
