@@ -305,6 +305,9 @@ def main():
             "ms_framing": round(scan_ms, 4), "ms_framing_plus_verify": round(read_ms, 4),
             "roofline": {"bound": "hbm", "achieved": round(scan_ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(scan_ach / HBM_PEAK_GBPS, 4),
+                         "traffic": (round(pmc["framing_bytes_per_unit"] * n_seg) if "framing_bytes_per_unit" in pmc
+                                     else None),
+                         "traffic_source": pmc.get("_path"),
                          "kernel": "segment_walk_kernel2<32768> + scan + compact",
                          "algorithmic_bytes_per_launch": seg_bytes}}
         del sb, rb
@@ -381,7 +384,10 @@ def main():
         lease = {"checks_per_s": round(total_groups / (lease_ms * 1e-3), 1), "unit": "hasLease checks/s (whole job)",
                  "ms_per_pass": round(lease_ms, 5), "parity_ok": lease_ok, "timeout_ms": TIMEOUT_MS,
                  "roofline": {"bound": "hbm", "achieved": round(lease_ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                              "frac": round(lease_ach / HBM_PEAK_GBPS, 4), "kernel": "lease_kernel<F> (F=4, 6)",
+                              "frac": round(lease_ach / HBM_PEAK_GBPS, 4), "kernel": "lease_kernel<0,7> (F=4, 6 tiers fused)",
+                              "traffic": (round(pmc["lease_bytes_per_unit"] * n_mine) if "lease_bytes_per_unit" in pmc
+                                          else None),
+                              "traffic_source": pmc.get("_path"),
                               "algorithmic_bytes_per_launch": lease_alg}}
         del lbatches
 
