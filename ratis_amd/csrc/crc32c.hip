@@ -23,6 +23,8 @@
 // No MFMA: CRC is table/XOR integer work and the kernel is HBM-bound.
 #include "rh_internal.h"
 
+#include <type_traits>
+
 #include <vector>
 
 namespace {
@@ -1108,6 +1110,190 @@ __global__ __launch_bounds__(1024) void crc_frames_kernel5(FrameArgs a) {
     }
 }
 
+// Calls f(integral_constant<I>) for I = I0..P-1 in order while it returns true.
+template <int I, int P, class Fn>
+__device__ __forceinline__ bool run_steps(Fn& f) {
+    if constexpr (I < P) {
+        if (!f(std::integral_constant<int, I>{})) return false;
+        return run_steps<I + 1, P>(f);
+    } else {
+        return true;
+    }
+}
+
+template <int Q, int PF>
+__global__ __launch_bounds__(1024) void crc_frames_kernel6(FrameArgs a) {
+    constexpr int S = 64;
+    constexpr int64_t W = (int64_t)Q * S;
+    constexpr int kSliceBytes = 128 * 1024;
+    constexpr int kLaneWords = (Q > 32 ? Q / 32 : 1) * 8 * 16 * 32;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    if (__builtin_amdgcn_groupstaticsize() != 0) __builtin_trap();  // lds_word assumes base 0
+    uint32_t* llane = lds + kSliceBytes / 4;
+    uint32_t* lzw = llane + kLaneWords;
+    for (int i = threadIdx.x; i < kSliceBytes / 4; i += blockDim.x) {
+        // word i at byte 4i = region<<16 | e<<8 | half<<7 | c<<2
+        const int region = i >> 14, e = (i >> 6) & 255, half = (i >> 5) & 1;
+        lds[i] = a.slice[((region * 2 + half) << 8) | e];
+    }
+    for (int i = threadIdx.x; i < kLaneWords; i += blockDim.x) llane[i] = a.lanetab[i];
+    for (int i = threadIdx.x; i < 1024; i += blockDim.x) lzw[i] = a.zwin[i];
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63;
+    const uint32_t c = lane & 31;
+    uint32_t lb[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) lb[k] = ((uint32_t)(k >> 1) << 16) | ((uint32_t)(k & 1) << 7) | (c << 2);
+    const uint32_t lbase = (Q > 32 ? (uint32_t)(lane >> 5) * (8 * 16 * 32) : 0u) + c;
+    const int gl = lane & (Q - 1);
+    const int gid = lane / Q;
+    constexpr int kGroupsPerWave = 64 / Q;
+    const uint64_t wave = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    const uint64_t fstride = nwaves * kGroupsPerWave;
+    const bool trailer = (a.flags & (RH_CRC_VERIFY | RH_CRC_STAMP)) != 0;
+
+    auto advance = [&](const Cursor& cc) {
+        Cursor nx = cc;
+        if (cc.f < a.n) {
+            if (cc.wi + 1 < cc.nw) {
+                nx.wi = cc.wi + 1;
+            } else {
+                nx.f = cc.f + fstride;
+                cursor_frame(a, trailer, W, nx);
+            }
+        }
+        return nx;
+    };
+    auto load_chunk = [&](const Cursor& cc, uint32_t (&dd)[17]) {
+        const bool act = cc.f < a.n && cc.wi < cc.nw;
+        const int64_t be = cc.E - (cc.nw - 1 - cc.wi) * W - (int64_t)(Q - 1 - gl) * S;
+        const int64_t b0 = be - S - cc.sh;
+        const bool safe = !act || (b0 >= 0 && b0 + 68 <= a.buf_len);
+        if (__all(safe)) {
+            if (act) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const u32x4a v = *reinterpret_cast<const u32x4a*>(a.buf + b0 + 16 * q);
+                    dd[4 * q] = v.x;
+                    dd[4 * q + 1] = v.y;
+                    dd[4 * q + 2] = v.z;
+                    dd[4 * q + 3] = v.w;
+                }
+                dd[16] = *reinterpret_cast<const uint32_t*>(a.buf + b0 + 64);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 17; ++i) dd[i] = 0;
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < 17; ++i) {
+                const int64_t p = b0 + 4 * i;
+                uint32_t v = 0;
+                if (act && p + 4 > cc.o && p < be) {
+                    if (p >= 0 && p + 4 <= a.buf_len)
+                        v = *reinterpret_cast<const uint32_t*>(a.buf + p);
+                    else
+                        v = load_dword_clamped_slow(a.buf, p, a.buf_len);
+                }
+                dd[i] = v;
+            }
+        }
+    };
+
+    Cursor cq[PF + 1];
+    uint32_t dq[PF + 1][17];
+    cq[0].f = wave * kGroupsPerWave + gid;
+    cursor_frame(a, trailer, W, cq[0]);
+    load_chunk(cq[0], dq[0]);
+#pragma unroll
+    for (int p = 1; p < PF; ++p) {
+        cq[p] = advance(cq[p - 1]);
+        load_chunk(cq[p], dq[p]);
+    }
+    uint32_t R = 0;
+    // Ring of PF+1 (cursor, chunk) slots rotated by unrolling PF+1 steps with compile-time slot
+    // indices: no register copies between windows (kernel5 shifted the ring with ~50 v_mov).
+    auto step = [&](auto sc) -> bool {
+        constexpr int s = decltype(sc)::value;
+        constexpr int P = PF + 1;
+        if (!__any(cq[s].f < a.n)) return false;
+        cq[(s + PF) % P] = advance(cq[(s + PF - 1) % P]);
+        load_chunk(cq[(s + PF) % P], dq[(s + PF) % P]);
+        const Cursor& cur = cq[s];
+        uint32_t (&d)[17] = dq[s];
+
+        const bool act = cur.f < a.n && cur.wi < cur.nw;
+        const int64_t q0l = cur.E - (cur.nw - 1 - cur.wi) * W - (int64_t)(Q - gl) * S - cur.sh - cur.o;
+        const bool special = act && q0l < 4;
+        if (__any(special)) {
+            const int64_t qc = q0l < -80 ? -80 : (q0l > 4 ? 4 : q0l);
+            const int q0 = (int)qc;
+#pragma unroll
+            for (int i = 0; i < 17; ++i) {
+                const int q = q0 + 4 * i;
+                uint32_t v = act ? d[i] : 0u;
+                v = (q <= -4) ? 0u : (q < 0 ? (v & (0xFFFFFFFFu << (8 * -q))) : v);
+                const uint32_t up = (q >= 0 && q < 4) ? (a.init >> (8 * q)) : 0u;
+                const uint32_t dn2 = (q < 0 && q > -4) ? (a.init << (8 * -q)) : 0u;
+                d[i] = (act && special) ? (v ^ up ^ dn2) : d[i];
+            }
+        }
+        uint32_t r = 0;
+        const uint32_t sh = cur.sh;
+        if (__all(sh == 0 || !act)) {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) r = fold_word_perm(lds, r, d[j], lb);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) r = fold_word_perm(lds, r, __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh), lb);
+        }
+        uint32_t z = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) z ^= llane[lbase + ((uint32_t)(k * 16) + ((r >> (4 * k)) & 15u)) * 32u];
+        r = act ? z : 0u;
+#pragma unroll
+        for (int dlt = 1; dlt < Q; dlt <<= 1) r ^= __shfl_xor(r, dlt);
+        if (cur.f < a.n) {
+            if (act) R = zshift(lzw, R) ^ r;
+            if (cur.wi + 1 >= cur.nw) {
+                if (gl == 0) {
+                    const uint64_t f = cur.f;
+                    uint32_t state = R;
+                    if (cur.Lc < 4) state ^= (uint32_t)((uint64_t)a.init >> (8 * cur.Lc));
+                    const uint32_t value = ~state;
+                    const int64_t E = cur.E;
+                    if (a.crc_out) a.crc_out[f] = cur.malformed ? 0u : value;
+                    if (cur.malformed) {
+                        if (a.bad_bits)
+                            atomicOr(reinterpret_cast<unsigned long long*>(a.bad_bits + (f >> 6)), 1ull << (f & 63));
+                        if (a.n_bad) atomicAdd(a.n_bad, 1ull);
+                    } else if (a.flags & RH_CRC_STAMP) {
+                        a.wbuf[E + 0] = (uint8_t)(value >> 24);
+                        a.wbuf[E + 1] = (uint8_t)(value >> 16);
+                        a.wbuf[E + 2] = (uint8_t)(value >> 8);
+                        a.wbuf[E + 3] = (uint8_t)value;
+                    } else if (a.flags & RH_CRC_VERIFY) {
+                        const uint32_t stored = ((uint32_t)a.buf[E] << 24) | ((uint32_t)a.buf[E + 1] << 16) |
+                                                ((uint32_t)a.buf[E + 2] << 8) | (uint32_t)a.buf[E + 3];
+                        if (stored != value) {
+                            if (a.bad_bits)
+                                atomicOr(reinterpret_cast<unsigned long long*>(a.bad_bits + (f >> 6)),
+                                         1ull << (f & 63));
+                            if (a.n_bad) atomicAdd(a.n_bad, 1ull);
+                        }
+                    }
+                }
+                R = 0;
+            }
+        }
+        return true;
+    };
+    while (run_steps<0, PF + 1>(step)) {
+    }
+}
+
 struct Variant {
     int q, s;
     bool repl;
@@ -1132,6 +1318,9 @@ constexpr Variant kVariants[] = {
     {16, 64, true},    // 15: v5, prefetch 2 windows
     {16, 64, true},    // 16: v5, prefetch 3 windows
     {32, 64, true},    // 17: v5, 32 lanes, prefetch 2
+    {16, 64, true},    // 18: v6 (v5 + copy-free slot ring), prefetch 2
+    {16, 64, true},    // 19: v6, prefetch 1
+    {16, 64, true},    // 20: v6, prefetch 3
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
@@ -1140,7 +1329,7 @@ int g_default_variant = 15;  // v5, 16-lane 1 KiB windows, 2 windows in flight (
 template <int Q, int S, bool REPL, int V = 1, int ILP = 1>
 int launch_variant(rh_ctx* ctx, const FrameArgs& fa, hipStream_t stream) {
     constexpr int LOGQ = __builtin_ctz(Q);
-    constexpr size_t lds = V == 5 ? (size_t)128 * 1024 + (size_t)(Q > 32 ? Q / 32 : 1) * 16384 + 4096
+    constexpr size_t lds = V >= 5 ? (size_t)128 * 1024 + (size_t)(Q > 32 ? Q / 32 : 1) * 16384 + 4096
                          : V == 4 ? (REPL ? 4 * 256 * 32 * 4 : 4 * 256 * 4) + (size_t)(Q > 32 ? Q / 32 : 1) * 16384 + 4096 +
                                         (ILP == 2 ? 4096 : 0)
                                   : (REPL ? 4 * 256 * 32 * 4 : 4 * 256 * 4) + (size_t)(LOGQ + 1) * 4096 + (ILP == 2 ? 4096 : 0);
@@ -1148,7 +1337,9 @@ int launch_variant(rh_ctx* ctx, const FrameArgs& fa, hipStream_t stream) {
     const int block = REPL ? 1024 : 256;
     const int per_cu = REPL ? 1 : 4;
     void (*kern)(FrameArgs);
-    if constexpr (V == 5)
+    if constexpr (V == 6)
+        kern = crc_frames_kernel6<Q, ILP>;
+    else if constexpr (V == 5)
         kern = crc_frames_kernel5<Q, ILP>;  // ILP carries the prefetch depth for v5
     else if constexpr (V == 4)
         kern = crc_frames_kernel4<Q, ILP, REPL>;
@@ -1244,6 +1435,9 @@ int rh_crc_launch_variant(rh_ctx* ctx, const rh_frames* f, uint32_t flags, int v
         case 15: return launch_variant<16, 64, true, 5, 2>(ctx, a, stream);
         case 16: return launch_variant<16, 64, true, 5, 3>(ctx, a, stream);
         case 17: return launch_variant<32, 64, true, 5, 2>(ctx, a, stream);
+        case 18: return launch_variant<16, 64, true, 6, 2>(ctx, a, stream);
+        case 19: return launch_variant<16, 64, true, 6, 1>(ctx, a, stream);
+        case 20: return launch_variant<16, 64, true, 6, 3>(ctx, a, stream);
     }
     return rh::fail(RH_E_INVAL, "unknown CRC kernel variant");
 }
