@@ -23,8 +23,6 @@
 // No MFMA: CRC is table/XOR integer work and the kernel is HBM-bound.
 #include "rh_internal.h"
 
-#include <type_traits>
-
 #include <vector>
 
 namespace {
@@ -1110,20 +1108,11 @@ __global__ __launch_bounds__(1024) void crc_frames_kernel5(FrameArgs a) {
     }
 }
 
-// Calls f(integral_constant<I>) for I = I0..P-1 in order while it returns true.
-template <int I, int P, class Fn>
-__device__ __forceinline__ bool run_steps(Fn& f) {
-    if constexpr (I < P) {
-        if (!f(std::integral_constant<int, I>{})) return false;
-        return run_steps<I + 1, P>(f);
-    } else {
-        return true;
-    }
-}
-
-template <int Q, int PF>
-__global__ __launch_bounds__(1024) void crc_frames_kernel6(FrameArgs a) {
-    constexpr int S = 64;
+// v7: v5 with S bytes per lane chunk (S = 128: the per-window cursor, load-address and combine
+// work is amortised over twice the bytes).
+template <int Q, int S, int PF>
+__global__ __launch_bounds__(1024) void crc_frames_kernel7(FrameArgs a) {
+    constexpr int NW = S / 4;  // words per lane chunk
     constexpr int64_t W = (int64_t)Q * S;
     constexpr int kSliceBytes = 128 * 1024;
     constexpr int kLaneWords = (Q > 32 ? Q / 32 : 1) * 8 * 16 * 32;
@@ -1166,29 +1155,29 @@ __global__ __launch_bounds__(1024) void crc_frames_kernel6(FrameArgs a) {
         }
         return nx;
     };
-    auto load_chunk = [&](const Cursor& cc, uint32_t (&dd)[17]) {
+    auto load_chunk = [&](const Cursor& cc, uint32_t (&dd)[NW + 1]) {
         const bool act = cc.f < a.n && cc.wi < cc.nw;
         const int64_t be = cc.E - (cc.nw - 1 - cc.wi) * W - (int64_t)(Q - 1 - gl) * S;
         const int64_t b0 = be - S - cc.sh;
-        const bool safe = !act || (b0 >= 0 && b0 + 68 <= a.buf_len);
+        const bool safe = !act || (b0 >= 0 && b0 + S + 4 <= a.buf_len);
         if (__all(safe)) {
             if (act) {
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
+                for (int q = 0; q < NW / 4; ++q) {
                     const u32x4a v = *reinterpret_cast<const u32x4a*>(a.buf + b0 + 16 * q);
                     dd[4 * q] = v.x;
                     dd[4 * q + 1] = v.y;
                     dd[4 * q + 2] = v.z;
                     dd[4 * q + 3] = v.w;
                 }
-                dd[16] = *reinterpret_cast<const uint32_t*>(a.buf + b0 + 64);
+                dd[NW] = *reinterpret_cast<const uint32_t*>(a.buf + b0 + S);
             } else {
 #pragma unroll
-                for (int i = 0; i < 17; ++i) dd[i] = 0;
+                for (int i = 0; i < NW + 1; ++i) dd[i] = 0;
             }
         } else {
 #pragma unroll
-            for (int i = 0; i < 17; ++i) {
+            for (int i = 0; i < NW + 1; ++i) {
                 const int64_t p = b0 + 4 * i;
                 uint32_t v = 0;
                 if (act && p + 4 > cc.o && p < be) {
@@ -1203,7 +1192,7 @@ __global__ __launch_bounds__(1024) void crc_frames_kernel6(FrameArgs a) {
     };
 
     Cursor cq[PF + 1];
-    uint32_t dq[PF + 1][17];
+    uint32_t dq[PF + 1][NW + 1];
     cq[0].f = wave * kGroupsPerWave + gid;
     cursor_frame(a, trailer, W, cq[0]);
     load_chunk(cq[0], dq[0]);
@@ -1213,25 +1202,20 @@ __global__ __launch_bounds__(1024) void crc_frames_kernel6(FrameArgs a) {
         load_chunk(cq[p], dq[p]);
     }
     uint32_t R = 0;
-    // Ring of PF+1 (cursor, chunk) slots rotated by unrolling PF+1 steps with compile-time slot
-    // indices: no register copies between windows (kernel5 shifted the ring with ~50 v_mov).
-    auto step = [&](auto sc) -> bool {
-        constexpr int s = decltype(sc)::value;
-        constexpr int P = PF + 1;
-        if (!__any(cq[s].f < a.n)) return false;
-        cq[(s + PF) % P] = advance(cq[(s + PF - 1) % P]);
-        load_chunk(cq[(s + PF) % P], dq[(s + PF) % P]);
-        const Cursor& cur = cq[s];
-        uint32_t (&d)[17] = dq[s];
+    while (__any(cq[0].f < a.n)) {
+        cq[PF] = advance(cq[PF - 1]);
+        load_chunk(cq[PF], dq[PF]);
+        const Cursor& cur = cq[0];
+        uint32_t (&d)[NW + 1] = dq[0];
 
         const bool act = cur.f < a.n && cur.wi < cur.nw;
         const int64_t q0l = cur.E - (cur.nw - 1 - cur.wi) * W - (int64_t)(Q - gl) * S - cur.sh - cur.o;
         const bool special = act && q0l < 4;
         if (__any(special)) {
-            const int64_t qc = q0l < -80 ? -80 : (q0l > 4 ? 4 : q0l);
+            const int64_t qc = q0l < -(S + 16) ? -(S + 16) : (q0l > 4 ? 4 : q0l);
             const int q0 = (int)qc;
 #pragma unroll
-            for (int i = 0; i < 17; ++i) {
+            for (int i = 0; i < NW + 1; ++i) {
                 const int q = q0 + 4 * i;
                 uint32_t v = act ? d[i] : 0u;
                 v = (q <= -4) ? 0u : (q < 0 ? (v & (0xFFFFFFFFu << (8 * -q))) : v);
@@ -1244,10 +1228,10 @@ __global__ __launch_bounds__(1024) void crc_frames_kernel6(FrameArgs a) {
         const uint32_t sh = cur.sh;
         if (__all(sh == 0 || !act)) {
 #pragma unroll
-            for (int j = 0; j < 16; ++j) r = fold_word_perm(lds, r, d[j], lb);
+            for (int j = 0; j < NW; ++j) r = fold_word_perm(lds, r, d[j], lb);
         } else {
 #pragma unroll
-            for (int j = 0; j < 16; ++j) r = fold_word_perm(lds, r, __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh), lb);
+            for (int j = 0; j < NW; ++j) r = fold_word_perm(lds, r, __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh), lb);
         }
         uint32_t z = 0;
 #pragma unroll
@@ -1288,11 +1272,15 @@ __global__ __launch_bounds__(1024) void crc_frames_kernel6(FrameArgs a) {
                 R = 0;
             }
         }
-        return true;
-    };
-    while (run_steps<0, PF + 1>(step)) {
+#pragma unroll
+        for (int p = 0; p < PF; ++p) {
+            cq[p] = cq[p + 1];
+#pragma unroll
+            for (int j = 0; j < NW + 1; ++j) dq[p][j] = dq[p + 1][j];
+        }
     }
 }
+
 
 struct Variant {
     int q, s;
@@ -1318,9 +1306,9 @@ constexpr Variant kVariants[] = {
     {16, 64, true},    // 15: v5, prefetch 2 windows
     {16, 64, true},    // 16: v5, prefetch 3 windows
     {32, 64, true},    // 17: v5, 32 lanes, prefetch 2
-    {16, 64, true},    // 18: v6 (v5 + copy-free slot ring), prefetch 2
-    {16, 64, true},    // 19: v6, prefetch 1
-    {16, 64, true},    // 20: v6, prefetch 3
+    {16, 128, true},   // 18: v7 (v5 with 128-byte lane chunks, 2 KiB windows), prefetch 1
+    {16, 128, true},   // 19: v7, prefetch 2
+    {8, 128, true},    // 20: v7, 8 lanes x 128 B = 1 KiB windows, prefetch 1
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
@@ -1337,8 +1325,8 @@ int launch_variant(rh_ctx* ctx, const FrameArgs& fa, hipStream_t stream) {
     const int block = REPL ? 1024 : 256;
     const int per_cu = REPL ? 1 : 4;
     void (*kern)(FrameArgs);
-    if constexpr (V == 6)
-        kern = crc_frames_kernel6<Q, ILP>;
+    if constexpr (V == 7)
+        kern = crc_frames_kernel7<Q, S, ILP>;
     else if constexpr (V == 5)
         kern = crc_frames_kernel5<Q, ILP>;  // ILP carries the prefetch depth for v5
     else if constexpr (V == 4)
@@ -1364,7 +1352,10 @@ int launch_variant(rh_ctx* ctx, const FrameArgs& fa, hipStream_t stream) {
     a.shift = ctx->d_shift + (size_t)__builtin_ctz(S) * 1024;
     a.shift32 = ctx->d_shift + (size_t)5 * 1024;
     a.zwin = ctx->d_shift + (size_t)__builtin_ctz(Q * S) * 1024;
-    a.lanetab = Q == 16 ? ctx->d_lane16 : (Q == 32 ? ctx->d_lane32 : ctx->d_lane64);
+    if constexpr (S == 128)
+        a.lanetab = Q == 16 ? ctx->d_lane16_s128 : ctx->d_lane8_s128;
+    else
+        a.lanetab = Q == 16 ? ctx->d_lane16 : (Q == 32 ? ctx->d_lane32 : ctx->d_lane64);
     hipLaunchKernelGGL(kern, dim3((uint32_t)grid), dim3(block), lds, stream, a);
     RH_HIP(hipGetLastError());
     return RH_OK;
@@ -1384,10 +1375,11 @@ int rh_crc_upload_tables(rh_ctx* ctx) {
         rh::build_crc_shift_table(1ull << m, reinterpret_cast<uint32_t(*)[256]>(sh.data() + (size_t)m * 1024));
     RH_HIP(hipMalloc(&ctx->d_shift, sh.size() * 4));
     RH_HIP(hipMemcpy(ctx->d_shift, sh.data(), sh.size() * 4, hipMemcpyHostToDevice));
-    uint32_t** dst[3] = {&ctx->d_lane16, &ctx->d_lane32, &ctx->d_lane64};
-    const int qs[3] = {16, 32, 64};
-    for (int i = 0; i < 3; ++i) {
-        std::vector<uint32_t> lt = rh::build_crc_lane_tables(qs[i], 64);
+    uint32_t** dst[5] = {&ctx->d_lane16, &ctx->d_lane32, &ctx->d_lane64, &ctx->d_lane16_s128, &ctx->d_lane8_s128};
+    const int qs[5] = {16, 32, 64, 16, 8};
+    const int ss[5] = {64, 64, 64, 128, 128};
+    for (int i = 0; i < 5; ++i) {
+        std::vector<uint32_t> lt = rh::build_crc_lane_tables(qs[i], ss[i]);
         RH_HIP(hipMalloc(dst[i], lt.size() * 4));
         RH_HIP(hipMemcpy(*dst[i], lt.data(), lt.size() * 4, hipMemcpyHostToDevice));
     }
@@ -1435,9 +1427,9 @@ int rh_crc_launch_variant(rh_ctx* ctx, const rh_frames* f, uint32_t flags, int v
         case 15: return launch_variant<16, 64, true, 5, 2>(ctx, a, stream);
         case 16: return launch_variant<16, 64, true, 5, 3>(ctx, a, stream);
         case 17: return launch_variant<32, 64, true, 5, 2>(ctx, a, stream);
-        case 18: return launch_variant<16, 64, true, 6, 2>(ctx, a, stream);
-        case 19: return launch_variant<16, 64, true, 6, 1>(ctx, a, stream);
-        case 20: return launch_variant<16, 64, true, 6, 3>(ctx, a, stream);
+        case 18: return launch_variant<16, 128, true, 7, 1>(ctx, a, stream);
+        case 19: return launch_variant<16, 128, true, 7, 2>(ctx, a, stream);
+        case 20: return launch_variant<8, 128, true, 7, 1>(ctx, a, stream);
     }
     return rh::fail(RH_E_INVAL, "unknown CRC kernel variant");
 }

@@ -129,6 +129,8 @@ RH_EXPORT int rh_shutdown(rh_ctx* ctx) {
     (void)hipFree(ctx->d_lane16);
     (void)hipFree(ctx->d_lane32);
     (void)hipFree(ctx->d_lane64);
+    (void)hipFree(ctx->d_lane16_s128);
+    (void)hipFree(ctx->d_lane8_s128);
     (void)hipFree(ctx->d_scratch);
     if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
     (void)hipStreamDestroy(ctx->stream);

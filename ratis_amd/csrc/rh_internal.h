@@ -46,6 +46,8 @@ struct rh_ctx {
     uint32_t* d_lane16 = nullptr;  // lane-distance nibble tables for 16/32/64-lane windows
     uint32_t* d_lane32 = nullptr;
     uint32_t* d_lane64 = nullptr;
+    uint32_t* d_lane16_s128 = nullptr;  // same for 16 / 8 lanes x 128-byte chunks (kernel v7)
+    uint32_t* d_lane8_s128 = nullptr;
     // scratch for host-buffer convenience calls
     std::mutex mu;
     void* d_scratch = nullptr;
