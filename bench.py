@@ -178,7 +178,7 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": (round(pmc["commit_bytes_per_unit"] * n_mine) if "commit_bytes_per_unit" in pmc else None),
                 "traffic_source": pmc.get("_path"),
-                "kernel": "commit_kernel<1,7,1> (fused stable F=4 + joint F=6 tiers)",
+                "kernel": "commit_kernel_r8<1,6,256,NT,NTS> (variant 14: fused stable F=4 + joint F=6 tiers)",
                 "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": round(kern_ms, 5)}
 
     # ------------------------------------------------------------------ PCIe-inclusive commit
@@ -384,7 +384,7 @@ def main():
         lease = {"checks_per_s": round(total_groups / (lease_ms * 1e-3), 1), "unit": "hasLease checks/s (whole job)",
                  "ms_per_pass": round(lease_ms, 5), "parity_ok": lease_ok, "timeout_ms": TIMEOUT_MS,
                  "roofline": {"bound": "hbm", "achieved": round(lease_ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                              "frac": round(lease_ach / HBM_PEAK_GBPS, 4), "kernel": "lease_kernel<0,7> (F=4, 6 tiers fused)",
+                              "frac": round(lease_ach / HBM_PEAK_GBPS, 4), "kernel": "lease_kernel<0,7,NT,8> (variant 2: F=4, 6 tiers fused)",
                               "traffic": (round(pmc["lease_bytes_per_unit"] * n_mine) if "lease_bytes_per_unit" in pmc
                                           else None),
                               "traffic_source": pmc.get("_path"),

@@ -289,11 +289,18 @@ int rh_segments_set_variant(int variant);
  *         3: 64x64 with shared bank-conflicting tables)
  *   4-6   v2: + one window prefetched;  7-10 v3: branch-free fold with guarded slow path
  *   11-13 v4: per-lane zero-advance (lane-distance nibble tables) instead of the tree
- *   14-17 v5: v4 + one-v_perm table addressing; 14: 1 window in flight, 15: 2 (DEFAULT), 16: 3,
- *         17: 32-lane windows, 2 in flight */
-/* Commit kernel variants: sub-tiles of 128 groups per wave, 0 = 1 (default), 1 = 2, 2 = 4. */
+ *   14-17 v5: v4 + one-v_perm table addressing; 14: 1 window in flight, 15: 2, 16: 3,
+ *         17: 32-lane windows, 2 in flight
+ *   18-20 v7: 128-byte lane chunks;  21-22 v5 with non-temporal loads (2 / 1 windows in flight) */
+/* Commit kernel variants (see commit.hip): 0-2 sorting network with 1/2/4 sub-tiles of 128
+ * groups per wave; 3 split F classes; 4-7 persistent software-pipelined; 8-14 rank-mask
+ * selection at 8 waves/SIMD (12-14 with non-temporal loads); 15 = 0 with non-temporal loads. */
 int rh_commit_num_variants(void);
 int rh_commit_set_variant(int variant);
+/* Lease kernel variants: 0 plain loads, 1 non-temporal loads, 2 = 1 at 8 waves/SIMD, 3 = 0 at
+ * 8 waves/SIMD. */
+int rh_lease_num_variants(void);
+int rh_lease_set_variant(int variant);
 int rh_crc32c_num_variants(void);
 int rh_crc32c_set_variant(int variant);
 int rh_crc32c_frames_launch_variant(rh_ctx* ctx, const rh_frames* frames, uint32_t flags, int variant,

@@ -179,6 +179,8 @@ _SIGNATURES = {
     "rh_commit_num_variants": (c_int, []),
     "rh_commit_set_variant": (c_int, [c_int]),
     "rh_crc32c_set_variant": (c_int, [c_int]),
+    "rh_lease_num_variants": (c_int, []),
+    "rh_lease_set_variant": (c_int, [c_int]),
     "rh_crc32c_frames_launch_variant": (c_int, [c_void_p, POINTER(RhFrames), c_uint32, c_int, c_void_p]),
 }
 

@@ -23,15 +23,21 @@ namespace {
 
 constexpr int kBlock = 256;            // 4 waves
 constexpr int kGroupsPerLane = 2;      // 16-byte loads per column per lane
-// Sub-tiles (of 128 groups) per wave: the launch variant.  Default T = 1 (measured fastest:
-// lowest VGPR count, highest occupancy; scripts/microbench.py).
-int g_commit_variant = 0;
+// Launch variant (identical results; scripts/microbench.py A/B).  Default 14: rank-mask
+// selection at 8 waves/SIMD with non-temporal loads and stores (fastest measured).
+int g_commit_variant = 14;
 constexpr int kVariantT[] = {1, 2, 4};
 // 0-2: v1 with T = 1, 2, 4 sub-tiles per wave (F classes [1,7] and [8,14])
 // 3:   v1, T = 1, F classes [1,4], [5,7], [8,14] (narrower register allocation)
 // 4-6: v2 persistent + prefetch, F classes [1,4], [5,7], [8,14]; 3/4/5 waves per SIMD
 // 7:   v2, F classes [1,7], [8,14], 4 waves per SIMD
-constexpr int kNumCommitVariants = 8;
+// 8:   v3 rank-mask selection, 64-VGPR budget (8 waves/SIMD), F classes [1,6], [7,14]
+// 9:   v3 rank-mask selection, unpinned budget, F classes [1,7], [8,14]
+// 10/11: v3 (8) with 512 / 1024-thread workgroups (fewer dispatches)
+// 12/13: v3 (8) with non-temporal loads, 256 / 512-thread workgroups
+// 14:    v3 (12) with non-temporal stores as well
+// 15:    v1 (0) with non-temporal loads
+constexpr int kNumCommitVariants = 16;
 
 // Order statistics of the voters selected by `member` (bit i = slot i, bit N-1 = self):
 // getSorted (LSI:1076-1095) + MinMajorityMax.valueOf(sorted, gap) (LSI:926-943).
@@ -54,6 +60,16 @@ __device__ __forceinline__ void order_stats(const int64_t (&vals)[N], uint32_t m
         mx = (j == n - 1) ? s[j] : mx;
     }
     // gapThreshold clamp; Java long subtraction wraps (LSI:929-933).
+    if (gap != -1 && (int64_t)((uint64_t)mj - (uint64_t)mn) > gap) mj = mn;
+}
+
+// Same result as order_stats, from rank masks shared by the new and the old conf.
+template <int N>
+__device__ __forceinline__ void order_stats_rank(const int64_t (&vals)[N], const uint32_t (&less)[N],
+                                                 uint32_t member, int64_t gap, int64_t& mn, int64_t& mj,
+                                                 int64_t& mx) {
+    const int n = __builtin_popcount(member);
+    rh_sort::select_ranks<N>(vals, less, member, (n - 1) >> 1, n, mn, mj, mx);
     if (gap != -1 && (int64_t)((uint64_t)mj - (uint64_t)mn) > gap) mj = mn;
 }
 
@@ -83,25 +99,33 @@ struct SubTile {
     uint32_t w[2];
 };
 
-template <int F, bool VEC>
+// 16-byte column load; NT marks it non-temporal (streamed once, no reuse in L2/MALL).
+template <bool NT, typename V>
+__device__ __forceinline__ V ld16(const void* p) {
+    if (NT) return __builtin_nontemporal_load(reinterpret_cast<const V*>(p));
+    return *reinterpret_cast<const V*>(p);
+}
+
+template <int F, bool VEC, bool NT = false>
 __device__ __forceinline__ void load_sub(const TierArgs& ta, uint64_t r0, bool commit_mode, SubTile<F>& st) {
     const rh_commit_soa& t = ta.t;
     if (VEC) {
 #pragma unroll
         for (int k = 0; k < F; ++k) {
-            const v2i64 x = *reinterpret_cast<const v2i64*>(t.follower_index + (uint64_t)k * ta.stride + r0);
+            const v2i64 x = ld16<NT, v2i64>(t.follower_index + (uint64_t)k * ta.stride + r0);
             st.fv[0][k] = x.x;
             st.fv[1][k] = x.y;
         }
-        const v2i64 s = *reinterpret_cast<const v2i64*>(t.self_index + r0);
+        const v2i64 s = ld16<NT, v2i64>(t.self_index + r0);
         st.self[0] = s.x;
         st.self[1] = s.y;
-        const v2u32 c = *reinterpret_cast<const v2u32*>(t.conf + r0);
+        const v2u32 c = NT ? __builtin_nontemporal_load(reinterpret_cast<const v2u32*>(t.conf + r0))
+                           : *reinterpret_cast<const v2u32*>(t.conf + r0);
         st.w[0] = c.x;
         st.w[1] = c.y;
         if (commit_mode) {
-            const v2i64 ci = *reinterpret_cast<const v2i64*>(t.commit_in + r0);
-            const v2i64 ts = *reinterpret_cast<const v2i64*>(t.term_start + r0);
+            const v2i64 ci = ld16<NT, v2i64>(t.commit_in + r0);
+            const v2i64 ts = ld16<NT, v2i64>(t.term_start + r0);
             st.cin[0] = ci.x;
             st.cin[1] = ci.y;
             st.tstart[0] = ts.x;
@@ -124,7 +148,18 @@ __device__ __forceinline__ void load_sub(const TierArgs& ta, uint64_t r0, bool c
     }
 }
 
-template <int F, bool VEC>
+template <bool NT>
+__device__ __forceinline__ void st16(int64_t* p, int64_t a, int64_t b) {
+    v2i64 v;
+    v.x = a;
+    v.y = b;
+    if (NT)
+        __builtin_nontemporal_store(v, reinterpret_cast<v2i64*>(p));
+    else
+        *reinterpret_cast<v2i64*>(p) = v;
+}
+
+template <int F, bool VEC, bool RANK = false, bool NTS = false>
 __device__ __forceinline__ void compute_store_sub(const TierArgs& ta, uint64_t wbase, bool commit_mode,
                                                   const SubTile<F>& st) {
     constexpr int N = F + 1;
@@ -154,14 +189,29 @@ __device__ __forceinline__ void compute_store_sub(const TierArgs& ta, uint64_t w
         // followers.isEmpty() && !includeSelf -> Optional.empty()  (LSI:964-966, 976-978)
         const bool v = (w & RH_CONF_ACTIVE) && mnew != 0 && (!trans[g] || mold != 0);
         int64_t a0, a1, a2;
-        order_stats<N>(vals, mnew ? mnew : 1u, gap, a0, a1, a2);
-        if (any_trans) {
-            if (trans[g]) {  // combine(): element-wise min (LSI:915-920)
-                int64_t b0, b1, b2;
-                order_stats<N>(vals, mold ? mold : 1u, gap, b0, b1, b2);
-                a0 = b0 < a0 ? b0 : a0;
-                a1 = b1 < a1 ? b1 : a1;
-                a2 = b2 < a2 ? b2 : a2;
+        if (RANK) {
+            uint32_t less[N];
+            rh_sort::rank_masks<N>(vals, less);
+            order_stats_rank<N>(vals, less, mnew ? mnew : 1u, gap, a0, a1, a2);
+            if (any_trans) {
+                if (trans[g]) {  // combine(): element-wise min (LSI:915-920)
+                    int64_t b0, b1, b2;
+                    order_stats_rank<N>(vals, less, mold ? mold : 1u, gap, b0, b1, b2);
+                    a0 = b0 < a0 ? b0 : a0;
+                    a1 = b1 < a1 ? b1 : a1;
+                    a2 = b2 < a2 ? b2 : a2;
+                }
+            }
+        } else {
+            order_stats<N>(vals, mnew ? mnew : 1u, gap, a0, a1, a2);
+            if (any_trans) {
+                if (trans[g]) {  // combine(): element-wise min (LSI:915-920)
+                    int64_t b0, b1, b2;
+                    order_stats<N>(vals, mold ? mold : 1u, gap, b0, b1, b2);
+                    a0 = b0 < a0 ? b0 : a0;
+                    a1 = b1 < a1 ? b1 : a1;
+                    a2 = b2 < a2 ? b2 : a2;
+                }
             }
         }
         valid[g] = v;
@@ -181,30 +231,10 @@ __device__ __forceinline__ void compute_store_sub(const TierArgs& ta, uint64_t w
 
     // ---- stores ----
     if (VEC) {
-        if (commit_mode) {
-            v2i64 c;
-            c.x = cout[0];
-            c.y = cout[1];
-            *reinterpret_cast<v2i64*>(t.commit_out + r0) = c;
-        }
-        if (t.min_out) {
-            v2i64 m;
-            m.x = mn[0];
-            m.y = mn[1];
-            *reinterpret_cast<v2i64*>(t.min_out + r0) = m;
-        }
-        if (t.maj_out) {
-            v2i64 m;
-            m.x = mj[0];
-            m.y = mj[1];
-            *reinterpret_cast<v2i64*>(t.maj_out + r0) = m;
-        }
-        if (t.max_out) {
-            v2i64 m;
-            m.x = mx[0];
-            m.y = mx[1];
-            *reinterpret_cast<v2i64*>(t.max_out + r0) = m;
-        }
+        if (commit_mode) st16<NTS>(t.commit_out + r0, cout[0], cout[1]);
+        if (t.min_out) st16<NTS>(t.min_out + r0, mn[0], mn[1]);
+        if (t.maj_out) st16<NTS>(t.maj_out + r0, mj[0], mj[1]);
+        if (t.max_out) st16<NTS>(t.max_out + r0, mx[0], mx[1]);
     } else {
 #pragma unroll
         for (int g = 0; g < 2; ++g) {
@@ -260,26 +290,26 @@ __device__ __forceinline__ void compute_store_sub(const TierArgs& ta, uint64_t w
 
 // One workgroup tile = 4 waves x T sub-tiles of 128 groups.  All T sub-tiles' loads are
 // issued before any compute, so a wave keeps T x (F+3) x 1 KiB in flight.
-template <int F, int T>
+template <int F, int T, bool RANK = false, int BLK = kBlock, bool NT = false, bool NTS = false>
 __device__ __forceinline__ void run_tile(const TierArgs& ta, uint64_t tile) {
     constexpr uint64_t kWaveGroups = 128ull * T;
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const uint64_t wchunk = tile * (kWaveGroups * (kBlock / 64)) + (uint64_t)wave * kWaveGroups;
+    const uint64_t wchunk = tile * (kWaveGroups * (BLK / 64)) + (uint64_t)wave * kWaveGroups;
     const bool commit_mode = ta.t.mode == RH_MODE_COMMIT;
     if (wchunk >= ta.t.n) return;
     const bool full = wchunk + kWaveGroups <= ta.t.n && ta.vec_ok;
     SubTile<F> st[T];
     if (full) {
 #pragma unroll
-        for (int s = 0; s < T; ++s) load_sub<F, true>(ta, wchunk + 128 * s + 2 * lane, commit_mode, st[s]);
+        for (int s = 0; s < T; ++s) load_sub<F, true, NT>(ta, wchunk + 128 * s + 2 * lane, commit_mode, st[s]);
 #pragma unroll
-        for (int s = 0; s < T; ++s) compute_store_sub<F, true>(ta, wchunk + 128 * s, commit_mode, st[s]);
+        for (int s = 0; s < T; ++s) compute_store_sub<F, true, RANK, NTS>(ta, wchunk + 128 * s, commit_mode, st[s]);
     } else {
 #pragma unroll
         for (int s = 0; s < T; ++s) {
             load_sub<F, false>(ta, wchunk + 128 * s + 2 * lane, commit_mode, st[s]);
-            compute_store_sub<F, false>(ta, wchunk + 128 * s, commit_mode, st[s]);
+            compute_store_sub<F, false, RANK>(ta, wchunk + 128 * s, commit_mode, st[s]);
         }
     }
 }
@@ -390,12 +420,12 @@ __global__ __launch_bounds__(kBlock) void commit_kernel_v2(const LaunchArgs args
 
 namespace {
 
-template <int F, int FHI, int T>
+template <int F, int FHI, int T, bool RANK = false, int BLK = kBlock, bool NT = false, bool NTS = false>
 __device__ __forceinline__ void dispatch_f(const TierArgs& ta, uint64_t tile) {
     if (ta.t.n_followers == F)
-        run_tile<F, T>(ta, tile);
+        run_tile<F, T, RANK, BLK, NT, NTS>(ta, tile);
     else if constexpr (F < FHI)
-        dispatch_f<F + 1, FHI, T>(ta, tile);
+        dispatch_f<F + 1, FHI, T, RANK, BLK, NT, NTS>(ta, tile);
 }
 
 // One launch evaluates every tier whose F lies in [FLO, FHI]; blocks are assigned to tiers
@@ -409,6 +439,44 @@ __global__ __launch_bounds__(kBlock) void commit_kernel(const LaunchArgs args) {
         if (i < args.n_tiers && b >= args.tier[i].block_begin) ti = i;
     const TierArgs& ta = args.tier[ti];
     dispatch_f<FLO, FHI, T>(ta, (uint64_t)(b - ta.block_begin));
+}
+
+// v3: rank-mask order statistics (no sorted copies) with the register budget pinned to 64
+// VGPRs, so 8 waves fit per SIMD: a 1M-group launch (7813 waves of 128 groups) is resident in
+// one round on 256 CUs instead of ~1.5 rounds at 5 waves/SIMD.
+template <int FLO, int FHI, int BLK = kBlock, bool NT = false, bool NTS = false>
+__global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(8, 8))) void commit_kernel_r8(
+    const LaunchArgs args) {
+    const uint32_t b = blockIdx.x;
+    int ti = 0;
+#pragma unroll
+    for (int i = 1; i < RH_MAX_TIERS; ++i)
+        if (i < args.n_tiers && b >= args.tier[i].block_begin) ti = i;
+    const TierArgs& ta = args.tier[ti];
+    dispatch_f<FLO, FHI, 1, true, BLK, NT, NTS>(ta, (uint64_t)(b - ta.block_begin));
+}
+
+// v1 (sorting network, T = 1) with non-temporal loads.
+template <int FLO, int FHI>
+__global__ __launch_bounds__(kBlock) void commit_kernel_nt(const LaunchArgs args) {
+    const uint32_t b = blockIdx.x;
+    int ti = 0;
+#pragma unroll
+    for (int i = 1; i < RH_MAX_TIERS; ++i)
+        if (i < args.n_tiers && b >= args.tier[i].block_begin) ti = i;
+    const TierArgs& ta = args.tier[ti];
+    dispatch_f<FLO, FHI, 1, false, kBlock, true>(ta, (uint64_t)(b - ta.block_begin));
+}
+
+template <int FLO, int FHI>
+__global__ __launch_bounds__(kBlock) void commit_kernel_r(const LaunchArgs args) {
+    const uint32_t b = blockIdx.x;
+    int ti = 0;
+#pragma unroll
+    for (int i = 1; i < RH_MAX_TIERS; ++i)
+        if (i < args.n_tiers && b >= args.tier[i].block_begin) ti = i;
+    const TierArgs& ta = args.tier[ti];
+    dispatch_f<FLO, FHI, 1, true>(ta, (uint64_t)(b - ta.block_begin));
 }
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
@@ -465,7 +533,8 @@ int launch_class_v2(const rh_commit_soa* tiers, int n_tiers, int flo, int fhi, i
 
 int launch_class(const rh_commit_soa* tiers, int n_tiers, int flo, int fhi, int variant, hipStream_t stream) {
     const int T = kVariantT[variant < 3 ? variant : 0];
-    const uint64_t kTile = (uint64_t)kBlock * kGroupsPerLane * T;  // groups per workgroup
+    const int blk = (variant == 10 || variant == 13) ? 512 : variant == 11 ? 1024 : kBlock;
+    const uint64_t kTile = (uint64_t)(flo == 1 ? blk : kBlock) * kGroupsPerLane * T;  // groups per workgroup
     LaunchArgs args{};
     uint64_t blocks = 0;
     for (int i = 0; i < n_tiers; ++i) {
@@ -486,7 +555,27 @@ int launch_class(const rh_commit_soa* tiers, int n_tiers, int flo, int fhi, int 
     }
     if (args.n_tiers == 0) return RH_OK;
     if (blocks > 0x7FFFFFFFull) return rh::fail(RH_E_RANGE, "commit launch: too many groups");
-    if (flo == 1 && fhi == 4)
+    if (variant >= 8 && flo == 1) {  // rank-mask selection, T = 1
+        const dim3 g((uint32_t)blocks), b(blk);
+        if (variant == 10)
+            hipLaunchKernelGGL((commit_kernel_r8<1, 6, 512>), g, b, 0, stream, args);
+        else if (variant == 11)
+            hipLaunchKernelGGL((commit_kernel_r8<1, 6, 1024>), g, b, 0, stream, args);
+        else if (variant == 12)
+            hipLaunchKernelGGL((commit_kernel_r8<1, 6, 256, true>), g, b, 0, stream, args);
+        else if (variant == 13)
+            hipLaunchKernelGGL((commit_kernel_r8<1, 6, 512, true>), g, b, 0, stream, args);
+        else if (variant == 14)
+            hipLaunchKernelGGL((commit_kernel_r8<1, 6, 256, true, true>), g, b, 0, stream, args);
+        else if (variant == 15)
+            hipLaunchKernelGGL((commit_kernel_nt<1, 7>), g, b, 0, stream, args);
+        else if (fhi == 6)
+            hipLaunchKernelGGL((commit_kernel_r8<1, 6>), g, b, 0, stream, args);
+        else
+            hipLaunchKernelGGL((commit_kernel_r<1, 7>), g, b, 0, stream, args);
+    } else if (flo == 7)  // wide tiers: sorting network (rank masks of 8+ values would not unroll)
+        launch_t<7, 14>(T, (uint32_t)blocks, args, stream);
+    else if (flo == 1 && fhi == 4)
         launch_t<1, 4>(T, (uint32_t)blocks, args, stream);
     else if (flo == 5 && fhi == 7)
         launch_t<5, 7>(T, (uint32_t)blocks, args, stream);
@@ -532,6 +621,18 @@ int rh_commit_launch_impl(rh_ctx* ctx, const rh_commit_soa* tiers, int n_tiers, 
             return rh::fail(RH_E_INVAL, "rh_commit_soa_launch: adv_rows needs adv_commit and adv_count");
     }
     int rc = RH_OK;
+    if (variant == 15) {
+        rc = launch_class(tiers, n_tiers, 1, 7, variant, stream);
+        return rc != RH_OK ? rc : launch_class(tiers, n_tiers, 8, 14, variant, stream);
+    }
+    if (variant == 8 || variant >= 10) {
+        rc = launch_class(tiers, n_tiers, 1, 6, variant, stream);
+        return rc != RH_OK ? rc : launch_class(tiers, n_tiers, 7, 14, variant, stream);
+    }
+    if (variant == 9) {
+        rc = launch_class(tiers, n_tiers, 1, 7, variant, stream);
+        return rc != RH_OK ? rc : launch_class(tiers, n_tiers, 8, 14, variant, stream);
+    }
     if (variant <= 2) {
         rc = launch_class(tiers, n_tiers, 1, 7, variant, stream);
     } else if (variant == 3) {

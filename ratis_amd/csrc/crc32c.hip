@@ -174,6 +174,8 @@ __device__ __noinline__ uint32_t load_dword_clamped_slow(const uint8_t* buf, int
     return v;
 }
 
+// 4-byte-aligned 16-byte vector for non-temporal loads (the builtin needs a vector type).
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4), aligned(4)));
 struct __attribute__((aligned(4))) u32x4a {
     uint32_t x, y, z, w;
 };
@@ -937,7 +939,7 @@ struct ChunkRing {
     uint32_t d[PF + 1][17];
 };
 
-template <int Q, int PF>
+template <int Q, int PF, bool NT = false>
 __global__ __launch_bounds__(1024) void crc_frames_kernel5(FrameArgs a) {
     constexpr int S = 64;
     constexpr int64_t W = (int64_t)Q * S;
@@ -991,11 +993,19 @@ __global__ __launch_bounds__(1024) void crc_frames_kernel5(FrameArgs a) {
             if (act) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
-                    const u32x4a v = *reinterpret_cast<const u32x4a*>(a.buf + b0 + 16 * q);
-                    dd[4 * q] = v.x;
-                    dd[4 * q + 1] = v.y;
-                    dd[4 * q + 2] = v.z;
-                    dd[4 * q + 3] = v.w;
+                    if (NT) {
+                        const u32x4v v = __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(a.buf + b0 + 16 * q));
+                        dd[4 * q] = v.x;
+                        dd[4 * q + 1] = v.y;
+                        dd[4 * q + 2] = v.z;
+                        dd[4 * q + 3] = v.w;
+                    } else {
+                        const u32x4a v = *reinterpret_cast<const u32x4a*>(a.buf + b0 + 16 * q);
+                        dd[4 * q] = v.x;
+                        dd[4 * q + 1] = v.y;
+                        dd[4 * q + 2] = v.z;
+                        dd[4 * q + 3] = v.w;
+                    }
                 }
                 dd[16] = *reinterpret_cast<const uint32_t*>(a.buf + b0 + 64);
             } else {
@@ -1309,6 +1319,8 @@ constexpr Variant kVariants[] = {
     {16, 128, true},   // 18: v7 (v5 with 128-byte lane chunks, 2 KiB windows), prefetch 1
     {16, 128, true},   // 19: v7, prefetch 2
     {8, 128, true},    // 20: v7, 8 lanes x 128 B = 1 KiB windows, prefetch 1
+    {16, 64, true},    // 21: v5 (15) with non-temporal 16-byte loads, prefetch 2
+    {16, 64, true},    // 22: v5 with non-temporal loads, prefetch 1
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
@@ -1327,8 +1339,8 @@ int launch_variant(rh_ctx* ctx, const FrameArgs& fa, hipStream_t stream) {
     void (*kern)(FrameArgs);
     if constexpr (V == 7)
         kern = crc_frames_kernel7<Q, S, ILP>;
-    else if constexpr (V == 5)
-        kern = crc_frames_kernel5<Q, ILP>;  // ILP carries the prefetch depth for v5
+    else if constexpr (V == 5 || V == 8)
+        kern = crc_frames_kernel5<Q, ILP, V == 8>;  // ILP carries the prefetch depth; 8 = NT loads
     else if constexpr (V == 4)
         kern = crc_frames_kernel4<Q, ILP, REPL>;
     else if constexpr (V == 3)
@@ -1430,6 +1442,8 @@ int rh_crc_launch_variant(rh_ctx* ctx, const rh_frames* f, uint32_t flags, int v
         case 18: return launch_variant<16, 128, true, 7, 1>(ctx, a, stream);
         case 19: return launch_variant<16, 128, true, 7, 2>(ctx, a, stream);
         case 20: return launch_variant<8, 128, true, 7, 1>(ctx, a, stream);
+        case 21: return launch_variant<16, 64, true, 8, 2>(ctx, a, stream);
+        case 22: return launch_variant<16, 64, true, 8, 1>(ctx, a, stream);
     }
     return rh::fail(RH_E_INVAL, "unknown CRC kernel variant");
 }

@@ -90,7 +90,13 @@ __device__ __forceinline__ void lease_one(const rh_lease_soa& t, const int64_t (
 // One wave = 128 groups, lane l holds groups 2l and 2l+1: every column is one 16-byte load per
 // lane (VEC; needs an even col_stride and 16-byte aligned columns) and the two ballots of the
 // wave interleave into its two bit words.
-template <int F, bool VEC>
+template <bool NT, typename V>
+__device__ __forceinline__ V lease_ld(const V* p) {
+    if (NT) return __builtin_nontemporal_load(p);
+    return *p;
+}
+
+template <int F, bool VEC, bool NT>
 __device__ __forceinline__ void lease_wave(const rh_lease_soa& t, uint64_t wbase) {
     const int lane = threadIdx.x & 63;
     const uint64_t r0 = wbase + 2 * (uint64_t)lane;
@@ -101,12 +107,12 @@ __device__ __forceinline__ void lease_wave(const rh_lease_soa& t, uint64_t wbase
     if (VEC && in1) {
 #pragma unroll
         for (int k = 0; k < F; ++k) {
-            const v2i64 x = *reinterpret_cast<const v2i64*>(t.follower_ts + (uint64_t)k * t.col_stride + r0);
+            const v2i64 x = lease_ld<NT>(reinterpret_cast<const v2i64*>(t.follower_ts + (uint64_t)k * t.col_stride + r0));
             ts0[k] = x.x;
             ts1[k] = x.y;
         }
-        const v2u32 c = *reinterpret_cast<const v2u32*>(t.conf + r0);
-        const v2i64 li = *reinterpret_cast<const v2i64*>(t.lease_in + r0);
+        const v2u32 c = lease_ld<NT>(reinterpret_cast<const v2u32*>(t.conf + r0));
+        const v2i64 li = lease_ld<NT>(reinterpret_cast<const v2i64*>(t.lease_in + r0));
         w0 = c.x;
         w1 = c.y;
         l0 = li.x;
@@ -161,20 +167,25 @@ struct LeaseLaunch {
     int n_tiers;
 };
 
-template <int F, int FHI>
+template <int F, int FHI, bool NT>
 __device__ __forceinline__ void lease_dispatch(const rh_lease_soa& t, bool vec, uint64_t wbase) {
     if constexpr (F <= FHI) {
         if ((int)t.n_followers == F) {
-            if (vec) lease_wave<F, true>(t, wbase);
-            else lease_wave<F, false>(t, wbase);
+            if (vec) lease_wave<F, true, NT>(t, wbase);
+            else lease_wave<F, false, NT>(t, wbase);
         } else {
-            lease_dispatch<F + 1, FHI>(t, vec, wbase);
+            lease_dispatch<F + 1, FHI, NT>(t, vec, wbase);
         }
     }
 }
 
-template <int FLO, int FHI>
-__global__ __launch_bounds__(kLeaseBlock) void lease_kernel(LeaseLaunch a) {
+// Variants (rh_lease_set_variant): 0 plain loads; 1 non-temporal loads; 2 non-temporal loads
+// with the register budget pinned to 8 waves/SIMD; 3 plain loads, 8 waves/SIMD.
+int g_lease_variant = 2;  // fastest measured
+constexpr int kNumLeaseVariants = 4;
+
+template <int FLO, int FHI, bool NT, int MINW>
+__global__ __launch_bounds__(kLeaseBlock) __attribute__((amdgpu_waves_per_eu(MINW, 8))) void lease_kernel(LeaseLaunch a) {
     const uint64_t b = blockIdx.x;
     int k = 0;
 #pragma unroll
@@ -183,7 +194,7 @@ __global__ __launch_bounds__(kLeaseBlock) void lease_kernel(LeaseLaunch a) {
     const rh_lease_soa& t = a.t[k];
     const uint64_t wbase = ((b - a.first_block[k]) * kLeaseBlock / 64 + (threadIdx.x >> 6)) * 128;
     if (wbase >= t.n) return;
-    lease_dispatch<FLO, FHI>(t, (a.vec_mask >> k) & 1u, wbase);
+    lease_dispatch<FLO, FHI, NT>(t, (a.vec_mask >> k) & 1u, wbase);
 }
 
 constexpr uint64_t kGroupsPerBlock = kLeaseBlock / 64 * 128;
@@ -207,8 +218,17 @@ int launch_class(const rh_lease_soa* tiers, int n_tiers, int flo, int fhi, hipSt
     if (a.n_tiers == 0) return RH_OK;
     a.first_block[a.n_tiers] = blocks;
     if (blocks > 0x7fffffffull) return rh::fail(RH_E_RANGE, "rh_lease_soa_launch: too many groups");
-    if (flo == 0) hipLaunchKernelGGL((lease_kernel<0, 7>), dim3((uint32_t)blocks), dim3(kLeaseBlock), 0, stream, a);
-    else hipLaunchKernelGGL((lease_kernel<8, 14>), dim3((uint32_t)blocks), dim3(kLeaseBlock), 0, stream, a);
+    const dim3 g((uint32_t)blocks), b(kLeaseBlock);
+    if (flo != 0)
+        hipLaunchKernelGGL((lease_kernel<8, 14, false, 1>), g, b, 0, stream, a);
+    else if (g_lease_variant == 1)
+        hipLaunchKernelGGL((lease_kernel<0, 7, true, 1>), g, b, 0, stream, a);
+    else if (g_lease_variant == 2)
+        hipLaunchKernelGGL((lease_kernel<0, 7, true, 8>), g, b, 0, stream, a);
+    else if (g_lease_variant == 3)
+        hipLaunchKernelGGL((lease_kernel<0, 7, false, 8>), g, b, 0, stream, a);
+    else
+        hipLaunchKernelGGL((lease_kernel<0, 7, false, 1>), g, b, 0, stream, a);
     RH_HIP(hipGetLastError());
     return RH_OK;
 }
@@ -232,5 +252,12 @@ int rh_lease_launch_impl(rh_ctx* ctx, const rh_lease_soa* tiers, int n_tiers, hi
     int rc = launch_class(tiers, n_tiers, 0, 7, stream);
     if (rc != RH_OK) return rc;
     return launch_class(tiers, n_tiers, 8, 14, stream);
+}
+
+int rh_lease_set_variant_impl(int v) {
+    if (v < 0 || v >= kNumLeaseVariants) return rh::fail(RH_E_INVAL, "unknown lease kernel variant");
+    g_lease_variant = v;
     return RH_OK;
 }
+
+int rh_lease_num_variants_impl() { return kNumLeaseVariants; }

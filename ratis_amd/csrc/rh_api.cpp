@@ -455,6 +455,10 @@ RH_EXPORT int rh_commit_set_variant(int variant) { return rh_commit_set_variant_
 
 RH_EXPORT int rh_crc32c_set_variant(int variant) { return rh_crc_set_default_variant(variant); }
 
+RH_EXPORT int rh_lease_num_variants(void) { return rh_lease_num_variants_impl(); }
+
+RH_EXPORT int rh_lease_set_variant(int variant) { return rh_lease_set_variant_impl(variant); }
+
 RH_EXPORT int rh_crc32c_frames_launch_variant(rh_ctx* ctx, const rh_frames* frames, uint32_t flags, int variant,
                                               void* stream) {
     if (!ctx) return rh::fail(RH_E_INVAL, "rh_crc32c_frames_launch_variant: ctx == NULL");

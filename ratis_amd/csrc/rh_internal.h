@@ -71,3 +71,5 @@ int rh_commit_num_variants_impl();
 int rh_segments_launch_impl(rh_ctx* ctx, const rh_segments* segs, hipStream_t stream);
 int rh_segments_set_variant_impl(int v);
 int rh_lease_launch_impl(rh_ctx* ctx, const rh_lease_soa* tiers, int n_tiers, hipStream_t stream);
+int rh_lease_set_variant_impl(int v);
+int rh_lease_num_variants_impl();

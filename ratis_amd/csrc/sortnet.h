@@ -71,3 +71,44 @@ __device__ __forceinline__ uint64_t spread32(uint64_t x) {
 }
 
 }  // namespace rh_bits
+
+namespace rh_sort {
+
+// Rank masks for order statistics without sorting (fewer live registers than a network on
+// copies, and one pass serves several member masks -- new and old conf of a joint group).
+// Bit j of less[i] is set iff element j precedes element i in the stable ascending order
+// (v[j] < v[i], or v[j] == v[i] and j < i).  For a member mask m, the member i with
+// popcount(less[i] & m) == r is the r-th smallest member: the same value Arrays.sort puts at
+// index r (ties are equal values, so the order among them does not matter).
+template <int N>
+__device__ __forceinline__ void rank_masks(const int64_t (&v)[N], uint32_t (&less)[N]) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) less[i] = 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+#pragma unroll
+        for (int j = i + 1; j < N; ++j) {
+            const bool jfirst = v[j] < v[i];
+            less[i] |= jfirst ? (1u << j) : 0u;
+            less[j] |= jfirst ? 0u : (1u << i);
+        }
+}
+
+// min / element of rank k / max of the members of m (m != 0, n = popcount(m), k < n).
+template <int N>
+__device__ __forceinline__ void select_ranks(const int64_t (&v)[N], const uint32_t (&less)[N], uint32_t m,
+                                             int k, int n, int64_t& mn, int64_t& mk, int64_t& mx) {
+    mn = v[0];
+    mk = v[0];
+    mx = v[0];
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const bool in = (m >> i) & 1u;
+        const int r = __builtin_popcount(less[i] & m);
+        mn = (in && r == 0) ? v[i] : mn;
+        mk = (in && r == k) ? v[i] : mk;
+        mx = (in && r == n - 1) ? v[i] : mx;
+    }
+}
+
+}  // namespace rh_sort

@@ -17,7 +17,7 @@ def main():
     ap.add_argument("--segments", type=int, default=32)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
-    ap.add_argument("--only", default="crc,framing,commit", help="comma list of sections to run")
+    ap.add_argument("--only", default="crc,framing,commit,lease", help="comma list of sections to run")
     a = ap.parse_args()
     import torch
 
@@ -131,12 +131,50 @@ def main():
             torch.cuda.synchronize()
             ms = e0.elapsed_time(e1) / 40
             cres[v].append(alg / (ms * 1e-3) / 1e9)
-    _lib.check(lib.rh_commit_set_variant(0))
+    _lib.check(lib.rh_commit_set_variant(14))
     for v in range(ncv):
         x = np.array(cres[v])
         print(json.dumps({"kernel": "commit", "variant": v, "median_GBps": round(float(np.median(x)), 1),
                           "min_GBps": round(float(x.min()), 1), "max_GBps": round(float(x.max()), 1),
                           "median_Gupd_s": round(float(np.median(x)) * 1e9 / alg * 1e6 / 1e9, 2)}))
+    del batches
+    # lease kernel variants over 8 rotating 1M-group batches (same groups and confs)
+    if "lease" in only:
+        now, ms, tmo = 1 << 60, 1_000_000, 100
+        rng = np.random.default_rng(5)
+        lb = []
+        lalg = 0
+        for r in range(8):
+            tiers = []
+            for h in host:
+                ts = now - rng.integers(-ms, 3 * tmo * ms, size=h.follower.shape, dtype=np.int64)
+                lin = now - rng.integers(0, 2 * tmo * ms, size=h.n, dtype=np.int64)
+                if r == 0:
+                    lalg += ts.size * 8 + h.n * 4 + h.n * 16 + 2 * ((h.n + 63) // 64) * 8
+                t = engine.LeaseTier(follower_ts=torch.from_numpy(ts).cuda(),
+                                     conf=torch.from_numpy(h.conf.view(np.int32)).cuda(),
+                                     lease_in=torch.from_numpy(lin).cuda())
+                tiers.append(t.alloc_outputs())
+            lb.append(tiers)
+        nlv = lib.rh_lease_num_variants()
+        lres = {v: [] for v in range(nlv)}
+        for r in range(a.rounds):
+            for v in range(nlv):
+                _lib.check(lib.rh_lease_set_variant(v))
+                for i in range(8):
+                    engine.lease_launch(ctx, lb[i], now, tmo)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for i in range(40):
+                    engine.lease_launch(ctx, lb[i % 8], now, tmo)
+                e1.record()
+                torch.cuda.synchronize()
+                lres[v].append(lalg / (e0.elapsed_time(e1) / 40 * 1e-3) / 1e9)
+        _lib.check(lib.rh_lease_set_variant(2))
+        for v in range(nlv):
+            x = np.array(lres[v])
+            print(json.dumps({"kernel": "lease", "variant": v, "median_GBps": round(float(np.median(x)), 1),
+                              "min_GBps": round(float(x.min()), 1), "max_GBps": round(float(x.max()), 1)}))
     ctx.close()
 
 

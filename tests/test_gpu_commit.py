@@ -81,7 +81,7 @@ def _random_case(rng, F, n, lo=-1, hi=60, full_masks=False):
     return follower, flush, conf, commit, ts
 
 
-@pytest.mark.parametrize("commit_variant", [0, 3, 4], indirect=True)
+@pytest.mark.parametrize("commit_variant", [0, 3, 4, 8, 9, 10, 11, 12, 13, 14, 15], indirect=True)
 @pytest.mark.parametrize("F", list(range(1, 15)))
 def test_every_follower_width(ctx, orc, F, commit_variant):
     rng = np.random.default_rng(100 + F)
@@ -155,10 +155,10 @@ def commit_variant(request):
     _lib.check(lib.rh_commit_set_variant(DEFAULT_COMMIT_VARIANT))
 
 
-DEFAULT_COMMIT_VARIANT = 0
+DEFAULT_COMMIT_VARIANT = 14
 
 
-@pytest.mark.parametrize("commit_variant", list(range(8)), indirect=True)
+@pytest.mark.parametrize("commit_variant", list(range(16)), indirect=True)
 def test_fused_multi_tier_launch_and_compaction(ctx, orc, commit_variant):
     import torch
 

@@ -57,8 +57,21 @@ def assert_same(ref, got):
     assert np.array_equal(ext, ref["extended_bits"])
 
 
+@pytest.fixture
+def lease_variant(request):
+    from ratis_amd import _lib
+    lib = _lib.load()
+    _lib.check(lib.rh_lease_set_variant(request.param))
+    yield request.param
+    _lib.check(lib.rh_lease_set_variant(DEFAULT_LEASE_VARIANT))
+
+
+DEFAULT_LEASE_VARIANT = 2
+
+
+@pytest.mark.parametrize("lease_variant", [0, 1, 2, 3], indirect=True)
 @pytest.mark.parametrize("F", list(range(0, 15)))
-def test_lease_every_follower_count(ctx, orc, F):
+def test_lease_every_follower_count(ctx, orc, F, lease_variant):
     rng = np.random.default_rng(1000 + F)
     n = 20_000 + F * 37          # not a multiple of 64
     ts, conf, lease_in = random_lease_tier(rng, n, F)
