@@ -72,6 +72,126 @@ def load_pmc(path):
         return {}
 
 
+def cpu_threads() -> int:
+    """Threads for the all-core CPU baseline: this process's CPU affinity, capped at the 16-CPU
+    share a one-GPU box gives a job (nproc there shows the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def host_cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def timed_passes(items, fn, seconds: float) -> dict:
+    """Runs fn(*item) repeatedly on one thread per item for `seconds`; fn returns the units one
+    pass processed.  Returns the aggregate units/s over the wall time of all threads."""
+    import threading
+    units = [0] * len(items)
+    passes = [0] * len(items)
+    t0 = time.perf_counter()
+    stop = t0 + seconds
+
+    def run(i):
+        while time.perf_counter() < stop:
+            units[i] += fn(*items[i])
+            passes[i] += 1
+    th = [threading.Thread(target=run, args=(i,)) for i in range(len(items))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    dt = time.perf_counter() - t0
+    return {"rate": sum(units) / dt, "passes": sum(passes), "seconds": dt}
+
+
+def delta_streaming(ctx, host, steps: int = 6) -> dict:
+    """The operating mode the Java module uses: resident RaftGroupTables (one per follower-slot
+    width), FollowerInfo/flush-index updates written in place into the pinned delta ring
+    (rh_deltas_acquire/submit: H2D + device updateToMax), then rh_commit_batch (kernel + D2H of
+    the advanced (slot, commit) list).  One step = one delta per group (90 % follower matchIndex,
+    10 % leader flushIndex) + one batched updateCommit over every group.  Wall-clock per step,
+    host fill of the pinned ring included; the fill alone is reported too."""
+    from ratis_amd import _lib, groups
+    rng = np.random.default_rng(99)
+    tabs, batches = [], []
+    for h in host:
+        F, n = h.follower.shape
+        tab = groups.RaftGroupTable(ctx, capacity=n, n_followers=F)
+        tab.load(0, n, match=h.follower, flush=h.flush, commit=h.commit, term_start=h.term_start, conf=h.conf)
+        tabs.append(tab)
+        per = []
+        for s in range(steps + 1):
+            d = np.zeros(n, dtype=groups.RaftGroupTable.DELTA_DTYPE)
+            d["slot"] = rng.permutation(n)
+            is_flush = rng.random(n) < 0.10
+            col = rng.integers(0, F, size=n)
+            d["column"] = np.where(is_flush, _lib.RH_COL_FLUSH, col)
+            cur = np.where(is_flush, h.flush[d["slot"]], h.follower[col, d["slot"]])
+            d["value"] = cur + (s + 1) * 512
+            per.append(d)
+        batches.append(per)
+
+    import ctypes
+
+    import torch
+    lib = _lib.load()
+    # pinned result buffers: rh_commit_batch copies the advanced (slot, commit) list into them
+    outs = [(torch.empty(h.n, dtype=torch.int64).pin_memory(), torch.empty(h.n, dtype=torch.int64).pin_memory())
+            for h in host]
+
+    def fill(s):
+        for tab, per in zip(tabs, batches):
+            ring = tab.acquire_deltas()
+            d = per[s]
+            ring.view(np.uint8)[: d.nbytes] = d.view(np.uint8)   # the producer's writes into the ring
+            tab.submit_deltas(d.size)
+
+    def commit():
+        adv = 0
+        cnt = ctypes.c_size_t()
+        for tab, (o_slot, o_commit) in zip(tabs, outs):
+            _lib.check(lib.rh_commit_batch(tab.handle, o_slot.data_ptr(), o_commit.data_ptr(), o_slot.numel(),
+                                           ctypes.byref(cnt), None))
+            adv += cnt.value
+        return adv
+
+    fill(0)
+    commit()  # warm-up
+    t0 = time.perf_counter()
+    advanced = 0
+    for s in range(1, steps + 1):
+        fill(s)
+        advanced += commit()
+    dt = (time.perf_counter() - t0) / steps
+    # the host fill alone (memcpy of one step's deltas into the pinned slots, nothing submitted)
+    f0 = time.perf_counter()
+    for tab, per in zip(tabs, batches):
+        ring = tab.acquire_deltas()
+        ring.view(np.uint8)[: per[0].nbytes] = per[0].view(np.uint8)
+        tab.submit_deltas(0)
+    fill_s = time.perf_counter() - f0
+    n_groups = sum(h.n for h in host)
+    for tab in tabs:
+        tab.close()
+    return {"commit_updates_per_s_incl_pcie": round(n_groups / dt, 1), "ms_per_step": round(dt * 1e3, 3),
+            "deltas_per_step": n_groups, "delta_bytes_h2d_per_step": n_groups * 24,
+            "host_fill_ms_per_step": round(fill_s * 1e3, 3),
+            "commit_updates_per_s_excl_host_fill": round(n_groups / (dt - fill_s), 1) if dt > fill_s else None,
+            "advanced_per_step": round(advanced / steps, 1),
+            "path": "rh_deltas_acquire/submit (pinned ring, H2D + updateToMax kernel) + rh_commit_batch "
+                    "(commit kernel + D2H of the advanced list), tables F=4 and F=6"}
+
+
 def main():
     args = parse()
     import torch
@@ -211,7 +331,8 @@ def main():
         ms = pa.elapsed_time(pb) / reps
         pcie["commit_updates_per_s_incl_pcie"] = round(n_mine / (ms * 1e-3), 1)
         pcie["commit_ms_incl_pcie_full_snapshot"] = round(ms, 4)
-        pcie["note"] = "full snapshot H2D (pinned) + kernel + commit D2H per batch; delta streaming moves less"
+        pcie["note"] = "full snapshot H2D (pinned) + kernel + commit D2H per batch"
+        pcie["delta_streaming"] = delta_streaming(ctx, host)
 
     # ------------------------------------------------------------------ CRC32C (config 5)
     crc = {}
@@ -392,19 +513,29 @@ def main():
         del lbatches
 
     # ------------------------------------------------------------------ CPU baseline (rank 0, N = 1)
+    # The oracle (scalar C restatement of the reference's Java arithmetic), timed on this host on a
+    # bounded sample: once on 1 thread, once on every core of this job's CPU share (ctypes drops the
+    # GIL, so Python threads run the C passes in parallel over static slices).
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        threads = cpu_threads()
         h = host[0]
-        reps = 0
-        tc = time.perf_counter()
-        while time.perf_counter() - tc < 5.0:
-            orc.commit_soa(h.follower, h.flush, h.conf, mode=0, gap=args.gap, commit_in=h.commit,
-                           term_start=h.term_start)
-            reps += 1
-        cdt = time.perf_counter() - tc
-        cpu = {"value": round(h.n * reps / cdt, 1), "unit": "updates/s", "cores": 1, "kind": "port",
-               "sample": f"{reps} passes of orc_commit_soa over the {h.n}-group stable tier of the same "
-                         f"snapshot ({cdt:.1f} s, scalar C restatement of LeaderStateImpl/RaftLogBase, 1 thread)"}
+        parts = [slice(h.n * i // threads, h.n * (i + 1) // threads) for i in range(threads)]
+        items = [(np.ascontiguousarray(h.follower[:, p]), h.flush[p].copy(), h.conf[p].copy(), h.commit[p].copy(),
+                  h.term_start[p].copy()) for p in parts]
+
+        def commit_pass(f, s, c, ci, ts):
+            orc.commit_soa(f, s, c, mode=0, gap=args.gap, commit_in=ci, term_start=ts)
+            return s.size
+        one = timed_passes([(h.follower, h.flush, h.conf, h.commit, h.term_start)], commit_pass, 4.0)
+        allc = timed_passes(items, commit_pass, 4.0)
+        cpu = {"value": round(allc["rate"], 1), "unit": "updates/s", "cores": threads, "kind": "port",
+               "sample": f"{allc['passes']} passes of orc_commit_soa over {threads} static slices of the "
+                         f"{h.n}-group stable tier of the same snapshot ({allc['seconds']:.1f} s, scalar C "
+                         f"restatement of LeaderStateImpl/RaftLogBase, {threads} threads)",
+               "single_core": {"value": round(one["rate"], 1), "cores": 1,
+                               "sample": f"{one['passes']} passes over the whole tier ({one['seconds']:.1f} s)"},
+               "host": host_cpu_model()}
         if args.crc_segments > 0:
             rng = np.random.default_rng(5)
             nseg = 8
@@ -413,29 +544,35 @@ def main():
             offs = (np.repeat(np.arange(nseg) * (32 << 20), fps) + 8
                     + np.tile(np.arange(fps) * 4096, nseg)).astype(np.uint64)
             lens = np.full(offs.size, 4096, dtype=np.uint32)
-            reps = 0
-            tc = time.perf_counter()
-            while time.perf_counter() - tc < 5.0:
-                orc.crc32c_frames(sample, offs, lens)
-                reps += 1
-            cdt = time.perf_counter() - tc
-            cpu_crc = {"value": round(reps * offs.size * 4096 / cdt / 1e9, 3), "unit": "GB/s", "cores": 1,
-                       "kind": "port",
-                       "sample": f"{reps} passes over 8 x 32 MiB segment images ({offs.size} 4 KiB frames), "
-                                 "PureJavaCrc32C slicing-by-8 restatement, 1 thread"}
-            crc["cpu_baseline"] = cpu_crc
+
+            def crc_pass(o, ln):
+                orc.crc32c_frames(sample, o, ln)
+                return o.size * 4096
+            cparts = [slice(offs.size * i // threads, offs.size * (i + 1) // threads) for i in range(threads)]
+            one = timed_passes([(offs, lens)], crc_pass, 4.0)
+            allc = timed_passes([(offs[p].copy(), lens[p].copy()) for p in cparts], crc_pass, 4.0)
+            crc["cpu_baseline"] = {
+                "value": round(allc["rate"] / 1e9, 3), "unit": "GB/s", "cores": threads, "kind": "port",
+                "sample": f"{allc['passes']} slice passes over 8 x 32 MiB segment images ({offs.size} 4 KiB frames) "
+                          f"split across {threads} threads, PureJavaCrc32C slicing-by-8 restatement ({allc['seconds']:.1f} s)",
+                "single_core": {"value": round(one["rate"] / 1e9, 3), "cores": 1,
+                                "sample": f"{one['passes']} passes over the 8 images ({one['seconds']:.1f} s)"}}
         if lease_inputs:
             ts, conf, lin = lease_inputs[0]
-            reps = 0
-            tc = time.perf_counter()
-            while time.perf_counter() - tc < 3.0:
-                orc.lease_soa(ts, conf, lin, 1 << 60, 100)
-                reps += 1
-            cdt = time.perf_counter() - tc
-            lease["cpu_baseline"] = {"value": round(conf.size * reps / cdt, 1), "unit": "checks/s", "cores": 1,
-                                     "kind": "port",
-                                     "sample": f"{reps} passes of orc_lease_soa over the {conf.size}-group stable "
-                                               f"tier ({cdt:.1f} s, literal LeaderLease restatement, 1 thread)"}
+            lparts = [slice(conf.size * i // threads, conf.size * (i + 1) // threads) for i in range(threads)]
+
+            def lease_pass(t, c, li):
+                orc.lease_soa(t, c, li, 1 << 60, 100)
+                return c.size
+            one = timed_passes([(ts, conf, lin)], lease_pass, 3.0)
+            allc = timed_passes([(np.ascontiguousarray(ts[:, p]), conf[p].copy(), lin[p].copy()) for p in lparts],
+                                lease_pass, 3.0)
+            lease["cpu_baseline"] = {
+                "value": round(allc["rate"], 1), "unit": "checks/s", "cores": threads, "kind": "port",
+                "sample": f"{allc['passes']} slice passes of orc_lease_soa over the {conf.size}-group stable tier "
+                          f"split across {threads} threads ({allc['seconds']:.1f} s, literal LeaderLease restatement)",
+                "single_core": {"value": round(one["rate"], 1), "cores": 1,
+                                "sample": f"{one['passes']} passes over the whole tier ({one['seconds']:.1f} s)"}}
 
     stats = shard.allreduce_stats({"groups_evaluated": n_mine * args.steps, "commits_advanced": advanced,
                                    "frames_verified": frames_verified, "bytes_verified": bytes_verified,

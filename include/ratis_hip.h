@@ -169,8 +169,20 @@ int rh_groups_load(rh_groups* g, uint64_t first, uint64_t n, const int64_t* matc
                    const int64_t* fcommit, const int64_t* flush, const int64_t* commit,
                    const int64_t* term_start, const uint32_t* conf);
 /* Copies deltas through a pinned staging ring and applies them on the device (monotone max,
- * exactly RaftLogIndex.updateToMax).  Thread-safe. */
+ * exactly RaftLogIndex.updateToMax).  Returns once the caller's buffer may be reused; the
+ * device work is ordered before the next rh_commit_batch / rh_watch_levels.  Thread-safe. */
 int rh_push_deltas(rh_groups* g, const rh_delta* deltas, size_t n);
+
+/* Zero-copy producer path over the same staging ring (two pinned slots of RH_DELTA_SLOT deltas):
+ * rh_deltas_acquire hands out the next slot to fill in place (waiting until its previous H2D
+ * has completed); rh_deltas_submit enqueues the H2D of its first n deltas and the device apply,
+ * and returns without waiting, so the producer fills the other slot while this one is in flight.
+ * One acquire/submit pair at a time per table.  Unlike rh_push_deltas, submitted deltas are not
+ * validated on the host: a delta with slot >= capacity or an unknown column is ignored by the
+ * device. */
+#define RH_DELTA_SLOT (1u << 20)
+int rh_deltas_acquire(rh_groups* g, rh_delta** out_buf, size_t* out_cap);
+int rh_deltas_submit(rh_groups* g, size_t n);
 /* RH_MODE_COMMIT: runs updateCommit for every active group, stores advanced commit indices in
  * the table, and returns (slot, new commit) of the groups that advanced, up to `cap`.
  * out_min (optional, host [capacity]) receives the watch-ALL level of every group.
@@ -216,6 +228,14 @@ int rh_crc32c_frames_launch(rh_ctx* ctx, const rh_frames* frames, uint32_t flags
 int rh_crc32c_verify_host(rh_ctx* ctx, const uint8_t* seg, uint64_t seg_len, const uint64_t* frame_off,
                           const uint32_t* frame_len, uint64_t n, uint32_t* crc_out, uint64_t* bad_bits,
                           uint64_t* n_bad);
+
+/* Checksum.update over one host span (PJC:54-91 update(byte[], off, len)): crc_state is the
+ * PureJavaCrc32C `crc` field before the call (0xFFFFFFFF after reset()); *out_state receives it
+ * after, so getValue() = ~*out_state.  The span is staged through the context's device scratch
+ * and folded by the frame kernel (synchronous).  For per-entry call sites prefer batching frames
+ * through rh_crc32c_frames_launch (RH_CRC_STAMP / RH_CRC_VERIFY); this entry serves the odd
+ * single span (e.g. a snapshot-file checksum). */
+int rh_crc32c(rh_ctx* ctx, uint32_t crc_state, const void* data, uint64_t n, uint32_t* out_state);
 
 /* ---- leader lease (LeaderStateImpl.hasLease LSI:1229-1249; LeaderLease LL:60-103) ------------
  * One tier = groups with the same follower-slot count F (0..14), same conf word as the commit

@@ -166,10 +166,13 @@ _SIGNATURES = {
     "rh_groups_load": (c_int, [c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p,
                                c_void_p, c_void_p]),
     "rh_push_deltas": (c_int, [c_void_p, POINTER(RhDelta), c_size_t]),
+    "rh_deltas_acquire": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_size_t)]),
+    "rh_deltas_submit": (c_int, [c_void_p, c_size_t]),
     "rh_commit_batch": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, POINTER(c_size_t), c_void_p]),
     "rh_watch_levels": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
     "rh_groups_read_commit": (c_int, [c_void_p, c_uint64, c_uint64, c_void_p]),
     "rh_crc32c_frames_launch": (c_int, [c_void_p, POINTER(RhFrames), c_uint32, c_void_p]),
+    "rh_crc32c": (c_int, [c_void_p, c_uint32, c_void_p, c_uint64, POINTER(c_uint32)]),
     "rh_crc32c_verify_host": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_uint64, c_void_p,
                                       c_void_p, POINTER(c_uint64)]),
     "rh_lease_soa_launch": (c_int, [c_void_p, POINTER(RhLeaseSoa), c_int, c_void_p]),

@@ -68,9 +68,14 @@ struct rh_groups {
     uint64_t* adv_rows = nullptr;
     int64_t* adv_commit = nullptr;
     unsigned long long* adv_count = nullptr;
-    // delta staging
+    // delta staging: two pinned host slots (the producer fills one while the other's H2D is in
+    // flight) and one device buffer (stream order serialises H2D -> apply -> next H2D)
     std::mutex mu;
-    rh_delta* h_deltas = nullptr;  // pinned
+    rh_delta* h_ring[2] = {nullptr, nullptr};
+    hipEvent_t ring_free[2] = {nullptr, nullptr};  // recorded after the slot's H2D
+    bool ring_used[2] = {false, false};
+    int ring_next = 0;
+    int ring_acquired = -1;                        // slot handed out by rh_deltas_acquire
     rh_delta* d_deltas = nullptr;
     size_t delta_cap = 0;
 };
@@ -182,7 +187,27 @@ void free_groups(rh_groups* g) {
     (void)hipFree(g->adv_commit);
     (void)hipFree(g->adv_count);
     (void)hipFree(g->d_deltas);
-    if (g->h_deltas) (void)hipHostFree(g->h_deltas);
+    for (int i = 0; i < 2; ++i) {
+        if (g->h_ring[i]) (void)hipHostFree(g->h_ring[i]);
+        if (g->ring_free[i]) (void)hipEventDestroy(g->ring_free[i]);
+    }
+}
+
+// Waits until ring slot i may be overwritten (its previous H2D has completed).
+int ring_wait(rh_groups* g, int i) {
+    if (g->ring_used[i]) RH_HIP(hipEventSynchronize(g->ring_free[i]));
+    return RH_OK;
+}
+
+// Enqueues H2D of the first n deltas of slot i and the device apply; does not wait.
+int ring_submit(rh_groups* g, int i, size_t n) {
+    hipStream_t s = g->ctx->stream;
+    RH_HIP(hipMemcpyAsync(g->d_deltas, g->h_ring[i], n * sizeof(rh_delta), hipMemcpyHostToDevice, s));
+    RH_HIP(hipEventRecord(g->ring_free[i], s));
+    g->ring_used[i] = true;
+    g->ring_next = i ^ 1;
+    return rh_apply_deltas_impl(s, g->d_deltas, n, g->capacity, g->stride, g->nf, g->match, g->fcommit, g->flush,
+                                g->commit);
 }
 
 // Fills n int64 with `v` on `s` (hipMemsetD32-free: a tiny kernel is overkill, use a host pattern).
@@ -237,11 +262,13 @@ RH_EXPORT int rh_groups_create(rh_ctx* ctx, uint64_t capacity, uint32_t n_follow
     if (rc == RH_OK) rc = dalloc(&g->adv_rows, S);
     if (rc == RH_OK) rc = dalloc(&g->adv_commit, S);
     if (rc == RH_OK) rc = dalloc(&g->adv_count, 1);
-    g->delta_cap = 1u << 16;
+    g->delta_cap = RH_DELTA_SLOT;
     if (rc == RH_OK) rc = dalloc(&g->d_deltas, g->delta_cap);
-    if (rc == RH_OK) {
-        hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&g->h_deltas), g->delta_cap * sizeof(rh_delta));
+    for (int i = 0; i < 2 && rc == RH_OK; ++i) {
+        hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&g->h_ring[i]), g->delta_cap * sizeof(rh_delta));
         if (e != hipSuccess) rc = rh::fail(RH_E_NOMEM, "hipHostMalloc(delta staging)");
+        if (rc == RH_OK && hipEventCreateWithFlags(&g->ring_free[i], hipEventDisableTiming) != hipSuccess)
+            rc = rh::fail(RH_E_DEVICE, "hipEventCreate(delta staging)");
     }
     hipStream_t s = ctx->stream;
     // every index starts at INVALID_LOG_INDEX (-1), every slot inactive (conf 0)
@@ -320,18 +347,45 @@ RH_EXPORT int rh_push_deltas(rh_groups* g, const rh_delta* deltas, size_t n) {
     }
     DeviceGuard dg(g->ctx->device);
     std::lock_guard<std::mutex> lk(g->mu);
-    hipStream_t s = g->ctx->stream;
+    if (g->ring_acquired >= 0) return rh::fail(RH_E_STATE, "rh_push_deltas: a staging slot is acquired");
     for (size_t done = 0; done < n;) {
         const size_t m = std::min(n - done, g->delta_cap);
-        std::memcpy(g->h_deltas, deltas + done, m * sizeof(rh_delta));
-        RH_HIP(hipMemcpyAsync(g->d_deltas, g->h_deltas, m * sizeof(rh_delta), hipMemcpyHostToDevice, s));
-        int rc = rh_apply_deltas_impl(s, g->d_deltas, m, g->capacity, g->stride, g->nf, g->match, g->fcommit,
-                                      g->flush, g->commit);
+        const int i = g->ring_next;
+        int rc = ring_wait(g, i);
+        if (rc == RH_OK) {
+            std::memcpy(g->h_ring[i], deltas + done, m * sizeof(rh_delta));
+            rc = ring_submit(g, i, m);
+        }
         if (rc != RH_OK) return rc;
-        RH_HIP(hipStreamSynchronize(s));  // staging buffer is reused by the next chunk
         done += m;
     }
     return RH_OK;
+}
+
+RH_EXPORT int rh_deltas_acquire(rh_groups* g, rh_delta** out_buf, size_t* out_cap) {
+    if (!g || !out_buf || !out_cap) return rh::fail(RH_E_INVAL, "rh_deltas_acquire: NULL argument");
+    DeviceGuard dg(g->ctx->device);
+    std::lock_guard<std::mutex> lk(g->mu);
+    if (g->ring_acquired >= 0) return rh::fail(RH_E_STATE, "rh_deltas_acquire: a slot is already acquired");
+    const int i = g->ring_next;
+    int rc = ring_wait(g, i);
+    if (rc != RH_OK) return rc;
+    g->ring_acquired = i;
+    *out_buf = g->h_ring[i];
+    *out_cap = g->delta_cap;
+    return RH_OK;
+}
+
+RH_EXPORT int rh_deltas_submit(rh_groups* g, size_t n) {
+    if (!g) return rh::fail(RH_E_INVAL, "rh_deltas_submit: groups == NULL");
+    DeviceGuard dg(g->ctx->device);
+    std::lock_guard<std::mutex> lk(g->mu);
+    const int i = g->ring_acquired;
+    if (i < 0) return rh::fail(RH_E_STATE, "rh_deltas_submit: no slot acquired");
+    if (n > g->delta_cap) return rh::fail(RH_E_INVAL, "rh_deltas_submit: n exceeds the slot capacity");
+    g->ring_acquired = -1;
+    if (n == 0) return RH_OK;
+    return ring_submit(g, i, n);
 }
 
 namespace {
@@ -464,6 +518,50 @@ RH_EXPORT int rh_crc32c_frames_launch_variant(rh_ctx* ctx, const rh_frames* fram
     if (!ctx) return rh::fail(RH_E_INVAL, "rh_crc32c_frames_launch_variant: ctx == NULL");
     DeviceGuard g(ctx->device);
     return rh_crc_launch_variant(ctx, frames, flags, variant, pick_stream(ctx, stream));
+}
+
+RH_EXPORT int rh_crc32c(rh_ctx* ctx, uint32_t crc_state, const void* data, uint64_t n, uint32_t* out_state) {
+    if (!ctx || !out_state) return rh::fail(RH_E_INVAL, "rh_crc32c: ctx/out_state == NULL");
+    if (n && !data) return rh::fail(RH_E_INVAL, "rh_crc32c: data == NULL");
+    if (n > 0x7FFFFFFFull) return rh::fail(RH_E_RANGE, "rh_crc32c: span longer than 2^31 - 1 (Java int length)");
+    *out_state = crc_state;
+    if (n == 0) return RH_OK;
+    DeviceGuard g(ctx->device);
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    const size_t o_len = (n + 255) / 256 * 256, total = o_len + 256;
+    if (ctx->scratch_bytes < total) {
+        (void)hipFree(ctx->d_scratch);
+        ctx->d_scratch = nullptr;
+        ctx->scratch_bytes = 0;
+        hipError_t e = hipMalloc(&ctx->d_scratch, total);
+        if (e != hipSuccess) return rh::fail(RH_E_NOMEM, "rh_crc32c: device scratch");
+        ctx->scratch_bytes = total;
+    }
+    uint8_t* base = static_cast<uint8_t*>(ctx->d_scratch);
+    hipStream_t s = ctx->stream;
+    // frame table of one span: offset 0 (8 B), length n (4 B), crc out (4 B)
+    struct {
+        uint64_t off;
+        uint32_t len;
+        uint32_t crc;
+    } hdr{0, (uint32_t)n, 0};
+    RH_HIP(hipMemcpyAsync(base, data, n, hipMemcpyHostToDevice, s));
+    RH_HIP(hipMemcpyAsync(base + o_len, &hdr, sizeof(hdr), hipMemcpyHostToDevice, s));
+    rh_frames f{};
+    f.buf = base;
+    f.buf_len = n;
+    f.frame_off = reinterpret_cast<const uint64_t*>(base + o_len);
+    f.frame_len = reinterpret_cast<const uint32_t*>(base + o_len + 8);
+    f.n = 1;
+    f.init_state = crc_state;
+    f.crc_out = reinterpret_cast<uint32_t*>(base + o_len + 12);
+    int rc = rh_crc_launch_impl(ctx, &f, 0, s);
+    if (rc != RH_OK) return rc;
+    uint32_t value = 0;
+    RH_HIP(hipMemcpyAsync(&value, base + o_len + 12, 4, hipMemcpyDeviceToHost, s));
+    RH_HIP(hipStreamSynchronize(s));
+    *out_state = ~value;  // getValue() = ~crc
+    return RH_OK;
 }
 
 RH_EXPORT int rh_crc32c_verify_host(rh_ctx* ctx, const uint8_t* seg, uint64_t seg_len, const uint64_t* frame_off,

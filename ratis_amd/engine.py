@@ -270,6 +270,16 @@ def crc32c_bytes(ctx: Context, data: torch.Tensor, init_state: int = 0xFFFFFFFF)
     return int(fb.crc_out.item()) & 0xFFFFFFFF
 
 
+def crc32c_update(ctx: Context, state: int, data: bytes) -> int:
+    """``PureJavaCrc32C.update(byte[], 0, len)`` on the internal state through ``rh_crc32c`` (host span
+    staged to the device).  Returns the new state; ``getValue() = ~state & 0xFFFFFFFF``."""
+    lib = _lib.load()
+    buf = ctypes.create_string_buffer(bytes(data), max(1, len(data)))
+    out = ctypes.c_uint32()
+    check(lib.rh_crc32c(ctx.handle, state & 0xFFFFFFFF, buf, len(data), ctypes.byref(out)))
+    return out.value
+
+
 # ---- segment framing ---------------------------------------------------------------------------
 RH_SEG_E_CHECKSUM = -2   # read_segments only: the first frame whose CRC does not verify
 

@@ -105,6 +105,22 @@ class RaftGroupTable:
         ptr = arr.ctypes.data_as(ctypes.POINTER(RhDelta))
         check(self._lib.rh_push_deltas(self.handle, ptr, n))
 
+    DELTA_DTYPE = np.dtype([("slot", "<u8"), ("column", "<u4"), ("reserved", "<u4"), ("value", "<i8")])
+
+    def acquire_deltas(self) -> np.ndarray:
+        """Zero-copy producer path: the next pinned staging slot as a structured numpy array
+        (fields slot/column/reserved/value) to fill in place; hand it over with
+        :meth:`submit_deltas`.  The view is valid only until that call."""
+        ptr = ctypes.c_void_p()
+        cap = ctypes.c_size_t()
+        check(self._lib.rh_deltas_acquire(self.handle, ctypes.byref(ptr), ctypes.byref(cap)))
+        raw = (ctypes.c_uint8 * (cap.value * self.DELTA_DTYPE.itemsize)).from_address(ptr.value)
+        return np.frombuffer(raw, dtype=self.DELTA_DTYPE)
+
+    def submit_deltas(self, n: int) -> None:
+        """Enqueues H2D + device apply of the first ``n`` deltas of the acquired slot (async)."""
+        check(self._lib.rh_deltas_submit(self.handle, int(n)))
+
     def update_match_index(self, slots, follower_slot: int, values) -> None:
         self.push_deltas(slots, _lib.rh_col_match(follower_slot), values)
 

@@ -21,7 +21,7 @@ for V in ${CRC_VARIANTS:-15}; do
   run crc${V}_c "SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VMEM" --what crc --variant $V
   run crc${V}_w "WRITE_SIZE" --what crc --variant $V
 done
-for V in ${COMMIT_VARIANTS:-0}; do
+for V in ${COMMIT_VARIANTS:-14}; do
   run commit${V}_a "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD" --what commit --variant $V
   run commit${V}_b "FETCH_SIZE GRBM_GUI_ACTIVE" --what commit --variant $V
   run commit${V}_w "WRITE_SIZE" --what commit --variant $V

@@ -26,7 +26,7 @@ def main():
     ap.add_argument("pmc_dir")
     ap.add_argument("--out", default=None)
     ap.add_argument("--crc", default="crc15")
-    ap.add_argument("--commit", default="commit0")
+    ap.add_argument("--commit", default="commit14")
     a = ap.parse_args()
     out = {"source": a.pmc_dir, "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), WRITE_SIZE x1, KiB x1024"}
     for name, key, tag in (("crc", "crc_frames_kernel", a.crc), ("commit", "commit_kernel", a.commit),

@@ -106,6 +106,24 @@ def test_continuation_state_split_invariance(ctx, orc):
         assert engine.crc32c_bytes(ctx, _dev(data[:n]), init_state=st) == (~orc.crc32c_update(st, d)) & 0xFFFFFFFF
 
 
+def test_single_span_entry_rh_crc32c(ctx, orc):
+    """rh_crc32c (host span, Checksum.update semantics on the internal state) == the oracle's
+    PureJavaCrc32C.update, chained across calls; RFC 3720 answers through getValue()."""
+    from ratis_amd import engine
+    ref = json.load(open(os.path.join(HERE, "golden", "crc_reference.json")))
+    for v in ref["rfc3720"]:
+        st = engine.crc32c_update(ctx, 0xFFFFFFFF, bytes.fromhex(v["hex"]))
+        assert (~st) & 0xFFFFFFFF == int(v["crc"], 16), v["name"]
+    rng = np.random.default_rng(21)
+    data = rng.integers(0, 256, size=70000, dtype=np.uint8).tobytes()
+    st_gpu = st_orc = 0xFFFFFFFF
+    for a, b in ((0, 0), (0, 1), (1, 4), (4, 4100), (4100, 4100), (4100, 69999), (69999, 70000)):
+        st_gpu = engine.crc32c_update(ctx, st_gpu, data[a:b])
+        st_orc = orc.crc32c_update(st_orc, data[a:b])
+        assert st_gpu == st_orc, (a, b)
+    assert (~st_gpu) & 0xFFFFFFFF == orc.crc32c(data)
+
+
 def test_raftlog_readwrite_segment_stamp_and_verify(ctx, orc):
     """TestRaftLogReadWrite scenario: the GPU writer stamps the same CRCs the oracle writer does;
     the verifier accepts the segment, then flags the frame holding byte 100 after corruption."""
