@@ -299,6 +299,23 @@ typedef struct rh_segments {
 } rh_segments;
 
 int rh_segments_scan_launch(rh_ctx* ctx, const rh_segments* segs, void* stream);
+
+/* ---- fused read path (LogSegment.readSegmentFile, LogSegment.java:166-196) ----------------
+ * Framing walk + CRC32C verification of every frame (decodeEntry's checksum, RDR:327-336) in ONE
+ * pass over HBM: fills every rh_segments output exactly as rh_segments_scan_launch does, plus the
+ * per-frame CRCs and the reader's verdict per segment -- the reader stops at the first frame
+ * whose CRC does not verify (ChecksumException at that frame's offset). */
+#define RH_SEG_E_CHECKSUM  -2   /* a frame's stored CRC != computed (ChecksumException, RDR:330-336) */
+typedef struct rh_segments_crc {
+    uint32_t* scratch_crc;        /* [n_seg * frames_per_seg_cap] computed CRC (getValue()) per slot */
+    uint32_t* seg_ok;             /* [n_seg] frames the reader accepts: those before the first CRC failure */
+    int32_t*  seg_read_status;    /* [n_seg] RH_SEG_E_CHECKSUM if a frame failed, else seg_status     */
+    uint64_t* seg_read_stop;      /* [n_seg] offset (in the segment) of that frame, else seg_stop     */
+    uint32_t* crc_out;            /* [frame_cap] optional: computed CRC per frame, dense order        */
+    uint64_t* bad_bits;           /* [ceil(frame_cap/64)] optional: stored != computed (zeroed here) */
+    unsigned long long* n_bad;    /* optional: CRC mismatches over all found frames (added)          */
+} rh_segments_crc;
+int rh_segments_read_launch(rh_ctx* ctx, const rh_segments* segs, const rh_segments_crc* crc, void* stream);
 /* Framing kernel variant (identical results): 0 = one wave per segment, 16 KiB LDS window;
  * 1 / 2 = one 256-thread block per segment, double-buffered 32 / 64 KiB windows (default 1). */
 int rh_segments_set_variant(int variant);

@@ -122,6 +122,7 @@ class RhLeaseSoa(ctypes.Structure):
 RH_SEG_END = 1
 RH_SEG_PARTIAL = 2
 RH_SEG_E_OVERSIZE = -1
+RH_SEG_E_CHECKSUM = -2
 RH_SEG_E_PADDING = -3
 RH_SEG_E_VARINT = -4
 RH_SEG_E_HEADER = -5
@@ -147,6 +148,18 @@ class RhSegments(ctypes.Structure):
         ("seg_status", c_void_p),
         ("seg_stop", c_void_p),
         ("total_frames", c_void_p),
+    ]
+
+
+class RhSegmentsCrc(ctypes.Structure):
+    _fields_ = [
+        ("scratch_crc", c_void_p),
+        ("seg_ok", c_void_p),
+        ("seg_read_status", c_void_p),
+        ("seg_read_stop", c_void_p),
+        ("crc_out", c_void_p),
+        ("bad_bits", c_void_p),
+        ("n_bad", c_void_p),
     ]
 
 
@@ -178,6 +191,7 @@ _SIGNATURES = {
     "rh_lease_soa_launch": (c_int, [c_void_p, POINTER(RhLeaseSoa), c_int, c_void_p]),
     "rh_segments_scan_launch": (c_int, [c_void_p, POINTER(RhSegments), c_void_p]),
     "rh_segments_set_variant": (c_int, [c_int]),
+    "rh_segments_read_launch": (c_int, [c_void_p, POINTER(RhSegments), POINTER(RhSegmentsCrc), c_void_p]),
     "rh_crc32c_num_variants": (c_int, []),
     "rh_commit_num_variants": (c_int, []),
     "rh_commit_set_variant": (c_int, [c_int]),

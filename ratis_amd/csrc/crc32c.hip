@@ -1387,10 +1387,17 @@ int rh_crc_upload_tables(rh_ctx* ctx) {
         rh::build_crc_shift_table(1ull << m, reinterpret_cast<uint32_t(*)[256]>(sh.data() + (size_t)m * 1024));
     RH_HIP(hipMalloc(&ctx->d_shift, sh.size() * 4));
     RH_HIP(hipMemcpy(ctx->d_shift, sh.data(), sh.size() * 4, hipMemcpyHostToDevice));
-    uint32_t** dst[5] = {&ctx->d_lane16, &ctx->d_lane32, &ctx->d_lane64, &ctx->d_lane16_s128, &ctx->d_lane8_s128};
-    const int qs[5] = {16, 32, 64, 16, 8};
-    const int ss[5] = {64, 64, 64, 128, 128};
-    for (int i = 0; i < 5; ++i) {
+    uint32_t** dst[6] = {&ctx->d_lane16, &ctx->d_lane32, &ctx->d_lane64, &ctx->d_lane16_s128, &ctx->d_lane8_s128,
+                         &ctx->d_lane16_s36};
+    const int qs[6] = {16, 32, 64, 16, 8, 16};
+    const int ss[6] = {64, 64, 64, 128, 128, 36};
+    {
+        uint32_t zu[4][256];
+        rh::build_crc_shift_table(576, zu);
+        RH_HIP(hipMalloc(&ctx->d_zu576, sizeof(zu)));
+        RH_HIP(hipMemcpy(ctx->d_zu576, zu, sizeof(zu), hipMemcpyHostToDevice));
+    }
+    for (int i = 0; i < 6; ++i) {
         std::vector<uint32_t> lt = rh::build_crc_lane_tables(qs[i], ss[i]);
         RH_HIP(hipMalloc(dst[i], lt.size() * 4));
         RH_HIP(hipMemcpy(*dst[i], lt.data(), lt.size() * 4, hipMemcpyHostToDevice));

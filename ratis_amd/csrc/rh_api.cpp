@@ -136,6 +136,8 @@ RH_EXPORT int rh_shutdown(rh_ctx* ctx) {
     (void)hipFree(ctx->d_lane64);
     (void)hipFree(ctx->d_lane16_s128);
     (void)hipFree(ctx->d_lane8_s128);
+    (void)hipFree(ctx->d_lane16_s36);
+    (void)hipFree(ctx->d_zu576);
     (void)hipFree(ctx->d_scratch);
     if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
     (void)hipStreamDestroy(ctx->stream);
@@ -497,6 +499,12 @@ RH_EXPORT int rh_segments_scan_launch(rh_ctx* ctx, const rh_segments* segs, void
     if (!ctx) return rh::fail(RH_E_INVAL, "rh_segments_scan_launch: ctx == NULL");
     DeviceGuard g(ctx->device);
     return rh_segments_launch_impl(ctx, segs, pick_stream(ctx, stream));
+}
+
+RH_EXPORT int rh_segments_read_launch(rh_ctx* ctx, const rh_segments* segs, const rh_segments_crc* crc, void* stream) {
+    if (!ctx) return rh::fail(RH_E_INVAL, "rh_segments_read_launch: ctx == NULL");
+    DeviceGuard g(ctx->device);
+    return rh_segments_read_impl(ctx, segs, crc, pick_stream(ctx, stream));
 }
 
 RH_EXPORT int rh_segments_set_variant(int variant) { return rh_segments_set_variant_impl(variant); }

@@ -594,6 +594,13 @@ hipError_t launch_walk2(const SegArgs& a, int cus, hipStream_t stream) {
 
 }  // namespace
 
+int rh_segments_scan_counts(const uint32_t* nframes, uint64_t n_seg, uint32_t cap, uint64_t* seg_first,
+                            unsigned long long* total, hipStream_t stream) {
+    hipLaunchKernelGGL(segment_scan_kernel, dim3(1), dim3(kScanThreads), 0, stream, nframes, n_seg, cap, seg_first, total);
+    RH_HIP(hipGetLastError());
+    return RH_OK;
+}
+
 int rh_segments_set_variant_impl(int v) {
     if (v < 0 || v > 2) return rh::fail(RH_E_RANGE, "rh_segments_set_variant: variant out of range [0, 2]");
     g_seg_variant = v;

@@ -28,7 +28,7 @@ from typing import Optional, Sequence
 import torch
 
 from . import _lib
-from ._lib import RH_MODE_COMMIT, RH_MODE_WATCH, RhCommitSoa, RhFrames, RhLeaseSoa, RhSegments, check
+from ._lib import RH_MODE_COMMIT, RH_MODE_WATCH, RhCommitSoa, RhFrames, RhLeaseSoa, RhSegments, RhSegmentsCrc, check
 
 
 def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
@@ -399,6 +399,37 @@ def read_segments(ctx: Context, batch: SegmentBatch, stream: Optional[torch.cuda
         else:
             stop = batch.seg_stop[:nseg].clone()
     return {"n_ok": n_ok, "status": status, "stop": stop, "frames": fb, "total_frames": batch.total_frames}
+
+
+def read_segments_fused(ctx: Context, batch: SegmentBatch, stream: Optional[torch.cuda.Stream] = None) -> dict:
+    """``LogSegment.readSegmentFile`` over every segment in ONE pass over HBM (rh_segments_read_launch):
+    the framing walk and every frame's CRC32C verify in the same kernel.  Fills the batch's framing
+    outputs exactly as :func:`segments_scan` does and returns the reader's verdict per segment
+    (``n_ok``, ``status``, ``stop``: the same values :func:`read_segments` derives) plus the dense
+    per-frame CRCs / mismatch bits.  Asynchronous: nothing is synchronised."""
+    batch.alloc_outputs()
+    dev, n, cap = batch.buf.device, batch.n_seg, batch.frames_per_seg_cap
+    out = {
+        "scratch_crc": torch.empty(max(1, n * cap), dtype=torch.int32, device=dev),
+        "n_ok": torch.empty(max(1, n), dtype=torch.int32, device=dev),
+        "status": torch.empty(max(1, n), dtype=torch.int32, device=dev),
+        "stop": torch.empty(max(1, n), dtype=torch.int64, device=dev),
+        "crc_out": torch.empty(batch.frame_cap, dtype=torch.int32, device=dev),
+        "bad_bits": torch.zeros((batch.frame_cap + 63) // 64, dtype=torch.int64, device=dev),
+        "n_bad": torch.zeros(1, dtype=torch.int64, device=dev),
+    }
+    c = RhSegmentsCrc()
+    c.scratch_crc = _ptr(out["scratch_crc"])
+    c.seg_ok = _ptr(out["n_ok"])
+    c.seg_read_status = _ptr(out["status"])
+    c.seg_read_stop = _ptr(out["stop"])
+    c.crc_out = _ptr(out["crc_out"])
+    c.bad_bits = _ptr(out["bad_bits"])
+    c.n_bad = _ptr(out["n_bad"])
+    g = batch.to_struct()
+    check(_lib.load().rh_segments_read_launch(ctx.handle, ctypes.byref(g), ctypes.byref(c), _stream_ptr(stream)))
+    out["total_frames"] = batch.total_frames
+    return out
 
 
 class _nullctx:

@@ -67,6 +67,9 @@ int main(void) {
   printf("rh_delta %zu\n", sizeof(rh_delta));
   printf("rh_segments %zu\n", sizeof(rh_segments));
   printf("rh_lease_soa %zu\n", sizeof(rh_lease_soa));
+  printf("rh_segments_crc %zu\n", sizeof(rh_segments_crc));
+  F(rh_segments_crc, scratch_crc) F(rh_segments_crc, seg_ok) F(rh_segments_crc, seg_read_status)
+  F(rh_segments_crc, seg_read_stop) F(rh_segments_crc, crc_out) F(rh_segments_crc, bad_bits) F(rh_segments_crc, n_bad)
   F(rh_commit_soa, n) F(rh_commit_soa, n_followers) F(rh_commit_soa, mode) F(rh_commit_soa, gap_threshold)
   F(rh_commit_soa, follower_index) F(rh_commit_soa, col_stride) F(rh_commit_soa, self_index)
   F(rh_commit_soa, commit_in) F(rh_commit_soa, term_start) F(rh_commit_soa, conf) F(rh_commit_soa, commit_out)
@@ -104,8 +107,10 @@ def test_struct_layouts_match_header(tmp_path):
     assert int(vals["rh_delta"]) == ctypes.sizeof(_lib.RhDelta)
     assert int(vals["rh_segments"]) == ctypes.sizeof(_lib.RhSegments)
     assert int(vals["rh_lease_soa"]) == ctypes.sizeof(_lib.RhLeaseSoa)
+    assert int(vals["rh_segments_crc"]) == ctypes.sizeof(_lib.RhSegmentsCrc)
     for cname, cls in (("rh_commit_soa", _lib.RhCommitSoa), ("rh_frames", _lib.RhFrames), ("rh_delta", _lib.RhDelta),
-                       ("rh_segments", _lib.RhSegments), ("rh_lease_soa", _lib.RhLeaseSoa)):
+                       ("rh_segments", _lib.RhSegments), ("rh_lease_soa", _lib.RhLeaseSoa),
+                       ("rh_segments_crc", _lib.RhSegmentsCrc)):
         for fname, _ in cls._fields_:
             assert int(vals[f"{cname}.{fname}"]) == getattr(cls, fname).offset, (cname, fname)
     assert int(vals["conf"]) == _lib.conf_pack(0x5, True, True, 0x3, True, True)

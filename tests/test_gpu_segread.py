@@ -1,0 +1,187 @@
+"""GPU parity of the fused read path (rh_segments_read_launch: framing walk + CRC32C verify of every
+frame in one pass = LogSegment.readSegmentFile, LogSegment.java:166-196) against the oracle's
+orc_segment_scan, which runs SegmentedRaftLogReader's verifyHeader / decodeEntry (with its
+checksum, RDR:327-336) / verifyTerminator literally, and against the two-pass path's framing.
+
+Covered: every damage kind of test_gpu_segment (header, truncation, varint, oversize, padding,
+flipped payload bits), frames long enough to leave the LDS ring (folded from HBM), thousands of
+tiny frames per window (the per-step frame/unit list fills up), CRC spans of 2 and 3 bytes (the
+reset() state reaches past the message), the TestRaftLogReadWrite segment and config-5 segments
+with planted corruptions."""
+import os
+
+import numpy as np
+import pytest
+
+from .test_gpu_segment import HEADER, KINDS, make_segment, pack
+
+pytestmark = pytest.mark.gpu
+
+
+def run_fused(ctx, buf, offs, lens, max_op=4 << 20, cap=4096):
+    import torch
+
+    from ratis_amd import engine
+    dev = torch.device("cuda")
+    b = engine.SegmentBatch(buf=torch.from_numpy(buf).to(dev), seg_off=torch.from_numpy(offs).to(dev),
+                            seg_len=torch.from_numpy(lens).to(dev), max_op=max_op, frames_per_seg_cap=cap)
+    out = engine.read_segments_fused(ctx, b)
+    torch.cuda.synchronize()
+    return b, out
+
+
+def _bits(words, n):
+    return np.unpackbits(np.asarray(words).view(np.uint64).view(np.uint8), bitorder="little")[:n].astype(bool)
+
+
+def check_fused(ctx, orc, b, out, buf, offs, lens, max_op=4 << 20, cap=4096):
+    import torch
+
+    from ratis_amd import engine
+    # 1. the reader's verdict per segment == the literal reader (framing + checksum)
+    n_ok, st, stop = out["n_ok"].cpu().numpy(), out["status"].cpu().numpy(), out["stop"].cpu().numpy()
+    for s in range(len(offs)):
+        ro, _, _, rst, rstop = orc.segment_scan(buf[offs[s]: offs[s] + lens[s]], max_op=max_op)
+        assert (st[s], stop[s], n_ok[s]) == (rst, rstop, len(ro)), s
+    # 2. framing outputs == the two-pass framing walk on the same buffer
+    b2 = engine.SegmentBatch(buf=b.buf, seg_off=b.seg_off, seg_len=b.seg_len, max_op=max_op, frames_per_seg_cap=cap)
+    engine.segments_scan(ctx, b2)
+    torch.cuda.synchronize()
+    for name in ("seg_nframes", "seg_status", "seg_stop", "seg_first"):
+        assert torch.equal(getattr(b, name)[: len(offs)], getattr(b2, name)[: len(offs)]), name
+    total = int(b.total_frames.item())
+    assert total == int(b2.total_frames.item())
+    assert torch.equal(b.frame_off[:total], b2.frame_off[:total])
+    assert torch.equal(b.frame_len[:total], b2.frame_len[:total])
+    # 3. every frame's CRC == PureJavaCrc32C over varint||proto; mismatch bit == (stored != computed)
+    fo = b.frame_off[:total].cpu().numpy()
+    fl = b.frame_len[:total].cpu().numpy()
+    got = out["crc_out"][:total].cpu().numpy().view(np.uint32)
+    want, _ = orc.crc32c_frames(buf, fo.astype(np.uint64), fl.astype(np.uint32))
+    assert np.array_equal(got, want)
+    stored = np.array([int.from_bytes(buf[o + l - 4: o + l].tobytes(), "big") for o, l in zip(fo, fl)], np.uint32)
+    bad = _bits(out["bad_bits"].cpu().numpy(), total)
+    assert np.array_equal(bad, stored != want)
+    assert int(out["n_bad"].item()) == int(bad.sum())
+    return total
+
+
+@pytest.mark.parametrize("big", [False, True])
+def test_fused_matches_reader_every_kind(ctx, orc, big):
+    rng = np.random.default_rng(70 + big)
+    kinds = [KINDS[i % len(KINDS)] for i in range(len(KINDS) * 6)]
+    made = [make_segment(orc, rng, k, big) for k in kinds]
+    buf, offs, lens = pack([m[0] for m in made], rng)
+    b, out = run_fused(ctx, buf, offs, lens)
+    check_fused(ctx, orc, b, out, buf, offs, lens)
+    from ratis_amd import _lib
+    st = set(out["status"].cpu().numpy().tolist())
+    for code in (_lib.RH_SEG_END, _lib.RH_SEG_PARTIAL, _lib.RH_SEG_E_OVERSIZE, _lib.RH_SEG_E_PADDING,
+                 _lib.RH_SEG_E_VARINT, _lib.RH_SEG_E_HEADER, _lib.RH_SEG_E_CHECKSUM):
+        assert code in st, code
+
+
+def test_fused_long_frames_folded_from_hbm(ctx, orc):
+    """Frames from 20 KiB to 600 KiB (past the 64 KiB ring), between runs of small frames, some
+    with a flipped bit: the long ones are folded straight from HBM by one group."""
+    rng = np.random.default_rng(5)
+    images = []
+    for i in range(10):
+        protos = []
+        for j in range(int(rng.integers(3, 12))):
+            n = int(rng.integers(20_000, 600_000)) if rng.random() < 0.4 else int(rng.integers(1, 5000))
+            protos.append(rng.integers(0, 256, n, dtype=np.uint8).tobytes())
+        frames = [orc.frame_write(p) for p in protos]
+        body = bytearray(HEADER + b"".join(frames) + bytes(int(rng.integers(0, 3000))))
+        if i % 3 == 1:  # corrupt one byte inside a long frame's payload
+            starts = np.cumsum([8] + [len(f) for f in frames])
+            k = int(np.argmax([len(f) for f in frames]))
+            body[int(starts[k]) + len(frames[k]) // 2] ^= 0x40
+        images.append(bytes(body))
+    buf, offs, lens = pack(images, rng)
+    b, out = run_fused(ctx, buf, offs, lens)
+    check_fused(ctx, orc, b, out, buf, offs, lens)
+    assert int(out["n_bad"].item()) >= 3
+
+
+def test_fused_tiny_frames_and_short_spans(ctx, orc):
+    """~2000 frames per 16 KiB window (the per-step list caps at 256 frames / 512 units and the walk
+    resumes inside the window) and 1- and 2-byte protos, whose CRC spans of 2 and 3 bytes leave part
+    of reset()'s 0xFFFFFFFF past the message."""
+    rng = np.random.default_rng(8)
+    images = []
+    for i in range(6):
+        fr = [orc.frame_write(bytes(rng.integers(0, 256, 1 + (j % 3), dtype=np.uint8))) for j in range(6000 + 17 * i)]
+        body = bytearray(HEADER + b"".join(fr) + bytes(100))
+        if i % 2:
+            body[int(rng.integers(8, len(body) - 200))] ^= 1
+        images.append(bytes(body))
+    buf, offs, lens = pack(images, rng)
+    b, out = run_fused(ctx, buf, offs, lens, cap=8192)
+    total = check_fused(ctx, orc, b, out, buf, offs, lens, cap=8192)
+    assert total > 30_000
+
+
+def test_fused_frame_capacity(ctx, orc):
+    from ratis_amd import _lib
+    rng = np.random.default_rng(3)
+    img = HEADER + b"".join(orc.frame_write(bytes([7]) * 5) for _ in range(100)) + bytes(100)
+    buf, offs, lens = pack([img, img], rng)
+    b, out = run_fused(ctx, buf, offs, lens, cap=64)
+    assert list(b.seg_status.cpu().numpy()) == [_lib.RH_SEG_E_CAPACITY] * 2
+    assert list(out["n_ok"].cpu().numpy()) == [64, 64]
+
+
+def test_fused_raftlog_readwrite_golden(ctx, orc):
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "raftlog_rw.npz"))
+    img = np.asarray(z["image"], dtype=np.uint8)
+    bad = img.copy()
+    bad[100] ^= 0xFF   # TestRaftLogReadWrite's corruption case: byte 100 flipped (:239-268)
+    rng = np.random.default_rng(0)
+    buf, offs, lens = pack([img.tobytes(), img.tobytes() + bytes(4096), bad.tobytes()], rng)
+    b, out = run_fused(ctx, buf, offs, lens)
+    check_fused(ctx, orc, b, out, buf, offs, lens)
+    assert list(out["n_ok"].cpu().numpy())[:2] == [100, 100]
+
+
+def test_fused_config5_segments(ctx, orc):
+    """32 MiB segments of 4 KiB frames with planted corruptions: the frame
+    table equals the generator's and the mismatch set equals the planted set."""
+    import torch
+
+    from ratis_amd import engine, workload
+    ss = workload.synth_segments(ctx, n_segments=6, corrupt_rate=3e-4, seed=41)
+    n = ss.n_segments
+    b = engine.SegmentBatch(buf=ss.batch.buf, seg_off=torch.arange(n, dtype=torch.int64, device="cuda") * ss.segment_size,
+                            seg_len=torch.full((n,), ss.segment_size, dtype=torch.int64, device="cuda"),
+                            frames_per_seg_cap=ss.frames_per_segment + 16)
+    out = engine.read_segments_fused(ctx, b)
+    torch.cuda.synchronize()
+    nf = n * ss.frames_per_segment
+    assert int(b.total_frames.item()) == nf
+    assert torch.equal(b.frame_off[:nf], ss.batch.frame_off) and torch.equal(b.frame_len[:nf], ss.batch.frame_len)
+    bad = np.nonzero(_bits(out["bad_bits"].cpu().numpy(), nf))[0]
+    assert np.array_equal(bad, ss.corrupted) and ss.corrupted.size > 0
+    fps = ss.frames_per_segment
+    ok = out["n_ok"].cpu().numpy()
+    for sgi in range(n):
+        mine = ss.corrupted[(ss.corrupted >= sgi * fps) & (ss.corrupted < (sgi + 1) * fps)]
+        assert int(ok[sgi]) == (int(mine[0]) - sgi * fps if mine.size else fps), sgi
+    idx = np.linspace(0, nf - 1, 48).astype(np.int64)
+    offs = b.frame_off.cpu().numpy()
+    got = out["crc_out"].cpu().numpy().view(np.uint32)
+    for i in idx:
+        fr = ss.batch.buf[int(offs[i]): int(offs[i]) + ss.frame_size - 4].cpu().numpy().tobytes()
+        assert orc.crc32c(fr) == int(got[i])
+
+
+def test_fused_bad_arguments(ctx):
+    import torch
+
+    from ratis_amd import _lib, engine
+    dev = torch.device("cuda")
+    b = engine.SegmentBatch(buf=torch.zeros(16, dtype=torch.uint8, device=dev),
+                            seg_off=torch.zeros(1, dtype=torch.int64, device=dev),
+                            seg_len=torch.full((1,), 16, dtype=torch.int64, device=dev), frames_per_seg_cap=0)
+    with pytest.raises(_lib.IllegalArgumentError):
+        engine.read_segments_fused(ctx, b)
