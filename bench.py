@@ -416,12 +416,36 @@ def main():
         f1.record(stream)
         barrier()
         read_ms = f0.elapsed_time(f1) / args.crc_steps
+        # fused: framing + verify in one pass over HBM (rh_segments_read_launch)
+        fbatch = engine.SegmentBatch(buf=fb.buf, seg_off=sb.seg_off, seg_len=sb.seg_len,
+                                     frames_per_seg_cap=ss.frames_per_segment + 16)
+        for _ in range(2):
+            fout = engine.read_segments_fused(ctx, fbatch, stream=stream)
+        barrier()
+        f0.record(stream)
+        for _ in range(args.crc_steps):
+            fout = engine.read_segments_fused(ctx, fbatch, stream=stream)
+        f1.record(stream)
+        barrier()
+        fused_ms = f0.elapsed_time(f1) / args.crc_steps
+        fbad = np.nonzero(np.unpackbits(fout["bad_bits"].cpu().numpy().view(np.uint8), bitorder="little")[: fb.n])[0]
+        fused_ok = bool(np.array_equal(fbad, ss.corrupted) and int(fbatch.total_frames.item()) == fb.n
+                        and torch.equal(fbatch.frame_off[: fb.n], fb.frame_off)
+                        and torch.equal(fout["crc_out"][: fb.n], fb.crc_out[: fb.n]))
+        del fbatch, fout
         seg_bytes = n_seg * ss.segment_size
         tot_seg_bytes = sum_over_ranks(seg_bytes)
         scan_ach = seg_bytes / (scan_ms * 1e-3) / 1e9
         crc["read_path"] = {
             "framing_GBps": round(tot_seg_bytes / (max_over_ranks(scan_ms) * 1e-3) / 1e9, 1),
             "framing_plus_verify_GBps": round(tot_seg_bytes / (max_over_ranks(read_ms) * 1e-3) / 1e9, 1),
+            "fused_read_GBps": round(tot_seg_bytes / (max_over_ranks(fused_ms) * 1e-3) / 1e9, 1),
+            "ms_fused_read": round(fused_ms, 4), "fused_parity_ok": fused_ok,
+            "fused_roofline": {"bound": "hbm", "achieved": round(seg_bytes / (fused_ms * 1e-3) / 1e9, 1),
+                               "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                               "frac": round(seg_bytes / (fused_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                               "kernel": "segment_read_kernel (framing + CRC verify, one pass) + scan + compact",
+                               "algorithmic_bytes_per_launch": seg_bytes},
             "unit": "GB/s (segment bytes, whole job)", "frames_found": nfr_found, "parity_ok": bool(frame_ok),
             "ms_framing": round(scan_ms, 4), "ms_framing_plus_verify": round(read_ms, 4),
             "roofline": {"bound": "hbm", "achieved": round(scan_ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
