@@ -191,6 +191,8 @@ _SIGNATURES = {
     "rh_lease_soa_launch": (c_int, [c_void_p, POINTER(RhLeaseSoa), c_int, c_void_p]),
     "rh_segments_scan_launch": (c_int, [c_void_p, POINTER(RhSegments), c_void_p]),
     "rh_segments_set_variant": (c_int, [c_int]),
+    "rh_segments_read_profile": (c_int, [c_int, c_void_p, c_uint64]),
+    "rh_segments_read_set_variant": (c_int, [c_int]),
     "rh_segments_read_launch": (c_int, [c_void_p, POINTER(RhSegments), POINTER(RhSegmentsCrc), c_void_p]),
     "rh_crc32c_num_variants": (c_int, []),
     "rh_commit_num_variants": (c_int, []),

@@ -138,6 +138,7 @@ RH_EXPORT int rh_shutdown(rh_ctx* ctx) {
     (void)hipFree(ctx->d_lane8_s128);
     (void)hipFree(ctx->d_lane16_s36);
     (void)hipFree(ctx->d_zu576);
+    for (uint32_t* p : ctx->d_read_tables) (void)hipFree(p);
     (void)hipFree(ctx->d_scratch);
     if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
     (void)hipStreamDestroy(ctx->stream);
@@ -508,6 +509,12 @@ RH_EXPORT int rh_segments_read_launch(rh_ctx* ctx, const rh_segments* segs, cons
 }
 
 RH_EXPORT int rh_segments_set_variant(int variant) { return rh_segments_set_variant_impl(variant); }
+
+RH_EXPORT int rh_segments_read_set_variant(int variant) { return rh_segments_read_set_variant_impl(variant); }
+
+RH_EXPORT int rh_segments_read_profile(int enable, uint64_t* out, uint64_t n) {
+    return rh_segments_read_profile_impl(enable, out, n);
+}
 
 RH_EXPORT int rh_crc32c_num_variants(void) { return rh_crc_num_variants(); }
 

@@ -50,6 +50,7 @@ struct rh_ctx {
     uint32_t* d_lane8_s128 = nullptr;
     uint32_t* d_lane16_s36 = nullptr;   // 16 lanes x 36-byte chunks (fused read kernel)
     uint32_t* d_zu576 = nullptr;        // [4][256]: advance over 576 zero bytes
+    uint32_t* d_read_tables[2] = {nullptr, nullptr};  // fused read kernel, per variant (segread.hip)
     // scratch for host-buffer convenience calls
     std::mutex mu;
     void* d_scratch = nullptr;
@@ -75,6 +76,8 @@ int rh_segments_set_variant_impl(int v);
 int rh_segments_scan_counts(const uint32_t* nframes, uint64_t n_seg, uint32_t cap, uint64_t* seg_first,
                             unsigned long long* total, hipStream_t stream);
 int rh_segments_read_impl(rh_ctx* ctx, const rh_segments* segs, const rh_segments_crc* crc, hipStream_t stream);
+int rh_segments_read_profile_impl(int enable, uint64_t* out, uint64_t n);
+int rh_segments_read_set_variant_impl(int v);
 int rh_lease_launch_impl(rh_ctx* ctx, const rh_lease_soa* tiers, int n_tiers, hipStream_t stream);
 int rh_lease_set_variant_impl(int v);
 int rh_lease_num_variants_impl();

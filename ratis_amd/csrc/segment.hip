@@ -343,6 +343,8 @@ __global__ __launch_bounds__(kBlock2) void segment_walk_kernel2(SegArgs a) {
         int status = sh_status;
         int64_t pos = sh_pos;
         Win<W> nxt;
+        // wave 0's speculation state: the last two frame lengths (equal = a run worth speculating on)
+        uint32_t last_fl = 0, prev_fl = 1;
         while (status == kWalking) {
             // (re)start the pipeline at the window holding pos
             int64_t k = (pos - A) / W;
@@ -356,12 +358,55 @@ __global__ __launch_bounds__(kBlock2) void segment_walk_kernel2(SegArgs a) {
                 nxt.store(ring, (int)((k + 1) & 1), t);   // ring now holds windows k, k+1
                 __syncthreads();
                 nxt.load(seg, L, A + (k + 2) * W, t);       // in flight during the walk
-                if (t == 0) {
+                if (t < 64) {
+                    // wave 0 walks, wave-uniformly (lane 0 stores the single-frame steps)
+                    const int lane = t;
                     const int64_t wend = A + (k + 1) * W;
                     uint32_t nfr = sh_nfr;
                     int st = kWalking;
                     int64_t p = pos;
                     while (p < wend) {
+                        {
+                            // Speculative run (a run of equal lengths was seen): lane j checks the
+                            // frame at p + j * s, s = the last length, with the fast loop's folded
+                            // predicate; the leading run of lanes that pass with length s is
+                            // accepted at once (frame j + 1 starts at p + (j + 1) s iff frames
+                            // 0..j all have length s).  Exact; a mismatch ends the run.
+                            const int64_t pend = wend < L - 8 ? wend : L - 8;
+                            if (last_fl == prev_fl && last_fl <= (1u << 25) && L <= 0x7fffffff && pend > p) {
+                                const uint32_t sd = last_fl, p32 = (uint32_t)p, pend32 = (uint32_t)pend;
+                                const uint32_t c = p32 + (uint32_t)lane * sd;
+                                const bool okp = c < pend32;
+                                const uint32_t q = (uint32_t)(((okp ? c : p32) - A) & MASK);
+                                const uint32_t q0 = q & ~3u;
+                                const uint32_t lo = *reinterpret_cast<const uint32_t*>(ring + q0);
+                                const uint32_t hi = *reinterpret_cast<const uint32_t*>(ring + q0 + 4);  // mirror
+                                const uint32_t v = (uint32_t)(((uint64_t)hi << 32 | lo) >> (8 * (q & 3)));
+                                const uint32_t stop4 = ~v & 0x80808080u;
+                                const int vl = (__builtin_ctz(stop4 | 0x80000000u) >> 3) + 1;
+                                const uint32_t nn = ((v & 0x7fu) | ((v >> 1) & 0x3f80u) | ((v >> 2) & 0x1fc000u) |
+                                                     ((v >> 3) & 0xfe00000u)) &
+                                                    (0xffffffffu >> (32 - 7 * vl));
+                                const uint32_t vs = nn < (1u << 7) ? 1u : nn < (1u << 14) ? 2u : nn < (1u << 21) ? 3u : 4u;
+                                const uint32_t fl = vs + nn + 4;
+                                const uint32_t left = okp ? (uint32_t)L - c : 0u;
+                                const bool ok = okp && (v & 0xffu) != 0 && stop4 != 0 && fl == sd &&
+                                                fl <= (left < a.max_op ? left : a.max_op) && nfr + (uint32_t)lane < a.cap;
+                                const uint64_t m = __builtin_amdgcn_ballot_w64(ok);
+                                const uint32_t nacc = __builtin_amdgcn_readfirstlane(~m ? (uint32_t)__builtin_ctzll(~m) : 64u);
+                                if (nacc) {
+                                    if ((uint32_t)lane < nacc) {
+                                        a.scratch_off[s * (uint64_t)a.cap + nfr + lane] = (uint64_t)base + c;
+                                        a.scratch_len[s * (uint64_t)a.cap + nfr + lane] = sd;
+                                    }
+                                    nfr += nacc;
+                                    p += (int64_t)nacc * sd;
+                                    if (nacc == 64) continue;
+                                }
+                                if (p >= wend) break;
+                                if (p < pend) prev_fl = 0;  // a different frame ended the run: scalar loop
+                            }
+                        }
                         {
                             // Fast loop for the common case, every check folded into two
                             // predicates: a non-zero first byte and a varint of <= 4 bytes wholly
@@ -392,11 +437,16 @@ __global__ __launch_bounds__(kBlock2) void segment_walk_kernel2(SegArgs a) {
                                     const uint32_t fl = vs + nn + 4;  // nn < 2^28: no overflow
                                     const uint32_t left = L32 - p32;
                                     if (fl > (left < mo ? left : mo)) break;
-                                    so[k] = (uint64_t)base + p32;
-                                    sl[k] = fl;
+                                    if (lane == 0) {
+                                        so[k] = (uint64_t)base + p32;
+                                        sl[k] = fl;
+                                    }
                                     ++k;
                                     p32 += fl;
                                     q = (q + fl) & (uint32_t)MASK;
+                                    prev_fl = last_fl;
+                                    last_fl = fl;
+                                    if (fl == prev_fl) break;  // a run: back to speculation
                                 }
                                 p = p32;
                             }
@@ -471,14 +521,20 @@ __global__ __launch_bounds__(kBlock2) void segment_walk_kernel2(SegArgs a) {
                             st = RH_SEG_E_CAPACITY;
                             break;
                         }
-                        a.scratch_off[s * (uint64_t)a.cap + nfr] = (uint64_t)(base + p);
-                        a.scratch_len[s * (uint64_t)a.cap + nfr] = (uint32_t)(total + 4);
+                        if (lane == 0) {
+                            a.scratch_off[s * (uint64_t)a.cap + nfr] = (uint64_t)(base + p);
+                            a.scratch_len[s * (uint64_t)a.cap + nfr] = (uint32_t)(total + 4);
+                        }
                         ++nfr;
                         p += total + 4;
+                        prev_fl = last_fl;
+                        last_fl = (uint32_t)(total + 4);
                     }
-                    sh_status = st;
-                    sh_pos = p;
-                    sh_nfr = nfr;
+                    if (lane == 0) {
+                        sh_status = st;
+                        sh_pos = p;
+                        sh_nfr = nfr;
+                    }
                 }
                 __syncthreads();
                 status = sh_status;

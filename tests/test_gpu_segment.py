@@ -257,3 +257,37 @@ def test_long_padding_tails(ctx, orc, seg_variant):
     buf, offs, lens = pack(images, rng)
     b = run_scan(ctx, buf, offs, lens)
     check_against_oracle(orc, b, buf, offs, lens)
+
+
+def speculation_images(orc, rng):
+    """Segments that exercise the speculative walk (a wave checks 64 equal-length frames at once):
+    runs broken by one frame of another length at lane positions 1..200, equal-length runs across
+    window and ring boundaries, runs ending at zero padding / EOF / a truncated frame / garbage after
+    the terminator, a malformed varint inside a run, and runs of 6-byte frames."""
+    images = []
+    for size in (6, 40, 577, 1000, 4096, 9000):
+        for brk in (1, 7, 31, 63, 64, 65, 200):
+            protos = [bytes(rng.integers(0, 256, size - 5 if size > 6 else 1, dtype=np.uint8)) for _ in range(300)]
+            if brk < len(protos):
+                protos[brk] = bytes(rng.integers(0, 256, max(1, len(protos[brk]) + 3), dtype=np.uint8))
+            body = bytearray(HEADER + b"".join(orc.frame_write(p) for p in protos))
+            tail = int(rng.integers(0, 4))
+            if tail == 1:
+                body += bytes(int(rng.integers(1, 5000)))          # zero padding
+            elif tail == 2:
+                body = body[: len(body) - int(rng.integers(1, 6))]  # truncated last frame
+            elif tail == 3:
+                body += bytes(100) + b"x" + bytes(7)              # garbage after the terminator
+            images.append(bytes(body))
+    fr = [orc.frame_write(bytes(50)) for _ in range(120)]
+    body = bytearray(HEADER + b"".join(fr))
+    body[8 + 90 * len(fr[0]): 8 + 90 * len(fr[0]) + 6] = b"\xff\xff\xff\xff\xff\xff"  # 6-byte varint
+    images.append(bytes(body))
+    return images
+
+
+def test_speculative_walk_edges(ctx, orc, seg_variant):
+    rng = np.random.default_rng(123)
+    buf, offs, lens = pack(speculation_images(orc, rng), rng)
+    b = run_scan(ctx, buf, offs, lens, cap=1024)
+    check_against_oracle(orc, b, buf, offs, lens)

@@ -13,9 +13,19 @@ import os
 import numpy as np
 import pytest
 
-from .test_gpu_segment import HEADER, KINDS, make_segment, pack
+from .test_gpu_segment import HEADER, KINDS, make_segment, pack, speculation_images
 
 pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(autouse=True, params=[0, 1], ids=["S36", "S20"])
+def read_variant(request):
+    """Every test runs on both fused-kernel variants (CRC unit = 16 lanes x 36 / x 20 bytes)."""
+    from ratis_amd import _lib
+    lib = _lib.load()
+    _lib.check(lib.rh_segments_read_set_variant(request.param))
+    yield request.param
+    _lib.check(lib.rh_segments_read_set_variant(0))
 
 
 def run_fused(ctx, buf, offs, lens, max_op=4 << 20, cap=4096):
@@ -185,3 +195,11 @@ def test_fused_bad_arguments(ctx):
                             seg_len=torch.full((1,), 16, dtype=torch.int64, device=dev), frames_per_seg_cap=0)
     with pytest.raises(_lib.IllegalArgumentError):
         engine.read_segments_fused(ctx, b)
+
+
+def test_fused_speculative_walk_edges(ctx, orc):
+    """The fused walker's speculation (test_gpu_segment.speculation_images)."""
+    rng = np.random.default_rng(123)
+    buf, offs, lens = pack(speculation_images(orc, rng), rng)
+    b, out = run_fused(ctx, buf, offs, lens, cap=1024)
+    check_fused(ctx, orc, b, out, buf, offs, lens, cap=1024)
