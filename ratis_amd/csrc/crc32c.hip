@@ -988,30 +988,29 @@ __global__ __launch_bounds__(1024) void crc_frames_kernel5(FrameArgs a) {
         const bool act = cc.f < a.n && cc.wi < cc.nw;
         const int64_t be = cc.E - (cc.nw - 1 - cc.wi) * W - (int64_t)(Q - 1 - gl) * S;
         const int64_t b0 = be - S - cc.sh;
-        const bool safe = !act || (b0 >= 0 && b0 + 68 <= a.buf_len);
+        const bool safe = act ? (b0 >= 0 && b0 + 68 <= a.buf_len) : a.buf_len >= 68;
         if (__all(safe)) {
-            if (act) {
+            // every lane loads (inactive lanes from the buffer start; their data is never used:
+            // the fold masks r with act): no divergent zero-fill of registers a load may still
+            // be writing, which would make the compiler drain the whole prefetch (vmcnt(0))
+            const uint8_t* src = a.buf + (act ? b0 : 0);
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    if (NT) {
-                        const u32x4v v = __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(a.buf + b0 + 16 * q));
-                        dd[4 * q] = v.x;
-                        dd[4 * q + 1] = v.y;
-                        dd[4 * q + 2] = v.z;
-                        dd[4 * q + 3] = v.w;
-                    } else {
-                        const u32x4a v = *reinterpret_cast<const u32x4a*>(a.buf + b0 + 16 * q);
-                        dd[4 * q] = v.x;
-                        dd[4 * q + 1] = v.y;
-                        dd[4 * q + 2] = v.z;
-                        dd[4 * q + 3] = v.w;
-                    }
+            for (int q = 0; q < 4; ++q) {
+                if (NT) {
+                    const u32x4v v = __builtin_nontemporal_load(reinterpret_cast<const u32x4v*>(src + 16 * q));
+                    dd[4 * q] = v.x;
+                    dd[4 * q + 1] = v.y;
+                    dd[4 * q + 2] = v.z;
+                    dd[4 * q + 3] = v.w;
+                } else {
+                    const u32x4a v = *reinterpret_cast<const u32x4a*>(src + 16 * q);
+                    dd[4 * q] = v.x;
+                    dd[4 * q + 1] = v.y;
+                    dd[4 * q + 2] = v.z;
+                    dd[4 * q + 3] = v.w;
                 }
-                dd[16] = *reinterpret_cast<const uint32_t*>(a.buf + b0 + 64);
-            } else {
-#pragma unroll
-                for (int i = 0; i < 17; ++i) dd[i] = 0;
             }
+            dd[16] = *reinterpret_cast<const uint32_t*>(src + 64);
         } else {
 #pragma unroll
             for (int i = 0; i < 17; ++i) {
@@ -1292,6 +1291,265 @@ __global__ __launch_bounds__(1024) void crc_frames_kernel7(FrameArgs a) {
 }
 
 
+// ---- v8: v5's fold with a copy-free prefetch ring and frame metadata staged in LDS -----------
+// v5 rotates its register ring by copying (dq[p] = dq[p + 1]), which makes the compiler wait for
+// the load it just issued (vmcnt(0) at the loop head), and reads each frame's offset/length from
+// HBM right when it needs them, which drains every load in flight.  v8 keeps the same 16-lane x
+// 64-byte fold and lane-distance tables, but
+//   * the loop body is unrolled over the 3 ring slots with static roles (load slot i+2 while
+//     folding slot i): a window's data is consumed two windows after its load was issued, and
+//     every wait in the loop is a counted vmcnt(N);
+//   * the frame table is staged per block in batches of 512 frames into LDS (one drain per batch),
+//     group g of the block taking frames g, g+64, ... of the batch;
+//   * the trailer for VERIFY comes from the last window's own chunk (one extra dword per lane), so
+//     the verify needs no dependent byte loads; the group's lane 15 (whose chunk ends at the CRC
+//     span's end) finalises the frame;
+//   * inactive lanes load from the buffer start instead of zero-filling registers in flight.
+// Frames whose chunks could leave the buffer (within 67 bytes of its start or 8 of its end),
+// malformed and empty ones take a guarded byte path after the batch's main loop.
+constexpr int kV8Batch = 512;
+struct MetaV8 {
+    int64_t o;    // frame start (bytes)
+    uint32_t lc;  // CRC-covered length
+    uint32_t fl;  // 0 = fast path; 1 = slow path (guarded), 2 = malformed
+};
+
+template <int PF>
+__global__ __launch_bounds__(1024) void crc_frames_kernel8(FrameArgs a) {
+    static_assert(PF == 2, "v8 ring: 3 slots");
+    constexpr int Q = 16, S = 64;
+    constexpr int64_t W = (int64_t)Q * S;
+    constexpr int kSliceBytes = 128 * 1024;
+    constexpr int kLaneWords = 8 * 16 * 32;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    if (__builtin_amdgcn_groupstaticsize() != 0) __builtin_trap();  // lds_word assumes base 0
+    uint32_t* llane = lds + kSliceBytes / 4;
+    uint32_t* lzw = llane + kLaneWords;
+    MetaV8* meta = reinterpret_cast<MetaV8*>(lzw + 1024);
+    uint32_t* slow = reinterpret_cast<uint32_t*>(meta + kV8Batch);  // [kV8Batch] slow-path frames
+    uint32_t* nslow = slow + kV8Batch;
+    for (int i = threadIdx.x; i < kSliceBytes / 4; i += blockDim.x) {
+        const int region = i >> 14, e = (i >> 6) & 255, half = (i >> 5) & 1;
+        lds[i] = a.slice[((region * 2 + half) << 8) | e];
+    }
+    for (int i = threadIdx.x; i < kLaneWords; i += blockDim.x) llane[i] = a.lanetab[i];
+    for (int i = threadIdx.x; i < 1024; i += blockDim.x) lzw[i] = a.zwin[i];
+
+    const int t = threadIdx.x;
+    const int lane = t & 63;
+    const uint32_t c = lane & 31;
+    uint32_t lb[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) lb[k] = ((uint32_t)(k >> 1) << 16) | ((uint32_t)(k & 1) << 7) | (c << 2);
+    const int gl = lane & (Q - 1);
+    const uint32_t grp = (uint32_t)t >> 4;  // 64 groups per block
+    const bool trailer = (a.flags & (RH_CRC_VERIFY | RH_CRC_STAMP)) != 0;
+    const uint32_t tl = trailer ? 4u : 0u;
+
+    for (uint64_t b0f = (uint64_t)blockIdx.x * kV8Batch; b0f < a.n; b0f += (uint64_t)gridDim.x * kV8Batch) {
+        const uint32_t nb = (uint32_t)(a.n - b0f < (uint64_t)kV8Batch ? a.n - b0f : (uint64_t)kV8Batch);
+        __syncthreads();  // previous batch done with meta / slow
+        if (t == 0) *nslow = 0;
+        __syncthreads();
+        if ((uint32_t)t < nb) {
+            const uint64_t f = b0f + (uint64_t)t;
+            const uint64_t o = a.off[f];
+            const int64_t L = (int64_t)a.len[f];
+            const bool malformed = o > (uint64_t)a.buf_len || L > a.buf_len - (int64_t)o || (trailer && L < 4);
+            MetaV8 m;
+            m.o = (int64_t)o;
+            m.lc = malformed ? 0u : (uint32_t)(L - (int64_t)tl);
+            const int64_t E = m.o + (int64_t)m.lc;
+            const bool unsafe = m.o < 67 || E + 8 > a.buf_len || m.lc < 8;
+            m.fl = malformed ? 2u : (unsafe ? 1u : 0u);
+            meta[t] = m;
+            if (m.fl) slow[atomicAdd(nslow, 1u)] = (uint32_t)t;
+        }
+        __syncthreads();
+
+        // ---- fast path: group grp walks the windows of batch frames grp, grp + 64, ... ----
+        struct Task {
+            uint32_t j;   // batch-local frame (>= nb: none)
+            uint32_t wi;  // window
+        };
+        auto skip = [&](uint32_t j) {  // next fast-path frame at or after j (stride 64)
+            while (j < nb && meta[j].fl != 0) j += 64;
+            return j;
+        };
+        auto next = [&](Task x) {
+            if (x.j >= nb) return x;
+            const uint32_t nw = (meta[x.j].lc + (uint32_t)W - 1) / (uint32_t)W;
+            if (x.wi + 1 < nw) return Task{x.j, x.wi + 1};
+            return Task{skip(x.j + 64), 0u};
+        };
+        // chunk of lane gl in task x: [be - S, be), be = E - (nw - 1 - wi) W - (Q - 1 - gl) S
+        auto load = [&](Task x, uint32_t (&dd)[18]) {
+            const uint8_t* src = a.buf;
+            if (x.j < nb) {
+                const MetaV8 m = meta[x.j];
+                const int64_t E = m.o + (int64_t)m.lc;
+                const int64_t nw = ((int64_t)m.lc + W - 1) / W;
+                const int64_t be = E - (nw - 1 - (int64_t)x.wi) * W - (int64_t)(Q - 1 - gl) * S;
+                const int64_t b0 = be - S - (int64_t)(E & 3);
+                if (be > m.o) src = a.buf + b0;  // inactive lanes: the buffer start (never used)
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const u32x4a v = *reinterpret_cast<const u32x4a*>(src + 16 * q);
+                dd[4 * q] = v.x;
+                dd[4 * q + 1] = v.y;
+                dd[4 * q + 2] = v.z;
+                dd[4 * q + 3] = v.w;
+            }
+            dd[16] = *reinterpret_cast<const uint32_t*>(src + 64);
+            dd[17] = *reinterpret_cast<const uint32_t*>(src + 68);
+        };
+        uint32_t R = 0;
+        auto fold = [&](Task x, uint32_t (&d)[18]) {
+            if (x.j >= nb) return;
+            const MetaV8 m = meta[x.j];
+            const int64_t E = m.o + (int64_t)m.lc;
+            const int64_t nw = ((int64_t)m.lc + W - 1) / W;
+            const uint32_t sh = (uint32_t)(E & 3);
+            const int64_t be = E - (nw - 1 - (int64_t)x.wi) * W - (int64_t)(Q - 1 - gl) * S;
+            const bool act = be > m.o;
+            const int64_t q0l = be - S - (int64_t)sh - m.o;  // chunk start (aligned) rel. to frame start
+            if (__any(act && q0l < 4)) {
+                const int q0 = (int)(q0l < -80 ? -80 : (q0l > 4 ? 4 : q0l));
+#pragma unroll
+                for (int i = 0; i < 17; ++i) {
+                    const int q = q0 + 4 * i;
+                    uint32_t v = d[i];
+                    v = (q <= -4) ? 0u : (q < 0 ? (v & (0xFFFFFFFFu << (8 * -q))) : v);
+                    const uint32_t up = (q >= 0 && q < 4) ? (a.init >> (8 * q)) : 0u;
+                    const uint32_t dn2 = (q < 0 && q > -4) ? (a.init << (8 * -q)) : 0u;
+                    d[i] = (act && q0l < 4) ? (v ^ up ^ dn2) : d[i];
+                }
+            }
+            uint32_t r = 0;
+            if (__all(sh == 0 || !act)) {
+#pragma unroll
+                for (int j = 0; j < 16; ++j) r = fold_word_perm(lds, r, d[j], lb);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 16; ++j) r = fold_word_perm(lds, r, __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh), lb);
+            }
+            uint32_t z = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) z ^= llane[c + ((uint32_t)(k * 16) + ((r >> (4 * k)) & 15u)) * 32u];
+            r = act ? z : 0u;
+            r ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+            r ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+            r ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r, 0x141, 0xF, 0xF, false);  // row_half_mirror
+            r ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r, 0x140, 0xF, 0xF, false);  // row_mirror
+            R = zshift(lzw, R) ^ r;
+            if ((int64_t)x.wi + 1 >= nw) {
+                if (gl == Q - 1) {  // this lane's chunk ends at E: d[16..17] hold bytes E - sh .. E + 8 - sh
+                    const uint64_t f = b0f + x.j;
+                    uint32_t state = R;
+                    if (m.lc < 4) state ^= (uint32_t)((uint64_t)a.init >> (8 * m.lc));
+                    const uint32_t value = ~state;
+                    if (a.crc_out) a.crc_out[f] = value;
+                    if (a.flags & RH_CRC_STAMP) {
+                        a.wbuf[E + 0] = (uint8_t)(value >> 24);
+                        a.wbuf[E + 1] = (uint8_t)(value >> 16);
+                        a.wbuf[E + 2] = (uint8_t)(value >> 8);
+                        a.wbuf[E + 3] = (uint8_t)value;
+                    } else if (a.flags & RH_CRC_VERIFY) {
+                        const uint32_t le = __builtin_amdgcn_alignbyte(d[17], d[16], sh);
+                        const uint32_t stored = __builtin_bswap32(le);  // big-endian trailer
+                        if (stored != value) {
+                            if (a.bad_bits)
+                                atomicOr(reinterpret_cast<unsigned long long*>(a.bad_bits + (f >> 6)), 1ull << (f & 63));
+                            if (a.n_bad) atomicAdd(a.n_bad, 1ull);
+                        }
+                    }
+                }
+                R = 0;
+            }
+        };
+        Task T0{a.buf_len >= 128 ? skip(grp) : nb, 0u};  // tiny buffers: every frame is guarded
+        Task T1 = next(T0);
+        Task T2 = next(T1);
+        uint32_t d0[18], d1[18], d2[18];
+        if (__any(T0.j < nb)) {
+            load(T0, d0);
+            load(T1, d1);
+        }
+        while (__any(T0.j < nb)) {
+            load(T2, d2);
+            fold(T0, d0);
+            T0 = next(T2);
+            if (!__any(T1.j < nb)) break;
+            load(T0, d0);
+            fold(T1, d1);
+            T1 = next(T0);
+            if (!__any(T2.j < nb)) break;
+            load(T1, d1);
+            fold(T2, d2);
+            T2 = next(T1);
+        }
+
+        // ---- guarded path: frames near the buffer ends, malformed and empty spans ----
+        __syncthreads();
+        const uint32_t ns = *nslow;
+        for (uint32_t i = grp; i < ns; i += 64) {
+            const uint32_t j = slow[i];
+            const MetaV8 m = meta[j];
+            const uint64_t f = b0f + j;
+            if (m.fl == 2) {
+                if (gl == 0) {
+                    if (a.crc_out) a.crc_out[f] = 0u;
+                    if (a.bad_bits) atomicOr(reinterpret_cast<unsigned long long*>(a.bad_bits + (f >> 6)), 1ull << (f & 63));
+                    if (a.n_bad) atomicAdd(a.n_bad, 1ull);
+                }
+                continue;
+            }
+            const int64_t E = m.o + (int64_t)m.lc;
+            const int64_t nw = ((int64_t)m.lc + W - 1) / W;
+            uint32_t Rs = 0;
+            for (int64_t wi = 0; wi < nw; ++wi) {
+                const int64_t be = E - (nw - 1 - wi) * W - (int64_t)(Q - 1 - gl) * S;
+                const int64_t bs = be - S > m.o ? be - S : m.o;
+                uint32_t r = 0;
+                for (int64_t p = bs; p < be; ++p) {  // byte-wise, reset()'s state in bytes 0..3
+                    uint32_t b = a.buf[p];
+                    if (p - m.o < 4) b ^= (a.init >> (8 * (p - m.o))) & 0xffu;
+                    r = (r >> 8) ^ a.slice[(r ^ b) & 0xffu];
+                }
+                uint32_t z = 0;
+#pragma unroll
+                for (int k = 0; k < 8; ++k) z ^= llane[c + ((uint32_t)(k * 16) + ((r >> (4 * k)) & 15u)) * 32u];
+                r = be > m.o ? z : 0u;
+#pragma unroll
+                for (int dlt = 1; dlt < Q; dlt <<= 1) r ^= __shfl_xor(r, dlt);
+                Rs = zshift(lzw, Rs) ^ r;
+            }
+            if (gl == 0) {
+                uint32_t state = Rs;
+                if (m.lc < 4) state ^= (uint32_t)((uint64_t)a.init >> (8 * m.lc));
+                const uint32_t value = ~state;
+                if (a.crc_out) a.crc_out[f] = value;
+                if (a.flags & RH_CRC_STAMP) {
+                    a.wbuf[E + 0] = (uint8_t)(value >> 24);
+                    a.wbuf[E + 1] = (uint8_t)(value >> 16);
+                    a.wbuf[E + 2] = (uint8_t)(value >> 8);
+                    a.wbuf[E + 3] = (uint8_t)value;
+                } else if (a.flags & RH_CRC_VERIFY) {
+                    const uint32_t stored = ((uint32_t)a.buf[E] << 24) | ((uint32_t)a.buf[E + 1] << 16) |
+                                            ((uint32_t)a.buf[E + 2] << 8) | (uint32_t)a.buf[E + 3];
+                    if (stored != value) {
+                        if (a.bad_bits)
+                            atomicOr(reinterpret_cast<unsigned long long*>(a.bad_bits + (f >> 6)), 1ull << (f & 63));
+                        if (a.n_bad) atomicAdd(a.n_bad, 1ull);
+                    }
+                }
+            }
+        }
+    }
+}
+
+
 struct Variant {
     int q, s;
     bool repl;
@@ -1321,15 +1579,17 @@ constexpr Variant kVariants[] = {
     {8, 128, true},    // 20: v7, 8 lanes x 128 B = 1 KiB windows, prefetch 1
     {16, 64, true},    // 21: v5 (15) with non-temporal 16-byte loads, prefetch 2
     {16, 64, true},    // 22: v5 with non-temporal loads, prefetch 1
+    {16, 64, true},    // 23: v8 (v5 fold, copy-free 3-slot ring, LDS-staged frame metadata)
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
-int g_default_variant = 15;  // v5, 16-lane 1 KiB windows, 2 windows in flight (fastest measured)
+int g_default_variant = 23;  // v8: v5's fold, copy-free 3-slot ring, LDS-staged metadata (fastest measured)
 
 template <int Q, int S, bool REPL, int V = 1, int ILP = 1>
 int launch_variant(rh_ctx* ctx, const FrameArgs& fa, hipStream_t stream) {
     constexpr int LOGQ = __builtin_ctz(Q);
-    constexpr size_t lds = V >= 5 ? (size_t)128 * 1024 + (size_t)(Q > 32 ? Q / 32 : 1) * 16384 + 4096
+    constexpr size_t lds = V == 9 ? (size_t)128 * 1024 + 16384 + 4096 + kV8Batch * sizeof(MetaV8) + kV8Batch * 4 + 16
+                         : V >= 5 ? (size_t)128 * 1024 + (size_t)(Q > 32 ? Q / 32 : 1) * 16384 + 4096
                          : V == 4 ? (REPL ? 4 * 256 * 32 * 4 : 4 * 256 * 4) + (size_t)(Q > 32 ? Q / 32 : 1) * 16384 + 4096 +
                                         (ILP == 2 ? 4096 : 0)
                                   : (REPL ? 4 * 256 * 32 * 4 : 4 * 256 * 4) + (size_t)(LOGQ + 1) * 4096 + (ILP == 2 ? 4096 : 0);
@@ -1337,7 +1597,9 @@ int launch_variant(rh_ctx* ctx, const FrameArgs& fa, hipStream_t stream) {
     const int block = REPL ? 1024 : 256;
     const int per_cu = REPL ? 1 : 4;
     void (*kern)(FrameArgs);
-    if constexpr (V == 7)
+    if constexpr (V == 9)
+        kern = crc_frames_kernel8<ILP>;
+    else if constexpr (V == 7)
         kern = crc_frames_kernel7<Q, S, ILP>;
     else if constexpr (V == 5 || V == 8)
         kern = crc_frames_kernel5<Q, ILP, V == 8>;  // ILP carries the prefetch depth; 8 = NT loads
@@ -1357,7 +1619,7 @@ int launch_variant(rh_ctx* ctx, const FrameArgs& fa, hipStream_t stream) {
     }
     const uint64_t groups = (fa.n + (64 / Q) - 1) / (64 / Q);   // wave-iterations needed
     uint64_t grid = (uint64_t)ctx->num_cus * per_cu;
-    const uint64_t need = (groups + (block / 64) - 1) / (block / 64);
+    const uint64_t need = V == 9 ? (fa.n + kV8Batch - 1) / kV8Batch : (groups + (block / 64) - 1) / (block / 64);
     if (need < grid) grid = need ? need : 1;
     FrameArgs a = fa;
     // per-level shift tables: S*2^j for j < LOGQ, then W
@@ -1451,6 +1713,7 @@ int rh_crc_launch_variant(rh_ctx* ctx, const rh_frames* f, uint32_t flags, int v
         case 20: return launch_variant<8, 128, true, 7, 1>(ctx, a, stream);
         case 21: return launch_variant<16, 64, true, 8, 2>(ctx, a, stream);
         case 22: return launch_variant<16, 64, true, 8, 1>(ctx, a, stream);
+        case 23: return launch_variant<16, 64, true, 9, 2>(ctx, a, stream);
     }
     return rh::fail(RH_E_INVAL, "unknown CRC kernel variant");
 }
