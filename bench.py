@@ -379,12 +379,12 @@ def main():
                "workload": f"config5: {args.crc_segments} x 32 MiB segments/GPU, 4 KiB frames "
                            f"({fb.n} frames/GPU, {ss.corrupted.size} corrupted)",
                "ms_per_pass": round(crc_ms, 4), "mismatches_found": int(bad.size), "parity_ok": crc_ok,
-               "variant": args.crc_variant if args.crc_variant is not None else 23,
+               "variant": args.crc_variant if args.crc_variant is not None else 24,
                "roofline": {"bound": "hbm", "achieved": round(crc_ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                             "frac": round(crc_ach / HBM_PEAK_GBPS, 4),
                             "traffic": (round(pmc["crc_bytes_per_unit"] * fb.n) if "crc_bytes_per_unit" in pmc else None),
                             "traffic_source": pmc.get("_path"),
-                            "kernel": "crc_frames_kernel8<2> (variant 23: copy-free 3-slot ring, LDS-staged frame table)",
+                            "kernel": "crc_frames_kernel8<2,2> (variant 24: copy-free 3-slot ring, LDS-staged frame table, 2 fold chains/lane)",
                             "algorithmic_bytes_per_launch": crc_alg, "avg_launch_ms": round(crc_kern_ms, 4)}}
         # ---- read path: framing walk, then framing + verify, over the same segment images
         n_seg = args.crc_segments

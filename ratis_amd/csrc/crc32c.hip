@@ -1314,9 +1314,10 @@ struct MetaV8 {
     uint32_t fl;  // 0 = fast path; 1 = slow path (guarded), 2 = malformed
 };
 
-template <int PF>
+template <int PF, int CH = 1>
 __global__ __launch_bounds__(1024) void crc_frames_kernel8(FrameArgs a) {
     static_assert(PF == 2, "v8 ring: 3 slots");
+    static_assert(CH == 1 || CH == 2 || CH == 4, "fold chains per lane");
     constexpr int Q = 16, S = 64;
     constexpr int64_t W = (int64_t)Q * S;
     constexpr int kSliceBytes = 128 * 1024;
@@ -1325,15 +1326,21 @@ __global__ __launch_bounds__(1024) void crc_frames_kernel8(FrameArgs a) {
     if (__builtin_amdgcn_groupstaticsize() != 0) __builtin_trap();  // lds_word assumes base 0
     uint32_t* llane = lds + kSliceBytes / 4;
     uint32_t* lzw = llane + kLaneWords;
-    MetaV8* meta = reinterpret_cast<MetaV8*>(lzw + 1024);
-    uint32_t* slow = reinterpret_cast<uint32_t*>(meta + kV8Batch);  // [kV8Batch] slow-path frames
-    uint32_t* nslow = slow + kV8Batch;
+    uint32_t* lch = lzw + 1024;  // [4][256]: advance over 64 / CH zero bytes (chain combine)
+    // batch frame table, struct-of-arrays: start, CRC-covered length, path; then the guarded list
+    int64_t* mo = reinterpret_cast<int64_t*>(lch + 1024);
+    uint32_t* mlc = reinterpret_cast<uint32_t*>(mo + kV8Batch);
+    uint8_t* mfl = reinterpret_cast<uint8_t*>(mlc + kV8Batch);
+    uint16_t* slow = reinterpret_cast<uint16_t*>(mfl + kV8Batch);  // [kV8Batch] guarded-path frames
+    uint32_t* nslow = reinterpret_cast<uint32_t*>(slow + kV8Batch);
+    auto meta = [&](uint32_t j) { return MetaV8{mo[j], mlc[j], mfl[j]}; };
     for (int i = threadIdx.x; i < kSliceBytes / 4; i += blockDim.x) {
         const int region = i >> 14, e = (i >> 6) & 255, half = (i >> 5) & 1;
         lds[i] = a.slice[((region * 2 + half) << 8) | e];
     }
     for (int i = threadIdx.x; i < kLaneWords; i += blockDim.x) llane[i] = a.lanetab[i];
     for (int i = threadIdx.x; i < 1024; i += blockDim.x) lzw[i] = a.zwin[i];
+    for (int i = threadIdx.x; i < 1024; i += blockDim.x) lch[i] = a.shift32[i];
 
     const int t = threadIdx.x;
     const int lane = t & 63;
@@ -1362,8 +1369,10 @@ __global__ __launch_bounds__(1024) void crc_frames_kernel8(FrameArgs a) {
             const int64_t E = m.o + (int64_t)m.lc;
             const bool unsafe = m.o < 67 || E + 8 > a.buf_len || m.lc < 8;
             m.fl = malformed ? 2u : (unsafe ? 1u : 0u);
-            meta[t] = m;
-            if (m.fl) slow[atomicAdd(nslow, 1u)] = (uint32_t)t;
+            mo[t] = m.o;
+            mlc[t] = m.lc;
+            mfl[t] = (uint8_t)m.fl;
+            if (m.fl) slow[atomicAdd(nslow, 1u)] = (uint16_t)t;
         }
         __syncthreads();
 
@@ -1373,12 +1382,12 @@ __global__ __launch_bounds__(1024) void crc_frames_kernel8(FrameArgs a) {
             uint32_t wi;  // window
         };
         auto skip = [&](uint32_t j) {  // next fast-path frame at or after j (stride 64)
-            while (j < nb && meta[j].fl != 0) j += 64;
+            while (j < nb && mfl[j] != 0) j += 64;
             return j;
         };
         auto next = [&](Task x) {
             if (x.j >= nb) return x;
-            const uint32_t nw = (meta[x.j].lc + (uint32_t)W - 1) / (uint32_t)W;
+            const uint32_t nw = (mlc[x.j] + (uint32_t)W - 1) / (uint32_t)W;
             if (x.wi + 1 < nw) return Task{x.j, x.wi + 1};
             return Task{skip(x.j + 64), 0u};
         };
@@ -1386,7 +1395,7 @@ __global__ __launch_bounds__(1024) void crc_frames_kernel8(FrameArgs a) {
         auto load = [&](Task x, uint32_t (&dd)[18]) {
             const uint8_t* src = a.buf;
             if (x.j < nb) {
-                const MetaV8 m = meta[x.j];
+                const MetaV8 m = meta(x.j);
                 const int64_t E = m.o + (int64_t)m.lc;
                 const int64_t nw = ((int64_t)m.lc + W - 1) / W;
                 const int64_t be = E - (nw - 1 - (int64_t)x.wi) * W - (int64_t)(Q - 1 - gl) * S;
@@ -1407,7 +1416,7 @@ __global__ __launch_bounds__(1024) void crc_frames_kernel8(FrameArgs a) {
         uint32_t R = 0;
         auto fold = [&](Task x, uint32_t (&d)[18]) {
             if (x.j >= nb) return;
-            const MetaV8 m = meta[x.j];
+            const MetaV8 m = meta(x.j);
             const int64_t E = m.o + (int64_t)m.lc;
             const int64_t nw = ((int64_t)m.lc + W - 1) / W;
             const uint32_t sh = (uint32_t)(E & 3);
@@ -1426,14 +1435,27 @@ __global__ __launch_bounds__(1024) void crc_frames_kernel8(FrameArgs a) {
                     d[i] = (act && q0l < 4) ? (v ^ up ^ dn2) : d[i];
                 }
             }
-            uint32_t r = 0;
+            // CH independent chains of 16 / CH words (the LDS round trips overlap), joined by
+            // Horner steps over 64 / CH zero bytes: CRC(A||B) = adv_|B|(crc A) ^ crc B from zero
+            constexpr int LW = 16 / CH;
+            uint32_t rc[CH];
+#pragma unroll
+            for (int q = 0; q < CH; ++q) rc[q] = 0;
             if (__all(sh == 0 || !act)) {
 #pragma unroll
-                for (int j = 0; j < 16; ++j) r = fold_word_perm(lds, r, d[j], lb);
+                for (int j = 0; j < LW; ++j)
+#pragma unroll
+                    for (int q = 0; q < CH; ++q) rc[q] = fold_word_perm(lds, rc[q], d[q * LW + j], lb);
             } else {
 #pragma unroll
-                for (int j = 0; j < 16; ++j) r = fold_word_perm(lds, r, __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh), lb);
+                for (int j = 0; j < LW; ++j)
+#pragma unroll
+                    for (int q = 0; q < CH; ++q)
+                        rc[q] = fold_word_perm(lds, rc[q], __builtin_amdgcn_alignbyte(d[q * LW + j + 1], d[q * LW + j], sh), lb);
             }
+            uint32_t r = rc[0];
+#pragma unroll
+            for (int q = 1; q < CH; ++q) r = zshift(lch, r) ^ rc[q];
             uint32_t z = 0;
 #pragma unroll
             for (int k = 0; k < 8; ++k) z ^= llane[c + ((uint32_t)(k * 16) + ((r >> (4 * k)) & 15u)) * 32u];
@@ -1495,7 +1517,7 @@ __global__ __launch_bounds__(1024) void crc_frames_kernel8(FrameArgs a) {
         const uint32_t ns = *nslow;
         for (uint32_t i = grp; i < ns; i += 64) {
             const uint32_t j = slow[i];
-            const MetaV8 m = meta[j];
+            const MetaV8 m = meta(j);
             const uint64_t f = b0f + j;
             if (m.fl == 2) {
                 if (gl == 0) {
@@ -1580,15 +1602,17 @@ constexpr Variant kVariants[] = {
     {16, 64, true},    // 21: v5 (15) with non-temporal 16-byte loads, prefetch 2
     {16, 64, true},    // 22: v5 with non-temporal loads, prefetch 1
     {16, 64, true},    // 23: v8 (v5 fold, copy-free 3-slot ring, LDS-staged frame metadata)
+    {16, 64, true},    // 24: v8 with 2 independent fold chains per lane
+    {16, 64, true},    // 25: v8 with 4 independent fold chains per lane
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
-int g_default_variant = 23;  // v8: v5's fold, copy-free 3-slot ring, LDS-staged metadata (fastest measured)
+XX
 
 template <int Q, int S, bool REPL, int V = 1, int ILP = 1>
 int launch_variant(rh_ctx* ctx, const FrameArgs& fa, hipStream_t stream) {
     constexpr int LOGQ = __builtin_ctz(Q);
-    constexpr size_t lds = V == 9 ? (size_t)128 * 1024 + 16384 + 4096 + kV8Batch * sizeof(MetaV8) + kV8Batch * 4 + 16
+    constexpr size_t lds = V >= 9 ? (size_t)128 * 1024 + 16384 + 8192 + kV8Batch * 15 + 16
                          : V >= 5 ? (size_t)128 * 1024 + (size_t)(Q > 32 ? Q / 32 : 1) * 16384 + 4096
                          : V == 4 ? (REPL ? 4 * 256 * 32 * 4 : 4 * 256 * 4) + (size_t)(Q > 32 ? Q / 32 : 1) * 16384 + 4096 +
                                         (ILP == 2 ? 4096 : 0)
@@ -1597,8 +1621,8 @@ int launch_variant(rh_ctx* ctx, const FrameArgs& fa, hipStream_t stream) {
     const int block = REPL ? 1024 : 256;
     const int per_cu = REPL ? 1 : 4;
     void (*kern)(FrameArgs);
-    if constexpr (V == 9)
-        kern = crc_frames_kernel8<ILP>;
+    if constexpr (V == 9 || V == 10 || V == 11)
+        kern = crc_frames_kernel8<ILP, V == 9 ? 1 : (V == 10 ? 2 : 4)>;
     else if constexpr (V == 7)
         kern = crc_frames_kernel7<Q, S, ILP>;
     else if constexpr (V == 5 || V == 8)
@@ -1619,12 +1643,12 @@ int launch_variant(rh_ctx* ctx, const FrameArgs& fa, hipStream_t stream) {
     }
     const uint64_t groups = (fa.n + (64 / Q) - 1) / (64 / Q);   // wave-iterations needed
     uint64_t grid = (uint64_t)ctx->num_cus * per_cu;
-    const uint64_t need = V == 9 ? (fa.n + kV8Batch - 1) / kV8Batch : (groups + (block / 64) - 1) / (block / 64);
+    const uint64_t need = V >= 9 ? (fa.n + kV8Batch - 1) / kV8Batch : (groups + (block / 64) - 1) / (block / 64);
     if (need < grid) grid = need ? need : 1;
     FrameArgs a = fa;
     // per-level shift tables: S*2^j for j < LOGQ, then W
     a.shift = ctx->d_shift + (size_t)__builtin_ctz(S) * 1024;
-    a.shift32 = ctx->d_shift + (size_t)5 * 1024;
+    a.shift32 = ctx->d_shift + (size_t)(V == 11 ? 4 : 5) * 1024;  // v8 chain combine: 64 / CH bytes
     a.zwin = ctx->d_shift + (size_t)__builtin_ctz(Q * S) * 1024;
     if constexpr (S == 128)
         a.lanetab = Q == 16 ? ctx->d_lane16_s128 : ctx->d_lane8_s128;
@@ -1714,6 +1738,8 @@ int rh_crc_launch_variant(rh_ctx* ctx, const rh_frames* f, uint32_t flags, int v
         case 21: return launch_variant<16, 64, true, 8, 2>(ctx, a, stream);
         case 22: return launch_variant<16, 64, true, 8, 1>(ctx, a, stream);
         case 23: return launch_variant<16, 64, true, 9, 2>(ctx, a, stream);
+        case 24: return launch_variant<16, 64, true, 10, 2>(ctx, a, stream);
+        case 25: return launch_variant<16, 64, true, 11, 2>(ctx, a, stream);
     }
     return rh::fail(RH_E_INVAL, "unknown CRC kernel variant");
 }

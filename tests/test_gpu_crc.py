@@ -44,7 +44,7 @@ def test_rfc3720_known_answers(ctx):
         assert engine.crc32c_bytes(ctx, _dev(data)) == int(v["crc"], 16), v["name"]
 
 
-@pytest.mark.parametrize("variant", list(range(24)))
+@pytest.mark.parametrize("variant", list(range(26)))
 def test_every_length_and_alignment(ctx, orc, variant):
     """Spans of every length 0..700 at every start alignment 0..15 (plain spans, flags=0)."""
     import torch
@@ -202,7 +202,7 @@ def test_frames_at_buffer_end_and_malformed(ctx, orc):
         assert int(fb.crc_out[0].item()) & 0xFFFFFFFF == c
 
 
-@pytest.mark.parametrize("variant", list(range(24)))
+@pytest.mark.parametrize("variant", list(range(26)))
 def test_config5_segments_reduced(ctx, orc, variant):
     """BASELINE config 5 shape (32 MiB segments, 4 KiB frames), 6 segments: every frame verifies
     except the planted corruptions; the segment parses as a valid Ratis segment in the oracle."""
