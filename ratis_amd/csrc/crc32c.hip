@@ -1607,7 +1607,7 @@ constexpr Variant kVariants[] = {
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
-XX
+int g_default_variant = 24;  // v8 with 2 fold chains per lane (fastest measured)
 
 template <int Q, int S, bool REPL, int V = 1, int ILP = 1>
 int launch_variant(rh_ctx* ctx, const FrameArgs& fa, hipStream_t stream) {
