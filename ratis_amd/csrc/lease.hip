@@ -25,7 +25,13 @@ typedef int64_t v2i64 __attribute__((ext_vector_type(2)));
 typedef uint32_t v2u32 __attribute__((ext_vector_type(2)));
 using rh_bits::spread32;
 
-__device__ __forceinline__ int64_t elapsed_ms(int64_t d) { return d / 1000000; }  // truncating, as Java
+// Timestamp.elapsedTimeMs < timeout, division-free: for timeout T >= 0 (the launcher rejects T < 0),
+// trunc(d / 10^6) < T  <=>  d <= lim(T), lim(0) = -10^6, lim(T >= 1) = T * 10^6 - 1 (saturating).
+// One int64 compare instead of a 64-bit division by a constant per timestamp.
+__device__ __forceinline__ int64_t ms_limit(int64_t T) {
+    return T == 0 ? -1000000 : (T > INT64_MAX / 1000000 ? INT64_MAX : T * 1000000 - 1);
+}
+__device__ __forceinline__ bool ms_below(int64_t d, int64_t lim) { return d <= lim; }
 
 // ((cnt-1)/2)-th smallest of the members' elapsed times; 0 (= currentTime()) for an empty list.
 template <int F>
@@ -58,12 +64,13 @@ template <int F>
 __device__ __forceinline__ void lease_one(const rh_lease_soa& t, const int64_t (&ts)[F > 0 ? F : 1], uint32_t w,
                                           int64_t lin, bool en, bool in, int64_t& lout, bool& has, bool& ext) {
     const int64_t now = t.now_nanos;
+    const int64_t lim = ms_limit(t.timeout_ms);
     int64_t d[F > 0 ? F : 1];
     uint32_t act = 0;
 #pragma unroll
     for (int k = 0; k < F; ++k) {
         d[k] = (int64_t)((uint64_t)now - (uint64_t)ts[k]);
-        act |= (elapsed_ms(d[k]) < t.timeout_ms ? 1u : 0u) << k;
+        act |= (ms_below(d[k], lim) ? 1u : 0u) << k;
     }
     const uint32_t nm = w & 0x3FFFu, om = (w >> 16) & 0x3FFFu;
     const bool self = (w & RH_CONF_SELF) != 0, self_old = (w & RH_CONF_SELF_OLD) != 0;
@@ -72,7 +79,7 @@ __device__ __forceinline__ void lease_one(const rh_lease_soa& t, const int64_t (
     const int cur_size = __builtin_popcount(nm) + (self ? 1 : 0);
     const int prev_size = trans ? __builtin_popcount(om) + (self_old ? 1 : 0) : 0;
     const bool singleton = cur_size == 1 && prev_size <= 1;
-    const bool valid_in = singleton || elapsed_ms((int64_t)((uint64_t)now - (uint64_t)lin)) < t.timeout_ms;
+    const bool valid_in = singleton || ms_below((int64_t)((uint64_t)now - (uint64_t)lin), lim);
     const bool maj = has_majority(nm, act, self) && (!trans || has_majority(om, act, self_old));
     ext = in && active && en && !valid_in && maj;
     lout = lin;
@@ -83,7 +90,7 @@ __device__ __forceinline__ void lease_one(const rh_lease_soa& t, const int64_t (
         // Timestamp.earliest(a, b) = a.compareTo(b) > 0 ? b : a, with a - b == dold - dc (wrapping)
         const int64_t dn = (int64_t)((uint64_t)dold - (uint64_t)dc) > 0 ? dold : dc;
         lout = (int64_t)((uint64_t)now - (uint64_t)dn);
-        has = singleton || elapsed_ms(dn) < t.timeout_ms;
+        has = singleton || ms_below(dn, lim);
     }
 }
 

@@ -131,3 +131,21 @@ def test_lease_bad_arguments(ctx):
                           lease_in=torch.zeros(8, dtype=torch.int64, device="cuda")).alloc_outputs()
     with pytest.raises(_lib.IllegalArgumentError):
         engine.lease_launch(ctx, [t2], NOW, -1)
+
+
+@pytest.mark.parametrize("timeout_ms", [0, 1, 7, 9_223_372_036_854, 9_223_372_036_855, (1 << 62)])
+def test_lease_ms_threshold_exact(ctx, orc, timeout_ms):
+    """The kernel's division-free form of elapsedTimeMs < timeout (d <= lim(T)) at every edge of the
+    truncating millisecond division: d = k*10^6 - 1, k*10^6, k*10^6 + 1 for k around T and around
+    -1, 0, and the saturation of T*10^6 near INT64_MAX."""
+    rng = np.random.default_rng(5 + timeout_ms % 1000)
+    T = min(timeout_ms, 9_223_372_036_854)
+    ks = [-2, -1, 0, 1, T - 1, T, T + 1]
+    ds = sorted({k * MS + e for k in ks for e in (-1, 0, 1) if abs(k * MS + e) < (1 << 62)})
+    n, F = 4 * len(ds) * 8, 4
+    ts, conf, lease_in = random_lease_tier(rng, n, F, timeout_ms=100, joint_rate=0.3)
+    pick = np.array(ds, dtype=np.int64)
+    ts[:, :] = NOW - pick[rng.integers(0, len(ds), size=(F, n))]
+    lease_in[:] = NOW - pick[rng.integers(0, len(ds), size=n)]
+    ref = orc.lease_soa(ts, conf, lease_in, NOW, timeout_ms)
+    assert_same(ref, run_gpu(ctx, ts, conf, lease_in, timeout_ms))
