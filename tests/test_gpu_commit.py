@@ -222,6 +222,66 @@ def test_full_size_config3_parity(ctx, orc):
             assert 0.01 < adv.mean() < 0.99   # both branches of the commit decision are exercised
 
 
+def test_full_size_config2_parity(ctx, orc):
+    """BASELINE config 2 at full size: 100k groups x 3 peers (stable confs), both gap settings."""
+    import torch
+
+    from ratis_amd import engine, workload
+    tiers_h = workload.commit_snapshot(100_000, joint_frac=0.0, peers=3)
+    for gap in (-1, 2048):
+        tiers = [workload.to_device(h, gap_threshold=gap).alloc_outputs(mode=0) for h in tiers_h]
+        engine.commit_launch(ctx, tiers, mode=0)
+        torch.cuda.synchronize()
+        for h, t in zip(tiers_h, tiers):
+            ref = orc.commit_soa(h.follower, h.flush, h.conf, mode=0, gap=gap, commit_in=h.commit,
+                                 term_start=h.term_start)
+            assert np.array_equal(t.commit_out.cpu().numpy(), ref["commit"])
+            assert np.array_equal(t.min_out.cpu().numpy(), ref["min"])
+
+
+def test_full_size_config4_sharded(ctx, orc):
+    """BASELINE config 4 at full size: 8M groups x 5 peers (10 % joint) placed on 8 shards by
+    floorMod(RaftGroupId.hashCode(), 8) (shard.py), each shard launched on its own as one rank
+    would.  Every shard equals the oracle, and the shards together equal one launch over all 8M
+    groups (groups are independent: sharding changes nothing)."""
+    import torch
+
+    from ratis_amd import engine, shard, workload
+    n = 8_000_000
+    tiers_h = workload.commit_snapshot(n, joint_frac=0.1, peers=5, seed=workload.SEED + 4)
+    msb, lsb = shard.random_group_ids(n, seed=44)
+    sh = shard.shard_of(msb, lsb, 8)
+    counts = np.bincount(sh, minlength=8)
+    assert counts.min() > 0.95 * n / 8 and counts.max() < 1.05 * n / 8   # hash spreads evenly
+    off = 0
+    whole = {}
+    for ti, h in enumerate(tiers_h):
+        idx_all = np.arange(off, off + h.n)
+        off += h.n
+        ref = orc.commit_soa(h.follower, h.flush, h.conf, mode=0, gap=-1, commit_in=h.commit,
+                             term_start=h.term_start)
+        got_commit = np.empty(h.n, np.int64)
+        got_min = np.empty(h.n, np.int64)
+        for r in range(8):
+            sel = np.nonzero(sh[idx_all] == r)[0]
+            part = workload.HostTier(h.follower[:, sel], h.flush[sel], h.commit[sel], h.term_start[sel],
+                                     h.conf[sel], h.voters_union[sel])
+            t = workload.to_device(part).alloc_outputs(mode=0)
+            engine.commit_launch(ctx, [t], mode=0)
+            torch.cuda.synchronize()
+            got_commit[sel] = t.commit_out.cpu().numpy()
+            got_min[sel] = t.min_out.cpu().numpy()
+            del t
+        assert np.array_equal(got_commit, ref["commit"]), ti
+        assert np.array_equal(got_min, ref["min"]), ti
+        whole[ti] = got_commit
+    tiers = [workload.to_device(h).alloc_outputs(mode=0) for h in tiers_h]
+    engine.commit_launch(ctx, tiers, mode=0)
+    torch.cuda.synchronize()
+    for ti, t in enumerate(tiers):
+        assert np.array_equal(t.commit_out.cpu().numpy(), whole[ti])
+
+
 def test_group_table_api_with_deltas(ctx, orc):
     """RaftGroupTable (rh_groups_*): bulk load, delta streaming (updateToMax), batched
     updateCommit and commitIndexChanged, against the oracle replaying the same host state."""

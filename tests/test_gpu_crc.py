@@ -228,3 +228,29 @@ def test_config5_segments_reduced(ctx, orc, variant):
         assert np.array_equal(crcs, fb.crc_out[:n0].cpu().numpy().view(np.uint32))
     else:
         assert st == orc.ORC_E_CHECKSUM and offs.size == first_bad
+
+
+def test_config5_full_size_one_gpu_share(ctx, orc):
+    """BASELINE config 5 at its full per-GPU size (256 x 32 MiB segments = 8 GiB of 4 KiB frames,
+    one GPU's share of the 64 GB run) with planted corruptions, default kernel: the mismatch set is
+    exactly the planted set, the mismatch count matches, and 64 frames spread over the buffer
+    equal the oracle's PureJavaCrc32C (size-independent checks at the full size)."""
+    import torch
+
+    from ratis_amd import _lib, engine, workload
+    ss = workload.synth_segments(ctx, n_segments=256, corrupt_rate=1e-6, seed=5)
+    fb = ss.batch
+    fb.n_bad.zero_()
+    fb.bad_bits.zero_()
+    engine.crc32c_frames(ctx, fb, flags=_lib.RH_CRC_VERIFY)
+    torch.cuda.synchronize()
+    bad = np.nonzero(_bits(fb.bad_bits.cpu().numpy(), fb.n))[0]
+    assert np.array_equal(bad, ss.corrupted) and ss.corrupted.size > 0
+    assert int(fb.n_bad.item()) == ss.corrupted.size
+    offs = fb.frame_off.cpu().numpy()
+    got = fb.crc_out.cpu().numpy().view(np.uint32)
+    for i in np.linspace(0, fb.n - 1, 64).astype(np.int64):
+        fr = fb.buf[int(offs[i]): int(offs[i]) + ss.frame_size - 4].cpu().numpy().tobytes()
+        assert orc.crc32c(fr) == int(got[i])
+    del ss, fb
+    torch.cuda.empty_cache()
