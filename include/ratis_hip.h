@@ -335,7 +335,11 @@ int rh_segments_read_profile(int enable, uint64_t* out, uint64_t n);
  *   11-13 v4: per-lane zero-advance (lane-distance nibble tables) instead of the tree
  *   14-17 v5: v4 + one-v_perm table addressing; 14: 1 window in flight, 15: 2, 16: 3,
  *         17: 32-lane windows, 2 in flight
- *   18-20 v7: 128-byte lane chunks;  21-22 v5 with non-temporal loads (2 / 1 windows in flight) */
+ *   18-20 v7: 128-byte lane chunks;  21-22 v5 with non-temporal loads (2 / 1 windows in flight)
+ *   23-25 v8: copy-free 3-slot ring + LDS-staged frame table, 1 / 2 / 4 fold chains per lane
+ *         (24 = default).  rh_crc32c_num_variants() counts these exact kernels (26); index 26
+ *         (rh_crc32c_frames_launch_variant only) is an access-pattern ablation whose CRCs are
+ *         NOT PureJavaCrc32C values. */
 /* Commit kernel variants (see commit.hip): 0-2 sorting network with 1/2/4 sub-tiles of 128
  * groups per wave; 3 split F classes; 4-7 persistent software-pipelined; 8-14 rank-mask
  * selection at 8 waves/SIMD (12-14 with non-temporal loads); 15 = 0 with non-temporal loads. */

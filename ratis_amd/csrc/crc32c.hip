@@ -1314,7 +1314,7 @@ struct MetaV8 {
     uint32_t fl;  // 0 = fast path; 1 = slow path (guarded), 2 = malformed
 };
 
-template <int PF, int CH = 1>
+template <int PF, int CH = 1, bool ABLATE = false>
 __global__ __launch_bounds__(1024) void crc_frames_kernel8(FrameArgs a) {
     static_assert(PF == 2, "v8 ring: 3 slots");
     static_assert(CH == 1 || CH == 2 || CH == 4, "fold chains per lane");
@@ -1441,7 +1441,8 @@ __global__ __launch_bounds__(1024) void crc_frames_kernel8(FrameArgs a) {
             uint32_t rc[CH];
 #pragma unroll
             for (int q = 0; q < CH; ++q) rc[q] = 0;
-            if (__all(sh == 0 || !act)) {
+            if (ABLATE) {
+            } else if (__all(sh == 0 || !act)) {
 #pragma unroll
                 for (int j = 0; j < LW; ++j)
 #pragma unroll
@@ -1456,6 +1457,11 @@ __global__ __launch_bounds__(1024) void crc_frames_kernel8(FrameArgs a) {
             uint32_t r = rc[0];
 #pragma unroll
             for (int q = 1; q < CH; ++q) r = zshift(lch, r) ^ rc[q];
+            if (ABLATE) {  // access-pattern ablation: same loads and outputs, no table work
+                r = 0;
+#pragma unroll
+                for (int j = 0; j < 17; ++j) r ^= d[j];
+            }
             uint32_t z = 0;
 #pragma unroll
             for (int k = 0; k < 8; ++k) z ^= llane[c + ((uint32_t)(k * 16) + ((r >> (4 * k)) & 15u)) * 32u];
@@ -1604,8 +1610,10 @@ constexpr Variant kVariants[] = {
     {16, 64, true},    // 23: v8 (v5 fold, copy-free 3-slot ring, LDS-staged frame metadata)
     {16, 64, true},    // 24: v8 with 2 independent fold chains per lane
     {16, 64, true},    // 25: v8 with 4 independent fold chains per lane
+    {16, 64, true},    // 26: ABLATION ONLY (wrong CRCs): v8's loads and stores without the table fold
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
+constexpr int kAblationVariant = 26;  // launchable by index for A/B, not counted as a CRC kernel
 
 int g_default_variant = 24;  // v8 with 2 fold chains per lane (fastest measured)
 
@@ -1621,7 +1629,9 @@ int launch_variant(rh_ctx* ctx, const FrameArgs& fa, hipStream_t stream) {
     const int block = REPL ? 1024 : 256;
     const int per_cu = REPL ? 1 : 4;
     void (*kern)(FrameArgs);
-    if constexpr (V == 9 || V == 10 || V == 11)
+    if constexpr (V == 12)
+        kern = crc_frames_kernel8<ILP, 1, true>;
+    else if constexpr (V == 9 || V == 10 || V == 11)
         kern = crc_frames_kernel8<ILP, V == 9 ? 1 : (V == 10 ? 2 : 4)>;
     else if constexpr (V == 7)
         kern = crc_frames_kernel7<Q, S, ILP>;
@@ -1740,6 +1750,7 @@ int rh_crc_launch_variant(rh_ctx* ctx, const rh_frames* f, uint32_t flags, int v
         case 23: return launch_variant<16, 64, true, 9, 2>(ctx, a, stream);
         case 24: return launch_variant<16, 64, true, 10, 2>(ctx, a, stream);
         case 25: return launch_variant<16, 64, true, 11, 2>(ctx, a, stream);
+        case 26: return launch_variant<16, 64, true, 12, 2>(ctx, a, stream);
     }
     return rh::fail(RH_E_INVAL, "unknown CRC kernel variant");
 }
@@ -1749,9 +1760,9 @@ int rh_crc_launch_impl(rh_ctx* ctx, const rh_frames* f, uint32_t flags, hipStrea
 }
 
 int rh_crc_set_default_variant(int v) {
-    if (v < 0 || v >= kNumVariants) return rh::fail(RH_E_INVAL, "unknown CRC kernel variant");
+    if (v < 0 || v >= kAblationVariant) return rh::fail(RH_E_INVAL, "unknown CRC kernel variant");
     g_default_variant = v;
     return RH_OK;
 }
 
-int rh_crc_num_variants() { return kNumVariants; }
+int rh_crc_num_variants() { return kAblationVariant; }  // exact variants 0..25

@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", default="crc,framing,commit,lease", help="comma list of sections to run")
+    ap.add_argument("--ablation", action="store_true", help="also time the CRC access-pattern ablation")
     a = ap.parse_args()
     import torch
 
@@ -41,6 +42,27 @@ def main():
     fb = ss.batch
     only = set(a.only.split(","))
     nv = engine.crc32c_num_variants() if "crc" in only else 0
+    if "crc" in only and a.ablation:
+        # access-pattern ablation (variant nv): v8's loads and stores, no table fold
+        for r in range(a.rounds):
+            engine.crc32c_frames(ctx, fb, flags=0, variant=nv)   # no verify: its CRCs are not exact
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(a.iters):
+                engine.crc32c_frames(ctx, fb, flags=0, variant=nv)
+            e1.record()
+            torch.cuda.synchronize()
+            print(json.dumps({"kernel": "crc32c_ablation_loads_only", "variant": nv,
+                              "GBps": round(ss.frame_bytes / (e0.elapsed_time(e1) / a.iters * 1e-3) / 1e9, 1)}), flush=True)
+            # the same kernel, exact variant 24, also without verify (same comparison basis)
+            engine.crc32c_frames(ctx, fb, flags=0, variant=24)
+            e0.record()
+            for _ in range(a.iters):
+                engine.crc32c_frames(ctx, fb, flags=0, variant=24)
+            e1.record()
+            torch.cuda.synchronize()
+            print(json.dumps({"kernel": "crc32c_no_verify", "variant": 24,
+                              "GBps": round(ss.frame_bytes / (e0.elapsed_time(e1) / a.iters * 1e-3) / 1e9, 1)}), flush=True)
     res = {v: [] for v in range(nv)}
     for r in range(a.rounds):
         for v in range(nv):
