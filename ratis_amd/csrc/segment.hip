@@ -530,6 +530,53 @@ __global__ __launch_bounds__(kBlock2) void segment_walk_kernel2(SegArgs a) {
                         prev_fl = last_fl;
                         last_fl = (uint32_t)(total + 4);
                     }
+                    // Header fast-forward: the window ended inside a run of equal lengths s, so
+                    // the run is followed straight through HBM, reading only frame HEADERS: each
+                    // round lane j loads the headers at p + j*s and p + (64+j)*s (two 8-byte
+                    // reads) and the leading run of frames that pass the fast loop's predicate
+                    // with length s is accepted -- up to 128 frames per round trip, the payload
+                    // bytes never touched (they are the CRC pass's).  The first frame that breaks
+                    // the run (or the segment tail) sends the block back to the LDS window walk,
+                    // restarting the ring at the new position.
+                    if (st == kWalking && p >= wend && last_fl == prev_fl && last_fl != 0 &&
+                        last_fl <= (1u << 24) && L <= 0x7fffffff) {
+                        const uint32_t sd = last_fl, pend32 = (uint32_t)(L - 8 > 0 ? L - 8 : 0);
+                        for (;;) {
+                            if (p >= (int64_t)pend32) break;
+                            const uint32_t p32 = (uint32_t)p;
+                            uint32_t okm[2];
+#pragma unroll
+                            for (int h = 0; h < 2; ++h) {
+                                const uint32_t cj = p32 + (uint32_t)(lane + 64 * h) * sd;  // < 2^31 + 2^31
+                                const bool okp = cj < pend32;
+                                const uint64_t ga = (uint64_t)base + (okp ? cj : p32);
+                                const uint32_t* wp = reinterpret_cast<const uint32_t*>(a.buf + (ga & ~3ull));
+                                const uint32_t lo = wp[0], hi = wp[1];
+                                const uint32_t v = (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * (ga & 3)));
+                                const uint32_t stop4 = ~v & 0x80808080u;
+                                const int vl = (__builtin_ctz(stop4 | 0x80000000u) >> 3) + 1;
+                                const uint32_t nn = ((v & 0x7fu) | ((v >> 1) & 0x3f80u) | ((v >> 2) & 0x1fc000u) |
+                                                     ((v >> 3) & 0xfe00000u)) &
+                                                    (0xffffffffu >> (32 - 7 * vl));
+                                const uint32_t vs = nn < (1u << 7) ? 1u : nn < (1u << 14) ? 2u : nn < (1u << 21) ? 3u : 4u;
+                                const uint32_t fl = vs + nn + 4;
+                                const uint32_t left = okp ? (uint32_t)L - cj : 0u;
+                                const bool ok = okp && (v & 0xffu) != 0 && stop4 != 0 && fl == sd &&
+                                                fl <= (left < a.max_op ? left : a.max_op) &&
+                                                nfr + (uint32_t)(lane + 64 * h) < a.cap;
+                                const uint64_t m = __builtin_amdgcn_ballot_w64(ok);
+                                okm[h] = __builtin_amdgcn_readfirstlane(~m ? (uint32_t)__builtin_ctzll(~m) : 64u);
+                            }
+                            const uint32_t nacc = okm[0] < 64 ? okm[0] : 64 + okm[1];
+                            for (uint32_t j = (uint32_t)lane; j < nacc; j += 64) {
+                                a.scratch_off[s * (uint64_t)a.cap + nfr + j] = (uint64_t)base + p32 + j * sd;
+                                a.scratch_len[s * (uint64_t)a.cap + nfr + j] = sd;
+                            }
+                            nfr += nacc;
+                            p += (int64_t)nacc * sd;
+                            if (nacc < 128) break;
+                        }
+                    }
                     if (lane == 0) {
                         sh_status = st;
                         sh_pos = p;
