@@ -416,22 +416,30 @@ def main():
         f1.record(stream)
         barrier()
         read_ms = f0.elapsed_time(f1) / args.crc_steps
-        # fused: framing + verify in one pass over HBM (rh_segments_read_launch)
+        # rh_segments_read_launch (LogSegment.readSegmentFile in one call): default variant 2 = framing
+        # walk + CRC v8 over the slotted frame table + verdict; variant 0 = the one-pass LDS-ring kernel
+        lib = _lib.load()
         fbatch = engine.SegmentBatch(buf=fb.buf, seg_off=sb.seg_off, seg_len=sb.seg_len,
                                      frames_per_seg_cap=ss.frames_per_segment + 16)
-        for _ in range(2):
-            fout = engine.read_segments_fused(ctx, fbatch, stream=stream)
-        barrier()
-        f0.record(stream)
-        for _ in range(args.crc_steps):
-            fout = engine.read_segments_fused(ctx, fbatch, stream=stream)
-        f1.record(stream)
-        barrier()
-        fused_ms = f0.elapsed_time(f1) / args.crc_steps
-        fbad = np.nonzero(np.unpackbits(fout["bad_bits"].cpu().numpy().view(np.uint8), bitorder="little")[: fb.n])[0]
-        fused_ok = bool(np.array_equal(fbad, ss.corrupted) and int(fbatch.total_frames.item()) == fb.n
+        read_api = {}
+        for var in (2, 0):
+            _lib.check(lib.rh_segments_read_set_variant(var))
+            for _ in range(2):
+                fout = engine.read_segments_fused(ctx, fbatch, stream=stream)
+            barrier()
+            f0.record(stream)
+            for _ in range(args.crc_steps):
+                fout = engine.read_segments_fused(ctx, fbatch, stream=stream)
+            f1.record(stream)
+            barrier()
+            ms_v = f0.elapsed_time(f1) / args.crc_steps
+            fbad = np.nonzero(np.unpackbits(fout["bad_bits"].cpu().numpy().view(np.uint8), bitorder="little")[: fb.n])[0]
+            ok_v = bool(np.array_equal(fbad, ss.corrupted) and int(fbatch.total_frames.item()) == fb.n
                         and torch.equal(fbatch.frame_off[: fb.n], fb.frame_off)
                         and torch.equal(fout["crc_out"][: fb.n], fb.crc_out[: fb.n]))
+            read_api[var] = (ms_v, ok_v)
+        _lib.check(lib.rh_segments_read_set_variant(2))
+        fused_ms, fused_ok = read_api[0]
         del fbatch, fout
         seg_bytes = n_seg * ss.segment_size
         tot_seg_bytes = sum_over_ranks(seg_bytes)
@@ -448,12 +456,15 @@ def main():
             "framing_traffic_bytes": (round(pmc["framing_bytes_per_unit"] * n_seg) if "framing_bytes_per_unit" in pmc
                                       else None),
             "framing_plus_verify_GBps": round(tot_seg_bytes / (max_over_ranks(read_ms) * 1e-3) / 1e9, 1),
+            "read_launch_GBps": round(tot_seg_bytes / (max_over_ranks(read_api[2][0]) * 1e-3) / 1e9, 1),
+            "ms_read_launch": round(read_api[2][0], 4), "read_launch_parity_ok": read_api[2][1],
+            "read_launch_note": "rh_segments_read_launch default (walk + CRC v8 + verdict in one call)",
             "fused_read_GBps": round(tot_seg_bytes / (max_over_ranks(fused_ms) * 1e-3) / 1e9, 1),
             "ms_fused_read": round(fused_ms, 4), "fused_parity_ok": fused_ok,
             "fused_roofline": {"bound": "hbm", "achieved": round(seg_bytes / (fused_ms * 1e-3) / 1e9, 1),
                                "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                                "frac": round(seg_bytes / (fused_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
-                               "kernel": "segment_read_kernel (framing + CRC verify, one pass) + scan + compact",
+                               "kernel": "segment_read_kernel<36> (variant 0: framing + CRC verify in one HBM pass) + scan + compact",
                                "algorithmic_bytes_per_launch": seg_bytes},
             "unit": "GB/s (segment bytes, whole job)", "frames_found": nfr_found, "parity_ok": bool(frame_ok),
             "ms_framing": round(scan_ms, 4), "ms_framing_plus_verify": round(read_ms, 4),

@@ -319,8 +319,9 @@ int rh_segments_read_launch(rh_ctx* ctx, const rh_segments* segs, const rh_segme
 /* Framing kernel variant (identical results): 0 = one wave per segment, 16 KiB LDS window;
  * 1 / 2 = one 256-thread block per segment, double-buffered 32 / 64 KiB windows (default 1). */
 int rh_segments_set_variant(int variant);
-/* Fused read kernel variants (identical results): 0 = 16 lanes x 36-byte slices per CRC unit,
- * 1 = 16 lanes x 20 bytes (default 0). */
+/* Read-path variants (identical results): 0 / 1 = one-pass LDS-ring kernel with 16 lanes x 36 / 20
+ * byte CRC units; 2 (default) = framing walk (header fast-forward) + CRC32C over the slotted frame
+ * table + verdict, which is faster. */
 int rh_segments_read_set_variant(int variant);
 /* Fused-read instrumentation (tuning only): enable = 1 zeroes the per-block cycle counters and
  * switches rh_segments_read_launch to the instrumented kernel, 0 switches back, -1 leaves it; if

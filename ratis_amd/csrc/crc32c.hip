@@ -132,6 +132,12 @@ struct FrameArgs {
     const uint32_t* shift32; // [4][256]: advance over 32 zero bytes (v3/v4, ILP = 2)
     const uint32_t* lanetab; // v4: lane-distance nibble tables (build_crc_lane_tables)
     const uint32_t* zwin;    // v4: [4][256] advance over one window (Q*64 bytes)
+    // v8 slot mode (the read path): the frame table is rh_segments' slotted scratch table, entry
+    // f = segment f / slot_cap, slot f % slot_cap, valid below min(slot_nframes[seg], slot_cap);
+    // a mismatch also lowers seg_first_bad[seg] to the slot index (atomicMin)
+    const uint32_t* slot_nframes;
+    uint32_t slot_cap;
+    uint32_t* seg_first_bad;
 };
 
 template <bool REPL>
@@ -1369,10 +1375,14 @@ __global__ __launch_bounds__(1024) void crc_frames_kernel8(FrameArgs a) {
             const int64_t E = m.o + (int64_t)m.lc;
             const bool unsafe = m.o < 67 || E + 8 > a.buf_len || m.lc < 8;
             m.fl = malformed ? 2u : (unsafe ? 1u : 0u);
+            if (a.slot_nframes) {  // slot mode: slots past the segment's frame count are skipped
+                const uint32_t nfs = a.slot_nframes[f / a.slot_cap];
+                if (f % a.slot_cap >= (nfs < a.slot_cap ? nfs : a.slot_cap)) m.fl = 3u;
+            }
             mo[t] = m.o;
             mlc[t] = m.lc;
             mfl[t] = (uint8_t)m.fl;
-            if (m.fl) slow[atomicAdd(nslow, 1u)] = (uint16_t)t;
+            if (m.fl == 1u || m.fl == 2u) slow[atomicAdd(nslow, 1u)] = (uint16_t)t;
         }
         __syncthreads();
 
@@ -1490,6 +1500,7 @@ __global__ __launch_bounds__(1024) void crc_frames_kernel8(FrameArgs a) {
                             if (a.bad_bits)
                                 atomicOr(reinterpret_cast<unsigned long long*>(a.bad_bits + (f >> 6)), 1ull << (f & 63));
                             if (a.n_bad) atomicAdd(a.n_bad, 1ull);
+                            if (a.seg_first_bad) atomicMin(a.seg_first_bad + f / a.slot_cap, (uint32_t)(f % a.slot_cap));
                         }
                     }
                 }
@@ -1530,6 +1541,7 @@ __global__ __launch_bounds__(1024) void crc_frames_kernel8(FrameArgs a) {
                     if (a.crc_out) a.crc_out[f] = 0u;
                     if (a.bad_bits) atomicOr(reinterpret_cast<unsigned long long*>(a.bad_bits + (f >> 6)), 1ull << (f & 63));
                     if (a.n_bad) atomicAdd(a.n_bad, 1ull);
+                    if (a.seg_first_bad) atomicMin(a.seg_first_bad + f / a.slot_cap, (uint32_t)(f % a.slot_cap));
                 }
                 continue;
             }
@@ -1570,6 +1582,7 @@ __global__ __launch_bounds__(1024) void crc_frames_kernel8(FrameArgs a) {
                         if (a.bad_bits)
                             atomicOr(reinterpret_cast<unsigned long long*>(a.bad_bits + (f >> 6)), 1ull << (f & 63));
                         if (a.n_bad) atomicAdd(a.n_bad, 1ull);
+                        if (a.seg_first_bad) atomicMin(a.seg_first_bad + f / a.slot_cap, (uint32_t)(f % a.slot_cap));
                     }
                 }
             }
@@ -1766,3 +1779,27 @@ int rh_crc_set_default_variant(int v) {
 }
 
 int rh_crc_num_variants() { return kAblationVariant; }  // exact variants 0..25
+
+// The read path's CRC pass (rh_segments_read_launch, default variant): crc_frames_kernel8 over the
+// slotted frame table the framing walk left in segs->scratch_off/len, VERIFY, CRCs into
+// crc->scratch_crc (slot-indexed), mismatches counted in crc->n_bad and the first bad slot of each
+// segment atomically lowered in crc->seg_ok (pre-set to 0xFFFFFFFF by the caller).
+int rh_crc_verify_slots(rh_ctx* ctx, const rh_segments* g, const rh_segments_crc* c, hipStream_t stream) {
+    FrameArgs a{};
+    a.buf = g->buf;
+    a.wbuf = nullptr;
+    a.buf_len = (int64_t)g->buf_len;
+    a.off = g->scratch_off;
+    a.len = g->scratch_len;
+    a.n = g->n_seg * (uint64_t)g->frames_per_seg_cap;
+    a.init = 0xFFFFFFFFu;
+    a.flags = RH_CRC_VERIFY;
+    a.crc_out = c->scratch_crc;
+    a.bad_bits = nullptr;
+    a.n_bad = c->n_bad;
+    a.slice = ctx->d_slice;
+    a.slot_nframes = g->seg_nframes;
+    a.slot_cap = g->frames_per_seg_cap;
+    a.seg_first_bad = c->seg_ok;
+    return launch_variant<16, 64, true, 10, 2>(ctx, a, stream);
+}

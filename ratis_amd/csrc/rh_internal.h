@@ -78,6 +78,7 @@ int rh_segments_scan_counts(const uint32_t* nframes, uint64_t n_seg, uint32_t ca
 int rh_segments_read_impl(rh_ctx* ctx, const rh_segments* segs, const rh_segments_crc* crc, hipStream_t stream);
 int rh_segments_read_profile_impl(int enable, uint64_t* out, uint64_t n);
 int rh_segments_read_set_variant_impl(int v);
+int rh_crc_verify_slots(rh_ctx* ctx, const rh_segments* segs, const rh_segments_crc* crc, hipStream_t stream);
 int rh_lease_launch_impl(rh_ctx* ctx, const rh_lease_soa* tiers, int n_tiers, hipStream_t stream);
 int rh_lease_set_variant_impl(int v);
 int rh_lease_num_variants_impl();

@@ -763,9 +763,31 @@ __global__ __launch_bounds__(256) void segment_compact_crc_kernel(ReadArgs a, co
 }
 
 // Fused-read variants (identical results): the unit's lane slice S in bytes.
-constexpr int kNumReadVariants = 2;
-constexpr int kReadS[kNumReadVariants] = {36, 20};
-int g_read_variant = 0;
+// 0 / 1: segment_read_kernel with 36 / 20-byte CRC units (one pass over HBM, LDS ring);
+// 2 (default): framing walk (segment_walk_kernel2, header fast-forward) then crc_frames_kernel8 over
+// the slotted frame table, then the verdict -- two passes, but the walk reads headers only.
+constexpr int kNumReadVariants = 3;
+constexpr int kReadS[kNumReadVariants] = {36, 20, 0};
+int g_read_variant = 2;
+
+// The reader's verdict per segment from the first bad slot (seg_ok pre-set to 0xFFFFFFFF, lowered
+// by the CRC pass): decodeEntry throws ChecksumException at the first frame whose CRC does not
+// verify (RDR:327-336), so the segment reads as that many frames, stopped at that frame's offset.
+__global__ __launch_bounds__(256) void segment_verdict_kernel(const uint64_t* seg_off, const uint32_t* seg_nframes,
+                                                              const int32_t* seg_status, const uint64_t* seg_stop,
+                                                              const uint64_t* scratch_off, uint64_t n_seg, uint32_t cap,
+                                                              uint32_t* seg_ok, int32_t* seg_rstatus,
+                                                              uint64_t* seg_rstop) {
+    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < n_seg; s += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t nfr = seg_nframes[s];
+        const uint32_t nfs = nfr < cap ? nfr : cap;
+        const uint32_t fb = seg_ok[s];
+        const bool bad = fb < nfs;
+        seg_ok[s] = bad ? fb : nfr;
+        seg_rstatus[s] = bad ? RH_SEG_E_CHECKSUM : seg_status[s];
+        seg_rstop[s] = bad ? scratch_off[s * (uint64_t)cap + fb] - seg_off[s] : seg_stop[s];
+    }
+}
 
 template <int S>
 hipError_t launch_read(const ReadArgs& a, uint64_t grid, hipStream_t stream) {
@@ -810,7 +832,7 @@ std::vector<uint32_t> build_read_tables(int S) {
 
 int rh_segments_read_set_variant_impl(int v) {
     if (v < 0 || v >= kNumReadVariants)
-        return rh::fail(RH_E_RANGE, "rh_segments_read_set_variant: variant out of range [0, 1]");
+        return rh::fail(RH_E_RANGE, "rh_segments_read_set_variant: variant out of range [0, 2]");
     g_read_variant = v;
     return RH_OK;
 }
@@ -829,6 +851,35 @@ int rh_segments_read_impl(rh_ctx* ctx, const rh_segments* g, const rh_segments_c
     if (g->buf_len > (uint64_t)INT64_MAX) return rh::fail(RH_E_RANGE, "rh_segments_read_launch: buf_len too large");
     if (!ctx->d_slice) return rh::fail(RH_E_STATE, "rh_segments_read_launch: CRC tables not uploaded");
     const int v = g_read_variant;
+    if (v == 2) {
+        int rc = rh_segments_launch_impl(ctx, g, stream);  // walk + scan + compaction
+        if (rc != RH_OK) return rc;
+        RH_HIP(hipMemsetAsync(c->seg_ok, 0xFF, (size_t)g->n_seg * 4, stream));
+        rc = rh_crc_verify_slots(ctx, g, c, stream);
+        if (rc != RH_OK) return rc;
+        if (c->crc_out || c->bad_bits) {  // dense per-frame CRCs / mismatch bits
+            if (c->bad_bits) RH_HIP(hipMemsetAsync(c->bad_bits, 0, (size_t)((g->frame_cap + 63) / 64) * 8, stream));
+            ReadArgs a{};
+            a.buf = g->buf;
+            a.n_seg = g->n_seg;
+            a.cap = g->frames_per_seg_cap;
+            a.scratch_off = g->scratch_off;
+            a.scratch_len = g->scratch_len;
+            a.scratch_crc = c->scratch_crc;
+            a.seg_nframes = g->seg_nframes;
+            const int cus = ctx->num_cus > 0 ? ctx->num_cus : 256;
+            const uint64_t cgrid = g->n_seg < (uint64_t)cus * 8 ? g->n_seg : (uint64_t)cus * 8;
+            hipLaunchKernelGGL(segment_compact_crc_kernel, dim3((uint32_t)cgrid), dim3(256), 0, stream, a, g->seg_first,
+                               g->frame_off, g->frame_len, g->frame_cap, c->crc_out, c->bad_bits);
+            RH_HIP(hipGetLastError());
+        }
+        const uint64_t vgrid = (g->n_seg + 255) / 256 < 1024 ? (g->n_seg + 255) / 256 : 1024;
+        hipLaunchKernelGGL(segment_verdict_kernel, dim3((uint32_t)vgrid), dim3(256), 0, stream, g->seg_off, g->seg_nframes,
+                           g->seg_status, g->seg_stop, g->scratch_off, g->n_seg, g->frames_per_seg_cap, c->seg_ok,
+                           c->seg_read_status, c->seg_read_stop);
+        RH_HIP(hipGetLastError());
+        return RH_OK;
+    }
     {
         std::lock_guard<std::mutex> lk(ctx->mu);
         if (!ctx->d_read_tables[v]) {
