@@ -317,7 +317,11 @@ typedef struct rh_segments_crc {
 } rh_segments_crc;
 int rh_segments_read_launch(rh_ctx* ctx, const rh_segments* segs, const rh_segments_crc* crc, void* stream);
 /* Framing kernel variant (identical results): 0 = one wave per segment, 16 KiB LDS window;
- * 1 / 2 = one 256-thread block per segment, double-buffered 32 / 64 KiB windows (default 1). */
+ * 1 / 2 = one 256-thread block per segment, double-buffered 32 / 64 KiB windows (default 1);
+ * 3 = 16 KiB windows plus a per-position frame-length table, switched on after a window of >= 24
+ * frames of differing lengths; 4 / 5 = the same kernel with the table never / always used (A/B).
+ * Measured: the table does not pay on gfx950 (ragged 64-2048 B frames, 32 segments: 1 = 129,
+ * 3 = 119, 5 = 62 GB/s) -- the per-frame cost is the walk's dependent latency, not the decode. */
 int rh_segments_set_variant(int variant);
 /* Read-path variants (identical results): 0 / 1 = one-pass LDS-ring kernel with 16 lanes x 36 / 20
  * byte CRC units; 2 (default) = framing walk (header fast-forward) + CRC32C over the slotted frame

@@ -263,6 +263,22 @@ __global__ __launch_bounds__(64) void segment_walk_kernel(SegArgs a) {
 constexpr int kBlock2 = 256;
 
 // Block-uniform 64-bit value, pinned to SGPRs (keeps the walker's compares scalar).
+// Per-frame outputs of the serial walk are staged one per lane (frame k -> lane k % 64) and
+// written 64 at a time as one coalesced store, instead of a single-lane store per frame.
+__device__ __forceinline__ void stage_put(uint64_t& so, uint32_t& sl, int lane, uint32_t k, uint64_t off,
+                                          uint32_t len) {
+    const bool me = lane == (int)(k & 63u);
+    so = me ? off : so;
+    sl = me ? len : sl;
+}
+__device__ __forceinline__ void stage_flush(uint64_t* so, uint32_t* sl, int lane, uint32_t n, uint64_t o,
+                                            uint32_t l) {
+    if ((uint32_t)lane < n) {
+        so[lane] = o;
+        sl[lane] = l;
+    }
+}
+
 __device__ __forceinline__ int64_t uniform64(int64_t v) {
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
     const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)v >> 32));
@@ -308,14 +324,21 @@ struct Win {
     }
 };
 
-template <int W>
+// NX (dense mode for ragged frame lengths): when the last window held many frames of differing
+// lengths, all 256 threads first decode the header at EVERY byte position of window k (the fast
+// loop's folded predicate) into an LDS table nx[pos] = frame length (0 = not a common-case frame),
+// then the walker only hops p -> p + nx[p] (one LDS read per frame instead of the ~70-instruction
+// scalar decode); anything nx marks 0 takes the rule-by-rule step.
+template <int W, bool NX = false, int DM = 0>
 __global__ __launch_bounds__(kBlock2) void segment_walk_kernel2(SegArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t ring[];  // [2W + 16]: 2 windows + mirror
+    extern __shared__ __attribute__((aligned(16))) uint8_t ring[];  // [2W + 16]: 2 windows + mirror (+ nx[W] u16)
     __shared__ int sh_status;
     __shared__ long long sh_pos;
     __shared__ uint32_t sh_nfr;
     __shared__ unsigned long long sh_min;
+    __shared__ int sh_dense;
     constexpr int64_t MASK = 2 * W - 1;
+    uint16_t* nx = reinterpret_cast<uint16_t*>(ring + 2 * W + 16);
     const int t = threadIdx.x;
     for (uint64_t s = blockIdx.x; s < a.n_seg; s += gridDim.x) {
         const int64_t base = uniform64((int64_t)a.seg_off[s]);
@@ -338,6 +361,7 @@ __global__ __launch_bounds__(kBlock2) void segment_walk_kernel2(SegArgs a) {
             sh_status = ok ? (8 >= L ? RH_SEG_END : kWalking) : (bad ? RH_SEG_E_HEADER : RH_SEG_END);
             sh_pos = ok ? 8 : 0;
             sh_nfr = 0;
+            sh_dense = 0;
         }
         __syncthreads();
         int status = sh_status;
@@ -358,14 +382,78 @@ __global__ __launch_bounds__(kBlock2) void segment_walk_kernel2(SegArgs a) {
                 nxt.store(ring, (int)((k + 1) & 1), t);   // ring now holds windows k, k+1
                 __syncthreads();
                 nxt.load(seg, L, A + (k + 2) * W, t);       // in flight during the walk
+                const bool dense = NX && sh_dense && L <= 0x7fffffff;
+                if (NX && dense) {
+                    // nx[i] for window position wstart + i: thread t decodes positions t*PP .. t*PP+PP-1
+                    // from PP + 8 ring bytes held in registers
+                    constexpr int PP = W / kBlock2;
+                    const int64_t wstart = A + k * W;
+                    const uint32_t q0 = (uint32_t)((k * W + (int64_t)t * PP) & MASK);  // 4-aligned
+                    uint32_t dw[PP / 4 + 2];
+#pragma unroll
+                    for (int i = 0; i < PP / 4 + 2; ++i)
+                        dw[i] = *reinterpret_cast<const uint32_t*>(ring + ((q0 + 4u * i) & (uint32_t)MASK));
+                    // 32-bit, branch-free form of the fast predicate (dense mode needs L < 2^31)
+                    const int32_t rel0 = (int32_t)(wstart + (int64_t)t * PP);  // segment-relative
+                    const int32_t lim_end = (int32_t)(L - 8);                 // 8 readable bytes
+                    const int32_t L32 = (int32_t)L;
+                    const int32_t mo = (int32_t)(a.max_op < 0x7fffffffu ? a.max_op : 0x7fffffffu);
+#pragma unroll
+                    for (int i = 0; i < PP; ++i) {
+                        const uint32_t v = __builtin_amdgcn_alignbyte(dw[(i >> 2) + 1], dw[i >> 2], i & 3);
+                        const int32_t q = rel0 + i;
+                        const uint32_t stop4 = ~v & 0x80808080u;
+                        const int vl = (__builtin_ctz(stop4 | 0x80000000u) >> 3) + 1;
+                        const uint32_t nn = ((v & 0x7fu) | ((v >> 1) & 0x3f80u) | ((v >> 2) & 0x1fc000u) |
+                                             ((v >> 3) & 0xfe00000u)) &
+                                            (0xffffffffu >> (32 - 7 * vl));
+                        // varint32_size(nn) for nn < 2^28: 1 + (bits above 7 / 7), via the bit length
+                        const uint32_t bl = 32 - __builtin_clz(nn | 1u);
+                        const uint32_t vs = (bl + 6) / 7;
+                        const int32_t fl = (int32_t)(vs + nn + 4);
+                        const int32_t left = L32 - q;
+                        const int32_t lim = left < mo ? left : mo;
+                        const bool ok = (q >= 0) & (q < lim_end) & ((v & 0xffu) != 0) & (stop4 != 0) & (fl <= lim) &
+                                        (fl < 65536);
+                        nx[t * PP + i] = ok ? (uint16_t)fl : (uint16_t)0;
+                    }
+                    __syncthreads();
+                }
                 if (t < 64) {
                     // wave 0 walks, wave-uniformly (lane 0 stores the single-frame steps)
                     const int lane = t;
                     const int64_t wend = A + (k + 1) * W;
                     uint32_t nfr = sh_nfr;
+                    const uint32_t nfr_w0 = nfr;
                     int st = kWalking;
                     int64_t p = pos;
                     while (p < wend) {
+                        if (NX && dense) {
+                            // hop through nx: one LDS read per frame
+                            const int64_t wstart = A + k * W;
+                            const uint32_t room = a.cap - nfr;
+                            uint64_t* so = a.scratch_off + s * (uint64_t)a.cap + nfr;
+                            uint32_t* sl = a.scratch_len + s * (uint64_t)a.cap + nfr;
+                            uint64_t st_o = 0;
+                            uint32_t st_l = 0;
+                            uint32_t kk = 0;
+                            while (p < wend && kk < room) {
+                                const uint32_t fl = __builtin_amdgcn_readfirstlane((uint32_t)nx[(uint32_t)(p - wstart)]);
+                                if (fl == 0) break;
+                                stage_put(st_o, st_l, lane, kk, (uint64_t)(base + p), fl);
+                                if ((kk & 63u) == 63u) stage_flush(so + (kk - 63), sl + (kk - 63), lane, 64, st_o, st_l);
+                                ++kk;
+                                p += fl;
+                                prev_fl = last_fl;
+                                last_fl = fl;
+                            }
+                            stage_flush(so + (kk & ~63u), sl + (kk & ~63u), lane, kk & 63u, st_o, st_l);
+                            nfr += kk;
+                            if (p >= wend) break;
+                            if (kk < room) {
+                                // fall through to the rule-by-rule step for the frame at p
+                            }
+                        }
                         {
                             // Speculative run (a run of equal lengths was seen): lane j checks the
                             // frame at p + j * s, s = the last length, with the fast loop's folded
@@ -418,13 +506,16 @@ __global__ __launch_bounds__(kBlock2) void segment_walk_kernel2(SegArgs a) {
                             uint32_t* sl = a.scratch_len + s * (uint64_t)a.cap + nfr;
                             uint32_t k = 0;
                             if (L <= 0x7fffffff && pend > p) {  // 32-bit offsets: all-scalar compares
+                                uint64_t st_o = 0;
+                                uint32_t st_l = 0;
                                 uint32_t p32 = (uint32_t)p;
                                 const uint32_t pend32 = (uint32_t)pend, L32 = (uint32_t)L, mo = a.max_op;
                                 uint32_t q = (uint32_t)((p - A) & MASK);
                                 while (p32 < pend32 && k < room) {
                                     const uint32_t q0 = q & ~3u;
-                                    const uint32_t lo = *reinterpret_cast<const uint32_t*>(ring + q0);
-                                    const uint32_t hi = *reinterpret_cast<const uint32_t*>(ring + q0 + 4);  // mirror
+                                    // wave-uniform: one readfirstlane, then the decode runs on the SALU
+                                    const uint32_t lo = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const uint32_t*>(ring + q0));
+                                    const uint32_t hi = __builtin_amdgcn_readfirstlane(*reinterpret_cast<const uint32_t*>(ring + q0 + 4));  // mirror
                                     const uint32_t v = (uint32_t)(((uint64_t)hi << 32 | lo) >> (8 * (q & 3)));
                                     const uint32_t stop4 = ~v & 0x80808080u;
                                     if ((v & 0xffu) == 0 || stop4 == 0) break;
@@ -437,10 +528,8 @@ __global__ __launch_bounds__(kBlock2) void segment_walk_kernel2(SegArgs a) {
                                     const uint32_t fl = vs + nn + 4;  // nn < 2^28: no overflow
                                     const uint32_t left = L32 - p32;
                                     if (fl > (left < mo ? left : mo)) break;
-                                    if (lane == 0) {
-                                        so[k] = (uint64_t)base + p32;
-                                        sl[k] = fl;
-                                    }
+                                    stage_put(st_o, st_l, lane, k, (uint64_t)base + p32, fl);
+                                    if ((k & 63u) == 63u) stage_flush(so + (k - 63), sl + (k - 63), lane, 64, st_o, st_l);
                                     ++k;
                                     p32 += fl;
                                     q = (q + fl) & (uint32_t)MASK;
@@ -448,6 +537,7 @@ __global__ __launch_bounds__(kBlock2) void segment_walk_kernel2(SegArgs a) {
                                     last_fl = fl;
                                     if (fl == prev_fl) break;  // a run: back to speculation
                                 }
+                                stage_flush(so + (k & ~63u), sl + (k & ~63u), lane, k & 63u, st_o, st_l);
                                 p = p32;
                             }
                             nfr += k;
@@ -581,6 +671,8 @@ __global__ __launch_bounds__(kBlock2) void segment_walk_kernel2(SegArgs a) {
                         sh_status = st;
                         sh_pos = p;
                         sh_nfr = nfr;
+                        // dense mode for the next window: >= 24 frames here and no equal-length run
+                        if (NX) sh_dense = DM == 1 ? 0 : DM == 2 ? 1 : (nfr - nfr_w0 >= 24u && last_fl != prev_fl) ? 1 : 0;
                     }
                 }
                 __syncthreads();
@@ -679,19 +771,20 @@ __global__ __launch_bounds__(256) void segment_compact_kernel(const uint64_t* sc
 
 int g_seg_variant = 1;
 
-template <int W>
+template <int W, bool NX = false, int DM = 0>
 hipError_t launch_walk2(const SegArgs& a, int cus, hipStream_t stream) {
+    constexpr int lds = 2 * W + 16 + (NX ? 2 * W : 0);
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(segment_walk_kernel2<W>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, 2 * W + 16);
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(segment_walk_kernel2<W, NX, DM>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    const int per_cu = 2 * W <= 65536 ? 2 : 1;
+    const int per_cu = lds <= 65536 + 16 + 32768 ? 2 : 1;
     const uint64_t cap = (uint64_t)cus * per_cu;
     const uint64_t grid = a.n_seg < cap ? a.n_seg : cap;
-    hipLaunchKernelGGL(segment_walk_kernel2<W>, dim3((uint32_t)grid), dim3(kBlock2), 2 * W + 16, stream, a);
+    hipLaunchKernelGGL((segment_walk_kernel2<W, NX, DM>), dim3((uint32_t)grid), dim3(kBlock2), lds, stream, a);
     return hipGetLastError();
 }
 
@@ -705,7 +798,7 @@ int rh_segments_scan_counts(const uint32_t* nframes, uint64_t n_seg, uint32_t ca
 }
 
 int rh_segments_set_variant_impl(int v) {
-    if (v < 0 || v > 2) return rh::fail(RH_E_RANGE, "rh_segments_set_variant: variant out of range [0, 2]");
+    if (v < 0 || v > 5) return rh::fail(RH_E_RANGE, "rh_segments_set_variant: variant out of range [0, 5]");
     g_seg_variant = v;
     return RH_OK;
 }
@@ -739,8 +832,14 @@ int rh_segments_launch_impl(rh_ctx* ctx, const rh_segments* g, hipStream_t strea
         hipLaunchKernelGGL(segment_walk_kernel, dim3((uint32_t)grid), dim3(64), 0, stream, a);
     } else if (v == 1) {
         RH_HIP(launch_walk2<32768>(a, cus, stream));
-    } else {
+    } else if (v == 2) {
         RH_HIP(launch_walk2<65536>(a, cus, stream));
+    } else if (v == 3) {
+        RH_HIP((launch_walk2<16384, true>(a, cus, stream)));
+    } else if (v == 4) {  // A/B: the dense table never used
+        RH_HIP((launch_walk2<16384, true, 1>(a, cus, stream)));
+    } else {  // A/B: the dense table on every window
+        RH_HIP((launch_walk2<16384, true, 2>(a, cus, stream)));
     }
     RH_HIP(hipGetLastError());
     hipLaunchKernelGGL(segment_scan_kernel, dim3(1), dim3(kScanThreads), 0, stream, g->seg_nframes, g->n_seg,

@@ -238,3 +238,76 @@ def synth_segments(ctx, n_segments: int, segment_size: int = 32 << 20, frame_siz
         buf[w] = buf[w] ^ 1
     torch.cuda.synchronize()
     return SegmentSet(fb, n_segments, segment_size, fps, frame_size, np.sort(bad), prefix_len)
+
+
+@dataclass
+class RaggedSegmentSet:
+    batch: object            # engine.FrameBatch over every frame of every segment
+    n_segments: int
+    segment_size: int
+    seg_nframes: np.ndarray  # int64 [n_segments]
+    corrupted: np.ndarray    # sorted global frame numbers with one payload bit flipped
+
+
+def synth_ragged_segments(ctx, n_segments: int, segment_size: int = 32 << 20, min_frame: int = 64,
+                          max_frame: int = 2048, seed: int = SEED, corrupt_rate: float = 0.0,
+                          device="cuda") -> RaggedSegmentSet:
+    """Closed segment images whose frames have seeded random lengths in [min_frame, max_frame]
+    (a log of differently sized entries, unlike config 5's fixed 4 KiB): header "RaftLog1",
+    frames varint(n) + n payload bytes + CRC (payload = seeded random bytes, not a parsed
+    LogEntryProto: framing and CRC never look inside it), zero padding.  CRCs stamped by the GPU
+    write-side kernel, then ``corrupt_rate`` of the frames get one payload bit flipped."""
+    import torch
+
+    from . import engine, segment
+    from ._lib import RH_CRC_STAMP
+
+    assert 6 <= min_frame <= max_frame <= (1 << 14)
+    rng = np.random.Generator(np.random.PCG64(seed))
+    offs, lens, counts = [], [], []
+    def frame_len(nn):  # varint_size(n) + n + 4, n < 2^14 here
+        return np.where(nn >= 128, 2, 1) + nn + 4
+
+    for s in range(n_segments):
+        cap = segment_size - 8
+        nn = rng.integers(max(1, min_frame - 5), max(1, max_frame - 6) + 1, size=cap // min_frame + 1)
+        fl = frame_len(nn)
+        end = np.cumsum(fl)
+        k = int(np.searchsorted(end, cap, side="right"))
+        fl = fl[:k]
+        start = 8 + np.concatenate([[0], np.cumsum(fl)[:-1]]) if k else np.zeros(0, np.int64)
+        offs.append(s * segment_size + start)
+        lens.append(fl)
+        counts.append(k)
+    off = np.concatenate(offs).astype(np.int64)
+    fl = np.concatenate(lens).astype(np.int64)
+    # n with varint_size(n) + n + 4 == fl (every fl above came from such an n)
+    n = fl - 5
+    two = n >= 128
+    n = np.where(two, fl - 6, n)
+    assert np.all((n >= 128) == two) and np.all(n >= 1) and np.all(frame_len(n) == fl)
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed)
+    buf = torch.randint(0, 256, (n_segments * segment_size,), dtype=torch.uint8, device=device, generator=gen)
+    segv = buf.view(n_segments, segment_size)
+    segv[:, :8] = torch.tensor(list(segment.HEADER), dtype=torch.uint8, device=device)
+    ends = np.array([o[-1] + l[-1] if len(o) else s * segment_size + 8 for s, (o, l) in enumerate(zip(offs, lens))])
+    for s in range(n_segments):
+        segv[s, int(ends[s] - s * segment_size):] = 0
+    b0 = np.where(two, (n & 0x7F) | 0x80, n).astype(np.uint8)
+    b1 = (n >> 7).astype(np.uint8)
+    o_t = torch.from_numpy(off).to(device)
+    buf[o_t] = torch.from_numpy(b0).to(device)
+    o2 = torch.from_numpy(off[two] + 1).to(device)
+    buf[o2] = torch.from_numpy(b1[two]).to(device)
+    fb = engine.FrameBatch(buf=buf, frame_off=o_t, frame_len=torch.from_numpy(fl.astype(np.int32)).to(device))
+    fb.alloc_outputs()
+    engine.crc32c_frames(ctx, fb, flags=RH_CRC_STAMP)
+    bad = np.nonzero(rng.random(off.size) < corrupt_rate)[0]
+    if bad.size:
+        hdr = np.where(two[bad], 2, 1)
+        where = off[bad] + hdr + rng.integers(0, n[bad])
+        w = torch.from_numpy(where).to(device)
+        buf[w] = buf[w] ^ 1
+    torch.cuda.synchronize()
+    return RaggedSegmentSet(fb, n_segments, segment_size, np.asarray(counts, np.int64), np.sort(bad))

@@ -90,7 +90,7 @@ def main():
                                  seg_off=torch.arange(n, device="cuda", dtype=torch.int64) * ss.segment_size,
                                  seg_len=torch.full((n,), ss.segment_size, device="cuda", dtype=torch.int64),
                                  frames_per_seg_cap=ss.frames_per_segment + 16)
-        for v in range(3):
+        for v in range(6):
             _lib.check(lib.rh_segments_set_variant(v))
             fr = []
             for r in range(a.rounds):
@@ -122,6 +122,34 @@ def main():
         torch.cuda.empty_cache()
         ss = workload.synth_segments(ctx, n_segments=a.segments, frame_size=512, corrupt_rate=0)
         framing(ss, "32MiBx512B")
+        del ss
+        torch.cuda.empty_cache()
+        for lo, hi in ((64, 2048), (64, 512)):
+            rs = workload.synth_ragged_segments(ctx, n_segments=a.segments, min_frame=lo, max_frame=hi)
+            n = rs.n_segments
+            sb = engine.SegmentBatch(buf=rs.batch.buf,
+                                     seg_off=torch.arange(n, device="cuda", dtype=torch.int64) * rs.segment_size,
+                                     seg_len=torch.full((n,), rs.segment_size, device="cuda", dtype=torch.int64),
+                                     frames_per_seg_cap=int(rs.seg_nframes.max()) + 16)
+            for v in range(6):
+                _lib.check(lib.rh_segments_set_variant(v))
+                fr = []
+                for r in range(a.rounds):
+                    engine.segments_scan(ctx, sb)
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record()
+                    for _ in range(a.iters):
+                        engine.segments_scan(ctx, sb)
+                    e1.record()
+                    torch.cuda.synchronize()
+                    fr.append(n * rs.segment_size / (e0.elapsed_time(e1) / a.iters * 1e-3) / 1e9)
+                    assert int(sb.total_frames.item()) == int(rs.seg_nframes.sum())
+                    assert torch.equal(sb.frame_off[: rs.batch.frame_off.numel()], rs.batch.frame_off)
+                x = np.array(fr)
+                print(json.dumps({"kernel": "segments_scan", "variant": v, "shape": f"32MiBx{lo}-{hi}B ragged", "segments": n,
+                                  "median_GBps": round(float(np.median(x)), 1)}), flush=True)
+            _lib.check(lib.rh_segments_set_variant(1))
+            ss = rs
     del ss
     # commit kernel variants over 8 rotating 1M-group batches (config 3)
     host = workload.commit_snapshot(1_000_000)

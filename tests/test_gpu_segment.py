@@ -120,7 +120,7 @@ def check_against_oracle(orc, b, buf, offs, lens, max_op=4 << 20, skip_crc=None)
         assert np.array_equal(fl[k: k + nfr[s]], rl), s
 
 
-@pytest.fixture(params=[0, 1, 2])
+@pytest.fixture(params=[0, 1, 2, 3, 5])
 def seg_variant(request):
     from ratis_amd import _lib
     lib = _lib.load()
@@ -291,3 +291,30 @@ def test_speculative_walk_edges(ctx, orc, seg_variant):
     buf, offs, lens = pack(speculation_images(orc, rng), rng)
     b = run_scan(ctx, buf, offs, lens, cap=1024)
     check_against_oracle(orc, b, buf, offs, lens)
+
+
+@pytest.mark.parametrize("lo,hi", [(6, 200), (64, 2048), (1000, 9000)])
+def test_ragged_frame_lengths(ctx, orc, seg_variant, lo, hi):
+    """Segments of differently sized frames (workload.synth_ragged_segments): the frame table
+    equals the generator's, and two whole segments equal the literal reader.  Covers the dense
+    per-position table of variant 3 (many small frames per window) and the switches between it,
+    the speculative runs and the scalar loop."""
+    import torch
+
+    from ratis_amd import engine, workload
+    rs = workload.synth_ragged_segments(ctx, 4, segment_size=4 << 20, min_frame=lo, max_frame=hi, seed=lo + hi)
+    n = rs.n_segments
+    b = engine.SegmentBatch(buf=rs.batch.buf, seg_off=torch.arange(n, device="cuda", dtype=torch.int64) * rs.segment_size,
+                            seg_len=torch.full((n,), rs.segment_size, device="cuda", dtype=torch.int64),
+                            frames_per_seg_cap=int(rs.seg_nframes.max()) + 16)
+    engine.segments_scan(ctx, b)
+    torch.cuda.synchronize()
+    nf = int(rs.seg_nframes.sum())
+    assert int(b.total_frames.item()) == nf
+    assert torch.equal(b.frame_off[:nf], rs.batch.frame_off)
+    assert torch.equal(b.frame_len[:nf], rs.batch.frame_len)
+    for sgi in (0, n - 1):
+        img = rs.batch.buf[sgi * rs.segment_size:(sgi + 1) * rs.segment_size].cpu().numpy()
+        ro, rl, _, rst, rstop = orc.segment_scan(img)
+        assert (int(b.seg_status[sgi].item()), int(b.seg_stop[sgi].item())) == (rst, rstop)
+        assert len(ro) == int(rs.seg_nframes[sgi])

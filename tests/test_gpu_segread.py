@@ -203,3 +203,28 @@ def test_fused_speculative_walk_edges(ctx, orc):
     buf, offs, lens = pack(speculation_images(orc, rng), rng)
     b, out = run_fused(ctx, buf, offs, lens, cap=1024)
     check_fused(ctx, orc, b, out, buf, offs, lens, cap=1024)
+
+
+def test_fused_ragged_segments_with_corruption(ctx, orc):
+    """Ragged frame lengths with planted corruptions through rh_segments_read_launch: the mismatch
+    set is exactly the planted set and every segment stops at its first planted frame."""
+    import torch
+
+    from ratis_amd import engine, workload
+    rs = workload.synth_ragged_segments(ctx, 6, segment_size=2 << 20, min_frame=20, max_frame=3000, seed=9,
+                                        corrupt_rate=3e-4)
+    n = rs.n_segments
+    b = engine.SegmentBatch(buf=rs.batch.buf, seg_off=torch.arange(n, device="cuda", dtype=torch.int64) * rs.segment_size,
+                            seg_len=torch.full((n,), rs.segment_size, device="cuda", dtype=torch.int64),
+                            frames_per_seg_cap=int(rs.seg_nframes.max()) + 16)
+    out = engine.read_segments_fused(ctx, b)
+    torch.cuda.synchronize()
+    nf = int(rs.seg_nframes.sum())
+    assert int(b.total_frames.item()) == nf
+    bad = np.nonzero(_bits(out["bad_bits"].cpu().numpy(), nf))[0]
+    assert np.array_equal(bad, rs.corrupted) and rs.corrupted.size > 0
+    first = np.concatenate([[0], np.cumsum(rs.seg_nframes)[:-1]])
+    ok = out["n_ok"].cpu().numpy()
+    for sgi in range(n):
+        mine = rs.corrupted[(rs.corrupted >= first[sgi]) & (rs.corrupted < first[sgi] + rs.seg_nframes[sgi])]
+        assert int(ok[sgi]) == (int(mine[0] - first[sgi]) if mine.size else int(rs.seg_nframes[sgi])), sgi
