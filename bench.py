@@ -47,7 +47,6 @@ def parse():
     p.add_argument("--gap", type=int, default=-1)
     p.add_argument("--crc-segments", type=int, default=256, help="32 MiB segments per GPU (0 = skip CRC)")
     p.add_argument("--crc-steps", type=int, default=20)
-    p.add_argument("--crc-variant", type=int, default=None)
     p.add_argument("--no-lease", action="store_true")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-pcie", action="store_true")
@@ -298,7 +297,7 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": (round(pmc["commit_bytes_per_unit"] * n_mine) if "commit_bytes_per_unit" in pmc else None),
                 "traffic_source": pmc.get("_path"),
-                "kernel": "commit_kernel_r8<1,6,256,NT,NTS> (variant 14: fused stable F=4 + joint F=6 tiers)",
+                "kernel": "commit_kernel_rank (fused stable F=4 + joint F=6 tiers)",
                 "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": round(kern_ms, 5)}
 
     # ------------------------------------------------------------------ PCIe-inclusive commit
@@ -342,20 +341,20 @@ def main():
                                      device=dev)
         fb = ss.batch
         for i in range(2):
-            engine.crc32c_frames(ctx, fb, flags=_lib.RH_CRC_VERIFY, variant=args.crc_variant, stream=stream)
+            engine.crc32c_frames(ctx, fb, flags=_lib.RH_CRC_VERIFY, stream=stream)
         barrier()
         c0 = torch.cuda.Event(enable_timing=True)
         c1 = torch.cuda.Event(enable_timing=True)
         c0.record(stream)
         for i in range(args.crc_steps):
-            engine.crc32c_frames(ctx, fb, flags=_lib.RH_CRC_VERIFY, variant=args.crc_variant, stream=stream)
+            engine.crc32c_frames(ctx, fb, flags=_lib.RH_CRC_VERIFY, stream=stream)
         c1.record(stream)
         barrier()
         crc_kern_ms = c0.elapsed_time(c1) / args.crc_steps
         crc_ms = max_over_ranks(crc_kern_ms)
         fb.n_bad.zero_()
         fb.bad_bits.zero_()
-        engine.crc32c_frames(ctx, fb, flags=_lib.RH_CRC_VERIFY, variant=args.crc_variant, stream=stream)
+        engine.crc32c_frames(ctx, fb, flags=_lib.RH_CRC_VERIFY, stream=stream)
         torch.cuda.synchronize()
         bad = np.nonzero(np.unpackbits(fb.bad_bits.cpu().numpy().view(np.uint8), bitorder="little")[: fb.n])[0]
         crc_ok = bool(np.array_equal(bad, ss.corrupted))
@@ -379,12 +378,11 @@ def main():
                "workload": f"config5: {args.crc_segments} x 32 MiB segments/GPU, 4 KiB frames "
                            f"({fb.n} frames/GPU, {ss.corrupted.size} corrupted)",
                "ms_per_pass": round(crc_ms, 4), "mismatches_found": int(bad.size), "parity_ok": crc_ok,
-               "variant": args.crc_variant if args.crc_variant is not None else 24,
                "roofline": {"bound": "hbm", "achieved": round(crc_ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                             "frac": round(crc_ach / HBM_PEAK_GBPS, 4),
                             "traffic": (round(pmc["crc_bytes_per_unit"] * fb.n) if "crc_bytes_per_unit" in pmc else None),
                             "traffic_source": pmc.get("_path"),
-                            "kernel": "crc_frames_kernel8<2,2> (variant 24: copy-free 3-slot ring, LDS-staged frame table, 2 fold chains/lane)",
+                            "kernel": "crc_frames_kernel (16 lanes x 64 B per 1 KiB window, copy-free 3-slot ring, LDS-staged frame table, 2 fold chains/lane)",
                             "algorithmic_bytes_per_launch": crc_alg, "avg_launch_ms": round(crc_kern_ms, 4)}}
         # ---- read path: framing walk, then framing + verify, over the same segment images
         n_seg = args.crc_segments
@@ -416,30 +414,23 @@ def main():
         f1.record(stream)
         barrier()
         read_ms = f0.elapsed_time(f1) / args.crc_steps
-        # rh_segments_read_launch (LogSegment.readSegmentFile in one call): default variant 2 = framing
-        # walk + CRC v8 over the slotted frame table + verdict; variant 0 = the one-pass LDS-ring kernel
-        lib = _lib.load()
+        # rh_segments_read_launch (LogSegment.readSegmentFile in one call): framing walk + CRC over
+        # the slotted frame table + verdict
         fbatch = engine.SegmentBatch(buf=fb.buf, seg_off=sb.seg_off, seg_len=sb.seg_len,
                                      frames_per_seg_cap=ss.frames_per_segment + 16)
-        read_api = {}
-        for var in (2, 0):
-            _lib.check(lib.rh_segments_read_set_variant(var))
-            for _ in range(2):
-                fout = engine.read_segments_fused(ctx, fbatch, stream=stream)
-            barrier()
-            f0.record(stream)
-            for _ in range(args.crc_steps):
-                fout = engine.read_segments_fused(ctx, fbatch, stream=stream)
-            f1.record(stream)
-            barrier()
-            ms_v = f0.elapsed_time(f1) / args.crc_steps
-            fbad = np.nonzero(np.unpackbits(fout["bad_bits"].cpu().numpy().view(np.uint8), bitorder="little")[: fb.n])[0]
-            ok_v = bool(np.array_equal(fbad, ss.corrupted) and int(fbatch.total_frames.item()) == fb.n
-                        and torch.equal(fbatch.frame_off[: fb.n], fb.frame_off)
-                        and torch.equal(fout["crc_out"][: fb.n], fb.crc_out[: fb.n]))
-            read_api[var] = (ms_v, ok_v)
-        _lib.check(lib.rh_segments_read_set_variant(2))
-        fused_ms, fused_ok = read_api[0]
+        for _ in range(2):
+            fout = engine.read_segments_fused(ctx, fbatch, stream=stream)
+        barrier()
+        f0.record(stream)
+        for _ in range(args.crc_steps):
+            fout = engine.read_segments_fused(ctx, fbatch, stream=stream)
+        f1.record(stream)
+        barrier()
+        rl_ms = f0.elapsed_time(f1) / args.crc_steps
+        fbad = np.nonzero(np.unpackbits(fout["bad_bits"].cpu().numpy().view(np.uint8), bitorder="little")[: fb.n])[0]
+        rl_ok = bool(np.array_equal(fbad, ss.corrupted) and int(fbatch.total_frames.item()) == fb.n
+                     and torch.equal(fbatch.frame_off[: fb.n], fb.frame_off)
+                     and torch.equal(fout["crc_out"][: fb.n], fb.crc_out[: fb.n]))
         del fbatch, fout
         seg_bytes = n_seg * ss.segment_size
         tot_seg_bytes = sum_over_ranks(seg_bytes)
@@ -456,16 +447,9 @@ def main():
             "framing_traffic_bytes": (round(pmc["framing_bytes_per_unit"] * n_seg) if "framing_bytes_per_unit" in pmc
                                       else None),
             "framing_plus_verify_GBps": round(tot_seg_bytes / (max_over_ranks(read_ms) * 1e-3) / 1e9, 1),
-            "read_launch_GBps": round(tot_seg_bytes / (max_over_ranks(read_api[2][0]) * 1e-3) / 1e9, 1),
-            "ms_read_launch": round(read_api[2][0], 4), "read_launch_parity_ok": read_api[2][1],
-            "read_launch_note": "rh_segments_read_launch default (walk + CRC v8 + verdict in one call)",
-            "fused_read_GBps": round(tot_seg_bytes / (max_over_ranks(fused_ms) * 1e-3) / 1e9, 1),
-            "ms_fused_read": round(fused_ms, 4), "fused_parity_ok": fused_ok,
-            "fused_roofline": {"bound": "hbm", "achieved": round(seg_bytes / (fused_ms * 1e-3) / 1e9, 1),
-                               "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                               "frac": round(seg_bytes / (fused_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
-                               "kernel": "segment_read_kernel<36> (variant 0: framing + CRC verify in one HBM pass) + scan + compact",
-                               "algorithmic_bytes_per_launch": seg_bytes},
+            "read_launch_GBps": round(tot_seg_bytes / (max_over_ranks(rl_ms) * 1e-3) / 1e9, 1),
+            "ms_read_launch": round(rl_ms, 4), "read_launch_parity_ok": rl_ok,
+            "read_launch_note": "rh_segments_read_launch (walk + CRC + verdict in one call)",
             "unit": "GB/s (segment bytes, whole job)", "frames_found": nfr_found, "parity_ok": bool(frame_ok),
             "ms_framing": round(scan_ms, 4), "ms_framing_plus_verify": round(read_ms, 4),
             "roofline": {"bound": "hbm", "achieved": round(read_ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
@@ -473,7 +457,7 @@ def main():
                          "traffic": ((round(pmc["framing_bytes_per_unit"] * n_seg) if "framing_bytes_per_unit" in pmc
                                       else 0) + round(pmc.get("crc_bytes_per_unit", 0) * fb.n)) or None,
                          "traffic_source": pmc.get("_path"),
-                         "kernel": "segment_walk_kernel2<32768> (+ scan, compact) then crc_frames_kernel8<2,2>",
+                         "kernel": "segment_walk_kernel<32768> (+ scan, compact) then crc_frames_kernel",
                          "algorithmic_bytes_per_launch": read_alg}}
         del sb, rb
         if not args.no_pcie:
@@ -549,7 +533,7 @@ def main():
         lease = {"checks_per_s": round(total_groups / (lease_ms * 1e-3), 1), "unit": "hasLease checks/s (whole job)",
                  "ms_per_pass": round(lease_ms, 5), "parity_ok": lease_ok, "timeout_ms": TIMEOUT_MS,
                  "roofline": {"bound": "hbm", "achieved": round(lease_ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                              "frac": round(lease_ach / HBM_PEAK_GBPS, 4), "kernel": "lease_kernel<0,7,NT,8> (variant 2: F=4, 6 tiers fused)",
+                              "frac": round(lease_ach / HBM_PEAK_GBPS, 4), "kernel": "lease_kernel<0,7,true,8> (F=4, 6 tiers fused)",
                               "traffic": (round(pmc["lease_bytes_per_unit"] * n_mine) if "lease_bytes_per_unit" in pmc
                                           else None),
                               "traffic_source": pmc.get("_path"),

@@ -23,8 +23,8 @@
  * Conventions (all entry points):
  *   - Plain C types only; no exception crosses the ABI.  Every int-returning function returns
  *     RH_OK (0) or a negative RH_E_* code; rh_last_error() then holds a message for the calling
- *     thread (the Java binding maps RH_E_INVAL to IllegalArgumentException, others to
- *     IOException -- see INTEGRATION.md).
+ *     thread (the Java binding maps RH_E_INVAL and RH_E_RANGE to IllegalArgumentException, the
+ *     others to IOException -- see INTEGRATION.md).
  *   - "_launch" functions take DEVICE pointers, enqueue work on `stream` (a hipStream_t, used
  *     as given: NULL is the HIP null stream; rh_ctx_stream() returns the context's own stream)
  *     and return without synchronising.
@@ -79,7 +79,10 @@ void* rh_ctx_stream(rh_ctx* ctx);
  *   bits 16..29  follower slot k is a voter of oldConf with a FollowerInfo
  *   bit   30     includeSelfInOldConf = conf.containsInOldConf(selfId)       (LSI:975)
  *   bit   31     active: this division is LEADER and should be evaluated (inactive => no result)
- * Listeners are never voters (PeerConfiguration keeps them in a separate map). */
+ * Listeners are never voters (PeerConfiguration keeps them in a separate map).
+ * A word is MALFORMED for a tier of F follower slots when bits 0..13 or 16..29 name a slot >= F:
+ * the commit and lease kernels then treat the group as inactive (no result, no commit, no lease)
+ * rather than evaluating a quorum over fewer voters. */
 #define RH_MAX_FOLLOWERS    14u
 #define RH_CONF_SELF        (1u << 14)
 #define RH_CONF_TRANSITIONAL (1u << 15)
@@ -215,12 +218,16 @@ typedef struct rh_frames {
     uint32_t init_state;          /* PureJavaCrc32C state before update(): 0xFFFFFFFF = reset() */
     uint32_t reserved;
     uint32_t* crc_out;            /* [n] optional: getValue() after update(frame bytes)          */
-    uint64_t* bad_bits;           /* [ceil(n/64)] optional (VERIFY): stored != computed         */
-    unsigned long long* n_bad;    /* optional (VERIFY): mismatches are atomically added here    */
+    uint64_t* bad_bits;           /* [ceil(n/64)] optional: stored != computed (VERIFY), or the
+                                     frame is malformed (any flags; see rh_crc32c_frames_launch) */
+    unsigned long long* n_bad;    /* optional: such frames are atomically added here             */
 } rh_frames;
 
-/* CRC of every frame (one launch).  Frames must lie inside [0, buf_len); lengths <= 2^31.
- * Spans shorter than 4 bytes are supported. */
+/* CRC of every frame (one launch).  Lengths <= 2^31; spans shorter than 4 bytes are supported.
+ * A MALFORMED frame -- one that does not lie inside [0, buf_len), or (VERIFY/STAMP) is shorter
+ * than its 4-byte trailer -- gets crc_out = 0 and, under EVERY flag setting, its bad bit set and
+ * n_bad incremented; in STAMP mode it is not stamped.  So bad_bits / n_bad report "mismatch or
+ * malformed" for VERIFY and "malformed" for STAMP and flags = 0. */
 int rh_crc32c_frames_launch(rh_ctx* ctx, const rh_frames* frames, uint32_t flags, void* stream);
 
 /* Host-buffer convenience (PCIe-inclusive): copies the segment image and frame table to the
@@ -269,7 +276,7 @@ int rh_lease_soa_launch(rh_ctx* ctx, const rh_lease_soa* tiers, int n_tiers, voi
  * padding is all zero (RDR:251-280).  The walk applies decodeEntry's size rules (maxOpSize, the
  * LimitedInputStream limit) and EOF rules; it does NOT check CRCs -- feed the produced frame table
  * to rh_crc32c_frames_launch(RH_CRC_VERIFY), exactly as readSegmentFile would verify each entry.
- * One wave per segment; the serial varint chain is walked out of LDS windows. */
+ * One 256-thread block per segment; the serial varint chain is walked out of LDS windows. */
 #define RH_SEG_END          1   /* clean end: EOF at an entry boundary or zero padding to EOF  */
 #define RH_SEG_PARTIAL      2   /* last entry truncated (readEntry returns null, RDR:221-229)  */
 #define RH_SEG_E_OVERSIZE  -1   /* entry larger than maxOpSize (RDR:314-317, limit checks)      */
@@ -277,6 +284,8 @@ int rh_lease_soa_launch(rh_ctx* ctx, const rh_lease_soa* tiers, int n_tiers, voi
 #define RH_SEG_E_VARINT    -4   /* malformed / truncated varint (CodedInputStream)             */
 #define RH_SEG_E_HEADER    -5   /* corrupted header (CorruptedFileException, RDR:201-204)       */
 #define RH_SEG_E_CAPACITY  -6   /* more frames than frames_per_seg_cap                          */
+#define RH_SEG_E_RANGE     -7   /* seg_off / seg_len outside [0, buf_len): a caller error, the
+                                   segment is not walked (nothing is clamped)                    */
 
 typedef struct rh_segments {
     const uint8_t* buf;           /* device: segment images                                     */
@@ -300,11 +309,11 @@ typedef struct rh_segments {
 
 int rh_segments_scan_launch(rh_ctx* ctx, const rh_segments* segs, void* stream);
 
-/* ---- fused read path (LogSegment.readSegmentFile, LogSegment.java:166-196) ----------------
- * Framing walk + CRC32C verification of every frame (decodeEntry's checksum, RDR:327-336) in ONE
- * pass over HBM: fills every rh_segments output exactly as rh_segments_scan_launch does, plus the
- * per-frame CRCs and the reader's verdict per segment -- the reader stops at the first frame
- * whose CRC does not verify (ChecksumException at that frame's offset). */
+/* ---- read path (LogSegment.readSegmentFile, LogSegment.java:166-196) ----------------------
+ * Framing walk + CRC32C verification of every frame (decodeEntry's checksum, RDR:327-336) in one
+ * call: fills every rh_segments output exactly as rh_segments_scan_launch does, plus the per-frame
+ * CRCs and the reader's verdict per segment -- the reader stops at the first frame whose CRC does
+ * not verify (ChecksumException at that frame's offset). */
 #define RH_SEG_E_CHECKSUM  -2   /* a frame's stored CRC != computed (ChecksumException, RDR:330-336) */
 typedef struct rh_segments_crc {
     uint32_t* scratch_crc;        /* [n_seg * frames_per_seg_cap] computed CRC (getValue()) per slot */
@@ -316,49 +325,6 @@ typedef struct rh_segments_crc {
     unsigned long long* n_bad;    /* optional: CRC mismatches over all found frames (added)          */
 } rh_segments_crc;
 int rh_segments_read_launch(rh_ctx* ctx, const rh_segments* segs, const rh_segments_crc* crc, void* stream);
-/* Framing kernel variant (identical results): 0 = one wave per segment, 16 KiB LDS window;
- * 1 / 2 = one 256-thread block per segment, double-buffered 32 / 64 KiB windows (default 1);
- * 3 = 16 KiB windows plus a per-position frame-length table, switched on after a window of >= 24
- * frames of differing lengths; 4 / 5 = the same kernel with the table never / always used (A/B).
- * Measured: the table does not pay on gfx950 (ragged 64-2048 B frames, 32 segments: 1 = 129,
- * 3 = 119, 5 = 62 GB/s) -- the per-frame cost is the walk's dependent latency, not the decode. */
-int rh_segments_set_variant(int variant);
-/* Read-path variants (identical results): 0 / 1 = one-pass LDS-ring kernel with 16 lanes x 36 / 20
- * byte CRC units; 2 (default) = framing walk (header fast-forward) + CRC32C over the slotted frame
- * table + verdict, which is faster. */
-int rh_segments_read_set_variant(int variant);
-/* Fused-read instrumentation (tuning only): enable = 1 zeroes the per-block cycle counters and
- * switches rh_segments_read_launch to the instrumented kernel, 0 switches back, -1 leaves it; if
- * out != NULL, the first n counters ([1024 blocks][8]) are copied to host memory (synchronises). */
-int rh_segments_read_profile(int enable, uint64_t* out, uint64_t n);
-
-/* ---- tuning hooks (bench / A-B experiments; results are identical for every variant) ---- */
-/* CRC kernel variants (identical results; see DESIGN.md "CRC kernel history"):
- *   0-3   v1: Q lanes x S bytes per window + log-tree combine (0: 64x64, 1: 16x256, 2: 8x512,
- *         3: 64x64 with shared bank-conflicting tables)
- *   4-6   v2: + one window prefetched;  7-10 v3: branch-free fold with guarded slow path
- *   11-13 v4: per-lane zero-advance (lane-distance nibble tables) instead of the tree
- *   14-17 v5: v4 + one-v_perm table addressing; 14: 1 window in flight, 15: 2, 16: 3,
- *         17: 32-lane windows, 2 in flight
- *   18-20 v7: 128-byte lane chunks;  21-22 v5 with non-temporal loads (2 / 1 windows in flight)
- *   23-25 v8: copy-free 3-slot ring + LDS-staged frame table, 1 / 2 / 4 fold chains per lane
- *         (24 = default).  rh_crc32c_num_variants() counts these exact kernels (26); index 26
- *         (rh_crc32c_frames_launch_variant only) is an access-pattern ablation whose CRCs are
- *         NOT PureJavaCrc32C values. */
-/* Commit kernel variants (see commit.hip): 0-2 sorting network with 1/2/4 sub-tiles of 128
- * groups per wave; 3 split F classes; 4-7 persistent software-pipelined; 8-14 rank-mask
- * selection at 8 waves/SIMD (12-14 with non-temporal loads); 15 = 0 with non-temporal loads. */
-int rh_commit_num_variants(void);
-int rh_commit_set_variant(int variant);
-/* Lease kernel variants: 0 plain loads, 1 non-temporal loads, 2 = 1 at 8 waves/SIMD, 3 = 0 at
- * 8 waves/SIMD. */
-int rh_lease_num_variants(void);
-int rh_lease_set_variant(int variant);
-int rh_crc32c_num_variants(void);
-int rh_crc32c_set_variant(int variant);
-int rh_crc32c_frames_launch_variant(rh_ctx* ctx, const rh_frames* frames, uint32_t flags, int variant,
-                                    void* stream);
-
 #ifdef __cplusplus
 }
 #endif

@@ -163,19 +163,21 @@ ORC_API uint64_t orc_crc32c_frames(const uint8_t* buf, const uint64_t* off, cons
 /* MinMajorityMax (LSI:904-944). */
 typedef struct { int64_t min, majority, max; } orc_mmm;
 
-static int cmp_i64(const void* a, const void* b) {
-    const int64_t x = *(const int64_t*)a, y = *(const int64_t*)b;
-    return (x > y) - (x < y);
-}
-
 /* LSI:1076-1095 getSorted: followers in list order, then self (logIndex) last, then
- * Arrays.sort ascending.  n == 0 throws IllegalArgumentException in Java; callers guard it. */
+ * Arrays.sort ascending.  For arrays shorter than 47 elements the JDK's DualPivotQuicksort.sort
+ * (long[]) is a plain insertion sort (INSERTION_SORT_THRESHOLD), which is what runs here (n <= 15).
+ * n == 0 throws IllegalArgumentException in Java; callers guard it. */
 static int orc_get_sorted(const int64_t* follower_vals, const uint8_t* member, int nf, int include_self,
                           int64_t self_val, int64_t* out) {
     int n = 0;
     for (int i = 0; i < nf; i++) if (member[i]) out[n++] = follower_vals[i];
     if (include_self) out[n++] = self_val;
-    qsort(out, (size_t)n, sizeof(int64_t), cmp_i64);
+    for (int i = 1; i < n; i++) {
+        const int64_t x = out[i];
+        int j = i - 1;
+        while (j >= 0 && out[j] > x) { out[j + 1] = out[j]; j--; }
+        out[j + 1] = x;
+    }
     return n;
 }
 
@@ -305,7 +307,11 @@ ORC_API void orc_commit_soa(uint64_t n, uint32_t nf, int mode, int64_t gap,
         }
         int64_t mmm[3];
         int valid = 0;
-        if (ORC_CONF_ACTIVE(w))
+        /* ABI rule (not Java's): a word naming a follower slot >= nf is malformed for this tier
+         * and yields no result -- never a majority over fewer voters (include/ratis_hip.h). */
+        const uint32_t fm = (1u << nf) - 1u;
+        const int fits = (ORC_CONF_NEW_MASK(w) & ~fm) == 0 && (ORC_CONF_OLD_MASK(w) & ~fm) == 0;
+        if (ORC_CONF_ACTIVE(w) && fits)
             valid = orc_get_majority_min(vals, (int)nf, in_new, in_old, (int)ORC_CONF_SELF(w),
                                          (int)ORC_CONF_TRANSITIONAL(w), (int)ORC_CONF_SELF_OLD(w),
                                          self_index[g], mode == 0 ? gap : -1, mmm);
@@ -416,7 +422,9 @@ ORC_API void orc_lease_soa(uint64_t n, uint32_t nf, int64_t now, int64_t timeout
     if (extended_bits) memset(extended_bits, 0, nwords * 8);
     for (uint64_t g = 0; g < n; g++) {
         const uint32_t w = conf[g];
-        if (!ORC_CONF_ACTIVE(w)) { lease_out[g] = lease_in[g]; continue; }
+        const uint32_t fm = (1u << nf) - 1u;   /* same malformed-word rule as orc_commit_soa */
+        const int fits = (ORC_CONF_NEW_MASK(w) & ~fm) == 0 && (ORC_CONF_OLD_MASK(w) & ~fm) == 0;
+        if (!ORC_CONF_ACTIVE(w) || !fits) { lease_out[g] = lease_in[g]; continue; }
         int64_t cur[16], old[16];
         int nc = 0, no = 0;
         for (uint32_t i = 0; i < nf; i++) {

@@ -127,6 +127,7 @@ RH_SEG_E_PADDING = -3
 RH_SEG_E_VARINT = -4
 RH_SEG_E_HEADER = -5
 RH_SEG_E_CAPACITY = -6
+RH_SEG_E_RANGE = -7
 
 
 class RhSegments(ctypes.Structure):
@@ -190,17 +191,7 @@ _SIGNATURES = {
                                       c_void_p, POINTER(c_uint64)]),
     "rh_lease_soa_launch": (c_int, [c_void_p, POINTER(RhLeaseSoa), c_int, c_void_p]),
     "rh_segments_scan_launch": (c_int, [c_void_p, POINTER(RhSegments), c_void_p]),
-    "rh_segments_set_variant": (c_int, [c_int]),
-    "rh_segments_read_profile": (c_int, [c_int, c_void_p, c_uint64]),
-    "rh_segments_read_set_variant": (c_int, [c_int]),
     "rh_segments_read_launch": (c_int, [c_void_p, POINTER(RhSegments), POINTER(RhSegmentsCrc), c_void_p]),
-    "rh_crc32c_num_variants": (c_int, []),
-    "rh_commit_num_variants": (c_int, []),
-    "rh_commit_set_variant": (c_int, [c_int]),
-    "rh_crc32c_set_variant": (c_int, [c_int]),
-    "rh_lease_num_variants": (c_int, []),
-    "rh_lease_set_variant": (c_int, [c_int]),
-    "rh_crc32c_frames_launch_variant": (c_int, [c_void_p, POINTER(RhFrames), c_uint32, c_int, c_void_p]),
 }
 
 

@@ -74,7 +74,11 @@ __device__ __forceinline__ void lease_one(const rh_lease_soa& t, const int64_t (
     }
     const uint32_t nm = w & 0x3FFFu, om = (w >> 16) & 0x3FFFu;
     const bool self = (w & RH_CONF_SELF) != 0, self_old = (w & RH_CONF_SELF_OLD) != 0;
-    const bool trans = (w & RH_CONF_TRANSITIONAL) != 0, active = (w & RH_CONF_ACTIVE) != 0;
+    // a word naming a follower slot >= F is malformed for this tier: treated as inactive (no
+    // lease, no extension), the same rule as the commit kernel and the oracle
+    constexpr uint32_t fm = (1u << F) - 1u;
+    const bool trans = (w & RH_CONF_TRANSITIONAL) != 0,
+               active = (w & RH_CONF_ACTIVE) != 0 && ((nm | om) & ~fm) == 0;
     // RaftConfigurationImpl.isSingleton (RCI:296-298)
     const int cur_size = __builtin_popcount(nm) + (self ? 1 : 0);
     const int prev_size = trans ? __builtin_popcount(om) + (self_old ? 1 : 0) : 0;
@@ -186,11 +190,6 @@ __device__ __forceinline__ void lease_dispatch(const rh_lease_soa& t, bool vec, 
     }
 }
 
-// Variants (rh_lease_set_variant): 0 plain loads; 1 non-temporal loads; 2 non-temporal loads
-// with the register budget pinned to 8 waves/SIMD; 3 plain loads, 8 waves/SIMD.
-int g_lease_variant = 2;  // fastest measured
-constexpr int kNumLeaseVariants = 4;
-
 template <int FLO, int FHI, bool NT, int MINW>
 __global__ __launch_bounds__(kLeaseBlock) __attribute__((amdgpu_waves_per_eu(MINW, 8))) void lease_kernel(LeaseLaunch a) {
     const uint64_t b = blockIdx.x;
@@ -226,16 +225,12 @@ int launch_class(const rh_lease_soa* tiers, int n_tiers, int flo, int fhi, hipSt
     a.first_block[a.n_tiers] = blocks;
     if (blocks > 0x7fffffffull) return rh::fail(RH_E_RANGE, "rh_lease_soa_launch: too many groups");
     const dim3 g((uint32_t)blocks), b(kLeaseBlock);
+    // F <= 7: non-temporal loads (every byte is read once), register budget pinned to 8
+    // waves/SIMD so a 1M-group launch is resident in one round; wider tiers: plain loads
     if (flo != 0)
         hipLaunchKernelGGL((lease_kernel<8, 14, false, 1>), g, b, 0, stream, a);
-    else if (g_lease_variant == 1)
-        hipLaunchKernelGGL((lease_kernel<0, 7, true, 1>), g, b, 0, stream, a);
-    else if (g_lease_variant == 2)
-        hipLaunchKernelGGL((lease_kernel<0, 7, true, 8>), g, b, 0, stream, a);
-    else if (g_lease_variant == 3)
-        hipLaunchKernelGGL((lease_kernel<0, 7, false, 8>), g, b, 0, stream, a);
     else
-        hipLaunchKernelGGL((lease_kernel<0, 7, false, 1>), g, b, 0, stream, a);
+        hipLaunchKernelGGL((lease_kernel<0, 7, true, 8>), g, b, 0, stream, a);
     RH_HIP(hipGetLastError());
     return RH_OK;
 }
@@ -260,11 +255,3 @@ int rh_lease_launch_impl(rh_ctx* ctx, const rh_lease_soa* tiers, int n_tiers, hi
     if (rc != RH_OK) return rc;
     return launch_class(tiers, n_tiers, 8, 14, stream);
 }
-
-int rh_lease_set_variant_impl(int v) {
-    if (v < 0 || v >= kNumLeaseVariants) return rh::fail(RH_E_INVAL, "unknown lease kernel variant");
-    g_lease_variant = v;
-    return RH_OK;
-}
-
-int rh_lease_num_variants_impl() { return kNumLeaseVariants; }

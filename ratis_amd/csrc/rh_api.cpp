@@ -132,13 +132,6 @@ RH_EXPORT int rh_shutdown(rh_ctx* ctx) {
     (void)hipFree(ctx->d_slice);
     (void)hipFree(ctx->d_shift);
     (void)hipFree(ctx->d_lane16);
-    (void)hipFree(ctx->d_lane32);
-    (void)hipFree(ctx->d_lane64);
-    (void)hipFree(ctx->d_lane16_s128);
-    (void)hipFree(ctx->d_lane8_s128);
-    (void)hipFree(ctx->d_lane16_s36);
-    (void)hipFree(ctx->d_zu576);
-    for (uint32_t* p : ctx->d_read_tables) (void)hipFree(p);
     (void)hipFree(ctx->d_scratch);
     if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
     (void)hipStreamDestroy(ctx->stream);
@@ -506,33 +499,6 @@ RH_EXPORT int rh_segments_read_launch(rh_ctx* ctx, const rh_segments* segs, cons
     if (!ctx) return rh::fail(RH_E_INVAL, "rh_segments_read_launch: ctx == NULL");
     DeviceGuard g(ctx->device);
     return rh_segments_read_impl(ctx, segs, crc, pick_stream(ctx, stream));
-}
-
-RH_EXPORT int rh_segments_set_variant(int variant) { return rh_segments_set_variant_impl(variant); }
-
-RH_EXPORT int rh_segments_read_set_variant(int variant) { return rh_segments_read_set_variant_impl(variant); }
-
-RH_EXPORT int rh_segments_read_profile(int enable, uint64_t* out, uint64_t n) {
-    return rh_segments_read_profile_impl(enable, out, n);
-}
-
-RH_EXPORT int rh_crc32c_num_variants(void) { return rh_crc_num_variants(); }
-
-RH_EXPORT int rh_commit_num_variants(void) { return rh_commit_num_variants_impl(); }
-
-RH_EXPORT int rh_commit_set_variant(int variant) { return rh_commit_set_variant_impl(variant); }
-
-RH_EXPORT int rh_crc32c_set_variant(int variant) { return rh_crc_set_default_variant(variant); }
-
-RH_EXPORT int rh_lease_num_variants(void) { return rh_lease_num_variants_impl(); }
-
-RH_EXPORT int rh_lease_set_variant(int variant) { return rh_lease_set_variant_impl(variant); }
-
-RH_EXPORT int rh_crc32c_frames_launch_variant(rh_ctx* ctx, const rh_frames* frames, uint32_t flags, int variant,
-                                              void* stream) {
-    if (!ctx) return rh::fail(RH_E_INVAL, "rh_crc32c_frames_launch_variant: ctx == NULL");
-    DeviceGuard g(ctx->device);
-    return rh_crc_launch_variant(ctx, frames, flags, variant, pick_stream(ctx, stream));
 }
 
 RH_EXPORT int rh_crc32c(rh_ctx* ctx, uint32_t crc_state, const void* data, uint64_t n, uint32_t* out_state) {

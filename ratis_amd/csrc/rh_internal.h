@@ -43,14 +43,7 @@ struct rh_ctx {
     // device copies of the CRC tables
     uint32_t* d_slice = nullptr;   // [4][256]
     uint32_t* d_shift = nullptr;   // [41][4][256]: zero-advance maps over 2^m bytes, m = 0..40
-    uint32_t* d_lane16 = nullptr;  // lane-distance nibble tables for 16/32/64-lane windows
-    uint32_t* d_lane32 = nullptr;
-    uint32_t* d_lane64 = nullptr;
-    uint32_t* d_lane16_s128 = nullptr;  // same for 16 / 8 lanes x 128-byte chunks (kernel v7)
-    uint32_t* d_lane8_s128 = nullptr;
-    uint32_t* d_lane16_s36 = nullptr;   // 16 lanes x 36-byte chunks (fused read kernel)
-    uint32_t* d_zu576 = nullptr;        // [4][256]: advance over 576 zero bytes
-    uint32_t* d_read_tables[2] = {nullptr, nullptr};  // fused read kernel, per variant (segread.hip)
+    uint32_t* d_lane16 = nullptr;  // lane-distance nibble tables of the 16-lane x 64-byte fold
     // scratch for host-buffer convenience calls
     std::mutex mu;
     void* d_scratch = nullptr;
@@ -66,19 +59,7 @@ int rh_apply_deltas_impl(hipStream_t stream, const rh_delta* d_deltas, uint64_t 
                          int64_t* flush, int64_t* commit);
 int rh_crc_launch_impl(rh_ctx* ctx, const rh_frames* f, uint32_t flags, hipStream_t stream);
 int rh_crc_upload_tables(rh_ctx* ctx);
-int rh_crc_launch_variant(rh_ctx* ctx, const rh_frames* f, uint32_t flags, int variant, hipStream_t stream);
-int rh_crc_set_default_variant(int v);
-int rh_crc_num_variants();
-int rh_commit_set_variant_impl(int v);
-int rh_commit_num_variants_impl();
 int rh_segments_launch_impl(rh_ctx* ctx, const rh_segments* segs, hipStream_t stream);
-int rh_segments_set_variant_impl(int v);
-int rh_segments_scan_counts(const uint32_t* nframes, uint64_t n_seg, uint32_t cap, uint64_t* seg_first,
-                            unsigned long long* total, hipStream_t stream);
 int rh_segments_read_impl(rh_ctx* ctx, const rh_segments* segs, const rh_segments_crc* crc, hipStream_t stream);
-int rh_segments_read_profile_impl(int enable, uint64_t* out, uint64_t n);
-int rh_segments_read_set_variant_impl(int v);
 int rh_crc_verify_slots(rh_ctx* ctx, const rh_segments* segs, const rh_segments_crc* crc, hipStream_t stream);
 int rh_lease_launch_impl(rh_ctx* ctx, const rh_lease_soa* tiers, int n_tiers, hipStream_t stream);
-int rh_lease_set_variant_impl(int v);
-int rh_lease_num_variants_impl();

@@ -9,15 +9,16 @@
 //   SegmentedRaftLogFormat header/terminator SegmentedRaftLogFormat.java:30-80
 //
 // The walk is a serial chain (each frame's length is a varint at its start), so the parallelism
-// is across segments: one wave per segment.  The wave stages a 16 KiB window of the segment in
-// LDS with wide coalesced loads; lane 0 walks every frame header inside the window out of LDS,
-// and the wave reloads at the walk position when it runs out.  Terminator padding is checked
-// by the whole wave.  Frames are written to a per-segment slotted table, then compacted.
+// is across segments: one 256-thread block per segment, two blocks per CU.  The segment streams
+// through a 2 x 32 KiB LDS ring; wave 0 walks the frames that start in the current window
+// (speculating on runs of equal-length frames: lane j checks the header at p + j*s), the block's
+// loads of the window after next are in flight meanwhile, and a run that leaves the window is
+// followed straight through HBM reading frame headers only.  Terminator padding is checked by
+// the whole block.  Frames are written to a per-segment slotted table, then compacted.
 #include "rh_internal.h"
 
 namespace {
 
-constexpr int kWin = 16384;     // LDS window bytes
 constexpr int kScanThreads = 1024;
 
 struct SegArgs {
@@ -50,211 +51,7 @@ struct __attribute__((aligned(4))) u32x4s {
     uint32_t x, y, z, w;
 };
 
-__global__ __launch_bounds__(64) void segment_walk_kernel(SegArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t win[kWin + 16];
-    const int lane = threadIdx.x;
-    for (uint64_t s = blockIdx.x; s < a.n_seg; s += gridDim.x) {
-        const int64_t base = (int64_t)a.seg_off[s];
-        int64_t L = (int64_t)a.seg_len[s];
-        if (base > a.buf_len) L = 0;
-        else if (L > a.buf_len - base) L = a.buf_len - base;   // never read past the buffer
-        const uint8_t* seg = a.buf + base;
-        int status = kWalking;
-        int64_t pos = 0;
-        uint32_t nfr = 0;
-        // ---- verifyHeader (RDR:179-205) ----
-        {
-            const char H[8] = {'R', 'a', 'f', 't', 'L', 'o', 'g', '1'};
-            const int64_t rl = L < 8 ? L : 8;
-            int match = 0;
-            int bad = 0;
-            for (int i = 0; i < rl; ++i) {
-                const uint8_t b = seg[i];
-                if (match == i && b == (uint8_t)H[i]) match = i + 1;
-                else if (b != 0) bad = 1;   // a non-terminator byte after the matched prefix
-            }
-            if (rl == 8 && match == 8) {
-                pos = 8;
-            } else {
-                status = bad ? RH_SEG_E_HEADER : RH_SEG_END;  // partially written header => empty
-                pos = 0;
-            }
-        }
-        int64_t wbase = -(int64_t)kWin * 4;  // no window yet
-        while (status == kWalking) {
-            if (pos >= L) {
-                status = RH_SEG_END;
-                break;
-            }
-            // window must hold the (up to 10) varint bytes at pos, or reach the segment end
-            if (!(pos >= wbase && (pos + 16 <= wbase + kWin || wbase + kWin >= L))) {
-                wbase = ((base + pos) & ~(int64_t)15) - base;  // 16-B aligned in the buffer
-                __syncthreads();
-                if (wbase >= 0 && wbase + kWin <= L) {
-                    u32x4s v[kWin / (64 * 16)];
-#pragma unroll
-                    for (int i = 0; i < kWin / (64 * 16); ++i)
-                        v[i] = *reinterpret_cast<const u32x4s*>(seg + wbase + (i * 64 + lane) * 16);
-#pragma unroll
-                    for (int i = 0; i < kWin / (64 * 16); ++i)
-                        *reinterpret_cast<u32x4s*>(win + (i * 64 + lane) * 16) = v[i];
-                } else
-#pragma unroll 4
-                for (int i = 0; i < kWin / (64 * 16); ++i) {
-                    const int off = (i * 64 + lane) * 16;
-                    const int64_t p = wbase + off;
-                    u32x4s v{0, 0, 0, 0};
-                    if (p >= 0 && p + 16 <= L) {
-                        v = *reinterpret_cast<const u32x4s*>(seg + p);
-                    } else if (p < L) {
-                        uint32_t w[4] = {0, 0, 0, 0};
-                        for (int k = p < 0 ? (int)-p : 0; k < 16 && p + k < L; ++k)
-                            w[k >> 2] |= (uint32_t)seg[p + k] << (8 * (k & 3));
-                        v = {w[0], w[1], w[2], w[3]};
-                    }
-                    *reinterpret_cast<u32x4s*>(win + off) = v;
-                }
-                __syncthreads();
-            }
-            // lane 0 walks every frame header available in the window
-            if (lane == 0) {
-                while (status == kWalking) {
-                    if (pos >= L) {
-                        status = RH_SEG_END;
-                        break;
-                    }
-                    if (!(pos + 16 <= wbase + kWin || wbase + kWin >= L)) break;  // reload
-                    const uint8_t* w = win + (pos - wbase);
-                    if (w[0] == 0) {  // terminator (SegmentedRaftLogFormat.isTerminator)
-                        status = kTermPending;
-                        break;
-                    }
-                    // CodedInputStream.readRawVarint32(firstByte, in); EOF -> truncatedMessage
-                    uint32_t result = 0;
-                    bool done = false, trunc = false;
-                    for (int i = 0; i < 5; ++i) {
-                        if (pos + i >= L) {
-                            trunc = true;
-                            break;
-                        }
-                        const uint8_t b = w[i];
-                        result |= (uint32_t)(b & 0x7f) << (7 * i);
-                        if ((b & 0x80) == 0) {
-                            done = true;
-                            break;
-                        }
-                    }
-                    if (!done && !trunc) {
-                        for (int i = 5; i < 10; ++i) {
-                            if (pos + i >= L) {
-                                trunc = true;
-                                break;
-                            }
-                            if ((w[i] & 0x80) == 0) {
-                                done = true;
-                                break;
-                            }
-                        }
-                    }
-                    if (!done) {
-                        status = RH_SEG_E_VARINT;
-                        break;
-                    }
-                    const int32_t n = (int32_t)result;
-                    if (n > (int32_t)a.max_op) {
-                        status = RH_SEG_E_OVERSIZE;
-                        break;
-                    }
-                    if (n < 0) {
-                        status = RH_SEG_E_VARINT;
-                        break;
-                    }
-                    const int64_t total = (int64_t)varint32_size((uint32_t)n) + n;
-                    if (total > (int64_t)a.max_op) {  // checkBufferSize assertion
-                        status = RH_SEG_E_OVERSIZE;
-                        break;
-                    }
-                    if (pos + total > L) {  // readFully EOF
-                        status = RH_SEG_PARTIAL;
-                        break;
-                    }
-                    bool stop = false;
-                    for (int k = 1; k <= 4; ++k) {  // readInt: checkLimit(1) before each read
-                        if (total + k > (int64_t)a.max_op) {
-                            status = RH_SEG_E_OVERSIZE;
-                            stop = true;
-                            break;
-                        }
-                        if (pos + total + k > L) {
-                            status = RH_SEG_PARTIAL;
-                            stop = true;
-                            break;
-                        }
-                    }
-                    if (stop) break;
-                    if (nfr >= a.cap) {
-                        status = RH_SEG_E_CAPACITY;
-                        break;
-                    }
-                    a.scratch_off[s * (uint64_t)a.cap + nfr] = (uint64_t)(base + pos);
-                    a.scratch_len[s * (uint64_t)a.cap + nfr] = (uint32_t)(total + 4);
-                    ++nfr;
-                    pos += total + 4;
-                }
-            }
-            status = __shfl(status, 0);
-            pos = __shfl(pos, 0);
-            nfr = __shfl(nfr, 0);
-        }
-        if (status == kTermPending) {
-            // verifyTerminator: every byte from pos to EOF must be zero; report the first that is not
-            int64_t first_bad = L;
-            for (int64_t p0 = pos; p0 < L; p0 += 64 * 16) {
-                const int64_t p = p0 + lane * 16;
-                int64_t my_bad = L;
-                if (p < L) {
-                    if (p + 16 <= L && ((base + p) & 3) == 0) {
-                        const u32x4s v = *reinterpret_cast<const u32x4s*>(seg + p);
-                        if (v.x | v.y | v.z | v.w)
-                            for (int k = 0; k < 16; ++k)
-                                if (seg[p + k]) {
-                                    my_bad = p + k;
-                                    break;
-                                }
-                    } else {
-                        for (int k = 0; k < 16 && p + k < L; ++k)
-                            if (seg[p + k]) {
-                                my_bad = p + k;
-                                break;
-                            }
-                    }
-                }
-                // wave min
-                for (int d = 32; d >= 1; d >>= 1) {
-                    const int64_t o = __shfl_xor(my_bad, d);
-                    my_bad = o < my_bad ? o : my_bad;
-                }
-                if (my_bad < L) {
-                    first_bad = my_bad;
-                    break;
-                }
-            }
-            if (first_bad < L) {
-                status = RH_SEG_E_PADDING;
-                pos = first_bad;
-            } else {
-                status = RH_SEG_END;  // stop stays at the terminator (the segment's logical end)
-            }
-        }
-        if (lane == 0) {
-            a.seg_nframes[s] = nfr;
-            a.seg_status[s] = status;
-            a.seg_stop[s] = (uint64_t)pos;
-        }
-    }
-}
-
-// ---- v2: one 256-thread block per segment, double-buffered windows ---------------------------
+// ---- one 256-thread block per segment, double-buffered windows ----------------------------------
 // The segment is cut into W-byte windows on a 16-B aligned grid.  Two windows live in an LDS ring
 // (2W bytes); while the walker (thread 0) walks the frames that START in window k, the block's
 // loads of window k+2 are in flight in registers, so HBM latency overlaps the serial walk.  Ring
@@ -324,28 +121,22 @@ struct Win {
     }
 };
 
-// NX (dense mode for ragged frame lengths): when the last window held many frames of differing
-// lengths, all 256 threads first decode the header at EVERY byte position of window k (the fast
-// loop's folded predicate) into an LDS table nx[pos] = frame length (0 = not a common-case frame),
-// then the walker only hops p -> p + nx[p] (one LDS read per frame instead of the ~70-instruction
-// scalar decode); anything nx marks 0 takes the rule-by-rule step.
-template <int W, bool NX = false, int DM = 0>
-__global__ __launch_bounds__(kBlock2) void segment_walk_kernel2(SegArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t ring[];  // [2W + 16]: 2 windows + mirror (+ nx[W] u16)
+template <int W>
+__global__ __launch_bounds__(kBlock2) void segment_walk_kernel(SegArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t ring[];  // [2W + 16]: 2 windows + mirror
     __shared__ int sh_status;
     __shared__ long long sh_pos;
     __shared__ uint32_t sh_nfr;
     __shared__ unsigned long long sh_min;
-    __shared__ int sh_dense;
     constexpr int64_t MASK = 2 * W - 1;
-    uint16_t* nx = reinterpret_cast<uint16_t*>(ring + 2 * W + 16);
     const int t = threadIdx.x;
     for (uint64_t s = blockIdx.x; s < a.n_seg; s += gridDim.x) {
-        const int64_t base = uniform64((int64_t)a.seg_off[s]);
-        int64_t L = (int64_t)a.seg_len[s];
-        if (base > a.buf_len) L = 0;
-        else if (L > a.buf_len - base) L = a.buf_len - base;
-        L = uniform64(L);
+        // a descriptor outside buf is a caller error, reported as RH_SEG_E_RANGE (never clamped:
+        // a cut-off tail would read as a half-written last entry)
+        const uint64_t soff = a.seg_off[s], slen = a.seg_len[s];
+        const bool range_bad = soff > (uint64_t)a.buf_len || slen > (uint64_t)a.buf_len - soff;
+        const int64_t base = uniform64(range_bad ? 0 : (int64_t)soff);
+        const int64_t L = uniform64(range_bad ? 0 : (int64_t)slen);
         const uint8_t* seg = a.buf + base;
         const int64_t A = (base & ~(int64_t)15) - base;
         if (t == 0) {  // verifyHeader (RDR:179-205)
@@ -358,10 +149,10 @@ __global__ __launch_bounds__(kBlock2) void segment_walk_kernel2(SegArgs a) {
                 else if (b != 0) bad = 1;
             }
             const bool ok = rl == 8 && match == 8;
-            sh_status = ok ? (8 >= L ? RH_SEG_END : kWalking) : (bad ? RH_SEG_E_HEADER : RH_SEG_END);
-            sh_pos = ok ? 8 : 0;
+            sh_status = range_bad ? RH_SEG_E_RANGE
+                                  : ok ? (8 >= L ? RH_SEG_END : kWalking) : (bad ? RH_SEG_E_HEADER : RH_SEG_END);
+            sh_pos = ok && !range_bad ? 8 : 0;
             sh_nfr = 0;
-            sh_dense = 0;
         }
         __syncthreads();
         int status = sh_status;
@@ -382,78 +173,14 @@ __global__ __launch_bounds__(kBlock2) void segment_walk_kernel2(SegArgs a) {
                 nxt.store(ring, (int)((k + 1) & 1), t);   // ring now holds windows k, k+1
                 __syncthreads();
                 nxt.load(seg, L, A + (k + 2) * W, t);       // in flight during the walk
-                const bool dense = NX && sh_dense && L <= 0x7fffffff;
-                if (NX && dense) {
-                    // nx[i] for window position wstart + i: thread t decodes positions t*PP .. t*PP+PP-1
-                    // from PP + 8 ring bytes held in registers
-                    constexpr int PP = W / kBlock2;
-                    const int64_t wstart = A + k * W;
-                    const uint32_t q0 = (uint32_t)((k * W + (int64_t)t * PP) & MASK);  // 4-aligned
-                    uint32_t dw[PP / 4 + 2];
-#pragma unroll
-                    for (int i = 0; i < PP / 4 + 2; ++i)
-                        dw[i] = *reinterpret_cast<const uint32_t*>(ring + ((q0 + 4u * i) & (uint32_t)MASK));
-                    // 32-bit, branch-free form of the fast predicate (dense mode needs L < 2^31)
-                    const int32_t rel0 = (int32_t)(wstart + (int64_t)t * PP);  // segment-relative
-                    const int32_t lim_end = (int32_t)(L - 8);                 // 8 readable bytes
-                    const int32_t L32 = (int32_t)L;
-                    const int32_t mo = (int32_t)(a.max_op < 0x7fffffffu ? a.max_op : 0x7fffffffu);
-#pragma unroll
-                    for (int i = 0; i < PP; ++i) {
-                        const uint32_t v = __builtin_amdgcn_alignbyte(dw[(i >> 2) + 1], dw[i >> 2], i & 3);
-                        const int32_t q = rel0 + i;
-                        const uint32_t stop4 = ~v & 0x80808080u;
-                        const int vl = (__builtin_ctz(stop4 | 0x80000000u) >> 3) + 1;
-                        const uint32_t nn = ((v & 0x7fu) | ((v >> 1) & 0x3f80u) | ((v >> 2) & 0x1fc000u) |
-                                             ((v >> 3) & 0xfe00000u)) &
-                                            (0xffffffffu >> (32 - 7 * vl));
-                        // varint32_size(nn) for nn < 2^28: 1 + (bits above 7 / 7), via the bit length
-                        const uint32_t bl = 32 - __builtin_clz(nn | 1u);
-                        const uint32_t vs = (bl + 6) / 7;
-                        const int32_t fl = (int32_t)(vs + nn + 4);
-                        const int32_t left = L32 - q;
-                        const int32_t lim = left < mo ? left : mo;
-                        const bool ok = (q >= 0) & (q < lim_end) & ((v & 0xffu) != 0) & (stop4 != 0) & (fl <= lim) &
-                                        (fl < 65536);
-                        nx[t * PP + i] = ok ? (uint16_t)fl : (uint16_t)0;
-                    }
-                    __syncthreads();
-                }
                 if (t < 64) {
                     // wave 0 walks, wave-uniformly (lane 0 stores the single-frame steps)
                     const int lane = t;
                     const int64_t wend = A + (k + 1) * W;
                     uint32_t nfr = sh_nfr;
-                    const uint32_t nfr_w0 = nfr;
                     int st = kWalking;
                     int64_t p = pos;
                     while (p < wend) {
-                        if (NX && dense) {
-                            // hop through nx: one LDS read per frame
-                            const int64_t wstart = A + k * W;
-                            const uint32_t room = a.cap - nfr;
-                            uint64_t* so = a.scratch_off + s * (uint64_t)a.cap + nfr;
-                            uint32_t* sl = a.scratch_len + s * (uint64_t)a.cap + nfr;
-                            uint64_t st_o = 0;
-                            uint32_t st_l = 0;
-                            uint32_t kk = 0;
-                            while (p < wend && kk < room) {
-                                const uint32_t fl = __builtin_amdgcn_readfirstlane((uint32_t)nx[(uint32_t)(p - wstart)]);
-                                if (fl == 0) break;
-                                stage_put(st_o, st_l, lane, kk, (uint64_t)(base + p), fl);
-                                if ((kk & 63u) == 63u) stage_flush(so + (kk - 63), sl + (kk - 63), lane, 64, st_o, st_l);
-                                ++kk;
-                                p += fl;
-                                prev_fl = last_fl;
-                                last_fl = fl;
-                            }
-                            stage_flush(so + (kk & ~63u), sl + (kk & ~63u), lane, kk & 63u, st_o, st_l);
-                            nfr += kk;
-                            if (p >= wend) break;
-                            if (kk < room) {
-                                // fall through to the rule-by-rule step for the frame at p
-                            }
-                        }
                         {
                             // Speculative run (a run of equal lengths was seen): lane j checks the
                             // frame at p + j * s, s = the last length, with the fast loop's folded
@@ -671,8 +398,6 @@ __global__ __launch_bounds__(kBlock2) void segment_walk_kernel2(SegArgs a) {
                         sh_status = st;
                         sh_pos = p;
                         sh_nfr = nfr;
-                        // dense mode for the next window: >= 24 frames here and no equal-length run
-                        if (NX) sh_dense = DM == 1 ? 0 : DM == 2 ? 1 : (nfr - nfr_w0 >= 24u && last_fl != prev_fl) ? 1 : 0;
                     }
                 }
                 __syncthreads();
@@ -769,22 +494,20 @@ __global__ __launch_bounds__(256) void segment_compact_kernel(const uint64_t* sc
     }
 }
 
-int g_seg_variant = 1;
+constexpr int kWalkWindow = 32768;  // 2 x 32 KiB LDS ring + mirror: two blocks per CU
 
-template <int W, bool NX = false, int DM = 0>
-hipError_t launch_walk2(const SegArgs& a, int cus, hipStream_t stream) {
-    constexpr int lds = 2 * W + 16 + (NX ? 2 * W : 0);
-    static bool attr_set = false;
+hipError_t launch_walk(const SegArgs& a, int cus, hipStream_t stream) {
+    constexpr int lds = 2 * kWalkWindow + 16;
+    static bool attr_set = false;  // set once per process; hipFuncSetAttribute is idempotent
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(segment_walk_kernel2<W, NX, DM>),
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(segment_walk_kernel<kWalkWindow>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
-    const int per_cu = lds <= 65536 + 16 + 32768 ? 2 : 1;
-    const uint64_t cap = (uint64_t)cus * per_cu;
+    const uint64_t cap = (uint64_t)cus * 2;
     const uint64_t grid = a.n_seg < cap ? a.n_seg : cap;
-    hipLaunchKernelGGL((segment_walk_kernel2<W, NX, DM>), dim3((uint32_t)grid), dim3(kBlock2), lds, stream, a);
+    hipLaunchKernelGGL((segment_walk_kernel<kWalkWindow>), dim3((uint32_t)grid), dim3(kBlock2), lds, stream, a);
     return hipGetLastError();
 }
 
@@ -794,12 +517,6 @@ int rh_segments_scan_counts(const uint32_t* nframes, uint64_t n_seg, uint32_t ca
                             unsigned long long* total, hipStream_t stream) {
     hipLaunchKernelGGL(segment_scan_kernel, dim3(1), dim3(kScanThreads), 0, stream, nframes, n_seg, cap, seg_first, total);
     RH_HIP(hipGetLastError());
-    return RH_OK;
-}
-
-int rh_segments_set_variant_impl(int v) {
-    if (v < 0 || v > 5) return rh::fail(RH_E_RANGE, "rh_segments_set_variant: variant out of range [0, 5]");
-    g_seg_variant = v;
     return RH_OK;
 }
 
@@ -827,21 +544,7 @@ int rh_segments_launch_impl(rh_ctx* ctx, const rh_segments* g, hipStream_t strea
     a.seg_stop = g->seg_stop;
     const int cus = ctx && ctx->num_cus > 0 ? ctx->num_cus : 256;
     uint64_t grid = g->n_seg < (uint64_t)cus * 8 ? g->n_seg : (uint64_t)cus * 8;
-    const int v = g_seg_variant;
-    if (v == 0) {
-        hipLaunchKernelGGL(segment_walk_kernel, dim3((uint32_t)grid), dim3(64), 0, stream, a);
-    } else if (v == 1) {
-        RH_HIP(launch_walk2<32768>(a, cus, stream));
-    } else if (v == 2) {
-        RH_HIP(launch_walk2<65536>(a, cus, stream));
-    } else if (v == 3) {
-        RH_HIP((launch_walk2<16384, true>(a, cus, stream)));
-    } else if (v == 4) {  // A/B: the dense table never used
-        RH_HIP((launch_walk2<16384, true, 1>(a, cus, stream)));
-    } else {  // A/B: the dense table on every window
-        RH_HIP((launch_walk2<16384, true, 2>(a, cus, stream)));
-    }
-    RH_HIP(hipGetLastError());
+    RH_HIP(launch_walk(a, cus, stream));
     hipLaunchKernelGGL(segment_scan_kernel, dim3(1), dim3(kScanThreads), 0, stream, g->seg_nframes, g->n_seg,
                        g->frames_per_seg_cap, g->seg_first, g->total_frames);
     RH_HIP(hipGetLastError());

@@ -238,19 +238,10 @@ class FrameBatch:
 
 
 def crc32c_frames(ctx: Context, batch: FrameBatch, flags: int = _lib.RH_CRC_VERIFY,
-                  init_state: int = 0xFFFFFFFF, variant: Optional[int] = None,
-                  stream: Optional[torch.cuda.Stream] = None) -> None:
+                  init_state: int = 0xFFFFFFFF, stream: Optional[torch.cuda.Stream] = None) -> None:
     """Enqueues the frame CRC kernel (asynchronous).  ``flags``: 0, RH_CRC_VERIFY or RH_CRC_STAMP."""
     f = batch.to_struct(init_state)
-    lib = _lib.load()
-    if variant is None:
-        check(lib.rh_crc32c_frames_launch(ctx.handle, ctypes.byref(f), flags, _stream_ptr(stream)))
-    else:
-        check(lib.rh_crc32c_frames_launch_variant(ctx.handle, ctypes.byref(f), flags, variant, _stream_ptr(stream)))
-
-
-def crc32c_num_variants() -> int:
-    return _lib.load().rh_crc32c_num_variants()
+    check(_lib.load().rh_crc32c_frames_launch(ctx.handle, ctypes.byref(f), flags, _stream_ptr(stream)))
 
 
 def crc32c_bytes(ctx: Context, data: torch.Tensor, init_state: int = 0xFFFFFFFF) -> int:
@@ -402,8 +393,8 @@ def read_segments(ctx: Context, batch: SegmentBatch, stream: Optional[torch.cuda
 
 
 def read_segments_fused(ctx: Context, batch: SegmentBatch, stream: Optional[torch.cuda.Stream] = None) -> dict:
-    """``LogSegment.readSegmentFile`` over every segment in ONE pass over HBM (rh_segments_read_launch):
-    the framing walk and every frame's CRC32C verify in the same kernel.  Fills the batch's framing
+    """``LogSegment.readSegmentFile`` over every segment in one call (rh_segments_read_launch): the
+    framing walk, every frame's CRC32C verify and the reader's verdict.  Fills the batch's framing
     outputs exactly as :func:`segments_scan` does and returns the reader's verdict per segment
     (``n_ok``, ``status``, ``stop``: the same values :func:`read_segments` derives) plus the dense
     per-frame CRCs / mismatch bits.  Asynchronous: nothing is synchronised."""

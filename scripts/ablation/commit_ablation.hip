@@ -70,9 +70,8 @@ int main() {
     CK(hipEventCreate(&a)); CK(hipEventCreate(&b));
     const double alg = 76.96e6;
     for (int round = 0; round < 3; ++round) {
-        // real kernel (library default variant)
-        for (int variant : {0, 3}) {
-            rh_commit_set_variant(variant);
+        // the shipped kernel
+        {
             CK(hipEventRecord(a, 0));
             for (int it = 0; it < 40; ++it) {
                 rh_commit_soa s[2] = {};
@@ -86,7 +85,7 @@ int main() {
             }
             CK(hipEventRecord(b, 0)); CK(hipEventSynchronize(b));
             float ms; CK(hipEventElapsedTime(&ms, a, b));
-            printf("{\"kernel\": \"commit_real_v%d\", \"us\": %.2f, \"GBps\": %.1f}\n", variant, ms * 1e3 / 40, alg / (ms / 40 * 1e-3) / 1e9);
+            printf("{\"kernel\": \"commit_real\", \"us\": %.2f, \"GBps\": %.1f}\n", ms * 1e3 / 40, alg / (ms / 40 * 1e-3) / 1e9);
         }
         // stream-only: one launch per tier (2 launches per batch)
         CK(hipEventRecord(a, 0));

@@ -15,17 +15,13 @@ run() {  # name "counters" driver-args...
   echo "$name rc=$rc"
   if [ $rc -ge 124 ]; then exit $rc; fi
 }
-for V in ${CRC_VARIANTS:-15}; do
-  run crc${V}_a "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS" --what crc --variant $V
-  run crc${V}_b "FETCH_SIZE GRBM_GUI_ACTIVE" --what crc --variant $V
-  run crc${V}_c "SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VMEM" --what crc --variant $V
-  run crc${V}_w "WRITE_SIZE" --what crc --variant $V
-done
-for V in ${COMMIT_VARIANTS:-14}; do
-  run commit${V}_a "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD" --what commit --variant $V
-  run commit${V}_b "FETCH_SIZE GRBM_GUI_ACTIVE" --what commit --variant $V
-  run commit${V}_w "WRITE_SIZE" --what commit --variant $V
-done
+run crc_a "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS" --what crc
+run crc_b "FETCH_SIZE GRBM_GUI_ACTIVE" --what crc
+run crc_c "SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_VMEM" --what crc
+run crc_w "WRITE_SIZE" --what crc
+run commit_a "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD" --what commit
+run commit_b "FETCH_SIZE GRBM_GUI_ACTIVE" --what commit
+run commit_w "WRITE_SIZE" --what commit
 if [ "${FRAMING:-1}" = "1" ]; then
   run framing_a "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_SALU SQ_INSTS_VMEM_RD" --what framing --segments 64
   run framing_b "FETCH_SIZE GRBM_GUI_ACTIVE" --what framing --segments 64

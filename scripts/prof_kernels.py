@@ -1,7 +1,7 @@
 """Minimal driver for rocprofv3 PMC passes: a few launches of one kernel configuration.
 
-    python scripts/prof_kernels.py --what crc --variant 0 --segments 32 --iters 5
-    python scripts/prof_kernels.py --what commit --variant 0 --iters 8
+    python scripts/prof_kernels.py --what crc --segments 32 --iters 5
+    python scripts/prof_kernels.py --what commit --iters 8
 """
 import argparse
 import os
@@ -13,7 +13,6 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--what", choices=["crc", "commit", "framing", "lease"], default="crc")
-    ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--segments", type=int, default=32)
     ap.add_argument("--iters", type=int, default=5)
     a = ap.parse_args()
@@ -56,11 +55,10 @@ def main():
     elif a.what == "crc":
         ss = workload.synth_segments(ctx, n_segments=a.segments, corrupt_rate=0)
         for _ in range(a.iters):
-            engine.crc32c_frames(ctx, ss.batch, flags=_lib.RH_CRC_VERIFY, variant=a.variant)
+            engine.crc32c_frames(ctx, ss.batch, flags=_lib.RH_CRC_VERIFY)
         torch.cuda.synchronize()
         print("frame_bytes", ss.frame_bytes, "frames", ss.batch.n)
     else:
-        _lib.check(_lib.load().rh_commit_set_variant(a.variant))
         host = workload.commit_snapshot(1_000_000)
         batches = []
         for r in range(8):

@@ -50,10 +50,9 @@ def test_invalid_arguments_fail_without_gpu():
     assert lib.rh_commit_soa_launch(None, None, 1, None) == _lib.RH_E_INVAL
     assert b"ctx" in lib.rh_last_error()
     assert lib.rh_groups_create(None, 10, 4, -1, None) == _lib.RH_E_INVAL
-    assert lib.rh_crc32c_set_variant(99) == _lib.RH_E_INVAL
+    assert lib.rh_crc32c_frames_launch(None, None, 0, None) == _lib.RH_E_INVAL
     with pytest.raises(_lib.IllegalArgumentError):
-        _lib.check(lib.rh_crc32c_set_variant(-1))
-    assert lib.rh_crc32c_set_variant(0) == _lib.RH_OK
+        _lib.check(lib.rh_lease_soa_launch(None, None, 1, None))
 
 
 C_LAYOUT = r"""

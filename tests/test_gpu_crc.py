@@ -2,7 +2,7 @@
 
 Covers PureJavaCrc32C semantics (RFC 3720 answers, every span length/alignment, continuation
 from a non-reset state = TestPureJavaCrc32C's split invariance), the SegmentedRaftLog frame
-writer/verifier (TestRaftLogReadWrite scenario and corruption), every kernel variant, frames
+writer/verifier (TestRaftLogReadWrite scenario and corruption), frames
 ending at the very end of the buffer, malformed frame tables, and the config-5 synthetic
 segments (a reduced segment count; the full 8 GiB run is checked in bench.py)."""
 import json
@@ -44,13 +44,13 @@ def test_rfc3720_known_answers(ctx):
         assert engine.crc32c_bytes(ctx, _dev(data)) == int(v["crc"], 16), v["name"]
 
 
-@pytest.mark.parametrize("variant", list(range(26)))
-def test_every_length_and_alignment(ctx, orc, variant):
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_every_length_and_alignment(ctx, orc, seed):
     """Spans of every length 0..700 at every start alignment 0..15 (plain spans, flags=0)."""
     import torch
 
     from ratis_amd import engine
-    rng = np.random.default_rng(variant)
+    rng = np.random.default_rng(seed)
     buf = rng.integers(0, 256, size=1 << 20, dtype=np.uint8)
     offs, lens = [], []
     pos = 0
@@ -63,7 +63,7 @@ def test_every_length_and_alignment(ctx, orc, variant):
     offs = np.array(offs, dtype=np.int64)
     lens = np.array(lens, dtype=np.int32)
     fb = _batch(buf, offs, lens)
-    engine.crc32c_frames(ctx, fb, flags=0, variant=variant)
+    engine.crc32c_frames(ctx, fb, flags=0)
     torch.cuda.synchronize()
     got = fb.crc_out.cpu().numpy().view(np.uint32)
     want = np.array([orc.crc32c(buf[o:o + l].tobytes()) for o, l in zip(offs, lens)], dtype=np.uint32)
@@ -79,9 +79,9 @@ def test_long_spans_multiwindow(ctx, orc):
     buf = rng.integers(0, 256, size=4 << 20, dtype=np.uint8)
     lens = np.array([4095, 4096, 4097, 8191, 65536 + 13, 1 << 20, (1 << 20) + 7], dtype=np.int32)
     offs = np.array([1, 8, 5000, 20000, 40001, 200003, 1 << 21], dtype=np.int64)
-    for v in range(engine.crc32c_num_variants()):
+    for v in range(1):
         fb = _batch(buf, offs, lens)
-        engine.crc32c_frames(ctx, fb, flags=0, variant=v)
+        engine.crc32c_frames(ctx, fb, flags=0)
         torch.cuda.synchronize()
         got = fb.crc_out.cpu().numpy().view(np.uint32)
         want = np.array([orc.crc32c(buf[o:o + l].tobytes()) for o, l in zip(offs, lens)], dtype=np.uint32)
@@ -202,18 +202,18 @@ def test_frames_at_buffer_end_and_malformed(ctx, orc):
         assert int(fb.crc_out[0].item()) & 0xFFFFFFFF == c
 
 
-@pytest.mark.parametrize("variant", list(range(26)))
-def test_config5_segments_reduced(ctx, orc, variant):
+@pytest.mark.parametrize("seed", [0, 1])
+def test_config5_segments_reduced(ctx, orc, seed):
     """BASELINE config 5 shape (32 MiB segments, 4 KiB frames), 6 segments: every frame verifies
     except the planted corruptions; the segment parses as a valid Ratis segment in the oracle."""
     import torch
 
     from ratis_amd import _lib, engine, workload
-    ss = workload.synth_segments(ctx, n_segments=6, corrupt_rate=2e-4, seed=31 + variant)
+    ss = workload.synth_segments(ctx, n_segments=6, corrupt_rate=2e-4, seed=31 + seed)
     fb = ss.batch
     fb.n_bad.zero_()
     fb.bad_bits.zero_()
-    engine.crc32c_frames(ctx, fb, flags=_lib.RH_CRC_VERIFY, variant=variant)
+    engine.crc32c_frames(ctx, fb, flags=_lib.RH_CRC_VERIFY)
     torch.cuda.synchronize()
     bad = np.nonzero(_bits(fb.bad_bits.cpu().numpy(), fb.n))[0]
     assert np.array_equal(bad, ss.corrupted) and ss.corrupted.size > 0

@@ -57,21 +57,8 @@ def assert_same(ref, got):
     assert np.array_equal(ext, ref["extended_bits"])
 
 
-@pytest.fixture
-def lease_variant(request):
-    from ratis_amd import _lib
-    lib = _lib.load()
-    _lib.check(lib.rh_lease_set_variant(request.param))
-    yield request.param
-    _lib.check(lib.rh_lease_set_variant(DEFAULT_LEASE_VARIANT))
-
-
-DEFAULT_LEASE_VARIANT = 2
-
-
-@pytest.mark.parametrize("lease_variant", [0, 1, 2, 3], indirect=True)
 @pytest.mark.parametrize("F", list(range(0, 15)))
-def test_lease_every_follower_count(ctx, orc, F, lease_variant):
+def test_lease_every_follower_count(ctx, orc, F):
     rng = np.random.default_rng(1000 + F)
     n = 20_000 + F * 37          # not a multiple of 64
     ts, conf, lease_in = random_lease_tier(rng, n, F)
@@ -149,3 +136,21 @@ def test_lease_ms_threshold_exact(ctx, orc, timeout_ms):
     lease_in[:] = NOW - pick[rng.integers(0, len(ds), size=n)]
     ref = orc.lease_soa(ts, conf, lease_in, NOW, timeout_ms)
     assert_same(ref, run_gpu(ctx, ts, conf, lease_in, timeout_ms))
+
+
+@pytest.mark.parametrize("F", [0, 1, 4, 7, 9])
+def test_lease_malformed_conf_words(ctx, orc, F):
+    """A conf word naming a follower slot >= F is malformed for the tier: no lease, no extension,
+    lease unchanged -- the same rule as the commit kernel and the oracle."""
+    rng = np.random.default_rng(77 + F)
+    n = 4096
+    ts, conf, lease_in = random_lease_tier(rng, n, F)
+    which = rng.integers(0, 3, size=n)
+    hi_new = np.uint32(1 << F) if F < 14 else np.uint32(0)
+    conf = (conf | np.where(which == 1, hi_new, 0).astype(np.uint32)
+            | (np.where(which == 2, hi_new, 0).astype(np.uint32) << 16)).astype(np.uint32)
+    got = run_gpu(ctx, ts, conf, lease_in, 100)
+    assert_same(orc.lease_soa(ts, conf, lease_in, NOW, 100), got)
+    bad = which > 0
+    has = np.unpackbits(got[1].view(np.uint8), bitorder="little")[:n].astype(bool)
+    assert not has[bad].any() and np.array_equal(got[0][bad], lease_in[bad])

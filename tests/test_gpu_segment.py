@@ -120,18 +120,9 @@ def check_against_oracle(orc, b, buf, offs, lens, max_op=4 << 20, skip_crc=None)
         assert np.array_equal(fl[k: k + nfr[s]], rl), s
 
 
-@pytest.fixture(params=[0, 1, 2, 3, 5])
-def seg_variant(request):
-    from ratis_amd import _lib
-    lib = _lib.load()
-    _lib.check(lib.rh_segments_set_variant(request.param))
-    yield request.param
-    _lib.check(lib.rh_segments_set_variant(1))
-
-
 @pytest.mark.parametrize("big", [False, True])
-def test_framing_matches_oracle_every_kind(ctx, orc, big, seg_variant):
-    rng = np.random.default_rng(7 + big + 10 * seg_variant)
+def test_framing_matches_oracle_every_kind(ctx, orc, big):
+    rng = np.random.default_rng(7 + big)
     kinds = [KINDS[i % len(KINDS)] for i in range(len(KINDS) * 6)]
     made = [make_segment(orc, rng, k, big) for k in kinds]
     buf, offs, lens = pack([m[0] for m in made], rng)
@@ -165,7 +156,7 @@ def test_read_segments_matches_oracle_including_crc(ctx, orc):
         assert (st[s], stop[s], n_ok[s]) == (rst, rstop, len(ro)), (s, kinds[s])
 
 
-def test_small_max_op_limits(ctx, orc, seg_variant):
+def test_small_max_op_limits(ctx, orc):
     """maxOpSize small enough that the LimitedInputStream checks on the varint, the body and the
     4 trailer reads (RDR:66-82, 314-317, 343-352) each decide some frame."""
     rng = np.random.default_rng(5)
@@ -178,7 +169,7 @@ def test_small_max_op_limits(ctx, orc, seg_variant):
         check_against_oracle(orc, b, buf, offs, lens, max_op=max_op)
 
 
-def test_frame_capacity_reports_and_truncates(ctx, orc, seg_variant):
+def test_frame_capacity_reports_and_truncates(ctx, orc):
     from ratis_amd import _lib
     rng = np.random.default_rng(3)
     img = HEADER + b"".join(orc.frame_write(bytes([7]) * 5) for _ in range(100)) + bytes(100)
@@ -205,7 +196,7 @@ def test_raftlog_readwrite_segment_golden(ctx, orc):
     assert list(b.seg_nframes.cpu().numpy()) == [100, 100]
 
 
-def test_config5_shape_many_segments(ctx, orc, seg_variant):
+def test_config5_shape_many_segments(ctx, orc):
     """32 MiB segments of 4 KiB frames, 4 segments from the synthetic
     generator: 8190 frames each, clean end at the zero padding; compared with the oracle walk."""
     import torch
@@ -239,7 +230,7 @@ def test_bad_arguments(ctx):
         engine.segments_scan(ctx, b)
 
 
-def test_long_padding_tails(ctx, orc, seg_variant):
+def test_long_padding_tails(ctx, orc):
     """Preallocated segments (mostly zero tail, as an open segment's file is): the terminator
     check must scan megabytes and report the exact first non-zero byte, or a clean end."""
     rng = np.random.default_rng(21)
@@ -286,7 +277,7 @@ def speculation_images(orc, rng):
     return images
 
 
-def test_speculative_walk_edges(ctx, orc, seg_variant):
+def test_speculative_walk_edges(ctx, orc):
     rng = np.random.default_rng(123)
     buf, offs, lens = pack(speculation_images(orc, rng), rng)
     b = run_scan(ctx, buf, offs, lens, cap=1024)
@@ -294,11 +285,10 @@ def test_speculative_walk_edges(ctx, orc, seg_variant):
 
 
 @pytest.mark.parametrize("lo,hi", [(6, 200), (64, 2048), (1000, 9000)])
-def test_ragged_frame_lengths(ctx, orc, seg_variant, lo, hi):
+def test_ragged_frame_lengths(ctx, orc, lo, hi):
     """Segments of differently sized frames (workload.synth_ragged_segments): the frame table
-    equals the generator's, and two whole segments equal the literal reader.  Covers the dense
-    per-position table of variant 3 (many small frames per window) and the switches between it,
-    the speculative runs and the scalar loop."""
+    equals the generator's, and two whole segments equal the literal reader.  Covers the switches
+    between the speculative runs and the scalar loop."""
     import torch
 
     from ratis_amd import engine, workload
@@ -318,3 +308,21 @@ def test_ragged_frame_lengths(ctx, orc, seg_variant, lo, hi):
         ro, rl, _, rst, rstop = orc.segment_scan(img)
         assert (int(b.seg_status[sgi].item()), int(b.seg_stop[sgi].item())) == (rst, rstop)
         assert len(ro) == int(rs.seg_nframes[sgi])
+
+
+def test_descriptor_out_of_buffer_is_range_error(ctx, orc):
+    """a segment descriptor outside buf reports RH_SEG_E_RANGE (0 frames, stop 0) and is
+    never clamped into a clean-looking or half-written segment; valid neighbours are unaffected."""
+    from ratis_amd import _lib
+    rng = np.random.default_rng(8)
+    seg = np.frombuffer(HEADER + b"".join(orc.frame_write(p) for p in _protos(rng, 20, False)), np.uint8)
+    n = seg.size
+    buf = np.concatenate([seg, seg]).astype(np.uint8)
+    offs = np.array([0, n, n + 5, 2 * n + 1, 1 << 40], dtype=np.int64)
+    lens = np.array([n, n, n, 4, 8], dtype=np.int64)   # #2 runs 5 bytes past the end, #3 and #4 start past it
+    b = run_scan(ctx, buf, offs, lens)
+    st = b.seg_status[:5].cpu().numpy()
+    nf = b.seg_nframes[:5].cpu().numpy()
+    assert st[0] == _lib.RH_SEG_END and st[1] == _lib.RH_SEG_END and nf[0] == nf[1] == 20
+    assert list(st[2:]) == [_lib.RH_SEG_E_RANGE] * 3 and not nf[2:].any()
+    assert not b.seg_stop[2:5].cpu().numpy().any()

@@ -18,16 +18,6 @@ from .test_gpu_segment import HEADER, KINDS, make_segment, pack, speculation_ima
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(autouse=True, params=[0, 1, 2], ids=["S36", "S20", "walk+crc"])
-def read_variant(request):
-    """Every test runs on every read-path variant (one-pass kernel with 36 / 20-byte units; walk + CRC)."""
-    from ratis_amd import _lib
-    lib = _lib.load()
-    _lib.check(lib.rh_segments_read_set_variant(request.param))
-    yield request.param
-    _lib.check(lib.rh_segments_read_set_variant(2))
-
-
 def run_fused(ctx, buf, offs, lens, max_op=4 << 20, cap=4096):
     import torch
 
