@@ -113,82 +113,96 @@ def timed_passes(items, fn, seconds: float) -> dict:
     return {"rate": sum(units) / dt, "passes": sum(passes), "seconds": dt}
 
 
-def delta_streaming(ctx, host, steps: int = 6) -> dict:
-    """The operating mode the Java module uses: resident RaftGroupTables (one per follower-slot
-    width), FollowerInfo/flush-index updates written in place into the pinned delta ring
-    (rh_deltas_acquire/submit: H2D + device updateToMax), then rh_commit_batch (kernel + D2H of
-    the advanced (slot, commit) list).  One step = one delta per group (90 % follower matchIndex,
-    10 % leader flushIndex) + one batched updateCommit over every group.  Wall-clock per step,
-    host fill of the pinned ring included; the fill alone is reported too."""
+def delta_streaming(ctx, host, steps: int = 8, fill_threads: int = 8) -> dict:
+    """The operating mode the Java module uses: one resident RaftGroupTable (stable F=4 and joint
+    F=6 tiers), FollowerInfo / flush-index updates written in place into the pinned delta ring
+    (rh_deltas_acquire / submit: H2D + device apply, which marks the touched groups dirty), then
+    rh_commit_batch_async over the dirty groups with its advanced-group events written straight
+    into host-mapped memory.  One step = one 16-byte delta per group (90 % a follower matchIndex,
+    10 % the leader flushIndex) + one batched updateCommit.  Pipelined: the host fills step s+1
+    while the device applies and evaluates step s, and collects step s-1's events meanwhile.
+    Wall-clock per step; the stages are also timed on their own."""
+    import ctypes
+    import threading
+
     from ratis_amd import _lib, groups
     rng = np.random.default_rng(99)
-    tabs, batches = [], []
+    n_all = sum(h.n for h in host)
+    tab = groups.RaftGroupTable(ctx, capacity=n_all)
+    first, bases = 0, []
     for h in host:
-        F, n = h.follower.shape
-        tab = groups.RaftGroupTable(ctx, capacity=n, n_followers=F)
-        tab.load(0, n, match=h.follower, flush=h.flush, commit=h.commit, term_start=h.term_start, conf=h.conf)
-        tabs.append(tab)
-        per = []
-        for s in range(steps + 1):
-            d = np.zeros(n, dtype=groups.RaftGroupTable.DELTA_DTYPE)
-            d["slot"] = rng.permutation(n)
-            is_flush = rng.random(n) < 0.10
-            col = rng.integers(0, F, size=n)
-            d["column"] = np.where(is_flush, _lib.RH_COL_FLUSH, col)
-            cur = np.where(is_flush, h.flush[d["slot"]], h.follower[col, d["slot"]])
-            d["value"] = cur + (s + 1) * 512
-            per.append(d)
-        batches.append(per)
+        tab.load(first, h.conf, h.flush, h.commit, h.term_start, match=h.follower)
+        bases.append(first)
+        first += h.n
+    per = []
+    for s in range(steps + 3):
+        parts = []
+        for h, b in zip(host, bases):
+            F = h.follower.shape[0]
+            slot = rng.permutation(h.n)
+            is_flush = rng.random(h.n) < 0.10
+            col = rng.integers(0, 4, size=h.n)          # followers 0..3 exist in both tiers
+            cur = np.where(is_flush, h.flush[slot], h.follower[col, slot])
+            parts.append(groups.make_deltas(b + slot, np.where(is_flush, _lib.RH_COL_FLUSH, col),
+                                            cur + (s + 1) * 512))
+            del F
+        per.append(np.concatenate(parts))
+    nbytes = per[0].nbytes
 
-    import ctypes
+    def fill(ring, d):
+        # the producers' writes into the pinned ring: fill_threads memmoves (ctypes drops the GIL)
+        dst, src = ring.ctypes.data, d.ctypes.data
+        cuts = np.linspace(0, d.nbytes, fill_threads + 1).astype(np.int64) // 16 * 16
+        cuts[-1] = d.nbytes
+        th = [threading.Thread(target=ctypes.memmove, args=(dst + int(a), src + int(a), int(b - a)))
+              for a, b in zip(cuts[:-1], cuts[1:])]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
 
-    import torch
-    lib = _lib.load()
-    # pinned result buffers: rh_commit_batch copies the advanced (slot, commit) list into them
-    outs = [(torch.empty(h.n, dtype=torch.int64).pin_memory(), torch.empty(h.n, dtype=torch.int64).pin_memory())
-            for h in host]
-
-    def fill(s):
-        for tab, per in zip(tabs, batches):
-            ring = tab.acquire_deltas()
-            d = per[s]
-            ring.view(np.uint8)[: d.nbytes] = d.view(np.uint8)   # the producer's writes into the ring
-            tab.submit_deltas(d.size)
-
-    def commit():
-        adv = 0
-        cnt = ctypes.c_size_t()
-        for tab, (o_slot, o_commit) in zip(tabs, outs):
-            _lib.check(lib.rh_commit_batch(tab.handle, o_slot.data_ptr(), o_commit.data_ptr(), o_slot.numel(),
-                                           ctypes.byref(cnt), None))
-            adv += cnt.value
-        return adv
-
-    fill(0)
-    commit()  # warm-up
-    t0 = time.perf_counter()
-    advanced = 0
-    for s in range(1, steps + 1):
-        fill(s)
-        advanced += commit()
-    dt = (time.perf_counter() - t0) / steps
-    # the host fill alone (memcpy of one step's deltas into the pinned slots, nothing submitted)
-    f0 = time.perf_counter()
-    for tab, per in zip(tabs, batches):
+    def step(d):
         ring = tab.acquire_deltas()
-        ring.view(np.uint8)[: per[0].nbytes] = per[0].view(np.uint8)
+        fill(ring, d)
+        tab.submit_deltas(d.size)
+        return tab.commit_async(watch_all=False)
+
+    tk = step(per[0])
+    tab.commit_wait_counts(tk)
+    # pipelined (the timed figure)
+    t0 = time.perf_counter()
+    prev, advanced = None, 0
+    for s in range(1, steps + 1):
+        tk = step(per[s])
+        if prev is not None:
+            advanced += tab.commit_wait_counts(prev)[0]
+        prev = tk
+    advanced += tab.commit_wait_counts(prev)[0]
+    dt = (time.perf_counter() - t0) / steps
+    # stages on their own: host fill of the pinned ring; device part (H2D + apply + evaluation +
+    # events) with the ring already filled, synchronous
+    f0 = time.perf_counter()
+    for s in range(3):
+        ring = tab.acquire_deltas()
+        fill(ring, per[steps + 1])
         tab.submit_deltas(0)
-    fill_s = time.perf_counter() - f0
-    n_groups = sum(h.n for h in host)
-    for tab in tabs:
-        tab.close()
-    return {"commit_updates_per_s_incl_pcie": round(n_groups / dt, 1), "ms_per_step": round(dt * 1e3, 3),
-            "deltas_per_step": n_groups, "delta_bytes_h2d_per_step": n_groups * 24,
-            "host_fill_ms_per_step": round(fill_s * 1e3, 3),
-            "commit_updates_per_s_excl_host_fill": round(n_groups / (dt - fill_s), 1) if dt > fill_s else None,
+    fill_s = (time.perf_counter() - f0) / 3
+    ring = tab.acquire_deltas()
+    fill(ring, per[steps + 2])
+    g0 = time.perf_counter()
+    tab.submit_deltas(per[steps + 2].size)
+    tab.commit_wait_counts(tab.commit_async(watch_all=False))
+    dev_s = time.perf_counter() - g0
+    tab.close()
+    return {"commit_updates_per_s_incl_pcie": round(n_all / dt, 1), "ms_per_step": round(dt * 1e3, 3),
+            "deltas_per_step": n_all, "delta_bytes_h2d_per_step": nbytes,
+            "h2d_bound_ms": round(nbytes / 50e9 * 1e3, 3),
+            "stage_ms": {"host_fill_pinned_ring": round(fill_s * 1e3, 3), "fill_threads": fill_threads,
+                         "device_h2d_apply_evaluate_events": round(dev_s * 1e3, 3)},
             "advanced_per_step": round(advanced / steps, 1),
-            "path": "rh_deltas_acquire/submit (pinned ring, H2D + updateToMax kernel) + rh_commit_batch "
-                    "(commit kernel + D2H of the advanced list), tables F=4 and F=6"}
+            "path": "rh_deltas_acquire/submit (pinned ring, 16 B deltas, H2D + apply marking dirty groups) + "
+                    "rh_commit_batch_async/_wait (dirty-group evaluation, advanced events in host-mapped "
+                    "memory), pipelined: fill of step s+1 overlaps the device work of step s"}
 
 
 def main():

@@ -143,61 +143,167 @@ typedef struct rh_commit_soa {
  * Optional.empty()) keep commit_out = commit_in and get INT64_MIN in min/maj/max_out. */
 int rh_commit_soa_launch(rh_ctx* ctx, const rh_commit_soa* tiers, int n_tiers, void* stream);
 
-/* ---- resident group table (the object the Java ratis-hip module holds) ------------------ */
+/* ---- resident group table (the object the Java ratis-hip module holds) ------------------
+ *
+ * One table per (process, GPU) holds the leader-side commit state of up to `capacity` leader
+ * divisions ("slots", the handle the Java module keeps per RaftGroup).  A slot owns its
+ * FollowerInfo matchIndex / commitIndex per follower slot k (0..13; k is the module's numbering
+ * of the division's peers), the leader's flushIndex, commitIndex, the current term's first log
+ * index, and the membership word.  Internally the slot lives in the narrowest SoA tier whose
+ * width (2, 4, 6, ..., 14 follower columns) covers every slot its conf word names; a conf change
+ * that needs a different width moves it (rh_group_reconf).  Everything below is asynchronous on
+ * the context stream in call order, except where a call says it blocks.
+ *
+ * Event model (LeaderStateImpl's UPDATE_COMMIT event queue, LSI:155-166, 846-854, 900-902): a
+ * delta to matchIndex / flushIndex / commitIndex, a start or a reconf marks the slot dirty, and
+ * rh_commit_batch evaluates updateCommit() for the dirty slots only (each once, however many
+ * deltas it received), reporting just the groups whose result changed.  The same holds for
+ * follower commitIndex deltas and rh_watch_levels (commitIndexChanged, LSI:606-622).
+ * Evaluating a clean slot again could not change its result, so this is exactly the reference's
+ * event-driven behaviour. */
 
-/* Column ids for deltas (FollowerInfo / RaftLog producers of the indices). */
-#define RH_COL_MATCH(k)   ((uint32_t)(k))        /* follower k matchIndex: updateToMax (FII:93-95)  */
-#define RH_COL_FCOMMIT(k) (16u + (uint32_t)(k))  /* follower k commitIndex: updateToMax (FII:103-105)*/
-#define RH_COL_FLUSH      32u                    /* leader flushIndex: increasing                   */
-#define RH_COL_COMMITTED  33u                    /* leader commitIndex raised outside the kernel
-                                                    (RLB:155-166 updateSnapshotIndex): to-max       */
-typedef struct rh_delta {
-    uint64_t slot;    /* group slot in the table                                             */
-    uint32_t column;  /* RH_COL_*                                                            */
-    uint32_t reserved;
+/* Column ids for deltas (FollowerInfo / RaftLog producers). */
+#define RH_COL_MATCH(k)   ((uint8_t)(k))        /* follower k matchIndex (FII:87-95)            */
+#define RH_COL_FCOMMIT(k) ((uint8_t)(16u + (k))) /* follower k commitIndex (FII:97-105)         */
+#define RH_COL_FLUSH      ((uint8_t)32u)         /* leader flushIndex (SegmentedRaftLogWorker
+                                                    .java:419-431)                              */
+#define RH_COL_COMMITTED  ((uint8_t)33u)         /* leader commitIndex raised outside the kernel
+                                                    (RaftLogBase.updateSnapshotIndex, RLB:155-166) */
+/* Operations (RaftLogIndex, ratis-server-api/.../raftlog/RaftLogIndex.java). */
+#define RH_OP_MAX 0u  /* updateToMax: matchIndex / commitIndex updates (FII:93-105)              */
+#define RH_OP_SET 1u  /* setUnconditionally: FollowerInfo.setSnapshotIndex sets matchIndex,
+                         possibly lower (FII:147-151)                                           */
+typedef struct rh_delta {  /* 16 bytes */
+    uint32_t slot;         /* division slot in the table                                        */
+    uint8_t  column;       /* RH_COL_*                                                          */
+    uint8_t  op;           /* RH_OP_*                                                           */
+    uint16_t reserved;     /* 0                                                                 */
     int64_t  value;
 } rh_delta;
+/* Ordering inside one batch: the device applies a batch's SET deltas before its MAX deltas, and
+ * two SETs to one (slot, column) race.  rh_push_deltas therefore cuts the caller's array into
+ * batches so that the result equals applying the deltas one by one in array order; a producer
+ * on the zero-copy path (rh_deltas_acquire/submit) must submit separately whenever a SET would
+ * follow another delta to the same (slot, column). */
 
-/* Creates a table of `capacity` group slots with `n_followers` follower slots each; all slots
- * start inactive with every index = -1. */
-int rh_groups_create(rh_ctx* ctx, uint64_t capacity, uint32_t n_followers, int64_t gap_threshold,
-                     rh_groups** out);
+/* An event of rh_commit_batch: `slot` and an index (the new commitIndex, or the changed
+ * watch-ALL level). 16 bytes. */
+typedef struct rh_index_event {
+    uint32_t slot;
+    uint32_t reserved;
+    int64_t  value;
+} rh_index_event;
+/* An event of rh_watch_levels: the changed commitIndexChanged() levels of one slot. 32 bytes.
+ * valid = 0 is Optional.empty() (levels INT64_MIN). */
+typedef struct rh_watch_event {
+    uint32_t slot;
+    uint32_t valid;
+    int64_t  min;       /* ALL_COMMITTED      */
+    int64_t  majority;  /* MAJORITY_COMMITTED */
+    int64_t  max;       /* MAJORITY           */
+} rh_watch_event;
+
+/* Results of one rh_commit_batch: library-owned pinned host memory, valid until the second
+ * rh_commit_batch_async after the one that produced them (two result buffers alternate). */
+typedef struct rh_commit_out {
+    const rh_index_event* advanced;   /* slots whose commitIndex was stored, new value (LSI:1017-1021,
+                                         RLB:121-142); the Java follow-up runs for these only    */
+    uint64_t n_advanced;
+    const rh_index_event* watch_all;  /* slots whose watch-ALL level (min, LSI:1025) changed       */
+    uint64_t n_watch_all;
+} rh_commit_out;
+
+/* Creates a table of `capacity` slots (< 2^28); every slot starts stopped. */
+int rh_groups_create(rh_ctx* ctx, uint64_t capacity, int64_t gap_threshold, rh_groups** out);
 int rh_groups_destroy(rh_groups* g);
-/* Sets the conf word and the leader-side indices of one slot (conf change / leader start). */
-int rh_group_set(rh_groups* g, uint64_t slot, uint32_t conf, int64_t flush_index,
-                 int64_t commit_index, int64_t term_start);
-/* Bulk host->device load of rows [first, first+n).  Host arrays are column-major like the
- * device SoA: match/fcommit are [F][n].  Any pointer may be NULL to leave that column. */
-int rh_groups_load(rh_groups* g, uint64_t first, uint64_t n, const int64_t* match,
+/* Leader start for `slot` (a new LeaderStateImpl: every FollowerInfo is new, matchIndex =
+ * commitIndex = -1, FII:42-43, LSI:421-430; StartupLogEntry's index is term_start, LSI:296-301).
+ * Also the way to re-arm a slot for a new leadership term.  Marks the slot dirty. */
+int rh_group_start(rh_groups* g, uint32_t slot, uint32_t conf, int64_t flush_index, int64_t commit_index,
+                   int64_t term_start);
+/* Conf change of a started slot (applyOldNewConf / replicateNewConf, LSI:624-633, 1064-1074;
+ * addSenders LSI:681-692; restart of a LogAppender LSI:704-724).  `src` (RH_MAX_FOLLOWERS
+ * entries, or NULL = identity) maps every new follower slot k to the old slot whose
+ * matchIndex / commitIndex it keeps (src[k] = k: the peer stays; another old slot: the module
+ * renumbered it), or -1 for a new FollowerInfo (index -1: a newcomer, or a recycled slot).  The
+ * slot moves to another tier when the new word needs a different width.  Marks it dirty. */
+int rh_group_reconf(rh_groups* g, uint32_t slot, uint32_t conf, const int8_t* src);
+/* Step down / group removal: the slot stops (no further results) and releases its row. */
+int rh_group_stop(rh_groups* g, uint32_t slot);
+/* Bulk start of slots [first, first + n) with explicit follower state (checkpoint restore, bench):
+ * host arrays, match / fcommit are [n_host_followers][n] (column k = follower slot k; columns a
+ * slot's tier has beyond n_host_followers start at -1).  NULL match / fcommit = all -1. */
+int rh_groups_load(rh_groups* g, uint32_t first, uint32_t n, uint32_t n_host_followers, const int64_t* match,
                    const int64_t* fcommit, const int64_t* flush, const int64_t* commit,
                    const int64_t* term_start, const uint32_t* conf);
-/* Copies deltas through a pinned staging ring and applies them on the device (monotone max,
- * exactly RaftLogIndex.updateToMax).  Returns once the caller's buffer may be reused; the
- * device work is ordered before the next rh_commit_batch / rh_watch_levels.  Thread-safe. */
+/* Copies deltas through a pinned staging ring and applies them on the device (RaftLogIndex
+ * semantics per op).  Deltas of stopped slots or of follower columns the slot's tier does not
+ * have are rejected (RH_E_INVAL, nothing applied).  Returns once the caller's buffer may be
+ * reused.  Thread-safe. */
 int rh_push_deltas(rh_groups* g, const rh_delta* deltas, size_t n);
-
 /* Zero-copy producer path over the same staging ring (two pinned slots of RH_DELTA_SLOT deltas):
- * rh_deltas_acquire hands out the next slot to fill in place (waiting until its previous H2D
- * has completed); rh_deltas_submit enqueues the H2D of its first n deltas and the device apply,
- * and returns without waiting, so the producer fills the other slot while this one is in flight.
- * One acquire/submit pair at a time per table.  Unlike rh_push_deltas, submitted deltas are not
- * validated on the host: a delta with slot >= capacity or an unknown column is ignored by the
- * device. */
+ * rh_deltas_acquire hands out the next slot to fill in place (waiting until its previous H2D has
+ * completed); rh_deltas_submit enqueues the H2D of its first n deltas and the device apply and
+ * returns without waiting, so the producer fills the other slot while this one is in flight.  One
+ * acquire/submit pair at a time per table.  Submitted deltas are not validated on the host: the
+ * device ignores a delta with a slot >= capacity, a stopped slot, an unknown column or op. */
 #define RH_DELTA_SLOT (1u << 20)
 int rh_deltas_acquire(rh_groups* g, rh_delta** out_buf, size_t* out_cap);
 int rh_deltas_submit(rh_groups* g, size_t n);
-/* RH_MODE_COMMIT: runs updateCommit for every active group, stores advanced commit indices in
- * the table, and returns (slot, new commit) of the groups that advanced, up to `cap`.
- * out_min (optional, host [capacity]) receives the watch-ALL level of every group.
- * Blocks until results are in the caller's buffers. */
-int rh_commit_batch(rh_groups* g, uint64_t* out_slots, int64_t* out_commit, size_t cap, size_t* out_n,
-                    int64_t* out_min);
-/* RH_MODE_WATCH over the follower commitIndex column: dense host outputs [capacity] (any may be
- * NULL) plus valid bits [ceil(capacity/64)]. */
-int rh_watch_levels(rh_groups* g, int64_t* out_min, int64_t* out_maj, int64_t* out_max,
-                    uint64_t* out_valid_bits);
-/* Reads back the resident commit index column (debug / checkpoint). */
-int rh_groups_read_commit(rh_groups* g, uint64_t first, uint64_t n, int64_t* out);
+/* Batched LeaderStateImpl.updateCommit() over the dirty slots (see the event model above): stores
+ * advanced commit indices in the table and fills *out.  Blocks until *out is ready.
+ * flags: RH_COMMIT_WATCH_ALL also reports the changed watch-ALL levels (the module sets it while
+ * the server has ALL-level watch requests, WatchRequests.java:146-219); without it out->watch_all
+ * is empty and the levels are neither compared nor stored, so the next batch that sets it reports
+ * every dirty slot whose level differs from the last one reported. */
+#define RH_COMMIT_WATCH_ALL 1u
+int rh_commit_batch(rh_groups* g, uint32_t flags, rh_commit_out* out);
+/* The same split in two: _async enqueues the evaluation (its events are written straight into
+ * host-mapped pinned memory) and returns a ticket; _wait blocks until that ticket's results are
+ * ready.  Deltas and other calls may be issued in between (they are ordered after it). */
+int rh_commit_batch_async(rh_groups* g, uint32_t flags, uint64_t* ticket);
+int rh_commit_batch_wait(rh_groups* g, uint64_t ticket, rh_commit_out* out);
+/* Batched commitIndexChanged() over the slots whose follower commitIndex or leader commitIndex
+ * changed: the slots whose {min, majority, max} levels changed, into library-owned pinned memory
+ * valid until the next rh_watch_levels.  Blocks. */
+int rh_watch_levels(rh_groups* g, const rh_watch_event** out_events, uint64_t* out_n);
+/* Reads back one column of slots [first, first + n) (debug / checkpoint / tests): column =
+ * RH_COL_MATCH(k) / RH_COL_FCOMMIT(k) / RH_COL_FLUSH / RH_COL_COMMITTED, or RH_COL_CONF (the
+ * membership word, as int64) and RH_COL_TERM_START.  Stopped slots read INT64_MIN; follower
+ * columns beyond a slot's tier read -1.  Blocks. */
+#define RH_COL_CONF       ((uint8_t)34u)
+#define RH_COL_TERM_START ((uint8_t)35u)
+int rh_groups_read(rh_groups* g, uint32_t first, uint32_t n, uint8_t column, int64_t* out);
+/* Follower width of the tier a slot lives in (0 = stopped), for tests and diagnostics. */
+int rh_group_tier(rh_groups* g, uint32_t slot, uint32_t* out_width);
+
+/* ---- one RaftServer across several GPUs ---------------------------------------------------
+ * A node owns one context and one resident table per device of `device_mask` (bit d = GPU d).
+ * A RaftGroup is placed on shard floorMod(UUID.hashCode(), n_shards) of its RaftGroupId
+ * (RaftId.hashCode = UUID.hashCode, RaftId.java:119-122), with no inter-GPU traffic on the hot
+ * path.  Node slot = shard * capacity_per_shard + table slot; every rh_groups call above has a
+ * node form that routes by it. */
+typedef struct rh_node rh_node;
+/* floorMod(UUID.hashCode(), n): hashCode = (int)(hilo >> 32) ^ (int)hilo, hilo = msb ^ lsb
+ * (java.util.UUID.hashCode).  Pure host function; no device needed. */
+int rh_shard_of(uint64_t uuid_msb, uint64_t uuid_lsb, int n_shards);
+int rh_node_create(uint32_t device_mask, uint64_t capacity_per_shard, int64_t gap_threshold, rh_node** out);
+int rh_node_destroy(rh_node* node);
+int rh_node_shards(rh_node* node);
+/* The shard table (for per-shard calls such as the zero-copy ring) and its context. */
+rh_groups* rh_node_groups(rh_node* node, int shard);
+rh_ctx* rh_node_ctx(rh_node* node, int shard);
+int rh_node_group_start(rh_node* node, uint32_t node_slot, uint32_t conf, int64_t flush_index,
+                        int64_t commit_index, int64_t term_start);
+int rh_node_group_reconf(rh_node* node, uint32_t node_slot, uint32_t conf, const int8_t* src);
+int rh_node_group_stop(rh_node* node, uint32_t node_slot);
+/* Splits the deltas by shard (node slots) and pushes each part to its shard's table. */
+int rh_node_push_deltas(rh_node* node, const rh_delta* deltas, size_t n);
+/* updateCommit on every shard (all launched before any is awaited); the events of all shards,
+ * with node slots, are gathered into the caller's arrays (up to the caps; the n_* counts are the
+ * totals).  Blocks. */
+int rh_node_commit_batch(rh_node* node, rh_index_event* advanced, uint64_t adv_cap, uint64_t* n_advanced,
+                         rh_index_event* watch_all, uint64_t watch_cap, uint64_t* n_watch_all);
 
 /* ===================================================================================== */
 /* 2. CRC32C (PureJavaCrc32C) over SegmentedRaftLog frames                               */

@@ -7,7 +7,8 @@ as HIP kernels for gfx950 behind the C ABI of include/ratis_hip.h (lib/libratis_
 Modules:
   _lib      ctypes binding of the C ABI (fails loudly if the native library is missing)
   engine    device-side API over torch-owned HBM: Context, CommitTier, FrameBatch, launches
-  groups    RaftGroupTable: the resident per-GPU table the Java ratis-hip module holds
+  groups    RaftGroupTable / RaftNode: the resident per-GPU table the Java ratis-hip module holds,
+            and one RaftServer's tables over several GPUs
   segment   segment/frame layout and LogEntryProto encoding (host side)
   workload  seeded synthetic workloads of BASELINE.json
   shard     RaftGroupId placement across GPUs and the RCCL stats all-reduce

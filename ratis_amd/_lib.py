@@ -33,6 +33,12 @@ RH_MAX_TIERS = 4
 
 RH_COL_FLUSH = 32
 RH_COL_COMMITTED = 33
+RH_COL_CONF = 34
+RH_COL_TERM_START = 35
+RH_OP_MAX = 0
+RH_OP_SET = 1
+RH_DELTA_SLOT = 1 << 20
+RH_COMMIT_WATCH_ALL = 1
 
 RH_CRC_VERIFY = 1
 RH_CRC_STAMP = 2
@@ -83,7 +89,20 @@ class RhCommitSoa(ctypes.Structure):
 
 
 class RhDelta(ctypes.Structure):
-    _fields_ = [("slot", c_uint64), ("column", c_uint32), ("reserved", c_uint32), ("value", c_int64)]
+    _fields_ = [("slot", c_uint32), ("column", ctypes.c_uint8), ("op", ctypes.c_uint8), ("reserved", ctypes.c_uint16),
+                ("value", c_int64)]
+
+
+class RhIndexEvent(ctypes.Structure):
+    _fields_ = [("slot", c_uint32), ("reserved", c_uint32), ("value", c_int64)]
+
+
+class RhWatchEvent(ctypes.Structure):
+    _fields_ = [("slot", c_uint32), ("valid", c_uint32), ("min", c_int64), ("majority", c_int64), ("max", c_int64)]
+
+
+class RhCommitOut(ctypes.Structure):
+    _fields_ = [("advanced", c_void_p), ("n_advanced", c_uint64), ("watch_all", c_void_p), ("n_watch_all", c_uint64)]
 
 
 class RhFrames(ctypes.Structure):
@@ -174,17 +193,34 @@ _SIGNATURES = {
     "rh_synchronize": (c_int, [c_void_p]),
     "rh_ctx_stream": (c_void_p, [c_void_p]),
     "rh_commit_soa_launch": (c_int, [c_void_p, POINTER(RhCommitSoa), c_int, c_void_p]),
-    "rh_groups_create": (c_int, [c_void_p, c_uint64, c_uint32, c_int64, POINTER(c_void_p)]),
+    "rh_groups_create": (c_int, [c_void_p, c_uint64, c_int64, POINTER(c_void_p)]),
     "rh_groups_destroy": (c_int, [c_void_p]),
-    "rh_group_set": (c_int, [c_void_p, c_uint64, c_uint32, c_int64, c_int64, c_int64]),
-    "rh_groups_load": (c_int, [c_void_p, c_uint64, c_uint64, c_void_p, c_void_p, c_void_p, c_void_p,
+    "rh_group_start": (c_int, [c_void_p, c_uint32, c_uint32, c_int64, c_int64, c_int64]),
+    "rh_group_reconf": (c_int, [c_void_p, c_uint32, c_uint32, c_void_p]),
+    "rh_group_stop": (c_int, [c_void_p, c_uint32]),
+    "rh_group_tier": (c_int, [c_void_p, c_uint32, POINTER(c_uint32)]),
+    "rh_groups_load": (c_int, [c_void_p, c_uint32, c_uint32, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p,
                                c_void_p, c_void_p]),
     "rh_push_deltas": (c_int, [c_void_p, POINTER(RhDelta), c_size_t]),
     "rh_deltas_acquire": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_size_t)]),
     "rh_deltas_submit": (c_int, [c_void_p, c_size_t]),
-    "rh_commit_batch": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, POINTER(c_size_t), c_void_p]),
-    "rh_watch_levels": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p]),
-    "rh_groups_read_commit": (c_int, [c_void_p, c_uint64, c_uint64, c_void_p]),
+    "rh_commit_batch": (c_int, [c_void_p, c_uint32, POINTER(RhCommitOut)]),
+    "rh_commit_batch_async": (c_int, [c_void_p, c_uint32, POINTER(c_uint64)]),
+    "rh_commit_batch_wait": (c_int, [c_void_p, c_uint64, POINTER(RhCommitOut)]),
+    "rh_watch_levels": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_uint64)]),
+    "rh_groups_read": (c_int, [c_void_p, c_uint32, c_uint32, ctypes.c_uint8, c_void_p]),
+    "rh_shard_of": (c_int, [c_uint64, c_uint64, c_int]),
+    "rh_node_create": (c_int, [c_uint32, c_uint64, c_int64, POINTER(c_void_p)]),
+    "rh_node_destroy": (c_int, [c_void_p]),
+    "rh_node_shards": (c_int, [c_void_p]),
+    "rh_node_groups": (c_void_p, [c_void_p, c_int]),
+    "rh_node_ctx": (c_void_p, [c_void_p, c_int]),
+    "rh_node_group_start": (c_int, [c_void_p, c_uint32, c_uint32, c_int64, c_int64, c_int64]),
+    "rh_node_group_reconf": (c_int, [c_void_p, c_uint32, c_uint32, c_void_p]),
+    "rh_node_group_stop": (c_int, [c_void_p, c_uint32]),
+    "rh_node_push_deltas": (c_int, [c_void_p, POINTER(RhDelta), c_size_t]),
+    "rh_node_commit_batch": (c_int, [c_void_p, c_void_p, c_uint64, POINTER(c_uint64), c_void_p, c_uint64,
+                                     POINTER(c_uint64)]),
     "rh_crc32c_frames_launch": (c_int, [c_void_p, POINTER(RhFrames), c_uint32, c_void_p]),
     "rh_crc32c": (c_int, [c_void_p, c_uint32, c_void_p, c_uint64, POINTER(c_uint32)]),
     "rh_crc32c_verify_host": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_uint64, c_void_p,

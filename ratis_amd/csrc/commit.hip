@@ -8,55 +8,19 @@
 //   RaftLogBase.updateCommitIndex         RaftLogBase.java:121-142
 // and, in WATCH mode, LeaderStateImpl.commitIndexChanged (LeaderStateImpl.java:612-622).
 //
-// Layout: one struct-of-arrays "tier" per follower-slot count F.  Every column is a contiguous
+// Per-group arithmetic: commit_eval.h.  Layout: one struct-of-arrays "tier" per follower-slot count F.  Every column is a contiguous
 // int64 array over the tier's groups, so a wave's loads of one column are one coalesced
 // 1 KiB request (2 groups per lane, 16 B per lane).  The order statistics over <= F+1 voters are
 // integer compare/select work in registers -- rank masks for F <= 6 (commit_kernel_rank), a
 // Batcher merge-exchange network for wider tiers (commit_kernel_net) -- no MFMA (this is not a
 // contraction).  The kernel is HBM-bound: 8(F+1)+20 bytes read and 16 bytes written per group.
 #include "rh_internal.h"
-#include "sortnet.h"
-
-#include <climits>
+#include "commit_eval.h"
 
 namespace {
 
 constexpr int kBlock = 256;            // 4 waves
 constexpr int kGroupsPerLane = 2;      // 16-byte loads per column per lane
-
-// Order statistics of the voters selected by `member` (bit i = slot i, bit N-1 = self):
-// getSorted (LSI:1076-1095) + MinMajorityMax.valueOf(sorted, gap) (LSI:926-943).
-// Non-members sort to the end as INT64_MAX; k < n so they are never selected.
-template <int N>
-__device__ __forceinline__ void order_stats(const int64_t (&vals)[N], uint32_t member, int64_t gap,
-                                            int64_t& mn, int64_t& mj, int64_t& mx) {
-    int64_t s[N];
-#pragma unroll
-    for (int i = 0; i < N; ++i) s[i] = ((member >> i) & 1u) ? vals[i] : INT64_MAX;
-    rh_sort::sort_net<N>(s);
-    const int n = __builtin_popcount(member);
-    const int k = (n - 1) >> 1;  // getMajority: sorted[(length - 1) / 2]
-    mn = s[0];
-    mj = s[0];
-    mx = s[0];
-#pragma unroll
-    for (int j = 1; j < N; ++j) {
-        mj = (j == k) ? s[j] : mj;
-        mx = (j == n - 1) ? s[j] : mx;
-    }
-    // gapThreshold clamp; Java long subtraction wraps (LSI:929-933).
-    if (gap != -1 && (int64_t)((uint64_t)mj - (uint64_t)mn) > gap) mj = mn;
-}
-
-// Same result as order_stats, from rank masks shared by the new and the old conf.
-template <int N>
-__device__ __forceinline__ void order_stats_rank(const int64_t (&vals)[N], const uint32_t (&less)[N],
-                                                 uint32_t member, int64_t gap, int64_t& mn, int64_t& mj,
-                                                 int64_t& mx) {
-    const int n = __builtin_popcount(member);
-    rh_sort::select_ranks<N>(vals, less, member, (n - 1) >> 1, n, mn, mj, mx);
-    if (gap != -1 && (int64_t)((uint64_t)mj - (uint64_t)mn) > gap) mj = mn;
-}
 
 struct TierArgs {
     rh_commit_soa t;
@@ -152,69 +116,23 @@ __device__ __forceinline__ void compute_store_sub(const TierArgs& ta, uint64_t w
     const int lane = threadIdx.x & 63;
     const uint64_t r0 = wbase + 2 * (uint64_t)lane;
 
-    // ---- getMajorityMin (LSI:956-984) ----
+    // ---- getMajorityMin (LSI:956-984) + updateCommit(majority, min) (LSI:1015-1026) ----
     const int64_t gap = commit_mode ? t.gap_threshold : -1;  // 2-arg overload passes -1 (LSI:952-954)
     bool valid[2], adv[2];
     int64_t mn[2], mj[2], mx[2], cout[2];
-    const uint32_t fmask = (1u << F) - 1u;
     bool trans[2];
 #pragma unroll
     for (int g = 0; g < 2; ++g) trans[g] = (st.w[g] & RH_CONF_ACTIVE) && (st.w[g] & RH_CONF_TRANSITIONAL);
     const bool any_trans = __any(trans[0] || trans[1]);
-
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
-        const uint32_t w = st.w[g];
         int64_t vals[N];
 #pragma unroll
         for (int k = 0; k < F; ++k) vals[k] = st.fv[g][k];
         vals[F] = st.self[g];
-        const uint32_t mnew = (w & fmask) | (((w >> 14) & 1u) << F);
-        const uint32_t mold = ((w >> RH_CONF_OLD_SHIFT) & fmask) | (((w >> 30) & 1u) << F);
-        // followers.isEmpty() && !includeSelf -> Optional.empty()  (LSI:964-966, 976-978).
-        // A word naming a follower slot >= F is malformed for this tier: no result, no commit
-        // (ABI rule shared with the lease kernel and the oracle; never a smaller quorum).
-        const bool fits = ((w & 0x3FFFu) & ~fmask) == 0 && (((w >> RH_CONF_OLD_SHIFT) & 0x3FFFu) & ~fmask) == 0;
-        const bool v = (w & RH_CONF_ACTIVE) && fits && mnew != 0 && (!trans[g] || mold != 0);
-        int64_t a0, a1, a2;
-        if (RANK) {
-            uint32_t less[N];
-            rh_sort::rank_masks<N>(vals, less);
-            order_stats_rank<N>(vals, less, mnew ? mnew : 1u, gap, a0, a1, a2);
-            if (any_trans) {
-                if (trans[g]) {  // combine(): element-wise min (LSI:915-920)
-                    int64_t b0, b1, b2;
-                    order_stats_rank<N>(vals, less, mold ? mold : 1u, gap, b0, b1, b2);
-                    a0 = b0 < a0 ? b0 : a0;
-                    a1 = b1 < a1 ? b1 : a1;
-                    a2 = b2 < a2 ? b2 : a2;
-                }
-            }
-        } else {
-            order_stats<N>(vals, mnew ? mnew : 1u, gap, a0, a1, a2);
-            if (any_trans) {
-                if (trans[g]) {  // combine(): element-wise min (LSI:915-920)
-                    int64_t b0, b1, b2;
-                    order_stats<N>(vals, mold ? mold : 1u, gap, b0, b1, b2);
-                    a0 = b0 < a0 ? b0 : a0;
-                    a1 = b1 < a1 ? b1 : a1;
-                    a2 = b2 < a2 ? b2 : a2;
-                }
-            }
-        }
-        valid[g] = v;
-        mn[g] = v ? a0 : INT64_MIN;
-        mj[g] = v ? a1 : INT64_MIN;
-        mx[g] = v ? a2 : INT64_MIN;
-        // ---- updateCommit(majority, min) (LSI:1015-1026) -> RaftLogBase.updateCommitIndex ----
-        // old = lastCommitted; if (majority > old) { newCommit = min(majority, flushIndex);
-        //   if (old < newCommit && termAt(newCommit) == currentTerm) commit = newCommit; }
-        const int64_t old = st.cin[g];
-        const int64_t flush = st.self[g];
-        const int64_t nc = a1 < flush ? a1 : flush;
-        const bool a = commit_mode && v && a1 > old && old < nc && nc >= st.tstart[g];
-        adv[g] = a;
-        cout[g] = a ? nc : old;
+        rh_eval::eval_group<F, RANK>(vals, st.w[g], gap, any_trans, valid[g], mn[g], mj[g], mx[g]);
+        adv[g] = commit_mode && rh_eval::commit_decision(valid[g], mj[g], st.cin[g], st.self[g], st.tstart[g], cout[g]);
+        if (!commit_mode) cout[g] = st.cin[g];
     }
 
     // ---- stores ----
@@ -392,39 +310,4 @@ int rh_commit_launch_impl(rh_ctx* ctx, const rh_commit_soa* tiers, int n_tiers, 
     }
     const int rc = launch_class(tiers, n_tiers, 1, 6, stream);
     return rc != RH_OK ? rc : launch_class(tiers, n_tiers, 7, 14, stream);
-}
-// ---- delta application: RaftLogIndex.updateToMax per (slot, column) ----------------------
-namespace {
-
-__global__ __launch_bounds__(256) void apply_deltas_kernel(const rh_delta* __restrict__ d, uint64_t n,
-                                                           uint64_t capacity, uint64_t stride,
-                                                           uint32_t nf, int64_t* match, int64_t* fcommit,
-                                                           int64_t* flush, int64_t* commit) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const rh_delta x = d[i];
-    if (x.slot >= capacity) return;  // validated on the host; never trust the ring blindly
-    int64_t* p = nullptr;
-    if (x.column < nf)
-        p = match + (uint64_t)x.column * stride + x.slot;
-    else if (x.column >= 16 && x.column < 16 + nf)
-        p = fcommit + (uint64_t)(x.column - 16) * stride + x.slot;
-    else if (x.column == RH_COL_FLUSH)
-        p = flush + x.slot;
-    else if (x.column == RH_COL_COMMITTED)
-        p = commit + x.slot;
-    if (p) atomicMax(reinterpret_cast<long long*>(p), (long long)x.value);
-}
-
-}  // namespace
-
-int rh_apply_deltas_impl(hipStream_t stream, const rh_delta* d_deltas, uint64_t n, uint64_t capacity,
-                         uint64_t stride, uint32_t n_followers, int64_t* match, int64_t* fcommit,
-                         int64_t* flush, int64_t* commit) {
-    if (n == 0) return RH_OK;
-    const uint64_t blocks = (n + 255) / 256;
-    hipLaunchKernelGGL(apply_deltas_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream, d_deltas, n,
-                       capacity, stride, n_followers, match, fcommit, flush, commit);
-    RH_HIP(hipGetLastError());
-    return RH_OK;
 }

@@ -1,0 +1,902 @@
+// Host side of the resident group table (rh_groups) and of the multi-GPU node (rh_node), see
+// include/ratis_hip.h.  Device kernels: table.hip.
+//
+// Reference (ratis tree): the per-division leader commit state this replaces is LeaderStateImpl's
+// FollowerInfoMap (LeaderStateImpl.java:262-294), FollowerInfoImpl (FollowerInfoImpl.java:42-151),
+// the UPDATE_COMMIT event queue (LeaderStateImpl.java:111-188, 846-854, 900-902) and the
+// RaftServerProxy's map of divisions (RaftServerProxy.java:89-150) for the multi-GPU node.
+#include <algorithm>
+#include <cstring>
+#include <new>
+#include <string>
+#include <unordered_set>
+#include <vector>
+
+#include "rh_internal.h"
+
+#define RH_EXPORT extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+using rh::CtrlOp;
+using rh::kNoRow;
+using rh::kTableTiers;
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+// Highest follower slot a conf word names (new or old mask), + 1; 0 for none.
+uint32_t needed_width(uint32_t conf) {
+    const uint32_t m = (conf & 0x3FFFu) | ((conf >> RH_CONF_OLD_SHIFT) & 0x3FFFu);
+    return m ? 32u - (uint32_t)__builtin_clz(m) : 0u;
+}
+
+struct TierHost {
+    uint32_t hw = 0;                      // rows handed out so far (high-water mark)
+    std::vector<uint32_t> free_rows;      // released rows, reusable
+    std::vector<uint32_t> pending_free;   // released by queued ops: reusable after the next flush
+};
+
+struct EvSet {
+    rh_index_event* adv = nullptr;   // host-mapped pinned [cap]
+    rh_index_event* wall = nullptr;
+    rh_index_event* d_adv = nullptr;  // device views of the same memory
+    rh_index_event* d_wall = nullptr;
+    unsigned long long* h_counts = nullptr;  // pinned [4]
+    hipEvent_t done = nullptr;
+    uint64_t ticket = 0;
+    bool pending = false;
+};
+
+}  // namespace
+
+struct rh_groups {
+    rh_ctx* ctx = nullptr;
+    uint64_t capacity = 0;
+    int64_t gap = -1;
+    std::mutex mu;
+    rh::TableDev dev;                         // device pointers (copied into every launch)
+    std::vector<uint32_t> slot_map;           // host mirror of dev.slot_map
+    std::vector<uint32_t> slot_conf;          // host mirror of each started slot's conf word
+    TierHost tiers[kTableTiers];
+    // control ops: queued on the host, applied by table_control_kernel in stream order
+    std::vector<CtrlOp> ops;
+    std::vector<uint32_t> op_stamp;           // slot -> batch generation that holds an op for it
+    uint32_t op_gen = 1;
+    CtrlOp* h_ops = nullptr;                  // pinned staging
+    CtrlOp* d_ops = nullptr;
+    size_t ops_cap = 0;
+    hipEvent_t ops_free = nullptr;
+    bool ops_used = false;
+    // delta staging: two pinned host slots, one device buffer (stream order serialises them)
+    rh_delta* h_ring[2] = {nullptr, nullptr};
+    hipEvent_t ring_free[2] = {nullptr, nullptr};
+    bool ring_used[2] = {false, false};
+    int ring_next = 0;
+    int ring_acquired = -1;
+    rh_delta* d_deltas = nullptr;
+    // events
+    EvSet ev[2];
+    uint64_t next_ticket = 1;
+    unsigned long long* d_counts = nullptr;   // [2 commit sets][4], then [8] for rh_watch_levels
+    rh_watch_event* watch = nullptr;          // host-mapped pinned [cap]
+    rh_watch_event* d_watch = nullptr;
+    int64_t* d_read = nullptr;
+    size_t read_cap = 0;
+};
+
+namespace {
+
+template <typename T>
+int dalloc(T** p, size_t count) {
+    *p = nullptr;
+    if (count == 0) return RH_OK;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(p), count * sizeof(T));
+    if (e != hipSuccess) return rh::fail(RH_E_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    return RH_OK;
+}
+
+template <typename T>
+int halloc_mapped(T** host, T** dev, size_t count) {
+    *host = nullptr;
+    *dev = nullptr;
+    hipError_t e = hipHostMalloc(reinterpret_cast<void**>(host), std::max<size_t>(count, 1) * sizeof(T), hipHostMallocMapped);
+    if (e != hipSuccess) return rh::fail(RH_E_NOMEM, "hipHostMalloc(mapped event buffer)");
+    e = hipHostGetDevicePointer(reinterpret_cast<void**>(dev), *host, 0);
+    if (e != hipSuccess) return rh::hip_fail(e, "hipHostGetDevicePointer");
+    return RH_OK;
+}
+
+void free_tier(rh::TableTier& t) {
+    for (void* p : {(void*)t.match, (void*)t.fcommit, (void*)t.flush, (void*)t.commit, (void*)t.tstart,
+                    (void*)t.conf, (void*)t.row_slot, (void*)t.wall, (void*)t.wmin, (void*)t.wmaj, (void*)t.wmax,
+                    (void*)t.dirty, (void*)t.wdirty})
+        (void)hipFree(p);
+    t = rh::TableTier{};
+}
+
+void free_groups(rh_groups* g) {
+    for (auto& t : g->dev.tier) free_tier(t);
+    (void)hipFree(g->dev.slot_map);
+    (void)hipFree(g->d_ops);
+    if (g->h_ops) (void)hipHostFree(g->h_ops);
+    if (g->ops_free) (void)hipEventDestroy(g->ops_free);
+    (void)hipFree(g->d_deltas);
+    for (int i = 0; i < 2; ++i) {
+        if (g->h_ring[i]) (void)hipHostFree(g->h_ring[i]);
+        if (g->ring_free[i]) (void)hipEventDestroy(g->ring_free[i]);
+        if (g->ev[i].adv) (void)hipHostFree(g->ev[i].adv);
+        if (g->ev[i].wall) (void)hipHostFree(g->ev[i].wall);
+        if (g->ev[i].h_counts) (void)hipHostFree(g->ev[i].h_counts);
+        if (g->ev[i].done) (void)hipEventDestroy(g->ev[i].done);
+    }
+    (void)hipFree(g->d_counts);
+    if (g->watch) (void)hipHostFree(g->watch);
+    (void)hipFree(g->d_read);
+}
+
+// (Re)allocates tier t with `rows` rows, keeping the first `keep` rows' contents.  Blocks (the
+// old arrays are released after the stream has drained every launch that still names them).
+int grow_tier(rh_groups* g, int t, uint32_t rows) {
+    rh::TableTier n{};
+    const rh::TableTier& o = g->dev.tier[t];
+    n.width = rh::width_of_tier(t);
+    n.rows = rows;
+    const size_t F = n.width;
+    int rc = RH_OK;
+    if (rc == RH_OK) rc = dalloc(&n.match, F * rows);
+    if (rc == RH_OK) rc = dalloc(&n.fcommit, F * rows);
+    if (rc == RH_OK) rc = dalloc(&n.flush, rows);
+    if (rc == RH_OK) rc = dalloc(&n.commit, rows);
+    if (rc == RH_OK) rc = dalloc(&n.tstart, rows);
+    if (rc == RH_OK) rc = dalloc(&n.conf, rows);
+    if (rc == RH_OK) rc = dalloc(&n.row_slot, rows);
+    if (rc == RH_OK) rc = dalloc(&n.wall, rows);
+    if (rc == RH_OK) rc = dalloc(&n.wmin, rows);
+    if (rc == RH_OK) rc = dalloc(&n.wmaj, rows);
+    if (rc == RH_OK) rc = dalloc(&n.wmax, rows);
+    if (rc == RH_OK) rc = dalloc(&n.dirty, rows);
+    if (rc == RH_OK) rc = dalloc(&n.wdirty, rows);
+    if (rc != RH_OK) {
+        free_tier(n);
+        return rc;
+    }
+    hipStream_t s = g->ctx->stream;
+    const uint32_t keep = o.rows;
+    auto cp = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
+        return bytes ? hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s) : hipSuccess;
+    };
+    hipError_t e = hipSuccess;
+    // fresh rows: inactive, clean, unowned
+    e = hipMemsetAsync(n.conf, 0, rows * 4, s);
+    if (e == hipSuccess) e = hipMemsetAsync(n.row_slot, 0xFF, rows * 4, s);
+    if (e == hipSuccess) e = hipMemsetAsync(n.dirty, 0, rows, s);
+    if (e == hipSuccess) e = hipMemsetAsync(n.wdirty, 0, rows, s);
+    for (size_t k = 0; k < F && e == hipSuccess && keep; ++k) {
+        e = cp(n.match + k * rows, o.match + k * keep, (size_t)keep * 8);
+        if (e == hipSuccess) e = cp(n.fcommit + k * rows, o.fcommit + k * keep, (size_t)keep * 8);
+    }
+    if (keep && e == hipSuccess) {
+        const size_t k8 = (size_t)keep * 8, k4 = (size_t)keep * 4;
+        if (e == hipSuccess) e = cp(n.flush, o.flush, k8);
+        if (e == hipSuccess) e = cp(n.commit, o.commit, k8);
+        if (e == hipSuccess) e = cp(n.tstart, o.tstart, k8);
+        if (e == hipSuccess) e = cp(n.conf, o.conf, k4);
+        if (e == hipSuccess) e = cp(n.row_slot, o.row_slot, k4);
+        if (e == hipSuccess) e = cp(n.wall, o.wall, k8);
+        if (e == hipSuccess) e = cp(n.wmin, o.wmin, k8);
+        if (e == hipSuccess) e = cp(n.wmaj, o.wmaj, k8);
+        if (e == hipSuccess) e = cp(n.wmax, o.wmax, k8);
+        if (e == hipSuccess) e = cp(n.dirty, o.dirty, keep);
+        if (e == hipSuccess) e = cp(n.wdirty, o.wdirty, keep);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) {
+        free_tier(n);
+        return rh::hip_fail(e, "rh_groups: tier growth");
+    }
+    rh::TableTier old = o;
+    g->dev.tier[t] = n;
+    free_tier(old);
+    return RH_OK;
+}
+
+// A row of tier t for a new occupant.
+int alloc_row(rh_groups* g, int t, uint32_t* row) {
+    TierHost& h = g->tiers[t];
+    if (!h.free_rows.empty()) {
+        *row = h.free_rows.back();
+        h.free_rows.pop_back();
+        return RH_OK;
+    }
+    if (h.hw >= g->dev.tier[t].rows) {
+        const uint64_t want = std::max<uint64_t>(1024, (uint64_t)g->dev.tier[t].rows * 2);
+        const uint64_t cap = (g->capacity + 127) / 128 * 128;
+        const uint32_t rows = (uint32_t)std::min<uint64_t>(std::max<uint64_t>(want, h.hw + 128), std::max<uint64_t>(cap, 128));
+        if (rows <= h.hw) return rh::fail(RH_E_RANGE, "rh_groups: tier full");
+        int rc = grow_tier(g, t, (rows + 127) / 128 * 128);
+        if (rc != RH_OK) return rc;
+    }
+    *row = h.hw++;
+    return RH_OK;
+}
+
+// Enqueues the H2D of the queued control ops and their kernel; rows they released become reusable.
+int flush_ops(rh_groups* g) {
+    const size_t n = g->ops.size();
+    if (n) {
+        hipStream_t s = g->ctx->stream;
+        if (g->ops_used) RH_HIP(hipEventSynchronize(g->ops_free));  // staging still being read
+        if (n > g->ops_cap) {
+            if (g->h_ops) (void)hipHostFree(g->h_ops);
+            (void)hipFree(g->d_ops);
+            g->h_ops = nullptr;
+            g->d_ops = nullptr;
+            g->ops_cap = 0;
+            const size_t cap = std::max<size_t>(n, 4096);
+            if (hipHostMalloc(reinterpret_cast<void**>(&g->h_ops), cap * sizeof(CtrlOp)) != hipSuccess)
+                return rh::fail(RH_E_NOMEM, "rh_groups: control-op staging");
+            int rc = dalloc(&g->d_ops, cap);
+            if (rc != RH_OK) return rc;
+            g->ops_cap = cap;
+        }
+        std::memcpy(g->h_ops, g->ops.data(), n * sizeof(CtrlOp));
+        RH_HIP(hipMemcpyAsync(g->d_ops, g->h_ops, n * sizeof(CtrlOp), hipMemcpyHostToDevice, s));
+        RH_HIP(hipEventRecord(g->ops_free, s));
+        g->ops_used = true;
+        int rc = rh_table_control(g->dev, g->d_ops, n, s);
+        if (rc != RH_OK) return rc;
+        g->ops.clear();
+    }
+    ++g->op_gen;
+    for (auto& t : g->tiers) {
+        t.free_rows.insert(t.free_rows.end(), t.pending_free.begin(), t.pending_free.end());
+        t.pending_free.clear();
+    }
+    return RH_OK;
+}
+
+// Queues one control op for `slot` (flushing first if the current batch already holds one).
+int queue_op(rh_groups* g, const CtrlOp& op) {
+    if (g->op_stamp[op.slot] == g->op_gen) {
+        int rc = flush_ops(g);
+        if (rc != RH_OK) return rc;
+    }
+    g->op_stamp[op.slot] = g->op_gen;
+    g->ops.push_back(op);
+    if (g->ops.size() >= (1u << 16)) return flush_ops(g);
+    return RH_OK;
+}
+
+uint32_t enc(int t, uint32_t row) { return ((uint32_t)t << 28) | row; }
+
+int do_stop(rh_groups* g, uint32_t slot) {
+    const uint32_t m = g->slot_map[slot];
+    if (m == kNoRow) return RH_OK;
+    CtrlOp op{};
+    op.kind = rh::kCtrlStop;
+    op.slot = slot;
+    op.src = m;
+    int rc = queue_op(g, op);
+    if (rc != RH_OK) return rc;
+    g->tiers[m >> 28].pending_free.push_back(m & rh::kRowMask);
+    g->slot_map[slot] = kNoRow;
+    g->slot_conf[slot] = 0;
+    return RH_OK;
+}
+
+int ring_wait(rh_groups* g, int i) {
+    if (g->ring_used[i]) RH_HIP(hipEventSynchronize(g->ring_free[i]));
+    return RH_OK;
+}
+
+// H2D of the first n deltas of ring slot i, then the SET and MAX phases (stream-ordered).
+int ring_submit(rh_groups* g, int i, size_t n, bool has_set) {
+    hipStream_t s = g->ctx->stream;
+    int rc = flush_ops(g);
+    if (rc != RH_OK) return rc;
+    RH_HIP(hipMemcpyAsync(g->d_deltas, g->h_ring[i], n * sizeof(rh_delta), hipMemcpyHostToDevice, s));
+    RH_HIP(hipEventRecord(g->ring_free[i], s));
+    g->ring_used[i] = true;
+    g->ring_next = i ^ 1;
+    if (has_set) {
+        rc = rh_table_apply_deltas(g->dev, g->d_deltas, n, 0, s);
+        if (rc != RH_OK) return rc;
+    }
+    return rh_table_apply_deltas(g->dev, g->d_deltas, n, 1, s);
+}
+
+int check_conf(uint32_t conf, const char* who) {
+    if (needed_width(conf) > RH_MAX_FOLLOWERS) return rh::fail(RH_E_RANGE, std::string(who) + ": conf names a slot > 13");
+    return RH_OK;
+}
+
+}  // namespace
+
+// ---- lifecycle -------------------------------------------------------------------------------------
+RH_EXPORT int rh_groups_create(rh_ctx* ctx, uint64_t capacity, int64_t gap_threshold, rh_groups** out) {
+    if (!ctx || !out) return rh::fail(RH_E_INVAL, "rh_groups_create: ctx/out == NULL");
+    *out = nullptr;
+    if (capacity == 0 || capacity >= (1ull << 28)) return rh::fail(RH_E_RANGE, "rh_groups_create: capacity must be in [1, 2^28)");
+    if (gap_threshold < -1) return rh::fail(RH_E_INVAL, "rh_groups_create: gap_threshold must be -1 or >= 0");
+    DeviceGuard dg(ctx->device);
+    rh_groups* g = new (std::nothrow) rh_groups();
+    if (!g) return rh::fail(RH_E_NOMEM, "rh_groups_create: out of host memory");
+    g->ctx = ctx;
+    g->capacity = capacity;
+    g->gap = gap_threshold;
+    g->dev.capacity = capacity;
+    g->dev.gap = gap_threshold;
+    for (int t = 0; t < kTableTiers; ++t) g->dev.tier[t].width = rh::width_of_tier(t);
+    int rc = RH_OK;
+    try {
+        g->slot_map.assign(capacity, kNoRow);
+        g->slot_conf.assign(capacity, 0);
+        g->op_stamp.assign(capacity, 0);
+    } catch (...) {
+        rc = rh::fail(RH_E_NOMEM, "rh_groups_create: out of host memory");
+    }
+    hipStream_t s = ctx->stream;
+    if (rc == RH_OK) rc = dalloc(&g->dev.slot_map, capacity);
+    if (rc == RH_OK && hipMemsetAsync(g->dev.slot_map, 0xFF, capacity * 4, s) != hipSuccess)
+        rc = rh::fail(RH_E_DEVICE, "rh_groups_create: init");
+    if (rc == RH_OK) rc = dalloc(&g->d_deltas, (size_t)RH_DELTA_SLOT);
+    for (int i = 0; i < 2 && rc == RH_OK; ++i) {
+        if (hipHostMalloc(reinterpret_cast<void**>(&g->h_ring[i]), (size_t)RH_DELTA_SLOT * sizeof(rh_delta)) != hipSuccess)
+            rc = rh::fail(RH_E_NOMEM, "hipHostMalloc(delta staging)");
+        if (rc == RH_OK && hipEventCreateWithFlags(&g->ring_free[i], hipEventDisableTiming) != hipSuccess)
+            rc = rh::fail(RH_E_DEVICE, "hipEventCreate(delta staging)");
+        if (rc == RH_OK) rc = halloc_mapped(&g->ev[i].adv, &g->ev[i].d_adv, capacity);
+        if (rc == RH_OK) rc = halloc_mapped(&g->ev[i].wall, &g->ev[i].d_wall, capacity);
+        if (rc == RH_OK && hipHostMalloc(reinterpret_cast<void**>(&g->ev[i].h_counts), 4 * sizeof(unsigned long long)) != hipSuccess)
+            rc = rh::fail(RH_E_NOMEM, "hipHostMalloc(event counters)");
+        if (rc == RH_OK && hipEventCreateWithFlags(&g->ev[i].done, hipEventDisableTiming) != hipSuccess)
+            rc = rh::fail(RH_E_DEVICE, "hipEventCreate(commit batch)");
+    }
+    if (rc == RH_OK) rc = halloc_mapped(&g->watch, &g->d_watch, capacity);
+    if (rc == RH_OK) rc = dalloc(&g->d_counts, 9);
+    if (rc == RH_OK && hipEventCreateWithFlags(&g->ops_free, hipEventDisableTiming) != hipSuccess)
+        rc = rh::fail(RH_E_DEVICE, "hipEventCreate(control ops)");
+    if (rc == RH_OK && hipStreamSynchronize(s) != hipSuccess) rc = rh::fail(RH_E_DEVICE, "rh_groups_create: sync");
+    if (rc != RH_OK) {
+        free_groups(g);
+        delete g;
+        return rc;
+    }
+    *out = g;
+    return RH_OK;
+}
+
+RH_EXPORT int rh_groups_destroy(rh_groups* g) {
+    if (!g) return rh::fail(RH_E_INVAL, "rh_groups_destroy: NULL");
+    DeviceGuard dg(g->ctx->device);
+    (void)hipStreamSynchronize(g->ctx->stream);
+    free_groups(g);
+    delete g;
+    return RH_OK;
+}
+
+// ---- control ---------------------------------------------------------------------------------------
+RH_EXPORT int rh_group_start(rh_groups* g, uint32_t slot, uint32_t conf, int64_t flush_index, int64_t commit_index,
+                             int64_t term_start) {
+    if (!g) return rh::fail(RH_E_INVAL, "rh_group_start: groups == NULL");
+    if (slot >= g->capacity) return rh::fail(RH_E_INVAL, "rh_group_start: slot out of range");
+    int rc = check_conf(conf, "rh_group_start");
+    if (rc != RH_OK) return rc;
+    DeviceGuard dg(g->ctx->device);
+    std::lock_guard<std::mutex> lk(g->mu);
+    rc = do_stop(g, slot);  // a re-armed slot drops its old row (and every FollowerInfo with it)
+    if (rc != RH_OK) return rc;
+    const int t = rh::tier_of_width(needed_width(conf));
+    uint32_t row = 0;
+    rc = alloc_row(g, t, &row);
+    if (rc != RH_OK) return rc;
+    CtrlOp op{};
+    op.kind = rh::kCtrlStart;
+    op.slot = slot;
+    op.dst = enc(t, row);
+    op.conf = conf;
+    op.flush = flush_index;
+    op.commit = commit_index;
+    op.tstart = term_start;
+    rc = queue_op(g, op);
+    if (rc != RH_OK) return rc;
+    g->slot_map[slot] = op.dst;
+    g->slot_conf[slot] = conf;
+    return RH_OK;
+}
+
+RH_EXPORT int rh_group_reconf(rh_groups* g, uint32_t slot, uint32_t conf, const int8_t* src) {
+    if (!g) return rh::fail(RH_E_INVAL, "rh_group_reconf: groups == NULL");
+    if (slot >= g->capacity) return rh::fail(RH_E_INVAL, "rh_group_reconf: slot out of range");
+    int rc = check_conf(conf, "rh_group_reconf");
+    if (rc != RH_OK) return rc;
+    if (src)
+        for (int k = 0; k < (int)RH_MAX_FOLLOWERS; ++k)
+            if (src[k] < -1 || src[k] >= (int)RH_MAX_FOLLOWERS)
+                return rh::fail(RH_E_INVAL, "rh_group_reconf: src entries must be -1 or a follower slot");
+    DeviceGuard dg(g->ctx->device);
+    std::lock_guard<std::mutex> lk(g->mu);
+    const uint32_t m = g->slot_map[slot];
+    if (m == kNoRow) return rh::fail(RH_E_STATE, "rh_group_reconf: slot not started");
+    const int t_old = (int)(m >> 28);
+    const int t_new = rh::tier_of_width(needed_width(conf));
+    CtrlOp op{};
+    op.slot = slot;
+    op.src = m;
+    op.conf = conf;
+    for (int k = 0; k < (int)RH_MAX_FOLLOWERS; ++k) op.map[k] = src ? src[k] : (int8_t)k;
+    if (t_new == t_old) {
+        op.kind = rh::kCtrlReconf;
+        op.dst = m;
+    } else {
+        uint32_t row = 0;
+        rc = alloc_row(g, t_new, &row);
+        if (rc != RH_OK) return rc;
+        op.kind = rh::kCtrlMove;
+        op.dst = enc(t_new, row);
+    }
+    rc = queue_op(g, op);
+    if (rc != RH_OK) return rc;
+    if (op.kind == rh::kCtrlMove) g->tiers[t_old].pending_free.push_back(m & rh::kRowMask);
+    g->slot_map[slot] = op.dst;
+    g->slot_conf[slot] = conf;
+    return RH_OK;
+}
+
+RH_EXPORT int rh_group_stop(rh_groups* g, uint32_t slot) {
+    if (!g) return rh::fail(RH_E_INVAL, "rh_group_stop: groups == NULL");
+    if (slot >= g->capacity) return rh::fail(RH_E_INVAL, "rh_group_stop: slot out of range");
+    DeviceGuard dg(g->ctx->device);
+    std::lock_guard<std::mutex> lk(g->mu);
+    return do_stop(g, slot);
+}
+
+RH_EXPORT int rh_group_tier(rh_groups* g, uint32_t slot, uint32_t* out_width) {
+    if (!g || !out_width) return rh::fail(RH_E_INVAL, "rh_group_tier: NULL argument");
+    if (slot >= g->capacity) return rh::fail(RH_E_INVAL, "rh_group_tier: slot out of range");
+    std::lock_guard<std::mutex> lk(g->mu);
+    const uint32_t m = g->slot_map[slot];
+    *out_width = m == kNoRow ? 0u : rh::width_of_tier((int)(m >> 28));
+    return RH_OK;
+}
+
+namespace {
+
+__global__ void table_load_kernel(rh::TableDev T, int t, const uint32_t* __restrict__ rows,
+                                  const uint32_t* __restrict__ slots, const int64_t* __restrict__ cols, uint32_t m) {
+    // cols: [F match][F fcommit][flush][commit][tstart][conf] x m, column-major
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const rh::TableTier& D = T.tier[t];
+    const uint32_t r = rows[i];
+    const uint64_t R = D.rows, F = D.width;
+    for (uint32_t k = 0; k < F; ++k) {
+        D.match[k * R + r] = cols[(uint64_t)k * m + i];
+        D.fcommit[k * R + r] = cols[(F + k) * m + i];
+    }
+    D.flush[r] = cols[(2 * F) * m + i];
+    D.commit[r] = cols[(2 * F + 1) * m + i];
+    D.tstart[r] = cols[(2 * F + 2) * m + i];
+    D.conf[r] = (uint32_t)cols[(2 * F + 3) * m + i];
+    D.wall[r] = INT64_MIN;
+    D.wmin[r] = INT64_MIN;
+    D.wmaj[r] = INT64_MIN;
+    D.wmax[r] = INT64_MIN;
+    D.dirty[r] = 1;
+    D.wdirty[r] = 1;
+    D.row_slot[r] = slots[i];
+    T.slot_map[slots[i]] = ((uint32_t)t << 28) | r;
+}
+
+}  // namespace
+
+RH_EXPORT int rh_groups_load(rh_groups* g, uint32_t first, uint32_t n, uint32_t n_host_followers, const int64_t* match,
+                             const int64_t* fcommit, const int64_t* flush, const int64_t* commit,
+                             const int64_t* term_start, const uint32_t* conf) {
+    if (!g) return rh::fail(RH_E_INVAL, "rh_groups_load: groups == NULL");
+    if ((uint64_t)first + n > g->capacity) return rh::fail(RH_E_INVAL, "rh_groups_load: slots out of range");
+    if (n == 0) return RH_OK;
+    if (!flush || !commit || !term_start || !conf)
+        return rh::fail(RH_E_INVAL, "rh_groups_load: flush, commit, term_start and conf are required");
+    if (n_host_followers > RH_MAX_FOLLOWERS) return rh::fail(RH_E_RANGE, "rh_groups_load: n_host_followers > 14");
+    for (uint32_t i = 0; i < n; ++i) {
+        int rc = check_conf(conf[i], "rh_groups_load");
+        if (rc != RH_OK) return rc;
+    }
+    DeviceGuard dg(g->ctx->device);
+    std::lock_guard<std::mutex> lk(g->mu);
+    for (uint32_t i = 0; i < n; ++i) {
+        int rc = do_stop(g, first + i);
+        if (rc != RH_OK) return rc;
+    }
+    int rc = flush_ops(g);  // launches the stops; the rows they released are reusable now
+    if (rc != RH_OK) return rc;
+    hipStream_t s = g->ctx->stream;
+    std::vector<std::vector<uint32_t>> members(kTableTiers);
+    for (uint32_t i = 0; i < n; ++i) members[rh::tier_of_width(needed_width(conf[i]))].push_back(i);
+    for (int t = 0; t < kTableTiers; ++t) {
+        const std::vector<uint32_t>& mem = members[t];
+        if (mem.empty()) continue;
+        const uint32_t m = (uint32_t)mem.size(), F = rh::width_of_tier(t);
+        std::vector<uint32_t> rows(m), slots(m);
+        for (uint32_t j = 0; j < m; ++j) {
+            rc = alloc_row(g, t, &rows[j]);
+            if (rc != RH_OK) return rc;
+            slots[j] = first + mem[j];
+        }
+        std::vector<int64_t> cols((size_t)(2 * F + 4) * m);
+        for (uint32_t j = 0; j < m; ++j) {
+            const uint32_t i = mem[j];
+            for (uint32_t k = 0; k < F; ++k) {
+                const bool have = k < n_host_followers;
+                cols[(size_t)k * m + j] = (have && match) ? match[(size_t)k * n + i] : -1;
+                cols[(size_t)(F + k) * m + j] = (have && fcommit) ? fcommit[(size_t)k * n + i] : -1;
+            }
+            cols[(size_t)(2 * F) * m + j] = flush[i];
+            cols[(size_t)(2 * F + 1) * m + j] = commit[i];
+            cols[(size_t)(2 * F + 2) * m + j] = term_start[i];
+            cols[(size_t)(2 * F + 3) * m + j] = (int64_t)conf[i];
+        }
+        uint32_t *d_rows = nullptr, *d_slots = nullptr;
+        int64_t* d_cols = nullptr;
+        rc = dalloc(&d_rows, m);
+        if (rc == RH_OK) rc = dalloc(&d_slots, m);
+        if (rc == RH_OK) rc = dalloc(&d_cols, cols.size());
+        hipError_t e = hipSuccess;
+        if (rc == RH_OK) {
+            e = hipMemcpyAsync(d_rows, rows.data(), m * 4, hipMemcpyHostToDevice, s);
+            if (e == hipSuccess) e = hipMemcpyAsync(d_slots, slots.data(), m * 4, hipMemcpyHostToDevice, s);
+            if (e == hipSuccess) e = hipMemcpyAsync(d_cols, cols.data(), cols.size() * 8, hipMemcpyHostToDevice, s);
+            if (e == hipSuccess) {
+                hipLaunchKernelGGL(table_load_kernel, dim3((m + 255) / 256), dim3(256), 0, s, g->dev, t, d_rows, d_slots,
+                                   d_cols, m);
+                e = hipGetLastError();
+            }
+            if (e == hipSuccess) e = hipStreamSynchronize(s);
+        }
+        (void)hipFree(d_rows);
+        (void)hipFree(d_slots);
+        (void)hipFree(d_cols);
+        if (rc != RH_OK) return rc;
+        if (e != hipSuccess) return rh::hip_fail(e, "rh_groups_load");
+        for (uint32_t j = 0; j < m; ++j) {
+            g->slot_map[slots[j]] = enc(t, rows[j]);
+            g->slot_conf[slots[j]] = conf[mem[j]];
+        }
+    }
+    return RH_OK;
+}
+
+// ---- deltas ------------------------------------------------------------------------------------------
+RH_EXPORT int rh_push_deltas(rh_groups* g, const rh_delta* deltas, size_t n) {
+    if (!g) return rh::fail(RH_E_INVAL, "rh_push_deltas: groups == NULL");
+    if (n == 0) return RH_OK;
+    if (!deltas) return rh::fail(RH_E_INVAL, "rh_push_deltas: deltas == NULL");
+    DeviceGuard dg(g->ctx->device);
+    std::lock_guard<std::mutex> lk(g->mu);
+    if (g->ring_acquired >= 0) return rh::fail(RH_E_STATE, "rh_push_deltas: a staging slot is acquired");
+    bool any_set = false;
+    for (size_t i = 0; i < n; ++i) {
+        const rh_delta& d = deltas[i];
+        const uint32_t m = d.slot < g->capacity ? g->slot_map[d.slot] : kNoRow;
+        const uint32_t w = m == kNoRow ? 0u : rh::width_of_tier((int)(m >> 28));
+        const uint32_t c = d.column;
+        const bool ok_col = c < w || (c >= 16 && c < 16 + w) || c == RH_COL_FLUSH || c == RH_COL_COMMITTED;
+        if (m == kNoRow || !ok_col || d.op > RH_OP_SET)
+            return rh::fail(RH_E_INVAL, "rh_push_deltas: delta " + std::to_string(i) +
+                                            " names a stopped slot, a column outside its tier or an unknown op");
+        any_set |= d.op == RH_OP_SET;
+    }
+    // Batches: a SET to a (slot, column) already touched in the current batch starts a new one, so
+    // SET-then-MAX phases reproduce the one-by-one order (ratis_hip.h, rh_delta).
+    std::unordered_set<uint64_t> touched;
+    size_t done = 0;
+    while (done < n) {
+        size_t end = std::min(n, done + (size_t)RH_DELTA_SLOT);
+        bool batch_set = false;
+        if (any_set) {
+            touched.clear();
+            for (size_t i = done; i < end; ++i) {
+                const uint64_t cell = (uint64_t)deltas[i].slot * 64 + deltas[i].column;
+                if (deltas[i].op == RH_OP_SET) {
+                    if (!touched.insert(cell).second) {
+                        end = i;
+                        break;
+                    }
+                    batch_set = true;
+                } else {
+                    touched.insert(cell);
+                }
+            }
+        }
+        const int i = g->ring_next;
+        int rc = ring_wait(g, i);
+        if (rc == RH_OK) {
+            std::memcpy(g->h_ring[i], deltas + done, (end - done) * sizeof(rh_delta));
+            rc = ring_submit(g, i, end - done, batch_set);
+        }
+        if (rc != RH_OK) return rc;
+        done = end;
+    }
+    return RH_OK;
+}
+
+RH_EXPORT int rh_deltas_acquire(rh_groups* g, rh_delta** out_buf, size_t* out_cap) {
+    if (!g || !out_buf || !out_cap) return rh::fail(RH_E_INVAL, "rh_deltas_acquire: NULL argument");
+    DeviceGuard dg(g->ctx->device);
+    std::lock_guard<std::mutex> lk(g->mu);
+    if (g->ring_acquired >= 0) return rh::fail(RH_E_STATE, "rh_deltas_acquire: a slot is already acquired");
+    const int i = g->ring_next;
+    int rc = ring_wait(g, i);
+    if (rc != RH_OK) return rc;
+    g->ring_acquired = i;
+    *out_buf = g->h_ring[i];
+    *out_cap = RH_DELTA_SLOT;
+    return RH_OK;
+}
+
+RH_EXPORT int rh_deltas_submit(rh_groups* g, size_t n) {
+    if (!g) return rh::fail(RH_E_INVAL, "rh_deltas_submit: groups == NULL");
+    DeviceGuard dg(g->ctx->device);
+    std::lock_guard<std::mutex> lk(g->mu);
+    const int i = g->ring_acquired;
+    if (i < 0) return rh::fail(RH_E_STATE, "rh_deltas_submit: no slot acquired");
+    if (n > RH_DELTA_SLOT) return rh::fail(RH_E_INVAL, "rh_deltas_submit: n exceeds the slot capacity");
+    g->ring_acquired = -1;
+    if (n == 0) return RH_OK;
+    return ring_submit(g, i, n, true);
+}
+
+// ---- evaluation -------------------------------------------------------------------------------------
+RH_EXPORT int rh_commit_batch_async(rh_groups* g, uint32_t flags, uint64_t* ticket) {
+    if (!g || !ticket) return rh::fail(RH_E_INVAL, "rh_commit_batch_async: NULL argument");
+    if (flags & ~RH_COMMIT_WATCH_ALL) return rh::fail(RH_E_INVAL, "rh_commit_batch_async: unknown flags");
+    DeviceGuard dg(g->ctx->device);
+    std::lock_guard<std::mutex> lk(g->mu);
+    const uint64_t tk = g->next_ticket++;
+    EvSet& e = g->ev[tk & 1];
+    if (e.pending) RH_HIP(hipEventSynchronize(e.done));  // its buffers are about to be rewritten
+    hipStream_t s = g->ctx->stream;
+    int rc = flush_ops(g);
+    if (rc != RH_OK) return rc;
+    unsigned long long* dc = g->d_counts + (tk & 1) * 4;
+    RH_HIP(hipMemsetAsync(dc, 0, 4 * sizeof(unsigned long long), s));
+    rh::TableEvents ev;
+    ev.adv = e.d_adv;
+    ev.wall = (flags & RH_COMMIT_WATCH_ALL) ? e.d_wall : nullptr;
+    ev.counts = dc;
+    ev.cap = g->capacity;
+    rc = rh_table_commit(g->dev, RH_MODE_COMMIT, ev, s);
+    if (rc != RH_OK) return rc;
+    RH_HIP(hipMemcpyAsync(e.h_counts, dc, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    RH_HIP(hipEventRecord(e.done, s));
+    e.ticket = tk;
+    e.pending = true;
+    *ticket = tk;
+    return RH_OK;
+}
+
+RH_EXPORT int rh_commit_batch_wait(rh_groups* g, uint64_t ticket, rh_commit_out* out) {
+    if (!g || !out) return rh::fail(RH_E_INVAL, "rh_commit_batch_wait: NULL argument");
+    DeviceGuard dg(g->ctx->device);
+    EvSet* e;
+    {
+        std::lock_guard<std::mutex> lk(g->mu);
+        e = &g->ev[ticket & 1];
+        if (e->ticket != ticket) return rh::fail(RH_E_STATE, "rh_commit_batch_wait: ticket unknown or superseded");
+    }
+    RH_HIP(hipEventSynchronize(e->done));
+    std::lock_guard<std::mutex> lk(g->mu);
+    if (e->ticket != ticket) return rh::fail(RH_E_STATE, "rh_commit_batch_wait: ticket superseded while waiting");
+    e->pending = false;
+    out->advanced = e->adv;
+    out->n_advanced = std::min<uint64_t>(e->h_counts[0], g->capacity);
+    out->watch_all = e->wall;
+    out->n_watch_all = std::min<uint64_t>(e->h_counts[1], g->capacity);
+    return RH_OK;
+}
+
+RH_EXPORT int rh_commit_batch(rh_groups* g, uint32_t flags, rh_commit_out* out) {
+    if (!g || !out) return rh::fail(RH_E_INVAL, "rh_commit_batch: NULL argument");
+    uint64_t tk = 0;
+    int rc = rh_commit_batch_async(g, flags, &tk);
+    return rc != RH_OK ? rc : rh_commit_batch_wait(g, tk, out);
+}
+
+RH_EXPORT int rh_watch_levels(rh_groups* g, const rh_watch_event** out_events, uint64_t* out_n) {
+    if (!g || !out_events || !out_n) return rh::fail(RH_E_INVAL, "rh_watch_levels: NULL argument");
+    DeviceGuard dg(g->ctx->device);
+    std::lock_guard<std::mutex> lk(g->mu);
+    hipStream_t s = g->ctx->stream;
+    int rc = flush_ops(g);
+    if (rc != RH_OK) return rc;
+    unsigned long long* dc = g->d_counts + 8 - 2;  // the WATCH kernel counts into dc[2] = d_counts[8]
+    RH_HIP(hipMemsetAsync(dc + 2, 0, sizeof(unsigned long long), s));
+    rh::TableEvents ev;
+    ev.watch = g->d_watch;
+    ev.counts = dc;
+    ev.cap = g->capacity;
+    rc = rh_table_commit(g->dev, RH_MODE_WATCH, ev, s);
+    if (rc != RH_OK) return rc;
+    unsigned long long cnt = 0;
+    RH_HIP(hipMemcpyAsync(&cnt, dc + 2, sizeof(cnt), hipMemcpyDeviceToHost, s));
+    RH_HIP(hipStreamSynchronize(s));
+    *out_events = g->watch;
+    *out_n = std::min<uint64_t>(cnt, g->capacity);
+    return RH_OK;
+}
+
+RH_EXPORT int rh_groups_read(rh_groups* g, uint32_t first, uint32_t n, uint8_t column, int64_t* out) {
+    if (!g || (!out && n)) return rh::fail(RH_E_INVAL, "rh_groups_read: NULL argument");
+    if ((uint64_t)first + n > g->capacity) return rh::fail(RH_E_INVAL, "rh_groups_read: slots out of range");
+    const uint32_t c = column;
+    if (!(c < RH_MAX_FOLLOWERS || (c >= 16 && c < 16 + RH_MAX_FOLLOWERS) || c == RH_COL_FLUSH || c == RH_COL_COMMITTED ||
+          c == RH_COL_CONF || c == RH_COL_TERM_START))
+        return rh::fail(RH_E_INVAL, "rh_groups_read: unknown column");
+    if (n == 0) return RH_OK;
+    DeviceGuard dg(g->ctx->device);
+    std::lock_guard<std::mutex> lk(g->mu);
+    hipStream_t s = g->ctx->stream;
+    int rc = flush_ops(g);
+    if (rc != RH_OK) return rc;
+    if (g->read_cap < n) {
+        (void)hipFree(g->d_read);
+        g->read_cap = 0;
+        rc = dalloc(&g->d_read, n);
+        if (rc != RH_OK) return rc;
+        g->read_cap = n;
+    }
+    rc = rh_table_read(g->dev, first, n, column, g->d_read, s);
+    if (rc != RH_OK) return rc;
+    RH_HIP(hipMemcpyAsync(out, g->d_read, (size_t)n * 8, hipMemcpyDeviceToHost, s));
+    RH_HIP(hipStreamSynchronize(s));
+    return RH_OK;
+}
+
+// ---- multi-GPU node ----------------------------------------------------------------------------------
+struct rh_node {
+    std::vector<rh_ctx*> ctx;
+    std::vector<rh_groups*> tab;
+    uint64_t cap = 0;
+};
+
+RH_EXPORT int rh_shard_of(uint64_t msb, uint64_t lsb, int n_shards) {
+    if (n_shards < 1) return rh::fail(RH_E_INVAL, "rh_shard_of: n_shards < 1");
+    const uint64_t hilo = msb ^ lsb;  // java.util.UUID.hashCode
+    const int32_t h = (int32_t)(uint32_t)(hilo >> 32) ^ (int32_t)(uint32_t)hilo;
+    const int32_t r = h % n_shards;   // Math.floorMod
+    return r < 0 ? r + n_shards : r;
+}
+
+RH_EXPORT int rh_node_create(uint32_t device_mask, uint64_t capacity_per_shard, int64_t gap_threshold, rh_node** out) {
+    if (!out) return rh::fail(RH_E_INVAL, "rh_node_create: out == NULL");
+    *out = nullptr;
+    if (device_mask == 0) return rh::fail(RH_E_INVAL, "rh_node_create: empty device mask");
+    if (capacity_per_shard * (uint64_t)__builtin_popcount(device_mask) > 0xFFFFFFFFull)
+        return rh::fail(RH_E_RANGE, "rh_node_create: node slots must fit 32 bits");
+    rh_node* nd = new (std::nothrow) rh_node();
+    if (!nd) return rh::fail(RH_E_NOMEM, "rh_node_create: out of host memory");
+    nd->cap = capacity_per_shard;
+    int rc = RH_OK;
+    for (int d = 0; d < 32 && rc == RH_OK; ++d) {
+        if (!((device_mask >> d) & 1u)) continue;
+        rh_ctx* c = nullptr;
+        rc = rh_init(d, &c);
+        if (rc != RH_OK) break;
+        nd->ctx.push_back(c);
+        rh_groups* t = nullptr;
+        rc = rh_groups_create(c, capacity_per_shard, gap_threshold, &t);
+        if (rc == RH_OK) nd->tab.push_back(t);
+    }
+    if (rc != RH_OK) {
+        (void)rh_node_destroy(nd);
+        return rc;
+    }
+    *out = nd;
+    return RH_OK;
+}
+
+RH_EXPORT int rh_node_destroy(rh_node* nd) {
+    if (!nd) return rh::fail(RH_E_INVAL, "rh_node_destroy: NULL");
+    for (rh_groups* t : nd->tab) (void)rh_groups_destroy(t);
+    for (rh_ctx* c : nd->ctx) (void)rh_shutdown(c);
+    delete nd;
+    return RH_OK;
+}
+
+RH_EXPORT int rh_node_shards(rh_node* nd) { return nd ? (int)nd->tab.size() : rh::fail(RH_E_INVAL, "rh_node_shards: NULL"); }
+
+RH_EXPORT rh_groups* rh_node_groups(rh_node* nd, int shard) {
+    return (nd && shard >= 0 && shard < (int)nd->tab.size()) ? nd->tab[shard] : nullptr;
+}
+
+RH_EXPORT rh_ctx* rh_node_ctx(rh_node* nd, int shard) {
+    return (nd && shard >= 0 && shard < (int)nd->ctx.size()) ? nd->ctx[shard] : nullptr;
+}
+
+namespace {
+int route(rh_node* nd, uint32_t node_slot, rh_groups** t, uint32_t* slot) {
+    if (!nd) return rh::fail(RH_E_INVAL, "rh_node: NULL");
+    const uint64_t sh = node_slot / nd->cap;
+    if (sh >= nd->tab.size()) return rh::fail(RH_E_INVAL, "rh_node: node slot out of range");
+    *t = nd->tab[sh];
+    *slot = (uint32_t)(node_slot % nd->cap);
+    return RH_OK;
+}
+}  // namespace
+
+RH_EXPORT int rh_node_group_start(rh_node* nd, uint32_t node_slot, uint32_t conf, int64_t flush_index,
+                                  int64_t commit_index, int64_t term_start) {
+    rh_groups* t;
+    uint32_t s;
+    int rc = route(nd, node_slot, &t, &s);
+    return rc != RH_OK ? rc : rh_group_start(t, s, conf, flush_index, commit_index, term_start);
+}
+
+RH_EXPORT int rh_node_group_reconf(rh_node* nd, uint32_t node_slot, uint32_t conf, const int8_t* src) {
+    rh_groups* t;
+    uint32_t s;
+    int rc = route(nd, node_slot, &t, &s);
+    return rc != RH_OK ? rc : rh_group_reconf(t, s, conf, src);
+}
+
+RH_EXPORT int rh_node_group_stop(rh_node* nd, uint32_t node_slot) {
+    rh_groups* t;
+    uint32_t s;
+    int rc = route(nd, node_slot, &t, &s);
+    return rc != RH_OK ? rc : rh_group_stop(t, s);
+}
+
+RH_EXPORT int rh_node_push_deltas(rh_node* nd, const rh_delta* deltas, size_t n) {
+    if (!nd || (n && !deltas)) return rh::fail(RH_E_INVAL, "rh_node_push_deltas: NULL argument");
+    const size_t S = nd->tab.size();
+    std::vector<std::vector<rh_delta>> part(S);
+    for (size_t i = 0; i < n; ++i) {
+        const uint64_t sh = deltas[i].slot / nd->cap;
+        if (sh >= S) return rh::fail(RH_E_INVAL, "rh_node_push_deltas: delta " + std::to_string(i) + " has a bad slot");
+        rh_delta d = deltas[i];
+        d.slot = (uint32_t)(d.slot % nd->cap);
+        part[sh].push_back(d);
+    }
+    for (size_t sh = 0; sh < S; ++sh) {
+        int rc = rh_push_deltas(nd->tab[sh], part[sh].data(), part[sh].size());
+        if (rc != RH_OK) return rc;
+    }
+    return RH_OK;
+}
+
+RH_EXPORT int rh_node_commit_batch(rh_node* nd, rh_index_event* advanced, uint64_t adv_cap, uint64_t* n_advanced,
+                                   rh_index_event* watch_all, uint64_t watch_cap, uint64_t* n_watch_all) {
+    if (!nd || !n_advanced || !n_watch_all) return rh::fail(RH_E_INVAL, "rh_node_commit_batch: NULL argument");
+    if ((adv_cap && !advanced) || (watch_cap && !watch_all))
+        return rh::fail(RH_E_INVAL, "rh_node_commit_batch: output arrays required");
+    const size_t S = nd->tab.size();
+    std::vector<uint64_t> tk(S);
+    for (size_t sh = 0; sh < S; ++sh) {  // every shard's evaluation is in flight before any wait
+        int rc = rh_commit_batch_async(nd->tab[sh], RH_COMMIT_WATCH_ALL, &tk[sh]);
+        if (rc != RH_OK) return rc;
+    }
+    uint64_t na = 0, nw = 0;
+    for (size_t sh = 0; sh < S; ++sh) {
+        rh_commit_out o{};
+        int rc = rh_commit_batch_wait(nd->tab[sh], tk[sh], &o);
+        if (rc != RH_OK) return rc;
+        const uint32_t base = (uint32_t)(sh * nd->cap);
+        for (uint64_t i = 0; i < o.n_advanced; ++i, ++na)
+            if (na < adv_cap) advanced[na] = rh_index_event{o.advanced[i].slot + base, 0u, o.advanced[i].value};
+        for (uint64_t i = 0; i < o.n_watch_all; ++i, ++nw)
+            if (nw < watch_cap) watch_all[nw] = rh_index_event{o.watch_all[i].slot + base, 0u, o.watch_all[i].value};
+    }
+    *n_advanced = na;
+    *n_watch_all = nw;
+    return RH_OK;
+}

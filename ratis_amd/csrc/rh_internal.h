@@ -34,6 +34,65 @@ void build_crc_slice_tables(CrcTables* t);
 void build_crc_shift_table(uint64_t nbytes, uint32_t out[4][256]);
 std::vector<uint32_t> build_crc_lane_tables(int Q, int S);
 
+// ---- resident table (rh_groups) device layout --------------------------------------------------
+// Tier t holds slots whose conf names follower slots < width = 2 (t + 1); every column is a
+// contiguous array over the tier's rows (row space), so the commit kernels see a tier exactly as
+// an rh_commit_soa.  slot_map: slot -> (tier << 28) | row, kNoRow = stopped.
+constexpr int kTableTiers = 7;
+constexpr uint32_t kNoRow = 0xFFFFFFFFu;
+constexpr uint32_t kRowMask = 0x0FFFFFFFu;
+__host__ __device__ inline int tier_of_width(uint32_t w) { return w <= 2 ? 0 : (int)((w + 1) / 2) - 1; }
+__host__ __device__ inline uint32_t width_of_tier(int t) { return 2u * (uint32_t)(t + 1); }
+
+struct TableTier {
+    uint32_t width = 0;         // follower columns F
+    uint32_t rows = 0;          // allocated rows (column stride), multiple of 128
+    int64_t* match = nullptr;   // [F][rows] FollowerInfo.matchIndex
+    int64_t* fcommit = nullptr; // [F][rows] FollowerInfo.commitIndex
+    int64_t* flush = nullptr;   // [rows] leader flushIndex
+    int64_t* commit = nullptr;  // [rows] leader commitIndex (lastCommittedIndex)
+    int64_t* tstart = nullptr;  // [rows] first index of the current term
+    uint32_t* conf = nullptr;   // [rows] membership word (0 on free rows)
+    uint32_t* row_slot = nullptr;  // [rows] row -> slot
+    int64_t* wall = nullptr;    // [rows] last watch-ALL level of updateCommit (INT64_MIN = none)
+    int64_t* wmin = nullptr;    // [rows] last commitIndexChanged levels
+    int64_t* wmaj = nullptr;
+    int64_t* wmax = nullptr;
+    uint8_t* dirty = nullptr;   // [rows] 1 = updateCommit pending
+    uint8_t* wdirty = nullptr;  // [rows] 1 = commitIndexChanged pending
+};
+
+struct TableDev {
+    TableTier tier[kTableTiers];
+    uint32_t* slot_map = nullptr;  // [capacity]
+    uint64_t capacity = 0;
+    int64_t gap = -1;
+};
+
+// Control operations on rows (rh_group_start / reconf / stop), applied in parallel by
+// table_control_kernel: within one launch every slot and every destination row appears once and
+// no destination row is a source row (the host splits and defers row reuse to guarantee it).
+enum CtrlKind : uint32_t { kCtrlStart = 1, kCtrlMove = 2, kCtrlStop = 3, kCtrlReconf = 4 };
+struct CtrlOp {
+    uint32_t kind;
+    uint32_t slot;
+    uint32_t dst;     // (tier << 28) | row written (START / MOVE / RECONF)
+    uint32_t src;     // (tier << 28) | row read (MOVE / RECONF) or freed (STOP)
+    uint32_t conf;
+    int8_t map[RH_MAX_FOLLOWERS];  // dst follower column k <- src column map[k] (-1: new FollowerInfo)
+    uint16_t pad;
+    int64_t flush, commit, tstart;  // START
+};
+
+// Event sinks of the table kernels (host-mapped pinned memory, counters in device memory).
+struct TableEvents {
+    rh_index_event* adv = nullptr;     // COMMIT: advanced
+    rh_index_event* wall = nullptr;    // COMMIT: watch-ALL changes
+    rh_watch_event* watch = nullptr;   // WATCH: level changes
+    unsigned long long* counts = nullptr;  // [0] adv, [1] wall, [2] watch
+    uint64_t cap = 0;
+};
+
 }  // namespace rh
 
 struct rh_ctx {
@@ -54,9 +113,13 @@ struct rh_ctx {
 
 // Launchers implemented in the .hip files (device pointers, async on `stream`).
 int rh_commit_launch_impl(rh_ctx* ctx, const rh_commit_soa* tiers, int n_tiers, hipStream_t stream);
-int rh_apply_deltas_impl(hipStream_t stream, const rh_delta* d_deltas, uint64_t n, uint64_t capacity,
-                         uint64_t stride, uint32_t n_followers, int64_t* match, int64_t* fcommit,
-                         int64_t* flush, int64_t* commit);
+// Resident table kernels (table.hip): delta apply (phase 0 = SET deltas, 1 = MAX deltas),
+// control ops, and updateCommit / commitIndexChanged over the dirty rows of every tier.
+int rh_table_apply_deltas(const rh::TableDev& t, const rh_delta* d_deltas, uint64_t n, int phase, hipStream_t stream);
+int rh_table_control(const rh::TableDev& t, const rh::CtrlOp* d_ops, uint64_t n, hipStream_t stream);
+int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev, hipStream_t stream);
+int rh_table_read(const rh::TableDev& t, uint32_t first, uint32_t n, uint8_t column, int64_t* d_out,
+                  hipStream_t stream);
 int rh_crc_launch_impl(rh_ctx* ctx, const rh_frames* f, uint32_t flags, hipStream_t stream);
 int rh_crc_upload_tables(rh_ctx* ctx);
 int rh_segments_launch_impl(rh_ctx* ctx, const rh_segments* segs, hipStream_t stream);

@@ -1,60 +1,123 @@
-"""RaftGroupTable: the resident per-GPU table of leader divisions (``rh_groups`` in the C ABI).
+"""RaftGroupTable / RaftNode: the resident per-GPU table of leader divisions (``rh_groups``) and the
+multi-GPU server built from them (``rh_node``), include/ratis_hip.h.
 
 This is the object the Java ``ratis-hip`` module holds.  Its methods mirror the
-reference's producers and consumers of the commit index, batched over every group of the table:
+reference's producers and consumers of the commit index, batched over every division of a
+server (paths relative to the ratis tree, ratis-server/.../server/impl/ unless noted):
 
-  =============================================  ============================================
-  reference (ratis tree)                         RaftGroupTable
-  =============================================  ============================================
-  FollowerInfo.updateMatchIndex                  :meth:`update_match_index` (monotone max)
+  ==============================================  ===========================================
+  reference                                       RaftGroupTable
+  ==============================================  ===========================================
+  new LeaderStateImpl: addSenders, StartupLogEntry :meth:`start`
+    LeaderStateImpl.java:296-301, 421-430, 681-692
+  applyOldNewConf / replicateNewConf / restart    :meth:`reconf`
+    LeaderStateImpl.java:624-633, 704-724, 1064-1074
+  step down / group removal                       :meth:`stop`
+  FollowerInfo.updateMatchIndex                   :meth:`update_match_index` (RH_OP_MAX)
     FollowerInfoImpl.java:93-95
-  FollowerInfo.updateCommitIndex                 :meth:`update_follower_commit_index`
+  FollowerInfo.setSnapshotIndex                   :meth:`set_snapshot_index` (RH_OP_SET)
+    FollowerInfoImpl.java:147-151
+  FollowerInfo.updateCommitIndex                  :meth:`update_follower_commit_index`
     FollowerInfoImpl.java:103-105
-  SegmentedRaftLogWorker flush-index advance     :meth:`update_flush_index`
-    SegmentedRaftLogWorker.java:419-431
-  RaftConfigurationImpl change / leader start    :meth:`set_group`
-    LeaderStateImpl.java:296-301, 624-633
-  LeaderStateImpl.updateCommit()                 :meth:`update_commit`
+  SegmentedRaftLogWorker flush-index advance      :meth:`update_flush_index`
+    raftlog/segmented/SegmentedRaftLogWorker.java:419-431
+  LeaderStateImpl.updateCommit() (dirty groups)   :meth:`update_commit`, :meth:`commit_async`
     LeaderStateImpl.java:946-950, 1015-1026
-  LeaderStateImpl.commitIndexChanged()           :meth:`commit_index_changed`
-    LeaderStateImpl.java:612-622
-  =============================================  ============================================
+  LeaderStateImpl.commitIndexChanged()            :meth:`commit_index_changed`
+    LeaderStateImpl.java:606-622
+  ==============================================  ===========================================
 
-Host arrays are numpy; all compute is the HIP kernel behind ``rh_commit_batch`` /
-``rh_watch_levels``.
+Host arrays are numpy; all compute is the HIP kernels behind the calls.  Errors raise
+``_lib.IllegalArgumentError`` for RH_E_INVAL / RH_E_RANGE (Java: IllegalArgumentException) and
+``_lib.RatisHipError`` otherwise.
 """
 from __future__ import annotations
 
 import ctypes
-from typing import Optional, Tuple
+from typing import Optional, Sequence, Tuple
 
 import numpy as np
 
 from . import _lib
-from ._lib import RhDelta, check
+from ._lib import RhCommitOut, RhDelta, check
+
+DELTA_DTYPE = np.dtype([("slot", "<u4"), ("column", "u1"), ("op", "u1"), ("reserved", "<u2"), ("value", "<i8")])
+INDEX_EVENT_DTYPE = np.dtype([("slot", "<u4"), ("reserved", "<u4"), ("value", "<i8")])
+WATCH_EVENT_DTYPE = np.dtype([("slot", "<u4"), ("valid", "<u4"), ("min", "<i8"), ("majority", "<i8"), ("max", "<i8")])
 
 
 def _p(a: Optional[np.ndarray]):
     return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
 
 
+def _view(ptr: int, n: int, dtype: np.dtype) -> np.ndarray:
+    if n == 0 or not ptr:
+        return np.zeros(0, dtype=dtype)
+    raw = (ctypes.c_uint8 * (n * dtype.itemsize)).from_address(ptr)
+    return np.frombuffer(raw, dtype=dtype)
+
+
+def make_deltas(slots, columns, values, ops=_lib.RH_OP_MAX) -> np.ndarray:
+    """Structured array of ``rh_delta`` (16 bytes each)."""
+    slots = np.asarray(slots, dtype=np.uint32).reshape(-1)
+    n = slots.size
+    d = np.zeros(n, dtype=DELTA_DTYPE)
+    d["slot"] = slots
+    d["column"] = np.broadcast_to(np.asarray(columns, dtype=np.uint8), (n,))
+    d["op"] = np.broadcast_to(np.asarray(ops, dtype=np.uint8), (n,))
+    d["value"] = np.broadcast_to(np.asarray(values, dtype=np.int64), (n,))
+    return d
+
+
+def _src_array(src: Optional[Sequence[int]]):
+    if src is None:
+        return None
+    a = np.full(_lib.RH_MAX_FOLLOWERS, -1, dtype=np.int8)
+    s = np.asarray(src, dtype=np.int64)
+    a[: s.size] = s
+    return a
+
+
+class CommitResult:
+    """Events of one batched updateCommit: copies of the library's pinned result buffers."""
+
+    def __init__(self, out: RhCommitOut):
+        adv = _view(out.advanced or 0, out.n_advanced, INDEX_EVENT_DTYPE)
+        wall = _view(out.watch_all or 0, out.n_watch_all, INDEX_EVENT_DTYPE)
+        o = np.argsort(adv["slot"], kind="stable")
+        self.advanced_slots = adv["slot"][o].astype(np.int64)
+        self.advanced_commit = adv["value"][o].copy()
+        o = np.argsort(wall["slot"], kind="stable")
+        self.watch_all_slots = wall["slot"][o].astype(np.int64)
+        self.watch_all_min = wall["value"][o].copy()
+
+
 class RaftGroupTable:
-    def __init__(self, ctx, capacity: int, n_followers: int, gap_threshold: int = -1):
+    def __init__(self, ctx, capacity: int, gap_threshold: int = -1):
         self._lib = _lib.load()
         self.ctx = ctx
         self.capacity = int(capacity)
-        self.n_followers = int(n_followers)
         self.gap_threshold = int(gap_threshold)
         h = ctypes.c_void_p()
-        check(self._lib.rh_groups_create(ctx.handle, self.capacity, self.n_followers, self.gap_threshold,
-                                         ctypes.byref(h)))
+        check(self._lib.rh_groups_create(ctx.handle, self.capacity, self.gap_threshold, ctypes.byref(h)))
         self._h = h
+
+    @classmethod
+    def _wrap(cls, handle, capacity: int, gap_threshold: int):
+        t = cls.__new__(cls)
+        t._lib = _lib.load()
+        t.ctx = None
+        t.capacity = capacity
+        t.gap_threshold = gap_threshold
+        t._h = ctypes.c_void_p(handle)
+        t._owned = False
+        return t
 
     # -- lifecycle --------------------------------------------------------------------------
     def close(self) -> None:
-        if self._h is not None:
+        if self._h is not None and getattr(self, "_owned", True):
             check(self._lib.rh_groups_destroy(self._h))
-            self._h = None
+        self._h = None
 
     def __enter__(self):
         return self
@@ -68,61 +131,59 @@ class RaftGroupTable:
             raise _lib.RatisHipError(_lib.RH_E_STATE, "RaftGroupTable closed")
         return self._h
 
-    # -- conf / bulk load -------------------------------------------------------------------
-    def set_group(self, slot: int, conf: int, flush_index: int, commit_index: int, term_start: int) -> None:
-        check(self._lib.rh_group_set(self.handle, slot, conf & 0xFFFFFFFF, flush_index, commit_index, term_start))
+    # -- control ----------------------------------------------------------------------------
+    def start(self, slot: int, conf: int, flush_index: int, commit_index: int, term_start: int) -> None:
+        check(self._lib.rh_group_start(self.handle, slot, conf & 0xFFFFFFFF, flush_index, commit_index, term_start))
 
-    def load(self, first: int, n: int, match: Optional[np.ndarray] = None, fcommit: Optional[np.ndarray] = None,
-             flush: Optional[np.ndarray] = None, commit: Optional[np.ndarray] = None,
-             term_start: Optional[np.ndarray] = None, conf: Optional[np.ndarray] = None) -> None:
-        def i64(a, shape):
-            if a is None:
-                return None
-            a = np.ascontiguousarray(a, dtype=np.int64)
-            if a.shape != shape:
-                raise ValueError(f"expected shape {shape}, got {a.shape}")
-            return a
+    def reconf(self, slot: int, conf: int, src: Optional[Sequence[int]] = None) -> None:
+        a = _src_array(src)
+        check(self._lib.rh_group_reconf(self.handle, slot, conf & 0xFFFFFFFF, _p(a)))
 
-        F = self.n_followers
-        match = i64(match, (F, n))
-        fcommit = i64(fcommit, (F, n))
-        flush, commit, term_start = i64(flush, (n,)), i64(commit, (n,)), i64(term_start, (n,))
-        if conf is not None:
-            conf = np.ascontiguousarray(conf).astype(np.uint32)
-            if conf.shape != (n,):
-                raise ValueError("conf shape")
-        check(self._lib.rh_groups_load(self.handle, first, n, _p(match), _p(fcommit), _p(flush), _p(commit),
-                                       _p(term_start), _p(conf)))
+    def stop(self, slot: int) -> None:
+        check(self._lib.rh_group_stop(self.handle, slot))
+
+    def tier_width(self, slot: int) -> int:
+        w = ctypes.c_uint32()
+        check(self._lib.rh_group_tier(self.handle, slot, ctypes.byref(w)))
+        return w.value
+
+    def load(self, first: int, conf: np.ndarray, flush: np.ndarray, commit: np.ndarray, term_start: np.ndarray,
+             match: Optional[np.ndarray] = None, fcommit: Optional[np.ndarray] = None) -> None:
+        """Bulk start of slots [first, first + n) with explicit follower state ([F, n] arrays)."""
+        conf = np.ascontiguousarray(conf).astype(np.uint32)
+        n = conf.size
+        f = 0
+        arrs = []
+        for a in (match, fcommit):
+            if a is not None:
+                a = np.ascontiguousarray(a, dtype=np.int64)
+                if a.ndim != 2 or a.shape[1] != n:
+                    raise ValueError("match / fcommit must be [F, n]")
+                f = max(f, a.shape[0])
+            arrs.append(a)
+        match, fcommit = arrs
+        if match is not None and fcommit is not None and match.shape != fcommit.shape:
+            raise ValueError("match and fcommit shapes differ")
+        cols = [np.ascontiguousarray(x, dtype=np.int64) for x in (flush, commit, term_start)]
+        if any(c.shape != (n,) for c in cols):
+            raise ValueError("flush / commit / term_start must be [n]")
+        check(self._lib.rh_groups_load(self.handle, first, n, f, _p(match), _p(fcommit), _p(cols[0]), _p(cols[1]),
+                                       _p(cols[2]), _p(conf)))
 
     # -- delta producers --------------------------------------------------------------------
-    def push_deltas(self, slots: np.ndarray, columns: np.ndarray, values: np.ndarray) -> None:
-        slots = np.asarray(slots, dtype=np.uint64)
-        n = slots.size
-        arr = np.zeros(n, dtype=[("slot", "<u8"), ("column", "<u4"), ("reserved", "<u4"), ("value", "<i8")])
-        arr["slot"] = slots
-        arr["column"] = np.broadcast_to(np.asarray(columns, dtype=np.uint32), (n,))
-        arr["value"] = np.broadcast_to(np.asarray(values, dtype=np.int64), (n,))
-        ptr = arr.ctypes.data_as(ctypes.POINTER(RhDelta))
-        check(self._lib.rh_push_deltas(self.handle, ptr, n))
+    def push(self, deltas: np.ndarray) -> None:
+        deltas = np.ascontiguousarray(deltas, dtype=DELTA_DTYPE)
+        check(self._lib.rh_push_deltas(self.handle, deltas.ctypes.data_as(ctypes.POINTER(RhDelta)), deltas.size))
 
-    DELTA_DTYPE = np.dtype([("slot", "<u8"), ("column", "<u4"), ("reserved", "<u4"), ("value", "<i8")])
-
-    def acquire_deltas(self) -> np.ndarray:
-        """Zero-copy producer path: the next pinned staging slot as a structured numpy array
-        (fields slot/column/reserved/value) to fill in place; hand it over with
-        :meth:`submit_deltas`.  The view is valid only until that call."""
-        ptr = ctypes.c_void_p()
-        cap = ctypes.c_size_t()
-        check(self._lib.rh_deltas_acquire(self.handle, ctypes.byref(ptr), ctypes.byref(cap)))
-        raw = (ctypes.c_uint8 * (cap.value * self.DELTA_DTYPE.itemsize)).from_address(ptr.value)
-        return np.frombuffer(raw, dtype=self.DELTA_DTYPE)
-
-    def submit_deltas(self, n: int) -> None:
-        """Enqueues H2D + device apply of the first ``n`` deltas of the acquired slot (async)."""
-        check(self._lib.rh_deltas_submit(self.handle, int(n)))
+    def push_deltas(self, slots, columns, values, ops=_lib.RH_OP_MAX) -> None:
+        self.push(make_deltas(slots, columns, values, ops))
 
     def update_match_index(self, slots, follower_slot: int, values) -> None:
         self.push_deltas(slots, _lib.rh_col_match(follower_slot), values)
+
+    def set_snapshot_index(self, slots, follower_slot: int, values) -> None:
+        """FollowerInfo.setSnapshotIndex: matchIndex set unconditionally (may go down)."""
+        self.push_deltas(slots, _lib.rh_col_match(follower_slot), values, _lib.RH_OP_SET)
 
     def update_follower_commit_index(self, slots, follower_slot: int, values) -> None:
         self.push_deltas(slots, _lib.rh_col_fcommit(follower_slot), values)
@@ -130,32 +191,117 @@ class RaftGroupTable:
     def update_flush_index(self, slots, values) -> None:
         self.push_deltas(slots, _lib.RH_COL_FLUSH, values)
 
+    def acquire_deltas(self) -> np.ndarray:
+        """Zero-copy producer path: the next pinned staging slot as a structured numpy array to
+        fill in place; hand it over with :meth:`submit_deltas`.  Valid only until that call."""
+        ptr = ctypes.c_void_p()
+        cap = ctypes.c_size_t()
+        check(self._lib.rh_deltas_acquire(self.handle, ctypes.byref(ptr), ctypes.byref(cap)))
+        return _view(ptr.value, cap.value, DELTA_DTYPE)
+
+    def submit_deltas(self, n: int) -> None:
+        """Enqueues H2D + device apply of the first ``n`` deltas of the acquired slot (async)."""
+        check(self._lib.rh_deltas_submit(self.handle, int(n)))
+
     # -- consumers --------------------------------------------------------------------------
-    def update_commit(self, want_min: bool = False) -> Tuple[np.ndarray, np.ndarray, Optional[np.ndarray]]:
-        """Batched ``LeaderStateImpl.updateCommit()``: returns (slots, new commit index) of the
-        groups whose commit index advanced (sorted by slot), and optionally the watch-ALL
-        level (``min``) of every slot (INT64_MIN where getMajorityMin is empty)."""
-        cap = self.capacity
-        slots = np.empty(cap, dtype=np.uint64)
-        commits = np.empty(cap, dtype=np.int64)
-        mins = np.empty(cap, dtype=np.int64) if want_min else None
-        n = ctypes.c_size_t()
-        check(self._lib.rh_commit_batch(self.handle, _p(slots), _p(commits), cap, ctypes.byref(n), _p(mins)))
-        k = n.value
-        order = np.argsort(slots[:k], kind="stable")
-        return slots[:k][order], commits[:k][order], mins
+    def commit_async(self, watch_all: bool = True) -> int:
+        tk = ctypes.c_uint64()
+        check(self._lib.rh_commit_batch_async(self.handle, _lib.RH_COMMIT_WATCH_ALL if watch_all else 0,
+                                              ctypes.byref(tk)))
+        return tk.value
 
-    def commit_index_changed(self) -> Tuple[np.ndarray, np.ndarray, np.ndarray, np.ndarray]:
-        """Batched ``commitIndexChanged()`` levels: (min, majority, max, valid[bool])."""
-        cap = self.capacity
-        mn, mj, mx = (np.empty(cap, dtype=np.int64) for _ in range(3))
-        bits = np.empty((cap + 63) // 64, dtype=np.uint64)
-        check(self._lib.rh_watch_levels(self.handle, _p(mn), _p(mj), _p(mx), _p(bits)))
-        valid = np.unpackbits(bits.view(np.uint8), bitorder="little")[:cap].astype(bool)
-        return mn, mj, mx, valid
+    def commit_wait(self, ticket: int) -> CommitResult:
+        out = RhCommitOut()
+        check(self._lib.rh_commit_batch_wait(self.handle, ticket, ctypes.byref(out)))
+        return CommitResult(out)
 
-    def read_commit(self, first: int = 0, n: Optional[int] = None) -> np.ndarray:
+    def commit_wait_counts(self, ticket: int) -> Tuple[int, int]:
+        """Like :meth:`commit_wait` but returns only (n_advanced, n_watch_all): the events stay in
+        the library's pinned buffers (the bench's pipelined loop)."""
+        out = RhCommitOut()
+        check(self._lib.rh_commit_batch_wait(self.handle, ticket, ctypes.byref(out)))
+        return int(out.n_advanced), int(out.n_watch_all)
+
+    def update_commit(self, watch_all: bool = True) -> CommitResult:
+        """Batched ``LeaderStateImpl.updateCommit()`` over the dirty slots: the slots whose commit
+        index advanced (sorted, with the new value) and, with ``watch_all``, the slots whose
+        watch-ALL level changed."""
+        out = RhCommitOut()
+        check(self._lib.rh_commit_batch(self.handle, _lib.RH_COMMIT_WATCH_ALL if watch_all else 0,
+                                        ctypes.byref(out)))
+        return CommitResult(out)
+
+    def commit_index_changed(self) -> np.ndarray:
+        """Batched ``commitIndexChanged()``: the changed levels (WATCH_EVENT_DTYPE, sorted by slot)."""
+        ptr = ctypes.c_void_p()
+        n = ctypes.c_uint64()
+        check(self._lib.rh_watch_levels(self.handle, ctypes.byref(ptr), ctypes.byref(n)))
+        ev = _view(ptr.value or 0, n.value, WATCH_EVENT_DTYPE).copy()
+        return ev[np.argsort(ev["slot"], kind="stable")]
+
+    def read(self, column: int, first: int = 0, n: Optional[int] = None) -> np.ndarray:
         n = self.capacity - first if n is None else n
         out = np.empty(n, dtype=np.int64)
-        check(self._lib.rh_groups_read_commit(self.handle, first, n, _p(out)))
+        check(self._lib.rh_groups_read(self.handle, first, n, column, _p(out)))
         return out
+
+    def read_commit(self, first: int = 0, n: Optional[int] = None) -> np.ndarray:
+        return self.read(_lib.RH_COL_COMMITTED, first, n)
+
+
+def shard_of(msb: int, lsb: int, n_shards: int) -> int:
+    """``rh_shard_of``: floorMod(RaftGroupId.hashCode(), n) computed by the library."""
+    return check(_lib.load().rh_shard_of(msb & (2**64 - 1), lsb & (2**64 - 1), n_shards))
+
+
+class RaftNode:
+    """``rh_node``: one RaftServer's leader divisions over every GPU of ``device_mask``."""
+
+    def __init__(self, device_mask: int, capacity_per_shard: int, gap_threshold: int = -1):
+        self._lib = _lib.load()
+        h = ctypes.c_void_p()
+        check(self._lib.rh_node_create(device_mask, capacity_per_shard, gap_threshold, ctypes.byref(h)))
+        self._h = h
+        self.capacity_per_shard = int(capacity_per_shard)
+        self.n_shards = check(self._lib.rh_node_shards(h))
+        self.tables = [RaftGroupTable._wrap(self._lib.rh_node_groups(h, s), capacity_per_shard, gap_threshold)
+                       for s in range(self.n_shards)]
+
+    def close(self) -> None:
+        if self._h is not None:
+            check(self._lib.rh_node_destroy(self._h))
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def place(self, msb: int, lsb: int, index_in_shard: int) -> int:
+        """Node slot of a RaftGroupId: its shard's base + the module's slot within that shard."""
+        return shard_of(msb, lsb, self.n_shards) * self.capacity_per_shard + index_in_shard
+
+    def start(self, node_slot: int, conf: int, flush_index: int, commit_index: int, term_start: int) -> None:
+        check(self._lib.rh_node_group_start(self._h, node_slot, conf & 0xFFFFFFFF, flush_index, commit_index,
+                                            term_start))
+
+    def reconf(self, node_slot: int, conf: int, src: Optional[Sequence[int]] = None) -> None:
+        check(self._lib.rh_node_group_reconf(self._h, node_slot, conf & 0xFFFFFFFF, _p(_src_array(src))))
+
+    def stop(self, node_slot: int) -> None:
+        check(self._lib.rh_node_group_stop(self._h, node_slot))
+
+    def push(self, deltas: np.ndarray) -> None:
+        deltas = np.ascontiguousarray(deltas, dtype=DELTA_DTYPE)
+        check(self._lib.rh_node_push_deltas(self._h, deltas.ctypes.data_as(ctypes.POINTER(RhDelta)), deltas.size))
+
+    def update_commit(self, cap: int) -> Tuple[np.ndarray, np.ndarray]:
+        """All shards' updateCommit events: (advanced, watch_all) structured arrays, node slots."""
+        adv = np.zeros(cap, dtype=INDEX_EVENT_DTYPE)
+        wall = np.zeros(cap, dtype=INDEX_EVENT_DTYPE)
+        na, nw = ctypes.c_uint64(), ctypes.c_uint64()
+        check(self._lib.rh_node_commit_batch(self._h, _p(adv), cap, ctypes.byref(na), _p(wall), cap, ctypes.byref(nw)))
+        a = adv[: min(na.value, cap)]
+        w = wall[: min(nw.value, cap)]
+        return a[np.argsort(a["slot"], kind="stable")], w[np.argsort(w["slot"], kind="stable")]

@@ -23,7 +23,8 @@ def declared_functions():
 def test_header_parses_into_function_list():
     names = declared_functions()
     for must in ("rh_init", "rh_commit_soa_launch", "rh_crc32c_frames_launch", "rh_push_deltas",
-                 "rh_commit_batch", "rh_crc32c_verify_host"):
+                 "rh_commit_batch", "rh_commit_batch_async", "rh_group_reconf", "rh_node_create",
+                 "rh_crc32c_verify_host"):
         assert must in names
 
 
@@ -49,7 +50,10 @@ def test_invalid_arguments_fail_without_gpu():
     lib = _lib.load()
     assert lib.rh_commit_soa_launch(None, None, 1, None) == _lib.RH_E_INVAL
     assert b"ctx" in lib.rh_last_error()
-    assert lib.rh_groups_create(None, 10, 4, -1, None) == _lib.RH_E_INVAL
+    assert lib.rh_groups_create(None, 10, -1, None) == _lib.RH_E_INVAL
+    assert lib.rh_node_create(0, 10, -1, None) == _lib.RH_E_INVAL
+    assert lib.rh_commit_batch(None, 0, None) == _lib.RH_E_INVAL
+    assert lib.rh_push_deltas(None, None, 0) == _lib.RH_E_INVAL
     assert lib.rh_crc32c_frames_launch(None, None, 0, None) == _lib.RH_E_INVAL
     with pytest.raises(_lib.IllegalArgumentError):
         _lib.check(lib.rh_lease_soa_launch(None, None, 1, None))
@@ -64,6 +68,13 @@ int main(void) {
   printf("rh_commit_soa %zu\n", sizeof(rh_commit_soa));
   printf("rh_frames %zu\n", sizeof(rh_frames));
   printf("rh_delta %zu\n", sizeof(rh_delta));
+  printf("rh_index_event %zu\n", sizeof(rh_index_event));
+  printf("rh_watch_event %zu\n", sizeof(rh_watch_event));
+  printf("rh_commit_out %zu\n", sizeof(rh_commit_out));
+  F(rh_index_event, slot) F(rh_index_event, reserved) F(rh_index_event, value)
+  F(rh_watch_event, slot) F(rh_watch_event, valid) F(rh_watch_event, min) F(rh_watch_event, majority)
+  F(rh_watch_event, max)
+  F(rh_commit_out, advanced) F(rh_commit_out, n_advanced) F(rh_commit_out, watch_all) F(rh_commit_out, n_watch_all)
   printf("rh_segments %zu\n", sizeof(rh_segments));
   printf("rh_lease_soa %zu\n", sizeof(rh_lease_soa));
   printf("rh_segments_crc %zu\n", sizeof(rh_segments_crc));
@@ -77,7 +88,7 @@ int main(void) {
   F(rh_commit_soa, adv_count) F(rh_commit_soa, adv_cap) F(rh_commit_soa, adv_row_base)
   F(rh_frames, buf) F(rh_frames, buf_len) F(rh_frames, frame_off) F(rh_frames, frame_len) F(rh_frames, n)
   F(rh_frames, init_state) F(rh_frames, reserved) F(rh_frames, crc_out) F(rh_frames, bad_bits) F(rh_frames, n_bad)
-  F(rh_delta, slot) F(rh_delta, column) F(rh_delta, reserved) F(rh_delta, value)
+  F(rh_delta, slot) F(rh_delta, column) F(rh_delta, op) F(rh_delta, reserved) F(rh_delta, value)
   F(rh_segments, buf) F(rh_segments, buf_len) F(rh_segments, seg_off) F(rh_segments, seg_len)
   F(rh_segments, n_seg) F(rh_segments, max_op) F(rh_segments, frames_per_seg_cap) F(rh_segments, scratch_off)
   F(rh_segments, scratch_len) F(rh_segments, frame_off) F(rh_segments, frame_len) F(rh_segments, frame_cap)
@@ -107,9 +118,14 @@ def test_struct_layouts_match_header(tmp_path):
     assert int(vals["rh_segments"]) == ctypes.sizeof(_lib.RhSegments)
     assert int(vals["rh_lease_soa"]) == ctypes.sizeof(_lib.RhLeaseSoa)
     assert int(vals["rh_segments_crc"]) == ctypes.sizeof(_lib.RhSegmentsCrc)
+    assert int(vals["rh_delta"]) == 16 and int(vals["rh_index_event"]) == 16 and int(vals["rh_watch_event"]) == 32
+    from ratis_amd import groups
+    assert groups.DELTA_DTYPE.itemsize == 16 and groups.INDEX_EVENT_DTYPE.itemsize == 16
+    assert groups.WATCH_EVENT_DTYPE.itemsize == 32
     for cname, cls in (("rh_commit_soa", _lib.RhCommitSoa), ("rh_frames", _lib.RhFrames), ("rh_delta", _lib.RhDelta),
                        ("rh_segments", _lib.RhSegments), ("rh_lease_soa", _lib.RhLeaseSoa),
-                       ("rh_segments_crc", _lib.RhSegmentsCrc)):
+                       ("rh_segments_crc", _lib.RhSegmentsCrc), ("rh_index_event", _lib.RhIndexEvent),
+                       ("rh_watch_event", _lib.RhWatchEvent), ("rh_commit_out", _lib.RhCommitOut)):
         for fname, _ in cls._fields_:
             assert int(vals[f"{cname}.{fname}"]) == getattr(cls, fname).offset, (cname, fname)
     assert int(vals["conf"]) == _lib.conf_pack(0x5, True, True, 0x3, True, True)

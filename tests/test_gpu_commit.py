@@ -1,6 +1,7 @@
 """GPU parity of the batched quorum-commit kernel against the CPU oracle (bit-exact).
 
-Every launch goes through the C ABI (rh_commit_soa_launch / rh_groups_*).  The oracle is
+Every launch goes through the C ABI (rh_commit_soa_launch; the resident table is in
+test_gpu_table.py).  The oracle is
 oracle/ratis_oracle.c (orc_commit_soa), itself pinned in tests/test_oracle.py."""
 import json
 import os
@@ -263,126 +264,6 @@ def test_full_size_config4_sharded(ctx, orc):
     torch.cuda.synchronize()
     for ti, t in enumerate(tiers):
         assert np.array_equal(t.commit_out.cpu().numpy(), whole[ti])
-
-
-def test_group_table_api_with_deltas(ctx, orc):
-    """RaftGroupTable (rh_groups_*): bulk load, delta streaming (updateToMax), batched
-    updateCommit and commitIndexChanged, against the oracle replaying the same host state."""
-    from ratis_amd import groups, workload
-    rng = np.random.default_rng(21)
-    h = workload.stable_tier(10_000, seed=5, peers=5)
-    F, n = h.follower.shape
-    tab = groups.RaftGroupTable(ctx, capacity=n, n_followers=F, gap_threshold=-1)
-    try:
-        fcommit = h.follower - rng.integers(0, 100, size=h.follower.shape)
-        tab.load(0, n, match=h.follower, fcommit=fcommit, flush=h.flush, commit=h.commit, term_start=h.term_start,
-                 conf=h.conf)
-        match = h.follower.copy()
-        flush = h.flush.copy()
-        commit = h.commit.copy()
-        for rnd in range(3):
-            # followers ack: some go forward, some stale (updateToMax keeps the max)
-            k = 5000
-            slots = rng.integers(0, n, size=k)
-            col = rng.integers(0, F, size=k)
-            val = match[col, slots] + rng.integers(-50, 3000, size=k)
-            tab.push_deltas(slots, col, val)
-            np.maximum.at(match, (col, slots), val)
-            fs = rng.integers(0, n, size=1000)
-            fv = flush[fs] + rng.integers(0, 500, size=1000)
-            tab.update_flush_index(fs, fv)
-            np.maximum.at(flush, fs, fv)
-            got_slots, got_commit, got_min = tab.update_commit(want_min=True)
-            ref = orc.commit_soa(match, flush, h.conf, mode=0, gap=-1, commit_in=commit, term_start=h.term_start)
-            adv = np.nonzero(_bits(ref["advanced_bits"], n))[0]
-            assert np.array_equal(got_slots.astype(np.int64), adv)
-            assert np.array_equal(got_commit, ref["commit"][adv])
-            assert np.array_equal(got_min, ref["min"])
-            commit = ref["commit"]
-            assert np.array_equal(tab.read_commit(), commit)
-        mn, mj, mx, valid = tab.commit_index_changed()
-        ref = orc.commit_soa(fcommit, commit, h.conf, mode=1)
-        assert np.array_equal(valid, _bits(ref["valid_bits"], n))
-        assert np.array_equal(mn, ref["min"]) and np.array_equal(mj, ref["maj"]) and np.array_equal(mx, ref["max"])
-    finally:
-        tab.close()
-
-
-def test_group_table_zero_copy_delta_ring(ctx, orc):
-    """rh_deltas_acquire/submit: deltas written in place into the pinned staging slots, two slots
-    in flight, interleaved with rh_push_deltas (including a batch larger than one slot); deltas
-    with a bad slot or column are ignored by the device; acquire/submit misuse is RH_E_STATE."""
-    from ratis_amd import _lib, groups, workload
-    rng = np.random.default_rng(33)
-    h = workload.stable_tier(50_000, seed=6, peers=5)
-    F, n = h.follower.shape
-    tab = groups.RaftGroupTable(ctx, capacity=n, n_followers=F)
-    try:
-        tab.load(0, n, match=h.follower, flush=h.flush, commit=h.commit, term_start=h.term_start, conf=h.conf)
-        match, flush, commit = h.follower.copy(), h.flush.copy(), h.commit.copy()
-        for rnd in range(4):
-            for _ in range(3):   # three submits per round: both slots cycle while in flight
-                k = int(rng.integers(1, 40_000))
-                slots = rng.integers(0, n, size=k)
-                col = rng.integers(0, F, size=k)
-                val = match[col, slots] + rng.integers(-50, 3000, size=k)
-                ring = tab.acquire_deltas()
-                assert ring.size == 1 << 20
-                ring["slot"][:k] = slots
-                ring["column"][:k] = col
-                ring["value"][:k] = val
-                ring["slot"][k] = n + 5          # ignored: slot out of range
-                ring["column"][k + 1] = 99       # ignored: unknown column
-                ring["slot"][k + 1] = 0
-                ring["value"][k:k + 2] = 1 << 60
-                tab.submit_deltas(k + 2)
-                np.maximum.at(match, (col, slots), val)
-            if rnd == 2:  # a push larger than one staging slot (chunked through both slots)
-                k = (1 << 20) + 12345
-                slots = rng.integers(0, n, size=k)
-                col = rng.integers(0, F, size=k)
-                val = match[col, slots] + rng.integers(-10, 100, size=k)
-                tab.push_deltas(slots, col, val)
-                np.maximum.at(match, (col, slots), val)
-            fs = rng.integers(0, n, size=2000)
-            fv = flush[fs] + rng.integers(0, 500, size=2000)
-            tab.update_flush_index(fs, fv)
-            np.maximum.at(flush, fs, fv)
-            got_slots, got_commit, _ = tab.update_commit()
-            ref = orc.commit_soa(match, flush, h.conf, mode=0, gap=-1, commit_in=commit, term_start=h.term_start)
-            adv = np.nonzero(_bits(ref["advanced_bits"], n))[0]
-            assert np.array_equal(got_slots.astype(np.int64), adv)
-            assert np.array_equal(got_commit, ref["commit"][adv])
-            commit = ref["commit"]
-        tab.acquire_deltas()
-        with pytest.raises(_lib.RatisHipError):
-            tab.acquire_deltas()              # one slot at a time
-        with pytest.raises(_lib.RatisHipError):
-            tab.push_deltas([1], [0], [1])    # push while a slot is acquired
-        tab.submit_deltas(0)
-        with pytest.raises(_lib.RatisHipError):
-            tab.submit_deltas(1)              # nothing acquired
-    finally:
-        tab.close()
-
-
-def test_group_table_rejects_bad_input(ctx):
-    from ratis_amd import _lib, groups
-    tab = groups.RaftGroupTable(ctx, capacity=100, n_followers=2)
-    try:
-        with pytest.raises(_lib.IllegalArgumentError):
-            tab.set_group(5, _lib.conf_pack(0b100, True, False, 0, False), 1, 1, 1)   # slot 2 >= F
-        with pytest.raises(_lib.IllegalArgumentError):
-            tab.push_deltas([100], [0], [1])                                        # slot out of range
-        with pytest.raises(_lib.IllegalArgumentError):
-            tab.push_deltas([1], [7], [1])                                          # column >= F
-        tab.set_group(5, _lib.conf_pack(0b11, True, False, 0, False), 10, 2, 0)
-        tab.update_match_index([5], 0, [9])
-        tab.update_match_index([5], 1, [8])
-        slots, commits, _ = tab.update_commit()
-        assert list(slots) == [5] and list(commits) == [9]   # sorted [8,9,10] -> majority 9
-    finally:
-        tab.close()
 
 
 @pytest.mark.parametrize("F", [1, 2, 4, 6, 7, 13])

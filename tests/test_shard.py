@@ -100,3 +100,16 @@ def test_two_rank_gloo_shard_and_stats_allreduce():
     for s in (s0, s1):                            # every rank sees the node-wide sums
         assert s["groups_evaluated"] == 40_000
         assert s["commits_advanced"] == a0 + a1
+
+
+def test_library_shard_of_matches_java_floor_mod():
+    """rh_shard_of (the C ABI's RaftGroupId placement, used by rh_node routing) equals
+    Math.floorMod(UUID.hashCode(), n) for every n = 1..8 -- a pure host function, no GPU."""
+    from ratis_amd import groups
+    msb, lsb = shard.random_group_ids(3000, seed=17)
+    for n in range(1, 9):
+        want = shard.shard_of(msb, lsb, n)
+        got = np.array([groups.shard_of(int(a), int(b), n) for a, b in zip(msb, lsb)])
+        assert np.array_equal(got, want), n
+    with pytest.raises(Exception):
+        groups.shard_of(1, 2, 0)
