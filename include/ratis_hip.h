@@ -376,6 +376,14 @@ typedef struct rh_lease_soa {
 
 int rh_lease_soa_launch(rh_ctx* ctx, const rh_lease_soa* tiers, int n_tiers, void* stream);
 
+/* The leader's per-heartbeat bookkeeping in ONE launch: updateCommit over the commit tiers and
+ * hasLease over the lease tiers (typically the same divisions, sharing their conf words).  Same
+ * results as rh_commit_soa_launch + rh_lease_soa_launch; commit tiers with F <= 6 and lease tiers
+ * with F <= 7 share one kernel (one launch ramp and tail instead of two), wider tiers of either
+ * kind run in their own launches on the same stream. */
+int rh_leader_soa_launch(rh_ctx* ctx, const rh_commit_soa* commit, int n_commit, const rh_lease_soa* lease,
+                         int n_lease, void* stream);
+
 /* ---- segment framing (SegmentedRaftLogReader.verifyHeader / decodeEntry / verifyTerminator) --
  * Walks each segment image: header "RaftLog1" (RDR:179-205), then frames varint32(n) || n bytes ||
  * 4-byte CRC while the first byte is non-zero (RDR:291-323), then checks that the terminator

@@ -116,6 +116,34 @@ def crc32c_frames(buf: np.ndarray, off: np.ndarray, frame_len: np.ndarray) -> Tu
     return out, int(bad)
 
 
+def crc32c_frames_all(buf: np.ndarray, off: np.ndarray, frame_len: np.ndarray, threads: int = 16):
+    """Every frame's PureJavaCrc32C over [off, off + len - 4) and whether it differs from the stored
+    big-endian trailer (SegmentedRaftLogReader.decodeEntry, RDR:327-336), on `threads` host threads
+    (ctypes releases the GIL; static slices).  Returns (crc uint32 [n], bad bool [n]).  The full
+    config-5 parity check: every frame of the 8 GiB image, independent of how it was stamped."""
+    import threading
+    buf = np.ascontiguousarray(buf, dtype=np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    ln = np.ascontiguousarray(frame_len, dtype=np.uint32)
+    n = off.size
+    crc = np.zeros(n, dtype=np.uint32)
+    L = load()
+    cuts = np.linspace(0, n, threads + 1).astype(np.int64)
+
+    def run(a, b):
+        if b > a:
+            L.orc_crc32c_frames(_p(buf), _p(off[a:b]), _p(ln[a:b]), b - a, _p(crc[a:b]))
+    th = [threading.Thread(target=run, args=(int(a), int(b))) for a, b in zip(cuts[:-1], cuts[1:])]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    end = (off + ln.astype(np.uint64)).astype(np.int64)
+    stored = ((buf[end - 4].astype(np.uint32) << 24) | (buf[end - 3].astype(np.uint32) << 16)
+              | (buf[end - 2].astype(np.uint32) << 8) | buf[end - 1].astype(np.uint32))
+    return crc, crc != stored
+
+
 def crc32c_py(data: bytes, state: int = 0xFFFFFFFF) -> int:
     """Bit-at-a-time CRC-32C (reflected 0x82F63B78), a third, table-free restatement."""
     c = state

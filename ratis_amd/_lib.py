@@ -226,6 +226,7 @@ _SIGNATURES = {
     "rh_crc32c_verify_host": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_uint64, c_void_p,
                                       c_void_p, POINTER(c_uint64)]),
     "rh_lease_soa_launch": (c_int, [c_void_p, POINTER(RhLeaseSoa), c_int, c_void_p]),
+    "rh_leader_soa_launch": (c_int, [c_void_p, POINTER(RhCommitSoa), c_int, POINTER(RhLeaseSoa), c_int, c_void_p]),
     "rh_segments_scan_launch": (c_int, [c_void_p, POINTER(RhSegments), c_void_p]),
     "rh_segments_read_launch": (c_int, [c_void_p, POINTER(RhSegments), POINTER(RhSegmentsCrc), c_void_p]),
 }

@@ -16,6 +16,7 @@
 // contraction).  The kernel is HBM-bound: 8(F+1)+20 bytes read and 16 bytes written per group.
 #include "rh_internal.h"
 #include "commit_eval.h"
+#include "lease_eval.h"
 
 namespace {
 
@@ -236,7 +237,8 @@ __device__ __forceinline__ int tier_of_block(const LaunchArgs& args, uint32_t b)
 // One launch covers every tier of the class; blocks are assigned to tiers in order and the F
 // switch is block-uniform, so it costs no divergence.
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void commit_kernel_rank(
-    const LaunchArgs args) {
+    const LaunchArgs a) {
+    const LaunchArgs& args = rh::kernarg_struct<LaunchArgs>();  // scalar loads, no scratch copy
     const int ti = tier_of_block(args, blockIdx.x);
     const TierArgs& ta = args.tier[ti];
     dispatch_f<1, 6, true, true, true>(ta, (uint64_t)(blockIdx.x - ta.block_begin));
@@ -244,7 +246,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
 
 // Tiers with F = 7..14 (8..15 voters): a Batcher network per conf (rank masks of 8+ values do
 // not stay in registers).
-__global__ __launch_bounds__(kBlock) void commit_kernel_net(const LaunchArgs args) {
+__global__ __launch_bounds__(kBlock) void commit_kernel_net(const LaunchArgs a) {
+    const LaunchArgs& args = rh::kernarg_struct<LaunchArgs>();
     const int ti = tier_of_block(args, blockIdx.x);
     const TierArgs& ta = args.tier[ti];
     dispatch_f<7, 14, false, false, false>(ta, (uint64_t)(blockIdx.x - ta.block_begin));
@@ -252,11 +255,11 @@ __global__ __launch_bounds__(kBlock) void commit_kernel_net(const LaunchArgs arg
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
-// One launch over the tiers whose F lies in [flo, fhi].
-int launch_class(const rh_commit_soa* tiers, int n_tiers, int flo, int fhi, hipStream_t stream) {
+// Kernel arguments for the tiers whose F lies in [flo, fhi].
+void build_args(const rh_commit_soa* tiers, int n_tiers, int flo, int fhi, LaunchArgs& args, uint64_t& blocks) {
     constexpr uint64_t kTile = (uint64_t)kBlock * kGroupsPerLane;  // groups per workgroup
-    LaunchArgs args{};
-    uint64_t blocks = 0;
+    args = LaunchArgs{};
+    blocks = 0;
     for (int i = 0; i < n_tiers; ++i) {
         const rh_commit_soa& t = tiers[i];
         if ((int)t.n_followers < flo || (int)t.n_followers > fhi || t.n == 0) continue;
@@ -273,6 +276,13 @@ int launch_class(const rh_commit_soa* tiers, int n_tiers, int flo, int fhi, hipS
                     (!t.max_out || aligned16(t.max_out));
         blocks += ta.n_blocks;
     }
+}
+
+// One launch over the tiers whose F lies in [flo, fhi].
+int launch_class(const rh_commit_soa* tiers, int n_tiers, int flo, int fhi, hipStream_t stream) {
+    LaunchArgs args;
+    uint64_t blocks = 0;
+    build_args(tiers, n_tiers, flo, fhi, args, blocks);
     if (args.n_tiers == 0) return RH_OK;
     if (blocks > 0x7FFFFFFFull) return rh::fail(RH_E_RANGE, "commit launch: too many groups");
     const dim3 g((uint32_t)blocks), b(kBlock);
@@ -284,10 +294,30 @@ int launch_class(const rh_commit_soa* tiers, int n_tiers, int flo, int fhi, hipS
     return RH_OK;
 }
 
-}  // namespace
+// ---- fused commit + lease launch (rh_leader_soa_launch) -------------------------------------------
+// The leader's per-heartbeat bookkeeping of every division in ONE launch: blocks [0, commit_blocks)
+// run updateCommit over the commit tiers (as commit_kernel_rank), the rest hasLease over the lease
+// tiers (as lease_kernel<0, 7>).  One launch ramp and tail instead of two; both halves fit the
+// same 64-VGPR / 8-waves-per-SIMD budget.
+struct LeaderArgs {
+    LaunchArgs commit;
+    rh_lease::LeaseLaunch lease;
+    uint32_t commit_blocks;
+};
 
-int rh_commit_launch_impl(rh_ctx* ctx, const rh_commit_soa* tiers, int n_tiers, hipStream_t stream) {
-    (void)ctx;
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void leader_kernel(const LeaderArgs arg) {
+    const LeaderArgs& a = rh::kernarg_struct<LeaderArgs>();
+    const uint32_t b = blockIdx.x;
+    if (b < a.commit_blocks) {
+        const int ti = tier_of_block(a.commit, b);
+        const TierArgs& ta = a.commit.tier[ti];
+        dispatch_f<1, 6, true, true, true>(ta, (uint64_t)(b - ta.block_begin));
+    } else {
+        rh_lease::lease_block(a.lease, (uint64_t)(b - a.commit_blocks));
+    }
+}
+
+int validate(const rh_commit_soa* tiers, int n_tiers) {
     if (!tiers || n_tiers < 1 || n_tiers > RH_MAX_TIERS)
         return rh::fail(RH_E_INVAL, "rh_commit_soa_launch: n_tiers must be in [1, RH_MAX_TIERS]");
     for (int i = 0; i < n_tiers; ++i) {
@@ -308,6 +338,35 @@ int rh_commit_launch_impl(rh_ctx* ctx, const rh_commit_soa* tiers, int n_tiers, 
         if (t.adv_rows && (!t.adv_commit || !t.adv_count))
             return rh::fail(RH_E_INVAL, "rh_commit_soa_launch: adv_rows needs adv_commit and adv_count");
     }
-    const int rc = launch_class(tiers, n_tiers, 1, 6, stream);
+    return RH_OK;
+}
+
+}  // namespace
+
+int rh_commit_launch_impl(rh_ctx* ctx, const rh_commit_soa* tiers, int n_tiers, hipStream_t stream) {
+    (void)ctx;
+    int rc = validate(tiers, n_tiers);
+    if (rc == RH_OK) rc = launch_class(tiers, n_tiers, 1, 6, stream);
     return rc != RH_OK ? rc : launch_class(tiers, n_tiers, 7, 14, stream);
+}
+
+int rh_leader_launch_impl(rh_ctx* ctx, const rh_commit_soa* commit, int n_commit, const rh_lease_soa* lease,
+                          int n_lease, hipStream_t stream) {
+    (void)ctx;
+    int rc = validate(commit, n_commit);
+    if (rc == RH_OK) rc = rh_lease_validate(lease, n_lease);
+    if (rc != RH_OK) return rc;
+    LeaderArgs a;
+    uint64_t cb = 0, lb = 0;
+    build_args(commit, n_commit, 1, 6, a.commit, cb);
+    rh_lease::build_lease_args(lease, n_lease, 0, 7, a.lease, lb);
+    if (cb + lb > 0x7FFFFFFFull) return rh::fail(RH_E_RANGE, "rh_leader_soa_launch: too many groups");
+    a.commit_blocks = (uint32_t)cb;
+    if (cb + lb) {
+        hipLaunchKernelGGL(leader_kernel, dim3((uint32_t)(cb + lb)), dim3(kBlock), 0, stream, a);
+        RH_HIP(hipGetLastError());
+    }
+    // tiers outside the fused kernel's classes: their own launches (same stream, same results)
+    rc = launch_class(commit, n_commit, 7, 14, stream);
+    return rc != RH_OK ? rc : rh_lease_launch_class(lease, n_lease, 8, 14, stream);
 }

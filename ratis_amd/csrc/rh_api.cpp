@@ -137,6 +137,13 @@ RH_EXPORT int rh_lease_soa_launch(rh_ctx* ctx, const rh_lease_soa* tiers, int n_
     return rh_lease_launch_impl(ctx, tiers, n_tiers, pick_stream(ctx, stream));
 }
 
+RH_EXPORT int rh_leader_soa_launch(rh_ctx* ctx, const rh_commit_soa* commit, int n_commit, const rh_lease_soa* lease,
+                                   int n_lease, void* stream) {
+    if (!ctx) return rh::fail(RH_E_INVAL, "rh_leader_soa_launch: ctx == NULL");
+    DeviceGuard g(ctx->device);
+    return rh_leader_launch_impl(ctx, commit, n_commit, lease, n_lease, pick_stream(ctx, stream));
+}
+
 // ---- segment framing -------------------------------------------------------------------------
 RH_EXPORT int rh_segments_scan_launch(rh_ctx* ctx, const rh_segments* segs, void* stream) {
     if (!ctx) return rh::fail(RH_E_INVAL, "rh_segments_scan_launch: ctx == NULL");

@@ -34,6 +34,16 @@ void build_crc_slice_tables(CrcTables* t);
 void build_crc_shift_table(uint64_t nbytes, uint32_t out[4][256]);
 std::vector<uint32_t> build_crc_lane_tables(int Q, int S);
 
+// The kernel's by-value argument struct, addressed in the kernarg segment (address space 4).
+// Indexing a tier array of the argument with a block-dependent index through this pointer gives
+// scalar loads from the kernarg segment; indexing the by-value parameter directly can make the
+// compiler copy the whole struct into scratch first (seen at 440-1240 bytes per lane).  Valid
+// for kernels whose only explicit argument is that struct (it then starts the segment).
+template <typename T>
+__device__ __forceinline__ const T& kernarg_struct() {
+    return *(const T*)(__builtin_amdgcn_kernarg_segment_ptr());
+}
+
 // ---- resident table (rh_groups) device layout --------------------------------------------------
 // Tier t holds slots whose conf names follower slots < width = 2 (t + 1); every column is a
 // contiguous array over the tier's rows (row space), so the commit kernels see a tier exactly as
@@ -126,3 +136,7 @@ int rh_segments_launch_impl(rh_ctx* ctx, const rh_segments* segs, hipStream_t st
 int rh_segments_read_impl(rh_ctx* ctx, const rh_segments* segs, const rh_segments_crc* crc, hipStream_t stream);
 int rh_crc_verify_slots(rh_ctx* ctx, const rh_segments* segs, const rh_segments_crc* crc, hipStream_t stream);
 int rh_lease_launch_impl(rh_ctx* ctx, const rh_lease_soa* tiers, int n_tiers, hipStream_t stream);
+int rh_lease_validate(const rh_lease_soa* tiers, int n_tiers);
+int rh_lease_launch_class(const rh_lease_soa* tiers, int n_tiers, int flo, int fhi, hipStream_t stream);
+int rh_leader_launch_impl(rh_ctx* ctx, const rh_commit_soa* commit, int n_commit, const rh_lease_soa* lease,
+                          int n_lease, hipStream_t stream);

@@ -487,3 +487,14 @@ def lease_launch(ctx: Context, tiers: Sequence[LeaseTier], now_nanos: int, timeo
     """Enqueues the lease kernel for every tier (asynchronous)."""
     arr = (RhLeaseSoa * len(tiers))(*[t.to_struct(now_nanos, timeout_ms) for t in tiers])
     check(_lib.load().rh_lease_soa_launch(ctx.handle, arr, len(tiers), _stream_ptr(stream)))
+
+
+def leader_launch(ctx: Context, commit_tiers: Sequence[CommitTier], lease_tiers: Sequence[LeaseTier], now_nanos: int,
+                  timeout_ms: int, stream: Optional[torch.cuda.Stream] = None) -> None:
+    """One fused launch: updateCommit over ``commit_tiers`` (COMMIT mode) and hasLease over
+    ``lease_tiers`` (rh_leader_soa_launch; asynchronous)."""
+    if not 1 <= len(commit_tiers) <= _lib.RH_MAX_TIERS or not 1 <= len(lease_tiers) <= _lib.RH_MAX_TIERS:
+        raise ValueError("1..4 tiers of each kind per launch")
+    c = (RhCommitSoa * len(commit_tiers))(*[t.to_struct(RH_MODE_COMMIT) for t in commit_tiers])
+    ls = (RhLeaseSoa * len(lease_tiers))(*[t.to_struct(now_nanos, timeout_ms) for t in lease_tiers])
+    check(_lib.load().rh_leader_soa_launch(ctx.handle, c, len(commit_tiers), ls, len(lease_tiers), _stream_ptr(stream)))

@@ -154,3 +154,35 @@ def test_lease_malformed_conf_words(ctx, orc, F):
     bad = which > 0
     has = np.unpackbits(got[1].view(np.uint8), bitorder="little")[:n].astype(bool)
     assert not has[bad].any() and np.array_equal(got[0][bad], lease_in[bad])
+
+
+def test_leader_fused_launch_equals_separate(ctx, orc):
+    """rh_leader_soa_launch (updateCommit + hasLease of the same divisions in one kernel, wider
+    tiers in their own launches) gives exactly the oracle's commit and lease results."""
+    import torch
+
+    from ratis_amd import engine, workload
+    rng = np.random.default_rng(31)
+    tiers_h = workload.commit_snapshot(150_000, joint_frac=0.1, peers=5, seed=41)
+    tiers_h.append(workload.stable_tier(5_000, seed=42, peers=10))   # F = 9: outside the fused classes
+    ctiers = [workload.to_device(h, gap_threshold=2048).alloc_outputs(mode=0) for h in tiers_h]
+    lease_in = []
+    ltiers = []
+    for h in tiers_h:
+        ts = NOW - rng.integers(-5 * MS, 300 * MS, size=h.follower.shape, dtype=np.int64)
+        lin = NOW - rng.integers(0, 200 * MS, h.n, dtype=np.int64)
+        lease_in.append((ts, h.conf, lin))
+        ltiers.append(engine.LeaseTier(follower_ts=torch.from_numpy(ts).cuda(),
+                                       conf=torch.from_numpy(h.conf.view(np.int32)).cuda(),
+                                       lease_in=torch.from_numpy(lin).cuda()).alloc_outputs())
+    engine.leader_launch(ctx, ctiers, ltiers, NOW, 100)
+    torch.cuda.synchronize()
+    for h, t in zip(tiers_h, ctiers):
+        ref = orc.commit_soa(h.follower, h.flush, h.conf, mode=0, gap=2048, commit_in=h.commit, term_start=h.term_start)
+        assert np.array_equal(t.commit_out.cpu().numpy(), ref["commit"])
+        assert np.array_equal(t.min_out.cpu().numpy(), ref["min"])
+    for (ts, conf, lin), t in zip(lease_in, ltiers):
+        nw = (t.n + 63) // 64
+        got = (t.lease_out.cpu().numpy(), t.has_lease_bits[:nw].cpu().numpy().view(np.uint64),
+               t.extended_bits[:nw].cpu().numpy().view(np.uint64))
+        assert_same(orc.lease_soa(ts, conf, lin, NOW, 100), got)
