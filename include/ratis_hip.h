@@ -203,8 +203,9 @@ typedef struct rh_watch_event {
     int64_t  max;       /* MAJORITY           */
 } rh_watch_event;
 
-/* Results of one rh_commit_batch: library-owned pinned host memory, valid until the second
- * rh_commit_batch_async after the one that produced them (two result buffers alternate). */
+/* Results of one rh_commit_batch: library-owned pinned host memory, valid until the third
+ * rh_commit_batch_async after the one that produced them (three result buffers rotate, so a
+ * producer can keep two evaluations in flight while it reads the third's events). */
 typedef struct rh_commit_out {
     const rh_index_event* advanced;   /* slots whose commitIndex was stored, new value (LSI:1017-1021,
                                          RLB:121-142); the Java follow-up runs for these only    */
@@ -301,9 +302,9 @@ int rh_node_group_stop(rh_node* node, uint32_t node_slot);
 int rh_node_push_deltas(rh_node* node, const rh_delta* deltas, size_t n);
 /* updateCommit on every shard (all launched before any is awaited); the events of all shards,
  * with node slots, are gathered into the caller's arrays (up to the caps; the n_* counts are the
- * totals).  Blocks. */
-int rh_node_commit_batch(rh_node* node, rh_index_event* advanced, uint64_t adv_cap, uint64_t* n_advanced,
-                         rh_index_event* watch_all, uint64_t watch_cap, uint64_t* n_watch_all);
+ * totals).  flags as rh_commit_batch.  Blocks. */
+int rh_node_commit_batch(rh_node* node, uint32_t flags, rh_index_event* advanced, uint64_t adv_cap,
+                         uint64_t* n_advanced, rh_index_event* watch_all, uint64_t watch_cap, uint64_t* n_watch_all);
 
 /* ===================================================================================== */
 /* 2. CRC32C (PureJavaCrc32C) over SegmentedRaftLog frames                               */

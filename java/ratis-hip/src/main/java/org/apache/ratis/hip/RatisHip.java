@@ -1,0 +1,161 @@
+/*
+ * ratis-hip: JNI binding of libratis_hip (include/ratis_hip.h in the ratis_amd repository), the
+ * MI355X leader-bookkeeping engine.  One RatisHip per RaftServerProxy wraps an rh_node: one
+ * resident group table per GPU of the device mask, RaftGroups placed by
+ * floorMod(RaftGroupId.hashCode(), #GPUs) (RaftId.java:119-122).
+ *
+ * Java 8 compatible (the reference's CI baseline, .github/workflows/ci.yaml:51).  Not compiled in
+ * the ratis_amd repository (its image has no JDK); the native half is java/ratis-hip/src/main/
+ * native/ratis_hip_jni.c, which the repository's tests compile against the C ABI.
+ *
+ * Error mapping (ratis_hip.h): RH_E_INVAL / RH_E_RANGE -> IllegalArgumentException (as the
+ * reference throws for bad arguments, e.g. LeaderStateImpl.java:396-399), every other negative
+ * status -> IOException; a frame whose checksum does not verify -> ChecksumException at its offset
+ * (SegmentedRaftLogReader.java:330-336) in the callers.
+ */
+package org.apache.ratis.hip;
+
+import java.io.IOException;
+import java.nio.ByteBuffer;
+import java.nio.ByteOrder;
+
+public final class RatisHip implements AutoCloseable {
+  static {
+    System.loadLibrary("ratis_hip_jni");   // links libratis_hip.so
+  }
+
+  // ---- membership word (ratis_hip.h, RH_CONF_*) ---------------------------------------------
+  public static final int MAX_FOLLOWERS = 14;
+  public static final int CONF_SELF = 1 << 14;
+  public static final int CONF_TRANSITIONAL = 1 << 15;
+  public static final int CONF_OLD_SHIFT = 16;
+  public static final int CONF_SELF_OLD = 1 << 30;
+  public static final int CONF_ACTIVE = 1 << 31;
+
+  /** rh_conf_pack: bit k of newMask / oldMask = follower slot k is a voter of conf / oldConf. */
+  public static int confWord(int newMask, boolean includeSelf, boolean transitional, int oldMask,
+      boolean includeSelfOld, boolean active) {
+    return (newMask & 0x3FFF) | (includeSelf ? CONF_SELF : 0) | (transitional ? CONF_TRANSITIONAL : 0)
+        | ((oldMask & 0x3FFF) << CONF_OLD_SHIFT) | (includeSelfOld ? CONF_SELF_OLD : 0) | (active ? CONF_ACTIVE : 0);
+  }
+
+  // ---- deltas (rh_delta: u32 slot, u8 column, u8 op, u16 reserved, i64 value; 16 bytes) -----
+  public static final int DELTA_BYTES = 16;
+  public static int colMatch(int followerSlot) { return followerSlot; }
+  public static int colFollowerCommit(int followerSlot) { return 16 + followerSlot; }
+  public static final int COL_FLUSH = 32;
+  public static final int COL_COMMITTED = 33;
+  public static final int OP_MAX = 0;   // RaftLogIndex.updateToMax
+  public static final int OP_SET = 1;   // RaftLogIndex.setUnconditionally (setSnapshotIndex)
+  public static final int COMMIT_WATCH_ALL = 1;
+
+  /** Writes one delta at the buffer's position (little-endian) and advances it. */
+  public static void putDelta(ByteBuffer ring, int slotInShard, int column, int op, long value) {
+    ring.putInt(slotInShard).put((byte) column).put((byte) op).putShort((short) 0).putLong(value);
+  }
+
+  private long node;        // rh_node*
+  private final int shards;
+  private final long capacityPerShard;
+
+  public RatisHip(int deviceMask, long capacityPerShard, long gapThreshold) throws IOException {
+    this.node = nodeCreate0(deviceMask, capacityPerShard, gapThreshold);
+    this.shards = nodeShards0(node);
+    this.capacityPerShard = capacityPerShard;
+  }
+
+  public int getShards() { return shards; }
+  public long getCapacityPerShard() { return capacityPerShard; }
+
+  /** Math.floorMod(UUID.hashCode(), shards) computed by the library (rh_shard_of). */
+  public int shardOf(long uuidMsb, long uuidLsb) {
+    return shardOf0(uuidMsb, uuidLsb, shards);
+  }
+
+  // ---- division lifecycle (node slots = shard * capacityPerShard + slot in shard) ------------
+  /** New LeaderStateImpl: every FollowerInfo new (index -1); termStart = StartupLogEntry index. */
+  public void start(int nodeSlot, int conf, long flushIndex, long commitIndex, long termStart) throws IOException {
+    groupStart0(node, nodeSlot, conf, flushIndex, commitIndex, termStart);
+  }
+
+  /** Conf change: src[k] = old follower slot kept by new slot k, or -1 for a new FollowerInfo. */
+  public void reconf(int nodeSlot, int conf, byte[] src) throws IOException {
+    groupReconf0(node, nodeSlot, conf, src);
+  }
+
+  public void stop(int nodeSlot) throws IOException {
+    groupStop0(node, nodeSlot);
+  }
+
+  // ---- delta producers ---------------------------------------------------------------------
+  /** Validated push of n deltas packed in a direct buffer (node slots); returns when reusable. */
+  public void pushDeltas(ByteBuffer direct, int n) throws IOException {
+    pushDeltas0(node, direct, n);
+  }
+
+  /**
+   * Zero-copy path of one shard: the next pinned staging slot as a little-endian direct buffer
+   * (capacity RH_DELTA_SLOT deltas, slots relative to the shard) to fill with {@link #putDelta}.
+   * Hand it back with {@link #submitDeltas}; one acquire/submit pair at a time per shard.
+   */
+  public ByteBuffer acquireDeltas(int shard) throws IOException {
+    return acquire0(node, shard).order(ByteOrder.LITTLE_ENDIAN);
+  }
+
+  public void submitDeltas(int shard, int n) throws IOException {
+    submit0(node, shard, n);
+  }
+
+  // ---- consumers ---------------------------------------------------------------------------
+  /**
+   * Batched LeaderStateImpl.updateCommit() over every shard's dirty divisions.  Fills
+   * advSlot/advCommit with the node slots whose commit index advanced and the new value, and
+   * (with COMMIT_WATCH_ALL) wallSlot/wallMin with the changed watch-ALL levels.  Returns
+   * (long) nAdvanced << 32 | nWatchAll; counts beyond the arrays are truncated.
+   */
+  public long commitBatch(int[] advSlot, long[] advCommit, int[] wallSlot, long[] wallMin) throws IOException {
+    return commitBatch0(node, advSlot, advCommit, wallSlot, wallMin);
+  }
+
+  /** Batched commitIndexChanged() of one shard: changed {min, majority, max} levels. */
+  public int watchLevels(int shard, int[] slot, long[] min, long[] majority, long[] max, boolean[] valid)
+      throws IOException {
+    return watchLevels0(node, shard, slot, min, majority, max, valid);
+  }
+
+  // ---- checksums (SegmentedRaftLogReader.decodeEntry, batched over a segment) ---------------
+  /**
+   * PCIe-inclusive verification of one segment image held in a direct buffer: every frame's
+   * PureJavaCrc32C (crcOut) and the mismatch bitmap (badBits); returns the number of mismatches.
+   */
+  public long verifyFrames(int shard, ByteBuffer segment, long[] frameOff, int[] frameLen, int[] crcOut,
+      long[] badBits) throws IOException {
+    return verifyHost0(node, shard, segment, segment.remaining(), frameOff, frameLen, frameOff.length, crcOut, badBits);
+  }
+
+  @Override
+  public void close() throws IOException {
+    if (node != 0) {
+      nodeDestroy0(node);
+      node = 0;
+    }
+  }
+
+  private static native long nodeCreate0(int deviceMask, long capacityPerShard, long gap) throws IOException;
+  private static native void nodeDestroy0(long node) throws IOException;
+  private static native int nodeShards0(long node);
+  private static native int shardOf0(long msb, long lsb, int shards);
+  private static native void groupStart0(long node, int slot, int conf, long flush, long commit, long termStart)
+      throws IOException;
+  private static native void groupReconf0(long node, int slot, int conf, byte[] src) throws IOException;
+  private static native void groupStop0(long node, int slot) throws IOException;
+  private static native void pushDeltas0(long node, ByteBuffer direct, int n) throws IOException;
+  private static native ByteBuffer acquire0(long node, int shard) throws IOException;
+  private static native void submit0(long node, int shard, int n) throws IOException;
+  private static native long commitBatch0(long node, int[] advSlot, long[] advCommit, int[] wallSlot, long[] wallMin)
+      throws IOException;
+  private static native int watchLevels0(long node, int shard, int[] slot, long[] min, long[] majority, long[] max,
+      boolean[] valid) throws IOException;
+  private static native long verifyHost0(long node, int shard, ByteBuffer seg, long len, long[] off, int[] flen,
+      int n, int[] crc, long[] bad) throws IOException;
+}

@@ -45,6 +45,8 @@ struct TierHost {
     std::vector<uint32_t> pending_free;   // released by queued ops: reusable after the next flush
 };
 
+constexpr int kEvSets = 3;  // results of the last three rh_commit_batch_async calls stay readable
+
 struct EvSet {
     rh_index_event* adv = nullptr;   // host-mapped pinned [cap]
     rh_index_event* wall = nullptr;
@@ -76,17 +78,20 @@ struct rh_groups {
     size_t ops_cap = 0;
     hipEvent_t ops_free = nullptr;
     bool ops_used = false;
-    // delta staging: two pinned host slots, one device buffer (stream order serialises them)
+    // delta staging: two pinned host slots, each with its own device buffer; the H2D copies run on
+    // a copy stream, so the copy of batch s+1 overlaps the apply / evaluation of batch s
     rh_delta* h_ring[2] = {nullptr, nullptr};
-    hipEvent_t ring_free[2] = {nullptr, nullptr};
+    rh_delta* d_ring[2] = {nullptr, nullptr};
+    hipEvent_t ring_free[2] = {nullptr, nullptr};   // H2D of the slot done (host slot reusable)
+    hipEvent_t ring_read[2] = {nullptr, nullptr};   // apply of the slot done (device slot reusable)
     bool ring_used[2] = {false, false};
     int ring_next = 0;
     int ring_acquired = -1;
-    rh_delta* d_deltas = nullptr;
+    hipStream_t copy_stream = nullptr;
     // events
-    EvSet ev[2];
+    EvSet ev[kEvSets];
     uint64_t next_ticket = 1;
-    unsigned long long* d_counts = nullptr;   // [2 commit sets][4], then [8] for rh_watch_levels
+    unsigned long long* d_counts = nullptr;   // [kEvSets][4], then one for rh_watch_levels
     rh_watch_event* watch = nullptr;          // host-mapped pinned [cap]
     rh_watch_event* d_watch = nullptr;
     int64_t* d_read = nullptr;
@@ -129,10 +134,13 @@ void free_groups(rh_groups* g) {
     (void)hipFree(g->d_ops);
     if (g->h_ops) (void)hipHostFree(g->h_ops);
     if (g->ops_free) (void)hipEventDestroy(g->ops_free);
-    (void)hipFree(g->d_deltas);
     for (int i = 0; i < 2; ++i) {
         if (g->h_ring[i]) (void)hipHostFree(g->h_ring[i]);
+        (void)hipFree(g->d_ring[i]);
         if (g->ring_free[i]) (void)hipEventDestroy(g->ring_free[i]);
+        if (g->ring_read[i]) (void)hipEventDestroy(g->ring_read[i]);
+    }
+    for (int i = 0; i < kEvSets; ++i) {
         if (g->ev[i].adv) (void)hipHostFree(g->ev[i].adv);
         if (g->ev[i].wall) (void)hipHostFree(g->ev[i].wall);
         if (g->ev[i].h_counts) (void)hipHostFree(g->ev[i].h_counts);
@@ -141,6 +149,7 @@ void free_groups(rh_groups* g) {
     (void)hipFree(g->d_counts);
     if (g->watch) (void)hipHostFree(g->watch);
     (void)hipFree(g->d_read);
+    if (g->copy_stream) (void)hipStreamDestroy(g->copy_stream);
 }
 
 // (Re)allocates tier t with `rows` rows, keeping the first `keep` rows' contents.  Blocks (the
@@ -298,20 +307,26 @@ int ring_wait(rh_groups* g, int i) {
     return RH_OK;
 }
 
-// H2D of the first n deltas of ring slot i, then the SET and MAX phases (stream-ordered).
+// H2D of the first n deltas of ring slot i on the copy stream (after the previous apply that read
+// device slot i), then the SET and MAX phases on the table stream (after that H2D).
 int ring_submit(rh_groups* g, int i, size_t n, bool has_set) {
-    hipStream_t s = g->ctx->stream;
+    hipStream_t s = g->ctx->stream, cs = g->copy_stream;
     int rc = flush_ops(g);
     if (rc != RH_OK) return rc;
-    RH_HIP(hipMemcpyAsync(g->d_deltas, g->h_ring[i], n * sizeof(rh_delta), hipMemcpyHostToDevice, s));
-    RH_HIP(hipEventRecord(g->ring_free[i], s));
+    if (g->ring_used[i]) RH_HIP(hipStreamWaitEvent(cs, g->ring_read[i], 0));
+    RH_HIP(hipMemcpyAsync(g->d_ring[i], g->h_ring[i], n * sizeof(rh_delta), hipMemcpyHostToDevice, cs));
+    RH_HIP(hipEventRecord(g->ring_free[i], cs));
+    RH_HIP(hipStreamWaitEvent(s, g->ring_free[i], 0));
     g->ring_used[i] = true;
     g->ring_next = i ^ 1;
     if (has_set) {
-        rc = rh_table_apply_deltas(g->dev, g->d_deltas, n, 0, s);
+        rc = rh_table_apply_deltas(g->dev, g->d_ring[i], n, 0, s);
         if (rc != RH_OK) return rc;
     }
-    return rh_table_apply_deltas(g->dev, g->d_deltas, n, 1, s);
+    rc = rh_table_apply_deltas(g->dev, g->d_ring[i], n, 1, s);
+    if (rc != RH_OK) return rc;
+    RH_HIP(hipEventRecord(g->ring_read[i], s));
+    return RH_OK;
 }
 
 int check_conf(uint32_t conf, const char* who) {
@@ -348,12 +363,19 @@ RH_EXPORT int rh_groups_create(rh_ctx* ctx, uint64_t capacity, int64_t gap_thres
     if (rc == RH_OK) rc = dalloc(&g->dev.slot_map, capacity);
     if (rc == RH_OK && hipMemsetAsync(g->dev.slot_map, 0xFF, capacity * 4, s) != hipSuccess)
         rc = rh::fail(RH_E_DEVICE, "rh_groups_create: init");
-    if (rc == RH_OK) rc = dalloc(&g->d_deltas, (size_t)RH_DELTA_SLOT);
+    if (rc == RH_OK && hipStreamCreateWithFlags(&g->copy_stream, hipStreamNonBlocking) != hipSuccess)
+        rc = rh::fail(RH_E_DEVICE, "rh_groups_create: copy stream");
     for (int i = 0; i < 2 && rc == RH_OK; ++i) {
+        rc = dalloc(&g->d_ring[i], (size_t)RH_DELTA_SLOT);
+        if (rc == RH_OK && hipEventCreateWithFlags(&g->ring_read[i], hipEventDisableTiming) != hipSuccess)
+            rc = rh::fail(RH_E_DEVICE, "hipEventCreate(delta staging)");
+        if (rc != RH_OK) break;
         if (hipHostMalloc(reinterpret_cast<void**>(&g->h_ring[i]), (size_t)RH_DELTA_SLOT * sizeof(rh_delta)) != hipSuccess)
             rc = rh::fail(RH_E_NOMEM, "hipHostMalloc(delta staging)");
         if (rc == RH_OK && hipEventCreateWithFlags(&g->ring_free[i], hipEventDisableTiming) != hipSuccess)
             rc = rh::fail(RH_E_DEVICE, "hipEventCreate(delta staging)");
+    }
+    for (int i = 0; i < kEvSets && rc == RH_OK; ++i) {
         if (rc == RH_OK) rc = halloc_mapped(&g->ev[i].adv, &g->ev[i].d_adv, capacity);
         if (rc == RH_OK) rc = halloc_mapped(&g->ev[i].wall, &g->ev[i].d_wall, capacity);
         if (rc == RH_OK && hipHostMalloc(reinterpret_cast<void**>(&g->ev[i].h_counts), 4 * sizeof(unsigned long long)) != hipSuccess)
@@ -362,7 +384,7 @@ RH_EXPORT int rh_groups_create(rh_ctx* ctx, uint64_t capacity, int64_t gap_thres
             rc = rh::fail(RH_E_DEVICE, "hipEventCreate(commit batch)");
     }
     if (rc == RH_OK) rc = halloc_mapped(&g->watch, &g->d_watch, capacity);
-    if (rc == RH_OK) rc = dalloc(&g->d_counts, 9);
+    if (rc == RH_OK) rc = dalloc(&g->d_counts, 4 * kEvSets + 1);
     if (rc == RH_OK && hipEventCreateWithFlags(&g->ops_free, hipEventDisableTiming) != hipSuccess)
         rc = rh::fail(RH_E_DEVICE, "hipEventCreate(control ops)");
     if (rc == RH_OK && hipStreamSynchronize(s) != hipSuccess) rc = rh::fail(RH_E_DEVICE, "rh_groups_create: sync");
@@ -379,6 +401,7 @@ RH_EXPORT int rh_groups_destroy(rh_groups* g) {
     if (!g) return rh::fail(RH_E_INVAL, "rh_groups_destroy: NULL");
     DeviceGuard dg(g->ctx->device);
     (void)hipStreamSynchronize(g->ctx->stream);
+    if (g->copy_stream) (void)hipStreamSynchronize(g->copy_stream);
     free_groups(g);
     delete g;
     return RH_OK;
@@ -663,12 +686,12 @@ RH_EXPORT int rh_commit_batch_async(rh_groups* g, uint32_t flags, uint64_t* tick
     DeviceGuard dg(g->ctx->device);
     std::lock_guard<std::mutex> lk(g->mu);
     const uint64_t tk = g->next_ticket++;
-    EvSet& e = g->ev[tk & 1];
+    EvSet& e = g->ev[tk % kEvSets];
     if (e.pending) RH_HIP(hipEventSynchronize(e.done));  // its buffers are about to be rewritten
     hipStream_t s = g->ctx->stream;
     int rc = flush_ops(g);
     if (rc != RH_OK) return rc;
-    unsigned long long* dc = g->d_counts + (tk & 1) * 4;
+    unsigned long long* dc = g->d_counts + (tk % kEvSets) * 4;
     RH_HIP(hipMemsetAsync(dc, 0, 4 * sizeof(unsigned long long), s));
     rh::TableEvents ev;
     ev.adv = e.d_adv;
@@ -691,7 +714,7 @@ RH_EXPORT int rh_commit_batch_wait(rh_groups* g, uint64_t ticket, rh_commit_out*
     EvSet* e;
     {
         std::lock_guard<std::mutex> lk(g->mu);
-        e = &g->ev[ticket & 1];
+        e = &g->ev[ticket % kEvSets];
         if (e->ticket != ticket) return rh::fail(RH_E_STATE, "rh_commit_batch_wait: ticket unknown or superseded");
     }
     RH_HIP(hipEventSynchronize(e->done));
@@ -719,7 +742,7 @@ RH_EXPORT int rh_watch_levels(rh_groups* g, const rh_watch_event** out_events, u
     hipStream_t s = g->ctx->stream;
     int rc = flush_ops(g);
     if (rc != RH_OK) return rc;
-    unsigned long long* dc = g->d_counts + 8 - 2;  // the WATCH kernel counts into dc[2] = d_counts[8]
+    unsigned long long* dc = g->d_counts + 4 * kEvSets - 2;  // the WATCH kernel counts into dc[2]
     RH_HIP(hipMemsetAsync(dc + 2, 0, sizeof(unsigned long long), s));
     rh::TableEvents ev;
     ev.watch = g->d_watch;
@@ -874,15 +897,16 @@ RH_EXPORT int rh_node_push_deltas(rh_node* nd, const rh_delta* deltas, size_t n)
     return RH_OK;
 }
 
-RH_EXPORT int rh_node_commit_batch(rh_node* nd, rh_index_event* advanced, uint64_t adv_cap, uint64_t* n_advanced,
-                                   rh_index_event* watch_all, uint64_t watch_cap, uint64_t* n_watch_all) {
+RH_EXPORT int rh_node_commit_batch(rh_node* nd, uint32_t flags, rh_index_event* advanced, uint64_t adv_cap,
+                                   uint64_t* n_advanced, rh_index_event* watch_all, uint64_t watch_cap,
+                                   uint64_t* n_watch_all) {
     if (!nd || !n_advanced || !n_watch_all) return rh::fail(RH_E_INVAL, "rh_node_commit_batch: NULL argument");
     if ((adv_cap && !advanced) || (watch_cap && !watch_all))
         return rh::fail(RH_E_INVAL, "rh_node_commit_batch: output arrays required");
     const size_t S = nd->tab.size();
     std::vector<uint64_t> tk(S);
     for (size_t sh = 0; sh < S; ++sh) {  // every shard's evaluation is in flight before any wait
-        int rc = rh_commit_batch_async(nd->tab[sh], RH_COMMIT_WATCH_ALL, &tk[sh]);
+        int rc = rh_commit_batch_async(nd->tab[sh], flags, &tk[sh]);
         if (rc != RH_OK) return rc;
     }
     uint64_t na = 0, nw = 0;

@@ -301,7 +301,8 @@ class RaftNode:
         adv = np.zeros(cap, dtype=INDEX_EVENT_DTYPE)
         wall = np.zeros(cap, dtype=INDEX_EVENT_DTYPE)
         na, nw = ctypes.c_uint64(), ctypes.c_uint64()
-        check(self._lib.rh_node_commit_batch(self._h, _p(adv), cap, ctypes.byref(na), _p(wall), cap, ctypes.byref(nw)))
+        check(self._lib.rh_node_commit_batch(self._h, _lib.RH_COMMIT_WATCH_ALL, _p(adv), cap, ctypes.byref(na),
+                                             _p(wall), cap, ctypes.byref(nw)))
         a = adv[: min(na.value, cap)]
         w = wall[: min(nw.value, cap)]
         return a[np.argsort(a["slot"], kind="stable")], w[np.argsort(w["slot"], kind="stable")]

@@ -1,0 +1,52 @@
+/*
+ * Test-only: the subset of the JNI function table that java/ratis-hip/src/main/native/
+ * ratis_hip_jni.c uses, declared with the JNI specification's C signatures so that
+ * tests/test_java_module.py can type-check that file (gcc -fsyntax-only) in an image without a
+ * JDK.  Never used to build the real JNI library, which takes the JDK's own jni.h.
+ */
+#ifndef RATIS_HIP_TEST_JNI_STUB_H
+#define RATIS_HIP_TEST_JNI_STUB_H
+#include <stdint.h>
+
+#define JNIEXPORT __attribute__((visibility("default")))
+#define JNICALL
+#define JNI_FALSE 0
+#define JNI_TRUE 1
+#define JNI_ABORT 2
+
+typedef int32_t jint;
+typedef int64_t jlong;
+typedef int8_t jbyte;
+typedef uint8_t jboolean;
+typedef jint jsize;
+
+typedef struct _jobject* jobject;
+typedef jobject jclass;
+typedef jobject jthrowable;
+typedef jobject jarray;
+typedef jarray jbyteArray;
+typedef jarray jintArray;
+typedef jarray jlongArray;
+typedef jarray jbooleanArray;
+
+struct JNINativeInterface_;
+typedef const struct JNINativeInterface_* JNIEnv;
+
+struct JNINativeInterface_ {
+    jclass (*FindClass)(JNIEnv*, const char*);
+    jint (*ThrowNew)(JNIEnv*, jclass, const char*);
+    jsize (*GetArrayLength)(JNIEnv*, jarray);
+    void (*GetByteArrayRegion)(JNIEnv*, jbyteArray, jsize, jsize, jbyte*);
+    void (*SetIntArrayRegion)(JNIEnv*, jintArray, jsize, jsize, const jint*);
+    void (*SetLongArrayRegion)(JNIEnv*, jlongArray, jsize, jsize, const jlong*);
+    void (*SetBooleanArrayRegion)(JNIEnv*, jbooleanArray, jsize, jsize, const jboolean*);
+    jint* (*GetIntArrayElements)(JNIEnv*, jintArray, jboolean*);
+    jlong* (*GetLongArrayElements)(JNIEnv*, jlongArray, jboolean*);
+    void (*ReleaseIntArrayElements)(JNIEnv*, jintArray, jint*, jint);
+    void (*ReleaseLongArrayElements)(JNIEnv*, jlongArray, jlong*, jint);
+    void* (*GetPrimitiveArrayCritical)(JNIEnv*, jarray, jboolean*);
+    void (*ReleasePrimitiveArrayCritical)(JNIEnv*, jarray, void*, jint);
+    jobject (*NewDirectByteBuffer)(JNIEnv*, void*, jlong);
+    void* (*GetDirectBufferAddress)(JNIEnv*, jobject);
+};
+#endif

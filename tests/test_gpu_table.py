@@ -261,7 +261,7 @@ def test_zero_copy_ring_pipelined_with_async_commit(ctx, orc):
         got = tab.commit_wait(prev[0])
         assert np.array_equal(got.advanced_slots, prev[1][0]) and np.array_equal(got.advanced_commit, prev[1][1])
         with pytest.raises(_lib.RatisHipError):
-            tab.commit_wait(prev[0] - 2)          # superseded ticket
+            tab.commit_wait(prev[0] - 3)          # superseded ticket
         tab.acquire_deltas()
         with pytest.raises(_lib.RatisHipError):
             tab.acquire_deltas()                  # one slot at a time
