@@ -93,6 +93,28 @@ RH_EXPORT int rh_init(int device, rh_ctx** out) {
     return RH_OK;
 }
 
+hipError_t rh::pool_alloc(rh_ctx* ctx, void** p, size_t bytes, hipStream_t stream) {
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        if (!ctx->pool) {
+            hipMemPoolProps props{};
+            props.allocType = hipMemAllocationTypePinned;
+            props.handleTypes = hipMemHandleTypeNone;
+            props.location.type = hipMemLocationTypeDevice;
+            props.location.id = ctx->device;
+            hipError_t e = hipMemPoolCreate(&ctx->pool, &props);
+            if (e != hipSuccess) {
+                ctx->pool = nullptr;
+                return e;
+            }
+            uint64_t keep = UINT64_MAX;  // never trim between calls
+            e = hipMemPoolSetAttribute(ctx->pool, hipMemPoolAttrReleaseThreshold, &keep);
+            if (e != hipSuccess) return e;
+        }
+    }
+    return hipMallocFromPoolAsync(p, bytes, ctx->pool, stream);
+}
+
 RH_EXPORT int rh_shutdown(rh_ctx* ctx) {
     if (!ctx) return rh::fail(RH_E_INVAL, "rh_shutdown: ctx == NULL");
     DeviceGuard g(ctx->device);
@@ -102,6 +124,7 @@ RH_EXPORT int rh_shutdown(rh_ctx* ctx) {
     (void)hipFree(ctx->d_lane16);
     (void)hipFree(ctx->d_scratch);
     if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
+    if (ctx->pool) (void)hipMemPoolDestroy(ctx->pool);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return RH_OK;

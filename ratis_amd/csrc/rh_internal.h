@@ -119,9 +119,16 @@ struct rh_ctx {
     size_t scratch_bytes = 0;
     void* h_pinned = nullptr;
     size_t pinned_bytes = 0;
+    hipMemPool_t pool = nullptr;  // stream-ordered scratch (rh::pool_alloc)
 };
 
 // Launchers implemented in the .hip files (device pointers, async on `stream`).
+namespace rh {
+// Stream-ordered device scratch from the context's memory pool (created on first use, keeps its
+// memory cached between calls): free with hipFreeAsync on the same stream.
+hipError_t pool_alloc(rh_ctx* ctx, void** p, size_t bytes, hipStream_t stream);
+}  // namespace rh
+
 int rh_commit_launch_impl(rh_ctx* ctx, const rh_commit_soa* tiers, int n_tiers, hipStream_t stream);
 // Resident table kernels (table.hip): delta apply (phase 0 = SET deltas, 1 = MAX deltas),
 // control ops, and updateCommit / commitIndexChanged over the dirty rows of every tier.

@@ -34,10 +34,18 @@ struct SegArgs {
     uint32_t* seg_nframes;
     int32_t* seg_status;
     uint64_t* seg_stop;
+    // piece-parallel framing hooks (framing of irregular logs, see "Piece-parallel framing" below)
+    uint32_t bail_min;            // > 0: defer a segment whose window walk is mostly scalar steps
+                                  // and that has at least bail_min bytes left (first pass)
+    uint32_t* seg_gmax;           // [n_seg] optional: largest frame length the walk saw
+    const uint64_t* resume_pos;   // non-NULL: resume pass -- only deferred segments are walked,
+    const uint32_t* resume_nfr;   // from resume_pos[s] with resume_nfr[s] frames already found
 };
 
 constexpr int kWalking = 0;
 constexpr int kTermPending = 100;
+constexpr int kDeferred = 101;  // internal: handed to the piece-parallel pass (never returned)
+constexpr int kBailScalar = 8;  // scalar-walked frames in one window that make a segment defer
 
 __device__ __forceinline__ int varint32_size(uint32_t v) {
     if ((v & (~0u << 7)) == 0) return 1;
@@ -139,7 +147,14 @@ __global__ __launch_bounds__(kBlock2) void segment_walk_kernel(SegArgs a) {
         const int64_t L = uniform64(range_bad ? 0 : (int64_t)slen);
         const uint8_t* seg = a.buf + base;
         const int64_t A = (base & ~(int64_t)15) - base;
-        if (t == 0) {  // verifyHeader (RDR:179-205)
+        if (a.resume_pos) {  // resume pass: deferred segments only, from where the pieces stopped
+            if (a.seg_status[s] != kDeferred) continue;  // block-uniform
+            if (t == 0) {
+                sh_status = kWalking;
+                sh_pos = (long long)a.resume_pos[s];
+                sh_nfr = a.resume_nfr[s];
+            }
+        } else if (t == 0) {  // verifyHeader (RDR:179-205)
             const char H[8] = {'R', 'a', 'f', 't', 'L', 'o', 'g', '1'};
             const int64_t rl = L < 8 ? L : 8;
             int match = 0, bad = 0;
@@ -160,6 +175,7 @@ __global__ __launch_bounds__(kBlock2) void segment_walk_kernel(SegArgs a) {
         Win<W> nxt;
         // wave 0's speculation state: the last two frame lengths (equal = a run worth speculating on)
         uint32_t last_fl = 0, prev_fl = 1;
+        uint32_t gmax = 0;  // largest frame length walked (sizes the piece pass's guess filter)
         while (status == kWalking) {
             // (re)start the pipeline at the window holding pos
             int64_t k = (pos - A) / W;
@@ -180,6 +196,7 @@ __global__ __launch_bounds__(kBlock2) void segment_walk_kernel(SegArgs a) {
                     uint32_t nfr = sh_nfr;
                     int st = kWalking;
                     int64_t p = pos;
+                    uint32_t nscalar = 0;  // frames of this window walked one at a time
                     while (p < wend) {
                         {
                             // Speculative run (a run of equal lengths was seen): lane j checks the
@@ -216,6 +233,7 @@ __global__ __launch_bounds__(kBlock2) void segment_walk_kernel(SegArgs a) {
                                     }
                                     nfr += nacc;
                                     p += (int64_t)nacc * sd;
+                                    gmax = sd > gmax ? sd : gmax;
                                     if (nacc == 64) continue;
                                 }
                                 if (p >= wend) break;
@@ -259,6 +277,7 @@ __global__ __launch_bounds__(kBlock2) void segment_walk_kernel(SegArgs a) {
                                     if ((k & 63u) == 63u) stage_flush(so + (k - 63), sl + (k - 63), lane, 64, st_o, st_l);
                                     ++k;
                                     p32 += fl;
+                                    gmax = fl > gmax ? fl : gmax;
                                     q = (q + fl) & (uint32_t)MASK;
                                     prev_fl = last_fl;
                                     last_fl = fl;
@@ -268,6 +287,7 @@ __global__ __launch_bounds__(kBlock2) void segment_walk_kernel(SegArgs a) {
                                 p = p32;
                             }
                             nfr += k;
+                            nscalar += k;
                         }
                         if (p >= wend) break;
                         if (p >= L) {
@@ -343,10 +363,16 @@ __global__ __launch_bounds__(kBlock2) void segment_walk_kernel(SegArgs a) {
                             a.scratch_len[s * (uint64_t)a.cap + nfr] = (uint32_t)(total + 4);
                         }
                         ++nfr;
+                        ++nscalar;
                         p += total + 4;
                         prev_fl = last_fl;
                         last_fl = (uint32_t)(total + 4);
+                        gmax = last_fl > gmax ? last_fl : gmax;
                     }
+                    // An irregular log (frames of differing lengths: the window went mostly one
+                    // frame at a time) with a long way to go is handed to the piece-parallel pass.
+                    if (a.bail_min && st == kWalking && nscalar >= (uint32_t)kBailScalar && L - p >= (int64_t)a.bail_min)
+                        st = kDeferred;
                     // Header fast-forward: the window ended inside a run of equal lengths s, so
                     // the run is followed straight through HBM, reading only frame HEADERS: each
                     // round lane j loads the headers at p + j*s and p + (64+j)*s (two 8-byte
@@ -448,6 +474,7 @@ __global__ __launch_bounds__(kBlock2) void segment_walk_kernel(SegArgs a) {
             a.seg_status[s] = status;
             a.seg_stop[s] = (uint64_t)pos;
         }
+        if (a.seg_gmax && t == 0) a.seg_gmax[s] = gmax;  // thread 0 = wave 0's lane 0
         __syncthreads();
     }
 }
@@ -490,6 +517,375 @@ __global__ __launch_bounds__(256) void segment_compact_kernel(const uint64_t* sc
                 frame_off[first + i] = scratch_off[s * (uint64_t)cap + i];
                 frame_len[first + i] = scratch_len[s * (uint64_t)cap + i];
             }
+        }
+    }
+}
+
+// ---- Piece-parallel framing (irregular logs) -----------------------------------------------------
+// The frame chain is serial, so a segment of differently sized frames walks one frame per step
+// (above).  A segment the walk defers (kDeferred: its window went mostly one frame at a time) is
+// cut into pieces of kPiece bytes from the deferral point p_d, and the chain is found in parallel:
+//   piece_guess_kernel  one 512-thread block per piece, the piece's first kGuessWin bytes in LDS.
+//                       Piece 0 starts at p_d.  Piece i >= 1 GUESSES its first frame: candidate
+//                       starts B_i, B_i + 1, ... are walked in rounds of 512 (one lane each) with
+//                       the fast-path rules; a walk survives if it leaves the window, or ends where
+//                       the rest of the window is zero (a terminator) or at EOF; it dies at any other
+//                       unparseable header or at a frame longer than gmax (4 x the largest frame
+//                       the deferring walk saw).  The lowest survivor is the guess g_i.
+//   piece_walk_kernel   one lane per piece, headers straight from HBM: walks from g_i to the piece
+//                       end -- frame count, exit (first position >= B_i+1, or where the fast walk
+//                       ended) and the first kHead positions (the head).
+//   piece_stitch_kernel one wave per segment, in piece order: the true entry e_i of piece i is the
+//                       exit of piece i-1's true walk.  Walks are deterministic, so once the walk
+//                       from e_i reaches a position of the guessed walk the two coincide: if e_i is
+//                       in the head (the usual case -- a false candidate before e_i that survives
+//                       has merged into the true chain, mostly at e_i itself), or the walk from e_i
+//                       meets the head within kHead steps, the guessed walk's count/exit give the
+//                       true ones; otherwise the piece is re-walked from e_i.  The result never
+//                       depends on the guess -- a bad guess only costs that walk.  Per piece: entry,
+//                       frame count and first slot; per segment: where the fast walk ended.
+//   piece_write_kernel  one lane per piece: walks from its entry writing its frames' slots.
+//   segment_walk_kernel (resume pass) takes each deferred segment from where the fast walk ended,
+//                       with the full decodeEntry / verifyTerminator rules (usually the terminator).
+// A frame is taken by the pieces only if it passes the fast loop's checks (non-zero first byte,
+// varint of <= 4 bytes, frame within maxOpSize and EOF, header more than 8 bytes before EOF), the
+// frames the serial walk accepts without its rule-by-rule step; everything else is the resume
+// pass's.  Integer byte work, no MFMA: the guess pass streams 1/4 of the bytes through LDS, the
+// walks touch one header per frame.
+constexpr uint32_t kPiece = 131072;      // bytes per piece
+constexpr uint32_t kGuessWin = 32768;    // bytes of a piece the guess pass looks at
+constexpr uint32_t kGuessLds = kGuessWin + 64;
+constexpr int kPieceThreads = 512;
+constexpr uint32_t kHead = 16;
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+
+// Frame length of the header v (bytes p..p+3, little-endian) if it passes the fast-path checks,
+// else 0.  left = L - p.  (Same folded predicate as the walk's fast loop.)
+__device__ __forceinline__ uint32_t fast_frame_len(uint32_t v, uint32_t left, uint32_t max_op) {
+    const uint32_t stop4 = ~v & 0x80808080u;
+    const int vl = (__builtin_ctz(stop4 | 0x80000000u) >> 3) + 1;
+    const uint32_t nn = ((v & 0x7fu) | ((v >> 1) & 0x3f80u) | ((v >> 2) & 0x1fc000u) | ((v >> 3) & 0xfe00000u)) &
+                        (0xffffffffu >> (32 - 7 * vl));
+    const uint32_t vs = nn < (1u << 7) ? 1u : nn < (1u << 14) ? 2u : nn < (1u << 21) ? 3u : 4u;
+    const uint32_t fl = vs + nn + 4;
+    const bool ok = (v & 0xffu) != 0 && stop4 != 0 && fl <= (left < max_op ? left : max_op);
+    return ok ? fl : 0u;
+}
+
+// 4 header bytes at absolute buffer offset ga, read from HBM as two aligned dwords.
+__device__ __forceinline__ uint32_t hbm_header(const uint8_t* buf, uint64_t ga) {
+    const uint32_t* wp = reinterpret_cast<const uint32_t*>(buf + (ga & ~3ull));
+    return (uint32_t)((((uint64_t)wp[1] << 32) | wp[0]) >> (8 * (ga & 3)));
+}
+
+// Fast-path frame length at segment position p, from HBM; 0 = the fast walk ends at p.
+__device__ __forceinline__ uint32_t hbm_frame_len(const uint8_t* buf, uint64_t base, uint32_t p, uint32_t L,
+                                                  uint32_t max_op) {
+    return p + 8 < L ? fast_frame_len(hbm_header(buf, base + p), L - p, max_op) : 0u;
+}
+
+struct PieceArgs {
+    const uint8_t* buf;
+    uint64_t buf_len;
+    const uint64_t* seg_off;
+    const uint64_t* seg_len;
+    uint64_t n_seg;
+    uint32_t max_op;
+    uint32_t cap;                // frames_per_seg_cap
+    uint64_t piece_cap;          // work items the scratch holds
+    const int32_t* seg_status;   // kDeferred = piece pass
+    const uint64_t* seg_stop;    // p_d
+    const uint32_t* seg_nframes; // frames found before p_d
+    const uint32_t* seg_gmax;
+    uint32_t* piece_first;       // [n_seg] first work item of the segment
+    uint32_t* piece_cnt;         // [n_seg] pieces of the segment (0: serial resume from p_d)
+    uint32_t* piece_seg;         // [piece_cap] segment of each work item (kNone: none)
+    unsigned int* n_pieces;      // work items in use
+    uint32_t* guess;             // [piece_cap] g (kNone: no survivor)
+    uint4* gwalk;                // [piece_cap] walk from g: {g, count, exit, ended}
+    uint32_t* head;              // [piece_cap][kHead] first positions of that walk (kNone-padded)
+    uint4* walk;                 // [piece_cap] true walk: {entry, count, first slot, 0}
+    uint64_t* resume_pos;        // [n_seg]
+    uint32_t* resume_nfr;        // [n_seg]
+    uint64_t* scratch_off;
+    uint32_t* scratch_len;
+};
+
+// Segment-relative bounds of piece i: [Bi, Bn).
+__device__ __forceinline__ void piece_bounds(uint32_t pd, uint32_t L, uint32_t i, uint32_t& Bi, uint32_t& Bn) {
+    Bi = pd + i * kPiece;
+    Bn = L - Bi > kPiece ? Bi + kPiece : L;
+}
+
+// One block: pieces per deferred segment (prefix sum) and the work-item -> segment map.
+__global__ __launch_bounds__(kScanThreads) void piece_plan_kernel(PieceArgs a) {
+    __shared__ uint64_t part[kScanThreads];
+    const int t = threadIdx.x;
+    const uint64_t per = (a.n_seg + kScanThreads - 1) / kScanThreads;
+    const uint64_t lo = t * per, hi = lo + per < a.n_seg ? lo + per : a.n_seg;
+    auto pieces_of = [&](uint64_t s) -> uint64_t {
+        if (a.seg_status[s] != kDeferred) return 0;
+        const uint64_t L = a.seg_len[s], pd = a.seg_stop[s];
+        if (L > 0x7fffffffull || pd >= L) return 0;
+        return (L - pd + kPiece - 1) / kPiece;
+    };
+    uint64_t sum = 0;
+    for (uint64_t s = lo; s < hi; ++s) sum += pieces_of(s);
+    part[t] = sum;
+    __syncthreads();
+    for (int d = 1; d < kScanThreads; d <<= 1) {
+        const uint64_t v = t >= d ? part[t - d] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    // the prefix is monotone: the segments that fit are a prefix of the deferred ones, and the
+    // work items in use end where the last of them ends (*n_pieces zeroed by the host)
+    uint64_t run = t ? part[t - 1] : 0;
+    for (uint64_t s = lo; s < hi; ++s) {
+        const uint64_t np = pieces_of(s);
+        const bool fits = run + np <= a.piece_cap;  // else: this segment walks serially
+        a.piece_first[s] = (uint32_t)(fits ? run : 0);
+        a.piece_cnt[s] = (uint32_t)(fits ? np : 0);
+        if (fits && np) {
+            for (uint64_t w = run; w < run + np; ++w) a.piece_seg[w] = (uint32_t)s;
+            atomicMax(a.n_pieces, (unsigned int)(run + np));
+        }
+        run += np;
+    }
+}
+
+// The guess per piece (see above).  Block-uniform control; LDS holds the guess window.
+__global__ __launch_bounds__(kPieceThreads) void piece_guess_kernel(PieceArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t img[kGuessLds];
+    __shared__ unsigned int sh_best;
+    __shared__ unsigned int sh_zero;  // image index where the all-zero tail of the window starts
+    const int t = threadIdx.x;
+    const unsigned int total = *a.n_pieces;
+    for (unsigned int w = blockIdx.x; w < total; w += gridDim.x) {
+        const uint32_t s = a.piece_seg[w];
+        if (s == kNone) continue;  // block-uniform
+        const uint32_t i = w - a.piece_first[s];
+        const uint32_t pd = (uint32_t)a.seg_stop[s];
+        if (i == 0) {  // the deferral point is a true frame position
+            if (t == 0) a.guess[w] = pd;
+            continue;
+        }
+        const uint64_t base = a.seg_off[s];
+        const uint32_t L = (uint32_t)a.seg_len[s];
+        uint32_t Bi, Bn;
+        piece_bounds(pd, L, i, Bi, Bn);
+        const uint32_t We = Bn - Bi > kGuessWin ? Bi + kGuessWin : Bn;  // guess window end
+        // image: segment bytes [Bi - o0, Bi - o0 + kGuessLds) on a 16-byte grid, zero past the
+        // region end min(We + 32, L); image index of segment position p = p - Bi + o0
+        const uint32_t o0 = (uint32_t)((base + Bi) & 15u);
+        const uint32_t rend = L - We > 32u ? We + 32u : L;
+        const uint32_t ilen = rend - Bi + o0;
+        if (t == 0) {
+            sh_best = kNone;
+            sh_zero = 0;
+        }
+        const uint8_t* src = a.buf + base + Bi - o0;
+        unsigned int lastnz = 0;  // 1 + highest image index holding a non-zero byte (this thread)
+        for (uint32_t c = (uint32_t)t * 16u; c < kGuessLds; c += kPieceThreads * 16u) {
+            u32x4s v{0, 0, 0, 0};
+            if (c + 16 <= ilen) {
+                v = *reinterpret_cast<const u32x4s*>(src + c);
+            } else if (c < ilen) {
+                uint32_t wv[4] = {0, 0, 0, 0};
+                for (uint32_t k = 0; c + k < ilen; ++k) wv[k >> 2] |= (uint32_t)src[c + k] << (8 * (k & 3));
+                v = {wv[0], wv[1], wv[2], wv[3]};
+            }
+            *reinterpret_cast<u32x4s*>(img + c) = v;
+            const uint32_t ww[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int k = 3; k >= 0; --k)
+                if (ww[k]) {
+                    const unsigned int e = c + 4u * k + 4u - (__builtin_clz(ww[k]) >> 3);
+                    lastnz = e > lastnz ? e : lastnz;
+                    break;
+                }
+        }
+        __syncthreads();
+        if (lastnz) atomicMax(&sh_zero, lastnz);
+        __syncthreads();
+        const uint32_t zpos = sh_zero >= o0 ? Bi + sh_zero - o0 : Bi;  // segment position
+        const uint32_t gm0 = a.seg_gmax[s] * 4u;
+        const uint32_t gmax = gm0 < 1024u ? 1024u : gm0 > kGuessWin ? kGuessWin : gm0;
+        const uint32_t ncand = We - Bi < 4u * gmax ? We - Bi : 4u * gmax;
+        // rounds of kPieceThreads candidate starts until one survives
+        for (uint32_t r0 = 0; r0 < ncand; r0 += kPieceThreads) {
+            const uint32_t ci = r0 + (uint32_t)t;
+            uint32_t p = Bi + ci;
+            bool alive = ci < ncand, surv = false;
+            while (alive) {
+                if (p >= We || p + 8 >= L) {  // left the window, or the rule-by-rule step's (EOF)
+                    surv = true;
+                    break;
+                }
+                const uint32_t q = p - Bi + o0;
+                const uint32_t lo = *reinterpret_cast<const uint32_t*>(img + (q & ~3u));
+                const uint32_t hi = *reinterpret_cast<const uint32_t*>(img + (q & ~3u) + 4);
+                const uint32_t v = (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * (q & 3)));
+                const uint32_t fl = fast_frame_len(v, L - p, a.max_op);
+                if (fl == 0) {  // the fast walk ends here: a terminator if the rest is zero
+                    surv = p >= zpos;
+                    break;
+                }
+                if (fl > gmax) break;  // implausible for this log: a false start
+                p += fl;
+            }
+            if (surv) atomicMin(&sh_best, ci);
+            __syncthreads();
+            const unsigned int best = sh_best;
+            __syncthreads();  // read by all before the next round may lower it
+            if (best != kNone) break;  // block-uniform
+        }
+        if (t == 0) a.guess[w] = sh_best == kNone ? kNone : Bi + sh_best;
+        __syncthreads();
+    }
+}
+
+// One lane per piece: the walk from the guess (see above), headers from HBM.
+__global__ __launch_bounds__(256) void piece_walk_kernel(PieceArgs a) {
+    const unsigned int total = *a.n_pieces;
+    for (unsigned int w = blockIdx.x * blockDim.x + threadIdx.x; w < total; w += gridDim.x * blockDim.x) {
+        const uint32_t s = a.piece_seg[w];
+        if (s == kNone) continue;
+        const uint32_t g = a.guess[w];
+        uint32_t* hd = a.head + (uint64_t)w * kHead;
+        uint32_t cnt = 0, p = g, ended = 0;
+        if (g != kNone) {
+            const uint64_t base = a.seg_off[s];
+            const uint32_t L = (uint32_t)a.seg_len[s];
+            uint32_t Bi, Bn;
+            piece_bounds((uint32_t)a.seg_stop[s], L, w - a.piece_first[s], Bi, Bn);
+            while (p < Bn) {
+                const uint32_t fl = hbm_frame_len(a.buf, base, p, L, a.max_op);
+                if (fl == 0) {
+                    ended = 1;
+                    break;
+                }
+                if (cnt < kHead) hd[cnt] = p;
+                ++cnt;
+                p += fl;
+            }
+        }
+        for (uint32_t k = cnt; k < kHead; ++k) hd[k] = kNone;
+        a.gwalk[w] = make_uint4(g, cnt, p, ended);
+    }
+}
+
+// One wave per segment: the true chain through the pieces (see above).  Control is wave-uniform;
+// lane k < kHead holds head position k of the piece being resolved.
+__global__ __launch_bounds__(64) void piece_stitch_kernel(PieceArgs a) {
+    const uint64_t s = blockIdx.x;
+    if (s >= a.n_seg || a.seg_status[s] != kDeferred) return;
+    const int lane = threadIdx.x;
+    const uint64_t base = a.seg_off[s];
+    const uint32_t L = (uint32_t)a.seg_len[s];
+    const uint32_t pd = (uint32_t)a.seg_stop[s];
+    const uint32_t np = a.piece_cnt[s], pf = a.piece_first[s];
+    uint32_t e = pd, total = a.seg_nframes[s];
+    uint64_t rpos = pd;
+    uint32_t rnfr = total;
+    bool done = false;
+    for (uint32_t c0 = 0; c0 < np && !done; c0 += 64) {
+        const uint32_t nc = np - c0 < 64 ? np - c0 : 64;
+        uint4 gr = make_uint4(kNone, 0, 0, 0);
+        if ((uint32_t)lane < nc) gr = a.gwalk[pf + c0 + lane];
+        uint4 out = make_uint4(0, 0, 0, 0);
+        for (uint32_t j = 0; j < nc && !done; ++j) {
+            const uint32_t w = pf + c0 + j;
+            uint32_t Bi, Bn;
+            piece_bounds(pd, L, c0 + j, Bi, Bn);
+            if (e >= Bn) {  // a frame spans this piece: nothing starts in it
+                if ((uint32_t)lane == j) out = make_uint4(e, 0, total, 0);
+                continue;
+            }
+            const uint32_t g = __builtin_amdgcn_readlane(gr.x, j);
+            uint32_t cnt = __builtin_amdgcn_readlane(gr.y, j);
+            uint32_t x = __builtin_amdgcn_readlane(gr.z, j);
+            uint32_t ended = __builtin_amdgcn_readlane(gr.w, j);
+            if (g != e) {
+                // Walk from the true entry until it meets the guessed walk's head (then the rest
+                // of the piece is the guessed walk: m steps + the guessed frames from there on),
+                // the piece end, or the end of the fast walk; past kHead steps without meeting it,
+                // finish the piece alone.
+                const uint32_t hv = (g != kNone && (uint32_t)lane < kHead) ? a.head[(uint64_t)w * kHead + lane] : kNone;
+                uint32_t p = e, m = 0;
+                bool met = false;
+                ended = 0;
+                while (p < Bn) {
+                    const uint64_t hit = __builtin_amdgcn_ballot_w64(hv == p);
+                    if (m < kHead && hit) {
+                        cnt = m + cnt - (uint32_t)__builtin_ctzll(hit);  // x, ended: the guessed walk's
+                        met = true;
+                        break;
+                    }
+                    const uint32_t fl = hbm_frame_len(a.buf, base, p, L, a.max_op);
+                    if (fl == 0) {
+                        ended = 1;
+                        break;
+                    }
+                    ++m;
+                    p += fl;
+                }
+                if (!met) {
+                    cnt = m;
+                    x = p;
+                } else {
+                    ended = __builtin_amdgcn_readlane(gr.w, j);
+                }
+            }
+            if (total + cnt > a.cap) {  // the slot capacity ends inside this piece: serial from e
+                rpos = e;
+                rnfr = total;
+                done = true;
+                break;
+            }
+            if ((uint32_t)lane == j) out = make_uint4(e, cnt, total, 0);
+            total += cnt;
+            if (ended) {
+                rpos = x;
+                rnfr = total;
+                done = true;
+                break;
+            }
+            e = x;
+        }
+        if ((uint32_t)lane < nc) a.walk[pf + c0 + lane] = out;
+        if (done)
+            for (uint32_t k = c0 + 64 + lane; k < np; k += 64) a.walk[pf + k] = make_uint4(0, 0, 0, 0);
+    }
+    if (!done) {  // unreachable (a header within 8 bytes of EOF ends every fast walk); be exact anyway
+        rpos = e;
+        rnfr = total;
+    }
+    if (lane == 0) {
+        a.resume_pos[s] = rpos;
+        a.resume_nfr[s] = rnfr;
+    }
+}
+
+// One lane per piece: the piece's frames into the segment's slots.
+__global__ __launch_bounds__(256) void piece_write_kernel(PieceArgs a) {
+    const unsigned int total = *a.n_pieces;
+    for (unsigned int w = blockIdx.x * blockDim.x + threadIdx.x; w < total; w += gridDim.x * blockDim.x) {
+        const uint32_t s = a.piece_seg[w];
+        if (s == kNone) continue;
+        const uint4 r = a.walk[w];
+        if (r.y == 0) continue;
+        const uint64_t base = a.seg_off[s];
+        const uint32_t L = (uint32_t)a.seg_len[s];
+        uint64_t* so = a.scratch_off + s * (uint64_t)a.cap + r.z;
+        uint32_t* sl = a.scratch_len + s * (uint64_t)a.cap + r.z;
+        uint32_t p = r.x;
+        for (uint32_t k = 0; k < r.y; ++k) {
+            const uint32_t fl = hbm_frame_len(a.buf, base, p, L, a.max_op);
+            so[k] = base + p;
+            sl[k] = fl;
+            p += fl;
         }
     }
 }
@@ -544,7 +940,65 @@ int rh_segments_launch_impl(rh_ctx* ctx, const rh_segments* g, hipStream_t strea
     a.seg_stop = g->seg_stop;
     const int cus = ctx && ctx->num_cus > 0 ? ctx->num_cus : 256;
     uint64_t grid = g->n_seg < (uint64_t)cus * 8 ? g->n_seg : (uint64_t)cus * 8;
+    // Piece-pass scratch (stream-ordered, from the context's pool): per segment 24 B, per piece
+    // 36 + 4 kHead B.  piece_cap bounds the pieces of non-overlapping segments; segments beyond it
+    // walk serially.
+    const uint64_t n_seg = g->n_seg;
+    const uint64_t piece_cap = g->buf_len / kPiece + n_seg + 1;
+    const size_t bytes = (size_t)piece_cap * (40 + 4 * kHead) + (size_t)n_seg * 24 + 64;
+    void* scratch = nullptr;
+    RH_HIP(rh::pool_alloc(ctx, &scratch, bytes, stream));
+    uint8_t* sp = static_cast<uint8_t*>(scratch);
+    PieceArgs pa{};
+    pa.gwalk = reinterpret_cast<uint4*>(sp);
+    pa.walk = pa.gwalk + piece_cap;
+    pa.resume_pos = reinterpret_cast<uint64_t*>(pa.walk + piece_cap);
+    pa.piece_first = reinterpret_cast<uint32_t*>(pa.resume_pos + n_seg);
+    pa.piece_cnt = pa.piece_first + n_seg;
+    uint32_t* seg_gmax = pa.piece_cnt + n_seg;
+    pa.seg_gmax = seg_gmax;
+    pa.resume_nfr = seg_gmax + n_seg;
+    pa.n_pieces = reinterpret_cast<unsigned int*>(pa.resume_nfr + n_seg);
+    pa.piece_seg = reinterpret_cast<uint32_t*>(pa.n_pieces + 4);
+    pa.guess = pa.piece_seg + piece_cap;
+    pa.head = pa.guess + piece_cap;
+    pa.buf = g->buf;
+    pa.buf_len = g->buf_len;
+    pa.seg_off = g->seg_off;
+    pa.seg_len = g->seg_len;
+    pa.n_seg = n_seg;
+    pa.max_op = g->max_op;
+    pa.cap = g->frames_per_seg_cap;
+    pa.piece_cap = piece_cap;
+    pa.seg_status = g->seg_status;
+    pa.seg_stop = g->seg_stop;
+    pa.seg_nframes = g->seg_nframes;
+    pa.scratch_off = g->scratch_off;
+    pa.scratch_len = g->scratch_len;
+    // 1. serial walk; irregular segments with >= 2 pieces to go are deferred
+    a.bail_min = 2 * kPiece;
+    a.seg_gmax = seg_gmax;
     RH_HIP(launch_walk(a, cus, stream));
+    // 2-6. piece-parallel framing of the deferred segments
+    RH_HIP(hipMemsetAsync(pa.n_pieces, 0, sizeof(unsigned int), stream));
+    hipLaunchKernelGGL(piece_plan_kernel, dim3(1), dim3(kScanThreads), 0, stream, pa);
+    RH_HIP(hipGetLastError());
+    hipLaunchKernelGGL(piece_guess_kernel, dim3((uint32_t)(4 * cus)), dim3(kPieceThreads), 0, stream, pa);
+    RH_HIP(hipGetLastError());
+    const uint64_t wgrid = (piece_cap + 255) / 256 < (uint64_t)cus * 8 ? (piece_cap + 255) / 256 : (uint64_t)cus * 8;
+    hipLaunchKernelGGL(piece_walk_kernel, dim3((uint32_t)wgrid), dim3(256), 0, stream, pa);
+    RH_HIP(hipGetLastError());
+    hipLaunchKernelGGL(piece_stitch_kernel, dim3((uint32_t)n_seg), dim3(64), 0, stream, pa);
+    RH_HIP(hipGetLastError());
+    hipLaunchKernelGGL(piece_write_kernel, dim3((uint32_t)wgrid), dim3(256), 0, stream, pa);
+    RH_HIP(hipGetLastError());
+    // 6. the deferred segments' ends (terminator check, rule-by-rule steps) and serial leftovers
+    a.bail_min = 0;
+    a.seg_gmax = nullptr;
+    a.resume_pos = pa.resume_pos;
+    a.resume_nfr = pa.resume_nfr;
+    RH_HIP(launch_walk(a, cus, stream));
+    RH_HIP(hipFreeAsync(scratch, stream));
     hipLaunchKernelGGL(segment_scan_kernel, dim3(1), dim3(kScanThreads), 0, stream, g->seg_nframes, g->n_seg,
                        g->frames_per_seg_cap, g->seg_first, g->total_frames);
     RH_HIP(hipGetLastError());

@@ -1,0 +1,249 @@
+"""GPU parity of the piece-parallel framing of irregular logs (segment.hip, "Piece-parallel
+framing") against the oracle's literal reader walk (orc_segment_scan: SegmentedRaftLogReader
+verifyHeader / decodeEntry / verifyTerminator, SegmentedRaftLogReader.java:179-341).
+
+A segment whose frames have differing lengths is deferred by the serial walk after its first
+window and framed by pieces of 64 KiB that guess their first frame; the stitch re-walks any piece
+whose guess is not the true entry.  So these cases cover: damage deep inside a deferred segment (in
+any piece, including the resume pass's rule-by-rule step), guesses that must fail (text-like and
+zero-filled payloads, frames longer than the guess filter, frames spanning whole pieces), the slot
+capacity running out inside a piece, and deferred segments mixed with ones the walk finishes."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HEADER = b"RaftLog1"
+MIB = 1 << 20
+
+
+def payload(rng, n, kind):
+    if kind == "random":
+        return rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+    if kind == "text":      # every byte a 1-byte varint: false walks survive and converge
+        return rng.integers(32, 127, n, dtype=np.uint8).tobytes()
+    if kind == "zeros":     # zero runs look like terminators
+        return bytes(n)
+    if kind == "mixed":
+        return payload(rng, n, ("random", "text", "zeros")[int(rng.integers(0, 3))])
+    raise AssertionError(kind)
+
+
+def ragged_image(orc, rng, size, lo=64, hi=2048, kind="random", pad=True):
+    """HEADER + frames of payload sizes in [lo, hi] up to ~size bytes (+ zero padding to size).
+    Returns (bytearray image, list of frame start offsets)."""
+    out = bytearray(HEADER)
+    starts = []
+    while True:
+        n = int(rng.integers(lo, hi + 1))
+        fr = orc.frame_write(payload(rng, n, kind))
+        if len(out) + len(fr) > size:
+            break
+        starts.append(len(out))
+        out += fr
+    if pad:
+        out += bytes(size - len(out))
+    return out, starts
+
+
+def damaged(orc, rng, kind):
+    size = 4 * MIB
+    if kind in ("random", "text", "zeros", "mixed"):
+        return bytes(ragged_image(orc, rng, size, kind=kind)[0])
+    img, st = ragged_image(orc, rng, size)
+    deep = [s for s in st if s > 300_000]
+    at = deep[int(rng.integers(0, len(deep)))]
+    if kind == "truncate":                       # last entry cut (PARTIAL)
+        return bytes(img[: at + int(rng.integers(1, 40))])
+    if kind == "truncate_exact":                 # EOF at an entry boundary (END, no padding)
+        return bytes(img[:at])
+    if kind == "terminator_garbage":             # terminator mid-segment, garbage later (E_PADDING)
+        img[at] = 0
+        img[min(len(img) - 1, at + int(rng.integers(1, 200_000)))] = 0x5A
+        return bytes(img)
+    if kind == "terminator_clean":               # zero from a frame start to EOF (END)
+        img[at:] = bytes(len(img) - at)
+        return bytes(img)
+    if kind == "varint_bad":                     # 6 continuation bytes (E_VARINT)
+        img[at: at + 6] = b"\xff" * 6
+        return bytes(img)
+    if kind == "oversize":                       # length > maxOpSize (E_OVERSIZE)
+        from ratis_amd import segment
+        v = segment.varint(5 << 20)
+        img[at: at + len(v)] = v
+        return bytes(img)
+    if kind in ("big_frame", "huge_frame", "big_frames_many"):
+        sizes = {"big_frame": [60_000], "huge_frame": [300_000], "big_frames_many": [20_000, 70_000, 9_000] * 3}[kind]
+        cut = img[:at]
+        big = b"".join(orc.frame_write(payload(rng, s, "random")) for s in sizes)
+        rest, _ = ragged_image(orc, rng, size, pad=False)
+        body = cut + big + rest[8:]
+        return bytes(body[:size]) if len(body) >= size else bytes(body) + bytes(size - len(body))
+    if kind == "five_byte_varint":               # a 5-byte varint header deep inside
+        img[at: at + 5] = b"\x85\x80\x80\x80\x00"
+        return bytes(img)
+    raise AssertionError(kind)
+
+
+def pack(images, rng):
+    offs, parts, pos = [], [], 0
+    for img in images:
+        gap = int(rng.integers(0, 40))
+        parts.append(bytes(rng.integers(0, 256, gap, dtype=np.uint8)))
+        pos += gap
+        offs.append(pos)
+        parts.append(img)
+        pos += len(img)
+    parts.append(bytes(rng.integers(0, 256, 64, dtype=np.uint8)))
+    return (np.frombuffer(b"".join(parts), dtype=np.uint8).copy(), np.asarray(offs, np.int64),
+            np.asarray([len(i) for i in images], np.int64))
+
+
+def scan(ctx, buf, offs, lens, cap=8192, max_op=4 << 20):
+    """rh_segments_read_launch: framing outputs in the batch + the reader's verdict (incl. CRC)."""
+    import torch
+
+    from ratis_amd import engine
+    b = engine.SegmentBatch(buf=torch.from_numpy(buf).cuda(), seg_off=torch.from_numpy(offs).cuda(),
+                            seg_len=torch.from_numpy(lens).cuda(), max_op=max_op, frames_per_seg_cap=cap)
+    r = engine.read_segments_fused(ctx, b)
+    torch.cuda.synchronize()
+    b.verdict = {k: r[k].cpu().numpy() for k in ("n_ok", "status", "stop")}
+    return b
+
+
+def check(orc, b, buf, offs, lens, cap=8192, max_op=4 << 20, names=None):
+    """The reader's verdict equals the literal reader's; the framing (which does not look at CRCs)
+    equals it too unless the literal reader stopped at a checksum, and then up to that frame."""
+    first = b.seg_first.cpu().numpy()
+    nfr = b.seg_nframes.cpu().numpy()
+    st = b.seg_status.cpu().numpy()
+    stop = b.seg_stop.cpu().numpy()
+    total = int(b.total_frames.item())
+    fo = b.frame_off[:total].cpu().numpy()
+    fl = b.frame_len[:total].cpu().numpy()
+    assert total == int(np.minimum(nfr, cap).sum())
+    v = b.verdict
+    for s in range(len(offs)):
+        img = buf[offs[s]: offs[s] + lens[s]]
+        ro, rl, _, rst, rstop = orc.segment_scan(img, max_op=max_op, cap=cap)
+        tag = (s, names[s] if names else None)
+        assert (v["status"][s], v["stop"][s], v["n_ok"][s]) == (rst, rstop, len(ro)), (tag, rst, rstop, len(ro))
+        k = first[s]
+        if rst != -2:  # ORC_E_CHECKSUM
+            assert (st[s], stop[s], nfr[s]) == (rst, rstop, len(ro)), (tag, (st[s], stop[s], nfr[s]))
+        assert nfr[s] >= len(ro), tag
+        assert np.array_equal(fo[k: k + len(ro)] - offs[s], ro), tag
+        assert np.array_equal(fl[k: k + len(ro)], rl), tag
+
+
+KINDS = ["random", "text", "zeros", "mixed", "truncate", "truncate_exact", "terminator_garbage",
+         "terminator_clean", "varint_bad", "oversize", "big_frame", "huge_frame", "big_frames_many",
+         "five_byte_varint"]
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_deferred_segment_matches_oracle(ctx, orc, kind):
+    rng = np.random.default_rng(1000 + KINDS.index(kind))
+    images = [damaged(orc, rng, kind) for _ in range(3)]
+    buf, offs, lens = pack(images, rng)
+    b = scan(ctx, buf, offs, lens)
+    check(orc, b, buf, offs, lens, names=[kind] * 3)
+
+
+def test_mixed_batch_deferred_and_serial(ctx, orc):
+    """Deferred ragged segments next to short segments and a uniform-frame segment (which the walk
+    finishes itself), at unaligned offsets in one buffer."""
+    rng = np.random.default_rng(77)
+    images, names = [], []
+    for i, kind in enumerate(KINDS):
+        images.append(damaged(orc, rng, kind))
+        names.append(kind)
+        small, _ = ragged_image(orc, rng, int(rng.integers(9, 90_000)), kind="random")
+        images.append(bytes(small))
+        names.append("small")
+    uni = HEADER + b"".join(orc.frame_write(bytes(rng.integers(0, 256, 1000, dtype=np.uint8))) for _ in range(3000))
+    images.append(uni + bytes(5000))
+    names.append("uniform")
+    buf, offs, lens = pack(images, rng)
+    b = scan(ctx, buf, offs, lens)
+    check(orc, b, buf, offs, lens, names=names)
+
+
+@pytest.mark.parametrize("cap", [100, 1000, 2047, 2900])
+def test_capacity_inside_a_piece(ctx, orc, cap):
+    """frames_per_seg_cap reached inside the piece pass: E_CAPACITY after exactly cap frames, the
+    walk stopped at frame #cap, the first cap frames equal to the literal reader's."""
+    from ratis_amd import _lib
+    rng = np.random.default_rng(cap)
+    images = [bytes(ragged_image(orc, rng, 4 * MIB)[0]) for _ in range(2)]
+    buf, offs, lens = pack(images, rng)
+    b = scan(ctx, buf, offs, lens, cap=cap)
+    assert list(b.seg_status.cpu().numpy()) == [_lib.RH_SEG_E_CAPACITY] * 2
+    assert list(b.seg_nframes.cpu().numpy()) == [cap, cap]
+    fo = b.frame_off[:2 * cap].cpu().numpy()
+    fl = b.frame_len[:2 * cap].cpu().numpy()
+    for s in range(2):
+        ro, rl, _, _, _ = orc.segment_scan(buf[offs[s]: offs[s] + lens[s]])
+        assert int(b.seg_stop[s].item()) == ro[cap]
+        assert np.array_equal(fo[s * cap:(s + 1) * cap] - offs[s], ro[:cap])
+        assert np.array_equal(fl[s * cap:(s + 1) * cap], rl[:cap])
+
+
+def test_small_max_op_in_pieces(ctx, orc):
+    """maxOpSize between the frame sizes: the first frame longer than it ends the walk deep inside."""
+    rng = np.random.default_rng(4)
+    images = [bytes(ragged_image(orc, rng, 2 * MIB, lo=64, hi=3000)[0]) for _ in range(2)]
+    buf, offs, lens = pack(images, rng)
+    for max_op in (2800, 3004, 1 << 20):
+        b = scan(ctx, buf, offs, lens, max_op=max_op)
+        check(orc, b, buf, offs, lens, max_op=max_op)
+
+
+def test_synthetic_ragged_32mib(ctx, orc):
+    """The bench shape (workload.synth_ragged_segments, 32 MiB, 64-2048 B frames): frame table equal
+    to the generator's and to the literal reader on two whole segments."""
+    import torch
+
+    from ratis_amd import engine, workload
+    rs = workload.synth_ragged_segments(ctx, 6, min_frame=64, max_frame=2048, seed=31)
+    n = rs.n_segments
+    b = engine.SegmentBatch(buf=rs.batch.buf, seg_off=torch.arange(n, device="cuda", dtype=torch.int64) * rs.segment_size,
+                            seg_len=torch.full((n,), rs.segment_size, device="cuda", dtype=torch.int64),
+                            frames_per_seg_cap=int(rs.seg_nframes.max()) + 16)
+    engine.segments_scan(ctx, b)
+    torch.cuda.synchronize()
+    nf = int(rs.seg_nframes.sum())
+    assert int(b.total_frames.item()) == nf
+    assert torch.equal(b.frame_off[:nf], rs.batch.frame_off)
+    assert torch.equal(b.frame_len[:nf], rs.batch.frame_len)
+    for sgi in (0, n - 1):
+        img = rs.batch.buf[sgi * rs.segment_size:(sgi + 1) * rs.segment_size].cpu().numpy()
+        ro, rl, _, rst, rstop = orc.segment_scan(img)
+        assert (int(b.seg_status[sgi].item()), int(b.seg_stop[sgi].item())) == (rst, rstop)
+        assert len(ro) == int(rs.seg_nframes[sgi])
+
+
+def test_read_path_over_deferred_segments(ctx, orc):
+    """rh_segments_read_launch (framing + CRC verify + verdict) over deferred segments with flipped
+    payload bits deep inside: the reader stops at the first bad frame."""
+    import torch
+
+    from ratis_amd import engine
+    rng = np.random.default_rng(12)
+    images = []
+    for i in range(4):
+        img, st = ragged_image(orc, rng, 3 * MIB)
+        if i % 2:
+            f = st[int(rng.integers(len(st) // 3, len(st)))]
+            img[f + 20] ^= 0x10
+        images.append(bytes(img))
+    buf, offs, lens = pack(images, rng)
+    b = engine.SegmentBatch(buf=torch.from_numpy(buf).cuda(), seg_off=torch.from_numpy(offs).cuda(),
+                            seg_len=torch.from_numpy(lens).cuda(), frames_per_seg_cap=8192)
+    r = engine.read_segments_fused(ctx, b)
+    torch.cuda.synchronize()
+    n_ok, st, stop = r["n_ok"].cpu().numpy(), r["status"].cpu().numpy(), r["stop"].cpu().numpy()
+    for s in range(len(offs)):
+        ro, _, _, rst, rstop = orc.segment_scan(buf[offs[s]: offs[s] + lens[s]])
+        assert (st[s], stop[s], n_ok[s]) == (rst, rstop, len(ro)), s
