@@ -115,6 +115,32 @@ def timed_passes(items, fn, seconds: float) -> dict:
     return {"rate": sum(units) / dt, "passes": sum(passes), "seconds": dt}
 
 
+class _producers:
+    """bench_support/libbench_producers.so: a pool of native threads standing in for the Java
+    RPC threads that write rh_delta records into the acquired staging slot (bench-only)."""
+
+    def __init__(self, threads: int):
+        import ctypes
+        path = os.path.join(ROOT, "bench_support", "_build", "libbench_producers.so")
+        self._lib = ctypes.CDLL(path)
+        self._lib.bp_create.restype = ctypes.c_void_p
+        self._lib.bp_create.argtypes = [ctypes.c_int]
+        self._lib.bp_fill.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+        self._lib.bp_destroy.argtypes = [ctypes.c_void_p]
+        self._pool = self._lib.bp_create(int(threads))
+        if not self._pool:
+            raise RuntimeError("bp_create failed")
+
+    def fill(self, dst: int, src: int, nbytes: int) -> None:
+        if self._lib.bp_fill(self._pool, dst, src, nbytes) != 0:
+            raise RuntimeError("bp_fill failed")
+
+    def close(self) -> None:
+        if self._pool:
+            self._lib.bp_destroy(self._pool)
+            self._pool = None
+
+
 def delta_streaming(ctx, host, steps: int = 12, fill_threads: int = 16) -> dict:
     """The operating mode the Java module uses: one resident RaftGroupTable (stable F=4 and joint
     F=6 tiers), FollowerInfo / flush-index updates written in place into the pinned delta ring
@@ -124,9 +150,6 @@ def delta_streaming(ctx, host, steps: int = 12, fill_threads: int = 16) -> dict:
     10 % the leader flushIndex) + one batched updateCommit.  Pipelined: the host fills step s+1
     while the device applies and evaluates step s, and collects step s-1's events meanwhile.
     Wall-clock per step; the stages are also timed on their own."""
-    import concurrent.futures
-    import ctypes
-
     from ratis_amd import _lib, groups
     rng = np.random.default_rng(99)
     n_all = sum(h.n for h in host)
@@ -151,17 +174,12 @@ def delta_streaming(ctx, host, steps: int = 12, fill_threads: int = 16) -> dict:
         per.append(np.concatenate(parts))
     nbytes = per[0].nbytes
 
-    pool = concurrent.futures.ThreadPoolExecutor(max_workers=fill_threads)
+    prod = _producers(fill_threads)
 
     def fill(ring, d):
-        # the producers' writes into the pinned ring: fill_threads memmoves on a persistent pool
-        # (ctypes drops the GIL)
-        dst, src = ring.ctypes.data, d.ctypes.data
-        cuts = np.linspace(0, d.nbytes, fill_threads + 1).astype(np.int64) // 16 * 16
-        cuts[-1] = d.nbytes
-        for f in [pool.submit(ctypes.memmove, dst + int(a), src + int(a), int(b - a))
-                  for a, b in zip(cuts[:-1], cuts[1:])]:
-            f.result()
+        # the producers' writes into the pinned ring (bench_support/producers.c: fill_threads native
+        # threads, each copying one contiguous share of the step's deltas)
+        prod.fill(ring.ctypes.data, d.ctypes.data, d.nbytes)
 
     def step(d):
         ring = tab.acquire_deltas()
@@ -196,7 +214,7 @@ def delta_streaming(ctx, host, steps: int = 12, fill_threads: int = 16) -> dict:
     tab.commit_wait_counts(tab.commit_async(watch_all=False))
     dev_s = time.perf_counter() - g0
     tab.close()
-    pool.shutdown()
+    prod.close()
     return {"commit_updates_per_s_incl_pcie": round(n_all / dt, 1), "ms_per_step": round(dt * 1e3, 3),
             "deltas_per_step": n_all, "delta_bytes_h2d_per_step": nbytes,
             "h2d_bound_ms": round(nbytes / 50e9 * 1e3, 3),
