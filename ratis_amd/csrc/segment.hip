@@ -530,33 +530,37 @@ __global__ __launch_bounds__(256) void segment_compact_kernel(const uint64_t* sc
 //                       starts B_i, B_i + 1, ... are walked in rounds of 512 (one lane each) with
 //                       the fast-path rules; a walk survives if it leaves the window, or ends where
 //                       the rest of the window is zero (a terminator) or at EOF; it dies at any other
-//                       unparseable header or at a frame longer than gmax (4 x the largest frame
+//                       unparseable header or at a frame longer than gmax (2 x the largest frame
 //                       the deferring walk saw).  The lowest survivor is the guess g_i.
 //   piece_walk_kernel   one lane per piece, headers straight from HBM: walks from g_i to the piece
-//                       end -- frame count, exit (first position >= B_i+1, or where the fast walk
-//                       ended) and the first kHead positions (the head).
+//                       end -- frame count, exit (first position >= B_{i+1}, or where the fast walk
+//                       ended) and the walk's frame lengths (the list, up to kList frames).
 //   piece_stitch_kernel one wave per segment, in piece order: the true entry e_i of piece i is the
 //                       exit of piece i-1's true walk.  Walks are deterministic, so once the walk
-//                       from e_i reaches a position of the guessed walk the two coincide: if e_i is
-//                       in the head (the usual case -- a false candidate before e_i that survives
-//                       has merged into the true chain, mostly at e_i itself), or the walk from e_i
-//                       meets the head within kHead steps, the guessed walk's count/exit give the
-//                       true ones; otherwise the piece is re-walked from e_i.  The result never
-//                       depends on the guess -- a bad guess only costs that walk.  Per piece: entry,
-//                       frame count and first slot; per segment: where the fast walk ended.
-//   piece_write_kernel  one lane per piece: walks from its entry writing its frames' slots.
+//                       from e_i reaches a position of the guessed walk the two coincide.  e_i is
+//                       usually g_i itself or on the listed walk (a false candidate that survives
+//                       has merged into the true chain); otherwise the walk from e_i steps through
+//                       HBM until it meets a listed position (the wave holds them all and checks
+//                       each step with one ballot), or to the piece end if it never does.  The
+//                       result never depends on the guess -- a bad guess only costs those steps.
+//                       Per piece: entry, frame count, first slot and the steps before the merge;
+//                       per segment: where the fast walk ended.
+//   piece_write_kernel  one wave per piece: the frames before the merge walked from the entry, the
+//                       rest expanded from the list (a wave prefix sum of lengths, 64 frames per
+//                       store), or -- list incomplete -- walked from the entry.
 //   segment_walk_kernel (resume pass) takes each deferred segment from where the fast walk ended,
 //                       with the full decodeEntry / verifyTerminator rules (usually the terminator).
 // A frame is taken by the pieces only if it passes the fast loop's checks (non-zero first byte,
 // varint of <= 4 bytes, frame within maxOpSize and EOF, header more than 8 bytes before EOF), the
 // frames the serial walk accepts without its rule-by-rule step; everything else is the resume
-// pass's.  Integer byte work, no MFMA: the guess pass streams 1/4 of the bytes through LDS, the
+// pass's.  Integer byte work, no MFMA: the guess pass streams 1/8 of the bytes through LDS, the
 // walks touch one header per frame.
 constexpr uint32_t kPiece = 131072;      // bytes per piece
-constexpr uint32_t kGuessWin = 32768;    // bytes of a piece the guess pass looks at
+constexpr uint32_t kGuessWin = 16384;    // bytes of a piece the guess pass looks at
 constexpr uint32_t kGuessLds = kGuessWin + 64;
 constexpr int kPieceThreads = 512;
-constexpr uint32_t kHead = 16;
+constexpr uint32_t kList = 1024;         // frame lengths (u16) a guessed walk records
+constexpr uint32_t kListPerLane = kList / 64;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 
 // Frame length of the header v (bytes p..p+3, little-endian) if it passes the fast-path checks,
@@ -584,6 +588,16 @@ __device__ __forceinline__ uint32_t hbm_frame_len(const uint8_t* buf, uint64_t b
     return p + 8 < L ? fast_frame_len(hbm_header(buf, base + p), L - p, max_op) : 0u;
 }
 
+// Inclusive prefix sum over the wave.
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t u = __shfl_up(v, d, 64);
+        v += lane >= d ? u : 0u;
+    }
+    return v;
+}
+
 struct PieceArgs {
     const uint8_t* buf;
     uint64_t buf_len;
@@ -602,9 +616,9 @@ struct PieceArgs {
     uint32_t* piece_seg;         // [piece_cap] segment of each work item (kNone: none)
     unsigned int* n_pieces;      // work items in use
     uint32_t* guess;             // [piece_cap] g (kNone: no survivor)
-    uint4* gwalk;                // [piece_cap] walk from g: {g, count, exit, ended}
-    uint32_t* head;              // [piece_cap][kHead] first positions of that walk (kNone-padded)
-    uint4* walk;                 // [piece_cap] true walk: {entry, count, first slot, 0}
+    uint4* gwalk;                // [piece_cap] walk from g: {g, count, exit, ended | list_ok << 1}
+    uint16_t* plen;              // [piece_cap][kList] frame lengths of that walk
+    uint4* walk;                 // [piece_cap] true walk: {entry, count, first slot, merge steps | kNone}
     uint64_t* resume_pos;        // [n_seg]
     uint32_t* resume_nfr;        // [n_seg]
     uint64_t* scratch_off;
@@ -660,6 +674,7 @@ __global__ __launch_bounds__(kPieceThreads) void piece_guess_kernel(PieceArgs a)
     __shared__ __attribute__((aligned(16))) uint8_t img[kGuessLds];
     __shared__ unsigned int sh_best;
     __shared__ unsigned int sh_zero;  // image index where the all-zero tail of the window starts
+    constexpr uint32_t kPer = (kGuessLds + kPieceThreads * 16 - 1) / (kPieceThreads * 16);
     const int t = threadIdx.x;
     const unsigned int total = *a.n_pieces;
     for (unsigned int w = blockIdx.x; w < total; w += gridDim.x) {
@@ -686,22 +701,29 @@ __global__ __launch_bounds__(kPieceThreads) void piece_guess_kernel(PieceArgs a)
             sh_zero = 0;
         }
         const uint8_t* src = a.buf + base + Bi - o0;
-        unsigned int lastnz = 0;  // 1 + highest image index holding a non-zero byte (this thread)
-        for (uint32_t c = (uint32_t)t * 16u; c < kGuessLds; c += kPieceThreads * 16u) {
-            u32x4s v{0, 0, 0, 0};
-            if (c + 16 <= ilen) {
-                v = *reinterpret_cast<const u32x4s*>(src + c);
-            } else if (c < ilen) {
-                uint32_t wv[4] = {0, 0, 0, 0};
-                for (uint32_t k = 0; c + k < ilen; ++k) wv[k >> 2] |= (uint32_t)src[c + k] << (8 * (k & 3));
-                v = {wv[0], wv[1], wv[2], wv[3]};
-            }
-            *reinterpret_cast<u32x4s*>(img + c) = v;
-            const uint32_t ww[4] = {v.x, v.y, v.z, v.w};
+        u32x4s v[kPer];
 #pragma unroll
-            for (int k = 3; k >= 0; --k)
-                if (ww[k]) {
-                    const unsigned int e = c + 4u * k + 4u - (__builtin_clz(ww[k]) >> 3);
+        for (uint32_t k = 0; k < kPer; ++k) {  // every load in flight before the first LDS store
+            const uint32_t c = ((uint32_t)t + k * kPieceThreads) * 16u;
+            v[k] = u32x4s{0, 0, 0, 0};
+            if (c + 16 <= ilen) v[k] = *reinterpret_cast<const u32x4s*>(src + c);
+        }
+        unsigned int lastnz = 0;  // 1 + highest image index holding a non-zero byte (this thread)
+#pragma unroll
+        for (uint32_t k = 0; k < kPer; ++k) {
+            const uint32_t c = ((uint32_t)t + k * kPieceThreads) * 16u;
+            if (c >= kGuessLds) continue;
+            if (c < ilen && c + 16 > ilen) {
+                uint32_t wv[4] = {0, 0, 0, 0};
+                for (uint32_t b = 0; c + b < ilen; ++b) wv[b >> 2] |= (uint32_t)src[c + b] << (8 * (b & 3));
+                v[k] = {wv[0], wv[1], wv[2], wv[3]};
+            }
+            *reinterpret_cast<u32x4s*>(img + c) = v[k];
+            const uint32_t ww[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+            for (int q = 3; q >= 0; --q)
+                if (ww[q]) {
+                    const unsigned int e = c + 4u * q + 4u - (__builtin_clz(ww[q]) >> 3);
                     lastnz = e > lastnz ? e : lastnz;
                     break;
                 }
@@ -710,7 +732,7 @@ __global__ __launch_bounds__(kPieceThreads) void piece_guess_kernel(PieceArgs a)
         if (lastnz) atomicMax(&sh_zero, lastnz);
         __syncthreads();
         const uint32_t zpos = sh_zero >= o0 ? Bi + sh_zero - o0 : Bi;  // segment position
-        const uint32_t gm0 = a.seg_gmax[s] * 4u;
+        const uint32_t gm0 = a.seg_gmax[s] * 2u;
         const uint32_t gmax = gm0 < 1024u ? 1024u : gm0 > kGuessWin ? kGuessWin : gm0;
         const uint32_t ncand = We - Bi < 4u * gmax ? We - Bi : 4u * gmax;
         // rounds of kPieceThreads candidate starts until one survives
@@ -726,8 +748,8 @@ __global__ __launch_bounds__(kPieceThreads) void piece_guess_kernel(PieceArgs a)
                 const uint32_t q = p - Bi + o0;
                 const uint32_t lo = *reinterpret_cast<const uint32_t*>(img + (q & ~3u));
                 const uint32_t hi = *reinterpret_cast<const uint32_t*>(img + (q & ~3u) + 4);
-                const uint32_t v = (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * (q & 3)));
-                const uint32_t fl = fast_frame_len(v, L - p, a.max_op);
+                const uint32_t hv = (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * (q & 3)));
+                const uint32_t fl = fast_frame_len(hv, L - p, a.max_op);
                 if (fl == 0) {  // the fast walk ends here: a terminator if the rest is zero
                     surv = p >= zpos;
                     break;
@@ -753,8 +775,8 @@ __global__ __launch_bounds__(256) void piece_walk_kernel(PieceArgs a) {
         const uint32_t s = a.piece_seg[w];
         if (s == kNone) continue;
         const uint32_t g = a.guess[w];
-        uint32_t* hd = a.head + (uint64_t)w * kHead;
-        uint32_t cnt = 0, p = g, ended = 0;
+        uint16_t* pl = a.plen + (uint64_t)w * kList;
+        uint32_t cnt = 0, p = g, ended = 0, lok = 1;
         if (g != kNone) {
             const uint64_t base = a.seg_off[s];
             const uint32_t L = (uint32_t)a.seg_len[s];
@@ -766,18 +788,19 @@ __global__ __launch_bounds__(256) void piece_walk_kernel(PieceArgs a) {
                     ended = 1;
                     break;
                 }
-                if (cnt < kHead) hd[cnt] = p;
+                if (cnt < kList) {
+                    pl[cnt] = (uint16_t)fl;
+                    lok &= fl < 65536u ? 1u : 0u;
+                }
                 ++cnt;
                 p += fl;
             }
         }
-        for (uint32_t k = cnt; k < kHead; ++k) hd[k] = kNone;
-        a.gwalk[w] = make_uint4(g, cnt, p, ended);
+        a.gwalk[w] = make_uint4(g, cnt, p, ended | (lok << 1));
     }
 }
 
-// One wave per segment: the true chain through the pieces (see above).  Control is wave-uniform;
-// lane k < kHead holds head position k of the piece being resolved.
+// One wave per segment: the true chain through the pieces (see above).  Control is wave-uniform.
 __global__ __launch_bounds__(64) void piece_stitch_kernel(PieceArgs a) {
     const uint64_t s = blockIdx.x;
     if (s >= a.n_seg || a.seg_status[s] != kDeferred) return;
@@ -794,34 +817,55 @@ __global__ __launch_bounds__(64) void piece_stitch_kernel(PieceArgs a) {
         const uint32_t nc = np - c0 < 64 ? np - c0 : 64;
         uint4 gr = make_uint4(kNone, 0, 0, 0);
         if ((uint32_t)lane < nc) gr = a.gwalk[pf + c0 + lane];
-        uint4 out = make_uint4(0, 0, 0, 0);
+        uint4 out = make_uint4(0, 0, 0, kNone);
         for (uint32_t j = 0; j < nc && !done; ++j) {
             const uint32_t w = pf + c0 + j;
             uint32_t Bi, Bn;
             piece_bounds(pd, L, c0 + j, Bi, Bn);
             if (e >= Bn) {  // a frame spans this piece: nothing starts in it
-                if ((uint32_t)lane == j) out = make_uint4(e, 0, total, 0);
+                if ((uint32_t)lane == j) out = make_uint4(e, 0, total, kNone);
                 continue;
             }
             const uint32_t g = __builtin_amdgcn_readlane(gr.x, j);
             uint32_t cnt = __builtin_amdgcn_readlane(gr.y, j);
             uint32_t x = __builtin_amdgcn_readlane(gr.z, j);
-            uint32_t ended = __builtin_amdgcn_readlane(gr.w, j);
+            const uint32_t gfl = __builtin_amdgcn_readlane(gr.w, j);
+            uint32_t ended = gfl & 1u, msteps = 0;
             if (g != e) {
-                // Walk from the true entry until it meets the guessed walk's head (then the rest
-                // of the piece is the guessed walk: m steps + the guessed frames from there on),
-                // the piece end, or the end of the fast walk; past kHead steps without meeting it,
-                // finish the piece alone.
-                const uint32_t hv = (g != kNone && (uint32_t)lane < kHead) ? a.head[(uint64_t)w * kHead + lane] : kNone;
+                // The guessed walk's listed positions: lane l holds frames [16 l, 16 l + 16).
+                const uint32_t nl = (g != kNone && (gfl & 2u)) ? (cnt < kList ? cnt : kList) : 0u;
+                uint32_t pos[kListPerLane];
+                uint32_t run = 0;
+                const uint16_t* pl = a.plen + (uint64_t)w * kList + (uint32_t)lane * kListPerLane;
+#pragma unroll
+                for (uint32_t k = 0; k < kListPerLane; ++k) {
+                    const uint32_t idx = (uint32_t)lane * kListPerLane + k;
+                    pos[k] = run;
+                    run += idx < nl ? (uint32_t)pl[k] : 0u;
+                }
+                const uint32_t incl = wave_incl_scan(run, lane);
+                const uint32_t off = g + incl - run;
+#pragma unroll
+                for (uint32_t k = 0; k < kListPerLane; ++k) pos[k] = (uint32_t)lane * kListPerLane + k < nl ? off + pos[k] : kNone;
+                const uint32_t last = nl ? g + __builtin_amdgcn_readlane(incl, 63) : 0u;  // end of the listed part
+                // Walk from the true entry until it meets a listed position (then the rest of the
+                // piece is the guessed walk from that frame on), passes the listed part, or ends.
                 uint32_t p = e, m = 0;
                 bool met = false;
                 ended = 0;
                 while (p < Bn) {
-                    const uint64_t hit = __builtin_amdgcn_ballot_w64(hv == p);
-                    if (m < kHead && hit) {
-                        cnt = m + cnt - (uint32_t)__builtin_ctzll(hit);  // x, ended: the guessed walk's
-                        met = true;
-                        break;
+                    if (p < last) {
+                        uint32_t jl = kNone;
+#pragma unroll
+                        for (uint32_t k = 0; k < kListPerLane; ++k)
+                            if (pos[k] == p) jl = (uint32_t)lane * kListPerLane + k;
+                        const uint64_t hit = __builtin_amdgcn_ballot_w64(jl != kNone);
+                        if (hit) {
+                            const uint32_t jj = __builtin_amdgcn_readlane(jl, __builtin_ctzll(hit));
+                            cnt = m + cnt - jj;  // x, ended: the guessed walk's
+                            met = true;
+                            break;
+                        }
                     }
                     const uint32_t fl = hbm_frame_len(a.buf, base, p, L, a.max_op);
                     if (fl == 0) {
@@ -834,8 +878,10 @@ __global__ __launch_bounds__(64) void piece_stitch_kernel(PieceArgs a) {
                 if (!met) {
                     cnt = m;
                     x = p;
+                    msteps = kNone;
                 } else {
-                    ended = __builtin_amdgcn_readlane(gr.w, j);
+                    ended = gfl & 1u;
+                    msteps = m;
                 }
             }
             if (total + cnt > a.cap) {  // the slot capacity ends inside this piece: serial from e
@@ -844,7 +890,7 @@ __global__ __launch_bounds__(64) void piece_stitch_kernel(PieceArgs a) {
                 done = true;
                 break;
             }
-            if ((uint32_t)lane == j) out = make_uint4(e, cnt, total, 0);
+            if ((uint32_t)lane == j) out = make_uint4(e, cnt, total, msteps);
             total += cnt;
             if (ended) {
                 rpos = x;
@@ -856,7 +902,7 @@ __global__ __launch_bounds__(64) void piece_stitch_kernel(PieceArgs a) {
         }
         if ((uint32_t)lane < nc) a.walk[pf + c0 + lane] = out;
         if (done)
-            for (uint32_t k = c0 + 64 + lane; k < np; k += 64) a.walk[pf + k] = make_uint4(0, 0, 0, 0);
+            for (uint32_t k = c0 + 64 + lane; k < np; k += 64) a.walk[pf + k] = make_uint4(0, 0, 0, kNone);
     }
     if (!done) {  // unreachable (a header within 8 bytes of EOF ends every fast walk); be exact anyway
         rpos = e;
@@ -868,18 +914,50 @@ __global__ __launch_bounds__(64) void piece_stitch_kernel(PieceArgs a) {
     }
 }
 
-// One lane per piece: the piece's frames into the segment's slots.
+// One wave per piece: the piece's frames into the segment's slots (see above).
 __global__ __launch_bounds__(256) void piece_write_kernel(PieceArgs a) {
     const unsigned int total = *a.n_pieces;
-    for (unsigned int w = blockIdx.x * blockDim.x + threadIdx.x; w < total; w += gridDim.x * blockDim.x) {
+    const int lane = threadIdx.x & 63;
+    const unsigned int nwaves = gridDim.x * (blockDim.x >> 6);
+    for (unsigned int w = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); w < total; w += nwaves) {
         const uint32_t s = a.piece_seg[w];
-        if (s == kNone) continue;
+        if (s == kNone) continue;  // wave-uniform
         const uint4 r = a.walk[w];
         if (r.y == 0) continue;
         const uint64_t base = a.seg_off[s];
         const uint32_t L = (uint32_t)a.seg_len[s];
         uint64_t* so = a.scratch_off + s * (uint64_t)a.cap + r.z;
         uint32_t* sl = a.scratch_len + s * (uint64_t)a.cap + r.z;
+        const uint4 gw = a.gwalk[w];
+        const uint32_t m = r.w;
+        if (m != kNone && (gw.w & 2u) && gw.y <= kList) {
+            // frames [0, m): walked from the entry; [m, count): list entries [jj, gcnt)
+            if (lane == 0) {
+                uint32_t p = r.x;
+                for (uint32_t k = 0; k < m; ++k) {
+                    const uint32_t fl = hbm_frame_len(a.buf, base, p, L, a.max_op);
+                    so[k] = base + p;
+                    sl[k] = fl;
+                    p += fl;
+                }
+            }
+            const uint32_t jj = gw.y - (r.y - m);
+            const uint16_t* pl = a.plen + (uint64_t)w * kList;
+            uint32_t run = gw.x;  // position of list entry c
+            for (uint32_t c = 0; c < gw.y; c += 64) {
+                const uint32_t idx = c + (uint32_t)lane;
+                const uint32_t len = idx < gw.y ? (uint32_t)pl[idx] : 0u;
+                const uint32_t incl = wave_incl_scan(len, lane);
+                if (idx >= jj && idx < gw.y) {
+                    const uint32_t k = m + idx - jj;
+                    so[k] = base + run + incl - len;
+                    sl[k] = len;
+                }
+                run += __builtin_amdgcn_readlane(incl, 63);
+            }
+            continue;
+        }
+        if (lane != 0) continue;
         uint32_t p = r.x;
         for (uint32_t k = 0; k < r.y; ++k) {
             const uint32_t fl = hbm_frame_len(a.buf, base, p, L, a.max_op);
@@ -941,11 +1019,11 @@ int rh_segments_launch_impl(rh_ctx* ctx, const rh_segments* g, hipStream_t strea
     const int cus = ctx && ctx->num_cus > 0 ? ctx->num_cus : 256;
     uint64_t grid = g->n_seg < (uint64_t)cus * 8 ? g->n_seg : (uint64_t)cus * 8;
     // Piece-pass scratch (stream-ordered, from the context's pool): per segment 24 B, per piece
-    // 36 + 4 kHead B.  piece_cap bounds the pieces of non-overlapping segments; segments beyond it
+    // 40 + 2 kList B.  piece_cap bounds the pieces of non-overlapping segments; segments beyond it
     // walk serially.
     const uint64_t n_seg = g->n_seg;
     const uint64_t piece_cap = g->buf_len / kPiece + n_seg + 1;
-    const size_t bytes = (size_t)piece_cap * (40 + 4 * kHead) + (size_t)n_seg * 24 + 64;
+    const size_t bytes = (size_t)piece_cap * (40 + 2 * kList) + (size_t)n_seg * 24 + 64;
     void* scratch = nullptr;
     RH_HIP(rh::pool_alloc(ctx, &scratch, bytes, stream));
     uint8_t* sp = static_cast<uint8_t*>(scratch);
@@ -961,7 +1039,7 @@ int rh_segments_launch_impl(rh_ctx* ctx, const rh_segments* g, hipStream_t strea
     pa.n_pieces = reinterpret_cast<unsigned int*>(pa.resume_nfr + n_seg);
     pa.piece_seg = reinterpret_cast<uint32_t*>(pa.n_pieces + 4);
     pa.guess = pa.piece_seg + piece_cap;
-    pa.head = pa.guess + piece_cap;
+    pa.plen = reinterpret_cast<uint16_t*>(pa.guess + piece_cap);
     pa.buf = g->buf;
     pa.buf_len = g->buf_len;
     pa.seg_off = g->seg_off;
@@ -990,7 +1068,8 @@ int rh_segments_launch_impl(rh_ctx* ctx, const rh_segments* g, hipStream_t strea
     RH_HIP(hipGetLastError());
     hipLaunchKernelGGL(piece_stitch_kernel, dim3((uint32_t)n_seg), dim3(64), 0, stream, pa);
     RH_HIP(hipGetLastError());
-    hipLaunchKernelGGL(piece_write_kernel, dim3((uint32_t)wgrid), dim3(256), 0, stream, pa);
+    const uint64_t pgrid = (piece_cap + 3) / 4 < (uint64_t)cus * 8 ? (piece_cap + 3) / 4 : (uint64_t)cus * 8;
+    hipLaunchKernelGGL(piece_write_kernel, dim3((uint32_t)pgrid), dim3(256), 0, stream, pa);
     RH_HIP(hipGetLastError());
     // 6. the deferred segments' ends (terminator check, rule-by-rule steps) and serial leftovers
     a.bail_min = 0;
