@@ -289,7 +289,8 @@ def ragged_read_path(ctx, args, rank, stream, barrier, max_over_ranks, sum_over_
     out = {"workload": f"{n} x 32 MiB segments/GPU, frames of 64-2048 B ({nf} frames/GPU, {rs.corrupted.size} corrupted)",
            "framing_GBps": round(tot / (max_over_ranks(scan_ms) * 1e-3) / 1e9, 1), "ms_framing": round(scan_ms, 4),
            "framing_note": ("serial walk of the first window, then piece-parallel framing (128 KiB pieces: LDS guess "
-                            "over 32 KiB, lane walks over HBM headers, stitch, slot writes), resume pass"),
+                            "over 16 KiB, lane walks over HBM headers recording frame lengths, stitch by list merge, "
+                            "list expansion into the slots), resume pass"),
            "read_launch_GBps": round(tot / (max_over_ranks(rl_ms) * 1e-3) / 1e9, 1), "ms_read_launch": round(rl_ms, 4),
            "parity_ok": bool(frame_ok and rl_ok and orc_ok),
            "parity_check": "frame table == generator's, mismatch set == planted set, CRCs == stamped, 2 segments == oracle reader",

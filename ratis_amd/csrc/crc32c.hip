@@ -175,7 +175,7 @@ __device__ __forceinline__ uint32_t fold_word_perm(const uint32_t* lds, uint32_t
 //     folding slot i): a window's data is consumed two windows after its load was issued, and
 //     every wait in the loop is a counted vmcnt(N);
 //   * the frame table is staged per block in batches of 512 frames into LDS (one drain per batch),
-//     group g of the block taking frames g, g+64, ... of the batch;
+//     and each 16-lane group takes the batch's next frame whenever it finishes one;
 //   * the trailer for VERIFY comes from the last window's own chunk (one extra dword per lane), so
 //     the verify needs no dependent byte loads; the group's lane 15 (whose chunk ends at the CRC
 //     span's end) finalises the frame;
@@ -210,6 +210,7 @@ __global__ __launch_bounds__(kCrcThreads) void crc_frames_kernel(FrameArgs a) {
     uint8_t* mfl = reinterpret_cast<uint8_t*>(mlc + kBatch);
     uint16_t* slow = reinterpret_cast<uint16_t*>(mfl + kBatch);  // [kBatch] guarded-path frames
     uint32_t* nslow = reinterpret_cast<uint32_t*>(slow + kBatch);
+    uint32_t* nexti = nslow + 1;  // next batch frame to hand out (dynamic assignment)
     auto meta = [&](uint32_t j) { return Meta{mo[j], mlc[j], mfl[j]}; };
     for (int i = threadIdx.x; i < kSliceBytes / 4; i += blockDim.x) {
         const int region = i >> 14, e = (i >> 6) & 255, half = (i >> 5) & 1;
@@ -233,7 +234,10 @@ __global__ __launch_bounds__(kCrcThreads) void crc_frames_kernel(FrameArgs a) {
     for (uint64_t b0f = (uint64_t)blockIdx.x * kBatch; b0f < a.n; b0f += (uint64_t)gridDim.x * kBatch) {
         const uint32_t nb = (uint32_t)(a.n - b0f < (uint64_t)kBatch ? a.n - b0f : (uint64_t)kBatch);
         __syncthreads();  // previous batch done with meta / slow
-        if (t == 0) *nslow = 0;
+        if (t == 0) {
+            *nslow = 0;
+            *nexti = 0;
+        }
         __syncthreads();
         if ((uint32_t)t < nb) {
             const uint64_t f = b0f + (uint64_t)t;
@@ -257,20 +261,28 @@ __global__ __launch_bounds__(kCrcThreads) void crc_frames_kernel(FrameArgs a) {
         }
         __syncthreads();
 
-        // ---- fast path: group grp walks the windows of batch frames grp, grp + 64, ... ----
+        // ---- fast path: each group walks the windows of the frames it takes from the batch ----
         struct Task {
             uint32_t j;   // batch-local frame (>= nb: none)
             uint32_t wi;  // window
         };
-        auto skip = [&](uint32_t j) {  // next fast-path frame at or after j (stride 64)
-            while (j < nb && mfl[j] != 0) j += 64;
-            return j;
+        // Frames are handed out dynamically: a group that finishes a frame takes the batch's next
+        // fast-path frame (one LDS atomic by the group's lane 0, broadcast to its 16 lanes), so
+        // groups stay balanced when frame lengths differ.  Control is uniform within a group.
+        auto grab = [&]() -> uint32_t {
+            uint32_t j;
+            do {
+                uint32_t v = 0;
+                if (gl == 0) v = atomicAdd(nexti, 1u);
+                j = (uint32_t)__shfl((int)v, lane & ~(Q - 1));
+            } while (j < nb && mfl[j] != 0);
+            return j < nb ? j : nb;
         };
         auto next = [&](Task x) {
             if (x.j >= nb) return x;
             const uint32_t nw = (mlc[x.j] + (uint32_t)W - 1) / (uint32_t)W;
             if (x.wi + 1 < nw) return Task{x.j, x.wi + 1};
-            return Task{skip(x.j + 64), 0u};
+            return Task{grab(), 0u};
         };
         // chunk of lane gl in task x: [be - S, be), be = E - (nw - 1 - wi) W - (Q - 1 - gl) S
         auto load = [&](Task x, uint32_t (&dd)[18]) {
@@ -372,7 +384,7 @@ __global__ __launch_bounds__(kCrcThreads) void crc_frames_kernel(FrameArgs a) {
                 R = 0;
             }
         };
-        Task T0{a.buf_len >= 128 ? skip(grp) : nb, 0u};  // tiny buffers: every frame is guarded
+        Task T0{a.buf_len >= 128 ? grab() : nb, 0u};  // tiny buffers: every frame is guarded
         Task T1 = next(T0);
         Task T2 = next(T1);
         uint32_t d0[18], d1[18], d2[18];
