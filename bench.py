@@ -45,6 +45,8 @@ def parse():
     p.add_argument("--groups-per-gpu", type=int, default=1_000_000)
     p.add_argument("--rotate", type=int, default=8)
     p.add_argument("--gap", type=int, default=-1)
+    p.add_argument("--layout", choices=["tiled", "plain"], default="tiled",
+                   help="commit tiers in the tiled (AoSoA, rh_commit_soa.tile_stride) or plain SoA layout")
     p.add_argument("--crc-segments", type=int, default=256, help="32 MiB segments per GPU (0 = skip CRC)")
     p.add_argument("--crc-steps", type=int, default=20)
     p.add_argument("--ragged-segments", type=int, default=256,
@@ -139,6 +141,19 @@ class _producers:
         if self._pool:
             self._lib.bp_destroy(self._pool)
             self._pool = None
+
+
+class HostShift:
+    """A workload.HostTier with every index column translated by d (the rotating batches)."""
+
+    def __init__(self, h, d):
+        self.follower, self.flush, self.commit, self.term_start = h.follower + d, h.flush + d, h.commit + d, h.term_start + d
+        self.conf = h.conf
+
+
+def out_col(t, name):
+    """An output column of a plain (CommitTier) or tiled (TiledCommitTier) commit tier."""
+    return t.column(name) if hasattr(t, "column") else getattr(t, name)
 
 
 def delta_streaming(ctx, host, steps: int = 12, fill_threads: int = 16) -> dict:
@@ -345,24 +360,24 @@ def main():
     n_mine = int(mine.sum())
     host = workload.commit_snapshot(n_mine, joint_frac=0.10, peers=5, seed=workload.SEED + 1000 * rank)
     alg_bytes = sum(h.algorithmic_bytes() for h in host)      # per launch (per batch)
-    base = [workload.to_device(h, device=dev, gap_threshold=args.gap) for h in host]
     # R rotating batches: batch r = batch 0 translated by r * 2^44 (every index column and the
     # term start).  The commit arithmetic is translation-equivariant, so batch r's results are
     # batch 0's + r * 2^44 (INT64_MIN stays for empty groups) -- checked after the timed loop.
     SHIFT = 1 << 44
-    batches = []
-    for r in range(args.rotate):
+
+    def make_batch(r, layout):
         tiers = []
-        for b in base:
-            def sh(x):
-                return x + r * SHIFT
-            t = engine.CommitTier(follower_index=sh(b.follower_index).contiguous(), self_index=sh(b.self_index),
-                                  conf=b.conf.clone(), commit_in=sh(b.commit_in), term_start=sh(b.term_start),
-                                  gap_threshold=args.gap)
-            t.alloc_outputs(mode=_lib.RH_MODE_COMMIT)
+        for h in host:
+            d = r * SHIFT
+            if layout == "tiled":
+                t = engine.TiledCommitTier.from_arrays(h.follower + d, h.flush + d, h.conf, h.commit + d,
+                                                       h.term_start + d, device=dev, gap_threshold=args.gap)
+            else:
+                t = workload.to_device(HostShift(h, d), device=dev, gap_threshold=args.gap)
+                t.alloc_outputs(mode=_lib.RH_MODE_COMMIT)
             tiers.append(t)
-        batches.append(tiers)
-    del base
+        return tiers
+    batches = [make_batch(r, args.layout) for r in range(args.rotate)]
     torch.cuda.synchronize()
 
     stream = torch.cuda.current_stream()
@@ -394,8 +409,8 @@ def main():
                                    term_start=h.term_start))
     for r, tiers in enumerate(batches[: min(args.rotate, args.steps)]):
         for h, t, ref in zip(host, tiers, ref0):
-            got_c = t.commit_out.cpu().numpy()
-            got_m = t.min_out.cpu().numpy()
+            got_c = out_col(t, "commit_out").cpu().numpy()
+            got_m = out_col(t, "min_out").cpu().numpy()
             want_m = np.where(ref["min"] == np.iinfo(np.int64).min, ref["min"], ref["min"] + r * SHIFT)
             check_ok &= bool(np.array_equal(got_c, ref["commit"] + r * SHIFT) and np.array_equal(got_m, want_m))
     advanced = 0
@@ -408,7 +423,7 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": (round(pmc["commit_bytes_per_unit"] * n_mine) if "commit_bytes_per_unit" in pmc else None),
                 "traffic_source": pmc.get("_path"),
-                "kernel": "commit_kernel_rank (fused stable F=4 + joint F=6 tiers)",
+                "kernel": f"commit_kernel_rank (fused stable F=4 + joint F=6 tiers, {args.layout} layout)",
                 "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": round(kern_ms, 5)}
 
     # ------------------------------------------------------------------ PCIe-inclusive commit
@@ -420,7 +435,7 @@ def main():
                        for k, v in (("f", h.follower), ("s", h.flush), ("c", h.commit), ("t", h.term_start),
                                     ("w", h.conf.view(np.int32)))})
         outs = [torch.empty(h.n, dtype=torch.int64).pin_memory() for h in host]
-        tiers = batches[0]
+        tiers = make_batch(0, "plain")
         reps = 5
         torch.cuda.synchronize()
         pa = torch.cuda.Event(enable_timing=True)
@@ -675,8 +690,8 @@ def main():
         for r in range(min(args.rotate, args.steps)):
             for h, t, ref in zip(host, batches[r], ref0):
                 want_m = np.where(ref["min"] == np.iinfo(np.int64).min, ref["min"], ref["min"] + r * SHIFT)
-                fused_ok &= bool(np.array_equal(t.commit_out.cpu().numpy(), ref["commit"] + r * SHIFT)
-                                 and np.array_equal(t.min_out.cpu().numpy(), want_m))
+                fused_ok &= bool(np.array_equal(out_col(t, "commit_out").cpu().numpy(), ref["commit"] + r * SHIFT)
+                                 and np.array_equal(out_col(t, "min_out").cpu().numpy(), want_m))
             for (ts, conf, lin), t in zip(lease_inputs, lbatches[r]):
                 ref = orc.lease_soa(ts, conf, lin, NOW, TIMEOUT_MS)
                 nw = (t.n + 63) // 64
@@ -785,6 +800,7 @@ def main():
                                "updateCommit + updateCommitIndex per group",
                    "groups_per_gpu": args.groups_per_gpu, "groups_this_job": total_groups, "peers": 5,
                    "joint_fraction": 0.10, "gap_threshold": args.gap, "rotating_batches": args.rotate,
+                   "layout": args.layout,
                    "sharding": f"RaftGroupId UUID.hashCode() floorMod {n_gpus}"},
         "roofline": roofline,
         "cpu_baseline": cpu,

@@ -135,7 +135,17 @@ typedef struct rh_commit_soa {
     unsigned long long* adv_count; /* single counter, shared by all tiers of a launch OK        */
     uint64_t adv_cap;
     uint64_t adv_row_base;         /* added to each row written to adv_rows (tier slot offset)   */
+    uint64_t tile_stride;          /* 0: every column is a plain array over the groups.  Else the
+                                      TILED layout: groups come in tiles of RH_TILE_GROUPS, every
+                                      per-group column (follower_index .. max_out) holds its 128
+                                      elements of a tile contiguously at its pointer + tile *
+                                      tile_stride bytes, and follower column k lies col_stride
+                                      elements after column 0 within the tile (col_stride >= 128).
+                                      tile_stride is a multiple of 16; every column must cover
+                                      ceil(n / 128) whole tiles.  One wave then reads one
+                                      contiguous run per tile instead of F + 4 separate ones.    */
 } rh_commit_soa;
+#define RH_TILE_GROUPS 128u
 
 #define RH_MAX_TIERS 4
 

@@ -85,6 +85,7 @@ class RhCommitSoa(ctypes.Structure):
         ("adv_count", c_void_p),
         ("adv_cap", c_uint64),
         ("adv_row_base", c_uint64),
+        ("tile_stride", c_uint64),
     ]
 
 

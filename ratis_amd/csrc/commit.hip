@@ -8,9 +8,11 @@
 //   RaftLogBase.updateCommitIndex         RaftLogBase.java:121-142
 // and, in WATCH mode, LeaderStateImpl.commitIndexChanged (LeaderStateImpl.java:612-622).
 //
-// Per-group arithmetic: commit_eval.h.  Layout: one struct-of-arrays "tier" per follower-slot count F.  Every column is a contiguous
-// int64 array over the tier's groups, so a wave's loads of one column are one coalesced
-// 1 KiB request (2 groups per lane, 16 B per lane).  The order statistics over <= F+1 voters are
+// Per-group arithmetic: commit_eval.h.  Layout: one struct-of-arrays "tier" per follower-slot
+// count F, either plain (every column a contiguous int64 array over the tier's groups) or tiled
+// (tiles of 128 groups holding 128 elements of every column back to back, so one wave's loads
+// are one contiguous run); either way a wave's load of one column is one coalesced 1 KiB request
+// (2 groups per lane, 16 B per lane).  The order statistics over <= F+1 voters are
 // integer compare/select work in registers -- rank masks for F <= 6 (commit_kernel_rank), a
 // Batcher merge-exchange network for wider tiers (commit_kernel_net) -- no MFMA (this is not a
 // contraction).  The kernel is HBM-bound: 8(F+1)+20 bytes read and 16 bytes written per group.
@@ -26,10 +28,20 @@ constexpr int kGroupsPerLane = 2;      // 16-byte loads per column per lane
 struct TierArgs {
     rh_commit_soa t;
     uint64_t stride;        // elements between follower columns
+    uint64_t tile64;        // tiled layout: int64 elements between tiles (0 = plain columns)
+    uint64_t tile32;        // tiled layout: uint32 elements between tiles
     uint32_t block_begin;   // first block of this tier in the launch
     uint32_t n_blocks;
     bool vec_ok;            // every column 16-byte aligned: full tiles use 16-byte loads
 };
+
+// Element index of group r in a per-group column: plain (r) or tiled (tile * tile elems + r % 128).
+__device__ __forceinline__ uint64_t ix64(const TierArgs& ta, uint64_t r) {
+    return ta.tile64 ? (r >> 7) * ta.tile64 + (r & 127u) : r;
+}
+__device__ __forceinline__ uint64_t ix32(const TierArgs& ta, uint64_t r) {
+    return ta.tile32 ? (r >> 7) * ta.tile32 + (r & 127u) : r;
+}
 
 struct LaunchArgs {
     TierArgs tier[RH_MAX_TIERS];
@@ -60,22 +72,23 @@ template <int F, bool VEC, bool NT = false>
 __device__ __forceinline__ void load_sub(const TierArgs& ta, uint64_t r0, bool commit_mode, SubTile<F>& st) {
     const rh_commit_soa& t = ta.t;
     if (VEC) {
+        const uint64_t e = ix64(ta, r0), e32 = ix32(ta, r0);  // r0 even: e, e + 1 in one tile
 #pragma unroll
         for (int k = 0; k < F; ++k) {
-            const v2i64 x = ld16<NT, v2i64>(t.follower_index + (uint64_t)k * ta.stride + r0);
+            const v2i64 x = ld16<NT, v2i64>(t.follower_index + (uint64_t)k * ta.stride + e);
             st.fv[0][k] = x.x;
             st.fv[1][k] = x.y;
         }
-        const v2i64 s = ld16<NT, v2i64>(t.self_index + r0);
+        const v2i64 s = ld16<NT, v2i64>(t.self_index + e);
         st.self[0] = s.x;
         st.self[1] = s.y;
-        const v2u32 c = NT ? __builtin_nontemporal_load(reinterpret_cast<const v2u32*>(t.conf + r0))
-                           : *reinterpret_cast<const v2u32*>(t.conf + r0);
+        const v2u32 c = NT ? __builtin_nontemporal_load(reinterpret_cast<const v2u32*>(t.conf + e32))
+                           : *reinterpret_cast<const v2u32*>(t.conf + e32);
         st.w[0] = c.x;
         st.w[1] = c.y;
         if (commit_mode) {
-            const v2i64 ci = ld16<NT, v2i64>(t.commit_in + r0);
-            const v2i64 ts = ld16<NT, v2i64>(t.term_start + r0);
+            const v2i64 ci = ld16<NT, v2i64>(t.commit_in + e);
+            const v2i64 ts = ld16<NT, v2i64>(t.term_start + e);
             st.cin[0] = ci.x;
             st.cin[1] = ci.y;
             st.tstart[0] = ts.x;
@@ -88,12 +101,13 @@ __device__ __forceinline__ void load_sub(const TierArgs& ta, uint64_t r0, bool c
         for (int g = 0; g < 2; ++g) {
             const uint64_t r = r0 + g;
             const bool in = r < t.n;
+            const uint64_t e = ix64(ta, r);
 #pragma unroll
-            for (int k = 0; k < F; ++k) st.fv[g][k] = in ? t.follower_index[(uint64_t)k * ta.stride + r] : 0;
-            st.self[g] = in ? t.self_index[r] : 0;
-            st.w[g] = in ? t.conf[r] : 0u;  // rows past n: inactive padding
-            st.cin[g] = (in && commit_mode) ? t.commit_in[r] : 0;
-            st.tstart[g] = (in && commit_mode) ? t.term_start[r] : 0;
+            for (int k = 0; k < F; ++k) st.fv[g][k] = in ? t.follower_index[(uint64_t)k * ta.stride + e] : 0;
+            st.self[g] = in ? t.self_index[e] : 0;
+            st.w[g] = in ? t.conf[ix32(ta, r)] : 0u;  // rows past n: inactive padding
+            st.cin[g] = (in && commit_mode) ? t.commit_in[e] : 0;
+            st.tstart[g] = (in && commit_mode) ? t.term_start[e] : 0;
         }
     }
 }
@@ -138,19 +152,21 @@ __device__ __forceinline__ void compute_store_sub(const TierArgs& ta, uint64_t w
 
     // ---- stores ----
     if (VEC) {
-        if (commit_mode) st16<NTS>(t.commit_out + r0, cout[0], cout[1]);
-        if (t.min_out) st16<NTS>(t.min_out + r0, mn[0], mn[1]);
-        if (t.maj_out) st16<NTS>(t.maj_out + r0, mj[0], mj[1]);
-        if (t.max_out) st16<NTS>(t.max_out + r0, mx[0], mx[1]);
+        const uint64_t e = ix64(ta, r0);
+        if (commit_mode) st16<NTS>(t.commit_out + e, cout[0], cout[1]);
+        if (t.min_out) st16<NTS>(t.min_out + e, mn[0], mn[1]);
+        if (t.maj_out) st16<NTS>(t.maj_out + e, mj[0], mj[1]);
+        if (t.max_out) st16<NTS>(t.max_out + e, mx[0], mx[1]);
     } else {
 #pragma unroll
         for (int g = 0; g < 2; ++g) {
             const uint64_t r = r0 + g;
             if (r < t.n) {
-                if (commit_mode) t.commit_out[r] = cout[g];
-                if (t.min_out) t.min_out[r] = mn[g];
-                if (t.maj_out) t.maj_out[r] = mj[g];
-                if (t.max_out) t.max_out[r] = mx[g];
+                const uint64_t e = ix64(ta, r);
+                if (commit_mode) t.commit_out[e] = cout[g];
+                if (t.min_out) t.min_out[e] = mn[g];
+                if (t.maj_out) t.maj_out[e] = mj[g];
+                if (t.max_out) t.max_out[e] = mx[g];
             }
         }
     }
@@ -266,6 +282,8 @@ void build_args(const rh_commit_soa* tiers, int n_tiers, int flo, int fhi, Launc
         TierArgs& ta = args.tier[args.n_tiers++];
         ta.t = t;
         ta.stride = t.col_stride ? t.col_stride : t.n;
+        ta.tile64 = t.tile_stride / 8;
+        ta.tile32 = t.tile_stride / 4;
         ta.block_begin = (uint32_t)blocks;
         ta.n_blocks = (uint32_t)((t.n + kTile - 1) / kTile);
         const bool cm = t.mode == RH_MODE_COMMIT;
@@ -329,8 +347,12 @@ int validate(const rh_commit_soa* tiers, int n_tiers) {
         if (t.n == 0) continue;
         if (!t.follower_index || !t.self_index || !t.conf)
             return rh::fail(RH_E_INVAL, "rh_commit_soa_launch: follower_index/self_index/conf required");
-        if (t.col_stride != 0 && t.col_stride < t.n)
+        if (t.tile_stride == 0 && t.col_stride != 0 && t.col_stride < t.n)
             return rh::fail(RH_E_INVAL, "rh_commit_soa_launch: col_stride < n");
+        if (t.tile_stride != 0 && (t.tile_stride % 16 != 0 || t.col_stride < RH_TILE_GROUPS ||
+                                   t.tile_stride < 8ull * RH_TILE_GROUPS))
+            return rh::fail(RH_E_INVAL, "rh_commit_soa_launch: tiled layout needs tile_stride % 16 == 0, "
+                                        "tile_stride >= 1024 and col_stride >= 128");
         if (t.mode == RH_MODE_COMMIT && (!t.commit_in || !t.term_start || !t.commit_out))
             return rh::fail(RH_E_INVAL, "rh_commit_soa_launch: COMMIT needs commit_in, term_start, commit_out");
         if (t.mode == RH_MODE_COMMIT && t.gap_threshold < -1)

@@ -23,7 +23,7 @@ from __future__ import annotations
 
 import ctypes
 from dataclasses import dataclass, field
-from typing import Optional, Sequence
+from typing import List, Optional, Sequence
 
 import torch
 
@@ -172,7 +172,95 @@ class CommitTier:
         return s
 
 
-def commit_launch(ctx: Context, tiers: Sequence[CommitTier], mode: int = RH_MODE_COMMIT,
+@dataclass
+class TiledCommitTier:
+    """A commit tier in the TILED layout of ``rh_commit_soa.tile_stride``: one int64 HBM buffer of
+    ceil(n / 128) tiles.  A tile holds, for its 128 groups, the F follower columns, self_index,
+    commit_in, term_start, commit_out, min_out (and maj_out, max_out with ``levels``), 128 int64
+    each, then the 128 uint32 membership words -- so a wave's loads are one contiguous run per
+    tile.  Rows past n in the last tile are padding (never evaluated).  Bit columns stay plain."""
+
+    n: int
+    n_followers: int
+    buf: torch.Tensor               # int64 [n_tiles, tile_elems]
+    levels: bool = False
+    gap_threshold: int = -1
+    valid_bits: Optional[torch.Tensor] = None
+    advanced_bits: Optional[torch.Tensor] = None
+
+    @staticmethod
+    def columns(F: int, levels: bool) -> List[str]:
+        return [f"f{k}" for k in range(F)] + ["self", "commit_in", "term_start", "commit_out", "min_out"] + \
+            (["maj_out", "max_out"] if levels else [])
+
+    @classmethod
+    def tile_elems(cls, F: int, levels: bool) -> int:
+        return len(cls.columns(F, levels)) * 128 + 64  # + 128 uint32 conf words
+
+    @classmethod
+    def from_arrays(cls, follower, self_index, conf, commit_in, term_start, device="cuda", gap_threshold: int = -1,
+                    levels: bool = False) -> "TiledCommitTier":
+        import numpy as np
+        F, n = follower.shape
+        nt = (n + 127) // 128
+        cols = cls.columns(F, levels)
+        te = cls.tile_elems(F, levels)
+        host = np.zeros((nt, te), dtype=np.int64)
+
+        def put(name, a):
+            c = cols.index(name)
+            pad = np.zeros(nt * 128, dtype=np.int64)
+            pad[:n] = a
+            host[:, c * 128:(c + 1) * 128] = pad.reshape(nt, 128)
+        for k in range(F):
+            put(f"f{k}", follower[k])
+        put("self", self_index)
+        put("commit_in", commit_in)
+        put("term_start", term_start)
+        cw = np.zeros(nt * 128, dtype=np.uint32)
+        cw[:n] = conf
+        host[:, len(cols) * 128:] = cw.reshape(nt, 128).view(np.int64)
+        t = cls(n=n, n_followers=F, buf=torch.from_numpy(host).to(device), levels=levels,
+                gap_threshold=gap_threshold)
+        nw = (n + 63) // 64
+        t.valid_bits = torch.zeros(nw, dtype=torch.int64, device=device)
+        t.advanced_bits = torch.zeros(nw, dtype=torch.int64, device=device)
+        return t
+
+    def column(self, name: str) -> torch.Tensor:
+        """Column ``name`` over the n groups (a gathered copy)."""
+        c = self.columns(self.n_followers, self.levels).index(name)
+        return self.buf[:, c * 128:(c + 1) * 128].reshape(-1)[:self.n]
+
+    def to_struct(self, mode: int) -> RhCommitSoa:
+        cols = self.columns(self.n_followers, self.levels)
+        base = self.buf.data_ptr()
+
+        def at(name):
+            return base + cols.index(name) * 128 * 8
+        s = RhCommitSoa()
+        s.n = self.n
+        s.n_followers = self.n_followers
+        s.mode = mode
+        s.gap_threshold = self.gap_threshold if mode == RH_MODE_COMMIT else -1
+        s.follower_index = at("f0")
+        s.col_stride = 128
+        s.self_index = at("self")
+        s.commit_in = at("commit_in")
+        s.term_start = at("term_start")
+        s.conf = base + len(cols) * 128 * 8
+        s.commit_out = at("commit_out") if mode == RH_MODE_COMMIT else None
+        s.min_out = at("min_out")
+        if self.levels:
+            s.maj_out = at("maj_out")
+            s.max_out = at("max_out")
+        s.valid_bits = _ptr(self.valid_bits)
+        s.advanced_bits = _ptr(self.advanced_bits) if mode == RH_MODE_COMMIT else None
+        s.tile_stride = self.buf.shape[1] * 8
+        return s
+
+
+def commit_launch(ctx: Context, tiers: Sequence, mode: int = RH_MODE_COMMIT,
                   stream: Optional[torch.cuda.Stream] = None) -> None:
     """Enqueues one fused commit kernel over up to RH_MAX_TIERS tiers (asynchronous)."""
     if not 1 <= len(tiers) <= _lib.RH_MAX_TIERS:

@@ -141,6 +141,13 @@ def to_device(tier: HostTier, device="cuda", gap_threshold: int = -1):
                       term_start=t(tier.term_start), gap_threshold=gap_threshold)
 
 
+def to_device_tiled(tier: HostTier, device="cuda", gap_threshold: int = -1, levels: bool = False):
+    """HostTier -> engine.TiledCommitTier (the AoSoA layout of rh_commit_soa.tile_stride)."""
+    from .engine import TiledCommitTier
+    return TiledCommitTier.from_arrays(tier.follower, tier.flush, tier.conf, tier.commit, tier.term_start,
+                                       device=device, gap_threshold=gap_threshold, levels=levels)
+
+
 # ------------------------------------------------------------------------------------------
 # Config 5: SegmentedRaftLog segments of fixed-size frames, synthesized in HBM
 # ------------------------------------------------------------------------------------------

@@ -103,7 +103,13 @@ def main():
                 tiers.append(t.alloc_outputs())
             batches.append(tiers)
         xs = [timed(lambda i=0: engine.commit_launch(ctx, batches[i % 8]), alg, 40) for _ in range(a.rounds)]
-        report("commit", xs, median_Gupd_s=round(float(np.median(xs)) * 1e9 / alg * 1e6 / 1e9, 2))
+        report("commit", xs, layout="plain", median_Gupd_s=round(float(np.median(xs)) * 1e9 / alg * 1e6 / 1e9, 2))
+        del batches
+        batches = [[engine.TiledCommitTier.from_arrays(h.follower + (r << 44), h.flush + (r << 44), h.conf,
+                                                       h.commit + (r << 44), h.term_start + (r << 44)) for h in host]
+                   for r in range(8)]
+        xs = [timed(lambda i=0: engine.commit_launch(ctx, batches[i % 8]), alg, 40) for _ in range(a.rounds)]
+        report("commit", xs, layout="tiled", median_Gupd_s=round(float(np.median(xs)) * 1e9 / alg * 1e6 / 1e9, 2))
         del batches
     if "lease" in only:
         now, ms, tmo = 1 << 60, 1_000_000, 100

@@ -86,6 +86,7 @@ int main(void) {
   F(rh_commit_soa, min_out) F(rh_commit_soa, maj_out) F(rh_commit_soa, max_out) F(rh_commit_soa, valid_bits)
   F(rh_commit_soa, advanced_bits) F(rh_commit_soa, adv_rows) F(rh_commit_soa, adv_commit)
   F(rh_commit_soa, adv_count) F(rh_commit_soa, adv_cap) F(rh_commit_soa, adv_row_base)
+  F(rh_commit_soa, tile_stride)
   F(rh_frames, buf) F(rh_frames, buf_len) F(rh_frames, frame_off) F(rh_frames, frame_len) F(rh_frames, n)
   F(rh_frames, init_state) F(rh_frames, reserved) F(rh_frames, crc_out) F(rh_frames, bad_bits) F(rh_frames, n_bad)
   F(rh_delta, slot) F(rh_delta, column) F(rh_delta, op) F(rh_delta, reserved) F(rh_delta, value)

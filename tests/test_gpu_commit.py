@@ -285,3 +285,56 @@ def test_malformed_conf_words_raw_launch(ctx, orc, F):
     assert not got["valid"][bad].any()
     assert np.array_equal(got["commit"][bad], commit[bad])
     assert got["valid"][~bad].any()
+
+
+@pytest.mark.parametrize("F", [1, 2, 4, 6, 7, 11, 14])
+def test_tiled_layout(ctx, orc, F):
+    """rh_commit_soa.tile_stride (AoSoA tiles of 128 groups) gives the plain layout's results:
+    both gap settings, COMMIT and WATCH (levels), a ragged last tile."""
+    import torch
+
+    from ratis_amd import engine
+    rng = np.random.default_rng(700 + F)
+    n = 128 * 37 + 45
+    follower, flush, conf, commit, ts = _random_case(rng, F, n)
+    for mode, gap in ((0, -1), (0, 9), (1, -1)):
+        t = engine.TiledCommitTier.from_arrays(follower, flush, conf, commit, ts, gap_threshold=gap, levels=True)
+        engine.commit_launch(ctx, [t], mode=mode)
+        torch.cuda.synchronize()
+        ref = orc.commit_soa(follower, flush, conf, mode=mode, gap=gap,
+                             commit_in=commit if mode == 0 else None, term_start=ts if mode == 0 else None)
+        assert np.array_equal(_bits(t.valid_bits.cpu().numpy(), n), _bits(ref["valid_bits"], n))
+        for col, key in (("min_out", "min"), ("maj_out", "maj"), ("max_out", "max")):
+            assert np.array_equal(t.column(col).cpu().numpy(), ref[key]), col
+        if mode == 0:
+            assert np.array_equal(t.column("commit_out").cpu().numpy(), ref["commit"])
+            assert np.array_equal(_bits(t.advanced_bits.cpu().numpy(), n), _bits(ref["advanced_bits"], n))
+        # the inputs are untouched (outputs live in their own columns of each tile)
+        assert np.array_equal(t.column("self").cpu().numpy(), flush)
+
+
+def test_tiled_layout_config3_full_size(ctx, orc):
+    """BASELINE config 3 (1M groups x 5 peers, 10 % joint: an F=4 and an F=6 tier in one launch)
+    in the tiled layout, every group against the oracle."""
+    import torch
+
+    from ratis_amd import engine, workload
+    host = workload.commit_snapshot(1_000_000, joint_frac=0.10, peers=5, seed=workload.SEED + 3)
+    tiers = [workload.to_device_tiled(h) for h in host]
+    engine.commit_launch(ctx, tiers)
+    torch.cuda.synchronize()
+    for h, t in zip(host, tiers):
+        ref = orc.commit_soa(h.follower, h.flush, h.conf, mode=0, gap=-1, commit_in=h.commit, term_start=h.term_start)
+        assert np.array_equal(t.column("commit_out").cpu().numpy(), ref["commit"])
+        assert np.array_equal(t.column("min_out").cpu().numpy(), ref["min"])
+
+
+def test_tiled_layout_rejects_bad_strides(ctx):
+    from ratis_amd import _lib, engine
+    rng = np.random.default_rng(5)
+    t = engine.TiledCommitTier.from_arrays(*_random_case(rng, 4, 300))
+    s = t.to_struct(0)
+    for field, bad in (("tile_stride", s.tile_stride + 8), ("col_stride", 64), ("tile_stride", 512)):
+        arr = (_lib.RhCommitSoa * 1)(t.to_struct(0))
+        setattr(arr[0], field, bad)
+        assert _lib.load().rh_commit_soa_launch(ctx.handle, arr, 1, None) == _lib.RH_E_INVAL
