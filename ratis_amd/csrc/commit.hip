@@ -125,7 +125,7 @@ __device__ __forceinline__ void st16(int64_t* p, int64_t a, int64_t b) {
 
 template <int F, bool VEC, bool RANK = false, bool NTS = false>
 __device__ __forceinline__ void compute_store_sub(const TierArgs& ta, uint64_t wbase, bool commit_mode,
-                                                  const SubTile<F>& st) {
+                                                  const SubTile<F>& st, uint64_t (&bits)[2][8]) {
     constexpr int N = F + 1;
     const rh_commit_soa& t = ta.t;
     const int lane = threadIdx.x & 63;
@@ -172,25 +172,24 @@ __device__ __forceinline__ void compute_store_sub(const TierArgs& ta, uint64_t w
     }
 
     // ---- per-wave bit words: bit j of word (wbase/64 + h) is row wbase + 64h + j ----
-    const uint64_t ve = __ballot(valid[0]), vo = __ballot(valid[1]);
-    const uint64_t ae = __ballot(adv[0]), ao = __ballot(adv[1]);
-    if (wbase < t.n) {
-        // ballots are wave-uniform: interleave them on the scalar unit, then lanes 0/1 store
-        const uint64_t word = wbase >> 6;
-        const uint64_t nwords = (t.n + 63) >> 6;
-        if (t.valid_bits) {
-            const uint64_t w0 = spread32(ve) | (spread32(vo) << 1);
-            const uint64_t w1 = spread32(ve >> 32) | (spread32(vo >> 32) << 1);
-            if (lane < 2 && word + lane < nwords) t.valid_bits[word + lane] = lane ? w1 : w0;
-        }
-        if (t.advanced_bits) {
-            const uint64_t w0 = spread32(ae) | (spread32(ao) << 1);
-            const uint64_t w1 = spread32(ae >> 32) | (spread32(ao >> 32) << 1);
-            if (lane < 2 && word + lane < nwords) t.advanced_bits[word + lane] = lane ? w1 : w0;
+    // Lane p fetches the 2 rows of lane 32h + p/2 (one ds_bpermute per word) and keeps row p & 1,
+    // so one ballot per word and column yields the word directly (no scalar bit interleave: the
+    // scalar unit is shared by the CU's waves).  Staged in LDS; run_tile stores the block's words.
+    const int wave = threadIdx.x >> 6;
+    if (t.valid_bits || t.advanced_bits) {
+        const int packed = (valid[0] ? 1 : 0) | (valid[1] ? 2 : 0) | (adv[0] ? 4 : 0) | (adv[1] ? 8 : 0);
+        const int lo = __shfl(packed, lane >> 1), hi = __shfl(packed, 32 + (lane >> 1));
+        const int sel = lane & 1;
+        const uint64_t v0 = __ballot((lo >> sel) & 1), v1 = __ballot((hi >> sel) & 1);
+        const uint64_t a0 = __ballot((lo >> (2 + sel)) & 1), a1 = __ballot((hi >> (2 + sel)) & 1);
+        if (lane < 2) {
+            bits[0][2 * wave + lane] = lane ? v1 : v0;
+            bits[1][2 * wave + lane] = lane ? a1 : a0;
         }
     }
 
     // ---- compacted advanced list: one atomic per wave ----
+    const uint64_t ae = t.adv_rows ? __ballot(adv[0]) : 0ull, ao = t.adv_rows ? __ballot(adv[1]) : 0ull;
     if (t.adv_rows && (ae | ao)) {
         const uint32_t cnt = __popcll(ae) + __popcll(ao);
         unsigned long long base = 0;
@@ -211,23 +210,34 @@ __device__ __forceinline__ void compute_store_sub(const TierArgs& ta, uint64_t w
     }
 }
 
-// One wave = one 128-group sub-tile: all loads of the tile are issued before any compute.
+// One wave = one 128-group sub-tile: all loads of the tile are issued before any compute.  The
+// block's bit words (8 per column) leave through LDS in one 64-byte store per column.
 template <int F, bool RANK, bool NT, bool NTS>
 __device__ __forceinline__ void run_tile(const TierArgs& ta, uint64_t tile) {
     constexpr uint64_t kWaveGroups = 128;
+    __shared__ uint64_t bits[2][8];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const uint64_t wchunk = tile * (kWaveGroups * (kBlock / 64)) + (uint64_t)wave * kWaveGroups;
     const bool commit_mode = ta.t.mode == RH_MODE_COMMIT;
-    if (wchunk >= ta.t.n) return;
-    const bool full = wchunk + kWaveGroups <= ta.t.n && ta.vec_ok;
-    SubTile<F> st;
-    if (full) {
-        load_sub<F, true, NT>(ta, wchunk + 2 * lane, commit_mode, st);
-        compute_store_sub<F, true, RANK, NTS>(ta, wchunk, commit_mode, st);
-    } else {
-        load_sub<F, false>(ta, wchunk + 2 * lane, commit_mode, st);
-        compute_store_sub<F, false, RANK>(ta, wchunk, commit_mode, st);
+    if (wchunk < ta.t.n) {
+        const bool full = wchunk + kWaveGroups <= ta.t.n && ta.vec_ok;
+        SubTile<F> st;
+        if (full) {
+            load_sub<F, true, NT>(ta, wchunk + 2 * lane, commit_mode, st);
+            compute_store_sub<F, true, RANK, NTS>(ta, wchunk, commit_mode, st, bits);
+        } else {
+            load_sub<F, false>(ta, wchunk + 2 * lane, commit_mode, st);
+            compute_store_sub<F, false, RANK>(ta, wchunk, commit_mode, st, bits);
+        }
+    }
+    if (!ta.t.valid_bits && !ta.t.advanced_bits) return;  // block-uniform
+    __syncthreads();
+    if (threadIdx.x < 16) {
+        const int col = threadIdx.x >> 3, k = threadIdx.x & 7;
+        uint64_t* dst = col ? ta.t.advanced_bits : ta.t.valid_bits;
+        const uint64_t word = tile * 8 + (uint64_t)k;
+        if (dst && word < ((ta.t.n + 63) >> 6)) dst[word] = bits[col][k];
     }
 }
 
@@ -271,13 +281,23 @@ __global__ __launch_bounds__(kBlock) void commit_kernel_net(const LaunchArgs a) 
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
-// Kernel arguments for the tiers whose F lies in [flo, fhi].
+// Kernel arguments for the tiers whose F lies in [flo, fhi].  Blocks go to the widest tiers first:
+// a joint-consensus tier (two confs, 7 voters) costs several times a stable tier's compute per
+// group, and its blocks dispatched last were the launch's tail (config 3: 17.2 -> 16.1 us).
 void build_args(const rh_commit_soa* tiers, int n_tiers, int flo, int fhi, LaunchArgs& args, uint64_t& blocks) {
     constexpr uint64_t kTile = (uint64_t)kBlock * kGroupsPerLane;  // groups per workgroup
     args = LaunchArgs{};
     blocks = 0;
-    for (int i = 0; i < n_tiers; ++i) {
-        const rh_commit_soa& t = tiers[i];
+    int order[RH_MAX_TIERS];
+    for (int i = 0; i < n_tiers; ++i) order[i] = i;
+    for (int i = 1; i < n_tiers; ++i)  // stable insertion sort by descending width
+        for (int j = i; j > 0 && tiers[order[j]].n_followers > tiers[order[j - 1]].n_followers; --j) {
+            const int x = order[j];
+            order[j] = order[j - 1];
+            order[j - 1] = x;
+        }
+    for (int oi = 0; oi < n_tiers; ++oi) {
+        const rh_commit_soa& t = tiers[order[oi]];
         if ((int)t.n_followers < flo || (int)t.n_followers > fhi || t.n == 0) continue;
         TierArgs& ta = args.tier[args.n_tiers++];
         ta.t = t;

@@ -185,6 +185,7 @@ class TiledCommitTier:
     buf: torch.Tensor               # int64 [n_tiles, tile_elems]
     levels: bool = False
     gap_threshold: int = -1
+    min_out: bool = True             # request the watch-ALL level column
     valid_bits: Optional[torch.Tensor] = None
     advanced_bits: Optional[torch.Tensor] = None
 
@@ -199,7 +200,7 @@ class TiledCommitTier:
 
     @classmethod
     def from_arrays(cls, follower, self_index, conf, commit_in, term_start, device="cuda", gap_threshold: int = -1,
-                    levels: bool = False) -> "TiledCommitTier":
+                    levels: bool = False, bits: bool = True) -> "TiledCommitTier":
         import numpy as np
         F, n = follower.shape
         nt = (n + 127) // 128
@@ -222,9 +223,10 @@ class TiledCommitTier:
         host[:, len(cols) * 128:] = cw.reshape(nt, 128).view(np.int64)
         t = cls(n=n, n_followers=F, buf=torch.from_numpy(host).to(device), levels=levels,
                 gap_threshold=gap_threshold)
-        nw = (n + 63) // 64
-        t.valid_bits = torch.zeros(nw, dtype=torch.int64, device=device)
-        t.advanced_bits = torch.zeros(nw, dtype=torch.int64, device=device)
+        if bits:
+            nw = (n + 63) // 64
+            t.valid_bits = torch.zeros(nw, dtype=torch.int64, device=device)
+            t.advanced_bits = torch.zeros(nw, dtype=torch.int64, device=device)
         return t
 
     def column(self, name: str) -> torch.Tensor:
@@ -250,7 +252,7 @@ class TiledCommitTier:
         s.term_start = at("term_start")
         s.conf = base + len(cols) * 128 * 8
         s.commit_out = at("commit_out") if mode == RH_MODE_COMMIT else None
-        s.min_out = at("min_out")
+        s.min_out = at("min_out") if self.min_out else None
         if self.levels:
             s.maj_out = at("maj_out")
             s.max_out = at("max_out")
