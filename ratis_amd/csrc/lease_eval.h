@@ -189,8 +189,17 @@ inline int build_lease_args(const rh_lease_soa* tiers, int n_tiers, int flo, int
                             uint64_t& blocks) {
     a = LeaseLaunch{};
     blocks = 0;
-    for (int i = 0; i < n_tiers; ++i) {
-        const rh_lease_soa& t = tiers[i];
+    // blocks to the widest tiers first (their per-group work is the launch's tail otherwise)
+    int order[RH_MAX_TIERS];
+    for (int i = 0; i < n_tiers; ++i) order[i] = i;
+    for (int i = 1; i < n_tiers; ++i)
+        for (int j = i; j > 0 && tiers[order[j]].n_followers > tiers[order[j - 1]].n_followers; --j) {
+            const int x = order[j];
+            order[j] = order[j - 1];
+            order[j - 1] = x;
+        }
+    for (int oi = 0; oi < n_tiers; ++oi) {
+        const rh_lease_soa& t = tiers[order[oi]];
         if (t.n == 0 || (int)t.n_followers < flo || (int)t.n_followers > fhi) continue;
         const bool vec = (t.n_followers == 0 || t.col_stride % 2 == 0) &&
                          (t.n_followers == 0 || ((uintptr_t)t.follower_ts & 15) == 0) &&

@@ -73,16 +73,10 @@ def main():
     else:
         host = workload.commit_snapshot(1_000_000)
         batches = []
-        for r in range(8):
-            tiers = []
-            for h in host:
-                t = workload.to_device(h)
-                t.follower_index += r << 44
-                t.self_index += r << 44
-                t.commit_in += r << 44
-                t.term_start += r << 44
-                tiers.append(t.alloc_outputs())
-            batches.append(tiers)
+        for r in range(8):  # the bench's default layout: tiled (rh_commit_soa.tile_stride)
+            d = r << 44
+            batches.append([engine.TiledCommitTier.from_arrays(h.follower + d, h.flush + d, h.conf, h.commit + d,
+                                                               h.term_start + d) for h in host])
         torch.cuda.synchronize()
         for i in range(a.iters):
             engine.commit_launch(ctx, batches[i % 8])
