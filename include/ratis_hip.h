@@ -284,9 +284,31 @@ int rh_watch_levels(rh_groups* g, const rh_watch_event** out_events, uint64_t* o
  * columns beyond a slot's tier read -1.  Blocks. */
 #define RH_COL_CONF       ((uint8_t)34u)
 #define RH_COL_TERM_START ((uint8_t)35u)
+/* Lease columns (readable, and writable through deltas: RH_OP_SET = Timestamp/AtomicBoolean set,
+ * RH_OP_MAX = the later timestamp / OR of the flag).  A new or re-armed slot starts with the lease
+ * disabled, no lease and no follower timestamps (INT64_MIN: never active) -- see rh_group_lease_start. */
+#define RH_COL_LEASE      ((uint8_t)36u)         /* LeaderLease.lease (System.nanoTime nanos, LL:38)   */
+#define RH_COL_LEASE_ON   ((uint8_t)37u)         /* LeaderLease.enabled 0/1 (LL:37; getAndSetEnabled,
+                                                    LSI:478, 744, 1042, 1226)                           */
+#define RH_COL_TS(k)      ((uint8_t)(48u + (k))) /* follower k lastRespondedAppendEntriesSendTime (nanos,
+                                                    FII:236-243; LogAppenderDefault.java:102)           */
 int rh_groups_read(rh_groups* g, uint32_t first, uint32_t n, uint8_t column, int64_t* out);
 /* Follower width of the tier a slot lives in (0 = stopped), for tests and diagnostics. */
 int rh_group_tier(rh_groups* g, uint32_t slot, uint32_t* out_width);
+
+/* ---- leader lease on the resident table (LeaderStateImpl.hasLease LSI:1229-1249, LeaderLease) --
+ * A started slot's LeaderLease (new with the LeaderStateImpl, LSI:388): lease = now, enabled as
+ * given, and every follower slot of its tier stamped with now (a new FollowerInfoImpl's
+ * lastRpcTime, FII:58).  Queued like deltas (after the calls before it).  Later responses arrive
+ * as RH_COL_TS(k) deltas; a follower added by rh_group_reconf starts unstamped until its delta. */
+int rh_group_lease_start(rh_groups* g, uint32_t slot, int64_t now_nanos, int enabled);
+/* hasLease() of every started slot at now_nanos (isRunning() && isReady() stay with the caller):
+ * if the lease is enabled and not valid, LeaderLease.extend from the followers' timestamps (majority
+ * of the current and old confs active within timeout_ms -> lease = the earliest majority-ack time),
+ * stored in the table.  *out_bits: library-owned pinned bitmap, bit s = slot s has the lease, valid
+ * until the next rh_lease_batch; *out_words = ceil(capacity / 64).  Blocks. */
+int rh_lease_batch(rh_groups* g, int64_t now_nanos, int64_t timeout_ms, const uint64_t** out_bits,
+                   uint64_t* out_words);
 
 /* ---- one RaftServer across several GPUs ---------------------------------------------------
  * A node owns one context and one resident table per device of `device_mask` (bit d = GPU d).
@@ -315,6 +337,10 @@ int rh_node_push_deltas(rh_node* node, const rh_delta* deltas, size_t n);
  * totals).  flags as rh_commit_batch.  Blocks. */
 int rh_node_commit_batch(rh_node* node, uint32_t flags, rh_index_event* advanced, uint64_t adv_cap,
                          uint64_t* n_advanced, rh_index_event* watch_all, uint64_t watch_cap, uint64_t* n_watch_all);
+/* rh_group_lease_start / rh_lease_batch on every shard; bit s of the caller's out_bits (at least
+ * ceil(shards * capacity_per_shard / 64) words) = node slot s has the lease.  Blocks. */
+int rh_node_group_lease_start(rh_node* node, uint32_t node_slot, int64_t now_nanos, int enabled);
+int rh_node_lease_batch(rh_node* node, int64_t now_nanos, int64_t timeout_ms, uint64_t* out_bits, uint64_t out_words);
 
 /* ===================================================================================== */
 /* 2. CRC32C (PureJavaCrc32C) over SegmentedRaftLog frames                               */

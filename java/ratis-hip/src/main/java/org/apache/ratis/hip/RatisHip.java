@@ -45,6 +45,9 @@ public final class RatisHip implements AutoCloseable {
   public static int colFollowerCommit(int followerSlot) { return 16 + followerSlot; }
   public static final int COL_FLUSH = 32;
   public static final int COL_COMMITTED = 33;
+  public static final int COL_LEASE = 36;     // LeaderLease.lease (nanos)
+  public static final int COL_LEASE_ON = 37;  // LeaderLease.enabled (getAndSetEnabled)
+  public static int colTs(int followerSlot) { return 48 + followerSlot; }  // lastRespondedAppendEntriesSendTime
   public static final int OP_MAX = 0;   // RaftLogIndex.updateToMax
   public static final int OP_SET = 1;   // RaftLogIndex.setUnconditionally (setSnapshotIndex)
   public static final int COMMIT_WATCH_ALL = 1;
@@ -123,6 +126,20 @@ public final class RatisHip implements AutoCloseable {
     return watchLevels0(node, shard, slot, min, majority, max, valid);
   }
 
+  // ---- leader lease (LeaderStateImpl.hasLease, LeaderLease) ----------------------------------
+  /** A new LeaderLease for the division (lease = now, enabled per config) with every follower slot
+   * stamped now, as a new LeaderStateImpl creates them (LeaderLease.java:37-38, FollowerInfoImpl.java:58).
+   * Later replies go in as COL_TS deltas (updateLastRespondedAppendEntriesSendTime). */
+  public void leaseStart(int slot, long nowNanos, boolean enabled) throws IOException {
+    leaseStart0(node, slot, nowNanos, enabled);
+  }
+
+  /** hasLease() of every node slot at nowNanos (without isRunning()/isReady()); extended leases
+   * stay in the table.  bits[s / 64] bit s % 64 = slot s; bits.length >= ceil(slots / 64). */
+  public void leaseBatch(long nowNanos, long timeoutMs, long[] bits) throws IOException {
+    leaseBatch0(node, nowNanos, timeoutMs, bits);
+  }
+
   // ---- checksums (SegmentedRaftLogReader.decodeEntry, batched over a segment) ---------------
   /**
    * PCIe-inclusive verification of one segment image held in a direct buffer: every frame's
@@ -156,6 +173,8 @@ public final class RatisHip implements AutoCloseable {
       throws IOException;
   private static native int watchLevels0(long node, int shard, int[] slot, long[] min, long[] majority, long[] max,
       boolean[] valid) throws IOException;
+  private static native void leaseStart0(long node, int slot, long nowNanos, boolean enabled) throws IOException;
+  private static native void leaseBatch0(long node, long nowNanos, long timeoutMs, long[] bits) throws IOException;
   private static native long verifyHost0(long node, int shard, ByteBuffer seg, long len, long[] off, int[] flen,
       int n, int[] crc, long[] bad) throws IOException;
 }

@@ -178,6 +178,22 @@ JNIEXPORT jint JNICALL CLS(watchLevels0)(JNIEnv* env, jclass c, jlong node, jint
     return (jint)n;
 }
 
+JNIEXPORT void JNICALL CLS(leaseStart0)(JNIEnv* env, jclass c, jlong node, jint slot, jlong now, jboolean enabled) {
+    (void)c;
+    check(env, rh_node_group_lease_start(N(node), (uint32_t)slot, (int64_t)now, enabled ? 1 : 0));
+}
+
+JNIEXPORT void JNICALL CLS(leaseBatch0)(JNIEnv* env, jclass c, jlong node, jlong now, jlong timeout_ms,
+                                        jlongArray bits) {
+    (void)c;
+    const jsize n = (*env)->GetArrayLength(env, bits);
+    jlong* b = (*env)->GetLongArrayElements(env, bits, NULL);
+    if (!b) return;
+    const int rc = rh_node_lease_batch(N(node), (int64_t)now, (int64_t)timeout_ms, (uint64_t*)b, (uint64_t)n);
+    (*env)->ReleaseLongArrayElements(env, bits, b, rc < 0 ? JNI_ABORT : 0);
+    check(env, rc);
+}
+
 JNIEXPORT jlong JNICALL CLS(verifyHost0)(JNIEnv* env, jclass c, jlong node, jint shard, jobject seg, jlong len,
                                          jlongArray off, jintArray flen, jint n, jintArray crc, jlongArray bad) {
     (void)c;

@@ -35,6 +35,12 @@ RH_COL_FLUSH = 32
 RH_COL_COMMITTED = 33
 RH_COL_CONF = 34
 RH_COL_TERM_START = 35
+RH_COL_LEASE = 36
+RH_COL_LEASE_ON = 37
+
+
+def RH_COL_TS(k: int) -> int:
+    return 48 + k
 RH_OP_MAX = 0
 RH_OP_SET = 1
 RH_DELTA_SLOT = 1 << 20
@@ -200,6 +206,10 @@ _SIGNATURES = {
     "rh_group_reconf": (c_int, [c_void_p, c_uint32, c_uint32, c_void_p]),
     "rh_group_stop": (c_int, [c_void_p, c_uint32]),
     "rh_group_tier": (c_int, [c_void_p, c_uint32, POINTER(c_uint32)]),
+    "rh_group_lease_start": (c_int, [c_void_p, c_uint32, c_int64, c_int]),
+    "rh_lease_batch": (c_int, [c_void_p, c_int64, c_int64, POINTER(c_void_p), POINTER(c_uint64)]),
+    "rh_node_group_lease_start": (c_int, [c_void_p, c_uint32, c_int64, c_int]),
+    "rh_node_lease_batch": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_uint64]),
     "rh_groups_load": (c_int, [c_void_p, c_uint32, c_uint32, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p,
                                c_void_p, c_void_p]),
     "rh_push_deltas": (c_int, [c_void_p, POINTER(RhDelta), c_size_t]),

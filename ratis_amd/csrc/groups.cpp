@@ -88,6 +88,8 @@ struct rh_groups {
     int ring_next = 0;
     int ring_acquired = -1;
     hipStream_t copy_stream = nullptr;
+    uint64_t* d_lbits = nullptr;  // rh_lease_batch: slot bitmap (device) and its pinned copy
+    uint64_t* h_lbits = nullptr;
     // events
     EvSet ev[kEvSets];
     uint64_t next_ticket = 1;
@@ -123,7 +125,7 @@ int halloc_mapped(T** host, T** dev, size_t count) {
 void free_tier(rh::TableTier& t) {
     for (void* p : {(void*)t.match, (void*)t.fcommit, (void*)t.flush, (void*)t.commit, (void*)t.tstart,
                     (void*)t.conf, (void*)t.row_slot, (void*)t.wall, (void*)t.wmin, (void*)t.wmaj, (void*)t.wmax,
-                    (void*)t.dirty, (void*)t.wdirty})
+                    (void*)t.dirty, (void*)t.wdirty, (void*)t.fts, (void*)t.lease, (void*)t.lon})
         (void)hipFree(p);
     t = rh::TableTier{};
 }
@@ -150,6 +152,8 @@ void free_groups(rh_groups* g) {
     if (g->watch) (void)hipHostFree(g->watch);
     (void)hipFree(g->d_read);
     if (g->copy_stream) (void)hipStreamDestroy(g->copy_stream);
+    (void)hipFree(g->d_lbits);
+    if (g->h_lbits) (void)hipHostFree(g->h_lbits);
 }
 
 // (Re)allocates tier t with `rows` rows, keeping the first `keep` rows' contents.  Blocks (the
@@ -174,6 +178,9 @@ int grow_tier(rh_groups* g, int t, uint32_t rows) {
     if (rc == RH_OK) rc = dalloc(&n.wmax, rows);
     if (rc == RH_OK) rc = dalloc(&n.dirty, rows);
     if (rc == RH_OK) rc = dalloc(&n.wdirty, rows);
+    if (rc == RH_OK) rc = dalloc(&n.fts, F * rows);
+    if (rc == RH_OK) rc = dalloc(&n.lease, rows);
+    if (rc == RH_OK) rc = dalloc(&n.lon, rows);
     if (rc != RH_OK) {
         free_tier(n);
         return rc;
@@ -189,9 +196,11 @@ int grow_tier(rh_groups* g, int t, uint32_t rows) {
     if (e == hipSuccess) e = hipMemsetAsync(n.row_slot, 0xFF, rows * 4, s);
     if (e == hipSuccess) e = hipMemsetAsync(n.dirty, 0, rows, s);
     if (e == hipSuccess) e = hipMemsetAsync(n.wdirty, 0, rows, s);
+    if (e == hipSuccess) e = hipMemsetAsync(n.lon, 0, rows, s);
     for (size_t k = 0; k < F && e == hipSuccess && keep; ++k) {
         e = cp(n.match + k * rows, o.match + k * keep, (size_t)keep * 8);
         if (e == hipSuccess) e = cp(n.fcommit + k * rows, o.fcommit + k * keep, (size_t)keep * 8);
+        if (e == hipSuccess) e = cp(n.fts + k * rows, o.fts + k * keep, (size_t)keep * 8);
     }
     if (keep && e == hipSuccess) {
         const size_t k8 = (size_t)keep * 8, k4 = (size_t)keep * 4;
@@ -206,6 +215,8 @@ int grow_tier(rh_groups* g, int t, uint32_t rows) {
         if (e == hipSuccess) e = cp(n.wmax, o.wmax, k8);
         if (e == hipSuccess) e = cp(n.dirty, o.dirty, keep);
         if (e == hipSuccess) e = cp(n.wdirty, o.wdirty, keep);
+        if (e == hipSuccess) e = cp(n.lease, o.lease, k8);
+        if (e == hipSuccess) e = cp(n.lon, o.lon, keep);
     }
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) {
@@ -385,6 +396,9 @@ RH_EXPORT int rh_groups_create(rh_ctx* ctx, uint64_t capacity, int64_t gap_thres
     }
     if (rc == RH_OK) rc = halloc_mapped(&g->watch, &g->d_watch, capacity);
     if (rc == RH_OK) rc = dalloc(&g->d_counts, 4 * kEvSets + 1);
+    if (rc == RH_OK) rc = dalloc(&g->d_lbits, (capacity + 63) / 64);
+    if (rc == RH_OK && hipHostMalloc(reinterpret_cast<void**>(&g->h_lbits), (capacity + 63) / 64 * 8) != hipSuccess)
+        rc = rh::fail(RH_E_NOMEM, "hipHostMalloc(lease bitmap)");
     if (rc == RH_OK && hipEventCreateWithFlags(&g->ops_free, hipEventDisableTiming) != hipSuccess)
         rc = rh::fail(RH_E_DEVICE, "hipEventCreate(control ops)");
     if (rc == RH_OK && hipStreamSynchronize(s) != hipSuccess) rc = rh::fail(RH_E_DEVICE, "rh_groups_create: sync");
@@ -505,7 +519,10 @@ __global__ void table_load_kernel(rh::TableDev T, int t, const uint32_t* __restr
     for (uint32_t k = 0; k < F; ++k) {
         D.match[k * R + r] = cols[(uint64_t)k * m + i];
         D.fcommit[k * R + r] = cols[(F + k) * m + i];
+        D.fts[k * R + r] = rh::kNoTimestamp;  // lease state as a fresh start: rh_group_lease_start
     }
+    D.lease[r] = rh::kNoTimestamp;
+    D.lon[r] = 0;
     D.flush[r] = cols[(2 * F) * m + i];
     D.commit[r] = cols[(2 * F + 1) * m + i];
     D.tstart[r] = cols[(2 * F + 2) * m + i];
@@ -613,7 +630,8 @@ RH_EXPORT int rh_push_deltas(rh_groups* g, const rh_delta* deltas, size_t n) {
         const uint32_t m = d.slot < g->capacity ? g->slot_map[d.slot] : kNoRow;
         const uint32_t w = m == kNoRow ? 0u : rh::width_of_tier((int)(m >> 28));
         const uint32_t c = d.column;
-        const bool ok_col = c < w || (c >= 16 && c < 16 + w) || c == RH_COL_FLUSH || c == RH_COL_COMMITTED;
+        const bool ok_col = c < w || (c >= 16 && c < 16 + w) || c == RH_COL_FLUSH || c == RH_COL_COMMITTED ||
+                            (c >= 48 && c < 48 + w) || c == RH_COL_LEASE || c == RH_COL_LEASE_ON;
         if (m == kNoRow || !ok_col || d.op > RH_OP_SET)
             return rh::fail(RH_E_INVAL, "rh_push_deltas: delta " + std::to_string(i) +
                                             " names a stopped slot, a column outside its tier or an unknown op");
@@ -763,7 +781,8 @@ RH_EXPORT int rh_groups_read(rh_groups* g, uint32_t first, uint32_t n, uint8_t c
     if ((uint64_t)first + n > g->capacity) return rh::fail(RH_E_INVAL, "rh_groups_read: slots out of range");
     const uint32_t c = column;
     if (!(c < RH_MAX_FOLLOWERS || (c >= 16 && c < 16 + RH_MAX_FOLLOWERS) || c == RH_COL_FLUSH || c == RH_COL_COMMITTED ||
-          c == RH_COL_CONF || c == RH_COL_TERM_START))
+          c == RH_COL_CONF || c == RH_COL_TERM_START || c == RH_COL_LEASE || c == RH_COL_LEASE_ON ||
+          (c >= 48 && c < 48 + RH_MAX_FOLLOWERS)))
         return rh::fail(RH_E_INVAL, "rh_groups_read: unknown column");
     if (n == 0) return RH_OK;
     DeviceGuard dg(g->ctx->device);
@@ -782,6 +801,48 @@ RH_EXPORT int rh_groups_read(rh_groups* g, uint32_t first, uint32_t n, uint8_t c
     if (rc != RH_OK) return rc;
     RH_HIP(hipMemcpyAsync(out, g->d_read, (size_t)n * 8, hipMemcpyDeviceToHost, s));
     RH_HIP(hipStreamSynchronize(s));
+    return RH_OK;
+}
+
+// ---- leader lease ------------------------------------------------------------------------------------
+RH_EXPORT int rh_group_lease_start(rh_groups* g, uint32_t slot, int64_t now_nanos, int enabled) {
+    if (!g) return rh::fail(RH_E_INVAL, "rh_group_lease_start: groups == NULL");
+    if (slot >= g->capacity) return rh::fail(RH_E_INVAL, "rh_group_lease_start: slot out of range");
+    uint32_t width = 0;
+    {
+        std::lock_guard<std::mutex> lk(g->mu);
+        const uint32_t m = g->slot_map[slot];
+        if (m == kNoRow) return rh::fail(RH_E_INVAL, "rh_group_lease_start: slot is stopped");
+        width = rh::width_of_tier((int)(m >> 28));
+    }
+    // LeaderLease(properties): lease = currentTime(), enabled per config (LL:37-38); every
+    // FollowerInfoImpl: lastRespondedAppendEntriesSendTime = lastRpcTime (FII:58) -- as SET deltas,
+    // ordered after the calls before this one
+    rh_delta d[RH_MAX_FOLLOWERS + 2];
+    size_t n = 0;
+    for (uint32_t k = 0; k < width; ++k) d[n++] = rh_delta{slot, RH_COL_TS(k), RH_OP_SET, 0, now_nanos};
+    d[n++] = rh_delta{slot, RH_COL_LEASE, RH_OP_SET, 0, now_nanos};
+    d[n++] = rh_delta{slot, RH_COL_LEASE_ON, RH_OP_SET, 0, enabled ? 1 : 0};
+    return rh_push_deltas(g, d, n);
+}
+
+RH_EXPORT int rh_lease_batch(rh_groups* g, int64_t now_nanos, int64_t timeout_ms, const uint64_t** out_bits,
+                             uint64_t* out_words) {
+    if (!g || !out_bits || !out_words) return rh::fail(RH_E_INVAL, "rh_lease_batch: NULL argument");
+    if (timeout_ms < 0) return rh::fail(RH_E_INVAL, "rh_lease_batch: timeout_ms < 0");
+    DeviceGuard dg(g->ctx->device);
+    std::lock_guard<std::mutex> lk(g->mu);
+    hipStream_t s = g->ctx->stream;
+    int rc = flush_ops(g);
+    if (rc != RH_OK) return rc;
+    const uint64_t words = (g->capacity + 63) / 64;
+    RH_HIP(hipMemsetAsync(g->d_lbits, 0, words * 8, s));
+    rc = rh_table_lease(g->dev, now_nanos, timeout_ms, g->d_lbits, s);
+    if (rc != RH_OK) return rc;
+    RH_HIP(hipMemcpyAsync(g->h_lbits, g->d_lbits, words * 8, hipMemcpyDeviceToHost, s));
+    RH_HIP(hipStreamSynchronize(s));
+    *out_bits = g->h_lbits;
+    *out_words = words;
     return RH_OK;
 }
 
@@ -922,5 +983,36 @@ RH_EXPORT int rh_node_commit_batch(rh_node* nd, uint32_t flags, rh_index_event* 
     }
     *n_advanced = na;
     *n_watch_all = nw;
+    return RH_OK;
+}
+
+RH_EXPORT int rh_node_group_lease_start(rh_node* nd, uint32_t node_slot, int64_t now_nanos, int enabled) {
+    rh_groups* t;
+    uint32_t s;
+    int rc = route(nd, node_slot, &t, &s);
+    return rc != RH_OK ? rc : rh_group_lease_start(t, s, now_nanos, enabled);
+}
+
+RH_EXPORT int rh_node_lease_batch(rh_node* nd, int64_t now_nanos, int64_t timeout_ms, uint64_t* out_bits,
+                                  uint64_t out_words) {
+    if (!nd || !out_bits) return rh::fail(RH_E_INVAL, "rh_node_lease_batch: NULL argument");
+    const uint64_t total = nd->cap * nd->tab.size();
+    if (out_words < (total + 63) / 64) return rh::fail(RH_E_INVAL, "rh_node_lease_batch: out_bits too small");
+    std::memset(out_bits, 0, (total + 63) / 64 * 8);
+    for (size_t sh = 0; sh < nd->tab.size(); ++sh) {
+        const uint64_t* bits = nullptr;
+        uint64_t words = 0;
+        int rc = rh_lease_batch(nd->tab[sh], now_nanos, timeout_ms, &bits, &words);
+        if (rc != RH_OK) return rc;
+        const uint64_t base = sh * nd->cap;  // node slot of the shard's slot 0
+        for (uint64_t w = 0; w < words; ++w) {
+            uint64_t x = bits[w];
+            while (x) {
+                const uint64_t s = w * 64 + (uint64_t)__builtin_ctzll(x);
+                x &= x - 1;
+                if (s < nd->cap) out_bits[(base + s) >> 6] |= 1ull << ((base + s) & 63);
+            }
+        }
+    }
     return RH_OK;
 }

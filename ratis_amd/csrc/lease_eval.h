@@ -52,17 +52,21 @@ __device__ __forceinline__ bool has_majority(uint32_t mask, uint32_t active, boo
 }
 
 // hasLease() for one group (see the file header for the elapsed-time form).
+// `never` (bit k = follower k has no timestamp yet; the resident table's unstamped columns) makes
+// a follower inactive and the oldest: it is never the majority-ack time when extend() runs.
 template <int F>
 __device__ __forceinline__ void lease_one(const rh_lease_soa& t, const int64_t (&ts)[F > 0 ? F : 1], uint32_t w,
-                                          int64_t lin, bool en, bool in, int64_t& lout, bool& has, bool& ext) {
+                                          int64_t lin, bool en, bool in, int64_t& lout, bool& has, bool& ext,
+                                          uint32_t never = 0u) {
     const int64_t now = t.now_nanos;
     const int64_t lim = ms_limit(t.timeout_ms);
     int64_t d[F > 0 ? F : 1];
     uint32_t act = 0;
 #pragma unroll
     for (int k = 0; k < F; ++k) {
-        d[k] = (int64_t)((uint64_t)now - (uint64_t)ts[k]);
-        act |= (ms_below(d[k], lim) ? 1u : 0u) << k;
+        const bool nv = (never >> k) & 1u;
+        d[k] = nv ? INT64_MAX : (int64_t)((uint64_t)now - (uint64_t)ts[k]);
+        act |= (!nv && ms_below(d[k], lim) ? 1u : 0u) << k;
     }
     const uint32_t nm = w & 0x3FFFu, om = (w >> 16) & 0x3FFFu;
     const bool self = (w & RH_CONF_SELF) != 0, self_old = (w & RH_CONF_SELF_OLD) != 0;

@@ -70,7 +70,14 @@ struct TableTier {
     int64_t* wmax = nullptr;
     uint8_t* dirty = nullptr;   // [rows] 1 = updateCommit pending
     uint8_t* wdirty = nullptr;  // [rows] 1 = commitIndexChanged pending
+    int64_t* fts = nullptr;     // [F][rows] FollowerInfo.lastRespondedAppendEntriesSendTime (nanos,
+                                //           kNoTimestamp until the module sets it)
+    int64_t* lease = nullptr;   // [rows] LeaderLease.lease (nanos)
+    uint8_t* lon = nullptr;     // [rows] LeaderLease.enabled
 };
+// A follower column that has no lastRespondedAppendEntriesSendTime yet (a FollowerInfo the module
+// has not stamped): never active, never the majority-ack time.
+constexpr int64_t kNoTimestamp = INT64_MIN;
 
 struct TableDev {
     TableTier tier[kTableTiers];
@@ -135,6 +142,8 @@ int rh_commit_launch_impl(rh_ctx* ctx, const rh_commit_soa* tiers, int n_tiers, 
 int rh_table_apply_deltas(const rh::TableDev& t, const rh_delta* d_deltas, uint64_t n, int phase, hipStream_t stream);
 int rh_table_control(const rh::TableDev& t, const rh::CtrlOp* d_ops, uint64_t n, hipStream_t stream);
 int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev, hipStream_t stream);
+int rh_table_lease(const rh::TableDev& t, int64_t now_nanos, int64_t timeout_ms, uint64_t* d_slot_bits,
+                   hipStream_t stream);
 int rh_table_read(const rh::TableDev& t, uint32_t first, uint32_t n, uint8_t column, int64_t* d_out,
                   hipStream_t stream);
 int rh_crc_launch_impl(rh_ctx* ctx, const rh_frames* f, uint32_t flags, hipStream_t stream);

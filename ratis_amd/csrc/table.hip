@@ -11,6 +11,9 @@
 //   table_commit_kernel   LeaderStateImpl.updateCommit() (COMMIT) or commitIndexChanged() (WATCH)
 //                         over the DIRTY rows of every tier; only changed results become events,
 //                         written straight into host-mapped pinned memory.
+//   table_lease_kernel    LeaderStateImpl.hasLease() (LSI:1229-1249) with LeaderLease.extend (LL:67-84)
+//                         for every started slot: lease_eval.h's arithmetic over the follower
+//                         timestamp columns, the lease stored in place, a slot-indexed bitmap out.
 //   table_read_kernel     slot-ordered read-back of one column.
 //
 // Rows of a tier are laid out exactly like an rh_commit_soa tier (column-major, 16-byte aligned
@@ -18,6 +21,7 @@
 // Integer compare/select work, no MFMA; HBM-bound over the dirty rows.
 #include "rh_internal.h"
 #include "commit_eval.h"
+#include "lease_eval.h"
 
 namespace {
 
@@ -55,7 +59,18 @@ __global__ __launch_bounds__(256) void table_apply_kernel(TableDev T, const rh_d
     int64_t* p = nullptr;
     bool commit_ev = false, watch_ev = false;
     const uint32_t c = x.column;
-    if (c < 16) {
+    if (c == RH_COL_LEASE_ON) {  // AtomicBoolean: SET stores, MAX ORs
+        if (phase == 0)
+            tt->lon[row] = x.value != 0;
+        else if (x.value != 0)
+            tt->lon[row] = 1;
+        return;
+    }
+    if (c >= 48 && c < 64) {
+        if (c - 48 < tt->width) p = tt->fts + (uint64_t)(c - 48) * tt->rows + row;
+    } else if (c == RH_COL_LEASE) {
+        p = tt->lease + row;
+    } else if (c < 16) {
         if (c < tt->width) p = tt->match + (uint64_t)c * tt->rows + row;
         commit_ev = true;
     } else if (c < 32) {
@@ -88,6 +103,7 @@ __global__ __launch_bounds__(256) void table_control_kernel(TableDev T, const Ct
         s.conf[r] = 0u;
         s.dirty[r] = 0;
         s.wdirty[r] = 0;
+        s.lon[r] = 0;
         s.row_slot[r] = rh::kNoRow;
         T.slot_map[op.slot] = rh::kNoRow;
         return;
@@ -99,7 +115,10 @@ __global__ __launch_bounds__(256) void table_control_kernel(TableDev T, const Ct
         for (uint32_t k = 0; k < D.width; ++k) {
             D.match[k * R + r] = -1;   // RaftLog.INVALID_LOG_INDEX (FollowerInfoImpl.java:42-43)
             D.fcommit[k * R + r] = -1;
+            D.fts[k * R + r] = rh::kNoTimestamp;
         }
+        D.lease[r] = rh::kNoTimestamp;  // rh_group_lease_start sets the LeaderLease
+        D.lon[r] = 0;
         D.flush[r] = op.flush;
         D.commit[r] = op.commit;
         D.tstart[r] = op.tstart;
@@ -111,16 +130,18 @@ __global__ __launch_bounds__(256) void table_control_kernel(TableDev T, const Ct
         const TableTier& S = T.tier[op.src >> 28];
         const uint32_t sr = op.src & rh::kRowMask;
         const uint64_t SR = S.rows;
-        int64_t m[RH_MAX_FOLLOWERS], f[RH_MAX_FOLLOWERS];
+        int64_t m[RH_MAX_FOLLOWERS], f[RH_MAX_FOLLOWERS], ts[RH_MAX_FOLLOWERS];
         for (uint32_t k = 0; k < D.width; ++k) {  // read all first: RECONF may permute in place
             const int src = op.map[k];
             const bool keep = src >= 0 && (uint32_t)src < S.width;
             m[k] = keep ? S.match[(uint64_t)src * SR + sr] : -1;
             f[k] = keep ? S.fcommit[(uint64_t)src * SR + sr] : -1;
+            ts[k] = keep ? S.fts[(uint64_t)src * SR + sr] : rh::kNoTimestamp;
         }
         for (uint32_t k = 0; k < D.width; ++k) {
             D.match[k * R + r] = m[k];
             D.fcommit[k * R + r] = f[k];
+            D.fts[k * R + r] = ts[k];
         }
         if (op.kind == rh::kCtrlMove) {
             D.flush[r] = S.flush[sr];
@@ -130,6 +151,9 @@ __global__ __launch_bounds__(256) void table_control_kernel(TableDev T, const Ct
             D.wmin[r] = S.wmin[sr];
             D.wmaj[r] = S.wmaj[sr];
             D.wmax[r] = S.wmax[sr];
+            D.lease[r] = S.lease[sr];
+            D.lon[r] = S.lon[sr];
+            S.lon[sr] = 0;
             S.conf[sr] = 0u;
             S.dirty[sr] = 0;
             S.wdirty[sr] = 0;
@@ -305,6 +329,39 @@ __global__ __launch_bounds__(kTBlock) void table_commit_kernel(TableDev T, TierR
     table_dispatch<FLO, FHI, FLO <= 6, WATCH>(T, t, wbase, ev);
 }
 
+// ---- hasLease over every started row -------------------------------------------------------------
+template <int F>
+__global__ __launch_bounds__(256) void table_lease_kernel(TableTier tt, int64_t now, int64_t timeout_ms,
+                                                          uint64_t* __restrict__ slot_bits) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= tt.rows) return;
+    const uint32_t w = tt.conf[r];
+    if (!(w & RH_CONF_ACTIVE)) return;  // free row
+    int64_t ts[F];
+    uint32_t never = 0;
+#pragma unroll
+    for (int k = 0; k < F; ++k) {
+        ts[k] = tt.fts[(uint64_t)k * tt.rows + r];
+        never |= (ts[k] == rh::kNoTimestamp ? 1u : 0u) << k;
+    }
+    rh_lease_soa t{};
+    t.now_nanos = now;
+    t.timeout_ms = timeout_ms;
+    int64_t lout;
+    bool has, ext;
+    rh_lease::lease_one<F>(t, ts, w, tt.lease[r], tt.lon[r] != 0, true, lout, has, ext, never);
+    if (ext) tt.lease[r] = lout;
+    if (has) {
+        const uint32_t slot = tt.row_slot[r];
+        atomicOr(reinterpret_cast<unsigned long long*>(slot_bits + (slot >> 6)), 1ull << (slot & 63));
+    }
+}
+
+template <int F>
+void launch_lease_width(const TableTier& tt, int64_t now, int64_t timeout_ms, uint64_t* bits, hipStream_t s) {
+    hipLaunchKernelGGL((table_lease_kernel<F>), dim3((tt.rows + 255) / 256), dim3(256), 0, s, tt, now, timeout_ms, bits);
+}
+
 // ---- read-back -------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void table_read_kernel(TableDev T, uint32_t first, uint32_t n, uint32_t column,
                                                          int64_t* __restrict__ out) {
@@ -321,6 +378,9 @@ __global__ __launch_bounds__(256) void table_read_kernel(TableDev T, uint32_t fi
         else if (column == RH_COL_COMMITTED) v = tt->commit[row];
         else if (column == RH_COL_CONF) v = (int64_t)tt->conf[row];
         else if (column == RH_COL_TERM_START) v = tt->tstart[row];
+        else if (column == RH_COL_LEASE) v = tt->lease[row];
+        else if (column == RH_COL_LEASE_ON) v = (int64_t)tt->lon[row];
+        else if (column >= 48 && column < 64) v = column - 48 < tt->width ? tt->fts[(column - 48) * R + row] : rh::kNoTimestamp;
     }
     out[i] = v;
 }
@@ -361,6 +421,26 @@ int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev, 
         } else {
             if (cls == 0) hipLaunchKernelGGL((table_commit_kernel<false, 2, 6>), g, b, 0, stream, t, tr, ev);
             else hipLaunchKernelGGL((table_commit_kernel<false, 8, 14>), g, b, 0, stream, t, tr, ev);
+        }
+        RH_HIP(hipGetLastError());
+    }
+    return RH_OK;
+}
+
+int rh_table_lease(const rh::TableDev& t, int64_t now_nanos, int64_t timeout_ms, uint64_t* d_slot_bits,
+                   hipStream_t stream) {
+    for (int i = 0; i < rh::kTableTiers; ++i) {
+        const TableTier& tt = t.tier[i];
+        if (!tt.rows) continue;
+        switch (tt.width) {
+            case 2: launch_lease_width<2>(tt, now_nanos, timeout_ms, d_slot_bits, stream); break;
+            case 4: launch_lease_width<4>(tt, now_nanos, timeout_ms, d_slot_bits, stream); break;
+            case 6: launch_lease_width<6>(tt, now_nanos, timeout_ms, d_slot_bits, stream); break;
+            case 8: launch_lease_width<8>(tt, now_nanos, timeout_ms, d_slot_bits, stream); break;
+            case 10: launch_lease_width<10>(tt, now_nanos, timeout_ms, d_slot_bits, stream); break;
+            case 12: launch_lease_width<12>(tt, now_nanos, timeout_ms, d_slot_bits, stream); break;
+            case 14: launch_lease_width<14>(tt, now_nanos, timeout_ms, d_slot_bits, stream); break;
+            default: return rh::fail(RH_E_STATE, "rh_lease_batch: unexpected tier width");
         }
         RH_HIP(hipGetLastError());
     }

@@ -239,6 +239,30 @@ class RaftGroupTable:
         ev = _view(ptr.value or 0, n.value, WATCH_EVENT_DTYPE).copy()
         return ev[np.argsort(ev["slot"], kind="stable")]
 
+    # -- leader lease (LeaderStateImpl.hasLease, LeaderLease) ---------------------------------
+    def lease_start(self, slot: int, now_nanos: int, enabled: bool = True) -> None:
+        """A new LeaderLease for ``slot`` (lease = now, enabled) with every follower stamped now."""
+        check(self._lib.rh_group_lease_start(self.handle, int(slot), int(now_nanos), 1 if enabled else 0))
+
+    def update_last_responded(self, slots, follower_slot: int, send_times) -> None:
+        """FollowerInfo.updateLastRespondedAppendEntriesSendTime (a Timestamp set)."""
+        self.push_deltas(slots, _lib.RH_COL_TS(follower_slot), send_times, ops=_lib.RH_OP_SET)
+
+    def set_lease_enabled(self, slots, enabled: bool) -> None:
+        """LeaderLease.getAndSetEnabled (step-down, leader not in the new conf)."""
+        n = np.size(slots)
+        self.push_deltas(slots, _lib.RH_COL_LEASE_ON, np.full(n, 1 if enabled else 0, np.int64), ops=_lib.RH_OP_SET)
+
+    def lease_batch(self, now_nanos: int, timeout_ms: int) -> np.ndarray:
+        """hasLease() (less isRunning()/isReady()) of every slot at now: bool [capacity]; extended
+        leases are stored in the table."""
+        ptr = ctypes.c_void_p()
+        words = ctypes.c_uint64()
+        check(self._lib.rh_lease_batch(self.handle, int(now_nanos), int(timeout_ms), ctypes.byref(ptr),
+                                       ctypes.byref(words)))
+        w = _view(ptr.value, words.value, np.dtype(np.uint64)).copy()
+        return np.unpackbits(w.view(np.uint8), bitorder="little")[: self.capacity].astype(bool)
+
     def read(self, column: int, first: int = 0, n: Optional[int] = None) -> np.ndarray:
         n = self.capacity - first if n is None else n
         out = np.empty(n, dtype=np.int64)
@@ -306,3 +330,13 @@ class RaftNode:
         a = adv[: min(na.value, cap)]
         w = wall[: min(nw.value, cap)]
         return a[np.argsort(a["slot"], kind="stable")], w[np.argsort(w["slot"], kind="stable")]
+
+    def lease_start(self, node_slot: int, now_nanos: int, enabled: bool = True) -> None:
+        check(self._lib.rh_node_group_lease_start(self._h, node_slot, int(now_nanos), 1 if enabled else 0))
+
+    def lease_batch(self, now_nanos: int, timeout_ms: int) -> np.ndarray:
+        """hasLease() of every node slot (bool [n_shards * capacity_per_shard])."""
+        total = self.n_shards * self.capacity_per_shard
+        bits = np.zeros((total + 63) // 64, dtype=np.uint64)
+        check(self._lib.rh_node_lease_batch(self._h, int(now_nanos), int(timeout_ms), _p(bits), bits.size))
+        return np.unpackbits(bits.view(np.uint8), bitorder="little")[:total].astype(bool)
