@@ -51,6 +51,8 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
   private final long tickNanos;
   private volatile boolean watchAll;       // some division has ALL-level watch requests
   private volatile boolean running = true;
+  private volatile long leaseTimeoutMs = -1;  // LeaderLease.leaseTimeoutMs; -1: no lease batches
+  private volatile long[] leaseBits;          // last rh_node_lease_batch: bit = node slot has the lease
 
   @SuppressWarnings("unchecked")
   public HipLeaderBookkeeper(int deviceMask, long capacityPerShard, long gapThreshold, long tickMicros)
@@ -73,6 +75,12 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
 
   public void setWatchAll(boolean enabled) {
     this.watchAll = enabled;
+  }
+
+  /** rpc.timeout.min x read.leader.lease.timeout.ratio (LeaderLease.java:45-48); the pump then
+   * evaluates hasLease() for every division each tick. */
+  public void setLeaseTimeoutMs(long ms) {
+    this.leaseTimeoutMs = ms;
   }
 
   /** A new leader division (new LeaderStateImpl, LeaderStateImpl.java:365-430). */
@@ -147,6 +155,16 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
           d.callback.onWatchAll(wallMin[i]);
         }
       }
+      final long timeout = leaseTimeoutMs;
+      if (timeout >= 0) {  // LeaderStateImpl.hasLease for every division: extend + isValid
+        final long[] bits = new long[(cap + 63) / 64];
+        try {
+          hip.leaseBatch(System.nanoTime(), timeout, bits);
+        } catch (IOException e) {
+          throw new IllegalStateException("ratis-hip: leaseBatch failed", e);
+        }
+        leaseBits = bits;
+      }
     }
   }
 
@@ -216,6 +234,7 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
           // a recycled slot still holds its previous peer's indices
           emit(s, RatisHip.colMatch(s), RatisHip.OP_SET, -1L);
           emit(s, RatisHip.colFollowerCommit(s), RatisHip.OP_SET, -1L);
+          emit(s, RatisHip.colTs(s), RatisHip.OP_SET, System.nanoTime());  // lastRpcTime (FollowerInfoImpl.java:58)
           return s;
         }
       }
@@ -319,6 +338,34 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
     /** A commit index raised outside updateCommit (RaftLogBase.updateSnapshotIndex, :155-166). */
     public void committedIndex(long value) {
       emit(-1, RatisHip.COL_COMMITTED, RatisHip.OP_MAX, value);
+    }
+
+    // ---- leader lease (LeaderStateImpl.hasLease, LeaderLease) --------------------------------
+    /** The division's LeaderLease (lease = now, enabled per config) with every follower stamped now. */
+    public void leaseStart(long nowNanos, boolean enabled) throws IOException {
+      synchronized (deltaLock) {
+        if (!started) {
+          return;
+        }
+        drainDeltas();
+        hip.leaseStart(nodeSlot, nowNanos, enabled);
+      }
+    }
+
+    /** FollowerInfo.updateLastRespondedAppendEntriesSendTime (FollowerInfoImpl.java:241-243). */
+    public void lastResponded(int followerSlot, long sendTimeNanos) {
+      emit(followerSlot, RatisHip.colTs(followerSlot), RatisHip.OP_SET, sendTimeNanos);
+    }
+
+    /** LeaderLease.getAndSetEnabled (LeaderStateImpl.java:478, 744, 1042, 1226). */
+    public void leaseEnabled(boolean enabled) {
+      emit(-1, RatisHip.COL_LEASE_ON, RatisHip.OP_SET, enabled ? 1L : 0L);
+    }
+
+    /** enabled && (singleton || the lease, extended if it could be, is valid) at the last tick. */
+    public boolean hasLease() {
+      final long[] bits = leaseBits;
+      return bits != null && ((bits[nodeSlot >>> 6] >>> (nodeSlot & 63)) & 1L) != 0;
     }
   }
 }

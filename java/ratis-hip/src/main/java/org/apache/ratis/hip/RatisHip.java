@@ -130,7 +130,7 @@ public final class RatisHip implements AutoCloseable {
   /** A new LeaderLease for the division (lease = now, enabled per config) with every follower slot
    * stamped now, as a new LeaderStateImpl creates them (LeaderLease.java:37-38, FollowerInfoImpl.java:58).
    * Later replies go in as COL_TS deltas (updateLastRespondedAppendEntriesSendTime). */
-  public void leaseStart(int slot, long nowNanos, boolean enabled) throws IOException {
+  public void leaseStart(int slot, long nowNanos, boolean enabled) throws IOException {  // node slot
     leaseStart0(node, slot, nowNanos, enabled);
   }
 

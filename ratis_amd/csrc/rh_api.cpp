@@ -95,7 +95,7 @@ RH_EXPORT int rh_init(int device, rh_ctx** out) {
 
 hipError_t rh::pool_alloc(rh_ctx* ctx, void** p, size_t bytes, hipStream_t stream) {
     {
-        std::lock_guard<std::mutex> lk(ctx->mu);
+        std::lock_guard<std::mutex> lk(ctx->pool_mu);
         if (!ctx->pool) {
             hipMemPoolProps props{};
             props.allocType = hipMemAllocationTypePinned;

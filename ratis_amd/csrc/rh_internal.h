@@ -122,6 +122,7 @@ struct rh_ctx {
     uint32_t* d_lane16 = nullptr;  // lane-distance nibble tables of the 16-lane x 64-byte fold
     // scratch for host-buffer convenience calls
     std::mutex mu;
+    std::mutex pool_mu;  // guards pool creation (pool_alloc may run under mu, e.g. in rh_crc32c)
     void* d_scratch = nullptr;
     size_t scratch_bytes = 0;
     void* h_pinned = nullptr;
