@@ -137,7 +137,6 @@ struct FrameArgs {
     const uint32_t* slot_nframes;
     uint32_t slot_cap;
     uint32_t* seg_first_bad;
-    unsigned long long* next_batch;  // batches handed out dynamically (zeroed before the launch)
 };
 
 __device__ __forceinline__ uint32_t zshift(const uint32_t* tab, uint32_t r) {
@@ -175,8 +174,7 @@ __device__ __forceinline__ uint32_t fold_word_perm(const uint32_t* lds, uint32_t
 //   * the loop body is unrolled over the 3 ring slots with static roles (load slot i+2 while
 //     folding slot i): a window's data is consumed two windows after its load was issued, and
 //     every wait in the loop is a counted vmcnt(N);
-//   * the frame table is staged per block in batches of 512 frames into LDS (one drain per batch;
-//     blocks take batches from a global counter),
+//   * the frame table is staged per block in batches of 512 frames into LDS (one drain per batch),
 //     and each 16-lane group takes the batch's next frame whenever it finishes one;
 //   * the trailer for VERIFY comes from the last window's own chunk (one extra dword per lane), so
 //     the verify needs no dependent byte loads; the group's lane 15 (whose chunk ends at the CRC
@@ -192,7 +190,7 @@ struct Meta {
 };
 
 constexpr int kCrcThreads = 1024;
-constexpr int kCrcLds = 128 * 1024 + 16384 + 8192 + kBatch * 15 + 24;
+constexpr int kCrcLds = 128 * 1024 + 16384 + 8192 + kBatch * 15 + 16;
 static_assert(kCrcLds <= 160 * 1024, "LDS budget");
 
 __global__ __launch_bounds__(kCrcThreads) void crc_frames_kernel(FrameArgs a) {
@@ -213,7 +211,6 @@ __global__ __launch_bounds__(kCrcThreads) void crc_frames_kernel(FrameArgs a) {
     uint16_t* slow = reinterpret_cast<uint16_t*>(mfl + kBatch);  // [kBatch] guarded-path frames
     uint32_t* nslow = reinterpret_cast<uint32_t*>(slow + kBatch);
     uint32_t* nexti = nslow + 1;  // next batch frame to hand out (dynamic assignment)
-    unsigned long long* sh_batch = reinterpret_cast<unsigned long long*>(nslow + 2);  // 8-aligned
     auto meta = [&](uint32_t j) { return Meta{mo[j], mlc[j], mfl[j]}; };
     for (int i = threadIdx.x; i < kSliceBytes / 4; i += blockDim.x) {
         const int region = i >> 14, e = (i >> 6) & 255, half = (i >> 5) & 1;
@@ -234,19 +231,14 @@ __global__ __launch_bounds__(kCrcThreads) void crc_frames_kernel(FrameArgs a) {
     const bool trailer = (a.flags & (RH_CRC_VERIFY | RH_CRC_STAMP)) != 0;
     const uint32_t tl = trailer ? 4u : 0u;
 
-    // Batches are handed out dynamically (one global atomic per batch): blocks that run on busier
-    // CUs take fewer, so the launch has no static tail.
-    for (;;) {
-        __syncthreads();  // previous batch done with meta / slow / sh_batch
+    for (uint64_t b0f = (uint64_t)blockIdx.x * kBatch; b0f < a.n; b0f += (uint64_t)gridDim.x * kBatch) {
+        const uint32_t nb = (uint32_t)(a.n - b0f < (uint64_t)kBatch ? a.n - b0f : (uint64_t)kBatch);
+        __syncthreads();  // previous batch done with meta / slow
         if (t == 0) {
             *nslow = 0;
             *nexti = 0;
-            *sh_batch = atomicAdd(a.next_batch, 1ull);
         }
         __syncthreads();
-        const uint64_t b0f = *sh_batch * (uint64_t)kBatch;
-        if (b0f >= a.n) break;  // block-uniform
-        const uint32_t nb = (uint32_t)(a.n - b0f < (uint64_t)kBatch ? a.n - b0f : (uint64_t)kBatch);
         if ((uint32_t)t < nb) {
             const uint64_t f = b0f + (uint64_t)t;
             const uint64_t o = a.off[f];
@@ -475,8 +467,8 @@ __global__ __launch_bounds__(kCrcThreads) void crc_frames_kernel(FrameArgs a) {
     }
 }
 
-// One launch: a persistent grid of at most one 1024-thread workgroup per CU, each taking 512-frame
-// batches from a launch-private counter until none is left.
+// One launch: a persistent grid of at most one 1024-thread workgroup per CU, each taking
+// 512-frame batches blockIdx.x, blockIdx.x + gridDim.x, ...
 int launch_frames(rh_ctx* ctx, FrameArgs a, hipStream_t stream) {
     static bool attr_set = false;  // set once per process; hipFuncSetAttribute is idempotent
     if (!attr_set) {
@@ -491,17 +483,8 @@ int launch_frames(rh_ctx* ctx, FrameArgs a, hipStream_t stream) {
     uint64_t grid = (uint64_t)(ctx->num_cus > 0 ? ctx->num_cus : 256);
     const uint64_t need = (a.n + kBatch - 1) / kBatch;
     if (need < grid) grid = need ? need : 1;
-    void* counter = nullptr;
-    RH_HIP(rh::pool_alloc(ctx, &counter, sizeof(unsigned long long), stream));
-    a.next_batch = static_cast<unsigned long long*>(counter);
-    hipError_t e = hipMemsetAsync(counter, 0, sizeof(unsigned long long), stream);
-    if (e == hipSuccess) {
-        hipLaunchKernelGGL(crc_frames_kernel, dim3((uint32_t)grid), dim3(kCrcThreads), kCrcLds, stream, a);
-        e = hipGetLastError();
-    }
-    const hipError_t ef = hipFreeAsync(counter, stream);
-    RH_HIP(e);
-    RH_HIP(ef);
+    hipLaunchKernelGGL(crc_frames_kernel, dim3((uint32_t)grid), dim3(kCrcThreads), kCrcLds, stream, a);
+    RH_HIP(hipGetLastError());
     return RH_OK;
 }
 
