@@ -156,7 +156,7 @@ def out_col(t, name):
     return t.column(name) if hasattr(t, "column") else getattr(t, name)
 
 
-def delta_streaming(ctx, host, steps: int = 12, fill_threads: int = 16) -> dict:
+def delta_streaming(ctx, host, steps: int = 12, fill_threads: int = 16, reps: int = 5) -> dict:
     """The operating mode the Java module uses: one resident RaftGroupTable (stable F=4 and joint
     F=6 tiers), FollowerInfo / flush-index updates written in place into the pinned delta ring
     (rh_deltas_acquire / submit: H2D + device apply, which marks the touched groups dirty), then
@@ -174,8 +174,8 @@ def delta_streaming(ctx, host, steps: int = 12, fill_threads: int = 16) -> dict:
         tab.load(first, h.conf, h.flush, h.commit, h.term_start, match=h.follower)
         bases.append(first)
         first += h.n
-    per = []
-    for s in range(steps + 3):
+    per = []   # fresh deltas for every step of every run (a re-applied MAX delta advances nothing)
+    for s in range(steps * reps + 3):
         parts = []
         for h, b in zip(host, bases):
             F = h.follower.shape[0]
@@ -204,33 +204,39 @@ def delta_streaming(ctx, host, steps: int = 12, fill_threads: int = 16) -> dict:
 
     tk = step(per[0])
     tab.commit_wait_counts(tk)
-    # pipelined (the timed figure)
-    t0 = time.perf_counter()
-    inflight, advanced = [], 0
-    for s in range(1, steps + 1):
-        inflight.append(step(per[s]))
-        if len(inflight) > 2:   # two evaluations in flight while the host fills the next step
-            advanced += tab.commit_wait_counts(inflight.pop(0))[0]
-    for tk in inflight:
-        advanced += tab.commit_wait_counts(tk)[0]
-    dt = (time.perf_counter() - t0) / steps
+    # pipelined (the timed figure): `reps` runs of `steps` steps, the median run reported (one
+    # run of a dozen sub-millisecond steps is at the mercy of a single host hiccup)
+    runs = []
+    for rep in range(reps):
+        t0 = time.perf_counter()
+        inflight, advanced = [], 0
+        for s in range(1, steps + 1):
+            inflight.append(step(per[rep * steps + s]))
+            if len(inflight) > 2:   # two evaluations in flight while the host fills the next step
+                advanced += tab.commit_wait_counts(inflight.pop(0))[0]
+        for tk in inflight:
+            advanced += tab.commit_wait_counts(tk)[0]
+        runs.append((time.perf_counter() - t0) / steps)
+    dt = float(np.median(runs))
     # stages on their own: host fill of the pinned ring; device part (H2D + apply + evaluation +
     # events) with the ring already filled, synchronous
+    last = steps * reps
     f0 = time.perf_counter()
     for s in range(3):
         ring = tab.acquire_deltas()
-        fill(ring, per[steps + 1])
+        fill(ring, per[last + 1])
         tab.submit_deltas(0)
     fill_s = (time.perf_counter() - f0) / 3
     ring = tab.acquire_deltas()
-    fill(ring, per[steps + 2])
+    fill(ring, per[last + 2])
     g0 = time.perf_counter()
-    tab.submit_deltas(per[steps + 2].size)
+    tab.submit_deltas(per[last + 2].size)
     tab.commit_wait_counts(tab.commit_async(watch_all=False))
     dev_s = time.perf_counter() - g0
     tab.close()
     prod.close()
     return {"commit_updates_per_s_incl_pcie": round(n_all / dt, 1), "ms_per_step": round(dt * 1e3, 3),
+            "ms_per_step_runs": [round(x * 1e3, 3) for x in runs], "runs": f"median of {reps} runs of {steps} steps",
             "deltas_per_step": n_all, "delta_bytes_h2d_per_step": nbytes,
             "h2d_bound_ms": round(nbytes / 50e9 * 1e3, 3),
             "stage_ms": {"host_fill_pinned_ring": round(fill_s * 1e3, 3), "fill_threads": fill_threads,

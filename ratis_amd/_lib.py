@@ -13,6 +13,9 @@ from ctypes import POINTER, c_char_p, c_int, c_int32, c_int64, c_size_t, c_uint3
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libratis_hip.so")
+# A/B builds of the same sources (scripts/ab_build.sh) are loaded by the tuning scripts through
+# RATIS_HIP_LIB; the product, tests, smoke() and bench.py use LIB_PATH.
+LIB_PATH = os.environ.get("RATIS_HIP_LIB", LIB_PATH)
 
 RH_OK = 0
 RH_E_INVAL = -1

@@ -137,6 +137,12 @@ struct FrameArgs {
     const uint32_t* slot_nframes;
     uint32_t slot_cap;
     uint32_t* seg_first_bad;
+    // lane split (set by the launcher): the frames the lane kernels fold (crc_class > 0) are not
+    // this kernel's.  If they are the majority it reads the list of its own frames, widx[0 ..
+    // counts[0]) (the scatter's), else it walks the whole table and skips them.
+    uint32_t lane_split;
+    const uint32_t* counts;
+    const uint32_t* widx;
 };
 
 __device__ __forceinline__ uint32_t zshift(const uint32_t* tab, uint32_t r) {
@@ -170,6 +176,23 @@ __device__ __forceinline__ uint32_t fold_word_perm(const uint32_t* lds, uint32_t
     return lds_word(lds, a3) ^ lds_word(lds, a2) ^ lds_word(lds, a1) ^ lds_word(lds, a0);
 }
 
+// Start of a frame inside a lane's chunk: the chunk's aligned words d[0..16] start q0l bytes
+// after the frame start (q0l < 4: the chunk holds frame bytes 0..3).  Bytes before the frame are
+// zeroed (a zero register absorbs leading zeros) and reset()'s state is XOR-ed into frame bytes
+// 0..3, so folding the chunk from a zero register is folding the frame from `init`.
+__device__ __forceinline__ void mask_frame_start(uint32_t (&d)[18], int64_t q0l, bool on, uint32_t init) {
+    const int q0 = (int)(q0l < -80 ? -80 : (q0l > 4 ? 4 : q0l));
+#pragma unroll
+    for (int i = 0; i < 17; ++i) {
+        const int q = q0 + 4 * i;
+        uint32_t v = d[i];
+        v = (q <= -4) ? 0u : (q < 0 ? (v & (0xFFFFFFFFu << (8 * -q))) : v);
+        const uint32_t up = (q >= 0 && q < 4) ? (init >> (8 * q)) : 0u;
+        const uint32_t dn2 = (q < 0 && q > -4) ? (init << (8 * -q)) : 0u;
+        d[i] = on ? (v ^ up ^ dn2) : d[i];
+    }
+}
+
 // ---- the kernel: copy-free prefetch ring, frame metadata staged in LDS ------------------------
 //   * the loop body is unrolled over the 3 ring slots with static roles (load slot i+2 while
 //     folding slot i): a window's data is consumed two windows after its load was issued, and
@@ -182,7 +205,16 @@ __device__ __forceinline__ uint32_t fold_word_perm(const uint32_t* lds, uint32_t
 //   * inactive lanes load from the buffer start instead of zero-filling registers in flight.
 // Frames whose chunks could leave the buffer (within 67 bytes of its start or 8 of its end),
 // malformed and empty ones take a guarded byte path after the batch's main loop.
-constexpr int kBatch = 512;
+// Chunk-count classes and the kernel each goes to (microbench over uniform and ragged shapes,
+// profiles/r02/crc_lanes/): spans up to 768 B on 4 lanes per frame, up to 1536 B on 8; longer
+// spans fill the 1 KiB windows well enough that the window kernel's per-frame dynamic assignment
+// wins (4 KiB frames: 4.3 vs 3.8 TB/s on 16 lanes per frame).
+constexpr int kQ4Chunks = 12;
+constexpr int kLaneChunks = 24;            // CRC spans up to 1536 B go to the lane kernels
+constexpr int kClasses = kLaneChunks + 1;  // class 0: window kernel; class c: c chunks of 64 B
+constexpr uint64_t kLaneMeanMax = 2048;    // mean frame length (buf_len / n) up to which the split runs
+
+constexpr int kBatch = 416;  // 160 KiB of LDS - 152 KiB of tables = 416 x 19 B of batch table
 struct Meta {
     int64_t o;    // frame start (bytes)
     uint32_t lc;  // CRC-covered length
@@ -190,7 +222,7 @@ struct Meta {
 };
 
 constexpr int kCrcThreads = 1024;
-constexpr int kCrcLds = 128 * 1024 + 16384 + 8192 + kBatch * 15 + 16;
+constexpr int kCrcLds = 128 * 1024 + 16384 + 8192 + kBatch * 19 + 16;
 static_assert(kCrcLds <= 160 * 1024, "LDS budget");
 
 __global__ __launch_bounds__(kCrcThreads) void crc_frames_kernel(FrameArgs a) {
@@ -201,13 +233,17 @@ __global__ __launch_bounds__(kCrcThreads) void crc_frames_kernel(FrameArgs a) {
     constexpr int kLaneWords = 8 * 16 * 32;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     if (__builtin_amdgcn_groupstaticsize() != 0) __builtin_trap();  // lds_word assumes base 0
+    const bool listed = a.lane_split && 2ull * a.counts[0] < a.n;  // read widx[] (uniform)
+    const uint64_t n_all = listed ? (uint64_t)a.counts[0] : a.n;
+    if ((uint64_t)blockIdx.x * kBatch >= n_all) return;  // no batch for this block: skip the table fill
     uint32_t* llane = lds + kSliceBytes / 4;
     uint32_t* lzw = llane + kLaneWords;
     uint32_t* lch = lzw + 1024;  // [4][256]: advance over 64 / CH zero bytes (chain combine)
     // batch frame table, struct-of-arrays: start, CRC-covered length, path; then the guarded list
     int64_t* mo = reinterpret_cast<int64_t*>(lch + 1024);
     uint32_t* mlc = reinterpret_cast<uint32_t*>(mo + kBatch);
-    uint8_t* mfl = reinterpret_cast<uint8_t*>(mlc + kBatch);
+    uint32_t* mf = mlc + kBatch;  // frame number
+    uint8_t* mfl = reinterpret_cast<uint8_t*>(mf + kBatch);
     uint16_t* slow = reinterpret_cast<uint16_t*>(mfl + kBatch);  // [kBatch] guarded-path frames
     uint32_t* nslow = reinterpret_cast<uint32_t*>(slow + kBatch);
     uint32_t* nexti = nslow + 1;  // next batch frame to hand out (dynamic assignment)
@@ -231,8 +267,8 @@ __global__ __launch_bounds__(kCrcThreads) void crc_frames_kernel(FrameArgs a) {
     const bool trailer = (a.flags & (RH_CRC_VERIFY | RH_CRC_STAMP)) != 0;
     const uint32_t tl = trailer ? 4u : 0u;
 
-    for (uint64_t b0f = (uint64_t)blockIdx.x * kBatch; b0f < a.n; b0f += (uint64_t)gridDim.x * kBatch) {
-        const uint32_t nb = (uint32_t)(a.n - b0f < (uint64_t)kBatch ? a.n - b0f : (uint64_t)kBatch);
+    for (uint64_t b0f = (uint64_t)blockIdx.x * kBatch; b0f < n_all; b0f += (uint64_t)gridDim.x * kBatch) {
+        const uint32_t nb = (uint32_t)(n_all - b0f < (uint64_t)kBatch ? n_all - b0f : (uint64_t)kBatch);
         __syncthreads();  // previous batch done with meta / slow
         if (t == 0) {
             *nslow = 0;
@@ -240,7 +276,8 @@ __global__ __launch_bounds__(kCrcThreads) void crc_frames_kernel(FrameArgs a) {
         }
         __syncthreads();
         if ((uint32_t)t < nb) {
-            const uint64_t f = b0f + (uint64_t)t;
+            const uint64_t f = listed ? (uint64_t)a.widx[b0f + (uint64_t)t] : b0f + (uint64_t)t;
+            mf[t] = (uint32_t)f;
             const uint64_t o = a.off[f];
             const int64_t L = (int64_t)a.len[f];
             const bool malformed = o > (uint64_t)a.buf_len || L > a.buf_len - (int64_t)o || (trailer && L < 4);
@@ -250,9 +287,11 @@ __global__ __launch_bounds__(kCrcThreads) void crc_frames_kernel(FrameArgs a) {
             const int64_t E = m.o + (int64_t)m.lc;
             const bool unsafe = m.o < 67 || E + 8 > a.buf_len || m.lc < 8;
             m.fl = malformed ? 2u : (unsafe ? 1u : 0u);
+            if (a.lane_split && !listed && m.fl == 0u && m.lc <= (uint32_t)kLaneChunks * 64u) m.fl = 3u;  // class > 0
             if (a.slot_nframes) {  // slot mode: slots past the segment's frame count are skipped
-                const uint32_t nfs = a.slot_nframes[f / a.slot_cap];
-                if (f % a.slot_cap >= (nfs < a.slot_cap ? nfs : a.slot_cap)) m.fl = 3u;
+                const uint32_t seg = (uint32_t)f / a.slot_cap, slot = (uint32_t)f - seg * a.slot_cap;
+                const uint32_t nfs = a.slot_nframes[seg];
+                if (slot >= (nfs < a.slot_cap ? nfs : a.slot_cap)) m.fl = 3u;
             }
             mo[t] = m.o;
             mlc[t] = m.lc;
@@ -316,18 +355,7 @@ __global__ __launch_bounds__(kCrcThreads) void crc_frames_kernel(FrameArgs a) {
             const int64_t be = E - (nw - 1 - (int64_t)x.wi) * W - (int64_t)(Q - 1 - gl) * S;
             const bool act = be > m.o;
             const int64_t q0l = be - S - (int64_t)sh - m.o;  // chunk start (aligned) rel. to frame start
-            if (__any(act && q0l < 4)) {
-                const int q0 = (int)(q0l < -80 ? -80 : (q0l > 4 ? 4 : q0l));
-#pragma unroll
-                for (int i = 0; i < 17; ++i) {
-                    const int q = q0 + 4 * i;
-                    uint32_t v = d[i];
-                    v = (q <= -4) ? 0u : (q < 0 ? (v & (0xFFFFFFFFu << (8 * -q))) : v);
-                    const uint32_t up = (q >= 0 && q < 4) ? (a.init >> (8 * q)) : 0u;
-                    const uint32_t dn2 = (q < 0 && q > -4) ? (a.init << (8 * -q)) : 0u;
-                    d[i] = (act && q0l < 4) ? (v ^ up ^ dn2) : d[i];
-                }
-            }
+            if (__any(act && q0l < 4)) mask_frame_start(d, q0l, act && q0l < 4, a.init);
             // CH independent chains of 16 / CH words (the LDS round trips overlap), joined by
             // Horner steps over 64 / CH zero bytes: CRC(A||B) = adv_|B|(crc A) ^ crc B from zero
             constexpr int LW = 16 / CH;
@@ -360,7 +388,7 @@ __global__ __launch_bounds__(kCrcThreads) void crc_frames_kernel(FrameArgs a) {
             R = zshift(lzw, R) ^ r;
             if ((int64_t)x.wi + 1 >= nw) {
                 if (gl == Q - 1) {  // this lane's chunk ends at E: d[16..17] hold bytes E - sh .. E + 8 - sh
-                    const uint64_t f = b0f + x.j;
+                    const uint64_t f = mf[x.j];
                     uint32_t state = R;
                     if (m.lc < 4) state ^= (uint32_t)((uint64_t)a.init >> (8 * m.lc));
                     const uint32_t value = ~state;
@@ -412,7 +440,7 @@ __global__ __launch_bounds__(kCrcThreads) void crc_frames_kernel(FrameArgs a) {
         for (uint32_t i = grp; i < ns; i += 64) {
             const uint32_t j = slow[i];
             const Meta m = meta(j);
-            const uint64_t f = b0f + j;
+            const uint64_t f = mf[j];
             if (m.fl == 2) {
                 if (gl == 0) {
                     if (a.crc_out) a.crc_out[f] = 0u;
@@ -467,24 +495,406 @@ __global__ __launch_bounds__(kCrcThreads) void crc_frames_kernel(FrameArgs a) {
     }
 }
 
-// One launch: a persistent grid of at most one 1024-thread workgroup per CU, each taking
-// 512-frame batches blockIdx.x, blockIdx.x + gridDim.x, ...
-int launch_frames(rh_ctx* ctx, FrameArgs a, hipStream_t stream) {
-    static bool attr_set = false;  // set once per process; hipFuncSetAttribute is idempotent
-    if (!attr_set) {
-        RH_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(crc_frames_kernel),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize, kCrcLds));
-        attr_set = true;
+// ---- lane-per-frame path --------------------------------------------------------------------
+// The window kernel's cost is per 1 KiB window, however little of it a short frame fills (it is
+// VALU-issue bound: ~0.25 ns of the chip per window).  Frames whose CRC span is at most
+// kLaneChunks x 64 B are instead folded one frame per lane: a lane walks its frame's end-anchored
+// 64-byte chunks and carries its register from chunk to chunk, so the work is proportional to the
+// frame's bytes and needs no cross-lane combine.  A counting sort by chunk count (classify +
+// scatter) makes the 64 frames of a wave the same length, so the wave's lanes start and finish
+// their frames together (the start-of-frame masking and the trailer check are wave-uniform steps).
+// Long frames and frames the fast path cannot load safely stay on the window kernel (class 0).
+constexpr int kLaneLds = 128 * 1024 + 4096 + 16384 + 4096;
+constexpr int kSortThreads = 256, kSortPer = 8, kSortTile = kSortThreads * kSortPer;
+
+struct LaneRec {  // one frame of the lane path, records ascending by chunk count
+    int64_t o;    // frame start
+    uint32_t lc;  // CRC-covered length (8 .. 4096)
+    uint32_t f;   // frame number (output index)
+};
+
+// class of frame f (-1: an empty slot of the slotted read-path table, no output at all)
+__device__ __forceinline__ int crc_class(const FrameArgs& a, uint64_t f, int64_t& o_out, uint32_t& lc_out) {
+    if (a.slot_nframes) {  // 32-bit division: the launcher keeps n below 2^32
+        const uint32_t seg = (uint32_t)f / a.slot_cap, slot = (uint32_t)f - seg * a.slot_cap;
+        const uint32_t nfs = a.slot_nframes[seg];
+        if (slot >= (nfs < a.slot_cap ? nfs : a.slot_cap)) return -1;
     }
+    const uint32_t tl = (a.flags & (RH_CRC_VERIFY | RH_CRC_STAMP)) ? 4u : 0u;
+    const uint64_t o = a.off[f];
+    const int64_t L = (int64_t)a.len[f];
+    // the window kernel's fast-path rules (malformed / guarded frames are its business)
+    if (o > (uint64_t)a.buf_len || L > a.buf_len - (int64_t)o || L < (int64_t)tl) return 0;
+    const int64_t lc = L - (int64_t)tl, E = (int64_t)o + lc;
+    if ((int64_t)o < 67 || E + 8 > a.buf_len || lc < 8 || lc > (int64_t)kLaneChunks * 64) return 0;
+    o_out = (int64_t)o;
+    lc_out = (uint32_t)lc;
+    return (int)((lc + 63) >> 6);
+}
+
+// counts[c] = frames of class c
+__global__ __launch_bounds__(kSortThreads) void crc_classify_kernel(FrameArgs a, uint32_t* counts) {
+    __shared__ uint32_t h[kClasses];
+    for (int i = threadIdx.x; i < kClasses; i += blockDim.x) h[i] = 0;
+    __syncthreads();
+    for (uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; f < a.n; f += (uint64_t)gridDim.x * blockDim.x) {
+        int64_t o;
+        uint32_t lc;
+        const int c = crc_class(a, f, o, lc);
+        const int c0 = __shfl(c, 0);
+        const uint32_t nact = (uint32_t)__popcll(__ballot(1));  // active lanes (a prefix of the wave)
+        if (__all(c == c0)) {  // a wave of one class (uniform logs): one atomic
+            if ((threadIdx.x & 63) == 0 && c0 >= 0) atomicAdd(&h[c0], nact);
+        } else if (c >= 0) {
+            atomicAdd(&h[c], 1u);
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kClasses; i += blockDim.x)
+        if (h[i]) atomicAdd(&counts[i], h[i]);
+}
+
+// Scatter: lane-path records by ascending chunk count into rec[], the window kernel's frame numbers
+// into widx[].  cursor[c] (zeroed) hands each block its range within class c.
+__global__ __launch_bounds__(kSortThreads) void crc_scatter_kernel(FrameArgs a, const uint32_t* counts, uint32_t* cursor,
+                                                                   LaneRec* rec, uint32_t* widx) {
+    __shared__ uint32_t h[kClasses], base[kClasses];
+    for (int i = threadIdx.x; i < kClasses; i += blockDim.x) h[i] = 0;
+    __syncthreads();
+    const uint64_t t0 = (uint64_t)blockIdx.x * kSortTile;
+    int cls[kSortPer];
+    uint32_t rank[kSortPer], lcs[kSortPer];
+    int64_t os[kSortPer];
+#pragma unroll
+    for (int k = 0; k < kSortPer; ++k) {
+        const uint64_t f = t0 + (uint64_t)k * kSortThreads + threadIdx.x;
+        cls[k] = f < a.n ? crc_class(a, f, os[k], lcs[k]) : -1;
+        const int c0 = __shfl(cls[k], 0);
+        if (__all(cls[k] == c0)) {  // a wave of one class: one atomic, ranks by lane
+            uint32_t b = 0;
+            if ((threadIdx.x & 63) == 0 && c0 >= 0) b = atomicAdd(&h[c0], 64u);
+            rank[k] = (uint32_t)__shfl((int)b, 0) + (uint32_t)(threadIdx.x & 63);
+        } else {
+            rank[k] = cls[k] >= 0 ? atomicAdd(&h[cls[k]], 1u) : 0u;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < kClasses) {
+        const int c = threadIdx.x;
+        uint32_t b = 0;  // class c's first record: classes 1..c-1 before it (class 0: its own list)
+        for (int j = 1; j < c; ++j) b += counts[j];
+        base[c] = b + (h[c] ? atomicAdd(&cursor[c], h[c]) : 0u);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kSortPer; ++k) {
+        const uint64_t f = t0 + (uint64_t)k * kSortThreads + threadIdx.x;
+        if (cls[k] > 0) {
+            LaneRec r;
+            r.o = os[k];
+            r.lc = lcs[k];
+            r.f = (uint32_t)f;
+            rec[base[cls[k]] + rank[k]] = r;
+        } else if (cls[k] == 0) {
+            widx[base[0] + rank[k]] = (uint32_t)f;
+        }
+    }
+}
+
+struct LaneArgs {
+    const uint8_t* buf;
+    uint8_t* wbuf;
+    const LaneRec* rec;
+    const uint32_t* counts;
+    uint32_t init;
+    uint32_t flags;
+    uint32_t* crc_out;
+    uint64_t* bad_bits;
+    unsigned long long* n_bad;
+    const uint32_t* slice;
+    const uint32_t* shift32;
+    const uint32_t* lanetab;  // Q > 1: lane-distance tables build_crc_lane_tables(Q, 64)
+    const uint32_t* zwin;     // Q > 1: advance over one Q x 64-byte window
+    uint32_t cls_lo, cls_hi;  // the chunk-count classes this launch folds
+    uint32_t slot_cap;
+    uint32_t* seg_first_bad;
+};
+
+// One wave = one group of G = 64 / Q consecutive records, Q lanes per frame (lane l: record
+// G g + l / Q, chunk position l % Q); groups g = wave, wave + waves, ... (the records ascend by
+// length, so every wave gets a like mix).  A frame's CRC span is cut into end-anchored windows of
+// Q chunks of 64 B.  A group runs nmax = its longest frame's window count steps; window k of the
+// group ends at E - W (nmax - 1 - k) for every frame, so shorter frames start later and all end at
+// step nmax - 1.  Q = 1: the lane carries its register from chunk to chunk (no combine).  Q > 1:
+// every chunk is folded from zero and the window's register is the XOR of the chunks advanced
+// over the bytes after them (lane tables + DPP reduce), windows chained by a W-byte advance.
+// Same 3-slot register ring with static roles as the window kernel.
+template <int Q>
+__global__ __launch_bounds__(kCrcThreads) void crc_lanes_kernel(LaneArgs a) {
+    constexpr int kSliceBytes = 128 * 1024;
+    constexpr int kWaves = kCrcThreads / 64;
+    constexpr int G = 64 / Q;
+    constexpr int64_t W = 64 * Q;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    if (__builtin_amdgcn_groupstaticsize() != 0) __builtin_trap();  // lds_word assumes base 0
+    uint32_t nbeg = 0, nrec = 0;  // this launch's records: rec[nbeg, nbeg + nrec)
+    for (uint32_t c = 1; c <= a.cls_hi; ++c) {
+        const uint32_t k = a.counts[c];
+        if (c < a.cls_lo) nbeg += k;
+        else nrec += k;
+    }
+    const LaneRec* rec = a.rec + nbeg;
+    const uint32_t ngroups = (nrec + G - 1) / G;
+    if ((uint32_t)blockIdx.x * kWaves >= ngroups) return;  // no group for this block
+    uint32_t* lch = lds + kSliceBytes / 4;
+    uint32_t* llane = lch + 1024;
+    uint32_t* lzw = llane + 4096;
+    for (int i = threadIdx.x; i < kSliceBytes / 4; i += blockDim.x) {
+        const int region = i >> 14, e = (i >> 6) & 255, half = (i >> 5) & 1;
+        lds[i] = a.slice[((region * 2 + half) << 8) | e];
+    }
+    for (int i = threadIdx.x; i < 1024; i += blockDim.x) lch[i] = a.shift32[i];
+    if constexpr (Q > 1) {
+        for (int i = threadIdx.x; i < 4096; i += blockDim.x) llane[i] = a.lanetab[i];
+        for (int i = threadIdx.x; i < 1024; i += blockDim.x) lzw[i] = a.zwin[i];
+    }
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63;
+    const int gl = lane & (Q - 1);  // chunk position within the window
+    const uint32_t c = lane & 31;
+    uint32_t lb[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) lb[k] = ((uint32_t)(k >> 1) << 16) | ((uint32_t)(k & 1) << 7) | (c << 2);
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane(blockIdx.x * kWaves + (threadIdx.x >> 6));
+    const uint32_t nwv = gridDim.x * kWaves;
+
+    struct Rec {
+        int64_t o;
+        uint32_t lc;
+        uint32_t f;  // 0xFFFFFFFF: no frame in this lane
+    };
+    struct Task {
+        Rec r;
+        uint32_t g;     // group (>= ngroups: done)
+        uint32_t k;     // step
+        uint32_t nmax;  // steps of the group
+    };
+    // Record of this lane's frame in group g.  The load is issued unconditionally (clamped index),
+    // so every step issues the same vector memory operations and the compiler's vmcnt waits stay
+    // counted -- a conditional load here cost a full drain of the ring at each group change.
+    auto fetch = [&](uint32_t g) -> Rec {
+        const uint64_t i = (uint64_t)g * G + (uint64_t)(lane / Q);
+        const bool ok = g < ngroups && i < nrec;
+        const LaneRec x = rec[ok ? i : 0];
+        return Rec{x.o, x.lc, ok ? x.f : 0xFFFFFFFFu};
+    };
+    auto enter = [&](uint32_t g, const Rec& r) -> Task {
+        Task t{r, g, 0u, 0u};
+        if (g < ngroups) {
+            const uint32_t last = nrec - 1 - g * G < (uint32_t)(G - 1) ? nrec - 1 - g * G : (uint32_t)(G - 1);
+            const uint32_t nw = (uint32_t)(((int64_t)r.lc + W - 1) / W);  // longest frame: the last one
+            t.nmax = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)nw, (int)(last * Q)));
+        }
+        return t;
+    };
+    Rec pre = fetch(wv + nwv);  // record of the group after the newest task's group
+    auto next = [&](const Task& x) -> Task {
+        Task t = x;
+        if (x.g < ngroups) t = x.k + 1 < x.nmax ? Task{x.r, x.g, x.k + 1, x.nmax} : enter(x.g + nwv, pre);
+        pre = fetch(t.g + nwv);  // every step (see fetch)
+        return t;
+    };
+    // chunk of task x in this lane: [be - 64, be), be = E - W (nmax - 1 - k) - 64 (Q - 1 - gl);
+    // loads 72 bytes from the 4-aligned b0 = be - 64 - (E & 3) (the last 8 hold the trailer)
+    auto chunk_end = [&](const Task& x) -> int64_t {
+        return x.r.o + (int64_t)x.r.lc - W * (int64_t)(x.nmax - 1 - x.k) - 64 * (int64_t)(Q - 1 - gl);
+    };
+    auto load = [&](const Task& x, uint32_t (&dd)[18]) {
+        const uint8_t* src = a.buf;
+        if (x.g < ngroups && x.r.f != 0xFFFFFFFFu) {
+            const int64_t be = chunk_end(x);
+            if (be > x.r.o) src = a.buf + (be - 64 - ((x.r.o + (int64_t)x.r.lc) & 3));
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const u32x4a v = *reinterpret_cast<const u32x4a*>(src + 16 * q);
+            dd[4 * q] = v.x;
+            dd[4 * q + 1] = v.y;
+            dd[4 * q + 2] = v.z;
+            dd[4 * q + 3] = v.w;
+        }
+        dd[16] = *reinterpret_cast<const uint32_t*>(src + 64);
+        dd[17] = *reinterpret_cast<const uint32_t*>(src + 68);
+    };
+    uint32_t R = 0;  // the frame's register over its windows (chunks, Q = 1) so far
+    auto fold = [&](const Task& x, uint32_t (&d)[18]) {
+        if (x.g >= ngroups) return;
+        const bool valid = x.r.f != 0xFFFFFFFFu;
+        const int64_t E = x.r.o + (int64_t)x.r.lc;
+        const uint32_t sh = (uint32_t)(E & 3);
+        const int64_t be = chunk_end(x);
+        const bool act = valid && be > x.r.o;
+        const int64_t q0l = be - 64 - (int64_t)sh - x.r.o;
+        if (__any(act && q0l < 4)) mask_frame_start(d, q0l, act && q0l < 4, a.init);
+        uint32_t r0 = Q == 1 ? R : 0u, r1 = 0;  // two chains of 8 words, joined over 32 zero bytes
+        if (__all(sh == 0 || !act)) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                r0 = fold_word_perm(lds, r0, d[j], lb);
+                r1 = fold_word_perm(lds, r1, d[8 + j], lb);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                r0 = fold_word_perm(lds, r0, __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh), lb);
+                r1 = fold_word_perm(lds, r1, __builtin_amdgcn_alignbyte(d[9 + j], d[8 + j], sh), lb);
+            }
+        }
+        uint32_t r = zshift(lch, r0) ^ r1;
+        if constexpr (Q == 1) {
+            R = act ? r : 0u;
+        } else {
+            uint32_t z = 0;
+#pragma unroll
+            for (int k = 0; k < 8; ++k) z ^= llane[c + ((uint32_t)(k * 16) + ((r >> (4 * k)) & 15u)) * 32u];
+            r = act ? z : 0u;
+            r ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
+            if constexpr (Q >= 4) r ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r, 0x4E, 0xF, 0xF, false);
+            if constexpr (Q >= 8) r ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r, 0x141, 0xF, 0xF, false);
+            if constexpr (Q >= 16) r ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r, 0x140, 0xF, 0xF, false);
+            R = zshift(lzw, R) ^ r;
+        }
+        if (x.k + 1 == x.nmax) {  // every frame of the group ends at this step
+            if (valid && gl == Q - 1) {  // the lane whose chunk ends at E
+                const uint32_t value = ~R;
+                const uint32_t f = x.r.f;
+                if (a.crc_out) a.crc_out[f] = value;
+                if (a.flags & RH_CRC_STAMP) {
+                    a.wbuf[E + 0] = (uint8_t)(value >> 24);
+                    a.wbuf[E + 1] = (uint8_t)(value >> 16);
+                    a.wbuf[E + 2] = (uint8_t)(value >> 8);
+                    a.wbuf[E + 3] = (uint8_t)value;
+                } else if (a.flags & RH_CRC_VERIFY) {
+                    const uint32_t stored = __builtin_bswap32(__builtin_amdgcn_alignbyte(d[17], d[16], sh));
+                    if (stored != value) {
+                        if (a.bad_bits)
+                            atomicOr(reinterpret_cast<unsigned long long*>(a.bad_bits + (f >> 6)), 1ull << (f & 63));
+                        if (a.n_bad) atomicAdd(a.n_bad, 1ull);
+                        if (a.seg_first_bad) atomicMin(a.seg_first_bad + f / a.slot_cap, f % a.slot_cap);
+                    }
+                }
+            }
+            R = 0;
+        }
+    };
+    Task T0 = enter(wv, fetch(wv));
+    Task T1 = next(T0);
+    Task T2 = next(T1);
+    uint32_t d0[18], d1[18], d2[18];
+    if (T0.g < ngroups) {
+        load(T0, d0);
+        load(T1, d1);
+    }
+    while (T0.g < ngroups) {
+        load(T2, d2);
+        fold(T0, d0);
+        T0 = next(T2);
+        if (T1.g >= ngroups) break;
+        load(T0, d0);
+        fold(T1, d1);
+        T1 = next(T0);
+        if (T2.g >= ngroups) break;
+        load(T1, d1);
+        fold(T2, d2);
+        T2 = next(T1);
+    }
+}
+
+template <int Q>
+hipError_t launch_lanes(const LaneArgs& l, uint64_t n, uint64_t cus, hipStream_t stream) {
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(crc_lanes_kernel<Q>),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, kLaneLds);
+    if (attr != hipSuccess) return attr;
+    constexpr uint64_t per_block = (uint64_t)(kCrcThreads / 64) * (64 / Q);  // frames of one round of groups
+    const uint64_t grid = (n + per_block - 1) / per_block < cus ? (n + per_block - 1) / per_block : cus;
+    hipLaunchKernelGGL(crc_lanes_kernel<Q>, dim3((uint32_t)grid), dim3(kCrcThreads), kLaneLds, stream, l);
+    return hipGetLastError();
+}
+
+// classify -> scatter -> lane kernels (4 and 8 lanes per frame) -> window kernel over the rest,
+// all on `stream`.
+int launch_frames(rh_ctx* ctx, FrameArgs a, hipStream_t stream) {
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(crc_frames_kernel),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, kCrcLds);
+    RH_HIP(attr);
+    if (a.n > 0xFFFFFFFFull) return rh::fail(RH_E_RANGE, "CRC launch: more than 2^32 - 1 frames in one launch");
     a.slice = ctx->d_slice;
     a.shift32 = ctx->d_shift + (size_t)5 * 1024;  // 2^5 = 32 bytes: the fold-chain join
     a.zwin = ctx->d_shift + (size_t)10 * 1024;    // 2^10 = one 1 KiB window
-    a.lanetab = ctx->d_lane16;
-    uint64_t grid = (uint64_t)(ctx->num_cus > 0 ? ctx->num_cus : 256);
-    const uint64_t need = (a.n + kBatch - 1) / kBatch;
-    if (need < grid) grid = need ? need : 1;
-    hipLaunchKernelGGL(crc_frames_kernel, dim3((uint32_t)grid), dim3(kCrcThreads), kCrcLds, stream, a);
+    a.lanetab = ctx->d_lane16 + (size_t)3 * 4096;  // Q = 16
+    const uint64_t cus = (uint64_t)(ctx->num_cus > 0 ? ctx->num_cus : 256);
+    // The lane split pays a classify + scatter pass (~4 % of a config-5 launch); it is taken when the
+    // buffer's mean frame length buf_len / n is at most kLaneMeanMax -- logs of short entries.
+    // Logs of long frames (config 5's 4 KiB) and single spans stay on the window kernel alone.
+    bool window_only = a.buf_len / a.n > kLaneMeanMax;
+#ifdef RH_AB_WINDOW_ONLY  // A/B build (scripts/ab_build.sh): every frame on the window kernel
+    window_only = true;
+#endif
+    if (window_only) {
+        const uint64_t wgrid = (a.n + kBatch - 1) / kBatch < cus ? (a.n + kBatch - 1) / kBatch : cus;
+        hipLaunchKernelGGL(crc_frames_kernel, dim3((uint32_t)wgrid), dim3(kCrcThreads), kCrcLds, stream, a);
+        RH_HIP(hipGetLastError());
+        return RH_OK;
+    }
+    // scratch: counts[kClasses], cursor[kClasses], rec[n], widx[n]
+    const size_t o_rec = 1024, o_widx = o_rec + (size_t)a.n * sizeof(LaneRec), bytes = o_widx + (size_t)a.n * 4;
+    void* scratch = nullptr;
+    RH_HIP(rh::pool_alloc(ctx, &scratch, bytes, stream));
+    uint8_t* sb = static_cast<uint8_t*>(scratch);
+    uint32_t* counts = reinterpret_cast<uint32_t*>(sb);
+    uint32_t* cursor = counts + kClasses;
+    LaneRec* rec = reinterpret_cast<LaneRec*>(sb + o_rec);
+    uint32_t* widx = reinterpret_cast<uint32_t*>(sb + o_widx);
+    RH_HIP(hipMemsetAsync(counts, 0, 2 * kClasses * sizeof(uint32_t), stream));
+    const uint64_t cgrid = (a.n + kSortThreads - 1) / kSortThreads < cus * 8 ? (a.n + kSortThreads - 1) / kSortThreads : cus * 8;
+    hipLaunchKernelGGL(crc_classify_kernel, dim3((uint32_t)cgrid), dim3(kSortThreads), 0, stream, a, counts);
     RH_HIP(hipGetLastError());
+    hipLaunchKernelGGL(crc_scatter_kernel, dim3((uint32_t)((a.n + kSortTile - 1) / kSortTile)), dim3(kSortThreads), 0,
+                       stream, a, counts, cursor, rec, widx);
+    RH_HIP(hipGetLastError());
+    LaneArgs l{};
+    l.buf = a.buf;
+    l.wbuf = a.wbuf;
+    l.rec = rec;
+    l.counts = counts;
+    l.init = a.init;
+    l.flags = a.flags;
+    l.crc_out = a.crc_out;
+    l.bad_bits = a.bad_bits;
+    l.n_bad = a.n_bad;
+    l.slice = a.slice;
+    l.shift32 = a.shift32;
+    l.slot_cap = a.slot_cap;
+    l.seg_first_bad = a.seg_first_bad;
+    // 4 lanes per frame for classes 1..12, 8 for 13..24 (lane tables: Q = 2, 4, 8, 16 at 4096 words each)
+    l.lanetab = ctx->d_lane16 + (size_t)1 * 4096;
+    l.zwin = ctx->d_shift + (size_t)8 * 1024;
+    l.cls_lo = 1;
+    l.cls_hi = kQ4Chunks;
+    RH_HIP(launch_lanes<4>(l, a.n, cus, stream));
+    l.lanetab = ctx->d_lane16 + (size_t)2 * 4096;
+    l.zwin = ctx->d_shift + (size_t)9 * 1024;
+    l.cls_lo = kQ4Chunks + 1;
+    l.cls_hi = kLaneChunks;
+    RH_HIP(launch_lanes<8>(l, a.n, cus, stream));
+    a.lane_split = 1;
+    a.counts = counts;
+    a.widx = widx;
+    const uint64_t wgrid = (a.n + kBatch - 1) / kBatch < cus ? (a.n + kBatch - 1) / kBatch : cus;
+    hipLaunchKernelGGL(crc_frames_kernel, dim3((uint32_t)wgrid), dim3(kCrcThreads), kCrcLds, stream, a);
+    RH_HIP(hipGetLastError());
+    RH_HIP(hipFreeAsync(scratch, stream));
     return RH_OK;
 }
 
@@ -502,7 +912,12 @@ int rh_crc_upload_tables(rh_ctx* ctx) {
         rh::build_crc_shift_table(1ull << m, reinterpret_cast<uint32_t(*)[256]>(sh.data() + (size_t)m * 1024));
     RH_HIP(hipMalloc(&ctx->d_shift, sh.size() * 4));
     RH_HIP(hipMemcpy(ctx->d_shift, sh.data(), sh.size() * 4, hipMemcpyHostToDevice));
-    const std::vector<uint32_t> lt = rh::build_crc_lane_tables(16, 64);
+    // lane-distance tables for Q = 2, 4, 8, 16 lanes per window (4096 words each)
+    std::vector<uint32_t> lt;
+    for (int q = 2; q <= 16; q *= 2) {
+        const std::vector<uint32_t> t = rh::build_crc_lane_tables(q, 64);
+        lt.insert(lt.end(), t.begin(), t.end());
+    }
     RH_HIP(hipMalloc(&ctx->d_lane16, lt.size() * 4));
     RH_HIP(hipMemcpy(ctx->d_lane16, lt.data(), lt.size() * 4, hipMemcpyHostToDevice));
     return RH_OK;

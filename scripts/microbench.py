@@ -64,6 +64,42 @@ def main():
         del ss, fb
         torch.cuda.empty_cache()
 
+    if "crcshape" in only:
+        # CRC cost per frame vs frame length (dense frame tables): uniform sizes, then ragged
+        for fsz in (256, 516, 1028, 2052, 4096):
+            ss = workload.synth_segments(ctx, n_segments=a.segments, frame_size=fsz, corrupt_rate=0)
+            fb = ss.batch
+            xs = [timed(lambda i=0: engine.crc32c_frames(ctx, fb, flags=_lib.RH_CRC_VERIFY), ss.frame_bytes, a.iters)
+                  for _ in range(a.rounds)]
+            assert int(fb.n_bad.item()) == 0
+            report("crc32c", xs, shape=f"uniform {fsz}B", frames=fb.n,
+                   ns_per_frame=round(ss.frame_bytes / float(np.median(xs)) / fb.n, 3))
+            del ss, fb
+            torch.cuda.empty_cache()
+        for lo, hi in ((64, 2048), (64, 512), (1024, 4096)):
+            rs = workload.synth_ragged_segments(ctx, n_segments=a.segments, min_frame=lo, max_frame=hi)
+            fb = rs.batch
+            nbytes = int(fb.frame_len.sum().item())
+            xs = [timed(lambda i=0: engine.crc32c_frames(ctx, fb, flags=_lib.RH_CRC_VERIFY), nbytes, a.iters)
+                  for _ in range(a.rounds)]
+            assert int(fb.n_bad.item()) == 0
+            report("crc32c", xs, shape=f"ragged {lo}-{hi}B", frames=fb.n,
+                   ns_per_frame=round(nbytes / float(np.median(xs)) / fb.n, 3))
+            del rs, fb
+            torch.cuda.empty_cache()
+
+    if "ragread" in only:
+        # rh_segments_read_launch (framing + CRC verify + verdict) over ragged 64-2048 B segments
+        rs = workload.synth_ragged_segments(ctx, n_segments=a.segments, min_frame=64, max_frame=2048)
+        n = rs.n_segments
+        sb = engine.SegmentBatch(buf=rs.batch.buf, seg_off=torch.arange(n, device="cuda", dtype=torch.int64) * rs.segment_size,
+                                 seg_len=torch.full((n,), rs.segment_size, device="cuda", dtype=torch.int64),
+                                 frames_per_seg_cap=int(rs.seg_nframes.max()) + 16)
+        xs = [timed(lambda i=0: engine.read_segments_fused(ctx, sb), n * rs.segment_size, a.iters) for _ in range(a.rounds)]
+        report("read_launch", xs, shape="ragged 64-2048B", segments=n)
+        del rs, sb
+        torch.cuda.empty_cache()
+
     def framing(sets, tag):
         buf, n, seg_size, cap, nfr = sets
         sb = engine.SegmentBatch(buf=buf, seg_off=torch.arange(n, device="cuda", dtype=torch.int64) * seg_size,

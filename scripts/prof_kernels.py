@@ -12,7 +12,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--what", choices=["crc", "commit", "framing", "ragged", "lease"], default="crc")
+    ap.add_argument("--what", choices=["crc", "commit", "framing", "ragged", "ragged_read", "lease"], default="crc")
     ap.add_argument("--max-frame", type=int, default=2048, help="ragged: frames of 64..max_frame bytes")
     ap.add_argument("--segments", type=int, default=32)
     ap.add_argument("--iters", type=int, default=5)
@@ -32,6 +32,17 @@ def main():
             engine.segments_scan(ctx, sb)
         torch.cuda.synchronize()
         print("seg_bytes", n * ss.segment_size, "segments", n)
+    elif a.what == "ragged_read":
+        rs = workload.synth_ragged_segments(ctx, n_segments=a.segments, min_frame=64, max_frame=a.max_frame, seed=7)
+        n = rs.n_segments
+        sb = engine.SegmentBatch(buf=rs.batch.buf,
+                                 seg_off=torch.arange(n, device="cuda", dtype=torch.int64) * rs.segment_size,
+                                 seg_len=torch.full((n,), rs.segment_size, device="cuda", dtype=torch.int64),
+                                 frames_per_seg_cap=int(rs.seg_nframes.max()) + 16)
+        for _ in range(a.iters):
+            engine.read_segments_fused(ctx, sb)
+        torch.cuda.synchronize()
+        print("seg_bytes", n * rs.segment_size, "segments", n)
     elif a.what == "ragged":
         rs = workload.synth_ragged_segments(ctx, n_segments=a.segments, min_frame=64, max_frame=a.max_frame, seed=7)
         n = rs.n_segments

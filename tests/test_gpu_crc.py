@@ -261,3 +261,82 @@ def test_config5_full_size_one_gpu_share(ctx, orc):
     assert np.array_equal(np.nonzero(want_bad)[0], ss.corrupted) and ss.corrupted.size > 0
     del ss, fb, img
     torch.cuda.empty_cache()
+
+
+def _mixed_frames(rng, n):
+    """n frames (whole length incl. the trailer) of every kind the launch classifies: the lane
+    kernels' class boundaries (CRC spans 8, 63..65, 767..769, 1535..1537 bytes), spans of 8..1600
+    bytes, long frames for the window kernel (1541..20000) and short ones for its guarded path
+    (4..11), laid out back to back at random alignments (mean length under 2 KiB, so the launch
+    takes the lane split); the frame table in random order."""
+    kinds = rng.random(n)
+    lens = np.where(kinds < 0.72, rng.integers(12, 1605, n),
+                    np.where(kinds < 0.84, rng.choice([12, 67, 68, 69, 771, 772, 773, 1539, 1540, 1541], n),
+                             np.where(kinds < 0.92, rng.integers(1541, 20001, n), rng.integers(4, 12, n))))
+    gaps = rng.integers(0, 4, n)
+    offs = 80 + np.cumsum(gaps + lens) - lens
+    perm = rng.permutation(n)
+    return offs[perm].astype(np.int64), lens[perm].astype(np.int32), int(offs[-1] + lens[-1] if n else 80) + 16
+
+
+@pytest.mark.parametrize("seed", [0, 1])
+def test_lane_and_window_paths_mixed_unsorted(ctx, orc, seed):
+    """The classify / sort / lane kernels / window kernel split: every frame's CRC, the stamped
+    image and the mismatch set equal the oracle's for an unsorted table of mixed lengths (all three
+    kernels, every chunk-count class boundary, groups mixing classes, waves running several
+    groups, the window kernel reading its frame list)."""
+    import torch
+
+    from ratis_amd import _lib, engine
+    rng = np.random.default_rng(100 + seed)
+    offs, lens, total = _mixed_frames(rng, 40000)
+    assert total / offs.size <= 2048   # the lane split is taken (rh_crc32c_frames_launch's rule)
+    img = rng.integers(0, 256, size=total, dtype=np.uint8)
+    want_crc, _ = orc.crc32c_frames_all(img, offs, lens)
+    end = offs + lens
+    for k in range(4):   # the oracle writer's trailers (OUT:100-107, big-endian)
+        img[end - 4 + k] = ((want_crc >> (24 - 8 * k)) & 0xFF).astype(np.uint8)
+    # STAMP from zeroed trailers reproduces the oracle writer's image byte for byte
+    blank = img.copy()
+    for k in range(4):
+        blank[end - 4 + k] = 0
+    fb = _batch(blank, offs, lens)
+    engine.crc32c_frames(ctx, fb, flags=_lib.RH_CRC_STAMP)
+    torch.cuda.synchronize()
+    assert np.array_equal(fb.buf.cpu().numpy(), img)
+    assert np.array_equal(fb.crc_out.cpu().numpy().view(np.uint32), want_crc)
+    # VERIFY after corrupting a few payloads
+    bad_at = rng.choice(offs.size, 25, replace=False)
+    img[offs[bad_at] + (lens[bad_at] - 4) // 2] ^= 0x10
+    want_crc, want_bad = orc.crc32c_frames_all(img, offs, lens)
+    fb = _batch(img, offs, lens)
+    engine.crc32c_frames(ctx, fb, flags=_lib.RH_CRC_VERIFY)
+    torch.cuda.synchronize()
+    assert np.array_equal(fb.crc_out.cpu().numpy().view(np.uint32), want_crc)
+    assert np.array_equal(_bits(fb.bad_bits.cpu().numpy(), offs.size), want_bad)
+    assert int(fb.n_bad.item()) == int(want_bad.sum()) and want_bad.sum() >= 20
+
+
+def test_lane_path_plain_spans_from_any_state(ctx, orc):
+    """flags = 0 (plain spans, no trailer) from a non-reset PureJavaCrc32C state, over spans on both
+    sides of the lane kernels' 1536-byte bound, in random table order (lane split taken)."""
+    import torch
+
+    from ratis_amd import engine
+    rng = np.random.default_rng(7)
+    n = 6000
+    lens = np.where(rng.random(n) < 0.85, rng.integers(0, 1700, n), rng.integers(1700, 9000, n)).astype(np.int32)
+    offs = (100 + np.cumsum(lens + rng.integers(0, 5, n)) - lens).astype(np.int64)
+    perm = rng.permutation(n)
+    offs, lens = offs[perm], lens[perm]
+    img = rng.integers(0, 256, size=int(offs.max() + 9100), dtype=np.uint8)
+    assert img.size / n <= 2048
+    st = 0x1234ABCD
+    fb = engine.FrameBatch(buf=_dev(img), frame_off=_dev(offs), frame_len=_dev(lens)).alloc_outputs()
+    engine.crc32c_frames(ctx, fb, flags=0, init_state=st)
+    torch.cuda.synchronize()
+    got = fb.crc_out.cpu().numpy().view(np.uint32)
+    want = np.array([(~orc.crc32c_update(st, img[o:o + l].tobytes())) & 0xFFFFFFFF for o, l in zip(offs, lens)],
+                    dtype=np.uint32)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, [(int(offs[i]), int(lens[i])) for i in bad[:10]]
