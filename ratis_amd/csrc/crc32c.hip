@@ -676,6 +676,7 @@ __global__ __launch_bounds__(kCrcThreads) void crc_lanes_kernel(LaneArgs a) {
     };
     struct Task {
         Rec r;
+        int64_t be;     // end of this lane's chunk: E - W (nmax - 1 - k) - 64 (Q - 1 - gl)
         uint32_t g;     // group (>= ngroups: done)
         uint32_t k;     // step
         uint32_t nmax;  // steps of the group
@@ -690,32 +691,28 @@ __global__ __launch_bounds__(kCrcThreads) void crc_lanes_kernel(LaneArgs a) {
         return Rec{x.o, x.lc, ok ? x.f : 0xFFFFFFFFu};
     };
     auto enter = [&](uint32_t g, const Rec& r) -> Task {
-        Task t{r, g, 0u, 0u};
+        Task t{r, 0, g, 0u, 0u};
         if (g < ngroups) {
             const uint32_t last = nrec - 1 - g * G < (uint32_t)(G - 1) ? nrec - 1 - g * G : (uint32_t)(G - 1);
             const uint32_t nw = (uint32_t)(((int64_t)r.lc + W - 1) / W);  // longest frame: the last one
             t.nmax = (uint32_t)__builtin_amdgcn_readfirstlane(__shfl((int)nw, (int)(last * Q)));
+            t.be = r.o + (int64_t)r.lc - W * (int64_t)(t.nmax - 1) - 64 * (int64_t)(Q - 1 - gl);
         }
         return t;
     };
     Rec pre = fetch(wv + nwv);  // record of the group after the newest task's group
     auto next = [&](const Task& x) -> Task {
         Task t = x;
-        if (x.g < ngroups) t = x.k + 1 < x.nmax ? Task{x.r, x.g, x.k + 1, x.nmax} : enter(x.g + nwv, pre);
+        if (x.g < ngroups) t = x.k + 1 < x.nmax ? Task{x.r, x.be + W, x.g, x.k + 1, x.nmax} : enter(x.g + nwv, pre);
         pre = fetch(t.g + nwv);  // every step (see fetch)
         return t;
     };
-    // chunk of task x in this lane: [be - 64, be), be = E - W (nmax - 1 - k) - 64 (Q - 1 - gl);
-    // loads 72 bytes from the 4-aligned b0 = be - 64 - (E & 3) (the last 8 hold the trailer)
-    auto chunk_end = [&](const Task& x) -> int64_t {
-        return x.r.o + (int64_t)x.r.lc - W * (int64_t)(x.nmax - 1 - x.k) - 64 * (int64_t)(Q - 1 - gl);
-    };
+    // chunk of task x in this lane: [be - 64, be); loads 72 bytes from the 4-aligned
+    // b0 = be - 64 - (E & 3) (the last 8 hold the trailer)
     auto load = [&](const Task& x, uint32_t (&dd)[18]) {
         const uint8_t* src = a.buf;
-        if (x.g < ngroups && x.r.f != 0xFFFFFFFFu) {
-            const int64_t be = chunk_end(x);
-            if (be > x.r.o) src = a.buf + (be - 64 - ((x.r.o + (int64_t)x.r.lc) & 3));
-        }
+        if (x.g < ngroups && x.r.f != 0xFFFFFFFFu && x.be > x.r.o)
+            src = a.buf + (x.be - 64 - (int64_t)((uint32_t)x.r.o + x.r.lc & 3u));
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const u32x4a v = *reinterpret_cast<const u32x4a*>(src + 16 * q);
@@ -733,7 +730,7 @@ __global__ __launch_bounds__(kCrcThreads) void crc_lanes_kernel(LaneArgs a) {
         const bool valid = x.r.f != 0xFFFFFFFFu;
         const int64_t E = x.r.o + (int64_t)x.r.lc;
         const uint32_t sh = (uint32_t)(E & 3);
-        const int64_t be = chunk_end(x);
+        const int64_t be = x.be;
         const bool act = valid && be > x.r.o;
         const int64_t q0l = be - 64 - (int64_t)sh - x.r.o;
         if (__any(act && q0l < 4)) mask_frame_start(d, q0l, act && q0l < 4, a.init);

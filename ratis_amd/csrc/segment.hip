@@ -555,11 +555,15 @@ __global__ __launch_bounds__(256) void segment_compact_kernel(const uint64_t* sc
 // frames the serial walk accepts without its rule-by-rule step; everything else is the resume
 // pass's.  Integer byte work, no MFMA: the guess pass streams 1/8 of the bytes through LDS, the
 // walks touch one header per frame.
-constexpr uint32_t kPiece = 131072;      // bytes per piece
+#ifndef RH_PIECE_BYTES  // A/B builds override (scripts/ab_build.sh)
+#define RH_PIECE_BYTES 131072
+#define RH_PIECE_LIST 1024
+#endif
+constexpr uint32_t kPiece = RH_PIECE_BYTES;  // bytes per piece
 constexpr uint32_t kGuessWin = 16384;    // bytes of a piece the guess pass looks at
 constexpr uint32_t kGuessLds = kGuessWin + 64;
 constexpr int kPieceThreads = 512;
-constexpr uint32_t kList = 1024;         // frame lengths (u16) a guessed walk records
+constexpr uint32_t kList = RH_PIECE_LIST;  // frame lengths (u16) a guessed walk records
 constexpr uint32_t kListPerLane = kList / 64;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 
@@ -669,7 +673,9 @@ __global__ __launch_bounds__(kScanThreads) void piece_plan_kernel(PieceArgs a) {
     }
 }
 
-// The guess per piece (see above).  Block-uniform control; LDS holds the guess window.
+// The guess per piece (see above).  Block-uniform control; LDS holds the guess window.  The next
+// piece's window is loaded into registers while the candidate rounds of this one run (its HBM
+// latency was the larger part of a piece's time), then stored into LDS after the last round.
 __global__ __launch_bounds__(kPieceThreads) void piece_guess_kernel(PieceArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t img[kGuessLds];
     __shared__ unsigned int sh_best;
@@ -677,45 +683,67 @@ __global__ __launch_bounds__(kPieceThreads) void piece_guess_kernel(PieceArgs a)
     constexpr uint32_t kPer = (kGuessLds + kPieceThreads * 16 - 1) / (kPieceThreads * 16);
     const int t = threadIdx.x;
     const unsigned int total = *a.n_pieces;
-    for (unsigned int w = blockIdx.x; w < total; w += gridDim.x) {
-        const uint32_t s = a.piece_seg[w];
-        if (s == kNone) continue;  // block-uniform
-        const uint32_t i = w - a.piece_first[s];
-        const uint32_t pd = (uint32_t)a.seg_stop[s];
-        if (i == 0) {  // the deferral point is a true frame position
-            if (t == 0) a.guess[w] = pd;
-            continue;
+    struct Item {
+        uint32_t s, Bi, We, L, o0, ilen;
+        uint64_t base;
+    };
+    // the next work item at or after w (stride gridDim.x) that needs a guess; a segment's first
+    // piece starts at the deferral point, a true frame position (no guess)
+    auto find = [&](unsigned int w) -> unsigned int {
+        for (; w < total; w += gridDim.x) {
+            const uint32_t s = a.piece_seg[w];
+            if (s == kNone) continue;  // block-uniform
+            if (w == a.piece_first[s]) {
+                if (t == 0) a.guess[w] = (uint32_t)a.seg_stop[s];
+                continue;
+            }
+            return w;
         }
-        const uint64_t base = a.seg_off[s];
-        const uint32_t L = (uint32_t)a.seg_len[s];
-        uint32_t Bi, Bn;
-        piece_bounds(pd, L, i, Bi, Bn);
-        const uint32_t We = Bn - Bi > kGuessWin ? Bi + kGuessWin : Bn;  // guess window end
-        // image: segment bytes [Bi - o0, Bi - o0 + kGuessLds) on a 16-byte grid, zero past the
-        // region end min(We + 32, L); image index of segment position p = p - Bi + o0
-        const uint32_t o0 = (uint32_t)((base + Bi) & 15u);
-        const uint32_t rend = L - We > 32u ? We + 32u : L;
-        const uint32_t ilen = rend - Bi + o0;
+        return total;
+    };
+    // image: segment bytes [Bi - o0, Bi - o0 + kGuessLds) on a 16-byte grid, zero past the region
+    // end min(We + 32, L); image index of segment position p = p - Bi + o0
+    auto describe = [&](unsigned int w) -> Item {
+        Item it{};
+        if (w >= total) return it;
+        it.s = a.piece_seg[w];
+        it.base = a.seg_off[it.s];
+        it.L = (uint32_t)a.seg_len[it.s];
+        uint32_t Bn;
+        piece_bounds((uint32_t)a.seg_stop[it.s], it.L, w - a.piece_first[it.s], it.Bi, Bn);
+        it.We = Bn - it.Bi > kGuessWin ? it.Bi + kGuessWin : Bn;  // guess window end
+        it.o0 = (uint32_t)((it.base + it.Bi) & 15u);
+        const uint32_t rend = it.L - it.We > 32u ? it.We + 32u : it.L;
+        it.ilen = rend - it.Bi + it.o0;
+        return it;
+    };
+    u32x4s v[kPer];
+    auto issue = [&](const Item& it) {  // every load in flight before any use
+        const uint8_t* src = a.buf + it.base + it.Bi - it.o0;
+#pragma unroll
+        for (uint32_t k = 0; k < kPer; ++k) {
+            const uint32_t c = ((uint32_t)t + k * kPieceThreads) * 16u;
+            v[k] = u32x4s{0, 0, 0, 0};
+            if (c + 16 <= it.ilen) v[k] = *reinterpret_cast<const u32x4s*>(src + c);
+        }
+    };
+    unsigned int w = find(blockIdx.x);
+    Item cur = describe(w);
+    if (w < total) issue(cur);
+    while (w < total) {
         if (t == 0) {
             sh_best = kNone;
             sh_zero = 0;
         }
-        const uint8_t* src = a.buf + base + Bi - o0;
-        u32x4s v[kPer];
-#pragma unroll
-        for (uint32_t k = 0; k < kPer; ++k) {  // every load in flight before the first LDS store
-            const uint32_t c = ((uint32_t)t + k * kPieceThreads) * 16u;
-            v[k] = u32x4s{0, 0, 0, 0};
-            if (c + 16 <= ilen) v[k] = *reinterpret_cast<const u32x4s*>(src + c);
-        }
         unsigned int lastnz = 0;  // 1 + highest image index holding a non-zero byte (this thread)
+        const uint8_t* src = a.buf + cur.base + cur.Bi - cur.o0;
 #pragma unroll
         for (uint32_t k = 0; k < kPer; ++k) {
             const uint32_t c = ((uint32_t)t + k * kPieceThreads) * 16u;
             if (c >= kGuessLds) continue;
-            if (c < ilen && c + 16 > ilen) {
+            if (c < cur.ilen && c + 16 > cur.ilen) {
                 uint32_t wv[4] = {0, 0, 0, 0};
-                for (uint32_t b = 0; c + b < ilen; ++b) wv[b >> 2] |= (uint32_t)src[c + b] << (8 * (b & 3));
+                for (uint32_t b = 0; c + b < cur.ilen; ++b) wv[b >> 2] |= (uint32_t)src[c + b] << (8 * (b & 3));
                 v[k] = {wv[0], wv[1], wv[2], wv[3]};
             }
             *reinterpret_cast<u32x4s*>(img + c) = v[k];
@@ -730,32 +758,39 @@ __global__ __launch_bounds__(kPieceThreads) void piece_guess_kernel(PieceArgs a)
         }
         __syncthreads();
         if (lastnz) atomicMax(&sh_zero, lastnz);
+        // the next piece's window into registers while this one's rounds run
+        const unsigned int w2 = find(w + gridDim.x);
+        const Item nxt = describe(w2);
+        if (w2 < total) issue(nxt);
         __syncthreads();
+        const uint32_t Bi = cur.Bi, We = cur.We, L = cur.L, o0 = cur.o0;
         const uint32_t zpos = sh_zero >= o0 ? Bi + sh_zero - o0 : Bi;  // segment position
-        const uint32_t gm0 = a.seg_gmax[s] * 2u;
+        const uint32_t gm0 = a.seg_gmax[cur.s] * 2u;
         const uint32_t gmax = gm0 < 1024u ? 1024u : gm0 > kGuessWin ? kGuessWin : gm0;
         const uint32_t ncand = We - Bi < 4u * gmax ? We - Bi : 4u * gmax;
-        // rounds of kPieceThreads candidate starts until one survives
+        // rounds of kPieceThreads candidate starts until one survives.  The walk is a lockstep
+        // loop of predicated steps (one uniform branch per step): a candidate's chain
+        //   leaves the window, or reaches the rule-by-rule step's EOF zone   -> survives
+        //   reaches a header the fast path rejects                          -> survives iff the
+        //                                                                      rest is zero (terminator)
+        //   meets a frame longer than gmax (implausible for this log)       -> dies
+        const uint32_t* img32 = reinterpret_cast<const uint32_t*>(img);
+        const uint32_t qend = We - Bi + o0;                        // window end (image index)
+        const uint32_t qeof = L >= Bi + 8 ? L - 8 - Bi + o0 : 0u;  // p + 8 >= L  <=>  q >= qeof
+        const uint32_t qz = zpos - Bi + o0;
         for (uint32_t r0 = 0; r0 < ncand; r0 += kPieceThreads) {
             const uint32_t ci = r0 + (uint32_t)t;
-            uint32_t p = Bi + ci;
-            bool alive = ci < ncand, surv = false;
-            while (alive) {
-                if (p >= We || p + 8 >= L) {  // left the window, or the rule-by-rule step's (EOF)
-                    surv = true;
-                    break;
-                }
-                const uint32_t q = p - Bi + o0;
-                const uint32_t lo = *reinterpret_cast<const uint32_t*>(img + (q & ~3u));
-                const uint32_t hi = *reinterpret_cast<const uint32_t*>(img + (q & ~3u) + 4);
-                const uint32_t hv = (uint32_t)((((uint64_t)hi << 32) | lo) >> (8 * (q & 3)));
-                const uint32_t fl = fast_frame_len(hv, L - p, a.max_op);
-                if (fl == 0) {  // the fast walk ends here: a terminator if the rest is zero
-                    surv = p >= zpos;
-                    break;
-                }
-                if (fl > gmax) break;  // implausible for this log: a false start
-                p += fl;
+            uint32_t q = ci + o0;  // image index of the walk position p = Bi + q - o0
+            bool run = ci < ncand, surv = false;
+            while (__any(run)) {
+                const bool out = q >= qend || q >= qeof;
+                const uint32_t qa = out ? 0u : q;  // in-image address for the lanes that read
+                const uint32_t wi = qa >> 2;
+                const uint32_t hv = __builtin_amdgcn_alignbyte(img32[wi + 1], img32[wi], qa & 3u);
+                const uint32_t fl = fast_frame_len(hv, L - (Bi + q - o0), a.max_op);
+                surv = surv || (run && (out || (fl == 0 && q >= qz)));
+                run = run && !out && fl != 0 && fl <= gmax;
+                q += run ? fl : 0u;
             }
             if (surv) atomicMin(&sh_best, ci);
             __syncthreads();
@@ -765,6 +800,8 @@ __global__ __launch_bounds__(kPieceThreads) void piece_guess_kernel(PieceArgs a)
         }
         if (t == 0) a.guess[w] = sh_best == kNone ? kNone : Bi + sh_best;
         __syncthreads();
+        w = w2;
+        cur = nxt;
     }
 }
 
@@ -972,13 +1009,10 @@ constexpr int kWalkWindow = 32768;  // 2 x 32 KiB LDS ring + mirror: two blocks 
 
 hipError_t launch_walk(const SegArgs& a, int cus, hipStream_t stream) {
     constexpr int lds = 2 * kWalkWindow + 16;
-    static bool attr_set = false;  // set once per process; hipFuncSetAttribute is idempotent
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(segment_walk_kernel<kWalkWindow>),
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, lds);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
+    // once per process (thread-safe static initialisation)
+    static const hipError_t attr = hipFuncSetAttribute(
+        reinterpret_cast<const void*>(segment_walk_kernel<kWalkWindow>), hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (attr != hipSuccess) return attr;
     const uint64_t cap = (uint64_t)cus * 2;
     const uint64_t grid = a.n_seg < cap ? a.n_seg : cap;
     hipLaunchKernelGGL((segment_walk_kernel<kWalkWindow>), dim3((uint32_t)grid), dim3(kBlock2), lds, stream, a);

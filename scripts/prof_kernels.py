@@ -12,9 +12,10 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--what", choices=["crc", "commit", "framing", "ragged", "ragged_read", "lease"], default="crc")
+    ap.add_argument("--what", choices=["crc", "crcshape", "crcragged", "commit", "framing", "ragged", "ragged_read", "lease"], default="crc")
     ap.add_argument("--max-frame", type=int, default=2048, help="ragged: frames of 64..max_frame bytes")
     ap.add_argument("--segments", type=int, default=32)
+    ap.add_argument("--frame-size", type=int, default=516, help="crcshape: uniform frame size")
     ap.add_argument("--iters", type=int, default=5)
     a = ap.parse_args()
     import torch
@@ -75,6 +76,18 @@ def main():
         torch.cuda.synchronize()
         alg = sum(h.follower.size * 8 + h.n * 20 + 2 * ((h.n + 63) // 64) * 8 for h in host)
         print("lease_bytes", alg, "groups", sum(h.n for h in host))
+    elif a.what == "crcshape":
+        ss = workload.synth_segments(ctx, n_segments=a.segments, frame_size=a.frame_size, corrupt_rate=0)
+        for _ in range(a.iters):
+            engine.crc32c_frames(ctx, ss.batch, flags=_lib.RH_CRC_VERIFY)
+        torch.cuda.synchronize()
+        print("frame_bytes", ss.frame_bytes, "frames", ss.batch.n)
+    elif a.what == "crcragged":
+        rs = workload.synth_ragged_segments(ctx, n_segments=a.segments, min_frame=64, max_frame=a.max_frame, seed=7)
+        for _ in range(a.iters):
+            engine.crc32c_frames(ctx, rs.batch, flags=_lib.RH_CRC_VERIFY)
+        torch.cuda.synchronize()
+        print("frames", rs.batch.n)
     elif a.what == "crc":
         ss = workload.synth_segments(ctx, n_segments=a.segments, corrupt_rate=0)
         for _ in range(a.iters):
