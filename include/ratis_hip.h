@@ -366,7 +366,12 @@ typedef struct rh_frames {
     unsigned long long* n_bad;    /* optional: such frames are atomically added here             */
 } rh_frames;
 
-/* CRC of every frame (one launch).  Lengths <= 2^31; spans shorter than 4 bytes are supported.
+/* CRC of every frame (one call; asynchronous on `stream`).  Lengths <= 2^31; spans shorter than 4
+ * bytes are supported; n < 2^32 (else RH_E_RANGE).  When the mean frame length buf_len / n is at
+ * most 2 KiB the call sorts the frames by length (20 B of stream-ordered scratch per frame from the
+ * context's pool) and folds spans up to 1536 B on 4 or 8 lanes per frame; every other frame, and
+ * every frame of a log of longer entries, on 16 lanes per 1 KiB window.  Results do not depend on
+ * the split.
  * A MALFORMED frame -- one that does not lie inside [0, buf_len), or (VERIFY/STAMP) is shorter
  * than its 4-byte trailer -- gets crc_out = 0 and, under EVERY flag setting, its bad bit set and
  * n_bad incremented; in STAMP mode it is not stamped.  So bad_bits / n_bad report "mismatch or
