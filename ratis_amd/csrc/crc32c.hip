@@ -137,6 +137,12 @@ struct FrameArgs {
     const uint32_t* slot_nframes;
     uint32_t slot_cap;
     uint32_t* seg_first_bad;
+    // slot mode, dense outputs (the read path's crc_out / bad_bits): slot s of segment g is frame
+    // seg_first[g] + s of the dense table (below frame_cap)
+    const uint64_t* seg_first;
+    uint32_t* dense_crc;
+    uint64_t* dense_bad;
+    uint64_t frame_cap;
     // lane split (set by the launcher): the frames the lane kernels fold (crc_class > 0) are not
     // this kernel's.  If they are the majority it reads the list of its own frames, widx[0 ..
     // counts[0]) (the scatter's), else it walks the whole table and skips them.
@@ -190,6 +196,29 @@ __device__ __forceinline__ void mask_frame_start(uint32_t (&d)[18], int64_t q0l,
         const uint32_t up = (q >= 0 && q < 4) ? (init >> (8 * q)) : 0u;
         const uint32_t dn2 = (q < 0 && q > -4) ? (init << (8 * -q)) : 0u;
         d[i] = on ? (v ^ up ^ dn2) : d[i];
+    }
+}
+
+// A frame's results: its CRC, and when `bad` (VERIFY mismatch, or malformed) its bad bit and count;
+// in slot mode also the segment's first bad slot and the dense per-frame outputs.
+template <typename A>
+__device__ __forceinline__ void emit_frame(const A& a, uint64_t f, uint32_t value, bool bad) {
+    if (a.crc_out) a.crc_out[f] = value;
+    if (bad) {
+        if (a.bad_bits) atomicOr(reinterpret_cast<unsigned long long*>(a.bad_bits + (f >> 6)), 1ull << (f & 63));
+        if (a.n_bad) atomicAdd(a.n_bad, 1ull);
+    }
+    if (a.seg_first_bad || a.seg_first) {  // slot mode (32-bit: the launcher keeps n below 2^32)
+        const uint32_t seg = (uint32_t)f / a.slot_cap, slot = (uint32_t)f - seg * a.slot_cap;
+        if (bad && a.seg_first_bad) atomicMin(a.seg_first_bad + seg, slot);
+        if (a.seg_first) {
+            const uint64_t d = a.seg_first[seg] + slot;
+            if (d < a.frame_cap) {
+                if (a.dense_crc) a.dense_crc[d] = value;
+                if (bad && a.dense_bad)
+                    atomicOr(reinterpret_cast<unsigned long long*>(a.dense_bad + (d >> 6)), 1ull << (d & 63));
+            }
+        }
     }
 }
 
@@ -392,7 +421,7 @@ __global__ __launch_bounds__(kCrcThreads) void crc_frames_kernel(FrameArgs a) {
                     uint32_t state = R;
                     if (m.lc < 4) state ^= (uint32_t)((uint64_t)a.init >> (8 * m.lc));
                     const uint32_t value = ~state;
-                    if (a.crc_out) a.crc_out[f] = value;
+                    bool bad = false;
                     if (a.flags & RH_CRC_STAMP) {
                         a.wbuf[E + 0] = (uint8_t)(value >> 24);
                         a.wbuf[E + 1] = (uint8_t)(value >> 16);
@@ -400,14 +429,9 @@ __global__ __launch_bounds__(kCrcThreads) void crc_frames_kernel(FrameArgs a) {
                         a.wbuf[E + 3] = (uint8_t)value;
                     } else if (a.flags & RH_CRC_VERIFY) {
                         const uint32_t le = __builtin_amdgcn_alignbyte(d[17], d[16], sh);
-                        const uint32_t stored = __builtin_bswap32(le);  // big-endian trailer
-                        if (stored != value) {
-                            if (a.bad_bits)
-                                atomicOr(reinterpret_cast<unsigned long long*>(a.bad_bits + (f >> 6)), 1ull << (f & 63));
-                            if (a.n_bad) atomicAdd(a.n_bad, 1ull);
-                            if (a.seg_first_bad) atomicMin(a.seg_first_bad + f / a.slot_cap, (uint32_t)(f % a.slot_cap));
-                        }
+                        bad = __builtin_bswap32(le) != value;  // big-endian trailer
                     }
+                    emit_frame(a, f, value, bad);
                 }
                 R = 0;
             }
@@ -442,12 +466,7 @@ __global__ __launch_bounds__(kCrcThreads) void crc_frames_kernel(FrameArgs a) {
             const Meta m = meta(j);
             const uint64_t f = mf[j];
             if (m.fl == 2) {
-                if (gl == 0) {
-                    if (a.crc_out) a.crc_out[f] = 0u;
-                    if (a.bad_bits) atomicOr(reinterpret_cast<unsigned long long*>(a.bad_bits + (f >> 6)), 1ull << (f & 63));
-                    if (a.n_bad) atomicAdd(a.n_bad, 1ull);
-                    if (a.seg_first_bad) atomicMin(a.seg_first_bad + f / a.slot_cap, (uint32_t)(f % a.slot_cap));
-                }
+                if (gl == 0) emit_frame(a, f, 0u, true);
                 continue;
             }
             const int64_t E = m.o + (int64_t)m.lc;
@@ -474,7 +493,7 @@ __global__ __launch_bounds__(kCrcThreads) void crc_frames_kernel(FrameArgs a) {
                 uint32_t state = Rs;
                 if (m.lc < 4) state ^= (uint32_t)((uint64_t)a.init >> (8 * m.lc));
                 const uint32_t value = ~state;
-                if (a.crc_out) a.crc_out[f] = value;
+                bool bad = false;
                 if (a.flags & RH_CRC_STAMP) {
                     a.wbuf[E + 0] = (uint8_t)(value >> 24);
                     a.wbuf[E + 1] = (uint8_t)(value >> 16);
@@ -483,13 +502,9 @@ __global__ __launch_bounds__(kCrcThreads) void crc_frames_kernel(FrameArgs a) {
                 } else if (a.flags & RH_CRC_VERIFY) {
                     const uint32_t stored = ((uint32_t)a.buf[E] << 24) | ((uint32_t)a.buf[E + 1] << 16) |
                                             ((uint32_t)a.buf[E + 2] << 8) | (uint32_t)a.buf[E + 3];
-                    if (stored != value) {
-                        if (a.bad_bits)
-                            atomicOr(reinterpret_cast<unsigned long long*>(a.bad_bits + (f >> 6)), 1ull << (f & 63));
-                        if (a.n_bad) atomicAdd(a.n_bad, 1ull);
-                        if (a.seg_first_bad) atomicMin(a.seg_first_bad + f / a.slot_cap, (uint32_t)(f % a.slot_cap));
-                    }
+                    bad = stored != value;
                 }
+                emit_frame(a, f, value, bad);
             }
         }
     }
@@ -618,6 +633,10 @@ struct LaneArgs {
     uint32_t cls_lo, cls_hi;  // the chunk-count classes this launch folds
     uint32_t slot_cap;
     uint32_t* seg_first_bad;
+    const uint64_t* seg_first;
+    uint32_t* dense_crc;
+    uint64_t* dense_bad;
+    uint64_t frame_cap;
 };
 
 // One wave = one group of G = 64 / Q consecutive records, Q lanes per frame (lane l: record
@@ -765,22 +784,16 @@ __global__ __launch_bounds__(kCrcThreads) void crc_lanes_kernel(LaneArgs a) {
         if (x.k + 1 == x.nmax) {  // every frame of the group ends at this step
             if (valid && gl == Q - 1) {  // the lane whose chunk ends at E
                 const uint32_t value = ~R;
-                const uint32_t f = x.r.f;
-                if (a.crc_out) a.crc_out[f] = value;
+                bool bad = false;
                 if (a.flags & RH_CRC_STAMP) {
                     a.wbuf[E + 0] = (uint8_t)(value >> 24);
                     a.wbuf[E + 1] = (uint8_t)(value >> 16);
                     a.wbuf[E + 2] = (uint8_t)(value >> 8);
                     a.wbuf[E + 3] = (uint8_t)value;
                 } else if (a.flags & RH_CRC_VERIFY) {
-                    const uint32_t stored = __builtin_bswap32(__builtin_amdgcn_alignbyte(d[17], d[16], sh));
-                    if (stored != value) {
-                        if (a.bad_bits)
-                            atomicOr(reinterpret_cast<unsigned long long*>(a.bad_bits + (f >> 6)), 1ull << (f & 63));
-                        if (a.n_bad) atomicAdd(a.n_bad, 1ull);
-                        if (a.seg_first_bad) atomicMin(a.seg_first_bad + f / a.slot_cap, f % a.slot_cap);
-                    }
+                    bad = __builtin_bswap32(__builtin_amdgcn_alignbyte(d[17], d[16], sh)) != value;
                 }
+                emit_frame(a, x.r.f, value, bad);
             }
             R = 0;
         }
@@ -874,6 +887,10 @@ int launch_frames(rh_ctx* ctx, FrameArgs a, hipStream_t stream) {
     l.shift32 = a.shift32;
     l.slot_cap = a.slot_cap;
     l.seg_first_bad = a.seg_first_bad;
+    l.seg_first = a.seg_first;
+    l.dense_crc = a.dense_crc;
+    l.dense_bad = a.dense_bad;
+    l.frame_cap = a.frame_cap;
     // 4 lanes per frame for classes 1..12, 8 for 13..24 (lane tables: Q = 2, 4, 8, 16 at 4096 words each)
     l.lanetab = ctx->d_lane16 + (size_t)1 * 4096;
     l.zwin = ctx->d_shift + (size_t)8 * 1024;
@@ -963,5 +980,11 @@ int rh_crc_verify_slots(rh_ctx* ctx, const rh_segments* g, const rh_segments_crc
     a.slot_nframes = g->seg_nframes;
     a.slot_cap = g->frames_per_seg_cap;
     a.seg_first_bad = c->seg_ok;
+    if (c->crc_out || c->bad_bits) {  // dense per-frame outputs straight from the CRC pass
+        a.seg_first = g->seg_first;
+        a.dense_crc = c->crc_out;
+        a.dense_bad = c->bad_bits;
+        a.frame_cap = g->frame_cap;
+    }
     return launch_frames(ctx, a, stream);
 }

@@ -100,6 +100,18 @@ def main():
         del rs, sb
         torch.cuda.empty_cache()
 
+    if "readc5" in only:
+        # rh_segments_read_launch over config-5 segments (4 KiB frames)
+        ss = workload.synth_segments(ctx, n_segments=a.segments, corrupt_rate=0)
+        n = ss.n_segments
+        sb = engine.SegmentBatch(buf=ss.batch.buf, seg_off=torch.arange(n, device="cuda", dtype=torch.int64) * ss.segment_size,
+                                 seg_len=torch.full((n,), ss.segment_size, device="cuda", dtype=torch.int64),
+                                 frames_per_seg_cap=ss.frames_per_segment + 16)
+        xs = [timed(lambda i=0: engine.read_segments_fused(ctx, sb), n * ss.segment_size, a.iters) for _ in range(a.rounds)]
+        report("read_launch", xs, shape="config5 4096B", segments=n)
+        del ss, sb
+        torch.cuda.empty_cache()
+
     def framing(sets, tag):
         buf, n, seg_size, cap, nfr = sets
         sb = engine.SegmentBatch(buf=buf, seg_off=torch.arange(n, device="cuda", dtype=torch.int64) * seg_size,
