@@ -143,10 +143,7 @@ struct FrameArgs {
     uint32_t* dense_crc;
     uint64_t* dense_bad;
     uint64_t frame_cap;
-    // lane split (set by the launcher): the frames the lane kernels fold (crc_class > 0) are not
-    // this kernel's.  If they are the majority it reads the list of its own frames, widx[0 ..
-    // counts[0]) (the scatter's), else it walks the whole table and skips them.
-    uint32_t lane_split;
+    // crc_frames_kernel<true> (the lane split's window pass): its frames are widx[0 .. counts[0])
     const uint32_t* counts;
     const uint32_t* widx;
 };
@@ -243,7 +240,10 @@ constexpr int kLaneChunks = 24;            // CRC spans up to 1536 B go to the l
 constexpr int kClasses = kLaneChunks + 1;  // class 0: window kernel; class c: c chunks of 64 B
 constexpr uint64_t kLaneMeanMax = 2048;    // mean frame length (buf_len / n) up to which the split runs
 
-constexpr int kBatch = 416;  // 160 KiB of LDS - 152 KiB of tables = 416 x 19 B of batch table
+// Batch table per block: 512 frames x 15 B (start, span, path, guarded list), or in the listed
+// variant 416 x 19 B (+ frame number): what 160 KiB of LDS leaves next to 152 KiB of tables.
+constexpr int kBatchOf(bool listed) { return listed ? 416 : 512; }
+constexpr int kBatch = kBatchOf(false);
 struct Meta {
     int64_t o;    // frame start (bytes)
     uint32_t lc;  // CRC-covered length
@@ -251,10 +251,14 @@ struct Meta {
 };
 
 constexpr int kCrcThreads = 1024;
-constexpr int kCrcLds = 128 * 1024 + 16384 + 8192 + kBatch * 19 + 16;
-static_assert(kCrcLds <= 160 * 1024, "LDS budget");
+constexpr int kCrcLdsOf(bool listed) { return 128 * 1024 + 16384 + 8192 + kBatchOf(listed) * (listed ? 19 : 15) + 16; }
+static_assert(kCrcLdsOf(false) <= 160 * 1024 && kCrcLdsOf(true) <= 160 * 1024, "LDS budget");
 
+// LISTED = false: every frame of the table (the plan for logs of long entries, config 5).
+// LISTED = true: the frames the length-class split left to this kernel, widx[0 .. counts[0]).
+template <bool LISTED>
 __global__ __launch_bounds__(kCrcThreads) void crc_frames_kernel(FrameArgs a) {
+    constexpr int kBatch = kBatchOf(LISTED);
     constexpr int CH = 2;  // independent fold chains per lane (measured: 1 / 4 chains are slower)
     constexpr int Q = 16, S = 64;
     constexpr int64_t W = (int64_t)Q * S;
@@ -262,17 +266,16 @@ __global__ __launch_bounds__(kCrcThreads) void crc_frames_kernel(FrameArgs a) {
     constexpr int kLaneWords = 8 * 16 * 32;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     if (__builtin_amdgcn_groupstaticsize() != 0) __builtin_trap();  // lds_word assumes base 0
-    const bool listed = a.lane_split && 2ull * a.counts[0] < a.n;  // read widx[] (uniform)
-    const uint64_t n_all = listed ? (uint64_t)a.counts[0] : a.n;
-    if ((uint64_t)blockIdx.x * kBatch >= n_all) return;  // no batch for this block: skip the table fill
+    const uint64_t n_all = LISTED ? (uint64_t)a.counts[0] : a.n;
+    if (LISTED && (uint64_t)blockIdx.x * kBatch >= n_all) return;  // no batch: skip the table fill
     uint32_t* llane = lds + kSliceBytes / 4;
     uint32_t* lzw = llane + kLaneWords;
     uint32_t* lch = lzw + 1024;  // [4][256]: advance over 64 / CH zero bytes (chain combine)
     // batch frame table, struct-of-arrays: start, CRC-covered length, path; then the guarded list
     int64_t* mo = reinterpret_cast<int64_t*>(lch + 1024);
     uint32_t* mlc = reinterpret_cast<uint32_t*>(mo + kBatch);
-    uint32_t* mf = mlc + kBatch;  // frame number
-    uint8_t* mfl = reinterpret_cast<uint8_t*>(mf + kBatch);
+    uint32_t* mf = mlc + kBatch;  // LISTED: frame number
+    uint8_t* mfl = reinterpret_cast<uint8_t*>(LISTED ? mf + kBatch : mlc + kBatch);
     uint16_t* slow = reinterpret_cast<uint16_t*>(mfl + kBatch);  // [kBatch] guarded-path frames
     uint32_t* nslow = reinterpret_cast<uint32_t*>(slow + kBatch);
     uint32_t* nexti = nslow + 1;  // next batch frame to hand out (dynamic assignment)
@@ -305,8 +308,8 @@ __global__ __launch_bounds__(kCrcThreads) void crc_frames_kernel(FrameArgs a) {
         }
         __syncthreads();
         if ((uint32_t)t < nb) {
-            const uint64_t f = listed ? (uint64_t)a.widx[b0f + (uint64_t)t] : b0f + (uint64_t)t;
-            mf[t] = (uint32_t)f;
+            const uint64_t f = LISTED ? (uint64_t)a.widx[b0f + (uint64_t)t] : b0f + (uint64_t)t;
+            if (LISTED) mf[t] = (uint32_t)f;
             const uint64_t o = a.off[f];
             const int64_t L = (int64_t)a.len[f];
             const bool malformed = o > (uint64_t)a.buf_len || L > a.buf_len - (int64_t)o || (trailer && L < 4);
@@ -316,7 +319,6 @@ __global__ __launch_bounds__(kCrcThreads) void crc_frames_kernel(FrameArgs a) {
             const int64_t E = m.o + (int64_t)m.lc;
             const bool unsafe = m.o < 67 || E + 8 > a.buf_len || m.lc < 8;
             m.fl = malformed ? 2u : (unsafe ? 1u : 0u);
-            if (a.lane_split && !listed && m.fl == 0u && m.lc <= (uint32_t)kLaneChunks * 64u) m.fl = 3u;  // class > 0
             if (a.slot_nframes) {  // slot mode: slots past the segment's frame count are skipped
                 const uint32_t seg = (uint32_t)f / a.slot_cap, slot = (uint32_t)f - seg * a.slot_cap;
                 const uint32_t nfs = a.slot_nframes[seg];
@@ -417,7 +419,7 @@ __global__ __launch_bounds__(kCrcThreads) void crc_frames_kernel(FrameArgs a) {
             R = zshift(lzw, R) ^ r;
             if ((int64_t)x.wi + 1 >= nw) {
                 if (gl == Q - 1) {  // this lane's chunk ends at E: d[16..17] hold bytes E - sh .. E + 8 - sh
-                    const uint64_t f = mf[x.j];
+                    const uint64_t f = LISTED ? (uint64_t)mf[x.j] : b0f + x.j;
                     uint32_t state = R;
                     if (m.lc < 4) state ^= (uint32_t)((uint64_t)a.init >> (8 * m.lc));
                     const uint32_t value = ~state;
@@ -464,7 +466,7 @@ __global__ __launch_bounds__(kCrcThreads) void crc_frames_kernel(FrameArgs a) {
         for (uint32_t i = grp; i < ns; i += 64) {
             const uint32_t j = slow[i];
             const Meta m = meta(j);
-            const uint64_t f = mf[j];
+            const uint64_t f = LISTED ? (uint64_t)mf[j] : b0f + j;
             if (m.fl == 2) {
                 if (gl == 0) emit_frame(a, f, 0u, true);
                 continue;
@@ -834,9 +836,15 @@ hipError_t launch_lanes(const LaneArgs& l, uint64_t n, uint64_t cus, hipStream_t
 
 // classify -> scatter -> lane kernels (4 and 8 lanes per frame) -> window kernel over the rest,
 // all on `stream`.
-int launch_frames(rh_ctx* ctx, FrameArgs a, hipStream_t stream) {
-    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(crc_frames_kernel),
-                                                       hipFuncAttributeMaxDynamicSharedMemorySize, kCrcLds);
+int launch_frames(rh_ctx* ctx, FrameArgs a, hipStream_t stream, bool* dense_written = nullptr) {
+    static const hipError_t attr = [] {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(crc_frames_kernel<false>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, kCrcLdsOf(false));
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute(reinterpret_cast<const void*>(crc_frames_kernel<true>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, kCrcLdsOf(true));
+        return e;
+    }();
     RH_HIP(attr);
     if (a.n > 0xFFFFFFFFull) return rh::fail(RH_E_RANGE, "CRC launch: more than 2^32 - 1 frames in one launch");
     a.slice = ctx->d_slice;
@@ -852,11 +860,19 @@ int launch_frames(rh_ctx* ctx, FrameArgs a, hipStream_t stream) {
     window_only = true;
 #endif
     if (window_only) {
+        // slot mode: the dense outputs are left to the caller's compaction (a dependent seg_first
+        // load at every frame's end costs the window kernel more than that pass, config 5: -4 %)
+        a.seg_first = nullptr;
+        a.dense_crc = nullptr;
+        a.dense_bad = nullptr;
+        if (dense_written) *dense_written = false;
         const uint64_t wgrid = (a.n + kBatch - 1) / kBatch < cus ? (a.n + kBatch - 1) / kBatch : cus;
-        hipLaunchKernelGGL(crc_frames_kernel, dim3((uint32_t)wgrid), dim3(kCrcThreads), kCrcLds, stream, a);
+        hipLaunchKernelGGL(crc_frames_kernel<false>, dim3((uint32_t)wgrid), dim3(kCrcThreads), kCrcLdsOf(false),
+                           stream, a);
         RH_HIP(hipGetLastError());
         return RH_OK;
     }
+    if (dense_written) *dense_written = a.seg_first != nullptr;
     // scratch: counts[kClasses], cursor[kClasses], rec[n], widx[n]
     const size_t o_rec = 1024, o_widx = o_rec + (size_t)a.n * sizeof(LaneRec), bytes = o_widx + (size_t)a.n * 4;
     void* scratch = nullptr;
@@ -902,11 +918,11 @@ int launch_frames(rh_ctx* ctx, FrameArgs a, hipStream_t stream) {
     l.cls_lo = kQ4Chunks + 1;
     l.cls_hi = kLaneChunks;
     RH_HIP(launch_lanes<8>(l, a.n, cus, stream));
-    a.lane_split = 1;
     a.counts = counts;
     a.widx = widx;
-    const uint64_t wgrid = (a.n + kBatch - 1) / kBatch < cus ? (a.n + kBatch - 1) / kBatch : cus;
-    hipLaunchKernelGGL(crc_frames_kernel, dim3((uint32_t)wgrid), dim3(kCrcThreads), kCrcLds, stream, a);
+    constexpr uint64_t kBL = kBatchOf(true);
+    const uint64_t wgrid = (a.n + kBL - 1) / kBL < cus ? (a.n + kBL - 1) / kBL : cus;
+    hipLaunchKernelGGL(crc_frames_kernel<true>, dim3((uint32_t)wgrid), dim3(kCrcThreads), kCrcLdsOf(true), stream, a);
     RH_HIP(hipGetLastError());
     RH_HIP(hipFreeAsync(scratch, stream));
     return RH_OK;
@@ -964,7 +980,8 @@ int rh_crc_launch_impl(rh_ctx* ctx, const rh_frames* f, uint32_t flags, hipStrea
 // framing walk left in segs->scratch_off/len, VERIFY, CRCs into crc->scratch_crc (slot-indexed),
 // mismatches counted in crc->n_bad and the first bad slot of each segment atomically lowered in
 // crc->seg_ok (pre-set to 0xFFFFFFFF by the caller).
-int rh_crc_verify_slots(rh_ctx* ctx, const rh_segments* g, const rh_segments_crc* c, hipStream_t stream) {
+int rh_crc_verify_slots(rh_ctx* ctx, const rh_segments* g, const rh_segments_crc* c, hipStream_t stream,
+                        bool* dense_written) {
     FrameArgs a{};
     a.buf = g->buf;
     a.wbuf = nullptr;
@@ -986,5 +1003,5 @@ int rh_crc_verify_slots(rh_ctx* ctx, const rh_segments* g, const rh_segments_crc
         a.dense_bad = c->bad_bits;
         a.frame_cap = g->frame_cap;
     }
-    return launch_frames(ctx, a, stream);
+    return launch_frames(ctx, a, stream, dense_written);
 }

@@ -151,7 +151,10 @@ int rh_crc_launch_impl(rh_ctx* ctx, const rh_frames* f, uint32_t flags, hipStrea
 int rh_crc_upload_tables(rh_ctx* ctx);
 int rh_segments_launch_impl(rh_ctx* ctx, const rh_segments* segs, hipStream_t stream);
 int rh_segments_read_impl(rh_ctx* ctx, const rh_segments* segs, const rh_segments_crc* crc, hipStream_t stream);
-int rh_crc_verify_slots(rh_ctx* ctx, const rh_segments* segs, const rh_segments_crc* crc, hipStream_t stream);
+// *dense_written: whether the pass also wrote crc->crc_out / bad_bits (the length-class plan);
+// else the caller compacts them from the slots.
+int rh_crc_verify_slots(rh_ctx* ctx, const rh_segments* segs, const rh_segments_crc* crc, hipStream_t stream,
+                        bool* dense_written);
 int rh_lease_launch_impl(rh_ctx* ctx, const rh_lease_soa* tiers, int n_tiers, hipStream_t stream);
 int rh_lease_validate(const rh_lease_soa* tiers, int n_tiers);
 int rh_lease_launch_class(const rh_lease_soa* tiers, int n_tiers, int flo, int fhi, hipStream_t stream);
