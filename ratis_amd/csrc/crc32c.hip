@@ -183,16 +183,21 @@ __device__ __forceinline__ uint32_t fold_word_perm(const uint32_t* lds, uint32_t
 // after the frame start (q0l < 4: the chunk holds frame bytes 0..3).  Bytes before the frame are
 // zeroed (a zero register absorbs leading zeros) and reset()'s state is XOR-ed into frame bytes
 // 0..3, so folding the chunk from a zero register is folding the frame from `init`.
+// Word i starts s = -(q0l + 4i) bytes before the frame start: it keeps its bytes >= s
+// (mask ~0 << 8 clamp(s, 0, 4)) and takes init shifted by s bytes, i.e. the low word of
+// (init << 32) >> (32 - 8 clamp(s, -4, 4)) -- both ends of that clamp give 0 (a 64-bit shift by
+// 0 or 64 = 0 mod 64 of a value whose low half is 0).  Lanes with `on` false: s <= -4 everywhere.
 __device__ __forceinline__ void mask_frame_start(uint32_t (&d)[18], int64_t q0l, bool on, uint32_t init) {
-    const int q0 = (int)(q0l < -80 ? -80 : (q0l > 4 ? 4 : q0l));
+    const int32_t s8_0 = on ? -8 * (int32_t)q0l : -32;  // 8 s for word 0 (q0l in (-68, 4) when on)
+    const uint64_t X = (uint64_t)init << 32;
 #pragma unroll
     for (int i = 0; i < 17; ++i) {
-        const int q = q0 + 4 * i;
-        uint32_t v = d[i];
-        v = (q <= -4) ? 0u : (q < 0 ? (v & (0xFFFFFFFFu << (8 * -q))) : v);
-        const uint32_t up = (q >= 0 && q < 4) ? (init >> (8 * q)) : 0u;
-        const uint32_t dn2 = (q < 0 && q > -4) ? (init << (8 * -q)) : 0u;
-        d[i] = on ? (v ^ up ^ dn2) : d[i];
+        const int32_t s8 = s8_0 - 32 * i;
+        const int32_t k = min(max(s8, 0), 32);   // garbage bits at the word's low end (v_med3)
+        const int32_t m = min(max(s8, -32), 32);
+        const uint32_t keep = (uint32_t)(~0ull << k);
+        const uint32_t inj = (uint32_t)(X >> ((uint32_t)(32 - m) & 63u));
+        d[i] = (d[i] & keep) ^ inj;
     }
 }
 
