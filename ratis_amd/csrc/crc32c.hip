@@ -240,8 +240,12 @@ __device__ __forceinline__ void emit_frame(const A& a, uint64_t f, uint32_t valu
 // profiles/r02/crc_lanes/): spans up to 768 B on 4 lanes per frame, up to 1536 B on 8; longer
 // spans fill the 1 KiB windows well enough that the window kernel's per-frame dynamic assignment
 // wins (4 KiB frames: 4.3 vs 3.8 TB/s on 16 lanes per frame).
-constexpr int kQ4Chunks = 12;
-constexpr int kLaneChunks = 24;            // CRC spans up to 1536 B go to the lane kernels
+#ifndef RH_Q4_CHUNKS  // A/B builds override (scripts/ab_build.sh)
+#define RH_Q4_CHUNKS 12
+#define RH_LANE_CHUNKS 24
+#endif
+constexpr int kQ4Chunks = RH_Q4_CHUNKS;
+constexpr int kLaneChunks = RH_LANE_CHUNKS;  // CRC spans up to 1536 B go to the lane kernels
 constexpr int kClasses = kLaneChunks + 1;  // class 0: window kernel; class c: c chunks of 64 B
 constexpr uint64_t kLaneMeanMax = 2048;    // mean frame length (buf_len / n) up to which the split runs
 
@@ -601,10 +605,13 @@ __global__ __launch_bounds__(kSortThreads) void crc_scatter_kernel(FrameArgs a, 
         }
     }
     __syncthreads();
+    __shared__ uint32_t cnt[kClasses];
+    if (threadIdx.x < kClasses) cnt[threadIdx.x] = counts[threadIdx.x];  // one load per class, in parallel
+    __syncthreads();
     if (threadIdx.x < kClasses) {
         const int c = threadIdx.x;
         uint32_t b = 0;  // class c's first record: classes 1..c-1 before it (class 0: its own list)
-        for (int j = 1; j < c; ++j) b += counts[j];
+        for (int j = 1; j < c; ++j) b += cnt[j];
         base[c] = b + (h[c] ? atomicAdd(&cursor[c], h[c]) : 0u);
     }
     __syncthreads();

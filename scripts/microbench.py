@@ -66,7 +66,7 @@ def main():
 
     if "crcshape" in only:
         # CRC cost per frame vs frame length (dense frame tables): uniform sizes, then ragged
-        for fsz in (256, 516, 1028, 2052, 4096):
+        for fsz in (256, 516, 772, 1028, 1284, 1540, 2052, 4096):
             ss = workload.synth_segments(ctx, n_segments=a.segments, frame_size=fsz, corrupt_rate=0)
             fb = ss.batch
             xs = [timed(lambda i=0: engine.crc32c_frames(ctx, fb, flags=_lib.RH_CRC_VERIFY), ss.frame_bytes, a.iters)
