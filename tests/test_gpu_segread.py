@@ -218,3 +218,26 @@ def test_fused_ragged_segments_with_corruption(ctx, orc):
     for sgi in range(n):
         mine = rs.corrupted[(rs.corrupted >= first[sgi]) & (rs.corrupted < first[sgi] + rs.seg_nframes[sgi])]
         assert int(ok[sgi]) == (int(mine[0] - first[sgi]) if mine.size else int(rs.seg_nframes[sgi])), sgi
+
+
+@pytest.mark.parametrize("lo,hi", [(20, 1500), (1200, 6000)])
+def test_fused_ragged_both_crc_plans_against_oracle(ctx, orc, lo, hi):
+    """Ragged segments through rh_segments_read_launch under both CRC plans -- the length-class
+    split with the dense outputs written by the CRC pass (mean slot length <= 2 KiB) and the
+    window kernel followed by the compaction pass (longer frames): the reader's verdict, the frame
+    table, every dense CRC and mismatch bit against the oracle, with planted corruptions."""
+    from ratis_amd import workload
+    rs = workload.synth_ragged_segments(ctx, 5, segment_size=2 << 20, min_frame=lo, max_frame=hi, seed=17 + lo,
+                                        corrupt_rate=3e-3)
+    n, size = rs.n_segments, rs.segment_size
+    cap = int(rs.seg_nframes.max()) + 16
+    split = (n * size) / (n * cap) <= 2048
+    assert split == (hi <= 1500)
+    buf = rs.batch.buf.cpu().numpy()
+    offs = np.arange(n, dtype=np.int64) * size
+    lens = np.full(n, size, dtype=np.int64)
+    b, out = run_fused(ctx, buf, offs, lens, cap=cap)
+    total = check_fused(ctx, orc, b, out, buf, offs, lens, cap=cap)
+    assert total == int(rs.seg_nframes.sum())
+    bad = np.nonzero(_bits(out["bad_bits"].cpu().numpy(), total))[0]
+    assert np.array_equal(bad, rs.corrupted) and rs.corrupted.size > 0
