@@ -52,6 +52,8 @@ def parse():
     p.add_argument("--ragged-segments", type=int, default=256,
                    help="32 MiB segments of 64-2048 B frames per GPU for the ragged read path (0 = skip)")
     p.add_argument("--no-lease", action="store_true")
+    p.add_argument("--lease-layout", choices=["tiled", "plain"], default="tiled",
+                   help="rh_lease_soa layout of the lease leg (tile_stride), as --layout for commit")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-pcie", action="store_true")
     p.add_argument("--pmc-json", default=None, help="default: the newest profiles/r*/pmc_traffic.json")
@@ -641,6 +643,9 @@ def main():
         for r in range(args.rotate):
             tiers = []
             for ts, conf, lin in lease_inputs:
+                if args.lease_layout == "tiled":
+                    tiers.append(engine.TiledLeaseTier.from_arrays(ts + r * SHIFT, conf, lin + r * SHIFT, device=dev))
+                    continue
                 t = engine.LeaseTier(follower_ts=torch.from_numpy(ts + r * SHIFT).to(dev),
                                      conf=torch.from_numpy(conf.view(np.int32)).to(dev),
                                      lease_in=torch.from_numpy(lin + r * SHIFT).to(dev))
@@ -673,7 +678,7 @@ def main():
         lease = {"checks_per_s": round(total_groups / (lease_ms * 1e-3), 1), "unit": "hasLease checks/s (whole job)",
                  "ms_per_pass": round(lease_ms, 5), "parity_ok": lease_ok, "timeout_ms": TIMEOUT_MS,
                  "roofline": {"bound": "hbm", "achieved": round(lease_ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                              "frac": round(lease_ach / HBM_PEAK_GBPS, 4), "kernel": "lease_kernel<0,7,true,8> (F=4, 6 tiers fused)",
+                              "frac": round(lease_ach / HBM_PEAK_GBPS, 4), "kernel": f"lease_kernel<0,7,true,8> (F=4 and F=6 tiers in one launch, {args.lease_layout} layout)",
                               "traffic": (round(pmc["lease_bytes_per_unit"] * n_mine) if "lease_bytes_per_unit" in pmc
                                           else None),
                               "traffic_source": pmc.get("_path"),

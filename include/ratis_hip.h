@@ -414,6 +414,13 @@ typedef struct rh_lease_soa {
     int64_t* lease_out;            /* [n] lease after extension; may alias lease_in               */
     uint64_t* has_lease_bits;      /* [ceil(n/64)] hasLease()                                     */
     uint64_t* extended_bits;       /* optional [ceil(n/64)]: the lease was set by extend()        */
+    uint64_t tile_stride;          /* 0: plain columns.  Else the TILED layout of rh_commit_soa:
+                                      every per-group column (follower_ts, conf, lease_in,
+                                      lease_out) holds its RH_TILE_GROUPS elements of a tile
+                                      contiguously at its pointer + tile * tile_stride bytes,
+                                      follower column k col_stride elements after column 0 within
+                                      the tile (col_stride >= 128); a multiple of 16.  Bit columns
+                                      stay plain. */
 } rh_lease_soa;
 
 int rh_lease_soa_launch(rh_ctx* ctx, const rh_lease_soa* tiers, int n_tiers, void* stream);

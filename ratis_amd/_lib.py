@@ -145,6 +145,7 @@ class RhLeaseSoa(ctypes.Structure):
         ("lease_out", c_void_p),
         ("has_lease_bits", c_void_p),
         ("extended_bits", c_void_p),
+        ("tile_stride", c_uint64),
     ]
 
 

@@ -63,7 +63,13 @@ int rh_lease_validate(const rh_lease_soa* tiers, int n_tiers) {
         if (t.n == 0) continue;
         if (!t.conf || !t.lease_in || !t.lease_out || !t.has_lease_bits || (t.n_followers && !t.follower_ts))
             return rh::fail(RH_E_INVAL, "rh_lease_soa_launch: conf/lease_in/lease_out/has_lease_bits required");
-        if (t.n_followers && t.col_stride < t.n) return rh::fail(RH_E_INVAL, "rh_lease_soa_launch: col_stride < n");
+        if (t.tile_stride) {
+            if (t.tile_stride % 16) return rh::fail(RH_E_INVAL, "rh_lease_soa_launch: tile_stride not a multiple of 16");
+            if (t.n_followers && t.col_stride < RH_TILE_GROUPS)
+                return rh::fail(RH_E_INVAL, "rh_lease_soa_launch: tiled col_stride < 128");
+        } else if (t.n_followers && t.col_stride < t.n) {
+            return rh::fail(RH_E_INVAL, "rh_lease_soa_launch: col_stride < n");
+        }
         if (t.timeout_ms < 0) return rh::fail(RH_E_INVAL, "rh_lease_soa_launch: timeout_ms < 0");
         if (t.n > (uint64_t)UINT32_MAX * kLeaseBlock) return rh::fail(RH_E_RANGE, "rh_lease_soa_launch: n too large");
     }

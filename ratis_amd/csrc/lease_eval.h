@@ -108,18 +108,22 @@ __device__ __forceinline__ void lease_wave(const rh_lease_soa& t, uint64_t wbase
     const int lane = threadIdx.x & 63;
     const uint64_t r0 = wbase + 2 * (uint64_t)lane;
     const bool in0 = r0 < t.n, in1 = r0 + 1 < t.n;
+    // element index of group r0 in an int64 / uint32 column: plain (r0) or tiled (tile * elements
+    // per tile + r0 % 128); r0 is even, so r0 + 1 is the next element in both layouts
+    const uint64_t e = t.tile_stride ? (r0 >> 7) * (t.tile_stride >> 3) + (r0 & 127u) : r0;
+    const uint64_t e32 = t.tile_stride ? (r0 >> 7) * (t.tile_stride >> 2) + (r0 & 127u) : r0;
     int64_t ts0[F > 0 ? F : 1], ts1[F > 0 ? F : 1];
     uint32_t w0 = 0, w1 = 0;
     int64_t l0 = 0, l1 = 0;
     if (VEC && in1) {
 #pragma unroll
         for (int k = 0; k < F; ++k) {
-            const v2i64 x = lease_ld<NT>(reinterpret_cast<const v2i64*>(t.follower_ts + (uint64_t)k * t.col_stride + r0));
+            const v2i64 x = lease_ld<NT>(reinterpret_cast<const v2i64*>(t.follower_ts + (uint64_t)k * t.col_stride + e));
             ts0[k] = x.x;
             ts1[k] = x.y;
         }
-        const v2u32 c = lease_ld<NT>(reinterpret_cast<const v2u32*>(t.conf + r0));
-        const v2i64 li = lease_ld<NT>(reinterpret_cast<const v2i64*>(t.lease_in + r0));
+        const v2u32 c = lease_ld<NT>(reinterpret_cast<const v2u32*>(t.conf + e32));
+        const v2i64 li = lease_ld<NT>(reinterpret_cast<const v2i64*>(t.lease_in + e));
         w0 = c.x;
         w1 = c.y;
         l0 = li.x;
@@ -127,13 +131,13 @@ __device__ __forceinline__ void lease_wave(const rh_lease_soa& t, uint64_t wbase
     } else {
 #pragma unroll
         for (int k = 0; k < F; ++k) {
-            ts0[k] = in0 ? t.follower_ts[(uint64_t)k * t.col_stride + r0] : t.now_nanos;
-            ts1[k] = in1 ? t.follower_ts[(uint64_t)k * t.col_stride + r0 + 1] : t.now_nanos;
+            ts0[k] = in0 ? t.follower_ts[(uint64_t)k * t.col_stride + e] : t.now_nanos;
+            ts1[k] = in1 ? t.follower_ts[(uint64_t)k * t.col_stride + e + 1] : t.now_nanos;
         }
-        w0 = in0 ? t.conf[r0] : 0u;
-        w1 = in1 ? t.conf[r0 + 1] : 0u;
-        l0 = in0 ? t.lease_in[r0] : 0;
-        l1 = in1 ? t.lease_in[r0 + 1] : 0;
+        w0 = in0 ? t.conf[e32] : 0u;
+        w1 = in1 ? t.conf[e32 + 1] : 0u;
+        l0 = in0 ? t.lease_in[e] : 0;
+        l1 = in1 ? t.lease_in[e + 1] : 0;
     }
     // r0 is even, so both groups' bits live in the same enabled word
     const uint64_t ew = (t.enabled_bits && in0) ? t.enabled_bits[r0 >> 6] : ~0ull;
@@ -144,10 +148,10 @@ __device__ __forceinline__ void lease_wave(const rh_lease_soa& t, uint64_t wbase
     lease_one<F>(t, ts0, w0, l0, e0, in0, o0, h0, x0);
     lease_one<F>(t, ts1, w1, l1, e1, in1, o1, h1, x1);
     if (VEC && in1) {
-        *reinterpret_cast<v2i64*>(t.lease_out + r0) = v2i64{o0, o1};
+        *reinterpret_cast<v2i64*>(t.lease_out + e) = v2i64{o0, o1};
     } else {
-        if (in0) t.lease_out[r0] = o0;
-        if (in1) t.lease_out[r0 + 1] = o1;
+        if (in0) t.lease_out[e] = o0;
+        if (in1) t.lease_out[e + 1] = o1;
     }
     const uint64_t he = __ballot(h0), ho = __ballot(h1);
     const uint64_t xe = __ballot(x0), xo = __ballot(x1);
@@ -205,7 +209,7 @@ inline int build_lease_args(const rh_lease_soa* tiers, int n_tiers, int flo, int
     for (int oi = 0; oi < n_tiers; ++oi) {
         const rh_lease_soa& t = tiers[order[oi]];
         if (t.n == 0 || (int)t.n_followers < flo || (int)t.n_followers > fhi) continue;
-        const bool vec = (t.n_followers == 0 || t.col_stride % 2 == 0) &&
+        const bool vec = (t.n_followers == 0 || t.col_stride % 2 == 0) && t.tile_stride % 16 == 0 &&
                          (t.n_followers == 0 || ((uintptr_t)t.follower_ts & 15) == 0) &&
                          ((uintptr_t)t.conf & 7) == 0 && ((uintptr_t)t.lease_in & 15) == 0 &&
                          ((uintptr_t)t.lease_out & 15) == 0;

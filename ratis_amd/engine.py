@@ -572,6 +572,81 @@ class LeaseTier:
         return t
 
 
+@dataclass
+class TiledLeaseTier:
+    """A lease tier in the TILED layout of ``rh_lease_soa.tile_stride``: one int64 HBM buffer of
+    ceil(n / 128) tiles, each holding for its 128 groups the F follower timestamp columns,
+    lease_in and lease_out (128 int64 each), then the 128 uint32 membership words -- one
+    contiguous run per tile for a wave's loads.  Bit columns stay plain."""
+
+    n: int
+    n_followers: int
+    buf: torch.Tensor                # int64 [n_tiles, tile_elems]
+    enabled_bits: Optional[torch.Tensor] = None
+    has_lease_bits: Optional[torch.Tensor] = None
+    extended_bits: Optional[torch.Tensor] = None
+
+    @staticmethod
+    def columns(F: int) -> List[str]:
+        return [f"ts{k}" for k in range(F)] + ["lease_in", "lease_out"]
+
+    @classmethod
+    def from_arrays(cls, follower_ts, conf, lease_in, device="cuda", extended: bool = True) -> "TiledLeaseTier":
+        import numpy as np
+        F = int(follower_ts.shape[0]) if follower_ts.ndim == 2 else 0
+        n = int(conf.size)
+        nt = (n + 127) // 128
+        cols = cls.columns(F)
+        te = len(cols) * 128 + 64
+        host = np.zeros((nt, te), dtype=np.int64)
+
+        def put(name, a):
+            c = cols.index(name)
+            pad = np.zeros(nt * 128, dtype=np.int64)
+            pad[:n] = a
+            host[:, c * 128:(c + 1) * 128] = pad.reshape(nt, 128)
+        for k in range(F):
+            put(f"ts{k}", follower_ts[k])
+        put("lease_in", lease_in)
+        cw = np.zeros(nt * 128, dtype=np.uint32)
+        cw[:n] = np.asarray(conf).view(np.uint32)
+        host[:, len(cols) * 128:] = cw.reshape(nt, 128).view(np.int64)
+        nw = max((n + 63) // 64, 1)
+        t = cls(n=n, n_followers=F, buf=torch.from_numpy(host).to(device),
+                has_lease_bits=torch.zeros(nw, dtype=torch.int64, device=device))
+        if extended:
+            t.extended_bits = torch.zeros(nw, dtype=torch.int64, device=device)
+        return t
+
+    def column(self, name: str) -> torch.Tensor:
+        """Column ``name`` over the n groups (a gathered copy)."""
+        c = self.columns(self.n_followers).index(name)
+        return self.buf[:, c * 128:(c + 1) * 128].reshape(-1)[:self.n]
+
+    @property
+    def lease_out(self) -> torch.Tensor:
+        return self.column("lease_out")
+
+    def to_struct(self, now_nanos: int, timeout_ms: int) -> RhLeaseSoa:
+        cols = self.columns(self.n_followers)
+        base = self.buf.data_ptr()
+        t = RhLeaseSoa()
+        t.n = self.n
+        t.n_followers = self.n_followers
+        t.now_nanos = now_nanos
+        t.timeout_ms = timeout_ms
+        t.follower_ts = base if self.n_followers else None
+        t.col_stride = 128
+        t.conf = base + len(cols) * 128 * 8
+        t.lease_in = base + cols.index("lease_in") * 128 * 8
+        t.enabled_bits = _ptr(self.enabled_bits)
+        t.lease_out = base + cols.index("lease_out") * 128 * 8
+        t.has_lease_bits = _ptr(self.has_lease_bits)
+        t.extended_bits = _ptr(self.extended_bits)
+        t.tile_stride = int(self.buf.shape[1]) * 8
+        return t
+
+
 def lease_launch(ctx: Context, tiers: Sequence[LeaseTier], now_nanos: int, timeout_ms: int,
                  stream: Optional[torch.cuda.Stream] = None) -> None:
     """Enqueues the lease kernel for every tier (asynchronous)."""

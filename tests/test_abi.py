@@ -98,7 +98,7 @@ int main(void) {
   F(rh_lease_soa, n) F(rh_lease_soa, n_followers) F(rh_lease_soa, reserved) F(rh_lease_soa, now_nanos)
   F(rh_lease_soa, timeout_ms) F(rh_lease_soa, follower_ts) F(rh_lease_soa, col_stride) F(rh_lease_soa, conf)
   F(rh_lease_soa, lease_in) F(rh_lease_soa, enabled_bits) F(rh_lease_soa, lease_out)
-  F(rh_lease_soa, has_lease_bits) F(rh_lease_soa, extended_bits)
+  F(rh_lease_soa, has_lease_bits) F(rh_lease_soa, extended_bits) F(rh_lease_soa, tile_stride)
   printf("conf %u\n", rh_conf_pack(0x5, 1, 1, 0x3, 1, 1));
   return 0;
 }

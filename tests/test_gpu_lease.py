@@ -186,3 +186,51 @@ def test_leader_fused_launch_equals_separate(ctx, orc):
         got = (t.lease_out.cpu().numpy(), t.has_lease_bits[:nw].cpu().numpy().view(np.uint64),
                t.extended_bits[:nw].cpu().numpy().view(np.uint64))
         assert_same(orc.lease_soa(ts, conf, lin, NOW, 100), got)
+
+
+@pytest.mark.parametrize("F", [0, 1, 3, 4, 6, 7, 8, 11, 14])
+def test_lease_tiled_layout(ctx, orc, F):
+    """The TILED layout (rh_lease_soa.tile_stride: 128-group tiles holding every per-group column)
+    gives the oracle's results for every follower-count class, incl. a partial last tile and an
+    enabled-bit column."""
+    import torch
+
+    from ratis_amd import engine
+    rng = np.random.default_rng(3000 + F)
+    n = 9_000 + 77 * F            # partial last tile, not a multiple of 64
+    ts, conf, lease_in = random_lease_tier(rng, n, F)
+    en = rng.integers(0, 1 << 63, (n + 63) // 64, dtype=np.int64).astype(np.uint64) | np.uint64(0x0FF00FF00FF00FF0)
+    t = engine.TiledLeaseTier.from_arrays(ts, conf, lease_in)
+    t.enabled_bits = torch.from_numpy(en.view(np.int64)).cuda()
+    engine.lease_launch(ctx, [t], NOW, 100)
+    torch.cuda.synchronize()
+    nw = (n + 63) // 64
+    ref = orc.lease_soa(ts, conf, lease_in, NOW, 100, en)
+    assert_same(ref, (t.lease_out.cpu().numpy(), t.has_lease_bits[:nw].cpu().numpy().view(np.uint64),
+                      t.extended_bits[:nw].cpu().numpy().view(np.uint64)))
+
+
+def test_leader_launch_tiled_commit_and_lease(ctx, orc):
+    """rh_leader_soa_launch over tiled commit tiers and tiled lease tiers of the same groups (the
+    bench's fused configuration) equals the oracle on both halves."""
+    import torch
+
+    from ratis_amd import engine, workload
+    host = workload.commit_snapshot(40_000, joint_frac=0.10, peers=5, seed=77)
+    rng = np.random.default_rng(78)
+    ctiers, ltiers, refs = [], [], []
+    for h in host:
+        ct = engine.TiledCommitTier.from_arrays(h.follower, h.flush, h.conf, h.commit, h.term_start)
+        ts = NOW - rng.integers(-MS, 300 * MS, size=h.follower.shape, dtype=np.int64)
+        lin = NOW - rng.integers(0, 200 * MS, size=h.n, dtype=np.int64)
+        ctiers.append(ct)
+        ltiers.append(engine.TiledLeaseTier.from_arrays(ts, h.conf, lin))
+        refs.append((orc.commit_soa(h.follower, h.flush, h.conf, mode=0, commit_in=h.commit, term_start=h.term_start),
+                     orc.lease_soa(ts, h.conf, lin, NOW, 100)))
+    engine.leader_launch(ctx, ctiers, ltiers, NOW, 100)
+    torch.cuda.synchronize()
+    for ct, lt, (rc, rl), h in zip(ctiers, ltiers, refs, host):
+        assert np.array_equal(ct.column("commit_out").cpu().numpy(), rc["commit"])
+        nw = (h.n + 63) // 64
+        assert np.array_equal(lt.lease_out.cpu().numpy(), rl["lease"])
+        assert np.array_equal(lt.has_lease_bits[:nw].cpu().numpy().view(np.uint64), rl["has_lease_bits"])
