@@ -560,9 +560,13 @@ __global__ __launch_bounds__(256) void segment_compact_kernel(const uint64_t* sc
 #define RH_PIECE_LIST 1024
 #endif
 constexpr uint32_t kPiece = RH_PIECE_BYTES;  // bytes per piece
-constexpr uint32_t kGuessWin = 16384;    // bytes of a piece the guess pass looks at
+#ifndef RH_GUESS_WIN  // A/B builds override (scripts/ab_build.sh)
+#define RH_GUESS_WIN 16384
+#define RH_PIECE_THREADS 256
+#endif
+constexpr uint32_t kGuessWin = RH_GUESS_WIN;  // bytes of a piece the guess pass looks at
 constexpr uint32_t kGuessLds = kGuessWin + 64;
-constexpr int kPieceThreads = 512;
+constexpr int kPieceThreads = RH_PIECE_THREADS;
 constexpr uint32_t kList = RH_PIECE_LIST;  // frame lengths (u16) a guessed walk records
 constexpr uint32_t kListPerLane = kList / 64;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
@@ -684,7 +688,7 @@ __global__ __launch_bounds__(kPieceThreads) void piece_guess_kernel(PieceArgs a)
     const int t = threadIdx.x;
     const unsigned int total = *a.n_pieces;
     struct Item {
-        uint32_t s, Bi, We, L, o0, ilen;
+        uint32_t s, Bi, We, L, o0, ilen, gmax;
         uint64_t base;
     };
     // the next work item at or after w (stride gridDim.x) that needs a guess; a segment's first
@@ -711,7 +715,12 @@ __global__ __launch_bounds__(kPieceThreads) void piece_guess_kernel(PieceArgs a)
         it.L = (uint32_t)a.seg_len[it.s];
         uint32_t Bn;
         piece_bounds((uint32_t)a.seg_stop[it.s], it.L, w - a.piece_first[it.s], it.Bi, Bn);
-        it.We = Bn - it.Bi > kGuessWin ? it.Bi + kGuessWin : Bn;  // guess window end
+        // frames longer than gmax (2x the largest the serial walk saw) kill a candidate; the window
+        // is 4 gmax (4..16 KiB) so that a false start cannot leave it in a step or two
+        const uint32_t gm0 = a.seg_gmax[it.s] * 2u;
+        it.gmax = gm0 < 1024u ? 1024u : gm0 > kGuessWin ? kGuessWin : gm0;
+        const uint32_t win = 4u * it.gmax < 4096u ? 4096u : 4u * it.gmax > kGuessWin ? kGuessWin : 4u * it.gmax;
+        it.We = Bn - it.Bi > win ? it.Bi + win : Bn;  // guess window end
         it.o0 = (uint32_t)((it.base + it.Bi) & 15u);
         const uint32_t rend = it.L - it.We > 32u ? it.We + 32u : it.L;
         it.ilen = rend - it.Bi + it.o0;
@@ -765,8 +774,7 @@ __global__ __launch_bounds__(kPieceThreads) void piece_guess_kernel(PieceArgs a)
         __syncthreads();
         const uint32_t Bi = cur.Bi, We = cur.We, L = cur.L, o0 = cur.o0;
         const uint32_t zpos = sh_zero >= o0 ? Bi + sh_zero - o0 : Bi;  // segment position
-        const uint32_t gm0 = a.seg_gmax[cur.s] * 2u;
-        const uint32_t gmax = gm0 < 1024u ? 1024u : gm0 > kGuessWin ? kGuessWin : gm0;
+        const uint32_t gmax = cur.gmax;
         const uint32_t ncand = We - Bi < 4u * gmax ? We - Bi : 4u * gmax;
         // rounds of kPieceThreads candidate starts until one survives.  The walk is a lockstep
         // loop of predicated steps (one uniform branch per step): a candidate's chain
