@@ -66,9 +66,8 @@ def main():
             for h in host:
                 ts = now - rng.integers(0, 300_000_000, size=h.follower.shape, dtype=np.int64)
                 lin = now - rng.integers(0, 200_000_000, size=h.n, dtype=np.int64)
-                tiers.append(engine.LeaseTier(follower_ts=torch.from_numpy(ts).cuda(),
-                                              conf=torch.from_numpy(h.conf.view(np.int32)).cuda(),
-                                              lease_in=torch.from_numpy(lin).cuda()).alloc_outputs())
+                # the bench's default layout: tiled (rh_lease_soa.tile_stride)
+                tiers.append(engine.TiledLeaseTier.from_arrays(ts, h.conf, lin))
             batches.append(tiers)
         torch.cuda.synchronize()
         for i in range(a.iters):
