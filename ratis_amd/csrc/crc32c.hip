@@ -539,16 +539,34 @@ struct LaneRec {  // one frame of the lane path, records ascending by chunk coun
     uint32_t f;   // frame number (output index)
 };
 
-// class of frame f (-1: an empty slot of the slotted read-path table, no output at all)
-__device__ __forceinline__ int crc_class(const FrameArgs& a, uint64_t f, int64_t& o_out, uint32_t& lc_out) {
-    if (a.slot_nframes) {  // 32-bit division: the launcher keeps n below 2^32
-        const uint32_t seg = (uint32_t)f / a.slot_cap, slot = (uint32_t)f - seg * a.slot_cap;
-        const uint32_t nfs = a.slot_nframes[seg];
-        if (slot >= (nfs < a.slot_cap ? nfs : a.slot_cap)) return -1;
+// A frame's table entry, loaded unconditionally (every load of a thread's frames in flight before
+// any is used: a dependent, conditional load chain per slot left the prepass waiting on memory).
+struct FrameIn {
+    uint64_t o;
+    uint32_t len;
+    uint32_t nfs;  // slot mode: frames of the slot's segment
+};
+__device__ __forceinline__ FrameIn load_frame(const FrameArgs& a, uint64_t f) {
+    FrameIn x{0, 0, 0};
+    if (f < a.n) {
+        x.o = a.off[f];
+        x.len = a.len[f];
+        if (a.slot_nframes) x.nfs = a.slot_nframes[(uint32_t)f / a.slot_cap];  // 32-bit: n < 2^32
+    }
+    return x;
+}
+
+// class of frame f (-1: none, or an empty slot of the slotted read-path table: no output at all)
+__device__ __forceinline__ int crc_class(const FrameArgs& a, uint64_t f, const FrameIn& x, int64_t& o_out,
+                                         uint32_t& lc_out) {
+    if (f >= a.n) return -1;
+    if (a.slot_nframes) {
+        const uint32_t slot = (uint32_t)f % a.slot_cap;
+        if (slot >= (x.nfs < a.slot_cap ? x.nfs : a.slot_cap)) return -1;
     }
     const uint32_t tl = (a.flags & (RH_CRC_VERIFY | RH_CRC_STAMP)) ? 4u : 0u;
-    const uint64_t o = a.off[f];
-    const int64_t L = (int64_t)a.len[f];
+    const uint64_t o = x.o;
+    const int64_t L = (int64_t)x.len;
     // the window kernel's fast-path rules (malformed / guarded frames are its business)
     if (o > (uint64_t)a.buf_len || L > a.buf_len - (int64_t)o || L < (int64_t)tl) return 0;
     const int64_t lc = L - (int64_t)tl, E = (int64_t)o + lc;
@@ -558,21 +576,27 @@ __device__ __forceinline__ int crc_class(const FrameArgs& a, uint64_t f, int64_t
     return (int)((lc + 63) >> 6);
 }
 
-// counts[c] = frames of class c
+// counts[c] = frames of class c; each thread takes kSortPer frames per round, loads first
 __global__ __launch_bounds__(kSortThreads) void crc_classify_kernel(FrameArgs a, uint32_t* counts) {
     __shared__ uint32_t h[kClasses];
     for (int i = threadIdx.x; i < kClasses; i += blockDim.x) h[i] = 0;
     __syncthreads();
-    for (uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; f < a.n; f += (uint64_t)gridDim.x * blockDim.x) {
-        int64_t o;
-        uint32_t lc;
-        const int c = crc_class(a, f, o, lc);
-        const int c0 = __shfl(c, 0);
-        const uint32_t nact = (uint32_t)__popcll(__ballot(1));  // active lanes (a prefix of the wave)
-        if (__all(c == c0)) {  // a wave of one class (uniform logs): one atomic
-            if ((threadIdx.x & 63) == 0 && c0 >= 0) atomicAdd(&h[c0], nact);
-        } else if (c >= 0) {
-            atomicAdd(&h[c], 1u);
+    const uint64_t step = (uint64_t)gridDim.x * kSortTile;
+    for (uint64_t t0 = (uint64_t)blockIdx.x * kSortTile; t0 < a.n; t0 += step) {
+        FrameIn x[kSortPer];
+#pragma unroll
+        for (int k = 0; k < kSortPer; ++k) x[k] = load_frame(a, t0 + (uint64_t)k * kSortThreads + threadIdx.x);
+#pragma unroll
+        for (int k = 0; k < kSortPer; ++k) {
+            int64_t o;
+            uint32_t lc;
+            const int c = crc_class(a, t0 + (uint64_t)k * kSortThreads + threadIdx.x, x[k], o, lc);
+            const int c0 = __shfl(c, 0);
+            if (__all(c == c0)) {  // a wave of one class (uniform logs): one atomic
+                if ((threadIdx.x & 63) == 0 && c0 >= 0) atomicAdd(&h[c0], 64u);
+            } else if (c >= 0) {
+                atomicAdd(&h[c], 1u);
+            }
         }
     }
     __syncthreads();
@@ -591,10 +615,13 @@ __global__ __launch_bounds__(kSortThreads) void crc_scatter_kernel(FrameArgs a, 
     int cls[kSortPer];
     uint32_t rank[kSortPer], lcs[kSortPer];
     int64_t os[kSortPer];
+    FrameIn x[kSortPer];
+#pragma unroll
+    for (int k = 0; k < kSortPer; ++k) x[k] = load_frame(a, t0 + (uint64_t)k * kSortThreads + threadIdx.x);
 #pragma unroll
     for (int k = 0; k < kSortPer; ++k) {
         const uint64_t f = t0 + (uint64_t)k * kSortThreads + threadIdx.x;
-        cls[k] = f < a.n ? crc_class(a, f, os[k], lcs[k]) : -1;
+        cls[k] = crc_class(a, f, x[k], os[k], lcs[k]);
         const int c0 = __shfl(cls[k], 0);
         if (__all(cls[k] == c0)) {  // a wave of one class: one atomic, ranks by lane
             uint32_t b = 0;
@@ -895,7 +922,8 @@ int launch_frames(rh_ctx* ctx, FrameArgs a, hipStream_t stream, bool* dense_writ
     LaneRec* rec = reinterpret_cast<LaneRec*>(sb + o_rec);
     uint32_t* widx = reinterpret_cast<uint32_t*>(sb + o_widx);
     RH_HIP(hipMemsetAsync(counts, 0, 2 * kClasses * sizeof(uint32_t), stream));
-    const uint64_t cgrid = (a.n + kSortThreads - 1) / kSortThreads < cus * 8 ? (a.n + kSortThreads - 1) / kSortThreads : cus * 8;
+    const uint64_t ntile = (a.n + kSortTile - 1) / kSortTile;
+    const uint64_t cgrid = ntile < cus * 8 ? ntile : cus * 8;
     hipLaunchKernelGGL(crc_classify_kernel, dim3((uint32_t)cgrid), dim3(kSortThreads), 0, stream, a, counts);
     RH_HIP(hipGetLastError());
     hipLaunchKernelGGL(crc_scatter_kernel, dim3((uint32_t)((a.n + kSortTile - 1) / kSortTile)), dim3(kSortThreads), 0,
