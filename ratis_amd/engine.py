@@ -271,6 +271,28 @@ def commit_launch(ctx: Context, tiers: Sequence, mode: int = RH_MODE_COMMIT,
     check(_lib.load().rh_commit_soa_launch(ctx.handle, arr, len(tiers), _stream_ptr(stream)))
 
 
+class PreparedLaunch:
+    """A launch whose rh_*_soa argument arrays are built once (the tier buffers do not move between
+    launches, as a long-lived host would hold them): calling it is one C-ABI call.  Rebuilding the
+    ctypes structs per launch costs ~10-20 us of Python -- as long as a 1M-group lease or commit
+    kernel, enough to leave the GPU waiting for the host."""
+
+    def __init__(self, fn_name: str, *arrays_and_counts):
+        self._fn = getattr(_lib.load(), fn_name)
+        self._args = arrays_and_counts      # keeps the ctypes arrays alive
+
+    def __call__(self, ctx: "Context", stream: Optional[torch.cuda.Stream] = None) -> None:
+        check(self._fn(ctx.handle, *self._args, _stream_ptr(stream)))
+
+
+def prepare_commit(tiers: Sequence, mode: int = RH_MODE_COMMIT) -> PreparedLaunch:
+    """commit_launch with the argument array built once."""
+    if not 1 <= len(tiers) <= _lib.RH_MAX_TIERS:
+        raise ValueError("1..4 tiers per launch")
+    return PreparedLaunch("rh_commit_soa_launch", (RhCommitSoa * len(tiers))(*[t.to_struct(mode) for t in tiers]),
+                          len(tiers))
+
+
 def unpack_bits(words: torch.Tensor, n: int) -> torch.Tensor:
     """Bit g of word g//64 -> bool tensor [n] (on the words' device)."""
     w = words.view(torch.int64)
@@ -652,6 +674,21 @@ def lease_launch(ctx: Context, tiers: Sequence[LeaseTier], now_nanos: int, timeo
     """Enqueues the lease kernel for every tier (asynchronous)."""
     arr = (RhLeaseSoa * len(tiers))(*[t.to_struct(now_nanos, timeout_ms) for t in tiers])
     check(_lib.load().rh_lease_soa_launch(ctx.handle, arr, len(tiers), _stream_ptr(stream)))
+
+
+def prepare_lease(tiers: Sequence, now_nanos: int, timeout_ms: int) -> PreparedLaunch:
+    """lease_launch with the argument array built once."""
+    return PreparedLaunch("rh_lease_soa_launch",
+                          (RhLeaseSoa * len(tiers))(*[t.to_struct(now_nanos, timeout_ms) for t in tiers]), len(tiers))
+
+
+def prepare_leader(commit_tiers: Sequence, lease_tiers: Sequence, now_nanos: int, timeout_ms: int) -> PreparedLaunch:
+    """leader_launch with the argument arrays built once."""
+    if not 1 <= len(commit_tiers) <= _lib.RH_MAX_TIERS or not 1 <= len(lease_tiers) <= _lib.RH_MAX_TIERS:
+        raise ValueError("1..4 tiers of each kind per launch")
+    c = (RhCommitSoa * len(commit_tiers))(*[t.to_struct(RH_MODE_COMMIT) for t in commit_tiers])
+    ls = (RhLeaseSoa * len(lease_tiers))(*[t.to_struct(now_nanos, timeout_ms) for t in lease_tiers])
+    return PreparedLaunch("rh_leader_soa_launch", c, len(commit_tiers), ls, len(lease_tiers))
 
 
 def leader_launch(ctx: Context, commit_tiers: Sequence[CommitTier], lease_tiers: Sequence[LeaseTier], now_nanos: int,
