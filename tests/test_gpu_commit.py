@@ -338,3 +338,30 @@ def test_tiled_layout_rejects_bad_strides(ctx):
         arr = (_lib.RhCommitSoa * 1)(t.to_struct(0))
         setattr(arr[0], field, bad)
         assert _lib.load().rh_commit_soa_launch(ctx.handle, arr, 1, None) == _lib.RH_E_INVAL
+
+
+def test_prepared_launches_match_per_call_launches(ctx, orc):
+    """engine.prepare_commit / prepare_lease / prepare_leader (argument arrays built once, as the
+    bench's timed loops use them) give the oracle's results, launched repeatedly."""
+    import torch
+
+    from ratis_amd import engine, workload
+    host = workload.commit_snapshot(30_000, joint_frac=0.10, peers=5, seed=91)
+    ct = [engine.TiledCommitTier.from_arrays(h.follower, h.flush, h.conf, h.commit, h.term_start) for h in host]
+    now, rng = 1 << 60, np.random.default_rng(92)
+    lin = [now - rng.integers(0, 200_000_000, size=h.n, dtype=np.int64) for h in host]
+    ts = [now - rng.integers(-1_000_000, 300_000_000, size=h.follower.shape, dtype=np.int64) for h in host]
+    lt = [engine.TiledLeaseTier.from_arrays(t, h.conf, li) for t, h, li in zip(ts, host, lin)]
+    launches = (engine.prepare_commit(ct), engine.prepare_lease(lt, now, 100), engine.prepare_leader(ct, lt, now, 100))
+    for k, p in enumerate(launches):
+        for _ in range(3):
+            p(ctx)
+        torch.cuda.synchronize()
+        for h, c, l, t, li in zip(host, ct, lt, ts, lin):
+            rc = orc.commit_soa(h.follower, h.flush, h.conf, mode=0, commit_in=h.commit, term_start=h.term_start)
+            assert np.array_equal(c.column("commit_out").cpu().numpy(), rc["commit"])
+            if k >= 1:   # the lease half has run
+                rl = orc.lease_soa(t, h.conf, li, now, 100)
+                assert np.array_equal(l.lease_out.cpu().numpy(), rl["lease"])
+                nw = (h.n + 63) // 64
+                assert np.array_equal(l.has_lease_bits[:nw].cpu().numpy().view(np.uint64), rl["has_lease_bits"])
