@@ -47,8 +47,12 @@ __device__ __forceinline__ bool locate(const TableDev& T, uint32_t slot, const T
 // ---- deltas --------------------------------------------------------------------------------------
 // phase 0 applies the batch's SET deltas (plain stores), phase 1 its MAX deltas (atomicMax): the
 // host orders batches so that this equals applying them one by one (ratis_hip.h, rh_delta).
-__global__ __launch_bounds__(256) void table_apply_kernel(TableDev T, const rh_delta* __restrict__ d, uint64_t n,
+__global__ __launch_bounds__(256) void table_apply_kernel(TableDev Targ, const rh_delta* __restrict__ d, uint64_t n,
                                                           int phase) {
+    // the tier is picked per thread: index the argument in the kernarg segment (scalar loads), not
+    // the by-value copy, which the compiler spilled whole into scratch (984 B per lane, 8x slower)
+    const TableDev& T = rh::kernarg_struct<TableDev>();
+    (void)Targ;
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const rh_delta x = d[i];
