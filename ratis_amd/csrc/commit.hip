@@ -23,6 +23,9 @@
 namespace {
 
 constexpr int kBlock = 256;            // 4 waves
+#ifndef RH_COMMIT_WAVES  // A/B builds override (scripts/ab_build.sh): waves per SIMD the F <= 6 kernels are pinned to
+#define RH_COMMIT_WAVES 8
+#endif
 constexpr int kGroupsPerLane = 2;      // 16-byte loads per column per lane
 
 struct TierArgs {
@@ -262,7 +265,7 @@ __device__ __forceinline__ int tier_of_block(const LaunchArgs& args, uint32_t b)
 // per SIMD: a 1M-group launch (7813 waves of 128 groups) is resident in one round on 256 CUs.
 // One launch covers every tier of the class; blocks are assigned to tiers in order and the F
 // switch is block-uniform, so it costs no divergence.
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void commit_kernel_rank(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RH_COMMIT_WAVES, 8))) void commit_kernel_rank(
     const LaunchArgs a) {
     const LaunchArgs& args = rh::kernarg_struct<LaunchArgs>();  // scalar loads, no scratch copy
     const int ti = tier_of_block(args, blockIdx.x);
@@ -343,7 +346,7 @@ struct LeaderArgs {
     uint32_t commit_blocks;
 };
 
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void leader_kernel(const LeaderArgs arg) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RH_COMMIT_WAVES, 8))) void leader_kernel(const LeaderArgs arg) {
     const LeaderArgs& a = rh::kernarg_struct<LeaderArgs>();
     const uint32_t b = blockIdx.x;
     if (b < a.commit_blocks) {
