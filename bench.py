@@ -52,6 +52,9 @@ def parse():
     p.add_argument("--ragged-segments", type=int, default=256,
                    help="32 MiB segments of 64-2048 B frames per GPU for the ragged read path (0 = skip)")
     p.add_argument("--no-lease", action="store_true")
+    p.add_argument("--graph", action="store_true",
+                   help="time the commit / lease / fused legs as one captured HIP graph of the K launches "
+                        "(measured equal or 1-2 %% slower than the prebuilt stream launches: profiles/r02/graph_timing/)")
     p.add_argument("--lease-layout", choices=["tiled", "plain"], default="tiled",
                    help="rh_lease_soa layout of the lease leg (tile_stride), as --layout for commit")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -156,6 +159,28 @@ class HostShift:
 def out_col(t, name):
     """An output column of a plain (CommitTier) or tiled (TiledCommitTier) commit tier."""
     return t.column(name) if hasattr(t, "column") else getattr(t, name)
+
+
+def captured(launches, steps: int, ctx, use_graph: bool):
+    """The K timed launches of a leg (launches[i % R] for i < K) as one callable: replayed from a
+    HIP graph captured once (the kernels run back to back without the host in between), or -- if
+    capture is off or fails -- issued one by one.  Returns (run, mode)."""
+    import torch
+    if use_graph:
+        try:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for i in range(steps):
+                    launches[i % len(launches)](ctx, None)   # on the capture stream
+            torch.cuda.synchronize()
+            return (lambda stream: g.replay()), "hipGraph"
+        except Exception as e:  # noqa: BLE001 -- report and time the plain launches instead
+            print(f"bench: graph capture failed ({e}); timing stream launches", file=sys.stderr)
+
+    def run(stream):
+        for i in range(steps):
+            launches[i % len(launches)](ctx, stream)
+    return run, "stream"
 
 
 def delta_streaming(ctx, host, steps: int = 12, fill_threads: int = 16, reps: int = 5) -> dict:
@@ -395,12 +420,13 @@ def main():
     for i in range(args.warmup):
         commit_launches[i % args.rotate](ctx, stream)
     barrier()
+    run_commit, launch_mode = captured(commit_launches, args.steps, ctx, args.graph)
+    barrier()
     t0 = torch.cuda.Event(enable_timing=True)
     t1 = torch.cuda.Event(enable_timing=True)
     wall0 = time.perf_counter()
     t0.record(stream)
-    for i in range(args.steps):
-        commit_launches[i % args.rotate](ctx, stream)
+    run_commit(stream)
     t1.record(stream)
     barrier()
     wall = time.perf_counter() - wall0
@@ -658,10 +684,11 @@ def main():
         for i in range(args.warmup):
             lease_launches[i % args.rotate](ctx, stream)
         barrier()
+        run_lease, _ = captured(lease_launches, args.steps, ctx, args.graph)
+        barrier()
         l0, l1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         l0.record(stream)
-        for i in range(args.steps):
-            lease_launches[i % args.rotate](ctx, stream)
+        run_lease(stream)
         l1.record(stream)
         barrier()
         lease_kern_ms = l0.elapsed_time(l1) / args.steps
@@ -692,9 +719,10 @@ def main():
         for i in range(args.warmup):
             leader_launches[i % args.rotate](ctx, stream)
         barrier()
+        run_leader, _ = captured(leader_launches, args.steps, ctx, args.graph)
+        barrier()
         l0.record(stream)
-        for i in range(args.steps):
-            leader_launches[i % args.rotate](ctx, stream)
+        run_leader(stream)
         l1.record(stream)
         barrier()
         fused_kern_ms = l0.elapsed_time(l1) / args.steps
@@ -813,7 +841,7 @@ def main():
                                "updateCommit + updateCommitIndex per group",
                    "groups_per_gpu": args.groups_per_gpu, "groups_this_job": total_groups, "peers": 5,
                    "joint_fraction": 0.10, "gap_threshold": args.gap, "rotating_batches": args.rotate,
-                   "layout": args.layout,
+                   "layout": args.layout, "timed_launches": launch_mode,
                    "sharding": f"RaftGroupId UUID.hashCode() floorMod {n_gpus}"},
         "roofline": roofline,
         "cpu_baseline": cpu,
