@@ -386,8 +386,10 @@ int rh_crc32c_verify_host(rh_ctx* ctx, const uint8_t* seg, uint64_t seg_len, con
 
 /* Checksum.update over one host span (PJC:54-91 update(byte[], off, len)): crc_state is the
  * PureJavaCrc32C `crc` field before the call (0xFFFFFFFF after reset()); *out_state receives it
- * after, so getValue() = ~*out_state.  The span is staged through the context's device scratch
- * and folded by the frame kernel (synchronous).  For per-entry call sites prefer batching frames
+ * after, so getValue() = ~*out_state.  Pure and reentrant: the span is staged through per-call
+ * stream-ordered scratch from the context's pool (no shared buffer, no lock; concurrent callers
+ * proceed independently) and folded by the frame kernel; the call returns when done.  As does
+ * rh_crc32c_verify_host.  For per-entry call sites prefer batching frames
  * through rh_crc32c_frames_launch (RH_CRC_STAMP / RH_CRC_VERIFY); this entry serves the odd
  * single span (e.g. a snapshot-file checksum). */
 int rh_crc32c(rh_ctx* ctx, uint32_t crc_state, const void* data, uint64_t n, uint32_t* out_state);

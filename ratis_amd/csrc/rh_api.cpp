@@ -122,7 +122,6 @@ RH_EXPORT int rh_shutdown(rh_ctx* ctx) {
     (void)hipFree(ctx->d_slice);
     (void)hipFree(ctx->d_shift);
     (void)hipFree(ctx->d_lane16);
-    (void)hipFree(ctx->d_scratch);
     if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
     if (ctx->pool) (void)hipMemPoolDestroy(ctx->pool);
     (void)hipStreamDestroy(ctx->stream);
@@ -187,18 +186,13 @@ RH_EXPORT int rh_crc32c(rh_ctx* ctx, uint32_t crc_state, const void* data, uint6
     *out_state = crc_state;
     if (n == 0) return RH_OK;
     DeviceGuard g(ctx->device);
-    std::lock_guard<std::mutex> lk(ctx->mu);
+    // per-call stream-ordered scratch from the context's pool: no shared buffer, no lock, so
+    // concurrent callers (Checksum.update from several threads) proceed independently
     const size_t o_len = (n + 255) / 256 * 256, total = o_len + 256;
-    if (ctx->scratch_bytes < total) {
-        (void)hipFree(ctx->d_scratch);
-        ctx->d_scratch = nullptr;
-        ctx->scratch_bytes = 0;
-        hipError_t e = hipMalloc(&ctx->d_scratch, total);
-        if (e != hipSuccess) return rh::fail(RH_E_NOMEM, "rh_crc32c: device scratch");
-        ctx->scratch_bytes = total;
-    }
-    uint8_t* base = static_cast<uint8_t*>(ctx->d_scratch);
     hipStream_t s = ctx->stream;
+    void* scratch = nullptr;
+    if (rh::pool_alloc(ctx, &scratch, total, s) != hipSuccess) return rh::fail(RH_E_NOMEM, "rh_crc32c: device scratch");
+    uint8_t* base = static_cast<uint8_t*>(scratch);
     // frame table of one span: offset 0 (8 B), length n (4 B), crc out (4 B)
     struct {
         uint64_t off;
@@ -216,10 +210,11 @@ RH_EXPORT int rh_crc32c(rh_ctx* ctx, uint32_t crc_state, const void* data, uint6
     f.init_state = crc_state;
     f.crc_out = reinterpret_cast<uint32_t*>(base + o_len + 12);
     int rc = rh_crc_launch_impl(ctx, &f, 0, s);
-    if (rc != RH_OK) return rc;
     uint32_t value = 0;
-    RH_HIP(hipMemcpyAsync(&value, base + o_len + 12, 4, hipMemcpyDeviceToHost, s));
+    if (rc == RH_OK) RH_HIP(hipMemcpyAsync(&value, base + o_len + 12, 4, hipMemcpyDeviceToHost, s));
+    RH_HIP(hipFreeAsync(scratch, s));
     RH_HIP(hipStreamSynchronize(s));
+    if (rc != RH_OK) return rc;
     *out_state = ~value;  // getValue() = ~crc
     return RH_OK;
 }
@@ -232,21 +227,15 @@ RH_EXPORT int rh_crc32c_verify_host(rh_ctx* ctx, const uint8_t* seg, uint64_t se
     *n_bad = 0;
     if (n == 0) return RH_OK;
     DeviceGuard g(ctx->device);
-    std::lock_guard<std::mutex> lk(ctx->mu);
     const size_t nwords = (n + 63) / 64;
     auto al = [](size_t x) { return (x + 255) / 256 * 256; };
     const size_t o_seg = 0, o_off = al(seg_len), o_len = o_off + al(n * 8), o_crc = o_len + al(n * 4),
                  o_bad = o_crc + al(n * 4), o_cnt = o_bad + al(nwords * 8), total = o_cnt + 256;
-    if (ctx->scratch_bytes < total) {
-        (void)hipFree(ctx->d_scratch);
-        ctx->d_scratch = nullptr;
-        ctx->scratch_bytes = 0;
-        hipError_t e = hipMalloc(&ctx->d_scratch, total);
-        if (e != hipSuccess) return rh::fail(RH_E_NOMEM, "rh_crc32c_verify_host: device scratch");
-        ctx->scratch_bytes = total;
-    }
-    uint8_t* base = static_cast<uint8_t*>(ctx->d_scratch);
     hipStream_t s = ctx->stream;
+    void* scratch = nullptr;  // per-call stream-ordered scratch (as rh_crc32c)
+    if (rh::pool_alloc(ctx, &scratch, total, s) != hipSuccess)
+        return rh::fail(RH_E_NOMEM, "rh_crc32c_verify_host: device scratch");
+    uint8_t* base = static_cast<uint8_t*>(scratch);
     RH_HIP(hipMemcpyAsync(base + o_seg, seg, seg_len, hipMemcpyHostToDevice, s));
     RH_HIP(hipMemcpyAsync(base + o_off, frame_off, n * 8, hipMemcpyHostToDevice, s));
     RH_HIP(hipMemcpyAsync(base + o_len, frame_len, n * 4, hipMemcpyHostToDevice, s));
@@ -262,12 +251,15 @@ RH_EXPORT int rh_crc32c_verify_host(rh_ctx* ctx, const uint8_t* seg, uint64_t se
     f.bad_bits = reinterpret_cast<uint64_t*>(base + o_bad);
     f.n_bad = reinterpret_cast<unsigned long long*>(base + o_cnt);
     int rc = rh_crc_launch_impl(ctx, &f, RH_CRC_VERIFY, s);
-    if (rc != RH_OK) return rc;
     unsigned long long cnt = 0;
-    if (crc_out) RH_HIP(hipMemcpyAsync(crc_out, base + o_crc, n * 4, hipMemcpyDeviceToHost, s));
-    if (bad_bits) RH_HIP(hipMemcpyAsync(bad_bits, base + o_bad, nwords * 8, hipMemcpyDeviceToHost, s));
-    RH_HIP(hipMemcpyAsync(&cnt, base + o_cnt, sizeof(cnt), hipMemcpyDeviceToHost, s));
+    if (rc == RH_OK) {
+        if (crc_out) RH_HIP(hipMemcpyAsync(crc_out, base + o_crc, n * 4, hipMemcpyDeviceToHost, s));
+        if (bad_bits) RH_HIP(hipMemcpyAsync(bad_bits, base + o_bad, nwords * 8, hipMemcpyDeviceToHost, s));
+        RH_HIP(hipMemcpyAsync(&cnt, base + o_cnt, sizeof(cnt), hipMemcpyDeviceToHost, s));
+    }
+    RH_HIP(hipFreeAsync(scratch, s));
     RH_HIP(hipStreamSynchronize(s));
+    if (rc != RH_OK) return rc;
     *n_bad = cnt;
     return RH_OK;
 }

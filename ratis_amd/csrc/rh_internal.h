@@ -120,11 +120,7 @@ struct rh_ctx {
     uint32_t* d_slice = nullptr;   // [4][256]
     uint32_t* d_shift = nullptr;   // [41][4][256]: zero-advance maps over 2^m bytes, m = 0..40
     uint32_t* d_lane16 = nullptr;  // lane-distance nibble tables of the 16-lane x 64-byte fold
-    // scratch for host-buffer convenience calls
-    std::mutex mu;
-    std::mutex pool_mu;  // guards pool creation (pool_alloc may run under mu, e.g. in rh_crc32c)
-    void* d_scratch = nullptr;
-    size_t scratch_bytes = 0;
+    std::mutex pool_mu;  // guards the pool's creation
     void* h_pinned = nullptr;
     size_t pinned_bytes = 0;
     hipMemPool_t pool = nullptr;  // stream-ordered scratch (rh::pool_alloc)

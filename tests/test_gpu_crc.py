@@ -340,3 +340,25 @@ def test_lane_path_plain_spans_from_any_state(ctx, orc):
                     dtype=np.uint32)
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, [(int(offs[i]), int(lens[i])) for i in bad[:10]]
+
+
+def test_single_span_entry_concurrent_callers(ctx, orc):
+    """rh_crc32c from several host threads at once (per-call pool scratch, no shared buffer):
+    every caller gets its own span's PureJavaCrc32C state."""
+    import threading
+
+    from ratis_amd import engine
+    rng = np.random.default_rng(33)
+    spans = [rng.integers(0, 256, size=int(rng.integers(1, 20000)), dtype=np.uint8).tobytes() for _ in range(48)]
+    got = [None] * len(spans)
+
+    def work(k):
+        for i in range(k, len(spans), 6):
+            got[i] = engine.crc32c_update(ctx, 0xFFFFFFFF, spans[i])
+    th = [threading.Thread(target=work, args=(k,)) for k in range(6)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    for i, sp in enumerate(spans):
+        assert got[i] == orc.crc32c_update(0xFFFFFFFF, sp), i
