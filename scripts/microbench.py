@@ -6,6 +6,7 @@ import argparse
 import json
 import os
 import sys
+import time
 
 import numpy as np
 
@@ -17,6 +18,7 @@ def main():
     ap.add_argument("--segments", type=int, default=32)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--warm-ms", type=float, default=60.0, help="untimed run of each kernel/shape before its rounds")
     ap.add_argument("--only", default="crc,framing,commit,lease", help="comma list of sections to run")
     a = ap.parse_args()
     import torch
@@ -40,7 +42,14 @@ def main():
     only = set(a.only.split(","))
 
     def timed(fn, nbytes, iters):
-        fn()
+        # run the kernel for --warm-ms first: launch times settle only after tens of ms of load
+        # (clock / power transient, profiles/r02/crc_warmup/), whatever the launch size
+        t0 = time.perf_counter()
+        while True:
+            fn()
+            torch.cuda.synchronize()
+            if (time.perf_counter() - t0) * 1e3 >= a.warm_ms:
+                break
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for i in range(iters):
