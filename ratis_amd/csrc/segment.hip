@@ -567,6 +567,10 @@ constexpr uint32_t kPiece = RH_PIECE_BYTES;  // bytes per piece
 constexpr uint32_t kGuessWin = RH_GUESS_WIN;  // bytes of a piece the guess pass looks at
 constexpr uint32_t kGuessLds = kGuessWin + 64;
 constexpr int kPieceThreads = RH_PIECE_THREADS;
+#ifndef RH_GUESS_BLOCKS_PER_CU  // A/B builds override (scripts/ab_build.sh)
+#define RH_GUESS_BLOCKS_PER_CU 4
+#endif
+constexpr int kGuessBlocksPerCu = RH_GUESS_BLOCKS_PER_CU;  // guess blocks resident per CU
 constexpr uint32_t kList = RH_PIECE_LIST;  // frame lengths (u16) a guessed walk records
 constexpr uint32_t kListPerLane = kList / 64;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
@@ -1103,7 +1107,7 @@ int rh_segments_launch_impl(rh_ctx* ctx, const rh_segments* g, hipStream_t strea
     RH_HIP(hipMemsetAsync(pa.n_pieces, 0, sizeof(unsigned int), stream));
     hipLaunchKernelGGL(piece_plan_kernel, dim3(1), dim3(kScanThreads), 0, stream, pa);
     RH_HIP(hipGetLastError());
-    hipLaunchKernelGGL(piece_guess_kernel, dim3((uint32_t)(4 * cus)), dim3(kPieceThreads), 0, stream, pa);
+    hipLaunchKernelGGL(piece_guess_kernel, dim3((uint32_t)(kGuessBlocksPerCu * cus)), dim3(kPieceThreads), 0, stream, pa);
     RH_HIP(hipGetLastError());
     const uint64_t wgrid = (piece_cap + 255) / 256 < (uint64_t)cus * 8 ? (piece_cap + 255) / 256 : (uint64_t)cus * 8;
     hipLaunchKernelGGL(piece_walk_kernel, dim3((uint32_t)wgrid), dim3(256), 0, stream, pa);
