@@ -568,7 +568,7 @@ constexpr uint32_t kGuessWin = RH_GUESS_WIN;  // bytes of a piece the guess pass
 constexpr uint32_t kGuessLds = kGuessWin + 64;
 constexpr int kPieceThreads = RH_PIECE_THREADS;
 #ifndef RH_GUESS_BLOCKS_PER_CU  // A/B builds override (scripts/ab_build.sh)
-#define RH_GUESS_BLOCKS_PER_CU 4
+#define RH_GUESS_BLOCKS_PER_CU 6
 #endif
 constexpr int kGuessBlocksPerCu = RH_GUESS_BLOCKS_PER_CU;  // guess blocks resident per CU
 constexpr uint32_t kList = RH_PIECE_LIST;  // frame lengths (u16) a guessed walk records
