@@ -274,6 +274,16 @@ int rh_commit_batch(rh_groups* g, uint32_t flags, rh_commit_out* out);
  * ready.  Deltas and other calls may be issued in between (they are ordered after it). */
 int rh_commit_batch_async(rh_groups* g, uint32_t flags, uint64_t* ticket);
 int rh_commit_batch_wait(rh_groups* g, uint64_t ticket, rh_commit_out* out);
+/* Where the evaluation kernels put their event records.  HOST_MAPPED (the default): straight into
+ * the pinned result buffers across PCIe, each workgroup's records as one contiguous run -- no copy
+ * afterwards, the kernel ends when its records have landed.  DEVICE: into HBM; rh_commit_batch_wait
+ * / rh_watch_levels then copy the counted prefix into the same pinned buffers (a D2H on the
+ * table's copy stream), so the kernel is not held up by PCIe writes.  Results are identical.  Not
+ * while an rh_commit_batch_async ticket is outstanding (RH_E_STATE); DEVICE allocates
+ * 112 B x capacity of HBM on first use. */
+#define RH_EVENTS_HOST_MAPPED 0
+#define RH_EVENTS_DEVICE      1
+int rh_groups_set_event_sink(rh_groups* g, int sink);
 /* Batched commitIndexChanged() over the slots whose follower commitIndex or leader commitIndex
  * changed: the slots whose {min, majority, max} levels changed, into library-owned pinned memory
  * valid until the next rh_watch_levels.  Blocks. */
@@ -321,6 +331,11 @@ typedef struct rh_node rh_node;
  * (java.util.UUID.hashCode).  Pure host function; no device needed. */
 int rh_shard_of(uint64_t uuid_msb, uint64_t uuid_lsb, int n_shards);
 int rh_node_create(uint32_t device_mask, uint64_t capacity_per_shard, int64_t gap_threshold, rh_node** out);
+/* The same with an explicit device per shard: shard i lives on GPU devices[i] (1 <= n_shards <= 64;
+ * a device may repeat -- several shards on one GPU, each with its own context, stream and table:
+ * how a one-GPU box runs the routing, gathering and lease bitmap of an 8-GPU server). */
+int rh_node_create_devices(const int* devices, int n_shards, uint64_t capacity_per_shard, int64_t gap_threshold,
+                           rh_node** out);
 int rh_node_destroy(rh_node* node);
 int rh_node_shards(rh_node* node);
 /* The shard table (for per-shard calls such as the zero-copy ring) and its context. */
@@ -386,12 +401,12 @@ int rh_crc32c_verify_host(rh_ctx* ctx, const uint8_t* seg, uint64_t seg_len, con
 
 /* Checksum.update over one host span (PJC:54-91 update(byte[], off, len)): crc_state is the
  * PureJavaCrc32C `crc` field before the call (0xFFFFFFFF after reset()); *out_state receives it
- * after, so getValue() = ~*out_state.  Pure and reentrant: the span is staged through per-call
- * stream-ordered scratch from the context's pool (no shared buffer, no lock; concurrent callers
- * proceed independently) and folded by the frame kernel; the call returns when done.  As does
- * rh_crc32c_verify_host.  For per-entry call sites prefer batching frames
- * through rh_crc32c_frames_launch (RH_CRC_STAMP / RH_CRC_VERIFY); this entry serves the odd
- * single span (e.g. a snapshot-file checksum). */
+ * after, so getValue() = ~*out_state.  Reentrant: the span is staged through per-call
+ * stream-ordered scratch from the context's pool (no shared staging buffer) and folded by the frame
+ * kernel on the context stream, so concurrent callers are safe but run one after another (and
+ * after other work on that stream); the call returns when done, as does rh_crc32c_verify_host.  For
+ * per-entry call sites prefer batching frames through rh_crc32c_frames_launch (RH_CRC_STAMP /
+ * RH_CRC_VERIFY); this entry serves the odd single span (e.g. a snapshot-file checksum). */
 int rh_crc32c(rh_ctx* ctx, uint32_t crc_state, const void* data, uint64_t n, uint32_t* out_state);
 
 /* ---- leader lease (LeaderStateImpl.hasLease LSI:1229-1249; LeaderLease LL:60-103) ------------
@@ -490,6 +505,33 @@ typedef struct rh_segments_crc {
     unsigned long long* n_bad;    /* optional: CRC mismatches over all found frames (added)          */
 } rh_segments_crc;
 int rh_segments_read_launch(rh_ctx* ctx, const rh_segments* segs, const rh_segments_crc* crc, void* stream);
+
+/* One segment's outcome of rh_segments_read_host: what LogSegment.readSegmentFile's reader loop
+ * (SegmentedRaftLogInputStream.nextEntry -> SegmentedRaftLogReader.readEntry / decodeEntry,
+ * LogSegment.java:166-196) meets in that file, minus the LogEntryProto parse. */
+typedef struct rh_segment_result {
+    int32_t  status;       /* RH_SEG_END / RH_SEG_PARTIAL (the reader returns null: normal end);
+                              RH_SEG_E_CHECKSUM (ChecksumException at `stop`, RDR:330-336),
+                              RH_SEG_E_OVERSIZE / _PADDING / _VARINT / _HEADER (IOException /
+                              CorruptedFileException); RH_SEG_E_CAPACITY / _RANGE: not read here    */
+    uint32_t n_ok;         /* entries the reader returns before it stops                           */
+    uint64_t stop;         /* offset in the segment where it stopped (the failing frame, or the end) */
+    uint64_t first_frame;  /* index of the segment's first frame in frame_off / frame_len / frame_crc */
+    uint32_t n_frames;     /* frames the framing walk found (>= n_ok)                              */
+    uint32_t reserved;
+} rh_segment_result;
+
+/* The read path over HOST segment images (PCIe-inclusive; what the Java module's bulk segment load
+ * calls): copies `image` and the segment table to the device, runs rh_segments_read_launch, and
+ * copies back each segment's result and the frame table in segment order -- offsets relative to
+ * the start of `image`, whole frame lengths (varint + entry + 4), computed CRCs.  Segment i is
+ * image[seg_off[i], seg_off[i] + seg_len[i]).  frames_per_seg_cap bounds the frames of one segment
+ * (a segment with more reports RH_SEG_E_CAPACITY: read it with the Java reader); the frame arrays
+ * hold frame_cap entries and *n_frames_total receives the total found.  Blocks. */
+int rh_segments_read_host(rh_ctx* ctx, const uint8_t* image, uint64_t image_len, const uint64_t* seg_off,
+                          const uint64_t* seg_len, uint64_t n_seg, uint32_t max_op, uint32_t frames_per_seg_cap,
+                          uint64_t* frame_off, uint32_t* frame_len, uint32_t* frame_crc, uint64_t frame_cap,
+                          rh_segment_result* results, uint64_t* n_frames_total);
 #ifdef __cplusplus
 }
 #endif

@@ -9,10 +9,20 @@
  *   - the per-division EventProcessor thread and its UPDATE_COMMIT queue (LeaderStateImpl.java:111-188,
  *     791-816): producers append 16-byte deltas; ONE pump thread pushes them and runs the batched
  *     updateCommit over the dirty divisions;
- *   - RaftLogBase.updateCommitIndex's decision (RaftLogBase.java:121-142).
- * The follow-up the reference runs after a successful updateCommitIndex -- getEntries, the real
- * ServerState.updateCommitIndex, StateMachineUpdater.notifyUpdater, watch release -- stays in the
- * division's LeaderStateImpl (Callback.onCommit), for the advanced divisions only.
+ *   - RaftLogBase.updateCommitIndex's decision (RaftLogBase.java:121-142);
+ *   - commitIndexChanged()'s watch levels (LeaderStateImpl.java:606-622) over the divisions whose
+ *     follower commitIndex or leader commitIndex changed;
+ *   - LeaderStateImpl.hasLease / LeaderLease.extend (LeaderStateImpl.java:1229-1249, LeaderLease.java).
+ * The follow-up the reference runs after a decision -- getEntries, the real
+ * ServerState.updateCommitIndex, StateMachineUpdater.notifyUpdater, the WatchRequests updates,
+ * notifySenders -- stays in the division's LeaderStateImpl (Callback), for the divisions with an
+ * event only.
+ *
+ * One pump tick: push the buffered deltas; start every shard's updateCommit evaluation (all GPUs in
+ * flight); per shard, wait and hand the advanced commits and changed watch-ALL levels to the
+ * divisions; per shard, commitIndexChanged's levels; the lease bitmap; recycle the slots released
+ * during the tick.  Nothing is allocated per tick: every result array is sized once, per shard
+ * capacity, and reused shard after shard.
  */
 package org.apache.ratis.hip;
 
@@ -30,51 +40,118 @@ import java.util.Map;
 import java.util.UUID;
 import java.util.concurrent.ConcurrentHashMap;
 import java.util.concurrent.TimeUnit;
+import java.util.concurrent.atomic.AtomicLongArray;
+import java.util.concurrent.atomic.AtomicReferenceArray;
 import java.util.concurrent.locks.LockSupport;
 
 public final class HipLeaderBookkeeper implements AutoCloseable {
   /** What a division's LeaderStateImpl does with the GPU's decisions (run on the pump thread). */
   public interface Callback {
-    /** updateCommit(majority, min) found a new commit index (LeaderStateImpl.java:1015-1026). */
+    /** updateCommit(majority, min) found a new commit index (LeaderStateImpl.java:1015-1024). */
     void onCommit(long newCommitIndex);
-    /** watchRequests.update(ALL, min) with a changed level (LeaderStateImpl.java:1025). */
+    /** updateCommit(majority, min)'s watchRequests.update(ALL, min), the level changed (LeaderStateImpl.java:1025). */
     void onWatchAll(long min);
+    /** commitIndexChanged()'s levels changed (LeaderStateImpl.java:612-622): ALL_COMMITTED = min,
+     *  MAJORITY_COMMITTED = majority, MAJORITY = max; the division then runs notifySenders(). */
+    void onWatchLevels(long min, long majority, long max);
   }
 
   private final RatisHip hip;
-  private final long capacity;
+  private final int shards;
+  private final int capacity;                        // divisions per shard
   private final Deque<Integer>[] freeSlots;
+  private final Deque<Integer> pendingFree = new ArrayDeque<>();   // released during the current tick
   private final Map<Integer, Division> divisions = new ConcurrentHashMap<>();
   private final ByteBuffer deltas;         // producers' deltas (node slots), drained by the pump
   private final Object deltaLock = new Object();
   private final Thread pump;
   private final long tickNanos;
-  private volatile boolean watchAll;       // some division has ALL-level watch requests
   private volatile boolean running = true;
+  private volatile Throwable failure;                // set when the pump died: no more results, no lease
   private volatile long leaseTimeoutMs = -1;  // LeaderLease.leaseTimeoutMs; -1: no lease batches
-  private volatile long[] leaseBits;          // last rh_node_lease_batch: bit = node slot has the lease
+
+  // ---- pump-thread result arrays: one shard's worth, reused for every shard and every tick -----
+  private final int[] advSlot;
+  private final long[] advCommit;
+  private final int[] wallSlot;
+  private final long[] wallMin;
+  private final int[] wSlot;
+  private final long[] wMin;
+  private final long[] wMaj;
+  private final long[] wMax;
+  private final boolean[] wValid;
+  private final long[] tickets;
+
+  /**
+   * The lease bitmap of one shard, published by the pump under a sequence number (odd while being
+   * written; every field is read and written with volatile / ordered accesses, so a reader that
+   * sees the same even number before and after its reads saw one consistent bitmap).  A bit
+   * answers hasLease() only until validUntil: the batch was evaluated at evaluation time + margin
+   * (a lease valid then is valid at every earlier moment: LeaderLease only moves forward), and
+   * after validUntil the bitmap says nothing -- a stalled or dead pump turns every lease off
+   * instead of freezing it (LeaderLease.java:60-62 checks at call time).
+   */
+  private static final class LeaseBits {
+    final AtomicLongArray bits;
+    volatile long seq;
+    volatile long validUntil;   // System.nanoTime() bound of this bitmap
+    volatile long batch;        // leaseBatchCount when it was evaluated
+
+    LeaseBits(int words) {
+      this.bits = new AtomicLongArray(words);
+    }
+  }
+
+  private final LeaseBits[][] lease;       // [shard][2]: written alternately
+  private final int[] leaseCurrent;        // [shard] which of the two is published (pump-owned)
+  private final AtomicReferenceArray<LeaseBits> leasePublished;
+  private final long[] leaseScratch;       // the native batch's output, copied into a LeaseBits
+  private volatile long leaseBatchCount;   // batches started so far
+  private final long leaseMarginNanos;
 
   @SuppressWarnings("unchecked")
   public HipLeaderBookkeeper(int deviceMask, long capacityPerShard, long gapThreshold, long tickMicros)
       throws IOException {
+    if (capacityPerShard < 1 || capacityPerShard > Integer.MAX_VALUE - 8) {
+      throw new IllegalArgumentException("capacityPerShard out of range: " + capacityPerShard);
+    }
     this.hip = new RatisHip(deviceMask, capacityPerShard, gapThreshold);
-    this.capacity = capacityPerShard;
-    this.freeSlots = new Deque[hip.getShards()];
-    for (int s = 0; s < freeSlots.length; s++) {
+    this.shards = hip.getShards();
+    this.capacity = (int) capacityPerShard;
+    this.freeSlots = new Deque[shards];
+    for (int s = 0; s < shards; s++) {
       freeSlots[s] = new ArrayDeque<>();
-      for (long i = capacityPerShard - 1; i >= 0; i--) {
-        freeSlots[s].push((int) i);
+      for (int i = capacity - 1; i >= 0; i--) {
+        freeSlots[s].push(i);
       }
     }
     this.deltas = ByteBuffer.allocateDirect(RatisHip.DELTA_BYTES << 20).order(ByteOrder.LITTLE_ENDIAN);
     this.tickNanos = TimeUnit.MICROSECONDS.toNanos(tickMicros);
+    // a bitmap stays meaningful for two ticks: long enough for the next one to replace it
+    this.leaseMarginNanos = 2 * tickNanos;
+    this.advSlot = new int[capacity];
+    this.advCommit = new long[capacity];
+    this.wallSlot = new int[capacity];
+    this.wallMin = new long[capacity];
+    this.wSlot = new int[capacity];
+    this.wMin = new long[capacity];
+    this.wMaj = new long[capacity];
+    this.wMax = new long[capacity];
+    this.wValid = new boolean[capacity];
+    this.tickets = new long[shards];
+    final int words = (capacity + 63) / 64;
+    this.lease = new LeaseBits[shards][2];
+    this.leaseCurrent = new int[shards];
+    this.leasePublished = new AtomicReferenceArray<>(shards);
+    this.leaseScratch = new long[words];
+    for (int s = 0; s < shards; s++) {
+      lease[s][0] = new LeaseBits(words);
+      lease[s][1] = new LeaseBits(words);
+      leasePublished.set(s, lease[s][0]);   // batch 0: answers no division (see hasLease)
+    }
     this.pump = new Thread(this::pumpLoop, "ratis-hip-commit-pump");
     this.pump.setDaemon(true);
     this.pump.start();
-  }
-
-  public void setWatchAll(boolean enabled) {
-    this.watchAll = enabled;
   }
 
   /** rpc.timeout.min x read.leader.lease.timeout.ratio (LeaderLease.java:45-48); the pump then
@@ -83,23 +160,48 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
     this.leaseTimeoutMs = ms;
   }
 
+  /** Why the pump stopped, or null while it runs. */
+  public Throwable getFailure() {
+    return failure;
+  }
+
+  private void checkRunning() {
+    final Throwable f = failure;
+    if (f != null) {
+      throw new IllegalStateException("ratis-hip: the commit pump has failed", f);
+    }
+  }
+
   /** A new leader division (new LeaderStateImpl, LeaderStateImpl.java:365-430). */
   public synchronized Division register(RaftGroupId groupId, RaftPeerId selfId, Callback callback) {
+    checkRunning();
     final UUID u = groupId.getUuid();
     final int shard = hip.shardOf(u.getMostSignificantBits(), u.getLeastSignificantBits());
     final Integer slot = freeSlots[shard].poll();
     if (slot == null) {
       throw new IllegalStateException("ratis-hip: shard " + shard + " is full (" + capacity + " divisions)");
     }
-    final int nodeSlot = (int) (shard * capacity + slot);
+    final int nodeSlot = shard * capacity + slot;
     final Division d = new Division(nodeSlot, selfId, callback);
     divisions.put(nodeSlot, d);
     return d;
   }
 
+  /**
+   * The division is gone: no event reaches it from now on (it leaves the map), and its slot waits
+   * for the end of the current pump tick before it can be handed out again -- an evaluation that
+   * was in flight when the division stopped can only deliver to an empty map entry, never to a
+   * new division that took the slot over.
+   */
   synchronized void release(Division d) {
     divisions.remove(d.nodeSlot);
-    freeSlots[(int) (d.nodeSlot / capacity)].push((int) (d.nodeSlot % capacity));
+    pendingFree.add(d.nodeSlot);
+  }
+
+  private synchronized void recycleSlots() {
+    for (Integer s; (s = pendingFree.poll()) != null; ) {
+      freeSlots[s / capacity].push(s % capacity);
+    }
   }
 
   /** Appends one delta; the caller holds deltaLock (one ordered stream of deltas and control ops). */
@@ -124,48 +226,77 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
   }
 
   private void pumpLoop() {
-    final int cap = (int) Math.min(Integer.MAX_VALUE - 8, capacity * hip.getShards());
-    final int[] advSlot = new int[cap];
-    final long[] advCommit = new long[cap];
-    final int[] wallSlot = new int[cap];
-    final long[] wallMin = new long[cap];
-    while (running) {
-      LockSupport.parkNanos(tickNanos);
-      synchronized (deltaLock) {
-        drainDeltas();
+    try {
+      while (running) {
+        LockSupport.parkNanos(tickNanos);
+        tick();
       }
-      final long counts;
-      try {
-        counts = watchAll ? hip.commitBatch(advSlot, advCommit, wallSlot, wallMin)
-                          : hip.commitBatch(advSlot, advCommit, null, null);
-      } catch (IOException e) {
-        throw new IllegalStateException("ratis-hip: commitBatch failed", e);
-      }
-      final int nAdv = (int) Math.min(counts >>> 32, cap);
+    } catch (Throwable t) {
+      failure = t;   // results stop; hasLease() turns false at once (see Division.hasLease)
+    }
+  }
+
+  /** One pump tick (see the class comment). */
+  void tick() throws IOException {
+    synchronized (deltaLock) {
+      drainDeltas();
+    }
+    // updateCommit() of every shard's dirty divisions: all shards in flight before any wait
+    for (int s = 0; s < shards; s++) {
+      tickets[s] = hip.commitAsync(s, RatisHip.COMMIT_WATCH_ALL);
+    }
+    for (int s = 0; s < shards; s++) {
+      final long counts = hip.commitWait(s, tickets[s], advSlot, advCommit, wallSlot, wallMin);
+      final int base = s * capacity;
+      final int nAdv = (int) Math.min(counts >>> 32, capacity);
       for (int i = 0; i < nAdv; i++) {
-        final Division d = divisions.get(advSlot[i]);
+        final Division d = divisions.get(base + advSlot[i]);
         if (d != null) {
           d.callback.onCommit(advCommit[i]);
         }
       }
-      final int nWall = (int) Math.min(counts & 0xFFFFFFFFL, cap);
+      final int nWall = (int) Math.min(counts & 0xFFFFFFFFL, capacity);
       for (int i = 0; i < nWall; i++) {
-        final Division d = divisions.get(wallSlot[i]);
+        final Division d = divisions.get(base + wallSlot[i]);
         if (d != null) {
           d.callback.onWatchAll(wallMin[i]);
         }
       }
-      final long timeout = leaseTimeoutMs;
-      if (timeout >= 0) {  // LeaderStateImpl.hasLease for every division: extend + isValid
-        final long[] bits = new long[(cap + 63) / 64];
-        try {
-          hip.leaseBatch(System.nanoTime(), timeout, bits);
-        } catch (IOException e) {
-          throw new IllegalStateException("ratis-hip: leaseBatch failed", e);
+    }
+    // commitIndexChanged() of the divisions whose follower / leader commitIndex changed
+    for (int s = 0; s < shards; s++) {
+      final int n = Math.min(hip.watchLevels(s, wSlot, wMin, wMaj, wMax, wValid), capacity);
+      final int base = s * capacity;
+      for (int i = 0; i < n; i++) {
+        if (!wValid[i]) {
+          continue;   // getMajorityMin was Optional.empty(): no watch update (LeaderStateImpl.java:613)
         }
-        leaseBits = bits;
+        final Division d = divisions.get(base + wSlot[i]);
+        if (d != null) {
+          d.callback.onWatchLevels(wMin[i], wMaj[i], wMax[i]);
+        }
       }
     }
+    final long timeout = leaseTimeoutMs;
+    if (timeout >= 0) {  // LeaderStateImpl.hasLease for every division: extend + isValid
+      final long batch = ++leaseBatchCount;
+      final long now = System.nanoTime();
+      for (int s = 0; s < shards; s++) {
+        hip.leaseBatch(s, now + leaseMarginNanos, timeout, leaseScratch);
+        final int next = leaseCurrent[s] ^ 1;
+        final LeaseBits lb = lease[s][next];
+        lb.seq = lb.seq + 1;                        // odd: being written (only the pump writes)
+        for (int w = 0; w < leaseScratch.length; w++) {
+          lb.bits.lazySet(w, leaseScratch[w]);
+        }
+        lb.validUntil = now + leaseMarginNanos;
+        lb.batch = batch;
+        lb.seq = lb.seq + 1;
+        leaseCurrent[s] = next;
+        leasePublished.set(s, lb);
+      }
+    }
+    recycleSlots();
   }
 
   @Override
@@ -204,6 +335,7 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
     private final Map<RaftPeerId, Integer> followerSlot = new HashMap<>();   // peers with a FollowerInfo
     private boolean started;   // guarded by deltaLock
     private int width;         // follower columns of the device tier; guarded by deltaLock
+    private volatile long leaseArmedAfter = Long.MAX_VALUE;   // lease batches up to this one predate leaseStart
 
     Division(int nodeSlot, RaftPeerId selfId, Callback callback) {
       this.nodeSlot = nodeSlot;
@@ -273,6 +405,7 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
 
     /** Leader start: every FollowerInfo new (-1); StartupLogEntry index = termStart (LeaderStateImpl.java:296-301). */
     public void start(int conf, long flushIndex, long commitIndex, long termStart) throws IOException {
+      checkRunning();
       synchronized (deltaLock) {
         drainDeltas();
         hip.start(nodeSlot, conf, flushIndex, commitIndex, termStart);
@@ -309,6 +442,7 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
         }
         drainDeltas();
         started = false;
+        leaseArmedAfter = Long.MAX_VALUE;
         hip.stop(nodeSlot);
       }
       release(this);
@@ -325,7 +459,8 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
       emit(followerSlot, RatisHip.colMatch(followerSlot), RatisHip.OP_SET, value);
     }
 
-    /** FollowerInfo.updateCommitIndex (FollowerInfoImpl.java:103-105). */
+    /** FollowerInfo.updateCommitIndex (FollowerInfoImpl.java:103-105): the pump's next watchLevels
+     *  reports the division if its commitIndexChanged() levels moved. */
     public void followerCommitIndex(int followerSlot, long value) {
       emit(followerSlot, RatisHip.colFollowerCommit(followerSlot), RatisHip.OP_MAX, value);
     }
@@ -348,6 +483,8 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
           return;
         }
         drainDeltas();
+        // batches already started may predate this lease: only a later one answers hasLease()
+        leaseArmedAfter = leaseBatchCount;
         hip.leaseStart(nodeSlot, nowNanos, enabled);
       }
     }
@@ -362,10 +499,32 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
       emit(-1, RatisHip.COL_LEASE_ON, RatisHip.OP_SET, enabled ? 1L : 0L);
     }
 
-    /** enabled && (singleton || the lease, extended if it could be, is valid) at the last tick. */
+    /**
+     * enabled && (singleton || the lease, extended if it could be, is valid), as of the latest
+     * lease batch -- evaluated for a moment at least as late as now, so a true answer holds now.
+     * False when no such batch exists: the pump has not run one since leaseStart, it has stalled
+     * past the bitmap's validity, or it has failed.
+     */
     public boolean hasLease() {
-      final long[] bits = leaseBits;
-      return bits != null && ((bits[nodeSlot >>> 6] >>> (nodeSlot & 63)) & 1L) != 0;
+      if (failure != null) {
+        return false;
+      }
+      final int shard = nodeSlot / capacity;
+      final int slot = nodeSlot % capacity;
+      for (;;) {
+        final LeaseBits lb = leasePublished.get(shard);
+        final long seq = lb.seq;
+        if ((seq & 1) != 0) {
+          continue;   // being rewritten: the pump published the other one meanwhile
+        }
+        final boolean bit = ((lb.bits.get(slot >>> 6) >>> (slot & 63)) & 1L) != 0;
+        final long validUntil = lb.validUntil;
+        final long batch = lb.batch;
+        if (lb.seq != seq) {
+          continue;
+        }
+        return bit && batch > leaseArmedAfter && System.nanoTime() - validUntil <= 0;
+      }
     }
   }
 }

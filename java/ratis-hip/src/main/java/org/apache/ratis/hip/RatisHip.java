@@ -11,7 +11,8 @@
  * Error mapping (ratis_hip.h): RH_E_INVAL / RH_E_RANGE -> IllegalArgumentException (as the
  * reference throws for bad arguments, e.g. LeaderStateImpl.java:396-399), every other negative
  * status -> IOException; a frame whose checksum does not verify -> ChecksumException at its offset
- * (SegmentedRaftLogReader.java:330-336) in the callers.
+ * (SegmentedRaftLogReader.java:330-336) in the callers.  Array and buffer sizes are checked here
+ * (and again in the native half) before any native call reads or writes them.
  */
 package org.apache.ratis.hip;
 
@@ -52,6 +53,17 @@ public final class RatisHip implements AutoCloseable {
   public static final int OP_SET = 1;   // RaftLogIndex.setUnconditionally (setSnapshotIndex)
   public static final int COMMIT_WATCH_ALL = 1;
 
+  // ---- segment read verdicts (ratis_hip.h RH_SEG_*) -----------------------------------------
+  public static final int SEG_END = 1;
+  public static final int SEG_PARTIAL = 2;
+  public static final int SEG_E_OVERSIZE = -1;
+  public static final int SEG_E_CHECKSUM = -2;
+  public static final int SEG_E_PADDING = -3;
+  public static final int SEG_E_VARINT = -4;
+  public static final int SEG_E_HEADER = -5;
+  public static final int SEG_E_CAPACITY = -6;
+  public static final int SEG_E_RANGE = -7;
+
   /** Writes one delta at the buffer's position (little-endian) and advances it. */
   public static void putDelta(ByteBuffer ring, int slotInShard, int column, int op, long value) {
     ring.putInt(slotInShard).put((byte) column).put((byte) op).putShort((short) 0).putLong(value);
@@ -75,6 +87,18 @@ public final class RatisHip implements AutoCloseable {
     return shardOf0(uuidMsb, uuidLsb, shards);
   }
 
+  private void checkShard(int shard) {
+    if (shard < 0 || shard >= shards) {
+      throw new IllegalArgumentException("no shard " + shard + " (" + shards + " shards)");
+    }
+  }
+
+  private static void checkLength(String what, int length, long needed) {
+    if (length < needed) {
+      throw new IllegalArgumentException(what + ".length = " + length + " < " + needed);
+    }
+  }
+
   // ---- division lifecycle (node slots = shard * capacityPerShard + slot in shard) ------------
   /** New LeaderStateImpl: every FollowerInfo new (index -1); termStart = StartupLogEntry index. */
   public void start(int nodeSlot, int conf, long flushIndex, long commitIndex, long termStart) throws IOException {
@@ -83,6 +107,9 @@ public final class RatisHip implements AutoCloseable {
 
   /** Conf change: src[k] = old follower slot kept by new slot k, or -1 for a new FollowerInfo. */
   public void reconf(int nodeSlot, int conf, byte[] src) throws IOException {
+    if (src != null) {
+      checkLength("src", src.length, MAX_FOLLOWERS);
+    }
     groupReconf0(node, nodeSlot, conf, src);
   }
 
@@ -91,8 +118,16 @@ public final class RatisHip implements AutoCloseable {
   }
 
   // ---- delta producers ---------------------------------------------------------------------
-  /** Validated push of n deltas packed in a direct buffer (node slots); returns when reusable. */
+  /** Validated push of the n deltas at the start of a direct buffer (node slots); returns when the
+   * buffer may be reused. */
   public void pushDeltas(ByteBuffer direct, int n) throws IOException {
+    if (!direct.isDirect()) {
+      throw new IllegalArgumentException("pushDeltas needs a direct buffer");
+    }
+    if (n < 0 || (long) n * DELTA_BYTES > direct.capacity()) {
+      throw new IllegalArgumentException("pushDeltas: " + n + " deltas do not fit the buffer's "
+          + direct.capacity() + " bytes");
+    }
     pushDeltas0(node, direct, n);
   }
 
@@ -102,10 +137,12 @@ public final class RatisHip implements AutoCloseable {
    * Hand it back with {@link #submitDeltas}; one acquire/submit pair at a time per shard.
    */
   public ByteBuffer acquireDeltas(int shard) throws IOException {
+    checkShard(shard);
     return acquire0(node, shard).order(ByteOrder.LITTLE_ENDIAN);
   }
 
   public void submitDeltas(int shard, int n) throws IOException {
+    checkShard(shard);
     submit0(node, shard, n);
   }
 
@@ -117,12 +154,43 @@ public final class RatisHip implements AutoCloseable {
    * (long) nAdvanced << 32 | nWatchAll; counts beyond the arrays are truncated.
    */
   public long commitBatch(int[] advSlot, long[] advCommit, int[] wallSlot, long[] wallMin) throws IOException {
+    checkLength("advCommit", advCommit.length, advSlot.length);
+    if (wallSlot != null) {
+      checkLength("wallMin", wallMin.length, wallSlot.length);
+    }
     return commitBatch0(node, advSlot, advCommit, wallSlot, wallMin);
   }
 
-  /** Batched commitIndexChanged() of one shard: changed {min, majority, max} levels. */
+  /** rh_commit_batch_async on one shard: the evaluation is in flight when this returns. */
+  public long commitAsync(int shard, int flags) throws IOException {
+    checkShard(shard);
+    return commitAsync0(node, shard, flags);
+  }
+
+  /**
+   * rh_commit_batch_wait on one shard: the shard's events (slots WITHIN the shard) copied into the
+   * caller's arrays, which must hold the shard capacity.  Returns nAdvanced << 32 | nWatchAll.
+   */
+  public long commitWait(int shard, long ticket, int[] advSlot, long[] advCommit, int[] wallSlot, long[] wallMin)
+      throws IOException {
+    checkShard(shard);
+    checkLength("advSlot", advSlot.length, capacityPerShard);
+    checkLength("advCommit", advCommit.length, capacityPerShard);
+    checkLength("wallSlot", wallSlot.length, capacityPerShard);
+    checkLength("wallMin", wallMin.length, capacityPerShard);
+    return commitWait0(node, shard, ticket, advSlot, advCommit, wallSlot, wallMin);
+  }
+
+  /** Batched commitIndexChanged() of one shard: changed {min, majority, max} levels (slots within
+   * the shard).  Every array must hold the shard capacity. */
   public int watchLevels(int shard, int[] slot, long[] min, long[] majority, long[] max, boolean[] valid)
       throws IOException {
+    checkShard(shard);
+    checkLength("slot", slot.length, capacityPerShard);
+    checkLength("min", min.length, capacityPerShard);
+    checkLength("majority", majority.length, capacityPerShard);
+    checkLength("max", max.length, capacityPerShard);
+    checkLength("valid", valid.length, capacityPerShard);
     return watchLevels0(node, shard, slot, min, majority, max, valid);
   }
 
@@ -137,17 +205,39 @@ public final class RatisHip implements AutoCloseable {
   /** hasLease() of every node slot at nowNanos (without isRunning()/isReady()); extended leases
    * stay in the table.  bits[s / 64] bit s % 64 = slot s; bits.length >= ceil(slots / 64). */
   public void leaseBatch(long nowNanos, long timeoutMs, long[] bits) throws IOException {
+    checkLength("bits", bits.length, (shards * capacityPerShard + 63) / 64);
     leaseBatch0(node, nowNanos, timeoutMs, bits);
+  }
+
+  /** hasLease() of one shard's slots at nowNanos; bits.length >= ceil(capacityPerShard / 64). */
+  public void leaseBatch(int shard, long nowNanos, long timeoutMs, long[] bits) throws IOException {
+    checkShard(shard);
+    checkLength("bits", bits.length, (capacityPerShard + 63) / 64);
+    leaseBatchShard0(node, shard, nowNanos, timeoutMs, bits);
   }
 
   // ---- checksums (SegmentedRaftLogReader.decodeEntry, batched over a segment) ---------------
   /**
-   * PCIe-inclusive verification of one segment image held in a direct buffer: every frame's
-   * PureJavaCrc32C (crcOut) and the mismatch bitmap (badBits); returns the number of mismatches.
+   * PCIe-inclusive verification of the frames of one segment image held in a direct buffer (from
+   * its position to its limit): every frame's PureJavaCrc32C (crcOut, optional) and the mismatch
+   * bitmap (badBits, optional); returns the number of mismatches.
    */
   public long verifyFrames(int shard, ByteBuffer segment, long[] frameOff, int[] frameLen, int[] crcOut,
       long[] badBits) throws IOException {
-    return verifyHost0(node, shard, segment, segment.remaining(), frameOff, frameLen, frameOff.length, crcOut, badBits);
+    checkShard(shard);
+    if (!segment.isDirect()) {
+      throw new IllegalArgumentException("verifyFrames needs a direct buffer");
+    }
+    final int n = frameOff.length;
+    checkLength("frameLen", frameLen.length, n);
+    if (crcOut != null) {
+      checkLength("crcOut", crcOut.length, n);
+    }
+    if (badBits != null) {
+      checkLength("badBits", badBits.length, (n + 63) / 64);
+    }
+    return verifyHost0(node, shard, segment, segment.position(), segment.remaining(), frameOff, frameLen, n, crcOut,
+        badBits);
   }
 
   @Override
@@ -157,6 +247,15 @@ public final class RatisHip implements AutoCloseable {
       node = 0;
     }
   }
+
+  // ---- a bare context for the log read path (HipLogReader) -----------------------------------
+  static native long ctxCreate0(int device) throws IOException;
+  static native void ctxDestroy0(long ctx) throws IOException;
+  /** rh_segments_read_host over image[0, imageLen) of a direct buffer; per segment s:
+   * segInts[3s..3s+2] = status, n_ok, n_frames; segLongs[2s..2s+1] = stop, first_frame. */
+  static native long readSegments0(long ctx, ByteBuffer image, long imageLen, long[] segOff, long[] segLen, int nSeg,
+      int maxOp, int capPerSeg, long[] frameOff, int[] frameLen, int[] frameCrc, int[] segInts, long[] segLongs)
+      throws IOException;
 
   private static native long nodeCreate0(int deviceMask, long capacityPerShard, long gap) throws IOException;
   private static native void nodeDestroy0(long node) throws IOException;
@@ -171,10 +270,15 @@ public final class RatisHip implements AutoCloseable {
   private static native void submit0(long node, int shard, int n) throws IOException;
   private static native long commitBatch0(long node, int[] advSlot, long[] advCommit, int[] wallSlot, long[] wallMin)
       throws IOException;
+  private static native long commitAsync0(long node, int shard, int flags) throws IOException;
+  private static native long commitWait0(long node, int shard, long ticket, int[] advSlot, long[] advCommit,
+      int[] wallSlot, long[] wallMin) throws IOException;
   private static native int watchLevels0(long node, int shard, int[] slot, long[] min, long[] majority, long[] max,
       boolean[] valid) throws IOException;
   private static native void leaseStart0(long node, int slot, long nowNanos, boolean enabled) throws IOException;
   private static native void leaseBatch0(long node, long nowNanos, long timeoutMs, long[] bits) throws IOException;
-  private static native long verifyHost0(long node, int shard, ByteBuffer seg, long len, long[] off, int[] flen,
-      int n, int[] crc, long[] bad) throws IOException;
+  private static native void leaseBatchShard0(long node, int shard, long nowNanos, long timeoutMs, long[] bits)
+      throws IOException;
+  private static native long verifyHost0(long node, int shard, ByteBuffer seg, long pos, long len, long[] off,
+      int[] flen, int n, int[] crc, long[] bad) throws IOException;
 }

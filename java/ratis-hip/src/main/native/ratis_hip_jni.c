@@ -10,7 +10,10 @@
  * is checked against the ABI header's prototypes.
  *
  * Error mapping: RH_E_INVAL / RH_E_RANGE -> IllegalArgumentException, other negative statuses ->
- * IOException, message = rh_last_error() (thread-local in the library).
+ * IOException, message = rh_last_error() (thread-local in the library).  Every array / buffer size
+ * is checked against the count the call will read or write before the library sees a pointer
+ * (RatisHip.java checks the same on the Java side): a short array throws
+ * IllegalArgumentException, a null one where the call needs it too.
  */
 #include <jni.h>
 #include <stdint.h>
@@ -21,26 +24,42 @@
 
 #define CLS(name) Java_org_apache_ratis_hip_RatisHip_##name
 
-static void throw_rh(JNIEnv* env, int rc) {
-    const char* cls = (rc == RH_E_INVAL || rc == RH_E_RANGE) ? "java/lang/IllegalArgumentException"
-                                                             : "java/io/IOException";
+static void throw_msg(JNIEnv* env, const char* cls, const char* msg) {
     jclass c = (*env)->FindClass(env, cls);
-    if (c) (*env)->ThrowNew(env, c, rh_last_error());
+    if (c) (*env)->ThrowNew(env, c, msg);
 }
+
+static void throw_rh(JNIEnv* env, int rc) {
+    throw_msg(env, (rc == RH_E_INVAL || rc == RH_E_RANGE) ? "java/lang/IllegalArgumentException" : "java/io/IOException",
+              rh_last_error());
+}
+
+static void throw_arg(JNIEnv* env, const char* msg) { throw_msg(env, "java/lang/IllegalArgumentException", msg); }
 
 static int check(JNIEnv* env, int rc) {
     if (rc < 0) throw_rh(env, rc);
     return rc;
 }
 
+/* 1 when `a` is non-null and holds at least `need` elements, else throws and returns 0. */
+static int has_len(JNIEnv* env, jarray a, int64_t need, const char* what) {
+    if (!a) {
+        throw_arg(env, what);
+        return 0;
+    }
+    if ((int64_t)(*env)->GetArrayLength(env, a) < need) {
+        throw_arg(env, what);
+        return 0;
+    }
+    return 1;
+}
+
 static rh_node* N(jlong h) { return (rh_node*)(intptr_t)h; }
+static rh_ctx* C(jlong h) { return (rh_ctx*)(intptr_t)h; }
 
 static rh_groups* shard_table(JNIEnv* env, jlong node, jint shard) {
     rh_groups* g = rh_node_groups(N(node), (int)shard);
-    if (!g) {
-        jclass c = (*env)->FindClass(env, "java/lang/IllegalArgumentException");
-        if (c) (*env)->ThrowNew(env, c, "no such shard");
-    }
+    if (!g) throw_arg(env, "no such shard");
     return g;
 }
 
@@ -78,10 +97,8 @@ JNIEXPORT void JNICALL CLS(groupReconf0)(JNIEnv* env, jclass c, jlong node, jint
     int8_t map[RH_MAX_FOLLOWERS];
     const int8_t* p = NULL;
     if (src) {
-        const jsize n = (*env)->GetArrayLength(env, src);
-        for (int k = 0; k < (int)RH_MAX_FOLLOWERS; ++k) map[k] = -1;
-        (*env)->GetByteArrayRegion(env, src, 0, n < (jsize)RH_MAX_FOLLOWERS ? n : (jsize)RH_MAX_FOLLOWERS,
-                                   (jbyte*)map);
+        if (!has_len(env, src, RH_MAX_FOLLOWERS, "src must hold 14 entries")) return;
+        (*env)->GetByteArrayRegion(env, src, 0, (jsize)RH_MAX_FOLLOWERS, (jbyte*)map);
         p = map;
     }
     check(env, rh_node_group_reconf(N(node), (uint32_t)slot, (uint32_t)conf, p));
@@ -94,9 +111,15 @@ JNIEXPORT void JNICALL CLS(groupStop0)(JNIEnv* env, jclass c, jlong node, jint s
 
 JNIEXPORT void JNICALL CLS(pushDeltas0)(JNIEnv* env, jclass c, jlong node, jobject direct, jint n) {
     (void)c;
-    const rh_delta* d = (const rh_delta*)(*env)->GetDirectBufferAddress(env, direct);
-    if (!d && n) {
-        throw_rh(env, RH_E_INVAL);
+    if (n < 0) {
+        throw_arg(env, "negative delta count");
+        return;
+    }
+    if (n == 0) return;
+    const rh_delta* d = direct ? (const rh_delta*)(*env)->GetDirectBufferAddress(env, direct) : NULL;
+    const jlong capb = direct ? (*env)->GetDirectBufferCapacity(env, direct) : -1;
+    if (!d || capb < 0 || (int64_t)n > capb / (jlong)sizeof(rh_delta)) {
+        throw_arg(env, "pushDeltas: not a direct buffer, or n deltas exceed its capacity");
         return;
     }
     check(env, rh_node_push_deltas(N(node), d, (size_t)n));
@@ -114,15 +137,39 @@ JNIEXPORT jobject JNICALL CLS(acquire0)(JNIEnv* env, jclass c, jlong node, jint 
 
 JNIEXPORT void JNICALL CLS(submit0)(JNIEnv* env, jclass c, jlong node, jint shard, jint n) {
     (void)c;
+    if (n < 0 || (uint64_t)n > RH_DELTA_SLOT) {
+        throw_arg(env, "submit: n outside [0, RH_DELTA_SLOT]");
+        return;
+    }
     rh_groups* g = shard_table(env, node, shard);
     if (g) check(env, rh_deltas_submit(g, (size_t)n));
+}
+
+/* Copies k events into (slot, value) arrays. */
+static void put_events(JNIEnv* env, const rh_index_event* ev, jsize k, jintArray slot, jlongArray value, jint base) {
+    if (k <= 0) return;
+    jint* s = (*env)->GetPrimitiveArrayCritical(env, slot, NULL);
+    jlong* v = s ? (*env)->GetPrimitiveArrayCritical(env, value, NULL) : NULL;
+    if (s && v)
+        for (jsize i = 0; i < k; ++i) {
+            s[i] = (jint)ev[i].slot + base;
+            v[i] = (jlong)ev[i].value;
+        }
+    if (v) (*env)->ReleasePrimitiveArrayCritical(env, value, v, 0);
+    if (s) (*env)->ReleasePrimitiveArrayCritical(env, slot, s, 0);
 }
 
 JNIEXPORT jlong JNICALL CLS(commitBatch0)(JNIEnv* env, jclass c, jlong node, jintArray adv_slot,
                                           jlongArray adv_commit, jintArray wall_slot, jlongArray wall_min) {
     (void)c;
-    const jsize acap = adv_slot ? (*env)->GetArrayLength(env, adv_slot) : 0;
+    if (!adv_slot) {
+        throw_arg(env, "advSlot == null");
+        return 0;
+    }
+    const jsize acap = (*env)->GetArrayLength(env, adv_slot);
     const jsize wcap = wall_slot ? (*env)->GetArrayLength(env, wall_slot) : 0;
+    if (!has_len(env, adv_commit, acap, "advCommit shorter than advSlot")) return 0;
+    if (wall_slot && !has_len(env, wall_min, wcap, "wallMin shorter than wallSlot")) return 0;
     rh_index_event* adv = (rh_index_event*)malloc(sizeof(rh_index_event) * (size_t)(acap ? acap : 1));
     rh_index_event* wall = (rh_index_event*)malloc(sizeof(rh_index_event) * (size_t)(wcap ? wcap : 1));
     uint64_t na = 0, nw = 0;
@@ -130,29 +177,43 @@ JNIEXPORT jlong JNICALL CLS(commitBatch0)(JNIEnv* env, jclass c, jlong node, jin
     int rc = (adv && wall) ? rh_node_commit_batch(N(node), flags, adv, (uint64_t)acap, &na, wall, (uint64_t)wcap, &nw)
                            : RH_E_NOMEM;
     if (rc >= 0) {
-        const jsize ka = (jsize)(na < (uint64_t)acap ? na : (uint64_t)acap);
-        const jsize kw = (jsize)(nw < (uint64_t)wcap ? nw : (uint64_t)wcap);
-        jint* s = ka ? (*env)->GetPrimitiveArrayCritical(env, adv_slot, NULL) : NULL;
-        jlong* v = ka ? (*env)->GetPrimitiveArrayCritical(env, adv_commit, NULL) : NULL;
-        for (jsize i = 0; i < ka; ++i) {
-            s[i] = (jint)adv[i].slot;
-            v[i] = (jlong)adv[i].value;
-        }
-        if (v) (*env)->ReleasePrimitiveArrayCritical(env, adv_commit, v, 0);
-        if (s) (*env)->ReleasePrimitiveArrayCritical(env, adv_slot, s, 0);
-        s = kw ? (*env)->GetPrimitiveArrayCritical(env, wall_slot, NULL) : NULL;
-        v = kw ? (*env)->GetPrimitiveArrayCritical(env, wall_min, NULL) : NULL;
-        for (jsize i = 0; i < kw; ++i) {
-            s[i] = (jint)wall[i].slot;
-            v[i] = (jlong)wall[i].value;
-        }
-        if (v) (*env)->ReleasePrimitiveArrayCritical(env, wall_min, v, 0);
-        if (s) (*env)->ReleasePrimitiveArrayCritical(env, wall_slot, s, 0);
+        put_events(env, adv, (jsize)(na < (uint64_t)acap ? na : (uint64_t)acap), adv_slot, adv_commit, 0);
+        if (wall_slot) put_events(env, wall, (jsize)(nw < (uint64_t)wcap ? nw : (uint64_t)wcap), wall_slot, wall_min, 0);
     }
     free(adv);
     free(wall);
     if (check(env, rc) < 0) return 0;
     return (jlong)((na << 32) | (nw & 0xFFFFFFFFull));
+}
+
+JNIEXPORT jlong JNICALL CLS(commitAsync0)(JNIEnv* env, jclass c, jlong node, jint shard, jint flags) {
+    (void)c;
+    rh_groups* g = shard_table(env, node, shard);
+    if (!g) return 0;
+    uint64_t tk = 0;
+    if (check(env, rh_commit_batch_async(g, (uint32_t)flags, &tk)) < 0) return 0;
+    return (jlong)tk;
+}
+
+/* The shard's events straight from the library's pinned result buffers into the caller's arrays
+ * (slots within the shard); the arrays hold at least the shard capacity (checked in RatisHip). */
+JNIEXPORT jlong JNICALL CLS(commitWait0)(JNIEnv* env, jclass c, jlong node, jint shard, jlong ticket,
+                                         jintArray adv_slot, jlongArray adv_commit, jintArray wall_slot,
+                                         jlongArray wall_min) {
+    (void)c;
+    rh_groups* g = shard_table(env, node, shard);
+    if (!g) return 0;
+    rh_commit_out o;
+    memset(&o, 0, sizeof(o));
+    if (check(env, rh_commit_batch_wait(g, (uint64_t)ticket, &o)) < 0) return 0;
+    if (!has_len(env, adv_slot, (int64_t)o.n_advanced, "advSlot shorter than the events") ||
+        !has_len(env, adv_commit, (int64_t)o.n_advanced, "advCommit shorter than the events") ||
+        !has_len(env, wall_slot, (int64_t)o.n_watch_all, "wallSlot shorter than the events") ||
+        !has_len(env, wall_min, (int64_t)o.n_watch_all, "wallMin shorter than the events"))
+        return 0;
+    put_events(env, o.advanced, (jsize)o.n_advanced, adv_slot, adv_commit, 0);
+    put_events(env, o.watch_all, (jsize)o.n_watch_all, wall_slot, wall_min, 0);
+    return (jlong)((o.n_advanced << 32) | (o.n_watch_all & 0xFFFFFFFFull));
 }
 
 JNIEXPORT jint JNICALL CLS(watchLevels0)(JNIEnv* env, jclass c, jlong node, jint shard, jintArray slot,
@@ -163,18 +224,31 @@ JNIEXPORT jint JNICALL CLS(watchLevels0)(JNIEnv* env, jclass c, jlong node, jint
     const rh_watch_event* ev = NULL;
     uint64_t n = 0;
     if (check(env, rh_watch_levels(g, &ev, &n)) < 0) return 0;
-    const jsize cap = (*env)->GetArrayLength(env, slot);
-    const jsize k = (jsize)(n < (uint64_t)cap ? n : (uint64_t)cap);
-    for (jsize i = 0; i < k; ++i) {
-        const jint s = (jint)ev[i].slot;
-        const jlong a = (jlong)ev[i].min, b = (jlong)ev[i].majority, d = (jlong)ev[i].max;
-        const jboolean v = ev[i].valid ? JNI_TRUE : JNI_FALSE;
-        (*env)->SetIntArrayRegion(env, slot, i, 1, &s);
-        (*env)->SetLongArrayRegion(env, mn, i, 1, &a);
-        (*env)->SetLongArrayRegion(env, mj, i, 1, &b);
-        (*env)->SetLongArrayRegion(env, mx, i, 1, &d);
-        (*env)->SetBooleanArrayRegion(env, valid, i, 1, &v);
-    }
+    if (!has_len(env, slot, (int64_t)n, "slot shorter than the events") ||
+        !has_len(env, mn, (int64_t)n, "min shorter than the events") ||
+        !has_len(env, mj, (int64_t)n, "majority shorter than the events") ||
+        !has_len(env, mx, (int64_t)n, "max shorter than the events") ||
+        !has_len(env, valid, (int64_t)n, "valid shorter than the events"))
+        return 0;
+    if (n == 0) return 0;
+    jint* s = (*env)->GetPrimitiveArrayCritical(env, slot, NULL);
+    jlong* a = s ? (*env)->GetPrimitiveArrayCritical(env, mn, NULL) : NULL;
+    jlong* b = a ? (*env)->GetPrimitiveArrayCritical(env, mj, NULL) : NULL;
+    jlong* d = b ? (*env)->GetPrimitiveArrayCritical(env, mx, NULL) : NULL;
+    jboolean* v = d ? (*env)->GetPrimitiveArrayCritical(env, valid, NULL) : NULL;
+    if (v)
+        for (uint64_t i = 0; i < n; ++i) {
+            s[i] = (jint)ev[i].slot;
+            a[i] = (jlong)ev[i].min;
+            b[i] = (jlong)ev[i].majority;
+            d[i] = (jlong)ev[i].max;
+            v[i] = ev[i].valid ? JNI_TRUE : JNI_FALSE;
+        }
+    if (v) (*env)->ReleasePrimitiveArrayCritical(env, valid, v, 0);
+    if (d) (*env)->ReleasePrimitiveArrayCritical(env, mx, d, 0);
+    if (b) (*env)->ReleasePrimitiveArrayCritical(env, mj, b, 0);
+    if (a) (*env)->ReleasePrimitiveArrayCritical(env, mn, a, 0);
+    if (s) (*env)->ReleasePrimitiveArrayCritical(env, slot, s, 0);
     return (jint)n;
 }
 
@@ -186,6 +260,10 @@ JNIEXPORT void JNICALL CLS(leaseStart0)(JNIEnv* env, jclass c, jlong node, jint 
 JNIEXPORT void JNICALL CLS(leaseBatch0)(JNIEnv* env, jclass c, jlong node, jlong now, jlong timeout_ms,
                                         jlongArray bits) {
     (void)c;
+    if (!bits) {
+        throw_arg(env, "bits == null");
+        return;
+    }
     const jsize n = (*env)->GetArrayLength(env, bits);
     jlong* b = (*env)->GetLongArrayElements(env, bits, NULL);
     if (!b) return;
@@ -194,26 +272,116 @@ JNIEXPORT void JNICALL CLS(leaseBatch0)(JNIEnv* env, jclass c, jlong node, jlong
     check(env, rc);
 }
 
-JNIEXPORT jlong JNICALL CLS(verifyHost0)(JNIEnv* env, jclass c, jlong node, jint shard, jobject seg, jlong len,
-                                         jlongArray off, jintArray flen, jint n, jintArray crc, jlongArray bad) {
+JNIEXPORT void JNICALL CLS(leaseBatchShard0)(JNIEnv* env, jclass c, jlong node, jint shard, jlong now,
+                                             jlong timeout_ms, jlongArray bits) {
+    (void)c;
+    rh_groups* g = shard_table(env, node, shard);
+    if (!g) return;
+    const uint64_t* w = NULL;
+    uint64_t words = 0;
+    if (check(env, rh_lease_batch(g, (int64_t)now, (int64_t)timeout_ms, &w, &words)) < 0) return;
+    if (!has_len(env, bits, (int64_t)words, "bits shorter than the shard bitmap")) return;
+    (*env)->SetLongArrayRegion(env, bits, 0, (jsize)words, (const jlong*)w);
+}
+
+JNIEXPORT jlong JNICALL CLS(verifyHost0)(JNIEnv* env, jclass c, jlong node, jint shard, jobject seg, jlong pos,
+                                         jlong len, jlongArray off, jintArray flen, jint n, jintArray crc,
+                                         jlongArray bad) {
     (void)c;
     rh_ctx* ctx = rh_node_ctx(N(node), (int)shard);
-    const uint8_t* p = (const uint8_t*)(*env)->GetDirectBufferAddress(env, seg);
-    if (!ctx || (!p && len)) {
-        throw_rh(env, RH_E_INVAL);
+    const uint8_t* base = seg ? (const uint8_t*)(*env)->GetDirectBufferAddress(env, seg) : NULL;
+    const jlong capb = seg ? (*env)->GetDirectBufferCapacity(env, seg) : -1;
+    if (!ctx || !base || pos < 0 || len < 0 || capb < 0 || pos > capb || len > capb - pos || n < 0) {
+        throw_arg(env, "verifyFrames: no such shard, not a direct buffer, or [position, limit) outside it");
         return 0;
     }
+    if (!has_len(env, off, n, "frameOff shorter than n") || !has_len(env, flen, n, "frameLen shorter than n") ||
+        (crc && !has_len(env, crc, n, "crcOut shorter than n")) ||
+        (bad && !has_len(env, bad, ((int64_t)n + 63) / 64, "badBits shorter than ceil(n / 64)")))
+        return 0;
     jlong* o = (*env)->GetLongArrayElements(env, off, NULL);
     jint* l = (*env)->GetIntArrayElements(env, flen, NULL);
     jint* cr = crc ? (*env)->GetIntArrayElements(env, crc, NULL) : NULL;
     jlong* b = bad ? (*env)->GetLongArrayElements(env, bad, NULL) : NULL;
     uint64_t nb = 0;
-    const int rc = rh_crc32c_verify_host(ctx, p, (uint64_t)len, (const uint64_t*)o, (const uint32_t*)l, (uint64_t)n,
-                                         (uint32_t*)cr, (uint64_t*)b, &nb);
+    const int rc = rh_crc32c_verify_host(ctx, base + pos, (uint64_t)len, (const uint64_t*)o, (const uint32_t*)l,
+                                         (uint64_t)n, (uint32_t*)cr, (uint64_t*)b, &nb);
     if (b) (*env)->ReleaseLongArrayElements(env, bad, b, 0);
     if (cr) (*env)->ReleaseIntArrayElements(env, crc, cr, 0);
     (*env)->ReleaseIntArrayElements(env, flen, l, JNI_ABORT);
     (*env)->ReleaseLongArrayElements(env, off, o, JNI_ABORT);
     if (check(env, rc) < 0) return 0;
     return (jlong)nb;
+}
+
+/* ---- the log read path (HipLogReader) -------------------------------------------------------- */
+JNIEXPORT jlong JNICALL CLS(ctxCreate0)(JNIEnv* env, jclass c, jint device) {
+    (void)c;
+    rh_ctx* ctx = NULL;
+    if (check(env, rh_init((int)device, &ctx)) < 0) return 0;
+    return (jlong)(intptr_t)ctx;
+}
+
+JNIEXPORT void JNICALL CLS(ctxDestroy0)(JNIEnv* env, jclass c, jlong ctx) {
+    (void)c;
+    check(env, rh_shutdown(C(ctx)));
+}
+
+JNIEXPORT jlong JNICALL CLS(readSegments0)(JNIEnv* env, jclass c, jlong ctx, jobject image, jlong image_len,
+                                           jlongArray seg_off, jlongArray seg_len, jint n_seg, jint max_op,
+                                           jint cap_per_seg, jlongArray frame_off, jintArray frame_len,
+                                           jintArray frame_crc, jintArray seg_ints, jlongArray seg_longs) {
+    (void)c;
+    const uint8_t* img = image ? (const uint8_t*)(*env)->GetDirectBufferAddress(env, image) : NULL;
+    const jlong capb = image ? (*env)->GetDirectBufferCapacity(env, image) : -1;
+    if (!img || image_len < 0 || capb < image_len || n_seg < 0 || max_op <= 0 || cap_per_seg <= 0) {
+        throw_arg(env, "readSegments: not a direct buffer, imageLen beyond it, or a bad count");
+        return 0;
+    }
+    if (!has_len(env, seg_off, n_seg, "segOff shorter than nSeg") || !has_len(env, seg_len, n_seg, "segLen shorter than nSeg") ||
+        !has_len(env, seg_ints, 3 * (int64_t)n_seg, "segInts shorter than 3 * nSeg") ||
+        !has_len(env, seg_longs, 2 * (int64_t)n_seg, "segLongs shorter than 2 * nSeg") || !frame_off || !frame_len) {
+        if (!(*env)->ExceptionCheck(env)) throw_arg(env, "frameOff / frameLen == null");
+        return 0;
+    }
+    const jsize fcap = (*env)->GetArrayLength(env, frame_off);
+    if (!has_len(env, frame_len, fcap, "frameLen shorter than frameOff") ||
+        (frame_crc && !has_len(env, frame_crc, fcap, "frameCrc shorter than frameOff")))
+        return 0;
+    rh_segment_result* res = (rh_segment_result*)calloc((size_t)(n_seg ? n_seg : 1), sizeof(rh_segment_result));
+    if (!res) {
+        throw_msg(env, "java/lang/OutOfMemoryError", "readSegments: results");
+        return 0;
+    }
+    jlong* so = (*env)->GetLongArrayElements(env, seg_off, NULL);
+    jlong* sl = (*env)->GetLongArrayElements(env, seg_len, NULL);
+    jlong* fo = (*env)->GetLongArrayElements(env, frame_off, NULL);
+    jint* fl = (*env)->GetIntArrayElements(env, frame_len, NULL);
+    jint* fc = frame_crc ? (*env)->GetIntArrayElements(env, frame_crc, NULL) : NULL;
+    uint64_t total = 0;
+    const int rc = rh_segments_read_host(C(ctx), img, (uint64_t)image_len, (const uint64_t*)so, (const uint64_t*)sl,
+                                         (uint64_t)n_seg, (uint32_t)max_op, (uint32_t)cap_per_seg, (uint64_t*)fo,
+                                         (uint32_t*)fl, (uint32_t*)fc, (uint64_t)fcap, res, &total);
+    if (fc) (*env)->ReleaseIntArrayElements(env, frame_crc, fc, rc < 0 ? JNI_ABORT : 0);
+    (*env)->ReleaseIntArrayElements(env, frame_len, fl, rc < 0 ? JNI_ABORT : 0);
+    (*env)->ReleaseLongArrayElements(env, frame_off, fo, rc < 0 ? JNI_ABORT : 0);
+    (*env)->ReleaseLongArrayElements(env, seg_len, sl, JNI_ABORT);
+    (*env)->ReleaseLongArrayElements(env, seg_off, so, JNI_ABORT);
+    if (rc >= 0) {
+        jint* si = (*env)->GetIntArrayElements(env, seg_ints, NULL);
+        jlong* sg = (*env)->GetLongArrayElements(env, seg_longs, NULL);
+        if (si && sg)
+            for (jint s = 0; s < n_seg; ++s) {
+                si[3 * s] = (jint)res[s].status;
+                si[3 * s + 1] = (jint)res[s].n_ok;
+                si[3 * s + 2] = (jint)res[s].n_frames;
+                sg[2 * s] = (jlong)res[s].stop;
+                sg[2 * s + 1] = (jlong)res[s].first_frame;
+            }
+        if (sg) (*env)->ReleaseLongArrayElements(env, seg_longs, sg, 0);
+        if (si) (*env)->ReleaseIntArrayElements(env, seg_ints, si, 0);
+    }
+    free(res);
+    if (check(env, rc) < 0) return 0;
+    return (jlong)total;
 }

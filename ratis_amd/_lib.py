@@ -48,6 +48,8 @@ RH_OP_MAX = 0
 RH_OP_SET = 1
 RH_DELTA_SLOT = 1 << 20
 RH_COMMIT_WATCH_ALL = 1
+RH_EVENTS_HOST_MAPPED = 0
+RH_EVENTS_DEVICE = 1
 
 RH_CRC_VERIFY = 1
 RH_CRC_STAMP = 2
@@ -194,6 +196,11 @@ class RhSegmentsCrc(ctypes.Structure):
     ]
 
 
+class RhSegmentResult(ctypes.Structure):
+    _fields_ = [("status", c_int32), ("n_ok", c_uint32), ("stop", c_uint64), ("first_frame", c_uint64),
+                ("n_frames", c_uint32), ("reserved", c_uint32)]
+
+
 # name -> (restype, argtypes); every function declared in include/ratis_hip.h
 _SIGNATURES = {
     "rh_abi_version": (c_int, []),
@@ -206,6 +213,7 @@ _SIGNATURES = {
     "rh_commit_soa_launch": (c_int, [c_void_p, POINTER(RhCommitSoa), c_int, c_void_p]),
     "rh_groups_create": (c_int, [c_void_p, c_uint64, c_int64, POINTER(c_void_p)]),
     "rh_groups_destroy": (c_int, [c_void_p]),
+    "rh_groups_set_event_sink": (c_int, [c_void_p, c_int]),
     "rh_group_start": (c_int, [c_void_p, c_uint32, c_uint32, c_int64, c_int64, c_int64]),
     "rh_group_reconf": (c_int, [c_void_p, c_uint32, c_uint32, c_void_p]),
     "rh_group_stop": (c_int, [c_void_p, c_uint32]),
@@ -226,6 +234,7 @@ _SIGNATURES = {
     "rh_groups_read": (c_int, [c_void_p, c_uint32, c_uint32, ctypes.c_uint8, c_void_p]),
     "rh_shard_of": (c_int, [c_uint64, c_uint64, c_int]),
     "rh_node_create": (c_int, [c_uint32, c_uint64, c_int64, POINTER(c_void_p)]),
+    "rh_node_create_devices": (c_int, [POINTER(c_int), c_int, c_uint64, c_int64, POINTER(c_void_p)]),
     "rh_node_destroy": (c_int, [c_void_p]),
     "rh_node_shards": (c_int, [c_void_p]),
     "rh_node_groups": (c_void_p, [c_void_p, c_int]),
@@ -244,6 +253,9 @@ _SIGNATURES = {
     "rh_leader_soa_launch": (c_int, [c_void_p, POINTER(RhCommitSoa), c_int, POINTER(RhLeaseSoa), c_int, c_void_p]),
     "rh_segments_scan_launch": (c_int, [c_void_p, POINTER(RhSegments), c_void_p]),
     "rh_segments_read_launch": (c_int, [c_void_p, POINTER(RhSegments), POINTER(RhSegmentsCrc), c_void_p]),
+    "rh_segments_read_host": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_uint64, c_uint32, c_uint32,
+                                      c_void_p, c_void_p, c_void_p, c_uint64, POINTER(RhSegmentResult),
+                                      POINTER(c_uint64)]),
 }
 
 

@@ -914,9 +914,9 @@ int launch_frames(rh_ctx* ctx, FrameArgs a, hipStream_t stream, bool* dense_writ
     if (dense_written) *dense_written = a.seg_first != nullptr;
     // scratch: counts[kClasses], cursor[kClasses], rec[n], widx[n]
     const size_t o_rec = 1024, o_widx = o_rec + (size_t)a.n * sizeof(LaneRec), bytes = o_widx + (size_t)a.n * 4;
-    void* scratch = nullptr;
-    RH_HIP(rh::pool_alloc(ctx, &scratch, bytes, stream));
-    uint8_t* sb = static_cast<uint8_t*>(scratch);
+    rh::PoolScratch scratch(stream);  // released on every exit path
+    RH_HIP(scratch.alloc(ctx, bytes));
+    uint8_t* sb = scratch.bytes();
     uint32_t* counts = reinterpret_cast<uint32_t*>(sb);
     uint32_t* cursor = counts + kClasses;
     LaneRec* rec = reinterpret_cast<LaneRec*>(sb + o_rec);
@@ -964,7 +964,6 @@ int launch_frames(rh_ctx* ctx, FrameArgs a, hipStream_t stream, bool* dense_writ
     const uint64_t wgrid = (a.n + kBL - 1) / kBL < cus ? (a.n + kBL - 1) / kBL : cus;
     hipLaunchKernelGGL(crc_frames_kernel<true>, dim3((uint32_t)wgrid), dim3(kCrcThreads), kCrcLdsOf(true), stream, a);
     RH_HIP(hipGetLastError());
-    RH_HIP(hipFreeAsync(scratch, stream));
     return RH_OK;
 }
 

@@ -52,10 +52,16 @@ struct EvSet {
     rh_index_event* wall = nullptr;
     rh_index_event* d_adv = nullptr;  // device views of the same memory
     rh_index_event* d_wall = nullptr;
-    unsigned long long* h_counts = nullptr;  // pinned [4]
+    rh_index_event* hbm_adv = nullptr;   // RH_EVENTS_DEVICE: the kernel's sink in HBM
+    rh_index_event* hbm_wall = nullptr;
+    uint64_t* h_bend = nullptr;      // host-mapped per-workgroup list ends (TableEvents::block_end)
+    uint64_t* d_bend = nullptr;
+    uint32_t bend_cap = 0;
+    uint32_t blocks = 0;             // entries of h_bend the pending evaluation writes
     hipEvent_t done = nullptr;
     uint64_t ticket = 0;
     bool pending = false;
+    bool hbm = false;   // this ticket's events are in hbm_adv / hbm_wall (copied out by _wait)
 };
 
 }  // namespace
@@ -93,9 +99,15 @@ struct rh_groups {
     // events
     EvSet ev[kEvSets];
     uint64_t next_ticket = 1;
-    unsigned long long* d_counts = nullptr;   // [kEvSets][4], then one for rh_watch_levels
+    unsigned long long* d_counts = nullptr;   // [2 modes][2]: alternating list counters (TableEvents)
+    int cpar[2] = {0, 0};                     // which word of each mode the next evaluation counts into
+    uint64_t* h_wbend = nullptr;              // rh_watch_levels' per-workgroup list ends
+    uint64_t* d_wbend = nullptr;
+    uint32_t wbend_cap = 0;
     rh_watch_event* watch = nullptr;          // host-mapped pinned [cap]
     rh_watch_event* d_watch = nullptr;
+    rh_watch_event* hbm_watch = nullptr;      // RH_EVENTS_DEVICE
+    int event_sink = RH_EVENTS_HOST_MAPPED;
     int64_t* d_read = nullptr;
     size_t read_cap = 0;
 };
@@ -145,9 +157,13 @@ void free_groups(rh_groups* g) {
     for (int i = 0; i < kEvSets; ++i) {
         if (g->ev[i].adv) (void)hipHostFree(g->ev[i].adv);
         if (g->ev[i].wall) (void)hipHostFree(g->ev[i].wall);
-        if (g->ev[i].h_counts) (void)hipHostFree(g->ev[i].h_counts);
+        if (g->ev[i].h_bend) (void)hipHostFree(g->ev[i].h_bend);
         if (g->ev[i].done) (void)hipEventDestroy(g->ev[i].done);
+        (void)hipFree(g->ev[i].hbm_adv);
+        (void)hipFree(g->ev[i].hbm_wall);
     }
+    (void)hipFree(g->hbm_watch);
+    if (g->h_wbend) (void)hipHostFree(g->h_wbend);
     (void)hipFree(g->d_counts);
     if (g->watch) (void)hipHostFree(g->watch);
     (void)hipFree(g->d_read);
@@ -298,6 +314,33 @@ int queue_op(rh_groups* g, const CtrlOp& op) {
 
 uint32_t enc(int t, uint32_t row) { return ((uint32_t)t << 28) | row; }
 
+// A host-mapped, zeroed array of at least `need` per-workgroup list ends (TableEvents::block_end).
+int ensure_bend(uint64_t** h, uint64_t** d, uint32_t* cap, uint32_t need) {
+    if (need <= *cap) return RH_OK;
+    if (*h) (void)hipHostFree(*h);
+    *h = *d = nullptr;
+    *cap = 0;
+    const uint32_t n = std::max<uint32_t>(need, 256);
+    int rc = halloc_mapped(h, d, n);
+    if (rc != RH_OK) return rc;
+    std::memset(*h, 0, (size_t)n * 8);
+    *cap = n;
+    return RH_OK;
+}
+
+// List lengths of an evaluation from its workgroups' range ends; the entries are cleared for reuse.
+void take_counts(uint64_t* bend, uint32_t blocks, uint64_t* n0, uint64_t* n1) {
+    uint64_t a = 0, b = 0;
+    for (uint32_t i = 0; i < blocks; ++i) {
+        const uint64_t x = bend[i];
+        a = std::max<uint64_t>(a, x & 0xFFFFFFFFull);
+        b = std::max<uint64_t>(b, x >> 32);
+        bend[i] = 0;
+    }
+    *n0 = a;
+    *n1 = b;
+}
+
 int do_stop(rh_groups* g, uint32_t slot) {
     const uint32_t m = g->slot_map[slot];
     if (m == kNoRow) return RH_OK;
@@ -389,13 +432,13 @@ RH_EXPORT int rh_groups_create(rh_ctx* ctx, uint64_t capacity, int64_t gap_thres
     for (int i = 0; i < kEvSets && rc == RH_OK; ++i) {
         if (rc == RH_OK) rc = halloc_mapped(&g->ev[i].adv, &g->ev[i].d_adv, capacity);
         if (rc == RH_OK) rc = halloc_mapped(&g->ev[i].wall, &g->ev[i].d_wall, capacity);
-        if (rc == RH_OK && hipHostMalloc(reinterpret_cast<void**>(&g->ev[i].h_counts), 4 * sizeof(unsigned long long)) != hipSuccess)
-            rc = rh::fail(RH_E_NOMEM, "hipHostMalloc(event counters)");
         if (rc == RH_OK && hipEventCreateWithFlags(&g->ev[i].done, hipEventDisableTiming) != hipSuccess)
             rc = rh::fail(RH_E_DEVICE, "hipEventCreate(commit batch)");
     }
     if (rc == RH_OK) rc = halloc_mapped(&g->watch, &g->d_watch, capacity);
-    if (rc == RH_OK) rc = dalloc(&g->d_counts, 4 * kEvSets + 1);
+    if (rc == RH_OK) rc = dalloc(&g->d_counts, 4);
+    if (rc == RH_OK && hipMemsetAsync(g->d_counts, 0, 4 * sizeof(unsigned long long), s) != hipSuccess)
+        rc = rh::fail(RH_E_DEVICE, "rh_groups_create: counters");
     if (rc == RH_OK) rc = dalloc(&g->d_lbits, (capacity + 63) / 64);
     if (rc == RH_OK && hipHostMalloc(reinterpret_cast<void**>(&g->h_lbits), (capacity + 63) / 64 * 8) != hipSuccess)
         rc = rh::fail(RH_E_NOMEM, "hipHostMalloc(lease bitmap)");
@@ -418,6 +461,37 @@ RH_EXPORT int rh_groups_destroy(rh_groups* g) {
     if (g->copy_stream) (void)hipStreamSynchronize(g->copy_stream);
     free_groups(g);
     delete g;
+    return RH_OK;
+}
+
+RH_EXPORT int rh_groups_set_event_sink(rh_groups* g, int sink) {
+    if (!g) return rh::fail(RH_E_INVAL, "rh_groups_set_event_sink: groups == NULL");
+    if (sink != RH_EVENTS_HOST_MAPPED && sink != RH_EVENTS_DEVICE)
+        return rh::fail(RH_E_INVAL, "rh_groups_set_event_sink: unknown sink");
+    DeviceGuard dg(g->ctx->device);
+    std::lock_guard<std::mutex> lk(g->mu);
+    for (const EvSet& e : g->ev)
+        if (e.pending) return rh::fail(RH_E_STATE, "rh_groups_set_event_sink: an evaluation is in flight");
+    if (sink == RH_EVENTS_DEVICE && !g->hbm_watch) {  // allocated on first use, kept until destroy
+        int rc = RH_OK;
+        for (int i = 0; i < kEvSets && rc == RH_OK; ++i) {
+            rc = dalloc(&g->ev[i].hbm_adv, g->capacity);
+            if (rc == RH_OK) rc = dalloc(&g->ev[i].hbm_wall, g->capacity);
+        }
+        if (rc == RH_OK) rc = dalloc(&g->hbm_watch, g->capacity);
+        if (rc != RH_OK) {
+            for (EvSet& e : g->ev) {
+                (void)hipFree(e.hbm_adv);
+                (void)hipFree(e.hbm_wall);
+                e.hbm_adv = e.hbm_wall = nullptr;
+            }
+            (void)hipFree(g->hbm_watch);
+    if (g->h_wbend) (void)hipHostFree(g->h_wbend);
+            g->hbm_watch = nullptr;
+            return rc;
+        }
+    }
+    g->event_sink = sink;
     return RH_OK;
 }
 
@@ -709,18 +783,24 @@ RH_EXPORT int rh_commit_batch_async(rh_groups* g, uint32_t flags, uint64_t* tick
     hipStream_t s = g->ctx->stream;
     int rc = flush_ops(g);
     if (rc != RH_OK) return rc;
-    unsigned long long* dc = g->d_counts + (tk % kEvSets) * 4;
-    RH_HIP(hipMemsetAsync(dc, 0, 4 * sizeof(unsigned long long), s));
+    const uint32_t blocks = rh::table_commit_blocks(g->dev);
+    rc = ensure_bend(&e.h_bend, &e.d_bend, &e.bend_cap, blocks);
+    if (rc != RH_OK) return rc;
+    const bool hbm = g->event_sink == RH_EVENTS_DEVICE;
     rh::TableEvents ev;
-    ev.adv = e.d_adv;
-    ev.wall = (flags & RH_COMMIT_WATCH_ALL) ? e.d_wall : nullptr;
-    ev.counts = dc;
+    ev.adv = hbm ? e.hbm_adv : e.d_adv;
+    ev.wall = (flags & RH_COMMIT_WATCH_ALL) ? (hbm ? e.hbm_wall : e.d_wall) : nullptr;
+    ev.counts = g->d_counts + g->cpar[0];
+    ev.counts_next = g->d_counts + (g->cpar[0] ^ 1);
+    ev.block_end = e.d_bend;
     ev.cap = g->capacity;
     rc = rh_table_commit(g->dev, RH_MODE_COMMIT, ev, s);
     if (rc != RH_OK) return rc;
-    RH_HIP(hipMemcpyAsync(e.h_counts, dc, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    if (blocks) g->cpar[0] ^= 1;  // the launch cleared the other word
     RH_HIP(hipEventRecord(e.done, s));
     e.ticket = tk;
+    e.hbm = hbm;
+    e.blocks = blocks;
     e.pending = true;
     *ticket = tk;
     return RH_OK;
@@ -738,11 +818,23 @@ RH_EXPORT int rh_commit_batch_wait(rh_groups* g, uint64_t ticket, rh_commit_out*
     RH_HIP(hipEventSynchronize(e->done));
     std::lock_guard<std::mutex> lk(g->mu);
     if (e->ticket != ticket) return rh::fail(RH_E_STATE, "rh_commit_batch_wait: ticket superseded while waiting");
+    uint64_t na = 0, nw = 0;
+    take_counts(e->h_bend, e->blocks, &na, &nw);
+    e->blocks = 0;
+    na = std::min<uint64_t>(na, g->capacity);
+    nw = std::min<uint64_t>(nw, g->capacity);
+    if (e->hbm) {  // RH_EVENTS_DEVICE: the counted prefixes to the pinned result buffers
+        e->hbm = false;
+        hipStream_t s = g->copy_stream;
+        if (na) RH_HIP(hipMemcpyAsync(e->adv, e->hbm_adv, na * sizeof(rh_index_event), hipMemcpyDeviceToHost, s));
+        if (nw) RH_HIP(hipMemcpyAsync(e->wall, e->hbm_wall, nw * sizeof(rh_index_event), hipMemcpyDeviceToHost, s));
+        if (na || nw) RH_HIP(hipStreamSynchronize(s));
+    }
     e->pending = false;
     out->advanced = e->adv;
-    out->n_advanced = std::min<uint64_t>(e->h_counts[0], g->capacity);
+    out->n_advanced = na;
     out->watch_all = e->wall;
-    out->n_watch_all = std::min<uint64_t>(e->h_counts[1], g->capacity);
+    out->n_watch_all = nw;
     return RH_OK;
 }
 
@@ -760,19 +852,29 @@ RH_EXPORT int rh_watch_levels(rh_groups* g, const rh_watch_event** out_events, u
     hipStream_t s = g->ctx->stream;
     int rc = flush_ops(g);
     if (rc != RH_OK) return rc;
-    unsigned long long* dc = g->d_counts + 4 * kEvSets - 2;  // the WATCH kernel counts into dc[2]
-    RH_HIP(hipMemsetAsync(dc + 2, 0, sizeof(unsigned long long), s));
+    const uint32_t blocks = rh::table_commit_blocks(g->dev);
+    rc = ensure_bend(&g->h_wbend, &g->d_wbend, &g->wbend_cap, blocks);
+    if (rc != RH_OK) return rc;
+    const bool hbm = g->event_sink == RH_EVENTS_DEVICE;
     rh::TableEvents ev;
-    ev.watch = g->d_watch;
-    ev.counts = dc;
+    ev.watch = hbm ? g->hbm_watch : g->d_watch;
+    ev.counts = g->d_counts + 2 + g->cpar[1];
+    ev.counts_next = g->d_counts + 2 + (g->cpar[1] ^ 1);
+    ev.block_end = g->d_wbend;
     ev.cap = g->capacity;
     rc = rh_table_commit(g->dev, RH_MODE_WATCH, ev, s);
     if (rc != RH_OK) return rc;
-    unsigned long long cnt = 0;
-    RH_HIP(hipMemcpyAsync(&cnt, dc + 2, sizeof(cnt), hipMemcpyDeviceToHost, s));
+    if (blocks) g->cpar[1] ^= 1;
     RH_HIP(hipStreamSynchronize(s));
+    uint64_t n = 0, unused = 0;
+    take_counts(g->h_wbend, blocks, &n, &unused);
+    n = std::min<uint64_t>(n, g->capacity);
+    if (hbm && n) {
+        RH_HIP(hipMemcpyAsync(g->watch, g->hbm_watch, n * sizeof(rh_watch_event), hipMemcpyDeviceToHost, s));
+        RH_HIP(hipStreamSynchronize(s));
+    }
     *out_events = g->watch;
-    *out_n = std::min<uint64_t>(cnt, g->capacity);
+    *out_n = n;
     return RH_OK;
 }
 
@@ -851,6 +953,10 @@ struct rh_node {
     std::vector<rh_ctx*> ctx;
     std::vector<rh_groups*> tab;
     uint64_t cap = 0;
+    std::mutex push_mu;                        // guards `part` (reused by every push)
+    std::vector<std::vector<rh_delta>> part;   // per-shard partitions of one rh_node_push_deltas
+    std::mutex batch_mu;                       // guards `tickets`
+    std::vector<uint64_t> tickets;
 };
 
 RH_EXPORT int rh_shard_of(uint64_t msb, uint64_t lsb, int n_shards) {
@@ -861,20 +967,33 @@ RH_EXPORT int rh_shard_of(uint64_t msb, uint64_t lsb, int n_shards) {
     return r < 0 ? r + n_shards : r;
 }
 
-RH_EXPORT int rh_node_create(uint32_t device_mask, uint64_t capacity_per_shard, int64_t gap_threshold, rh_node** out) {
-    if (!out) return rh::fail(RH_E_INVAL, "rh_node_create: out == NULL");
+RH_EXPORT int rh_node_create_devices(const int* devices, int n_shards, uint64_t capacity_per_shard,
+                                     int64_t gap_threshold, rh_node** out) {
+    if (!out) return rh::fail(RH_E_INVAL, "rh_node_create_devices: out == NULL");
     *out = nullptr;
-    if (device_mask == 0) return rh::fail(RH_E_INVAL, "rh_node_create: empty device mask");
-    if (capacity_per_shard * (uint64_t)__builtin_popcount(device_mask) > 0xFFFFFFFFull)
-        return rh::fail(RH_E_RANGE, "rh_node_create: node slots must fit 32 bits");
+    if (!devices || n_shards < 1 || n_shards > 64)
+        return rh::fail(RH_E_INVAL, "rh_node_create_devices: need 1..64 devices");
+    if (capacity_per_shard * (uint64_t)n_shards > 0xFFFFFFFFull)
+        return rh::fail(RH_E_RANGE, "rh_node_create_devices: node slots must fit 32 bits");
+    int ndev = 0;
+    int rc = rh_device_count(&ndev);
+    if (rc != RH_OK) return rc;
+    for (int i = 0; i < n_shards; ++i)
+        if (devices[i] < 0 || devices[i] >= ndev)
+            return rh::fail(RH_E_INVAL, "rh_node_create_devices: no such device " + std::to_string(devices[i]));
     rh_node* nd = new (std::nothrow) rh_node();
-    if (!nd) return rh::fail(RH_E_NOMEM, "rh_node_create: out of host memory");
+    if (!nd) return rh::fail(RH_E_NOMEM, "rh_node_create_devices: out of host memory");
     nd->cap = capacity_per_shard;
-    int rc = RH_OK;
-    for (int d = 0; d < 32 && rc == RH_OK; ++d) {
-        if (!((device_mask >> d) & 1u)) continue;
+    try {
+        nd->part.resize((size_t)n_shards);
+        nd->tickets.resize((size_t)n_shards);
+    } catch (...) {
+        delete nd;
+        return rh::fail(RH_E_NOMEM, "rh_node_create_devices: out of host memory");
+    }
+    for (int i = 0; i < n_shards && rc == RH_OK; ++i) {
         rh_ctx* c = nullptr;
-        rc = rh_init(d, &c);
+        rc = rh_init(devices[i], &c);
         if (rc != RH_OK) break;
         nd->ctx.push_back(c);
         rh_groups* t = nullptr;
@@ -887,6 +1006,17 @@ RH_EXPORT int rh_node_create(uint32_t device_mask, uint64_t capacity_per_shard, 
     }
     *out = nd;
     return RH_OK;
+}
+
+RH_EXPORT int rh_node_create(uint32_t device_mask, uint64_t capacity_per_shard, int64_t gap_threshold, rh_node** out) {
+    if (!out) return rh::fail(RH_E_INVAL, "rh_node_create: out == NULL");
+    *out = nullptr;
+    if (device_mask == 0) return rh::fail(RH_E_INVAL, "rh_node_create: empty device mask");
+    int devs[32];
+    int n = 0;
+    for (int d = 0; d < 32; ++d)
+        if ((device_mask >> d) & 1u) devs[n++] = d;
+    return rh_node_create_devices(devs, n, capacity_per_shard, gap_threshold, out);
 }
 
 RH_EXPORT int rh_node_destroy(rh_node* nd) {
@@ -943,16 +1073,25 @@ RH_EXPORT int rh_node_group_stop(rh_node* nd, uint32_t node_slot) {
 RH_EXPORT int rh_node_push_deltas(rh_node* nd, const rh_delta* deltas, size_t n) {
     if (!nd || (n && !deltas)) return rh::fail(RH_E_INVAL, "rh_node_push_deltas: NULL argument");
     const size_t S = nd->tab.size();
-    std::vector<std::vector<rh_delta>> part(S);
-    for (size_t i = 0; i < n; ++i) {
-        const uint64_t sh = deltas[i].slot / nd->cap;
-        if (sh >= S) return rh::fail(RH_E_INVAL, "rh_node_push_deltas: delta " + std::to_string(i) + " has a bad slot");
-        rh_delta d = deltas[i];
-        d.slot = (uint32_t)(d.slot % nd->cap);
-        part[sh].push_back(d);
+    for (size_t i = 0; i < n; ++i)  // validate every delta before any shard receives one
+        if (deltas[i].slot / nd->cap >= S)
+            return rh::fail(RH_E_INVAL, "rh_node_push_deltas: delta " + std::to_string(i) + " has a bad slot");
+    if (S == 1) return rh_push_deltas(nd->tab[0], deltas, n);  // node slot == table slot
+    std::lock_guard<std::mutex> lk(nd->push_mu);
+    try {
+        for (auto& p : nd->part) p.clear();  // keeps the capacity: no allocation once warmed up
+        for (size_t i = 0; i < n; ++i) {
+            rh_delta d = deltas[i];
+            const uint64_t sh = d.slot / nd->cap;
+            d.slot = (uint32_t)(d.slot % nd->cap);
+            nd->part[sh].push_back(d);
+        }
+    } catch (...) {
+        return rh::fail(RH_E_NOMEM, "rh_node_push_deltas: out of host memory");
     }
     for (size_t sh = 0; sh < S; ++sh) {
-        int rc = rh_push_deltas(nd->tab[sh], part[sh].data(), part[sh].size());
+        if (nd->part[sh].empty()) continue;
+        int rc = rh_push_deltas(nd->tab[sh], nd->part[sh].data(), nd->part[sh].size());
         if (rc != RH_OK) return rc;
     }
     return RH_OK;
@@ -965,7 +1104,8 @@ RH_EXPORT int rh_node_commit_batch(rh_node* nd, uint32_t flags, rh_index_event* 
     if ((adv_cap && !advanced) || (watch_cap && !watch_all))
         return rh::fail(RH_E_INVAL, "rh_node_commit_batch: output arrays required");
     const size_t S = nd->tab.size();
-    std::vector<uint64_t> tk(S);
+    std::lock_guard<std::mutex> lk(nd->batch_mu);
+    std::vector<uint64_t>& tk = nd->tickets;
     for (size_t sh = 0; sh < S; ++sh) {  // every shard's evaluation is in flight before any wait
         int rc = rh_commit_batch_async(nd->tab[sh], flags, &tk[sh]);
         if (rc != RH_OK) return rc;

@@ -186,13 +186,13 @@ RH_EXPORT int rh_crc32c(rh_ctx* ctx, uint32_t crc_state, const void* data, uint6
     *out_state = crc_state;
     if (n == 0) return RH_OK;
     DeviceGuard g(ctx->device);
-    // per-call stream-ordered scratch from the context's pool: no shared buffer, no lock, so
-    // concurrent callers (Checksum.update from several threads) proceed independently
+    // per-call stream-ordered scratch from the context's pool (no shared staging buffer); the work
+    // is enqueued on the context stream, so concurrent callers are safe but run one after another
     const size_t o_len = (n + 255) / 256 * 256, total = o_len + 256;
     hipStream_t s = ctx->stream;
-    void* scratch = nullptr;
-    if (rh::pool_alloc(ctx, &scratch, total, s) != hipSuccess) return rh::fail(RH_E_NOMEM, "rh_crc32c: device scratch");
-    uint8_t* base = static_cast<uint8_t*>(scratch);
+    rh::PoolScratch scratch(s);  // released on every exit path
+    if (scratch.alloc(ctx, total) != hipSuccess) return rh::fail(RH_E_NOMEM, "rh_crc32c: device scratch");
+    uint8_t* base = scratch.bytes();
     // frame table of one span: offset 0 (8 B), length n (4 B), crc out (4 B)
     struct {
         uint64_t off;
@@ -212,7 +212,6 @@ RH_EXPORT int rh_crc32c(rh_ctx* ctx, uint32_t crc_state, const void* data, uint6
     int rc = rh_crc_launch_impl(ctx, &f, 0, s);
     uint32_t value = 0;
     if (rc == RH_OK) RH_HIP(hipMemcpyAsync(&value, base + o_len + 12, 4, hipMemcpyDeviceToHost, s));
-    RH_HIP(hipFreeAsync(scratch, s));
     RH_HIP(hipStreamSynchronize(s));
     if (rc != RH_OK) return rc;
     *out_state = ~value;  // getValue() = ~crc
@@ -232,10 +231,9 @@ RH_EXPORT int rh_crc32c_verify_host(rh_ctx* ctx, const uint8_t* seg, uint64_t se
     const size_t o_seg = 0, o_off = al(seg_len), o_len = o_off + al(n * 8), o_crc = o_len + al(n * 4),
                  o_bad = o_crc + al(n * 4), o_cnt = o_bad + al(nwords * 8), total = o_cnt + 256;
     hipStream_t s = ctx->stream;
-    void* scratch = nullptr;  // per-call stream-ordered scratch (as rh_crc32c)
-    if (rh::pool_alloc(ctx, &scratch, total, s) != hipSuccess)
-        return rh::fail(RH_E_NOMEM, "rh_crc32c_verify_host: device scratch");
-    uint8_t* base = static_cast<uint8_t*>(scratch);
+    rh::PoolScratch scratch(s);  // per-call stream-ordered scratch (as rh_crc32c), freed on every exit
+    if (scratch.alloc(ctx, total) != hipSuccess) return rh::fail(RH_E_NOMEM, "rh_crc32c_verify_host: device scratch");
+    uint8_t* base = scratch.bytes();
     RH_HIP(hipMemcpyAsync(base + o_seg, seg, seg_len, hipMemcpyHostToDevice, s));
     RH_HIP(hipMemcpyAsync(base + o_off, frame_off, n * 8, hipMemcpyHostToDevice, s));
     RH_HIP(hipMemcpyAsync(base + o_len, frame_len, n * 4, hipMemcpyHostToDevice, s));
@@ -257,9 +255,114 @@ RH_EXPORT int rh_crc32c_verify_host(rh_ctx* ctx, const uint8_t* seg, uint64_t se
         if (bad_bits) RH_HIP(hipMemcpyAsync(bad_bits, base + o_bad, nwords * 8, hipMemcpyDeviceToHost, s));
         RH_HIP(hipMemcpyAsync(&cnt, base + o_cnt, sizeof(cnt), hipMemcpyDeviceToHost, s));
     }
-    RH_HIP(hipFreeAsync(scratch, s));
     RH_HIP(hipStreamSynchronize(s));
     if (rc != RH_OK) return rc;
     *n_bad = cnt;
+    return RH_OK;
+}
+
+// ---- host-image read path (LogSegment.readSegmentFile over many files in one call) -------------
+RH_EXPORT int rh_segments_read_host(rh_ctx* ctx, const uint8_t* image, uint64_t image_len, const uint64_t* seg_off,
+                                    const uint64_t* seg_len, uint64_t n_seg, uint32_t max_op,
+                                    uint32_t frames_per_seg_cap, uint64_t* frame_off, uint32_t* frame_len,
+                                    uint32_t* frame_crc, uint64_t frame_cap, rh_segment_result* results,
+                                    uint64_t* n_frames_total) {
+    if (!ctx || !n_frames_total) return rh::fail(RH_E_INVAL, "rh_segments_read_host: ctx/n_frames_total == NULL");
+    *n_frames_total = 0;
+    if (n_seg == 0) return RH_OK;
+    if (!seg_off || !seg_len || !results || (image_len && !image))
+        return rh::fail(RH_E_INVAL, "rh_segments_read_host: NULL input");
+    if (frame_cap && (!frame_off || !frame_len)) return rh::fail(RH_E_INVAL, "rh_segments_read_host: NULL frame arrays");
+    if (frames_per_seg_cap == 0) return rh::fail(RH_E_INVAL, "rh_segments_read_host: frames_per_seg_cap == 0");
+    if (n_seg > (1ull << 32)) return rh::fail(RH_E_RANGE, "rh_segments_read_host: too many segments");
+    DeviceGuard g(ctx->device);
+    const uint64_t slots = n_seg * (uint64_t)frames_per_seg_cap;
+    const uint64_t dcap = std::max<uint64_t>(1, std::min<uint64_t>(frame_cap, slots));
+    auto al = [](uint64_t x) { return (x + 255) / 256 * 256; };
+    // device layout: image | seg_off | seg_len | scratch off/len/crc | dense off/len/crc | per-segment
+    // first/nframes/status/stop/ok/read_status/read_stop | total
+    uint64_t o = 0;
+    const uint64_t o_img = o; o += al(image_len);
+    const uint64_t o_soff = o; o += al(n_seg * 8);
+    const uint64_t o_slen = o; o += al(n_seg * 8);
+    const uint64_t o_xoff = o; o += al(slots * 8);
+    const uint64_t o_xlen = o; o += al(slots * 4);
+    const uint64_t o_xcrc = o; o += al(slots * 4);
+    const uint64_t o_foff = o; o += al(dcap * 8);
+    const uint64_t o_flen = o; o += al(dcap * 4);
+    const uint64_t o_fcrc = o; o += al(dcap * 4);
+    const uint64_t o_first = o; o += al(n_seg * 8);
+    const uint64_t o_nfr = o; o += al(n_seg * 4);
+    const uint64_t o_st = o; o += al(n_seg * 4);
+    const uint64_t o_stop = o; o += al(n_seg * 8);
+    const uint64_t o_ok = o; o += al(n_seg * 4);
+    const uint64_t o_rst = o; o += al(n_seg * 4);
+    const uint64_t o_rstop = o; o += al(n_seg * 8);
+    const uint64_t o_tot = o; o += 256;
+    hipStream_t s = ctx->stream;
+    rh::PoolScratch scratch(s);
+    if (scratch.alloc(ctx, o) != hipSuccess) return rh::fail(RH_E_NOMEM, "rh_segments_read_host: device scratch");
+    uint8_t* b = scratch.bytes();
+    if (image_len) RH_HIP(hipMemcpyAsync(b + o_img, image, image_len, hipMemcpyHostToDevice, s));
+    RH_HIP(hipMemcpyAsync(b + o_soff, seg_off, n_seg * 8, hipMemcpyHostToDevice, s));
+    RH_HIP(hipMemcpyAsync(b + o_slen, seg_len, n_seg * 8, hipMemcpyHostToDevice, s));
+    rh_segments sg{};
+    sg.buf = b + o_img;
+    sg.buf_len = image_len;
+    sg.seg_off = reinterpret_cast<const uint64_t*>(b + o_soff);
+    sg.seg_len = reinterpret_cast<const uint64_t*>(b + o_slen);
+    sg.n_seg = n_seg;
+    sg.max_op = max_op;
+    sg.frames_per_seg_cap = frames_per_seg_cap;
+    sg.scratch_off = reinterpret_cast<uint64_t*>(b + o_xoff);
+    sg.scratch_len = reinterpret_cast<uint32_t*>(b + o_xlen);
+    sg.frame_off = reinterpret_cast<uint64_t*>(b + o_foff);
+    sg.frame_len = reinterpret_cast<uint32_t*>(b + o_flen);
+    sg.frame_cap = dcap;
+    sg.seg_first = reinterpret_cast<uint64_t*>(b + o_first);
+    sg.seg_nframes = reinterpret_cast<uint32_t*>(b + o_nfr);
+    sg.seg_status = reinterpret_cast<int32_t*>(b + o_st);
+    sg.seg_stop = reinterpret_cast<uint64_t*>(b + o_stop);
+    sg.total_frames = reinterpret_cast<unsigned long long*>(b + o_tot);
+    rh_segments_crc cr{};
+    cr.scratch_crc = reinterpret_cast<uint32_t*>(b + o_xcrc);
+    cr.seg_ok = reinterpret_cast<uint32_t*>(b + o_ok);
+    cr.seg_read_status = reinterpret_cast<int32_t*>(b + o_rst);
+    cr.seg_read_stop = reinterpret_cast<uint64_t*>(b + o_rstop);
+    cr.crc_out = reinterpret_cast<uint32_t*>(b + o_fcrc);
+    int rc = rh_segments_read_impl(ctx, &sg, &cr, s);
+    if (rc != RH_OK) return rc;
+    std::vector<uint64_t> first(n_seg), rstop(n_seg);
+    std::vector<uint32_t> nfr(n_seg), ok(n_seg);
+    std::vector<int32_t> rst(n_seg);
+    unsigned long long total = 0;
+    try {
+        RH_HIP(hipMemcpyAsync(first.data(), b + o_first, n_seg * 8, hipMemcpyDeviceToHost, s));
+        RH_HIP(hipMemcpyAsync(nfr.data(), b + o_nfr, n_seg * 4, hipMemcpyDeviceToHost, s));
+        RH_HIP(hipMemcpyAsync(ok.data(), b + o_ok, n_seg * 4, hipMemcpyDeviceToHost, s));
+        RH_HIP(hipMemcpyAsync(rst.data(), b + o_rst, n_seg * 4, hipMemcpyDeviceToHost, s));
+        RH_HIP(hipMemcpyAsync(rstop.data(), b + o_rstop, n_seg * 8, hipMemcpyDeviceToHost, s));
+        RH_HIP(hipMemcpyAsync(&total, b + o_tot, sizeof(total), hipMemcpyDeviceToHost, s));
+        RH_HIP(hipStreamSynchronize(s));
+    } catch (...) {
+        return rh::fail(RH_E_NOMEM, "rh_segments_read_host: out of host memory");
+    }
+    const uint64_t nout = std::min<uint64_t>(total, frame_cap);
+    if (nout) {
+        RH_HIP(hipMemcpyAsync(frame_off, b + o_foff, nout * 8, hipMemcpyDeviceToHost, s));
+        RH_HIP(hipMemcpyAsync(frame_len, b + o_flen, nout * 4, hipMemcpyDeviceToHost, s));
+        if (frame_crc) RH_HIP(hipMemcpyAsync(frame_crc, b + o_fcrc, nout * 4, hipMemcpyDeviceToHost, s));
+        RH_HIP(hipStreamSynchronize(s));
+    }
+    for (uint64_t i = 0; i < n_seg; ++i) {
+        rh_segment_result& r = results[i];
+        r.status = rst[i];
+        r.n_frames = std::min<uint32_t>(nfr[i], frames_per_seg_cap);
+        r.n_ok = std::min<uint32_t>(ok[i], r.n_frames);
+        r.stop = rstop[i];
+        r.first_frame = first[i];
+        r.reserved = 0;
+    }
+    *n_frames_total = total;
     return RH_OK;
 }

@@ -101,14 +101,26 @@ struct CtrlOp {
     int64_t flush, commit, tstart;  // START
 };
 
-// Event sinks of the table kernels (host-mapped pinned memory, counters in device memory).
+// Event sinks of the table kernels.  Records go to adv / wall / watch (host-mapped pinned memory,
+// or HBM under RH_EVENTS_DEVICE).  Every workgroup takes its range of the lists from one device
+// counter word (kind 0 in the low 32 bits, kind 1 in the high 32) and writes the end of its range
+// (packed the same way) into its own entry of `block_end`, host-mapped memory: the host reads the
+// list lengths as the maxima over those entries, so no memset and no read-back of the counter sits
+// on the stream.  The counters alternate between two words per kind of evaluation: a launch
+// counts into `counts` and clears `counts_next`, the word the following evaluation counts into.
 struct TableEvents {
     rh_index_event* adv = nullptr;     // COMMIT: advanced
     rh_index_event* wall = nullptr;    // COMMIT: watch-ALL changes
     rh_watch_event* watch = nullptr;   // WATCH: level changes
-    unsigned long long* counts = nullptr;  // [0] adv, [1] wall, [2] watch
+    unsigned long long* counts = nullptr;       // device word of this evaluation (zero at launch)
+    unsigned long long* counts_next = nullptr;  // device word of the next one: cleared by block 0
+    uint64_t* block_end = nullptr;              // host-mapped [blocks]: packed end of each block's range
+    uint32_t block_base = 0;                     // this launch's first entry in block_end
     uint64_t cap = 0;
 };
+// Workgroups the table evaluation launches for a table (both width classes): the size of the
+// block_end array an evaluation needs.
+uint32_t table_commit_blocks(const TableDev& t);
 
 }  // namespace rh
 
@@ -131,6 +143,19 @@ namespace rh {
 // Stream-ordered device scratch from the context's memory pool (created on first use, keeps its
 // memory cached between calls): free with hipFreeAsync on the same stream.
 hipError_t pool_alloc(rh_ctx* ctx, void** p, size_t bytes, hipStream_t stream);
+// Pool scratch released (hipFreeAsync on its stream) on every exit path, error returns included.
+struct PoolScratch {
+    void* p = nullptr;
+    hipStream_t s;
+    explicit PoolScratch(hipStream_t stream) : s(stream) {}
+    ~PoolScratch() {
+        if (p) (void)hipFreeAsync(p, s);
+    }
+    PoolScratch(const PoolScratch&) = delete;
+    PoolScratch& operator=(const PoolScratch&) = delete;
+    hipError_t alloc(rh_ctx* ctx, size_t bytes) { return pool_alloc(ctx, &p, bytes, s); }
+    uint8_t* bytes() const { return static_cast<uint8_t*>(p); }
+};
 }  // namespace rh
 
 int rh_commit_launch_impl(rh_ctx* ctx, const rh_commit_soa* tiers, int n_tiers, hipStream_t stream);

@@ -570,7 +570,10 @@ constexpr int kPieceThreads = RH_PIECE_THREADS;
 #ifndef RH_GUESS_BLOCKS_PER_CU  // A/B builds override (scripts/ab_build.sh)
 #define RH_GUESS_BLOCKS_PER_CU 6
 #endif
-constexpr int kGuessBlocksPerCu = RH_GUESS_BLOCKS_PER_CU;  // guess blocks resident per CU
+// Guess-pass grid size: blocks LAUNCHED per CU (the grid of persistent blocks that take pieces in
+// turn), not a residency figure -- how many are resident at once is set by their LDS (~16.5 KB
+// each) and waves.  6 per CU beat 4 and 8 on grid / tail balance (profiles/r02/guess_grid/).
+constexpr int kGuessBlocksPerCu = RH_GUESS_BLOCKS_PER_CU;
 constexpr uint32_t kList = RH_PIECE_LIST;  // frame lengths (u16) a guessed walk records
 constexpr uint32_t kListPerLane = kList / 64;
 constexpr uint32_t kNone = 0xFFFFFFFFu;
@@ -1070,9 +1073,9 @@ int rh_segments_launch_impl(rh_ctx* ctx, const rh_segments* g, hipStream_t strea
     const uint64_t n_seg = g->n_seg;
     const uint64_t piece_cap = g->buf_len / kPiece + n_seg + 1;
     const size_t bytes = (size_t)piece_cap * (40 + 2 * kList) + (size_t)n_seg * 24 + 64;
-    void* scratch = nullptr;
-    RH_HIP(rh::pool_alloc(ctx, &scratch, bytes, stream));
-    uint8_t* sp = static_cast<uint8_t*>(scratch);
+    rh::PoolScratch scratch(stream);  // released on every exit path (after the last pass using it)
+    RH_HIP(scratch.alloc(ctx, bytes));
+    uint8_t* sp = scratch.bytes();
     PieceArgs pa{};
     pa.gwalk = reinterpret_cast<uint4*>(sp);
     pa.walk = pa.gwalk + piece_cap;
@@ -1123,7 +1126,6 @@ int rh_segments_launch_impl(rh_ctx* ctx, const rh_segments* g, hipStream_t strea
     a.resume_pos = pa.resume_pos;
     a.resume_nfr = pa.resume_nfr;
     RH_HIP(launch_walk(a, cus, stream));
-    RH_HIP(hipFreeAsync(scratch, stream));
     hipLaunchKernelGGL(segment_scan_kernel, dim3(1), dim3(kScanThreads), 0, stream, g->seg_nframes, g->n_seg,
                        g->frames_per_seg_cap, g->seg_first, g->total_frames);
     RH_HIP(hipGetLastError());

@@ -172,15 +172,48 @@ __global__ __launch_bounds__(256) void table_control_kernel(TableDev T, const Ct
 }
 
 // ---- updateCommit / commitIndexChanged over the dirty rows ---------------------------------------
+// One workgroup = 16 waves x 128 rows.  Every wave evaluates its rows' results in registers, the
+// block gathers its events in LDS in wave order, takes ONE range of the output list with ONE
+// device-scope atomic (a single counter word saturates at ~88 returning atomics per us,
+// MI355X_MICROARCH.md 'dequeue': one per 128-row wave cost ~90 us per 1M rows), and copies the
+// records out as contiguous 16-byte-per-lane stores (host-mapped memory: full PCIe write lines).
 struct TierRange {
-    uint32_t block_begin[rh::kTableTiers + 1];  // blocks of tier t: [block_begin[t], block_begin[t+1])
+    uint32_t block_begin[rh::kTableTiers + 1];  // blocks of launch slot i: [block_begin[i], block_begin[i+1])
+    int8_t tier[rh::kTableTiers];               // tier of launch slot i (widest first)
+    int32_t n_slots;
 };
 
-constexpr int kTBlock = 256;  // 4 waves x 128 rows
+#ifndef RH_TABLE_BLOCK_WAVES                 // A/B: waves per workgroup (128 rows each)
+#define RH_TABLE_BLOCK_WAVES 12
+#endif
+#ifndef RH_TABLE_WPE                         // A/B: waves per SIMD the widths-2..6 kernel is pinned to
+#define RH_TABLE_WPE 6
+#endif
+constexpr int kTWaves = RH_TABLE_BLOCK_WAVES;
+constexpr int kTBlock = kTWaves * 64;
+constexpr uint32_t kTRows = kTWaves * 128;   // rows per workgroup
+#ifndef RH_TABLE_NT                          // A/B: non-temporal column loads (1) or plain (0)
+#define RH_TABLE_NT 0
+#endif
+
+template <typename V>
+__device__ __forceinline__ V tload(const void* p) {
+    if (RH_TABLE_NT) return __builtin_nontemporal_load(reinterpret_cast<const V*>(p));
+    return *reinterpret_cast<const V*>(p);
+}
+
+// Event staging of one workgroup in LDS: wave w owns 128 records of each kind at w * 128 (kind 0 =
+// advanced commit (COMMIT) / changed levels (WATCH), kind 1 = changed watch-ALL level (COMMIT)), so
+// a wave writes its records as soon as it has them and keeps nothing live across the barrier.
+struct Stage {
+    uint32_t cnt[2][kTWaves];
+    uint32_t pre[2][kTWaves + 1];  // exclusive prefix of cnt over the waves
+    unsigned long long base;        // the block's range in the output lists (both kinds packed)
+};
 
 template <int F, bool RANK, bool WATCH>
-__device__ __forceinline__ void table_wave(const TableDev& T, const TableTier& tt, uint64_t wbase,
-                                           const TableEvents& ev) {
+__device__ __forceinline__ void table_wave(const TableDev& T, const TableTier& tt, uint64_t wbase, bool wall_on,
+                                           unsigned char* stage, Stage& sc) {
     constexpr int N = F + 1;
     const int lane = threadIdx.x & 63;
     const uint64_t r0 = wbase + 2 * (uint64_t)lane;  // rows is a multiple of 128: r0 + 1 < rows
@@ -188,37 +221,40 @@ __device__ __forceinline__ void table_wave(const TableDev& T, const TableTier& t
     const uint16_t dd = *reinterpret_cast<const uint16_t*>(dflag + r0);
     const bool d0 = (dd & 0xFFu) != 0, d1 = (dd >> 8) != 0;
     const bool need = d0 || d1;
-    if (!__any(need)) return;  // the whole 128-row sub-tile is clean: nothing read
+    if (!__any(need)) return;  // the whole 128-row sub-tile is clean: 1 byte per row read
     int64_t fv[2][F], self[2] = {0, 0}, cin[2] = {0, 0}, ts[2] = {0, 0};
     int64_t p0[2] = {0, 0}, p1[2] = {0, 0}, p2[2] = {0, 0};
-    uint32_t w[2] = {0u, 0u};
-    if (need) {
+    uint32_t w[2] = {0u, 0u}, slot[2] = {0u, 0u};
+    if (need) {  // every load of the row pair is issued before any result is used
         const int64_t* col = WATCH ? tt.fcommit : tt.match;
 #pragma unroll
         for (int k = 0; k < F; ++k) {
-            const v2i64 x = *reinterpret_cast<const v2i64*>(col + (uint64_t)k * tt.rows + r0);
+            const v2i64 x = tload<v2i64>(col + (uint64_t)k * tt.rows + r0);
             fv[0][k] = x.x;
             fv[1][k] = x.y;
         }
-        const v2u32 c = *reinterpret_cast<const v2u32*>(tt.conf + r0);
+        const v2u32 c = tload<v2u32>(tt.conf + r0);
+        const v2u32 sl = tload<v2u32>(tt.row_slot + r0);
+        const v2i64 cm = tload<v2i64>(tt.commit + r0);
+        slot[0] = sl.x;
+        slot[1] = sl.y;
         w[0] = d0 ? c.x : 0u;  // a clean row is evaluated as inactive and produces nothing
         w[1] = d1 ? c.y : 0u;
-        const v2i64 cm = *reinterpret_cast<const v2i64*>(tt.commit + r0);
         cin[0] = cm.x;
         cin[1] = cm.y;
         if (WATCH) {
             self[0] = cm.x;  // lastCommittedIndex is the self value (LSI:613)
             self[1] = cm.y;
-            const v2i64 a = *reinterpret_cast<const v2i64*>(tt.wmin + r0);
-            const v2i64 b = *reinterpret_cast<const v2i64*>(tt.wmaj + r0);
-            const v2i64 e = *reinterpret_cast<const v2i64*>(tt.wmax + r0);
+            const v2i64 a = tload<v2i64>(tt.wmin + r0);
+            const v2i64 b = tload<v2i64>(tt.wmaj + r0);
+            const v2i64 e = tload<v2i64>(tt.wmax + r0);
             p0[0] = a.x, p0[1] = a.y, p1[0] = b.x, p1[1] = b.y, p2[0] = e.x, p2[1] = e.y;
         } else {
-            const v2i64 fl = *reinterpret_cast<const v2i64*>(tt.flush + r0);
-            const v2i64 st = *reinterpret_cast<const v2i64*>(tt.tstart + r0);
+            const v2i64 fl = tload<v2i64>(tt.flush + r0);
+            const v2i64 st = tload<v2i64>(tt.tstart + r0);
             self[0] = fl.x, self[1] = fl.y, ts[0] = st.x, ts[1] = st.y;
-            if (ev.wall) {  // watch-ALL levels are compared only when reported (RH_COMMIT_WATCH_ALL)
-                const v2i64 wa = *reinterpret_cast<const v2i64*>(tt.wall + r0);
+            if (wall_on) {  // watch-ALL levels are compared only when reported (RH_COMMIT_WATCH_ALL)
+                const v2i64 wa = tload<v2i64>(tt.wall + r0);
                 p0[0] = wa.x, p0[1] = wa.y;
             }
         }
@@ -231,106 +267,173 @@ __device__ __forceinline__ void table_wave(const TableDev& T, const TableTier& t
 #pragma unroll
     for (int g = 0; g < 2; ++g) trans[g] = (w[g] & RH_CONF_ACTIVE) && (w[g] & RH_CONF_TRANSITIONAL);
     const bool any_trans = __any(trans[0] || trans[1]);
-    bool adv[2] = {false, false}, chg[2] = {false, false}, valid[2];
-    int64_t mn[2], mj[2], mx[2], nc[2];
+    bool e0[2], e1[2] = {false, false};
+    uint32_t valid[2];
+    int64_t x0[2], x1[2], x2[2];  // COMMIT: new commit, min; WATCH: min, majority, max
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
         int64_t vals[N];
 #pragma unroll
         for (int k = 0; k < F; ++k) vals[k] = fv[g][k];
         vals[F] = self[g];
-        rh_eval::eval_group<F, RANK>(vals, w[g], gap, any_trans, valid[g], mn[g], mj[g], mx[g]);
+        bool v;
+        int64_t mn, mj, mx;
+        rh_eval::eval_group<F, RANK>(vals, w[g], gap, any_trans, v, mn, mj, mx);
         const bool dg = g ? d1 : d0;
+        valid[g] = v ? 1u : 0u;
         if (WATCH) {
-            chg[g] = dg && (mn[g] != p0[g] || mj[g] != p1[g] || mx[g] != p2[g]);
+            e0[g] = dg && (mn != p0[g] || mj != p1[g] || mx != p2[g]);
+            x0[g] = mn, x1[g] = mj, x2[g] = mx;
         } else {
-            adv[g] = dg && rh_eval::commit_decision(valid[g], mj[g], cin[g], self[g], ts[g], nc[g]);
-            chg[g] = dg && ev.wall && mn[g] != p0[g];  // watch-ALL level changed (LSI:1025)
+            int64_t nc;
+            e0[g] = dg && rh_eval::commit_decision(v, mj, cin[g], self[g], ts[g], nc);
+            e1[g] = dg && wall_on && mn != p0[g];  // watch-ALL level changed (LSI:1025)
+            x0[g] = nc, x1[g] = mn, x2[g] = 0;
         }
     }
-    // stores: only what changed, plus clearing the dirty flags of this lane's rows
+    // table stores: only what changed, plus clearing the dirty flags of this lane's rows
     if (need) *reinterpret_cast<uint16_t*>(dflag + r0) = 0;
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
         const uint64_t r = r0 + g;
         if (WATCH) {
-            if (chg[g]) {
-                tt.wmin[r] = mn[g];
-                tt.wmaj[r] = mj[g];
-                tt.wmax[r] = mx[g];
+            if (e0[g]) {
+                tt.wmin[r] = x0[g];
+                tt.wmaj[r] = x1[g];
+                tt.wmax[r] = x2[g];
             }
         } else {
-            if (adv[g]) {
-                tt.commit[r] = nc[g];
+            if (e0[g]) {
+                tt.commit[r] = x0[g];
                 tt.wdirty[r] = 1;  // the commit index changed: commitIndexChanged follows (LSI:1003)
             }
-            if (chg[g]) tt.wall[r] = mn[g];
+            if (e1[g]) tt.wall[r] = x1[g];
         }
     }
-    // events: one atomic per wave and event kind, records written to host-mapped memory
+    // events: compacted into this wave's LDS region, in row order
+    const int wave = threadIdx.x >> 6;
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    if (!WATCH) {
-        const uint64_t ae = __ballot(adv[0]), ao = __ballot(adv[1]);
-        if (ae | ao) {
-            unsigned long long base = 0;
-            if (lane == 0) base = atomicAdd(&ev.counts[0], (unsigned long long)(__popcll(ae) + __popcll(ao)));
-            base = __shfl(base, 0);
-            uint64_t pos = base + __popcll(ae & lt) + __popcll(ao & lt);
-#pragma unroll
-            for (int g = 0; g < 2; ++g)
-                if (adv[g]) {
-                    if (pos < ev.cap) {
-                        rh_index_event e{tt.row_slot[r0 + g], 0u, nc[g]};
-                        ev.adv[pos] = e;
-                    }
-                    ++pos;
-                }
-        }
-    }
-    const uint64_t ce = __ballot(chg[0]), co = __ballot(chg[1]);
-    if (ce | co) {
-        unsigned long long base = 0;
-        if (lane == 0)
-            base = atomicAdd(&ev.counts[WATCH ? 2 : 1], (unsigned long long)(__popcll(ce) + __popcll(co)));
-        base = __shfl(base, 0);
-        uint64_t pos = base + __popcll(ce & lt) + __popcll(co & lt);
+    const uint64_t a0 = __ballot(e0[0]), a1 = __ballot(e0[1]);
+    uint32_t p = (uint32_t)(__popcll(a0 & lt) + __popcll(a1 & lt));
+    if (WATCH) {
+        rh_watch_event* sw = reinterpret_cast<rh_watch_event*>(stage) + wave * 128;
 #pragma unroll
         for (int g = 0; g < 2; ++g)
-            if (chg[g]) {
-                if (pos < ev.cap) {
-                    const uint32_t slot = tt.row_slot[r0 + g];
-                    if (WATCH) {
-                        rh_watch_event e{slot, valid[g] ? 1u : 0u, mn[g], mj[g], mx[g]};
-                        ev.watch[pos] = e;
-                    } else {
-                        rh_index_event e{slot, 0u, mn[g]};
-                        ev.wall[pos] = e;
-                    }
-                }
-                ++pos;
-            }
+            if (e0[g]) sw[p++] = rh_watch_event{slot[g], valid[g], x0[g], x1[g], x2[g]};
+    } else {
+        rh_index_event* sa = reinterpret_cast<rh_index_event*>(stage) + wave * 128;
+        rh_index_event* sw = sa + kTRows;
+        const uint64_t c0 = __ballot(e1[0]), c1 = __ballot(e1[1]);
+        uint32_t q = (uint32_t)(__popcll(c0 & lt) + __popcll(c1 & lt));
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            if (e0[g]) sa[p++] = rh_index_event{slot[g], 0u, x0[g]};
+            if (e1[g]) sw[q++] = rh_index_event{slot[g], 0u, x1[g]};
+        }
+        if (lane == 0) sc.cnt[1][wave] = (uint32_t)(__popcll(c0) + __popcll(c1));
     }
+    if (lane == 0) sc.cnt[0][wave] = (uint32_t)(__popcll(a0) + __popcll(a1));
 }
 
 template <int F, int FHI, bool RANK, bool WATCH>
-__device__ __forceinline__ void table_dispatch(const TableDev& T, int t, uint64_t wbase, const TableEvents& ev) {
+__device__ __forceinline__ void table_dispatch(const TableDev& T, int t, uint64_t wbase, bool wall_on,
+                                               unsigned char* stage, Stage& sc) {
     if ((int)rh::width_of_tier(t) == F)
-        table_wave<F, RANK, WATCH>(T, T.tier[t], wbase, ev);
+        table_wave<F, RANK, WATCH>(T, T.tier[t], wbase, wall_on, stage, sc);
     else if constexpr (F + 2 <= FHI)
-        table_dispatch<F + 2, FHI, RANK, WATCH>(T, t, wbase, ev);
+        table_dispatch<F + 2, FHI, RANK, WATCH>(T, t, wbase, wall_on, stage, sc);
 }
 
-// Widths 2..6: rank-mask order statistics; widths 8..14: Batcher networks (commit.hip's split).
 template <bool WATCH, int FLO, int FHI>
-__global__ __launch_bounds__(kTBlock) void table_commit_kernel(TableDev T, TierRange tr, TableEvents ev) {
+__device__ __forceinline__ void table_commit_block(const TierRange& tr, const TableEvents& ev) {
+    const TableDev& T = rh::kernarg_struct<TableDev>();  // block-uniform tier index: scalar loads
+    // COMMIT: [0, 32 KiB) advanced records, [32, 64 KiB) watch-ALL records; WATCH: level records
+    __shared__ __attribute__((aligned(16))) unsigned char stage[kTRows * sizeof(rh_watch_event)];
+    __shared__ Stage sc;
     const uint32_t b = blockIdx.x;
-    int t = 0;
+    int i = 0;
 #pragma unroll
-    for (int i = 1; i < rh::kTableTiers; ++i)
-        if (b >= tr.block_begin[i]) t = i;
-    const uint64_t wbase = ((uint64_t)(b - tr.block_begin[t]) * (kTBlock / 64) + (threadIdx.x >> 6)) * 128;
-    if (wbase >= T.tier[t].rows) return;
-    table_dispatch<FLO, FHI, FLO <= 6, WATCH>(T, t, wbase, ev);
+    for (int k = 1; k < rh::kTableTiers; ++k)
+        if (k < tr.n_slots && b >= tr.block_begin[k]) i = k;
+    const int t = tr.tier[i];
+    const int wave = threadIdx.x >> 6;
+    const uint64_t wbase = ((uint64_t)(b - tr.block_begin[i]) * kTWaves + wave) * 128;
+    const bool wall_on = !WATCH && ev.wall != nullptr;
+    if (threadIdx.x < 2 * kTWaves) (&sc.cnt[0][0])[threadIdx.x] = 0u;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && ev.counts_next) *ev.counts_next = 0ull;  // the next evaluation's word
+    __syncthreads();
+    if (wbase < T.tier[t].rows) table_dispatch<FLO, FHI, FLO <= 6, WATCH>(T, t, wbase, wall_on, stage, sc);
+    __syncthreads();
+
+    // ---- one range of the output lists per block (one device-scope atomic), then a contiguous copy
+    if (threadIdx.x == 0) {
+        uint32_t a0 = 0, a1 = 0;
+        for (int k = 0; k < kTWaves; ++k) {
+            sc.pre[0][k] = a0;
+            sc.pre[1][k] = a1;
+            a0 += sc.cnt[0][k];
+            a1 += sc.cnt[1][k];
+        }
+        sc.pre[0][kTWaves] = a0;
+        sc.pre[1][kTWaves] = a1;
+        // low word: kind 0, high word: kind 1 (each < 2^28: no carry)
+        const unsigned long long add = (unsigned long long)a0 | ((unsigned long long)a1 << 32);
+        sc.base = (a0 | a1) ? atomicAdd(ev.counts, add) : 0ull;
+        if (a0 | a1) ev.block_end[ev.block_base + blockIdx.x] = sc.base + add;  // host-mapped: list lengths
+    }
+    __syncthreads();
+    const uint32_t tot0 = sc.pre[0][kTWaves], tot1 = sc.pre[1][kTWaves];
+    if (!(tot0 | tot1)) return;
+    const uint64_t b0 = sc.base & 0xFFFFFFFFull, b1 = sc.base >> 32;
+    const uint64_t lim0 = b0 >= ev.cap ? 0 : (b0 + tot0 <= ev.cap ? tot0 : ev.cap - b0);
+    const uint64_t lim1 = b1 >= ev.cap ? 0 : (b1 + tot1 <= ev.cap ? tot1 : ev.cap - b1);
+    // record e of the block lives in the region of wave k with pre[k] <= e < pre[k + 1]
+    typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+    const v4u32* src = reinterpret_cast<const v4u32*>(stage);
+    if (WATCH) {  // 32-byte records: two 16-byte words each
+        v4u32* dst = reinterpret_cast<v4u32*>(ev.watch + b0);
+        for (uint32_t j = threadIdx.x; j < 2 * lim0; j += kTBlock) {
+            const uint32_t e = j >> 1;
+            uint32_t k = 0;
+#pragma unroll
+            for (int m = 1; m < kTWaves; ++m) k += e >= sc.pre[0][m] ? 1u : 0u;
+            dst[j] = src[2 * (k * 128 + (e - sc.pre[0][k])) + (j & 1)];
+        }
+    } else {
+        v4u32* da = reinterpret_cast<v4u32*>(ev.adv + b0);
+        for (uint32_t e = threadIdx.x; e < lim0; e += kTBlock) {
+            uint32_t k = 0;
+#pragma unroll
+            for (int m = 1; m < kTWaves; ++m) k += e >= sc.pre[0][m] ? 1u : 0u;
+            da[e] = src[k * 128 + (e - sc.pre[0][k])];
+        }
+        if (ev.wall) {
+            v4u32* dw = reinterpret_cast<v4u32*>(ev.wall + b1);
+            for (uint32_t e = threadIdx.x; e < lim1; e += kTBlock) {
+                uint32_t k = 0;
+#pragma unroll
+                for (int m = 1; m < kTWaves; ++m) k += e >= sc.pre[1][m] ? 1u : 0u;
+                dw[e] = src[kTRows + k * 128 + (e - sc.pre[1][k])];
+            }
+        }
+    }
+}
+
+// Widths 2..6: rank-mask order statistics, 6 waves per SIMD (<= 84 VGPRs: the row pair's columns
+// are all in flight before the compute; at 64 VGPRs the compiler spilled 52 B per lane): two
+// 12-wave workgroups (2 x 48 KiB of event staging) per CU.  Widths 8..14: Batcher networks
+// (commit.hip's split) with the registers their 15-value networks need; these tiers are rare.
+template <bool WATCH>
+__global__ __launch_bounds__(kTBlock) __attribute__((amdgpu_waves_per_eu(RH_TABLE_WPE, 8))) void table_commit_kernel_rank(
+    TableDev Targ, TierRange tr, TableEvents ev) {
+    (void)Targ;
+    table_commit_block<WATCH, 2, 6>(tr, ev);
+}
+
+template <bool WATCH>
+__global__ __launch_bounds__(kTBlock) void table_commit_kernel_net(TableDev Targ, TierRange tr, TableEvents ev) {
+    (void)Targ;
+    table_commit_block<WATCH, 8, 14>(tr, ev);
 }
 
 // ---- hasLease over every started row -------------------------------------------------------------
@@ -406,27 +509,42 @@ int rh_table_control(const rh::TableDev& t, const rh::CtrlOp* d_ops, uint64_t n,
     return RH_OK;
 }
 
-int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev, hipStream_t stream) {
-    // one launch per width class over every non-empty tier of the class
+static uint32_t class_blocks(const rh::TableDev& t, int cls) {
+    uint32_t blocks = 0;
+    for (int i = 0; i < rh::kTableTiers; ++i)
+        if ((cls == 0 ? i <= 2 : i >= 3) && t.tier[i].rows) blocks += (t.tier[i].rows + kTRows - 1) / kTRows;
+    return blocks;
+}
+
+uint32_t rh::table_commit_blocks(const rh::TableDev& t) { return class_blocks(t, 0) + class_blocks(t, 1); }
+
+int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev_in, hipStream_t stream) {
+    // one launch per width class over every non-empty tier of the class, widest tier first (a
+    // joint-consensus tier's rows cost several times a stable row's compute: dispatched last they
+    // were the launch's tail, commit.hip build_args)
+    rh::TableEvents ev = ev_in;
     for (int cls = 0; cls < 2; ++cls) {
         TierRange tr{};
         uint32_t blocks = 0;
-        for (int i = 0; i < rh::kTableTiers; ++i) {
-            tr.block_begin[i] = blocks;
+        for (int i = rh::kTableTiers - 1; i >= 0; --i) {
             const bool in_cls = cls == 0 ? i <= 2 : i >= 3;
-            if (in_cls && t.tier[i].rows) blocks += (uint32_t)(t.tier[i].rows / (2 * kTBlock) + (t.tier[i].rows % (2 * kTBlock) != 0));
+            if (!in_cls || !t.tier[i].rows) continue;
+            tr.block_begin[tr.n_slots] = blocks;
+            tr.tier[tr.n_slots++] = (int8_t)i;
+            blocks += (t.tier[i].rows + kTRows - 1) / kTRows;
         }
-        tr.block_begin[rh::kTableTiers] = blocks;
+        for (int s = tr.n_slots; s <= rh::kTableTiers; ++s) tr.block_begin[s] = blocks;
         if (blocks == 0) continue;
         const dim3 g(blocks), b(kTBlock);
         if (mode == RH_MODE_WATCH) {
-            if (cls == 0) hipLaunchKernelGGL((table_commit_kernel<true, 2, 6>), g, b, 0, stream, t, tr, ev);
-            else hipLaunchKernelGGL((table_commit_kernel<true, 8, 14>), g, b, 0, stream, t, tr, ev);
+            if (cls == 0) hipLaunchKernelGGL(table_commit_kernel_rank<true>, g, b, 0, stream, t, tr, ev);
+            else hipLaunchKernelGGL(table_commit_kernel_net<true>, g, b, 0, stream, t, tr, ev);
         } else {
-            if (cls == 0) hipLaunchKernelGGL((table_commit_kernel<false, 2, 6>), g, b, 0, stream, t, tr, ev);
-            else hipLaunchKernelGGL((table_commit_kernel<false, 8, 14>), g, b, 0, stream, t, tr, ev);
+            if (cls == 0) hipLaunchKernelGGL(table_commit_kernel_rank<false>, g, b, 0, stream, t, tr, ev);
+            else hipLaunchKernelGGL(table_commit_kernel_net<false>, g, b, 0, stream, t, tr, ev);
         }
         RH_HIP(hipGetLastError());
+        ev.block_base += blocks;
     }
     return RH_OK;
 }

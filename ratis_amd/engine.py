@@ -535,6 +535,38 @@ def read_segments_fused(ctx: Context, batch: SegmentBatch, stream: Optional[torc
     return out
 
 
+def read_segments_host(ctx: Context, image, seg_off, seg_len, max_op: int = 4 << 20, frames_per_seg_cap: int = 4096,
+                       frame_cap: Optional[int] = None) -> dict:
+    """``rh_segments_read_host``: LogSegment.readSegmentFile's framing + checksum verdict for every
+    segment of a HOST image (numpy uint8), PCIe included -- the call the Java module's bulk segment
+    load makes.  Returns numpy arrays: per segment ``status``, ``n_ok``, ``stop``, ``first_frame``,
+    ``n_frames``; per frame ``frame_off`` (in ``image``), ``frame_len``, ``frame_crc``; ``total``."""
+    import numpy as np
+    lib = _lib.load()
+    img = np.ascontiguousarray(image, dtype=np.uint8)
+    so = np.ascontiguousarray(seg_off, dtype=np.uint64)
+    sl = np.ascontiguousarray(seg_len, dtype=np.uint64)
+    n = so.size
+    cap = n * frames_per_seg_cap if frame_cap is None else int(frame_cap)
+    fo = np.zeros(max(cap, 1), dtype=np.uint64)
+    fl = np.zeros(max(cap, 1), dtype=np.uint32)
+    fc = np.zeros(max(cap, 1), dtype=np.uint32)
+    res = (_lib.RhSegmentResult * max(n, 1))()
+    total = ctypes.c_uint64()
+    vp = ctypes.c_void_p
+    check(lib.rh_segments_read_host(ctx.handle, vp(img.ctypes.data), img.size, vp(so.ctypes.data), vp(sl.ctypes.data),
+                                    n, max_op, frames_per_seg_cap, vp(fo.ctypes.data), vp(fl.ctypes.data),
+                                    vp(fc.ctypes.data), cap, res, ctypes.byref(total)))
+    k = min(total.value, cap)
+    return {"status": np.array([r.status for r in res[:n]], dtype=np.int32),
+            "n_ok": np.array([r.n_ok for r in res[:n]], dtype=np.int64),
+            "stop": np.array([r.stop for r in res[:n]], dtype=np.int64),
+            "first_frame": np.array([r.first_frame for r in res[:n]], dtype=np.int64),
+            "n_frames": np.array([r.n_frames for r in res[:n]], dtype=np.int64),
+            "frame_off": fo[:k].astype(np.int64), "frame_len": fl[:k].astype(np.int64), "frame_crc": fc[:k],
+            "total": int(total.value)}
+
+
 class _nullctx:
     def __enter__(self):
         return self

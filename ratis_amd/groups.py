@@ -131,6 +131,11 @@ class RaftGroupTable:
             raise _lib.RatisHipError(_lib.RH_E_STATE, "RaftGroupTable closed")
         return self._h
 
+    def set_event_sink(self, sink: int) -> None:
+        """``rh_groups_set_event_sink``: RH_EVENTS_HOST_MAPPED (kernel writes events across PCIe,
+        the default) or RH_EVENTS_DEVICE (events staged in HBM, copied out by the wait)."""
+        check(self._lib.rh_groups_set_event_sink(self.handle, int(sink)))
+
     # -- control ----------------------------------------------------------------------------
     def start(self, slot: int, conf: int, flush_index: int, commit_index: int, term_start: int) -> None:
         check(self._lib.rh_group_start(self.handle, slot, conf & 0xFFFFFFFF, flush_index, commit_index, term_start))
@@ -279,12 +284,19 @@ def shard_of(msb: int, lsb: int, n_shards: int) -> int:
 
 
 class RaftNode:
-    """``rh_node``: one RaftServer's leader divisions over every GPU of ``device_mask``."""
+    """``rh_node``: one RaftServer's leader divisions over every GPU of ``device_mask`` -- or, with
+    ``devices``, one shard per listed device (repeats allowed: several shards on one GPU)."""
 
-    def __init__(self, device_mask: int, capacity_per_shard: int, gap_threshold: int = -1):
+    def __init__(self, device_mask: int, capacity_per_shard: int, gap_threshold: int = -1,
+                 devices: Optional[Sequence[int]] = None):
         self._lib = _lib.load()
         h = ctypes.c_void_p()
-        check(self._lib.rh_node_create(device_mask, capacity_per_shard, gap_threshold, ctypes.byref(h)))
+        if devices is not None:
+            arr = (ctypes.c_int * len(devices))(*[int(d) for d in devices])
+            check(self._lib.rh_node_create_devices(arr, len(devices), capacity_per_shard, gap_threshold,
+                                                   ctypes.byref(h)))
+        else:
+            check(self._lib.rh_node_create(device_mask, capacity_per_shard, gap_threshold, ctypes.byref(h)))
         self._h = h
         self.capacity_per_shard = int(capacity_per_shard)
         self.n_shards = check(self._lib.rh_node_shards(h))
@@ -340,3 +352,53 @@ class RaftNode:
         bits = np.zeros((total + 63) // 64, dtype=np.uint64)
         check(self._lib.rh_node_lease_batch(self._h, int(now_nanos), int(timeout_ms), _p(bits), bits.size))
         return np.unpackbits(bits.view(np.uint8), bitorder="little")[:total].astype(bool)
+
+
+class LeaderPump:
+    """Python twin of the Java module's pump (java/ratis-hip/.../HipLeaderBookkeeper.tick): one
+    tick = push the buffered deltas, start every shard's updateCommit (all shards in flight), per
+    shard hand the advanced commits and watch-ALL levels to the divisions, per shard
+    commitIndexChanged()'s levels (LeaderStateImpl.java:606-622).  ``callbacks[node_slot]`` gets
+    ``on_commit(value)``, ``on_watch_all(min)`` and ``on_watch_levels(min, majority, max)`` (the
+    last only for a present getMajorityMin, as commitIndexChanged's ifPresent)."""
+
+    def __init__(self, node: RaftNode):
+        self.node = node
+        self.callbacks = {}
+        self._pending = []
+
+    def register(self, node_slot: int, callback) -> None:
+        self.callbacks[int(node_slot)] = callback
+
+    def emit(self, deltas: np.ndarray) -> None:
+        self._pending.append(np.ascontiguousarray(deltas, dtype=DELTA_DTYPE))
+
+    def tick(self) -> dict:
+        if self._pending:
+            self.node.push(np.concatenate(self._pending))
+            self._pending = []
+        cap = self.node.capacity_per_shard
+        tickets = [t.commit_async(watch_all=True) for t in self.node.tables]
+        n = {"commit": 0, "watch_all": 0, "watch_levels": 0}
+        for s, (t, tk) in enumerate(zip(self.node.tables, tickets)):
+            r = t.commit_wait(tk)
+            for slot, v in zip(r.advanced_slots, r.advanced_commit):
+                cb = self.callbacks.get(s * cap + int(slot))
+                if cb is not None:
+                    cb.on_commit(int(v))
+                    n["commit"] += 1
+            for slot, v in zip(r.watch_all_slots, r.watch_all_min):
+                cb = self.callbacks.get(s * cap + int(slot))
+                if cb is not None:
+                    cb.on_watch_all(int(v))
+                    n["watch_all"] += 1
+        for s, t in enumerate(self.node.tables):
+            ev = t.commit_index_changed()
+            for e in ev:
+                if not e["valid"]:
+                    continue
+                cb = self.callbacks.get(s * cap + int(e["slot"]))
+                if cb is not None:
+                    cb.on_watch_levels(int(e["min"]), int(e["majority"]), int(e["max"]))
+                    n["watch_levels"] += 1
+        return n

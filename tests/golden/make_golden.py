@@ -11,6 +11,12 @@ Sources of truth (the reference is pure Java and cannot run in this image, SURVE
     (LeaderStateImpl.java:904-1026) and RaftLogBase.updateCommitIndex (RaftLogBase.java:121-142);
     every expected value is written by hand below and re-checked here against both oracle
     restatements before it is saved.
+  * reference_sequences.json -- the exact sequences two reference unit tests assert, transcribed
+    with the values the test computes: TestRaftLogIndex.testIndex (TestRaftLogIndex.java:44-83:
+    RaftLogIndex.updateIncreasingly / updateToMax / setUnconditionally / updateUnconditionally,
+    each step's `updated` flag and the index after it) and TestPeerConfiguration's odd/even quorum
+    cases (TestPeerConfiguration.java:45-70: hasMajority / majorityRejectVotes), re-checked here
+    against a restatement of RaftLogIndex.java:45-86 and PeerConfiguration.java:157-184.
   * raftlog_rw.npz -- the TestRaftLogReadWrite scenario (TestRaftLogReadWrite.java:92-121):
     100 SimpleOperation entries, the expected file size (header + sum(varint(s)+s+4)) and the
     per-frame CRCs computed by the pinned CRC oracle.
@@ -98,7 +104,81 @@ CASES = [
 ]
 
 
+# TestRaftLogIndex.testIndex: one RaftLogIndex("index", 900) driven through four sections; `i` is
+# index.get() + 1 at the start of each section (TestRaftLogIndex.java:53, 61, 69, 77).  Each step:
+# (op, argument, expected `updated`, expected index after, throws).  The updateIncreasingly section
+# ends with the failure case (:56-57): getAndSet runs before the precondition throws, so the index
+# is left at i - 1 = 900 and the updateToMax section starts from 900 (`updated` is never returned
+# there: None).
+RAFT_LOG_INDEX = [
+    ("updateIncreasingly", 900, [("set", 901, True, 901, False), ("set", 901, False, 901, False),
+                                 ("set", 900, None, 900, True)]),
+    ("updateToMax", 900, [("set", 901, True, 901, False), ("set", 901, False, 901, False),
+                          ("set", 900, False, 901, False)]),
+    ("setUnconditionally", 901, [("set", 902, True, 902, False), ("set", 902, False, 902, False),
+                                 ("set", 901, True, 901, False)]),
+    ("updateUnconditionally", 901, [("add", 1, True, 902, False), ("add", 0, False, 902, False),
+                                    ("add", -1, True, 901, False)]),
+]
+
+# TestPeerConfiguration: voters (self "0" first), then the assertions of :51-54 and :64-69.
+PEER_CONFIGURATION = [
+    {"name": "testOddNodesQuorum", "voters": ["0", "1", "2"], "self": "0",
+     "has_majority": [{"others": ["1"], "expected": True}],
+     "majority_reject_votes": [{"rejected": ["1"], "expected": False}]},
+    {"name": "testEvenNodeQuorum", "voters": ["0", "1", "2", "3"], "self": "0",
+     "has_majority": [{"others": ["1"], "expected": False}, {"others": ["1", "2"], "expected": True}],
+     "majority_reject_votes": [{"rejected": ["1"], "expected": False}, {"rejected": ["1", "2"], "expected": True}]},
+]
+
+
+def raft_log_index_step(kind: str, old: int, op: str, arg: int):
+    """RaftLogIndex.java:45-86 restated: returns (updated, new value, throws)."""
+    if kind == "updateIncreasingly":      # getAndSet, then Preconditions.assertTrue(old <= new)
+        return old != arg, arg, not old <= arg
+    if kind == "updateToMax":             # getAndUpdate(max), updated = old < new
+        return old < arg, max(old, arg), False
+    if kind == "setUnconditionally":      # getAndSet, updated = old != new
+        return old != arg, arg, False
+    new = old + arg                       # updateUnconditionally(n -> n + arg)
+    return old != new, new, False
+
+
+def peer_has_majority(voters, others, self_id):
+    """PeerConfiguration.hasMajority(others, selfId) (:152-169): num > size / 2."""
+    num = (1 if self_id in voters else 0) + sum(1 for p in voters if p in others)
+    return num > len(voters) // 2
+
+
+def peer_majority_reject_votes(voters, rejected):
+    """PeerConfiguration.majorityRejectVotes (:175-183): size - |rejected in conf| <= size / 2."""
+    return len(voters) - sum(1 for p in rejected if p in voters) <= len(voters) // 2
+
+
+def reference_sequences() -> dict:
+    seqs = []
+    for kind, init, steps in RAFT_LOG_INDEX:
+        v = init
+        out = []
+        for op, arg, upd, after, throws in steps:
+            got = raft_log_index_step(kind, v, op, arg)
+            assert (None if throws else got[0], got[1], got[2]) == (upd, after, throws), (kind, op, arg, got)
+            v = after
+            out.append({"op": op, "arg": arg, "updated": upd, "after": after, "throws": throws})
+        seqs.append({"method": kind, "initial": init, "steps": out})
+    for c in PEER_CONFIGURATION:
+        for h in c["has_majority"]:
+            assert peer_has_majority(c["voters"], h["others"], c["self"]) == h["expected"], (c["name"], h)
+        for r in c["majority_reject_votes"]:
+            assert peer_majority_reject_votes(c["voters"], r["rejected"]) == r["expected"], (c["name"], r)
+    return {"source": {"raft_log_index": "ratis-test/.../server/raftlog/TestRaftLogIndex.java:44-83",
+                       "peer_configuration": "ratis-test/.../server/impl/TestPeerConfiguration.java:45-70"},
+            "raft_log_index": seqs, "peer_configuration": PEER_CONFIGURATION}
+
+
 def main():
+    json.dump(reference_sequences(), open(os.path.join(HERE, "reference_sequences.json"), "w"), indent=1)
+
     # ---- CRC -------------------------------------------------------------------------------
     tab = orc.crc32c_tables()
     ours = hashlib.sha256(tab.astype("<u4").tobytes()).hexdigest()

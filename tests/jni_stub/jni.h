@@ -48,5 +48,7 @@ struct JNINativeInterface_ {
     void (*ReleasePrimitiveArrayCritical)(JNIEnv*, jarray, void*, jint);
     jobject (*NewDirectByteBuffer)(JNIEnv*, void*, jlong);
     void* (*GetDirectBufferAddress)(JNIEnv*, jobject);
+    jlong (*GetDirectBufferCapacity)(JNIEnv*, jobject);
+    jboolean (*ExceptionCheck)(JNIEnv*);
 };
 #endif

@@ -99,6 +99,9 @@ int main(void) {
   F(rh_lease_soa, timeout_ms) F(rh_lease_soa, follower_ts) F(rh_lease_soa, col_stride) F(rh_lease_soa, conf)
   F(rh_lease_soa, lease_in) F(rh_lease_soa, enabled_bits) F(rh_lease_soa, lease_out)
   F(rh_lease_soa, has_lease_bits) F(rh_lease_soa, extended_bits) F(rh_lease_soa, tile_stride)
+  printf("rh_segment_result %zu\n", sizeof(rh_segment_result));
+  F(rh_segment_result, status) F(rh_segment_result, n_ok) F(rh_segment_result, stop)
+  F(rh_segment_result, first_frame) F(rh_segment_result, n_frames) F(rh_segment_result, reserved)
   printf("conf %u\n", rh_conf_pack(0x5, 1, 1, 0x3, 1, 1));
   return 0;
 }
@@ -119,6 +122,7 @@ def test_struct_layouts_match_header(tmp_path):
     assert int(vals["rh_segments"]) == ctypes.sizeof(_lib.RhSegments)
     assert int(vals["rh_lease_soa"]) == ctypes.sizeof(_lib.RhLeaseSoa)
     assert int(vals["rh_segments_crc"]) == ctypes.sizeof(_lib.RhSegmentsCrc)
+    assert int(vals["rh_segment_result"]) == ctypes.sizeof(_lib.RhSegmentResult) == 32
     assert int(vals["rh_delta"]) == 16 and int(vals["rh_index_event"]) == 16 and int(vals["rh_watch_event"]) == 32
     from ratis_amd import groups
     assert groups.DELTA_DTYPE.itemsize == 16 and groups.INDEX_EVENT_DTYPE.itemsize == 16
@@ -126,7 +130,8 @@ def test_struct_layouts_match_header(tmp_path):
     for cname, cls in (("rh_commit_soa", _lib.RhCommitSoa), ("rh_frames", _lib.RhFrames), ("rh_delta", _lib.RhDelta),
                        ("rh_segments", _lib.RhSegments), ("rh_lease_soa", _lib.RhLeaseSoa),
                        ("rh_segments_crc", _lib.RhSegmentsCrc), ("rh_index_event", _lib.RhIndexEvent),
-                       ("rh_watch_event", _lib.RhWatchEvent), ("rh_commit_out", _lib.RhCommitOut)):
+                       ("rh_watch_event", _lib.RhWatchEvent), ("rh_commit_out", _lib.RhCommitOut),
+                       ("rh_segment_result", _lib.RhSegmentResult)):
         for fname, _ in cls._fields_:
             assert int(vals[f"{cname}.{fname}"]) == getattr(cls, fname).offset, (cname, fname)
     assert int(vals["conf"]) == _lib.conf_pack(0x5, True, True, 0x3, True, True)

@@ -1,0 +1,98 @@
+"""The Java module's pump sequence (HipLeaderBookkeeper.tick) replayed in Python over a 2-shard
+rh_node (ratis_amd.groups.LeaderPump), with divisions that apply the callbacks the way the
+seams patch's LeaderStateImpl does (updateFromHip: updateCommit's follow-up and
+watchRequests.update(ALL, min); commitIndexChanged's ALL_COMMITTED / MAJORITY_COMMITTED / MAJORITY;
+WatchRequests queues only move forward, WatchRequests.java:146-149).  Checked against
+tests/table_model.py step by step; in particular a step that carries ONLY follower commitIndex
+reports (LeaderStateImpl.onFollowerCommitIndex -> commitIndexChanged, :606-622) must move the
+ALL_COMMITTED / MAJORITY_COMMITTED levels with no commit event."""
+import numpy as np
+import pytest
+
+from tests.table_model import COL_FLUSH, TableModel
+from tests.test_gpu_table import conf_word
+
+pytestmark = pytest.mark.gpu
+IMIN = np.iinfo(np.int64).min
+
+
+class Division:
+    """The per-division state the seams touch: the commit index and the WatchRequests levels."""
+
+    def __init__(self, commit):
+        self.commit = commit
+        self.levels = {"ALL": IMIN, "ALL_COMMITTED": IMIN, "MAJORITY_COMMITTED": IMIN, "MAJORITY": IMIN}
+        self.notified = 0
+
+    def _update(self, level, v):   # WatchRequests.update: a queue only moves forward
+        self.levels[level] = max(self.levels[level], v)
+
+    def on_commit(self, v):
+        self.commit = max(self.commit, v)
+
+    def on_watch_all(self, v):
+        self._update("ALL", v)
+
+    def on_watch_levels(self, mn, mj, mx):
+        self._update("ALL_COMMITTED", mn)
+        self._update("MAJORITY_COMMITTED", mj)
+        self._update("MAJORITY", mx)
+        self.notified += 1
+
+
+def test_pump_replica_follower_commit_only_step(ctx, orc):
+    from ratis_amd import groups
+    rng = np.random.default_rng(61)
+    cap, n = 500, 700
+    with groups.RaftNode(0, cap, devices=[0, 0]) as node:
+        pump = groups.LeaderPump(node)
+        model = TableModel(2 * cap)
+        slots = np.concatenate([np.arange(0, n // 2), cap + np.arange(0, n - n // 2)])
+        divs = {}
+        w = conf_word(0b1111)
+        for s in slots:
+            base = int(rng.integers(1 << 20, 1 << 30))
+            node.start(int(s), w, base, base - 100, base - 500)
+            model.start(int(s), w, base, base - 100, base - 500)
+            divs[int(s)] = Division(base - 100)
+            pump.register(int(s), divs[int(s)])
+        want_levels = {int(s): {"ALL": IMIN, "ALL_COMMITTED": IMIN, "MAJORITY_COMMITTED": IMIN, "MAJORITY": IMIN}
+                       for s in slots}
+
+        def step(d):
+            pump.emit(d)
+            model.apply(d)
+            got = pump.tick()
+            a_s, a_c, w_s, w_m = model.commit_batch(orc)
+            for s, v in zip(a_s, a_c):
+                assert divs[int(s)].commit == v
+            for s, v in zip(w_s, w_m):
+                want_levels[int(s)]["ALL"] = max(want_levels[int(s)]["ALL"], int(v))
+            m_s, m_lev, m_valid = model.watch(orc)
+            for j, s in enumerate(m_s):
+                if m_valid[j]:
+                    for name, k in (("ALL_COMMITTED", 0), ("MAJORITY_COMMITTED", 1), ("MAJORITY", 2)):
+                        want_levels[int(s)][name] = max(want_levels[int(s)][name], int(m_lev[k, j]))
+            for s in slots:
+                assert divs[int(s)].levels == want_levels[int(s)], int(s)
+            assert got["commit"] == a_s.size
+            return got
+
+        # replies: matchIndex advances and flush advances -> commits, then the levels follow
+        d = groups.make_deltas(np.repeat(slots, 5), np.tile([0, 1, 2, 3, COL_FLUSH], slots.size),
+                               np.repeat(model.flush[slots], 5) + rng.integers(0, 300, 5 * slots.size))
+        first = step(d)
+        assert first["commit"] > n // 2 and first["watch_all"] > n // 2
+        # follower commitIndex reports ONLY (LeaderStateImpl.onFollowerCommitIndex): no commit event,
+        # but the ALL_COMMITTED / MAJORITY_COMMITTED levels move
+        before = {int(s): dict(divs[int(s)].levels) for s in slots}
+        cols = np.tile(16 + np.arange(4), slots.size)
+        vals = np.repeat(model.commit[slots], 4) - rng.integers(0, 3, 4 * slots.size)
+        got = step(groups.make_deltas(np.repeat(slots, 4), cols, vals))
+        assert got["commit"] == 0 and got["watch_all"] == 0 and got["watch_levels"] > n // 2
+        moved_ac = sum(divs[int(s)].levels["ALL_COMMITTED"] > before[int(s)]["ALL_COMMITTED"] for s in slots)
+        moved_mc = sum(divs[int(s)].levels["MAJORITY_COMMITTED"] > before[int(s)]["MAJORITY_COMMITTED"] for s in slots)
+        assert moved_ac > n // 2 and moved_mc > n // 2
+        # and a quiet tick reports nothing
+        got = step(groups.make_deltas(np.zeros(0, np.int64), 0, 0))
+        assert got == {"commit": 0, "watch_all": 0, "watch_levels": 0}

@@ -241,3 +241,39 @@ def test_fused_ragged_both_crc_plans_against_oracle(ctx, orc, lo, hi):
     assert total == int(rs.seg_nframes.sum())
     bad = np.nonzero(_bits(out["bad_bits"].cpu().numpy(), total))[0]
     assert np.array_equal(bad, rs.corrupted) and rs.corrupted.size > 0
+
+
+@pytest.mark.parametrize("big", [False, True])
+def test_host_image_read_path_matches_reader(ctx, orc, big):
+    """rh_segments_read_host (the Java module's bulk LogSegment load: host image in, the reader's
+    verdict and the verified frame table out, PCIe included) against the literal reader, per
+    segment: status, stop offset, accepted entries, their offsets / lengths and CRCs."""
+    from ratis_amd import _lib, engine
+    rng = np.random.default_rng(170 + big)
+    kinds = [KINDS[i % len(KINDS)] for i in range(len(KINDS) * 4)]
+    made = [make_segment(orc, rng, k, big) for k in kinds]
+    buf, offs, lens = pack([m[0] for m in made], rng)
+    r = engine.read_segments_host(ctx, buf, offs, lens)
+    seen = set()
+    for s in range(len(offs)):
+        ro, rl, rc, rst, rstop = orc.segment_scan(buf[offs[s]: offs[s] + lens[s]])
+        assert (r["status"][s], r["stop"][s], r["n_ok"][s]) == (rst, rstop, len(ro)), s
+        f0 = r["first_frame"][s]
+        k = len(ro)
+        assert np.array_equal(r["frame_off"][f0:f0 + k] - offs[s], ro), s
+        assert np.array_equal(r["frame_len"][f0:f0 + k], rl), s
+        assert np.array_equal(r["frame_crc"][f0:f0 + k], rc), s
+        seen.add(int(rst))
+    assert {_lib.RH_SEG_END, _lib.RH_SEG_PARTIAL, _lib.RH_SEG_E_CHECKSUM, _lib.RH_SEG_E_HEADER} <= seen
+    # a segment with more frames than frames_per_seg_cap is reported, not truncated silently
+    # (unless the reader already stops at a checksum failure inside the slots it has)
+    r2 = engine.read_segments_host(ctx, buf, offs, lens, frames_per_seg_cap=2)
+    n_cap = 0
+    for s in range(len(offs)):
+        ro, _, _, rst, _ = orc.segment_scan(buf[offs[s]: offs[s] + lens[s]])
+        if len(ro) > 2:
+            assert r2["status"][s] == _lib.RH_SEG_E_CAPACITY, s
+            n_cap += 1
+        elif rst == _lib.RH_SEG_E_CHECKSUM and len(ro) < 2:
+            assert r2["status"][s] == _lib.RH_SEG_E_CHECKSUM, s
+    assert n_cap > 0
