@@ -30,7 +30,8 @@ def main():
     a = ap.parse_args()
     out = {"source": a.pmc_dir, "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), WRITE_SIZE x1, KiB x1024"}
     for name, key, tag in (("crc", "crc_frames_kernel", a.crc), ("commit", "commit_kernel", a.commit),
-                           ("framing", "segment_walk_kernel", "framing"), ("lease", "lease_kernel", "lease")):
+                           ("framing", "segment_walk_kernel", "framing"), ("lease", "lease_kernel", "lease"),
+                           ("table", "table_commit_kernel_rank", "table")):
         if not os.path.exists(os.path.join(a.pmc_dir, f"{tag}_b", "run_counter_collection.csv")):
             continue
         f = per_kernel(os.path.join(a.pmc_dir, f"{tag}_b", "run_counter_collection.csv"), key)

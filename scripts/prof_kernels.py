@@ -12,7 +12,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--what", choices=["crc", "crcshape", "crcragged", "commit", "framing", "ragged", "ragged_read", "lease"], default="crc")
+    ap.add_argument("--what", choices=["crc", "crcshape", "crcragged", "commit", "framing", "ragged", "ragged_read", "lease", "table"], default="crc")
     ap.add_argument("--max-frame", type=int, default=2048, help="ragged: frames of 64..max_frame bytes")
     ap.add_argument("--segments", type=int, default=32)
     ap.add_argument("--frame-size", type=int, default=516, help="crcshape: uniform frame size")
@@ -55,6 +55,31 @@ def main():
             engine.segments_scan(ctx, sb)
         torch.cuda.synchronize()
         print("seg_bytes", n * rs.segment_size, "segments", n)
+    elif a.what == "table":
+        # the resident table's updateCommit (table_commit_kernel_rank) with every row dirty: one
+        # matchIndex / flushIndex delta per group per iteration, events staged in HBM
+        import numpy as np
+
+        from ratis_amd import groups
+        host = workload.commit_snapshot(1_000_000, seed=workload.SEED + 1)
+        n = sum(h.n for h in host)
+        tab = groups.RaftGroupTable(ctx, capacity=n)
+        first = 0
+        for h in host:
+            tab.load(first, h.conf, h.flush, h.commit, h.term_start, match=h.follower)
+            first += h.n
+        tab.set_event_sink(_lib.RH_EVENTS_DEVICE)
+        tab.commit_wait_counts(tab.commit_async(watch_all=True))
+        cur = np.concatenate([h.flush for h in host])
+        rng = np.random.default_rng(4)
+        for i in range(a.iters):
+            cur += 512
+            col = np.where(rng.random(n) < 0.1, _lib.RH_COL_FLUSH, rng.integers(0, 4, n))
+            tab.push(groups.make_deltas(np.arange(n), col, cur))
+            tab.commit_wait_counts(tab.commit_async(watch_all=True))
+        torch.cuda.synchronize()
+        f_mean = (host[0].n * 4 + (n - host[0].n) * 6) / n
+        print("alg_bytes", int(n * (8 * f_mean + 45)), "rows", n)
     elif a.what == "lease":
         import numpy as np
         host = workload.commit_snapshot(1_000_000)
