@@ -820,6 +820,162 @@ __global__ __launch_bounds__(kPieceThreads) void piece_guess_kernel(PieceArgs a)
     }
 }
 
+// The same guess with ONE WAVE per piece and every lane busy.  In the rounds above a wave walks
+// until its longest-lived candidate dies (~9 steps for the longest of 64 false chains), while a
+// false candidate dies after ~2 steps on average: three quarters of the lane-steps were idle
+// (PMC: ~6,300 VALU instructions per piece, issue-bound).  Here candidates are handed out in
+// increasing order to whichever lanes are free after each step (refill); a candidate that
+// survives lowers `best`, candidates above `best` are dropped and no longer handed out, and the
+// piece is done when no lane is walking: every candidate below `best` has then died, so `best` is
+// the LOWEST survivor -- the guess the rounds produce, exactly.
+#ifndef RH_GUESS_REFILL  // A/B builds override: 0 = the block rounds above
+#define RH_GUESS_REFILL 1
+#endif
+#ifndef RH_GUESS_WAVE_BLOCKS_PER_CU
+#define RH_GUESS_WAVE_BLOCKS_PER_CU 8  // 8 x 16.5 KB windows of LDS per CU
+#endif
+constexpr int kGuessWaveBlocksPerCu = RH_GUESS_WAVE_BLOCKS_PER_CU;
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t u = __shfl_xor(v, d, 64);
+        v = u < v ? u : v;
+    }
+    return v;
+}
+
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t u = __shfl_xor(v, d, 64);
+        v = u > v ? u : v;
+    }
+    return v;
+}
+
+__global__ __launch_bounds__(64) void piece_guess_wave_kernel(PieceArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t img[kGuessLds];
+    constexpr uint32_t kPer = (kGuessLds + 64 * 16 - 1) / (64 * 16);
+    const int t = threadIdx.x;
+    const unsigned int total = *a.n_pieces;
+    struct Item {
+        uint32_t s, Bi, We, L, o0, ilen, gmax;
+        uint64_t base;
+    };
+    auto find = [&](unsigned int w) -> unsigned int {  // as piece_guess_kernel
+        for (; w < total; w += gridDim.x) {
+            const uint32_t s = a.piece_seg[w];
+            if (s == kNone) continue;
+            if (w == a.piece_first[s]) {
+                if (t == 0) a.guess[w] = (uint32_t)a.seg_stop[s];
+                continue;
+            }
+            return w;
+        }
+        return total;
+    };
+    auto describe = [&](unsigned int w) -> Item {  // as piece_guess_kernel
+        Item it{};
+        if (w >= total) return it;
+        it.s = a.piece_seg[w];
+        it.base = a.seg_off[it.s];
+        it.L = (uint32_t)a.seg_len[it.s];
+        uint32_t Bn;
+        piece_bounds((uint32_t)a.seg_stop[it.s], it.L, w - a.piece_first[it.s], it.Bi, Bn);
+        const uint32_t gm0 = a.seg_gmax[it.s] * 2u;
+        it.gmax = gm0 < 1024u ? 1024u : gm0 > kGuessWin ? kGuessWin : gm0;
+        const uint32_t win = 4u * it.gmax < 4096u ? 4096u : 4u * it.gmax > kGuessWin ? kGuessWin : 4u * it.gmax;
+        it.We = Bn - it.Bi > win ? it.Bi + win : Bn;
+        it.o0 = (uint32_t)((it.base + it.Bi) & 15u);
+        const uint32_t rend = it.L - it.We > 32u ? it.We + 32u : it.L;
+        it.ilen = rend - it.Bi + it.o0;
+        return it;
+    };
+    u32x4s v[kPer];
+    auto issue = [&](const Item& it) {
+        const uint8_t* src = a.buf + it.base + it.Bi - it.o0;
+#pragma unroll
+        for (uint32_t k = 0; k < kPer; ++k) {
+            const uint32_t c = ((uint32_t)t + k * 64u) * 16u;
+            v[k] = u32x4s{0, 0, 0, 0};
+            if (c + 16 <= it.ilen) v[k] = *reinterpret_cast<const u32x4s*>(src + c);
+        }
+    };
+    unsigned int w = find(blockIdx.x);
+    Item cur = describe(w);
+    if (w < total) issue(cur);
+    while (w < total) {
+        unsigned int lastnz = 0;
+        const uint8_t* src = a.buf + cur.base + cur.Bi - cur.o0;
+#pragma unroll
+        for (uint32_t k = 0; k < kPer; ++k) {
+            const uint32_t c = ((uint32_t)t + k * 64u) * 16u;
+            if (c >= kGuessLds) continue;
+            if (c < cur.ilen && c + 16 > cur.ilen) {
+                uint32_t wv[4] = {0, 0, 0, 0};
+                for (uint32_t b = 0; c + b < cur.ilen; ++b) wv[b >> 2] |= (uint32_t)src[c + b] << (8 * (b & 3));
+                v[k] = {wv[0], wv[1], wv[2], wv[3]};
+            }
+            *reinterpret_cast<u32x4s*>(img + c) = v[k];
+            const uint32_t ww[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+            for (int q = 3; q >= 0; --q)
+                if (ww[q]) {
+                    const unsigned int e = c + 4u * q + 4u - (__builtin_clz(ww[q]) >> 3);
+                    lastnz = e > lastnz ? e : lastnz;
+                    break;
+                }
+        }
+        const unsigned int zimg = wave_max_u32(lastnz);
+        __syncthreads();  // the window is in LDS (one wave: a wait, not a rendezvous)
+        const unsigned int w2 = find(w + gridDim.x);
+        const Item nxt = describe(w2);
+        if (w2 < total) issue(nxt);
+        const uint32_t Bi = cur.Bi, We = cur.We, L = cur.L, o0 = cur.o0;
+        const uint32_t zpos = zimg >= o0 ? Bi + zimg - o0 : Bi;
+        const uint32_t gmax = cur.gmax;
+        const uint32_t ncand = We - Bi < 4u * gmax ? We - Bi : 4u * gmax;
+        const uint32_t* img32 = reinterpret_cast<const uint32_t*>(img);
+        const uint32_t qend = We - Bi + o0;
+        const uint32_t qeof = L >= Bi + 8 ? L - 8 - Bi + o0 : 0u;
+        const uint32_t qz = zpos - Bi + o0;
+        uint32_t best = kNone, limit = ncand, next = 64u;
+        uint32_t cand = (uint32_t)t, q = cand + o0;
+        bool run = cand < limit;
+        while (__any(run)) {
+            const bool out = q >= qend || q >= qeof;
+            const uint32_t qa = out ? 0u : q;
+            const uint32_t wi = qa >> 2;
+            const uint32_t hv = __builtin_amdgcn_alignbyte(img32[wi + 1], img32[wi], qa & 3u);
+            const uint32_t fl = fast_frame_len(hv, L - (Bi + q - o0), a.max_op);
+            const bool surv = run && (out || (fl == 0 && q >= qz));
+            if (__any(surv)) {  // rare: the true chain (or a false one) left the window
+                best = min(best, wave_min_u32(surv ? cand : kNone));
+                limit = best;
+            }
+            run = run && !surv && !out && fl != 0 && fl <= gmax && cand < limit;
+            q += run ? fl : 0u;
+            // refill: free lanes take the next candidates, in lane order
+            const uint64_t freeb = __ballot(!run);
+            if (freeb != 0 && next < limit) {
+                const uint32_t k = __builtin_amdgcn_mbcnt_hi((uint32_t)(freeb >> 32),
+                                                             __builtin_amdgcn_mbcnt_lo((uint32_t)freeb, 0u));
+                if (!run) {
+                    cand = next + k;
+                    q = cand + o0;
+                    run = cand < limit;
+                }
+                next += (uint32_t)__popcll(freeb);
+            }
+        }
+        if (t == 0) a.guess[w] = best == kNone ? kNone : Bi + best;
+        __syncthreads();  // the window may be overwritten
+        w = w2;
+        cur = nxt;
+    }
+}
+
 // One lane per piece: the walk from the guess (see above), headers from HBM.
 __global__ __launch_bounds__(256) void piece_walk_kernel(PieceArgs a) {
     const unsigned int total = *a.n_pieces;
@@ -1110,7 +1266,10 @@ int rh_segments_launch_impl(rh_ctx* ctx, const rh_segments* g, hipStream_t strea
     RH_HIP(hipMemsetAsync(pa.n_pieces, 0, sizeof(unsigned int), stream));
     hipLaunchKernelGGL(piece_plan_kernel, dim3(1), dim3(kScanThreads), 0, stream, pa);
     RH_HIP(hipGetLastError());
-    hipLaunchKernelGGL(piece_guess_kernel, dim3((uint32_t)(kGuessBlocksPerCu * cus)), dim3(kPieceThreads), 0, stream, pa);
+    if (RH_GUESS_REFILL)
+        hipLaunchKernelGGL(piece_guess_wave_kernel, dim3((uint32_t)(kGuessWaveBlocksPerCu * cus)), dim3(64), 0, stream, pa);
+    else
+        hipLaunchKernelGGL(piece_guess_kernel, dim3((uint32_t)(kGuessBlocksPerCu * cus)), dim3(kPieceThreads), 0, stream, pa);
     RH_HIP(hipGetLastError());
     const uint64_t wgrid = (piece_cap + 255) / 256 < (uint64_t)cus * 8 ? (piece_cap + 255) / 256 : (uint64_t)cus * 8;
     hipLaunchKernelGGL(piece_walk_kernel, dim3((uint32_t)wgrid), dim3(256), 0, stream, pa);
