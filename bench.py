@@ -66,19 +66,22 @@ def parse():
 
 def load_pmc(path):
     """Per-unit HBM traffic measured by rocprofv3 PMC passes (scripts/pmc.sh + pmc_summary.py),
-    committed under profiles/rNN/.  Used only to fill roofline.traffic."""
+    committed under profiles/rNN/.  Used only to fill roofline.traffic.  Without --pmc-json every
+    profiles/r*/pmc_traffic.json is read oldest first, so each kernel's figure comes from the newest
+    round that measured it; "_src" records which file that was per kernel."""
     import glob
-    if path is None:
-        cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")))
-        if not cands:
-            return {}
-        path = cands[-1]
-    try:
-        d = json.load(open(path))
-        d["_path"] = os.path.relpath(path, ROOT)
-        return d
-    except Exception:
-        return {}
+    paths = [path] if path else sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")))
+    out = {"_src": {}}
+    for p in paths:
+        try:
+            d = json.load(open(p))
+        except Exception:
+            continue
+        for k, v in d.items():
+            out[k] = v
+            if k.endswith("_bytes_per_unit"):
+                out["_src"][k[: -len("_bytes_per_unit")]] = os.path.relpath(p, ROOT)
+    return out
 
 
 def cpu_threads() -> int:
@@ -288,7 +291,7 @@ def queue_gate(stream, cycles: int = 400_000) -> None:
         pass
 
 
-def table_commit_leg(ctx, host, reps: int = 8, fracs=(1.0, 0.1)) -> dict:
+def table_commit_leg(ctx, host, reps: int = 8, fracs=(1.0, 0.1), pmc=None) -> dict:
     """The kernel the Java module drives: rh_commit_batch over the resident table (config-3
     groups, stable F=4 and joint F=6 tiers), after deltas marked `frac` of the groups dirty (one
     matchIndex / flushIndex update per dirty group, as delta_streaming's steps).  Timed on the
@@ -365,7 +368,11 @@ def table_commit_leg(ctx, host, reps: int = 8, fracs=(1.0, 0.1)) -> dict:
             "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(ach / HBM_PEAK_GBPS, 4), "algorithmic_bytes_per_launch": int(alg),
                          "kernel": "table_commit_kernel_rank<false> (events staged in HBM), incl. counter reset "
-                                   "and count read-back"}}
+                                   "and count read-back",
+                         # PMC passes (scripts/prof_kernels.py table case) run the all-dirty step
+                         "traffic": (round(pmc["table_bytes_per_unit"] * n_all)
+                                     if frac >= 1.0 and pmc and "table_bytes_per_unit" in pmc else None),
+                         "traffic_source": (pmc or {}).get("_src", {}).get("table") if frac >= 1.0 else None}}
     for tab in tabs.values():
         tab.close()
     out["workload"] = (f"resident table of {n_all} config-3 groups (F=4 and F=6 tiers); deltas mark the dirty "
@@ -559,7 +566,7 @@ def main():
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBPS, 4),
                 "traffic": (round(pmc["commit_bytes_per_unit"] * n_mine) if "commit_bytes_per_unit" in pmc else None),
-                "traffic_source": pmc.get("_path"),
+                "traffic_source": pmc["_src"].get("commit"),
                 "kernel": f"commit_kernel_rank (fused stable F=4 + joint F=6 tiers, {args.layout} layout)",
                 "algorithmic_bytes_per_launch": alg_bytes, "avg_launch_ms": round(kern_ms, 5)}
 
@@ -621,7 +628,7 @@ def main():
                               "frac": round(lease_ach / HBM_PEAK_GBPS, 4), "kernel": f"lease_kernel<0,7,true,8> (F=4 and F=6 tiers in one launch, {args.lease_layout} layout)",
                               "traffic": (round(pmc["lease_bytes_per_unit"] * n_mine) if "lease_bytes_per_unit" in pmc
                                           else None),
-                              "traffic_source": pmc.get("_path"),
+                              "traffic_source": pmc["_src"].get("lease"),
                               "algorithmic_bytes_per_launch": lease_alg}}
         # ---- the fused launch: updateCommit + hasLease of the same 1M divisions in ONE kernel
         # (rh_leader_soa_launch), rotating over the same batches
@@ -696,7 +703,7 @@ def main():
         pcie["commit_ms_incl_pcie_full_snapshot"] = round(ms, 4)
         pcie["note"] = "full snapshot H2D (pinned) + kernel + commit D2H per batch"
         pcie["delta_streaming"] = delta_streaming(ctx, host, fill_threads=cpu_threads())
-        pcie["delta_streaming"]["table_commit"] = table_commit_leg(ctx, host)
+        pcie["delta_streaming"]["table_commit"] = table_commit_leg(ctx, host, pmc=pmc)
 
     # ------------------------------------------------------------------ CRC32C (config 5)
     crc = {}
@@ -754,7 +761,7 @@ def main():
                "roofline": {"bound": "hbm", "achieved": round(crc_ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                             "frac": round(crc_ach / HBM_PEAK_GBPS, 4),
                             "traffic": (round(pmc["crc_bytes_per_unit"] * fb.n) if "crc_bytes_per_unit" in pmc else None),
-                            "traffic_source": pmc.get("_path"),
+                            "traffic_source": pmc["_src"].get("crc"),
                             "kernel": "crc_frames_kernel (16 lanes x 64 B per 1 KiB window, copy-free 3-slot ring, LDS-staged frame table, 2 fold chains/lane)",
                             "algorithmic_bytes_per_launch": crc_alg, "avg_launch_ms": round(crc_kern_ms, 4)}}
         # ---- read path: framing walk, then framing + verify, over the same segment images
@@ -829,7 +836,7 @@ def main():
                          "frac": round(read_ach / HBM_PEAK_GBPS, 4),
                          "traffic": ((round(pmc["framing_bytes_per_unit"] * n_seg) if "framing_bytes_per_unit" in pmc
                                       else 0) + round(pmc.get("crc_bytes_per_unit", 0) * fb.n)) or None,
-                         "traffic_source": pmc.get("_path"),
+                         "traffic_source": [pmc["_src"].get("framing"), pmc["_src"].get("crc")],
                          "kernel": "segment_walk_kernel<32768> (+ scan, compact) then crc_frames_kernel",
                          "algorithmic_bytes_per_launch": read_alg}}
         del sb, rb
