@@ -111,6 +111,79 @@ std::vector<uint32_t> build_crc_lane_tables(int Q, int S) {
     return out;
 }
 
+namespace {
+Map32 zero_byte_map() {  // advance over one zero byte: r -> (r >> 8) ^ T0[r & 0xff]
+    CrcTables st;
+    build_crc_slice_tables(&st);
+    Map32 one{};
+    for (int i = 0; i < 32; ++i) {
+        const uint32_t x = 1u << i;
+        one.col[i] = (x >> 8) ^ st.slice[0][x & 0xffu];
+    }
+    return one;
+}
+
+Map32 map_pow(Map32 p, uint64_t n) {
+    Map32 acc{};
+    for (int i = 0; i < 32; ++i) acc.col[i] = 1u << i;
+    for (; n; n >>= 1) {
+        if (n & 1u) acc = compose(p, acc);
+        p = compose(p, p);
+    }
+    return acc;
+}
+
+// Inverse over GF(2) by Gauss-Jordan on the rows (the zero-byte advance is invertible: the
+// Castagnoli polynomial has a non-zero constant term, so x is a unit modulo it).
+Map32 invert(const Map32& m) {
+    uint32_t row[32], inv[32];
+    for (int r = 0; r < 32; ++r) {
+        row[r] = 0;
+        for (int c = 0; c < 32; ++c) row[r] |= ((m.col[c] >> r) & 1u) << c;
+        inv[r] = 1u << r;
+    }
+    for (int c = 0; c < 32; ++c) {
+        int p = c;
+        while (p < 32 && !((row[p] >> c) & 1u)) ++p;
+        if (p == 32) return Map32{};  // singular (not reached)
+        std::swap(row[p], row[c]);
+        std::swap(inv[p], inv[c]);
+        for (int r = 0; r < 32; ++r)
+            if (r != c && ((row[r] >> c) & 1u)) {
+                row[r] ^= row[c];
+                inv[r] ^= inv[c];
+            }
+    }
+    Map32 out{};
+    for (int c = 0; c < 32; ++c)
+        for (int r = 0; r < 32; ++r) out.col[c] |= ((inv[r] >> c) & 1u) << r;
+    return out;
+}
+}  // namespace
+
+std::vector<uint32_t> build_crc_inverse_lane_tables() {
+    const Map32 back = invert(zero_byte_map());
+    std::vector<uint32_t> out((size_t)32 * 8 * 16);
+    for (int c = 0; c < 32; ++c) {
+        const Map32 m = map_pow(back, (uint64_t)64 * (uint64_t)(31 - c));
+        for (int k = 0; k < 8; ++k)
+            for (int nib = 0; nib < 16; ++nib) out[((size_t)c * 8 + k) * 16 + nib] = apply(m, (uint32_t)nib << (4 * k));
+    }
+    return out;
+}
+
+std::vector<uint32_t> build_crc_init_terms(uint32_t init) {
+    CrcTables st;
+    build_crc_slice_tables(&st);
+    std::vector<uint32_t> out((size_t)kCrcInitSpan + 1);
+    uint32_t x = init;
+    for (uint32_t k = 0; k <= kCrcInitSpan; ++k) {
+        out[k] = x;
+        x = (x >> 8) ^ st.slice[0][x & 0xffu];
+    }
+    return out;
+}
+
 }  // namespace rh
 
 namespace {
@@ -873,9 +946,385 @@ hipError_t launch_lanes(const LaneArgs& l, uint64_t n, uint64_t cus, hipStream_t
     return hipGetLastError();
 }
 
+// ---- packed path: every frame's 64-byte chunks packed across the wave, in table order -----------
+// The lane kernels above fold whole windows of Q chunks per frame, so a frame pays up to a window
+// of padding, the start-of-frame masking runs in every window that holds a frame start, and the
+// frames must first be sorted by length.  Here a wave takes 64 frames of the table in order (a
+// task) and folds their chunks back to back, 64 chunks per step, whatever the frames' lengths:
+//   * a frame's span is cut into end-anchored chunks 0..k (k = ceil(span / 64) - 1); chunk 0 (the
+//     one holding the frame start, bytes before it zeroed) is folded for all 64 frames in ONE
+//     masked pass per task, so the steps fold chunks 1..k unmasked;
+//   * reset()'s state is not injected into the bytes: it enters as A^span(init), one table lookup
+//     per frame (initv), A = the zero-byte advance;
+//   * in a step, lane l holds packed chunk 64 s + l; its register R (folded from zero) is advanced
+//     to the end of its 32-lane half with the lane table of distance 64 (31 - l mod 32) (LDS,
+//     bank = lane & 31, conflict free), a prefix XOR inside each half (DPP) sums every frame's
+//     chunks there, and the part of a frame begun before the half enters as one uniform 2 KiB
+//     advance (scalar table loads) -- the frame's register at the end of the half;
+//   * a frame ending in the step stores that value; the task's emit pass moves it back to the frame
+//     end with the inverse lane map (global table, once per frame), XORs the init term and checks
+//     or stamps the trailer.
+// Chunk k - m of a frame ending at E covers [E - 64 (m + 1), E - 64 m): the wave's loads of a step
+// are one contiguous run when its frames are contiguous (a segment's frame table).
+// Frames the fast path cannot load safely, malformed ones and spans over kCrcInitSpan go to a list
+// for the window kernel (crc_frames_kernel<true>).
+constexpr int kPackWaves = kCrcThreads / 64;
+constexpr int kPackTabBytes = 128 * 1024 + 4096 + 16384;  // slicing tables, 32-byte join, lane maps
+constexpr int kPackLds = kPackTabBytes + kPackWaves * 512;  // + per wave: 64 step marks, 64 frame values
+static_assert(kPackLds <= 160 * 1024, "LDS budget");
+
+struct PackArgs {
+    FrameArgs f;                       // buffers, outputs, slot-mode fields (f.n = table entries)
+    const uint32_t* ftab;              // build_crc_lane_tables(32, 64)
+    const uint32_t* inv;               // build_crc_inverse_lane_tables()
+    const uint32_t* z64;               // [4][256] advance over 64 zero bytes
+    const uint32_t* z2k;               // [4][256] advance over 2048 zero bytes (uniform lookups)
+    const uint32_t* initv;             // [kCrcInitSpan + 1]: A^k(init)
+    const uint64_t* seg_first;         // slot mode: dense frame d lives in segment upper_bound - 1
+    const unsigned long long* total;   // slot mode: frames in the dense numbering
+    uint64_t n_seg;
+    uint32_t* counts;                  // counts[0]: frames listed for the window kernel (zeroed)
+    uint32_t* widx;
+};
+
+typedef __attribute__((address_space(4))) const uint32_t const_u32_t;
+// Zero-advance of a wave-uniform register: scalar loads through the constant cache.
+__device__ __forceinline__ uint32_t zshift_uniform(const uint32_t* tab, uint32_t r) {
+    r = __builtin_amdgcn_readfirstlane(r);
+    const_u32_t* t = (const_u32_t*)tab;
+    return t[r & 0xffu] ^ t[256 + ((r >> 8) & 0xffu)] ^ t[512 + ((r >> 16) & 0xffu)] ^ t[768 + (r >> 24)];
+}
+
+// Inclusive XOR prefix inside each 32-lane half (row shifts, then row 0 / row 2's last lane into
+// rows 1 / 3).
+__device__ __forceinline__ uint32_t half_prefix_xor(uint32_t x) {
+    x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, false);  // row_shr:1
+    x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, false);  // row_shr:2
+    x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, false);  // row_shr:4
+    x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, false);  // row_shr:8
+    x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    return x;
+}
+
+__device__ __forceinline__ uint32_t wave_scan_add(uint32_t v, int lane) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t u = (uint32_t)__shfl_up((int)v, d, 64);
+        v += lane >= d ? u : 0u;
+    }
+    return v;
+}
+
+// 64 bytes at the 4-aligned b0 plus the next word: the chunk [b0 + sh, b0 + sh + 64).
+__device__ __forceinline__ void load_chunk(const uint8_t* src, uint32_t (&d)[17]) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const u32x4a v = *reinterpret_cast<const u32x4a*>(src + 16 * q);
+        d[4 * q] = v.x;
+        d[4 * q + 1] = v.y;
+        d[4 * q + 2] = v.z;
+        d[4 * q + 3] = v.w;
+    }
+    d[16] = *reinterpret_cast<const uint32_t*>(src + 64);
+}
+
+// CRC register of the 16 words (from zero): two chains of 8 joined over 32 zero bytes.
+__device__ __forceinline__ uint32_t fold16(const uint32_t* lds, const uint32_t* lch, const uint32_t (&w)[16],
+                                           const uint32_t (&lb)[4]) {
+    uint32_t r0 = 0, r1 = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        r0 = fold_word_perm(lds, r0, w[j], lb);
+        r1 = fold_word_perm(lds, r1, w[8 + j], lb);
+    }
+    return zshift(lch, r0) ^ r1;
+}
+
+template <bool SLOT>
+__global__ __launch_bounds__(kCrcThreads) void crc_pack_kernel(PackArgs p) {
+    const FrameArgs& a = p.f;
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+    if (__builtin_amdgcn_groupstaticsize() != 0) __builtin_trap();  // lds_word assumes base 0
+    const uint64_t nfr = SLOT ? (uint64_t)*p.total : a.n;
+    const uint64_t ntask = (nfr + 63) / 64;
+    if ((uint64_t)blockIdx.x * kPackWaves >= ntask) return;  // block-uniform
+    constexpr int kSliceBytes = 128 * 1024;
+    uint32_t* lch = lds + kSliceBytes / 4;
+    uint32_t* lf = lch + 1024;
+    for (int i = threadIdx.x; i < kSliceBytes / 4; i += blockDim.x) {
+        const int region = i >> 14, e = (i >> 6) & 255, half = (i >> 5) & 1;
+        lds[i] = a.slice[((region * 2 + half) << 8) | e];
+    }
+    for (int i = threadIdx.x; i < 1024; i += blockDim.x) lch[i] = a.shift32[i];
+    for (int i = threadIdx.x; i < 4096; i += blockDim.x) lf[i] = p.ftab[i];
+    __syncthreads();
+
+    const int lane = threadIdx.x & 63;
+    const uint32_t c = lane & 31;
+    uint32_t lb[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) lb[k] = ((uint32_t)(k >> 1) << 16) | ((uint32_t)(k & 1) << 7) | (c << 2);
+    const uint32_t wid = threadIdx.x >> 6;
+    uint32_t* mark = lds + kPackTabBytes / 4 + wid * 128;  // [64] step marks
+    uint32_t* vst = mark + 64;                               // [64] frame registers (end of half)
+    const uint32_t tl = (a.flags & (RH_CRC_VERIFY | RH_CRC_STAMP)) ? 4u : 0u;
+    const uint32_t hs = (uint32_t)lane & 32u;
+
+    for (uint64_t t = (uint64_t)blockIdx.x * kPackWaves + wid; t < ntask; t += (uint64_t)gridDim.x * kPackWaves) {
+        // ---- the task's 64 frames: lane j holds frame j ----
+        const uint64_t d = t * 64 + (uint64_t)lane;
+        const bool have = d < nfr;
+        uint64_t f = d;
+        if (SLOT && have) {  // largest segment with seg_first <= d (seg_first[0] = 0)
+            uint64_t lo = 0, hi = p.n_seg;
+            while (hi - lo > 1) {
+                const uint64_t mid = (lo + hi) >> 1;
+                if (p.seg_first[mid] <= d) lo = mid;
+                else hi = mid;
+            }
+            f = lo * (uint64_t)a.slot_cap + (d - p.seg_first[lo]);
+        }
+        uint64_t o = 0;
+        uint32_t L = 0;
+        if (have) {
+            o = a.off[f];
+            L = a.len[f];
+        }
+        const bool malformed = o > (uint64_t)a.buf_len || (int64_t)L > a.buf_len - (int64_t)o || L < tl;
+        const int64_t lcs = (int64_t)L - (int64_t)tl;
+        const int64_t E = (int64_t)o + lcs;
+        const bool pk = have && !malformed && o >= 67 && E + 8 <= a.buf_len && lcs >= 8 && lcs <= (int64_t)rh::kCrcInitSpan;
+        const bool left = have && !pk;
+        const uint64_t lb_left = __ballot(left);
+        if (lb_left) {  // the window kernel's frames (guarded, malformed, long)
+            uint32_t base = 0;
+            if (lane == 0) base = atomicAdd(p.counts, (uint32_t)__popcll(lb_left));
+            base = (uint32_t)__shfl((int)base, 0);
+            if (left)
+                p.widx[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(lb_left >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)lb_left, 0u))] =
+                    (uint32_t)f;
+        }
+        const uint32_t lc = pk ? (uint32_t)lcs : 0u;
+        const uint32_t k = pk ? (lc - 1) >> 6 : 0u;  // chunks after chunk 0
+        const uint32_t Qi = wave_scan_add(k, lane);
+        const uint32_t Q = Qi - k;                   // packed position of the frame's chunk 1
+        const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)Qi, 63);
+        const uint32_t sh = (uint32_t)E & 3u;
+        // trailer and init term (needed at the end of the task; loaded now)
+        uint32_t tw0 = 0, tw1 = 0, iv = 0;
+        if (pk) {
+            const uint32_t* tp = reinterpret_cast<const uint32_t*>(a.buf + (E & ~(int64_t)3));
+            tw0 = tp[0];
+            tw1 = tp[1];
+            iv = p.initv[lc];
+        }
+        mark[lane] = 0;
+        // ---- chunk 0 of every frame: bytes before the frame start zeroed ----
+        uint32_t f0, fs;
+        {
+            uint32_t dd[17];
+            load_chunk(pk ? a.buf + (E - 64 * (int64_t)k - 64 - sh) : a.buf, dd);
+            uint32_t w[16];
+            const int32_t g8 = 8 * (int32_t)((k + 1) * 64 - lc);  // 8 x bytes before the frame
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int32_t kk = min(max(g8 - 32 * i, 0), 32);
+                w[i] = __builtin_amdgcn_alignbyte(dd[i + 1], dd[i], sh) & (uint32_t)(~0ull << kk);
+            }
+            f0 = fold16(lds, lch, w, lb);
+            fs = 0;
+            if (k > 0) {  // chunk 0 seen from the end of chunk 1
+#pragma unroll
+                for (int q = 0; q < 4; ++q) fs ^= p.z64[256 * q + ((f0 >> (8 * q)) & 0xffu)];
+            }
+        }
+
+        // ---- steps: 64 packed chunks (1..k of the frames, in order) each ----
+        struct Step {
+            uint32_t j, i, m, fs;  // frame lane, chunk index (>= 1), chunks after it, chunk-0 term
+            int64_t be;            // chunk end
+            uint32_t sh;
+            bool valid;
+        };
+        auto map = [&](uint32_t s, uint32_t jprev) -> Step {
+            if (k > 0 && (Q >> 6) == s) mark[Q & 63u] = ((s + 1u) << 8) | (uint32_t)lane;
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t rd = mark[lane];
+            const uint64_t M = __ballot((rd >> 8) == s + 1u) & (~0ull >> (63 - lane));
+            const int src = M ? 63 - __builtin_clzll(M) : 0;
+            const uint32_t jr = (uint32_t)__shfl((int)rd, src) & 0xffu;
+            Step x;
+            x.j = M ? jr : jprev;
+            const uint32_t P = s * 64u + (uint32_t)lane;
+            x.valid = P < T;
+            const uint32_t Qj = (uint32_t)__shfl((int)Q, (int)x.j);
+            const uint32_t kj = (uint32_t)__shfl((int)k, (int)x.j);
+            const uint32_t elo = (uint32_t)__shfl((int)(uint32_t)E, (int)x.j);
+            const uint32_t ehi = (uint32_t)__shfl((int)(uint32_t)((uint64_t)E >> 32), (int)x.j);
+            x.fs = (uint32_t)__shfl((int)fs, (int)x.j);
+            x.i = P - Qj + 1u;
+            x.m = kj - x.i;
+            const int64_t Ej = (int64_t)(((uint64_t)ehi << 32) | elo);
+            x.be = Ej - 64 * (int64_t)x.m;
+            x.sh = elo & 3u;
+            return x;
+        };
+        auto load = [&](const Step& x, uint32_t (&dd)[17]) {
+            load_chunk(x.valid ? a.buf + (x.be - 64 - (int64_t)x.sh) : a.buf, dd);
+        };
+        const uint32_t nsteps = (T + 63) >> 6;
+        uint32_t carry = 0;  // register of the frame running past the previous step (at its end)
+        Step cur{};
+        uint32_t dc[17];
+        if (nsteps) {
+            cur = map(0, 0);
+            load(cur, dc);
+        }
+        for (uint32_t s = 0; s < nsteps; ++s) {
+            Step nx{};
+            uint32_t dn[17];
+            if (s + 1 < nsteps) {
+                nx = map(s + 1, (uint32_t)__builtin_amdgcn_readlane((int)cur.j, 63));
+                load(nx, dn);
+            }
+            uint32_t w[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) w[i] = __builtin_amdgcn_alignbyte(dc[i + 1], dc[i], cur.sh);
+            uint32_t R = fold16(lds, lch, w, lb);
+            R ^= cur.i == 1u ? cur.fs : 0u;
+            uint32_t y = 0;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) y ^= lf[c + ((uint32_t)(q * 16) + ((R >> (4 * q)) & 15u)) * 32u];
+            y = cur.valid ? y : 0u;
+            const uint32_t px = half_prefix_xor(y);
+            const int a0 = lane - (int)cur.i + 1;  // lane of the frame's chunk 1 (may be < 0)
+            const bool cont = a0 < (int)hs;        // the frame began before this half
+            const int src = (cont ? (int)hs : a0) - 1;
+            const uint32_t before = (uint32_t)__shfl((int)px, src < 0 ? 0 : src);
+            const uint32_t seg = px ^ (cont ? 0u : (src >= (int)hs ? before : 0u));
+            const uint64_t contM = __ballot(cont);
+            const uint32_t K0 = zshift_uniform(p.z2k, carry);  // the carried frame at the end of half 0
+            const uint32_t s31 = (uint32_t)__builtin_amdgcn_readlane((int)seg, 31);
+            const uint32_t K1 = zshift_uniform(p.z2k, s31 ^ (((contM >> 31) & 1u) ? K0 : 0u));
+            const uint32_t tot = seg ^ (cont ? (hs ? K1 : K0) : 0u);
+            const bool ends = cur.valid && cur.m == 0u;
+            if (ends) vst[cur.j] = tot;
+            const uint64_t runM = __ballot(cur.valid && cur.m != 0u);
+            carry = ((runM >> 63) & 1u) ? (uint32_t)__builtin_amdgcn_readlane((int)tot, 63) : 0u;
+            cur = nx;
+#pragma unroll
+            for (int i = 0; i < 17; ++i) dc[i] = dn[i];
+        }
+        __builtin_amdgcn_wave_barrier();
+
+        // ---- emit: frame lane j finishes frame j ----
+        if (pk) {
+            uint32_t V = f0;
+            if (k > 0) {
+                const uint32_t tot = vst[lane];
+                const uint32_t* im = p.inv + (size_t)((Q + k - 1u) & 31u) * 128u;
+                V = 0;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) V ^= im[q * 16 + ((tot >> (4 * q)) & 15u)];
+            }
+            const uint32_t value = ~(V ^ iv);
+            bool bad = false;
+            if (a.flags & RH_CRC_STAMP) {
+                a.wbuf[E + 0] = (uint8_t)(value >> 24);
+                a.wbuf[E + 1] = (uint8_t)(value >> 16);
+                a.wbuf[E + 2] = (uint8_t)(value >> 8);
+                a.wbuf[E + 3] = (uint8_t)value;
+            } else if (a.flags & RH_CRC_VERIFY) {
+                bad = __builtin_bswap32(__builtin_amdgcn_alignbyte(tw1, tw0, sh)) != value;
+            }
+            emit_frame(a, f, value, bad);
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+// A^k(init) for k = 0..kCrcInitSpan (a start state other than reset()'s; that one is cached in ctx)
+__global__ __launch_bounds__(256) void crc_init_terms_kernel(const uint32_t* shift, uint32_t init, uint32_t* out) {
+    const uint32_t kk = blockIdx.x * blockDim.x + threadIdx.x;
+    if (kk > rh::kCrcInitSpan) return;
+    uint32_t x = init;
+    for (int b = 0; b < 16; ++b)
+        if ((kk >> b) & 1u) x = zshift(shift + (size_t)b * 1024, x);
+    out[kk] = x;
+}
+
+// Slot mode of the packed kernel (the read path): dense frame numbering over the slotted table.
+struct SlotPlan {
+    const uint64_t* seg_first = nullptr;
+    const unsigned long long* total = nullptr;
+    uint64_t n_seg = 0;
+};
+
+#ifndef RH_CRC_PACK  // A/B builds override: 0 = the length-class split (classify / sort / lane kernels)
+#define RH_CRC_PACK 1
+#endif
+
+// packed kernel -> window kernel over the frames it lists, all on `stream`.
+int launch_pack(rh_ctx* ctx, FrameArgs a, const SlotPlan& sp, hipStream_t stream) {
+    static const hipError_t attr = [] {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(crc_pack_kernel<false>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, kPackLds);
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute(reinterpret_cast<const void*>(crc_pack_kernel<true>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, kPackLds);
+        return e;
+    }();
+    RH_HIP(attr);
+    const uint64_t cus = (uint64_t)(ctx->num_cus > 0 ? ctx->num_cus : 256);
+    // scratch: counts, the window kernel's list widx[n], the init terms of a non-reset start state
+    const bool own_init = a.init != 0xFFFFFFFFu;
+    const size_t o_widx = 256, o_init = o_widx + ((size_t)a.n * 4 + 255) / 256 * 256;
+    const size_t bytes = o_init + (own_init ? ((size_t)rh::kCrcInitSpan + 1) * 4 : 0);
+    rh::PoolScratch scratch(stream);
+    RH_HIP(scratch.alloc(ctx, bytes));
+    uint32_t* counts = reinterpret_cast<uint32_t*>(scratch.bytes());
+    uint32_t* widx = reinterpret_cast<uint32_t*>(scratch.bytes() + o_widx);
+    RH_HIP(hipMemsetAsync(counts, 0, 4, stream));
+    PackArgs p{};
+    p.initv = ctx->d_initff;
+    if (own_init) {
+        uint32_t* iv = reinterpret_cast<uint32_t*>(scratch.bytes() + o_init);
+        hipLaunchKernelGGL(crc_init_terms_kernel, dim3((rh::kCrcInitSpan + 256) / 256), dim3(256), 0, stream, ctx->d_shift,
+                           a.init, iv);
+        RH_HIP(hipGetLastError());
+        p.initv = iv;
+    }
+    p.f = a;
+    p.ftab = ctx->d_lane16 + (size_t)4 * 4096;  // Q = 32
+    p.inv = ctx->d_inv32;
+    p.z64 = ctx->d_shift + (size_t)6 * 1024;
+    p.z2k = ctx->d_shift + (size_t)11 * 1024;
+    p.seg_first = sp.seg_first;
+    p.total = sp.total;
+    p.n_seg = sp.n_seg;
+    p.counts = counts;
+    p.widx = widx;
+    if (sp.total) {
+        hipLaunchKernelGGL(crc_pack_kernel<true>, dim3((uint32_t)cus), dim3(kCrcThreads), kPackLds, stream, p);
+    } else {
+        const uint64_t tasks = (a.n + 63) / 64, blocks = (tasks + kPackWaves - 1) / kPackWaves;
+        hipLaunchKernelGGL(crc_pack_kernel<false>, dim3((uint32_t)(blocks < cus ? blocks : cus)), dim3(kCrcThreads),
+                           kPackLds, stream, p);
+    }
+    RH_HIP(hipGetLastError());
+    a.counts = counts;
+    a.widx = widx;
+    constexpr uint64_t kBL = kBatchOf(true);
+    const uint64_t wgrid = (a.n + kBL - 1) / kBL < cus ? (a.n + kBL - 1) / kBL : cus;
+    hipLaunchKernelGGL(crc_frames_kernel<true>, dim3((uint32_t)wgrid), dim3(kCrcThreads), kCrcLdsOf(true), stream, a);
+    RH_HIP(hipGetLastError());
+    return RH_OK;
+}
+
 // classify -> scatter -> lane kernels (4 and 8 lanes per frame) -> window kernel over the rest,
 // all on `stream`.
-int launch_frames(rh_ctx* ctx, FrameArgs a, hipStream_t stream, bool* dense_written = nullptr) {
+int launch_frames(rh_ctx* ctx, FrameArgs a, hipStream_t stream, bool* dense_written = nullptr,
+                  const SlotPlan& sp = SlotPlan{}) {
     static const hipError_t attr = [] {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(crc_frames_kernel<false>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, kCrcLdsOf(false));
@@ -898,6 +1347,9 @@ int launch_frames(rh_ctx* ctx, FrameArgs a, hipStream_t stream, bool* dense_writ
 #ifdef RH_AB_WINDOW_ONLY  // A/B build (scripts/ab_build.sh): every frame on the window kernel
     window_only = true;
 #endif
+#ifdef RH_AB_PACK_ALL  // A/B build: every frame table on the packed kernel
+    window_only = false;
+#endif
     if (window_only) {
         // slot mode: the dense outputs are left to the caller's compaction (a dependent seg_first
         // load at every frame's end costs the window kernel more than that pass, config 5: -4 %)
@@ -912,6 +1364,7 @@ int launch_frames(rh_ctx* ctx, FrameArgs a, hipStream_t stream, bool* dense_writ
         return RH_OK;
     }
     if (dense_written) *dense_written = a.seg_first != nullptr;
+    if (RH_CRC_PACK && (sp.total || !a.slot_nframes)) return launch_pack(ctx, a, sp, stream);
     // scratch: counts[kClasses], cursor[kClasses], rec[n], widx[n]
     const size_t o_rec = 1024, o_widx = o_rec + (size_t)a.n * sizeof(LaneRec), bytes = o_widx + (size_t)a.n * 4;
     rh::PoolScratch scratch(stream);  // released on every exit path
@@ -981,14 +1434,21 @@ int rh_crc_upload_tables(rh_ctx* ctx) {
         rh::build_crc_shift_table(1ull << m, reinterpret_cast<uint32_t(*)[256]>(sh.data() + (size_t)m * 1024));
     RH_HIP(hipMalloc(&ctx->d_shift, sh.size() * 4));
     RH_HIP(hipMemcpy(ctx->d_shift, sh.data(), sh.size() * 4, hipMemcpyHostToDevice));
-    // lane-distance tables for Q = 2, 4, 8, 16 lanes per window (4096 words each)
+    // lane-distance tables for Q = 2, 4, 8, 16, 32 lanes per window (4096 words each)
     std::vector<uint32_t> lt;
-    for (int q = 2; q <= 16; q *= 2) {
+    for (int q = 2; q <= 32; q *= 2) {
         const std::vector<uint32_t> t = rh::build_crc_lane_tables(q, 64);
         lt.insert(lt.end(), t.begin(), t.end());
     }
     RH_HIP(hipMalloc(&ctx->d_lane16, lt.size() * 4));
     RH_HIP(hipMemcpy(ctx->d_lane16, lt.data(), lt.size() * 4, hipMemcpyHostToDevice));
+    // packed kernel: inverse lane maps and reset()'s init term per span length
+    const std::vector<uint32_t> inv = rh::build_crc_inverse_lane_tables();
+    RH_HIP(hipMalloc(&ctx->d_inv32, inv.size() * 4));
+    RH_HIP(hipMemcpy(ctx->d_inv32, inv.data(), inv.size() * 4, hipMemcpyHostToDevice));
+    const std::vector<uint32_t> iff = rh::build_crc_init_terms(0xFFFFFFFFu);
+    RH_HIP(hipMalloc(&ctx->d_initff, iff.size() * 4));
+    RH_HIP(hipMemcpy(ctx->d_initff, iff.data(), iff.size() * 4, hipMemcpyHostToDevice));
     return RH_OK;
 }
 
@@ -1042,5 +1502,9 @@ int rh_crc_verify_slots(rh_ctx* ctx, const rh_segments* g, const rh_segments_crc
         a.dense_bad = c->bad_bits;
         a.frame_cap = g->frame_cap;
     }
-    return launch_frames(ctx, a, stream, dense_written);
+    SlotPlan sp;
+    sp.seg_first = g->seg_first;
+    sp.total = g->total_frames;
+    sp.n_seg = g->n_seg;
+    return launch_frames(ctx, a, stream, dense_written, sp);
 }

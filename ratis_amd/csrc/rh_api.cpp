@@ -122,6 +122,8 @@ RH_EXPORT int rh_shutdown(rh_ctx* ctx) {
     (void)hipFree(ctx->d_slice);
     (void)hipFree(ctx->d_shift);
     (void)hipFree(ctx->d_lane16);
+    (void)hipFree(ctx->d_inv32);
+    (void)hipFree(ctx->d_initff);
     if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
     if (ctx->pool) (void)hipMemPoolDestroy(ctx->pool);
     (void)hipStreamDestroy(ctx->stream);

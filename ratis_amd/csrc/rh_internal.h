@@ -33,6 +33,11 @@ void build_crc_slice_tables(CrcTables* t);
 // Zero-advance map for `nbytes` zero bytes, as 4 byte-indexed tables (out[4][256]).
 void build_crc_shift_table(uint64_t nbytes, uint32_t out[4][256]);
 std::vector<uint32_t> build_crc_lane_tables(int Q, int S);
+// Packed CRC kernel: inverse lane maps (advance BACK over 64 (31 - c) zero bytes, c = 0..31,
+// nibble layout [c][8][16]) and the init term A^k(init) for spans k = 0..kCrcInitSpan.
+std::vector<uint32_t> build_crc_inverse_lane_tables();
+constexpr uint32_t kCrcInitSpan = 65535;
+std::vector<uint32_t> build_crc_init_terms(uint32_t init);
 
 // The kernel's by-value argument struct, addressed in the kernarg segment (address space 4).
 // Indexing a tier array of the argument with a block-dependent index through this pointer gives
@@ -131,7 +136,9 @@ struct rh_ctx {
     // device copies of the CRC tables
     uint32_t* d_slice = nullptr;   // [4][256]
     uint32_t* d_shift = nullptr;   // [41][4][256]: zero-advance maps over 2^m bytes, m = 0..40
-    uint32_t* d_lane16 = nullptr;  // lane-distance nibble tables of the 16-lane x 64-byte fold
+    uint32_t* d_lane16 = nullptr;  // lane-distance nibble tables (Q = 2, 4, 8, 16, 32 lanes x 64 B)
+    uint32_t* d_inv32 = nullptr;   // [32][8][16] inverse lane maps of the packed CRC kernel
+    uint32_t* d_initff = nullptr;  // [kCrcInitSpan + 1] advance of reset()'s 0xFFFFFFFF over k zero bytes
     std::mutex pool_mu;  // guards the pool's creation
     void* h_pinned = nullptr;
     size_t pinned_bytes = 0;
