@@ -1074,15 +1074,35 @@ __global__ __launch_bounds__(kCrcThreads) void crc_pack_kernel(PackArgs p) {
         // ---- the task's 64 frames: lane j holds frame j ----
         const uint64_t d = t * 64 + (uint64_t)lane;
         const bool have = d < nfr;
-        uint64_t f = d;
-        if (SLOT && have) {  // largest segment with seg_first <= d (seg_first[0] = 0)
+        uint64_t f = d, seg = 0;
+        uint32_t slot = 0;
+        if (SLOT) {
+            // the task's first frame: the largest segment with seg_first <= 64 t (seg_first[0] = 0),
+            // a wave-uniform search (scalar loads); a lane past that segment's end steps forward
+            const const_u32_t* sf = (const const_u32_t*)p.seg_first;  // u64 entries as u32 pairs
+            auto first_of = [&](uint64_t s) -> uint64_t {
+                const uint32_t i = __builtin_amdgcn_readfirstlane((uint32_t)s);
+                return ((uint64_t)sf[2 * (uint64_t)i + 1] << 32) | sf[2 * (uint64_t)i];
+            };
+            const uint64_t d0 = t * 64;
             uint64_t lo = 0, hi = p.n_seg;
             while (hi - lo > 1) {
                 const uint64_t mid = (lo + hi) >> 1;
-                if (p.seg_first[mid] <= d) lo = mid;
+                if (first_of(mid) <= d0) lo = mid;
                 else hi = mid;
             }
-            f = lo * (uint64_t)a.slot_cap + (d - p.seg_first[lo]);
+            seg = lo;
+            uint64_t next = seg + 1 < p.n_seg ? first_of(seg + 1) : ~0ull;
+            uint64_t base = first_of(seg);
+            while (__any(have && d >= next)) {  // rare: the task crosses into later segments
+                if (have && d >= next) {
+                    ++seg;
+                    base = next;
+                    next = seg + 1 < p.n_seg ? p.seg_first[seg + 1] : ~0ull;
+                }
+            }
+            slot = (uint32_t)(d - base);
+            f = seg * (uint64_t)a.slot_cap + slot;
         }
         uint64_t o = 0;
         uint32_t L = 0;
@@ -1237,7 +1257,20 @@ __global__ __launch_bounds__(kCrcThreads) void crc_pack_kernel(PackArgs p) {
             } else if (a.flags & RH_CRC_VERIFY) {
                 bad = __builtin_bswap32(__builtin_amdgcn_alignbyte(tw1, tw0, sh)) != value;
             }
-            emit_frame(a, f, value, bad);
+            if (!SLOT) {
+                emit_frame(a, f, value, bad);
+            } else {  // emit_frame's slot mode, with the segment and dense index already known
+                if (a.crc_out) a.crc_out[f] = value;
+                if (bad) {
+                    if (a.n_bad) atomicAdd(a.n_bad, 1ull);
+                    if (a.seg_first_bad) atomicMin(a.seg_first_bad + seg, slot);
+                }
+                if (d < a.frame_cap) {
+                    if (a.dense_crc) a.dense_crc[d] = value;
+                    if (bad && a.dense_bad)
+                        atomicOr(reinterpret_cast<unsigned long long*>(a.dense_bad + (d >> 6)), 1ull << (d & 63));
+                }
+            }
         }
         __builtin_amdgcn_wave_barrier();
     }

@@ -152,7 +152,8 @@ __global__ __launch_bounds__(kBlock2) void segment_walk_kernel(SegArgs a) {
             if (t == 0) {
                 sh_status = kWalking;
                 sh_pos = (long long)a.resume_pos[s];
-                sh_nfr = a.resume_nfr[s];
+                // never past the slot table, whatever the piece pass left (room = cap - nfr below)
+                sh_nfr = a.resume_nfr[s] < a.cap ? a.resume_nfr[s] : a.cap;
             }
         } else if (t == 0) {  // verifyHeader (RDR:179-205)
             const char H[8] = {'R', 'a', 'f', 't', 'L', 'o', 'g', '1'};
@@ -505,14 +506,22 @@ __global__ __launch_bounds__(kScanThreads) void segment_scan_kernel(const uint32
     if (t == kScanThreads - 1) *total = part[t];
 }
 
+// Work items of kCompactSlots slots of one segment each (a segment of 32k frames spreads over
+// several CUs: one block per segment left most of the chip idle).
+constexpr uint32_t kCompactSlots = 4096;
 __global__ __launch_bounds__(256) void segment_compact_kernel(const uint64_t* scratch_off, const uint32_t* scratch_len,
                                                               const uint32_t* nframes, const uint64_t* seg_first,
                                                               uint64_t n_seg, uint32_t cap, uint64_t* frame_off,
                                                               uint32_t* frame_len, uint64_t frame_cap) {
-    for (uint64_t s = blockIdx.x; s < n_seg; s += gridDim.x) {
+    const uint64_t per = (cap + kCompactSlots - 1) / kCompactSlots;
+    for (uint64_t it = blockIdx.x; it < n_seg * per; it += gridDim.x) {
+        const uint64_t s = it / per;
+        const uint32_t lo = (uint32_t)(it - s * per) * kCompactSlots;
         const uint32_t n = nframes[s] < cap ? nframes[s] : cap;
+        if (lo >= n) continue;  // block-uniform
+        const uint32_t hi = n - lo < kCompactSlots ? n : lo + kCompactSlots;
         const uint64_t first = seg_first[s];
-        for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        for (uint32_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
             if (first + i < frame_cap) {
                 frame_off[first + i] = scratch_off[s * (uint64_t)cap + i];
                 frame_len[first + i] = scratch_len[s * (uint64_t)cap + i];
@@ -576,6 +585,7 @@ constexpr int kPieceThreads = RH_PIECE_THREADS;
 constexpr int kGuessBlocksPerCu = RH_GUESS_BLOCKS_PER_CU;
 constexpr uint32_t kList = RH_PIECE_LIST;  // frame lengths (u16) a guessed walk records
 constexpr uint32_t kListPerLane = kList / 64;
+constexpr uint32_t kAList = 16;  // merge-walk frame lengths kept per piece (the true frames before the meeting)
 constexpr uint32_t kNone = 0xFFFFFFFFu;
 
 // Frame length of the header v (bytes p..p+3, little-endian) if it passes the fast-path checks,
@@ -633,7 +643,9 @@ struct PieceArgs {
     uint32_t* guess;             // [piece_cap] g (kNone: no survivor)
     uint4* gwalk;                // [piece_cap] walk from g: {g, count, exit, ended | list_ok << 1}
     uint16_t* plen;              // [piece_cap][kList] frame lengths of that walk
+    uint16_t* alen;              // [piece_cap][kAList] frame lengths of the merge walk (pre) up to the meeting
     uint4* walk;                 // [piece_cap] true walk: {entry, count, first slot, merge steps | kNone}
+    uint4* pre;                  // [piece_cap] merge from the assumed entry (piece_walk_kernel)
     uint64_t* resume_pos;        // [n_seg]
     uint32_t* resume_nfr;        // [n_seg]
     uint64_t* scratch_off;
@@ -976,6 +988,37 @@ __global__ __launch_bounds__(64) void piece_guess_wave_kernel(PieceArgs a) {
     }
 }
 
+// The walk from p to the piece end through HBM headers, recording the frame lengths in pl.  The
+// lengths are buffered in registers and stored 8 at a time (16 B): on gfx9 vmcnt counts stores too,
+// and a store per frame made every header load wait for the previous frame's store first (the
+// loop's dependent chain then paid two memory round trips per frame).  __restrict__: the header
+// loads never alias the list.
+__device__ __forceinline__ uint32_t walk_piece(const uint8_t* __restrict__ buf, uint16_t* __restrict__ pl, uint64_t base,
+                                               uint32_t p, uint32_t Bn, uint32_t L, uint32_t max_op, uint32_t& cnt,
+                                               uint32_t& ended, uint32_t& lok) {
+    uint32_t acc[4] = {0, 0, 0, 0};
+    while (p < Bn) {
+        const uint32_t fl = hbm_frame_len(buf, base, p, L, max_op);
+        if (fl == 0) {
+            ended = 1;
+            break;
+        }
+        if (cnt < kList) {
+            const uint32_t k = cnt & 7u;
+            const uint32_t v = (fl < 65536u ? fl : 0xFFFFu) << (16 * (k & 1u));
+#pragma unroll
+            for (uint32_t q = 0; q < 4; ++q) acc[q] = (k >> 1) == q ? ((k & 1u) ? acc[q] | v : v) : acc[q];
+            lok &= fl < 65536u ? 1u : 0u;
+            if (k == 7u) *reinterpret_cast<uint4*>(pl + (cnt - 7u)) = make_uint4(acc[0], acc[1], acc[2], acc[3]);
+        }
+        ++cnt;
+        p += fl;
+    }
+    const uint32_t c = cnt < kList ? cnt : kList;  // the lengths of a partial last group of 8
+    for (uint32_t k = c & ~7u; k < c; ++k) pl[k] = (uint16_t)(acc[(k & 7u) >> 1] >> (16 * (k & 1u)));
+    return p;
+}
+
 // One lane per piece: the walk from the guess (see above), headers from HBM.
 __global__ __launch_bounds__(256) void piece_walk_kernel(PieceArgs a) {
     const unsigned int total = *a.n_pieces;
@@ -990,27 +1033,140 @@ __global__ __launch_bounds__(256) void piece_walk_kernel(PieceArgs a) {
             const uint32_t L = (uint32_t)a.seg_len[s];
             uint32_t Bi, Bn;
             piece_bounds((uint32_t)a.seg_stop[s], L, w - a.piece_first[s], Bi, Bn);
-            while (p < Bn) {
-                const uint32_t fl = hbm_frame_len(a.buf, base, p, L, a.max_op);
-                if (fl == 0) {
-                    ended = 1;
-                    break;
-                }
-                if (cnt < kList) {
-                    pl[cnt] = (uint16_t)fl;
-                    lok &= fl < 65536u ? 1u : 0u;
-                }
-                ++cnt;
-                p += fl;
-            }
+            p = walk_piece(a.buf, pl, base, p, Bn, L, a.max_op, cnt, ended, lok);
         }
         a.gwalk[w] = make_uint4(g, cnt, p, ended | (lok << 1));
+        // The next piece's merge (see piece_stitch_kernel): if this walk is the true one, the next
+        // piece's true entry is its exit p.  Almost every guess is a false start whose chain merged
+        // into the true one, so walk from p (chain A) and from the next guess (chain B) in position
+        // order until they meet: A's steps before the meeting point are the true frames the guessed
+        // walk missed, B's the false ones it has.  Headers from HBM; bounded, else left to the stitch.
+        // pre[w + 1] = {assumed entry, A steps, met ? B steps : A's exit, met | ended << 1}.
+        if (w == a.piece_first[s]) a.pre[w] = make_uint4(kNone, 0, 0, 0);
+        if (w + 1 < total && a.piece_seg[w + 1] == s) {
+            uint4 pr = make_uint4(kNone, 0, 0, 0);
+            const uint32_t gb = a.guess[w + 1];
+            if (g != kNone && !ended && gb != kNone) {
+                const uint64_t base = a.seg_off[s];
+                const uint32_t L = (uint32_t)a.seg_len[s];
+                uint32_t Bi, Bn;
+                piece_bounds((uint32_t)a.seg_stop[s], L, w + 1 - a.piece_first[s], Bi, Bn);
+                uint32_t pa = p, pb = gb, ma = 0, mb = 0, fa_end = 0, steps = 0;
+                uint32_t al[kAList / 2] = {};  // A's frame lengths (u16 pairs), stored once at the end
+                bool alfit = true;             // every one of them below 64 KiB
+                bool bdone = false, met = false, give_up = false;
+                while (true) {
+                    if (pa == pb) {
+                        met = true;
+                        break;
+                    }
+                    if (pa >= Bn || (bdone && pa > pb)) break;  // not met: A's walk is the true one
+                    if (++steps > 48) {
+                        give_up = true;
+                        break;
+                    }
+                    if (pa < pb || bdone) {
+                        const uint32_t fl = hbm_frame_len(a.buf, base, pa, L, a.max_op);
+                        if (fl == 0) {
+                            fa_end = 1;
+                            break;
+                        }
+                        if (ma < kAList) {
+                            const uint32_t v = (fl & 0xFFFFu) << (16 * (ma & 1u));
+                            alfit = alfit && fl < 65536u;
+#pragma unroll
+                            for (uint32_t q = 0; q < kAList / 2; ++q) al[q] = (ma >> 1) == q ? (al[q] | v) : al[q];
+                        }
+                        pa += fl;
+                        ++ma;
+                    } else {
+                        const uint32_t fl = pb < Bn ? hbm_frame_len(a.buf, base, pb, L, a.max_op) : 0u;
+                        if (fl == 0) bdone = true;  // B's walk ends at pb (a meeting is still possible there)
+                        else {
+                            pb += fl;
+                            ++mb;
+                        }
+                    }
+                }
+                if (!give_up) {
+                    // bit 2: al holds every one of A's frames before the meeting (the write uses them)
+                    const bool alok = met && ma <= kAList && alfit;
+                    pr = make_uint4(p, ma, met ? mb : pa, (met ? 1u : 0u) | (fa_end << 1) | (alok ? 4u : 0u));
+                    if (alok) {
+                        uint4* dst = reinterpret_cast<uint4*>(a.alen + (uint64_t)(w + 1) * kAList);
+                        dst[0] = make_uint4(al[0], al[1], al[2], al[3]);
+                        dst[1] = make_uint4(al[4], al[5], al[6], al[7]);
+                    }
+                }
+            }
+            a.pre[w + 1] = pr;
+        }
     }
+}
+
+// The true walk of piece w from entry e (!= its guess g): through HBM headers until it meets a
+// listed position of the guessed walk (from there the two coincide) or passes the listed part or
+// ends.  Wave-uniform; the guessed walk's positions are rebuilt in registers (lane l: frames
+// [16 l, 16 l + 16)).  In: gr = gwalk[w].  Out: cnt / x / ended of the true walk, msteps = steps
+// before the meeting point (kNone: never met).
+struct MergeOut {
+    uint32_t cnt, x, ended, msteps;
+};
+__device__ __forceinline__ MergeOut merge_walk(const PieceArgs& a, uint32_t w, uint4 gr, uint32_t e, uint32_t Bn,
+                                               uint64_t base, uint32_t L, int lane) {
+    const uint32_t g = gr.x, gfl = gr.w;
+    uint32_t cnt = gr.y, x = gr.z;
+    const uint32_t nl = (g != kNone && (gfl & 2u)) ? (cnt < kList ? cnt : kList) : 0u;
+    uint32_t pos[kListPerLane];
+    uint32_t run = 0;
+    const uint16_t* pl = a.plen + (uint64_t)w * kList + (uint32_t)lane * kListPerLane;
+#pragma unroll
+    for (uint32_t k = 0; k < kListPerLane; ++k) {
+        const uint32_t idx = (uint32_t)lane * kListPerLane + k;
+        pos[k] = run;
+        run += idx < nl ? (uint32_t)pl[k] : 0u;
+    }
+    const uint32_t incl = wave_incl_scan(run, lane);
+    const uint32_t off = g + incl - run;
+#pragma unroll
+    for (uint32_t k = 0; k < kListPerLane; ++k) pos[k] = (uint32_t)lane * kListPerLane + k < nl ? off + pos[k] : kNone;
+    const uint32_t last = nl ? g + __builtin_amdgcn_readlane(incl, 63) : 0u;  // end of the listed part
+    uint32_t p = e, m = 0, ended = 0;
+    bool met = false;
+    while (p < Bn) {
+        if (p < last) {
+            uint32_t jl = kNone;
+#pragma unroll
+            for (uint32_t k = 0; k < kListPerLane; ++k)
+                if (pos[k] == p) jl = (uint32_t)lane * kListPerLane + k;
+            const uint64_t hit = __builtin_amdgcn_ballot_w64(jl != kNone);
+            if (hit) {
+                const uint32_t jj = __builtin_amdgcn_readlane(jl, __builtin_ctzll(hit));
+                cnt = m + cnt - jj;  // x, ended: the guessed walk's
+                met = true;
+                break;
+            }
+        }
+        const uint32_t fl = hbm_frame_len(a.buf, base, p, L, a.max_op);
+        if (fl == 0) {
+            ended = 1;
+            break;
+        }
+        ++m;
+        p += fl;
+    }
+    if (!met) return MergeOut{m, p, ended, kNone};
+    return MergeOut{cnt, x, gfl & 1u, m};
 }
 
 // One wave per segment: the true chain through the pieces (see above).  Control is wave-uniform.
 __global__ __launch_bounds__(64) void piece_stitch_kernel(PieceArgs a) {
     const uint64_t s = blockIdx.x;
+#ifdef RH_STITCH_STATS
+    const uint64_t t_0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t t_1 = 0, t_2 = 0;
+    uint32_t npass = 0, nser = 0;
+#endif
     if (s >= a.n_seg || a.seg_status[s] != kDeferred) return;
     const int lane = threadIdx.x;
     const uint64_t base = a.seg_off[s];
@@ -1021,97 +1177,185 @@ __global__ __launch_bounds__(64) void piece_stitch_kernel(PieceArgs a) {
     uint64_t rpos = pd;
     uint32_t rnfr = total;
     bool done = false;
-    for (uint32_t c0 = 0; c0 < np && !done; c0 += 64) {
-        const uint32_t nc = np - c0 < 64 ? np - c0 : 64;
-        uint4 gr = make_uint4(kNone, 0, 0, 0);
-        if ((uint32_t)lane < nc) gr = a.gwalk[pf + c0 + lane];
-        uint4 out = make_uint4(0, 0, 0, kNone);
-        for (uint32_t j = 0; j < nc && !done; ++j) {
-            const uint32_t w = pf + c0 + j;
-            uint32_t Bi, Bn;
-            piece_bounds(pd, L, c0 + j, Bi, Bn);
-            if (e >= Bn) {  // a frame spans this piece: nothing starts in it
-                if ((uint32_t)lane == j) out = make_uint4(e, 0, total, kNone);
-                continue;
-            }
-            const uint32_t g = __builtin_amdgcn_readlane(gr.x, j);
-            uint32_t cnt = __builtin_amdgcn_readlane(gr.y, j);
-            uint32_t x = __builtin_amdgcn_readlane(gr.z, j);
-            const uint32_t gfl = __builtin_amdgcn_readlane(gr.w, j);
-            uint32_t ended = gfl & 1u, msteps = 0;
-            if (g != e) {
-                // The guessed walk's listed positions: lane l holds frames [16 l, 16 l + 16).
-                const uint32_t nl = (g != kNone && (gfl & 2u)) ? (cnt < kList ? cnt : kList) : 0u;
-                uint32_t pos[kListPerLane];
-                uint32_t run = 0;
-                const uint16_t* pl = a.plen + (uint64_t)w * kList + (uint32_t)lane * kListPerLane;
+    uint32_t j = 0;  // pieces [0, j) resolved (their walk entries written)
+    constexpr uint32_t K = 8;  // pieces per lane in a parallel pass (512 = 64 MiB of segment)
+    const uint4 kDefault = make_uint4(0, 0, 0, kNone);
+    while (j < np && !done) {
+        // ---- parallel pass over pieces j + lane K + k: each takes as its entry the previous
+        // piece's guessed exit (the first one: the true entry e).  While every piece's true exit
+        // is its guessed exit, those entries are the true ones and a piece's walk follows from
+        // pre / gwalk alone; the pass stops at the first piece where that fails (unknown merge,
+        // exit differing, walk ended, a frame spanning the piece, slot capacity).
+        const uint32_t P = np - j < 64 * K ? np - j : 64 * K;
+        uint4 gr[K], pr[K];
 #pragma unroll
-                for (uint32_t k = 0; k < kListPerLane; ++k) {
-                    const uint32_t idx = (uint32_t)lane * kListPerLane + k;
-                    pos[k] = run;
-                    run += idx < nl ? (uint32_t)pl[k] : 0u;
-                }
-                const uint32_t incl = wave_incl_scan(run, lane);
-                const uint32_t off = g + incl - run;
-#pragma unroll
-                for (uint32_t k = 0; k < kListPerLane; ++k) pos[k] = (uint32_t)lane * kListPerLane + k < nl ? off + pos[k] : kNone;
-                const uint32_t last = nl ? g + __builtin_amdgcn_readlane(incl, 63) : 0u;  // end of the listed part
-                // Walk from the true entry until it meets a listed position (then the rest of the
-                // piece is the guessed walk from that frame on), passes the listed part, or ends.
-                uint32_t p = e, m = 0;
-                bool met = false;
-                ended = 0;
-                while (p < Bn) {
-                    if (p < last) {
-                        uint32_t jl = kNone;
-#pragma unroll
-                        for (uint32_t k = 0; k < kListPerLane; ++k)
-                            if (pos[k] == p) jl = (uint32_t)lane * kListPerLane + k;
-                        const uint64_t hit = __builtin_amdgcn_ballot_w64(jl != kNone);
-                        if (hit) {
-                            const uint32_t jj = __builtin_amdgcn_readlane(jl, __builtin_ctzll(hit));
-                            cnt = m + cnt - jj;  // x, ended: the guessed walk's
-                            met = true;
-                            break;
-                        }
-                    }
-                    const uint32_t fl = hbm_frame_len(a.buf, base, p, L, a.max_op);
-                    if (fl == 0) {
-                        ended = 1;
-                        break;
-                    }
-                    ++m;
-                    p += fl;
-                }
-                if (!met) {
-                    cnt = m;
-                    x = p;
-                    msteps = kNone;
-                } else {
-                    ended = gfl & 1u;
-                    msteps = m;
-                }
+        for (uint32_t k = 0; k < K; ++k) {
+            const uint32_t i = (uint32_t)lane * K + k;
+            gr[k] = make_uint4(kNone, 0, 0, 0);
+            pr[k] = make_uint4(kNone, 0, 0, 0);
+            if (i < P) {
+                gr[k] = a.gwalk[pf + j + i];
+                pr[k] = a.pre[pf + j + i];
             }
-            if (total + cnt > a.cap) {  // the slot capacity ends inside this piece: serial from e
-                rpos = e;
-                rnfr = total;
-                done = true;
-                break;
-            }
-            if ((uint32_t)lane == j) out = make_uint4(e, cnt, total, msteps);
-            total += cnt;
-            if (ended) {
-                rpos = x;
-                rnfr = total;
-                done = true;
-                break;
-            }
-            e = x;
         }
-        if ((uint32_t)lane < nc) a.walk[pf + c0 + lane] = out;
-        if (done)
-            for (uint32_t k = c0 + 64 + lane; k < np; k += 64) a.walk[pf + k] = make_uint4(0, 0, 0, kNone);
+#ifdef RH_STITCH_STATS
+        if (!t_1) t_1 = __builtin_amdgcn_s_memrealtime() + (gr[0].x & 0);
+        ++npass;
+#endif
+        const uint32_t prevx = (uint32_t)__shfl_up((int)gr[K - 1].z, 1, 64);
+        uint32_t ent[K], cnt[K], xx[K], ms[K], incl[K], excl[K];
+        bool kn[K], en[K];
+        uint32_t run = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < K; ++k) {
+            const uint32_t i = (uint32_t)lane * K + k;
+            ent[k] = k ? gr[k - 1].z : (lane ? prevx : e);
+            uint32_t Bi, Bn;
+            piece_bounds(pd, L, j + i, Bi, Bn);
+            kn[k] = i < P && ent[k] < Bn;
+            cnt[k] = gr[k].y;
+            xx[k] = gr[k].z;
+            en[k] = gr[k].w & 1u;
+            ms[k] = 0;
+            if (ent[k] != gr[k].x) {
+                if (pr[k].x == ent[k]) {
+                    if (pr[k].w & 1u) {  // met after pr.y true and pr.z false frames
+                        cnt[k] = pr[k].y + gr[k].y - pr[k].z;
+                        ms[k] = pr[k].y;
+                    } else {  // never met: the true walk is the merge walk's
+                        cnt[k] = pr[k].y;
+                        xx[k] = pr[k].z;
+                        en[k] = (pr[k].w >> 1) & 1u;
+                        ms[k] = kNone;
+                    }
+                } else {
+                    kn[k] = false;
+                }
+            }
+            excl[k] = run;
+            run += kn[k] ? cnt[k] : 0u;
+            incl[k] = run;
+        }
+        const uint32_t lincl = wave_incl_scan(run, lane);
+        const uint32_t lexcl = lincl - run;
+        uint32_t kb = K;  // this lane's first piece that breaks the chain
+#pragma unroll
+        for (uint32_t k = 0; k < K; ++k) {
+            incl[k] += lexcl;  // frames of the pass up to and including piece k
+            excl[k] += lexcl;  // ... before piece k
+            kn[k] = kn[k] && total + incl[k] <= a.cap;
+            const bool chain = kn[k] && !en[k] && xx[k] == gr[k].z;  // the next entry is true
+            if (kb == K && !chain) kb = k;
+        }
+        const uint32_t first = wave_min_u32(kb < K ? (uint32_t)lane * K + kb : kNone);  // wave-uniform
+        // values of the piece `first` (or of the pass's last piece) from the lane holding it
+        const uint32_t at = first < P ? first : P - 1;
+        const uint32_t atk = at % K;
+        uint32_t v_incl = 0, v_excl = 0, v_x = 0, v_ent = 0, v_en = 0, v_kn = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < K; ++k)
+            if (k == atk) {
+                v_incl = incl[k];
+                v_excl = excl[k];
+                v_x = xx[k];
+                v_ent = ent[k];
+                v_en = en[k];
+                v_kn = kn[k];
+            }
+        const int src = (int)(at / K);
+        v_incl = (uint32_t)__shfl((int)v_incl, src);
+        v_excl = (uint32_t)__shfl((int)v_excl, src);
+        v_x = (uint32_t)__shfl((int)v_x, src);
+        v_ent = (uint32_t)__shfl((int)v_ent, src);
+        v_en = (uint32_t)__shfl((int)v_en, src);
+        v_kn = (uint32_t)__shfl((int)v_kn, src);
+        const bool all = first >= P;  // every piece of the pass chains
+        const uint32_t ntake = all ? P : (v_kn ? first + 1 : first);
+#pragma unroll
+        for (uint32_t k = 0; k < K; ++k) {
+            const uint32_t i = (uint32_t)lane * K + k;
+            if (i < ntake) a.walk[pf + j + i] = make_uint4(ent[k], cnt[k], total + incl[k] - cnt[k], ms[k]);
+        }
+        if (all || v_kn) {
+            j += ntake;
+            total += v_incl;
+            if (!all && v_en) {
+                rpos = v_x;
+                rnfr = total;
+                done = true;
+            } else {
+                e = v_x;  // the next pass starts from the true exit
+            }
+            continue;
+        }
+        // ---- piece j + first: the serial merge walk from its true entry ----
+#ifdef RH_STITCH_STATS
+        ++nser;
+        if (!t_2) t_2 = __builtin_amdgcn_s_memrealtime();
+#endif
+        j += first;
+        total += v_excl;  // the frames of the pieces before it
+        e = v_ent;
+        const uint32_t w = pf + j;
+        uint32_t Bi, Bn;
+        piece_bounds(pd, L, j, Bi, Bn);
+        if (e >= Bn) {  // a frame spans this piece: nothing starts in it
+            if (lane == 0) a.walk[w] = make_uint4(e, 0, total, kNone);
+            ++j;
+            continue;
+        }
+        const uint4 g4 = a.gwalk[w];
+        const uint4 p4 = a.pre[w];
+        const uint32_t g = __builtin_amdgcn_readfirstlane(g4.x);
+        uint32_t cnt1 = __builtin_amdgcn_readfirstlane(g4.y);
+        uint32_t x1 = __builtin_amdgcn_readfirstlane(g4.z);
+        const uint32_t gfl = __builtin_amdgcn_readfirstlane(g4.w);
+        uint32_t ended = gfl & 1u, msteps = 0;
+        const uint32_t pe = __builtin_amdgcn_readfirstlane(p4.x);
+        if (pe == e && g != e) {  // piece_walk_kernel's merge from this entry
+            const uint32_t ma = __builtin_amdgcn_readfirstlane(p4.y);
+            const uint32_t z = __builtin_amdgcn_readfirstlane(p4.z);
+            const uint32_t fm = __builtin_amdgcn_readfirstlane(p4.w);
+            if (fm & 1u) {
+                cnt1 = ma + cnt1 - z;
+                msteps = ma;
+            } else {
+                cnt1 = ma;
+                x1 = z;
+                ended = (fm >> 1) & 1u;
+                msteps = kNone;
+            }
+        } else if (g != e) {
+            const MergeOut r = merge_walk(a, w, make_uint4(g, cnt1, x1, gfl), e, Bn, base, L, lane);
+#ifdef RH_STITCH_STATS
+            if (lane == 0 && s < 4)
+                printf("seg %u piece %u fallback pe=%u e=%u g=%u met=%d m=%u cnt=%u\n", (unsigned)s, j, pe, e, g,
+                       r.msteps != kNone, r.msteps, r.cnt);
+#endif
+            cnt1 = r.cnt;
+            x1 = r.x;
+            ended = r.ended;
+            msteps = r.msteps;
+        }
+        if (total + cnt1 > a.cap) {  // the slot capacity ends inside this piece: serial from e
+            rpos = e;
+            rnfr = total;
+            done = true;
+            break;
+        }
+        if (lane == 0) a.walk[w] = make_uint4(e, cnt1, total, msteps);
+        total += cnt1;
+        ++j;
+        if (ended) {
+            rpos = x1;
+            rnfr = total;
+            done = true;
+            break;
+        }
+        e = x1;
     }
+    if (done)
+        for (uint32_t i = j + (uint32_t)lane; i < np; i += 64) a.walk[pf + i] = kDefault;
     if (!done) {  // unreachable (a header within 8 bytes of EOF ends every fast walk); be exact anyway
         rpos = e;
         rnfr = total;
@@ -1120,6 +1364,12 @@ __global__ __launch_bounds__(64) void piece_stitch_kernel(PieceArgs a) {
         a.resume_pos[s] = rpos;
         a.resume_nfr[s] = rnfr;
     }
+#ifdef RH_STITCH_STATS
+    const uint64_t t_3 = __builtin_amdgcn_s_memrealtime();
+    if (lane == 0 && s < 6)
+        printf("seg %u np %u passes %u serial %u: start->loads %u, ->first serial %u, total %u (x10ns)\n", (unsigned)s, np,
+               npass, nser, (unsigned)(t_1 - t_0), (unsigned)(t_2 ? t_2 - t_0 : 0), (unsigned)(t_3 - t_0));
+#endif
 }
 
 // One wave per piece: the piece's frames into the segment's slots (see above).
@@ -1139,8 +1389,17 @@ __global__ __launch_bounds__(256) void piece_write_kernel(PieceArgs a) {
         const uint4 gw = a.gwalk[w];
         const uint32_t m = r.w;
         if (m != kNone && (gw.w & 2u) && gw.y <= kList) {
-            // frames [0, m): walked from the entry; [m, count): list entries [jj, gcnt)
-            if (lane == 0) {
+            // frames [0, m): the true walk from the entry -- the lengths piece_walk_kernel's merge
+            // walk kept (pre bit 2, same entry), else walked again; [m, count): list entries [jj, gcnt)
+            const uint4 pr = a.pre[w];
+            if (m > 0 && pr.x == r.x && (pr.w & 4u) && pr.y == m) {
+                const uint32_t len = (uint32_t)lane < m ? (uint32_t)a.alen[(uint64_t)w * kAList + lane] : 0u;
+                const uint32_t incl = wave_incl_scan(len, lane);
+                if ((uint32_t)lane < m) {
+                    so[lane] = base + r.x + incl - len;
+                    sl[lane] = len;
+                }
+            } else if (lane == 0) {
                 uint32_t p = r.x;
                 for (uint32_t k = 0; k < m; ++k) {
                     const uint32_t fl = hbm_frame_len(a.buf, base, p, L, a.max_op);
@@ -1222,20 +1481,20 @@ int rh_segments_launch_impl(rh_ctx* ctx, const rh_segments* g, hipStream_t strea
     a.seg_status = g->seg_status;
     a.seg_stop = g->seg_stop;
     const int cus = ctx && ctx->num_cus > 0 ? ctx->num_cus : 256;
-    uint64_t grid = g->n_seg < (uint64_t)cus * 8 ? g->n_seg : (uint64_t)cus * 8;
     // Piece-pass scratch (stream-ordered, from the context's pool): per segment 24 B, per piece
-    // 40 + 2 kList B.  piece_cap bounds the pieces of non-overlapping segments; segments beyond it
+    // 56 + 2 kList + 2 kAList B.  piece_cap bounds the pieces of non-overlapping segments; segments beyond it
     // walk serially.
     const uint64_t n_seg = g->n_seg;
     const uint64_t piece_cap = g->buf_len / kPiece + n_seg + 1;
-    const size_t bytes = (size_t)piece_cap * (40 + 2 * kList) + (size_t)n_seg * 24 + 64;
+    const size_t bytes = (size_t)piece_cap * (56 + 2 * kList + 2 * kAList) + (size_t)n_seg * 24 + 64;
     rh::PoolScratch scratch(stream);  // released on every exit path (after the last pass using it)
     RH_HIP(scratch.alloc(ctx, bytes));
     uint8_t* sp = scratch.bytes();
     PieceArgs pa{};
     pa.gwalk = reinterpret_cast<uint4*>(sp);
     pa.walk = pa.gwalk + piece_cap;
-    pa.resume_pos = reinterpret_cast<uint64_t*>(pa.walk + piece_cap);
+    pa.pre = pa.walk + piece_cap;
+    pa.resume_pos = reinterpret_cast<uint64_t*>(pa.pre + piece_cap);
     pa.piece_first = reinterpret_cast<uint32_t*>(pa.resume_pos + n_seg);
     pa.piece_cnt = pa.piece_first + n_seg;
     uint32_t* seg_gmax = pa.piece_cnt + n_seg;
@@ -1245,6 +1504,7 @@ int rh_segments_launch_impl(rh_ctx* ctx, const rh_segments* g, hipStream_t strea
     pa.piece_seg = reinterpret_cast<uint32_t*>(pa.n_pieces + 4);
     pa.guess = pa.piece_seg + piece_cap;
     pa.plen = reinterpret_cast<uint16_t*>(pa.guess + piece_cap);
+    pa.alen = pa.plen + (size_t)piece_cap * kList;
     pa.buf = g->buf;
     pa.buf_len = g->buf_len;
     pa.seg_off = g->seg_off;
@@ -1288,7 +1548,9 @@ int rh_segments_launch_impl(rh_ctx* ctx, const rh_segments* g, hipStream_t strea
     hipLaunchKernelGGL(segment_scan_kernel, dim3(1), dim3(kScanThreads), 0, stream, g->seg_nframes, g->n_seg,
                        g->frames_per_seg_cap, g->seg_first, g->total_frames);
     RH_HIP(hipGetLastError());
-    hipLaunchKernelGGL(segment_compact_kernel, dim3((uint32_t)grid), dim3(256), 0, stream, g->scratch_off,
+    const uint64_t citems = g->n_seg * ((g->frames_per_seg_cap + kCompactSlots - 1) / kCompactSlots);
+    const uint64_t cgrid = citems < (uint64_t)cus * 8 ? citems : (uint64_t)cus * 8;
+    hipLaunchKernelGGL(segment_compact_kernel, dim3((uint32_t)cgrid), dim3(256), 0, stream, g->scratch_off,
                        g->scratch_len, g->seg_nframes, g->seg_first, g->n_seg, g->frames_per_seg_cap, g->frame_off,
                        g->frame_len, g->frame_cap);
     RH_HIP(hipGetLastError());
