@@ -1060,7 +1060,11 @@ __global__ __launch_bounds__(256) void piece_walk_kernel(PieceArgs a) {
                         met = true;
                         break;
                     }
-                    if (pa >= Bn || (bdone && pa > pb)) break;  // not met: A's walk is the true one
+                    if (pa >= Bn) break;  // not met: A's walk (to the piece end) is the true one
+                    if (bdone && pa > pb) {  // B died before A reached it: a false survivor -- the
+                        give_up = true;      // rest of A's walk is the stitch's (windowed) walk
+                        break;
+                    }
                     if (++steps > 48) {
                         give_up = true;
                         break;
@@ -1112,8 +1116,13 @@ __global__ __launch_bounds__(256) void piece_walk_kernel(PieceArgs a) {
 struct MergeOut {
     uint32_t cnt, x, ended, msteps;
 };
+// The walk streams the segment through two 8 KiB LDS windows (the next one loaded while the
+// current one is walked): a false-survivor guess leaves a whole piece (~125 frames) to walk, and a
+// header load per frame from HBM made that one memory round trip per frame.
+constexpr uint32_t kMergeWin = 8192;
+constexpr uint32_t kMergePer = kMergeWin / (64 * 16);  // 16-B loads per lane per window
 __device__ __forceinline__ MergeOut merge_walk(const PieceArgs& a, uint32_t w, uint4 gr, uint32_t e, uint32_t Bn,
-                                               uint64_t base, uint32_t L, int lane) {
+                                               uint64_t base, uint32_t L, int lane, uint8_t* ring) {
     const uint32_t g = gr.x, gfl = gr.w;
     uint32_t cnt = gr.y, x = gr.z;
     const uint32_t nl = (g != kNone && (gfl & 2u)) ? (cnt < kList ? cnt : kList) : 0u;
@@ -1133,6 +1142,25 @@ __device__ __forceinline__ MergeOut merge_walk(const PieceArgs& a, uint32_t w, u
     const uint32_t last = nl ? g + __builtin_amdgcn_readlane(incl, 63) : 0u;  // end of the listed part
     uint32_t p = e, m = 0, ended = 0;
     bool met = false;
+    // windows: absolute buffer addresses [W, W + kMergeWin), W 16-B aligned; slot 0/1 of ring
+    u32x4s nx[kMergePer];
+    auto fetch = [&](uint64_t W) {
+#pragma unroll
+        for (uint32_t k = 0; k < kMergePer; ++k) {
+            const uint64_t q = W + ((uint64_t)k * 64 + (uint64_t)lane) * 16;
+            nx[k] = q + 16 <= a.buf_len ? *reinterpret_cast<const u32x4s*>(a.buf + q) : u32x4s{0, 0, 0, 0};
+        }
+    };
+    auto put = [&](uint32_t slot) {
+#pragma unroll
+        for (uint32_t k = 0; k < kMergePer; ++k)
+            *reinterpret_cast<u32x4s*>(ring + slot * kMergeWin + ((uint32_t)k * 64 + (uint32_t)lane) * 16) = nx[k];
+    };
+    uint64_t Wc = (base + p) & ~15ull, Wn = Wc + kMergeWin;
+    uint32_t slot = 0;
+    fetch(Wc);
+    put(0);
+    fetch(Wn);
     while (p < Bn) {
         if (p < last) {
             uint32_t jl = kNone;
@@ -1147,7 +1175,29 @@ __device__ __forceinline__ MergeOut merge_walk(const PieceArgs& a, uint32_t w, u
                 break;
             }
         }
-        const uint32_t fl = hbm_frame_len(a.buf, base, p, L, a.max_op);
+        if (p + 8 >= L) {  // hbm_frame_len's EOF zone: the fast walk ends
+            ended = 1;
+            break;
+        }
+        const uint64_t q = base + p;
+        if ((q & ~3ull) + 8 > Wc + kMergeWin) {  // the header is not inside the current window
+            if ((q & ~3ull) >= Wn && (q & ~3ull) + 8 <= Wn + kMergeWin) {
+                slot ^= 1u;
+                put(slot);  // the prefetched next window
+                Wc = Wn;
+            } else {        // a long frame jumped past it: load the window at q
+                Wc = q & ~15ull;
+                fetch(Wc);
+                slot ^= 1u;
+                put(slot);
+            }
+            Wn = Wc + kMergeWin;
+            fetch(Wn);
+        }
+        const uint32_t o = (uint32_t)((q & ~3ull) - Wc) + slot * kMergeWin;
+        const uint32_t hv = __builtin_amdgcn_alignbyte(*reinterpret_cast<const uint32_t*>(ring + o + 4),
+                                                       *reinterpret_cast<const uint32_t*>(ring + o), (uint32_t)(q & 3u));
+        const uint32_t fl = fast_frame_len(hv, L - p, a.max_op);
         if (fl == 0) {
             ended = 1;
             break;
@@ -1161,6 +1211,7 @@ __device__ __forceinline__ MergeOut merge_walk(const PieceArgs& a, uint32_t w, u
 
 // One wave per segment: the true chain through the pieces (see above).  Control is wave-uniform.
 __global__ __launch_bounds__(64) void piece_stitch_kernel(PieceArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t ring[2 * kMergeWin];  // merge_walk's windows
     const uint64_t s = blockIdx.x;
 #ifdef RH_STITCH_STATS
     const uint64_t t_0 = __builtin_amdgcn_s_memrealtime();
@@ -1326,11 +1377,11 @@ __global__ __launch_bounds__(64) void piece_stitch_kernel(PieceArgs a) {
                 msteps = kNone;
             }
         } else if (g != e) {
-            const MergeOut r = merge_walk(a, w, make_uint4(g, cnt1, x1, gfl), e, Bn, base, L, lane);
+            const MergeOut r = merge_walk(a, w, make_uint4(g, cnt1, x1, gfl), e, Bn, base, L, lane, ring);
 #ifdef RH_STITCH_STATS
-            if (lane == 0 && s < 4)
-                printf("seg %u piece %u fallback pe=%u e=%u g=%u met=%d m=%u cnt=%u\n", (unsigned)s, j, pe, e, g,
-                       r.msteps != kNone, r.msteps, r.cnt);
+            if (lane == 0)
+                printf("FALLBACK seg %u piece %u pe=%u e=%u g=%u Bi=%u met=%d m=%u cnt=%u gcnt=%u pflags=%u\n", (unsigned)s, j,
+                       pe, e, g, Bi, r.msteps != kNone, r.msteps, r.cnt, cnt1, __builtin_amdgcn_readfirstlane(p4.w));
 #endif
             cnt1 = r.cnt;
             x1 = r.x;
@@ -1366,9 +1417,10 @@ __global__ __launch_bounds__(64) void piece_stitch_kernel(PieceArgs a) {
     }
 #ifdef RH_STITCH_STATS
     const uint64_t t_3 = __builtin_amdgcn_s_memrealtime();
-    if (lane == 0 && s < 6)
-        printf("seg %u np %u passes %u serial %u: start->loads %u, ->first serial %u, total %u (x10ns)\n", (unsigned)s, np,
-               npass, nser, (unsigned)(t_1 - t_0), (unsigned)(t_2 ? t_2 - t_0 : 0), (unsigned)(t_3 - t_0));
+    if (lane == 0)
+        printf("STITCH seg %u np %u passes %u serial %u t0 %llu loads %u first_serial %u end %u\n", (unsigned)s, np,
+               npass, nser, (unsigned long long)t_0, (unsigned)(t_1 - t_0), (unsigned)(t_2 ? t_2 - t_0 : 0),
+               (unsigned)(t_3 - t_0));
 #endif
 }
 
@@ -1434,6 +1486,10 @@ __global__ __launch_bounds__(256) void piece_write_kernel(PieceArgs a) {
         }
     }
 }
+
+#ifdef RH_AB_FENCE_PROBE
+__global__ void empty_probe_kernel(int) {}
+#endif
 
 constexpr int kWalkWindow = 32768;  // 2 x 32 KiB LDS ring + mirror: two blocks per CU
 
@@ -1534,6 +1590,9 @@ int rh_segments_launch_impl(rh_ctx* ctx, const rh_segments* g, hipStream_t strea
     const uint64_t wgrid = (piece_cap + 255) / 256 < (uint64_t)cus * 8 ? (piece_cap + 255) / 256 : (uint64_t)cus * 8;
     hipLaunchKernelGGL(piece_walk_kernel, dim3((uint32_t)wgrid), dim3(256), 0, stream, pa);
     RH_HIP(hipGetLastError());
+#ifdef RH_AB_FENCE_PROBE
+    hipLaunchKernelGGL(empty_probe_kernel, dim3((uint32_t)n_seg), dim3(64), 0, stream, 0);
+#endif
     hipLaunchKernelGGL(piece_stitch_kernel, dim3((uint32_t)n_seg), dim3(64), 0, stream, pa);
     RH_HIP(hipGetLastError());
     const uint64_t pgrid = (piece_cap + 3) / 4 < (uint64_t)cus * 8 ? (piece_cap + 3) / 4 : (uint64_t)cus * 8;
