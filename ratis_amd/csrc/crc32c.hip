@@ -979,6 +979,7 @@ struct PackArgs {
     const uint32_t* inv;               // build_crc_inverse_lane_tables()
     const uint32_t* z64;               // [4][256] advance over 64 zero bytes
     const uint32_t* z2k;               // [4][256] advance over 2048 zero bytes (uniform lookups)
+    const uint32_t* z4k;               // [4][256] advance over 4096 zero bytes (uniform lookups)
     const uint32_t* initv;             // [kCrcInitSpan + 1]: A^k(init)
     const uint64_t* seg_first;         // slot mode: dense frame d lives in segment upper_bound - 1
     const unsigned long long* total;   // slot mode: frames in the dense numbering
@@ -1041,7 +1042,10 @@ __device__ __forceinline__ uint32_t fold16(const uint32_t* lds, const uint32_t* 
 }
 
 template <bool SLOT>
-__global__ __launch_bounds__(kCrcThreads) void crc_pack_kernel(PackArgs p) {
+__global__ __launch_bounds__(kCrcThreads) void crc_pack_kernel(PackArgs pk_arg) {
+    // slot variant: fields read from the kernarg segment where used (scalar loads the compiler can
+    // repeat), not held in SGPRs across the step loop -- its extra pointers spilled
+    const PackArgs& p = SLOT ? rh::kernarg_struct<PackArgs>() : pk_arg;
     const FrameArgs& a = p.f;
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
     if (__builtin_amdgcn_groupstaticsize() != 0) __builtin_trap();  // lds_word assumes base 0
@@ -1074,8 +1078,7 @@ __global__ __launch_bounds__(kCrcThreads) void crc_pack_kernel(PackArgs p) {
         // ---- the task's 64 frames: lane j holds frame j ----
         const uint64_t d = t * 64 + (uint64_t)lane;
         const bool have = d < nfr;
-        uint64_t f = d, seg = 0;
-        uint32_t slot = 0;
+        uint32_t f = (uint32_t)d;  // table entry (the launcher keeps tables below 2^32 entries)
         if (SLOT) {
             // the task's first frame: the largest segment with seg_first <= 64 t (seg_first[0] = 0),
             // a wave-uniform search (scalar loads); a lane past that segment's end steps forward
@@ -1091,7 +1094,7 @@ __global__ __launch_bounds__(kCrcThreads) void crc_pack_kernel(PackArgs p) {
                 if (first_of(mid) <= d0) lo = mid;
                 else hi = mid;
             }
-            seg = lo;
+            uint64_t seg = lo;
             uint64_t next = seg + 1 < p.n_seg ? first_of(seg + 1) : ~0ull;
             uint64_t base = first_of(seg);
             while (__any(have && d >= next)) {  // rare: the task crosses into later segments
@@ -1101,8 +1104,7 @@ __global__ __launch_bounds__(kCrcThreads) void crc_pack_kernel(PackArgs p) {
                     next = seg + 1 < p.n_seg ? p.seg_first[seg + 1] : ~0ull;
                 }
             }
-            slot = (uint32_t)(d - base);
-            f = seg * (uint64_t)a.slot_cap + slot;
+            f = (uint32_t)(seg * (uint64_t)a.slot_cap + (d - base));
         }
         uint64_t o = 0;
         uint32_t L = 0;
@@ -1212,6 +1214,8 @@ __global__ __launch_bounds__(kCrcThreads) void crc_pack_kernel(PackArgs p) {
             for (int i = 0; i < 16; ++i) w[i] = __builtin_amdgcn_alignbyte(dc[i + 1], dc[i], cur.sh);
             uint32_t R = fold16(lds, lch, w, lb);
             R ^= cur.i == 1u ? cur.fs : 0u;
+            const uint32_t K0 = zshift_uniform(p.z2k, carry);  // off the step's dependent chain
+            const uint32_t C4 = zshift_uniform(p.z4k, carry);
             uint32_t y = 0;
 #pragma unroll
             for (int q = 0; q < 8; ++q) y ^= lf[c + ((uint32_t)(q * 16) + ((R >> (4 * q)) & 15u)) * 32u];
@@ -1223,9 +1227,11 @@ __global__ __launch_bounds__(kCrcThreads) void crc_pack_kernel(PackArgs p) {
             const uint32_t before = (uint32_t)__shfl((int)px, src < 0 ? 0 : src);
             const uint32_t seg = px ^ (cont ? 0u : (src >= (int)hs ? before : 0u));
             const uint64_t contM = __ballot(cont);
-            const uint32_t K0 = zshift_uniform(p.z2k, carry);  // the carried frame at the end of half 0
+            // the carried frame at the end of half 0 (K0) and of half 1 -- by linearity the half-1
+            // term splits into Z2k(half 0's running frame) ^ Z4k(carry): only the former waits on
+            // this step's prefix
             const uint32_t s31 = (uint32_t)__builtin_amdgcn_readlane((int)seg, 31);
-            const uint32_t K1 = zshift_uniform(p.z2k, s31 ^ (((contM >> 31) & 1u) ? K0 : 0u));
+            const uint32_t K1 = zshift_uniform(p.z2k, s31) ^ (((contM >> 31) & 1u) ? C4 : 0u);
             const uint32_t tot = seg ^ (cont ? (hs ? K1 : K0) : 0u);
             const bool ends = cur.valid && cur.m == 0u;
             if (ends) vst[cur.j] = tot;
@@ -1259,11 +1265,12 @@ __global__ __launch_bounds__(kCrcThreads) void crc_pack_kernel(PackArgs p) {
             }
             if (!SLOT) {
                 emit_frame(a, f, value, bad);
-            } else {  // emit_frame's slot mode, with the segment and dense index already known
+            } else {  // emit_frame's slot mode, with the dense index already known
                 if (a.crc_out) a.crc_out[f] = value;
                 if (bad) {
                     if (a.n_bad) atomicAdd(a.n_bad, 1ull);
-                    if (a.seg_first_bad) atomicMin(a.seg_first_bad + seg, slot);
+                    const uint32_t seg = f / a.slot_cap;
+                    if (a.seg_first_bad) atomicMin(a.seg_first_bad + seg, f - seg * a.slot_cap);
                 }
                 if (d < a.frame_cap) {
                     if (a.dense_crc) a.dense_crc[d] = value;
@@ -1332,6 +1339,7 @@ int launch_pack(rh_ctx* ctx, FrameArgs a, const SlotPlan& sp, hipStream_t stream
     p.inv = ctx->d_inv32;
     p.z64 = ctx->d_shift + (size_t)6 * 1024;
     p.z2k = ctx->d_shift + (size_t)11 * 1024;
+    p.z4k = ctx->d_shift + (size_t)12 * 1024;
     p.seg_first = sp.seg_first;
     p.total = sp.total;
     p.n_seg = sp.n_seg;

@@ -30,7 +30,10 @@ def _usage():
 # spill a few registers of their widest (joint-consensus) path.  Same-box A/B of the commit kernel
 # at 8, 7 and 6 waves per SIMD (21, 4 and 0 spilled VGPRs): 4.53-4.62 TB/s for all three
 # (profiles/r02/commit_waves/), so the pin stays; the allowance is a few dozen bytes per lane.
-SPILL_ALLOWED = {"commit_kernel_rank": 48, "leader_kernel": 48, "lease_kernel": 32}
+# crc_pack_kernel<true> (the read path's slot mode) runs at the 128-VGPR cap of its 1024-thread
+# workgroup: a few per-lane constants are stored at kernel entry and reloaded once per 64-frame
+# task (a few scratch loads per task, none in the step loop; gfx950 ISA checked, round 3).
+SPILL_ALLOWED = {"commit_kernel_rank": 48, "leader_kernel": 48, "lease_kernel": 32, "crc_pack_kernel": 24}
 
 
 def test_no_kernel_uses_scratch():
