@@ -847,6 +847,10 @@ __global__ __launch_bounds__(kPieceThreads) void piece_guess_kernel(PieceArgs a)
 #define RH_GUESS_WAVE_BLOCKS_PER_CU 8  // 8 x 16.5 KB windows of LDS per CU
 #endif
 constexpr int kGuessWaveBlocksPerCu = RH_GUESS_WAVE_BLOCKS_PER_CU;
+#ifndef RH_GUESS_WIN_MULT  // A/B builds override: survival window = this many gmax (4..16 KiB)
+#define RH_GUESS_WIN_MULT 4
+#endif
+constexpr uint32_t kWinMult = RH_GUESS_WIN_MULT;
 
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
 #pragma unroll
@@ -897,7 +901,7 @@ __global__ __launch_bounds__(64) void piece_guess_wave_kernel(PieceArgs a) {
         piece_bounds((uint32_t)a.seg_stop[it.s], it.L, w - a.piece_first[it.s], it.Bi, Bn);
         const uint32_t gm0 = a.seg_gmax[it.s] * 2u;
         it.gmax = gm0 < 1024u ? 1024u : gm0 > kGuessWin ? kGuessWin : gm0;
-        const uint32_t win = 4u * it.gmax < 4096u ? 4096u : 4u * it.gmax > kGuessWin ? kGuessWin : 4u * it.gmax;
+        const uint32_t win = kWinMult * it.gmax < 4096u ? 4096u : kWinMult * it.gmax > kGuessWin ? kGuessWin : kWinMult * it.gmax;
         it.We = Bn - it.Bi > win ? it.Bi + win : Bn;
         it.o0 = (uint32_t)((it.base + it.Bi) & 15u);
         const uint32_t rend = it.L - it.We > 32u ? it.We + 32u : it.L;
@@ -1121,8 +1125,9 @@ struct MergeOut {
 // header load per frame from HBM made that one memory round trip per frame.
 constexpr uint32_t kMergeWin = 8192;
 constexpr uint32_t kMergePer = kMergeWin / (64 * 16);  // 16-B loads per lane per window
+// rec (LDS, kList entries): the true walk's frame lengths as walked (lane 0 stores them).
 __device__ __forceinline__ MergeOut merge_walk(const PieceArgs& a, uint32_t w, uint4 gr, uint32_t e, uint32_t Bn,
-                                               uint64_t base, uint32_t L, int lane, uint8_t* ring) {
+                                               uint64_t base, uint32_t L, int lane, uint8_t* ring, uint16_t* rec) {
     const uint32_t g = gr.x, gfl = gr.w;
     uint32_t cnt = gr.y, x = gr.z;
     const uint32_t nl = (g != kNone && (gfl & 2u)) ? (cnt < kList ? cnt : kList) : 0u;
@@ -1202,6 +1207,7 @@ __device__ __forceinline__ MergeOut merge_walk(const PieceArgs& a, uint32_t w, u
             ended = 1;
             break;
         }
+        if (lane == 0 && m < kList) rec[m] = (uint16_t)(fl < 65536u ? fl : 0u);
         ++m;
         p += fl;
     }
@@ -1212,6 +1218,7 @@ __device__ __forceinline__ MergeOut merge_walk(const PieceArgs& a, uint32_t w, u
 // One wave per segment: the true chain through the pieces (see above).  Control is wave-uniform.
 __global__ __launch_bounds__(64) void piece_stitch_kernel(PieceArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t ring[2 * kMergeWin];  // merge_walk's windows
+    __shared__ uint16_t rec[kList];                                        // ... and its frame lengths
     const uint64_t s = blockIdx.x;
 #ifdef RH_STITCH_STATS
     const uint64_t t_0 = __builtin_amdgcn_s_memrealtime();
@@ -1377,7 +1384,7 @@ __global__ __launch_bounds__(64) void piece_stitch_kernel(PieceArgs a) {
                 msteps = kNone;
             }
         } else if (g != e) {
-            const MergeOut r = merge_walk(a, w, make_uint4(g, cnt1, x1, gfl), e, Bn, base, L, lane, ring);
+            const MergeOut r = merge_walk(a, w, make_uint4(g, cnt1, x1, gfl), e, Bn, base, L, lane, ring, rec);
 #ifdef RH_STITCH_STATS
             if (lane == 0)
                 printf("FALLBACK seg %u piece %u pe=%u e=%u g=%u Bi=%u met=%d m=%u cnt=%u gcnt=%u pflags=%u\n", (unsigned)s, j,
@@ -1387,6 +1394,23 @@ __global__ __launch_bounds__(64) void piece_stitch_kernel(PieceArgs a) {
             x1 = r.x;
             ended = r.ended;
             msteps = r.msteps;
+            if (msteps == kNone) {
+                // never met: the walk just made IS the piece's true walk -- its lengths become the
+                // piece's list and its guessed walk, so piece_write expands them (instead of
+                // re-walking every frame of the piece through HBM)
+                const uint32_t nr = cnt1 < kList ? cnt1 : kList;
+                bool fits = cnt1 <= kList;
+                __builtin_amdgcn_wave_barrier();
+                uint16_t* pl = a.plen + (uint64_t)w * kList;
+                for (uint32_t i = (uint32_t)lane; i < nr; i += 64) {
+                    const uint16_t v = rec[i];
+                    pl[i] = v;
+                    fits = fits && v != 0;
+                }
+                fits = __builtin_amdgcn_ballot_w64(!fits) == 0;
+                if (lane == 0) a.gwalk[w] = make_uint4(e, cnt1, x1, ended | (fits ? 2u : 0u));
+                msteps = 0;
+            }
         }
         if (total + cnt1 > a.cap) {  // the slot capacity ends inside this piece: serial from e
             rpos = e;
