@@ -560,10 +560,13 @@ __global__ __launch_bounds__(kCrcThreads) void crc_frames_kernel(FrameArgs a) {
                 const int64_t be = E - (nw - 1 - wi) * W - (int64_t)(Q - 1 - gl) * S;
                 const int64_t bs = be - S > m.o ? be - S : m.o;
                 uint32_t r = 0;
-                for (int64_t p = bs; p < be; ++p) {  // byte-wise, reset()'s state in bytes 0..3
+                // byte-wise, reset()'s state in bytes 0..3; T0 from this lane's LDS copy (a global
+                // table made every byte a dependent L2 round trip: ~13 us per 1 KiB window)
+#pragma unroll 4
+                for (int64_t p = bs; p < be; ++p) {
                     uint32_t b = a.buf[p];
                     if (p - m.o < 4) b ^= (a.init >> (8 * (p - m.o))) & 0xffu;
-                    r = (r >> 8) ^ a.slice[(r ^ b) & 0xffu];
+                    r = (r >> 8) ^ lds_word(lds, (((r ^ b) & 0xffu) << 8) | (c << 2));
                 }
                 uint32_t z = 0;
 #pragma unroll

@@ -847,6 +847,9 @@ __global__ __launch_bounds__(kPieceThreads) void piece_guess_kernel(PieceArgs a)
 #define RH_GUESS_WAVE_BLOCKS_PER_CU 8  // 8 x 16.5 KB windows of LDS per CU
 #endif
 constexpr int kGuessWaveBlocksPerCu = RH_GUESS_WAVE_BLOCKS_PER_CU;
+#ifndef RH_GUESS_SLOTS  // A/B builds override: candidate slots per lane in the refill loop
+#define RH_GUESS_SLOTS 1
+#endif
 #ifndef RH_GUESS_WIN_MULT  // A/B builds override: survival window = this many gmax (4..16 KiB)
 #define RH_GUESS_WIN_MULT 4
 #endif
@@ -922,8 +925,9 @@ __global__ __launch_bounds__(64) void piece_guess_wave_kernel(PieceArgs a) {
     Item cur = describe(w);
     if (w < total) issue(cur);
     while (w < total) {
-        unsigned int lastnz = 0;
         const uint8_t* src = a.buf + cur.base + cur.Bi - cur.o0;
+        const uint32_t qend0 = cur.We - cur.Bi + cur.o0;  // window end (image index)
+        bool tailnz = false;  // a non-zero 16 bytes wholly in [window end, region end)
 #pragma unroll
         for (uint32_t k = 0; k < kPer; ++k) {
             const uint32_t c = ((uint32_t)t + k * 64u) * 16u;
@@ -934,16 +938,29 @@ __global__ __launch_bounds__(64) void piece_guess_wave_kernel(PieceArgs a) {
                 v[k] = {wv[0], wv[1], wv[2], wv[3]};
             }
             *reinterpret_cast<u32x4s*>(img + c) = v[k];
-            const uint32_t ww[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
-#pragma unroll
-            for (int q = 3; q >= 0; --q)
-                if (ww[q]) {
-                    const unsigned int e = c + 4u * q + 4u - (__builtin_clz(ww[q]) >> 3);
-                    lastnz = e > lastnz ? e : lastnz;
-                    break;
-                }
+            tailnz = tailnz || (c >= qend0 && c + 16 <= cur.ilen && (v[k].x | v[k].y | v[k].z | v[k].w) != 0);
         }
-        const unsigned int zimg = wave_max_u32(lastnz);
+        // Where the window's all-zero tail starts (the terminator test of the survival rule) matters
+        // only if it starts inside the window: a non-zero byte past the window end rules that out
+        // (every mid-segment piece); else the exact position, from the registers still held.
+        unsigned int zimg = cur.ilen;
+        if (!__any(tailnz)) {
+            unsigned int lastnz = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < kPer; ++k) {
+                const uint32_t c = ((uint32_t)t + k * 64u) * 16u;
+                if (c >= kGuessLds) continue;
+                const uint32_t ww[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+                for (int q = 3; q >= 0; --q)
+                    if (ww[q]) {
+                        const unsigned int e = c + 4u * q + 4u - (__builtin_clz(ww[q]) >> 3);
+                        lastnz = e > lastnz ? e : lastnz;
+                        break;
+                    }
+            }
+            zimg = wave_max_u32(lastnz);
+        }
         __syncthreads();  // the window is in LDS (one wave: a wait, not a rendezvous)
         const unsigned int w2 = find(w + gridDim.x);
         const Item nxt = describe(w2);
@@ -956,7 +973,9 @@ __global__ __launch_bounds__(64) void piece_guess_wave_kernel(PieceArgs a) {
         const uint32_t qend = We - Bi + o0;
         const uint32_t qeof = L >= Bi + 8 ? L - 8 - Bi + o0 : 0u;
         const uint32_t qz = zpos - Bi + o0;
-        uint32_t best = kNone, limit = ncand, next = 64u;
+        uint32_t best = kNone, limit = ncand;
+#if RH_GUESS_SLOTS == 1
+        uint32_t next = 64u;
         uint32_t cand = (uint32_t)t, q = cand + o0;
         bool run = cand < limit;
         while (__any(run)) {
@@ -985,6 +1004,51 @@ __global__ __launch_bounds__(64) void piece_guess_wave_kernel(PieceArgs a) {
                 next += (uint32_t)__popcll(freeb);
             }
         }
+#else
+        // two candidate slots per lane, walked in lockstep (their LDS reads issued together: the
+        // loop is latency-bound); refill hands the next candidates to slot A's free lanes, then
+        // slot B's, in lane order -- still every candidate below the lowest survivor is walked
+        // until it dies, so the guess is the same
+        uint32_t next = 128u;
+        uint32_t candA = (uint32_t)t, qA = candA + o0, candB = 64u + (uint32_t)t, qB = candB + o0;
+        bool runA = candA < limit, runB = candB < limit;
+        while (__any(runA || runB)) {
+            const bool outA = qA >= qend || qA >= qeof, outB = qB >= qend || qB >= qeof;
+            const uint32_t qa = outA ? 0u : qA, qb = outB ? 0u : qB;
+            const uint32_t hvA = __builtin_amdgcn_alignbyte(img32[(qa >> 2) + 1], img32[qa >> 2], qa & 3u);
+            const uint32_t hvB = __builtin_amdgcn_alignbyte(img32[(qb >> 2) + 1], img32[qb >> 2], qb & 3u);
+            const uint32_t flA = fast_frame_len(hvA, L - (Bi + qA - o0), a.max_op);
+            const uint32_t flB = fast_frame_len(hvB, L - (Bi + qB - o0), a.max_op);
+            const bool survA = runA && (outA || (flA == 0 && qA >= qz));
+            const bool survB = runB && (outB || (flB == 0 && qB >= qz));
+            if (__any(survA || survB)) {
+                const uint32_t sA = survA ? candA : kNone, sB = survB ? candB : kNone;
+                best = min(best, wave_min_u32(sA < sB ? sA : sB));
+                limit = best;
+            }
+            runA = runA && !survA && !outA && flA != 0 && flA <= gmax && candA < limit;
+            runB = runB && !survB && !outB && flB != 0 && flB <= gmax && candB < limit;
+            qA += runA ? flA : 0u;
+            qB += runB ? flB : 0u;
+            const uint64_t fa = __ballot(!runA), fb = __ballot(!runB);
+            if ((fa | fb) != 0 && next < limit) {
+                const uint32_t na = (uint32_t)__popcll(fa);
+                const uint32_t ka = __builtin_amdgcn_mbcnt_hi((uint32_t)(fa >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fa, 0u));
+                const uint32_t kb = na + __builtin_amdgcn_mbcnt_hi((uint32_t)(fb >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fb, 0u));
+                if (!runA) {
+                    candA = next + ka;
+                    qA = candA + o0;
+                    runA = candA < limit;
+                }
+                if (!runB) {
+                    candB = next + kb;
+                    qB = candB + o0;
+                    runB = candB < limit;
+                }
+                next += na + (uint32_t)__popcll(fb);
+            }
+        }
+#endif
         if (t == 0) a.guess[w] = best == kNone ? kNone : Bi + best;
         __syncthreads();  // the window may be overwritten
         w = w2;
