@@ -1118,7 +1118,8 @@ __global__ __launch_bounds__(kCrcThreads) void crc_pack_kernel(PackArgs pk_arg) 
         const bool malformed = o > (uint64_t)a.buf_len || (int64_t)L > a.buf_len - (int64_t)o || L < tl;
         const int64_t lcs = (int64_t)L - (int64_t)tl;
         const int64_t E = (int64_t)o + lcs;
-        const bool pk = have && !malformed && o >= 67 && E + 8 <= a.buf_len && lcs >= 8 && lcs <= (int64_t)rh::kCrcInitSpan;
+        // (frames within 67 bytes of the buffer start: chunk 0's words before byte 0 load as zero)
+        const bool pk = have && !malformed && E + 8 <= a.buf_len && lcs >= 8 && lcs <= (int64_t)rh::kCrcInitSpan;
         const bool left = have && !pk;
         const uint64_t lb_left = __ballot(left);
         if (lb_left) {  // the window kernel's frames (guarded, malformed, long)
@@ -1148,7 +1149,14 @@ __global__ __launch_bounds__(kCrcThreads) void crc_pack_kernel(PackArgs pk_arg) 
         uint32_t f0, fs;
         {
             uint32_t dd[17];
-            load_chunk(pk ? a.buf + (E - 64 * (int64_t)k - 64 - sh) : a.buf, dd);
+            const int64_t b0 = E - 64 * (int64_t)k - 64 - (int64_t)sh;  // chunk 0's 4-aligned start
+            if (__any(pk && b0 < 0)) {  // a frame near the buffer start (rare): word by word
+#pragma unroll
+                for (int i = 0; i < 17; ++i)
+                    dd[i] = pk && b0 + 4 * i >= 0 ? *reinterpret_cast<const uint32_t*>(a.buf + b0 + 4 * i) : 0u;
+            } else {
+                load_chunk(pk ? a.buf + b0 : a.buf, dd);
+            }
             uint32_t w[16];
             const int32_t g8 = 8 * (int32_t)((k + 1) * 64 - lc);  // 8 x bytes before the frame
 #pragma unroll
