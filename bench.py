@@ -295,10 +295,10 @@ def table_commit_leg(ctx, host, reps: int = 8, fracs=(1.0, 0.1), pmc=None) -> di
     """The kernel the Java module drives: rh_commit_batch over the resident table (config-3
     groups, stable F=4 and joint F=6 tiers), after deltas marked `frac` of the groups dirty (one
     matchIndex / flushIndex update per dirty group, as delta_streaming's steps).  Timed on the
-    table's own stream with HIP events around each rh_commit_batch_async (counter reset + the
-    evaluation kernel + the 8-byte count read-back), for both event sinks: RH_EVENTS_DEVICE (events
-    staged in HBM: the kernel alone, `roofline`) and RH_EVENTS_HOST_MAPPED (records written across
-    PCIe by the kernel).  Results are checked against a second table fed the same deltas and
+    table's own stream with HIP events around each rh_commit_batch_async (the evaluation kernel
+    alone: list lengths come back through host-mapped per-workgroup ends, no memset or read-back on
+    the stream), for both event sinks: RH_EVENTS_DEVICE (events staged in HBM, `roofline`) and
+    RH_EVENTS_HOST_MAPPED (records written across PCIe by the kernel).  Results are checked against a second table fed the same deltas and
     evaluated with the other sink (the events must be identical)."""
     import torch
 
@@ -367,8 +367,7 @@ def table_commit_leg(ctx, host, reps: int = 8, fracs=(1.0, 0.1), pmc=None) -> di
             "sinks_agree": res["sinks_agree"],
             "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(ach / HBM_PEAK_GBPS, 4), "algorithmic_bytes_per_launch": int(alg),
-                         "kernel": "table_commit_kernel_rank<false> (events staged in HBM), incl. counter reset "
-                                   "and count read-back",
+                         "kernel": "table_commit_kernel_rank<false> (events staged in HBM)",
                          # PMC passes (scripts/prof_kernels.py table case) run the all-dirty step
                          "traffic": (round(pmc["table_bytes_per_unit"] * n_all)
                                      if frac >= 1.0 and pmc and "table_bytes_per_unit" in pmc else None),
@@ -381,7 +380,7 @@ def table_commit_leg(ctx, host, reps: int = 8, fracs=(1.0, 0.1), pmc=None) -> di
     return out
 
 
-def ragged_read_path(ctx, args, rank, stream, barrier, max_over_ranks, sum_over_ranks) -> dict:
+def ragged_read_path(ctx, args, rank, stream, barrier, max_over_ranks, sum_over_ranks, pmc=None) -> dict:
     """Segments of differently sized frames (64-2048 B, seeded random payloads, 1 in 10^5 frames
     with a flipped payload bit): framing alone (the serial walk defers each segment after its first
     window to the piece-parallel pass) and rh_segments_read_launch (framing + CRC verify + verdict).
@@ -443,15 +442,19 @@ def ragged_read_path(ctx, args, rank, stream, barrier, max_over_ranks, sum_over_
     out = {"workload": f"{n} x 32 MiB segments/GPU, frames of 64-2048 B ({nf} frames/GPU, {rs.corrupted.size} corrupted)",
            "framing_GBps": round(tot / (max_over_ranks(scan_ms) * 1e-3) / 1e9, 1), "ms_framing": round(scan_ms, 4),
            "framing_note": ("serial walk of the first window, then piece-parallel framing (128 KiB pieces: LDS guess "
-                            "over 16 KiB, lane walks over HBM headers recording frame lengths, stitch by list merge, "
-                            "list expansion into the slots), resume pass"),
+                            "over 16 KiB, lane walks over HBM headers recording frame lengths and the next piece's "
+                            "merge, stitch in parallel passes, list expansion into the slots), resume pass"),
            "read_launch_GBps": round(tot / (max_over_ranks(rl_ms) * 1e-3) / 1e9, 1), "ms_read_launch": round(rl_ms, 4),
            "parity_ok": bool(frame_ok and rl_ok and orc_ok),
            "parity_check": "frame table == generator's, mismatch set == planted set, CRCs == stamped, 2 segments == oracle reader",
            "roofline": {"bound": "hbm", "achieved": round(read_ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                         "frac": round(read_ach / HBM_PEAK_GBPS, 4),
-                        "kernel": "rh_segments_read_launch (piece framing + crc_frames_kernel slot mode + verdict)",
-                        "algorithmic_bytes_per_launch": read_alg, "avg_launch_ms": round(rl_ms, 4)}}
+                        "kernel": "rh_segments_read_launch (piece framing + crc_pack_kernel slot mode + verdict)",
+                        "algorithmic_bytes_per_launch": read_alg, "avg_launch_ms": round(rl_ms, 4),
+                        # every kernel of one read launch, PMC (scripts/pmc_ragged.py), per segment byte
+                        "traffic": (round(pmc["ragged_read_bytes_per_unit"] * seg_bytes)
+                                    if pmc and "ragged_read_bytes_per_unit" in pmc else None),
+                        "traffic_source": (pmc or {}).get("_src", {}).get("ragged_read")}}
     del sb, fbatch, fout, rs
     return out
 
@@ -866,7 +869,7 @@ def main():
         torch.cuda.empty_cache()
         if args.ragged_segments:
             crc["read_path"]["ragged"] = ragged_read_path(ctx, args, rank, stream, barrier, max_over_ranks,
-                                                          sum_over_ranks)
+                                                          sum_over_ranks, pmc=pmc)
             torch.cuda.empty_cache()
 
     # ------------------------------------------------------------------ CPU baseline (rank 0, N = 1)
