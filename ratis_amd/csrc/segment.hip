@@ -568,7 +568,11 @@ __global__ __launch_bounds__(256) void segment_compact_kernel(const uint64_t* sc
 #define RH_PIECE_BYTES 131072
 #define RH_PIECE_LIST 1024
 #endif
-constexpr uint32_t kPiece = RH_PIECE_BYTES;  // bytes per piece
+constexpr uint32_t kPiece = RH_PIECE_BYTES;  // bytes per piece (or twice that: see piece_plan_kernel)
+#ifndef RH_PIECE_ADAPT  // A/B builds override: 0 = every segment at kPiece
+#define RH_PIECE_ADAPT 1
+#endif
+constexpr uint32_t kBigPieceMean = 512;  // mean frame bytes from which a segment takes 2 kPiece
 #ifndef RH_GUESS_WIN  // A/B builds override (scripts/ab_build.sh)
 #define RH_GUESS_WIN 16384
 #define RH_PIECE_THREADS 256
@@ -638,6 +642,7 @@ struct PieceArgs {
     const uint32_t* seg_gmax;
     uint32_t* piece_first;       // [n_seg] first work item of the segment
     uint32_t* piece_cnt;         // [n_seg] pieces of the segment (0: serial resume from p_d)
+    uint32_t* seg_psz;           // [n_seg] piece size of the segment (bytes)
     uint32_t* piece_seg;         // [piece_cap] segment of each work item (kNone: none)
     unsigned int* n_pieces;      // work items in use
     uint32_t* guess;             // [piece_cap] g (kNone: no survivor)
@@ -653,9 +658,10 @@ struct PieceArgs {
 };
 
 // Segment-relative bounds of piece i: [Bi, Bn).
-__device__ __forceinline__ void piece_bounds(uint32_t pd, uint32_t L, uint32_t i, uint32_t& Bi, uint32_t& Bn) {
-    Bi = pd + i * kPiece;
-    Bn = L - Bi > kPiece ? Bi + kPiece : L;
+__device__ __forceinline__ void piece_bounds(uint32_t pd, uint32_t L, uint32_t i, uint32_t P, uint32_t& Bi,
+                                             uint32_t& Bn) {
+    Bi = pd + i * P;
+    Bn = L - Bi > P ? Bi + P : L;
 }
 
 // One block: pieces per deferred segment (prefix sum) and the work-item -> segment map.
@@ -664,11 +670,20 @@ __global__ __launch_bounds__(kScanThreads) void piece_plan_kernel(PieceArgs a) {
     const int t = threadIdx.x;
     const uint64_t per = (a.n_seg + kScanThreads - 1) / kScanThreads;
     const uint64_t lo = t * per, hi = lo + per < a.n_seg ? lo + per : a.n_seg;
+    // Piece size per segment: kPiece, or 2 kPiece for a log whose frames the deferring walk saw
+    // average >= kBigPieceMean bytes (a piece's walk is a chain of one header load per frame, its
+    // guess a fixed cost: long frames afford longer pieces -- 64-2048 B frames +7 % read launch at
+    // 256 KiB, 64-512 B frames -6 % framing, same-box A/B, profiles/r03/piece_size/)
+    auto psize_of = [&](uint64_t s) -> uint32_t {
+        const uint64_t pd = a.seg_stop[s], nf = a.seg_nframes[s];
+        return (RH_PIECE_ADAPT && nf && pd / nf >= kBigPieceMean) ? 2 * kPiece : kPiece;
+    };
     auto pieces_of = [&](uint64_t s) -> uint64_t {
         if (a.seg_status[s] != kDeferred) return 0;
         const uint64_t L = a.seg_len[s], pd = a.seg_stop[s];
         if (L > 0x7fffffffull || pd >= L) return 0;
-        return (L - pd + kPiece - 1) / kPiece;
+        const uint64_t P = psize_of(s);
+        return (L - pd + P - 1) / P;
     };
     uint64_t sum = 0;
     for (uint64_t s = lo; s < hi; ++s) sum += pieces_of(s);
@@ -688,6 +703,7 @@ __global__ __launch_bounds__(kScanThreads) void piece_plan_kernel(PieceArgs a) {
         const bool fits = run + np <= a.piece_cap;  // else: this segment walks serially
         a.piece_first[s] = (uint32_t)(fits ? run : 0);
         a.piece_cnt[s] = (uint32_t)(fits ? np : 0);
+        a.seg_psz[s] = psize_of(s);
         if (fits && np) {  // 16-byte stores over the aligned middle (a store per piece was ~10 us)
             uint64_t w = run;
             const uint64_t e = run + np;
@@ -737,7 +753,7 @@ __global__ __launch_bounds__(kPieceThreads) void piece_guess_kernel(PieceArgs a)
         it.base = a.seg_off[it.s];
         it.L = (uint32_t)a.seg_len[it.s];
         uint32_t Bn;
-        piece_bounds((uint32_t)a.seg_stop[it.s], it.L, w - a.piece_first[it.s], it.Bi, Bn);
+        piece_bounds((uint32_t)a.seg_stop[it.s], it.L, w - a.piece_first[it.s], a.seg_psz[it.s], it.Bi, Bn);
         // frames longer than gmax (2x the largest the serial walk saw) kill a candidate; the window
         // is 4 gmax (4..16 KiB) so that a false start cannot leave it in a step or two
         const uint32_t gm0 = a.seg_gmax[it.s] * 2u;
@@ -905,7 +921,7 @@ __global__ __launch_bounds__(64) void piece_guess_wave_kernel(PieceArgs a) {
         it.base = a.seg_off[it.s];
         it.L = (uint32_t)a.seg_len[it.s];
         uint32_t Bn;
-        piece_bounds((uint32_t)a.seg_stop[it.s], it.L, w - a.piece_first[it.s], it.Bi, Bn);
+        piece_bounds((uint32_t)a.seg_stop[it.s], it.L, w - a.piece_first[it.s], a.seg_psz[it.s], it.Bi, Bn);
         const uint32_t gm0 = a.seg_gmax[it.s] * 2u;
         it.gmax = gm0 < 1024u ? 1024u : gm0 > kGuessWin ? kGuessWin : gm0;
         const uint32_t win = kWinMult * it.gmax < 4096u ? 4096u : kWinMult * it.gmax > kGuessWin ? kGuessWin : kWinMult * it.gmax;
@@ -1104,7 +1120,7 @@ __global__ __launch_bounds__(256) void piece_walk_kernel(PieceArgs a) {
             const uint64_t base = a.seg_off[s];
             const uint32_t L = (uint32_t)a.seg_len[s];
             uint32_t Bi, Bn;
-            piece_bounds((uint32_t)a.seg_stop[s], L, w - a.piece_first[s], Bi, Bn);
+            piece_bounds((uint32_t)a.seg_stop[s], L, w - a.piece_first[s], a.seg_psz[s], Bi, Bn);
             p = walk_piece(a.buf, pl, base, p, Bn, L, a.max_op, cnt, ended, lok);
         }
         a.gwalk[w] = make_uint4(g, cnt, p, ended | (lok << 1));
@@ -1122,7 +1138,7 @@ __global__ __launch_bounds__(256) void piece_walk_kernel(PieceArgs a) {
                 const uint64_t base = a.seg_off[s];
                 const uint32_t L = (uint32_t)a.seg_len[s];
                 uint32_t Bi, Bn;
-                piece_bounds((uint32_t)a.seg_stop[s], L, w + 1 - a.piece_first[s], Bi, Bn);
+                piece_bounds((uint32_t)a.seg_stop[s], L, w + 1 - a.piece_first[s], a.seg_psz[s], Bi, Bn);
                 uint32_t pa = p, pb = gb, ma = 0, mb = 0, fa_end = 0, steps = 0;
                 uint32_t al[kAList / 2] = {};  // A's frame lengths (u16 pairs), stored once at the end
                 bool alfit = true;             // every one of them below 64 KiB
@@ -1298,7 +1314,7 @@ __global__ __launch_bounds__(64) void piece_stitch_kernel(PieceArgs a) {
     const uint64_t base = a.seg_off[s];
     const uint32_t L = (uint32_t)a.seg_len[s];
     const uint32_t pd = (uint32_t)a.seg_stop[s];
-    const uint32_t np = a.piece_cnt[s], pf = a.piece_first[s];
+    const uint32_t np = a.piece_cnt[s], pf = a.piece_first[s], PS = a.seg_psz[s];  // pieces, first, size
     uint32_t e = pd, total = a.seg_nframes[s];
     uint64_t rpos = pd;
     uint32_t rnfr = total;
@@ -1337,7 +1353,7 @@ __global__ __launch_bounds__(64) void piece_stitch_kernel(PieceArgs a) {
             const uint32_t i = (uint32_t)lane * K + k;
             ent[k] = k ? gr[k - 1].z : (lane ? prevx : e);
             uint32_t Bi, Bn;
-            piece_bounds(pd, L, j + i, Bi, Bn);
+            piece_bounds(pd, L, j + i, PS, Bi, Bn);
             kn[k] = i < P && ent[k] < Bn;
             cnt[k] = gr[k].y;
             xx[k] = gr[k].z;
@@ -1424,7 +1440,7 @@ __global__ __launch_bounds__(64) void piece_stitch_kernel(PieceArgs a) {
         e = v_ent;
         const uint32_t w = pf + j;
         uint32_t Bi, Bn;
-        piece_bounds(pd, L, j, Bi, Bn);
+        piece_bounds(pd, L, j, PS, Bi, Bn);
         if (e >= Bn) {  // a frame spans this piece: nothing starts in it
             if (lane == 0) a.walk[w] = make_uint4(e, 0, total, kNone);
             ++j;
@@ -1629,12 +1645,12 @@ int rh_segments_launch_impl(rh_ctx* ctx, const rh_segments* g, hipStream_t strea
     a.seg_status = g->seg_status;
     a.seg_stop = g->seg_stop;
     const int cus = ctx && ctx->num_cus > 0 ? ctx->num_cus : 256;
-    // Piece-pass scratch (stream-ordered, from the context's pool): per segment 24 B, per piece
+    // Piece-pass scratch (stream-ordered, from the context's pool): per segment 28 B, per piece
     // 56 + 2 kList + 2 kAList B.  piece_cap bounds the pieces of non-overlapping segments; segments beyond it
     // walk serially.
     const uint64_t n_seg = g->n_seg;
     const uint64_t piece_cap = g->buf_len / kPiece + n_seg + 1;
-    const size_t bytes = (size_t)piece_cap * (56 + 2 * kList + 2 * kAList) + (size_t)n_seg * 24 + 64;
+    const size_t bytes = (size_t)piece_cap * (56 + 2 * kList + 2 * kAList) + (size_t)n_seg * 28 + 64;
     rh::PoolScratch scratch(stream);  // released on every exit path (after the last pass using it)
     RH_HIP(scratch.alloc(ctx, bytes));
     uint8_t* sp = scratch.bytes();
@@ -1648,7 +1664,8 @@ int rh_segments_launch_impl(rh_ctx* ctx, const rh_segments* g, hipStream_t strea
     uint32_t* seg_gmax = pa.piece_cnt + n_seg;
     pa.seg_gmax = seg_gmax;
     pa.resume_nfr = seg_gmax + n_seg;
-    pa.n_pieces = reinterpret_cast<unsigned int*>(pa.resume_nfr + n_seg);
+    pa.seg_psz = pa.resume_nfr + n_seg;
+    pa.n_pieces = reinterpret_cast<unsigned int*>(pa.seg_psz + n_seg);
     pa.piece_seg = reinterpret_cast<uint32_t*>(pa.n_pieces + 4);
     pa.guess = pa.piece_seg + piece_cap;
     pa.plen = reinterpret_cast<uint16_t*>(pa.guess + piece_cap);
