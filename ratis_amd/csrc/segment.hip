@@ -573,6 +573,9 @@ constexpr uint32_t kPiece = RH_PIECE_BYTES;  // bytes per piece (or twice that: 
 #define RH_PIECE_ADAPT 1
 #endif
 constexpr uint32_t kBigPieceMean = 512;  // mean frame bytes from which a segment takes 2 kPiece
+#ifndef RH_HUGE_PIECE_MEAN  // A/B builds override: mean frame bytes from which a segment takes 4 kPiece
+#define RH_HUGE_PIECE_MEAN 0xFFFFFFFFull
+#endif
 #ifndef RH_GUESS_WIN  // A/B builds override (scripts/ab_build.sh)
 #define RH_GUESS_WIN 16384
 #define RH_PIECE_THREADS 256
@@ -676,7 +679,9 @@ __global__ __launch_bounds__(kScanThreads) void piece_plan_kernel(PieceArgs a) {
     // 256 KiB, 64-512 B frames -6 % framing, same-box A/B, profiles/r03/piece_size/)
     auto psize_of = [&](uint64_t s) -> uint32_t {
         const uint64_t pd = a.seg_stop[s], nf = a.seg_nframes[s];
-        return (RH_PIECE_ADAPT && nf && pd / nf >= kBigPieceMean) ? 2 * kPiece : kPiece;
+        if (!RH_PIECE_ADAPT || !nf) return kPiece;
+        const uint64_t mean = pd / nf;
+        return mean >= RH_HUGE_PIECE_MEAN ? 4 * kPiece : mean >= kBigPieceMean ? 2 * kPiece : kPiece;
     };
     auto pieces_of = [&](uint64_t s) -> uint64_t {
         if (a.seg_status[s] != kDeferred) return 0;

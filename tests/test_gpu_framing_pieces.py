@@ -247,3 +247,39 @@ def test_read_path_over_deferred_segments(ctx, orc):
     for s in range(len(offs)):
         ro, _, _, rst, rstop = orc.segment_scan(buf[offs[s]: offs[s] + lens[s]])
         assert (st[s], stop[s], n_ok[s]) == (rst, rstop, len(ro)), s
+
+
+@pytest.mark.parametrize("min_frame,max_frame", [(64, 2048), (64, 512)])
+def test_ragged_read_launch_bench_scale(ctx, orc, min_frame, max_frame):
+    """rh_segments_read_launch at the bench's scale (128 x 32 MiB of ragged frames, 1e-5 of them
+    with a flipped payload bit): at ~1e-4 per piece a guess is a false survivor that clears the
+    guess window and dies mid-piece, so runs of this size take the stitch's windowed fallback walk
+    and its recorded-length list.  Frame table == the generator's, every clean frame's CRC == the
+    stamped one, the mismatch set == the planted set, and each segment's verdict stops at its first
+    planted corruption (decodeEntry's ChecksumException), else reads every frame."""
+    import torch
+
+    from ratis_amd import engine, workload
+    rs = workload.synth_ragged_segments(ctx, 128, min_frame=min_frame, max_frame=max_frame, seed=77,
+                                        corrupt_rate=1e-5)
+    n, size = rs.n_segments, rs.segment_size
+    nf = int(rs.seg_nframes.sum())
+    b = engine.SegmentBatch(buf=rs.batch.buf, seg_off=torch.arange(n, device="cuda", dtype=torch.int64) * size,
+                            seg_len=torch.full((n,), size, device="cuda", dtype=torch.int64),
+                            frames_per_seg_cap=int(rs.seg_nframes.max()) + 16)
+    r = engine.read_segments_fused(ctx, b)
+    torch.cuda.synchronize()
+    assert int(b.total_frames.item()) == nf
+    assert torch.equal(b.frame_off[:nf], rs.batch.frame_off)
+    assert torch.equal(b.frame_len[:nf], rs.batch.frame_len)
+    bad = np.nonzero(np.unpackbits(r["bad_bits"].cpu().numpy().view(np.uint8), bitorder="little")[:nf])[0]
+    assert np.array_equal(bad, rs.corrupted)
+    clean = torch.ones(nf, dtype=torch.bool, device="cuda")
+    clean[torch.from_numpy(rs.corrupted).cuda()] = False
+    assert torch.equal(r["crc_out"][:nf][clean], rs.batch.crc_out[:nf][clean])
+    first = np.concatenate([[0], np.cumsum(rs.seg_nframes)])
+    n_ok = r["n_ok"].cpu().numpy()
+    for s in range(n):
+        planted = rs.corrupted[(rs.corrupted >= first[s]) & (rs.corrupted < first[s + 1])]
+        want = int(planted[0] - first[s]) if planted.size else int(rs.seg_nframes[s])
+        assert int(n_ok[s]) == want, s
