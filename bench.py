@@ -468,13 +468,22 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    # RH_BENCH_BACKEND=gloo + more ranks than GPUs: a rehearsal of the N > 1 path on a 1-GPU box
+    # (ranks share the device; timings are not per-GPU figures).  The driver's runs use RCCL with
+    # one rank per GPU, where local % device_count() == local.
+    backend = os.environ.get("RH_BENCH_BACKEND", "nccl")
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
+        local %= torch.cuda.device_count()
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     n_gpus = world
     dev = torch.device("cuda", local)
     ctx = engine.Context(local)
+    red_dev = dev if backend == "nccl" else torch.device("cpu")
 
     def barrier():
         if world > 1:
@@ -484,14 +493,14 @@ def main():
     def max_over_ranks(x: float) -> float:
         if world == 1:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device=dev)
+        t = torch.tensor([x], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
     def sum_over_ranks(x: int) -> int:
         if world == 1:
             return x
-        t = torch.tensor([x], dtype=torch.int64, device=dev)
+        t = torch.tensor([x], dtype=torch.int64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         return int(t.item())
 
