@@ -1212,7 +1212,10 @@ struct MergeOut {
 // The walk streams the segment through two 8 KiB LDS windows (the next one loaded while the
 // current one is walked): a false-survivor guess leaves a whole piece (~125 frames) to walk, and a
 // header load per frame from HBM made that one memory round trip per frame.
-constexpr uint32_t kMergeWin = 8192;
+#ifndef RH_MERGE_WIN
+#define RH_MERGE_WIN 8192
+#endif
+constexpr uint32_t kMergeWin = RH_MERGE_WIN;
 constexpr uint32_t kMergePer = kMergeWin / (64 * 16);  // 16-B loads per lane per window
 // rec (LDS, kList entries): the true walk's frame lengths as walked (lane 0 stores them).
 __device__ __forceinline__ MergeOut merge_walk(const PieceArgs& a, uint32_t w, uint4 gr, uint32_t e, uint32_t Bn,
@@ -1312,7 +1315,8 @@ __global__ __launch_bounds__(64) void piece_stitch_kernel(PieceArgs a) {
 #ifdef RH_STITCH_STATS
     const uint64_t t_0 = __builtin_amdgcn_s_memrealtime();
     uint64_t t_1 = 0, t_2 = 0;
-    uint32_t npass = 0, nser = 0;
+    uint32_t npass = 0, nser = 0, n_mw = 0;
+    uint64_t t_mw = 0;
 #endif
     if (s >= a.n_seg || a.seg_status[s] != kDeferred) return;
     const int lane = threadIdx.x;
@@ -1473,11 +1477,13 @@ __global__ __launch_bounds__(64) void piece_stitch_kernel(PieceArgs a) {
                 msteps = kNone;
             }
         } else if (g != e) {
+#ifdef RH_STITCH_STATS
+            const uint64_t tm0 = __builtin_amdgcn_s_memrealtime();
+#endif
             const MergeOut r = merge_walk(a, w, make_uint4(g, cnt1, x1, gfl), e, Bn, base, L, lane, ring, rec);
 #ifdef RH_STITCH_STATS
-            if (lane == 0)
-                printf("FALLBACK seg %u piece %u pe=%u e=%u g=%u Bi=%u met=%d m=%u cnt=%u gcnt=%u pflags=%u\n", (unsigned)s, j,
-                       pe, e, g, Bi, r.msteps != kNone, r.msteps, r.cnt, cnt1, __builtin_amdgcn_readfirstlane(p4.w));
+            t_mw += __builtin_amdgcn_s_memrealtime() + (r.cnt & 0) - tm0;
+            n_mw += r.msteps == kNone ? r.cnt : r.msteps;
 #endif
             cnt1 = r.cnt;
             x1 = r.x;
@@ -1531,9 +1537,9 @@ __global__ __launch_bounds__(64) void piece_stitch_kernel(PieceArgs a) {
 #ifdef RH_STITCH_STATS
     const uint64_t t_3 = __builtin_amdgcn_s_memrealtime();
     if (lane == 0)
-        printf("STITCH seg %u np %u passes %u serial %u t0 %llu loads %u first_serial %u end %u\n", (unsigned)s, np,
-               npass, nser, (unsigned long long)t_0, (unsigned)(t_1 - t_0), (unsigned)(t_2 ? t_2 - t_0 : 0),
-               (unsigned)(t_3 - t_0));
+        printf("STITCH seg %u np %u passes %u serial %u t0 %llu loads %u first_serial %u end %u merge_walk %u steps %u\n",
+               (unsigned)s, np, npass, nser, (unsigned long long)t_0, (unsigned)(t_1 - t_0),
+               (unsigned)(t_2 ? t_2 - t_0 : 0), (unsigned)(t_3 - t_0), (unsigned)t_mw, n_mw);
 #endif
 }
 
