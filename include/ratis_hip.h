@@ -269,25 +269,35 @@ int rh_deltas_submit(rh_groups* g, size_t n);
  * every dirty slot whose level differs from the last one reported. */
 #define RH_COMMIT_WATCH_ALL 1u
 int rh_commit_batch(rh_groups* g, uint32_t flags, rh_commit_out* out);
-/* The same split in two: _async enqueues the evaluation (its events are written straight into
- * host-mapped pinned memory) and returns a ticket; _wait blocks until that ticket's results are
- * ready.  Deltas and other calls may be issued in between (they are ordered after it). */
+/* The same split in two: _async enqueues the evaluation and returns a ticket; _wait blocks until that
+ * ticket's results are ready.  Deltas and other calls may be issued in between (they are ordered
+ * after it). */
 int rh_commit_batch_async(rh_groups* g, uint32_t flags, uint64_t* ticket);
 int rh_commit_batch_wait(rh_groups* g, uint64_t ticket, rh_commit_out* out);
-/* Where the evaluation kernels put their event records.  HOST_MAPPED (the default): straight into
- * the pinned result buffers across PCIe, each workgroup's records as one contiguous run -- no copy
- * afterwards, the kernel ends when its records have landed.  DEVICE: into HBM; rh_commit_batch_wait
- * / rh_watch_levels then copy the counted prefix into the same pinned buffers (a D2H on the
- * table's copy stream), so the kernel is not held up by PCIe writes.  Results are identical.  Not
- * while an rh_commit_batch_async ticket is outstanding (RH_E_STATE); DEVICE allocates
- * 112 B x capacity of HBM on first use. */
+/* Where the result lists are assembled.  Both sinks run the same evaluation kernel, which stages its
+ * records in HBM (one region per XCD head) and never writes across PCIe; a gather kernel then packs
+ * the regions into contiguous lists.  HOST_MAPPED (the default): the gather writes the lists straight
+ * into the pinned result buffers (PCIe writes by the GPU), visible when the ticket completes.
+ * DEVICE: the gather packs into HBM and rh_commit_batch_wait / rh_watch_levels_wait copy the counted
+ * prefix into the same pinned buffers (a D2H on the table's copy stream).  Results are identical.
+ * Not while an evaluation is outstanding (RH_E_STATE); DEVICE allocates 112 B x capacity of HBM on
+ * first use. */
 #define RH_EVENTS_HOST_MAPPED 0
 #define RH_EVENTS_DEVICE      1
 int rh_groups_set_event_sink(rh_groups* g, int sink);
+/* Diagnostics (benchmarks): with timing enabled every evaluation records HIP events around its
+ * evaluation kernel(s) and around the gather; rh_groups_last_timing returns the last evaluation's
+ * two device times in ms (blocks until it has completed; RH_E_STATE before any timed evaluation). */
+int rh_groups_timing(rh_groups* g, int enable);
+int rh_groups_last_timing(rh_groups* g, float* eval_ms, float* gather_ms);
 /* Batched commitIndexChanged() over the slots whose follower commitIndex or leader commitIndex
  * changed: the slots whose {min, majority, max} levels changed, into library-owned pinned memory
- * valid until the next rh_watch_levels.  Blocks. */
+ * valid until the next rh_watch_levels / rh_watch_levels_async.  Blocks. */
 int rh_watch_levels(rh_groups* g, const rh_watch_event** out_events, uint64_t* out_n);
+/* The same split in two (one evaluation outstanding per table: a second _async first waits for the
+ * first, whose list it then replaces).  _wait fails with RH_E_STATE when none is outstanding. */
+int rh_watch_levels_async(rh_groups* g);
+int rh_watch_levels_wait(rh_groups* g, const rh_watch_event** out_events, uint64_t* out_n);
 /* Reads back one column of slots [first, first + n) (debug / checkpoint / tests): column =
  * RH_COL_MATCH(k) / RH_COL_FCOMMIT(k) / RH_COL_FLUSH / RH_COL_COMMITTED, or RH_COL_CONF (the
  * membership word, as int64) and RH_COL_TERM_START.  Stopped slots read INT64_MIN; follower
@@ -319,6 +329,10 @@ int rh_group_lease_start(rh_groups* g, uint32_t slot, int64_t now_nanos, int ena
  * until the next rh_lease_batch; *out_words = ceil(capacity / 64).  Blocks. */
 int rh_lease_batch(rh_groups* g, int64_t now_nanos, int64_t timeout_ms, const uint64_t** out_bits,
                    uint64_t* out_words);
+/* The same split in two, as rh_watch_levels_async / _wait (one batch outstanding per table; the
+ * bitmap stays valid until the next rh_lease_batch / rh_lease_batch_async). */
+int rh_lease_batch_async(rh_groups* g, int64_t now_nanos, int64_t timeout_ms);
+int rh_lease_batch_wait(rh_groups* g, const uint64_t** out_bits, uint64_t* out_words);
 
 /* ---- one RaftServer across several GPUs ---------------------------------------------------
  * A node owns one context and one resident table per device of `device_mask` (bit d = GPU d).
@@ -352,8 +366,12 @@ int rh_node_push_deltas(rh_node* node, const rh_delta* deltas, size_t n);
  * totals).  flags as rh_commit_batch.  Blocks. */
 int rh_node_commit_batch(rh_node* node, uint32_t flags, rh_index_event* advanced, uint64_t adv_cap,
                          uint64_t* n_advanced, rh_index_event* watch_all, uint64_t watch_cap, uint64_t* n_watch_all);
-/* rh_group_lease_start / rh_lease_batch on every shard; bit s of the caller's out_bits (at least
- * ceil(shards * capacity_per_shard / 64) words) = node slot s has the lease.  Blocks. */
+/* commitIndexChanged() on every shard (all launched before any is awaited): the changed levels of
+ * all shards, with node slots, into the caller's array (up to cap; *out_n = the total).  Blocks. */
+int rh_node_watch_levels(rh_node* node, rh_watch_event* out, uint64_t cap, uint64_t* out_n);
+/* rh_group_lease_start / rh_lease_batch on every shard (all shards' passes in flight before any
+ * wait); bit s of the caller's out_bits (at least ceil(shards * capacity_per_shard / 64) words) =
+ * node slot s has the lease.  Blocks. */
 int rh_node_group_lease_start(rh_node* node, uint32_t node_slot, int64_t now_nanos, int enabled);
 int rh_node_lease_batch(rh_node* node, int64_t now_nanos, int64_t timeout_ms, uint64_t* out_bits, uint64_t out_words);
 
@@ -398,6 +416,20 @@ int rh_crc32c_frames_launch(rh_ctx* ctx, const rh_frames* frames, uint32_t flags
 int rh_crc32c_verify_host(rh_ctx* ctx, const uint8_t* seg, uint64_t seg_len, const uint64_t* frame_off,
                           const uint32_t* frame_len, uint64_t n, uint32_t* crc_out, uint64_t* bad_bits,
                           uint64_t* n_bad);
+
+/* The write side over a HOST buffer (PCIe-inclusive; what the Java module's flush seam calls,
+ * SegmentedRaftLogOutputStream.write OUT:86-110 deferred to BufferedWriteChannel's flush): frame i =
+ * buf[frame_off[i], frame_off[i] + frame_len[i]), varint + entry + a 4-byte trailer; every trailer
+ * is overwritten with the big-endian PureJavaCrc32C of the bytes before it (reset() state), exactly
+ * what write() puts there.  Only the span the frames cover is copied to the device and only the
+ * CRCs come back.  Every frame must hold its trailer and lie inside the buffer (RH_E_INVAL, nothing
+ * stamped).  Blocks.  A buffer registered with rh_host_register (the worker's reused write buffer)
+ * crosses PCIe without staging. */
+int rh_crc32c_stamp_host(rh_ctx* ctx, uint8_t* buf, uint64_t buf_len, const uint64_t* frame_off,
+                         const uint32_t* frame_len, uint64_t n);
+/* Page-locks a host buffer for direct DMA (hipHostRegister) until rh_host_unregister. */
+int rh_host_register(rh_ctx* ctx, void* p, uint64_t n);
+int rh_host_unregister(rh_ctx* ctx, void* p);
 
 /* Checksum.update over one host span (PJC:54-91 update(byte[], off, len)): crc_state is the
  * PureJavaCrc32C `crc` field before the call (0xFFFFFFFF after reset()); *out_state receives it

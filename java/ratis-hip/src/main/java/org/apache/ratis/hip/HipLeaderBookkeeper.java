@@ -18,11 +18,21 @@
  * notifySenders -- stays in the division's LeaderStateImpl (Callback), for the divisions with an
  * event only.
  *
- * One pump tick: push the buffered deltas; start every shard's updateCommit evaluation (all GPUs in
- * flight); per shard, wait and hand the advanced commits and changed watch-ALL levels to the
- * divisions; per shard, commitIndexChanged's levels; the lease bitmap; recycle the slots released
- * during the tick.  Nothing is allocated per tick: every result array is sized once, per shard
- * capacity, and reused shard after shard.
+ * One pump tick: push the buffered deltas; put every shard's updateCommit evaluation, its
+ * commitIndexChanged evaluation and (with a lease timeout) its hasLease pass in flight -- every GPU
+ * busy before any wait; then per shard, wait and hand the advanced commits and changed watch-ALL
+ * levels to the divisions, then commitIndexChanged's levels, then publish the lease bitmap; recycle
+ * the slots released during the tick.  Nothing is allocated per tick: every result array is sized
+ * once, per shard capacity, and reused shard after shard.
+ *
+ * FALLBACK.  A division the GPU table cannot hold leaves it for good and reverts to the reference's
+ * own per-division path (updateCommit / commitIndexChanged / hasLease in LeaderStateImpl; the
+ * FollowerInfos are kept by Java in both modes): a 15th follower slot (the table has 14 per
+ * division; a joint change of two 8-peer confs reaches 15), a full shard at register, a control
+ * call the library rejects (RH_E_RANGE / RH_E_INVAL) or fails, and -- for every division -- a pump
+ * that died.  Division.isFallback() is what every seam checks; Callback.onFallback() lets the
+ * division catch up in Java at once; getFallbackCount() / getFallbackCount(reason) count them
+ * (SURVEY section 7: "fall back to the CPU path.  Count that fallback").
  */
 package org.apache.ratis.hip;
 
@@ -54,7 +64,13 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
     /** commitIndexChanged()'s levels changed (LeaderStateImpl.java:612-622): ALL_COMMITTED = min,
      *  MAJORITY_COMMITTED = majority, MAJORITY = max; the division then runs notifySenders(). */
     void onWatchLevels(long min, long majority, long max);
+    /** The division left the GPU table (see FALLBACK above): from now on it runs the reference's
+     *  per-division path; it should evaluate updateCommit / commitIndexChanged once now. */
+    void onFallback();
   }
+
+  /** Why a division runs the Java path. */
+  public enum FallbackReason { SHARD_FULL, FOLLOWER_SLOTS, REJECTED, DEVICE_ERROR, PUMP_FAILED }
 
   private final RatisHip hip;
   private final int shards;
@@ -69,6 +85,7 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
   private volatile boolean running = true;
   private volatile Throwable failure;                // set when the pump died: no more results, no lease
   private volatile long leaseTimeoutMs = -1;  // LeaderLease.leaseTimeoutMs; -1: no lease batches
+  private final AtomicLongArray fallbacks = new AtomicLongArray(FallbackReason.values().length);
 
   // ---- pump-thread result arrays: one shard's worth, reused for every shard and every tick -----
   private final int[] advSlot;
@@ -165,25 +182,45 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
     return failure;
   }
 
-  private void checkRunning() {
-    final Throwable f = failure;
-    if (f != null) {
-      throw new IllegalStateException("ratis-hip: the commit pump has failed", f);
+  /** Divisions that fell back to the Java path so far (every reason). */
+  public long getFallbackCount() {
+    long n = 0;
+    for (int i = 0; i < fallbacks.length(); i++) {
+      n += fallbacks.get(i);
     }
+    return n;
   }
 
-  /** A new leader division (new LeaderStateImpl, LeaderStateImpl.java:365-430). */
+  public long getFallbackCount(FallbackReason reason) {
+    return fallbacks.get(reason.ordinal());
+  }
+
+  /**
+   * A new leader division (new LeaderStateImpl, LeaderStateImpl.java:365-430).  Never fails: a
+   * division the GPU cannot take (its shard is full, or the pump has failed) is returned in
+   * fallback, and the caller runs the reference's path for it.
+   */
   public synchronized Division register(RaftGroupId groupId, RaftPeerId selfId, Callback callback) {
-    checkRunning();
+    if (failure != null) {
+      return fallenBack(selfId, callback, FallbackReason.PUMP_FAILED);
+    }
     final UUID u = groupId.getUuid();
     final int shard = hip.shardOf(u.getMostSignificantBits(), u.getLeastSignificantBits());
     final Integer slot = freeSlots[shard].poll();
     if (slot == null) {
-      throw new IllegalStateException("ratis-hip: shard " + shard + " is full (" + capacity + " divisions)");
+      return fallenBack(selfId, callback, FallbackReason.SHARD_FULL);
     }
     final int nodeSlot = shard * capacity + slot;
     final Division d = new Division(nodeSlot, selfId, callback);
     divisions.put(nodeSlot, d);
+    return d;
+  }
+
+  /** A division that never enters the table (no slot): the Java path from the start. */
+  private Division fallenBack(RaftPeerId selfId, Callback callback, FallbackReason reason) {
+    final Division d = new Division(-1, selfId, callback);
+    d.fallback = true;
+    fallbacks.incrementAndGet(reason.ordinal());
     return d;
   }
 
@@ -233,6 +270,10 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
       }
     } catch (Throwable t) {
       failure = t;   // results stop; hasLease() turns false at once (see Division.hasLease)
+      // every division reverts to the reference's per-division path
+      for (Division d : divisions.values()) {
+        d.fallBack(FallbackReason.PUMP_FAILED);
+      }
     }
   }
 
@@ -241,9 +282,18 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
     synchronized (deltaLock) {
       drainDeltas();
     }
-    // updateCommit() of every shard's dirty divisions: all shards in flight before any wait
+    final long timeout = leaseTimeoutMs;
+    final long batch = timeout >= 0 ? ++leaseBatchCount : 0;
+    final long now = System.nanoTime();
+    // every shard's updateCommit(), then commitIndexChanged() (stream order on the shard's GPU: the
+    // commits the first stores are the second's input) and hasLease(): all shards in flight before
+    // any wait
     for (int s = 0; s < shards; s++) {
       tickets[s] = hip.commitAsync(s, RatisHip.COMMIT_WATCH_ALL);
+      hip.watchAsync(s);
+      if (timeout >= 0) {
+        hip.leaseAsync(s, now + leaseMarginNanos, timeout);
+      }
     }
     for (int s = 0; s < shards; s++) {
       final long counts = hip.commitWait(s, tickets[s], advSlot, advCommit, wallSlot, wallMin);
@@ -262,11 +312,8 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
           d.callback.onWatchAll(wallMin[i]);
         }
       }
-    }
-    // commitIndexChanged() of the divisions whose follower / leader commitIndex changed
-    for (int s = 0; s < shards; s++) {
-      final int n = Math.min(hip.watchLevels(s, wSlot, wMin, wMaj, wMax, wValid), capacity);
-      final int base = s * capacity;
+      // commitIndexChanged() of the divisions whose follower / leader commitIndex changed
+      final int n = Math.min(hip.watchWait(s, wSlot, wMin, wMaj, wMax, wValid), capacity);
       for (int i = 0; i < n; i++) {
         if (!wValid[i]) {
           continue;   // getMajorityMin was Optional.empty(): no watch update (LeaderStateImpl.java:613)
@@ -276,13 +323,8 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
           d.callback.onWatchLevels(wMin[i], wMaj[i], wMax[i]);
         }
       }
-    }
-    final long timeout = leaseTimeoutMs;
-    if (timeout >= 0) {  // LeaderStateImpl.hasLease for every division: extend + isValid
-      final long batch = ++leaseBatchCount;
-      final long now = System.nanoTime();
-      for (int s = 0; s < shards; s++) {
-        hip.leaseBatch(s, now + leaseMarginNanos, timeout, leaseScratch);
+      if (timeout >= 0) {  // LeaderStateImpl.hasLease for every division: extend + isValid
+        hip.leaseWait(s, leaseScratch);
         final int next = leaseCurrent[s] ^ 1;
         final LeaseBits lb = lease[s][next];
         lb.seq = lb.seq + 1;                        // odd: being written (only the pump writes)
@@ -329,18 +371,57 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
    * (FollowerInfoImpl.java:42-43); the follower's next reply carries its current matchIndex.
    */
   public final class Division {
-    private final int nodeSlot;
+    private final int nodeSlot;   // -1: never had one (fell back at register)
     private final RaftPeerId selfId;
     private final Callback callback;
     private final Map<RaftPeerId, Integer> followerSlot = new HashMap<>();   // peers with a FollowerInfo
     private boolean started;   // guarded by deltaLock
     private int width;         // follower columns of the device tier; guarded by deltaLock
+    private volatile boolean fallback;   // the reference's per-division path from now on
     private volatile long leaseArmedAfter = Long.MAX_VALUE;   // lease batches up to this one predate leaseStart
 
     Division(int nodeSlot, RaftPeerId selfId, Callback callback) {
       this.nodeSlot = nodeSlot;
       this.selfId = selfId;
       this.callback = callback;
+    }
+
+    /** True once the division runs the reference's own path (every seam checks this). */
+    public boolean isFallback() {
+      return fallback;
+    }
+
+    /**
+     * Leaves the GPU table for good (see FALLBACK in the class comment): the slot is stopped and
+     * released, later deltas are dropped, and the division is told to evaluate in Java now.
+     * Idempotent; never throws (a device error while stopping is moot: nothing reads the slot).
+     */
+    void fallBack(FallbackReason reason) {
+      boolean release = false;
+      synchronized (deltaLock) {
+        if (fallback) {
+          return;
+        }
+        fallback = true;
+        leaseArmedAfter = Long.MAX_VALUE;
+        if (nodeSlot >= 0) {
+          release = true;
+          if (started) {
+            started = false;
+            try {
+              drainDeltas();
+              hip.stop(nodeSlot);
+            } catch (IOException | RuntimeException ignored) {
+              // the slot is released below and never evaluated for this division again
+            }
+          }
+        }
+      }
+      fallbacks.incrementAndGet(reason.ordinal());
+      if (release) {
+        release(this);
+      }
+      callback.onFallback();
     }
 
     private void emit(int follower, int column, int op, long value) {
@@ -353,8 +434,14 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
       LockSupport.unpark(pump);
     }
 
-    /** addSenders (LeaderStateImpl.java:681-692): the peer gets a FollowerInfo and a slot. */
+    /**
+     * addSenders (LeaderStateImpl.java:681-692): the peer gets a FollowerInfo and a slot.  Returns
+     * the slot, or -1 once the division is in fallback -- which a 15th follower puts it in.
+     */
     public synchronized int addFollower(RaftPeerId peer) {
+      if (fallback) {
+        return -1;
+      }
       final Integer k = followerSlot.get(peer);
       if (k != null) {
         return k;
@@ -370,7 +457,8 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
           return s;
         }
       }
-      throw new IllegalStateException("ratis-hip: more than " + RatisHip.MAX_FOLLOWERS + " followers");
+      fallBack(FallbackReason.FOLLOWER_SLOTS);   // more than 14 followers: the Java path holds any number
+      return -1;
     }
 
     /** stopAndRemoveSenders (LeaderStateImpl.java:694-702): the slot becomes reusable. */
@@ -403,34 +491,62 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
           oldConf != null && oldConf.contains(selfId), true);
     }
 
-    /** Leader start: every FollowerInfo new (-1); StartupLogEntry index = termStart (LeaderStateImpl.java:296-301). */
-    public void start(int conf, long flushIndex, long commitIndex, long termStart) throws IOException {
-      checkRunning();
+    /**
+     * Leader start: every FollowerInfo new (-1); StartupLogEntry index = termStart
+     * (LeaderStateImpl.java:296-301).  A start the library rejects or fails puts the division in
+     * fallback instead of failing the leader.
+     */
+    public void start(int conf, long flushIndex, long commitIndex, long termStart) {
+      FallbackReason why = null;
       synchronized (deltaLock) {
-        drainDeltas();
-        hip.start(nodeSlot, conf, flushIndex, commitIndex, termStart);
-        width = tierWidth(conf);
-        started = true;
+        if (fallback) {
+          return;
+        }
+        try {
+          drainDeltas();
+          hip.start(nodeSlot, conf, flushIndex, commitIndex, termStart);
+          width = tierWidth(conf);
+          started = true;
+        } catch (IllegalArgumentException e) {
+          why = FallbackReason.REJECTED;
+        } catch (IOException | RuntimeException e) {
+          why = FallbackReason.DEVICE_ERROR;
+        }
+      }
+      if (why != null) {
+        fallBack(why);
       }
     }
 
     /**
      * Conf change (applyOldNewConf / replicateNewConf, LeaderStateImpl.java:624-633, 1064-1074):
      * the membership word changes and every slot keeps its follower's indices (a new peer's slot
-     * was reset to -1 when addFollower gave it out; a slot the wider tier adds starts at -1).
+     * was reset to -1 when addFollower gave it out; a slot the wider tier adds starts at -1).  A
+     * reconf the library rejects (RH_E_RANGE: no row in the wider tier) or fails puts the division
+     * in fallback.
      */
-    public void reconf(int conf) throws IOException {
+    public void reconf(int conf) {
       final byte[] src = new byte[RatisHip.MAX_FOLLOWERS];
       for (int k = 0; k < src.length; k++) {
         src[k] = (byte) k;
       }
+      FallbackReason why = null;
       synchronized (deltaLock) {
-        if (!started) {
+        if (!started || fallback) {
           return;
         }
-        drainDeltas();
-        hip.reconf(nodeSlot, conf, src);
-        width = tierWidth(conf);
+        try {
+          drainDeltas();
+          hip.reconf(nodeSlot, conf, src);
+          width = tierWidth(conf);
+        } catch (IllegalArgumentException e) {
+          why = FallbackReason.REJECTED;
+        } catch (IOException | RuntimeException e) {
+          why = FallbackReason.DEVICE_ERROR;
+        }
+      }
+      if (why != null) {
+        fallBack(why);
       }
     }
 
@@ -449,20 +565,27 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
     }
 
     // ---- producers (called where the reference updates FollowerInfo / the flush index) -------
+    // Each is a no-op for a follower without a slot (-1) and once the division is in fallback.
     /** FollowerInfo.updateMatchIndex (FollowerInfoImpl.java:93-95), after the RPC reply. */
     public void matchIndex(int followerSlot, long value) {
-      emit(followerSlot, RatisHip.colMatch(followerSlot), RatisHip.OP_MAX, value);
+      if (followerSlot >= 0) {
+        emit(followerSlot, RatisHip.colMatch(followerSlot), RatisHip.OP_MAX, value);
+      }
     }
 
     /** FollowerInfo.setSnapshotIndex (FollowerInfoImpl.java:147-151): matchIndex set as is. */
     public void snapshotIndex(int followerSlot, long value) {
-      emit(followerSlot, RatisHip.colMatch(followerSlot), RatisHip.OP_SET, value);
+      if (followerSlot >= 0) {
+        emit(followerSlot, RatisHip.colMatch(followerSlot), RatisHip.OP_SET, value);
+      }
     }
 
     /** FollowerInfo.updateCommitIndex (FollowerInfoImpl.java:103-105): the pump's next watchLevels
      *  reports the division if its commitIndexChanged() levels moved. */
     public void followerCommitIndex(int followerSlot, long value) {
-      emit(followerSlot, RatisHip.colFollowerCommit(followerSlot), RatisHip.OP_MAX, value);
+      if (followerSlot >= 0) {
+        emit(followerSlot, RatisHip.colFollowerCommit(followerSlot), RatisHip.OP_MAX, value);
+      }
     }
 
     /** The leader's flush-index advance (SegmentedRaftLogWorker.java:419-431). */
@@ -477,21 +600,33 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
 
     // ---- leader lease (LeaderStateImpl.hasLease, LeaderLease) --------------------------------
     /** The division's LeaderLease (lease = now, enabled per config) with every follower stamped now. */
-    public void leaseStart(long nowNanos, boolean enabled) throws IOException {
+    public void leaseStart(long nowNanos, boolean enabled) {
+      FallbackReason why = null;
       synchronized (deltaLock) {
-        if (!started) {
+        if (!started || fallback) {
           return;
         }
-        drainDeltas();
-        // batches already started may predate this lease: only a later one answers hasLease()
-        leaseArmedAfter = leaseBatchCount;
-        hip.leaseStart(nodeSlot, nowNanos, enabled);
+        try {
+          drainDeltas();
+          // batches already started may predate this lease: only a later one answers hasLease()
+          leaseArmedAfter = leaseBatchCount;
+          hip.leaseStart(nodeSlot, nowNanos, enabled);
+        } catch (IllegalArgumentException e) {
+          why = FallbackReason.REJECTED;
+        } catch (IOException | RuntimeException e) {
+          why = FallbackReason.DEVICE_ERROR;
+        }
+      }
+      if (why != null) {
+        fallBack(why);
       }
     }
 
     /** FollowerInfo.updateLastRespondedAppendEntriesSendTime (FollowerInfoImpl.java:241-243). */
     public void lastResponded(int followerSlot, long sendTimeNanos) {
-      emit(followerSlot, RatisHip.colTs(followerSlot), RatisHip.OP_SET, sendTimeNanos);
+      if (followerSlot >= 0) {
+        emit(followerSlot, RatisHip.colTs(followerSlot), RatisHip.OP_SET, sendTimeNanos);
+      }
     }
 
     /** LeaderLease.getAndSetEnabled (LeaderStateImpl.java:478, 744, 1042, 1226). */
@@ -503,10 +638,11 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
      * enabled && (singleton || the lease, extended if it could be, is valid), as of the latest
      * lease batch -- evaluated for a moment at least as late as now, so a true answer holds now.
      * False when no such batch exists: the pump has not run one since leaseStart, it has stalled
-     * past the bitmap's validity, or it has failed.
+     * past the bitmap's validity, or it has failed; and in fallback (the caller then asks the
+     * reference's LeaderLease instead).
      */
     public boolean hasLease() {
-      if (failure != null) {
+      if (failure != null || fallback || nodeSlot < 0) {
         return false;
       }
       final int shard = nodeSlot / capacity;

@@ -194,6 +194,37 @@ public final class RatisHip implements AutoCloseable {
     return watchLevels0(node, shard, slot, min, majority, max, valid);
   }
 
+  /** rh_watch_levels_async on one shard: commitIndexChanged() of its dirty divisions in flight
+   *  (after the shard's commit evaluation, in stream order). */
+  public void watchAsync(int shard) throws IOException {
+    checkShard(shard);
+    watchAsync0(node, shard);
+  }
+
+  /** rh_watch_levels_wait on one shard: the outstanding evaluation's changed levels, as
+   *  {@link #watchLevels}.  Every array must hold the shard capacity. */
+  public int watchWait(int shard, int[] slot, long[] min, long[] majority, long[] max, boolean[] valid)
+      throws IOException {
+    checkShard(shard);
+    checkLength("slot", slot.length, capacityPerShard);
+    checkLength("min", min.length, capacityPerShard);
+    checkLength("majority", majority.length, capacityPerShard);
+    checkLength("max", max.length, capacityPerShard);
+    checkLength("valid", valid.length, capacityPerShard);
+    return watchWait0(node, shard, slot, min, majority, max, valid);
+  }
+
+  /** Where every shard's result lists are assembled (rh_groups_set_event_sink): EVENTS_HOST_MAPPED
+   *  (the default) or EVENTS_DEVICE.  Not while an evaluation is outstanding. */
+  public void setEventSink(int sink) throws IOException {
+    for (int s = 0; s < shards; s++) {
+      setEventSink0(node, s, sink);
+    }
+  }
+
+  public static final int EVENTS_HOST_MAPPED = 0;
+  public static final int EVENTS_DEVICE = 1;
+
   // ---- leader lease (LeaderStateImpl.hasLease, LeaderLease) ----------------------------------
   /** A new LeaderLease for the division (lease = now, enabled per config) with every follower slot
    * stamped now, as a new LeaderStateImpl creates them (LeaderLease.java:37-38, FollowerInfoImpl.java:58).
@@ -214,6 +245,20 @@ public final class RatisHip implements AutoCloseable {
     checkShard(shard);
     checkLength("bits", bits.length, (capacityPerShard + 63) / 64);
     leaseBatchShard0(node, shard, nowNanos, timeoutMs, bits);
+  }
+
+  /** rh_lease_batch_async on one shard: its hasLease() pass at nowNanos in flight. */
+  public void leaseAsync(int shard, long nowNanos, long timeoutMs) throws IOException {
+    checkShard(shard);
+    leaseAsync0(node, shard, nowNanos, timeoutMs);
+  }
+
+  /** rh_lease_batch_wait on one shard: the outstanding pass's bitmap; bits.length >=
+   *  ceil(capacityPerShard / 64). */
+  public void leaseWait(int shard, long[] bits) throws IOException {
+    checkShard(shard);
+    checkLength("bits", bits.length, (capacityPerShard + 63) / 64);
+    leaseWait0(node, shard, bits);
   }
 
   // ---- checksums (SegmentedRaftLogReader.decodeEntry, batched over a segment) ---------------
@@ -275,6 +320,12 @@ public final class RatisHip implements AutoCloseable {
       int[] wallSlot, long[] wallMin) throws IOException;
   private static native int watchLevels0(long node, int shard, int[] slot, long[] min, long[] majority, long[] max,
       boolean[] valid) throws IOException;
+  private static native void watchAsync0(long node, int shard) throws IOException;
+  private static native int watchWait0(long node, int shard, int[] slot, long[] min, long[] majority, long[] max,
+      boolean[] valid) throws IOException;
+  private static native void setEventSink0(long node, int shard, int sink) throws IOException;
+  private static native void leaseAsync0(long node, int shard, long nowNanos, long timeoutMs) throws IOException;
+  private static native void leaseWait0(long node, int shard, long[] bits) throws IOException;
   private static native void leaseStart0(long node, int slot, long nowNanos, boolean enabled) throws IOException;
   private static native void leaseBatch0(long node, long nowNanos, long timeoutMs, long[] bits) throws IOException;
   private static native void leaseBatchShard0(long node, int shard, long nowNanos, long timeoutMs, long[] bits)

@@ -216,14 +216,9 @@ JNIEXPORT jlong JNICALL CLS(commitWait0)(JNIEnv* env, jclass c, jlong node, jint
     return (jlong)((o.n_advanced << 32) | (o.n_watch_all & 0xFFFFFFFFull));
 }
 
-JNIEXPORT jint JNICALL CLS(watchLevels0)(JNIEnv* env, jclass c, jlong node, jint shard, jintArray slot,
-                                         jlongArray mn, jlongArray mj, jlongArray mx, jbooleanArray valid) {
-    (void)c;
-    rh_groups* g = shard_table(env, node, shard);
-    if (!g) return 0;
-    const rh_watch_event* ev = NULL;
-    uint64_t n = 0;
-    if (check(env, rh_watch_levels(g, &ev, &n)) < 0) return 0;
+/* Copies n level-change events into the caller's arrays (checked to hold them). */
+static jint put_levels(JNIEnv* env, const rh_watch_event* ev, uint64_t n, jintArray slot, jlongArray mn,
+                       jlongArray mj, jlongArray mx, jbooleanArray valid) {
     if (!has_len(env, slot, (int64_t)n, "slot shorter than the events") ||
         !has_len(env, mn, (int64_t)n, "min shorter than the events") ||
         !has_len(env, mj, (int64_t)n, "majority shorter than the events") ||
@@ -250,6 +245,57 @@ JNIEXPORT jint JNICALL CLS(watchLevels0)(JNIEnv* env, jclass c, jlong node, jint
     if (a) (*env)->ReleasePrimitiveArrayCritical(env, mn, a, 0);
     if (s) (*env)->ReleasePrimitiveArrayCritical(env, slot, s, 0);
     return (jint)n;
+}
+
+JNIEXPORT jint JNICALL CLS(watchLevels0)(JNIEnv* env, jclass c, jlong node, jint shard, jintArray slot,
+                                         jlongArray mn, jlongArray mj, jlongArray mx, jbooleanArray valid) {
+    (void)c;
+    rh_groups* g = shard_table(env, node, shard);
+    if (!g) return 0;
+    const rh_watch_event* ev = NULL;
+    uint64_t n = 0;
+    if (check(env, rh_watch_levels(g, &ev, &n)) < 0) return 0;
+    return put_levels(env, ev, n, slot, mn, mj, mx, valid);
+}
+
+JNIEXPORT void JNICALL CLS(watchAsync0)(JNIEnv* env, jclass c, jlong node, jint shard) {
+    (void)c;
+    rh_groups* g = shard_table(env, node, shard);
+    if (g) check(env, rh_watch_levels_async(g));
+}
+
+JNIEXPORT jint JNICALL CLS(watchWait0)(JNIEnv* env, jclass c, jlong node, jint shard, jintArray slot,
+                                       jlongArray mn, jlongArray mj, jlongArray mx, jbooleanArray valid) {
+    (void)c;
+    rh_groups* g = shard_table(env, node, shard);
+    if (!g) return 0;
+    const rh_watch_event* ev = NULL;
+    uint64_t n = 0;
+    if (check(env, rh_watch_levels_wait(g, &ev, &n)) < 0) return 0;
+    return put_levels(env, ev, n, slot, mn, mj, mx, valid);
+}
+
+JNIEXPORT void JNICALL CLS(setEventSink0)(JNIEnv* env, jclass c, jlong node, jint shard, jint sink) {
+    (void)c;
+    rh_groups* g = shard_table(env, node, shard);
+    if (g) check(env, rh_groups_set_event_sink(g, (int)sink));
+}
+
+JNIEXPORT void JNICALL CLS(leaseAsync0)(JNIEnv* env, jclass c, jlong node, jint shard, jlong now, jlong timeout_ms) {
+    (void)c;
+    rh_groups* g = shard_table(env, node, shard);
+    if (g) check(env, rh_lease_batch_async(g, (int64_t)now, (int64_t)timeout_ms));
+}
+
+JNIEXPORT void JNICALL CLS(leaseWait0)(JNIEnv* env, jclass c, jlong node, jint shard, jlongArray bits) {
+    (void)c;
+    rh_groups* g = shard_table(env, node, shard);
+    if (!g) return;
+    const uint64_t* w = NULL;
+    uint64_t words = 0;
+    if (check(env, rh_lease_batch_wait(g, &w, &words)) < 0) return;
+    if (!has_len(env, bits, (int64_t)words, "bits shorter than the shard bitmap")) return;
+    (*env)->SetLongArrayRegion(env, bits, 0, (jsize)words, (const jlong*)w);
 }
 
 JNIEXPORT void JNICALL CLS(leaseStart0)(JNIEnv* env, jclass c, jlong node, jint slot, jlong now, jboolean enabled) {

@@ -231,6 +231,13 @@ _SIGNATURES = {
     "rh_commit_batch_async": (c_int, [c_void_p, c_uint32, POINTER(c_uint64)]),
     "rh_commit_batch_wait": (c_int, [c_void_p, c_uint64, POINTER(RhCommitOut)]),
     "rh_watch_levels": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_uint64)]),
+    "rh_watch_levels_async": (c_int, [c_void_p]),
+    "rh_groups_timing": (c_int, [c_void_p, c_int]),
+    "rh_groups_last_timing": (c_int, [c_void_p, POINTER(ctypes.c_float), POINTER(ctypes.c_float)]),
+    "rh_watch_levels_wait": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_uint64)]),
+    "rh_lease_batch_async": (c_int, [c_void_p, c_int64, c_int64]),
+    "rh_lease_batch_wait": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_uint64)]),
+    "rh_node_watch_levels": (c_int, [c_void_p, c_void_p, c_uint64, POINTER(c_uint64)]),
     "rh_groups_read": (c_int, [c_void_p, c_uint32, c_uint32, ctypes.c_uint8, c_void_p]),
     "rh_shard_of": (c_int, [c_uint64, c_uint64, c_int]),
     "rh_node_create": (c_int, [c_uint32, c_uint64, c_int64, POINTER(c_void_p)]),
@@ -247,6 +254,9 @@ _SIGNATURES = {
                                      POINTER(c_uint64)]),
     "rh_crc32c_frames_launch": (c_int, [c_void_p, POINTER(RhFrames), c_uint32, c_void_p]),
     "rh_crc32c": (c_int, [c_void_p, c_uint32, c_void_p, c_uint64, POINTER(c_uint32)]),
+    "rh_crc32c_stamp_host": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_uint64]),
+    "rh_host_register": (c_int, [c_void_p, c_void_p, c_uint64]),
+    "rh_host_unregister": (c_int, [c_void_p, c_void_p]),
     "rh_crc32c_verify_host": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_uint64, c_void_p,
                                       c_void_p, POINTER(c_uint64)]),
     "rh_lease_soa_launch": (c_int, [c_void_p, POINTER(RhLeaseSoa), c_int, c_void_p]),

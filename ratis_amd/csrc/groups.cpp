@@ -48,20 +48,18 @@ struct TierHost {
 constexpr int kEvSets = 3;  // results of the last three rh_commit_batch_async calls stay readable
 
 struct EvSet {
-    rh_index_event* adv = nullptr;   // host-mapped pinned [cap]
+    rh_index_event* adv = nullptr;   // host-mapped pinned [cap]: the contiguous result lists
     rh_index_event* wall = nullptr;
     rh_index_event* d_adv = nullptr;  // device views of the same memory
     rh_index_event* d_wall = nullptr;
-    rh_index_event* hbm_adv = nullptr;   // RH_EVENTS_DEVICE: the kernel's sink in HBM
+    rh_index_event* hbm_adv = nullptr;   // RH_EVENTS_DEVICE: the gather's contiguous lists in HBM
     rh_index_event* hbm_wall = nullptr;
-    uint64_t* h_bend = nullptr;      // host-mapped per-workgroup list ends (TableEvents::block_end)
-    uint64_t* d_bend = nullptr;
-    uint32_t bend_cap = 0;
-    uint32_t blocks = 0;             // entries of h_bend the pending evaluation writes
+    uint64_t* h_cnt = nullptr;       // host-mapped [2]: list lengths, written by the gather kernel
+    uint64_t* d_cnt = nullptr;
     hipEvent_t done = nullptr;
     uint64_t ticket = 0;
     bool pending = false;
-    bool hbm = false;   // this ticket's events are in hbm_adv / hbm_wall (copied out by _wait)
+    bool hbm = false;   // this ticket's lists are in hbm_adv / hbm_wall (copied out by _wait)
 };
 
 }  // namespace
@@ -96,17 +94,26 @@ struct rh_groups {
     hipStream_t copy_stream = nullptr;
     uint64_t* d_lbits = nullptr;  // rh_lease_batch: slot bitmap (device) and its pinned copy
     uint64_t* h_lbits = nullptr;
-    // events
+    // events (rh_internal.h, TableEvents): head words, HBM staging regions, result sets
     EvSet ev[kEvSets];
     uint64_t next_ticket = 1;
-    unsigned long long* d_counts = nullptr;   // [2 modes][2]: alternating list counters (TableEvents)
-    int cpar[2] = {0, 0};                     // which word of each mode the next evaluation counts into
-    uint64_t* h_wbend = nullptr;              // rh_watch_levels' per-workgroup list ends
-    uint64_t* d_wbend = nullptr;
-    uint32_t wbend_cap = 0;
-    rh_watch_event* watch = nullptr;          // host-mapped pinned [cap]
+    unsigned long long* d_heads = nullptr;    // [2 modes][2 parities][kHeads * kHeadStride]
+    int cpar[2] = {0, 0};                     // which parity set of each mode the next evaluation counts into
+    rh_index_event* st_adv = nullptr;         // staging: kHeads regions of st_region records each
+    rh_index_event* st_wall = nullptr;
+    rh_watch_event* st_watch = nullptr;
+    uint64_t st_region = 0;
+    rh_watch_event* watch = nullptr;          // host-mapped pinned [cap]: rh_watch_levels' list
     rh_watch_event* d_watch = nullptr;
     rh_watch_event* hbm_watch = nullptr;      // RH_EVENTS_DEVICE
+    uint64_t* h_wcnt = nullptr;               // host-mapped [2]: its length (gather kernel)
+    uint64_t* d_wcnt = nullptr;
+    hipEvent_t wdone = nullptr;
+    bool wpending = false, whbm = false;
+    hipEvent_t ldone = nullptr;               // rh_lease_batch_async's bitmap D2H
+    bool lpending = false;
+    hipEvent_t tev[3] = {nullptr, nullptr, nullptr};  // rh_groups_timing: around evaluation and gather
+    bool timing = false, timed = false;
     int event_sink = RH_EVENTS_HOST_MAPPED;
     int64_t* d_read = nullptr;
     size_t read_cap = 0;
@@ -135,11 +142,18 @@ int halloc_mapped(T** host, T** dev, size_t count) {
 }
 
 void free_tier(rh::TableTier& t) {
-    for (void* p : {(void*)t.match, (void*)t.fcommit, (void*)t.flush, (void*)t.commit, (void*)t.tstart,
-                    (void*)t.conf, (void*)t.row_slot, (void*)t.wall, (void*)t.wmin, (void*)t.wmaj, (void*)t.wmax,
-                    (void*)t.dirty, (void*)t.wdirty, (void*)t.fts, (void*)t.lease, (void*)t.lon})
-        (void)hipFree(p);
+    (void)hipFree(t.base);
+    (void)hipFree(t.sum);
     t = rh::TableTier{};
+}
+
+void free_staging(rh_groups* g) {
+    (void)hipFree(g->st_adv);
+    (void)hipFree(g->st_wall);
+    (void)hipFree(g->st_watch);
+    g->st_adv = g->st_wall = nullptr;
+    g->st_watch = nullptr;
+    g->st_region = 0;
 }
 
 void free_groups(rh_groups* g) {
@@ -157,87 +171,54 @@ void free_groups(rh_groups* g) {
     for (int i = 0; i < kEvSets; ++i) {
         if (g->ev[i].adv) (void)hipHostFree(g->ev[i].adv);
         if (g->ev[i].wall) (void)hipHostFree(g->ev[i].wall);
-        if (g->ev[i].h_bend) (void)hipHostFree(g->ev[i].h_bend);
+        if (g->ev[i].h_cnt) (void)hipHostFree(g->ev[i].h_cnt);
         if (g->ev[i].done) (void)hipEventDestroy(g->ev[i].done);
         (void)hipFree(g->ev[i].hbm_adv);
         (void)hipFree(g->ev[i].hbm_wall);
     }
+    free_staging(g);
     (void)hipFree(g->hbm_watch);
-    if (g->h_wbend) (void)hipHostFree(g->h_wbend);
-    (void)hipFree(g->d_counts);
+    (void)hipFree(g->d_heads);
     if (g->watch) (void)hipHostFree(g->watch);
+    if (g->h_wcnt) (void)hipHostFree(g->h_wcnt);
+    if (g->wdone) (void)hipEventDestroy(g->wdone);
+    if (g->ldone) (void)hipEventDestroy(g->ldone);
+    for (hipEvent_t e : g->tev)
+        if (e) (void)hipEventDestroy(e);
     (void)hipFree(g->d_read);
     if (g->copy_stream) (void)hipStreamDestroy(g->copy_stream);
     (void)hipFree(g->d_lbits);
     if (g->h_lbits) (void)hipHostFree(g->h_lbits);
 }
 
-// (Re)allocates tier t with `rows` rows, keeping the first `keep` rows' contents.  Blocks (the
-// old arrays are released after the stream has drained every launch that still names them).
+// (Re)allocates tier t with `rows` rows (a multiple of 128), keeping the old rows' contents: tiles
+// keep their position, so the old tiles and summaries are one copy each and the new tiles start
+// free.  Blocks (the old arrays are released after the stream has drained every launch that still
+// names them).
 int grow_tier(rh_groups* g, int t, uint32_t rows) {
     rh::TableTier n{};
     const rh::TableTier& o = g->dev.tier[t];
     n.width = rh::width_of_tier(t);
     n.rows = rows;
-    const size_t F = n.width;
-    int rc = RH_OK;
-    if (rc == RH_OK) rc = dalloc(&n.match, F * rows);
-    if (rc == RH_OK) rc = dalloc(&n.fcommit, F * rows);
-    if (rc == RH_OK) rc = dalloc(&n.flush, rows);
-    if (rc == RH_OK) rc = dalloc(&n.commit, rows);
-    if (rc == RH_OK) rc = dalloc(&n.tstart, rows);
-    if (rc == RH_OK) rc = dalloc(&n.conf, rows);
-    if (rc == RH_OK) rc = dalloc(&n.row_slot, rows);
-    if (rc == RH_OK) rc = dalloc(&n.wall, rows);
-    if (rc == RH_OK) rc = dalloc(&n.wmin, rows);
-    if (rc == RH_OK) rc = dalloc(&n.wmaj, rows);
-    if (rc == RH_OK) rc = dalloc(&n.wmax, rows);
-    if (rc == RH_OK) rc = dalloc(&n.dirty, rows);
-    if (rc == RH_OK) rc = dalloc(&n.wdirty, rows);
-    if (rc == RH_OK) rc = dalloc(&n.fts, F * rows);
-    if (rc == RH_OK) rc = dalloc(&n.lease, rows);
-    if (rc == RH_OK) rc = dalloc(&n.lon, rows);
+    const uint64_t TB = rh::tile::bytes(n.width);
+    const uint32_t tiles = rows / rh::kTileRows, keep = o.rows / rh::kTileRows;
+    int rc = dalloc(&n.base, (size_t)tiles * TB);
+    if (rc == RH_OK) rc = dalloc(&n.sum, (size_t)tiles * 2);
     if (rc != RH_OK) {
         free_tier(n);
         return rc;
     }
     hipStream_t s = g->ctx->stream;
-    const uint32_t keep = o.rows;
-    auto cp = [&](void* dst, const void* src, size_t bytes) -> hipError_t {
-        return bytes ? hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, s) : hipSuccess;
-    };
     hipError_t e = hipSuccess;
-    // fresh rows: inactive, clean, unowned
-    e = hipMemsetAsync(n.conf, 0, rows * 4, s);
-    if (e == hipSuccess) e = hipMemsetAsync(n.row_slot, 0xFF, rows * 4, s);
-    if (e == hipSuccess) e = hipMemsetAsync(n.dirty, 0, rows, s);
-    if (e == hipSuccess) e = hipMemsetAsync(n.wdirty, 0, rows, s);
-    if (e == hipSuccess) e = hipMemsetAsync(n.lon, 0, rows, s);
-    for (size_t k = 0; k < F && e == hipSuccess && keep; ++k) {
-        e = cp(n.match + k * rows, o.match + k * keep, (size_t)keep * 8);
-        if (e == hipSuccess) e = cp(n.fcommit + k * rows, o.fcommit + k * keep, (size_t)keep * 8);
-        if (e == hipSuccess) e = cp(n.fts + k * rows, o.fts + k * keep, (size_t)keep * 8);
+    if (keep) {
+        e = hipMemcpyAsync(n.base, o.base, (size_t)keep * TB, hipMemcpyDeviceToDevice, s);
+        if (e == hipSuccess) e = hipMemcpyAsync(n.sum, o.sum, (size_t)keep * 2, hipMemcpyDeviceToDevice, s);
     }
-    if (keep && e == hipSuccess) {
-        const size_t k8 = (size_t)keep * 8, k4 = (size_t)keep * 4;
-        if (e == hipSuccess) e = cp(n.flush, o.flush, k8);
-        if (e == hipSuccess) e = cp(n.commit, o.commit, k8);
-        if (e == hipSuccess) e = cp(n.tstart, o.tstart, k8);
-        if (e == hipSuccess) e = cp(n.conf, o.conf, k4);
-        if (e == hipSuccess) e = cp(n.row_slot, o.row_slot, k4);
-        if (e == hipSuccess) e = cp(n.wall, o.wall, k8);
-        if (e == hipSuccess) e = cp(n.wmin, o.wmin, k8);
-        if (e == hipSuccess) e = cp(n.wmaj, o.wmaj, k8);
-        if (e == hipSuccess) e = cp(n.wmax, o.wmax, k8);
-        if (e == hipSuccess) e = cp(n.dirty, o.dirty, keep);
-        if (e == hipSuccess) e = cp(n.wdirty, o.wdirty, keep);
-        if (e == hipSuccess) e = cp(n.lease, o.lease, k8);
-        if (e == hipSuccess) e = cp(n.lon, o.lon, keep);
-    }
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    if (e != hipSuccess) {
+    if (e == hipSuccess) rc = rh_table_init_tiles(n, keep, tiles - keep, s);
+    if (e == hipSuccess && rc == RH_OK) e = hipStreamSynchronize(s);
+    if (e != hipSuccess || rc != RH_OK) {
         free_tier(n);
-        return rh::hip_fail(e, "rh_groups: tier growth");
+        return rc != RH_OK ? rc : rh::hip_fail(e, "rh_groups: tier growth");
     }
     rh::TableTier old = o;
     g->dev.tier[t] = n;
@@ -314,31 +295,79 @@ int queue_op(rh_groups* g, const CtrlOp& op) {
 
 uint32_t enc(int t, uint32_t row) { return ((uint32_t)t << 28) | row; }
 
-// A host-mapped, zeroed array of at least `need` per-workgroup list ends (TableEvents::block_end).
-int ensure_bend(uint64_t** h, uint64_t** d, uint32_t* cap, uint32_t need) {
-    if (need <= *cap) return RH_OK;
-    if (*h) (void)hipHostFree(*h);
-    *h = *d = nullptr;
-    *cap = 0;
-    const uint32_t n = std::max<uint32_t>(need, 256);
-    int rc = halloc_mapped(h, d, n);
-    if (rc != RH_OK) return rc;
-    std::memset(*h, 0, (size_t)n * 8);
-    *cap = n;
+// HBM staging for an evaluation of `blocks` workgroups: kHeads regions of ceil(blocks / kHeads) *
+// rows-per-workgroup records per kind (rh_internal.h, TableEvents).  Grows only; blocks while it
+// reallocates (the stream still reads the old arrays until it drains).
+int ensure_staging(rh_groups* g, uint32_t blocks) {
+    const uint64_t region = (uint64_t)((blocks + rh::kHeads - 1) / rh::kHeads) * rh::table_block_rows();
+    if (region <= g->st_region) return RH_OK;
+    RH_HIP(hipStreamSynchronize(g->ctx->stream));
+    free_staging(g);
+    const uint64_t n = region * rh::kHeads;
+    int rc = dalloc(&g->st_adv, n);
+    if (rc == RH_OK) rc = dalloc(&g->st_wall, n);
+    if (rc == RH_OK) rc = dalloc(&g->st_watch, n);
+    if (rc != RH_OK) {
+        free_staging(g);
+        return rc;
+    }
+    g->st_region = region;
     return RH_OK;
 }
 
-// List lengths of an evaluation from its workgroups' range ends; the entries are cleared for reuse.
-void take_counts(uint64_t* bend, uint32_t blocks, uint64_t* n0, uint64_t* n1) {
-    uint64_t a = 0, b = 0;
-    for (uint32_t i = 0; i < blocks; ++i) {
-        const uint64_t x = bend[i];
-        a = std::max<uint64_t>(a, x & 0xFFFFFFFFull);
-        b = std::max<uint64_t>(b, x >> 32);
-        bend[i] = 0;
+// The head words of (mode, parity).
+unsigned long long* heads_of(rh_groups* g, int mode, int parity) {
+    return g->d_heads + (size_t)(mode * 2 + parity) * rh::kHeads * rh::kHeadStride;
+}
+
+// After a failed evaluation launch (some workgroups may have counted into a head, a later launch
+// of the pair may not have run): drain the stream and zero every head word, so the next
+// evaluation starts from clean counters whichever parity it uses.
+int reset_heads(rh_groups* g) {
+    hipStream_t s = g->ctx->stream;
+    (void)hipStreamSynchronize(s);
+    RH_HIP(hipMemsetAsync(g->d_heads, 0, (size_t)4 * rh::kHeads * rh::kHeadStride * 8, s));
+    RH_HIP(hipStreamSynchronize(s));
+    return RH_OK;
+}
+
+// Enqueues one evaluation (mode) of the dirty rows and the gather of its events into the
+// contiguous lists (adv / wall or watch, each `cap` records; counts_out host-mapped).
+int evaluate(rh_groups* g, int mode, bool wall_on, rh_index_event* adv, rh_index_event* wall,
+             rh_watch_event* watch, uint64_t* counts_out, uint64_t* h_counts) {
+    hipStream_t s = g->ctx->stream;
+    int rc = flush_ops(g);
+    if (rc != RH_OK) return rc;
+    const uint32_t blocks = rh::table_commit_blocks(g->dev);
+    if (blocks == 0) {   // no tier has rows: nothing can be dirty
+        h_counts[0] = h_counts[1] = 0;
+        return RH_OK;
     }
-    *n0 = a;
-    *n1 = b;
+    rc = ensure_staging(g, blocks);
+    if (rc != RH_OK) return rc;
+    const int m = mode == RH_MODE_WATCH ? 1 : 0;
+    rh::TableEvents ev;
+    ev.adv = g->st_adv;
+    ev.wall = wall_on ? g->st_wall : nullptr;
+    ev.watch = g->st_watch;
+    ev.region = g->st_region;
+    ev.heads = heads_of(g, m, g->cpar[m]);
+    ev.heads_next = heads_of(g, m, g->cpar[m] ^ 1);
+    if (g->timing) RH_HIP(hipEventRecord(g->tev[0], s));
+    rc = rh_table_commit(g->dev, mode, ev, s);
+    if (rc == RH_OK && g->timing) RH_HIP(hipEventRecord(g->tev[1], s));
+    if (rc == RH_OK) rc = rh_table_gather(mode, ev, adv, wall, watch, g->capacity, counts_out, s);
+    if (rc == RH_OK && g->timing) {
+        RH_HIP(hipEventRecord(g->tev[2], s));
+        g->timed = true;
+    }
+    if (rc != RH_OK) {
+        const std::string msg = rh_last_error();
+        (void)reset_heads(g);
+        return rh::fail(rc, msg);
+    }
+    g->cpar[m] ^= 1;  // the launch cleared the other set
+    return RH_OK;
 }
 
 int do_stop(rh_groups* g, uint32_t slot) {
@@ -432,12 +461,18 @@ RH_EXPORT int rh_groups_create(rh_ctx* ctx, uint64_t capacity, int64_t gap_thres
     for (int i = 0; i < kEvSets && rc == RH_OK; ++i) {
         if (rc == RH_OK) rc = halloc_mapped(&g->ev[i].adv, &g->ev[i].d_adv, capacity);
         if (rc == RH_OK) rc = halloc_mapped(&g->ev[i].wall, &g->ev[i].d_wall, capacity);
+        if (rc == RH_OK) rc = halloc_mapped(&g->ev[i].h_cnt, &g->ev[i].d_cnt, 2);
         if (rc == RH_OK && hipEventCreateWithFlags(&g->ev[i].done, hipEventDisableTiming) != hipSuccess)
             rc = rh::fail(RH_E_DEVICE, "hipEventCreate(commit batch)");
     }
     if (rc == RH_OK) rc = halloc_mapped(&g->watch, &g->d_watch, capacity);
-    if (rc == RH_OK) rc = dalloc(&g->d_counts, 4);
-    if (rc == RH_OK && hipMemsetAsync(g->d_counts, 0, 4 * sizeof(unsigned long long), s) != hipSuccess)
+    if (rc == RH_OK) rc = halloc_mapped(&g->h_wcnt, &g->d_wcnt, 2);
+    if (rc == RH_OK && hipEventCreateWithFlags(&g->wdone, hipEventDisableTiming) != hipSuccess)
+        rc = rh::fail(RH_E_DEVICE, "hipEventCreate(watch levels)");
+    if (rc == RH_OK && hipEventCreateWithFlags(&g->ldone, hipEventDisableTiming) != hipSuccess)
+        rc = rh::fail(RH_E_DEVICE, "hipEventCreate(lease batch)");
+    if (rc == RH_OK) rc = dalloc(&g->d_heads, (size_t)4 * rh::kHeads * rh::kHeadStride);
+    if (rc == RH_OK && hipMemsetAsync(g->d_heads, 0, (size_t)4 * rh::kHeads * rh::kHeadStride * 8, s) != hipSuccess)
         rc = rh::fail(RH_E_DEVICE, "rh_groups_create: counters");
     if (rc == RH_OK) rc = dalloc(&g->d_lbits, (capacity + 63) / 64);
     if (rc == RH_OK && hipHostMalloc(reinterpret_cast<void**>(&g->h_lbits), (capacity + 63) / 64 * 8) != hipSuccess)
@@ -472,6 +507,7 @@ RH_EXPORT int rh_groups_set_event_sink(rh_groups* g, int sink) {
     std::lock_guard<std::mutex> lk(g->mu);
     for (const EvSet& e : g->ev)
         if (e.pending) return rh::fail(RH_E_STATE, "rh_groups_set_event_sink: an evaluation is in flight");
+    if (g->wpending) return rh::fail(RH_E_STATE, "rh_groups_set_event_sink: a watch evaluation is in flight");
     if (sink == RH_EVENTS_DEVICE && !g->hbm_watch) {  // allocated on first use, kept until destroy
         int rc = RH_OK;
         for (int i = 0; i < kEvSets && rc == RH_OK; ++i) {
@@ -486,12 +522,33 @@ RH_EXPORT int rh_groups_set_event_sink(rh_groups* g, int sink) {
                 e.hbm_adv = e.hbm_wall = nullptr;
             }
             (void)hipFree(g->hbm_watch);
-    if (g->h_wbend) (void)hipHostFree(g->h_wbend);
             g->hbm_watch = nullptr;
             return rc;
         }
     }
     g->event_sink = sink;
+    return RH_OK;
+}
+
+RH_EXPORT int rh_groups_timing(rh_groups* g, int enable) {
+    if (!g) return rh::fail(RH_E_INVAL, "rh_groups_timing: groups == NULL");
+    DeviceGuard dg(g->ctx->device);
+    std::lock_guard<std::mutex> lk(g->mu);
+    for (hipEvent_t& e : g->tev)
+        if (!e && hipEventCreate(&e) != hipSuccess) return rh::fail(RH_E_DEVICE, "hipEventCreate(timing)");
+    g->timing = enable != 0;
+    g->timed = false;
+    return RH_OK;
+}
+
+RH_EXPORT int rh_groups_last_timing(rh_groups* g, float* eval_ms, float* gather_ms) {
+    if (!g || !eval_ms || !gather_ms) return rh::fail(RH_E_INVAL, "rh_groups_last_timing: NULL argument");
+    DeviceGuard dg(g->ctx->device);
+    std::lock_guard<std::mutex> lk(g->mu);
+    if (!g->timed) return rh::fail(RH_E_STATE, "rh_groups_last_timing: no timed evaluation");
+    RH_HIP(hipEventSynchronize(g->tev[2]));
+    RH_HIP(hipEventElapsedTime(eval_ms, g->tev[0], g->tev[1]));
+    RH_HIP(hipEventElapsedTime(gather_ms, g->tev[1], g->tev[2]));
     return RH_OK;
 }
 
@@ -587,27 +644,30 @@ __global__ void table_load_kernel(rh::TableDev T, int t, const uint32_t* __restr
     // cols: [F match][F fcommit][flush][commit][tstart][conf] x m, column-major
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= m) return;
+    namespace tl = rh::tile;
     const rh::TableTier& D = T.tier[t];
     const uint32_t r = rows[i];
-    const uint64_t R = D.rows, F = D.width;
+    const uint32_t F = D.width;
     for (uint32_t k = 0; k < F; ++k) {
-        D.match[k * R + r] = cols[(uint64_t)k * m + i];
-        D.fcommit[k * R + r] = cols[(F + k) * m + i];
-        D.fts[k * R + r] = rh::kNoTimestamp;  // lease state as a fresh start: rh_group_lease_start
+        *D.i64(tl::match(k), r) = cols[(uint64_t)k * m + i];
+        *D.i64(tl::fcommit(F, k), r) = cols[(F + k) * m + i];
+        *D.i64(tl::fts(F, k), r) = rh::kNoTimestamp;  // lease state as a fresh start: rh_group_lease_start
     }
-    D.lease[r] = rh::kNoTimestamp;
-    D.lon[r] = 0;
-    D.flush[r] = cols[(2 * F) * m + i];
-    D.commit[r] = cols[(2 * F + 1) * m + i];
-    D.tstart[r] = cols[(2 * F + 2) * m + i];
-    D.conf[r] = (uint32_t)cols[(2 * F + 3) * m + i];
-    D.wall[r] = INT64_MIN;
-    D.wmin[r] = INT64_MIN;
-    D.wmaj[r] = INT64_MIN;
-    D.wmax[r] = INT64_MIN;
-    D.dirty[r] = 1;
-    D.wdirty[r] = 1;
-    D.row_slot[r] = slots[i];
+    *D.i64(tl::lease(F), r) = rh::kNoTimestamp;
+    *D.u8(tl::kLon, r) = 0;
+    *D.i64(tl::flush(F), r) = cols[(2 * F) * m + i];
+    *D.i64(tl::commit(F), r) = cols[(2 * F + 1) * m + i];
+    *D.i64(tl::tstart(F), r) = cols[(2 * F + 2) * m + i];
+    *D.u32(tl::kConf, r) = (uint32_t)cols[(2 * F + 3) * m + i];
+    *D.i64(tl::wall(F), r) = INT64_MIN;
+    *D.i64(tl::wmin(F), r) = INT64_MIN;
+    *D.i64(tl::wmaj(F), r) = INT64_MIN;
+    *D.i64(tl::wmax(F), r) = INT64_MIN;
+    *D.u8(tl::kDirty, r) = 1;
+    *D.u8(tl::kWdirty, r) = 1;
+    *D.summary(r, 0) = 1;
+    *D.summary(r, 1) = 1;
+    *D.u32(tl::kSlot, r) = slots[i];
     T.slot_map[slots[i]] = ((uint32_t)t << 28) | r;
 }
 
@@ -780,27 +840,16 @@ RH_EXPORT int rh_commit_batch_async(rh_groups* g, uint32_t flags, uint64_t* tick
     const uint64_t tk = g->next_ticket++;
     EvSet& e = g->ev[tk % kEvSets];
     if (e.pending) RH_HIP(hipEventSynchronize(e.done));  // its buffers are about to be rewritten
-    hipStream_t s = g->ctx->stream;
-    int rc = flush_ops(g);
-    if (rc != RH_OK) return rc;
-    const uint32_t blocks = rh::table_commit_blocks(g->dev);
-    rc = ensure_bend(&e.h_bend, &e.d_bend, &e.bend_cap, blocks);
-    if (rc != RH_OK) return rc;
+    e.pending = false;
+    e.ticket = 0;
     const bool hbm = g->event_sink == RH_EVENTS_DEVICE;
-    rh::TableEvents ev;
-    ev.adv = hbm ? e.hbm_adv : e.d_adv;
-    ev.wall = (flags & RH_COMMIT_WATCH_ALL) ? (hbm ? e.hbm_wall : e.d_wall) : nullptr;
-    ev.counts = g->d_counts + g->cpar[0];
-    ev.counts_next = g->d_counts + (g->cpar[0] ^ 1);
-    ev.block_end = e.d_bend;
-    ev.cap = g->capacity;
-    rc = rh_table_commit(g->dev, RH_MODE_COMMIT, ev, s);
+    const bool wall_on = (flags & RH_COMMIT_WATCH_ALL) != 0;
+    int rc = evaluate(g, RH_MODE_COMMIT, wall_on, hbm ? e.hbm_adv : e.d_adv, wall_on ? (hbm ? e.hbm_wall : e.d_wall) : nullptr,
+                      nullptr, e.d_cnt, e.h_cnt);
     if (rc != RH_OK) return rc;
-    if (blocks) g->cpar[0] ^= 1;  // the launch cleared the other word
-    RH_HIP(hipEventRecord(e.done, s));
+    RH_HIP(hipEventRecord(e.done, g->ctx->stream));
     e.ticket = tk;
     e.hbm = hbm;
-    e.blocks = blocks;
     e.pending = true;
     *ticket = tk;
     return RH_OK;
@@ -813,16 +862,13 @@ RH_EXPORT int rh_commit_batch_wait(rh_groups* g, uint64_t ticket, rh_commit_out*
     {
         std::lock_guard<std::mutex> lk(g->mu);
         e = &g->ev[ticket % kEvSets];
-        if (e->ticket != ticket) return rh::fail(RH_E_STATE, "rh_commit_batch_wait: ticket unknown or superseded");
+        if (e->ticket != ticket || ticket == 0) return rh::fail(RH_E_STATE, "rh_commit_batch_wait: ticket unknown or superseded");
     }
     RH_HIP(hipEventSynchronize(e->done));
     std::lock_guard<std::mutex> lk(g->mu);
     if (e->ticket != ticket) return rh::fail(RH_E_STATE, "rh_commit_batch_wait: ticket superseded while waiting");
-    uint64_t na = 0, nw = 0;
-    take_counts(e->h_bend, e->blocks, &na, &nw);
-    e->blocks = 0;
-    na = std::min<uint64_t>(na, g->capacity);
-    nw = std::min<uint64_t>(nw, g->capacity);
+    const uint64_t na = std::min<uint64_t>(e->h_cnt[0], g->capacity);
+    const uint64_t nw = std::min<uint64_t>(e->h_cnt[1], g->capacity);
     if (e->hbm) {  // RH_EVENTS_DEVICE: the counted prefixes to the pinned result buffers
         e->hbm = false;
         hipStream_t s = g->copy_stream;
@@ -845,37 +891,42 @@ RH_EXPORT int rh_commit_batch(rh_groups* g, uint32_t flags, rh_commit_out* out) 
     return rc != RH_OK ? rc : rh_commit_batch_wait(g, tk, out);
 }
 
-RH_EXPORT int rh_watch_levels(rh_groups* g, const rh_watch_event** out_events, uint64_t* out_n) {
-    if (!g || !out_events || !out_n) return rh::fail(RH_E_INVAL, "rh_watch_levels: NULL argument");
+RH_EXPORT int rh_watch_levels_async(rh_groups* g) {
+    if (!g) return rh::fail(RH_E_INVAL, "rh_watch_levels_async: groups == NULL");
     DeviceGuard dg(g->ctx->device);
     std::lock_guard<std::mutex> lk(g->mu);
-    hipStream_t s = g->ctx->stream;
-    int rc = flush_ops(g);
-    if (rc != RH_OK) return rc;
-    const uint32_t blocks = rh::table_commit_blocks(g->dev);
-    rc = ensure_bend(&g->h_wbend, &g->d_wbend, &g->wbend_cap, blocks);
-    if (rc != RH_OK) return rc;
+    if (g->wpending) RH_HIP(hipEventSynchronize(g->wdone));  // the previous list is about to be rewritten
+    g->wpending = false;
     const bool hbm = g->event_sink == RH_EVENTS_DEVICE;
-    rh::TableEvents ev;
-    ev.watch = hbm ? g->hbm_watch : g->d_watch;
-    ev.counts = g->d_counts + 2 + g->cpar[1];
-    ev.counts_next = g->d_counts + 2 + (g->cpar[1] ^ 1);
-    ev.block_end = g->d_wbend;
-    ev.cap = g->capacity;
-    rc = rh_table_commit(g->dev, RH_MODE_WATCH, ev, s);
+    int rc = evaluate(g, RH_MODE_WATCH, false, nullptr, nullptr, hbm ? g->hbm_watch : g->d_watch, g->d_wcnt, g->h_wcnt);
     if (rc != RH_OK) return rc;
-    if (blocks) g->cpar[1] ^= 1;
-    RH_HIP(hipStreamSynchronize(s));
-    uint64_t n = 0, unused = 0;
-    take_counts(g->h_wbend, blocks, &n, &unused);
-    n = std::min<uint64_t>(n, g->capacity);
-    if (hbm && n) {
-        RH_HIP(hipMemcpyAsync(g->watch, g->hbm_watch, n * sizeof(rh_watch_event), hipMemcpyDeviceToHost, s));
-        RH_HIP(hipStreamSynchronize(s));
+    RH_HIP(hipEventRecord(g->wdone, g->ctx->stream));
+    g->whbm = hbm;
+    g->wpending = true;
+    return RH_OK;
+}
+
+RH_EXPORT int rh_watch_levels_wait(rh_groups* g, const rh_watch_event** out_events, uint64_t* out_n) {
+    if (!g || !out_events || !out_n) return rh::fail(RH_E_INVAL, "rh_watch_levels_wait: NULL argument");
+    DeviceGuard dg(g->ctx->device);
+    std::lock_guard<std::mutex> lk(g->mu);
+    if (!g->wpending) return rh::fail(RH_E_STATE, "rh_watch_levels_wait: no watch evaluation in flight");
+    RH_HIP(hipEventSynchronize(g->wdone));
+    const uint64_t n = std::min<uint64_t>(g->h_wcnt[0], g->capacity);
+    if (g->whbm && n) {
+        RH_HIP(hipMemcpyAsync(g->watch, g->hbm_watch, n * sizeof(rh_watch_event), hipMemcpyDeviceToHost, g->copy_stream));
+        RH_HIP(hipStreamSynchronize(g->copy_stream));
     }
+    g->wpending = false;
     *out_events = g->watch;
     *out_n = n;
     return RH_OK;
+}
+
+RH_EXPORT int rh_watch_levels(rh_groups* g, const rh_watch_event** out_events, uint64_t* out_n) {
+    if (!g || !out_events || !out_n) return rh::fail(RH_E_INVAL, "rh_watch_levels: NULL argument");
+    int rc = rh_watch_levels_async(g);
+    return rc != RH_OK ? rc : rh_watch_levels_wait(g, out_events, out_n);
 }
 
 RH_EXPORT int rh_groups_read(rh_groups* g, uint32_t first, uint32_t n, uint8_t column, int64_t* out) {
@@ -928,12 +979,13 @@ RH_EXPORT int rh_group_lease_start(rh_groups* g, uint32_t slot, int64_t now_nano
     return rh_push_deltas(g, d, n);
 }
 
-RH_EXPORT int rh_lease_batch(rh_groups* g, int64_t now_nanos, int64_t timeout_ms, const uint64_t** out_bits,
-                             uint64_t* out_words) {
-    if (!g || !out_bits || !out_words) return rh::fail(RH_E_INVAL, "rh_lease_batch: NULL argument");
-    if (timeout_ms < 0) return rh::fail(RH_E_INVAL, "rh_lease_batch: timeout_ms < 0");
+RH_EXPORT int rh_lease_batch_async(rh_groups* g, int64_t now_nanos, int64_t timeout_ms) {
+    if (!g) return rh::fail(RH_E_INVAL, "rh_lease_batch_async: groups == NULL");
+    if (timeout_ms < 0) return rh::fail(RH_E_INVAL, "rh_lease_batch_async: timeout_ms < 0");
     DeviceGuard dg(g->ctx->device);
     std::lock_guard<std::mutex> lk(g->mu);
+    if (g->lpending) RH_HIP(hipEventSynchronize(g->ldone));  // the pinned bitmap is about to be rewritten
+    g->lpending = false;
     hipStream_t s = g->ctx->stream;
     int rc = flush_ops(g);
     if (rc != RH_OK) return rc;
@@ -942,10 +994,28 @@ RH_EXPORT int rh_lease_batch(rh_groups* g, int64_t now_nanos, int64_t timeout_ms
     rc = rh_table_lease(g->dev, now_nanos, timeout_ms, g->d_lbits, s);
     if (rc != RH_OK) return rc;
     RH_HIP(hipMemcpyAsync(g->h_lbits, g->d_lbits, words * 8, hipMemcpyDeviceToHost, s));
-    RH_HIP(hipStreamSynchronize(s));
-    *out_bits = g->h_lbits;
-    *out_words = words;
+    RH_HIP(hipEventRecord(g->ldone, s));
+    g->lpending = true;
     return RH_OK;
+}
+
+RH_EXPORT int rh_lease_batch_wait(rh_groups* g, const uint64_t** out_bits, uint64_t* out_words) {
+    if (!g || !out_bits || !out_words) return rh::fail(RH_E_INVAL, "rh_lease_batch_wait: NULL argument");
+    DeviceGuard dg(g->ctx->device);
+    std::lock_guard<std::mutex> lk(g->mu);
+    if (!g->lpending) return rh::fail(RH_E_STATE, "rh_lease_batch_wait: no lease batch in flight");
+    RH_HIP(hipEventSynchronize(g->ldone));
+    g->lpending = false;
+    *out_bits = g->h_lbits;
+    *out_words = (g->capacity + 63) / 64;
+    return RH_OK;
+}
+
+RH_EXPORT int rh_lease_batch(rh_groups* g, int64_t now_nanos, int64_t timeout_ms, const uint64_t** out_bits,
+                             uint64_t* out_words) {
+    if (!g || !out_bits || !out_words) return rh::fail(RH_E_INVAL, "rh_lease_batch: NULL argument");
+    int rc = rh_lease_batch_async(g, now_nanos, timeout_ms);
+    return rc != RH_OK ? rc : rh_lease_batch_wait(g, out_bits, out_words);
 }
 
 // ---- multi-GPU node ----------------------------------------------------------------------------------
@@ -1136,13 +1206,19 @@ RH_EXPORT int rh_node_group_lease_start(rh_node* nd, uint32_t node_slot, int64_t
 RH_EXPORT int rh_node_lease_batch(rh_node* nd, int64_t now_nanos, int64_t timeout_ms, uint64_t* out_bits,
                                   uint64_t out_words) {
     if (!nd || !out_bits) return rh::fail(RH_E_INVAL, "rh_node_lease_batch: NULL argument");
+    if (timeout_ms < 0) return rh::fail(RH_E_INVAL, "rh_node_lease_batch: timeout_ms < 0");
     const uint64_t total = nd->cap * nd->tab.size();
     if (out_words < (total + 63) / 64) return rh::fail(RH_E_INVAL, "rh_node_lease_batch: out_bits too small");
+    std::lock_guard<std::mutex> lk(nd->batch_mu);
+    for (size_t sh = 0; sh < nd->tab.size(); ++sh) {  // every shard's pass in flight before any wait
+        int rc = rh_lease_batch_async(nd->tab[sh], now_nanos, timeout_ms);
+        if (rc != RH_OK) return rc;
+    }
     std::memset(out_bits, 0, (total + 63) / 64 * 8);
     for (size_t sh = 0; sh < nd->tab.size(); ++sh) {
         const uint64_t* bits = nullptr;
         uint64_t words = 0;
-        int rc = rh_lease_batch(nd->tab[sh], now_nanos, timeout_ms, &bits, &words);
+        int rc = rh_lease_batch_wait(nd->tab[sh], &bits, &words);
         if (rc != RH_OK) return rc;
         const uint64_t base = sh * nd->cap;  // node slot of the shard's slot 0
         for (uint64_t w = 0; w < words; ++w) {
@@ -1154,5 +1230,29 @@ RH_EXPORT int rh_node_lease_batch(rh_node* nd, int64_t now_nanos, int64_t timeou
             }
         }
     }
+    return RH_OK;
+}
+
+RH_EXPORT int rh_node_watch_levels(rh_node* nd, rh_watch_event* out, uint64_t cap, uint64_t* out_n) {
+    if (!nd || !out_n || (cap && !out)) return rh::fail(RH_E_INVAL, "rh_node_watch_levels: NULL argument");
+    std::lock_guard<std::mutex> lk(nd->batch_mu);
+    for (size_t sh = 0; sh < nd->tab.size(); ++sh) {  // every shard's evaluation in flight before any wait
+        int rc = rh_watch_levels_async(nd->tab[sh]);
+        if (rc != RH_OK) return rc;
+    }
+    uint64_t n = 0;
+    for (size_t sh = 0; sh < nd->tab.size(); ++sh) {
+        const rh_watch_event* ev = nullptr;
+        uint64_t k = 0;
+        int rc = rh_watch_levels_wait(nd->tab[sh], &ev, &k);
+        if (rc != RH_OK) return rc;
+        const uint32_t base = (uint32_t)(sh * nd->cap);
+        for (uint64_t i = 0; i < k; ++i, ++n)
+            if (n < cap) {
+                out[n] = ev[i];
+                out[n].slot += base;
+            }
+    }
+    *out_n = n;
     return RH_OK;
 }

@@ -263,6 +263,78 @@ RH_EXPORT int rh_crc32c_verify_host(rh_ctx* ctx, const uint8_t* seg, uint64_t se
     return RH_OK;
 }
 
+// ---- write side: the trailers of a flush batch (SegmentedRaftLogOutputStream.write, OUT:86-110) ----
+RH_EXPORT int rh_host_register(rh_ctx* ctx, void* p, uint64_t n) {
+    if (!ctx || !p || n == 0) return rh::fail(RH_E_INVAL, "rh_host_register: ctx/p == NULL or n == 0");
+    DeviceGuard g(ctx->device);
+    RH_HIP(hipHostRegister(p, n, hipHostRegisterDefault));
+    return RH_OK;
+}
+
+RH_EXPORT int rh_host_unregister(rh_ctx* ctx, void* p) {
+    if (!ctx || !p) return rh::fail(RH_E_INVAL, "rh_host_unregister: ctx/p == NULL");
+    DeviceGuard g(ctx->device);
+    RH_HIP(hipHostUnregister(p));
+    return RH_OK;
+}
+
+RH_EXPORT int rh_crc32c_stamp_host(rh_ctx* ctx, uint8_t* buf, uint64_t buf_len, const uint64_t* frame_off,
+                                   const uint32_t* frame_len, uint64_t n) {
+    if (!ctx) return rh::fail(RH_E_INVAL, "rh_crc32c_stamp_host: ctx == NULL");
+    if (n == 0) return RH_OK;
+    if (!buf || !frame_off || !frame_len) return rh::fail(RH_E_INVAL, "rh_crc32c_stamp_host: NULL input");
+    if (n >= (1ull << 32)) return rh::fail(RH_E_RANGE, "rh_crc32c_stamp_host: n >= 2^32");
+    // every frame must lie in the buffer and hold its trailer: nothing is stamped otherwise
+    uint64_t lo = UINT64_MAX, hi = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t o = frame_off[i], l = frame_len[i];
+        if (l < 4 || o > buf_len || l > buf_len - o)
+            return rh::fail(RH_E_INVAL, "rh_crc32c_stamp_host: frame " + std::to_string(i) +
+                                            " is shorter than its trailer or outside the buffer");
+        lo = std::min(lo, o);
+        hi = std::max(hi, o + l);
+    }
+    DeviceGuard g(ctx->device);
+    // only the span the frames cover crosses PCIe (a flush batch is one contiguous run); the CRCs come
+    // back as 4 B per frame and the host writes the big-endian trailers
+    auto al = [](uint64_t x) { return (x + 255) / 256 * 256; };
+    const uint64_t span = hi - lo;
+    const uint64_t o_img = 0, o_off = al(span), o_len = o_off + al(n * 8), o_crc = o_len + al(n * 4),
+                   total = o_crc + al(n * 4);
+    hipStream_t s = ctx->stream;
+    rh::PoolScratch scratch(s);
+    if (scratch.alloc(ctx, total) != hipSuccess) return rh::fail(RH_E_NOMEM, "rh_crc32c_stamp_host: device scratch");
+    uint8_t* base = scratch.bytes();
+    std::vector<uint64_t> rel(n);
+    for (uint64_t i = 0; i < n; ++i) rel[i] = frame_off[i] - lo;
+    std::vector<uint32_t> crc(n);
+    RH_HIP(hipMemcpyAsync(base + o_img, buf + lo, span, hipMemcpyHostToDevice, s));
+    RH_HIP(hipMemcpyAsync(base + o_off, rel.data(), n * 8, hipMemcpyHostToDevice, s));
+    RH_HIP(hipMemcpyAsync(base + o_len, frame_len, n * 4, hipMemcpyHostToDevice, s));
+    rh_frames f{};
+    f.buf = base + o_img;
+    f.buf_len = span;
+    f.frame_off = reinterpret_cast<const uint64_t*>(base + o_off);
+    f.frame_len = reinterpret_cast<const uint32_t*>(base + o_len);
+    f.n = n;
+    f.init_state = 0xFFFFFFFFu;   // checksum.reset() before every entry (OUT:100-103)
+    f.crc_out = reinterpret_cast<uint32_t*>(base + o_crc);
+    // STAMP also writes the device copy's trailers; only crc_out comes back
+    int rc = rh_crc_launch_impl(ctx, &f, RH_CRC_STAMP, s);
+    if (rc == RH_OK) RH_HIP(hipMemcpyAsync(crc.data(), base + o_crc, n * 4, hipMemcpyDeviceToHost, s));
+    RH_HIP(hipStreamSynchronize(s));
+    if (rc != RH_OK) return rc;
+    for (uint64_t i = 0; i < n; ++i) {   // buf.putInt((int) checksum.getValue()): big-endian
+        uint8_t* t = buf + frame_off[i] + frame_len[i] - 4;
+        const uint32_t c = crc[i];
+        t[0] = (uint8_t)(c >> 24);
+        t[1] = (uint8_t)(c >> 16);
+        t[2] = (uint8_t)(c >> 8);
+        t[3] = (uint8_t)c;
+    }
+    return RH_OK;
+}
+
 // ---- host-image read path (LogSegment.readSegmentFile over many files in one call) -------------
 RH_EXPORT int rh_segments_read_host(rh_ctx* ctx, const uint8_t* image, uint64_t image_len, const uint64_t* seg_off,
                                     const uint64_t* seg_len, uint64_t n_seg, uint32_t max_op,

@@ -50,35 +50,62 @@ __device__ __forceinline__ const T& kernarg_struct() {
 }
 
 // ---- resident table (rh_groups) device layout --------------------------------------------------
-// Tier t holds slots whose conf names follower slots < width = 2 (t + 1); every column is a
-// contiguous array over the tier's rows (row space), so the commit kernels see a tier exactly as
-// an rh_commit_soa.  slot_map: slot -> (tier << 28) | row, kNoRow = stopped.
+// Tier t holds slots whose conf names follower slots < width = 2 (t + 1).  Rows come in TILES of
+// kTileRows = 128 (one wave of the evaluation kernel: two rows per lane): a tile holds its 128
+// elements of every column back to back, so one wave's reads of a column are one contiguous 1 KiB
+// run and an updateCommit evaluation reads ONE contiguous run per tile (the rh_commit_soa TILED
+// layout, commit.hip).  Byte offsets inside a tile of a tier with F follower columns (tile::):
+//
+//   [0, 128)      dirty    u8    1 = updateCommit pending (UPDATE_COMMIT event, LSI:846-854)
+//   [128, 256)    wdirty   u8    1 = commitIndexChanged pending
+//   [256, 384)    lon      u8    LeaderLease.enabled
+//   [512, 1024)   conf     u32   membership word (0 on free rows)
+//   [1024, 1536)  row_slot u32   row -> slot (kNoRow on free rows)
+//   then int64 columns of 1 KiB each:
+//   match[F] flush tstart commit wall | fcommit[F] wmin wmaj wmax | fts[F] lease
+//
+// COMMIT reads dirty + [conf .. wall] (one run), WATCH wdirty + conf, row_slot, commit, fcommit..wmax,
+// the lease pass conf + fts + lease.  slot_map: slot -> (tier << 28) | row, kNoRow = stopped.
+// Beside the tiles a per-tier SUMMARY of two bytes per tile (sum[2 tile] = some row of the tile is
+// dirty, sum[2 tile + 1] = some row is wdirty), set by every kernel that sets a flag: an evaluation
+// wave whose tile is clean returns after reading that byte, without touching the tile.
 constexpr int kTableTiers = 7;
 constexpr uint32_t kNoRow = 0xFFFFFFFFu;
 constexpr uint32_t kRowMask = 0x0FFFFFFFu;
+constexpr uint32_t kTileRows = 128;
 __host__ __device__ inline int tier_of_width(uint32_t w) { return w <= 2 ? 0 : (int)((w + 1) / 2) - 1; }
 __host__ __device__ inline uint32_t width_of_tier(int t) { return 2u * (uint32_t)(t + 1); }
 
+namespace tile {
+constexpr uint32_t kDirty = 0, kWdirty = 128, kLon = 256, kConf = 512, kSlot = 1024, kMatch = 1536;
+__host__ __device__ constexpr uint32_t match(uint32_t k) { return kMatch + 1024u * k; }
+__host__ __device__ constexpr uint32_t flush(uint32_t F) { return kMatch + 1024u * F; }
+__host__ __device__ constexpr uint32_t tstart(uint32_t F) { return flush(F) + 1024u; }
+__host__ __device__ constexpr uint32_t commit(uint32_t F) { return flush(F) + 2048u; }
+__host__ __device__ constexpr uint32_t wall(uint32_t F) { return flush(F) + 3072u; }
+__host__ __device__ constexpr uint32_t fcommit(uint32_t F, uint32_t k) { return kMatch + 1024u * (F + 4 + k); }
+__host__ __device__ constexpr uint32_t wmin(uint32_t F) { return fcommit(F, F); }
+__host__ __device__ constexpr uint32_t wmaj(uint32_t F) { return wmin(F) + 1024u; }
+__host__ __device__ constexpr uint32_t wmax(uint32_t F) { return wmin(F) + 2048u; }
+__host__ __device__ constexpr uint32_t fts(uint32_t F, uint32_t k) { return kMatch + 1024u * (2 * F + 7 + k); }
+__host__ __device__ constexpr uint32_t lease(uint32_t F) { return fts(F, F); }
+__host__ __device__ constexpr uint32_t bytes(uint32_t F) { return kMatch + 1024u * (3 * F + 8); }
+}  // namespace tile
+
 struct TableTier {
     uint32_t width = 0;         // follower columns F
-    uint32_t rows = 0;          // allocated rows (column stride), multiple of 128
-    int64_t* match = nullptr;   // [F][rows] FollowerInfo.matchIndex
-    int64_t* fcommit = nullptr; // [F][rows] FollowerInfo.commitIndex
-    int64_t* flush = nullptr;   // [rows] leader flushIndex
-    int64_t* commit = nullptr;  // [rows] leader commitIndex (lastCommittedIndex)
-    int64_t* tstart = nullptr;  // [rows] first index of the current term
-    uint32_t* conf = nullptr;   // [rows] membership word (0 on free rows)
-    uint32_t* row_slot = nullptr;  // [rows] row -> slot
-    int64_t* wall = nullptr;    // [rows] last watch-ALL level of updateCommit (INT64_MIN = none)
-    int64_t* wmin = nullptr;    // [rows] last commitIndexChanged levels
-    int64_t* wmaj = nullptr;
-    int64_t* wmax = nullptr;
-    uint8_t* dirty = nullptr;   // [rows] 1 = updateCommit pending
-    uint8_t* wdirty = nullptr;  // [rows] 1 = commitIndexChanged pending
-    int64_t* fts = nullptr;     // [F][rows] FollowerInfo.lastRespondedAppendEntriesSendTime (nanos,
-                                //           kNoTimestamp until the module sets it)
-    int64_t* lease = nullptr;   // [rows] LeaderLease.lease (nanos)
-    uint8_t* lon = nullptr;     // [rows] LeaderLease.enabled
+    uint32_t rows = 0;          // allocated rows, a multiple of kTileRows
+    uint8_t* base = nullptr;    // [rows / 128] tiles of tile::bytes(width)
+    uint8_t* sum = nullptr;     // [rows / 128][2] tile summaries (dirty, wdirty)
+    // element `r` of the column at tile offset `off` (element size sizeof(T))
+    template <typename T>
+    __host__ __device__ T* at(uint32_t off, uint64_t r) const {
+        return reinterpret_cast<T*>(base + (r >> 7) * (uint64_t)tile::bytes(width) + off + (r & 127) * sizeof(T));
+    }
+    __host__ __device__ int64_t* i64(uint32_t off, uint64_t r) const { return at<int64_t>(off, r); }
+    __host__ __device__ uint32_t* u32(uint32_t off, uint64_t r) const { return at<uint32_t>(off, r); }
+    __host__ __device__ uint8_t* u8(uint32_t off, uint64_t r) const { return at<uint8_t>(off, r); }
+    __host__ __device__ uint8_t* summary(uint64_t r, int watch) const { return sum + 2 * (r >> 7) + watch; }
 };
 // A follower column that has no lastRespondedAppendEntriesSendTime yet (a FollowerInfo the module
 // has not stamped): never active, never the majority-ack time.
@@ -106,26 +133,31 @@ struct CtrlOp {
     int64_t flush, commit, tstart;  // START
 };
 
-// Event sinks of the table kernels.  Records go to adv / wall / watch (host-mapped pinned memory,
-// or HBM under RH_EVENTS_DEVICE).  Every workgroup takes its range of the lists from one device
-// counter word (kind 0 in the low 32 bits, kind 1 in the high 32) and writes the end of its range
-// (packed the same way) into its own entry of `block_end`, host-mapped memory: the host reads the
-// list lengths as the maxima over those entries, so no memset and no read-back of the counter sits
-// on the stream.  The counters alternate between two words per kind of evaluation: a launch
-// counts into `counts` and clears `counts_next`, the word the following evaluation counts into.
+// Event lists of the evaluation kernels.  A single device-scope counter word admits ~88 returning
+// atomics per us (MI355X_MICROARCH.md, 'dequeue' / 'fanin'): one per workgroup held a sparse
+// evaluation of 1M rows at ~8 us.  So the lists are SHARDED over kHeads head words, one per XCD
+// under round-robin workgroup placement (head = launch-global block index & 7): workgroup b takes
+// its range of region (b & 7) from that region's head, in the HBM staging arrays, and a gather
+// kernel (table_gather_kernel) then packs the kHeads regions into the contiguous result lists.  A
+// region holds ceil(blocks / kHeads) * kTRows records: a workgroup emits at most one record of a
+// kind per row, so no region can overflow.  Head words pack kind 0 (low 32 bits) and kind 1 (high);
+// an evaluation counts into `heads` and clears `heads_next`, the set the following evaluation of
+// the same mode counts into (no memset on the stream).
+constexpr int kHeads = 8;
+constexpr int kHeadStride = 32;   // u64 words between heads: each on its own 256-B line
 struct TableEvents {
-    rh_index_event* adv = nullptr;     // COMMIT: advanced
-    rh_index_event* wall = nullptr;    // COMMIT: watch-ALL changes
-    rh_watch_event* watch = nullptr;   // WATCH: level changes
-    unsigned long long* counts = nullptr;       // device word of this evaluation (zero at launch)
-    unsigned long long* counts_next = nullptr;  // device word of the next one: cleared by block 0
-    uint64_t* block_end = nullptr;              // host-mapped [blocks]: packed end of each block's range
-    uint32_t block_base = 0;                     // this launch's first entry in block_end
-    uint64_t cap = 0;
+    rh_index_event* adv = nullptr;     // COMMIT: advanced (staging, kHeads regions)
+    rh_index_event* wall = nullptr;    // COMMIT: watch-ALL changes (staging), or null (not reported)
+    rh_watch_event* watch = nullptr;   // WATCH: level changes (staging)
+    uint64_t region = 0;               // records per head region
+    unsigned long long* heads = nullptr;       // this evaluation's kHeads words (zero at launch)
+    unsigned long long* heads_next = nullptr;  // the next evaluation's: cleared by block 0
+    uint32_t block_base = 0;                    // launch-global index of this launch's block 0
 };
-// Workgroups the table evaluation launches for a table (both width classes): the size of the
-// block_end array an evaluation needs.
+// Workgroups the table evaluation launches for a table (both width classes).
 uint32_t table_commit_blocks(const TableDev& t);
+// Rows per evaluation workgroup (the staging region unit).
+uint32_t table_block_rows();
 
 }  // namespace rh
 
@@ -171,6 +203,13 @@ int rh_commit_launch_impl(rh_ctx* ctx, const rh_commit_soa* tiers, int n_tiers, 
 int rh_table_apply_deltas(const rh::TableDev& t, const rh_delta* d_deltas, uint64_t n, int phase, hipStream_t stream);
 int rh_table_control(const rh::TableDev& t, const rh::CtrlOp* d_ops, uint64_t n, hipStream_t stream);
 int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev, hipStream_t stream);
+// Packs an evaluation's kHeads staging regions into contiguous lists (up to `cap` records per kind)
+// and writes the two list lengths to counts_out[0..1] (host-mapped): COMMIT (adv, wall; wall may
+// be null) or WATCH (watch records into out_watch, length in counts_out[0]).
+int rh_table_gather(int mode, const rh::TableEvents& ev, rh_index_event* out_adv, rh_index_event* out_wall,
+                    rh_watch_event* out_watch, uint64_t cap, uint64_t* counts_out, hipStream_t stream);
+// Initialises tiles [first_tile, n_tiles) of a tier as free rows (conf 0, row_slot kNoRow, clean).
+int rh_table_init_tiles(const rh::TableTier& t, uint32_t first_tile, uint32_t n_tiles, hipStream_t stream);
 int rh_table_lease(const rh::TableDev& t, int64_t now_nanos, int64_t timeout_ms, uint64_t* d_slot_bits,
                    hipStream_t stream);
 int rh_table_read(const rh::TableDev& t, uint32_t first, uint32_t n, uint8_t column, int64_t* d_out,

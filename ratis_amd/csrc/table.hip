@@ -10,14 +10,15 @@
 //                         conf change with follower carry-over / reset, step down.
 //   table_commit_kernel   LeaderStateImpl.updateCommit() (COMMIT) or commitIndexChanged() (WATCH)
 //                         over the DIRTY rows of every tier; only changed results become events,
-//                         written straight into host-mapped pinned memory.
+//                         staged in HBM per XCD head; table_gather_kernel packs them into the
+//                         contiguous result lists (host-mapped pinned memory or HBM).
 //   table_lease_kernel    LeaderStateImpl.hasLease() (LSI:1229-1249) with LeaderLease.extend (LL:67-84)
 //                         for every started slot: lease_eval.h's arithmetic over the follower
 //                         timestamp columns, the lease stored in place, a slot-indexed bitmap out.
 //   table_read_kernel     slot-ordered read-back of one column.
 //
-// Rows of a tier are laid out exactly like an rh_commit_soa tier (column-major, 16-byte aligned
-// columns), so the per-group arithmetic is commit_eval.h's, shared with the raw SoA kernels.
+// Rows of a tier are laid out in 128-row tiles (rh_internal.h, tile::), the TILED layout of the
+// raw rh_commit_soa kernels; the per-group arithmetic is commit_eval.h's, shared with them.
 // Integer compare/select work, no MFMA; HBM-bound over the dirty rows.
 #include "rh_internal.h"
 #include "commit_eval.h"
@@ -29,6 +30,7 @@ using rh::CtrlOp;
 using rh::TableDev;
 using rh::TableEvents;
 using rh::TableTier;
+namespace tile = rh::tile;
 
 typedef int64_t v2i64 __attribute__((ext_vector_type(2)));
 typedef uint32_t v2u32 __attribute__((ext_vector_type(2)));
@@ -42,6 +44,13 @@ __device__ __forceinline__ bool locate(const TableDev& T, uint32_t slot, const T
     tt = &T.tier[t];
     row = m & rh::kRowMask;
     return row < tt->rows;
+}
+
+// Marks a row dirty for updateCommit (watch = 0) or commitIndexChanged (watch = 1), with its tile's
+// summary byte (plain byte stores: every writer stores 1).
+__device__ __forceinline__ void mark(const TableTier& tt, uint64_t r, int watch) {
+    *tt.u8(watch ? tile::kWdirty : tile::kDirty, r) = 1;
+    *tt.summary(r, watch) = 1;
 }
 
 // ---- deltas --------------------------------------------------------------------------------------
@@ -62,29 +71,30 @@ __global__ __launch_bounds__(256) void table_apply_kernel(TableDev Targ, const r
     if (!locate(T, x.slot, tt, row)) return;  // stopped slot / out of range: ignored
     int64_t* p = nullptr;
     bool commit_ev = false, watch_ev = false;
-    const uint32_t c = x.column;
+    const uint32_t c = x.column, F = tt->width;
     if (c == RH_COL_LEASE_ON) {  // AtomicBoolean: SET stores, MAX ORs
+        uint8_t* f = tt->u8(tile::kLon, row);
         if (phase == 0)
-            tt->lon[row] = x.value != 0;
+            *f = x.value != 0;
         else if (x.value != 0)
-            tt->lon[row] = 1;
+            *f = 1;
         return;
     }
     if (c >= 48 && c < 64) {
-        if (c - 48 < tt->width) p = tt->fts + (uint64_t)(c - 48) * tt->rows + row;
+        if (c - 48 < F) p = tt->i64(tile::fts(F, c - 48), row);
     } else if (c == RH_COL_LEASE) {
-        p = tt->lease + row;
+        p = tt->i64(tile::lease(F), row);
     } else if (c < 16) {
-        if (c < tt->width) p = tt->match + (uint64_t)c * tt->rows + row;
+        if (c < F) p = tt->i64(tile::match(c), row);
         commit_ev = true;
     } else if (c < 32) {
-        if (c - 16 < tt->width) p = tt->fcommit + (uint64_t)(c - 16) * tt->rows + row;
+        if (c - 16 < F) p = tt->i64(tile::fcommit(F, c - 16), row);
         watch_ev = true;
     } else if (c == RH_COL_FLUSH) {
-        p = tt->flush + row;
+        p = tt->i64(tile::flush(F), row);
         commit_ev = true;
     } else if (c == RH_COL_COMMITTED) {
-        p = tt->commit + row;
+        p = tt->i64(tile::commit(F), row);
         commit_ev = watch_ev = true;
     }
     if (!p) return;
@@ -92,102 +102,120 @@ __global__ __launch_bounds__(256) void table_apply_kernel(TableDev Targ, const r
         *p = x.value;
     else
         atomicMax(reinterpret_cast<long long*>(p), (long long)x.value);
-    if (commit_ev) tt->dirty[row] = 1;
-    if (watch_ev) tt->wdirty[row] = 1;
+    if (commit_ev) mark(*tt, row, 0);
+    if (watch_ev) mark(*tt, row, 1);
 }
 
 // ---- control ops ---------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void table_control_kernel(TableDev T, const CtrlOp* __restrict__ ops, uint64_t n) {
+__global__ __launch_bounds__(256) void table_control_kernel(TableDev Targ, const CtrlOp* __restrict__ ops, uint64_t n) {
+    const TableDev& T = rh::kernarg_struct<TableDev>();
+    (void)Targ;
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const CtrlOp op = ops[i];
     if (op.kind == rh::kCtrlStop) {
         const TableTier& s = T.tier[op.src >> 28];
         const uint32_t r = op.src & rh::kRowMask;
-        s.conf[r] = 0u;
-        s.dirty[r] = 0;
-        s.wdirty[r] = 0;
-        s.lon[r] = 0;
-        s.row_slot[r] = rh::kNoRow;
+        *s.u32(tile::kConf, r) = 0u;
+        *s.u8(tile::kDirty, r) = 0;
+        *s.u8(tile::kWdirty, r) = 0;
+        *s.u8(tile::kLon, r) = 0;
+        *s.u32(tile::kSlot, r) = rh::kNoRow;
         T.slot_map[op.slot] = rh::kNoRow;
         return;
     }
     const TableTier& D = T.tier[op.dst >> 28];
     const uint32_t r = op.dst & rh::kRowMask;
-    const uint64_t R = D.rows;
+    const uint32_t DF = D.width;
     if (op.kind == rh::kCtrlStart) {
-        for (uint32_t k = 0; k < D.width; ++k) {
-            D.match[k * R + r] = -1;   // RaftLog.INVALID_LOG_INDEX (FollowerInfoImpl.java:42-43)
-            D.fcommit[k * R + r] = -1;
-            D.fts[k * R + r] = rh::kNoTimestamp;
+        for (uint32_t k = 0; k < DF; ++k) {
+            *D.i64(tile::match(k), r) = -1;   // RaftLog.INVALID_LOG_INDEX (FollowerInfoImpl.java:42-43)
+            *D.i64(tile::fcommit(DF, k), r) = -1;
+            *D.i64(tile::fts(DF, k), r) = rh::kNoTimestamp;
         }
-        D.lease[r] = rh::kNoTimestamp;  // rh_group_lease_start sets the LeaderLease
-        D.lon[r] = 0;
-        D.flush[r] = op.flush;
-        D.commit[r] = op.commit;
-        D.tstart[r] = op.tstart;
-        D.wall[r] = INT64_MIN;
-        D.wmin[r] = INT64_MIN;
-        D.wmaj[r] = INT64_MIN;
-        D.wmax[r] = INT64_MIN;
+        *D.i64(tile::lease(DF), r) = rh::kNoTimestamp;  // rh_group_lease_start sets the LeaderLease
+        *D.u8(tile::kLon, r) = 0;
+        *D.i64(tile::flush(DF), r) = op.flush;
+        *D.i64(tile::commit(DF), r) = op.commit;
+        *D.i64(tile::tstart(DF), r) = op.tstart;
+        *D.i64(tile::wall(DF), r) = INT64_MIN;
+        *D.i64(tile::wmin(DF), r) = INT64_MIN;
+        *D.i64(tile::wmaj(DF), r) = INT64_MIN;
+        *D.i64(tile::wmax(DF), r) = INT64_MIN;
     } else {  // MOVE (to another tier) or RECONF (same row): follower columns through the map
         const TableTier& S = T.tier[op.src >> 28];
         const uint32_t sr = op.src & rh::kRowMask;
-        const uint64_t SR = S.rows;
+        const uint32_t SF = S.width;
         int64_t m[RH_MAX_FOLLOWERS], f[RH_MAX_FOLLOWERS], ts[RH_MAX_FOLLOWERS];
-        for (uint32_t k = 0; k < D.width; ++k) {  // read all first: RECONF may permute in place
+        for (uint32_t k = 0; k < DF; ++k) {  // read all first: RECONF may permute in place
             const int src = op.map[k];
-            const bool keep = src >= 0 && (uint32_t)src < S.width;
-            m[k] = keep ? S.match[(uint64_t)src * SR + sr] : -1;
-            f[k] = keep ? S.fcommit[(uint64_t)src * SR + sr] : -1;
-            ts[k] = keep ? S.fts[(uint64_t)src * SR + sr] : rh::kNoTimestamp;
+            const bool keep = src >= 0 && (uint32_t)src < SF;
+            m[k] = keep ? *S.i64(tile::match(src), sr) : -1;
+            f[k] = keep ? *S.i64(tile::fcommit(SF, src), sr) : -1;
+            ts[k] = keep ? *S.i64(tile::fts(SF, src), sr) : rh::kNoTimestamp;
         }
-        for (uint32_t k = 0; k < D.width; ++k) {
-            D.match[k * R + r] = m[k];
-            D.fcommit[k * R + r] = f[k];
-            D.fts[k * R + r] = ts[k];
+        for (uint32_t k = 0; k < DF; ++k) {
+            *D.i64(tile::match(k), r) = m[k];
+            *D.i64(tile::fcommit(DF, k), r) = f[k];
+            *D.i64(tile::fts(DF, k), r) = ts[k];
         }
         if (op.kind == rh::kCtrlMove) {
-            D.flush[r] = S.flush[sr];
-            D.commit[r] = S.commit[sr];
-            D.tstart[r] = S.tstart[sr];
-            D.wall[r] = S.wall[sr];
-            D.wmin[r] = S.wmin[sr];
-            D.wmaj[r] = S.wmaj[sr];
-            D.wmax[r] = S.wmax[sr];
-            D.lease[r] = S.lease[sr];
-            D.lon[r] = S.lon[sr];
-            S.lon[sr] = 0;
-            S.conf[sr] = 0u;
-            S.dirty[sr] = 0;
-            S.wdirty[sr] = 0;
-            S.row_slot[sr] = rh::kNoRow;
+            *D.i64(tile::flush(DF), r) = *S.i64(tile::flush(SF), sr);
+            *D.i64(tile::commit(DF), r) = *S.i64(tile::commit(SF), sr);
+            *D.i64(tile::tstart(DF), r) = *S.i64(tile::tstart(SF), sr);
+            *D.i64(tile::wall(DF), r) = *S.i64(tile::wall(SF), sr);
+            *D.i64(tile::wmin(DF), r) = *S.i64(tile::wmin(SF), sr);
+            *D.i64(tile::wmaj(DF), r) = *S.i64(tile::wmaj(SF), sr);
+            *D.i64(tile::wmax(DF), r) = *S.i64(tile::wmax(SF), sr);
+            *D.i64(tile::lease(DF), r) = *S.i64(tile::lease(SF), sr);
+            *D.u8(tile::kLon, r) = *S.u8(tile::kLon, sr);
+            *S.u8(tile::kLon, sr) = 0;
+            *S.u32(tile::kConf, sr) = 0u;
+            *S.u8(tile::kDirty, sr) = 0;
+            *S.u8(tile::kWdirty, sr) = 0;
+            *S.u32(tile::kSlot, sr) = rh::kNoRow;
         }
     }
-    D.conf[r] = op.conf;
-    D.row_slot[r] = op.slot;
-    D.dirty[r] = 1;
-    D.wdirty[r] = 1;
+    *D.u32(tile::kConf, r) = op.conf;
+    *D.u32(tile::kSlot, r) = op.slot;
+    mark(D, r, 0);
+    mark(D, r, 1);
     T.slot_map[op.slot] = op.dst;
 }
 
+// Fresh tiles: every row free (conf 0, unowned), clean, lease off; summaries clear.
+__global__ __launch_bounds__(128) void table_init_tiles_kernel(TableTier tt, uint32_t first_tile) {
+    const uint64_t r = (uint64_t)(first_tile + blockIdx.x) * rh::kTileRows + threadIdx.x;
+    *tt.u8(tile::kDirty, r) = 0;
+    *tt.u8(tile::kWdirty, r) = 0;
+    *tt.u8(tile::kLon, r) = 0;
+    *tt.u32(tile::kConf, r) = 0u;
+    *tt.u32(tile::kSlot, r) = rh::kNoRow;
+    if (threadIdx.x < 2) *tt.summary(r, (int)threadIdx.x) = 0;
+}
+
 // ---- updateCommit / commitIndexChanged over the dirty rows ---------------------------------------
-// One workgroup = 16 waves x 128 rows.  Every wave evaluates its rows' results in registers, the
-// block gathers its events in LDS in wave order, takes ONE range of the output list with ONE
-// device-scope atomic (a single counter word saturates at ~88 returning atomics per us,
-// MI355X_MICROARCH.md 'dequeue': one per 128-row wave cost ~90 us per 1M rows), and copies the
-// records out as contiguous 16-byte-per-lane stores (host-mapped memory: full PCIe write lines).
+// One workgroup = kTWaves waves, one 128-row tile per wave.  Every wave evaluates its rows' results
+// in registers, the block gathers its events in LDS in wave order, takes ONE range of its head's
+// staging region with ONE device-scope atomic on that head (rh_internal.h, TableEvents: the heads
+// are sharded per XCD), and copies the records out as contiguous 16-byte-per-lane stores.
 struct TierRange {
     uint32_t block_begin[rh::kTableTiers + 1];  // blocks of launch slot i: [block_begin[i], block_begin[i+1])
     int8_t tier[rh::kTableTiers];               // tier of launch slot i (widest first)
     int32_t n_slots;
 };
 
-#ifndef RH_TABLE_BLOCK_WAVES                 // A/B: waves per workgroup (128 rows each)
+#ifndef RH_TABLE_BLOCK_WAVES                 // A/B: waves per workgroup (one tile each)
 #define RH_TABLE_BLOCK_WAVES 12
 #endif
 #ifndef RH_TABLE_WPE                         // A/B: waves per SIMD the widths-2..6 kernel is pinned to
 #define RH_TABLE_WPE 6
+#endif
+#ifndef RH_TABLE_PERSIST                     // A/B: cap the evaluation grid at this many workgroups (0: none)
+#define RH_TABLE_PERSIST 0
+#endif
+#ifndef RH_TABLE_SUMMARY                     // A/B: skip clean tiles by their summary byte (1) or not (0)
+#define RH_TABLE_SUMMARY 1
 #endif
 constexpr int kTWaves = RH_TABLE_BLOCK_WAVES;
 constexpr int kTBlock = kTWaves * 64;
@@ -197,7 +225,7 @@ constexpr uint32_t kTRows = kTWaves * 128;   // rows per workgroup
 #endif
 
 template <typename V>
-__device__ __forceinline__ V tload(const void* p) {
+__device__ __forceinline__ V tload(const uint8_t* p) {
     if (RH_TABLE_NT) return __builtin_nontemporal_load(reinterpret_cast<const V*>(p));
     return *reinterpret_cast<const V*>(p);
 }
@@ -208,34 +236,40 @@ __device__ __forceinline__ V tload(const void* p) {
 struct Stage {
     uint32_t cnt[2][kTWaves];
     uint32_t pre[2][kTWaves + 1];  // exclusive prefix of cnt over the waves
-    unsigned long long base;        // the block's range in the output lists (both kinds packed)
+    unsigned long long base;        // the block's range in its head's region (both kinds packed)
 };
 
 template <int F, bool RANK, bool WATCH>
-__device__ __forceinline__ void table_wave(const TableDev& T, const TableTier& tt, uint64_t wbase, bool wall_on,
+__device__ __forceinline__ void table_wave(const TableDev& T, const TableTier& tt, uint64_t tl, bool wall_on,
                                            unsigned char* stage, Stage& sc) {
     constexpr int N = F + 1;
+    constexpr uint64_t TB = tile::bytes(F);
     const int lane = threadIdx.x & 63;
-    const uint64_t r0 = wbase + 2 * (uint64_t)lane;  // rows is a multiple of 128: r0 + 1 < rows
-    uint8_t* dflag = WATCH ? tt.wdirty : tt.dirty;
-    const uint16_t dd = *reinterpret_cast<const uint16_t*>(dflag + r0);
+    uint8_t* tb = tt.base + tl * TB;   // this wave's tile: rows 128 tl .. 128 tl + 127
+    uint8_t* sump = tt.sum + 2 * tl + (WATCH ? 1 : 0);
+    if (RH_TABLE_SUMMARY && *sump == 0) return;  // clean tile: its flag line is not read
+    uint8_t* dflag = tb + (WATCH ? tile::kWdirty : tile::kDirty) + 2 * lane;
+    const uint16_t dd = *reinterpret_cast<const uint16_t*>(dflag);
     const bool d0 = (dd & 0xFFu) != 0, d1 = (dd >> 8) != 0;
     const bool need = d0 || d1;
-    if (!__any(need)) return;  // the whole 128-row sub-tile is clean: 1 byte per row read
+    if (!__any(need)) {
+        if (lane == 0) *sump = 0;
+        return;
+    }
     int64_t fv[2][F], self[2] = {0, 0}, cin[2] = {0, 0}, ts[2] = {0, 0};
     int64_t p0[2] = {0, 0}, p1[2] = {0, 0}, p2[2] = {0, 0};
     uint32_t w[2] = {0u, 0u}, slot[2] = {0u, 0u};
+    const uint32_t l16 = 16u * lane, l8 = 8u * lane;
     if (need) {  // every load of the row pair is issued before any result is used
-        const int64_t* col = WATCH ? tt.fcommit : tt.match;
 #pragma unroll
         for (int k = 0; k < F; ++k) {
-            const v2i64 x = tload<v2i64>(col + (uint64_t)k * tt.rows + r0);
+            const v2i64 x = tload<v2i64>(tb + (WATCH ? tile::fcommit(F, k) : tile::match(k)) + l16);
             fv[0][k] = x.x;
             fv[1][k] = x.y;
         }
-        const v2u32 c = tload<v2u32>(tt.conf + r0);
-        const v2u32 sl = tload<v2u32>(tt.row_slot + r0);
-        const v2i64 cm = tload<v2i64>(tt.commit + r0);
+        const v2u32 c = tload<v2u32>(tb + tile::kConf + l8);
+        const v2u32 sl = tload<v2u32>(tb + tile::kSlot + l8);
+        const v2i64 cm = tload<v2i64>(tb + tile::commit(F) + l16);
         slot[0] = sl.x;
         slot[1] = sl.y;
         w[0] = d0 ? c.x : 0u;  // a clean row is evaluated as inactive and produces nothing
@@ -245,16 +279,16 @@ __device__ __forceinline__ void table_wave(const TableDev& T, const TableTier& t
         if (WATCH) {
             self[0] = cm.x;  // lastCommittedIndex is the self value (LSI:613)
             self[1] = cm.y;
-            const v2i64 a = tload<v2i64>(tt.wmin + r0);
-            const v2i64 b = tload<v2i64>(tt.wmaj + r0);
-            const v2i64 e = tload<v2i64>(tt.wmax + r0);
+            const v2i64 a = tload<v2i64>(tb + tile::wmin(F) + l16);
+            const v2i64 b = tload<v2i64>(tb + tile::wmaj(F) + l16);
+            const v2i64 e = tload<v2i64>(tb + tile::wmax(F) + l16);
             p0[0] = a.x, p0[1] = a.y, p1[0] = b.x, p1[1] = b.y, p2[0] = e.x, p2[1] = e.y;
         } else {
-            const v2i64 fl = tload<v2i64>(tt.flush + r0);
-            const v2i64 st = tload<v2i64>(tt.tstart + r0);
+            const v2i64 fl = tload<v2i64>(tb + tile::flush(F) + l16);
+            const v2i64 st = tload<v2i64>(tb + tile::tstart(F) + l16);
             self[0] = fl.x, self[1] = fl.y, ts[0] = st.x, ts[1] = st.y;
             if (wall_on) {  // watch-ALL levels are compared only when reported (RH_COMMIT_WATCH_ALL)
-                const v2i64 wa = tload<v2i64>(tt.wall + r0);
+                const v2i64 wa = tload<v2i64>(tb + tile::wall(F) + l16);
                 p0[0] = wa.x, p0[1] = wa.y;
             }
         }
@@ -291,29 +325,31 @@ __device__ __forceinline__ void table_wave(const TableDev& T, const TableTier& t
             x0[g] = nc, x1[g] = mn, x2[g] = 0;
         }
     }
-    // table stores: only what changed, plus clearing the dirty flags of this lane's rows
-    if (need) *reinterpret_cast<uint16_t*>(dflag + r0) = 0;
+    // table stores: only what changed, plus clearing this lane's dirty flags and the tile summary
+    if (need) *reinterpret_cast<uint16_t*>(dflag) = 0;
+    if (lane == 0) *sump = 0;
+    const uint64_t a0 = __ballot(e0[0]), a1 = __ballot(e0[1]);
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
-        const uint64_t r = r0 + g;
+        const uint32_t ro = 2u * lane + g;
         if (WATCH) {
             if (e0[g]) {
-                tt.wmin[r] = x0[g];
-                tt.wmaj[r] = x1[g];
-                tt.wmax[r] = x2[g];
+                reinterpret_cast<int64_t*>(tb + tile::wmin(F))[ro] = x0[g];
+                reinterpret_cast<int64_t*>(tb + tile::wmaj(F))[ro] = x1[g];
+                reinterpret_cast<int64_t*>(tb + tile::wmax(F))[ro] = x2[g];
             }
         } else {
             if (e0[g]) {
-                tt.commit[r] = x0[g];
-                tt.wdirty[r] = 1;  // the commit index changed: commitIndexChanged follows (LSI:1003)
+                reinterpret_cast<int64_t*>(tb + tile::commit(F))[ro] = x0[g];
+                tb[tile::kWdirty + ro] = 1;  // the commit index changed: commitIndexChanged follows (LSI:1003)
             }
-            if (e1[g]) tt.wall[r] = x1[g];
+            if (e1[g]) reinterpret_cast<int64_t*>(tb + tile::wall(F))[ro] = x1[g];
         }
     }
+    if (!WATCH && (a0 | a1) && lane == 0) tt.sum[2 * tl + 1] = 1;
     // events: compacted into this wave's LDS region, in row order
     const int wave = threadIdx.x >> 6;
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    const uint64_t a0 = __ballot(e0[0]), a1 = __ballot(e0[1]);
     uint32_t p = (uint32_t)(__popcll(a0 & lt) + __popcll(a1 & lt));
     if (WATCH) {
         rh_watch_event* sw = reinterpret_cast<rh_watch_event*>(stage) + wave * 128;
@@ -336,36 +372,43 @@ __device__ __forceinline__ void table_wave(const TableDev& T, const TableTier& t
 }
 
 template <int F, int FHI, bool RANK, bool WATCH>
-__device__ __forceinline__ void table_dispatch(const TableDev& T, int t, uint64_t wbase, bool wall_on,
+__device__ __forceinline__ void table_dispatch(const TableDev& T, int t, uint64_t tl, bool wall_on,
                                                unsigned char* stage, Stage& sc) {
     if ((int)rh::width_of_tier(t) == F)
-        table_wave<F, RANK, WATCH>(T, T.tier[t], wbase, wall_on, stage, sc);
+        table_wave<F, RANK, WATCH>(T, T.tier[t], tl, wall_on, stage, sc);
     else if constexpr (F + 2 <= FHI)
-        table_dispatch<F + 2, FHI, RANK, WATCH>(T, t, wbase, wall_on, stage, sc);
+        table_dispatch<F + 2, FHI, RANK, WATCH>(T, t, tl, wall_on, stage, sc);
 }
 
+#ifndef RH_TABLE_NOEVENTS                    // A/B (timing only, WRONG results): skip the event hand-off
+#define RH_TABLE_NOEVENTS 0
+#endif
+
+// One workgroup iteration (launch-local block index b of the class).  Without RH_TABLE_PERSIST a
+// workgroup runs exactly its own index; with it the grid is capped at a resident size (a multiple
+// of kHeads) and workgroups loop over b = blockIdx.x, blockIdx.x + gridDim.x, ... -- every
+// iteration keeps the head of its launch-global index (and, under round-robin placement, its XCD).
 template <bool WATCH, int FLO, int FHI>
-__device__ __forceinline__ void table_commit_block(const TierRange& tr, const TableEvents& ev) {
-    const TableDev& T = rh::kernarg_struct<TableDev>();  // block-uniform tier index: scalar loads
-    // COMMIT: [0, 32 KiB) advanced records, [32, 64 KiB) watch-ALL records; WATCH: level records
-    __shared__ __attribute__((aligned(16))) unsigned char stage[kTRows * sizeof(rh_watch_event)];
-    __shared__ Stage sc;
-    const uint32_t b = blockIdx.x;
+__device__ __forceinline__ void table_block_iter(const TableDev& T, const TierRange& tr, const TableEvents& ev,
+                                                 uint32_t b, unsigned char* stage, Stage& sc) {
+    const int wave = threadIdx.x >> 6;
+    const bool wall_on = !WATCH && ev.wall != nullptr;
     int i = 0;
 #pragma unroll
     for (int k = 1; k < rh::kTableTiers; ++k)
         if (k < tr.n_slots && b >= tr.block_begin[k]) i = k;
     const int t = tr.tier[i];
-    const int wave = threadIdx.x >> 6;
-    const uint64_t wbase = ((uint64_t)(b - tr.block_begin[i]) * kTWaves + wave) * 128;
-    const bool wall_on = !WATCH && ev.wall != nullptr;
+    const uint64_t tl = (uint64_t)(b - tr.block_begin[i]) * kTWaves + wave;   // tile of this wave
     if (threadIdx.x < 2 * kTWaves) (&sc.cnt[0][0])[threadIdx.x] = 0u;
-    if (blockIdx.x == 0 && threadIdx.x == 0 && ev.counts_next) *ev.counts_next = 0ull;  // the next evaluation's word
+    if (b == 0 && threadIdx.x < rh::kHeads && ev.heads_next)
+        ev.heads_next[threadIdx.x * rh::kHeadStride] = 0ull;  // the next evaluation's heads
+    __syncthreads();   // also: a previous iteration's copy-out is done with `stage`
+    if (tl * rh::kTileRows < T.tier[t].rows) table_dispatch<FLO, FHI, FLO <= 6, WATCH>(T, t, tl, wall_on, stage, sc);
     __syncthreads();
-    if (wbase < T.tier[t].rows) table_dispatch<FLO, FHI, FLO <= 6, WATCH>(T, t, wbase, wall_on, stage, sc);
-    __syncthreads();
+    if (RH_TABLE_NOEVENTS) return;
 
-    // ---- one range of the output lists per block (one device-scope atomic), then a contiguous copy
+    // ---- one range of the head's region per block (one device-scope atomic), then a contiguous copy
+    const uint32_t h = (ev.block_base + b) & (rh::kHeads - 1);
     if (threadIdx.x == 0) {
         uint32_t a0 = 0, a1 = 0;
         for (int k = 0; k < kTWaves; ++k) {
@@ -378,20 +421,20 @@ __device__ __forceinline__ void table_commit_block(const TierRange& tr, const Ta
         sc.pre[1][kTWaves] = a1;
         // low word: kind 0, high word: kind 1 (each < 2^28: no carry)
         const unsigned long long add = (unsigned long long)a0 | ((unsigned long long)a1 << 32);
-        sc.base = (a0 | a1) ? atomicAdd(ev.counts, add) : 0ull;
-        if (a0 | a1) ev.block_end[ev.block_base + blockIdx.x] = sc.base + add;  // host-mapped: list lengths
+        sc.base = (a0 | a1) ? atomicAdd(ev.heads + h * rh::kHeadStride, add) : 0ull;
     }
     __syncthreads();
     const uint32_t tot0 = sc.pre[0][kTWaves], tot1 = sc.pre[1][kTWaves];
     if (!(tot0 | tot1)) return;
+    const uint64_t R = ev.region;
     const uint64_t b0 = sc.base & 0xFFFFFFFFull, b1 = sc.base >> 32;
-    const uint64_t lim0 = b0 >= ev.cap ? 0 : (b0 + tot0 <= ev.cap ? tot0 : ev.cap - b0);
-    const uint64_t lim1 = b1 >= ev.cap ? 0 : (b1 + tot1 <= ev.cap ? tot1 : ev.cap - b1);
+    const uint64_t lim0 = b0 >= R ? 0 : (b0 + tot0 <= R ? tot0 : R - b0);
+    const uint64_t lim1 = b1 >= R ? 0 : (b1 + tot1 <= R ? tot1 : R - b1);
     // record e of the block lives in the region of wave k with pre[k] <= e < pre[k + 1]
     typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
     const v4u32* src = reinterpret_cast<const v4u32*>(stage);
     if (WATCH) {  // 32-byte records: two 16-byte words each
-        v4u32* dst = reinterpret_cast<v4u32*>(ev.watch + b0);
+        v4u32* dst = reinterpret_cast<v4u32*>(ev.watch + h * R + b0);
         for (uint32_t j = threadIdx.x; j < 2 * lim0; j += kTBlock) {
             const uint32_t e = j >> 1;
             uint32_t k = 0;
@@ -400,7 +443,7 @@ __device__ __forceinline__ void table_commit_block(const TierRange& tr, const Ta
             dst[j] = src[2 * (k * 128 + (e - sc.pre[0][k])) + (j & 1)];
         }
     } else {
-        v4u32* da = reinterpret_cast<v4u32*>(ev.adv + b0);
+        v4u32* da = reinterpret_cast<v4u32*>(ev.adv + h * R + b0);
         for (uint32_t e = threadIdx.x; e < lim0; e += kTBlock) {
             uint32_t k = 0;
 #pragma unroll
@@ -408,7 +451,7 @@ __device__ __forceinline__ void table_commit_block(const TierRange& tr, const Ta
             da[e] = src[k * 128 + (e - sc.pre[0][k])];
         }
         if (ev.wall) {
-            v4u32* dw = reinterpret_cast<v4u32*>(ev.wall + b1);
+            v4u32* dw = reinterpret_cast<v4u32*>(ev.wall + h * R + b1);
             for (uint32_t e = threadIdx.x; e < lim1; e += kTBlock) {
                 uint32_t k = 0;
 #pragma unroll
@@ -416,6 +459,20 @@ __device__ __forceinline__ void table_commit_block(const TierRange& tr, const Ta
                 dw[e] = src[kTRows + k * 128 + (e - sc.pre[1][k])];
             }
         }
+    }
+}
+
+template <bool WATCH, int FLO, int FHI>
+__device__ __forceinline__ void table_commit_block(const TierRange& tr, const TableEvents& ev) {
+    const TableDev& T = rh::kernarg_struct<TableDev>();  // block-uniform tier index: scalar loads
+    // COMMIT: [0, 24 KiB) advanced records, [24, 48 KiB) watch-ALL records; WATCH: level records
+    __shared__ __attribute__((aligned(16))) unsigned char stage[kTRows * sizeof(rh_watch_event)];
+    __shared__ Stage sc;
+    if (RH_TABLE_PERSIST > 0) {
+        const uint32_t nblocks = tr.block_begin[rh::kTableTiers];
+        for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x) table_block_iter<WATCH, FLO, FHI>(T, tr, ev, b, stage, sc);
+    } else {
+        table_block_iter<WATCH, FLO, FHI>(T, tr, ev, blockIdx.x, stage, sc);
     }
 }
 
@@ -436,19 +493,69 @@ __global__ __launch_bounds__(kTBlock) void table_commit_kernel_net(TableDev Targ
     table_commit_block<WATCH, 8, 14>(tr, ev);
 }
 
+// ---- packing the head regions into the contiguous result lists ------------------------------------
+// Grid-stride over the records; each thread moves 16-byte words.  The list lengths are the head
+// words' sums (the evaluation's atomics are complete at this kernel's start).
+template <bool WATCH>
+__global__ __launch_bounds__(256) void table_gather_kernel(TableEvents ev, rh_index_event* __restrict__ out_adv,
+                                                           rh_index_event* __restrict__ out_wall,
+                                                           rh_watch_event* __restrict__ out_watch, uint64_t cap,
+                                                           uint64_t* counts_out) {
+    typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+    const uint64_t R = ev.region;
+    uint64_t pre0[rh::kHeads + 1], pre1[rh::kHeads + 1];
+    pre0[0] = pre1[0] = 0;
+#pragma unroll
+    for (int h = 0; h < rh::kHeads; ++h) {
+        const unsigned long long x = ev.heads[h * rh::kHeadStride];
+        const uint64_t c0 = x & 0xFFFFFFFFull, c1 = x >> 32;
+        pre0[h + 1] = pre0[h] + (c0 < R ? c0 : R);
+        pre1[h + 1] = pre1[h] + (c1 < R ? c1 : R);
+    }
+    const uint64_t tot0 = pre0[rh::kHeads], tot1 = WATCH ? 0 : pre1[rh::kHeads];
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        counts_out[0] = tot0;
+        counts_out[1] = tot1;
+    }
+    const uint64_t n0 = tot0 < cap ? tot0 : cap;
+    const uint64_t n1 = (out_wall && !WATCH) ? (tot1 < cap ? tot1 : cap) : 0;
+    const uint64_t words0 = WATCH ? 2 * n0 : n0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < words0 + n1; j += stride) {
+        if (j < words0) {
+            const uint64_t e = WATCH ? j >> 1 : j;
+            int h = 0;
+#pragma unroll
+            for (int m = 1; m < rh::kHeads; ++m) h += e >= pre0[m] ? 1 : 0;
+            const uint64_t s = h * R + (e - pre0[h]);
+            if (WATCH)
+                reinterpret_cast<v4u32*>(out_watch)[j] = reinterpret_cast<const v4u32*>(ev.watch)[2 * s + (j & 1)];
+            else
+                reinterpret_cast<v4u32*>(out_adv)[e] = reinterpret_cast<const v4u32*>(ev.adv)[s];
+        } else {
+            const uint64_t e = j - words0;
+            int h = 0;
+#pragma unroll
+            for (int m = 1; m < rh::kHeads; ++m) h += e >= pre1[m] ? 1 : 0;
+            const uint64_t s = h * R + (e - pre1[h]);
+            reinterpret_cast<v4u32*>(out_wall)[e] = reinterpret_cast<const v4u32*>(ev.wall)[s];
+        }
+    }
+}
+
 // ---- hasLease over every started row -------------------------------------------------------------
 template <int F>
 __global__ __launch_bounds__(256) void table_lease_kernel(TableTier tt, int64_t now, int64_t timeout_ms,
                                                           uint64_t* __restrict__ slot_bits) {
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= tt.rows) return;
-    const uint32_t w = tt.conf[r];
+    const uint32_t w = *tt.u32(tile::kConf, r);
     if (!(w & RH_CONF_ACTIVE)) return;  // free row
     int64_t ts[F];
     uint32_t never = 0;
 #pragma unroll
     for (int k = 0; k < F; ++k) {
-        ts[k] = tt.fts[(uint64_t)k * tt.rows + r];
+        ts[k] = *tt.i64(tile::fts(F, k), r);
         never |= (ts[k] == rh::kNoTimestamp ? 1u : 0u) << k;
     }
     rh_lease_soa t{};
@@ -456,10 +563,11 @@ __global__ __launch_bounds__(256) void table_lease_kernel(TableTier tt, int64_t 
     t.timeout_ms = timeout_ms;
     int64_t lout;
     bool has, ext;
-    rh_lease::lease_one<F>(t, ts, w, tt.lease[r], tt.lon[r] != 0, true, lout, has, ext, never);
-    if (ext) tt.lease[r] = lout;
+    int64_t* lease = tt.i64(tile::lease(F), r);
+    rh_lease::lease_one<F>(t, ts, w, *lease, *tt.u8(tile::kLon, r) != 0, true, lout, has, ext, never);
+    if (ext) *lease = lout;
     if (has) {
-        const uint32_t slot = tt.row_slot[r];
+        const uint32_t slot = *tt.u32(tile::kSlot, r);
         atomicOr(reinterpret_cast<unsigned long long*>(slot_bits + (slot >> 6)), 1ull << (slot & 63));
     }
 }
@@ -470,24 +578,26 @@ void launch_lease_width(const TableTier& tt, int64_t now, int64_t timeout_ms, ui
 }
 
 // ---- read-back -------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void table_read_kernel(TableDev T, uint32_t first, uint32_t n, uint32_t column,
+__global__ __launch_bounds__(256) void table_read_kernel(TableDev Targ, uint32_t first, uint32_t n, uint32_t column,
                                                          int64_t* __restrict__ out) {
+    const TableDev& T = rh::kernarg_struct<TableDev>();
+    (void)Targ;
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const TableTier* tt;
     uint32_t row;
     int64_t v = INT64_MIN;
     if (locate(T, first + i, tt, row)) {
-        const uint64_t R = tt->rows;
-        if (column < 16) v = column < tt->width ? tt->match[column * R + row] : -1;
-        else if (column < 32) v = column - 16 < tt->width ? tt->fcommit[(column - 16) * R + row] : -1;
-        else if (column == RH_COL_FLUSH) v = tt->flush[row];
-        else if (column == RH_COL_COMMITTED) v = tt->commit[row];
-        else if (column == RH_COL_CONF) v = (int64_t)tt->conf[row];
-        else if (column == RH_COL_TERM_START) v = tt->tstart[row];
-        else if (column == RH_COL_LEASE) v = tt->lease[row];
-        else if (column == RH_COL_LEASE_ON) v = (int64_t)tt->lon[row];
-        else if (column >= 48 && column < 64) v = column - 48 < tt->width ? tt->fts[(column - 48) * R + row] : rh::kNoTimestamp;
+        const uint32_t F = tt->width;
+        if (column < 16) v = column < F ? *tt->i64(tile::match(column), row) : -1;
+        else if (column < 32) v = column - 16 < F ? *tt->i64(tile::fcommit(F, column - 16), row) : -1;
+        else if (column == RH_COL_FLUSH) v = *tt->i64(tile::flush(F), row);
+        else if (column == RH_COL_COMMITTED) v = *tt->i64(tile::commit(F), row);
+        else if (column == RH_COL_CONF) v = (int64_t)*tt->u32(tile::kConf, row);
+        else if (column == RH_COL_TERM_START) v = *tt->i64(tile::tstart(F), row);
+        else if (column == RH_COL_LEASE) v = *tt->i64(tile::lease(F), row);
+        else if (column == RH_COL_LEASE_ON) v = (int64_t)*tt->u8(tile::kLon, row);
+        else if (column >= 48 && column < 64) v = column - 48 < F ? *tt->i64(tile::fts(F, column - 48), row) : rh::kNoTimestamp;
     }
     out[i] = v;
 }
@@ -517,6 +627,7 @@ static uint32_t class_blocks(const rh::TableDev& t, int cls) {
 }
 
 uint32_t rh::table_commit_blocks(const rh::TableDev& t) { return class_blocks(t, 0) + class_blocks(t, 1); }
+uint32_t rh::table_block_rows() { return kTRows; }
 
 int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev_in, hipStream_t stream) {
     // one launch per width class over every non-empty tier of the class, widest tier first (a
@@ -535,7 +646,9 @@ int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev_i
         }
         for (int s = tr.n_slots; s <= rh::kTableTiers; ++s) tr.block_begin[s] = blocks;
         if (blocks == 0) continue;
-        const dim3 g(blocks), b(kTBlock);
+        // RH_TABLE_PERSIST > 0 caps the grid (a multiple of kHeads): resident workgroups loop
+        const uint32_t grid = (RH_TABLE_PERSIST > 0 && blocks > (uint32_t)RH_TABLE_PERSIST) ? (uint32_t)RH_TABLE_PERSIST : blocks;
+        const dim3 g(grid), b(kTBlock);
         if (mode == RH_MODE_WATCH) {
             if (cls == 0) hipLaunchKernelGGL(table_commit_kernel_rank<true>, g, b, 0, stream, t, tr, ev);
             else hipLaunchKernelGGL(table_commit_kernel_net<true>, g, b, 0, stream, t, tr, ev);
@@ -546,6 +659,24 @@ int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev_i
         RH_HIP(hipGetLastError());
         ev.block_base += blocks;
     }
+    return RH_OK;
+}
+
+int rh_table_gather(int mode, const rh::TableEvents& ev, rh_index_event* out_adv, rh_index_event* out_wall,
+                    rh_watch_event* out_watch, uint64_t cap, uint64_t* counts_out, hipStream_t stream) {
+    const dim3 g(256), b(256);
+    if (mode == RH_MODE_WATCH)
+        hipLaunchKernelGGL(table_gather_kernel<true>, g, b, 0, stream, ev, out_adv, out_wall, out_watch, cap, counts_out);
+    else
+        hipLaunchKernelGGL(table_gather_kernel<false>, g, b, 0, stream, ev, out_adv, out_wall, out_watch, cap, counts_out);
+    RH_HIP(hipGetLastError());
+    return RH_OK;
+}
+
+int rh_table_init_tiles(const rh::TableTier& t, uint32_t first_tile, uint32_t n_tiles, hipStream_t stream) {
+    if (n_tiles == 0) return RH_OK;
+    hipLaunchKernelGGL(table_init_tiles_kernel, dim3(n_tiles), dim3(rh::kTileRows), 0, stream, t, first_tile);
+    RH_HIP(hipGetLastError());
     return RH_OK;
 }
 

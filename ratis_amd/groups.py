@@ -244,6 +244,28 @@ class RaftGroupTable:
         ev = _view(ptr.value or 0, n.value, WATCH_EVENT_DTYPE).copy()
         return ev[np.argsort(ev["slot"], kind="stable")]
 
+    def set_timing(self, enable: bool = True) -> None:
+        """``rh_groups_timing``: HIP events around every evaluation kernel and its gather."""
+        check(self._lib.rh_groups_timing(self.handle, 1 if enable else 0))
+
+    def last_timing(self) -> Tuple[float, float]:
+        """(evaluation ms, gather ms) of the last timed evaluation (``rh_groups_last_timing``)."""
+        a, b = ctypes.c_float(), ctypes.c_float()
+        check(self._lib.rh_groups_last_timing(self.handle, ctypes.byref(a), ctypes.byref(b)))
+        return float(a.value), float(b.value)
+
+    def watch_async(self) -> None:
+        """``rh_watch_levels_async``: commitIndexChanged() of the dirty slots, in flight."""
+        check(self._lib.rh_watch_levels_async(self.handle))
+
+    def watch_wait(self) -> np.ndarray:
+        """``rh_watch_levels_wait``: the outstanding evaluation's changed levels, sorted by slot."""
+        ptr = ctypes.c_void_p()
+        n = ctypes.c_uint64()
+        check(self._lib.rh_watch_levels_wait(self.handle, ctypes.byref(ptr), ctypes.byref(n)))
+        ev = _view(ptr.value or 0, n.value, WATCH_EVENT_DTYPE).copy()
+        return ev[np.argsort(ev["slot"], kind="stable")]
+
     # -- leader lease (LeaderStateImpl.hasLease, LeaderLease) ---------------------------------
     def lease_start(self, slot: int, now_nanos: int, enabled: bool = True) -> None:
         """A new LeaderLease for ``slot`` (lease = now, enabled) with every follower stamped now."""
@@ -265,6 +287,18 @@ class RaftGroupTable:
         words = ctypes.c_uint64()
         check(self._lib.rh_lease_batch(self.handle, int(now_nanos), int(timeout_ms), ctypes.byref(ptr),
                                        ctypes.byref(words)))
+        w = _view(ptr.value, words.value, np.dtype(np.uint64)).copy()
+        return np.unpackbits(w.view(np.uint8), bitorder="little")[: self.capacity].astype(bool)
+
+    def lease_async(self, now_nanos: int, timeout_ms: int) -> None:
+        """``rh_lease_batch_async``: the hasLease pass in flight."""
+        check(self._lib.rh_lease_batch_async(self.handle, int(now_nanos), int(timeout_ms)))
+
+    def lease_wait(self) -> np.ndarray:
+        """``rh_lease_batch_wait``: the outstanding pass's bitmap, bool [capacity]."""
+        ptr = ctypes.c_void_p()
+        words = ctypes.c_uint64()
+        check(self._lib.rh_lease_batch_wait(self.handle, ctypes.byref(ptr), ctypes.byref(words)))
         w = _view(ptr.value, words.value, np.dtype(np.uint64)).copy()
         return np.unpackbits(w.view(np.uint8), bitorder="little")[: self.capacity].astype(bool)
 
@@ -343,6 +377,14 @@ class RaftNode:
         w = wall[: min(nw.value, cap)]
         return a[np.argsort(a["slot"], kind="stable")], w[np.argsort(w["slot"], kind="stable")]
 
+    def watch_levels(self, cap: int) -> np.ndarray:
+        """All shards' commitIndexChanged() level changes (node slots), sorted by slot."""
+        out = np.zeros(max(cap, 1), dtype=WATCH_EVENT_DTYPE)
+        n = ctypes.c_uint64()
+        check(self._lib.rh_node_watch_levels(self._h, _p(out), cap, ctypes.byref(n)))
+        ev = out[: min(n.value, cap)]
+        return ev[np.argsort(ev["slot"], kind="stable")]
+
     def lease_start(self, node_slot: int, now_nanos: int, enabled: bool = True) -> None:
         check(self._lib.rh_node_group_lease_start(self._h, node_slot, int(now_nanos), 1 if enabled else 0))
 
@@ -356,16 +398,19 @@ class RaftNode:
 
 class LeaderPump:
     """Python twin of the Java module's pump (java/ratis-hip/.../HipLeaderBookkeeper.tick): one
-    tick = push the buffered deltas, start every shard's updateCommit (all shards in flight), per
-    shard hand the advanced commits and watch-ALL levels to the divisions, per shard
-    commitIndexChanged()'s levels (LeaderStateImpl.java:606-622).  ``callbacks[node_slot]`` gets
+    tick = push the buffered deltas; put every shard's updateCommit, commitIndexChanged() and (with
+    a lease timeout) hasLease pass in flight -- all shards before any wait; then per shard hand the
+    advanced commits and watch-ALL levels to the divisions, then commitIndexChanged()'s levels
+    (LeaderStateImpl.java:606-622), then the lease bitmap.  ``callbacks[node_slot]`` gets
     ``on_commit(value)``, ``on_watch_all(min)`` and ``on_watch_levels(min, majority, max)`` (the
     last only for a present getMajorityMin, as commitIndexChanged's ifPresent)."""
 
-    def __init__(self, node: RaftNode):
+    def __init__(self, node: RaftNode, lease_timeout_ms: int = -1):
         self.node = node
         self.callbacks = {}
         self._pending = []
+        self.lease_timeout_ms = lease_timeout_ms
+        self.lease_bits = None
 
     def register(self, node_slot: int, callback) -> None:
         self.callbacks[int(node_slot)] = callback
@@ -373,13 +418,20 @@ class LeaderPump:
     def emit(self, deltas: np.ndarray) -> None:
         self._pending.append(np.ascontiguousarray(deltas, dtype=DELTA_DTYPE))
 
-    def tick(self) -> dict:
+    def tick(self, now_nanos: int = 0) -> dict:
         if self._pending:
             self.node.push(np.concatenate(self._pending))
             self._pending = []
         cap = self.node.capacity_per_shard
-        tickets = [t.commit_async(watch_all=True) for t in self.node.tables]
+        lease = self.lease_timeout_ms >= 0
+        tickets = []
+        for t in self.node.tables:   # every shard's passes in flight before any wait (stream order:
+            tickets.append(t.commit_async(watch_all=True))   # commit, then its commitIndexChanged)
+            t.watch_async()
+            if lease:
+                t.lease_async(now_nanos, self.lease_timeout_ms)
         n = {"commit": 0, "watch_all": 0, "watch_levels": 0}
+        bits = []
         for s, (t, tk) in enumerate(zip(self.node.tables, tickets)):
             r = t.commit_wait(tk)
             for slot, v in zip(r.advanced_slots, r.advanced_commit):
@@ -392,13 +444,14 @@ class LeaderPump:
                 if cb is not None:
                     cb.on_watch_all(int(v))
                     n["watch_all"] += 1
-        for s, t in enumerate(self.node.tables):
-            ev = t.commit_index_changed()
-            for e in ev:
+            for e in t.watch_wait():
                 if not e["valid"]:
                     continue
                 cb = self.callbacks.get(s * cap + int(e["slot"]))
                 if cb is not None:
                     cb.on_watch_levels(int(e["min"]), int(e["majority"]), int(e["max"]))
                     n["watch_levels"] += 1
+            if lease:
+                bits.append(t.lease_wait())
+        self.lease_bits = np.concatenate(bits) if lease else None
         return n

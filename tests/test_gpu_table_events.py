@@ -1,0 +1,202 @@
+"""GPU parity of the resident table's event path (round 4): the evaluation kernel stages its records
+per XCD head in HBM and a gather kernel packs them into the contiguous result lists
+(ratis_amd/csrc/rh_internal.h, TableEvents).  Checked against tests/table_model.py (the reference's
+FollowerInfo / LeaderStateImpl semantics over the oracle's commit arithmetic):
+
+  * both sinks (HOST_MAPPED: gather into pinned memory; DEVICE: gather into HBM + D2H in _wait),
+    for updateCommit (advanced + watch-ALL) and commitIndexChanged, on a table large enough that
+    every head region is used (>= 8 workgroups per evaluation kind);
+  * sparse dirty sets, where most 128-row tiles are clean and skipped by their summary byte;
+  * evaluations whose ticket is superseded without a wait, and an evaluation after them;
+  * the async forms of commitIndexChanged and hasLease (rh_watch_levels_async / _wait,
+    rh_lease_batch_async / _wait), their misuse, and the node forms over 4 shards on one GPU."""
+import numpy as np
+import pytest
+
+from tests.table_model import TableModel
+from tests.test_gpu_table import compare, conf_word, random_deltas
+
+pytestmark = pytest.mark.gpu
+
+
+def _loaded(ctx, model, n, seed):
+    from ratis_amd import groups, workload
+    tiers = workload.commit_snapshot(n, joint_frac=0.1, peers=5, seed=seed)
+    tab = groups.RaftGroupTable(ctx, capacity=sum(t.n for t in tiers))
+    first = 0
+    for h in tiers:
+        tab.load(first, h.conf, h.flush, h.commit, h.term_start, match=h.follower)
+        if model is not None:
+            model.load(first, h.conf, h.flush, h.commit, h.term_start, match=h.follower)
+        first += h.n
+    return tab, first
+
+
+@pytest.mark.parametrize("sink", ["host_mapped", "device"])
+def test_event_sinks_match_model_over_every_head(ctx, orc, sink):
+    from ratis_amd import _lib
+    rng = np.random.default_rng(404)
+    n = 60_000   # 40+ workgroups of 1,536 rows: every one of the 8 head regions holds records
+    model = TableModel(n)
+    tab, n = _loaded(ctx, model, n, seed=41)
+    try:
+        tab.set_event_sink(_lib.RH_EVENTS_DEVICE if sink == "device" else _lib.RH_EVENTS_HOST_MAPPED)
+        compare(tab, model, orc, columns=False)
+        live = np.arange(n)
+        for step, k in enumerate([n // 2, 3 * n, n // 100, 7, 0]):
+            d = random_deltas(rng, model, live, k) if k else np.zeros(0, dtype=_lib_delta_dtype())
+            tab.push(d)
+            model.apply(d)
+            got = compare(tab, model, orc, columns=step == 1)
+            if k == 0:
+                assert got.advanced_slots.size == 0 and got.watch_all_slots.size == 0
+    finally:
+        tab.close()
+
+
+def _lib_delta_dtype():
+    from ratis_amd.groups import DELTA_DTYPE
+    return DELTA_DTYPE
+
+
+def test_sparse_dirty_tiles_are_skipped_exactly(ctx, orc):
+    """A few dirty rows in a large table: the clean tiles' waves return on their summary byte; the
+    dirty rows (first / last row of a tile, both rows of one lane, the table's last tile) report."""
+    from ratis_amd import groups
+    rng = np.random.default_rng(9)
+    n = 40_000
+    model = TableModel(n)
+    tab, n = _loaded(ctx, model, n, seed=3)
+    try:
+        compare(tab, model, orc, columns=False)
+        for rows in ([0], [127, 128], [254, 255], [n - 1], list(rng.choice(n, 50, replace=False))):
+            s = np.array(rows, dtype=np.int64)
+            d = groups.make_deltas(s, np.zeros(s.size, np.int64), model.flush[s] + 1000)   # follower 0 jumps ahead
+            d2 = groups.make_deltas(s, np.ones(s.size, np.int64), model.flush[s] + 1000)
+            d = np.concatenate([d, d2])
+            tab.push(d)
+            model.apply(d)
+            got = compare(tab, model, orc, columns=False)
+            assert set(got.advanced_slots.tolist()) <= set(rows)
+            r = tab.update_commit()                       # nothing dirty any more: no events
+            assert r.advanced_slots.size == 0 and r.watch_all_slots.size == 0
+            model.commit_batch(orc)
+    finally:
+        tab.close()
+
+
+def test_superseded_tickets_do_not_leak_into_later_results(ctx, orc):
+    """kEvSets + 1 evaluations in flight with only the last waited (the others superseded), then
+    evaluations that are waited: every waited list equals the model's for its step."""
+    from ratis_amd import _lib
+    rng = np.random.default_rng(77)
+    model = TableModel(30_000)
+    tab, n = _loaded(ctx, model, 30_000, seed=5)
+    try:
+        compare(tab, model, orc, columns=False)
+        live = np.arange(n)
+        expect = None
+        tickets = []
+        for step in range(4):
+            d = random_deltas(rng, model, live, 20_000, fcommit=False)
+            tab.push(d)
+            model.apply(d)
+            tickets.append(tab.commit_async(watch_all=True))
+            expect = model.commit_batch(orc)
+        for tk in tickets[:-3]:
+            with pytest.raises(_lib.RatisHipError):
+                tab.commit_wait(tk)                       # its result set was reused
+        got = tab.commit_wait(tickets[-1])
+        assert np.array_equal(got.advanced_slots, expect[0]) and np.array_equal(got.advanced_commit, expect[1])
+        assert np.array_equal(got.watch_all_slots, expect[2]) and np.array_equal(got.watch_all_min, expect[3])
+        for step in range(3):
+            d = random_deltas(rng, model, live, 5_000, fcommit=False)
+            tab.push(d)
+            model.apply(d)
+            compare(tab, model, orc, watch=False, columns=False)
+    finally:
+        tab.close()
+
+
+def test_async_watch_and_lease_forms(ctx, orc):
+    from ratis_amd import _lib, groups
+    rng = np.random.default_rng(12)
+    model = TableModel(20_000)
+    tab, n = _loaded(ctx, model, 20_000, seed=8)
+    twin, _ = _loaded(ctx, None, 20_000, seed=8)
+    try:
+        with pytest.raises(_lib.RatisHipError):
+            tab.watch_wait()                              # nothing in flight
+        with pytest.raises(_lib.RatisHipError):
+            tab.lease_wait()
+        compare(tab, model, orc, watch=False, columns=False)
+        twin.update_commit()
+        live = np.arange(n)
+        for step in range(3):
+            d = random_deltas(rng, model, live, 8_000)
+            tab.push(d)
+            twin.push(d)
+            model.apply(d)
+            compare(tab, model, orc, watch=False, columns=False)
+            twin.update_commit()
+            tab.watch_async()
+            ev = tab.watch_wait()
+            m_s, m_lev, m_valid = model.watch(orc)
+            assert np.array_equal(ev["slot"].astype(np.int64), m_s)
+            assert np.array_equal(ev["min"], m_lev[0]) and np.array_equal(ev["max"], m_lev[2])
+            assert np.array_equal(ev["majority"], m_lev[1]) and np.array_equal(ev["valid"].astype(bool), m_valid)
+            assert np.array_equal(twin.commit_index_changed()["slot"], ev["slot"])
+        # lease: async / wait against the blocking form on the twin fed the same stamps
+        now = 1 << 50
+        for s in range(0, n, 3):
+            tab.lease_start(s, now, True)
+            twin.lease_start(s, now, True)
+        for k in range(3):   # 3 of 4 followers of every even slot reply late: a majority at 150 ms
+            sl = np.arange(0, n, 2)
+            st = now + 140_000_000 - rng.integers(0, 30_000_000, sl.size)
+            tab.update_last_responded(sl, k, st)
+            twin.update_last_responded(sl, k, st)
+        for dt in (50_000_000, 150_000_000):
+            tab.lease_async(now + dt, 100)
+            a = tab.lease_wait()
+            b = twin.lease_batch(now + dt, 100)
+            assert np.array_equal(a, b) and a.any()
+        tab.lease_async(now, 100)
+        tab.lease_async(now + 1, 100)                     # a second batch replaces the first
+        assert tab.lease_wait().shape == (tab.capacity,)
+    finally:
+        tab.close()
+        twin.close()
+
+
+def test_node_watch_levels_and_lease_over_four_shards(ctx, orc):
+    from ratis_amd import groups
+    rng = np.random.default_rng(21)
+    cap = 3000
+    with groups.RaftNode(0, cap, devices=[0, 0, 0, 0]) as node:
+        models = [TableModel(cap) for _ in range(4)]
+        for sh in range(4):
+            for s in range(0, cap, 2):
+                w = conf_word(int(rng.integers(1, 1 << 6)))
+                node.start(sh * cap + s, w, 5000, 100, 50)
+                models[sh].start(s, w, 5000, 100, 50)
+        deltas = []
+        for sh in range(4):
+            d = random_deltas(rng, models[sh], np.arange(0, cap, 2), 4000)
+            models[sh].apply(d)
+            d = d.copy()
+            d["slot"] += sh * cap
+            deltas.append(d)
+        node.push(np.concatenate(deltas))
+        node.update_commit(4 * cap)
+        for m in models:
+            m.commit_batch(orc)
+        ev = node.watch_levels(4 * cap)
+        want = []
+        for sh, m in enumerate(models):
+            s, lev, valid = m.watch(orc)
+            want.append(s + sh * cap)
+        assert np.array_equal(ev["slot"].astype(np.int64), np.concatenate(want))
+        assert node.watch_levels(4 * cap).size == 0       # nothing changed since
+        bits = node.lease_batch(1 << 40, 100)             # no lease started: no division has one
+        assert bits.shape == (4 * cap,) and not bits.any()

@@ -107,22 +107,28 @@ def _method_body(src: str, signature: str) -> str:
 
 def test_pump_runs_watch_levels_and_watch_all_without_allocating():
     """commitIndexChanged (LeaderStateImpl.java:606-622) and updateCommit's watch ALL (:1025) in HIP
-    mode: every tick evaluates with RH_COMMIT_WATCH_ALL and runs watchLevels on every shard, and
-    allocates nothing (result arrays sized once per shard capacity)."""
+    mode: every tick evaluates with RH_COMMIT_WATCH_ALL, puts every shard's commit, watch and lease
+    passes in flight before any wait (rh_*_async), waits them per shard, and allocates nothing
+    (result arrays sized once per shard capacity)."""
     book = open(BOOKKEEPER_JAVA).read()
     tick = _method_body(book, "void tick()")
     assert "hip.commitAsync(s, RatisHip.COMMIT_WATCH_ALL)" in tick
-    assert "hip.commitWait(" in tick and "hip.watchLevels(" in tick
+    assert "hip.commitWait(" in tick and "hip.watchWait(" in tick and "hip.leaseWait(" in tick
     assert "onWatchLevels(" in tick and "onWatchAll(" in tick and "onCommit(" in tick
     assert not re.search(r"\bnew\b", tick), "tick() allocates"
     assert "capacity * hip.getShards()" not in book and "capacity * shards" not in book
+    # every shard's three passes are issued in the first loop, before the first wait
+    first_wait = tick.index("hip.commitWait(")
+    for call in ("hip.commitAsync(", "hip.watchAsync(", "hip.leaseAsync("):
+        assert tick.index(call) < first_wait, call
+    assert "hip.watchLevels(" not in tick and "hip.leaseBatch(" not in tick
 
 
 def test_seams_implement_every_callback_and_the_checksum_backend():
     book = open(BOOKKEEPER_JAVA).read()
     iface = _method_body(book, "public interface Callback")
     callbacks = set(re.findall(r"void (\w+)\(", iface))
-    assert callbacks == {"onCommit", "onWatchAll", "onWatchLevels"}
+    assert callbacks == {"onCommit", "onWatchAll", "onWatchLevels", "onFallback"}
     patch = open(PATCH).read()
     added = "\n".join(l[1:] for l in patch.splitlines() if l.startswith("+") and not l.startswith("+++"))
     cb = _method_body(added, "private final class HipCallback implements HipLeaderBookkeeper.Callback")
@@ -149,3 +155,113 @@ def test_log_reader_native_matches_the_abi():
         assert f"res[s].{f}" in body, f
     hdr = open(os.path.join(ROOT, "include", "ratis_hip.h")).read()
     assert "int rh_segments_read_host(" in hdr
+
+
+def _patched_java(path_suffix: str) -> str:
+    """The reference file as the seams patch leaves it (requires /root/reference)."""
+    import tempfile
+    files = re.findall(r"^diff --git a/(\S+) b/", open(PATCH).read(), re.M)
+    f = next(x for x in files if x.endswith(path_suffix))
+    with tempfile.TemporaryDirectory() as d:
+        dst = os.path.join(d, f)
+        os.makedirs(os.path.dirname(dst), exist_ok=True)
+        shutil.copyfile(os.path.join(REFERENCE, f), dst)
+        r = subprocess.run(["git", "apply", "--include", f, PATCH], cwd=d, capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr
+        return open(dst).read()
+
+
+def _added_lines() -> str:
+    patch = open(PATCH).read()
+    return "\n".join(l[1:] for l in patch.splitlines() if l.startswith("+") and not l.startswith("+++"))
+
+
+def test_fallback_replaces_every_membership_failure():
+    """HIP mode never fails a leader for what the GPU table cannot hold (fall back to
+    the CPU path and count it): no seam throws for membership size, the bookkeeper counts fallbacks
+    by reason, a 15th follower / full shard / rejected or failed control call / dead pump each put
+    the division in fallback, and the division then answers through the reference's path."""
+    book = open(BOOKKEEPER_JAVA).read()
+    added = _added_lines()
+    # no seam turns a library rejection into an exception any more
+    assert "ratis-hip start failed" not in added and "ratis-hip reconf failed" not in added
+    assert "more than \" + RatisHip.MAX_FOLLOWERS" not in book
+    assert not re.search(r"throw new IllegalStateException\(\"ratis-hip: (shard|more than)", book)
+    # the stat and its reasons
+    assert "public long getFallbackCount()" in book and "public long getFallbackCount(FallbackReason reason)" in book
+    reasons = set(re.findall(r"FallbackReason\.(\w+)", book))
+    assert reasons >= {"SHARD_FULL", "FOLLOWER_SLOTS", "REJECTED", "DEVICE_ERROR", "PUMP_FAILED"}, reasons
+    add = _method_body(book, "public synchronized int addFollower(")
+    assert "fallBack(FallbackReason.FOLLOWER_SLOTS)" in add and "return -1;" in add
+    reg = _method_body(book, "public synchronized Division register(")
+    assert "FallbackReason.SHARD_FULL" in reg and "throw" not in reg
+    for m in ("public void start(", "public void reconf(", "public void leaseStart("):
+        body = _method_body(book, m)
+        assert "FallbackReason.REJECTED" in body and "FallbackReason.DEVICE_ERROR" in body, m
+        assert "catch (IllegalArgumentException" in body, m
+    pump = _method_body(book, "private void pumpLoop()")
+    assert "d.fallBack(FallbackReason.PUMP_FAILED)" in pump
+    fb = _method_body(book, "void fallBack(FallbackReason reason)")
+    assert "callback.onFallback()" in fb and "hip.stop(nodeSlot)" in fb and "release(this)" in fb
+    # producers ignore a follower without a slot
+    for m in ("public void matchIndex(", "public void snapshotIndex(", "public void followerCommitIndex(",
+              "public void lastResponded("):
+        assert "followerSlot >= 0" in _method_body(book, m), m
+    assert "fallback" in _method_body(book, "public boolean hasLease()")
+    # the seams: every HIP branch of LeaderStateImpl is taken only while the division is active
+    assert "private boolean hipActive()" in added
+    assert "return hip != null && !hip.isFallback();" in added
+    branches = re.findall(r"if \((hip != null|hipActive\(\))[^)]*\)", added)
+    null_only = [b for b in re.findall(r"if \(hip != null\)", added)]
+    # `hip != null` remains only where fallback does not matter: start (a fallen-back division
+    # ignores it), stop / removeFollower (harmless), and the UPDATE_COMMIT handler (applies GPU decisions)
+    assert len(null_only) <= 4, null_only
+    assert sum(1 for b in branches if b == "hipActive()") >= 10
+    cb = _method_body(added, "public void onFallback()")
+    assert "eventQueue.submit(updateCommitEvent)" in cb and "commitIndexChanged()" in cb
+
+
+def test_hip_mode_does_not_rerun_the_java_arithmetic():
+    """In HIP mode LeaderStateImpl no longer evaluates getMajorityMin in Java: updateCommit's
+    follow-up runs notifySenders() instead of commitIndexChanged() (LeaderStateImpl.java:1009), and
+    checkStaging marks the division for the GPU instead of executing updateCommit (:866); the
+    UPDATE_COMMIT event runs the Java updateCommit() only in JAVA mode or after a fallback."""
+    if not os.path.isdir(REFERENCE):
+        pytest.skip("reference tree not present")
+    src = _patched_java("server/impl/LeaderStateImpl.java")
+    assert "new StateUpdateEvent(StateUpdateEvent.Type.UPDATE_COMMIT, this::onUpdateCommitEvent)" in src
+    assert "hipUpdateEvent" not in src
+    handler = _method_body(src, "private void onUpdateCommitEvent()")
+    assert "updateFromHip();" in handler and "if (!hipActive())" in handler and "updateCommit();" in handler
+    follow = _method_body(src, "private void updateCommit(LogEntryHeader[] entriesToCommit)")
+    i = follow.index("if (hipActive())")
+    assert follow.index("notifySenders();", i) < follow.index("commitIndexChanged();", i)
+    staging = _method_body(src, "private void checkStaging()")
+    i = staging.index("if (hipActive())")
+    assert staging.index("submitUpdateCommitEvent();", i) < staging.index("updateCommitEvent.execute();", i)
+    # the only Java getMajorityMin callers left run in JAVA mode / fallback
+    assert _method_body(src, "private void onUpdateCommitEvent()").count("updateCommit()") == 1
+
+
+def test_bulk_load_streams_batches_with_two_images():
+    """SegmentedRaftLog.loadLogSegments no longer materialises every batch before loading: it takes
+    segments one by one from a HipLogReader.Pipeline (batch k + 1 read and verified while batch k
+    loads), which holds exactly two image buffers and hands a batch's back after its last segment;
+    batches are planned under HIP_BATCH_BYTES and MAX_FRAMES_PER_BATCH frame slots (no silent
+    clamp of the frame table)."""
+    added = _added_lines()
+    assert "List<HipLogReader.Segment>" not in added
+    assert "try (HipLogReader.Pipeline verified =" in added and "verified.next()" in added
+    plan = _method_body(added, "private HipLogReader.Pipeline hipVerify(")
+    assert "HipLogReader.MAX_FRAMES_PER_BATCH" in plan and "new HipLogReader.Plan(" in plan
+    assert "reader.pipeline(plans, maxOp)" in plan
+    reader = open(os.path.join(JAVA, "java", "org", "apache", "ratis", "hip", "HipLogReader.java")).read()
+    pipe = _method_body(reader, "Pipeline(List<Plan> plans, int maxOpSize)")
+    assert pipe.count("free.add(ByteBuffer.allocateDirect(bytes))") == 2
+    assert "free.take()" in pipe and "ready.put(readInto(buf," in pipe
+    nxt = _method_body(reader, "public Segment next()")
+    assert "free.offer(current.image)" in nxt
+    assert "Integer.MAX_VALUE - 8" not in reader          # the old silent clamp (ADVICE r03)
+    assert "MAX_FRAMES_PER_BATCH" in _method_body(reader, "public Plan(List<File> files, int framesPerFile)")
+    # one context per GPU of the mask, batches spread round robin
+    assert "RatisHip.ctxCreate0(d)" in reader and "Math.floorMod(ctxIndex, ctx.length)" in reader
