@@ -279,6 +279,80 @@ def delta_streaming(ctx, host, steps: int = 12, fill_threads: int = 16, reps: in
                     "device slots) overlap the apply and evaluation of step s"}
 
 
+def _placeholder_frames(rng, nbytes: int, lo: int = 64, hi: int = 2048):
+    """A flush batch as SegmentedRaftLogOutputStream.write lays it out (varint32(n) || n entry bytes
+    || 4-byte trailer), trailers zero, ~nbytes long: (image uint8, frame offsets, frame lengths)."""
+    sizes, total = [], 0
+    while total < nbytes:
+        n = int(rng.integers(lo, hi + 1))
+        v = 1 if n < 128 else 2
+        sizes.append((n, v))
+        total += v + n + 4
+    img = rng.integers(0, 256, total, dtype=np.uint8)
+    off = np.empty(len(sizes), dtype=np.uint64)
+    ln = np.empty(len(sizes), dtype=np.uint32)
+    pos = 0
+    for i, (n, v) in enumerate(sizes):
+        off[i], ln[i] = pos, v + n + 4
+        if v == 1:
+            img[pos] = n
+        else:
+            img[pos], img[pos + 1] = (n & 0x7F) | 0x80, n >> 7
+        img[pos + v + n: pos + v + n + 4] = 0
+        pos += v + n + 4
+    return img, off, ln
+
+
+def write_stamp_leg(ctx, reps: int = 25) -> dict:
+    """The write side's decision input: the trailers of one flush batch stamped
+    on the GPU from a registered host buffer (rh_crc32c_stamp_host: H2D of the batch + the CRC kernel
+    + D2H of 4 B per frame + the host writing the trailers; host wall clock per call) against the
+    oracle's PureJavaCrc32C restatement (slicing-by-8 C, one core) over the same frames -- at flush
+    sizes up to raft.server.log.write.buffer.size's default 8 MiB.  The crossover is the smallest
+    measured flush from which the GPU call is faster; the Java module stamps on the GPU from there
+    (the writer seam).  Entries of 64-2048 B."""
+    import time
+
+    from oracle import oracle as orc
+    from ratis_amd import engine
+    rng = np.random.default_rng(17)
+    out = {"sizes": [], "frames": [], "gpu_us": [], "gpu_GBps": [], "cpu_1core_us": [], "cpu_1core_GBps": []}
+    parity = True
+    for nbytes in (16 << 10, 32 << 10, 64 << 10, 128 << 10, 256 << 10, 1 << 20, 8 << 20):
+        img, off, ln = _placeholder_frames(rng, nbytes)
+        buf = img.copy()
+        with engine.HostRegistration(ctx, buf):
+            engine.stamp_host(ctx, buf, off, ln)   # warm-up (scratch pool, code objects)
+            g = []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                engine.stamp_host(ctx, buf, off, ln)
+                g.append(time.perf_counter() - t0)
+        c = []
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            crc, _ = orc.crc32c_frames(img, off, ln)
+            c.append(time.perf_counter() - t0)
+        end = (off + ln.astype(np.uint64)).astype(np.int64)
+        stored = ((buf[end - 4].astype(np.uint32) << 24) | (buf[end - 3].astype(np.uint32) << 16)
+                  | (buf[end - 2].astype(np.uint32) << 8) | buf[end - 1].astype(np.uint32))
+        parity &= bool(np.array_equal(stored, crc))
+        gs, cs = float(np.median(g)), float(np.median(c))
+        out["sizes"].append(int(img.size))
+        out["frames"].append(int(off.size))
+        out["gpu_us"].append(round(gs * 1e6, 1))
+        out["gpu_GBps"].append(round(img.size / gs / 1e9, 2))
+        out["cpu_1core_us"].append(round(cs * 1e6, 1))
+        out["cpu_1core_GBps"].append(round(img.size / cs / 1e9, 2))
+    faster = [s for s, a, b in zip(out["sizes"], out["gpu_us"], out["cpu_1core_us"]) if a < b]
+    out["crossover_bytes"] = min(faster) if faster else None
+    out["parity_ok"] = parity
+    out["note"] = ("GPU: rh_crc32c_stamp_host from a registered (page-locked) buffer, PCIe both ways included; "
+                   "CPU: the oracle's C slicing-by-8 restatement of PureJavaCrc32C on one core (no JVM on the "
+                   "box: the Java PureJavaCrc32C is not faster than this); median of %d calls" % reps)
+    return out
+
+
 def queue_gate(stream, cycles: int = 400_000) -> None:
     """Occupies `stream` for ~0.2 ms with a spin kernel (torch.cuda._sleep) so that the launches the
     host enqueues next are all queued before the GPU reaches the timed region's start event: the
@@ -379,7 +453,7 @@ def table_commit_leg(ctx, host, reps: int = 8, fracs=(1.0, 0.1, 0.01), pmc=None)
                             "traffic": (round(pmc["table_bytes_per_unit"] * n_all)
                                         if frac >= 1.0 and pmc and "table_bytes_per_unit" in pmc else None),
                             "traffic_source": (pmc or {}).get("_src", {}).get("table") if frac >= 1.0 else None}
-        out[f"dirty_{int(round(frac * 100))}pct"] = case
+        out[f"dirty_{frac * 100:g}pct"] = case
     for tab in tabs.values():
         tab.close()
     out["workload"] = (f"resident table of {n_all} config-3 groups (F=4 and F=6 tiers); deltas mark the dirty "
@@ -724,6 +798,7 @@ def main():
         pcie["note"] = "full snapshot H2D (pinned) + kernel + commit D2H per batch"
         pcie["delta_streaming"] = delta_streaming(ctx, host, fill_threads=cpu_threads())
         pcie["delta_streaming"]["table_commit"] = table_commit_leg(ctx, host, pmc=pmc)
+        pcie["write_stamp"] = write_stamp_leg(ctx)
 
     # ------------------------------------------------------------------ CRC32C (config 5)
     crc = {}

@@ -285,11 +285,13 @@ int rh_commit_batch_wait(rh_groups* g, uint64_t ticket, rh_commit_out* out);
 #define RH_EVENTS_HOST_MAPPED 0
 #define RH_EVENTS_DEVICE      1
 int rh_groups_set_event_sink(rh_groups* g, int sink);
-/* Diagnostics (benchmarks): with timing enabled every evaluation records HIP events around its
- * evaluation kernel(s) and around the gather; rh_groups_last_timing returns the last evaluation's
- * two device times in ms (blocks until it has completed; RH_E_STATE before any timed evaluation). */
+/* Diagnostics (benchmarks, tests): with timing enabled every evaluation records HIP events around
+ * its evaluation kernel(s) and around the gather; rh_groups_last_timing returns the last
+ * evaluation's two device times in ms (blocks until it has completed; RH_E_STATE before any timed
+ * evaluation) and, if list_evaluated is not NULL, whether it ran over the dirty-row lists (1: only
+ * the rows marked since the previous evaluation of its kind were visited; 0: every tile). */
 int rh_groups_timing(rh_groups* g, int enable);
-int rh_groups_last_timing(rh_groups* g, float* eval_ms, float* gather_ms);
+int rh_groups_last_timing(rh_groups* g, float* eval_ms, float* gather_ms, int* list_evaluated);
 /* Batched commitIndexChanged() over the slots whose follower commitIndex or leader commitIndex
  * changed: the slots whose {min, majority, max} levels changed, into library-owned pinned memory
  * valid until the next rh_watch_levels / rh_watch_levels_async.  Blocks. */
@@ -427,7 +429,8 @@ int rh_crc32c_verify_host(rh_ctx* ctx, const uint8_t* seg, uint64_t seg_len, con
  * crosses PCIe without staging. */
 int rh_crc32c_stamp_host(rh_ctx* ctx, uint8_t* buf, uint64_t buf_len, const uint64_t* frame_off,
                          const uint32_t* frame_len, uint64_t n);
-/* Page-locks a host buffer for direct DMA (hipHostRegister) until rh_host_unregister. */
+/* Page-locks a host buffer for direct DMA from every GPU (hipHostRegister, portable) until
+ * rh_host_unregister. */
 int rh_host_register(rh_ctx* ctx, void* p, uint64_t n);
 int rh_host_unregister(rh_ctx* ctx, void* p);
 

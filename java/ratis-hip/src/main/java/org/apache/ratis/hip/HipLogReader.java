@@ -260,6 +260,34 @@ public final class HipLogReader implements AutoCloseable {
     return new Batch(image, start, frameOff, frameLen, frameCrc, segInts, segLongs);
   }
 
+  // ---- the write side of the same backend (HipFrameStamper) -----------------------------------
+  /** Page-locks a direct buffer (the log worker's reused write buffer) for DMA from every GPU. */
+  void register(ByteBuffer direct) throws IOException {
+    synchronized (ctxLock[0]) {
+      RatisHip.hostRegister0(ctx[0], direct);
+    }
+  }
+
+  void unregister(ByteBuffer direct) throws IOException {
+    synchronized (ctxLock[0]) {
+      if (ctx[0] != 0) {
+        RatisHip.hostUnregister0(ctx[0], direct);
+      }
+    }
+  }
+
+  /** rh_crc32c_stamp_host: the trailers of frames [off[i], off[i] + len[i]) of buf[0, limit)
+   *  written in place (big-endian PureJavaCrc32C of the bytes before each). */
+  void stampFrames(ByteBuffer direct, int limit, long[] off, int[] len, int n) throws IOException {
+    final int c = Math.floorMod(nextCtx.getAndIncrement(), ctx.length);
+    synchronized (ctxLock[c]) {
+      if (ctx[c] == 0) {
+        throw new IOException("HipLogReader is closed");
+      }
+      RatisHip.stampHost0(ctx[c], direct, limit, off, len, n);
+    }
+  }
+
   /** The bulk load of one directory: batch k + 1 read and verified while the caller loads batch k. */
   public Pipeline pipeline(List<Plan> plans, int maxOpSize) {
     return new Pipeline(plans, maxOpSize);

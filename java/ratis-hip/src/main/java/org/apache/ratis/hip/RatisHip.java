@@ -302,6 +302,12 @@ public final class RatisHip implements AutoCloseable {
       int maxOp, int capPerSeg, long[] frameOff, int[] frameLen, int[] frameCrc, int[] segInts, long[] segLongs)
       throws IOException;
 
+  /** rh_crc32c_stamp_host over buf[0, bufLen) of a direct buffer. */
+  static native void stampHost0(long ctx, ByteBuffer buf, long bufLen, long[] off, int[] len, int n) throws IOException;
+  /** rh_host_register / rh_host_unregister of a whole direct buffer. */
+  static native void hostRegister0(long ctx, ByteBuffer buf) throws IOException;
+  static native void hostUnregister0(long ctx, ByteBuffer buf) throws IOException;
+
   private static native long nodeCreate0(int deviceMask, long capacityPerShard, long gap) throws IOException;
   private static native void nodeDestroy0(long node) throws IOException;
   private static native int nodeShards0(long node);

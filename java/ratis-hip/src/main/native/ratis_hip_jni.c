@@ -431,3 +431,46 @@ JNIEXPORT jlong JNICALL CLS(readSegments0)(JNIEnv* env, jclass c, jlong ctx, job
     if (check(env, rc) < 0) return 0;
     return (jlong)total;
 }
+
+/* ---- the write side (HipFrameStamper) ------------------------------------------------------------ */
+JNIEXPORT void JNICALL CLS(stampHost0)(JNIEnv* env, jclass c, jlong ctx, jobject buf, jlong buf_len, jlongArray off,
+                                       jintArray len, jint n) {
+    (void)c;
+    uint8_t* base = buf ? (uint8_t*)(*env)->GetDirectBufferAddress(env, buf) : NULL;
+    const jlong capb = buf ? (*env)->GetDirectBufferCapacity(env, buf) : -1;
+    if (!base || buf_len < 0 || capb < buf_len || n < 0) {
+        throw_arg(env, "stampFrames: not a direct buffer, bufLen beyond it, or n < 0");
+        return;
+    }
+    if (n == 0) return;
+    if (!has_len(env, off, n, "off shorter than n") || !has_len(env, len, n, "len shorter than n")) return;
+    jlong* o = (*env)->GetLongArrayElements(env, off, NULL);
+    jint* l = o ? (*env)->GetIntArrayElements(env, len, NULL) : NULL;
+    int rc = RH_E_NOMEM;
+    if (o && l)
+        rc = rh_crc32c_stamp_host(C(ctx), base, (uint64_t)buf_len, (const uint64_t*)o, (const uint32_t*)l, (uint64_t)n);
+    if (l) (*env)->ReleaseIntArrayElements(env, len, l, JNI_ABORT);
+    if (o) (*env)->ReleaseLongArrayElements(env, off, o, JNI_ABORT);
+    check(env, rc);
+}
+
+JNIEXPORT void JNICALL CLS(hostRegister0)(JNIEnv* env, jclass c, jlong ctx, jobject buf) {
+    (void)c;
+    void* base = buf ? (*env)->GetDirectBufferAddress(env, buf) : NULL;
+    const jlong capb = buf ? (*env)->GetDirectBufferCapacity(env, buf) : -1;
+    if (!base || capb <= 0) {
+        throw_arg(env, "register: not a direct buffer");
+        return;
+    }
+    check(env, rh_host_register(C(ctx), base, (uint64_t)capb));
+}
+
+JNIEXPORT void JNICALL CLS(hostUnregister0)(JNIEnv* env, jclass c, jlong ctx, jobject buf) {
+    (void)c;
+    void* base = buf ? (*env)->GetDirectBufferAddress(env, buf) : NULL;
+    if (!base) {
+        throw_arg(env, "unregister: not a direct buffer");
+        return;
+    }
+    check(env, rh_host_unregister(C(ctx), base));
+}

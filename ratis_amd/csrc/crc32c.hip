@@ -1504,6 +1504,79 @@ int rh_crc_upload_tables(rh_ctx* ctx) {
     return RH_OK;
 }
 
+// ---- small flush batches: one lane per frame ----------------------------------------------------
+// The write side's batches (rh_crc32c_stamp_host) are a few to a few thousand short frames, where the
+// window and packed kernels' fixed costs (128-156 KiB of LDS tables staged per workgroup, a second
+// launch) dominate.  Here a lane folds its own frame with PJC's own slicing-by-8 (PJC:54-91: eight
+// table lookups per 8-byte word, T[k] = the register after a byte and k zero bytes), the 8 KiB of
+// tables built in LDS from the context's four slicing-by-4 tables.  Latency-bound per lane (one
+// dependent table round per 8 bytes), parallel over frames.  Frames must be well formed (the caller
+// checks): [off, off + len) inside the buffer and len >= 4 under STAMP / VERIFY.
+__global__ __launch_bounds__(64) void crc_serial_kernel(const uint8_t* __restrict__ buf, uint8_t* wbuf,
+                                                         const uint64_t* __restrict__ off,
+                                                         const uint32_t* __restrict__ len, uint64_t n,
+                                                         uint32_t init, uint32_t flags, const uint32_t* __restrict__ slice4,
+                                                         uint32_t* crc_out) {
+    __shared__ uint32_t T[8][256];
+    for (uint32_t i = threadIdx.x; i < 1024; i += blockDim.x) T[i >> 8][i & 255] = slice4[i];
+    __syncthreads();
+    for (int k = 4; k < 8; ++k) {   // T[k][b] = T[k-1][b] advanced over one more zero byte
+        for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
+            const uint32_t x = T[k - 1][i];
+            T[k][i] = (x >> 8) ^ T[0][x & 0xffu];
+        }
+        __syncthreads();
+    }
+    const uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= n) return;
+    const uint8_t* p = buf + off[f];
+    const uint32_t span = (flags & (RH_CRC_STAMP | RH_CRC_VERIFY)) ? len[f] - 4 : len[f];
+    const uint8_t* e = p + span;
+    uint32_t c = init;
+    auto step8 = [&](uint32_t lo, uint32_t hi) {   // one PJC slicing-by-8 round over 8 bytes
+        lo ^= c;
+        c = T[7][lo & 0xffu] ^ T[6][(lo >> 8) & 0xffu] ^ T[5][(lo >> 16) & 0xffu] ^ T[4][lo >> 24] ^
+            T[3][hi & 0xffu] ^ T[2][(hi >> 8) & 0xffu] ^ T[1][(hi >> 16) & 0xffu] ^ T[0][hi >> 24];
+    };
+    while (p < e && (reinterpret_cast<uintptr_t>(p) & 15)) c = (c >> 8) ^ T[0][(c ^ *p++) & 0xffu];
+    // 128 bytes per round: the eight 16-byte loads are all in flight before the first fold, so a
+    // lane pays one memory latency per 128 bytes, not per 8
+    typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+    for (; p + 128 <= e; p += 128) {
+        v4u32 q[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) q[k] = reinterpret_cast<const v4u32*>(p)[k];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            step8(q[k].x, q[k].y);
+            step8(q[k].z, q[k].w);
+        }
+    }
+    for (; p + 8 <= e; p += 8) {
+        const uint64_t w = *reinterpret_cast<const uint64_t*>(p);
+        step8((uint32_t)w, (uint32_t)(w >> 32));
+    }
+    while (p < e) c = (c >> 8) ^ T[0][(c ^ *p++) & 0xffu];
+    const uint32_t v = ~c;   // getValue()
+    if (crc_out) crc_out[f] = v;
+    if (flags & RH_CRC_STAMP) {
+        uint8_t* t = wbuf + off[f] + span;
+        t[0] = (uint8_t)(v >> 24);
+        t[1] = (uint8_t)(v >> 16);
+        t[2] = (uint8_t)(v >> 8);
+        t[3] = (uint8_t)v;
+    }
+}
+
+int rh_crc_serial_launch(rh_ctx* ctx, const rh_frames* f, uint32_t flags, hipStream_t stream) {
+    if (f->n == 0) return RH_OK;
+    // one wave per workgroup: the frames spread over as many CUs as there are waves of them
+    hipLaunchKernelGGL(crc_serial_kernel, dim3((uint32_t)((f->n + 63) / 64)), dim3(64), 0, stream, f->buf, f->buf,
+                       f->frame_off, f->frame_len, f->n, f->init_state, flags, ctx->d_slice, f->crc_out);
+    RH_HIP(hipGetLastError());
+    return RH_OK;
+}
+
 int rh_crc_launch_impl(rh_ctx* ctx, const rh_frames* f, uint32_t flags, hipStream_t stream) {
     if (!f) return rh::fail(RH_E_INVAL, "rh_crc32c_frames_launch: frames == NULL");
     if ((flags & ~(RH_CRC_VERIFY | RH_CRC_STAMP)) || flags == (RH_CRC_VERIFY | RH_CRC_STAMP))

@@ -16,6 +16,10 @@
 
 #define RH_EXPORT extern "C" __attribute__((visibility("default")))
 
+#ifndef RH_LIST_DIV   // A/B: list mode while at most capacity / RH_LIST_DIV rows can be dirty
+#define RH_LIST_DIV 32
+#endif
+
 namespace {
 
 using rh::CtrlOp;
@@ -112,6 +116,14 @@ struct rh_groups {
     bool wpending = false, whbm = false;
     hipEvent_t ldone = nullptr;               // rh_lease_batch_async's bitmap D2H
     bool lpending = false;
+    // dirty-row lists (rh_internal.h, TableLists), per kind (0 = updateCommit, 1 = commitIndexChanged)
+    uint32_t* d_lrows[2] = {nullptr, nullptr};   // [kTableTiers][kHeads][lcap]
+    unsigned long long* d_lheads = nullptr;      // [2 kinds][2 sets][kTableTiers * kHeads * kHeadStride]
+    uint32_t lcap = 0;
+    int lpar[2] = {0, 0};       // the set appends go to
+    bool lvalid[2] = {true, true};   // every row marked since the kind's last evaluation is listed
+    uint64_t lmarks[2] = {0, 0};     // bound on the rows marked since then
+    bool last_list = false;     // the last evaluation ran over the dirty-row lists (diagnostics)
     hipEvent_t tev[3] = {nullptr, nullptr, nullptr};  // rh_groups_timing: around evaluation and gather
     bool timing = false, timed = false;
     int event_sink = RH_EVENTS_HOST_MAPPED;
@@ -177,6 +189,9 @@ void free_groups(rh_groups* g) {
         (void)hipFree(g->ev[i].hbm_wall);
     }
     free_staging(g);
+    (void)hipFree(g->d_lrows[0]);
+    (void)hipFree(g->d_lrows[1]);
+    (void)hipFree(g->d_lheads);
     (void)hipFree(g->hbm_watch);
     (void)hipFree(g->d_heads);
     if (g->watch) (void)hipHostFree(g->watch);
@@ -272,6 +287,7 @@ int flush_ops(rh_groups* g) {
         int rc = rh_table_control(g->dev, g->d_ops, n, s);
         if (rc != RH_OK) return rc;
         g->ops.clear();
+        g->lvalid[0] = g->lvalid[1] = false;   // control ops mark rows with plain stores: no lists
     }
     ++g->op_gen;
     for (auto& t : g->tiers) {
@@ -320,6 +336,27 @@ unsigned long long* heads_of(rh_groups* g, int mode, int parity) {
     return g->d_heads + (size_t)(mode * 2 + parity) * rh::kHeads * rh::kHeadStride;
 }
 
+constexpr size_t kListRegions = (size_t)rh::kTableTiers * rh::kHeads;
+
+unsigned long long* lheads_of(rh_groups* g, int kind, int set) {
+    return g->d_lheads + (size_t)(kind * 2 + set) * kListRegions * rh::kHeadStride;
+}
+
+// The list `kind` for `n_marks` more possible markings: maintained while the bound stays within the
+// list capacity; past it the kind's list is given up until its next evaluation (a tile evaluation).
+rh::TableLists lists_for(rh_groups* g, int kind, uint64_t n_marks) {
+    rh::TableLists l;
+    if (g->lvalid[kind] && g->lmarks[kind] + n_marks <= g->lcap) {
+        g->lmarks[kind] += n_marks;
+        l.rows = g->d_lrows[kind];
+        l.heads = lheads_of(g, kind, g->lpar[kind]);
+        l.cap = g->lcap;
+    } else {
+        g->lvalid[kind] = false;
+    }
+    return l;
+}
+
 // After a failed evaluation launch (some workgroups may have counted into a head, a later launch
 // of the pair may not have run): drain the stream and zero every head word, so the next
 // evaluation starts from clean counters whichever parity it uses.
@@ -327,7 +364,9 @@ int reset_heads(rh_groups* g) {
     hipStream_t s = g->ctx->stream;
     (void)hipStreamSynchronize(s);
     RH_HIP(hipMemsetAsync(g->d_heads, 0, (size_t)4 * rh::kHeads * rh::kHeadStride * 8, s));
+    RH_HIP(hipMemsetAsync(g->d_lheads, 0, (size_t)4 * kListRegions * rh::kHeadStride * 8, s));
     RH_HIP(hipStreamSynchronize(s));
+    g->lvalid[0] = g->lvalid[1] = false;   // the next evaluations run the tile kernels
     return RH_OK;
 }
 
@@ -343,7 +382,8 @@ int evaluate(rh_groups* g, int mode, bool wall_on, rh_index_event* adv, rh_index
         h_counts[0] = h_counts[1] = 0;
         return RH_OK;
     }
-    rc = ensure_staging(g, blocks);
+    // the list evaluation writes at most lcap records of a kind into any one head region
+    rc = ensure_staging(g, std::max<uint32_t>(blocks, (uint32_t)((uint64_t)g->lcap * rh::kHeads / rh::table_block_rows() + 1)));
     if (rc != RH_OK) return rc;
     const int m = mode == RH_MODE_WATCH ? 1 : 0;
     rh::TableEvents ev;
@@ -353,8 +393,21 @@ int evaluate(rh_groups* g, int mode, bool wall_on, rh_index_event* adv, rh_index
     ev.region = g->st_region;
     ev.heads = heads_of(g, m, g->cpar[m]);
     ev.heads_next = heads_of(g, m, g->cpar[m] ^ 1);
+    ev.lheads_next = lheads_of(g, m, g->lpar[m] ^ 1);
+    const bool list = g->lvalid[m];   // every row marked since the last evaluation is listed
     if (g->timing) RH_HIP(hipEventRecord(g->tev[0], s));
-    rc = rh_table_commit(g->dev, mode, ev, s);
+    if (list) {
+        rh::TableLists l;
+        l.rows = g->d_lrows[m];
+        l.heads = lheads_of(g, m, g->lpar[m]);
+        l.cap = g->lcap;
+        // COMMIT marks the rows whose commit advanced for commitIndexChanged: at most the listed ones
+        const rh::TableLists lw = m == 0 ? lists_for(g, 1, g->lmarks[0]) : rh::TableLists{};
+        rc = rh_table_commit_lists(g->dev, mode, l, lw, ev, s);
+    } else {
+        if (m == 0) g->lvalid[1] = false;   // the tile kernel marks wdirty with plain stores
+        rc = rh_table_commit(g->dev, mode, ev, s);
+    }
     if (rc == RH_OK && g->timing) RH_HIP(hipEventRecord(g->tev[1], s));
     if (rc == RH_OK) rc = rh_table_gather(mode, ev, adv, wall, watch, g->capacity, counts_out, s);
     if (rc == RH_OK && g->timing) {
@@ -367,6 +420,10 @@ int evaluate(rh_groups* g, int mode, bool wall_on, rh_index_event* adv, rh_index
         return rh::fail(rc, msg);
     }
     g->cpar[m] ^= 1;  // the launch cleared the other set
+    g->lpar[m] ^= 1;  // ... and the other list set of this kind: fresh lists from here on
+    g->lmarks[m] = 0;
+    g->lvalid[m] = true;
+    g->last_list = list;
     return RH_OK;
 }
 
@@ -402,11 +459,13 @@ int ring_submit(rh_groups* g, int i, size_t n, bool has_set) {
     RH_HIP(hipStreamWaitEvent(s, g->ring_free[i], 0));
     g->ring_used[i] = true;
     g->ring_next = i ^ 1;
+    // every delta marks at most one row per kind
+    const rh::TableLists lc = lists_for(g, 0, n), lw = lists_for(g, 1, n);
     if (has_set) {
-        rc = rh_table_apply_deltas(g->dev, g->d_ring[i], n, 0, s);
+        rc = rh_table_apply_deltas(g->dev, g->d_ring[i], n, 0, lc, lw, s);
         if (rc != RH_OK) return rc;
     }
-    rc = rh_table_apply_deltas(g->dev, g->d_ring[i], n, 1, s);
+    rc = rh_table_apply_deltas(g->dev, g->d_ring[i], n, 1, lc, lw, s);
     if (rc != RH_OK) return rc;
     RH_HIP(hipEventRecord(g->ring_read[i], s));
     return RH_OK;
@@ -471,6 +530,12 @@ RH_EXPORT int rh_groups_create(rh_ctx* ctx, uint64_t capacity, int64_t gap_thres
         rc = rh::fail(RH_E_DEVICE, "hipEventCreate(watch levels)");
     if (rc == RH_OK && hipEventCreateWithFlags(&g->ldone, hipEventDisableTiming) != hipSuccess)
         rc = rh::fail(RH_E_DEVICE, "hipEventCreate(lease batch)");
+    // list capacity: a list evaluation is chosen while at most capacity / RH_LIST_DIV rows can be dirty
+    g->lcap = (uint32_t)std::max<uint64_t>(1024, capacity / RH_LIST_DIV);
+    for (int k = 0; k < 2 && rc == RH_OK; ++k) rc = dalloc(&g->d_lrows[k], kListRegions * g->lcap);
+    if (rc == RH_OK) rc = dalloc(&g->d_lheads, (size_t)4 * kListRegions * rh::kHeadStride);
+    if (rc == RH_OK && hipMemsetAsync(g->d_lheads, 0, (size_t)4 * kListRegions * rh::kHeadStride * 8, s) != hipSuccess)
+        rc = rh::fail(RH_E_DEVICE, "rh_groups_create: list counters");
     if (rc == RH_OK) rc = dalloc(&g->d_heads, (size_t)4 * rh::kHeads * rh::kHeadStride);
     if (rc == RH_OK && hipMemsetAsync(g->d_heads, 0, (size_t)4 * rh::kHeads * rh::kHeadStride * 8, s) != hipSuccess)
         rc = rh::fail(RH_E_DEVICE, "rh_groups_create: counters");
@@ -541,7 +606,7 @@ RH_EXPORT int rh_groups_timing(rh_groups* g, int enable) {
     return RH_OK;
 }
 
-RH_EXPORT int rh_groups_last_timing(rh_groups* g, float* eval_ms, float* gather_ms) {
+RH_EXPORT int rh_groups_last_timing(rh_groups* g, float* eval_ms, float* gather_ms, int* list_evaluated) {
     if (!g || !eval_ms || !gather_ms) return rh::fail(RH_E_INVAL, "rh_groups_last_timing: NULL argument");
     DeviceGuard dg(g->ctx->device);
     std::lock_guard<std::mutex> lk(g->mu);
@@ -549,6 +614,7 @@ RH_EXPORT int rh_groups_last_timing(rh_groups* g, float* eval_ms, float* gather_
     RH_HIP(hipEventSynchronize(g->tev[2]));
     RH_HIP(hipEventElapsedTime(eval_ms, g->tev[0], g->tev[1]));
     RH_HIP(hipEventElapsedTime(gather_ms, g->tev[1], g->tev[2]));
+    if (list_evaluated) *list_evaluated = g->last_list ? 1 : 0;
     return RH_OK;
 }
 
@@ -694,6 +760,7 @@ RH_EXPORT int rh_groups_load(rh_groups* g, uint32_t first, uint32_t n, uint32_t 
     }
     int rc = flush_ops(g);  // launches the stops; the rows they released are reusable now
     if (rc != RH_OK) return rc;
+    g->lvalid[0] = g->lvalid[1] = false;   // the load marks its rows with plain stores
     hipStream_t s = g->ctx->stream;
     std::vector<std::vector<uint32_t>> members(kTableTiers);
     for (uint32_t i = 0; i < n; ++i) members[rh::tier_of_width(needed_width(conf[i]))].push_back(i);

@@ -267,7 +267,7 @@ RH_EXPORT int rh_crc32c_verify_host(rh_ctx* ctx, const uint8_t* seg, uint64_t se
 RH_EXPORT int rh_host_register(rh_ctx* ctx, void* p, uint64_t n) {
     if (!ctx || !p || n == 0) return rh::fail(RH_E_INVAL, "rh_host_register: ctx/p == NULL or n == 0");
     DeviceGuard g(ctx->device);
-    RH_HIP(hipHostRegister(p, n, hipHostRegisterDefault));
+    RH_HIP(hipHostRegister(p, n, hipHostRegisterPortable));   // every GPU's contexts may read it
     return RH_OK;
 }
 
@@ -278,6 +278,10 @@ RH_EXPORT int rh_host_unregister(rh_ctx* ctx, void* p) {
     return RH_OK;
 }
 
+// frames up to this length go one lane per frame (crc_serial_kernel): 64 KiB is 8k dependent
+// table rounds, ~40 us on one lane; longer ones to the streaming plans
+constexpr uint64_t kSerialMaxFrame = 64 << 10;
+
 RH_EXPORT int rh_crc32c_stamp_host(rh_ctx* ctx, uint8_t* buf, uint64_t buf_len, const uint64_t* frame_off,
                                    const uint32_t* frame_len, uint64_t n) {
     if (!ctx) return rh::fail(RH_E_INVAL, "rh_crc32c_stamp_host: ctx == NULL");
@@ -285,9 +289,10 @@ RH_EXPORT int rh_crc32c_stamp_host(rh_ctx* ctx, uint8_t* buf, uint64_t buf_len, 
     if (!buf || !frame_off || !frame_len) return rh::fail(RH_E_INVAL, "rh_crc32c_stamp_host: NULL input");
     if (n >= (1ull << 32)) return rh::fail(RH_E_RANGE, "rh_crc32c_stamp_host: n >= 2^32");
     // every frame must lie in the buffer and hold its trailer: nothing is stamped otherwise
-    uint64_t lo = UINT64_MAX, hi = 0;
+    uint64_t lo = UINT64_MAX, hi = 0, max_len = 0;
     for (uint64_t i = 0; i < n; ++i) {
         const uint64_t o = frame_off[i], l = frame_len[i];
+        max_len = std::max(max_len, l);
         if (l < 4 || o > buf_len || l > buf_len - o)
             return rh::fail(RH_E_INVAL, "rh_crc32c_stamp_host: frame " + std::to_string(i) +
                                             " is shorter than its trailer or outside the buffer");
@@ -295,33 +300,46 @@ RH_EXPORT int rh_crc32c_stamp_host(rh_ctx* ctx, uint8_t* buf, uint64_t buf_len, 
         hi = std::max(hi, o + l);
     }
     DeviceGuard g(ctx->device);
-    // only the span the frames cover crosses PCIe (a flush batch is one contiguous run); the CRCs come
-    // back as 4 B per frame and the host writes the big-endian trailers
+    // only the span the frames cover crosses PCIe (a flush batch is one contiguous run); the frame
+    // table goes over from the context's pinned staging in one copy, the CRCs come back into it as
+    // 4 B per frame, and the host writes the big-endian trailers
     auto al = [](uint64_t x) { return (x + 255) / 256 * 256; };
     const uint64_t span = hi - lo;
-    const uint64_t o_img = 0, o_off = al(span), o_len = o_off + al(n * 8), o_crc = o_len + al(n * 4),
-                   total = o_crc + al(n * 4);
+    const uint64_t t_off = 0, t_len = al(n * 8), t_crc = t_len + al(n * 4), t_bytes = t_crc + al(n * 4);
+    const uint64_t o_img = 0, o_tab = al(span), total = o_tab + t_bytes;
+    std::lock_guard<std::mutex> lk(ctx->stage_mu);
+    if (ctx->pinned_bytes < t_bytes) {
+        if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
+        ctx->h_pinned = nullptr;
+        ctx->pinned_bytes = 0;
+        const size_t want = std::max<size_t>(t_bytes, (size_t)1 << 20);
+        if (hipHostMalloc(&ctx->h_pinned, want) != hipSuccess) return rh::fail(RH_E_NOMEM, "rh_crc32c_stamp_host: pinned staging");
+        ctx->pinned_bytes = want;
+    }
+    uint8_t* st = static_cast<uint8_t*>(ctx->h_pinned);
+    uint64_t* rel = reinterpret_cast<uint64_t*>(st + t_off);
+    for (uint64_t i = 0; i < n; ++i) rel[i] = frame_off[i] - lo;
+    std::memcpy(st + t_len, frame_len, n * 4);
+    const uint32_t* crc = reinterpret_cast<const uint32_t*>(st + t_crc);
     hipStream_t s = ctx->stream;
     rh::PoolScratch scratch(s);
     if (scratch.alloc(ctx, total) != hipSuccess) return rh::fail(RH_E_NOMEM, "rh_crc32c_stamp_host: device scratch");
     uint8_t* base = scratch.bytes();
-    std::vector<uint64_t> rel(n);
-    for (uint64_t i = 0; i < n; ++i) rel[i] = frame_off[i] - lo;
-    std::vector<uint32_t> crc(n);
     RH_HIP(hipMemcpyAsync(base + o_img, buf + lo, span, hipMemcpyHostToDevice, s));
-    RH_HIP(hipMemcpyAsync(base + o_off, rel.data(), n * 8, hipMemcpyHostToDevice, s));
-    RH_HIP(hipMemcpyAsync(base + o_len, frame_len, n * 4, hipMemcpyHostToDevice, s));
+    RH_HIP(hipMemcpyAsync(base + o_tab, st, t_crc, hipMemcpyHostToDevice, s));
     rh_frames f{};
     f.buf = base + o_img;
     f.buf_len = span;
-    f.frame_off = reinterpret_cast<const uint64_t*>(base + o_off);
-    f.frame_len = reinterpret_cast<const uint32_t*>(base + o_len);
+    f.frame_off = reinterpret_cast<const uint64_t*>(base + o_tab + t_off);
+    f.frame_len = reinterpret_cast<const uint32_t*>(base + o_tab + t_len);
     f.n = n;
     f.init_state = 0xFFFFFFFFu;   // checksum.reset() before every entry (OUT:100-103)
-    f.crc_out = reinterpret_cast<uint32_t*>(base + o_crc);
-    // STAMP also writes the device copy's trailers; only crc_out comes back
-    int rc = rh_crc_launch_impl(ctx, &f, RH_CRC_STAMP, s);
-    if (rc == RH_OK) RH_HIP(hipMemcpyAsync(crc.data(), base + o_crc, n * 4, hipMemcpyDeviceToHost, s));
+    f.crc_out = reinterpret_cast<uint32_t*>(base + o_tab + t_crc);
+    // STAMP also writes the device copy's trailers; only crc_out comes back.  Batches of short frames
+    // (a flush batch of log entries) go one lane per frame; long entries to the window / packed plans
+    int rc = max_len <= kSerialMaxFrame ? rh_crc_serial_launch(ctx, &f, RH_CRC_STAMP, s)
+                                        : rh_crc_launch_impl(ctx, &f, RH_CRC_STAMP, s);
+    if (rc == RH_OK) RH_HIP(hipMemcpyAsync(st + t_crc, base + o_tab + t_crc, n * 4, hipMemcpyDeviceToHost, s));
     RH_HIP(hipStreamSynchronize(s));
     if (rc != RH_OK) return rc;
     for (uint64_t i = 0; i < n; ++i) {   // buf.putInt((int) checksum.getValue()): big-endian

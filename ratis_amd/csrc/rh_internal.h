@@ -153,7 +153,21 @@ struct TableEvents {
     unsigned long long* heads = nullptr;       // this evaluation's kHeads words (zero at launch)
     unsigned long long* heads_next = nullptr;  // the next evaluation's: cleared by block 0
     uint32_t block_base = 0;                    // launch-global index of this launch's block 0
+    unsigned long long* lheads_next = nullptr;  // the other list-head set of the evaluated kind: cleared
 };
+// DIRTY-ROW LISTS (list mode).  While the host knows that few rows can be dirty (the deltas and
+// control ops since the last evaluation of a kind bound the rows they can mark), every 0 -> 1
+// transition of a row's dirty / wdirty flag (found with a 32-bit atomicOr on the flag's word) also
+// appends the row to a list, per (tier, head): kHeads regions of `cap` entries per tier, each with its
+// own head word.  The evaluation then runs over the listed rows only (table_list_kernel: work
+// proportional to the dirty rows, not to the table).  Two head sets per kind alternate like the
+// event heads: appends go to `heads`; the evaluation that consumes them clears the other set.
+struct TableLists {
+    uint32_t* rows = nullptr;            // [kTableTiers][kHeads][cap] row indices within the tier
+    unsigned long long* heads = nullptr; // [kTableTiers][kHeads] words, kHeadStride apart (null: no list)
+    uint32_t cap = 0;
+};
+
 // Workgroups the table evaluation launches for a table (both width classes).
 uint32_t table_commit_blocks(const TableDev& t);
 // Rows per evaluation workgroup (the staging region unit).
@@ -172,6 +186,7 @@ struct rh_ctx {
     uint32_t* d_inv32 = nullptr;   // [32][8][16] inverse lane maps of the packed CRC kernel
     uint32_t* d_initff = nullptr;  // [kCrcInitSpan + 1] advance of reset()'s 0xFFFFFFFF over k zero bytes
     std::mutex pool_mu;  // guards the pool's creation
+    std::mutex stage_mu;  // guards the pinned staging below (rh_crc32c_stamp_host's frame table / CRCs)
     void* h_pinned = nullptr;
     size_t pinned_bytes = 0;
     hipMemPool_t pool = nullptr;  // stream-ordered scratch (rh::pool_alloc)
@@ -200,7 +215,12 @@ struct PoolScratch {
 int rh_commit_launch_impl(rh_ctx* ctx, const rh_commit_soa* tiers, int n_tiers, hipStream_t stream);
 // Resident table kernels (table.hip): delta apply (phase 0 = SET deltas, 1 = MAX deltas),
 // control ops, and updateCommit / commitIndexChanged over the dirty rows of every tier.
-int rh_table_apply_deltas(const rh::TableDev& t, const rh_delta* d_deltas, uint64_t n, int phase, hipStream_t stream);
+int rh_table_apply_deltas(const rh::TableDev& t, const rh_delta* d_deltas, uint64_t n, int phase,
+                          const rh::TableLists& lc, const rh::TableLists& lw, hipStream_t stream);
+// List-mode evaluation of the listed rows of one kind (mode); COMMIT appends the rows whose commit
+// advanced to the watch list `lw` (when it is maintained).  Events as rh_table_commit.
+int rh_table_commit_lists(const rh::TableDev& t, int mode, const rh::TableLists& l, const rh::TableLists& lw,
+                          const rh::TableEvents& ev, hipStream_t stream);
 int rh_table_control(const rh::TableDev& t, const rh::CtrlOp* d_ops, uint64_t n, hipStream_t stream);
 int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev, hipStream_t stream);
 // Packs an evaluation's kHeads staging regions into contiguous lists (up to `cap` records per kind)
@@ -215,6 +235,8 @@ int rh_table_lease(const rh::TableDev& t, int64_t now_nanos, int64_t timeout_ms,
 int rh_table_read(const rh::TableDev& t, uint32_t first, uint32_t n, uint8_t column, int64_t* d_out,
                   hipStream_t stream);
 int rh_crc_launch_impl(rh_ctx* ctx, const rh_frames* f, uint32_t flags, hipStream_t stream);
+// One lane per frame (crc_serial_kernel): small batches of well-formed frames (no bad bits / counts).
+int rh_crc_serial_launch(rh_ctx* ctx, const rh_frames* f, uint32_t flags, hipStream_t stream);
 int rh_crc_upload_tables(rh_ctx* ctx);
 int rh_segments_launch_impl(rh_ctx* ctx, const rh_segments* segs, hipStream_t stream);
 int rh_segments_read_impl(rh_ctx* ctx, const rh_segments* segs, const rh_segments_crc* crc, hipStream_t stream);

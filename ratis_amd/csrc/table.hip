@@ -30,6 +30,7 @@ using rh::CtrlOp;
 using rh::TableDev;
 using rh::TableEvents;
 using rh::TableTier;
+using rh::TableLists;
 namespace tile = rh::tile;
 
 typedef int64_t v2i64 __attribute__((ext_vector_type(2)));
@@ -53,57 +54,106 @@ __device__ __forceinline__ void mark(const TableTier& tt, uint64_t r, int watch)
     *tt.summary(r, watch) = 1;
 }
 
+// The same with a dirty-row list maintained (list mode): the flag is set through its 32-bit word
+// with an atomicOr, and the return value says whether this call made the 0 -> 1 transition (the
+// caller then appends the row).  Without a list: plain stores, no transition reported.
+__device__ __forceinline__ bool mark_listed(const TableTier& tt, uint64_t r, int watch, bool listed) {
+    uint8_t* f = tt.u8(watch ? tile::kWdirty : tile::kDirty, r);
+    *tt.summary(r, watch) = 1;
+    if (!listed) {
+        *f = 1;
+        return false;
+    }
+    uint32_t* w = reinterpret_cast<uint32_t*>(reinterpret_cast<uintptr_t>(f) & ~(uintptr_t)3);
+    const uint32_t sh = 8u * (uint32_t)(reinterpret_cast<uintptr_t>(f) & 3);
+    const uint32_t old = atomicOr(w, 1u << sh);
+    return ((old >> sh) & 0xFFu) == 0u;
+}
+
+// Appends the rows of the lanes with `want` to list l, region (tier t, head h): one returning
+// atomic per (wave, tier) present.  Every lane of the wave must call it (ballots).
+__device__ __forceinline__ void list_append(const TableLists& l, bool want, int t, uint32_t row, uint32_t h) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    uint64_t pend = __ballot(want);
+    while (pend) {
+        const int leader = __ffsll((long long)pend) - 1;
+        const int tl = __shfl(t, leader);
+        const bool mine = want && t == tl;
+        const uint64_t grp = __ballot(mine);
+        const uint32_t reg = (uint32_t)tl * rh::kHeads + h;
+        uint32_t base = 0;
+        if (lane == leader)
+            base = (uint32_t)atomicAdd(l.heads + (uint64_t)reg * rh::kHeadStride, (unsigned long long)__popcll(grp));
+        base = (uint32_t)__shfl((int)base, leader);
+        if (mine) {
+            const uint32_t idx = base + (uint32_t)__popcll(grp & lt);
+            if (idx < l.cap) l.rows[(uint64_t)reg * l.cap + idx] = row;   // the host's bound keeps idx < cap
+        }
+        pend &= ~grp;
+    }
+}
+
 // ---- deltas --------------------------------------------------------------------------------------
 // phase 0 applies the batch's SET deltas (plain stores), phase 1 its MAX deltas (atomicMax): the
-// host orders batches so that this equals applying them one by one (ratis_hip.h, rh_delta).
+// host orders batches so that this equals applying them one by one (ratis_hip.h, rh_delta).  With
+// dirty-row lists (lc / lw .rows non-null) the rows a delta newly marks are appended to them.
 __global__ __launch_bounds__(256) void table_apply_kernel(TableDev Targ, const rh_delta* __restrict__ d, uint64_t n,
-                                                          int phase) {
+                                                          int phase, TableLists lc, TableLists lw) {
     // the tier is picked per thread: index the argument in the kernarg segment (scalar loads), not
     // the by-value copy, which the compiler spilled whole into scratch (984 B per lane, 8x slower)
     const TableDev& T = rh::kernarg_struct<TableDev>();
     (void)Targ;
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const rh_delta x = d[i];
-    if (x.op != (phase == 0 ? RH_OP_SET : RH_OP_MAX)) return;
-    const TableTier* tt;
-    uint32_t row;
-    if (!locate(T, x.slot, tt, row)) return;  // stopped slot / out of range: ignored
-    int64_t* p = nullptr;
-    bool commit_ev = false, watch_ev = false;
-    const uint32_t c = x.column, F = tt->width;
-    if (c == RH_COL_LEASE_ON) {  // AtomicBoolean: SET stores, MAX ORs
-        uint8_t* f = tt->u8(tile::kLon, row);
+    bool ac = false, aw = false;   // this delta newly marked its row (list mode)
+    int t = 0;
+    uint32_t row = 0;
+    do {   // one pass; `break` = the delta has no (further) effect
+        if (i >= n) break;
+        const rh_delta x = d[i];
+        if (x.op != (phase == 0 ? RH_OP_SET : RH_OP_MAX)) break;
+        const TableTier* tt;
+        if (!locate(T, x.slot, tt, row)) break;  // stopped slot / out of range: ignored
+        t = (int)(T.slot_map[x.slot] >> 28);
+        int64_t* p = nullptr;
+        bool commit_ev = false, watch_ev = false;
+        const uint32_t c = x.column, F = tt->width;
+        if (c == RH_COL_LEASE_ON) {  // AtomicBoolean: SET stores, MAX ORs
+            uint8_t* f = tt->u8(tile::kLon, row);
+            if (phase == 0)
+                *f = x.value != 0;
+            else if (x.value != 0)
+                *f = 1;
+            break;
+        }
+        if (c >= 48 && c < 64) {
+            if (c - 48 < F) p = tt->i64(tile::fts(F, c - 48), row);
+        } else if (c == RH_COL_LEASE) {
+            p = tt->i64(tile::lease(F), row);
+        } else if (c < 16) {
+            if (c < F) p = tt->i64(tile::match(c), row);
+            commit_ev = true;
+        } else if (c < 32) {
+            if (c - 16 < F) p = tt->i64(tile::fcommit(F, c - 16), row);
+            watch_ev = true;
+        } else if (c == RH_COL_FLUSH) {
+            p = tt->i64(tile::flush(F), row);
+            commit_ev = true;
+        } else if (c == RH_COL_COMMITTED) {
+            p = tt->i64(tile::commit(F), row);
+            commit_ev = watch_ev = true;
+        }
+        if (!p) break;
         if (phase == 0)
-            *f = x.value != 0;
-        else if (x.value != 0)
-            *f = 1;
-        return;
-    }
-    if (c >= 48 && c < 64) {
-        if (c - 48 < F) p = tt->i64(tile::fts(F, c - 48), row);
-    } else if (c == RH_COL_LEASE) {
-        p = tt->i64(tile::lease(F), row);
-    } else if (c < 16) {
-        if (c < F) p = tt->i64(tile::match(c), row);
-        commit_ev = true;
-    } else if (c < 32) {
-        if (c - 16 < F) p = tt->i64(tile::fcommit(F, c - 16), row);
-        watch_ev = true;
-    } else if (c == RH_COL_FLUSH) {
-        p = tt->i64(tile::flush(F), row);
-        commit_ev = true;
-    } else if (c == RH_COL_COMMITTED) {
-        p = tt->i64(tile::commit(F), row);
-        commit_ev = watch_ev = true;
-    }
-    if (!p) return;
-    if (phase == 0)
-        *p = x.value;
-    else
-        atomicMax(reinterpret_cast<long long*>(p), (long long)x.value);
-    if (commit_ev) mark(*tt, row, 0);
-    if (watch_ev) mark(*tt, row, 1);
+            *p = x.value;
+        else
+            atomicMax(reinterpret_cast<long long*>(p), (long long)x.value);
+        if (commit_ev) ac = mark_listed(*tt, row, 0, lc.rows != nullptr);
+        if (watch_ev) aw = mark_listed(*tt, row, 1, lw.rows != nullptr);
+    } while (false);
+    const uint32_t h = blockIdx.x & (rh::kHeads - 1);
+    if (lc.rows) list_append(lc, ac, t, row, h);   // kernel arguments: uniform branches
+    if (lw.rows) list_append(lw, aw, t, row, h);
 }
 
 // ---- control ops ---------------------------------------------------------------------------------
@@ -319,7 +369,7 @@ __device__ __forceinline__ void table_wave(const TableDev& T, const TableTier& t
             e0[g] = dg && (mn != p0[g] || mj != p1[g] || mx != p2[g]);
             x0[g] = mn, x1[g] = mj, x2[g] = mx;
         } else {
-            int64_t nc;
+            int64_t nc = cin[g];
             e0[g] = dg && rh_eval::commit_decision(v, mj, cin[g], self[g], ts[g], nc);
             e1[g] = dg && wall_on && mn != p0[g];  // watch-ALL level changed (LSI:1025)
             x0[g] = nc, x1[g] = mn, x2[g] = 0;
@@ -402,6 +452,8 @@ __device__ __forceinline__ void table_block_iter(const TableDev& T, const TierRa
     if (threadIdx.x < 2 * kTWaves) (&sc.cnt[0][0])[threadIdx.x] = 0u;
     if (b == 0 && threadIdx.x < rh::kHeads && ev.heads_next)
         ev.heads_next[threadIdx.x * rh::kHeadStride] = 0ull;  // the next evaluation's heads
+    if (b == 0 && threadIdx.x < rh::kTableTiers * rh::kHeads && ev.lheads_next)
+        ev.lheads_next[threadIdx.x * rh::kHeadStride] = 0ull;  // the next list set of this kind
     __syncthreads();   // also: a previous iteration's copy-out is done with `stage`
     if (tl * rh::kTileRows < T.tier[t].rows) table_dispatch<FLO, FHI, FLO <= 6, WATCH>(T, t, tl, wall_on, stage, sc);
     __syncthreads();
@@ -491,6 +543,161 @@ template <bool WATCH>
 __global__ __launch_bounds__(kTBlock) void table_commit_kernel_net(TableDev Targ, TierRange tr, TableEvents ev) {
     (void)Targ;
     table_commit_block<WATCH, 8, 14>(tr, ev);
+}
+
+// ---- list mode: updateCommit / commitIndexChanged over the listed rows only ---------------------
+// One lane per listed row (random rows: each lane loads its row's 8-byte column elements).  The
+// lanes of a wave may hold rows of different tiers (widths): the row evaluation is instantiated per
+// width and the wave runs the widths its lanes hold.  Events: one atomic per wave on the head of
+// its workgroup (blockIdx & 7), records written straight into that head's staging region.
+template <int F, bool WATCH>
+__device__ __forceinline__ void list_row(const TableDev& T, const TableTier& tt, uint32_t r, bool wall_on,
+                                         bool wlisted, bool& e0, bool& e1, bool& wtrans, int64_t& x0, int64_t& x1,
+                                         int64_t& x2, uint32_t& valid, uint32_t& slot) {
+    int64_t vals[F + 1];
+#pragma unroll
+    for (int k = 0; k < F; ++k) vals[k] = *tt.i64(WATCH ? tile::fcommit(F, k) : tile::match(k), r);
+    const uint32_t w = *tt.u32(tile::kConf, r);
+    slot = *tt.u32(tile::kSlot, r);
+    const int64_t cm = *tt.i64(tile::commit(F), r);
+    // the row's commitIndexChanged flag, read with its columns: a listed row is in this list once,
+    // so its lane alone may set the flag here (plain store; no atomic to find the transition)
+    const uint8_t wd = WATCH ? 0 : *tt.u8(tile::kWdirty, r);
+    int64_t self, ts = 0, p0 = 0, p1 = 0, p2 = 0;
+    if (WATCH) {
+        self = cm;  // lastCommittedIndex is the self value (LSI:613)
+        p0 = *tt.i64(tile::wmin(F), r);
+        p1 = *tt.i64(tile::wmaj(F), r);
+        p2 = *tt.i64(tile::wmax(F), r);
+    } else {
+        self = *tt.i64(tile::flush(F), r);
+        ts = *tt.i64(tile::tstart(F), r);
+        if (wall_on) p0 = *tt.i64(tile::wall(F), r);
+    }
+    vals[F] = self;
+    const bool trans = (w & RH_CONF_ACTIVE) && (w & RH_CONF_TRANSITIONAL);   // lane-local: always exact
+    bool v;
+    int64_t mn, mj, mx;
+    rh_eval::eval_group<F, (F <= 6)>(vals, w, WATCH ? -1 : T.gap, trans, v, mn, mj, mx);
+    valid = v ? 1u : 0u;
+    if (WATCH) {
+        e0 = mn != p0 || mj != p1 || mx != p2;
+        x0 = mn, x1 = mj, x2 = mx;
+        if (e0) {
+            *tt.i64(tile::wmin(F), r) = mn;
+            *tt.i64(tile::wmaj(F), r) = mj;
+            *tt.i64(tile::wmax(F), r) = mx;
+        }
+        *tt.u8(tile::kWdirty, r) = 0;
+    } else {
+        int64_t nc;
+        e0 = rh_eval::commit_decision(v, mj, cm, self, ts, nc);
+        e1 = wall_on && mn != p0;  // watch-ALL level changed (LSI:1025)
+        x0 = nc, x1 = mn, x2 = 0;
+        *tt.u8(tile::kDirty, r) = 0;
+        if (e0) {
+            *tt.i64(tile::commit(F), r) = nc;
+            // the commit index changed: commitIndexChanged follows (listed if the flag was clear)
+            *tt.u8(tile::kWdirty, r) = 1;
+            *tt.summary(r, 1) = 1;
+            wtrans = wlisted && wd == 0;
+        }
+        if (e1) *tt.i64(tile::wall(F), r) = mn;
+    }
+}
+
+template <bool WATCH>
+__global__ __launch_bounds__(256) void table_list_kernel(TableDev Targ, TableLists L, TableLists Lw, TableEvents ev) {
+    const TableDev& T = rh::kernarg_struct<TableDev>();
+    (void)Targ;
+    constexpr int NR = rh::kTableTiers * rh::kHeads;
+    __shared__ uint32_t pre[NR + 1];
+    // lanes pick tiers per row: from LDS, not by per-lane loads of the kernarg segment
+    __shared__ __attribute__((aligned(16))) unsigned char tiers_mem[sizeof(TableTier) * rh::kTableTiers];
+    TableTier* tiers = reinterpret_cast<TableTier*>(tiers_mem);
+    static_assert(NR < 64, "one wave scans the region counts");
+    if (threadIdx.x == 64) {
+#pragma unroll
+        for (int k = 0; k < rh::kTableTiers; ++k) tiers[k] = T.tier[k];   // uniform index: scalar loads
+    }
+    if (threadIdx.x < 64) {   // wave 0: inclusive scan of the region counts across its lanes
+        uint32_t c = 0;
+        if (threadIdx.x < NR) {
+            const unsigned long long x = L.heads[(uint64_t)threadIdx.x * rh::kHeadStride];
+            c = (uint32_t)(x < L.cap ? x : L.cap);
+        }
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)c, d);
+            if ((int)threadIdx.x >= d) c += y;
+        }
+        if (threadIdx.x < NR) pre[threadIdx.x + 1] = c;
+        if (threadIdx.x == 0) pre[0] = 0;
+    }
+    if (blockIdx.x == 0 && threadIdx.x < rh::kHeads && ev.heads_next)
+        ev.heads_next[threadIdx.x * rh::kHeadStride] = 0ull;   // the next evaluation's event heads
+    if (blockIdx.x == 0 && threadIdx.x < NR && ev.lheads_next)
+        ev.lheads_next[(uint64_t)threadIdx.x * rh::kHeadStride] = 0ull;   // the next list set of this kind
+    __syncthreads();
+    const uint32_t N = pre[NR];
+    const int lane = threadIdx.x & 63;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const uint32_t h = blockIdx.x & (rh::kHeads - 1);
+    const uint64_t R = ev.region;
+    const bool wall_on = !WATCH && ev.wall != nullptr;
+    // entries are dealt out lane-major over EVERY wave of the grid (entry e -> wave e % W, pass
+    // e / W): a sparse list keeps all CUs' memory pipelines busy instead of filling a few waves
+    const uint32_t W = gridDim.x * (blockDim.x >> 6);
+    const uint32_t wg = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    for (uint32_t pass = 0; (uint64_t)pass * W * 64 < N; ++pass) {
+        const uint32_t e = (pass * 64 + (uint32_t)lane) * W + wg;
+        bool e0 = false, e1 = false, wtrans = false;
+        int64_t x0 = 0, x1 = 0, x2 = 0;
+        uint32_t valid = 0, slot = 0, row = 0;
+        int t = 0;
+        if (e < N) {
+            int rg = 0;   // the region holding entry e: the last r with pre[r] <= e
+#pragma unroll
+            for (int step = 32; step > 0; step >>= 1)
+                if (rg + step <= NR - 1 && pre[rg + step] <= e) rg += step;
+            t = rg / rh::kHeads;
+            row = L.rows[(uint64_t)rg * L.cap + (e - pre[rg])];
+            const TableTier tt = tiers[t];
+            const bool wl = Lw.rows != nullptr;
+            switch (tt.width) {
+                case 2: list_row<2, WATCH>(T, tt, row, wall_on, wl, e0, e1, wtrans, x0, x1, x2, valid, slot); break;
+                case 4: list_row<4, WATCH>(T, tt, row, wall_on, wl, e0, e1, wtrans, x0, x1, x2, valid, slot); break;
+                case 6: list_row<6, WATCH>(T, tt, row, wall_on, wl, e0, e1, wtrans, x0, x1, x2, valid, slot); break;
+                case 8: list_row<8, WATCH>(T, tt, row, wall_on, wl, e0, e1, wtrans, x0, x1, x2, valid, slot); break;
+                case 10: list_row<10, WATCH>(T, tt, row, wall_on, wl, e0, e1, wtrans, x0, x1, x2, valid, slot); break;
+                case 12: list_row<12, WATCH>(T, tt, row, wall_on, wl, e0, e1, wtrans, x0, x1, x2, valid, slot); break;
+                default: list_row<14, WATCH>(T, tt, row, wall_on, wl, e0, e1, wtrans, x0, x1, x2, valid, slot); break;
+            }
+        }
+        // events: one range of the head's region per wave.  Its atomic is issued before the watch
+        // list's, so the two round trips overlap
+        const uint64_t a = __ballot(e0), c = WATCH ? 0ull : __ballot(e1);
+        unsigned long long rb = 0;
+        if (lane == 0 && (a | c))
+            rb = atomicAdd(ev.heads + h * rh::kHeadStride,
+                           (unsigned long long)__popcll(a) | ((unsigned long long)__popcll(c) << 32));
+        if (!WATCH && Lw.rows) list_append(Lw, wtrans, t, row, h);   // kernel argument: uniform
+        if (!(a | c)) continue;
+        const uint32_t b0 = (uint32_t)__shfl((int)(uint32_t)rb, 0), b1 = (uint32_t)__shfl((int)(uint32_t)(rb >> 32), 0);
+        if (e0) {
+            const uint64_t k = b0 + (uint64_t)__popcll(a & lt);
+            if (k < R) {
+                if (WATCH)
+                    ev.watch[h * R + k] = rh_watch_event{slot, valid, x0, x1, x2};
+                else
+                    ev.adv[h * R + k] = rh_index_event{slot, 0u, x0};
+            }
+        }
+        if (!WATCH && e1) {
+            const uint64_t k = b1 + (uint64_t)__popcll(c & lt);
+            if (k < R) ev.wall[h * R + k] = rh_index_event{slot, 0u, x1};
+        }
+    }
 }
 
 // ---- packing the head regions into the contiguous result lists ------------------------------------
@@ -604,10 +811,11 @@ __global__ __launch_bounds__(256) void table_read_kernel(TableDev Targ, uint32_t
 
 }  // namespace
 
-int rh_table_apply_deltas(const rh::TableDev& t, const rh_delta* d_deltas, uint64_t n, int phase, hipStream_t stream) {
+int rh_table_apply_deltas(const rh::TableDev& t, const rh_delta* d_deltas, uint64_t n, int phase,
+                          const rh::TableLists& lc, const rh::TableLists& lw, hipStream_t stream) {
     if (n == 0) return RH_OK;
     const uint64_t blocks = (n + 255) / 256;
-    hipLaunchKernelGGL(table_apply_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream, t, d_deltas, n, phase);
+    hipLaunchKernelGGL(table_apply_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream, t, d_deltas, n, phase, lc, lw);
     RH_HIP(hipGetLastError());
     return RH_OK;
 }
@@ -659,6 +867,18 @@ int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev_i
         RH_HIP(hipGetLastError());
         ev.block_base += blocks;
     }
+    return RH_OK;
+}
+
+int rh_table_commit_lists(const rh::TableDev& t, int mode, const rh::TableLists& l, const rh::TableLists& lw,
+                          const rh::TableEvents& ev, hipStream_t stream) {
+    // a resident-sized grid (one round); the listed rows are strided over it
+    const dim3 g(512), b(256);
+    if (mode == RH_MODE_WATCH)
+        hipLaunchKernelGGL(table_list_kernel<true>, g, b, 0, stream, t, l, rh::TableLists{}, ev);
+    else
+        hipLaunchKernelGGL(table_list_kernel<false>, g, b, 0, stream, t, l, lw, ev);
+    RH_HIP(hipGetLastError());
     return RH_OK;
 }
 

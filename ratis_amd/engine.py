@@ -567,6 +567,40 @@ def read_segments_host(ctx: Context, image, seg_off, seg_len, max_op: int = 4 <<
             "total": int(total.value)}
 
 
+def stamp_host(ctx: Context, buf, frame_off, frame_len) -> None:
+    """``rh_crc32c_stamp_host``: every frame's 4-byte trailer in the HOST buffer ``buf`` (numpy uint8,
+    modified in place) overwritten with the big-endian PureJavaCrc32C of the bytes before it --
+    SegmentedRaftLogOutputStream.write's trailers (OUT:86-110) for a whole flush batch, PCIe
+    included."""
+    import numpy as np
+    lib = _lib.load()
+    assert isinstance(buf, np.ndarray) and buf.dtype == np.uint8 and buf.flags["C_CONTIGUOUS"]
+    off = np.ascontiguousarray(frame_off, dtype=np.uint64)
+    ln = np.ascontiguousarray(frame_len, dtype=np.uint32)
+    vp = ctypes.c_void_p
+    check(lib.rh_crc32c_stamp_host(ctx.handle, vp(buf.ctypes.data), buf.size, vp(off.ctypes.data),
+                                   vp(ln.ctypes.data), off.size))
+
+
+class HostRegistration:
+    """``rh_host_register`` / ``rh_host_unregister`` of a numpy buffer (a context manager)."""
+
+    def __init__(self, ctx: Context, buf):
+        self._ctx, self._buf = ctx, buf
+        check(_lib.load().rh_host_register(ctx.handle, ctypes.c_void_p(buf.ctypes.data), buf.nbytes))
+
+    def close(self) -> None:
+        if self._buf is not None:
+            check(_lib.load().rh_host_unregister(self._ctx.handle, ctypes.c_void_p(self._buf.ctypes.data)))
+            self._buf = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
 class _nullctx:
     def __enter__(self):
         return self

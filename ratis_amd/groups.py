@@ -251,8 +251,14 @@ class RaftGroupTable:
     def last_timing(self) -> Tuple[float, float]:
         """(evaluation ms, gather ms) of the last timed evaluation (``rh_groups_last_timing``)."""
         a, b = ctypes.c_float(), ctypes.c_float()
-        check(self._lib.rh_groups_last_timing(self.handle, ctypes.byref(a), ctypes.byref(b)))
+        check(self._lib.rh_groups_last_timing(self.handle, ctypes.byref(a), ctypes.byref(b), None))
         return float(a.value), float(b.value)
+
+    def last_was_list(self) -> bool:
+        """Whether the last (timed) evaluation ran over the dirty-row lists (list mode)."""
+        a, b, m = ctypes.c_float(), ctypes.c_float(), ctypes.c_int()
+        check(self._lib.rh_groups_last_timing(self.handle, ctypes.byref(a), ctypes.byref(b), ctypes.byref(m)))
+        return bool(m.value)
 
     def watch_async(self) -> None:
         """``rh_watch_levels_async``: commitIndexChanged() of the dirty slots, in flight."""

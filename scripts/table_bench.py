@@ -15,12 +15,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--groups", type=int, default=1_000_000)
     ap.add_argument("--reps", type=int, default=8)
+    ap.add_argument("--fracs", type=str, default="1.0,0.1,0.01")
     a = ap.parse_args()
     import bench
     from ratis_amd import engine, workload
     ctx = engine.Context(0)
     host = workload.commit_snapshot(a.groups, joint_frac=0.10, peers=5, seed=workload.SEED + 1)
-    r = bench.table_commit_leg(ctx, host, reps=a.reps, fracs=(1.0, 0.1, 0.01))
+    r = bench.table_commit_leg(ctx, host, reps=a.reps, fracs=tuple(float(x) for x in a.fracs.split(",")))
     print(json.dumps({"lib": os.environ.get("RATIS_HIP_LIB", "default"), "table_commit": r}))
 
 

@@ -200,3 +200,56 @@ def test_node_watch_levels_and_lease_over_four_shards(ctx, orc):
         assert node.watch_levels(4 * cap).size == 0       # nothing changed since
         bits = node.lease_batch(1 << 40, 100)             # no lease started: no division has one
         assert bits.shape == (4 * cap,) and not bits.any()
+
+
+@pytest.mark.parametrize("seed", [3, 4])
+def test_list_and_tile_evaluations_interleaved(ctx, orc, seed):
+    """Sparse pushes run over the dirty-row lists (list mode), dense ones over every tile: steps of
+    either kind, follower-commit-only steps (commitIndexChanged from the watch list), control ops
+    (which give the lists up until the next evaluation) and the zero-copy ring, all against the
+    model -- and both modes must actually run."""
+    from ratis_amd import groups
+    rng = np.random.default_rng(seed)
+    n = 50_000
+    model = TableModel(n)
+    tab, n = _loaded(ctx, model, n, seed=seed + 10)
+    modes = {"commit": set(), "watch": set()}
+    try:
+        tab.set_timing(True)
+        compare(tab, model, orc, columns=False)
+        live = np.arange(n)
+        for step in range(14):
+            k = int(rng.choice([3, 40, 700, 1500, 20_000, 120_000]))
+            if step % 5 == 4:   # follower commitIndex reports only
+                s = rng.choice(live, size=min(k, 2000))
+                col = 16 + rng.integers(0, 4, s.size)
+                d = groups.make_deltas(s, col, model.commit[s] - rng.integers(0, 3, s.size))
+            else:
+                d = random_deltas(rng, model, live, k, fcommit=step % 2 == 0)
+            if step == 7:       # a control op between pushes: lists given up, tiles evaluated
+                w = conf_word(0b1111)
+                tab.start(5, w, 10_000, 9_000, 8_000)
+                model.start(5, w, 10_000, 9_000, 8_000)
+            if step % 3 == 2:
+                ring = tab.acquire_deltas()
+                ring[: d.size] = d
+                tab.submit_deltas(d.size)
+            else:
+                tab.push(d)
+            model.apply(d)
+            got = tab.update_commit()
+            modes["commit"].add(tab.last_was_list())
+            a_s, a_c, w_s, w_m = model.commit_batch(orc)
+            assert np.array_equal(got.advanced_slots, a_s) and np.array_equal(got.advanced_commit, a_c), step
+            assert np.array_equal(got.watch_all_slots, w_s) and np.array_equal(got.watch_all_min, w_m), step
+            ev = tab.commit_index_changed()
+            modes["watch"].add(tab.last_was_list())
+            m_s, m_lev, m_valid = model.watch(orc)
+            assert np.array_equal(ev["slot"].astype(np.int64), m_s), step
+            assert np.array_equal(ev["min"], m_lev[0]) and np.array_equal(ev["majority"], m_lev[1]), step
+            assert np.array_equal(ev["max"], m_lev[2]) and np.array_equal(ev["valid"].astype(bool), m_valid), step
+        assert modes["commit"] == {True, False} and modes["watch"] == {True, False}, modes
+        for col in [0, 1, 16, 32, 33]:
+            assert np.array_equal(tab.read(col), model.column(col)), col
+    finally:
+        tab.close()

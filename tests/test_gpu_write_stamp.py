@@ -1,0 +1,73 @@
+"""GPU parity of the write side over host buffers (rh_crc32c_stamp_host): a flush batch of frames
+written with placeholder trailers, stamped in one call, must equal byte for byte what the oracle's
+writer (orc_frame_write = SegmentedRaftLogOutputStream.write, OUT:86-110: varint32(n) || entry ||
+big-endian PureJavaCrc32C) produces for the same entries -- at the flush sizes the bench compares
+(64 KiB, 1 MiB, 8 MiB = raft.server.log.write.buffer.size's default), from pageable and from
+registered (page-locked) memory, with frames at any offset of the buffer and the bytes around them
+untouched; malformed tables stamp nothing."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _flush_batch(orc, rng, nbytes, lo=1, hi=2040, lead=0):
+    """Entries of random sizes framed by the oracle writer until ~nbytes; returns (expected image,
+    placeholder image with zero trailers, frame offsets, frame lengths)."""
+    parts, off, ln = [], [], []
+    pos = lead
+    while pos < nbytes:
+        proto = rng.integers(0, 256, int(rng.integers(lo, hi + 1)), dtype=np.uint8).tobytes()
+        fr = orc.frame_write(proto)
+        off.append(pos)
+        ln.append(len(fr))
+        parts.append(np.frombuffer(fr, dtype=np.uint8))
+        pos += len(fr)
+    want = np.concatenate([rng.integers(0, 256, lead, dtype=np.uint8)] + parts + [rng.integers(0, 256, 37, dtype=np.uint8)])
+    buf = want.copy()
+    off = np.array(off, dtype=np.uint64)
+    ln = np.array(ln, dtype=np.uint32)
+    for o, l in zip(off, ln):
+        buf[int(o) + int(l) - 4: int(o) + int(l)] = 0
+    return want, buf, off, ln
+
+
+@pytest.mark.parametrize("nbytes", [64 << 10, 1 << 20, 8 << 20])
+def test_stamped_flush_batch_equals_oracle_writer(ctx, orc, nbytes):
+    from ratis_amd import engine
+    rng = np.random.default_rng(nbytes)
+    want, buf, off, ln = _flush_batch(orc, rng, nbytes, lead=int(rng.integers(0, 300)))
+    engine.stamp_host(ctx, buf, off, ln)
+    assert np.array_equal(buf, want)
+    # the same from page-locked memory (the worker's write buffer is registered once)
+    want2, buf2, off2, ln2 = _flush_batch(orc, rng, nbytes, lo=100, hi=4000)
+    with engine.HostRegistration(ctx, buf2):
+        engine.stamp_host(ctx, buf2, off2, ln2)
+    assert np.array_equal(buf2, want2)
+
+
+def test_stamp_edge_frames_and_errors(ctx, orc):
+    from ratis_amd import _lib, engine
+    rng = np.random.default_rng(5)
+    # an empty entry (5-byte frame), 1-byte entries, a multi-byte varint (>= 128 B) entry, a 300 KiB entry
+    protos = [b"", b"\x01", bytes(range(200)), rng.integers(0, 256, 300 << 10, dtype=np.uint8).tobytes(), b"\x07" * 127]
+    frames = [orc.frame_write(p) for p in protos]
+    want = np.frombuffer(b"".join(frames), dtype=np.uint8).copy()
+    off = np.cumsum([0] + [len(f) for f in frames[:-1]]).astype(np.uint64)
+    ln = np.array([len(f) for f in frames], dtype=np.uint32)
+    buf = want.copy()
+    for o, l in zip(off, ln):
+        buf[int(o) + int(l) - 4: int(o) + int(l)] = 0xAB
+    engine.stamp_host(ctx, buf, off, ln)
+    assert np.array_equal(buf, want)
+    engine.stamp_host(ctx, buf, off[:0], ln[:0])            # no frames: nothing to do
+    before = buf.copy()
+    buf[int(off[1]) + int(ln[1]) - 4] ^= 0xFF
+    spoiled = buf.copy()
+    with pytest.raises(_lib.IllegalArgumentError):           # a frame past the buffer end: nothing stamped
+        engine.stamp_host(ctx, buf, np.append(off, buf.size - 2), np.append(ln, 8))
+    assert np.array_equal(buf, spoiled)
+    with pytest.raises(_lib.IllegalArgumentError):           # shorter than its trailer
+        engine.stamp_host(ctx, buf, off[:1], np.array([3], dtype=np.uint32))
+    engine.stamp_host(ctx, buf, off, ln)
+    assert np.array_equal(buf, before)

@@ -265,3 +265,37 @@ def test_bulk_load_streams_batches_with_two_images():
     assert "MAX_FRAMES_PER_BATCH" in _method_body(reader, "public Plan(List<File> files, int framesPerFile)")
     # one context per GPU of the mask, batches spread round robin
     assert "RatisHip.ctxCreate0(d)" in reader and "Math.floorMod(ctxIndex, ctx.length)" in reader
+
+
+def test_writer_seam_stamps_flush_batches():
+    """The write side (north_star: the PureJavaCrc32C/Checksum call sites): in
+    HIP checksum mode SegmentedRaftLogOutputStream.write (OUT:86-110) leaves a placeholder trailer
+    and records the frame; BufferedWriteChannel.flushBuffer stamps every pending trailer just before
+    the buffer goes to the file -- on the GPU from the measured crossover (bench.py write_stamp leg,
+    HipFrameStamper.DEFAULT_MIN_GPU_BYTES, the config key's default), else PureJavaCrc32C per frame;
+    the worker registers its write buffer once and unregisters it before freeing it."""
+    if not os.path.isdir(REFERENCE):
+        pytest.skip("reference tree not present")
+    chan = _patched_java("segmented/BufferedWriteChannel.java")
+    flush = _method_body(chan, "private void flushBuffer()")
+    assert flush.index("beforeFlush.accept(writeBuffer)") < flush.index("writeBuffer.flip()")
+    outs = _patched_java("segmented/SegmentedRaftLogOutputStream.java")
+    write = _method_body(outs, "public void write(LogEntryProto entry)")
+    i = write.index("if (stamper != null)")
+    assert "buf.putInt(0);" in write[i:] and "stamper.add(pos, total);" in write[i:]
+    assert "checksum.update(duplicated);" in write   # the reference path stays for JAVA mode
+    assert "out.setBeforeFlush(buf -> stamper.stamp(buf, frame -> {" in outs
+    worker = _patched_java("segmented/SegmentedRaftLogWorker.java")
+    assert "this.hipStamper = newHipStamper(properties, writeBuffer);" in worker
+    assert "preallocatedSize, writeBuffer, hipStamper);" in worker
+    close = _method_body(worker, "void close()")
+    assert close.index("IOUtils.cleanup(LOG, hipStamper)") < close.index("PlatformDependent.freeDirectBuffer(writeBuffer)")
+    keys = _patched_java("server/RaftServerConfigKeys.java")
+    assert 'CHECKSUM_GPU_MIN_BYTES_DEFAULT = SizeInBytes.valueOf("256KB")' in keys
+    stamper = open(os.path.join(JAVA, "java", "org", "apache", "ratis", "hip", "HipFrameStamper.java")).read()
+    assert "DEFAULT_MIN_GPU_BYTES = 256 << 10" in stamper
+    st = _method_body(stamper, "public boolean stamp(ByteBuffer buf, FrameChecksum cpu)")
+    assert "bytes >= minGpuBytes" in st and "gpu.stampFrames(buf, buf.position(), off, len, n)" in st
+    assert "cpu.crc(d)" in st
+    jni = open(JNI_C).read()
+    assert "rh_crc32c_stamp_host(C(ctx)" in jni and "rh_host_register(C(ctx)" in jni
