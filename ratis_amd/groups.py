@@ -417,6 +417,7 @@ class LeaderPump:
         self._pending = []
         self.lease_timeout_ms = lease_timeout_ms
         self.lease_bits = None
+        self.fallbacks = {}   # reason -> divisions that left the table (HipLeaderBookkeeper.getFallbackCount)
 
     def register(self, node_slot: int, callback) -> None:
         self.callbacks[int(node_slot)] = callback
@@ -424,10 +425,19 @@ class LeaderPump:
     def emit(self, deltas: np.ndarray) -> None:
         self._pending.append(np.ascontiguousarray(deltas, dtype=DELTA_DTYPE))
 
-    def tick(self, now_nanos: int = 0) -> dict:
+    def drain(self) -> None:
+        """Pushes the buffered deltas now (HipLeaderBookkeeper.drainDeltas, before a control call)."""
         if self._pending:
             self.node.push(np.concatenate(self._pending))
             self._pending = []
+
+    def division(self, node_slot: int, callback) -> "PumpDivision":
+        d = PumpDivision(self, int(node_slot), callback)
+        self.register(node_slot, callback)
+        return d
+
+    def tick(self, now_nanos: int = 0) -> dict:
+        self.drain()
         cap = self.node.capacity_per_shard
         lease = self.lease_timeout_ms >= 0
         tickets = []
@@ -461,3 +471,101 @@ class LeaderPump:
                 bits.append(t.lease_wait())
         self.lease_bits = np.concatenate(bits) if lease else None
         return n
+
+
+class PumpDivision:
+    """Python twin of HipLeaderBookkeeper.Division: the division's follower slots (addFollower,
+    first free slot of 14), its membership word, its control calls and producers, and FALLBACK --
+    a 15th follower (or a control call the library rejects) makes the division leave the table:
+    its slot is stopped, later deltas are dropped, no event reaches it, the pump counts it and
+    ``callback.on_fallback()`` runs (the reference's own per-division path from then on)."""
+
+    MAX_FOLLOWERS = 14
+
+    def __init__(self, pump: LeaderPump, node_slot: int, callback):
+        self.pump, self.node_slot, self.callback = pump, node_slot, callback
+        self.follower_slot = {}
+        self.started = False
+        self.fallback = False
+        self.width = 0
+
+    def fall_back(self, reason: str) -> None:
+        if self.fallback:
+            return
+        self.fallback = True
+        if self.started:
+            self.started = False
+            self.pump.drain()
+            self.pump.node.stop(self.node_slot)
+        self.pump.callbacks.pop(self.node_slot, None)
+        self.pump.fallbacks[reason] = self.pump.fallbacks.get(reason, 0) + 1
+        if hasattr(self.callback, "on_fallback"):
+            self.callback.on_fallback()
+
+    def _emit(self, follower: int, column: int, op: int, value: int) -> None:
+        if not self.started or self.fallback or follower >= self.width:
+            return
+        self.pump.emit(make_deltas([self.node_slot], [column], [value], op))
+
+    def add_follower(self, peer) -> int:
+        if self.fallback:
+            return -1
+        if peer in self.follower_slot:
+            return self.follower_slot[peer]
+        used = set(self.follower_slot.values())
+        for k in range(self.MAX_FOLLOWERS):
+            if k not in used:
+                self.follower_slot[peer] = k
+                self._emit(k, _lib.rh_col_match(k), _lib.RH_OP_SET, -1)
+                self._emit(k, _lib.rh_col_fcommit(k), _lib.RH_OP_SET, -1)
+                return k
+        self.fall_back("FOLLOWER_SLOTS")
+        return -1
+
+    def remove_follower(self, peer) -> None:
+        self.follower_slot.pop(peer, None)
+
+    def conf_word(self, conf, old=None, self_in_conf=True, self_in_old=True) -> int:
+        n = sum(1 << self.follower_slot[p] for p in conf if p in self.follower_slot)
+        o = sum(1 << self.follower_slot[p] for p in (old or ()) if p in self.follower_slot)
+        return _lib.conf_pack(n, self_in_conf, old is not None, o, old is not None and self_in_old, True)
+
+    @staticmethod
+    def _width(conf: int) -> int:
+        m = (conf & 0x3FFF) | ((conf >> 16) & 0x3FFF)
+        w = m.bit_length()
+        return 2 if w <= 2 else 2 * ((w + 1) // 2)
+
+    def start(self, conf: int, flush: int, commit: int, term_start: int) -> None:
+        if self.fallback:
+            return
+        self.pump.drain()
+        try:
+            self.pump.node.start(self.node_slot, conf, flush, commit, term_start)
+        except _lib.RatisHipError:
+            self.fall_back("REJECTED")
+            return
+        self.width = self._width(conf)
+        self.started = True
+
+    def reconf(self, conf: int) -> None:
+        if not self.started or self.fallback:
+            return
+        self.pump.drain()
+        try:
+            self.pump.node.reconf(self.node_slot, conf)
+        except _lib.RatisHipError:
+            self.fall_back("REJECTED")
+            return
+        self.width = self._width(conf)
+
+    def match_index(self, k: int, v: int) -> None:
+        if k >= 0:
+            self._emit(k, _lib.rh_col_match(k), _lib.RH_OP_MAX, v)
+
+    def follower_commit_index(self, k: int, v: int) -> None:
+        if k >= 0:
+            self._emit(k, _lib.rh_col_fcommit(k), _lib.RH_OP_MAX, v)
+
+    def flush_index(self, v: int) -> None:
+        self._emit(-1, _lib.RH_COL_FLUSH, _lib.RH_OP_MAX, v)

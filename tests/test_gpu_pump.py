@@ -96,3 +96,74 @@ def test_pump_replica_follower_commit_only_step(ctx, orc):
         # and a quiet tick reports nothing
         got = step(groups.make_deltas(np.zeros(0, np.int64), 0, 0))
         assert got == {"commit": 0, "watch_all": 0, "watch_levels": 0}
+
+
+def test_pump_replica_fallback_at_fifteen_followers(ctx, orc):
+    """HipLeaderBookkeeper's FALLBACK in the pump replica: a division reconfigured to a joint
+    change of two 8-peer confs needs 15 follower slots; its 15th addFollower makes it leave the
+    table (slot stopped, counted, on_fallback called), after which its deltas are dropped and no
+    event reaches it -- while a 6-follower division on the same node keeps exact parity with the
+    model, tick after tick."""
+    from ratis_amd import groups
+    rng = np.random.default_rng(15)
+    cap = 64
+    with groups.RaftNode(0, cap, devices=[0, 0]) as node:
+        pump = groups.LeaderPump(node)
+        model = TableModel(2 * cap)
+        fell = []
+
+        class Cb(Division):
+            def on_fallback(self):
+                fell.append(True)
+
+        a_cb, b_cb = Division(0), Cb(0)
+        a = pump.division(3, a_cb)                 # shard 0
+        b = pump.division(cap + 5, b_cb)           # shard 1
+        a_peers = [f"a{i}" for i in range(6)]
+        b_old = [f"b{i}" for i in range(8)]
+        b_new = ["b0"] + [f"c{i}" for i in range(7)]   # union with b_old: 15 followers
+        for p in a_peers:
+            a.add_follower(p)
+        for p in b_old:
+            b.add_follower(p)
+        wa, wb = a.conf_word(a_peers), b.conf_word(b_old)
+        a.start(wa, 10_000, 9_000, 9_500)
+        b.start(wb, 20_000, 19_000, 19_500)
+        model.start(3, wa, 10_000, 9_000, 9_500)
+        model.start(cap + 5, wb, 20_000, 19_000, 19_500)
+        assert node.tables[0].tier_width(3) == 6 and node.tables[1].tier_width(5) == 8
+
+        def step(deltas_a, deltas_b):
+            for k, v in deltas_a:
+                a.match_index(k, v)
+            for k, v in deltas_b:
+                b.match_index(k, v)
+            for k, v in deltas_a:
+                model.apply(groups.make_deltas([3], [k], [v]))
+            if not b.fallback:
+                for k, v in deltas_b:
+                    model.apply(groups.make_deltas([cap + 5], [k], [v]))
+            before_b = b_cb.commit
+            got = pump.tick()
+            a_s, a_c, _, _ = model.commit_batch(orc)
+            model.watch(orc)
+            if 3 in a_s.tolist():
+                assert a_cb.commit == int(a_c[a_s.tolist().index(3)])
+            return got, before_b
+
+        step([(k, 10_000 + 50 * k) for k in range(6)], [(k, 20_000 + 10 * k) for k in range(8)])
+        assert a_cb.commit > 9_000 and b_cb.commit > 19_000
+        # the joint change: new peers get slots 8..13, the 15th peer has none -> fallback
+        slots = [b.add_follower(p) for p in b_new]
+        assert slots == [0] + list(range(8, 14)) + [-1]
+        assert b.fallback and fell == [True] and pump.fallbacks == {"FOLLOWER_SLOTS": 1}
+        assert node.tables[1].tier_width(5) == 0           # the slot left the table
+        b.reconf(b.conf_word(b_new, b_old))                # ignored: the division runs in Java now
+        model.stop(cap + 5)
+        a.flush_index(20_000)                              # the leader's log grows: commits can move on
+        model.apply(groups.make_deltas([3], [COL_FLUSH], [20_000]))
+        for t in range(4):
+            _, before_b = step([(k, 10_500 + 100 * t + int(rng.integers(0, 90))) for k in range(6)],
+                               [(k, 30_000 + t) for k in range(8)])
+            assert b_cb.commit == before_b                 # no event reaches the fallen-back division
+        assert a_cb.commit >= 10_500

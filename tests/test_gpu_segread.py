@@ -277,3 +277,43 @@ def test_host_image_read_path_matches_reader(ctx, orc, big):
         elif rst == _lib.RH_SEG_E_CHECKSUM and len(ro) < 2:
             assert r2["status"][s] == _lib.RH_SEG_E_CHECKSUM, s
     assert n_cap > 0
+
+
+def test_fused_ragged_bench_scale_against_oracle(ctx, orc):
+    """The ragged read path at the bench's own scale per segment (32 x 32 MiB = 1 GiB, 64-2048 B
+    frames, corruptions planted at the bench's rate), checked against the oracle -- not only against
+    the generator's self-stamped trailers: every segment's verdict, stop offset and accepted frame
+    table against the literal reader (orc_segment_scan), every frame's CRC recomputed from the bytes
+    by the oracle (16 host threads), and the mismatch set against the oracle's own stored-vs-computed
+    comparison AND the planted set."""
+    import torch
+
+    from ratis_amd import engine, workload
+    rs = workload.synth_ragged_segments(ctx, 32, segment_size=32 << 20, min_frame=64, max_frame=2048,
+                                        seed=workload.SEED + 4242, corrupt_rate=1e-5)
+    n, size = rs.n_segments, rs.segment_size
+    cap = int(rs.seg_nframes.max()) + 16
+    b = engine.SegmentBatch(buf=rs.batch.buf, seg_off=torch.arange(n, device="cuda", dtype=torch.int64) * size,
+                            seg_len=torch.full((n,), size, device="cuda", dtype=torch.int64), frames_per_seg_cap=cap)
+    out = engine.read_segments_fused(ctx, b)
+    torch.cuda.synchronize()
+    total = int(b.total_frames.item())
+    assert total == int(rs.seg_nframes.sum()) > 500_000
+    buf = rs.batch.buf.cpu().numpy()
+    fo = b.frame_off[:total].cpu().numpy().astype(np.uint64)
+    fl = b.frame_len[:total].cpu().numpy().astype(np.uint32)
+    first = b.seg_first[:n].cpu().numpy()
+    n_ok, st, stop = out["n_ok"].cpu().numpy(), out["status"].cpu().numpy(), out["stop"].cpu().numpy()
+    for s in range(n):
+        seg = buf[s * size: (s + 1) * size]
+        ro, rl, rc, rst, rstop = orc.segment_scan(seg, cap=cap)
+        assert (st[s], stop[s], n_ok[s]) == (rst, rstop, len(ro)), s
+        k = len(ro)
+        assert np.array_equal(fo[first[s]: first[s] + k].astype(np.int64) - s * size, ro), s
+        assert np.array_equal(fl[first[s]: first[s] + k], rl), s
+    crc, bad_ref = orc.crc32c_frames_all(buf, fo, fl, threads=16)
+    assert np.array_equal(out["crc_out"][:total].cpu().numpy().view(np.uint32), crc)
+    bad = _bits(out["bad_bits"].cpu().numpy(), total)
+    assert np.array_equal(bad, bad_ref)
+    assert np.array_equal(np.nonzero(bad)[0], rs.corrupted) and rs.corrupted.size > 0
+    assert int(out["n_bad"].item()) == int(bad.sum())
