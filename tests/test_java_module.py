@@ -299,3 +299,25 @@ def test_writer_seam_stamps_flush_batches():
     assert "cpu.crc(d)" in st
     jni = open(JNI_C).read()
     assert "rh_crc32c_stamp_host(C(ctx)" in jni and "rh_host_register(C(ctx)" in jni
+
+
+def test_cache_miss_reload_reads_through_the_gpu():
+    """Missing item #3 of round 3: a cache miss (LogSegment.LogEntryLoader.load, LogSegment.java:
+    265-293) re-reads its segment file. In HIP checksum mode the cache hands every segment it adds
+    (addSegment, setOpenSegment) the device mask, and the loader reads the file through
+    HipLogReader (framing + every entry's CRC on the GPU) and decodes it with readSegmentFileHip;
+    a GPU failure falls back to the reference's readSegmentFile, never fails the read."""
+    if not os.path.isdir(REFERENCE):
+        pytest.skip("reference tree not present")
+    seg = _patched_java("segmented/LogSegment.java")
+    load = _method_body(seg, "public LogEntryProto load(LogRecord key)")
+    i = load.index("hipDeviceMask != 0 ? hipReload(file, startEnd) : null")
+    assert load.index("readSegmentFileHip(file, startEnd, getLogCorruptionPolicy(), verified, reload)") > i
+    assert "readSegmentFile(file, startEnd, maxOpSize, getLogCorruptionPolicy(), raftLogMetrics, reload)" in load
+    rl = _method_body(seg, "private HipLogReader.Segment hipReload(File file, LogSegmentStartEnd startEnd)")
+    assert "HipLogReader.get(hipDeviceMask).read(Collections.singletonList(file)" in rl
+    assert "HipLogReader.MAX_FRAMES_PER_BATCH" in rl and "return null;" in rl
+    cache = _patched_java("segmented/SegmentedRaftLogCache.java")
+    assert "RaftServerConfigKeys.Hip.checksumBackend(properties) == RaftServerConfigKeys.Hip.Backend.HIP" in cache
+    for m in ("void addSegment(LogSegment segment)", "private void setOpenSegment(LogSegment openSegment)"):
+        assert "setHipDeviceMask(hipDeviceMask);" in _method_body(cache, m), m
