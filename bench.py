@@ -369,12 +369,14 @@ def table_commit_leg(ctx, host, reps: int = 8, fracs=(1.0, 0.1, 0.01), pmc=None)
     """The kernel the Java module drives: rh_commit_batch over the resident table (config-3
     groups, stable F=4 and joint F=6 tiers, 128-row tiled layout), after deltas marked `frac` of the
     groups dirty (one matchIndex / flushIndex update per dirty group, as delta_streaming's steps).
-    One evaluation = the evaluation kernel (records staged in HBM per XCD head) + the gather kernel
-    that packs them into the result lists; the library's timing events (rh_groups_timing) time the
-    two on the table's own stream, HIP events around rh_commit_batch_async the pair.  Both sinks:
-    RH_EVENTS_HOST_MAPPED (the default, what the Java module runs: the gather writes the lists into
-    pinned host memory) and RH_EVENTS_DEVICE (the gather packs into HBM, _wait copies the prefix).
-    `roofline` = the evaluation kernel.  The two tables' events must be identical."""
+    One evaluation = one kernel that evaluates the dirty rows and writes its event records straight
+    into the result lists (the tile kernel over every 128-row tile, or the list kernel over the
+    dirty-row lists when few rows can be dirty); the library's timing events (rh_groups_timing) time
+    it on the table's own stream, HIP events around rh_commit_batch_async the call.  Every sink:
+    RH_EVENTS_HOST_MAPPED (the lists are pinned host memory, written across PCIe), RH_EVENTS_DEVICE
+    (the lists in HBM, _wait copies the counted prefix) and RH_EVENTS_AUTO (the default, what the
+    Java module and rh_node run: DEVICE for tile evaluations, HOST_MAPPED for list evaluations).
+    `roofline` = AUTO's evaluation, events included.  The tables' events must be identical."""
     import torch
 
     from ratis_amd import _lib, groups
@@ -384,7 +386,7 @@ def table_commit_leg(ctx, host, reps: int = 8, fracs=(1.0, 0.1, 0.01), pmc=None)
     F = [h.follower.shape[0] for h in host]
     stream = torch.cuda.ExternalStream(lib.rh_ctx_stream(ctx.handle))
     tabs = {}
-    for sink in (_lib.RH_EVENTS_HOST_MAPPED, _lib.RH_EVENTS_DEVICE):
+    for sink in (_lib.RH_EVENTS_HOST_MAPPED, _lib.RH_EVENTS_DEVICE, _lib.RH_EVENTS_AUTO):
         tab = groups.RaftGroupTable(ctx, capacity=n_all)
         first = 0
         for h in host:
@@ -397,7 +399,7 @@ def table_commit_leg(ctx, host, reps: int = 8, fracs=(1.0, 0.1, 0.01), pmc=None)
     cur_f = np.concatenate([h.follower[:4] for h in host], axis=1)   # followers 0..3 exist in both tiers
     cur_s = np.concatenate([h.flush for h in host])
     out = {}
-    names = {_lib.RH_EVENTS_HOST_MAPPED: "host_mapped", _lib.RH_EVENTS_DEVICE: "device"}
+    names = {_lib.RH_EVENTS_HOST_MAPPED: "host_mapped", _lib.RH_EVENTS_DEVICE: "device", _lib.RH_EVENTS_AUTO: "auto"}
     for frac in fracs:
         k = n_all if frac >= 1.0 else int(n_all * frac)
         res = {}
@@ -420,18 +422,18 @@ def table_commit_leg(ctx, host, reps: int = 8, fracs=(1.0, 0.1, 0.01), pmc=None)
                 got[sink] = tab.commit_wait(tk)
                 torch.cuda.synchronize()
                 if r:   # the first round is a warm-up
-                    ev_ms, ga_ms = tab.last_timing()
-                    res.setdefault((sink, "pair"), []).append(e0.elapsed_time(e1))
-                    res.setdefault((sink, "eval"), []).append(ev_ms)
-                    res.setdefault((sink, "gather"), []).append(ga_ms)
-            a, b = got[_lib.RH_EVENTS_DEVICE], got[_lib.RH_EVENTS_HOST_MAPPED]
-            ok = (np.array_equal(a.advanced_slots, b.advanced_slots) and np.array_equal(a.advanced_commit, b.advanced_commit)
-                  and np.array_equal(a.watch_all_slots, b.watch_all_slots) and np.array_equal(a.watch_all_min, b.watch_all_min))
+                    res.setdefault((sink, "call"), []).append(e0.elapsed_time(e1))
+                    res.setdefault((sink, "eval"), []).append(tab.last_timing())
+                    res.setdefault((sink, "list"), []).append(tab.last_was_list())
+            a = got[_lib.RH_EVENTS_DEVICE]
+            ok = all(np.array_equal(a.advanced_slots, b.advanced_slots) and np.array_equal(a.advanced_commit, b.advanced_commit)
+                     and np.array_equal(a.watch_all_slots, b.watch_all_slots) and np.array_equal(a.watch_all_min, b.watch_all_min)
+                     for b in got.values())
             res["sinks_agree"] = res.get("sinks_agree", True) and bool(ok)
             res["advanced"] = int(a.advanced_slots.size)
             res["watch_all"] = int(a.watch_all_slots.size)
         med = {key: float(np.median(v)) for key, v in res.items() if isinstance(key, tuple)}
-        eval_ms = float(np.median(res[(_lib.RH_EVENTS_HOST_MAPPED, "eval")] + res[(_lib.RH_EVENTS_DEVICE, "eval")]))
+        eval_ms = float(np.median(res[(_lib.RH_EVENTS_AUTO, "eval")]))   # the module's sink
         # algorithmic bytes: 1 dirty byte per row; per dirty row its columns (F matchIndex, conf,
         # row slot, commit, flush, term start, previous watch-ALL level) and the flag clear; per
         # event 16 B of record (+ 8 B commit / watch level and 1 B watch-dirty flag stored)
@@ -440,15 +442,18 @@ def table_commit_leg(ctx, host, reps: int = 8, fracs=(1.0, 0.1, 0.01), pmc=None)
         per_dirty = 8 * f_mean + 4 + 4 + 8 + 8 + 8 + 8 + 1
         alg = n_all * 1 + k * per_dirty + res["advanced"] * (16 + 8 + 1) + res["watch_all"] * (16 + 8)
         ach = alg / (eval_ms * 1e-3) / 1e9
+        list_mode = bool(np.all(res[(_lib.RH_EVENTS_AUTO, "list")]))
         case = {"dirty_groups": k, "advanced": res["advanced"], "watch_all_changed": res["watch_all"],
-                "ms_evaluation_kernel": round(eval_ms, 4),
+                "ms_evaluation": round(eval_ms, 4), "list_mode": list_mode,
                 "sinks_agree": res["sinks_agree"]}
         for sink, nm in names.items():
-            case[nm] = {"ms_evaluation": round(med[(sink, "eval")], 4), "ms_gather": round(med[(sink, "gather")], 4),
-                        "ms_evaluation_and_gather_hip_events": round(med[(sink, "pair")], 4)}
+            case[nm] = {"ms_evaluation": round(med[(sink, "eval")], 4),
+                        "ms_commit_batch_async_hip_events": round(med[(sink, "call")], 4)}
         case["roofline"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                             "frac": round(ach / HBM_PEAK_GBPS, 4), "algorithmic_bytes_per_launch": int(alg),
-                            "kernel": "table_commit_kernel_rank<false> (records staged in HBM per XCD head)",
+                            "kernel": ("table_list_kernel<false>" if list_mode else "table_commit_kernel_rank<false>")
+                            + (" (RH_EVENTS_AUTO: records into the pinned lists)" if list_mode
+                               else " (RH_EVENTS_AUTO: records into the HBM lists)"),
                             # PMC passes (scripts/prof_kernels.py table case) run the all-dirty step
                             "traffic": (round(pmc["table_bytes_per_unit"] * n_all)
                                         if frac >= 1.0 and pmc and "table_bytes_per_unit" in pmc else None),
@@ -458,7 +463,7 @@ def table_commit_leg(ctx, host, reps: int = 8, fracs=(1.0, 0.1, 0.01), pmc=None)
         tab.close()
     out["workload"] = (f"resident table of {n_all} config-3 groups (F=4 and F=6 tiers); deltas mark the dirty "
                        "fraction, then one rh_commit_batch (RH_COMMIT_WATCH_ALL) per step; median of "
-                       f"{reps} steps per case; host_mapped is the sink the Java module runs")
+                       f"{reps} steps per case; auto is the sink the Java module runs")
     return out
 
 

@@ -274,24 +274,26 @@ int rh_commit_batch(rh_groups* g, uint32_t flags, rh_commit_out* out);
  * after it). */
 int rh_commit_batch_async(rh_groups* g, uint32_t flags, uint64_t* ticket);
 int rh_commit_batch_wait(rh_groups* g, uint64_t ticket, rh_commit_out* out);
-/* Where the result lists are assembled.  Both sinks run the same evaluation kernel, which stages its
- * records in HBM (one region per XCD head) and never writes across PCIe; a gather kernel then packs
- * the regions into contiguous lists.  HOST_MAPPED (the default): the gather writes the lists straight
- * into the pinned result buffers (PCIe writes by the GPU), visible when the ticket completes.
- * DEVICE: the gather packs into HBM and rh_commit_batch_wait / rh_watch_levels_wait copy the counted
- * prefix into the same pinned buffers (a D2H on the table's copy stream).  Results are identical.
- * Not while an evaluation is outstanding (RH_E_STATE); DEVICE allocates 112 B x capacity of HBM on
- * first use. */
+/* Where the result lists are assembled.  Every sink runs the same evaluation kernels, which write
+ * their records straight into contiguous lists (one range per workgroup) and the list lengths into
+ * pinned memory.  HOST_MAPPED: the lists are the pinned result buffers themselves (PCIe writes by
+ * the GPU), visible when the ticket completes.  DEVICE: the lists are in HBM (112 B x capacity) and
+ * rh_commit_batch_wait / rh_watch_levels_wait copy the counted prefix into the same pinned buffers
+ * (a D2H on the table's copy stream).  AUTO (the default): per evaluation, DEVICE when it visits
+ * every tile (up to one record per row: the kernel writes at HBM speed and the copy engine moves
+ * the lists) and HOST_MAPPED when it runs over the dirty-row lists (few records: no copy).  Results
+ * are identical.  Not while an evaluation is outstanding (RH_E_STATE). */
 #define RH_EVENTS_HOST_MAPPED 0
 #define RH_EVENTS_DEVICE      1
+#define RH_EVENTS_AUTO        2
 int rh_groups_set_event_sink(rh_groups* g, int sink);
 /* Diagnostics (benchmarks, tests): with timing enabled every evaluation records HIP events around
- * its evaluation kernel(s) and around the gather; rh_groups_last_timing returns the last
- * evaluation's two device times in ms (blocks until it has completed; RH_E_STATE before any timed
- * evaluation) and, if list_evaluated is not NULL, whether it ran over the dirty-row lists (1: only
- * the rows marked since the previous evaluation of its kind were visited; 0: every tile). */
+ * its evaluation kernel(s); rh_groups_last_timing returns the last evaluation's device time in ms
+ * (blocks until it has completed; RH_E_STATE before any timed evaluation) and, if list_evaluated is
+ * not NULL, whether it ran over the dirty-row lists (1: only the rows marked since the previous
+ * evaluation of its kind were visited; 0: every tile). */
 int rh_groups_timing(rh_groups* g, int enable);
-int rh_groups_last_timing(rh_groups* g, float* eval_ms, float* gather_ms, int* list_evaluated);
+int rh_groups_last_timing(rh_groups* g, float* eval_ms, int* list_evaluated);
 /* Batched commitIndexChanged() over the slots whose follower commitIndex or leader commitIndex
  * changed: the slots whose {min, majority, max} levels changed, into library-owned pinned memory
  * valid until the next rh_watch_levels / rh_watch_levels_async.  Blocks. */

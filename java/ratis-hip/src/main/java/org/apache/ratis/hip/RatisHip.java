@@ -214,8 +214,8 @@ public final class RatisHip implements AutoCloseable {
     return watchWait0(node, shard, slot, min, majority, max, valid);
   }
 
-  /** Where every shard's result lists are assembled (rh_groups_set_event_sink): EVENTS_HOST_MAPPED
-   *  (the default) or EVENTS_DEVICE.  Not while an evaluation is outstanding. */
+  /** Where every shard's result lists are assembled (rh_groups_set_event_sink): EVENTS_AUTO (the
+   *  default), EVENTS_HOST_MAPPED or EVENTS_DEVICE.  Not while an evaluation is outstanding. */
   public void setEventSink(int sink) throws IOException {
     for (int s = 0; s < shards; s++) {
       setEventSink0(node, s, sink);
@@ -224,6 +224,8 @@ public final class RatisHip implements AutoCloseable {
 
   public static final int EVENTS_HOST_MAPPED = 0;
   public static final int EVENTS_DEVICE = 1;
+  /** The default: HBM lists for evaluations over every tile, pinned lists for dirty-row-list ones. */
+  public static final int EVENTS_AUTO = 2;
 
   // ---- leader lease (LeaderStateImpl.hasLease, LeaderLease) ----------------------------------
   /** A new LeaderLease for the division (lease = now, enabled per config) with every follower slot

@@ -50,6 +50,7 @@ RH_DELTA_SLOT = 1 << 20
 RH_COMMIT_WATCH_ALL = 1
 RH_EVENTS_HOST_MAPPED = 0
 RH_EVENTS_DEVICE = 1
+RH_EVENTS_AUTO = 2
 
 RH_CRC_VERIFY = 1
 RH_CRC_STAMP = 2
@@ -233,7 +234,7 @@ _SIGNATURES = {
     "rh_watch_levels": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_uint64)]),
     "rh_watch_levels_async": (c_int, [c_void_p]),
     "rh_groups_timing": (c_int, [c_void_p, c_int]),
-    "rh_groups_last_timing": (c_int, [c_void_p, POINTER(ctypes.c_float), POINTER(ctypes.c_float), POINTER(c_int)]),
+    "rh_groups_last_timing": (c_int, [c_void_p, POINTER(ctypes.c_float), POINTER(c_int)]),
     "rh_watch_levels_wait": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_uint64)]),
     "rh_lease_batch_async": (c_int, [c_void_p, c_int64, c_int64]),
     "rh_lease_batch_wait": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_uint64)]),

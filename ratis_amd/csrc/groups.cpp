@@ -56,7 +56,7 @@ struct EvSet {
     rh_index_event* wall = nullptr;
     rh_index_event* d_adv = nullptr;  // device views of the same memory
     rh_index_event* d_wall = nullptr;
-    rh_index_event* hbm_adv = nullptr;   // RH_EVENTS_DEVICE: the gather's contiguous lists in HBM
+    rh_index_event* hbm_adv = nullptr;   // the lists in HBM (RH_EVENTS_DEVICE, RH_EVENTS_AUTO's tile evaluations)
     rh_index_event* hbm_wall = nullptr;
     uint64_t* h_cnt = nullptr;       // host-mapped [2]: list lengths, written by the gather kernel
     uint64_t* d_cnt = nullptr;
@@ -98,19 +98,14 @@ struct rh_groups {
     hipStream_t copy_stream = nullptr;
     uint64_t* d_lbits = nullptr;  // rh_lease_batch: slot bitmap (device) and its pinned copy
     uint64_t* h_lbits = nullptr;
-    // events (rh_internal.h, TableEvents): head words, HBM staging regions, result sets
+    // events (rh_internal.h, TableEvents): the evaluation counter words, result sets
     EvSet ev[kEvSets];
     uint64_t next_ticket = 1;
-    unsigned long long* d_heads = nullptr;    // [2 modes][2 parities][kHeads * kHeadStride]
-    int cpar[2] = {0, 0};                     // which parity set of each mode the next evaluation counts into
-    rh_index_event* st_adv = nullptr;         // staging: kHeads regions of st_region records each
-    rh_index_event* st_wall = nullptr;
-    rh_watch_event* st_watch = nullptr;
-    uint64_t st_region = 0;
+    unsigned long long* d_evw = nullptr;      // [2 * kHeadStride]: counter word, then the done word
     rh_watch_event* watch = nullptr;          // host-mapped pinned [cap]: rh_watch_levels' list
     rh_watch_event* d_watch = nullptr;
-    rh_watch_event* hbm_watch = nullptr;      // RH_EVENTS_DEVICE
-    uint64_t* h_wcnt = nullptr;               // host-mapped [2]: its length (gather kernel)
+    rh_watch_event* hbm_watch = nullptr;      // in HBM (as hbm_adv)
+    uint64_t* h_wcnt = nullptr;               // host-mapped [2]: its length (the evaluation's last workgroup)
     uint64_t* d_wcnt = nullptr;
     hipEvent_t wdone = nullptr;
     bool wpending = false, whbm = false;
@@ -124,9 +119,9 @@ struct rh_groups {
     bool lvalid[2] = {true, true};   // every row marked since the kind's last evaluation is listed
     uint64_t lmarks[2] = {0, 0};     // bound on the rows marked since then
     bool last_list = false;     // the last evaluation ran over the dirty-row lists (diagnostics)
-    hipEvent_t tev[3] = {nullptr, nullptr, nullptr};  // rh_groups_timing: around evaluation and gather
+    hipEvent_t tev[2] = {nullptr, nullptr};  // rh_groups_timing: around the evaluation
     bool timing = false, timed = false;
-    int event_sink = RH_EVENTS_HOST_MAPPED;
+    int event_sink = RH_EVENTS_AUTO;
     int64_t* d_read = nullptr;
     size_t read_cap = 0;
 };
@@ -159,15 +154,6 @@ void free_tier(rh::TableTier& t) {
     t = rh::TableTier{};
 }
 
-void free_staging(rh_groups* g) {
-    (void)hipFree(g->st_adv);
-    (void)hipFree(g->st_wall);
-    (void)hipFree(g->st_watch);
-    g->st_adv = g->st_wall = nullptr;
-    g->st_watch = nullptr;
-    g->st_region = 0;
-}
-
 void free_groups(rh_groups* g) {
     for (auto& t : g->dev.tier) free_tier(t);
     (void)hipFree(g->dev.slot_map);
@@ -188,12 +174,11 @@ void free_groups(rh_groups* g) {
         (void)hipFree(g->ev[i].hbm_adv);
         (void)hipFree(g->ev[i].hbm_wall);
     }
-    free_staging(g);
     (void)hipFree(g->d_lrows[0]);
     (void)hipFree(g->d_lrows[1]);
     (void)hipFree(g->d_lheads);
     (void)hipFree(g->hbm_watch);
-    (void)hipFree(g->d_heads);
+    (void)hipFree(g->d_evw);
     if (g->watch) (void)hipHostFree(g->watch);
     if (g->h_wcnt) (void)hipHostFree(g->h_wcnt);
     if (g->wdone) (void)hipEventDestroy(g->wdone);
@@ -311,31 +296,6 @@ int queue_op(rh_groups* g, const CtrlOp& op) {
 
 uint32_t enc(int t, uint32_t row) { return ((uint32_t)t << 28) | row; }
 
-// HBM staging for an evaluation of `blocks` workgroups: kHeads regions of ceil(blocks / kHeads) *
-// rows-per-workgroup records per kind (rh_internal.h, TableEvents).  Grows only; blocks while it
-// reallocates (the stream still reads the old arrays until it drains).
-int ensure_staging(rh_groups* g, uint32_t blocks) {
-    const uint64_t region = (uint64_t)((blocks + rh::kHeads - 1) / rh::kHeads) * rh::table_block_rows();
-    if (region <= g->st_region) return RH_OK;
-    RH_HIP(hipStreamSynchronize(g->ctx->stream));
-    free_staging(g);
-    const uint64_t n = region * rh::kHeads;
-    int rc = dalloc(&g->st_adv, n);
-    if (rc == RH_OK) rc = dalloc(&g->st_wall, n);
-    if (rc == RH_OK) rc = dalloc(&g->st_watch, n);
-    if (rc != RH_OK) {
-        free_staging(g);
-        return rc;
-    }
-    g->st_region = region;
-    return RH_OK;
-}
-
-// The head words of (mode, parity).
-unsigned long long* heads_of(rh_groups* g, int mode, int parity) {
-    return g->d_heads + (size_t)(mode * 2 + parity) * rh::kHeads * rh::kHeadStride;
-}
-
 constexpr size_t kListRegions = (size_t)rh::kTableTiers * rh::kHeads;
 
 unsigned long long* lheads_of(rh_groups* g, int kind, int set) {
@@ -357,24 +317,36 @@ rh::TableLists lists_for(rh_groups* g, int kind, uint64_t n_marks) {
     return l;
 }
 
-// After a failed evaluation launch (some workgroups may have counted into a head, a later launch
-// of the pair may not have run): drain the stream and zero every head word, so the next
-// evaluation starts from clean counters whichever parity it uses.
+// After a failed evaluation launch (some workgroups may have counted, a later launch of the
+// evaluation may not have run): drain the stream and zero the counter words and every list head,
+// so the next evaluation starts from clean counters.
 int reset_heads(rh_groups* g) {
     hipStream_t s = g->ctx->stream;
     (void)hipStreamSynchronize(s);
-    RH_HIP(hipMemsetAsync(g->d_heads, 0, (size_t)4 * rh::kHeads * rh::kHeadStride * 8, s));
+    RH_HIP(hipMemsetAsync(g->d_evw, 0, (size_t)2 * rh::kHeadStride * 8, s));
     RH_HIP(hipMemsetAsync(g->d_lheads, 0, (size_t)4 * kListRegions * rh::kHeadStride * 8, s));
     RH_HIP(hipStreamSynchronize(s));
     g->lvalid[0] = g->lvalid[1] = false;   // the next evaluations run the tile kernels
     return RH_OK;
 }
 
-// Enqueues one evaluation (mode) of the dirty rows and the gather of its events into the
-// contiguous lists (adv / wall or watch, each `cap` records; counts_out host-mapped).
-int evaluate(rh_groups* g, int mode, bool wall_on, rh_index_event* adv, rh_index_event* wall,
-             rh_watch_event* watch, uint64_t* counts_out, uint64_t* h_counts) {
+// The result lists an evaluation may write: [0] the pinned buffers (device pointers of the host
+// mapping), [1] their HBM twins.
+struct EvTargets {
+    rh_index_event* adv[2] = {nullptr, nullptr};
+    rh_index_event* wall[2] = {nullptr, nullptr};
+    rh_watch_event* watch[2] = {nullptr, nullptr};
+};
+
+// Enqueues one evaluation (mode) of the dirty rows, its events written into the lists adv / wall
+// or watch of `t` (each `capacity` records; their lengths to counts_out, host-mapped).  The sink
+// picks the set: HOST_MAPPED [0], DEVICE [1], AUTO [1] for a tile evaluation (up to every row's
+// records: written at HBM speed, copied by DMA in _wait) and [0] for a list evaluation (few
+// records: written across PCIe by the kernel, no copy).  *hbm: whether [1] was used.
+int evaluate(rh_groups* g, int mode, bool wall_on, const EvTargets& t, uint64_t* counts_out, uint64_t* h_counts,
+             bool* hbm) {
     hipStream_t s = g->ctx->stream;
+    *hbm = false;
     int rc = flush_ops(g);
     if (rc != RH_OK) return rc;
     const uint32_t blocks = rh::table_commit_blocks(g->dev);
@@ -382,19 +354,18 @@ int evaluate(rh_groups* g, int mode, bool wall_on, rh_index_event* adv, rh_index
         h_counts[0] = h_counts[1] = 0;
         return RH_OK;
     }
-    // the list evaluation writes at most lcap records of a kind into any one head region
-    rc = ensure_staging(g, std::max<uint32_t>(blocks, (uint32_t)((uint64_t)g->lcap * rh::kHeads / rh::table_block_rows() + 1)));
-    if (rc != RH_OK) return rc;
     const int m = mode == RH_MODE_WATCH ? 1 : 0;
-    rh::TableEvents ev;
-    ev.adv = g->st_adv;
-    ev.wall = wall_on ? g->st_wall : nullptr;
-    ev.watch = g->st_watch;
-    ev.region = g->st_region;
-    ev.heads = heads_of(g, m, g->cpar[m]);
-    ev.heads_next = heads_of(g, m, g->cpar[m] ^ 1);
-    ev.lheads_next = lheads_of(g, m, g->lpar[m] ^ 1);
     const bool list = g->lvalid[m];   // every row marked since the last evaluation is listed
+    const int k = (g->event_sink == RH_EVENTS_DEVICE || (g->event_sink == RH_EVENTS_AUTO && !list)) ? 1 : 0;
+    rh::TableEvents ev;
+    ev.adv = t.adv[k];
+    ev.wall = wall_on ? t.wall[k] : nullptr;
+    ev.watch = t.watch[k];
+    ev.cap = g->capacity;
+    ev.cnt = g->d_evw;
+    ev.done = reinterpret_cast<unsigned int*>(g->d_evw + rh::kHeadStride);
+    ev.counts_out = counts_out;
+    ev.lheads_next = lheads_of(g, m, g->lpar[m] ^ 1);
     if (g->timing) RH_HIP(hipEventRecord(g->tev[0], s));
     if (list) {
         rh::TableLists l;
@@ -402,16 +373,15 @@ int evaluate(rh_groups* g, int mode, bool wall_on, rh_index_event* adv, rh_index
         l.heads = lheads_of(g, m, g->lpar[m]);
         l.cap = g->lcap;
         // COMMIT marks the rows whose commit advanced for commitIndexChanged: at most the listed ones
+        const uint64_t bound = g->lmarks[m];
         const rh::TableLists lw = m == 0 ? lists_for(g, 1, g->lmarks[0]) : rh::TableLists{};
-        rc = rh_table_commit_lists(g->dev, mode, l, lw, ev, s);
+        rc = rh_table_commit_lists(g->dev, mode, l, lw, bound, ev, s);
     } else {
         if (m == 0) g->lvalid[1] = false;   // the tile kernel marks wdirty with plain stores
         rc = rh_table_commit(g->dev, mode, ev, s);
     }
-    if (rc == RH_OK && g->timing) RH_HIP(hipEventRecord(g->tev[1], s));
-    if (rc == RH_OK) rc = rh_table_gather(mode, ev, adv, wall, watch, g->capacity, counts_out, s);
     if (rc == RH_OK && g->timing) {
-        RH_HIP(hipEventRecord(g->tev[2], s));
+        RH_HIP(hipEventRecord(g->tev[1], s));
         g->timed = true;
     }
     if (rc != RH_OK) {
@@ -419,7 +389,7 @@ int evaluate(rh_groups* g, int mode, bool wall_on, rh_index_event* adv, rh_index
         (void)reset_heads(g);
         return rh::fail(rc, msg);
     }
-    g->cpar[m] ^= 1;  // the launch cleared the other set
+    *hbm = k == 1;
     g->lpar[m] ^= 1;  // ... and the other list set of this kind: fresh lists from here on
     g->lmarks[m] = 0;
     g->lvalid[m] = true;
@@ -520,11 +490,14 @@ RH_EXPORT int rh_groups_create(rh_ctx* ctx, uint64_t capacity, int64_t gap_thres
     for (int i = 0; i < kEvSets && rc == RH_OK; ++i) {
         if (rc == RH_OK) rc = halloc_mapped(&g->ev[i].adv, &g->ev[i].d_adv, capacity);
         if (rc == RH_OK) rc = halloc_mapped(&g->ev[i].wall, &g->ev[i].d_wall, capacity);
+        if (rc == RH_OK) rc = dalloc(&g->ev[i].hbm_adv, capacity);
+        if (rc == RH_OK) rc = dalloc(&g->ev[i].hbm_wall, capacity);
         if (rc == RH_OK) rc = halloc_mapped(&g->ev[i].h_cnt, &g->ev[i].d_cnt, 2);
         if (rc == RH_OK && hipEventCreateWithFlags(&g->ev[i].done, hipEventDisableTiming) != hipSuccess)
             rc = rh::fail(RH_E_DEVICE, "hipEventCreate(commit batch)");
     }
     if (rc == RH_OK) rc = halloc_mapped(&g->watch, &g->d_watch, capacity);
+    if (rc == RH_OK) rc = dalloc(&g->hbm_watch, capacity);
     if (rc == RH_OK) rc = halloc_mapped(&g->h_wcnt, &g->d_wcnt, 2);
     if (rc == RH_OK && hipEventCreateWithFlags(&g->wdone, hipEventDisableTiming) != hipSuccess)
         rc = rh::fail(RH_E_DEVICE, "hipEventCreate(watch levels)");
@@ -536,8 +509,8 @@ RH_EXPORT int rh_groups_create(rh_ctx* ctx, uint64_t capacity, int64_t gap_thres
     if (rc == RH_OK) rc = dalloc(&g->d_lheads, (size_t)4 * kListRegions * rh::kHeadStride);
     if (rc == RH_OK && hipMemsetAsync(g->d_lheads, 0, (size_t)4 * kListRegions * rh::kHeadStride * 8, s) != hipSuccess)
         rc = rh::fail(RH_E_DEVICE, "rh_groups_create: list counters");
-    if (rc == RH_OK) rc = dalloc(&g->d_heads, (size_t)4 * rh::kHeads * rh::kHeadStride);
-    if (rc == RH_OK && hipMemsetAsync(g->d_heads, 0, (size_t)4 * rh::kHeads * rh::kHeadStride * 8, s) != hipSuccess)
+    if (rc == RH_OK) rc = dalloc(&g->d_evw, (size_t)2 * rh::kHeadStride);
+    if (rc == RH_OK && hipMemsetAsync(g->d_evw, 0, (size_t)2 * rh::kHeadStride * 8, s) != hipSuccess)
         rc = rh::fail(RH_E_DEVICE, "rh_groups_create: counters");
     if (rc == RH_OK) rc = dalloc(&g->d_lbits, (capacity + 63) / 64);
     if (rc == RH_OK && hipHostMalloc(reinterpret_cast<void**>(&g->h_lbits), (capacity + 63) / 64 * 8) != hipSuccess)
@@ -566,31 +539,13 @@ RH_EXPORT int rh_groups_destroy(rh_groups* g) {
 
 RH_EXPORT int rh_groups_set_event_sink(rh_groups* g, int sink) {
     if (!g) return rh::fail(RH_E_INVAL, "rh_groups_set_event_sink: groups == NULL");
-    if (sink != RH_EVENTS_HOST_MAPPED && sink != RH_EVENTS_DEVICE)
+    if (sink != RH_EVENTS_HOST_MAPPED && sink != RH_EVENTS_DEVICE && sink != RH_EVENTS_AUTO)
         return rh::fail(RH_E_INVAL, "rh_groups_set_event_sink: unknown sink");
     DeviceGuard dg(g->ctx->device);
     std::lock_guard<std::mutex> lk(g->mu);
     for (const EvSet& e : g->ev)
         if (e.pending) return rh::fail(RH_E_STATE, "rh_groups_set_event_sink: an evaluation is in flight");
     if (g->wpending) return rh::fail(RH_E_STATE, "rh_groups_set_event_sink: a watch evaluation is in flight");
-    if (sink == RH_EVENTS_DEVICE && !g->hbm_watch) {  // allocated on first use, kept until destroy
-        int rc = RH_OK;
-        for (int i = 0; i < kEvSets && rc == RH_OK; ++i) {
-            rc = dalloc(&g->ev[i].hbm_adv, g->capacity);
-            if (rc == RH_OK) rc = dalloc(&g->ev[i].hbm_wall, g->capacity);
-        }
-        if (rc == RH_OK) rc = dalloc(&g->hbm_watch, g->capacity);
-        if (rc != RH_OK) {
-            for (EvSet& e : g->ev) {
-                (void)hipFree(e.hbm_adv);
-                (void)hipFree(e.hbm_wall);
-                e.hbm_adv = e.hbm_wall = nullptr;
-            }
-            (void)hipFree(g->hbm_watch);
-            g->hbm_watch = nullptr;
-            return rc;
-        }
-    }
     g->event_sink = sink;
     return RH_OK;
 }
@@ -606,14 +561,13 @@ RH_EXPORT int rh_groups_timing(rh_groups* g, int enable) {
     return RH_OK;
 }
 
-RH_EXPORT int rh_groups_last_timing(rh_groups* g, float* eval_ms, float* gather_ms, int* list_evaluated) {
-    if (!g || !eval_ms || !gather_ms) return rh::fail(RH_E_INVAL, "rh_groups_last_timing: NULL argument");
+RH_EXPORT int rh_groups_last_timing(rh_groups* g, float* eval_ms, int* list_evaluated) {
+    if (!g || !eval_ms) return rh::fail(RH_E_INVAL, "rh_groups_last_timing: NULL argument");
     DeviceGuard dg(g->ctx->device);
     std::lock_guard<std::mutex> lk(g->mu);
     if (!g->timed) return rh::fail(RH_E_STATE, "rh_groups_last_timing: no timed evaluation");
-    RH_HIP(hipEventSynchronize(g->tev[2]));
+    RH_HIP(hipEventSynchronize(g->tev[1]));
     RH_HIP(hipEventElapsedTime(eval_ms, g->tev[0], g->tev[1]));
-    RH_HIP(hipEventElapsedTime(gather_ms, g->tev[1], g->tev[2]));
     if (list_evaluated) *list_evaluated = g->last_list ? 1 : 0;
     return RH_OK;
 }
@@ -909,10 +863,12 @@ RH_EXPORT int rh_commit_batch_async(rh_groups* g, uint32_t flags, uint64_t* tick
     if (e.pending) RH_HIP(hipEventSynchronize(e.done));  // its buffers are about to be rewritten
     e.pending = false;
     e.ticket = 0;
-    const bool hbm = g->event_sink == RH_EVENTS_DEVICE;
     const bool wall_on = (flags & RH_COMMIT_WATCH_ALL) != 0;
-    int rc = evaluate(g, RH_MODE_COMMIT, wall_on, hbm ? e.hbm_adv : e.d_adv, wall_on ? (hbm ? e.hbm_wall : e.d_wall) : nullptr,
-                      nullptr, e.d_cnt, e.h_cnt);
+    EvTargets t;
+    t.adv[0] = e.d_adv, t.adv[1] = e.hbm_adv;
+    t.wall[0] = e.d_wall, t.wall[1] = e.hbm_wall;
+    bool hbm = false;
+    int rc = evaluate(g, RH_MODE_COMMIT, wall_on, t, e.d_cnt, e.h_cnt, &hbm);
     if (rc != RH_OK) return rc;
     RH_HIP(hipEventRecord(e.done, g->ctx->stream));
     e.ticket = tk;
@@ -936,7 +892,7 @@ RH_EXPORT int rh_commit_batch_wait(rh_groups* g, uint64_t ticket, rh_commit_out*
     if (e->ticket != ticket) return rh::fail(RH_E_STATE, "rh_commit_batch_wait: ticket superseded while waiting");
     const uint64_t na = std::min<uint64_t>(e->h_cnt[0], g->capacity);
     const uint64_t nw = std::min<uint64_t>(e->h_cnt[1], g->capacity);
-    if (e->hbm) {  // RH_EVENTS_DEVICE: the counted prefixes to the pinned result buffers
+    if (e->hbm) {  // lists in HBM: the counted prefixes to the pinned result buffers
         e->hbm = false;
         hipStream_t s = g->copy_stream;
         if (na) RH_HIP(hipMemcpyAsync(e->adv, e->hbm_adv, na * sizeof(rh_index_event), hipMemcpyDeviceToHost, s));
@@ -964,8 +920,10 @@ RH_EXPORT int rh_watch_levels_async(rh_groups* g) {
     std::lock_guard<std::mutex> lk(g->mu);
     if (g->wpending) RH_HIP(hipEventSynchronize(g->wdone));  // the previous list is about to be rewritten
     g->wpending = false;
-    const bool hbm = g->event_sink == RH_EVENTS_DEVICE;
-    int rc = evaluate(g, RH_MODE_WATCH, false, nullptr, nullptr, hbm ? g->hbm_watch : g->d_watch, g->d_wcnt, g->h_wcnt);
+    EvTargets t;
+    t.watch[0] = g->d_watch, t.watch[1] = g->hbm_watch;
+    bool hbm = false;
+    int rc = evaluate(g, RH_MODE_WATCH, false, t, g->d_wcnt, g->h_wcnt, &hbm);
     if (rc != RH_OK) return rc;
     RH_HIP(hipEventRecord(g->wdone, g->ctx->stream));
     g->whbm = hbm;

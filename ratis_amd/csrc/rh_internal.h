@@ -133,26 +133,28 @@ struct CtrlOp {
     int64_t flush, commit, tstart;  // START
 };
 
-// Event lists of the evaluation kernels.  A single device-scope counter word admits ~88 returning
-// atomics per us (MI355X_MICROARCH.md, 'dequeue' / 'fanin'): one per workgroup held a sparse
-// evaluation of 1M rows at ~8 us.  So the lists are SHARDED over kHeads head words, one per XCD
-// under round-robin workgroup placement (head = launch-global block index & 7): workgroup b takes
-// its range of region (b & 7) from that region's head, in the HBM staging arrays, and a gather
-// kernel (table_gather_kernel) then packs the kHeads regions into the contiguous result lists.  A
-// region holds ceil(blocks / kHeads) * kTRows records: a workgroup emits at most one record of a
-// kind per row, so no region can overflow.  Head words pack kind 0 (low 32 bits) and kind 1 (high);
-// an evaluation counts into `heads` and clears `heads_next`, the set the following evaluation of
-// the same mode counts into (no memset on the stream).
-constexpr int kHeads = 8;
-constexpr int kHeadStride = 32;   // u64 words between heads: each on its own 256-B line
+// Event lists of the evaluation kernels, written straight into the result lists of the sink
+// (pinned host memory or HBM).  A workgroup gathers its records (LDS), takes ONE range of each list
+// with ONE device-scope atomic on the evaluation's counter word `cnt` (kind 0 in bits 0..27, kind 1
+// in bits 28..55: advanced / watch-ALL for COMMIT, level changes for WATCH) and copies them out
+// contiguously.  Tile kernels: a workgroup then counts itself on `done`; the launch's last one
+// zeroes `done` and, in the launch that ends the evaluation (`publish`), takes the counter with an
+// exchange to zero and writes the two list lengths to counts_out (host-mapped).  List kernel (at
+// most 240 workgroups): the done count rides in the counter word's top byte, so one atomic per
+// workgroup both reserves its range and tells the last one the totals.  No gather pass, no memset,
+// no count read-back on the stream.  The tile kernels have one workgroup per 1,536 rows; the list
+// kernel's grid is sized to the listed rows, so its atomics scale with the dirty set.
+constexpr int kHeads = 8;          // list regions per tier (dirty-row lists, below)
+constexpr int kHeadStride = 32;    // u64 words between head / counter words: each on its own 256-B line
 struct TableEvents {
-    rh_index_event* adv = nullptr;     // COMMIT: advanced (staging, kHeads regions)
-    rh_index_event* wall = nullptr;    // COMMIT: watch-ALL changes (staging), or null (not reported)
-    rh_watch_event* watch = nullptr;   // WATCH: level changes (staging)
-    uint64_t region = 0;               // records per head region
-    unsigned long long* heads = nullptr;       // this evaluation's kHeads words (zero at launch)
-    unsigned long long* heads_next = nullptr;  // the next evaluation's: cleared by block 0
-    uint32_t block_base = 0;                    // launch-global index of this launch's block 0
+    rh_index_event* adv = nullptr;     // COMMIT: advanced (the result list)
+    rh_index_event* wall = nullptr;    // COMMIT: watch-ALL changes, or null (not reported)
+    rh_watch_event* watch = nullptr;   // WATCH: level changes
+    uint64_t cap = 0;                  // records per list
+    unsigned long long* cnt = nullptr; // the evaluation's counter word (zero at its first launch)
+    unsigned int* done = nullptr;      // workgroups done in this launch (zero at launch)
+    uint64_t* counts_out = nullptr;    // [2] list lengths (host-mapped), written by the publishing launch
+    int publish = 0;                   // this launch ends the evaluation
     unsigned long long* lheads_next = nullptr;  // the other list-head set of the evaluated kind: cleared
 };
 // DIRTY-ROW LISTS (list mode).  While the host knows that few rows can be dirty (the deltas and
@@ -170,8 +172,6 @@ struct TableLists {
 
 // Workgroups the table evaluation launches for a table (both width classes).
 uint32_t table_commit_blocks(const TableDev& t);
-// Rows per evaluation workgroup (the staging region unit).
-uint32_t table_block_rows();
 
 }  // namespace rh
 
@@ -219,15 +219,11 @@ int rh_table_apply_deltas(const rh::TableDev& t, const rh_delta* d_deltas, uint6
                           const rh::TableLists& lc, const rh::TableLists& lw, hipStream_t stream);
 // List-mode evaluation of the listed rows of one kind (mode); COMMIT appends the rows whose commit
 // advanced to the watch list `lw` (when it is maintained).  Events as rh_table_commit.
+// `bound`: an upper bound on the listed rows (the host's mark count): sizes the grid.
 int rh_table_commit_lists(const rh::TableDev& t, int mode, const rh::TableLists& l, const rh::TableLists& lw,
-                          const rh::TableEvents& ev, hipStream_t stream);
+                          uint64_t bound, const rh::TableEvents& ev, hipStream_t stream);
 int rh_table_control(const rh::TableDev& t, const rh::CtrlOp* d_ops, uint64_t n, hipStream_t stream);
 int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev, hipStream_t stream);
-// Packs an evaluation's kHeads staging regions into contiguous lists (up to `cap` records per kind)
-// and writes the two list lengths to counts_out[0..1] (host-mapped): COMMIT (adv, wall; wall may
-// be null) or WATCH (watch records into out_watch, length in counts_out[0]).
-int rh_table_gather(int mode, const rh::TableEvents& ev, rh_index_event* out_adv, rh_index_event* out_wall,
-                    rh_watch_event* out_watch, uint64_t cap, uint64_t* counts_out, hipStream_t stream);
 // Initialises tiles [first_tile, n_tiles) of a tier as free rows (conf 0, row_slot kNoRow, clean).
 int rh_table_init_tiles(const rh::TableTier& t, uint32_t first_tile, uint32_t n_tiles, hipStream_t stream);
 int rh_table_lease(const rh::TableDev& t, int64_t now_nanos, int64_t timeout_ms, uint64_t* d_slot_bits,

@@ -10,8 +10,9 @@
 //                         conf change with follower carry-over / reset, step down.
 //   table_commit_kernel   LeaderStateImpl.updateCommit() (COMMIT) or commitIndexChanged() (WATCH)
 //                         over the DIRTY rows of every tier; only changed results become events,
-//                         staged in HBM per XCD head; table_gather_kernel packs them into the
-//                         contiguous result lists (host-mapped pinned memory or HBM).
+//                         written straight into the result lists (host-mapped pinned memory or
+//                         HBM) with one counter atomic per workgroup.
+//   table_list_kernel     the same over the dirty-row lists (list mode: work ~ the dirty rows).
 //   table_lease_kernel    LeaderStateImpl.hasLease() (LSI:1229-1249) with LeaderLease.extend (LL:67-84)
 //                         for every started slot: lease_eval.h's arithmetic over the follower
 //                         timestamp columns, the lease stored in place, a slot-indexed bitmap out.
@@ -246,9 +247,9 @@ __global__ __launch_bounds__(128) void table_init_tiles_kernel(TableTier tt, uin
 
 // ---- updateCommit / commitIndexChanged over the dirty rows ---------------------------------------
 // One workgroup = kTWaves waves, one 128-row tile per wave.  Every wave evaluates its rows' results
-// in registers, the block gathers its events in LDS in wave order, takes ONE range of its head's
-// staging region with ONE device-scope atomic on that head (rh_internal.h, TableEvents: the heads
-// are sharded per XCD), and copies the records out as contiguous 16-byte-per-lane stores.
+// in registers, the block gathers its events in LDS in wave order, takes ONE range of each result
+// list with ONE device-scope atomic on the evaluation's counter word (rh_internal.h, TableEvents)
+// and copies the records out as contiguous 16-byte-per-lane stores.
 struct TierRange {
     uint32_t block_begin[rh::kTableTiers + 1];  // blocks of launch slot i: [block_begin[i], block_begin[i+1])
     int8_t tier[rh::kTableTiers];               // tier of launch slot i (widest first)
@@ -260,9 +261,6 @@ struct TierRange {
 #endif
 #ifndef RH_TABLE_WPE                         // A/B: waves per SIMD the widths-2..6 kernel is pinned to
 #define RH_TABLE_WPE 6
-#endif
-#ifndef RH_TABLE_PERSIST                     // A/B: cap the evaluation grid at this many workgroups (0: none)
-#define RH_TABLE_PERSIST 0
 #endif
 #ifndef RH_TABLE_SUMMARY                     // A/B: skip clean tiles by their summary byte (1) or not (0)
 #define RH_TABLE_SUMMARY 1
@@ -286,7 +284,7 @@ __device__ __forceinline__ V tload(const uint8_t* p) {
 struct Stage {
     uint32_t cnt[2][kTWaves];
     uint32_t pre[2][kTWaves + 1];  // exclusive prefix of cnt over the waves
-    unsigned long long base;        // the block's range in its head's region (both kinds packed)
+    unsigned long long base;        // the block's range of the lists (both kinds packed)
 };
 
 template <int F, bool RANK, bool WATCH>
@@ -430,14 +428,32 @@ __device__ __forceinline__ void table_dispatch(const TableDev& T, int t, uint64_
         table_dispatch<F + 2, FHI, RANK, WATCH>(T, t, tl, wall_on, stage, sc);
 }
 
-#ifndef RH_TABLE_NOEVENTS                    // A/B (timing only, WRONG results): skip the event hand-off
-#define RH_TABLE_NOEVENTS 0
-#endif
+// The evaluation's counter word: kind 0 in bits 0..27, kind 1 in bits 28..55 (a kind has at most
+// one record per row, capacity < 2^28), and -- list kernel -- workgroups done in bits 56..63.
+constexpr int kCntBits = 28;
+constexpr unsigned long long kCntMask = (1ull << kCntBits) - 1;
+constexpr int kDoneShift = 56;
+constexpr uint32_t kListMaxGrid = 240;   // < 2^(64 - kDoneShift)
 
-// One workgroup iteration (launch-local block index b of the class).  Without RH_TABLE_PERSIST a
-// workgroup runs exactly its own index; with it the grid is capped at a resident size (a multiple
-// of kHeads) and workgroups loop over b = blockIdx.x, blockIdx.x + gridDim.x, ... -- every
-// iteration keeps the head of its launch-global index (and, under round-robin placement, its XCD).
+__device__ __forceinline__ void publish_counts(const TableEvents& ev, unsigned long long c) {
+    ev.counts_out[0] = c & kCntMask;
+    ev.counts_out[1] = (c >> kCntBits) & kCntMask;
+}
+
+// Thread 0 of a workgroup, after its counter atomic: counts the workgroup done; the launch's last
+// one zeroes `done` and, when the launch ends the evaluation, takes the counter (exchange to zero:
+// the next evaluation starts from it) and publishes the list lengths.  `after` is the counter
+// atomic's return value (0 without one): the done increment depends on it, so it issues only once
+// the counter atomic has been performed (both execute at the memory side, MI355X_MICROARCH.md
+// 'Global float atomics') -- no fence, which at agent scope would write back this XCD's L2.
+__device__ __forceinline__ void block_done(const TableEvents& ev, unsigned long long after) {
+    if (atomicAdd(ev.done, 1u + (unsigned int)(after >> 63)) + 1u != gridDim.x) return;
+    atomicExch(ev.done, 0u);
+    if (!ev.publish) return;
+    publish_counts(ev, atomicExch(ev.cnt, 0ull));
+}
+
+// One workgroup (block index b of the launch).
 template <bool WATCH, int FLO, int FHI>
 __device__ __forceinline__ void table_block_iter(const TableDev& T, const TierRange& tr, const TableEvents& ev,
                                                  uint32_t b, unsigned char* stage, Stage& sc) {
@@ -450,17 +466,13 @@ __device__ __forceinline__ void table_block_iter(const TableDev& T, const TierRa
     const int t = tr.tier[i];
     const uint64_t tl = (uint64_t)(b - tr.block_begin[i]) * kTWaves + wave;   // tile of this wave
     if (threadIdx.x < 2 * kTWaves) (&sc.cnt[0][0])[threadIdx.x] = 0u;
-    if (b == 0 && threadIdx.x < rh::kHeads && ev.heads_next)
-        ev.heads_next[threadIdx.x * rh::kHeadStride] = 0ull;  // the next evaluation's heads
     if (b == 0 && threadIdx.x < rh::kTableTiers * rh::kHeads && ev.lheads_next)
         ev.lheads_next[threadIdx.x * rh::kHeadStride] = 0ull;  // the next list set of this kind
-    __syncthreads();   // also: a previous iteration's copy-out is done with `stage`
+    __syncthreads();
     if (tl * rh::kTileRows < T.tier[t].rows) table_dispatch<FLO, FHI, FLO <= 6, WATCH>(T, t, tl, wall_on, stage, sc);
     __syncthreads();
-    if (RH_TABLE_NOEVENTS) return;
 
-    // ---- one range of the head's region per block (one device-scope atomic), then a contiguous copy
-    const uint32_t h = (ev.block_base + b) & (rh::kHeads - 1);
+    // ---- one range of each list per block (one device-scope atomic), then a contiguous copy
     if (threadIdx.x == 0) {
         uint32_t a0 = 0, a1 = 0;
         for (int k = 0; k < kTWaves; ++k) {
@@ -471,22 +483,22 @@ __device__ __forceinline__ void table_block_iter(const TableDev& T, const TierRa
         }
         sc.pre[0][kTWaves] = a0;
         sc.pre[1][kTWaves] = a1;
-        // low word: kind 0, high word: kind 1 (each < 2^28: no carry)
-        const unsigned long long add = (unsigned long long)a0 | ((unsigned long long)a1 << 32);
-        sc.base = (a0 | a1) ? atomicAdd(ev.heads + h * rh::kHeadStride, add) : 0ull;
+        const unsigned long long add = (unsigned long long)a0 | ((unsigned long long)a1 << kCntBits);
+        sc.base = (a0 | a1) ? atomicAdd(ev.cnt, add) : 0ull;
+        block_done(ev, sc.base);
     }
     __syncthreads();
     const uint32_t tot0 = sc.pre[0][kTWaves], tot1 = sc.pre[1][kTWaves];
     if (!(tot0 | tot1)) return;
-    const uint64_t R = ev.region;
-    const uint64_t b0 = sc.base & 0xFFFFFFFFull, b1 = sc.base >> 32;
+    const uint64_t R = ev.cap;   // a list holds one record per row at most: never reached
+    const uint64_t b0 = sc.base & kCntMask, b1 = (sc.base >> kCntBits) & kCntMask;
     const uint64_t lim0 = b0 >= R ? 0 : (b0 + tot0 <= R ? tot0 : R - b0);
     const uint64_t lim1 = b1 >= R ? 0 : (b1 + tot1 <= R ? tot1 : R - b1);
     // record e of the block lives in the region of wave k with pre[k] <= e < pre[k + 1]
     typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
     const v4u32* src = reinterpret_cast<const v4u32*>(stage);
     if (WATCH) {  // 32-byte records: two 16-byte words each
-        v4u32* dst = reinterpret_cast<v4u32*>(ev.watch + h * R + b0);
+        v4u32* dst = reinterpret_cast<v4u32*>(ev.watch + b0);
         for (uint32_t j = threadIdx.x; j < 2 * lim0; j += kTBlock) {
             const uint32_t e = j >> 1;
             uint32_t k = 0;
@@ -495,7 +507,7 @@ __device__ __forceinline__ void table_block_iter(const TableDev& T, const TierRa
             dst[j] = src[2 * (k * 128 + (e - sc.pre[0][k])) + (j & 1)];
         }
     } else {
-        v4u32* da = reinterpret_cast<v4u32*>(ev.adv + h * R + b0);
+        v4u32* da = reinterpret_cast<v4u32*>(ev.adv + b0);
         for (uint32_t e = threadIdx.x; e < lim0; e += kTBlock) {
             uint32_t k = 0;
 #pragma unroll
@@ -503,7 +515,7 @@ __device__ __forceinline__ void table_block_iter(const TableDev& T, const TierRa
             da[e] = src[k * 128 + (e - sc.pre[0][k])];
         }
         if (ev.wall) {
-            v4u32* dw = reinterpret_cast<v4u32*>(ev.wall + h * R + b1);
+            v4u32* dw = reinterpret_cast<v4u32*>(ev.wall + b1);
             for (uint32_t e = threadIdx.x; e < lim1; e += kTBlock) {
                 uint32_t k = 0;
 #pragma unroll
@@ -520,12 +532,7 @@ __device__ __forceinline__ void table_commit_block(const TierRange& tr, const Ta
     // COMMIT: [0, 24 KiB) advanced records, [24, 48 KiB) watch-ALL records; WATCH: level records
     __shared__ __attribute__((aligned(16))) unsigned char stage[kTRows * sizeof(rh_watch_event)];
     __shared__ Stage sc;
-    if (RH_TABLE_PERSIST > 0) {
-        const uint32_t nblocks = tr.block_begin[rh::kTableTiers];
-        for (uint32_t b = blockIdx.x; b < nblocks; b += gridDim.x) table_block_iter<WATCH, FLO, FHI>(T, tr, ev, b, stage, sc);
-    } else {
-        table_block_iter<WATCH, FLO, FHI>(T, tr, ev, blockIdx.x, stage, sc);
-    }
+    table_block_iter<WATCH, FLO, FHI>(T, tr, ev, blockIdx.x, stage, sc);
 }
 
 // Widths 2..6: rank-mask order statistics, 6 waves per SIMD (<= 84 VGPRs: the row pair's columns
@@ -548,8 +555,10 @@ __global__ __launch_bounds__(kTBlock) void table_commit_kernel_net(TableDev Targ
 // ---- list mode: updateCommit / commitIndexChanged over the listed rows only ---------------------
 // One lane per listed row (random rows: each lane loads its row's 8-byte column elements).  The
 // lanes of a wave may hold rows of different tiers (widths): the row evaluation is instantiated per
-// width and the wave runs the widths its lanes hold.  Events: one atomic per wave on the head of
-// its workgroup (blockIdx & 7), records written straight into that head's staging region.
+// width and the wave runs the widths its lanes hold.  Events: per pass one counter atomic per
+// workgroup (its waves' counts summed in LDS), records written straight into the result lists;
+// the last pass's atomic also counts the workgroup done (the counter word's top byte), so the
+// workgroup that completes the count knows the list lengths from its own atomic's return.
 template <int F, bool WATCH>
 __device__ __forceinline__ void list_row(const TableDev& T, const TableTier& tt, uint32_t r, bool wall_on,
                                          bool wlisted, bool& e0, bool& e1, bool& wtrans, int64_t& x0, int64_t& x1,
@@ -634,22 +643,23 @@ __global__ __launch_bounds__(256) void table_list_kernel(TableDev Targ, TableLis
         if (threadIdx.x < NR) pre[threadIdx.x + 1] = c;
         if (threadIdx.x == 0) pre[0] = 0;
     }
-    if (blockIdx.x == 0 && threadIdx.x < rh::kHeads && ev.heads_next)
-        ev.heads_next[threadIdx.x * rh::kHeadStride] = 0ull;   // the next evaluation's event heads
     if (blockIdx.x == 0 && threadIdx.x < NR && ev.lheads_next)
         ev.lheads_next[(uint64_t)threadIdx.x * rh::kHeadStride] = 0ull;   // the next list set of this kind
     __syncthreads();
     const uint32_t N = pre[NR];
     const int lane = threadIdx.x & 63;
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    const uint32_t h = blockIdx.x & (rh::kHeads - 1);
-    const uint64_t R = ev.region;
+    const uint32_t h = blockIdx.x & (rh::kHeads - 1);   // the watch-list region rows are appended to
+    const uint64_t R = ev.cap;
     const bool wall_on = !WATCH && ev.wall != nullptr;
+    const int wave = threadIdx.x >> 6;
+    __shared__ uint32_t wcnt[2][4];        // per pass: the waves' record counts
+    __shared__ unsigned long long lbase;   // per pass: the workgroup's range of the lists
     // entries are dealt out lane-major over EVERY wave of the grid (entry e -> wave e % W, pass
     // e / W): a sparse list keeps all CUs' memory pipelines busy instead of filling a few waves
     const uint32_t W = gridDim.x * (blockDim.x >> 6);
     const uint32_t wg = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    for (uint32_t pass = 0; (uint64_t)pass * W * 64 < N; ++pass) {
+    for (uint32_t pass = 0; pass == 0 || (uint64_t)pass * W * 64 < N; ++pass) {   // >= 1 pass: done counts
         const uint32_t e = (pass * 64 + (uint32_t)lane) * W + wg;
         bool e0 = false, e1 = false, wtrans = false;
         int64_t x0 = 0, x1 = 0, x2 = 0;
@@ -674,78 +684,43 @@ __global__ __launch_bounds__(256) void table_list_kernel(TableDev Targ, TableLis
                 default: list_row<14, WATCH>(T, tt, row, wall_on, wl, e0, e1, wtrans, x0, x1, x2, valid, slot); break;
             }
         }
-        // events: one range of the head's region per wave.  Its atomic is issued before the watch
-        // list's, so the two round trips overlap
+        // events: one range of the lists per workgroup and pass
         const uint64_t a = __ballot(e0), c = WATCH ? 0ull : __ballot(e1);
-        unsigned long long rb = 0;
-        if (lane == 0 && (a | c))
-            rb = atomicAdd(ev.heads + h * rh::kHeadStride,
-                           (unsigned long long)__popcll(a) | ((unsigned long long)__popcll(c) << 32));
+        if (lane == 0) {
+            wcnt[0][wave] = (uint32_t)__popcll(a);
+            wcnt[1][wave] = (uint32_t)__popcll(c);
+        }
+        __syncthreads();
+        // the watch list's appends and the counter atomic are in flight together
         if (!WATCH && Lw.rows) list_append(Lw, wtrans, t, row, h);   // kernel argument: uniform
-        if (!(a | c)) continue;
-        const uint32_t b0 = (uint32_t)__shfl((int)(uint32_t)rb, 0), b1 = (uint32_t)__shfl((int)(uint32_t)(rb >> 32), 0);
+        if (threadIdx.x == 0) {
+            const bool last = (uint64_t)(pass + 1) * W * 64 >= N;
+            const unsigned long long s0 = wcnt[0][0] + wcnt[0][1] + wcnt[0][2] + wcnt[0][3];
+            const unsigned long long s1 = wcnt[1][0] + wcnt[1][1] + wcnt[1][2] + wcnt[1][3];
+            const unsigned long long add = s0 | (s1 << kCntBits) | (last ? 1ull << kDoneShift : 0ull);
+            const unsigned long long old = add ? atomicAdd(ev.cnt, add) : 0ull;
+            lbase = old;
+            if (last && ((old + add) >> kDoneShift) == gridDim.x) {   // every workgroup has counted
+                publish_counts(ev, old + add);
+                atomicExch(ev.cnt, 0ull);   // the next evaluation's counter
+            }
+        }
+        __syncthreads();
+        uint32_t b0 = (uint32_t)(lbase & kCntMask), b1 = (uint32_t)((lbase >> kCntBits) & kCntMask);
+        for (int k = 0; k < wave; ++k) b0 += wcnt[0][k], b1 += wcnt[1][k];
+        __syncthreads();   // wcnt / lbase are the next pass's
         if (e0) {
             const uint64_t k = b0 + (uint64_t)__popcll(a & lt);
             if (k < R) {
                 if (WATCH)
-                    ev.watch[h * R + k] = rh_watch_event{slot, valid, x0, x1, x2};
+                    ev.watch[k] = rh_watch_event{slot, valid, x0, x1, x2};
                 else
-                    ev.adv[h * R + k] = rh_index_event{slot, 0u, x0};
+                    ev.adv[k] = rh_index_event{slot, 0u, x0};
             }
         }
         if (!WATCH && e1) {
             const uint64_t k = b1 + (uint64_t)__popcll(c & lt);
-            if (k < R) ev.wall[h * R + k] = rh_index_event{slot, 0u, x1};
-        }
-    }
-}
-
-// ---- packing the head regions into the contiguous result lists ------------------------------------
-// Grid-stride over the records; each thread moves 16-byte words.  The list lengths are the head
-// words' sums (the evaluation's atomics are complete at this kernel's start).
-template <bool WATCH>
-__global__ __launch_bounds__(256) void table_gather_kernel(TableEvents ev, rh_index_event* __restrict__ out_adv,
-                                                           rh_index_event* __restrict__ out_wall,
-                                                           rh_watch_event* __restrict__ out_watch, uint64_t cap,
-                                                           uint64_t* counts_out) {
-    typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
-    const uint64_t R = ev.region;
-    uint64_t pre0[rh::kHeads + 1], pre1[rh::kHeads + 1];
-    pre0[0] = pre1[0] = 0;
-#pragma unroll
-    for (int h = 0; h < rh::kHeads; ++h) {
-        const unsigned long long x = ev.heads[h * rh::kHeadStride];
-        const uint64_t c0 = x & 0xFFFFFFFFull, c1 = x >> 32;
-        pre0[h + 1] = pre0[h] + (c0 < R ? c0 : R);
-        pre1[h + 1] = pre1[h] + (c1 < R ? c1 : R);
-    }
-    const uint64_t tot0 = pre0[rh::kHeads], tot1 = WATCH ? 0 : pre1[rh::kHeads];
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-        counts_out[0] = tot0;
-        counts_out[1] = tot1;
-    }
-    const uint64_t n0 = tot0 < cap ? tot0 : cap;
-    const uint64_t n1 = (out_wall && !WATCH) ? (tot1 < cap ? tot1 : cap) : 0;
-    const uint64_t words0 = WATCH ? 2 * n0 : n0;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < words0 + n1; j += stride) {
-        if (j < words0) {
-            const uint64_t e = WATCH ? j >> 1 : j;
-            int h = 0;
-#pragma unroll
-            for (int m = 1; m < rh::kHeads; ++m) h += e >= pre0[m] ? 1 : 0;
-            const uint64_t s = h * R + (e - pre0[h]);
-            if (WATCH)
-                reinterpret_cast<v4u32*>(out_watch)[j] = reinterpret_cast<const v4u32*>(ev.watch)[2 * s + (j & 1)];
-            else
-                reinterpret_cast<v4u32*>(out_adv)[e] = reinterpret_cast<const v4u32*>(ev.adv)[s];
-        } else {
-            const uint64_t e = j - words0;
-            int h = 0;
-#pragma unroll
-            for (int m = 1; m < rh::kHeads; ++m) h += e >= pre1[m] ? 1 : 0;
-            const uint64_t s = h * R + (e - pre1[h]);
-            reinterpret_cast<v4u32*>(out_wall)[e] = reinterpret_cast<const v4u32*>(ev.wall)[s];
+            if (k < R) ev.wall[k] = rh_index_event{slot, 0u, x1};
         }
     }
 }
@@ -835,13 +810,13 @@ static uint32_t class_blocks(const rh::TableDev& t, int cls) {
 }
 
 uint32_t rh::table_commit_blocks(const rh::TableDev& t) { return class_blocks(t, 0) + class_blocks(t, 1); }
-uint32_t rh::table_block_rows() { return kTRows; }
 
 int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev_in, hipStream_t stream) {
     // one launch per width class over every non-empty tier of the class, widest tier first (a
     // joint-consensus tier's rows cost several times a stable row's compute: dispatched last they
     // were the launch's tail, commit.hip build_args)
     rh::TableEvents ev = ev_in;
+    const int last_cls = class_blocks(t, 1) ? 1 : 0;   // its launch publishes the list lengths
     for (int cls = 0; cls < 2; ++cls) {
         TierRange tr{};
         uint32_t blocks = 0;
@@ -854,9 +829,8 @@ int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev_i
         }
         for (int s = tr.n_slots; s <= rh::kTableTiers; ++s) tr.block_begin[s] = blocks;
         if (blocks == 0) continue;
-        // RH_TABLE_PERSIST > 0 caps the grid (a multiple of kHeads): resident workgroups loop
-        const uint32_t grid = (RH_TABLE_PERSIST > 0 && blocks > (uint32_t)RH_TABLE_PERSIST) ? (uint32_t)RH_TABLE_PERSIST : blocks;
-        const dim3 g(grid), b(kTBlock);
+        ev.publish = cls == last_cls;
+        const dim3 g(blocks), b(kTBlock);
         if (mode == RH_MODE_WATCH) {
             if (cls == 0) hipLaunchKernelGGL(table_commit_kernel_rank<true>, g, b, 0, stream, t, tr, ev);
             else hipLaunchKernelGGL(table_commit_kernel_net<true>, g, b, 0, stream, t, tr, ev);
@@ -865,30 +839,21 @@ int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev_i
             else hipLaunchKernelGGL(table_commit_kernel_net<false>, g, b, 0, stream, t, tr, ev);
         }
         RH_HIP(hipGetLastError());
-        ev.block_base += blocks;
     }
     return RH_OK;
 }
 
 int rh_table_commit_lists(const rh::TableDev& t, int mode, const rh::TableLists& l, const rh::TableLists& lw,
-                          const rh::TableEvents& ev, hipStream_t stream) {
-    // a resident-sized grid (one round); the listed rows are strided over it
-    const dim3 g(512), b(256);
+                          uint64_t bound, const rh::TableEvents& ev_in, hipStream_t stream) {
+    // one listed row per lane up to a resident-sized grid (one round), strided over it beyond
+    const uint64_t want = (bound + 255) / 256;
+    const dim3 g((uint32_t)(want < 1 ? 1 : (want > kListMaxGrid ? kListMaxGrid : want))), b(256);
+    rh::TableEvents ev = ev_in;
+    ev.publish = 1;
     if (mode == RH_MODE_WATCH)
         hipLaunchKernelGGL(table_list_kernel<true>, g, b, 0, stream, t, l, rh::TableLists{}, ev);
     else
         hipLaunchKernelGGL(table_list_kernel<false>, g, b, 0, stream, t, l, lw, ev);
-    RH_HIP(hipGetLastError());
-    return RH_OK;
-}
-
-int rh_table_gather(int mode, const rh::TableEvents& ev, rh_index_event* out_adv, rh_index_event* out_wall,
-                    rh_watch_event* out_watch, uint64_t cap, uint64_t* counts_out, hipStream_t stream) {
-    const dim3 g(256), b(256);
-    if (mode == RH_MODE_WATCH)
-        hipLaunchKernelGGL(table_gather_kernel<true>, g, b, 0, stream, ev, out_adv, out_wall, out_watch, cap, counts_out);
-    else
-        hipLaunchKernelGGL(table_gather_kernel<false>, g, b, 0, stream, ev, out_adv, out_wall, out_watch, cap, counts_out);
     RH_HIP(hipGetLastError());
     return RH_OK;
 }

@@ -245,19 +245,19 @@ class RaftGroupTable:
         return ev[np.argsort(ev["slot"], kind="stable")]
 
     def set_timing(self, enable: bool = True) -> None:
-        """``rh_groups_timing``: HIP events around every evaluation kernel and its gather."""
+        """``rh_groups_timing``: HIP events around every evaluation (its kernels, events included)."""
         check(self._lib.rh_groups_timing(self.handle, 1 if enable else 0))
 
-    def last_timing(self) -> Tuple[float, float]:
-        """(evaluation ms, gather ms) of the last timed evaluation (``rh_groups_last_timing``)."""
-        a, b = ctypes.c_float(), ctypes.c_float()
-        check(self._lib.rh_groups_last_timing(self.handle, ctypes.byref(a), ctypes.byref(b), None))
-        return float(a.value), float(b.value)
+    def last_timing(self) -> float:
+        """Device ms of the last timed evaluation (``rh_groups_last_timing``)."""
+        a = ctypes.c_float()
+        check(self._lib.rh_groups_last_timing(self.handle, ctypes.byref(a), None))
+        return float(a.value)
 
     def last_was_list(self) -> bool:
         """Whether the last (timed) evaluation ran over the dirty-row lists (list mode)."""
-        a, b, m = ctypes.c_float(), ctypes.c_float(), ctypes.c_int()
-        check(self._lib.rh_groups_last_timing(self.handle, ctypes.byref(a), ctypes.byref(b), ctypes.byref(m)))
+        a, m = ctypes.c_float(), ctypes.c_int()
+        check(self._lib.rh_groups_last_timing(self.handle, ctypes.byref(a), ctypes.byref(m)))
         return bool(m.value)
 
     def watch_async(self) -> None:

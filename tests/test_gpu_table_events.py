@@ -1,11 +1,12 @@
-"""GPU parity of the resident table's event path (round 4): the evaluation kernel stages its records
-per XCD head in HBM and a gather kernel packs them into the contiguous result lists
-(ratis_amd/csrc/rh_internal.h, TableEvents).  Checked against tests/table_model.py (the reference's
-FollowerInfo / LeaderStateImpl semantics over the oracle's commit arithmetic):
+"""GPU parity of the resident table's event path (round 4): the evaluation kernels write their
+records straight into the contiguous result lists, one range per workgroup, and the evaluation's
+last workgroup publishes the list lengths (ratis_amd/csrc/rh_internal.h, TableEvents).  Checked
+against tests/table_model.py (the reference's FollowerInfo / LeaderStateImpl semantics over the
+oracle's commit arithmetic):
 
-  * both sinks (HOST_MAPPED: gather into pinned memory; DEVICE: gather into HBM + D2H in _wait),
-    for updateCommit (advanced + watch-ALL) and commitIndexChanged, on a table large enough that
-    every head region is used (>= 8 workgroups per evaluation kind);
+  * every sink (HOST_MAPPED: lists in pinned memory; DEVICE: lists in HBM + D2H in _wait; AUTO, the
+    default: DEVICE for tile evaluations, HOST_MAPPED for list evaluations), for
+    updateCommit (advanced + watch-ALL) and commitIndexChanged, on a table of 40+ workgroups;
   * sparse dirty sets, where most 128-row tiles are clean and skipped by their summary byte;
   * evaluations whose ticket is superseded without a wait, and an evaluation after them;
   * the async forms of commitIndexChanged and hasLease (rh_watch_levels_async / _wait,
@@ -32,15 +33,16 @@ def _loaded(ctx, model, n, seed):
     return tab, first
 
 
-@pytest.mark.parametrize("sink", ["host_mapped", "device"])
-def test_event_sinks_match_model_over_every_head(ctx, orc, sink):
+@pytest.mark.parametrize("sink", ["host_mapped", "device", "auto"])
+def test_event_sinks_match_model(ctx, orc, sink):
     from ratis_amd import _lib
     rng = np.random.default_rng(404)
-    n = 60_000   # 40+ workgroups of 1,536 rows: every one of the 8 head regions holds records
+    n = 60_000   # 40+ workgroups of 1,536 rows, each taking its range of the lists
     model = TableModel(n)
     tab, n = _loaded(ctx, model, n, seed=41)
     try:
-        tab.set_event_sink(_lib.RH_EVENTS_DEVICE if sink == "device" else _lib.RH_EVENTS_HOST_MAPPED)
+        tab.set_event_sink({"device": _lib.RH_EVENTS_DEVICE, "host_mapped": _lib.RH_EVENTS_HOST_MAPPED,
+                            "auto": _lib.RH_EVENTS_AUTO}[sink])
         compare(tab, model, orc, columns=False)
         live = np.arange(n)
         for step, k in enumerate([n // 2, 3 * n, n // 100, 7, 0]):
