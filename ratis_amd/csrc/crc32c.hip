@@ -1044,6 +1044,14 @@ __device__ __forceinline__ uint32_t fold16(const uint32_t* lds, const uint32_t* 
     return zshift(lch, r0) ^ r1;
 }
 
+// A/B: 1 folds chunk 0 in the steps (a per-lane mask on every word of every step) instead of one
+// masked chunk-0 pass per task.  It removes the chunk-0 pass's refetched lines (ragged 64-2048 B,
+// 64 x 32 MiB: FETCH_SIZE 2545 -> 2402 MB) but the masking makes the step VALU-heavier: crc_pack
+// 1054 -> 1086 us at 128 segments (profiles/r04/ragged_c0/).  Off.
+#ifndef RH_PACK_C0STEP
+#define RH_PACK_C0STEP 0
+#endif
+
 template <bool SLOT>
 __global__ __launch_bounds__(kCrcThreads) void crc_pack_kernel(PackArgs pk_arg) {
     // slot variant: fields read from the kernarg segment where used (scalar loads the compiler can
@@ -1132,8 +1140,10 @@ __global__ __launch_bounds__(kCrcThreads) void crc_pack_kernel(PackArgs pk_arg) 
         }
         const uint32_t lc = pk ? (uint32_t)lcs : 0u;
         const uint32_t k = pk ? (lc - 1) >> 6 : 0u;  // chunks after chunk 0
-        const uint32_t Qi = wave_scan_add(k, lane);
-        const uint32_t Q = Qi - k;                   // packed position of the frame's chunk 1
+        // packed chunks per frame: 1..k (chunk 0 in its own pass) or 0..k (chunk 0 in the steps)
+        const uint32_t kp = RH_PACK_C0STEP ? (pk ? k + 1u : 0u) : k;
+        const uint32_t Qi = wave_scan_add(kp, lane);
+        const uint32_t Q = Qi - kp;                  // packed position of the frame's first packed chunk
         const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)Qi, 63);
         const uint32_t sh = (uint32_t)E & 3u;
         // trailer and init term (needed at the end of the task; loaded now)
@@ -1146,8 +1156,8 @@ __global__ __launch_bounds__(kCrcThreads) void crc_pack_kernel(PackArgs pk_arg) 
         }
         mark[lane] = 0;
         // ---- chunk 0 of every frame: bytes before the frame start zeroed ----
-        uint32_t f0, fs;
-        {
+        uint32_t f0 = 0, fs = 0;
+        if (!RH_PACK_C0STEP) {
             uint32_t dd[17];
             const int64_t b0 = E - 64 * (int64_t)k - 64 - (int64_t)sh;  // chunk 0's 4-aligned start
             if (__any(pk && b0 < 0)) {  // a frame near the buffer start (rare): word by word
@@ -1174,13 +1184,14 @@ __global__ __launch_bounds__(kCrcThreads) void crc_pack_kernel(PackArgs pk_arg) 
 
         // ---- steps: 64 packed chunks (1..k of the frames, in order) each ----
         struct Step {
-            uint32_t j, i, m, fs;  // frame lane, chunk index (>= 1), chunks after it, chunk-0 term
+            uint32_t j, i, m, fs;  // frame lane, chunk index, chunks after it, chunk-0 term
             int64_t be;            // chunk end
             uint32_t sh;
+            int32_t g8;            // RH_PACK_C0STEP: 8 x the bytes before the frame start (chunk 0)
             bool valid;
         };
         auto map = [&](uint32_t s, uint32_t jprev) -> Step {
-            if (k > 0 && (Q >> 6) == s) mark[Q & 63u] = ((s + 1u) << 8) | (uint32_t)lane;
+            if (kp > 0 && (Q >> 6) == s) mark[Q & 63u] = ((s + 1u) << 8) | (uint32_t)lane;
             __builtin_amdgcn_wave_barrier();
             const uint32_t rd = mark[lane];
             const uint64_t M = __ballot((rd >> 8) == s + 1u) & (~0ull >> (63 - lane));
@@ -1194,16 +1205,28 @@ __global__ __launch_bounds__(kCrcThreads) void crc_pack_kernel(PackArgs pk_arg) 
             const uint32_t kj = (uint32_t)__shfl((int)k, (int)x.j);
             const uint32_t elo = (uint32_t)__shfl((int)(uint32_t)E, (int)x.j);
             const uint32_t ehi = (uint32_t)__shfl((int)(uint32_t)((uint64_t)E >> 32), (int)x.j);
-            x.fs = (uint32_t)__shfl((int)fs, (int)x.j);
-            x.i = P - Qj + 1u;
+            x.fs = RH_PACK_C0STEP ? 0u : (uint32_t)__shfl((int)fs, (int)x.j);
+            x.i = P - Qj + (RH_PACK_C0STEP ? 0u : 1u);
             x.m = kj - x.i;
+            x.g8 = 0;
+            if (RH_PACK_C0STEP) {
+                const uint32_t lcj = (uint32_t)__shfl((int)lc, (int)x.j);
+                x.g8 = x.i == 0u ? 8 * (int32_t)((kj + 1u) * 64u - lcj) : 0;
+            }
             const int64_t Ej = (int64_t)(((uint64_t)ehi << 32) | elo);
             x.be = Ej - 64 * (int64_t)x.m;
             x.sh = elo & 3u;
             return x;
         };
         auto load = [&](const Step& x, uint32_t (&dd)[17]) {
-            load_chunk(x.valid ? a.buf + (x.be - 64 - (int64_t)x.sh) : a.buf, dd);
+            const int64_t b0 = x.be - 64 - (int64_t)x.sh;
+            if (RH_PACK_C0STEP && __any(x.valid && b0 < 0)) {  // chunk 0 of a frame near the buffer start (rare)
+#pragma unroll
+                for (int i = 0; i < 17; ++i)
+                    dd[i] = x.valid && b0 + 4 * i >= 0 ? *reinterpret_cast<const uint32_t*>(a.buf + b0 + 4 * i) : 0u;
+                return;
+            }
+            load_chunk(x.valid ? a.buf + b0 : a.buf, dd);
         };
         const uint32_t nsteps = (T + 63) >> 6;
         uint32_t carry = 0;  // register of the frame running past the previous step (at its end)
@@ -1222,9 +1245,15 @@ __global__ __launch_bounds__(kCrcThreads) void crc_pack_kernel(PackArgs pk_arg) 
             }
             uint32_t w[16];
 #pragma unroll
-            for (int i = 0; i < 16; ++i) w[i] = __builtin_amdgcn_alignbyte(dc[i + 1], dc[i], cur.sh);
+            for (int i = 0; i < 16; ++i) {
+                w[i] = __builtin_amdgcn_alignbyte(dc[i + 1], dc[i], cur.sh);
+                if (RH_PACK_C0STEP) {  // chunk 0: the bytes before the frame start zeroed
+                    const int32_t kk = min(max(cur.g8 - 32 * i, 0), 32);
+                    w[i] &= (uint32_t)(~0ull << kk);
+                }
+            }
             uint32_t R = fold16(lds, lch, w, lb);
-            R ^= cur.i == 1u ? cur.fs : 0u;
+            if (!RH_PACK_C0STEP) R ^= cur.i == 1u ? cur.fs : 0u;
             const uint32_t K0 = zshift_uniform(p.z2k, carry);  // off the step's dependent chain
             const uint32_t C4 = zshift_uniform(p.z4k, carry);
             uint32_t y = 0;
@@ -1232,7 +1261,7 @@ __global__ __launch_bounds__(kCrcThreads) void crc_pack_kernel(PackArgs pk_arg) 
             for (int q = 0; q < 8; ++q) y ^= lf[c + ((uint32_t)(q * 16) + ((R >> (4 * q)) & 15u)) * 32u];
             y = cur.valid ? y : 0u;
             const uint32_t px = half_prefix_xor(y);
-            const int a0 = lane - (int)cur.i + 1;  // lane of the frame's chunk 1 (may be < 0)
+            const int a0 = lane - (int)cur.i + (RH_PACK_C0STEP ? 0 : 1);  // lane of the frame's first packed chunk (may be < 0)
             const bool cont = a0 < (int)hs;        // the frame began before this half
             const int src = (cont ? (int)hs : a0) - 1;
             const uint32_t before = (uint32_t)__shfl((int)px, src < 0 ? 0 : src);
@@ -1257,9 +1286,9 @@ __global__ __launch_bounds__(kCrcThreads) void crc_pack_kernel(PackArgs pk_arg) 
         // ---- emit: frame lane j finishes frame j ----
         if (pk) {
             uint32_t V = f0;
-            if (k > 0) {
+            if (RH_PACK_C0STEP || k > 0) {
                 const uint32_t tot = vst[lane];
-                const uint32_t* im = p.inv + (size_t)((Q + k - 1u) & 31u) * 128u;
+                const uint32_t* im = p.inv + (size_t)((Q + kp - 1u) & 31u) * 128u;   // its last chunk's position
                 V = 0;
 #pragma unroll
                 for (int q = 0; q < 8; ++q) V ^= im[q * 16 + ((tot >> (4 * q)) & 15u)];

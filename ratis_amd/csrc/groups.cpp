@@ -373,9 +373,8 @@ int evaluate(rh_groups* g, int mode, bool wall_on, const EvTargets& t, uint64_t*
         l.heads = lheads_of(g, m, g->lpar[m]);
         l.cap = g->lcap;
         // COMMIT marks the rows whose commit advanced for commitIndexChanged: at most the listed ones
-        const uint64_t bound = g->lmarks[m];
         const rh::TableLists lw = m == 0 ? lists_for(g, 1, g->lmarks[0]) : rh::TableLists{};
-        rc = rh_table_commit_lists(g->dev, mode, l, lw, bound, ev, s);
+        rc = rh_table_commit_lists(g->dev, mode, l, lw, ev, s);
     } else {
         if (m == 0) g->lvalid[1] = false;   // the tile kernel marks wdirty with plain stores
         rc = rh_table_commit(g->dev, mode, ev, s);

@@ -219,9 +219,8 @@ int rh_table_apply_deltas(const rh::TableDev& t, const rh_delta* d_deltas, uint6
                           const rh::TableLists& lc, const rh::TableLists& lw, hipStream_t stream);
 // List-mode evaluation of the listed rows of one kind (mode); COMMIT appends the rows whose commit
 // advanced to the watch list `lw` (when it is maintained).  Events as rh_table_commit.
-// `bound`: an upper bound on the listed rows (the host's mark count): sizes the grid.
 int rh_table_commit_lists(const rh::TableDev& t, int mode, const rh::TableLists& l, const rh::TableLists& lw,
-                          uint64_t bound, const rh::TableEvents& ev, hipStream_t stream);
+                          const rh::TableEvents& ev, hipStream_t stream);
 int rh_table_control(const rh::TableDev& t, const rh::CtrlOp* d_ops, uint64_t n, hipStream_t stream);
 int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev, hipStream_t stream);
 // Initialises tiles [first_tile, n_tiles) of a tier as free rows (conf 0, row_slot kNoRow, clean).

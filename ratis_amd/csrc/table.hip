@@ -659,7 +659,16 @@ __global__ __launch_bounds__(256) void table_list_kernel(TableDev Targ, TableLis
     // e / W): a sparse list keeps all CUs' memory pipelines busy instead of filling a few waves
     const uint32_t W = gridDim.x * (blockDim.x >> 6);
     const uint32_t wg = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    for (uint32_t pass = 0; pass == 0 || (uint64_t)pass * W * 64 < N; ++pass) {   // >= 1 pass: done counts
+    // Workgroup b holds entries iff its wave 4b does (lane 0, pass 0): the first min(grid, ceil(N / 4))
+    // workgroups.  Each counts itself done in its last pass holding entries; the one completing
+    // that count publishes.  An empty list: workgroup 0 publishes zero lengths.
+    if (N == 0) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) publish_counts(ev, 0ull);
+        return;
+    }
+    const uint32_t nw_per = blockDim.x >> 6;
+    const uint64_t active = (N + nw_per - 1) / nw_per < gridDim.x ? (N + nw_per - 1) / nw_per : gridDim.x;
+    for (uint32_t pass = 0; (uint64_t)pass * W * 64 < N; ++pass) {
         const uint32_t e = (pass * 64 + (uint32_t)lane) * W + wg;
         bool e0 = false, e1 = false, wtrans = false;
         int64_t x0 = 0, x1 = 0, x2 = 0;
@@ -694,13 +703,14 @@ __global__ __launch_bounds__(256) void table_list_kernel(TableDev Targ, TableLis
         // the watch list's appends and the counter atomic are in flight together
         if (!WATCH && Lw.rows) list_append(Lw, wtrans, t, row, h);   // kernel argument: uniform
         if (threadIdx.x == 0) {
-            const bool last = (uint64_t)(pass + 1) * W * 64 >= N;
+            const uint64_t w0 = (uint64_t)blockIdx.x * nw_per;   // this workgroup's wave 0, lane 0
+            const bool last = (uint64_t)pass * W * 64 + w0 < N && (uint64_t)(pass + 1) * W * 64 + w0 >= N;
             const unsigned long long s0 = wcnt[0][0] + wcnt[0][1] + wcnt[0][2] + wcnt[0][3];
             const unsigned long long s1 = wcnt[1][0] + wcnt[1][1] + wcnt[1][2] + wcnt[1][3];
             const unsigned long long add = s0 | (s1 << kCntBits) | (last ? 1ull << kDoneShift : 0ull);
             const unsigned long long old = add ? atomicAdd(ev.cnt, add) : 0ull;
             lbase = old;
-            if (last && ((old + add) >> kDoneShift) == gridDim.x) {   // every workgroup has counted
+            if (last && ((old + add) >> kDoneShift) == active) {   // every workgroup holding entries has counted
                 publish_counts(ev, old + add);
                 atomicExch(ev.cnt, 0ull);   // the next evaluation's counter
             }
@@ -844,10 +854,11 @@ int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev_i
 }
 
 int rh_table_commit_lists(const rh::TableDev& t, int mode, const rh::TableLists& l, const rh::TableLists& lw,
-                          uint64_t bound, const rh::TableEvents& ev_in, hipStream_t stream) {
-    // one listed row per lane up to a resident-sized grid (one round), strided over it beyond
-    const uint64_t want = (bound + 255) / 256;
-    const dim3 g((uint32_t)(want < 1 ? 1 : (want > kListMaxGrid ? kListMaxGrid : want))), b(256);
+                          const rh::TableEvents& ev_in, hipStream_t stream) {
+    // the listed rows are dealt lane-major over every wave of a near-chip-wide grid: a few rows per
+    // wave on ~every CU (random rows: the chain of dependent loads is latency-bound per CU, so the
+    // rows are spread, not packed into few waves)
+    const dim3 g(kListMaxGrid), b(256);
     rh::TableEvents ev = ev_in;
     ev.publish = 1;
     if (mode == RH_MODE_WATCH)
