@@ -6,6 +6,7 @@
 // the UPDATE_COMMIT event queue (LeaderStateImpl.java:111-188, 846-854, 900-902) and the
 // RaftServerProxy's map of divisions (RaftServerProxy.java:89-150) for the multi-GPU node.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -122,6 +123,7 @@ struct rh_groups {
     hipEvent_t tev[2] = {nullptr, nullptr};  // rh_groups_timing: around the evaluation
     bool timing = false, timed = false;
     int event_sink = RH_EVENTS_AUTO;
+    uint32_t cbits = 28;   // bits per list count in the evaluation's counter word (TableEvents)
     int64_t* d_read = nullptr;
     size_t read_cap = 0;
 };
@@ -365,6 +367,7 @@ int evaluate(rh_groups* g, int mode, bool wall_on, const EvTargets& t, uint64_t*
     ev.cnt = g->d_evw;
     ev.done = reinterpret_cast<unsigned int*>(g->d_evw + rh::kHeadStride);
     ev.counts_out = counts_out;
+    ev.cbits = g->cbits;
     ev.lheads_next = lheads_of(g, m, g->lpar[m] ^ 1);
     if (g->timing) RH_HIP(hipEventRecord(g->tev[0], s));
     if (list) {
@@ -502,6 +505,11 @@ RH_EXPORT int rh_groups_create(rh_ctx* ctx, uint64_t capacity, int64_t gap_thres
         rc = rh::fail(RH_E_DEVICE, "hipEventCreate(watch levels)");
     if (rc == RH_OK && hipEventCreateWithFlags(&g->ldone, hipEventDisableTiming) != hipSuccess)
         rc = rh::fail(RH_E_DEVICE, "hipEventCreate(lease batch)");
+    // 24-bit counts leave 16 bits of done count in the word (every tile workgroup packed); the
+    // environment can force 28 (tests: the separate done word of large tables)
+    g->cbits = capacity < (1ull << 24) ? 24u : 28u;
+    if (const char* e = std::getenv("RATIS_HIP_TABLE_CNT_BITS"))
+        if (std::atoi(e) == 28) g->cbits = 28u;
     // list capacity: a list evaluation is chosen while at most capacity / RH_LIST_DIV rows can be dirty
     g->lcap = (uint32_t)std::max<uint64_t>(1024, capacity / RH_LIST_DIV);
     for (int k = 0; k < 2 && rc == RH_OK; ++k) rc = dalloc(&g->d_lrows[k], kListRegions * g->lcap);

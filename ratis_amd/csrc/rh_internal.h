@@ -135,15 +135,16 @@ struct CtrlOp {
 
 // Event lists of the evaluation kernels, written straight into the result lists of the sink
 // (pinned host memory or HBM).  A workgroup gathers its records (LDS), takes ONE range of each list
-// with ONE device-scope atomic on the evaluation's counter word `cnt` (kind 0 in bits 0..27, kind 1
-// in bits 28..55: advanced / watch-ALL for COMMIT, level changes for WATCH) and copies them out
-// contiguously.  Tile kernels: a workgroup then counts itself on `done`; the launch's last one
-// zeroes `done` and, in the launch that ends the evaluation (`publish`), takes the counter with an
-// exchange to zero and writes the two list lengths to counts_out (host-mapped).  List kernel (at
-// most 240 workgroups): the done count rides in the counter word's top byte, so one atomic per
-// workgroup both reserves its range and tells the last one the totals.  No gather pass, no memset,
-// no count read-back on the stream.  The tile kernels have one workgroup per 1,536 rows; the list
-// kernel's grid is sized to the listed rows, so its atomics scale with the dirty set.
+// with ONE device-scope atomic on the evaluation's counter word `cnt` and copies them out
+// contiguously.  The word holds kind 0 in bits [0, cbits) and kind 1 in [cbits, 2 cbits) (advanced /
+// watch-ALL for COMMIT, level changes for WATCH; cbits = 24 for capacities below 2^24, else 28)
+// and, when they fit above (`packed`: always in the list kernel, whose grid is at most 240
+// workgroups; in the tile kernels below 2^16 workgroups at cbits 24), the workgroups done -- so one
+// atomic both reserves a workgroup's range and tells the last one the totals.  Otherwise the tile
+// kernels count themselves on the separate `done` word.  The workgroup completing the
+// evaluation's count (done_target: the workgroups of every launch of it) writes the two list
+// lengths to counts_out (host-mapped) and zeroes the words for the next evaluation: no gather
+// pass, no memset, no count read-back on the stream.
 constexpr int kHeads = 8;          // list regions per tier (dirty-row lists, below)
 constexpr int kHeadStride = 32;    // u64 words between head / counter words: each on its own 256-B line
 struct TableEvents {
@@ -153,8 +154,10 @@ struct TableEvents {
     uint64_t cap = 0;                  // records per list
     unsigned long long* cnt = nullptr; // the evaluation's counter word (zero at its first launch)
     unsigned int* done = nullptr;      // workgroups done in this launch (zero at launch)
-    uint64_t* counts_out = nullptr;    // [2] list lengths (host-mapped), written by the publishing launch
-    int publish = 0;                   // this launch ends the evaluation
+    uint64_t* counts_out = nullptr;    // [2] list lengths (host-mapped)
+    uint32_t cbits = 28;               // bits per count in `cnt`
+    int packed = 0;                    // tile kernels: the done count rides in `cnt` above the counts
+    uint32_t done_target = 0;          // tile kernels: workgroups done that end the evaluation (0: not this launch)
     unsigned long long* lheads_next = nullptr;  // the other list-head set of the evaluated kind: cleared
 };
 // DIRTY-ROW LISTS (list mode).  While the host knows that few rows can be dirty (the deltas and

@@ -428,28 +428,27 @@ __device__ __forceinline__ void table_dispatch(const TableDev& T, int t, uint64_
         table_dispatch<F + 2, FHI, RANK, WATCH>(T, t, tl, wall_on, stage, sc);
 }
 
-// The evaluation's counter word: kind 0 in bits 0..27, kind 1 in bits 28..55 (a kind has at most
-// one record per row, capacity < 2^28), and -- list kernel -- workgroups done in bits 56..63.
-constexpr int kCntBits = 28;
-constexpr unsigned long long kCntMask = (1ull << kCntBits) - 1;
-constexpr int kDoneShift = 56;
-constexpr uint32_t kListMaxGrid = 240;   // < 2^(64 - kDoneShift)
+// The evaluation's counter word (rh_internal.h, TableEvents): kind 0 in bits [0, cbits), kind 1 in
+// [cbits, 2 cbits), workgroups done above when the count fits there (`packed`; the list kernel
+// always: at most kListMaxGrid workgroups < 2^8).
+constexpr uint32_t kListMaxGrid = 240;
 
 __device__ __forceinline__ void publish_counts(const TableEvents& ev, unsigned long long c) {
-    ev.counts_out[0] = c & kCntMask;
-    ev.counts_out[1] = (c >> kCntBits) & kCntMask;
+    const unsigned long long m = (1ull << ev.cbits) - 1;
+    ev.counts_out[0] = c & m;
+    ev.counts_out[1] = (c >> ev.cbits) & m;
 }
 
-// Thread 0 of a workgroup, after its counter atomic: counts the workgroup done; the launch's last
-// one zeroes `done` and, when the launch ends the evaluation, takes the counter (exchange to zero:
-// the next evaluation starts from it) and publishes the list lengths.  `after` is the counter
-// atomic's return value (0 without one): the done increment depends on it, so it issues only once
-// the counter atomic has been performed (both execute at the memory side, MI355X_MICROARCH.md
-// 'Global float atomics') -- no fence, which at agent scope would write back this XCD's L2.
+// Thread 0 of a tile-kernel workgroup after its counter atomic, when the done count has its own
+// word: counts the workgroup done; the one completing the evaluation's count (done_target, 0 in
+// a launch that does not end the evaluation) zeroes both words and publishes the list lengths.
+// `after` is the counter atomic's return value (0 without one): the done increment depends on it,
+// so it issues only once the counter atomic has been performed (both execute at the memory side,
+// MI355X_MICROARCH.md 'Global float atomics') -- no fence, which at agent scope would write back
+// this XCD's L2.
 __device__ __forceinline__ void block_done(const TableEvents& ev, unsigned long long after) {
-    if (atomicAdd(ev.done, 1u + (unsigned int)(after >> 63)) + 1u != gridDim.x) return;
+    if (atomicAdd(ev.done, 1u + (unsigned int)(after >> 63)) + 1u != ev.done_target) return;
     atomicExch(ev.done, 0u);
-    if (!ev.publish) return;
     publish_counts(ev, atomicExch(ev.cnt, 0ull));
 }
 
@@ -483,15 +482,24 @@ __device__ __forceinline__ void table_block_iter(const TableDev& T, const TierRa
         }
         sc.pre[0][kTWaves] = a0;
         sc.pre[1][kTWaves] = a1;
-        const unsigned long long add = (unsigned long long)a0 | ((unsigned long long)a1 << kCntBits);
-        sc.base = (a0 | a1) ? atomicAdd(ev.cnt, add) : 0ull;
-        block_done(ev, sc.base);
+        const uint32_t cb = ev.cbits;
+        const unsigned long long add = (unsigned long long)a0 | ((unsigned long long)a1 << cb) |
+                                       (ev.packed ? 1ull << (2 * cb) : 0ull);
+        const unsigned long long old = add ? atomicAdd(ev.cnt, add) : 0ull;
+        sc.base = old;
+        if (!ev.packed) {
+            block_done(ev, old);
+        } else if (ev.done_target && ((old + add) >> (2 * cb)) == ev.done_target) {   // the last workgroup
+            publish_counts(ev, old + add);
+            atomicExch(ev.cnt, 0ull);   // the next evaluation's counter
+        }
     }
     __syncthreads();
     const uint32_t tot0 = sc.pre[0][kTWaves], tot1 = sc.pre[1][kTWaves];
     if (!(tot0 | tot1)) return;
     const uint64_t R = ev.cap;   // a list holds one record per row at most: never reached
-    const uint64_t b0 = sc.base & kCntMask, b1 = (sc.base >> kCntBits) & kCntMask;
+    const unsigned long long cm = (1ull << ev.cbits) - 1;
+    const uint64_t b0 = sc.base & cm, b1 = (sc.base >> ev.cbits) & cm;
     const uint64_t lim0 = b0 >= R ? 0 : (b0 + tot0 <= R ? tot0 : R - b0);
     const uint64_t lim1 = b1 >= R ? 0 : (b1 + tot1 <= R ? tot1 : R - b1);
     // record e of the block lives in the region of wave k with pre[k] <= e < pre[k + 1]
@@ -707,16 +715,18 @@ __global__ __launch_bounds__(256) void table_list_kernel(TableDev Targ, TableLis
             const bool last = (uint64_t)pass * W * 64 + w0 < N && (uint64_t)(pass + 1) * W * 64 + w0 >= N;
             const unsigned long long s0 = wcnt[0][0] + wcnt[0][1] + wcnt[0][2] + wcnt[0][3];
             const unsigned long long s1 = wcnt[1][0] + wcnt[1][1] + wcnt[1][2] + wcnt[1][3];
-            const unsigned long long add = s0 | (s1 << kCntBits) | (last ? 1ull << kDoneShift : 0ull);
+            const uint32_t cb = ev.cbits;
+            const unsigned long long add = s0 | (s1 << cb) | (last ? 1ull << (2 * cb) : 0ull);
             const unsigned long long old = add ? atomicAdd(ev.cnt, add) : 0ull;
             lbase = old;
-            if (last && ((old + add) >> kDoneShift) == active) {   // every workgroup holding entries has counted
+            if (last && ((old + add) >> (2 * cb)) == active) {   // every workgroup holding entries has counted
                 publish_counts(ev, old + add);
                 atomicExch(ev.cnt, 0ull);   // the next evaluation's counter
             }
         }
         __syncthreads();
-        uint32_t b0 = (uint32_t)(lbase & kCntMask), b1 = (uint32_t)((lbase >> kCntBits) & kCntMask);
+        const unsigned long long cm = (1ull << ev.cbits) - 1;
+        uint32_t b0 = (uint32_t)(lbase & cm), b1 = (uint32_t)((lbase >> ev.cbits) & cm);
         for (int k = 0; k < wave; ++k) b0 += wcnt[0][k], b1 += wcnt[1][k];
         __syncthreads();   // wcnt / lbase are the next pass's
         if (e0) {
@@ -827,6 +837,9 @@ int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev_i
     // were the launch's tail, commit.hip build_args)
     rh::TableEvents ev = ev_in;
     const int last_cls = class_blocks(t, 1) ? 1 : 0;   // its launch publishes the list lengths
+    const uint32_t total = rh::table_commit_blocks(t);
+    // the done count rides in the counter word when the evaluation's workgroups fit above the counts
+    ev.packed = 2 * ev.cbits < 64 && (uint64_t)total < (1ull << (64 - 2 * ev.cbits)) ? 1 : 0;
     for (int cls = 0; cls < 2; ++cls) {
         TierRange tr{};
         uint32_t blocks = 0;
@@ -839,7 +852,7 @@ int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev_i
         }
         for (int s = tr.n_slots; s <= rh::kTableTiers; ++s) tr.block_begin[s] = blocks;
         if (blocks == 0) continue;
-        ev.publish = cls == last_cls;
+        ev.done_target = cls == last_cls ? total : 0u;   // workgroups of both launches count
         const dim3 g(blocks), b(kTBlock);
         if (mode == RH_MODE_WATCH) {
             if (cls == 0) hipLaunchKernelGGL(table_commit_kernel_rank<true>, g, b, 0, stream, t, tr, ev);
@@ -860,7 +873,6 @@ int rh_table_commit_lists(const rh::TableDev& t, int mode, const rh::TableLists&
     // rows are spread, not packed into few waves)
     const dim3 g(kListMaxGrid), b(256);
     rh::TableEvents ev = ev_in;
-    ev.publish = 1;
     if (mode == RH_MODE_WATCH)
         hipLaunchKernelGGL(table_list_kernel<true>, g, b, 0, stream, t, l, rh::TableLists{}, ev);
     else

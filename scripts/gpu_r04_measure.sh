@@ -12,7 +12,7 @@ cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/bench_prof -o run --output-format csv -- python3 $R/bench.py --steps 20 --warmup 5 > $O/bench_prof.log 2>&1 || { tail -20 $O/bench_prof.log; exit 1; }
 echo bench-prof done
 run() { local name=$1 ctrs=$2; shift 2
-  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $ctrs -d "$O/pmc/$name" -o run --output-format csv -- python3 $R/scripts/prof_kernels.py "$@" > "$O/pmc/$name.log" 2>&1
+  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $ctrs -d "$O/pmc/$name" -o run --output-format csv -- python3 $R/scripts/prof_kernels.py "$@" > "$O/$name.log" 2>&1
   local rc=$?; echo "$name rc=$rc"; if [ $rc -ne 0 ]; then exit $rc; fi; }
 run table_a "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD" --what table --iters 6
 run table_b "FETCH_SIZE GRBM_GUI_ACTIVE" --what table --iters 6

@@ -53,6 +53,9 @@ def main():
                     units = int(parts[3])
                 if parts[:1] in (["alg_bytes"], ["seg_bytes"], ["lease_bytes"]) and len(parts) >= 4:
                     units = int(parts[3])
+                if parts[:1] == ["alg_bytes"]:
+                    out[f"{name}_algorithmic_bytes_per_launch"] = int(parts[1])
+                    out[f"{name}_traffic_over_algorithmic"] = round((fetch + write) / int(parts[1]), 3)
         if units:
             out[f"{name}_units_per_launch"] = units
             out[f"{name}_bytes_per_unit"] = round((fetch + write) / units, 2)

@@ -56,8 +56,9 @@ def main():
         torch.cuda.synchronize()
         print("seg_bytes", n * rs.segment_size, "segments", n)
     elif a.what == "table":
-        # the resident table's updateCommit (table_commit_kernel_rank) with every row dirty: one
-        # matchIndex / flushIndex delta per group per iteration, events staged in HBM
+        # the resident table's updateCommit (table_commit_kernel_rank) with every row dirty, the
+        # bench's table_commit 100 % step (bench.table_commit_leg): per row one delta, 10 % flush /
+        # 90 % matchIndex of followers 0..3, +512 over the row's current value; RH_EVENTS_AUTO
         import numpy as np
 
         from ratis_amd import groups
@@ -68,18 +69,27 @@ def main():
         for h in host:
             tab.load(first, h.conf, h.flush, h.commit, h.term_start, match=h.follower)
             first += h.n
-        tab.set_event_sink(_lib.RH_EVENTS_DEVICE)
         tab.commit_wait_counts(tab.commit_async(watch_all=True))
-        cur = np.concatenate([h.flush for h in host])
-        rng = np.random.default_rng(4)
+        cur_f = np.concatenate([h.follower[:4] for h in host], axis=1)
+        cur_s = np.concatenate([h.flush for h in host])
+        rng = np.random.default_rng(7)
+        ev = []
         for i in range(a.iters):
-            cur += 512
-            col = np.where(rng.random(n) < 0.1, _lib.RH_COL_FLUSH, rng.integers(0, 4, n))
-            tab.push(groups.make_deltas(np.arange(n), col, cur))
-            tab.commit_wait_counts(tab.commit_async(watch_all=True))
+            slot = rng.permutation(n)
+            is_flush = rng.random(n) < 0.10
+            col = rng.integers(0, 4, size=n)
+            val = np.where(is_flush, cur_s[slot], cur_f[col, slot]) + 512
+            cur_s[slot[is_flush]] = val[is_flush]
+            cur_f[col[~is_flush], slot[~is_flush]] = val[~is_flush]
+            tab.push(groups.make_deltas(slot, np.where(is_flush, _lib.RH_COL_FLUSH, col), val))
+            ev.append(tab.commit_wait_counts(tab.commit_async(watch_all=True)))
         torch.cuda.synchronize()
         f_mean = (host[0].n * 4 + (n - host[0].n) * 6) / n
-        print("alg_bytes", int(n * (8 * f_mean + 45)), "rows", n)
+        na = sum(e[0] for e in ev) / len(ev)
+        nw = sum(e[1] for e in ev) / len(ev)
+        # bench.table_commit_leg's algorithmic bytes of a 100 % step (mean over the iterations)
+        alg = n * 1 + n * (8 * f_mean + 4 + 4 + 8 + 8 + 8 + 8 + 1) + na * (16 + 8 + 1) + nw * (16 + 8)
+        print("alg_bytes", int(alg), "rows", n, "advanced", int(na), "watch_all", int(nw))
     elif a.what == "lease":
         import numpy as np
         host = workload.commit_snapshot(1_000_000)

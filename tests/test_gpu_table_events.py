@@ -255,3 +255,40 @@ def test_list_and_tile_evaluations_interleaved(ctx, orc, seed):
             assert np.array_equal(tab.read(col), model.column(col)), col
     finally:
         tab.close()
+
+
+def test_separate_done_word_of_large_tables(ctx, orc, monkeypatch):
+    """28-bit list counts (tables of 2^24 rows and more) leave 8 bits of done count in the counter
+    word: tile evaluations of more than 255 workgroups then count themselves on the separate done
+    word (TableEvents.packed = 0).  Forced here on a 400k-row table (261 workgroups) through the
+    library's test knob, with 3000 ten-follower groups beside config 3's so that both width
+    classes launch (the second launch publishes)."""
+    from ratis_amd import _lib, groups, workload
+    monkeypatch.setenv("RATIS_HIP_TABLE_CNT_BITS", "28")
+    rng = np.random.default_rng(28)
+    tiers = workload.commit_snapshot(400_000, joint_frac=0.1, peers=5, seed=28)
+    n0 = sum(t.n for t in tiers)
+    n = n0 + 3000
+    model = TableModel(n)
+    tab = groups.RaftGroupTable(ctx, capacity=n)
+    try:
+        first = 0
+        for h in tiers:
+            tab.load(first, h.conf, h.flush, h.commit, h.term_start, match=h.follower)
+            model.load(first, h.conf, h.flush, h.commit, h.term_start, match=h.follower)
+            first += h.n
+        w = conf_word(0b1111111111)
+        for s_ in range(n0, n):
+            tab.start(s_, w, 5000, 100, 50)
+            model.start(s_, w, 5000, 100, 50)
+        live = np.arange(n)
+        for sink in (_lib.RH_EVENTS_AUTO, _lib.RH_EVENTS_HOST_MAPPED):
+            tab.set_event_sink(sink)
+            compare(tab, model, orc, columns=False)
+            for k in (n, n // 10, 500):
+                d = random_deltas(rng, model, live, k)
+                tab.push(d)
+                model.apply(d)
+                compare(tab, model, orc, columns=False)
+    finally:
+        tab.close()
