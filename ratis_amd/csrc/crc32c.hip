@@ -1405,7 +1405,7 @@ int launch_pack(rh_ctx* ctx, FrameArgs a, const SlotPlan& sp, hipStream_t stream
 // classify -> scatter -> lane kernels (4 and 8 lanes per frame) -> window kernel over the rest,
 // all on `stream`.
 int launch_frames(rh_ctx* ctx, FrameArgs a, hipStream_t stream, bool* dense_written = nullptr,
-                  const SlotPlan& sp = SlotPlan{}) {
+                  const SlotPlan& sp = SlotPlan{}, bool force_window = false) {
     static const hipError_t attr = [] {
         hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(crc_frames_kernel<false>),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, kCrcLdsOf(false));
@@ -1424,7 +1424,7 @@ int launch_frames(rh_ctx* ctx, FrameArgs a, hipStream_t stream, bool* dense_writ
     // The lane split pays a classify + scatter pass (~4 % of a config-5 launch); it is taken when the
     // buffer's mean frame length buf_len / n is at most kLaneMeanMax -- logs of short entries.
     // Logs of long frames (config 5's 4 KiB) and single spans stay on the window kernel alone.
-    bool window_only = a.buf_len / a.n > kLaneMeanMax;
+    bool window_only = force_window || a.buf_len / a.n > kLaneMeanMax;
 #ifdef RH_AB_WINDOW_ONLY  // A/B build (scripts/ab_build.sh): every frame on the window kernel
     window_only = true;
 #endif
@@ -1568,18 +1568,30 @@ __global__ __launch_bounds__(64) void crc_serial_kernel(const uint8_t* __restric
             T[3][hi & 0xffu] ^ T[2][(hi >> 8) & 0xffu] ^ T[1][(hi >> 16) & 0xffu] ^ T[0][hi >> 24];
     };
     while (p < e && (reinterpret_cast<uintptr_t>(p) & 15)) c = (c >> 8) ^ T[0][(c ^ *p++) & 0xffu];
-    // 128 bytes per round: the eight 16-byte loads are all in flight before the first fold, so a
-    // lane pays one memory latency per 128 bytes, not per 8
+    // 128 bytes per round, the next round's eight 16-byte loads issued before this round's fold:
+    // the lane's memory latency hides behind its LDS chain (two buffers with static roles)
     typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
-    for (; p + 128 <= e; p += 128) {
-        v4u32 q[8];
+    v4u32 qa[8], qb[8];
+    auto load128 = [&](v4u32 (&q)[8], const uint8_t* src) {
 #pragma unroll
-        for (int k = 0; k < 8; ++k) q[k] = reinterpret_cast<const v4u32*>(p)[k];
+        for (int k = 0; k < 8; ++k) q[k] = reinterpret_cast<const v4u32*>(src)[k];
+    };
+    auto fold128 = [&](const v4u32 (&q)[8]) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
             step8(q[k].x, q[k].y);
             step8(q[k].z, q[k].w);
         }
+    };
+    if (p + 128 <= e) load128(qa, p);
+    while (p + 128 <= e) {
+        if (p + 256 <= e) load128(qb, p + 128);
+        fold128(qa);
+        p += 128;
+        if (p + 128 > e) break;
+        if (p + 256 <= e) load128(qa, p + 128);
+        fold128(qb);
+        p += 128;
     }
     for (; p + 8 <= e; p += 8) {
         const uint64_t w = *reinterpret_cast<const uint64_t*>(p);
@@ -1606,7 +1618,7 @@ int rh_crc_serial_launch(rh_ctx* ctx, const rh_frames* f, uint32_t flags, hipStr
     return RH_OK;
 }
 
-int rh_crc_launch_impl(rh_ctx* ctx, const rh_frames* f, uint32_t flags, hipStream_t stream) {
+int rh_crc_launch_impl(rh_ctx* ctx, const rh_frames* f, uint32_t flags, hipStream_t stream, bool window_only) {
     if (!f) return rh::fail(RH_E_INVAL, "rh_crc32c_frames_launch: frames == NULL");
     if ((flags & ~(RH_CRC_VERIFY | RH_CRC_STAMP)) || flags == (RH_CRC_VERIFY | RH_CRC_STAMP))
         return rh::fail(RH_E_INVAL, "rh_crc32c_frames_launch: flags must be 0, VERIFY or STAMP");
@@ -1626,7 +1638,7 @@ int rh_crc_launch_impl(rh_ctx* ctx, const rh_frames* f, uint32_t flags, hipStrea
     a.crc_out = f->crc_out;
     a.bad_bits = f->bad_bits;
     a.n_bad = f->n_bad;
-    return launch_frames(ctx, a, stream);
+    return launch_frames(ctx, a, stream, nullptr, SlotPlan{}, window_only);
 }
 
 // The read path's CRC pass (rh_segments_read_launch): the kernel over the slotted frame table the

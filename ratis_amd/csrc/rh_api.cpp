@@ -267,7 +267,8 @@ RH_EXPORT int rh_crc32c_verify_host(rh_ctx* ctx, const uint8_t* seg, uint64_t se
 RH_EXPORT int rh_host_register(rh_ctx* ctx, void* p, uint64_t n) {
     if (!ctx || !p || n == 0) return rh::fail(RH_E_INVAL, "rh_host_register: ctx/p == NULL or n == 0");
     DeviceGuard g(ctx->device);
-    RH_HIP(hipHostRegister(p, n, hipHostRegisterPortable));   // every GPU's contexts may read it
+    // every GPU's contexts may read it; mapped: rh_crc32c_stamp_host's kernel reads and stamps it in place
+    RH_HIP(hipHostRegister(p, n, hipHostRegisterPortable | hipHostRegisterMapped));
     return RH_OK;
 }
 
@@ -278,8 +279,16 @@ RH_EXPORT int rh_host_unregister(rh_ctx* ctx, void* p) {
     return RH_OK;
 }
 
-// frames up to this length go one lane per frame (crc_serial_kernel): 64 KiB is 8k dependent
-// table rounds, ~40 us on one lane; longer ones to the streaming plans
+// rh_crc32c_stamp_host's plan (A/B builds override): 0 = the span and the frame table copied in,
+// one lane per frame (crc_serial_kernel), the CRCs copied back, trailers written by the host; 1 =
+// the same copies around the window kernel; 2 = the span copied in, the window kernel reading the
+// frame table from and writing the CRCs to the mapped pinned staging (one copy, no D2H).  (Reading
+// the frames themselves across PCIe would leave the batch's first frame -- within 67 bytes of the
+// mapping's start -- to the window kernel's byte-wise guarded path: a PCIe round trip per 4 bytes.)
+#ifndef RH_STAMP_PLAN
+#define RH_STAMP_PLAN 2
+#endif
+// plan 0: frames up to this length go one lane per frame; longer ones to the streaming plans
 constexpr uint64_t kSerialMaxFrame = 64 << 10;
 
 RH_EXPORT int rh_crc32c_stamp_host(rh_ctx* ctx, uint8_t* buf, uint64_t buf_len, const uint64_t* frame_off,
@@ -300,46 +309,65 @@ RH_EXPORT int rh_crc32c_stamp_host(rh_ctx* ctx, uint8_t* buf, uint64_t buf_len, 
         hi = std::max(hi, o + l);
     }
     DeviceGuard g(ctx->device);
-    // only the span the frames cover crosses PCIe (a flush batch is one contiguous run); the frame
-    // table goes over from the context's pinned staging in one copy, the CRCs come back into it as
-    // 4 B per frame, and the host writes the big-endian trailers
+    hipStream_t s = ctx->stream;
+    // the frame table (offsets relative to the span's start, lengths) and the CRCs in the context's
+    // pinned staging
     auto al = [](uint64_t x) { return (x + 255) / 256 * 256; };
     const uint64_t span = hi - lo;
     const uint64_t t_off = 0, t_len = al(n * 8), t_crc = t_len + al(n * 4), t_bytes = t_crc + al(n * 4);
-    const uint64_t o_img = 0, o_tab = al(span), total = o_tab + t_bytes;
     std::lock_guard<std::mutex> lk(ctx->stage_mu);
     if (ctx->pinned_bytes < t_bytes) {
         if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
         ctx->h_pinned = nullptr;
         ctx->pinned_bytes = 0;
         const size_t want = std::max<size_t>(t_bytes, (size_t)1 << 20);
-        if (hipHostMalloc(&ctx->h_pinned, want) != hipSuccess) return rh::fail(RH_E_NOMEM, "rh_crc32c_stamp_host: pinned staging");
+        if (hipHostMalloc(&ctx->h_pinned, want, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess)
+            return rh::fail(RH_E_NOMEM, "rh_crc32c_stamp_host: pinned staging");
         ctx->pinned_bytes = want;
     }
     uint8_t* st = static_cast<uint8_t*>(ctx->h_pinned);
+    // the device image has kPad bytes before the span and after it: no frame lies within the window
+    // kernel's guard distances of the image ends (67 B before, 8 B after), so none takes its byte-wise
+    // guarded path (one dependent load per byte)
+    constexpr uint64_t kPad = 128;
     uint64_t* rel = reinterpret_cast<uint64_t*>(st + t_off);
-    for (uint64_t i = 0; i < n; ++i) rel[i] = frame_off[i] - lo;
+    for (uint64_t i = 0; i < n; ++i) rel[i] = frame_off[i] - lo + kPad;
     std::memcpy(st + t_len, frame_len, n * 4);
+    rh_frames f{};
+    f.buf_len = kPad + span + kPad;
+    f.n = n;
+    f.init_state = 0xFFFFFFFFu;   // checksum.reset() before every entry (OUT:100-103)
+    // only the span the frames cover crosses PCIe (a flush batch is one contiguous run); the CRCs
+    // come back as 4 B per frame and the host writes the big-endian trailers
+    const uint64_t o_img = 0, o_tab = al(kPad + span + kPad), total = o_tab + (RH_STAMP_PLAN == 2 ? 0 : t_bytes);
     const uint32_t* crc = reinterpret_cast<const uint32_t*>(st + t_crc);
-    hipStream_t s = ctx->stream;
     rh::PoolScratch scratch(s);
     if (scratch.alloc(ctx, total) != hipSuccess) return rh::fail(RH_E_NOMEM, "rh_crc32c_stamp_host: device scratch");
     uint8_t* base = scratch.bytes();
-    RH_HIP(hipMemcpyAsync(base + o_img, buf + lo, span, hipMemcpyHostToDevice, s));
-    RH_HIP(hipMemcpyAsync(base + o_tab, st, t_crc, hipMemcpyHostToDevice, s));
-    rh_frames f{};
+    RH_HIP(hipMemcpyAsync(base + o_img + kPad, buf + lo, span, hipMemcpyHostToDevice, s));
     f.buf = base + o_img;
-    f.buf_len = span;
-    f.frame_off = reinterpret_cast<const uint64_t*>(base + o_tab + t_off);
-    f.frame_len = reinterpret_cast<const uint32_t*>(base + o_tab + t_len);
-    f.n = n;
-    f.init_state = 0xFFFFFFFFu;   // checksum.reset() before every entry (OUT:100-103)
-    f.crc_out = reinterpret_cast<uint32_t*>(base + o_tab + t_crc);
-    // STAMP also writes the device copy's trailers; only crc_out comes back.  Batches of short frames
-    // (a flush batch of log entries) go one lane per frame; long entries to the window / packed plans
-    int rc = max_len <= kSerialMaxFrame ? rh_crc_serial_launch(ctx, &f, RH_CRC_STAMP, s)
-                                        : rh_crc_launch_impl(ctx, &f, RH_CRC_STAMP, s);
-    if (rc == RH_OK) RH_HIP(hipMemcpyAsync(st + t_crc, base + o_tab + t_crc, n * 4, hipMemcpyDeviceToHost, s));
+    // STAMP also writes the device copy's trailers
+    int rc;
+    if (RH_STAMP_PLAN == 2) {   // the frame table and the CRCs through the staging's device mapping
+        uint8_t* dst = nullptr;
+        RH_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&dst), st, 0));
+        f.frame_off = reinterpret_cast<const uint64_t*>(dst + t_off);
+        f.frame_len = reinterpret_cast<const uint32_t*>(dst + t_len);
+        f.crc_out = reinterpret_cast<uint32_t*>(dst + t_crc);
+        // up to one window-kernel batch (512 frames, one workgroup) on the window kernel; more
+        // frames one lane each over many CUs (its single workgroup per 512 frames would serialise
+        // them; measured 996 frames: 88 vs 94 us per call)
+        rc = (n > 512 && max_len <= kSerialMaxFrame) ? rh_crc_serial_launch(ctx, &f, RH_CRC_STAMP, s)
+                                                   : rh_crc_launch_impl(ctx, &f, RH_CRC_STAMP, s, true);
+    } else {
+        RH_HIP(hipMemcpyAsync(base + o_tab, st, t_crc, hipMemcpyHostToDevice, s));
+        f.frame_off = reinterpret_cast<const uint64_t*>(base + o_tab + t_off);
+        f.frame_len = reinterpret_cast<const uint32_t*>(base + o_tab + t_len);
+        f.crc_out = reinterpret_cast<uint32_t*>(base + o_tab + t_crc);
+        rc = (RH_STAMP_PLAN == 0 && max_len <= kSerialMaxFrame) ? rh_crc_serial_launch(ctx, &f, RH_CRC_STAMP, s)
+                                                              : rh_crc_launch_impl(ctx, &f, RH_CRC_STAMP, s, true);
+        if (rc == RH_OK) RH_HIP(hipMemcpyAsync(st + t_crc, base + o_tab + t_crc, n * 4, hipMemcpyDeviceToHost, s));
+    }
     RH_HIP(hipStreamSynchronize(s));
     if (rc != RH_OK) return rc;
     for (uint64_t i = 0; i < n; ++i) {   // buf.putInt((int) checksum.getValue()): big-endian

@@ -232,7 +232,8 @@ int rh_table_lease(const rh::TableDev& t, int64_t now_nanos, int64_t timeout_ms,
                    hipStream_t stream);
 int rh_table_read(const rh::TableDev& t, uint32_t first, uint32_t n, uint8_t column, int64_t* d_out,
                   hipStream_t stream);
-int rh_crc_launch_impl(rh_ctx* ctx, const rh_frames* f, uint32_t flags, hipStream_t stream);
+// window_only: every frame on the window kernel (one launch, no packed pass): small batches
+int rh_crc_launch_impl(rh_ctx* ctx, const rh_frames* f, uint32_t flags, hipStream_t stream, bool window_only = false);
 // One lane per frame (crc_serial_kernel): small batches of well-formed frames (no bad bits / counts).
 int rh_crc_serial_launch(rh_ctx* ctx, const rh_frames* f, uint32_t flags, hipStream_t stream);
 int rh_crc_upload_tables(rh_ctx* ctx);
