@@ -119,6 +119,7 @@ struct rh_groups {
     int lpar[2] = {0, 0};       // the set appends go to
     bool lvalid[2] = {true, true};   // every row marked since the kind's last evaluation is listed
     uint64_t lmarks[2] = {0, 0};     // bound on the rows marked since then
+    uint64_t marks[2] = {0, 0};      // deltas of each kind since its last evaluation (lists or not)
     bool last_list = false;     // the last evaluation ran over the dirty-row lists (diagnostics)
     hipEvent_t tev[2] = {nullptr, nullptr};  // rh_groups_timing: around the evaluation
     bool timing = false, timed = false;
@@ -380,7 +381,10 @@ int evaluate(rh_groups* g, int mode, bool wall_on, const EvTargets& t, uint64_t*
         rc = rh_table_commit_lists(g->dev, mode, l, lw, ev, s);
     } else {
         if (m == 0) g->lvalid[1] = false;   // the tile kernel marks wdirty with plain stores
-        rc = rh_table_commit(g->dev, mode, ev, s);
+        // a quarter of the rows or more possibly dirty: the loads go out with the flag loads
+        uint64_t rows = 0;
+        for (const auto& tt : g->dev.tier) rows += tt.rows;
+        rc = rh_table_commit(g->dev, mode, ev, g->marks[m] * 4 >= rows, s);
     }
     if (rc == RH_OK && g->timing) {
         RH_HIP(hipEventRecord(g->tev[1], s));
@@ -394,6 +398,8 @@ int evaluate(rh_groups* g, int mode, bool wall_on, const EvTargets& t, uint64_t*
     *hbm = k == 1;
     g->lpar[m] ^= 1;  // ... and the other list set of this kind: fresh lists from here on
     g->lmarks[m] = 0;
+    if (m == 0) g->marks[1] += g->marks[0];   // rows whose commit advanced are marked for commitIndexChanged
+    g->marks[m] = 0;
     g->lvalid[m] = true;
     g->last_list = list;
     return RH_OK;
@@ -433,6 +439,8 @@ int ring_submit(rh_groups* g, int i, size_t n, bool has_set) {
     g->ring_next = i ^ 1;
     // every delta marks at most one row per kind
     const rh::TableLists lc = lists_for(g, 0, n), lw = lists_for(g, 1, n);
+    g->marks[0] += n;
+    g->marks[1] += n;
     if (has_set) {
         rc = rh_table_apply_deltas(g->dev, g->d_ring[i], n, 0, lc, lw, s);
         if (rc != RH_OK) return rc;

@@ -287,7 +287,13 @@ struct Stage {
     unsigned long long base;        // the block's range of the lists (both kinds packed)
 };
 
-template <int F, bool RANK, bool WATCH>
+// SPEC (chosen per evaluation by the host, rh_table_commit): the evaluation follows deltas that
+// may have marked a large part of the table, so nearly every tile and most of its column lines hold
+// a dirty row -- the column loads are issued with the flag load instead of after it (one dependent
+// HBM trip per wave fewer) and the tile summary is not consulted.  Measured (1M rows, same box,
+// profiles/r04/table_spec/): 100 % dirty 23.7 -> 22.2 us, but 4 % dirty 18.3 -> 21.4 us (clean
+// lines loaded): hence the host's choice.
+template <int F, bool RANK, bool WATCH, bool SPEC>
 __device__ __forceinline__ void table_wave(const TableDev& T, const TableTier& tt, uint64_t tl, bool wall_on,
                                            unsigned char* stage, Stage& sc) {
     constexpr int N = F + 1;
@@ -295,12 +301,12 @@ __device__ __forceinline__ void table_wave(const TableDev& T, const TableTier& t
     const int lane = threadIdx.x & 63;
     uint8_t* tb = tt.base + tl * TB;   // this wave's tile: rows 128 tl .. 128 tl + 127
     uint8_t* sump = tt.sum + 2 * tl + (WATCH ? 1 : 0);
-    if (RH_TABLE_SUMMARY && *sump == 0) return;  // clean tile: its flag line is not read
+    if (!SPEC && RH_TABLE_SUMMARY && *sump == 0) return;  // clean tile: its flag line is not read
     uint8_t* dflag = tb + (WATCH ? tile::kWdirty : tile::kDirty) + 2 * lane;
     const uint16_t dd = *reinterpret_cast<const uint16_t*>(dflag);
     const bool d0 = (dd & 0xFFu) != 0, d1 = (dd >> 8) != 0;
     const bool need = d0 || d1;
-    if (!__any(need)) {
+    if (!SPEC && !__any(need)) {
         if (lane == 0) *sump = 0;
         return;
     }
@@ -308,7 +314,7 @@ __device__ __forceinline__ void table_wave(const TableDev& T, const TableTier& t
     int64_t p0[2] = {0, 0}, p1[2] = {0, 0}, p2[2] = {0, 0};
     uint32_t w[2] = {0u, 0u}, slot[2] = {0u, 0u};
     const uint32_t l16 = 16u * lane, l8 = 8u * lane;
-    if (need) {  // every load of the row pair is issued before any result is used
+    if (SPEC || need) {  // every load of the row pair is issued before any result is used
 #pragma unroll
         for (int k = 0; k < F; ++k) {
             const v2i64 x = tload<v2i64>(tb + (WATCH ? tile::fcommit(F, k) : tile::match(k)) + l16);
@@ -419,13 +425,13 @@ __device__ __forceinline__ void table_wave(const TableDev& T, const TableTier& t
     if (lane == 0) sc.cnt[0][wave] = (uint32_t)(__popcll(a0) + __popcll(a1));
 }
 
-template <int F, int FHI, bool RANK, bool WATCH>
+template <int F, int FHI, bool RANK, bool WATCH, bool SPEC>
 __device__ __forceinline__ void table_dispatch(const TableDev& T, int t, uint64_t tl, bool wall_on,
                                                unsigned char* stage, Stage& sc) {
     if ((int)rh::width_of_tier(t) == F)
-        table_wave<F, RANK, WATCH>(T, T.tier[t], tl, wall_on, stage, sc);
+        table_wave<F, RANK, WATCH, SPEC>(T, T.tier[t], tl, wall_on, stage, sc);
     else if constexpr (F + 2 <= FHI)
-        table_dispatch<F + 2, FHI, RANK, WATCH>(T, t, tl, wall_on, stage, sc);
+        table_dispatch<F + 2, FHI, RANK, WATCH, SPEC>(T, t, tl, wall_on, stage, sc);
 }
 
 // The evaluation's counter word (rh_internal.h, TableEvents): kind 0 in bits [0, cbits), kind 1 in
@@ -453,7 +459,7 @@ __device__ __forceinline__ void block_done(const TableEvents& ev, unsigned long 
 }
 
 // One workgroup (block index b of the launch).
-template <bool WATCH, int FLO, int FHI>
+template <bool WATCH, int FLO, int FHI, bool SPEC>
 __device__ __forceinline__ void table_block_iter(const TableDev& T, const TierRange& tr, const TableEvents& ev,
                                                  uint32_t b, unsigned char* stage, Stage& sc) {
     const int wave = threadIdx.x >> 6;
@@ -468,7 +474,7 @@ __device__ __forceinline__ void table_block_iter(const TableDev& T, const TierRa
     if (b == 0 && threadIdx.x < rh::kTableTiers * rh::kHeads && ev.lheads_next)
         ev.lheads_next[threadIdx.x * rh::kHeadStride] = 0ull;  // the next list set of this kind
     __syncthreads();
-    if (tl * rh::kTileRows < T.tier[t].rows) table_dispatch<FLO, FHI, FLO <= 6, WATCH>(T, t, tl, wall_on, stage, sc);
+    if (tl * rh::kTileRows < T.tier[t].rows) table_dispatch<FLO, FHI, FLO <= 6, WATCH, SPEC>(T, t, tl, wall_on, stage, sc);
     __syncthreads();
 
     // ---- one range of each list per block (one device-scope atomic), then a contiguous copy
@@ -534,30 +540,30 @@ __device__ __forceinline__ void table_block_iter(const TableDev& T, const TierRa
     }
 }
 
-template <bool WATCH, int FLO, int FHI>
+template <bool WATCH, int FLO, int FHI, bool SPEC>
 __device__ __forceinline__ void table_commit_block(const TierRange& tr, const TableEvents& ev) {
     const TableDev& T = rh::kernarg_struct<TableDev>();  // block-uniform tier index: scalar loads
     // COMMIT: [0, 24 KiB) advanced records, [24, 48 KiB) watch-ALL records; WATCH: level records
     __shared__ __attribute__((aligned(16))) unsigned char stage[kTRows * sizeof(rh_watch_event)];
     __shared__ Stage sc;
-    table_block_iter<WATCH, FLO, FHI>(T, tr, ev, blockIdx.x, stage, sc);
+    table_block_iter<WATCH, FLO, FHI, SPEC>(T, tr, ev, blockIdx.x, stage, sc);
 }
 
 // Widths 2..6: rank-mask order statistics, 6 waves per SIMD (<= 84 VGPRs: the row pair's columns
 // are all in flight before the compute; at 64 VGPRs the compiler spilled 52 B per lane): two
 // 12-wave workgroups (2 x 48 KiB of event staging) per CU.  Widths 8..14: Batcher networks
 // (commit.hip's split) with the registers their 15-value networks need; these tiers are rare.
-template <bool WATCH>
+template <bool WATCH, bool SPEC>
 __global__ __launch_bounds__(kTBlock) __attribute__((amdgpu_waves_per_eu(RH_TABLE_WPE, 8))) void table_commit_kernel_rank(
     TableDev Targ, TierRange tr, TableEvents ev) {
     (void)Targ;
-    table_commit_block<WATCH, 2, 6>(tr, ev);
+    table_commit_block<WATCH, 2, 6, SPEC>(tr, ev);
 }
 
-template <bool WATCH>
+template <bool WATCH, bool SPEC>
 __global__ __launch_bounds__(kTBlock) void table_commit_kernel_net(TableDev Targ, TierRange tr, TableEvents ev) {
     (void)Targ;
-    table_commit_block<WATCH, 8, 14>(tr, ev);
+    table_commit_block<WATCH, 8, 14, SPEC>(tr, ev);
 }
 
 // ---- list mode: updateCommit / commitIndexChanged over the listed rows only ---------------------
@@ -831,7 +837,7 @@ static uint32_t class_blocks(const rh::TableDev& t, int cls) {
 
 uint32_t rh::table_commit_blocks(const rh::TableDev& t) { return class_blocks(t, 0) + class_blocks(t, 1); }
 
-int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev_in, hipStream_t stream) {
+int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev_in, bool spec, hipStream_t stream) {
     // one launch per width class over every non-empty tier of the class, widest tier first (a
     // joint-consensus tier's rows cost several times a stable row's compute: dispatched last they
     // were the launch's tail, commit.hip build_args)
@@ -855,11 +861,15 @@ int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev_i
         ev.done_target = cls == last_cls ? total : 0u;   // workgroups of both launches count
         const dim3 g(blocks), b(kTBlock);
         if (mode == RH_MODE_WATCH) {
-            if (cls == 0) hipLaunchKernelGGL(table_commit_kernel_rank<true>, g, b, 0, stream, t, tr, ev);
-            else hipLaunchKernelGGL(table_commit_kernel_net<true>, g, b, 0, stream, t, tr, ev);
+            if (cls == 0 && spec) hipLaunchKernelGGL((table_commit_kernel_rank<true, true>), g, b, 0, stream, t, tr, ev);
+            else if (cls == 0) hipLaunchKernelGGL((table_commit_kernel_rank<true, false>), g, b, 0, stream, t, tr, ev);
+            else if (spec) hipLaunchKernelGGL((table_commit_kernel_net<true, true>), g, b, 0, stream, t, tr, ev);
+            else hipLaunchKernelGGL((table_commit_kernel_net<true, false>), g, b, 0, stream, t, tr, ev);
         } else {
-            if (cls == 0) hipLaunchKernelGGL(table_commit_kernel_rank<false>, g, b, 0, stream, t, tr, ev);
-            else hipLaunchKernelGGL(table_commit_kernel_net<false>, g, b, 0, stream, t, tr, ev);
+            if (cls == 0 && spec) hipLaunchKernelGGL((table_commit_kernel_rank<false, true>), g, b, 0, stream, t, tr, ev);
+            else if (cls == 0) hipLaunchKernelGGL((table_commit_kernel_rank<false, false>), g, b, 0, stream, t, tr, ev);
+            else if (spec) hipLaunchKernelGGL((table_commit_kernel_net<false, true>), g, b, 0, stream, t, tr, ev);
+            else hipLaunchKernelGGL((table_commit_kernel_net<false, false>), g, b, 0, stream, t, tr, ev);
         }
         RH_HIP(hipGetLastError());
     }
