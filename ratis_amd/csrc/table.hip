@@ -437,7 +437,11 @@ __device__ __forceinline__ void table_dispatch(const TableDev& T, int t, uint64_
 // The evaluation's counter word (rh_internal.h, TableEvents): kind 0 in bits [0, cbits), kind 1 in
 // [cbits, 2 cbits), workgroups done above when the count fits there (`packed`; the list kernel
 // always: at most kListMaxGrid workgroups < 2^8).
-constexpr uint32_t kListMaxGrid = 240;
+#ifndef RH_LIST_WAVES   // A/B: waves per list-kernel workgroup (the grid keeps 960 waves)
+#define RH_LIST_WAVES 4
+#endif
+constexpr uint32_t kListWaves = RH_LIST_WAVES;
+constexpr uint32_t kListMaxGrid = 960 / kListWaves;   // < 2^8 workgroups: the done count's byte
 
 __device__ __forceinline__ void publish_counts(const TableEvents& ev, unsigned long long c) {
     const unsigned long long m = (1ull << ev.cbits) - 1;
@@ -630,7 +634,7 @@ __device__ __forceinline__ void list_row(const TableDev& T, const TableTier& tt,
 }
 
 template <bool WATCH>
-__global__ __launch_bounds__(256) void table_list_kernel(TableDev Targ, TableLists L, TableLists Lw, TableEvents ev) {
+__global__ __launch_bounds__(kListWaves * 64) void table_list_kernel(TableDev Targ, TableLists L, TableLists Lw, TableEvents ev) {
     const TableDev& T = rh::kernarg_struct<TableDev>();
     (void)Targ;
     constexpr int NR = rh::kTableTiers * rh::kHeads;
@@ -667,7 +671,7 @@ __global__ __launch_bounds__(256) void table_list_kernel(TableDev Targ, TableLis
     const uint64_t R = ev.cap;
     const bool wall_on = !WATCH && ev.wall != nullptr;
     const int wave = threadIdx.x >> 6;
-    __shared__ uint32_t wcnt[2][4];        // per pass: the waves' record counts
+    __shared__ uint32_t wcnt[2][kListWaves];   // per pass: the waves' record counts
     __shared__ unsigned long long lbase;   // per pass: the workgroup's range of the lists
     // entries are dealt out lane-major over EVERY wave of the grid (entry e -> wave e % W, pass
     // e / W): a sparse list keeps all CUs' memory pipelines busy instead of filling a few waves
@@ -719,8 +723,9 @@ __global__ __launch_bounds__(256) void table_list_kernel(TableDev Targ, TableLis
         if (threadIdx.x == 0) {
             const uint64_t w0 = (uint64_t)blockIdx.x * nw_per;   // this workgroup's wave 0, lane 0
             const bool last = (uint64_t)pass * W * 64 + w0 < N && (uint64_t)(pass + 1) * W * 64 + w0 >= N;
-            const unsigned long long s0 = wcnt[0][0] + wcnt[0][1] + wcnt[0][2] + wcnt[0][3];
-            const unsigned long long s1 = wcnt[1][0] + wcnt[1][1] + wcnt[1][2] + wcnt[1][3];
+            unsigned long long s0 = 0, s1 = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < kListWaves; ++k) s0 += wcnt[0][k], s1 += wcnt[1][k];
             const uint32_t cb = ev.cbits;
             const unsigned long long add = s0 | (s1 << cb) | (last ? 1ull << (2 * cb) : 0ull);
             const unsigned long long old = add ? atomicAdd(ev.cnt, add) : 0ull;
@@ -881,7 +886,7 @@ int rh_table_commit_lists(const rh::TableDev& t, int mode, const rh::TableLists&
     // the listed rows are dealt lane-major over every wave of a near-chip-wide grid: a few rows per
     // wave on ~every CU (random rows: the chain of dependent loads is latency-bound per CU, so the
     // rows are spread, not packed into few waves)
-    const dim3 g(kListMaxGrid), b(256);
+    const dim3 g(kListMaxGrid), b(kListWaves * 64);
     rh::TableEvents ev = ev_in;
     if (mode == RH_MODE_WATCH)
         hipLaunchKernelGGL(table_list_kernel<true>, g, b, 0, stream, t, l, rh::TableLists{}, ev);
