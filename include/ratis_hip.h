@@ -445,6 +445,12 @@ int rh_host_unregister(rh_ctx* ctx, void* p);
  * per-entry call sites prefer batching frames through rh_crc32c_frames_launch (RH_CRC_STAMP /
  * RH_CRC_VERIFY); this entry serves the odd single span (e.g. a snapshot-file checksum). */
 int rh_crc32c(rh_ctx* ctx, uint32_t crc_state, const void* data, uint64_t n, uint32_t* out_state);
+/* The SURVEY 8(b) `rh_crc32c` contract as a pure host function: Checksum.update over one span on
+ * PureJavaCrc32C's internal state (0xFFFFFFFF after reset(); getValue() = ~state), returning the
+ * new state.  Pure and reentrant, no context, no device (the CPU's CRC32 instruction, SSE4.2, or a
+ * byte table without it); NULL or empty spans return crc_state.  For one-off spans -- the batched
+ * paths above stay on the GPU. */
+uint32_t rh_crc32c_update(uint32_t crc_state, const void* data, uint64_t n);
 
 /* ---- leader lease (LeaderStateImpl.hasLease LSI:1229-1249; LeaderLease LL:60-103) ------------
  * One tier = groups with the same follower-slot count F (0..14), same conf word as the commit

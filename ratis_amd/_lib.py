@@ -255,6 +255,7 @@ _SIGNATURES = {
                                      POINTER(c_uint64)]),
     "rh_crc32c_frames_launch": (c_int, [c_void_p, POINTER(RhFrames), c_uint32, c_void_p]),
     "rh_crc32c": (c_int, [c_void_p, c_uint32, c_void_p, c_uint64, POINTER(c_uint32)]),
+    "rh_crc32c_update": (c_uint32, [c_uint32, c_void_p, c_uint64]),
     "rh_crc32c_stamp_host": (c_int, [c_void_p, c_void_p, c_uint64, c_void_p, c_void_p, c_uint64]),
     "rh_host_register": (c_int, [c_void_p, c_void_p, c_uint64]),
     "rh_host_unregister": (c_int, [c_void_p, c_void_p]),

@@ -181,6 +181,50 @@ RH_EXPORT int rh_segments_read_launch(rh_ctx* ctx, const rh_segments* segs, cons
     return rh_segments_read_impl(ctx, segs, crc, pick_stream(ctx, stream));
 }
 
+// ---- single span on the host: the SURVEY 8(b) rh_crc32c contract (pure, reentrant) -------------
+// PureJavaCrc32C's register (PJC:54-91: c = (c >>> 8) ^ T[(c ^ b) & 0xff], reflected Castagnoli
+// polynomial 0x82F63B78, no inversion inside update) is exactly what the SSE4.2 CRC32 instruction
+// advances, 8 bytes per instruction; without it, a byte-wise table built once.  Not a fallback of the
+// batched paths: those stay on the GPU; this serves the odd single span where a PCIe round trip would
+// cost more than the span (a snapshot file's checksum, a Java caller's one-off update).
+namespace {
+const uint32_t* host_crc_table() {
+    static const std::vector<uint32_t> t = [] {
+        std::vector<uint32_t> v(256);
+        for (uint32_t b = 0; b < 256; ++b) {
+            uint32_t c = b;
+            for (int k = 0; k < 8; ++k) c = (c >> 1) ^ (0x82F63B78u & (0u - (c & 1u)));
+            v[b] = c;
+        }
+        return v;
+    }();
+    return t.data();
+}
+
+__attribute__((target("sse4.2"))) uint32_t crc_sse42(uint32_t c, const uint8_t* p, uint64_t n) {
+    uint64_t c64 = c;
+    for (; n && (reinterpret_cast<uintptr_t>(p) & 7); --n) c64 = __builtin_ia32_crc32qi((uint32_t)c64, *p++);
+    for (; n >= 8; n -= 8, p += 8) {
+        uint64_t w;
+        std::memcpy(&w, p, 8);
+        c64 = __builtin_ia32_crc32di(c64, w);
+    }
+    for (; n; --n) c64 = __builtin_ia32_crc32qi((uint32_t)c64, *p++);
+    return (uint32_t)c64;
+}
+}  // namespace
+
+RH_EXPORT uint32_t rh_crc32c_update(uint32_t crc_state, const void* data, uint64_t n) {
+    const uint8_t* p = static_cast<const uint8_t*>(data);
+    if (!p || n == 0) return crc_state;
+    static const bool sse42 = __builtin_cpu_supports("sse4.2");
+    if (sse42) return crc_sse42(crc_state, p, n);
+    const uint32_t* t = host_crc_table();
+    uint32_t c = crc_state;
+    for (uint64_t i = 0; i < n; ++i) c = (c >> 8) ^ t[(c ^ p[i]) & 0xffu];
+    return c;
+}
+
 RH_EXPORT int rh_crc32c(rh_ctx* ctx, uint32_t crc_state, const void* data, uint64_t n, uint32_t* out_state) {
     if (!ctx || !out_state) return rh::fail(RH_E_INVAL, "rh_crc32c: ctx/out_state == NULL");
     if (n && !data) return rh::fail(RH_E_INVAL, "rh_crc32c: data == NULL");

@@ -383,6 +383,13 @@ def crc32c_update(ctx: Context, state: int, data: bytes) -> int:
     return out.value
 
 
+def crc32c_update_host(state: int, data: bytes) -> int:
+    """``rh_crc32c_update``: the same on the host (pure, no context or device; SURVEY 8(b)'s
+    ``rh_crc32c``).  Returns the new state."""
+    buf = ctypes.create_string_buffer(bytes(data), max(1, len(data)))
+    return int(_lib.load().rh_crc32c_update(state & 0xFFFFFFFF, buf, len(data)))
+
+
 # ---- segment framing ---------------------------------------------------------------------------
 RH_SEG_E_CHECKSUM = -2   # read_segments only: the first frame whose CRC does not verify
 

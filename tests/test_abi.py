@@ -135,3 +135,31 @@ def test_struct_layouts_match_header(tmp_path):
         for fname, _ in cls._fields_:
             assert int(vals[f"{cname}.{fname}"]) == getattr(cls, fname).offset, (cname, fname)
     assert int(vals["conf"]) == _lib.conf_pack(0x5, True, True, 0x3, True, True)
+
+
+def test_host_crc32c_update_matches_the_oracle(orc):
+    """rh_crc32c_update (SURVEY 8(b)'s pure host rh_crc32c: Checksum.update on PureJavaCrc32C's
+    internal state) against the oracle's PJC restatement: RFC 3720 answers through getValue(),
+    chained updates over every alignment and span length near the 8-byte steps, and the NULL /
+    empty spans.  A host function: runs here, without a GPU."""
+    import json
+
+    import numpy as np
+
+    from ratis_amd import engine
+    ref = json.load(open(os.path.join(ROOT, "tests", "golden", "crc_reference.json")))
+    for v in ref["rfc3720"]:
+        st = engine.crc32c_update_host(0xFFFFFFFF, bytes.fromhex(v["hex"]))
+        assert (~st) & 0xFFFFFFFF == int(v["crc"], 16), v["name"]
+    rng = np.random.default_rng(5)
+    data = rng.integers(0, 256, size=5000, dtype=np.uint8).tobytes()
+    for a in range(0, 17):
+        for n in (0, 1, 7, 8, 9, 15, 16, 17, 63, 64, 65, 1000):
+            st0 = int(rng.integers(0, 1 << 32))
+            assert engine.crc32c_update_host(st0, data[a:a + n]) == orc.crc32c_update(st0, data[a:a + n]), (a, n)
+    st = 0xFFFFFFFF
+    for a, b in ((0, 3), (3, 11), (11, 4000), (4000, 5000)):
+        st = engine.crc32c_update_host(st, data[a:b])
+    assert (~st) & 0xFFFFFFFF == orc.crc32c(data)
+    from ratis_amd import _lib
+    assert _lib.load().rh_crc32c_update(0x1234, None, 10) == 0x1234
