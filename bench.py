@@ -371,8 +371,9 @@ def table_commit_leg(ctx, host, reps: int = 8, fracs=(1.0, 0.1, 0.01), pmc=None)
     groups dirty (one matchIndex / flushIndex update per dirty group, as delta_streaming's steps).
     One evaluation = one kernel that evaluates the dirty rows and writes its event records straight
     into the result lists (the tile kernel over every 128-row tile, or the list kernel over the
-    dirty-row lists when few rows can be dirty); the library's timing events (rh_groups_timing) time
-    it on the table's own stream, HIP events around rh_commit_batch_async the call.  Every sink:
+    dirty-row lists when few rows can be dirty); the library's timing events (rh_groups_timing: HIP
+    events on the evaluation's own launch, stamped at its kernel boundaries by hipExtLaunchKernel)
+    time it on the table's stream, HIP events around rh_commit_batch_async the call.  Every sink:
     RH_EVENTS_HOST_MAPPED (the lists are pinned host memory, written across PCIe), RH_EVENTS_DEVICE
     (the lists in HBM, _wait copies the counted prefix) and RH_EVENTS_AUTO (the default, what the
     Java module and rh_node run: DEVICE for tile evaluations, HOST_MAPPED for list evaluations).

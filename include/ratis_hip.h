@@ -287,8 +287,9 @@ int rh_commit_batch_wait(rh_groups* g, uint64_t ticket, rh_commit_out* out);
 #define RH_EVENTS_DEVICE      1
 #define RH_EVENTS_AUTO        2
 int rh_groups_set_event_sink(rh_groups* g, int sink);
-/* Diagnostics (benchmarks, tests): with timing enabled every evaluation records HIP events around
- * its evaluation kernel(s); rh_groups_last_timing returns the last evaluation's device time in ms
+/* Diagnostics (benchmarks, tests): with timing enabled every evaluation's kernel launch(es) carry HIP
+ * events stamped at the dispatch's start and completion (hipExtLaunchKernel: the kernel boundaries,
+ * as a profiler reports them); rh_groups_last_timing returns the last evaluation's device time in ms
  * (blocks until it has completed; RH_E_STATE before any timed evaluation) and, if list_evaluated is
  * not NULL, whether it ran over the dirty-row lists (1: only the rows marked since the previous
  * evaluation of its kind were visited; 0: every tile). */

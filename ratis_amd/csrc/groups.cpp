@@ -370,7 +370,7 @@ int evaluate(rh_groups* g, int mode, bool wall_on, const EvTargets& t, uint64_t*
     ev.counts_out = counts_out;
     ev.cbits = g->cbits;
     ev.lheads_next = lheads_of(g, m, g->lpar[m] ^ 1);
-    if (g->timing) RH_HIP(hipEventRecord(g->tev[0], s));
+    hipEvent_t t0 = g->timing ? g->tev[0] : nullptr, t1 = g->timing ? g->tev[1] : nullptr;
     if (list) {
         rh::TableLists l;
         l.rows = g->d_lrows[m];
@@ -378,18 +378,15 @@ int evaluate(rh_groups* g, int mode, bool wall_on, const EvTargets& t, uint64_t*
         l.cap = g->lcap;
         // COMMIT marks the rows whose commit advanced for commitIndexChanged: at most the listed ones
         const rh::TableLists lw = m == 0 ? lists_for(g, 1, g->lmarks[0]) : rh::TableLists{};
-        rc = rh_table_commit_lists(g->dev, mode, l, lw, ev, s);
+        rc = rh_table_commit_lists(g->dev, mode, l, lw, ev, s, t0, t1);
     } else {
         if (m == 0) g->lvalid[1] = false;   // the tile kernel marks wdirty with plain stores
         // a quarter of the rows or more possibly dirty: the loads go out with the flag loads
         uint64_t rows = 0;
         for (const auto& tt : g->dev.tier) rows += tt.rows;
-        rc = rh_table_commit(g->dev, mode, ev, g->marks[m] * 4 >= rows, s);
+        rc = rh_table_commit(g->dev, mode, ev, g->marks[m] * 4 >= rows, s, t0, t1);
     }
-    if (rc == RH_OK && g->timing) {
-        RH_HIP(hipEventRecord(g->tev[1], s));
-        g->timed = true;
-    }
+    if (rc == RH_OK && g->timing) g->timed = true;
     if (rc != RH_OK) {
         const std::string msg = rh_last_error();
         (void)reset_heads(g);

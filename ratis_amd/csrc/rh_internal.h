@@ -222,11 +222,13 @@ int rh_table_apply_deltas(const rh::TableDev& t, const rh_delta* d_deltas, uint6
                           const rh::TableLists& lc, const rh::TableLists& lw, hipStream_t stream);
 // List-mode evaluation of the listed rows of one kind (mode); COMMIT appends the rows whose commit
 // advanced to the watch list `lw` (when it is maintained).  Events as rh_table_commit.
+// t0 / t1 (may be null): timing events stamped at the evaluation's kernel boundaries.
 int rh_table_commit_lists(const rh::TableDev& t, int mode, const rh::TableLists& l, const rh::TableLists& lw,
-                          const rh::TableEvents& ev, hipStream_t stream);
+                          const rh::TableEvents& ev, hipStream_t stream, hipEvent_t t0, hipEvent_t t1);
 int rh_table_control(const rh::TableDev& t, const rh::CtrlOp* d_ops, uint64_t n, hipStream_t stream);
 // spec: issue every column load with the dirty-flag load (a large part of the table is dirty).
-int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev, bool spec, hipStream_t stream);
+int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev, bool spec, hipStream_t stream,
+                    hipEvent_t t0, hipEvent_t t1);
 // Initialises tiles [first_tile, n_tiles) of a tier as free rows (conf 0, row_slot kNoRow, clean).
 int rh_table_init_tiles(const rh::TableTier& t, uint32_t first_tile, uint32_t n_tiles, hipStream_t stream);
 int rh_table_lease(const rh::TableDev& t, int64_t now_nanos, int64_t timeout_ms, uint64_t* d_slot_bits,

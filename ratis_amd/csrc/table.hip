@@ -21,6 +21,8 @@
 // Rows of a tier are laid out in 128-row tiles (rh_internal.h, tile::), the TILED layout of the
 // raw rh_commit_soa kernels; the per-group arithmetic is commit_eval.h's, shared with them.
 // Integer compare/select work, no MFMA; HBM-bound over the dirty rows.
+#include <hip/hip_ext.h>
+
 #include "rh_internal.h"
 #include "commit_eval.h"
 #include "lease_eval.h"
@@ -842,11 +844,23 @@ static uint32_t class_blocks(const rh::TableDev& t, int cls) {
 
 uint32_t rh::table_commit_blocks(const rh::TableDev& t) { return class_blocks(t, 0) + class_blocks(t, 1); }
 
-int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev_in, bool spec, hipStream_t stream) {
+// Evaluation launches.  With timing events (rh_groups_timing) hipExtLaunchKernel stamps them at
+// the dispatch's own start and completion (the kernel boundaries rocprof reports), not as separate
+// stream packets around it: t0 on the evaluation's first launch, t1 on its last.
+template <typename K, typename... A>
+hipError_t eval_launch(K kernel, dim3 g, dim3 b, hipStream_t stream, hipEvent_t t0, hipEvent_t t1, A... args) {
+    if (t0 || t1) hipExtLaunchKernelGGL(kernel, g, b, 0, stream, t0, t1, 0u, args...);
+    else hipLaunchKernelGGL(kernel, g, b, 0, stream, args...);
+    return hipGetLastError();
+}
+
+int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev_in, bool spec, hipStream_t stream,
+                    hipEvent_t t0, hipEvent_t t1) {
     // one launch per width class over every non-empty tier of the class, widest tier first (a
     // joint-consensus tier's rows cost several times a stable row's compute: dispatched last they
     // were the launch's tail, commit.hip build_args)
     rh::TableEvents ev = ev_in;
+    const int first_cls = class_blocks(t, 0) ? 0 : 1;
     const int last_cls = class_blocks(t, 1) ? 1 : 0;   // its launch publishes the list lengths
     const uint32_t total = rh::table_commit_blocks(t);
     // the done count rides in the counter word when the evaluation's workgroups fit above the counts
@@ -865,34 +879,37 @@ int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev_i
         if (blocks == 0) continue;
         ev.done_target = cls == last_cls ? total : 0u;   // workgroups of both launches count
         const dim3 g(blocks), b(kTBlock);
+        const hipEvent_t a0 = cls == first_cls ? t0 : nullptr, a1 = cls == last_cls ? t1 : nullptr;
+        hipError_t e;
         if (mode == RH_MODE_WATCH) {
-            if (cls == 0 && spec) hipLaunchKernelGGL((table_commit_kernel_rank<true, true>), g, b, 0, stream, t, tr, ev);
-            else if (cls == 0) hipLaunchKernelGGL((table_commit_kernel_rank<true, false>), g, b, 0, stream, t, tr, ev);
-            else if (spec) hipLaunchKernelGGL((table_commit_kernel_net<true, true>), g, b, 0, stream, t, tr, ev);
-            else hipLaunchKernelGGL((table_commit_kernel_net<true, false>), g, b, 0, stream, t, tr, ev);
+            if (cls == 0 && spec) e = eval_launch(table_commit_kernel_rank<true, true>, g, b, stream, a0, a1, t, tr, ev);
+            else if (cls == 0) e = eval_launch(table_commit_kernel_rank<true, false>, g, b, stream, a0, a1, t, tr, ev);
+            else if (spec) e = eval_launch(table_commit_kernel_net<true, true>, g, b, stream, a0, a1, t, tr, ev);
+            else e = eval_launch(table_commit_kernel_net<true, false>, g, b, stream, a0, a1, t, tr, ev);
         } else {
-            if (cls == 0 && spec) hipLaunchKernelGGL((table_commit_kernel_rank<false, true>), g, b, 0, stream, t, tr, ev);
-            else if (cls == 0) hipLaunchKernelGGL((table_commit_kernel_rank<false, false>), g, b, 0, stream, t, tr, ev);
-            else if (spec) hipLaunchKernelGGL((table_commit_kernel_net<false, true>), g, b, 0, stream, t, tr, ev);
-            else hipLaunchKernelGGL((table_commit_kernel_net<false, false>), g, b, 0, stream, t, tr, ev);
+            if (cls == 0 && spec) e = eval_launch(table_commit_kernel_rank<false, true>, g, b, stream, a0, a1, t, tr, ev);
+            else if (cls == 0) e = eval_launch(table_commit_kernel_rank<false, false>, g, b, stream, a0, a1, t, tr, ev);
+            else if (spec) e = eval_launch(table_commit_kernel_net<false, true>, g, b, stream, a0, a1, t, tr, ev);
+            else e = eval_launch(table_commit_kernel_net<false, false>, g, b, stream, a0, a1, t, tr, ev);
         }
-        RH_HIP(hipGetLastError());
+        RH_HIP(e);
     }
     return RH_OK;
 }
 
 int rh_table_commit_lists(const rh::TableDev& t, int mode, const rh::TableLists& l, const rh::TableLists& lw,
-                          const rh::TableEvents& ev_in, hipStream_t stream) {
+                          const rh::TableEvents& ev_in, hipStream_t stream, hipEvent_t t0, hipEvent_t t1) {
     // the listed rows are dealt lane-major over every wave of a near-chip-wide grid: a few rows per
     // wave on ~every CU (random rows: the chain of dependent loads is latency-bound per CU, so the
     // rows are spread, not packed into few waves)
     const dim3 g(kListMaxGrid), b(kListWaves * 64);
     rh::TableEvents ev = ev_in;
+    hipError_t e;
     if (mode == RH_MODE_WATCH)
-        hipLaunchKernelGGL(table_list_kernel<true>, g, b, 0, stream, t, l, rh::TableLists{}, ev);
+        e = eval_launch(table_list_kernel<true>, g, b, stream, t0, t1, t, l, rh::TableLists{}, ev);
     else
-        hipLaunchKernelGGL(table_list_kernel<false>, g, b, 0, stream, t, l, lw, ev);
-    RH_HIP(hipGetLastError());
+        e = eval_launch(table_list_kernel<false>, g, b, stream, t0, t1, t, l, lw, ev);
+    RH_HIP(e);
     return RH_OK;
 }
 
