@@ -381,10 +381,17 @@ int evaluate(rh_groups* g, int mode, bool wall_on, const EvTargets& t, uint64_t*
         rc = rh_table_commit_lists(g->dev, mode, l, lw, ev, s, t0, t1);
     } else {
         if (m == 0) g->lvalid[1] = false;   // the tile kernel marks wdirty with plain stores
-        // a quarter of the rows or more possibly dirty: the loads go out with the flag loads
+        // tiles at or past a tier's high-water mark hold no row ever handed out (clean): the
+        // evaluation covers the tiles below it only
+        rh::TableDev ed = g->dev;
         uint64_t rows = 0;
-        for (const auto& tt : g->dev.tier) rows += tt.rows;
-        rc = rh_table_commit(g->dev, mode, ev, g->marks[m] * 4 >= rows, s, t0, t1);
+        for (int t = 0; t < rh::kTableTiers; ++t) {
+            const uint64_t hw = ((uint64_t)g->tiers[t].hw + rh::kTileRows - 1) / rh::kTileRows * rh::kTileRows;
+            ed.tier[t].rows = (uint32_t)std::min<uint64_t>(ed.tier[t].rows, hw);
+            rows += ed.tier[t].rows;
+        }
+        // a quarter of the rows or more possibly dirty: the loads go out with the flag loads
+        rc = rh_table_commit(ed, mode, ev, g->marks[m] * 4 >= rows, s, t0, t1);
     }
     if (rc == RH_OK && g->timing) g->timed = true;
     if (rc != RH_OK) {
