@@ -187,7 +187,7 @@ def captured(launches, steps: int, ctx, use_graph: bool):
     return run, "stream"
 
 
-def delta_streaming(ctx, host, steps: int = 12, fill_threads: int = 16, reps: int = 5) -> dict:
+def delta_streaming(ctx, host, steps: int = 12, fill_threads: int = 16, reps: int = 5, sink=None) -> dict:
     """The operating mode the Java module uses: one resident RaftGroupTable (stable F=4 and joint
     F=6 tiers), FollowerInfo / flush-index updates written in place into the pinned delta ring
     (rh_deltas_acquire / submit: H2D + device apply, which marks the touched groups dirty), then
@@ -200,6 +200,8 @@ def delta_streaming(ctx, host, steps: int = 12, fill_threads: int = 16, reps: in
     rng = np.random.default_rng(99)
     n_all = sum(h.n for h in host)
     tab = groups.RaftGroupTable(ctx, capacity=n_all)
+    if sink is not None:
+        tab.set_event_sink(sink)
     first, bases = 0, []
     for h in host:
         tab.load(first, h.conf, h.flush, h.commit, h.term_start, match=h.follower)

@@ -279,10 +279,11 @@ int rh_commit_batch_wait(rh_groups* g, uint64_t ticket, rh_commit_out* out);
  * pinned memory.  HOST_MAPPED: the lists are the pinned result buffers themselves (PCIe writes by
  * the GPU), visible when the ticket completes.  DEVICE: the lists are in HBM (112 B x capacity) and
  * rh_commit_batch_wait / rh_watch_levels_wait copy the counted prefix into the same pinned buffers
- * (a D2H on the table's copy stream).  AUTO (the default): per evaluation, DEVICE when it visits
- * every tile (up to one record per row: the kernel writes at HBM speed and the copy engine moves
- * the lists) and HOST_MAPPED when it runs over the dirty-row lists (few records: no copy).  Results
- * are identical.  Not while an evaluation is outstanding (RH_E_STATE). */
+ * (a D2H on the table's copy stream).  AUTO (the default): an evaluation over every tile (up to one
+ * record per row) writes HBM lists at HBM speed and a drain kernel on a side stream moves the
+ * counted prefixes into the pinned buffers across PCIe while the table stream goes on (the ticket
+ * completes after it; no host-issued copy); an evaluation over the dirty-row lists (few records)
+ * writes the pinned buffers directly.  Results are identical.  Not while an evaluation is outstanding (RH_E_STATE). */
 #define RH_EVENTS_HOST_MAPPED 0
 #define RH_EVENTS_DEVICE      1
 #define RH_EVENTS_AUTO        2

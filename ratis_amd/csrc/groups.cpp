@@ -96,7 +96,10 @@ struct rh_groups {
     bool ring_used[2] = {false, false};
     int ring_next = 0;
     int ring_acquired = -1;
-    hipStream_t copy_stream = nullptr;
+    hipStream_t copy_stream = nullptr;       // H2D of delta slots and control ops
+    hipStream_t d2h_stream = nullptr;        // the result lists' way to the host: RH_EVENTS_DEVICE's D2H in
+                                             // _wait, RH_EVENTS_AUTO's drain kernel after the evaluation
+    hipEvent_t evaluated = nullptr;          // recorded after an evaluation: orders the drain behind it
     uint64_t* d_lbits = nullptr;  // rh_lease_batch: slot bitmap (device) and its pinned copy
     uint64_t* h_lbits = nullptr;
     // events (rh_internal.h, TableEvents): the evaluation counter words, result sets
@@ -190,6 +193,8 @@ void free_groups(rh_groups* g) {
         if (e) (void)hipEventDestroy(e);
     (void)hipFree(g->d_read);
     if (g->copy_stream) (void)hipStreamDestroy(g->copy_stream);
+    if (g->d2h_stream) (void)hipStreamDestroy(g->d2h_stream);
+    if (g->evaluated) (void)hipEventDestroy(g->evaluated);
     (void)hipFree(g->d_lbits);
     if (g->h_lbits) (void)hipHostFree(g->h_lbits);
 }
@@ -489,6 +494,10 @@ RH_EXPORT int rh_groups_create(rh_ctx* ctx, uint64_t capacity, int64_t gap_thres
     if (rc == RH_OK) rc = dalloc(&g->dev.slot_map, capacity);
     if (rc == RH_OK && hipMemsetAsync(g->dev.slot_map, 0xFF, capacity * 4, s) != hipSuccess)
         rc = rh::fail(RH_E_DEVICE, "rh_groups_create: init");
+    if (rc == RH_OK && hipStreamCreateWithFlags(&g->d2h_stream, hipStreamNonBlocking) != hipSuccess)
+        rc = rh::fail(RH_E_DEVICE, "rh_groups_create: result copy stream");
+    if (rc == RH_OK && hipEventCreateWithFlags(&g->evaluated, hipEventDisableTiming) != hipSuccess)
+        rc = rh::fail(RH_E_DEVICE, "rh_groups_create: evaluation event");
     if (rc == RH_OK && hipStreamCreateWithFlags(&g->copy_stream, hipStreamNonBlocking) != hipSuccess)
         rc = rh::fail(RH_E_DEVICE, "rh_groups_create: copy stream");
     for (int i = 0; i < 2 && rc == RH_OK; ++i) {
@@ -551,6 +560,7 @@ RH_EXPORT int rh_groups_destroy(rh_groups* g) {
     DeviceGuard dg(g->ctx->device);
     (void)hipStreamSynchronize(g->ctx->stream);
     if (g->copy_stream) (void)hipStreamSynchronize(g->copy_stream);
+    if (g->d2h_stream) (void)hipStreamSynchronize(g->d2h_stream);
     free_groups(g);
     delete g;
     return RH_OK;
@@ -889,7 +899,17 @@ RH_EXPORT int rh_commit_batch_async(rh_groups* g, uint32_t flags, uint64_t* tick
     bool hbm = false;
     int rc = evaluate(g, RH_MODE_COMMIT, wall_on, t, e.d_cnt, e.h_cnt, &hbm);
     if (rc != RH_OK) return rc;
-    RH_HIP(hipEventRecord(e.done, g->ctx->stream));
+    if (hbm && g->event_sink == RH_EVENTS_AUTO) {   // drained into the pinned lists on the side stream
+        RH_HIP(hipEventRecord(g->evaluated, g->ctx->stream));
+        RH_HIP(hipStreamWaitEvent(g->d2h_stream, g->evaluated, 0));
+        rc = rh_table_drain(e.d_cnt, e.hbm_adv, e.d_adv, wall_on ? e.hbm_wall : nullptr, e.d_wall, 16, g->capacity,
+                            g->d2h_stream);
+        if (rc != RH_OK) return rc;
+        RH_HIP(hipEventRecord(e.done, g->d2h_stream));
+        hbm = false;   // nothing left for _wait to copy
+    } else {
+        RH_HIP(hipEventRecord(e.done, g->ctx->stream));
+    }
     e.ticket = tk;
     e.hbm = hbm;
     e.pending = true;
@@ -913,7 +933,7 @@ RH_EXPORT int rh_commit_batch_wait(rh_groups* g, uint64_t ticket, rh_commit_out*
     const uint64_t nw = std::min<uint64_t>(e->h_cnt[1], g->capacity);
     if (e->hbm) {  // lists in HBM: the counted prefixes to the pinned result buffers
         e->hbm = false;
-        hipStream_t s = g->copy_stream;
+        hipStream_t s = g->d2h_stream;
         if (na) RH_HIP(hipMemcpyAsync(e->adv, e->hbm_adv, na * sizeof(rh_index_event), hipMemcpyDeviceToHost, s));
         if (nw) RH_HIP(hipMemcpyAsync(e->wall, e->hbm_wall, nw * sizeof(rh_index_event), hipMemcpyDeviceToHost, s));
         if (na || nw) RH_HIP(hipStreamSynchronize(s));
@@ -944,7 +964,16 @@ RH_EXPORT int rh_watch_levels_async(rh_groups* g) {
     bool hbm = false;
     int rc = evaluate(g, RH_MODE_WATCH, false, t, g->d_wcnt, g->h_wcnt, &hbm);
     if (rc != RH_OK) return rc;
-    RH_HIP(hipEventRecord(g->wdone, g->ctx->stream));
+    if (hbm && g->event_sink == RH_EVENTS_AUTO) {   // drained into the pinned list on the side stream
+        RH_HIP(hipEventRecord(g->evaluated, g->ctx->stream));
+        RH_HIP(hipStreamWaitEvent(g->d2h_stream, g->evaluated, 0));
+        rc = rh_table_drain(g->d_wcnt, g->hbm_watch, g->d_watch, nullptr, nullptr, 32, g->capacity, g->d2h_stream);
+        if (rc != RH_OK) return rc;
+        RH_HIP(hipEventRecord(g->wdone, g->d2h_stream));
+        hbm = false;
+    } else {
+        RH_HIP(hipEventRecord(g->wdone, g->ctx->stream));
+    }
     g->whbm = hbm;
     g->wpending = true;
     return RH_OK;
@@ -958,8 +987,8 @@ RH_EXPORT int rh_watch_levels_wait(rh_groups* g, const rh_watch_event** out_even
     RH_HIP(hipEventSynchronize(g->wdone));
     const uint64_t n = std::min<uint64_t>(g->h_wcnt[0], g->capacity);
     if (g->whbm && n) {
-        RH_HIP(hipMemcpyAsync(g->watch, g->hbm_watch, n * sizeof(rh_watch_event), hipMemcpyDeviceToHost, g->copy_stream));
-        RH_HIP(hipStreamSynchronize(g->copy_stream));
+        RH_HIP(hipMemcpyAsync(g->watch, g->hbm_watch, n * sizeof(rh_watch_event), hipMemcpyDeviceToHost, g->d2h_stream));
+        RH_HIP(hipStreamSynchronize(g->d2h_stream));
     }
     g->wpending = false;
     *out_events = g->watch;

@@ -229,6 +229,12 @@ int rh_table_control(const rh::TableDev& t, const rh::CtrlOp* d_ops, uint64_t n,
 // spec: issue every column load with the dirty-flag load (a large part of the table is dirty).
 int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev, bool spec, hipStream_t stream,
                     hipEvent_t t0, hipEvent_t t1);
+// Copies the counted prefixes of HBM result lists into the pinned lists (device pointers of the
+// host mapping): list a (records of rec_bytes0 = 16 or 32 B, length counts[0]) and, if b is not
+// null, list b (16 B records, length counts[1]); counts = the host-mapped lengths the evaluation
+// published.  Enqueued on `stream` (ordered after the evaluation by the caller).
+int rh_table_drain(const uint64_t* counts, const void* a, void* a_out, const void* b, void* b_out, uint32_t rec_bytes0,
+                   uint64_t cap, hipStream_t stream);
 // Initialises tiles [first_tile, n_tiles) of a tier as free rows (conf 0, row_slot kNoRow, clean).
 int rh_table_init_tiles(const rh::TableTier& t, uint32_t first_tile, uint32_t n_tiles, hipStream_t stream);
 int rh_table_lease(const rh::TableDev& t, int64_t now_nanos, int64_t timeout_ms, uint64_t* d_slot_bits,

@@ -913,6 +913,31 @@ int rh_table_commit_lists(const rh::TableDev& t, int mode, const rh::TableLists&
     return RH_OK;
 }
 
+// ---- AUTO sink: a tile evaluation's HBM lists drained into the pinned lists ------------------------
+// On its own stream after the evaluation: the counted prefixes (lengths from the host-mapped counts
+// the evaluation published) move across PCIe as GPU writes, 16 B per thread and step, while the table
+// stream goes on (the next deltas' apply, the next evaluation) and no host thread issues a copy.
+__global__ __launch_bounds__(256) void table_drain_kernel(const uint64_t* __restrict__ counts, const uint4* __restrict__ a,
+                                                          uint4* __restrict__ a_out, const uint4* __restrict__ b,
+                                                          uint4* __restrict__ b_out, uint32_t words0, uint64_t cap) {
+    const uint64_t n0 = (counts[0] < cap ? counts[0] : cap) * words0;
+    const uint64_t n1 = b ? (counts[1] < cap ? counts[1] : cap) : 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n0 + n1; j += stride) {
+        if (j < n0) a_out[j] = a[j];
+        else b_out[j - n0] = b[j - n0];
+    }
+}
+
+int rh_table_drain(const uint64_t* counts, const void* a, void* a_out, const void* b, void* b_out, uint32_t rec_bytes0,
+                   uint64_t cap, hipStream_t stream) {
+    hipLaunchKernelGGL(table_drain_kernel, dim3(512), dim3(256), 0, stream, counts, static_cast<const uint4*>(a),
+                       static_cast<uint4*>(a_out), static_cast<const uint4*>(b), static_cast<uint4*>(b_out),
+                       rec_bytes0 / 16u, cap);
+    RH_HIP(hipGetLastError());
+    return RH_OK;
+}
+
 int rh_table_init_tiles(const rh::TableTier& t, uint32_t first_tile, uint32_t n_tiles, hipStream_t stream) {
     if (n_tiles == 0) return RH_OK;
     hipLaunchKernelGGL(table_init_tiles_kernel, dim3(n_tiles), dim3(rh::kTileRows), 0, stream, t, first_tile);
