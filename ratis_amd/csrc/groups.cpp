@@ -116,8 +116,8 @@ struct rh_groups {
     hipEvent_t ldone = nullptr;               // rh_lease_batch_async's bitmap D2H
     bool lpending = false;
     // dirty-row lists (rh_internal.h, TableLists), per kind (0 = updateCommit, 1 = commitIndexChanged)
-    uint32_t* d_lrows[2] = {nullptr, nullptr};   // [kTableTiers][kHeads][lcap]
-    unsigned long long* d_lheads = nullptr;      // [2 kinds][2 sets][kTableTiers * kHeads * kHeadStride]
+    uint32_t* d_lrows[2] = {nullptr, nullptr};   // [kHeads][lcap]: (tier << 28) | row
+    unsigned long long* d_lheads = nullptr;      // [2 kinds][2 sets][kHeads * kHeadStride]
     uint32_t lcap = 0;
     int lpar[2] = {0, 0};       // the set appends go to
     bool lvalid[2] = {true, true};   // every row marked since the kind's last evaluation is listed
@@ -304,7 +304,7 @@ int queue_op(rh_groups* g, const CtrlOp& op) {
 
 uint32_t enc(int t, uint32_t row) { return ((uint32_t)t << 28) | row; }
 
-constexpr size_t kListRegions = (size_t)rh::kTableTiers * rh::kHeads;
+constexpr size_t kListRegions = (size_t)rh::kHeads;   // one list region per XCD head (entries carry their tier)
 
 unsigned long long* lheads_of(rh_groups* g, int kind, int set) {
     return g->d_lheads + (size_t)(kind * 2 + set) * kListRegions * rh::kHeadStride;

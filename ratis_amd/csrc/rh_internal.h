@@ -163,13 +163,14 @@ struct TableEvents {
 // DIRTY-ROW LISTS (list mode).  While the host knows that few rows can be dirty (the deltas and
 // control ops since the last evaluation of a kind bound the rows they can mark), every 0 -> 1
 // transition of a row's dirty / wdirty flag (found with a 32-bit atomicOr on the flag's word) also
-// appends the row to a list, per (tier, head): kHeads regions of `cap` entries per tier, each with its
-// own head word.  The evaluation then runs over the listed rows only (table_list_kernel: work
-// proportional to the dirty rows, not to the table).  Two head sets per kind alternate like the
-// event heads: appends go to `heads`; the evaluation that consumes them clears the other set.
+// appends the row to a list: kHeads regions (one per XCD head, the writer's blockIdx & 7) of `cap`
+// entries, each with its own head word; an entry is (tier << 28) | row.  The evaluation then runs
+// over the listed rows only (table_list_kernel: work proportional to the dirty rows, not to the
+// table).  Two head sets per kind alternate: appends go to `heads`; the evaluation that consumes
+// them clears the other set.
 struct TableLists {
-    uint32_t* rows = nullptr;            // [kTableTiers][kHeads][cap] row indices within the tier
-    unsigned long long* heads = nullptr; // [kTableTiers][kHeads] words, kHeadStride apart (null: no list)
+    uint32_t* rows = nullptr;            // [kHeads][cap] entries: (tier << 28) | row within the tier
+    unsigned long long* heads = nullptr; // [kHeads] words, kHeadStride apart (null: no list)
     uint32_t cap = 0;
 };
 

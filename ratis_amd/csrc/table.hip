@@ -73,27 +73,20 @@ __device__ __forceinline__ bool mark_listed(const TableTier& tt, uint64_t r, int
     return ((old >> sh) & 0xFFu) == 0u;
 }
 
-// Appends the rows of the lanes with `want` to list l, region (tier t, head h): one returning
-// atomic per (wave, tier) present.  Every lane of the wave must call it (ballots).
+// Appends the rows of the lanes with `want` to list l, region h (an XCD head): one returning
+// atomic per wave.  An entry is the row with its tier in the top 4 bits (rh::kRowMask below).
+// Every lane of the wave must call it (ballot).
 __device__ __forceinline__ void list_append(const TableLists& l, bool want, int t, uint32_t row, uint32_t h) {
     const int lane = threadIdx.x & 63;
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    uint64_t pend = __ballot(want);
-    while (pend) {
-        const int leader = __ffsll((long long)pend) - 1;
-        const int tl = __shfl(t, leader);
-        const bool mine = want && t == tl;
-        const uint64_t grp = __ballot(mine);
-        const uint32_t reg = (uint32_t)tl * rh::kHeads + h;
-        uint32_t base = 0;
-        if (lane == leader)
-            base = (uint32_t)atomicAdd(l.heads + (uint64_t)reg * rh::kHeadStride, (unsigned long long)__popcll(grp));
-        base = (uint32_t)__shfl((int)base, leader);
-        if (mine) {
-            const uint32_t idx = base + (uint32_t)__popcll(grp & lt);
-            if (idx < l.cap) l.rows[(uint64_t)reg * l.cap + idx] = row;   // the host's bound keeps idx < cap
-        }
-        pend &= ~grp;
+    const uint64_t grp = __ballot(want);
+    if (!grp) return;
+    uint32_t base = 0;
+    if (lane == 0) base = (uint32_t)atomicAdd(l.heads + (uint64_t)h * rh::kHeadStride, (unsigned long long)__popcll(grp));
+    base = (uint32_t)__shfl((int)base, 0);
+    if (want) {
+        const uint32_t idx = base + (uint32_t)__popcll(grp & lt);
+        if (idx < l.cap) l.rows[(uint64_t)h * l.cap + idx] = ((uint32_t)t << 28) | row;   // the host's bound keeps idx < cap
     }
 }
 
@@ -477,7 +470,7 @@ __device__ __forceinline__ void table_block_iter(const TableDev& T, const TierRa
     const int t = tr.tier[i];
     const uint64_t tl = (uint64_t)(b - tr.block_begin[i]) * kTWaves + wave;   // tile of this wave
     if (threadIdx.x < 2 * kTWaves) (&sc.cnt[0][0])[threadIdx.x] = 0u;
-    if (b == 0 && threadIdx.x < rh::kTableTiers * rh::kHeads && ev.lheads_next)
+    if (b == 0 && threadIdx.x < rh::kHeads && ev.lheads_next)
         ev.lheads_next[threadIdx.x * rh::kHeadStride] = 0ull;  // the next list set of this kind
     __syncthreads();
     if (tl * rh::kTileRows < T.tier[t].rows) table_dispatch<FLO, FHI, FLO <= 6, WATCH, SPEC>(T, t, tl, wall_on, stage, sc);
@@ -575,9 +568,15 @@ __global__ __launch_bounds__(kTBlock) void table_commit_kernel_net(TableDev Targ
 // ---- list mode: updateCommit / commitIndexChanged over the listed rows only ---------------------
 // One lane per listed row (random rows: each lane loads its row's 8-byte column elements).  The
 // lanes of a wave may hold rows of different tiers (widths): the row evaluation is instantiated per
-// width and the wave runs the widths its lanes hold.  Events: per pass one counter atomic per
+// width and the wave runs the widths its lanes hold.  Entries are dealt per region: wave wg takes
+// head region r = wg % kHeads at rank k = wg / kHeads, and in pass p lane j takes the region's
+// entry (64 p + j) Wr + k (Wr = the region's waves: a sparse list spreads over all of them, a few
+// rows per wave on nearly every CU) -- so a wave loads its region's count and its first entries in
+// one trip (the entries speculatively, below the capacity), with no scan of the counts before the
+// rows are loaded; wave 0 of each workgroup loads all eight counts for the bookkeeping (passes,
+// workgroups holding entries, this workgroup's last pass).  Events: per pass one counter atomic per
 // workgroup (its waves' counts summed in LDS), records written straight into the result lists;
-// the last pass's atomic also counts the workgroup done (the counter word's top byte), so the
+// the last pass's atomic also counts the workgroup done (the counter word's top bits), so the
 // workgroup that completes the count knows the list lengths from its own atomic's return.
 template <int F, bool WATCH>
 __device__ __forceinline__ void list_row(const TableDev& T, const TableTier& tt, uint32_t r, bool wall_on,
@@ -635,74 +634,97 @@ __device__ __forceinline__ void list_row(const TableDev& T, const TableTier& tt,
     }
 }
 
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) v = max(v, (uint32_t)__shfl_xor((int)v, d));
+    return v;
+}
+
 template <bool WATCH>
 __global__ __launch_bounds__(kListWaves * 64) void table_list_kernel(TableDev Targ, TableLists L, TableLists Lw, TableEvents ev) {
     const TableDev& T = rh::kernarg_struct<TableDev>();
     (void)Targ;
-    constexpr int NR = rh::kTableTiers * rh::kHeads;
-    __shared__ uint32_t pre[NR + 1];
+    constexpr uint32_t NR = rh::kHeads;
     // lanes pick tiers per row: from LDS, not by per-lane loads of the kernarg segment
     __shared__ __attribute__((aligned(16))) unsigned char tiers_mem[sizeof(TableTier) * rh::kTableTiers];
     TableTier* tiers = reinterpret_cast<TableTier*>(tiers_mem);
-    static_assert(NR < 64, "one wave scans the region counts");
+    __shared__ uint32_t wcnt[2][kListWaves];   // per pass: the waves' record counts
+    __shared__ unsigned long long lbase;       // per pass: the workgroup's range of the lists
+    __shared__ uint32_t book[3];               // passes, workgroups holding entries, this one's last pass + 1
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t W = gridDim.x * kListWaves, wg = blockIdx.x * kListWaves + (uint32_t)wave;
+    const uint32_t r = wg % NR, k = wg / NR, Wr = (W - r + NR - 1) / NR;
+    // one trip: this wave's region count and first entries; wave 0 also every region's count
+    const unsigned long long hr = L.heads[(uint64_t)r * rh::kHeadStride];
+    const uint32_t i0 = (uint32_t)lane * Wr + k;
+    const uint32_t ent0 = i0 < L.cap ? L.rows[(uint64_t)r * L.cap + i0] : 0u;
+    uint32_t cl = 0;
+    if (wave == 0 && lane < (int)NR) {
+        const unsigned long long x = L.heads[(uint64_t)lane * rh::kHeadStride];
+        cl = (uint32_t)(x < L.cap ? x : L.cap);
+    }
     if (threadIdx.x == 64) {
 #pragma unroll
-        for (int k = 0; k < rh::kTableTiers; ++k) tiers[k] = T.tier[k];   // uniform index: scalar loads
-    }
-    if (threadIdx.x < 64) {   // wave 0: inclusive scan of the region counts across its lanes
-        uint32_t c = 0;
-        if (threadIdx.x < NR) {
-            const unsigned long long x = L.heads[(uint64_t)threadIdx.x * rh::kHeadStride];
-            c = (uint32_t)(x < L.cap ? x : L.cap);
-        }
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = (uint32_t)__shfl_up((int)c, d);
-            if ((int)threadIdx.x >= d) c += y;
-        }
-        if (threadIdx.x < NR) pre[threadIdx.x + 1] = c;
-        if (threadIdx.x == 0) pre[0] = 0;
+        for (int q = 0; q < rh::kTableTiers; ++q) tiers[q] = T.tier[q];   // uniform index: scalar loads
     }
     if (blockIdx.x == 0 && threadIdx.x < NR && ev.lheads_next)
         ev.lheads_next[(uint64_t)threadIdx.x * rh::kHeadStride] = 0ull;   // the next list set of this kind
-    __syncthreads();
-    const uint32_t N = pre[NR];
-    const int lane = threadIdx.x & 63;
+    const uint32_t cnt = (uint32_t)(hr < L.cap ? hr : L.cap);
+    if (wave == 0) {
+        // wave g holds entries in pass p iff 64 p Wr(g % NR) + g / NR < count[g % NR]
+        uint32_t np = 0;
+        if (lane < (int)NR) {
+            const uint32_t wr = (W - (uint32_t)lane + NR - 1) / NR;
+            np = (cl + wr * 64u - 1) / (wr * 64u);
+        }
+        np = wave_max_u32(np);
+        uint32_t act = 0;
+        for (uint32_t b0 = 0; b0 < gridDim.x; b0 += 64) {   // uniform trip count: every lane shuffles
+            const uint32_t b = b0 + (uint32_t)lane;
+            bool any = false;
+#pragma unroll
+            for (uint32_t w = 0; w < kListWaves; ++w) {
+                const uint32_t g = b * kListWaves + w;
+                const uint32_t cg = (uint32_t)__shfl((int)cl, (int)(g % NR));
+                any |= b < gridDim.x && g / NR < cg;
+            }
+            act += (uint32_t)__popcll(__ballot(any));
+        }
+        // this workgroup's last pass holding entries, + 1 (0: none): lane w < kListWaves for wave w
+        const uint32_t g = blockIdx.x * kListWaves + (uint32_t)(lane % kListWaves), rg = g % NR, kg = g / NR;
+        const uint32_t wr = (W - rg + NR - 1) / NR;
+        const uint32_t cg = (uint32_t)__shfl((int)cl, (int)rg);
+        uint32_t lp1 = kg < cg ? (cg - 1 - kg) / (wr * 64u) + 1 : 0u;
+        lp1 = wave_max_u32(lane < (int)kListWaves ? lp1 : 0u);
+        if (lane == 0) {
+            book[0] = np;
+            book[1] = act;
+            book[2] = lp1;
+        }
+    }
+    __syncthreads();   // the tier table and the bookkeeping (the loads above are still in flight)
+    const uint32_t np = book[0], active = book[1], lp1 = book[2];
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const uint32_t h = blockIdx.x & (rh::kHeads - 1);   // the watch-list region rows are appended to
     const uint64_t R = ev.cap;
     const bool wall_on = !WATCH && ev.wall != nullptr;
-    const int wave = threadIdx.x >> 6;
-    __shared__ uint32_t wcnt[2][kListWaves];   // per pass: the waves' record counts
-    __shared__ unsigned long long lbase;   // per pass: the workgroup's range of the lists
-    // entries are dealt out lane-major over EVERY wave of the grid (entry e -> wave e % W, pass
-    // e / W): a sparse list keeps all CUs' memory pipelines busy instead of filling a few waves
-    const uint32_t W = gridDim.x * (blockDim.x >> 6);
-    const uint32_t wg = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    // Workgroup b holds entries iff its wave 4b does (lane 0, pass 0): the first min(grid, ceil(N / 4))
-    // workgroups.  Each counts itself done in its last pass holding entries; the one completing
-    // that count publishes.  An empty list: workgroup 0 publishes zero lengths.
-    if (N == 0) {
+    const bool wl = Lw.rows != nullptr;
+    if (active == 0) {   // empty lists
         if (blockIdx.x == 0 && threadIdx.x == 0) publish_counts(ev, 0ull);
         return;
     }
-    const uint32_t nw_per = blockDim.x >> 6;
-    const uint64_t active = (N + nw_per - 1) / nw_per < gridDim.x ? (N + nw_per - 1) / nw_per : gridDim.x;
-    for (uint32_t pass = 0; (uint64_t)pass * W * 64 < N; ++pass) {
-        const uint32_t e = (pass * 64 + (uint32_t)lane) * W + wg;
+    for (uint32_t pass = 0; pass < np; ++pass) {
+        const uint32_t idx = (pass * 64u + (uint32_t)lane) * Wr + k;
+        const bool has = idx < cnt;
         bool e0 = false, e1 = false, wtrans = false;
         int64_t x0 = 0, x1 = 0, x2 = 0;
         uint32_t valid = 0, slot = 0, row = 0;
         int t = 0;
-        if (e < N) {
-            int rg = 0;   // the region holding entry e: the last r with pre[r] <= e
-#pragma unroll
-            for (int step = 32; step > 0; step >>= 1)
-                if (rg + step <= NR - 1 && pre[rg + step] <= e) rg += step;
-            t = rg / rh::kHeads;
-            row = L.rows[(uint64_t)rg * L.cap + (e - pre[rg])];
-            const TableTier tt = tiers[t];
-            const bool wl = Lw.rows != nullptr;
+        if (has) {
+            const uint32_t ent = pass == 0 ? ent0 : L.rows[(uint64_t)r * L.cap + idx];
+            t = (int)(ent >> 28);
+            row = ent & rh::kRowMask;
+            const TableTier tt = tiers[t < rh::kTableTiers ? t : 0];
             switch (tt.width) {
                 case 2: list_row<2, WATCH>(T, tt, row, wall_on, wl, e0, e1, wtrans, x0, x1, x2, valid, slot); break;
                 case 4: list_row<4, WATCH>(T, tt, row, wall_on, wl, e0, e1, wtrans, x0, x1, x2, valid, slot); break;
@@ -721,13 +743,12 @@ __global__ __launch_bounds__(kListWaves * 64) void table_list_kernel(TableDev Ta
         }
         __syncthreads();
         // the watch list's appends and the counter atomic are in flight together
-        if (!WATCH && Lw.rows) list_append(Lw, wtrans, t, row, h);   // kernel argument: uniform
+        if (!WATCH && wl) list_append(Lw, wtrans, t, row, h);   // kernel argument: uniform
         if (threadIdx.x == 0) {
-            const uint64_t w0 = (uint64_t)blockIdx.x * nw_per;   // this workgroup's wave 0, lane 0
-            const bool last = (uint64_t)pass * W * 64 + w0 < N && (uint64_t)(pass + 1) * W * 64 + w0 >= N;
+            const bool last = pass + 1 == lp1;
             unsigned long long s0 = 0, s1 = 0;
 #pragma unroll
-            for (uint32_t k = 0; k < kListWaves; ++k) s0 += wcnt[0][k], s1 += wcnt[1][k];
+            for (uint32_t q = 0; q < kListWaves; ++q) s0 += wcnt[0][q], s1 += wcnt[1][q];
             const uint32_t cb = ev.cbits;
             const unsigned long long add = s0 | (s1 << cb) | (last ? 1ull << (2 * cb) : 0ull);
             const unsigned long long old = add ? atomicAdd(ev.cnt, add) : 0ull;
@@ -740,20 +761,20 @@ __global__ __launch_bounds__(kListWaves * 64) void table_list_kernel(TableDev Ta
         __syncthreads();
         const unsigned long long cm = (1ull << ev.cbits) - 1;
         uint32_t b0 = (uint32_t)(lbase & cm), b1 = (uint32_t)((lbase >> ev.cbits) & cm);
-        for (int k = 0; k < wave; ++k) b0 += wcnt[0][k], b1 += wcnt[1][k];
-        __syncthreads();   // wcnt / lbase are the next pass's
+        for (int q = 0; q < wave; ++q) b0 += wcnt[0][q], b1 += wcnt[1][q];
+        if (pass + 1 < np) __syncthreads();   // wcnt / lbase are the next pass's (np: uniform)
         if (e0) {
-            const uint64_t k = b0 + (uint64_t)__popcll(a & lt);
-            if (k < R) {
+            const uint64_t kk = b0 + (uint64_t)__popcll(a & lt);
+            if (kk < R) {
                 if (WATCH)
-                    ev.watch[k] = rh_watch_event{slot, valid, x0, x1, x2};
+                    ev.watch[kk] = rh_watch_event{slot, valid, x0, x1, x2};
                 else
-                    ev.adv[k] = rh_index_event{slot, 0u, x0};
+                    ev.adv[kk] = rh_index_event{slot, 0u, x0};
             }
         }
         if (!WATCH && e1) {
-            const uint64_t k = b1 + (uint64_t)__popcll(c & lt);
-            if (k < R) ev.wall[k] = rh_index_event{slot, 0u, x1};
+            const uint64_t kk = b1 + (uint64_t)__popcll(c & lt);
+            if (kk < R) ev.wall[kk] = rh_index_event{slot, 0u, x1};
         }
     }
 }
