@@ -145,7 +145,7 @@ struct CtrlOp {
 // evaluation's count (done_target: the workgroups of every launch of it) writes the two list
 // lengths to counts_out (host-mapped) and zeroes the words for the next evaluation: no gather
 // pass, no memset, no count read-back on the stream.
-constexpr int kHeads = 8;          // list regions per tier (dirty-row lists, below)
+constexpr int kHeads = 8;          // dirty-row list regions, one per XCD head (below)
 constexpr int kHeadStride = 32;    // u64 words between head / counter words: each on its own 256-B line
 struct TableEvents {
     rh_index_event* adv = nullptr;     // COMMIT: advanced (the result list)
