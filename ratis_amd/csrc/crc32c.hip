@@ -241,15 +241,35 @@ __device__ __forceinline__ uint32_t lds_word(const uint32_t*, uint32_t byte_addr
     return *reinterpret_cast<lds_u32_t*>(static_cast<uintptr_t>(byte_addr));
 }
 
-__device__ __forceinline__ uint32_t fold_word_perm(const uint32_t* lds, uint32_t r, uint32_t w,
-                                                   const uint32_t (&lb)[4]) {
-    const uint32_t x = r ^ w;
+// a ^ b ^ c in one VALU op (gfx950 v_bitop3_b32, truth table 0x96)
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// The register after folding one word: x = register ^ word (the word's bytes already XOR-ed in);
+// returns that register ^ `wn` -- with wn = the next word this is the next step's x, so a word costs
+// four v_perm and two bitop3 (the four lookups and the next word joined in two 3-input XORs).
+__device__ __forceinline__ uint32_t fold_x(const uint32_t* lds, uint32_t x, const uint32_t (&lb)[4], uint32_t wn) {
     // selector: out byte0 = lb.b0 (0), byte1 = x.byte j (4 + j), byte2 = lb.b2 (2), byte3 = lb.b3 (3)
     const uint32_t a3 = __builtin_amdgcn_perm(x, lb[3], 0x03020400u);  // byte 0 of x -> T3
     const uint32_t a2 = __builtin_amdgcn_perm(x, lb[2], 0x03020500u);  // byte 1 -> T2
     const uint32_t a1 = __builtin_amdgcn_perm(x, lb[1], 0x03020600u);  // byte 2 -> T1
     const uint32_t a0 = __builtin_amdgcn_perm(x, lb[0], 0x03020700u);  // byte 3 -> T0
-    return lds_word(lds, a3) ^ lds_word(lds, a2) ^ lds_word(lds, a1) ^ lds_word(lds, a0);
+    return xor3(xor3(lds_word(lds, a3), lds_word(lds, a2), lds_word(lds, a1)), lds_word(lds, a0), wn);
+}
+
+// zshift(tab, r) ^ extra
+__device__ __forceinline__ uint32_t zshift_x(const uint32_t* tab, uint32_t r, uint32_t extra) {
+    return xor3(xor3(tab[r & 0xffu], tab[256 + ((r >> 8) & 0xffu)], tab[512 + ((r >> 16) & 0xffu)]), tab[768 + (r >> 24)],
+                extra);
+}
+
+// A lane table's map of the register r (8 nibble-indexed lookups, copy c of each table entry).
+__device__ __forceinline__ uint32_t lane_advance(const uint32_t* tab, uint32_t c, uint32_t r) {
+    uint32_t t[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t[k] = tab[c + ((uint32_t)(k * 16) + ((r >> (4 * k)) & 15u)) * 32u];
+    return xor3(xor3(xor3(t[0], t[1], t[2]), t[3], t[4]), t[5], t[6]) ^ t[7];
 }
 
 // Start of a frame inside a lane's chunk: the chunk's aligned words d[0..16] start q0l bytes
@@ -473,32 +493,31 @@ __global__ __launch_bounds__(kCrcThreads) void crc_frames_kernel(FrameArgs a) {
             // Horner steps over 64 / CH zero bytes: CRC(A||B) = adv_|B|(crc A) ^ crc B from zero
             constexpr int LW = 16 / CH;
             uint32_t rc[CH];
-#pragma unroll
-            for (int q = 0; q < CH; ++q) rc[q] = 0;
             if (__all(sh == 0 || !act)) {
 #pragma unroll
+                for (int q = 0; q < CH; ++q) rc[q] = d[q * LW];
+#pragma unroll
                 for (int j = 0; j < LW; ++j)
 #pragma unroll
-                    for (int q = 0; q < CH; ++q) rc[q] = fold_word_perm(lds, rc[q], d[q * LW + j], lb);
+                    for (int q = 0; q < CH; ++q) rc[q] = fold_x(lds, rc[q], lb, j + 1 < LW ? d[q * LW + j + 1] : 0u);
             } else {
+                auto wd = [&](int q, int j) { return __builtin_amdgcn_alignbyte(d[q * LW + j + 1], d[q * LW + j], sh); };
+#pragma unroll
+                for (int q = 0; q < CH; ++q) rc[q] = wd(q, 0);
 #pragma unroll
                 for (int j = 0; j < LW; ++j)
 #pragma unroll
-                    for (int q = 0; q < CH; ++q)
-                        rc[q] = fold_word_perm(lds, rc[q], __builtin_amdgcn_alignbyte(d[q * LW + j + 1], d[q * LW + j], sh), lb);
+                    for (int q = 0; q < CH; ++q) rc[q] = fold_x(lds, rc[q], lb, j + 1 < LW ? wd(q, j + 1) : 0u);
             }
             uint32_t r = rc[0];
 #pragma unroll
-            for (int q = 1; q < CH; ++q) r = zshift(lch, r) ^ rc[q];
-            uint32_t z = 0;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) z ^= llane[c + ((uint32_t)(k * 16) + ((r >> (4 * k)) & 15u)) * 32u];
-            r = act ? z : 0u;
+            for (int q = 1; q < CH; ++q) r = zshift_x(lch, r, rc[q]);
+            r = act ? lane_advance(llane, c, r) : 0u;
             r ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
             r ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
             r ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r, 0x141, 0xF, 0xF, false);  // row_half_mirror
             r ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r, 0x140, 0xF, 0xF, false);  // row_mirror
-            R = zshift(lzw, R) ^ r;
+            R = zshift_x(lzw, R, r);
             if ((int64_t)x.wi + 1 >= nw) {
                 if (gl == Q - 1) {  // this lane's chunk ends at E: d[16..17] hold bytes E - sh .. E + 8 - sh
                     const uint64_t f = LISTED ? (uint64_t)mf[x.j] : b0f + x.j;
@@ -870,33 +889,30 @@ __global__ __launch_bounds__(kCrcThreads) void crc_lanes_kernel(LaneArgs a) {
         const bool act = valid && be > x.r.o;
         const int64_t q0l = be - 64 - (int64_t)sh - x.r.o;
         if (__any(act && q0l < 4)) mask_frame_start(d, q0l, act && q0l < 4, a.init);
-        uint32_t r0 = Q == 1 ? R : 0u, r1 = 0;  // two chains of 8 words, joined over 32 zero bytes
-        if (__all(sh == 0 || !act)) {
+        // two chains of 8 words, joined over 32 zero bytes
+        auto chains = [&](auto W) {
+            uint32_t x0 = (Q == 1 ? R : 0u) ^ W(0), x1 = W(8);
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                r0 = fold_word_perm(lds, r0, d[j], lb);
-                r1 = fold_word_perm(lds, r1, d[8 + j], lb);
+                x0 = fold_x(lds, x0, lb, j < 7 ? W(j + 1) : 0u);
+                x1 = fold_x(lds, x1, lb, j < 7 ? W(9 + j) : 0u);
             }
-        } else {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                r0 = fold_word_perm(lds, r0, __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh), lb);
-                r1 = fold_word_perm(lds, r1, __builtin_amdgcn_alignbyte(d[9 + j], d[8 + j], sh), lb);
-            }
-        }
-        uint32_t r = zshift(lch, r0) ^ r1;
+            return zshift_x(lch, x0, x1);
+        };
+        uint32_t r;
+        if (__all(sh == 0 || !act))
+            r = chains([&](int i) { return d[i]; });
+        else
+            r = chains([&](int i) { return __builtin_amdgcn_alignbyte(d[i + 1], d[i], sh); });
         if constexpr (Q == 1) {
             R = act ? r : 0u;
         } else {
-            uint32_t z = 0;
-#pragma unroll
-            for (int k = 0; k < 8; ++k) z ^= llane[c + ((uint32_t)(k * 16) + ((r >> (4 * k)) & 15u)) * 32u];
-            r = act ? z : 0u;
+            r = act ? lane_advance(llane, c, r) : 0u;
             r ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r, 0xB1, 0xF, 0xF, false);  // quad_perm [1,0,3,2]
             if constexpr (Q >= 4) r ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r, 0x4E, 0xF, 0xF, false);
             if constexpr (Q >= 8) r ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r, 0x141, 0xF, 0xF, false);
             if constexpr (Q >= 16) r ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)r, 0x140, 0xF, 0xF, false);
-            R = zshift(lzw, R) ^ r;
+            R = zshift_x(lzw, R, r);
         }
         if (x.k + 1 == x.nmax) {  // every frame of the group ends at this step
             if (valid && gl == Q - 1) {  // the lane whose chunk ends at E
@@ -971,7 +987,13 @@ hipError_t launch_lanes(const LaneArgs& l, uint64_t n, uint64_t cus, hipStream_t
 // are one contiguous run when its frames are contiguous (a segment's frame table).
 // Frames the fast path cannot load safely, malformed ones and spans over kCrcInitSpan go to a list
 // for the window kernel (crc_frames_kernel<true>).
-constexpr int kPackWaves = kCrcThreads / 64;
+// Steps of loads in flight per wave beyond the one being folded: 1 (two register sets, 16 waves
+// per CU) or 2 (three sets; the registers that takes allow 12 waves per CU).
+#ifndef RH_PACK_DEPTH
+#define RH_PACK_DEPTH 1
+#endif
+constexpr int kPackThreads = RH_PACK_DEPTH >= 2 ? 768 : kCrcThreads;
+constexpr int kPackWaves = kPackThreads / 64;
 constexpr int kPackTabBytes = 128 * 1024 + 4096 + 16384;  // slicing tables, 32-byte join, lane maps
 constexpr int kPackLds = kPackTabBytes + kPackWaves * 512;  // + per wave: 64 step marks, 64 frame values
 static_assert(kPackLds <= 160 * 1024, "LDS budget");
@@ -1032,16 +1054,17 @@ __device__ __forceinline__ void load_chunk(const uint8_t* src, uint32_t (&d)[17]
     d[16] = *reinterpret_cast<const uint32_t*>(src + 64);
 }
 
-// CRC register of the 16 words (from zero): two chains of 8 joined over 32 zero bytes.
+// CRC register of the 16 words (from zero), XOR `extra`: two chains of 8 joined over 32 zero bytes
+// (`extra` rides in the second chain's last fold).
 __device__ __forceinline__ uint32_t fold16(const uint32_t* lds, const uint32_t* lch, const uint32_t (&w)[16],
-                                           const uint32_t (&lb)[4]) {
-    uint32_t r0 = 0, r1 = 0;
+                                           const uint32_t (&lb)[4], uint32_t extra = 0u) {
+    uint32_t x0 = w[0], x1 = w[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-        r0 = fold_word_perm(lds, r0, w[j], lb);
-        r1 = fold_word_perm(lds, r1, w[8 + j], lb);
+        x0 = fold_x(lds, x0, lb, j < 7 ? w[j + 1] : 0u);
+        x1 = fold_x(lds, x1, lb, j < 7 ? w[9 + j] : extra);
     }
-    return zshift(lch, r0) ^ r1;
+    return zshift_x(lch, x0, x1);
 }
 
 // A/B: 1 folds chunk 0 in the steps (a per-lane mask on every word of every step) instead of one
@@ -1053,7 +1076,7 @@ __device__ __forceinline__ uint32_t fold16(const uint32_t* lds, const uint32_t* 
 #endif
 
 template <bool SLOT>
-__global__ __launch_bounds__(kCrcThreads) void crc_pack_kernel(PackArgs pk_arg) {
+__global__ __launch_bounds__(kPackThreads) void crc_pack_kernel(PackArgs pk_arg) {
     // slot variant: fields read from the kernarg segment where used (scalar loads the compiler can
     // repeat), not held in SGPRs across the step loop -- its extra pointers spilled
     const PackArgs& p = SLOT ? rh::kernarg_struct<PackArgs>() : pk_arg;
@@ -1230,17 +1253,12 @@ __global__ __launch_bounds__(kCrcThreads) void crc_pack_kernel(PackArgs pk_arg) 
         };
         const uint32_t nsteps = (T + 63) >> 6;
         uint32_t carry = 0;  // register of the frame running past the previous step (at its end)
-        Step cur{};
-        uint32_t dc[17];
-        if (nsteps) {
-            cur = map(0, 0);
-            load(cur, dc);
-        }
-        for (uint32_t s = 0; s < nsteps; ++s) {
-            Step nx{};
-            uint32_t dn[17];
-            if (s + 1 < nsteps) {
-                nx = map(s + 1, (uint32_t)__builtin_amdgcn_readlane((int)cur.j, 63));
+        // one step: fold `cur` (its chunk in dc) while step s + D's map and loads go out into nx / dn
+        // (pm: step s + D - 1, whose last lane's frame carries into step s + D)
+        constexpr uint32_t D = RH_PACK_DEPTH;
+        auto step = [&](uint32_t s, Step& cur, uint32_t (&dc)[17], const Step& pm, Step& nx, uint32_t (&dn)[17]) {
+            if (s + D < nsteps) {
+                nx = map(s + D, (uint32_t)__builtin_amdgcn_readlane((int)pm.j, 63));
                 load(nx, dn);
             }
             uint32_t w[16];
@@ -1252,14 +1270,10 @@ __global__ __launch_bounds__(kCrcThreads) void crc_pack_kernel(PackArgs pk_arg) 
                     w[i] &= (uint32_t)(~0ull << kk);
                 }
             }
-            uint32_t R = fold16(lds, lch, w, lb);
-            if (!RH_PACK_C0STEP) R ^= cur.i == 1u ? cur.fs : 0u;
+            const uint32_t R = fold16(lds, lch, w, lb, !RH_PACK_C0STEP && cur.i == 1u ? cur.fs : 0u);
             const uint32_t K0 = zshift_uniform(p.z2k, carry);  // off the step's dependent chain
             const uint32_t C4 = zshift_uniform(p.z4k, carry);
-            uint32_t y = 0;
-#pragma unroll
-            for (int q = 0; q < 8; ++q) y ^= lf[c + ((uint32_t)(q * 16) + ((R >> (4 * q)) & 15u)) * 32u];
-            y = cur.valid ? y : 0u;
+            const uint32_t y = cur.valid ? lane_advance(lf, c, R) : 0u;
             const uint32_t px = half_prefix_xor(y);
             const int a0 = lane - (int)cur.i + (RH_PACK_C0STEP ? 0 : 1);  // lane of the frame's first packed chunk (may be < 0)
             const bool cont = a0 < (int)hs;        // the frame began before this half
@@ -1277,9 +1291,34 @@ __global__ __launch_bounds__(kCrcThreads) void crc_pack_kernel(PackArgs pk_arg) 
             if (ends) vst[cur.j] = tot;
             const uint64_t runM = __ballot(cur.valid && cur.m != 0u);
             carry = ((runM >> 63) & 1u) ? (uint32_t)__builtin_amdgcn_readlane((int)tot, 63) : 0u;
-            cur = nx;
-#pragma unroll
-            for (int i = 0; i < 17; ++i) dc[i] = dn[i];
+        };
+        // D + 1 register sets in turn (no copy of a prefetched chunk from one set to another)
+        Step sa{}, sb{};
+        uint32_t da[17], db[17];
+        if (nsteps) {
+            sa = map(0, 0);
+            load(sa, da);
+        }
+        if constexpr (D == 1) {
+            for (uint32_t s = 0; s < nsteps; s += 2) {
+                step(s, sa, da, sa, sb, db);
+                if (s + 1 >= nsteps) break;
+                step(s + 1, sb, db, sb, sa, da);
+            }
+        } else {
+            Step sc{};
+            uint32_t dd3[17];
+            if (nsteps > 1) {
+                sb = map(1, (uint32_t)__builtin_amdgcn_readlane((int)sa.j, 63));
+                load(sb, db);
+            }
+            for (uint32_t s = 0; s < nsteps; s += 3) {
+                step(s, sa, da, sb, sc, dd3);
+                if (s + 1 >= nsteps) break;
+                step(s + 1, sb, db, sc, sa, da);
+                if (s + 2 >= nsteps) break;
+                step(s + 2, sc, dd3, sa, sb, db);
+            }
         }
         __builtin_amdgcn_wave_barrier();
 
@@ -1386,10 +1425,10 @@ int launch_pack(rh_ctx* ctx, FrameArgs a, const SlotPlan& sp, hipStream_t stream
     p.counts = counts;
     p.widx = widx;
     if (sp.total) {
-        hipLaunchKernelGGL(crc_pack_kernel<true>, dim3((uint32_t)cus), dim3(kCrcThreads), kPackLds, stream, p);
+        hipLaunchKernelGGL(crc_pack_kernel<true>, dim3((uint32_t)cus), dim3(kPackThreads), kPackLds, stream, p);
     } else {
         const uint64_t tasks = (a.n + 63) / 64, blocks = (tasks + kPackWaves - 1) / kPackWaves;
-        hipLaunchKernelGGL(crc_pack_kernel<false>, dim3((uint32_t)(blocks < cus ? blocks : cus)), dim3(kCrcThreads),
+        hipLaunchKernelGGL(crc_pack_kernel<false>, dim3((uint32_t)(blocks < cus ? blocks : cus)), dim3(kPackThreads),
                            kPackLds, stream, p);
     }
     RH_HIP(hipGetLastError());
