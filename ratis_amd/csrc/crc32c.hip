@@ -995,13 +995,20 @@ hipError_t launch_lanes(const LaneArgs& l, uint64_t n, uint64_t cus, hipStream_t
 constexpr int kPackThreads = RH_PACK_DEPTH >= 2 ? 768 : kCrcThreads;
 constexpr int kPackWaves = kPackThreads / 64;
 constexpr int kPackTabBytes = 128 * 1024 + 4096 + 16384;  // slicing tables, 32-byte join, lane maps
-constexpr int kPackLds = kPackTabBytes + kPackWaves * 512;  // + per wave: 64 step marks, 64 frame values
+// Fold chains per 64-byte chunk: 2 (8 words each, one 32-byte join) or 4 (4 words each, joined as
+// a tree: two 16-byte joins, then one 32-byte join; the 16-byte table takes the last 4 KiB of LDS).
+#ifndef RH_PACK_CHAINS
+#define RH_PACK_CHAINS 2
+#endif
+constexpr int kPackLds = kPackTabBytes + kPackWaves * 512 +  // + per wave: 64 step marks, 64 frame values
+                         (RH_PACK_CHAINS == 4 ? 4096 : 0);
 static_assert(kPackLds <= 160 * 1024, "LDS budget");
 
 struct PackArgs {
     FrameArgs f;                       // buffers, outputs, slot-mode fields (f.n = table entries)
     const uint32_t* ftab;              // build_crc_lane_tables(32, 64)
     const uint32_t* inv;               // build_crc_inverse_lane_tables()
+    const uint32_t* z16;               // [4][256] advance over 16 zero bytes (RH_PACK_CHAINS 4)
     const uint32_t* z64;               // [4][256] advance over 64 zero bytes
     const uint32_t* z2k;               // [4][256] advance over 2048 zero bytes (uniform lookups)
     const uint32_t* z4k;               // [4][256] advance over 4096 zero bytes (uniform lookups)
@@ -1067,6 +1074,19 @@ __device__ __forceinline__ uint32_t fold16(const uint32_t* lds, const uint32_t* 
     return zshift_x(lch, x0, x1);
 }
 
+// The same over four chains of 4 words: half the dependent LDS rounds per chain, three joins.
+__device__ __forceinline__ uint32_t fold16_4(const uint32_t* lds, const uint32_t* lch, const uint32_t* lz16,
+                                             const uint32_t (&w)[16], const uint32_t (&lb)[4], uint32_t extra = 0u) {
+    uint32_t x[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) x[q] = w[4 * q];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) x[q] = fold_x(lds, x[q], lb, j < 3 ? w[4 * q + j + 1] : (q == 3 ? extra : 0u));
+    return zshift_x(lch, zshift_x(lz16, x[0], x[1]), zshift_x(lz16, x[2], x[3]));
+}
+
 // A/B: 1 folds chunk 0 in the steps (a per-lane mask on every word of every step) instead of one
 // masked chunk-0 pass per task.  It removes the chunk-0 pass's refetched lines (ragged 64-2048 B,
 // 64 x 32 MiB: FETCH_SIZE 2545 -> 2402 MB) but the masking makes the step VALU-heavier: crc_pack
@@ -1095,6 +1115,9 @@ __global__ __launch_bounds__(kPackThreads) void crc_pack_kernel(PackArgs pk_arg)
     }
     for (int i = threadIdx.x; i < 1024; i += blockDim.x) lch[i] = a.shift32[i];
     for (int i = threadIdx.x; i < 4096; i += blockDim.x) lf[i] = p.ftab[i];
+    uint32_t* lz16 = lds + kPackTabBytes / 4 + kPackWaves * 128;
+    if (RH_PACK_CHAINS == 4)
+        for (int i = threadIdx.x; i < 1024; i += blockDim.x) lz16[i] = p.z16[i];
     __syncthreads();
 
     const int lane = threadIdx.x & 63;
@@ -1102,6 +1125,10 @@ __global__ __launch_bounds__(kPackThreads) void crc_pack_kernel(PackArgs pk_arg)
     uint32_t lb[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) lb[k] = ((uint32_t)(k >> 1) << 16) | ((uint32_t)(k & 1) << 7) | (c << 2);
+    auto fold = [&](const uint32_t (&w)[16], uint32_t extra) {
+        if constexpr (RH_PACK_CHAINS == 4) return fold16_4(lds, lch, lz16, w, lb, extra);
+        else return fold16(lds, lch, w, lb, extra);
+    };
     const uint32_t wid = threadIdx.x >> 6;
     uint32_t* mark = lds + kPackTabBytes / 4 + wid * 128;  // [64] step marks
     uint32_t* vst = mark + 64;                               // [64] frame registers (end of half)
@@ -1197,7 +1224,7 @@ __global__ __launch_bounds__(kPackThreads) void crc_pack_kernel(PackArgs pk_arg)
                 const int32_t kk = min(max(g8 - 32 * i, 0), 32);
                 w[i] = __builtin_amdgcn_alignbyte(dd[i + 1], dd[i], sh) & (uint32_t)(~0ull << kk);
             }
-            f0 = fold16(lds, lch, w, lb);
+            f0 = fold(w, 0u);
             fs = 0;
             if (k > 0) {  // chunk 0 seen from the end of chunk 1
 #pragma unroll
@@ -1270,7 +1297,7 @@ __global__ __launch_bounds__(kPackThreads) void crc_pack_kernel(PackArgs pk_arg)
                     w[i] &= (uint32_t)(~0ull << kk);
                 }
             }
-            const uint32_t R = fold16(lds, lch, w, lb, !RH_PACK_C0STEP && cur.i == 1u ? cur.fs : 0u);
+            const uint32_t R = fold(w, !RH_PACK_C0STEP && cur.i == 1u ? cur.fs : 0u);
             const uint32_t K0 = zshift_uniform(p.z2k, carry);  // off the step's dependent chain
             const uint32_t C4 = zshift_uniform(p.z4k, carry);
             const uint32_t y = cur.valid ? lane_advance(lf, c, R) : 0u;
@@ -1416,6 +1443,7 @@ int launch_pack(rh_ctx* ctx, FrameArgs a, const SlotPlan& sp, hipStream_t stream
     p.f = a;
     p.ftab = ctx->d_lane16 + (size_t)4 * 4096;  // Q = 32
     p.inv = ctx->d_inv32;
+    p.z16 = ctx->d_shift + (size_t)4 * 1024;
     p.z64 = ctx->d_shift + (size_t)6 * 1024;
     p.z2k = ctx->d_shift + (size_t)11 * 1024;
     p.z4k = ctx->d_shift + (size_t)12 * 1024;
