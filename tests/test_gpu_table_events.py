@@ -257,6 +257,57 @@ def test_list_and_tile_evaluations_interleaved(ctx, orc, seed):
         tab.close()
 
 
+def test_list_mode_over_every_width(ctx, orc):
+    """List entries carry their tier ((tier << 28) | row) and a wave's lanes may hold rows of
+    different widths: a table started over every width (1..14 followers, some in joint consensus)
+    gets sparse pushes that run in list mode -- commit and commitIndexChanged -- against the model,
+    with a control op between two of them (lists given up once, then list mode again)."""
+    from ratis_amd import groups
+    rng = np.random.default_rng(77)
+    n = 4000
+    model = TableModel(n)
+    with groups.RaftGroupTable(ctx, capacity=n) as tab:
+        tab.set_timing(True)
+        for s in range(n):
+            F = 1 + s % 14
+            new = int(rng.integers(1, 1 << F))
+            c = conf_word(new, old_mask=int(rng.integers(0, 1 << F))) if s % 5 == 0 else conf_word(new)
+            b = int(rng.integers(1000, 1 << 40))
+            args = (s, c, b, b - int(rng.integers(0, 2000)), b - int(rng.integers(-500, 3000)))
+            tab.start(*args)
+            model.start(*args)
+        assert {tab.tier_width(s) for s in range(n)} == {2, 4, 6, 8, 10, 12, 14}
+        compare(tab, model, orc, columns=False)          # after control ops: tile evaluations
+        live = np.arange(n)
+        modes = []
+        # a push of k deltas bounds k markings of each kind, the commit evaluation k more for
+        # commitIndexChanged: both lists hold while 2 k <= lcap = 1024 (4000 rows)
+        for step, k in enumerate([5, 60, 400, 1000, 30, 450, 250]):
+            if step == 4:
+                tab.stop(17)
+                model.stop(17)
+                live = live[live != 17]
+            d = random_deltas(rng, model, live, k)
+            tab.push(d)
+            model.apply(d)
+            got = tab.update_commit()
+            a_s, a_c, w_s, w_m = model.commit_batch(orc)
+            assert np.array_equal(got.advanced_slots, a_s) and np.array_equal(got.advanced_commit, a_c), step
+            assert np.array_equal(got.watch_all_slots, w_s) and np.array_equal(got.watch_all_min, w_m), step
+            ml = tab.last_was_list()
+            ev = tab.commit_index_changed()
+            m_s, m_lev, m_valid = model.watch(orc)
+            assert np.array_equal(ev["slot"].astype(np.int64), m_s), step
+            assert np.array_equal(ev["min"], m_lev[0]) and np.array_equal(ev["majority"], m_lev[1]), step
+            assert np.array_equal(ev["max"], m_lev[2]) and np.array_equal(ev["valid"].astype(bool), m_valid), step
+            modes.append((ml, tab.last_was_list()))
+        assert modes[3] == (True, False), modes              # 2 k > lcap: the watch list given up
+        assert modes[4] == (False, False), modes             # the control op gave both lists up
+        assert all(m == (True, True) for i, m in enumerate(modes) if i not in (3, 4)), modes
+        for col in [0, 1, 7, 13, 16, 29, 32, 33]:
+            assert np.array_equal(tab.read(col), model.column(col)), col
+
+
 def test_separate_done_word_of_large_tables(ctx, orc, monkeypatch):
     """28-bit list counts (tables of 2^24 rows and more) leave 8 bits of done count in the counter
     word: tile evaluations of more than 255 workgroups then count themselves on the separate done
