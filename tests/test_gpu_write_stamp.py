@@ -71,3 +71,49 @@ def test_stamp_edge_frames_and_errors(ctx, orc):
         engine.stamp_host(ctx, buf, off[:1], np.array([3], dtype=np.uint32))
     engine.stamp_host(ctx, buf, off, ln)
     assert np.array_equal(buf, before)
+
+
+def _frames(orc, rng, sizes, gap=0):
+    """One frame per entry size, gap random bytes between frames; returns (expected image,
+    placeholder image, offsets, lengths)."""
+    parts, off, ln = [], [], []
+    pos = 0
+    for sz in sizes:
+        g = rng.integers(0, 256, int(rng.integers(0, gap + 1)) if gap else 0, dtype=np.uint8)
+        parts.append(g)
+        pos += g.size
+        fr = np.frombuffer(orc.frame_write(rng.integers(0, 256, int(sz), dtype=np.uint8).tobytes()), dtype=np.uint8)
+        off.append(pos)
+        ln.append(fr.size)
+        parts.append(fr)
+        pos += fr.size
+    want = np.concatenate(parts)
+    buf = want.copy()
+    for o, l in zip(off, ln):
+        buf[o + l - 4: o + l] = 0x5A
+    return want, buf, np.array(off, dtype=np.uint64), np.array(ln, dtype=np.uint32)
+
+
+@pytest.mark.parametrize("case", ["512_window", "513_serial", "long_frame_over_512", "shuffled_with_gaps"])
+def test_stamp_plan_boundaries(ctx, orc, case):
+    """rh_crc32c_stamp_host's plan choice (rh_api.cpp, RH_STAMP_PLAN 2): up to 512 frames one
+    window-kernel batch, more frames one lane each (frames up to 64 KiB), more frames with a longer
+    one on the window kernel over several batches; and a table whose frames are not in buffer order
+    with bytes between them (only the covered span crosses PCIe)."""
+    from ratis_amd import engine
+    rng = np.random.default_rng(len(case))
+    if case == "512_window":
+        sizes = rng.integers(0, 700, 512)
+    elif case == "513_serial":
+        sizes = rng.integers(0, 700, 513)
+    elif case == "long_frame_over_512":
+        sizes = np.append(rng.integers(0, 700, 599), 70 << 10)
+        rng.shuffle(sizes)
+    else:
+        sizes = rng.integers(0, 3000, 300)
+    want, buf, off, ln = _frames(orc, rng, sizes, gap=40 if case == "shuffled_with_gaps" else 0)
+    if case == "shuffled_with_gaps":
+        p = rng.permutation(off.size)
+        off, ln = off[p], ln[p]
+    engine.stamp_host(ctx, buf, off, ln)
+    assert np.array_equal(buf, want)
