@@ -84,6 +84,39 @@ def load_pmc(path):
     return out
 
 
+class _Legs:
+    """roctx ranges naming the bench's timed legs (rocprofv3 --marker-trace records them): every
+    kernel dispatch of a profiled run is attributed to the leg whose range holds it
+    (scripts/prof_legs.py), so each roofline's avg_launch_ms can be checked against the kernel
+    trace.  Without the profiler the calls are no-ops; without the library, nothing is called."""
+
+    def __init__(self):
+        import ctypes
+        self._lib = None
+        for name in ("librocprofiler-sdk-roctx.so.1", "librocprofiler-sdk-roctx.so"):
+            try:
+                lib = ctypes.CDLL(name)
+                lib.roctxRangePushA.argtypes = [ctypes.c_char_p]
+                lib.roctxRangePushA.restype = ctypes.c_int
+                lib.roctxRangePop.restype = ctypes.c_int
+                self._lib = lib
+                break
+            except (OSError, AttributeError):
+                continue
+
+    def push(self, name: str, steps: int = 1) -> None:
+        """Opens the range of a leg that times `steps` steps (the name carries the count)."""
+        if self._lib is not None:
+            self._lib.roctxRangePushA(f"leg:{name}#{steps}".encode())
+
+    def pop(self) -> None:
+        if self._lib is not None:
+            self._lib.roctxRangePop()
+
+
+LEGS = _Legs()
+
+
 def cpu_threads() -> int:
     """Threads for the all-core CPU baseline: this process's CPU affinity, capped at the 16-CPU
     share a one-GPU box gives a job (nproc there shows the whole machine)."""
@@ -138,6 +171,9 @@ class _producers:
         self._lib.bp_create.argtypes = [ctypes.c_int]
         self._lib.bp_fill.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
         self._lib.bp_destroy.argtypes = [ctypes.c_void_p]
+        self._lib.bp_push.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_size_t]
+        self._lib.bp_threads.argtypes = [ctypes.c_void_p]
         self._pool = self._lib.bp_create(int(threads))
         if not self._pool:
             raise RuntimeError("bp_create failed")
@@ -145,6 +181,13 @@ class _producers:
     def fill(self, dst: int, src: int, nbytes: int) -> None:
         if self._lib.bp_fill(self._pool, dst, src, nbytes) != 0:
             raise RuntimeError("bp_fill failed")
+
+    def push(self, fn: int, node: int, src: int, shares: int, chunk: int) -> int:
+        """Every producer pushes its share of src (record offsets `shares`) through fn(node, ...)."""
+        return self._lib.bp_push(self._pool, fn, node, src, shares, chunk)
+
+    def threads(self) -> int:
+        return self._lib.bp_threads(self._pool)
 
     def close(self) -> None:
         if self._pool:
@@ -241,6 +284,7 @@ def delta_streaming(ctx, host, steps: int = 12, fill_threads: int = 16, reps: in
     # run of a dozen sub-millisecond steps is at the mercy of a single host hiccup)
     runs = []
     for rep in range(reps):
+        LEGS.push("delta_streaming", steps)
         t0 = time.perf_counter()
         inflight, advanced = [], 0
         for s in range(1, steps + 1):
@@ -250,6 +294,7 @@ def delta_streaming(ctx, host, steps: int = 12, fill_threads: int = 16, reps: in
         for tk in inflight:
             advanced += tab.commit_wait_counts(tk)[0]
         runs.append((time.perf_counter() - t0) / steps)
+        LEGS.pop()
     dt = float(np.median(runs))
     # stages on their own: host fill of the pinned ring; device part (H2D + apply + evaluation +
     # events) with the ring already filled, synchronous
@@ -279,6 +324,159 @@ def delta_streaming(ctx, host, steps: int = 12, fill_threads: int = 16, reps: in
                     "rh_commit_batch_async/_wait (dirty-group evaluation, advanced events in host-mapped "
                     "memory), pipelined: the host fill of step s+1 and its H2D (copy stream, double-buffered "
                     "device slots) overlap the apply and evaluation of step s"}
+
+
+def reply_mix_leg(host, threads: int = 16, steps: int = 8, active_frac: float = 0.25, repeat_frac: float = 0.25,
+                  chunk: int = 4096) -> dict:
+    """The delta path the Java module runs (HipLeaderBookkeeper: per-thread DeltaBuffers of 4096
+    deltas pushed through rh_node_push_deltas by their own producer threads, the multi-producer
+    staging, then the pump's updateCommit + commitIndexChanged), fed the reference's per-reply
+    mix.  Per step a quarter of config 3's divisions are active; each gets one flushIndex MAX (the
+    log worker, SegmentedRaftLogWorker.java:419-431) and one reply from each of its 4 followers --
+    SET lastRespondedAppendEntriesSendTime, MAX matchIndex, MAX commitIndex
+    (GrpcLogAppender.java:491, 516; FollowerInfoImpl.java:93-105, 241-243) -- and a quarter of the
+    followers reply twice in the step (SET after SET on one cell, later MAXes).  `threads` native
+    producers own the divisions d % threads (an appender thread serves its followers' replies in
+    order).  Pipelined as the pump: step s's evaluations are in flight while the producers push
+    step s+1.  PCIe included (the deltas are host memory).  Parity: after the run, every
+    follower's matchIndex / commitIndex / timestamp and every flushIndex equals the one-by-one
+    result, and each step's advanced set equals an oracle evaluation of the same snapshot."""
+    import ctypes
+
+    from oracle import oracle as orc
+    from ratis_amd import _lib, groups
+    lib = _lib.load()
+    rng = np.random.default_rng(123)
+    n_all = sum(h.n for h in host)
+    node = groups.RaftNode(0, n_all, devices=[0])
+    tab = node.tables[0]
+    first = 0
+    for h in host:
+        tab.load(first, h.conf, h.flush, h.commit, h.term_start, match=h.follower,
+                 fcommit=h.follower - 3)
+        first += h.n
+    tab.commit_wait_counts(tab.commit_async(watch_all=True))   # the load marked every row dirty
+    tab.watch_async()
+    tab.watch_wait()
+    com0 = tab.read(_lib.RH_COL_COMMITTED)
+    match = np.concatenate([h.follower[:4] for h in host], axis=1)   # followers 0..3 exist in both tiers
+    fcom = match - 3
+    ts = np.full((4, n_all), np.iinfo(np.int64).min, np.int64)   # no timestamp yet (rh_groups_load)
+    flush = np.concatenate([h.flush for h in host])
+    T = threads
+    A = int(n_all * active_frac)
+    per_step = []
+    for s in range(steps + 1):
+        act = np.sort(rng.choice(n_all, A, replace=False))
+        owner = act % T
+        act = act[np.argsort(owner, kind="stable")]
+        owner = act % T
+        # first part, 13 deltas per active division: flush MAX, then each follower's reply
+        flush_v = flush[act] + rng.integers(1, 600, A)
+        m1 = match[:, act] + rng.integers(1, 500, (4, A))
+        t1 = (s * 10 + 1) * 1_000_000 + np.arange(4)[:, None]
+        c1 = np.maximum(fcom[:, act], m1 - rng.integers(0, 64, (4, A)))
+        first_part = np.zeros((A, 13), dtype=groups.DELTA_DTYPE)
+        first_part["slot"] = act[:, None]
+        first_part["column"][:, 0], first_part["value"][:, 0] = _lib.RH_COL_FLUSH, flush_v
+        for k in range(4):
+            b = 1 + 3 * k
+            first_part["column"][:, b], first_part["op"][:, b], first_part["value"][:, b] = _lib.RH_COL_TS(k), _lib.RH_OP_SET, t1[k]
+            first_part["column"][:, b + 1], first_part["value"][:, b + 1] = _lib.rh_col_match(k), m1[k]
+            first_part["column"][:, b + 2], first_part["value"][:, b + 2] = _lib.rh_col_fcommit(k), c1[k]
+        # second replies (repeat_frac of the (division, follower) pairs): later send time, further
+        # matchIndex -- or a stale one, which the MAX ignores
+        rep = rng.random((4, A)) < repeat_frac
+        kk, jj = np.nonzero(rep)
+        m2 = m1[kk, jj] + rng.integers(-50, 400, kk.size)
+        t2 = t1[kk, 0] + 5_000_000
+        c2 = np.maximum(c1[kk, jj], m2 - 10)
+        second = np.zeros((kk.size, 3), dtype=groups.DELTA_DTYPE)
+        second["slot"] = act[jj][:, None]
+        second["column"][:, 0], second["op"][:, 0], second["value"][:, 0] = 48 + kk, _lib.RH_OP_SET, t2
+        second["column"][:, 1], second["value"][:, 1] = kk, m2
+        second["column"][:, 2], second["value"][:, 2] = 16 + kk, c2
+        # the one-by-one state after the step (the parity reference)
+        flush[act] = np.maximum(flush[act], flush_v)
+        match[:, act] = np.maximum(match[:, act], m1)
+        fcom[:, act] = np.maximum(fcom[:, act], c1)
+        ts[:, act] = t1
+        np.maximum.at(match, (kk, act[jj]), m2)
+        np.maximum.at(fcom, (kk, act[jj]), c2)
+        ts[kk, act[jj]] = t2
+        # producer t's share: its divisions' first parts, then their second replies
+        sown = owner[jj]
+        so = np.argsort(sown, kind="stable")
+        second = second[so]
+        shares = [0]
+        parts = []
+        for t in range(T):
+            a = first_part[owner == t].reshape(-1)
+            b = second[sown[so] == t].reshape(-1)
+            parts += [a, b]
+            shares.append(shares[-1] + a.size + b.size)
+        per_step.append((np.concatenate(parts), np.array(shares, dtype=np.uint64), int(A * 4 + kk.size)))
+    prod = _producers(T)
+    if prod.threads() != T:
+        T = prod.threads()
+    push_fn = ctypes.cast(lib.rh_node_push_deltas, ctypes.c_void_p).value
+    node_h = node._h.value
+
+    def push(d, sh):
+        if prod.push(push_fn, node_h, d.ctypes.data, sh.ctypes.data, chunk) != 0:
+            raise RuntimeError("rh_node_push_deltas failed in a producer thread")
+    push(*per_step[0][:2])   # warm-up step (not timed)
+    tk = tab.commit_async(watch_all=True)
+    tab.watch_async()
+    tab.commit_wait_counts(tk)
+    tab.watch_wait()
+    LEGS.push("reply_mix", steps)
+    t0 = time.perf_counter()
+    inflight = None
+    advanced = 0
+    for s in range(1, steps + 1):
+        push(*per_step[s][:2])
+        if inflight is not None:   # the previous step's evaluations, in flight while this step pushed
+            advanced += tab.commit_wait_counts(inflight)[0]
+            tab.watch_wait()
+        inflight = tab.commit_async(watch_all=True)
+        tab.watch_async()
+    advanced += tab.commit_wait_counts(inflight)[0]
+    tab.watch_wait()
+    dt = (time.perf_counter() - t0) / steps
+    LEGS.pop()
+    ok = (np.array_equal(tab.read(_lib.RH_COL_FLUSH), flush)
+          and all(np.array_equal(tab.read(_lib.rh_col_match(k)), match[k]) for k in range(4))
+          and all(np.array_equal(tab.read(_lib.rh_col_fcommit(k)), fcom[k]) for k in range(4))
+          and all(np.array_equal(tab.read(_lib.RH_COL_TS(k)), ts[k]) for k in range(4)))
+    # every index only grows here, and updateCommit's rule is monotone in them (a commit accepted at
+    # one step is <= the final snapshot's, which passes the term check too): the commit the
+    # pipelined evaluations reached is the oracle's rule on the final snapshot from the start commit
+    conf = np.concatenate([h.conf for h in host])
+    tstart = np.concatenate([h.term_start for h in host])
+    com = tab.read(_lib.RH_COL_COMMITTED)
+    lo = 0
+    for h in host:
+        hi = lo + h.n
+        fol = h.follower.copy()
+        fol[:4] = match[:, lo:hi]
+        r = orc.commit_soa(fol, flush[lo:hi], conf[lo:hi], mode=0, gap=-1, commit_in=com0[lo:hi], term_start=tstart[lo:hi])
+        ok &= bool(np.array_equal(r["commit"], com[lo:hi]))
+        lo = hi
+    n_deltas = int(np.mean([p[0].size for p in per_step[1:]]))
+    replies = int(np.mean([p[2] for p in per_step[1:]]))
+    prod.close()
+    node.close()
+    return {"ms_per_step": round(dt * 1e3, 3), "replies_per_s_incl_pcie": round(replies / dt, 1),
+            "deltas_per_s_incl_pcie": round(n_deltas / dt, 1), "replies_per_step": replies,
+            "deltas_per_step": n_deltas, "delta_bytes_h2d_per_step": n_deltas * 16,
+            "h2d_bound_ms": round(n_deltas * 16 / 50e9 * 1e3, 3), "producer_threads": T,
+            "deltas_per_push_call": chunk, "active_divisions_per_step": A, "advanced_per_step": round(advanced / steps, 1),
+            "parity_ok": bool(ok),
+            "path": "per-thread buffers -> rh_node_push_deltas from every producer thread at once (multi-producer "
+                    "staging: one CAS per call, copies in parallel) -> H2D per full 1M-delta slot + three-phase apply "
+                    "(last SET wins, later MAXes) -> rh_commit_batch_async + rh_watch_levels_async per step, "
+                    "pipelined one step deep"}
 
 
 def _placeholder_frames(rng, nbytes: int, lo: int = 64, hi: int = 2048):
@@ -389,6 +587,7 @@ def table_commit_leg(ctx, host, reps: int = 8, fracs=(1.0, 0.1, 0.01), pmc=None)
     F = [h.follower.shape[0] for h in host]
     stream = torch.cuda.ExternalStream(lib.rh_ctx_stream(ctx.handle))
     tabs = {}
+    names = {_lib.RH_EVENTS_HOST_MAPPED: "host_mapped", _lib.RH_EVENTS_DEVICE: "device", _lib.RH_EVENTS_AUTO: "auto"}
     for sink in (_lib.RH_EVENTS_HOST_MAPPED, _lib.RH_EVENTS_DEVICE, _lib.RH_EVENTS_AUTO):
         tab = groups.RaftGroupTable(ctx, capacity=n_all)
         first = 0
@@ -402,7 +601,6 @@ def table_commit_leg(ctx, host, reps: int = 8, fracs=(1.0, 0.1, 0.01), pmc=None)
     cur_f = np.concatenate([h.follower[:4] for h in host], axis=1)   # followers 0..3 exist in both tiers
     cur_s = np.concatenate([h.flush for h in host])
     out = {}
-    names = {_lib.RH_EVENTS_HOST_MAPPED: "host_mapped", _lib.RH_EVENTS_DEVICE: "device", _lib.RH_EVENTS_AUTO: "auto"}
     for frac in fracs:
         k = n_all if frac >= 1.0 else int(n_all * frac)
         res = {}
@@ -418,12 +616,14 @@ def table_commit_leg(ctx, host, reps: int = 8, fracs=(1.0, 0.1, 0.01), pmc=None)
             for sink, tab in tabs.items():
                 tab.push(d)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                LEGS.push(f"table_{frac * 100:g}pct_{names[sink]}" if r else "table_warmup")
                 queue_gate(stream)   # the evaluation is enqueued before the GPU reaches e0
                 e0.record(stream)
                 tk = tab.commit_async(watch_all=True)
                 e1.record(stream)
                 got[sink] = tab.commit_wait(tk)
                 torch.cuda.synchronize()
+                LEGS.pop()
                 if r:   # the first round is a warm-up
                     res.setdefault((sink, "call"), []).append(e0.elapsed_time(e1))
                     res.setdefault((sink, "eval"), []).append(tab.last_timing())
@@ -493,11 +693,13 @@ def ragged_read_path(ctx, args, rank, stream, barrier, max_over_ranks, sum_over_
         engine.segments_scan(ctx, sb, stream=stream)
     barrier()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    LEGS.push("ragged_framing", steps)
     e0.record(stream)
     for _ in range(steps):
         engine.segments_scan(ctx, sb, stream=stream)
     e1.record(stream)
     barrier()
+    LEGS.pop()
     scan_ms = e0.elapsed_time(e1) / steps
     frame_ok = (int(sb.total_frames.item()) == nf and torch.equal(sb.frame_off[:nf], rs.batch.frame_off)
                 and torch.equal(sb.frame_len[:nf], rs.batch.frame_len))
@@ -505,11 +707,13 @@ def ragged_read_path(ctx, args, rank, stream, barrier, max_over_ranks, sum_over_
     for _ in range(2):
         fout = engine.read_segments_fused(ctx, fbatch, stream=stream)
     barrier()
+    LEGS.push("ragged_read_launch", steps)
     e0.record(stream)
     for _ in range(steps):
         fout = engine.read_segments_fused(ctx, fbatch, stream=stream)
     e1.record(stream)
     barrier()
+    LEGS.pop()
     rl_ms = e0.elapsed_time(e1) / steps
     fbad = np.nonzero(np.unpackbits(fout["bad_bits"].cpu().numpy().view(np.uint8), bitorder="little")[:nf])[0]
     clean = torch.ones(nf, dtype=torch.bool, device=dev)
@@ -632,6 +836,7 @@ def main():
     barrier()
     t0 = torch.cuda.Event(enable_timing=True)
     t1 = torch.cuda.Event(enable_timing=True)
+    LEGS.push("commit", args.steps)
     queue_gate(stream)
     wall0 = time.perf_counter()
     t0.record(stream)
@@ -639,6 +844,7 @@ def main():
     t1.record(stream)
     barrier()
     wall = time.perf_counter() - wall0
+    LEGS.pop()
     elapsed_ms = max_over_ranks(t0.elapsed_time(t1))
     # average launch duration over the timed region (back-to-back launches on one stream, so it
     # includes the ~1-2 us kernel boundaries; rocprofv3's per-kernel average is kernel-only)
@@ -706,11 +912,13 @@ def main():
         run_lease, _ = captured(lease_launches, args.steps, ctx, args.graph)
         barrier()
         l0, l1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        LEGS.push("lease", args.steps)
         queue_gate(stream)
         l0.record(stream)
         run_lease(stream)
         l1.record(stream)
         barrier()
+        LEGS.pop()
         lease_kern_ms = l0.elapsed_time(l1) / args.steps
         lease_ms = max_over_ranks(lease_kern_ms)
         lease_ok = True
@@ -741,11 +949,13 @@ def main():
         barrier()
         run_leader, _ = captured(leader_launches, args.steps, ctx, args.graph)
         barrier()
+        LEGS.push("fused", args.steps)
         queue_gate(stream)
         l0.record(stream)
         run_leader(stream)
         l1.record(stream)
         barrier()
+        LEGS.pop()
         fused_kern_ms = l0.elapsed_time(l1) / args.steps
         fused_ms = max_over_ranks(fused_kern_ms)
         fused_ok = True
@@ -806,6 +1016,7 @@ def main():
         pcie["note"] = "full snapshot H2D (pinned) + kernel + commit D2H per batch"
         pcie["delta_streaming"] = delta_streaming(ctx, host, fill_threads=cpu_threads())
         pcie["delta_streaming"]["table_commit"] = table_commit_leg(ctx, host, pmc=pmc)
+        pcie["delta_streaming"]["reply_mix"] = reply_mix_leg(host, threads=cpu_threads())
         pcie["write_stamp"] = write_stamp_leg(ctx)
 
     # ------------------------------------------------------------------ CRC32C (config 5)
@@ -824,11 +1035,13 @@ def main():
         barrier()
         c0 = torch.cuda.Event(enable_timing=True)
         c1 = torch.cuda.Event(enable_timing=True)
+        LEGS.push("crc", args.crc_steps)
         c0.record(stream)
         for i in range(args.crc_steps):
             engine.crc32c_frames(ctx, fb, flags=_lib.RH_CRC_VERIFY, stream=stream)
         c1.record(stream)
         barrier()
+        LEGS.pop()
         crc_kern_ms = c0.elapsed_time(c1) / args.crc_steps
         crc_ms = max_over_ranks(crc_kern_ms)
         fb.n_bad.zero_()
@@ -877,11 +1090,13 @@ def main():
             engine.segments_scan(ctx, sb, stream=stream)
         barrier()
         f0, f1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        LEGS.push("framing", args.crc_steps)
         f0.record(stream)
         for _ in range(args.crc_steps):
             engine.segments_scan(ctx, sb, stream=stream)
         f1.record(stream)
         barrier()
+        LEGS.pop()
         scan_ms = f0.elapsed_time(f1) / args.crc_steps
         nfr_found = int(sb.total_frames.item())
         frame_ok = (nfr_found == fb.n and torch.equal(sb.frame_off[:fb.n], fb.frame_off)
@@ -890,12 +1105,14 @@ def main():
         rb = engine.FrameBatch(buf=fb.buf, frame_off=sb.frame_off[:fb.n], frame_len=sb.frame_len[:fb.n])
         rb.alloc_outputs()
         barrier()
+        LEGS.push("framing_plus_verify", args.crc_steps)
         f0.record(stream)
         for _ in range(args.crc_steps):
             engine.segments_scan(ctx, sb, stream=stream)
             engine.crc32c_frames(ctx, rb, flags=_lib.RH_CRC_VERIFY, stream=stream)
         f1.record(stream)
         barrier()
+        LEGS.pop()
         read_ms = f0.elapsed_time(f1) / args.crc_steps
         # rh_segments_read_launch (LogSegment.readSegmentFile in one call): framing walk + CRC over
         # the slotted frame table + verdict
@@ -904,11 +1121,13 @@ def main():
         for _ in range(2):
             fout = engine.read_segments_fused(ctx, fbatch, stream=stream)
         barrier()
+        LEGS.push("read_launch", args.crc_steps)
         f0.record(stream)
         for _ in range(args.crc_steps):
             fout = engine.read_segments_fused(ctx, fbatch, stream=stream)
         f1.record(stream)
         barrier()
+        LEGS.pop()
         rl_ms = f0.elapsed_time(f1) / args.crc_steps
         fbad = np.nonzero(np.unpackbits(fout["bad_bits"].cpu().numpy().view(np.uint8), bitorder="little")[: fb.n])[0]
         rl_ok = bool(np.array_equal(fbad, ss.corrupted) and int(fbatch.total_frames.item()) == fb.n

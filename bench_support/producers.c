@@ -4,6 +4,10 @@
  * each write their 16-byte rh_delta straight into the pinned staging slot that rh_deltas_acquire
  * hands out.  bench.py replays that with a pool of persistent native threads that copy their share
  * of a pre-generated step into the slot -- no Python thread-pool dispatch in the timed loop.
+ * bp_push replays the Java module's own producer path instead: every thread owns a share of the
+ * step's deltas (the divisions / followers whose appender it is) and hands them to
+ * rh_node_push_deltas in buffer-sized calls, concurrently with the other threads
+ * (HipLeaderBookkeeper.DeltaBuffer, 4096 deltas).
  *
  * Not product code: libratis_hip never links this, and it touches no GPU API.
  */
@@ -36,6 +40,13 @@ struct bp_pool {
     char* dst;
     const char* src;
     size_t bytes;
+    /* bp_push rounds */
+    int mode;               /* 0: copy (bp_fill), 1: push (bp_push) */
+    int (*push)(void*, const void*, size_t);
+    void* node;
+    const uint64_t* shares; /* [n + 1] record offsets: producer i pushes [shares[i], shares[i + 1]) */
+    size_t chunk;           /* records per push call */
+    int rc;                 /* first failing push's return code (0: all succeeded) */
 };
 
 /* share `id` of `parts`, cut on 16-byte record boundaries */
@@ -44,6 +55,26 @@ static void copy_share(bp_pool* p, int id, int parts) {
     const size_t lo = recs * (size_t)id / (size_t)parts * 16;
     const size_t hi = (id == parts - 1) ? p->bytes : recs * (size_t)(id + 1) / (size_t)parts * 16;
     if (hi > lo) memcpy(p->dst + lo, p->src + lo, hi - lo);
+}
+
+/* producer `id` pushes its share in calls of `chunk` records */
+static void push_share(bp_pool* p, int id) {
+    const uint64_t lo = p->shares[id], hi = p->shares[id + 1];
+    for (uint64_t i = lo; i < hi; i += p->chunk) {
+        const uint64_t k = hi - i < p->chunk ? hi - i : p->chunk;
+        const int rc = p->push(p->node, p->src + i * 16, (size_t)k);
+        if (rc != 0) {
+            __atomic_compare_exchange_n(&p->rc, &(int){0}, rc, 0, __ATOMIC_RELAXED, __ATOMIC_RELAXED);
+            return;
+        }
+    }
+}
+
+static void run_share(bp_pool* p, int id) {
+    if (p->mode == 1)
+        push_share(p, id);
+    else
+        copy_share(p, id, p->n + 1);
 }
 
 static void* worker(void* a) {
@@ -56,7 +87,7 @@ static void* worker(void* a) {
         if (p->quit) break;
         seen = p->gen;
         pthread_mutex_unlock(&p->mu);
-        copy_share(p, me->id, p->n + 1);
+        run_share(p, me->id);
         pthread_mutex_lock(&p->mu);
         if (++p->done == p->n) pthread_cond_signal(&p->fin);
     }
@@ -84,10 +115,43 @@ BP_EXPORT void* bp_create(int threads) {
 
 /* Copies bytes from src to dst, every producer (pool threads and the caller) taking one
  * contiguous share; returns when all shares are written. */
+static void round_wait(bp_pool* p) {
+    pthread_mutex_lock(&p->mu);
+    while (p->done < p->n) pthread_cond_wait(&p->fin, &p->mu);
+    pthread_mutex_unlock(&p->mu);
+}
+
+/* Every producer (pool threads and the caller: n + 1 shares) pushes its share of `src` through
+ * push(node, records, count) in calls of `chunk` records, all at the same time; returns when all
+ * have finished: 0, or the first failing call's return code. */
+BP_EXPORT int bp_push(void* pool, void* push, void* node, const void* src, const uint64_t* shares, size_t chunk) {
+    bp_pool* p = (bp_pool*)pool;
+    if (!p || !push || !chunk) return -1;
+    pthread_mutex_lock(&p->mu);
+    p->mode = 1;
+    p->push = (int (*)(void*, const void*, size_t))push;
+    p->node = node;
+    p->src = (const char*)src;
+    p->shares = shares;
+    p->chunk = chunk;
+    p->rc = 0;
+    p->done = 0;
+    p->gen++;
+    pthread_cond_broadcast(&p->go);
+    pthread_mutex_unlock(&p->mu);
+    push_share(p, p->n);
+    round_wait(p);
+    return p->rc;
+}
+
+/* Producers in all: the pool threads + the calling thread. */
+BP_EXPORT int bp_threads(void* pool) { return pool ? ((bp_pool*)pool)->n + 1 : 0; }
+
 BP_EXPORT int bp_fill(void* pool, void* dst, const void* src, size_t bytes) {
     bp_pool* p = (bp_pool*)pool;
     if (!p) return -1;
     pthread_mutex_lock(&p->mu);
+    p->mode = 0;
     p->dst = (char*)dst;
     p->src = (const char*)src;
     p->bytes = bytes;

@@ -190,11 +190,11 @@ typedef struct rh_delta {  /* 16 bytes */
     uint16_t reserved;     /* 0                                                                 */
     int64_t  value;
 } rh_delta;
-/* Ordering inside one batch: the device applies a batch's SET deltas before its MAX deltas, and
- * two SETs to one (slot, column) race.  rh_push_deltas therefore cuts the caller's array into
- * batches so that the result equals applying the deltas one by one in array order; a producer
- * on the zero-copy path (rh_deltas_acquire/submit) must submit separately whenever a SET would
- * follow another delta to the same (slot, column). */
+/* Ordering: every batch the device applies (a staging slot of rh_push_deltas calls, or one
+ * rh_deltas_submit) leaves each (slot, column) where applying its deltas one by one in batch order
+ * leaves it -- the last SET wins and only the MAX deltas after it count (RaftLogIndex semantics per
+ * call, FollowerInfoImpl.java:93-105, 147-151) -- whatever mix of SETs and MAXes, repeated SETs
+ * included, the batch holds. */
 
 /* An event of rh_commit_batch: `slot` and an index (the new commitIndex, or the changed
  * watch-ALL level). 16 bytes. */
@@ -247,10 +247,14 @@ int rh_group_stop(rh_groups* g, uint32_t slot);
 int rh_groups_load(rh_groups* g, uint32_t first, uint32_t n, uint32_t n_host_followers, const int64_t* match,
                    const int64_t* fcommit, const int64_t* flush, const int64_t* commit,
                    const int64_t* term_start, const uint32_t* conf);
-/* Copies deltas through a pinned staging ring and applies them on the device (RaftLogIndex
- * semantics per op).  Deltas of stopped slots or of follower columns the slot's tier does not
- * have are rejected (RH_E_INVAL, nothing applied).  Returns once the caller's buffer may be
- * reused.  Thread-safe. */
+/* Copies deltas into the pinned staging ring (RaftLogIndex semantics per op, see Ordering above).
+ * Deltas of stopped slots or of follower columns the slot's tier does not have are rejected
+ * (RH_E_INVAL, nothing applied).  Returns once the caller's buffer may be reused.  Multi-producer:
+ * concurrent calls copy into ranges of the open slot reserved with one atomic each, never waiting
+ * for an evaluation, a _wait call or another producer's copy; a call's deltas keep their order and
+ * calls that do not overlap in time keep theirs.  Staged deltas reach the device when the slot is
+ * full or before the next evaluation, read, zero-copy acquire, or control call on a slot they
+ * target -- always before anything issued after the push returned. */
 int rh_push_deltas(rh_groups* g, const rh_delta* deltas, size_t n);
 /* Zero-copy producer path over the same staging ring (two pinned slots of RH_DELTA_SLOT deltas):
  * rh_deltas_acquire hands out the next slot to fill in place (waiting until its previous H2D has
@@ -271,7 +275,8 @@ int rh_deltas_submit(rh_groups* g, size_t n);
 int rh_commit_batch(rh_groups* g, uint32_t flags, rh_commit_out* out);
 /* The same split in two: _async enqueues the evaluation and returns a ticket; _wait blocks until that
  * ticket's results are ready.  Deltas and other calls may be issued in between (they are ordered
- * after it). */
+ * after it).  No call holds the table's locks while it waits on the device: producers pushing
+ * deltas during any _wait (or an _async waiting for an unread earlier result) proceed at once. */
 int rh_commit_batch_async(rh_groups* g, uint32_t flags, uint64_t* ticket);
 int rh_commit_batch_wait(rh_groups* g, uint64_t ticket, rh_commit_out* out);
 /* Where the result lists are assembled.  Every sink runs the same evaluation kernels, which write

@@ -7,8 +7,10 @@
  *     follower slots k per division, the membership word of RaftConfigurationImpl's conf / oldConf
  *     restricted to peers with a FollowerInfo (LeaderStateImpl.java:291-293);
  *   - the per-division EventProcessor thread and its UPDATE_COMMIT queue (LeaderStateImpl.java:111-188,
- *     791-816): producers append 16-byte deltas; ONE pump thread pushes them and runs the batched
- *     updateCommit over the dirty divisions;
+ *     791-816): producers append 16-byte deltas to a buffer of their own thread (no lock shared
+ *     between producers; a full buffer is pushed by its producer, the multi-producer rh_push_deltas);
+ *     ONE pump thread pushes what is left each tick and runs the batched updateCommit over the dirty
+ *     divisions;
  *   - RaftLogBase.updateCommitIndex's decision (RaftLogBase.java:121-142);
  *   - commitIndexChanged()'s watch levels (LeaderStateImpl.java:606-622) over the divisions whose
  *     follower commitIndex or leader commitIndex changed;
@@ -47,12 +49,16 @@ import java.util.Collection;
 import java.util.Deque;
 import java.util.HashMap;
 import java.util.Map;
+import java.util.Queue;
 import java.util.UUID;
 import java.util.concurrent.ConcurrentHashMap;
+import java.util.concurrent.ConcurrentLinkedQueue;
 import java.util.concurrent.TimeUnit;
+import java.util.concurrent.atomic.AtomicBoolean;
 import java.util.concurrent.atomic.AtomicLongArray;
 import java.util.concurrent.atomic.AtomicReferenceArray;
 import java.util.concurrent.locks.LockSupport;
+import java.util.concurrent.locks.ReentrantReadWriteLock;
 
 public final class HipLeaderBookkeeper implements AutoCloseable {
   /** What a division's LeaderStateImpl does with the GPU's decisions (run on the pump thread). */
@@ -78,8 +84,13 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
   private final Deque<Integer>[] freeSlots;
   private final Deque<Integer> pendingFree = new ArrayDeque<>();   // released during the current tick
   private final Map<Integer, Division> divisions = new ConcurrentHashMap<>();
-  private final ByteBuffer deltas;         // producers' deltas (node slots), drained by the pump
-  private final Object deltaLock = new Object();
+  /** Deltas per producer thread: an appender thread (GrpcLogAppender / LogAppenderDefault, one per
+   *  follower) or the log worker writes into its own buffer, so producers never contend with each
+   *  other -- only, briefly, with the pump flushing that buffer. */
+  private static final int BUFFER_DELTAS = 4096;
+  private final Queue<DeltaBuffer> buffers = new ConcurrentLinkedQueue<>();
+  private final ThreadLocal<DeltaBuffer> localBuffer = ThreadLocal.withInitial(this::newBuffer);
+  private final AtomicBoolean wake = new AtomicBoolean();   // one unpark of the pump per tick at most
   private final Thread pump;
   private final long tickNanos;
   private volatile boolean running = true;
@@ -142,7 +153,6 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
         freeSlots[s].push(i);
       }
     }
-    this.deltas = ByteBuffer.allocateDirect(RatisHip.DELTA_BYTES << 20).order(ByteOrder.LITTLE_ENDIAN);
     this.tickNanos = TimeUnit.MICROSECONDS.toNanos(tickMicros);
     // a bitmap stays meaningful for two ticks: long enough for the next one to replace it
     this.leaseMarginNanos = 2 * tickNanos;
@@ -241,31 +251,59 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
     }
   }
 
-  /** Appends one delta; the caller holds deltaLock (one ordered stream of deltas and control ops). */
-  private void putDeltaLocked(int nodeSlot, int column, int op, long value) {
-    if (deltas.remaining() < RatisHip.DELTA_BYTES) {
-      drainDeltas();
+  /**
+   * One producer thread's deltas, in its call order.  Its monitor is taken by that producer (append,
+   * and push when full) and by whoever flushes every buffer (the pump each tick, a control call
+   * before it reaches the library): a buffer is pushed whole under its monitor, so one thread's
+   * deltas reach the library in order.  Uncontended in the common case.
+   */
+  private final class DeltaBuffer {
+    private final ByteBuffer bb =
+        ByteBuffer.allocateDirect(RatisHip.DELTA_BYTES * BUFFER_DELTAS).order(ByteOrder.LITTLE_ENDIAN);
+
+    synchronized void put(int nodeSlot, int column, int op, long value) {
+      if (bb.remaining() < RatisHip.DELTA_BYTES) {
+        flushLocked();
+      }
+      RatisHip.putDelta(bb, nodeSlot, column, op, value);
     }
-    RatisHip.putDelta(deltas, nodeSlot, column, op, value);
+
+    synchronized void flush() {
+      flushLocked();
+    }
+
+    private void flushLocked() {
+      final int n = bb.position() / RatisHip.DELTA_BYTES;
+      if (n == 0) {
+        return;
+      }
+      try {
+        hip.pushDeltas(bb, n);   // multi-producer: other buffers push concurrently
+      } catch (IOException e) {
+        throw new IllegalStateException("ratis-hip: pushDeltas failed", e);
+      }
+      bb.clear();
+    }
   }
 
-  private void drainDeltas() {
-    final int n = deltas.position() / RatisHip.DELTA_BYTES;
-    if (n == 0) {
-      return;
+  private DeltaBuffer newBuffer() {
+    final DeltaBuffer b = new DeltaBuffer();
+    buffers.add(b);
+    return b;
+  }
+
+  /** Pushes every producer's buffered deltas (the pump each tick; a control call before it runs). */
+  private void flushAllDeltas() {
+    for (DeltaBuffer b : buffers) {
+      b.flush();
     }
-    try {
-      hip.pushDeltas(deltas, n);
-    } catch (IOException e) {
-      throw new IllegalStateException("ratis-hip: pushDeltas failed", e);
-    }
-    deltas.clear();
   }
 
   private void pumpLoop() {
     try {
       while (running) {
         LockSupport.parkNanos(tickNanos);
+        wake.set(false);   // deltas emitted from here on may unpark the pump once more
         tick();
       }
     } catch (Throwable t) {
@@ -279,9 +317,7 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
 
   /** One pump tick (see the class comment). */
   void tick() throws IOException {
-    synchronized (deltaLock) {
-      drainDeltas();
-    }
+    flushAllDeltas();
     final long timeout = leaseTimeoutMs;
     final long batch = timeout >= 0 ? ++leaseBatchCount : 0;
     final long now = System.nanoTime();
@@ -362,21 +398,25 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
   /**
    * One leader division's handle: its node slot and the numbering of its followers.
    *
-   * Deltas and the control calls (start / reconf / stop) go through one ordered stream under
-   * deltaLock: buffered deltas are pushed before a control call reaches the library, so a delta
-   * never lands on a slot after it was stopped (or recycled), and a delta is only emitted for a
-   * column the division's current tier has (rh_push_deltas rejects the others).  Dropping a
-   * follower column outside the tier loses nothing the commit rule reads: that slot is not in the
-   * membership word, and the widening reconf starts it at -1, as a new FollowerInfoImpl does
-   * (FollowerInfoImpl.java:42-43); the follower's next reply carries its current matchIndex.
+   * Deltas and the control calls (start / reconf / stop) are ordered per division by its
+   * read-write lock: producers emit under the READ lock (any number at once, each into its own
+   * thread's buffer), a control call holds the WRITE lock while it pushes every buffer and then
+   * calls the library -- so a delta emitted before the call reaches the library before it, none is
+   * emitted during it, and a delta never lands on a slot after it was stopped (or recycled).  A
+   * delta is only emitted for a column the division's current tier has (rh_push_deltas rejects the
+   * others).  Dropping a follower column outside the tier loses nothing the commit rule reads: that
+   * slot is not in the membership word, and the widening reconf starts it at -1, as a new
+   * FollowerInfoImpl does (FollowerInfoImpl.java:42-43); the follower's next reply carries its
+   * current matchIndex.
    */
   public final class Division {
     private final int nodeSlot;   // -1: never had one (fell back at register)
     private final RaftPeerId selfId;
     private final Callback callback;
     private final Map<RaftPeerId, Integer> followerSlot = new HashMap<>();   // peers with a FollowerInfo
-    private boolean started;   // guarded by deltaLock
-    private int width;         // follower columns of the device tier; guarded by deltaLock
+    private final ReentrantReadWriteLock order = new ReentrantReadWriteLock();
+    private boolean started;   // guarded by `order` (written under the write lock)
+    private int width;         // follower columns of the device tier; guarded by `order`
     private volatile boolean fallback;   // the reference's per-division path from now on
     private volatile long leaseArmedAfter = Long.MAX_VALUE;   // lease batches up to this one predate leaseStart
 
@@ -398,7 +438,8 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
      */
     void fallBack(FallbackReason reason) {
       boolean release = false;
-      synchronized (deltaLock) {
+      order.writeLock().lock();
+      try {
         if (fallback) {
           return;
         }
@@ -409,13 +450,15 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
           if (started) {
             started = false;
             try {
-              drainDeltas();
+              flushAllDeltas();
               hip.stop(nodeSlot);
             } catch (IOException | RuntimeException ignored) {
               // the slot is released below and never evaluated for this division again
             }
           }
         }
+      } finally {
+        order.writeLock().unlock();
       }
       fallbacks.incrementAndGet(reason.ordinal());
       if (release) {
@@ -425,13 +468,18 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
     }
 
     private void emit(int follower, int column, int op, long value) {
-      synchronized (deltaLock) {
+      order.readLock().lock();
+      try {
         if (!started || follower >= width) {
           return;
         }
-        putDeltaLocked(nodeSlot, column, op, value);
+        localBuffer.get().put(nodeSlot, column, op, value);
+      } finally {
+        order.readLock().unlock();
       }
-      LockSupport.unpark(pump);
+      if (!wake.get() && wake.compareAndSet(false, true)) {
+        LockSupport.unpark(pump);   // the first delta since the pump's last wake-up only
+      }
     }
 
     /**
@@ -498,12 +546,13 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
      */
     public void start(int conf, long flushIndex, long commitIndex, long termStart) {
       FallbackReason why = null;
-      synchronized (deltaLock) {
+      order.writeLock().lock();
+      try {
         if (fallback) {
           return;
         }
         try {
-          drainDeltas();
+          flushAllDeltas();
           hip.start(nodeSlot, conf, flushIndex, commitIndex, termStart);
           width = tierWidth(conf);
           started = true;
@@ -512,6 +561,8 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
         } catch (IOException | RuntimeException e) {
           why = FallbackReason.DEVICE_ERROR;
         }
+      } finally {
+        order.writeLock().unlock();
       }
       if (why != null) {
         fallBack(why);
@@ -531,12 +582,13 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
         src[k] = (byte) k;
       }
       FallbackReason why = null;
-      synchronized (deltaLock) {
+      order.writeLock().lock();
+      try {
         if (!started || fallback) {
           return;
         }
         try {
-          drainDeltas();
+          flushAllDeltas();
           hip.reconf(nodeSlot, conf, src);
           width = tierWidth(conf);
         } catch (IllegalArgumentException e) {
@@ -544,6 +596,8 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
         } catch (IOException | RuntimeException e) {
           why = FallbackReason.DEVICE_ERROR;
         }
+      } finally {
+        order.writeLock().unlock();
       }
       if (why != null) {
         fallBack(why);
@@ -552,14 +606,17 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
 
     /** Step-down (LeaderStateImpl.stop, LeaderStateImpl.java:470-490): the node slot is released. */
     public void stop() throws IOException {
-      synchronized (deltaLock) {
+      order.writeLock().lock();
+      try {
         if (!started) {
           return;
         }
-        drainDeltas();
+        flushAllDeltas();
         started = false;
         leaseArmedAfter = Long.MAX_VALUE;
         hip.stop(nodeSlot);
+      } finally {
+        order.writeLock().unlock();
       }
       release(this);
     }
@@ -602,12 +659,13 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
     /** The division's LeaderLease (lease = now, enabled per config) with every follower stamped now. */
     public void leaseStart(long nowNanos, boolean enabled) {
       FallbackReason why = null;
-      synchronized (deltaLock) {
+      order.writeLock().lock();
+      try {
         if (!started || fallback) {
           return;
         }
         try {
-          drainDeltas();
+          flushAllDeltas();
           // batches already started may predate this lease: only a later one answers hasLease()
           leaseArmedAfter = leaseBatchCount;
           hip.leaseStart(nodeSlot, nowNanos, enabled);
@@ -616,6 +674,8 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
         } catch (IOException | RuntimeException e) {
           why = FallbackReason.DEVICE_ERROR;
         }
+      } finally {
+        order.writeLock().unlock();
       }
       if (why != null) {
         fallBack(why);

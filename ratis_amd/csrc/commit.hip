@@ -27,6 +27,9 @@ constexpr int kBlock = 256;            // 4 waves
 #define RH_COMMIT_WAVES 8
 #endif
 constexpr int kGroupsPerLane = 2;      // 16-byte loads per column per lane
+#ifndef RH_COMMIT_BITS_DIRECT  // A/B builds: 1 = each wave stores its bit words itself (no LDS staging)
+#define RH_COMMIT_BITS_DIRECT 0
+#endif
 
 struct TierArgs {
     rh_commit_soa t;
@@ -185,10 +188,21 @@ __device__ __forceinline__ void compute_store_sub(const TierArgs& ta, uint64_t w
         const int sel = lane & 1;
         const uint64_t v0 = __ballot((lo >> sel) & 1), v1 = __ballot((hi >> sel) & 1);
         const uint64_t a0 = __ballot((lo >> (2 + sel)) & 1), a1 = __ballot((hi >> (2 + sel)) & 1);
+#if RH_COMMIT_BITS_DIRECT
+        // A/B: every wave stores its own two words per column (no LDS staging, no block barrier)
+        (void)wave;
+        (void)bits;
+        const uint64_t word = (wbase >> 6) + (uint64_t)lane;
+        if (lane < 2 && word < ((t.n + 63) >> 6)) {
+            if (t.valid_bits) t.valid_bits[word] = lane ? v1 : v0;
+            if (t.advanced_bits) t.advanced_bits[word] = lane ? a1 : a0;
+        }
+#else
         if (lane < 2) {
             bits[0][2 * wave + lane] = lane ? v1 : v0;
             bits[1][2 * wave + lane] = lane ? a1 : a0;
         }
+#endif
     }
 
     // ---- compacted advanced list: one atomic per wave ----
@@ -234,7 +248,7 @@ __device__ __forceinline__ void run_tile(const TierArgs& ta, uint64_t tile) {
             compute_store_sub<F, false, RANK>(ta, wchunk, commit_mode, st, bits);
         }
     }
-    if (!ta.t.valid_bits && !ta.t.advanced_bits) return;  // block-uniform
+    if (RH_COMMIT_BITS_DIRECT || (!ta.t.valid_bits && !ta.t.advanced_bits)) return;  // block-uniform
     __syncthreads();
     if (threadIdx.x < 16) {
         const int col = threadIdx.x >> 3, k = threadIdx.x & 7;

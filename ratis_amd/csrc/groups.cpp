@@ -6,11 +6,12 @@
 // the UPDATE_COMMIT event queue (LeaderStateImpl.java:111-188, 846-854, 900-902) and the
 // RaftServerProxy's map of divisions (RaftServerProxy.java:89-150) for the multi-GPU node.
 #include <algorithm>
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <shared_mutex>
 #include <string>
-#include <unordered_set>
 #include <vector>
 
 #include "rh_internal.h"
@@ -74,6 +75,11 @@ struct rh_groups {
     uint64_t capacity = 0;
     int64_t gap = -1;
     std::mutex mu;
+    // Delta staging (rh_push_deltas, multi-producer): `smu` shared = producers validating and copying
+    // into the open host slot at ranges reserved with one CAS on `fill`; exclusive = whoever
+    // submits the staged deltas (a full slot, an evaluation, a control op on a staged slot, a read,
+    // the zero-copy path).  Lock order: smu, then mu.  `mu` guards everything else.
+    std::shared_mutex smu;
     rh::TableDev dev;                         // device pointers (copied into every launch)
     std::vector<uint32_t> slot_map;           // host mirror of dev.slot_map
     std::vector<uint32_t> slot_conf;          // host mirror of each started slot's conf word
@@ -96,6 +102,12 @@ struct rh_groups {
     bool ring_used[2] = {false, false};
     int ring_next = 0;
     int ring_acquired = -1;
+    int open = -1;                            // host slot open for rh_push_deltas (-1: none)
+    std::atomic<uint64_t> fill{0};            // deltas reserved in the open slot
+    std::atomic<bool> staged_set{false};      // some staged delta is a SET
+    uint32_t stage_gen = 1;                   // generation of the open slot's contents
+    std::vector<uint32_t> slot_staged;        // slot -> stage_gen of its last staged delta (atomic stores)
+    uint32_t apply_gen = 0;                   // order-key generation of the last batch with SETs
     hipStream_t copy_stream = nullptr;       // H2D of delta slots and control ops
     hipStream_t d2h_stream = nullptr;        // the result lists' way to the host: RH_EVENTS_DEVICE's D2H in
                                              // _wait, RH_EVENTS_AUTO's drain kernel after the evaluation
@@ -113,8 +125,10 @@ struct rh_groups {
     uint64_t* d_wcnt = nullptr;
     hipEvent_t wdone = nullptr;
     bool wpending = false, whbm = false;
+    uint64_t wgen = 0;                        // watch evaluations started (a waiter re-validates it)
     hipEvent_t ldone = nullptr;               // rh_lease_batch_async's bitmap D2H
     bool lpending = false;
+    uint64_t lgen = 0;
     // dirty-row lists (rh_internal.h, TableLists), per kind (0 = updateCommit, 1 = commitIndexChanged)
     uint32_t* d_lrows[2] = {nullptr, nullptr};   // [kHeads][lcap]: (tier << 28) | row
     unsigned long long* d_lheads = nullptr;      // [2 kinds][2 sets][kHeads * kHeadStride]
@@ -157,6 +171,7 @@ int halloc_mapped(T** host, T** dev, size_t count) {
 void free_tier(rh::TableTier& t) {
     (void)hipFree(t.base);
     (void)hipFree(t.sum);
+    (void)hipFree(t.shadow);
     t = rh::TableTier{};
 }
 
@@ -212,6 +227,7 @@ int grow_tier(rh_groups* g, int t, uint32_t rows) {
     const uint32_t tiles = rows / rh::kTileRows, keep = o.rows / rh::kTileRows;
     int rc = dalloc(&n.base, (size_t)tiles * TB);
     if (rc == RH_OK) rc = dalloc(&n.sum, (size_t)tiles * 2);
+    if (rc == RH_OK) rc = dalloc(&n.shadow, (size_t)tiles * TB);
     if (rc != RH_OK) {
         free_tier(n);
         return rc;
@@ -222,6 +238,8 @@ int grow_tier(rh_groups* g, int t, uint32_t rows) {
         e = hipMemcpyAsync(n.base, o.base, (size_t)keep * TB, hipMemcpyDeviceToDevice, s);
         if (e == hipSuccess) e = hipMemcpyAsync(n.sum, o.sum, (size_t)keep * 2, hipMemcpyDeviceToDevice, s);
     }
+    // order keys of earlier batches never matter again (a key counts only within its generation)
+    if (e == hipSuccess) e = hipMemsetAsync(n.shadow, 0, (size_t)tiles * TB, s);
     if (e == hipSuccess) rc = rh_table_init_tiles(n, keep, tiles - keep, s);
     if (e == hipSuccess && rc == RH_OK) e = hipStreamSynchronize(s);
     if (e != hipSuccess || rc != RH_OK) {
@@ -435,7 +453,8 @@ int ring_wait(rh_groups* g, int i) {
 }
 
 // H2D of the first n deltas of ring slot i on the copy stream (after the previous apply that read
-// device slot i), then the SET and MAX phases on the table stream (after that H2D).
+// device slot i), then the apply phases on the table stream (after that H2D).  has_set: the batch
+// may hold SET deltas (their order keys are recorded first, rh_internal.h ApplyPhase).
 int ring_submit(rh_groups* g, int i, size_t n, bool has_set) {
     hipStream_t s = g->ctx->stream, cs = g->copy_stream;
     int rc = flush_ops(g);
@@ -450,14 +469,78 @@ int ring_submit(rh_groups* g, int i, size_t n, bool has_set) {
     const rh::TableLists lc = lists_for(g, 0, n), lw = lists_for(g, 1, n);
     g->marks[0] += n;
     g->marks[1] += n;
+    uint32_t gen = 0;
     if (has_set) {
-        rc = rh_table_apply_deltas(g->dev, g->d_ring[i], n, 0, lc, lw, s);
+        if (g->apply_gen == 0xFFFFFFFFu) {   // generations wrapped: no stale key may look current
+            for (const rh::TableTier& t : g->dev.tier)
+                if (t.shadow) RH_HIP(hipMemsetAsync(t.shadow, 0, (size_t)(t.rows / rh::kTileRows) * rh::tile::bytes(t.width), s));
+            g->apply_gen = 0;
+        }
+        gen = ++g->apply_gen;
+        rc = rh_table_apply_deltas(g->dev, g->d_ring[i], n, kApplyKeys, gen, lc, lw, s);
+        if (rc == RH_OK) rc = rh_table_apply_deltas(g->dev, g->d_ring[i], n, kApplySet, gen, lc, lw, s);
         if (rc != RH_OK) return rc;
     }
-    rc = rh_table_apply_deltas(g->dev, g->d_ring[i], n, 1, lc, lw, s);
+    rc = rh_table_apply_deltas(g->dev, g->d_ring[i], n, kApplyMax, gen, lc, lw, s);
     if (rc != RH_OK) return rc;
     RH_HIP(hipEventRecord(g->ring_read[i], s));
     return RH_OK;
+}
+
+// ---- delta staging (callers hold smu exclusively and mu) ----
+// Submits the deltas staged in the open slot (H2D + apply, ordered after every call before this).
+int stage_submit(rh_groups* g) {
+    if (g->open < 0) return RH_OK;
+    const int i = g->open;
+    const uint64_t n = std::min<uint64_t>(g->fill.load(std::memory_order_relaxed), RH_DELTA_SLOT);
+    g->open = -1;
+    g->fill.store(0, std::memory_order_relaxed);
+    const bool has_set = g->staged_set.exchange(false, std::memory_order_relaxed);
+    ++g->stage_gen;
+    if (n == 0) return RH_OK;
+    return ring_submit(g, i, n, has_set);
+}
+
+// Submits the staged deltas if any targets `slot` (a control op on it must follow them).
+int stage_submit_for(rh_groups* g, uint32_t slot) {
+    if (g->open < 0 || g->slot_staged[slot] != g->stage_gen) return RH_OK;
+    return stage_submit(g);
+}
+
+// Opens the next host slot for rh_push_deltas (waiting until its previous H2D has completed).
+int stage_open(rh_groups* g) {
+    int rc = stage_submit(g);
+    if (rc != RH_OK) return rc;
+    const int i = g->ring_next;
+    rc = ring_wait(g, i);
+    if (rc != RH_OK) return rc;
+    g->open = i;
+    g->fill.store(0, std::memory_order_relaxed);
+    return RH_OK;
+}
+
+// The exclusive side of the staging: both locks, staged deltas submitted first.
+struct Exclusive {
+    std::unique_lock<std::shared_mutex> x;
+    std::unique_lock<std::mutex> m;
+    explicit Exclusive(rh_groups* g) : x(g->smu), m(g->mu) {}
+    void unlock() {
+        m.unlock();
+        x.unlock();
+    }
+    void lock() {
+        x.lock();
+        m.lock();
+    }
+};
+
+// Waits for `ev` with both locks released (producers and readers go on meanwhile), then takes them
+// again.
+int wait_unlocked(Exclusive& ex, hipEvent_t ev) {
+    ex.unlock();
+    const hipError_t e = hipEventSynchronize(ev);
+    ex.lock();
+    return e == hipSuccess ? RH_OK : rh::hip_fail(e, "hipEventSynchronize");
 }
 
 int check_conf(uint32_t conf, const char* who) {
@@ -487,6 +570,7 @@ RH_EXPORT int rh_groups_create(rh_ctx* ctx, uint64_t capacity, int64_t gap_thres
         g->slot_map.assign(capacity, kNoRow);
         g->slot_conf.assign(capacity, 0);
         g->op_stamp.assign(capacity, 0);
+        g->slot_staged.assign(capacity, 0);
     } catch (...) {
         rc = rh::fail(RH_E_NOMEM, "rh_groups_create: out of host memory");
     }
@@ -593,11 +677,14 @@ RH_EXPORT int rh_groups_timing(rh_groups* g, int enable) {
 RH_EXPORT int rh_groups_last_timing(rh_groups* g, float* eval_ms, int* list_evaluated) {
     if (!g || !eval_ms) return rh::fail(RH_E_INVAL, "rh_groups_last_timing: NULL argument");
     DeviceGuard dg(g->ctx->device);
-    std::lock_guard<std::mutex> lk(g->mu);
+    std::unique_lock<std::mutex> lk(g->mu);
     if (!g->timed) return rh::fail(RH_E_STATE, "rh_groups_last_timing: no timed evaluation");
-    RH_HIP(hipEventSynchronize(g->tev[1]));
-    RH_HIP(hipEventElapsedTime(eval_ms, g->tev[0], g->tev[1]));
-    if (list_evaluated) *list_evaluated = g->last_list ? 1 : 0;
+    const hipEvent_t t0 = g->tev[0], t1 = g->tev[1];
+    const bool was_list = g->last_list;
+    lk.unlock();   // no table lock across a device wait
+    RH_HIP(hipEventSynchronize(t1));
+    RH_HIP(hipEventElapsedTime(eval_ms, t0, t1));
+    if (list_evaluated) *list_evaluated = was_list ? 1 : 0;
     return RH_OK;
 }
 
@@ -609,7 +696,9 @@ RH_EXPORT int rh_group_start(rh_groups* g, uint32_t slot, uint32_t conf, int64_t
     int rc = check_conf(conf, "rh_group_start");
     if (rc != RH_OK) return rc;
     DeviceGuard dg(g->ctx->device);
-    std::lock_guard<std::mutex> lk(g->mu);
+    Exclusive ex(g);
+    rc = stage_submit_for(g, slot);   // deltas staged for the slot come before its re-start
+    if (rc != RH_OK) return rc;
     rc = do_stop(g, slot);  // a re-armed slot drops its old row (and every FollowerInfo with it)
     if (rc != RH_OK) return rc;
     const int t = rh::tier_of_width(needed_width(conf));
@@ -641,9 +730,11 @@ RH_EXPORT int rh_group_reconf(rh_groups* g, uint32_t slot, uint32_t conf, const 
             if (src[k] < -1 || src[k] >= (int)RH_MAX_FOLLOWERS)
                 return rh::fail(RH_E_INVAL, "rh_group_reconf: src entries must be -1 or a follower slot");
     DeviceGuard dg(g->ctx->device);
-    std::lock_guard<std::mutex> lk(g->mu);
+    Exclusive ex(g);
     const uint32_t m = g->slot_map[slot];
     if (m == kNoRow) return rh::fail(RH_E_STATE, "rh_group_reconf: slot not started");
+    rc = stage_submit_for(g, slot);   // deltas staged for the slot apply under its old conf
+    if (rc != RH_OK) return rc;
     const int t_old = (int)(m >> 28);
     const int t_new = rh::tier_of_width(needed_width(conf));
     CtrlOp op{};
@@ -673,8 +764,9 @@ RH_EXPORT int rh_group_stop(rh_groups* g, uint32_t slot) {
     if (!g) return rh::fail(RH_E_INVAL, "rh_group_stop: groups == NULL");
     if (slot >= g->capacity) return rh::fail(RH_E_INVAL, "rh_group_stop: slot out of range");
     DeviceGuard dg(g->ctx->device);
-    std::lock_guard<std::mutex> lk(g->mu);
-    return do_stop(g, slot);
+    Exclusive ex(g);
+    int rc = stage_submit_for(g, slot);
+    return rc != RH_OK ? rc : do_stop(g, slot);
 }
 
 RH_EXPORT int rh_group_tier(rh_groups* g, uint32_t slot, uint32_t* out_width) {
@@ -736,12 +828,14 @@ RH_EXPORT int rh_groups_load(rh_groups* g, uint32_t first, uint32_t n, uint32_t 
         if (rc != RH_OK) return rc;
     }
     DeviceGuard dg(g->ctx->device);
-    std::lock_guard<std::mutex> lk(g->mu);
+    Exclusive ex(g);
+    int rc = stage_submit(g);
+    if (rc != RH_OK) return rc;
     for (uint32_t i = 0; i < n; ++i) {
-        int rc = do_stop(g, first + i);
+        rc = do_stop(g, first + i);
         if (rc != RH_OK) return rc;
     }
-    int rc = flush_ops(g);  // launches the stops; the rows they released are reusable now
+    rc = flush_ops(g);  // launches the stops; the rows they released are reusable now
     if (rc != RH_OK) return rc;
     g->lvalid[0] = g->lvalid[1] = false;   // the load marks its rows with plain stores
     hipStream_t s = g->ctx->stream;
@@ -801,56 +895,65 @@ RH_EXPORT int rh_groups_load(rh_groups* g, uint32_t first, uint32_t n, uint32_t 
 }
 
 // ---- deltas ------------------------------------------------------------------------------------------
+// Multi-producer: each call validates its deltas and copies them into the open pinned slot at a range
+// it reserved with one CAS, holding the staging lock SHARED -- producers on other threads copy at the
+// same time, and no producer waits for an evaluation, a watch or lease wait, or another producer's
+// copy.  The slot goes to the device (H2D + apply) when it is full or when an evaluation, a read, a
+// control op on a staged slot or the zero-copy path needs the deltas before it; the device applies a
+// batch in slot order with one-by-one semantics (rh_internal.h, ApplyPhase), so a call's deltas
+// keep their array order and calls that do not overlap in time keep theirs.
 RH_EXPORT int rh_push_deltas(rh_groups* g, const rh_delta* deltas, size_t n) {
     if (!g) return rh::fail(RH_E_INVAL, "rh_push_deltas: groups == NULL");
     if (n == 0) return RH_OK;
     if (!deltas) return rh::fail(RH_E_INVAL, "rh_push_deltas: deltas == NULL");
-    DeviceGuard dg(g->ctx->device);
-    std::lock_guard<std::mutex> lk(g->mu);
-    if (g->ring_acquired >= 0) return rh::fail(RH_E_STATE, "rh_push_deltas: a staging slot is acquired");
-    bool any_set = false;
-    for (size_t i = 0; i < n; ++i) {
-        const rh_delta& d = deltas[i];
-        const uint32_t m = d.slot < g->capacity ? g->slot_map[d.slot] : kNoRow;
-        const uint32_t w = m == kNoRow ? 0u : rh::width_of_tier((int)(m >> 28));
-        const uint32_t c = d.column;
-        const bool ok_col = c < w || (c >= 16 && c < 16 + w) || c == RH_COL_FLUSH || c == RH_COL_COMMITTED ||
-                            (c >= 48 && c < 48 + w) || c == RH_COL_LEASE || c == RH_COL_LEASE_ON;
-        if (m == kNoRow || !ok_col || d.op > RH_OP_SET)
-            return rh::fail(RH_E_INVAL, "rh_push_deltas: delta " + std::to_string(i) +
-                                            " names a stopped slot, a column outside its tier or an unknown op");
-        any_set |= d.op == RH_OP_SET;
-    }
-    // Batches: a SET to a (slot, column) already touched in the current batch starts a new one, so
-    // SET-then-MAX phases reproduce the one-by-one order (ratis_hip.h, rh_delta).
-    std::unordered_set<uint64_t> touched;
+    bool validated = false, any_set = false;
     size_t done = 0;
     while (done < n) {
-        size_t end = std::min(n, done + (size_t)RH_DELTA_SLOT);
-        bool batch_set = false;
-        if (any_set) {
-            touched.clear();
-            for (size_t i = done; i < end; ++i) {
-                const uint64_t cell = (uint64_t)deltas[i].slot * 64 + deltas[i].column;
-                if (deltas[i].op == RH_OP_SET) {
-                    if (!touched.insert(cell).second) {
-                        end = i;
+        {
+            std::shared_lock<std::shared_mutex> sl(g->smu);   // the slot map changes only under exclusive
+            if (g->ring_acquired >= 0) return rh::fail(RH_E_STATE, "rh_push_deltas: a staging slot is acquired");
+            if (!validated) {
+                for (size_t i = 0; i < n; ++i) {
+                    const rh_delta& d = deltas[i];
+                    const uint32_t m = d.slot < g->capacity ? g->slot_map[d.slot] : kNoRow;
+                    const uint32_t w = m == kNoRow ? 0u : rh::width_of_tier((int)(m >> 28));
+                    const uint32_t c = d.column;
+                    const bool ok_col = c < w || (c >= 16 && c < 16 + w) || c == RH_COL_FLUSH || c == RH_COL_COMMITTED ||
+                                        (c >= 48 && c < 48 + w) || c == RH_COL_LEASE || c == RH_COL_LEASE_ON;
+                    if (m == kNoRow || !ok_col || d.op > RH_OP_SET)
+                        return rh::fail(RH_E_INVAL, "rh_push_deltas: delta " + std::to_string(i) +
+                                                        " names a stopped slot, a column outside its tier or an unknown op");
+                    any_set |= d.op == RH_OP_SET;
+                }
+                validated = true;
+            }
+            if (g->open >= 0) {
+                uint64_t r = g->fill.load(std::memory_order_relaxed), take = 0;
+                do {
+                    if (r >= RH_DELTA_SLOT) {
+                        take = 0;
                         break;
                     }
-                    batch_set = true;
-                } else {
-                    touched.insert(cell);
+                    take = std::min<uint64_t>(n - done, RH_DELTA_SLOT - r);
+                } while (!g->fill.compare_exchange_weak(r, r + take, std::memory_order_relaxed));
+                if (take) {
+                    if (any_set) g->staged_set.store(true, std::memory_order_relaxed);
+                    std::memcpy(g->h_ring[g->open] + r, deltas + done, take * sizeof(rh_delta));
+                    const uint32_t sg = g->stage_gen;
+                    for (size_t i = done; i < done + take; ++i) __atomic_store_n(&g->slot_staged[deltas[i].slot], sg, __ATOMIC_RELAXED);
+                    done += take;
+                    continue;
                 }
             }
         }
-        const int i = g->ring_next;
-        int rc = ring_wait(g, i);
-        if (rc == RH_OK) {
-            std::memcpy(g->h_ring[i], deltas + done, (end - done) * sizeof(rh_delta));
-            rc = ring_submit(g, i, end - done, batch_set);
+        // no open slot, or it is full: submit it and open the next one
+        DeviceGuard dg(g->ctx->device);
+        Exclusive ex(g);
+        if (g->ring_acquired >= 0) return rh::fail(RH_E_STATE, "rh_push_deltas: a staging slot is acquired");
+        if (g->open < 0 || g->fill.load(std::memory_order_relaxed) >= RH_DELTA_SLOT) {
+            int rc = stage_open(g);
+            if (rc != RH_OK) return rc;
         }
-        if (rc != RH_OK) return rc;
-        done = end;
     }
     return RH_OK;
 }
@@ -858,10 +961,12 @@ RH_EXPORT int rh_push_deltas(rh_groups* g, const rh_delta* deltas, size_t n) {
 RH_EXPORT int rh_deltas_acquire(rh_groups* g, rh_delta** out_buf, size_t* out_cap) {
     if (!g || !out_buf || !out_cap) return rh::fail(RH_E_INVAL, "rh_deltas_acquire: NULL argument");
     DeviceGuard dg(g->ctx->device);
-    std::lock_guard<std::mutex> lk(g->mu);
+    Exclusive ex(g);
     if (g->ring_acquired >= 0) return rh::fail(RH_E_STATE, "rh_deltas_acquire: a slot is already acquired");
+    int rc = stage_submit(g);   // the pushed deltas precede the acquired slot's
+    if (rc != RH_OK) return rc;
     const int i = g->ring_next;
-    int rc = ring_wait(g, i);
+    rc = ring_wait(g, i);
     if (rc != RH_OK) return rc;
     g->ring_acquired = i;
     *out_buf = g->h_ring[i];
@@ -872,7 +977,7 @@ RH_EXPORT int rh_deltas_acquire(rh_groups* g, rh_delta** out_buf, size_t* out_ca
 RH_EXPORT int rh_deltas_submit(rh_groups* g, size_t n) {
     if (!g) return rh::fail(RH_E_INVAL, "rh_deltas_submit: groups == NULL");
     DeviceGuard dg(g->ctx->device);
-    std::lock_guard<std::mutex> lk(g->mu);
+    Exclusive ex(g);
     const int i = g->ring_acquired;
     if (i < 0) return rh::fail(RH_E_STATE, "rh_deltas_submit: no slot acquired");
     if (n > RH_DELTA_SLOT) return rh::fail(RH_E_INVAL, "rh_deltas_submit: n exceeds the slot capacity");
@@ -882,22 +987,30 @@ RH_EXPORT int rh_deltas_submit(rh_groups* g, size_t n) {
 }
 
 // ---- evaluation -------------------------------------------------------------------------------------
+// No table lock is held across a device wait: a wait for an earlier evaluation (its result buffers
+// are about to be rewritten) and the _wait calls release both locks first, then re-validate.
 RH_EXPORT int rh_commit_batch_async(rh_groups* g, uint32_t flags, uint64_t* ticket) {
     if (!g || !ticket) return rh::fail(RH_E_INVAL, "rh_commit_batch_async: NULL argument");
     if (flags & ~RH_COMMIT_WATCH_ALL) return rh::fail(RH_E_INVAL, "rh_commit_batch_async: unknown flags");
     DeviceGuard dg(g->ctx->device);
-    std::lock_guard<std::mutex> lk(g->mu);
+    Exclusive ex(g);
     const uint64_t tk = g->next_ticket++;
     EvSet& e = g->ev[tk % kEvSets];
-    if (e.pending) RH_HIP(hipEventSynchronize(e.done));  // its buffers are about to be rewritten
-    e.pending = false;
+    while (e.pending) {   // an unread earlier result set: wait for it before rewriting its buffers
+        const uint64_t was = e.ticket;
+        int rc = wait_unlocked(ex, e.done);
+        if (rc != RH_OK) return rc;
+        if (e.pending && e.ticket == was) e.pending = false;
+    }
     e.ticket = 0;
+    int rc = stage_submit(g);   // the deltas pushed before this call
+    if (rc != RH_OK) return rc;
     const bool wall_on = (flags & RH_COMMIT_WATCH_ALL) != 0;
     EvTargets t;
     t.adv[0] = e.d_adv, t.adv[1] = e.hbm_adv;
     t.wall[0] = e.d_wall, t.wall[1] = e.hbm_wall;
     bool hbm = false;
-    int rc = evaluate(g, RH_MODE_COMMIT, wall_on, t, e.d_cnt, e.h_cnt, &hbm);
+    rc = evaluate(g, RH_MODE_COMMIT, wall_on, t, e.d_cnt, e.h_cnt, &hbm);
     if (rc != RH_OK) return rc;
     if (hbm && g->event_sink == RH_EVENTS_AUTO) {   // drained into the pinned lists on the side stream
         RH_HIP(hipEventRecord(g->evaluated, g->ctx->stream));
@@ -921,22 +1034,29 @@ RH_EXPORT int rh_commit_batch_wait(rh_groups* g, uint64_t ticket, rh_commit_out*
     if (!g || !out) return rh::fail(RH_E_INVAL, "rh_commit_batch_wait: NULL argument");
     DeviceGuard dg(g->ctx->device);
     EvSet* e;
+    hipEvent_t done;
     {
         std::lock_guard<std::mutex> lk(g->mu);
         e = &g->ev[ticket % kEvSets];
         if (e->ticket != ticket || ticket == 0) return rh::fail(RH_E_STATE, "rh_commit_batch_wait: ticket unknown or superseded");
+        done = e->done;
     }
-    RH_HIP(hipEventSynchronize(e->done));
-    std::lock_guard<std::mutex> lk(g->mu);
+    RH_HIP(hipEventSynchronize(done));
+    std::unique_lock<std::mutex> lk(g->mu);
     if (e->ticket != ticket) return rh::fail(RH_E_STATE, "rh_commit_batch_wait: ticket superseded while waiting");
     const uint64_t na = std::min<uint64_t>(e->h_cnt[0], g->capacity);
     const uint64_t nw = std::min<uint64_t>(e->h_cnt[1], g->capacity);
-    if (e->hbm) {  // lists in HBM: the counted prefixes to the pinned result buffers
+    if (e->hbm) {  // lists in HBM (DEVICE sink): the counted prefixes to the pinned result buffers
         e->hbm = false;
         hipStream_t s = g->d2h_stream;
         if (na) RH_HIP(hipMemcpyAsync(e->adv, e->hbm_adv, na * sizeof(rh_index_event), hipMemcpyDeviceToHost, s));
         if (nw) RH_HIP(hipMemcpyAsync(e->wall, e->hbm_wall, nw * sizeof(rh_index_event), hipMemcpyDeviceToHost, s));
-        if (na || nw) RH_HIP(hipStreamSynchronize(s));
+        RH_HIP(hipEventRecord(e->done, s));
+        done = e->done;
+        lk.unlock();   // the set stays this ticket's (pending) while the copy runs
+        RH_HIP(hipEventSynchronize(done));
+        lk.lock();
+        if (e->ticket != ticket) return rh::fail(RH_E_STATE, "rh_commit_batch_wait: ticket superseded while waiting");
     }
     e->pending = false;
     out->advanced = e->adv;
@@ -956,13 +1076,19 @@ RH_EXPORT int rh_commit_batch(rh_groups* g, uint32_t flags, rh_commit_out* out) 
 RH_EXPORT int rh_watch_levels_async(rh_groups* g) {
     if (!g) return rh::fail(RH_E_INVAL, "rh_watch_levels_async: groups == NULL");
     DeviceGuard dg(g->ctx->device);
-    std::lock_guard<std::mutex> lk(g->mu);
-    if (g->wpending) RH_HIP(hipEventSynchronize(g->wdone));  // the previous list is about to be rewritten
-    g->wpending = false;
+    Exclusive ex(g);
+    while (g->wpending) {   // the previous list is about to be rewritten: wait for it, unlocked
+        const uint64_t was = g->wgen;
+        int rc = wait_unlocked(ex, g->wdone);
+        if (rc != RH_OK) return rc;
+        if (g->wpending && g->wgen == was) g->wpending = false;
+    }
+    int rc = stage_submit(g);
+    if (rc != RH_OK) return rc;
     EvTargets t;
     t.watch[0] = g->d_watch, t.watch[1] = g->hbm_watch;
     bool hbm = false;
-    int rc = evaluate(g, RH_MODE_WATCH, false, t, g->d_wcnt, g->h_wcnt, &hbm);
+    rc = evaluate(g, RH_MODE_WATCH, false, t, g->d_wcnt, g->h_wcnt, &hbm);
     if (rc != RH_OK) return rc;
     if (hbm && g->event_sink == RH_EVENTS_AUTO) {   // drained into the pinned list on the side stream
         RH_HIP(hipEventRecord(g->evaluated, g->ctx->stream));
@@ -975,6 +1101,7 @@ RH_EXPORT int rh_watch_levels_async(rh_groups* g) {
         RH_HIP(hipEventRecord(g->wdone, g->ctx->stream));
     }
     g->whbm = hbm;
+    ++g->wgen;
     g->wpending = true;
     return RH_OK;
 }
@@ -982,13 +1109,24 @@ RH_EXPORT int rh_watch_levels_async(rh_groups* g) {
 RH_EXPORT int rh_watch_levels_wait(rh_groups* g, const rh_watch_event** out_events, uint64_t* out_n) {
     if (!g || !out_events || !out_n) return rh::fail(RH_E_INVAL, "rh_watch_levels_wait: NULL argument");
     DeviceGuard dg(g->ctx->device);
-    std::lock_guard<std::mutex> lk(g->mu);
+    std::unique_lock<std::mutex> lk(g->mu);
     if (!g->wpending) return rh::fail(RH_E_STATE, "rh_watch_levels_wait: no watch evaluation in flight");
-    RH_HIP(hipEventSynchronize(g->wdone));
+    const uint64_t gen = g->wgen;
+    hipEvent_t done = g->wdone;
+    lk.unlock();   // no table lock across a device wait
+    RH_HIP(hipEventSynchronize(done));
+    lk.lock();
+    if (!g->wpending || g->wgen != gen) return rh::fail(RH_E_STATE, "rh_watch_levels_wait: superseded while waiting");
     const uint64_t n = std::min<uint64_t>(g->h_wcnt[0], g->capacity);
-    if (g->whbm && n) {
+    if (g->whbm && n) {   // DEVICE sink: the counted prefix to the pinned list
+        g->whbm = false;
         RH_HIP(hipMemcpyAsync(g->watch, g->hbm_watch, n * sizeof(rh_watch_event), hipMemcpyDeviceToHost, g->d2h_stream));
-        RH_HIP(hipStreamSynchronize(g->d2h_stream));
+        RH_HIP(hipEventRecord(g->wdone, g->d2h_stream));
+        done = g->wdone;
+        lk.unlock();
+        RH_HIP(hipEventSynchronize(done));
+        lk.lock();
+        if (!g->wpending || g->wgen != gen) return rh::fail(RH_E_STATE, "rh_watch_levels_wait: superseded while waiting");
     }
     g->wpending = false;
     *out_events = g->watch;
@@ -1012,9 +1150,10 @@ RH_EXPORT int rh_groups_read(rh_groups* g, uint32_t first, uint32_t n, uint8_t c
         return rh::fail(RH_E_INVAL, "rh_groups_read: unknown column");
     if (n == 0) return RH_OK;
     DeviceGuard dg(g->ctx->device);
-    std::lock_guard<std::mutex> lk(g->mu);
+    Exclusive ex(g);
     hipStream_t s = g->ctx->stream;
-    int rc = flush_ops(g);
+    int rc = stage_submit(g);   // the deltas pushed before this call
+    if (rc == RH_OK) rc = flush_ops(g);
     if (rc != RH_OK) return rc;
     if (g->read_cap < n) {
         (void)hipFree(g->d_read);
@@ -1026,6 +1165,7 @@ RH_EXPORT int rh_groups_read(rh_groups* g, uint32_t first, uint32_t n, uint8_t c
     rc = rh_table_read(g->dev, first, n, column, g->d_read, s);
     if (rc != RH_OK) return rc;
     RH_HIP(hipMemcpyAsync(out, g->d_read, (size_t)n * 8, hipMemcpyDeviceToHost, s));
+    // the read-back buffer is the table's: keep the lock (a read is a diagnostic, not the hot path)
     RH_HIP(hipStreamSynchronize(s));
     return RH_OK;
 }
@@ -1056,11 +1196,16 @@ RH_EXPORT int rh_lease_batch_async(rh_groups* g, int64_t now_nanos, int64_t time
     if (!g) return rh::fail(RH_E_INVAL, "rh_lease_batch_async: groups == NULL");
     if (timeout_ms < 0) return rh::fail(RH_E_INVAL, "rh_lease_batch_async: timeout_ms < 0");
     DeviceGuard dg(g->ctx->device);
-    std::lock_guard<std::mutex> lk(g->mu);
-    if (g->lpending) RH_HIP(hipEventSynchronize(g->ldone));  // the pinned bitmap is about to be rewritten
-    g->lpending = false;
+    Exclusive ex(g);
+    while (g->lpending) {   // the pinned bitmap is about to be rewritten: wait for it, unlocked
+        const uint64_t was = g->lgen;
+        int rc = wait_unlocked(ex, g->ldone);
+        if (rc != RH_OK) return rc;
+        if (g->lpending && g->lgen == was) g->lpending = false;
+    }
     hipStream_t s = g->ctx->stream;
-    int rc = flush_ops(g);
+    int rc = stage_submit(g);
+    if (rc == RH_OK) rc = flush_ops(g);
     if (rc != RH_OK) return rc;
     const uint64_t words = (g->capacity + 63) / 64;
     RH_HIP(hipMemsetAsync(g->d_lbits, 0, words * 8, s));
@@ -1068,6 +1213,7 @@ RH_EXPORT int rh_lease_batch_async(rh_groups* g, int64_t now_nanos, int64_t time
     if (rc != RH_OK) return rc;
     RH_HIP(hipMemcpyAsync(g->h_lbits, g->d_lbits, words * 8, hipMemcpyDeviceToHost, s));
     RH_HIP(hipEventRecord(g->ldone, s));
+    ++g->lgen;
     g->lpending = true;
     return RH_OK;
 }
@@ -1075,9 +1221,14 @@ RH_EXPORT int rh_lease_batch_async(rh_groups* g, int64_t now_nanos, int64_t time
 RH_EXPORT int rh_lease_batch_wait(rh_groups* g, const uint64_t** out_bits, uint64_t* out_words) {
     if (!g || !out_bits || !out_words) return rh::fail(RH_E_INVAL, "rh_lease_batch_wait: NULL argument");
     DeviceGuard dg(g->ctx->device);
-    std::lock_guard<std::mutex> lk(g->mu);
+    std::unique_lock<std::mutex> lk(g->mu);
     if (!g->lpending) return rh::fail(RH_E_STATE, "rh_lease_batch_wait: no lease batch in flight");
-    RH_HIP(hipEventSynchronize(g->ldone));
+    const uint64_t gen = g->lgen;
+    const hipEvent_t done = g->ldone;
+    lk.unlock();   // no table lock across a device wait
+    RH_HIP(hipEventSynchronize(done));
+    lk.lock();
+    if (!g->lpending || g->lgen != gen) return rh::fail(RH_E_STATE, "rh_lease_batch_wait: superseded while waiting");
     g->lpending = false;
     *out_bits = g->h_lbits;
     *out_words = (g->capacity + 63) / 64;
@@ -1096,8 +1247,6 @@ struct rh_node {
     std::vector<rh_ctx*> ctx;
     std::vector<rh_groups*> tab;
     uint64_t cap = 0;
-    std::mutex push_mu;                        // guards `part` (reused by every push)
-    std::vector<std::vector<rh_delta>> part;   // per-shard partitions of one rh_node_push_deltas
     std::mutex batch_mu;                       // guards `tickets`
     std::vector<uint64_t> tickets;
 };
@@ -1128,7 +1277,6 @@ RH_EXPORT int rh_node_create_devices(const int* devices, int n_shards, uint64_t 
     if (!nd) return rh::fail(RH_E_NOMEM, "rh_node_create_devices: out of host memory");
     nd->cap = capacity_per_shard;
     try {
-        nd->part.resize((size_t)n_shards);
         nd->tickets.resize((size_t)n_shards);
     } catch (...) {
         delete nd;
@@ -1220,21 +1368,24 @@ RH_EXPORT int rh_node_push_deltas(rh_node* nd, const rh_delta* deltas, size_t n)
         if (deltas[i].slot / nd->cap >= S)
             return rh::fail(RH_E_INVAL, "rh_node_push_deltas: delta " + std::to_string(i) + " has a bad slot");
     if (S == 1) return rh_push_deltas(nd->tab[0], deltas, n);  // node slot == table slot
-    std::lock_guard<std::mutex> lk(nd->push_mu);
+    // per-shard partitions in the calling thread's own buffers (producers share nothing here; the
+    // capacity stays between calls: no allocation once warmed up)
+    thread_local std::vector<std::vector<rh_delta>> part;
     try {
-        for (auto& p : nd->part) p.clear();  // keeps the capacity: no allocation once warmed up
+        if (part.size() < S) part.resize(S);
+        for (size_t sh = 0; sh < S; ++sh) part[sh].clear();
         for (size_t i = 0; i < n; ++i) {
             rh_delta d = deltas[i];
             const uint64_t sh = d.slot / nd->cap;
             d.slot = (uint32_t)(d.slot % nd->cap);
-            nd->part[sh].push_back(d);
+            part[sh].push_back(d);
         }
     } catch (...) {
         return rh::fail(RH_E_NOMEM, "rh_node_push_deltas: out of host memory");
     }
     for (size_t sh = 0; sh < S; ++sh) {
-        if (nd->part[sh].empty()) continue;
-        int rc = rh_push_deltas(nd->tab[sh], nd->part[sh].data(), nd->part[sh].size());
+        if (part[sh].empty()) continue;
+        int rc = rh_push_deltas(nd->tab[sh], part[sh].data(), part[sh].size());
         if (rc != RH_OK) return rc;
     }
     return RH_OK;

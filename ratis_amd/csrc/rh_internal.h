@@ -97,10 +97,19 @@ struct TableTier {
     uint32_t rows = 0;          // allocated rows, a multiple of kTileRows
     uint8_t* base = nullptr;    // [rows / 128] tiles of tile::bytes(width)
     uint8_t* sum = nullptr;     // [rows / 128][2] tile summaries (dirty, wdirty)
+    // Delta order keys, laid out like `base` (the key of the int64 cell at tile offset o, row r, sits at
+    // the same offset of `shadow`; the u8 lease-enabled cell's key uses the conf / row-slot bytes,
+    // which no delta targets): (batch generation << 32) | index in the batch of the cell's last SET.
+    uint8_t* shadow = nullptr;
     // element `r` of the column at tile offset `off` (element size sizeof(T))
     template <typename T>
     __host__ __device__ T* at(uint32_t off, uint64_t r) const {
         return reinterpret_cast<T*>(base + (r >> 7) * (uint64_t)tile::bytes(width) + off + (r & 127) * sizeof(T));
+    }
+    // the order key of the delta target at tile offset `off` (int64 column, or tile::kLon)
+    __host__ __device__ unsigned long long* key(uint32_t off, uint64_t r) const {
+        const uint32_t o = off == tile::kLon ? tile::kConf : off;
+        return reinterpret_cast<unsigned long long*>(shadow + (r >> 7) * (uint64_t)tile::bytes(width) + o + (r & 127) * 8);
     }
     __host__ __device__ int64_t* i64(uint32_t off, uint64_t r) const { return at<int64_t>(off, r); }
     __host__ __device__ uint32_t* u32(uint32_t off, uint64_t r) const { return at<uint32_t>(off, r); }
@@ -219,7 +228,13 @@ struct PoolScratch {
 int rh_commit_launch_impl(rh_ctx* ctx, const rh_commit_soa* tiers, int n_tiers, hipStream_t stream);
 // Resident table kernels (table.hip): delta apply (phase 0 = SET deltas, 1 = MAX deltas),
 // control ops, and updateCommit / commitIndexChanged over the dirty rows of every tier.
-int rh_table_apply_deltas(const rh::TableDev& t, const rh_delta* d_deltas, uint64_t n, int phase,
+// Phases of one batch (rh_delta order semantics, ratis_hip.h): kApplyKeys records each SET target's
+// last SET (the highest batch index: its order key in the tier's shadow), kApplySet stores the SET
+// that holds its target's key, kApplyMax applies the MAX deltas that come after their target's last
+// SET (all of them when gen == 0: a batch without SETs).  gen: the batch generation (>= 1) of the
+// keys, 0 for a batch without SETs.
+enum ApplyPhase : int { kApplySet = 0, kApplyMax = 1, kApplyKeys = 2 };
+int rh_table_apply_deltas(const rh::TableDev& t, const rh_delta* d_deltas, uint64_t n, int phase, uint32_t gen,
                           const rh::TableLists& lc, const rh::TableLists& lw, hipStream_t stream);
 // List-mode evaluation of the listed rows of one kind (mode); COMMIT appends the rows whose commit
 // advanced to the watch list `lw` (when it is maintained).  Events as rh_table_commit.

@@ -91,11 +91,16 @@ __device__ __forceinline__ void list_append(const TableLists& l, bool want, int 
 }
 
 // ---- deltas --------------------------------------------------------------------------------------
-// phase 0 applies the batch's SET deltas (plain stores), phase 1 its MAX deltas (atomicMax): the
-// host orders batches so that this equals applying them one by one (ratis_hip.h, rh_delta).  With
-// dirty-row lists (lc / lw .rows non-null) the rows a delta newly marks are appended to them.
+// One batch is applied in call order (its index in the batch) with the semantics of applying the
+// deltas one by one: per target cell, the LAST SET wins and only the MAX deltas after it count.
+// kApplyKeys: every SET raises its cell's key to (gen << 32) | index (64-bit atomicMax: the last SET
+// holds the highest key); kApplySet: the SET holding its cell's key stores its value; kApplyMax: a
+// MAX before its cell's last SET is dropped, the others atomicMax -- stream order puts the store
+// before them.  A batch without SETs (gen == 0) runs kApplyMax alone, unchecked.  Every delta of a
+// phase that applies (SET: kApplySet, MAX: kApplyMax) marks its row dirty -- the UPDATE_COMMIT event
+// of LSI:846-854 -- and with dirty-row lists (lc / lw .rows non-null) appends a row it newly marks.
 __global__ __launch_bounds__(256) void table_apply_kernel(TableDev Targ, const rh_delta* __restrict__ d, uint64_t n,
-                                                          int phase, TableLists lc, TableLists lw) {
+                                                          int phase, uint32_t gen, TableLists lc, TableLists lw) {
     // the tier is picked per thread: index the argument in the kernarg segment (scalar loads), not
     // the by-value copy, which the compiler spilled whole into scratch (984 B per lane, 8x slower)
     const TableDev& T = rh::kernarg_struct<TableDev>();
@@ -104,49 +109,62 @@ __global__ __launch_bounds__(256) void table_apply_kernel(TableDev Targ, const r
     bool ac = false, aw = false;   // this delta newly marked its row (list mode)
     int t = 0;
     uint32_t row = 0;
+    const unsigned long long key = ((unsigned long long)gen << 32) | (unsigned long long)i;
     do {   // one pass; `break` = the delta has no (further) effect
         if (i >= n) break;
         const rh_delta x = d[i];
-        if (x.op != (phase == 0 ? RH_OP_SET : RH_OP_MAX)) break;
+        if (x.op != (phase == kApplyMax ? RH_OP_MAX : RH_OP_SET)) break;
         const TableTier* tt;
         if (!locate(T, x.slot, tt, row)) break;  // stopped slot / out of range: ignored
         t = (int)(T.slot_map[x.slot] >> 28);
-        int64_t* p = nullptr;
+        uint32_t off = 0xFFFFFFFFu;
         bool commit_ev = false, watch_ev = false;
         const uint32_t c = x.column, F = tt->width;
-        if (c == RH_COL_LEASE_ON) {  // AtomicBoolean: SET stores, MAX ORs
-            uint8_t* f = tt->u8(tile::kLon, row);
-            if (phase == 0)
-                *f = x.value != 0;
-            else if (x.value != 0)
-                *f = 1;
-            break;
-        }
-        if (c >= 48 && c < 64) {
-            if (c - 48 < F) p = tt->i64(tile::fts(F, c - 48), row);
+        if (c == RH_COL_LEASE_ON) {
+            off = tile::kLon;
+        } else if (c >= 48 && c < 64) {
+            if (c - 48 < F) off = tile::fts(F, c - 48);
         } else if (c == RH_COL_LEASE) {
-            p = tt->i64(tile::lease(F), row);
+            off = tile::lease(F);
         } else if (c < 16) {
-            if (c < F) p = tt->i64(tile::match(c), row);
+            if (c < F) off = tile::match(c);
             commit_ev = true;
         } else if (c < 32) {
-            if (c - 16 < F) p = tt->i64(tile::fcommit(F, c - 16), row);
+            if (c - 16 < F) off = tile::fcommit(F, c - 16);
             watch_ev = true;
         } else if (c == RH_COL_FLUSH) {
-            p = tt->i64(tile::flush(F), row);
+            off = tile::flush(F);
             commit_ev = true;
         } else if (c == RH_COL_COMMITTED) {
-            p = tt->i64(tile::commit(F), row);
+            off = tile::commit(F);
             commit_ev = watch_ev = true;
         }
-        if (!p) break;
-        if (phase == 0)
-            *p = x.value;
-        else
-            atomicMax(reinterpret_cast<long long*>(p), (long long)x.value);
+        if (off == 0xFFFFFFFFu) break;
+        if (phase == kApplyKeys) {
+            atomicMax(tt->key(off, row), key);
+            break;
+        }
+        const bool last = phase == kApplySet ? *tt->key(off, row) == key
+                                             : (gen == 0 || !(*tt->key(off, row) > key && (*tt->key(off, row) >> 32) == gen));
+        if (last) {
+            if (off == tile::kLon) {  // AtomicBoolean: SET stores, MAX ORs
+                uint8_t* f = tt->u8(tile::kLon, row);
+                if (phase == kApplySet)
+                    *f = x.value != 0;
+                else if (x.value != 0)
+                    *f = 1;
+            } else {
+                int64_t* p = tt->i64(off, row);
+                if (phase == kApplySet)
+                    *p = x.value;
+                else
+                    atomicMax(reinterpret_cast<long long*>(p), (long long)x.value);
+            }
+        }
         if (commit_ev) ac = mark_listed(*tt, row, 0, lc.rows != nullptr);
         if (watch_ev) aw = mark_listed(*tt, row, 1, lw.rows != nullptr);
     } while (false);
+    if (phase == kApplyKeys) return;   // uniform: marks come with the SET phase
     const uint32_t h = blockIdx.x & (rh::kHeads - 1);
     if (lc.rows) list_append(lc, ac, t, row, h);   // kernel arguments: uniform branches
     if (lw.rows) list_append(lw, aw, t, row, h);
@@ -840,11 +858,12 @@ __global__ __launch_bounds__(256) void table_read_kernel(TableDev Targ, uint32_t
 
 }  // namespace
 
-int rh_table_apply_deltas(const rh::TableDev& t, const rh_delta* d_deltas, uint64_t n, int phase,
+int rh_table_apply_deltas(const rh::TableDev& t, const rh_delta* d_deltas, uint64_t n, int phase, uint32_t gen,
                           const rh::TableLists& lc, const rh::TableLists& lw, hipStream_t stream) {
     if (n == 0) return RH_OK;
     const uint64_t blocks = (n + 255) / 256;
-    hipLaunchKernelGGL(table_apply_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream, t, d_deltas, n, phase, lc, lw);
+    hipLaunchKernelGGL(table_apply_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream, t, d_deltas, n, phase, gen, lc,
+                       lw);
     RH_HIP(hipGetLastError());
     return RH_OK;
 }

@@ -34,7 +34,8 @@ Host arrays are numpy; all compute is the HIP kernels behind the calls.  Errors 
 from __future__ import annotations
 
 import ctypes
-from typing import Optional, Sequence, Tuple
+import threading
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 
@@ -402,9 +403,38 @@ class RaftNode:
         return np.unpackbits(bits.view(np.uint8), bitorder="little")[:total].astype(bool)
 
 
+class _DeltaBuffer:
+    """One producer thread's deltas (HipLeaderBookkeeper.DeltaBuffer): appended under its own lock,
+    pushed whole when full or when the pump / a control call flushes every buffer."""
+
+    CAP = 4096
+
+    def __init__(self, node: "RaftNode"):
+        self.node = node
+        self.lock = threading.Lock()
+        self.parts: List[np.ndarray] = []
+        self.n = 0
+
+    def put(self, deltas: np.ndarray) -> None:
+        with self.lock:
+            self.parts.append(deltas)
+            self.n += deltas.size
+            if self.n >= self.CAP:
+                self._flush_locked()
+
+    def flush(self) -> None:
+        with self.lock:
+            self._flush_locked()
+
+    def _flush_locked(self) -> None:
+        if self.parts:
+            self.node.push(np.concatenate(self.parts))
+            self.parts, self.n = [], 0
+
+
 class LeaderPump:
     """Python twin of the Java module's pump (java/ratis-hip/.../HipLeaderBookkeeper.tick): one
-    tick = push the buffered deltas; put every shard's updateCommit, commitIndexChanged() and (with
+    tick = push every producer thread's buffered deltas; put every shard's updateCommit, commitIndexChanged() and (with
     a lease timeout) hasLease pass in flight -- all shards before any wait; then per shard hand the
     advanced commits and watch-ALL levels to the divisions, then commitIndexChanged()'s levels
     (LeaderStateImpl.java:606-622), then the lease bitmap.  ``callbacks[node_slot]`` gets
@@ -414,7 +444,9 @@ class LeaderPump:
     def __init__(self, node: RaftNode, lease_timeout_ms: int = -1):
         self.node = node
         self.callbacks = {}
-        self._pending = []
+        self._buffers: List[_DeltaBuffer] = []   # one per producer thread (thread-local)
+        self._local = threading.local()
+        self._reg = threading.Lock()
         self.lease_timeout_ms = lease_timeout_ms
         self.lease_bits = None
         self.fallbacks = {}   # reason -> divisions that left the table (HipLeaderBookkeeper.getFallbackCount)
@@ -423,13 +455,20 @@ class LeaderPump:
         self.callbacks[int(node_slot)] = callback
 
     def emit(self, deltas: np.ndarray) -> None:
-        self._pending.append(np.ascontiguousarray(deltas, dtype=DELTA_DTYPE))
+        b = getattr(self._local, "buf", None)
+        if b is None:
+            b = self._local.buf = _DeltaBuffer(self.node)
+            with self._reg:
+                self._buffers.append(b)
+        b.put(np.ascontiguousarray(deltas, dtype=DELTA_DTYPE))
 
     def drain(self) -> None:
-        """Pushes the buffered deltas now (HipLeaderBookkeeper.drainDeltas, before a control call)."""
-        if self._pending:
-            self.node.push(np.concatenate(self._pending))
-            self._pending = []
+        """Pushes every producer's buffered deltas now (HipLeaderBookkeeper.flushAllDeltas: each tick,
+        and before a control call)."""
+        with self._reg:
+            bufs = list(self._buffers)
+        for b in bufs:
+            b.flush()
 
     def division(self, node_slot: int, callback) -> "PumpDivision":
         d = PumpDivision(self, int(node_slot), callback)

@@ -1,0 +1,17 @@
+# Round 5: per-dispatch kernel trace of the bench run with every timed leg marked (roctx ranges,
+# scripts/prof_legs.py), and the headline kernel's size sweep under the same trace.
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+O=$R/gpurun_out/${1:-r05a}
+mkdir -p $O && export TMPDIR=/tmp
+cd /tmp
+if [ "${SWEEP:-1}" = 1 ]; then
+timeout -k 10 300 rocprofv3 --kernel-trace --marker-trace -d $O/sweep_prof -o run --output-format csv -- python3 -u $R/scripts/commit_sweep.py ${SWEEP_ARGS:-} > $O/sweep.log 2>&1 || { tail -30 $O/sweep.log; exit 1; }
+cat $O/sweep.log | grep -v "^W" | tail -12
+python3 $R/scripts/prof_legs.py $O/sweep_prof > $O/sweep_legs.md || exit 1
+fi
+if [ "${BENCH:-1}" = 1 ]; then
+timeout -k 10 600 rocprofv3 --kernel-trace --marker-trace --stats -d $O/bench_prof -o run --output-format csv -- python3 -u $R/bench.py ${BENCH_ARGS:-} > $O/bench.log 2>&1 || { tail -30 $O/bench.log; exit 1; }
+python3 $R/scripts/prof_legs.py $O/bench_prof $O/bench.log > $O/bench_legs.md || exit 1
+tail -20 $O/bench_legs.md
+fi
