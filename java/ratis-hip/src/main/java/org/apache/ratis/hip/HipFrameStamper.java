@@ -13,6 +13,11 @@
  * the reference's either way.  minGpuBytes is the crossover measured by bench.py's write_stamp leg
  * (INTEGRATION.md): below it the PCIe round trip costs more than the CPU checksum.
  *
+ * A GPU call that fails never fails the flush: the same frames are stamped by the CPU path, the
+ * failure is counted (getGpuFailures), and after MAX_GPU_FAILURES of them the stamper stays on the
+ * CPU.  The write buffer is page-locked lazily, at the first batch large enough for the GPU, so a
+ * worker whose batches never reach minGpuBytes pins no host memory.
+ *
  * Single-threaded, like BufferedWriteChannel (the log worker's thread).
  */
 package org.apache.ratis.hip;
@@ -30,10 +35,14 @@ public final class HipFrameStamper implements AutoCloseable {
 
   /** Flush batches from this size on go to the GPU (bench.py write_stamp leg: crossover_bytes). */
   public static final int DEFAULT_MIN_GPU_BYTES = 256 << 10;
+  /** GPU failures after which the stamper stays on the CPU path. */
+  static final int MAX_GPU_FAILURES = 3;
 
   private final HipLogReader gpu;
   private final int minGpuBytes;
-  private final ByteBuffer registered;
+  private final ByteBuffer writeBuffer;
+  private boolean registered;       // writeBuffer page-locked (at the first GPU-sized batch)
+  private long gpuFailures;
   private long[] off = new long[1024];
   private int[] len = new int[1024];
   private int n;
@@ -41,15 +50,15 @@ public final class HipFrameStamper implements AutoCloseable {
   private long gpuBatches;
   private long cpuBatches;
 
-  /** writeBuffer: the worker's reused direct write buffer, page-locked here for the stamper's lifetime. */
+  /** writeBuffer: the worker's reused direct write buffer, page-locked (from its first GPU-sized batch
+   *  on) for the stamper's lifetime. */
   public HipFrameStamper(int deviceMask, int minGpuBytes, ByteBuffer writeBuffer) throws IOException {
     if (minGpuBytes < 0) {
       throw new IllegalArgumentException("minGpuBytes < 0: " + minGpuBytes);
     }
     this.gpu = HipLogReader.get(deviceMask);
     this.minGpuBytes = minGpuBytes;
-    gpu.register(writeBuffer);
-    this.registered = writeBuffer;
+    this.writeBuffer = writeBuffer;
   }
 
   /** A frame whose trailer is a placeholder: [pos, pos + length) of the write buffer, length = varint
@@ -73,25 +82,34 @@ public final class HipFrameStamper implements AutoCloseable {
     if (n == 0) {
       return false;
     }
-    final boolean onGpu = bytes >= minGpuBytes && buf.isDirect();
-    try {
-      if (onGpu) {
-        gpu.stampFrames(buf, buf.position(), off, len, n);
-        gpuBatches++;
-      } else {
-        for (int i = 0; i < n; i++) {
-          final int pos = (int) off[i];
-          final int end = pos + len[i] - 4;
-          final ByteBuffer d = buf.duplicate();
-          d.position(pos).limit(end);
-          buf.putInt(end, cpu.crc(d));
+    boolean onGpu = false;
+    if (bytes >= minGpuBytes && buf.isDirect() && gpuFailures < MAX_GPU_FAILURES) {
+      try {
+        if (!registered && buf == writeBuffer) {
+          gpu.register(writeBuffer);
+          registered = true;
         }
-        cpuBatches++;
+        gpu.stampFrames(buf, buf.position(), off, len, n);
+        onGpu = true;
+        gpuBatches++;
+      } catch (IOException | RuntimeException e) {
+        gpuFailures++;   // the CPU path below stamps the same frames: the file gets the reference's bytes
       }
-    } finally {
-      n = 0;
-      bytes = 0;
     }
+    if (!onGpu) {
+      for (int i = 0; i < n; i++) {
+        final int pos = (int) off[i];
+        final int end = pos + len[i] - 4;
+        final ByteBuffer d = buf.duplicate();
+        d.position(pos).limit(end);
+        buf.putInt(end, cpu.crc(d));
+      }
+      cpuBatches++;
+    }
+    // only now is every pending trailer written: a batch whose CPU path threw keeps its frames, and
+    // the next stamp() (the close() flush included) writes them
+    n = 0;
+    bytes = 0;
     return onGpu;
   }
 
@@ -104,8 +122,16 @@ public final class HipFrameStamper implements AutoCloseable {
     return cpuBatches;
   }
 
+  /** GPU calls that failed (their batches were stamped by the CPU path). */
+  public long getGpuFailures() {
+    return gpuFailures;
+  }
+
   @Override
   public void close() throws IOException {
-    gpu.unregister(registered);
+    if (registered) {
+      registered = false;
+      gpu.unregister(writeBuffer);
+    }
   }
 }

@@ -27,8 +27,14 @@ constexpr int kBlock = 256;            // 4 waves
 #define RH_COMMIT_WAVES 8
 #endif
 constexpr int kGroupsPerLane = 2;      // 16-byte loads per column per lane
-#ifndef RH_COMMIT_BITS_DIRECT  // A/B builds: 1 = each wave stores its bit words itself (no LDS staging)
-#define RH_COMMIT_BITS_DIRECT 0
+#ifndef RH_COMMIT_BITS_DIRECT  // 1 = each wave stores its bit words itself (no LDS staging, no barrier)
+#define RH_COMMIT_BITS_DIRECT 1
+#endif
+#ifndef RH_COMMIT_ABL_NOEVAL  // ablation only (wrong results): trivial arithmetic instead of eval_group
+#define RH_COMMIT_ABL_NOEVAL 0
+#endif
+#ifndef RH_COMMIT_NTS  // 1 = non-temporal result stores (A/B: plain stores measured 0.2 us faster per 1M-group launch)
+#define RH_COMMIT_NTS 0
 #endif
 
 struct TierArgs {
@@ -49,9 +55,12 @@ __device__ __forceinline__ uint64_t ix32(const TierArgs& ta, uint64_t r) {
     return ta.tile32 ? (r >> 7) * ta.tile32 + (r & 127u) : r;
 }
 
+// The block -> tier map leads the struct (one scalar load), then the tiers' arguments.
 struct LaunchArgs {
+    uint32_t n_tiers;
+    uint32_t begin[RH_MAX_TIERS];   // = tier[i].block_begin
+    uint32_t pad[3];
     TierArgs tier[RH_MAX_TIERS];
-    int n_tiers;
 };
 
 using rh_bits::spread32;
@@ -151,7 +160,17 @@ __device__ __forceinline__ void compute_store_sub(const TierArgs& ta, uint64_t w
 #pragma unroll
         for (int k = 0; k < F; ++k) vals[k] = st.fv[g][k];
         vals[F] = st.self[g];
+#if RH_COMMIT_ABL_NOEVAL
+        (void)any_trans;
+        valid[g] = (st.w[g] & RH_CONF_ACTIVE) != 0;
+        mn[g] = vals[0];
+#pragma unroll
+        for (int k = 1; k < N; ++k) mn[g] ^= vals[k];   // every loaded column stays live
+        mj[g] = mn[g] + 1;
+        mx[g] = mn[g] + 2;
+#else
         rh_eval::eval_group<F, RANK>(vals, st.w[g], gap, any_trans, valid[g], mn[g], mj[g], mx[g]);
+#endif
         adv[g] = commit_mode && rh_eval::commit_decision(valid[g], mj[g], st.cin[g], st.self[g], st.tstart[g], cout[g]);
         if (!commit_mode) cout[g] = st.cin[g];
     }
@@ -270,7 +289,7 @@ __device__ __forceinline__ int tier_of_block(const LaunchArgs& args, uint32_t b)
     int ti = 0;
 #pragma unroll
     for (int i = 1; i < RH_MAX_TIERS; ++i)
-        if (i < args.n_tiers && b >= args.tier[i].block_begin) ti = i;
+        if (i < (int)args.n_tiers && b >= args.begin[i]) ti = i;
     return ti;
 }
 
@@ -284,7 +303,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RH_COMMI
     const LaunchArgs& args = rh::kernarg_struct<LaunchArgs>();  // scalar loads, no scratch copy
     const int ti = tier_of_block(args, blockIdx.x);
     const TierArgs& ta = args.tier[ti];
-    dispatch_f<1, 6, true, true, true>(ta, (uint64_t)(blockIdx.x - ta.block_begin));
+    dispatch_f<1, 6, true, true, RH_COMMIT_NTS>(ta, (uint64_t)(blockIdx.x - ta.block_begin));
 }
 
 // Tiers with F = 7..14 (8..15 voters): a Batcher network per conf (rank masks of 8+ values do
@@ -322,6 +341,7 @@ void build_args(const rh_commit_soa* tiers, int n_tiers, int flo, int fhi, Launc
         ta.tile64 = t.tile_stride / 8;
         ta.tile32 = t.tile_stride / 4;
         ta.block_begin = (uint32_t)blocks;
+        args.begin[args.n_tiers - 1] = (uint32_t)blocks;
         ta.n_blocks = (uint32_t)((t.n + kTile - 1) / kTile);
         const bool cm = t.mode == RH_MODE_COMMIT;
         ta.vec_ok = aligned16(t.follower_index) && (ta.stride % 2 == 0) && aligned16(t.self_index) &&
@@ -366,7 +386,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RH_COMMI
     if (b < a.commit_blocks) {
         const int ti = tier_of_block(a.commit, b);
         const TierArgs& ta = a.commit.tier[ti];
-        dispatch_f<1, 6, true, true, true>(ta, (uint64_t)(b - ta.block_begin));
+        dispatch_f<1, 6, true, true, RH_COMMIT_NTS>(ta, (uint64_t)(b - ta.block_begin));
     } else {
         rh_lease::lease_block(a.lease, (uint64_t)(b - a.commit_blocks));
     }

@@ -1607,8 +1607,10 @@ int rh_crc_upload_tables(rh_ctx* ctx) {
 // table lookups per 8-byte word, T[k] = the register after a byte and k zero bytes), the 8 KiB of
 // tables built in LDS from the context's four slicing-by-4 tables.  Latency-bound per lane (one
 // dependent table round per 8 bytes), parallel over frames.  Frames must be well formed (the caller
-// checks): [off, off + len) inside the buffer and len >= 4 under STAMP / VERIFY.
-__global__ __launch_bounds__(64) void crc_serial_kernel(const uint8_t* __restrict__ buf, uint8_t* wbuf,
+// checks): [off, off + len) inside the buffer and len >= 4 under STAMP / VERIFY.  Only the CRCs are
+// written (crc_out, required): under STAMP the caller writes the trailers from them (the host copy is
+// the one that goes to the file), so the device image is never written.
+__global__ __launch_bounds__(64) void crc_serial_kernel(const uint8_t* __restrict__ buf,
                                                          const uint64_t* __restrict__ off,
                                                          const uint32_t* __restrict__ len, uint64_t n,
                                                          uint32_t init, uint32_t flags, const uint32_t* __restrict__ slice4,
@@ -1665,21 +1667,14 @@ __global__ __launch_bounds__(64) void crc_serial_kernel(const uint8_t* __restric
         step8((uint32_t)w, (uint32_t)(w >> 32));
     }
     while (p < e) c = (c >> 8) ^ T[0][(c ^ *p++) & 0xffu];
-    const uint32_t v = ~c;   // getValue()
-    if (crc_out) crc_out[f] = v;
-    if (flags & RH_CRC_STAMP) {
-        uint8_t* t = wbuf + off[f] + span;
-        t[0] = (uint8_t)(v >> 24);
-        t[1] = (uint8_t)(v >> 16);
-        t[2] = (uint8_t)(v >> 8);
-        t[3] = (uint8_t)v;
-    }
+    crc_out[f] = ~c;   // getValue()
 }
 
 int rh_crc_serial_launch(rh_ctx* ctx, const rh_frames* f, uint32_t flags, hipStream_t stream) {
     if (f->n == 0) return RH_OK;
+    if (!f->crc_out) return rh::fail(RH_E_INVAL, "crc serial launch: crc_out required");
     // one wave per workgroup: the frames spread over as many CUs as there are waves of them
-    hipLaunchKernelGGL(crc_serial_kernel, dim3((uint32_t)((f->n + 63) / 64)), dim3(64), 0, stream, f->buf, f->buf,
+    hipLaunchKernelGGL(crc_serial_kernel, dim3((uint32_t)((f->n + 63) / 64)), dim3(64), 0, stream, f->buf,
                        f->frame_off, f->frame_len, f->n, f->init_state, flags, ctx->d_slice, f->crc_out);
     RH_HIP(hipGetLastError());
     return RH_OK;

@@ -248,10 +248,14 @@ def test_bulk_load_streams_batches_with_two_images():
     segments one by one from a HipLogReader.Pipeline (batch k + 1 read and verified while batch k
     loads), which holds exactly two image buffers and hands a batch's back after its last segment;
     batches are planned under HIP_BATCH_BYTES and MAX_FRAMES_PER_BATCH frame slots (no silent
-    clamp of the frame table)."""
+    clamp of the frame table).  A failure to create the pipeline or of one of its batches falls back
+    to the reference's reader for the remaining segments."""
     added = _added_lines()
     assert "List<HipLogReader.Segment>" not in added
-    assert "try (HipLogReader.Pipeline verified =" in added and "verified.next()" in added
+    assert "HipLogReader.Pipeline verified = null;" in added and "v = verified.next();" in added
+    # a GPU that fails never fails the load: the rest is read by the reference's reader (ADVICE r04)
+    assert "verified = hipVerify(paths);" in added and "closeQuietly(verified);" in added
+    assert added.count("} catch (IOException | RuntimeException e) {") >= 2
     plan = _method_body(added, "private HipLogReader.Pipeline hipVerify(")
     assert "HipLogReader.MAX_FRAMES_PER_BATCH" in plan and "new HipLogReader.Plan(" in plan
     assert "reader.pipeline(plans, maxOp)" in plan
@@ -297,6 +301,12 @@ def test_writer_seam_stamps_flush_batches():
     st = _method_body(stamper, "public boolean stamp(ByteBuffer buf, FrameChecksum cpu)")
     assert "bytes >= minGpuBytes" in st and "gpu.stampFrames(buf, buf.position(), off, len, n)" in st
     assert "cpu.crc(d)" in st
+    # a failing GPU call falls back to the CPU path for the same frames (never fails the flush);
+    # the pending frames are dropped only after one path wrote every trailer
+    g, c = st.index("gpu.stampFrames("), st.index("cpu.crc(d)")
+    assert "catch (IOException | RuntimeException e)" in st[g:c] and "gpuFailures++" in st[g:c]
+    assert "finally" not in st and st.rindex("n = 0;") > c
+    assert "gpu.register(writeBuffer)" in st   # page-locked lazily, at the first GPU-sized batch
     jni = open(JNI_C).read()
     assert "rh_crc32c_stamp_host(C(ctx)" in jni and "rh_host_register(C(ctx)" in jni
 
