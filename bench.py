@@ -429,20 +429,23 @@ def reply_mix_leg(host, threads: int = 16, steps: int = 8, active_frac: float = 
     tk = tab.commit_async(watch_all=True)
     tab.watch_async()
     tab.commit_wait_counts(tk)
-    tab.watch_wait()
+    tab.watch_wait_count()
     LEGS.push("reply_mix", steps)
     t0 = time.perf_counter()
     inflight = None
     advanced = 0
+    push_s = 0.0
     for s in range(1, steps + 1):
+        p0 = time.perf_counter()
         push(*per_step[s][:2])
+        push_s += time.perf_counter() - p0
         if inflight is not None:   # the previous step's evaluations, in flight while this step pushed
             advanced += tab.commit_wait_counts(inflight)[0]
-            tab.watch_wait()
+            tab.watch_wait_count()
         inflight = tab.commit_async(watch_all=True)
         tab.watch_async()
     advanced += tab.commit_wait_counts(inflight)[0]
-    tab.watch_wait()
+    tab.watch_wait_count()
     dt = (time.perf_counter() - t0) / steps
     LEGS.pop()
     ok = (np.array_equal(tab.read(_lib.RH_COL_FLUSH), flush)
@@ -467,7 +470,8 @@ def reply_mix_leg(host, threads: int = 16, steps: int = 8, active_frac: float = 
     replies = int(np.mean([p[2] for p in per_step[1:]]))
     prod.close()
     node.close()
-    return {"ms_per_step": round(dt * 1e3, 3), "replies_per_s_incl_pcie": round(replies / dt, 1),
+    return {"ms_per_step": round(dt * 1e3, 3), "ms_producers_per_step": round(push_s / steps * 1e3, 3),
+            "replies_per_s_incl_pcie": round(replies / dt, 1),
             "deltas_per_s_incl_pcie": round(n_deltas / dt, 1), "replies_per_step": replies,
             "deltas_per_step": n_deltas, "delta_bytes_h2d_per_step": n_deltas * 16,
             "h2d_bound_ms": round(n_deltas * 16 / 50e9 * 1e3, 3), "producer_threads": T,

@@ -253,8 +253,8 @@ int rh_groups_load(rh_groups* g, uint32_t first, uint32_t n, uint32_t n_host_fol
  * concurrent calls copy into ranges of the open slot reserved with one atomic each, never waiting
  * for an evaluation, a _wait call or another producer's copy; a call's deltas keep their order and
  * calls that do not overlap in time keep theirs.  Staged deltas reach the device when the slot is
- * full or before the next evaluation, read, zero-copy acquire, or control call on a slot they
- * target -- always before anything issued after the push returned. */
+ * full or before the next evaluation, read, zero-copy acquire or control call -- always before
+ * anything issued after the push returned. */
 int rh_push_deltas(rh_groups* g, const rh_delta* deltas, size_t n);
 /* Zero-copy producer path over the same staging ring (two pinned slots of RH_DELTA_SLOT deltas):
  * rh_deltas_acquire hands out the next slot to fill in place (waiting until its previous H2D has

@@ -105,8 +105,6 @@ struct rh_groups {
     int open = -1;                            // host slot open for rh_push_deltas (-1: none)
     std::atomic<uint64_t> fill{0};            // deltas reserved in the open slot
     std::atomic<bool> staged_set{false};      // some staged delta is a SET
-    uint32_t stage_gen = 1;                   // generation of the open slot's contents
-    std::vector<uint32_t> slot_staged;        // slot -> stage_gen of its last staged delta (atomic stores)
     uint32_t apply_gen = 0;                   // order-key generation of the last batch with SETs
     hipStream_t copy_stream = nullptr;       // H2D of delta slots and control ops
     hipStream_t d2h_stream = nullptr;        // the result lists' way to the host: RH_EVENTS_DEVICE's D2H in
@@ -496,15 +494,8 @@ int stage_submit(rh_groups* g) {
     g->open = -1;
     g->fill.store(0, std::memory_order_relaxed);
     const bool has_set = g->staged_set.exchange(false, std::memory_order_relaxed);
-    ++g->stage_gen;
     if (n == 0) return RH_OK;
     return ring_submit(g, i, n, has_set);
-}
-
-// Submits the staged deltas if any targets `slot` (a control op on it must follow them).
-int stage_submit_for(rh_groups* g, uint32_t slot) {
-    if (g->open < 0 || g->slot_staged[slot] != g->stage_gen) return RH_OK;
-    return stage_submit(g);
 }
 
 // Opens the next host slot for rh_push_deltas (waiting until its previous H2D has completed).
@@ -570,7 +561,6 @@ RH_EXPORT int rh_groups_create(rh_ctx* ctx, uint64_t capacity, int64_t gap_thres
         g->slot_map.assign(capacity, kNoRow);
         g->slot_conf.assign(capacity, 0);
         g->op_stamp.assign(capacity, 0);
-        g->slot_staged.assign(capacity, 0);
     } catch (...) {
         rc = rh::fail(RH_E_NOMEM, "rh_groups_create: out of host memory");
     }
@@ -697,7 +687,7 @@ RH_EXPORT int rh_group_start(rh_groups* g, uint32_t slot, uint32_t conf, int64_t
     if (rc != RH_OK) return rc;
     DeviceGuard dg(g->ctx->device);
     Exclusive ex(g);
-    rc = stage_submit_for(g, slot);   // deltas staged for the slot come before its re-start
+    rc = stage_submit(g);   // the deltas pushed before this call apply before it
     if (rc != RH_OK) return rc;
     rc = do_stop(g, slot);  // a re-armed slot drops its old row (and every FollowerInfo with it)
     if (rc != RH_OK) return rc;
@@ -733,7 +723,7 @@ RH_EXPORT int rh_group_reconf(rh_groups* g, uint32_t slot, uint32_t conf, const 
     Exclusive ex(g);
     const uint32_t m = g->slot_map[slot];
     if (m == kNoRow) return rh::fail(RH_E_STATE, "rh_group_reconf: slot not started");
-    rc = stage_submit_for(g, slot);   // deltas staged for the slot apply under its old conf
+    rc = stage_submit(g);   // the deltas pushed before this call apply under the old conf
     if (rc != RH_OK) return rc;
     const int t_old = (int)(m >> 28);
     const int t_new = rh::tier_of_width(needed_width(conf));
@@ -765,7 +755,7 @@ RH_EXPORT int rh_group_stop(rh_groups* g, uint32_t slot) {
     if (slot >= g->capacity) return rh::fail(RH_E_INVAL, "rh_group_stop: slot out of range");
     DeviceGuard dg(g->ctx->device);
     Exclusive ex(g);
-    int rc = stage_submit_for(g, slot);
+    int rc = stage_submit(g);
     return rc != RH_OK ? rc : do_stop(g, slot);
 }
 
@@ -898,10 +888,12 @@ RH_EXPORT int rh_groups_load(rh_groups* g, uint32_t first, uint32_t n, uint32_t 
 // Multi-producer: each call validates its deltas and copies them into the open pinned slot at a range
 // it reserved with one CAS, holding the staging lock SHARED -- producers on other threads copy at the
 // same time, and no producer waits for an evaluation, a watch or lease wait, or another producer's
-// copy.  The slot goes to the device (H2D + apply) when it is full or when an evaluation, a read, a
-// control op on a staged slot or the zero-copy path needs the deltas before it; the device applies a
-// batch in slot order with one-by-one semantics (rh_internal.h, ApplyPhase), so a call's deltas
-// keep their array order and calls that do not overlap in time keep theirs.
+// copy.  Nothing per delta is written outside the caller's reserved range (a per-slot stamp array
+// written by every producer thrashed its cache lines between cores: 10 ms per 4M deltas).  The slot
+// goes to the device (H2D + apply) when it is full or when an evaluation, a read, a control op or the
+// zero-copy path needs the deltas before it; the device applies a batch in slot order with
+// one-by-one semantics (rh_internal.h, ApplyPhase), so a call's deltas keep their array order and
+// calls that do not overlap in time keep theirs.
 RH_EXPORT int rh_push_deltas(rh_groups* g, const rh_delta* deltas, size_t n) {
     if (!g) return rh::fail(RH_E_INVAL, "rh_push_deltas: groups == NULL");
     if (n == 0) return RH_OK;
@@ -939,8 +931,6 @@ RH_EXPORT int rh_push_deltas(rh_groups* g, const rh_delta* deltas, size_t n) {
                 if (take) {
                     if (any_set) g->staged_set.store(true, std::memory_order_relaxed);
                     std::memcpy(g->h_ring[g->open] + r, deltas + done, take * sizeof(rh_delta));
-                    const uint32_t sg = g->stage_gen;
-                    for (size_t i = done; i < done + take; ++i) __atomic_store_n(&g->slot_staged[deltas[i].slot], sg, __ATOMIC_RELAXED);
                     done += take;
                     continue;
                 }

@@ -273,6 +273,14 @@ class RaftGroupTable:
         ev = _view(ptr.value or 0, n.value, WATCH_EVENT_DTYPE).copy()
         return ev[np.argsort(ev["slot"], kind="stable")]
 
+    def watch_wait_count(self) -> int:
+        """Like :meth:`watch_wait` but returns only the number of changed levels: the events stay in
+        the library's pinned list (the bench's pipelined loop)."""
+        ptr = ctypes.c_void_p()
+        n = ctypes.c_uint64()
+        check(self._lib.rh_watch_levels_wait(self.handle, ctypes.byref(ptr), ctypes.byref(n)))
+        return int(n.value)
+
     # -- leader lease (LeaderStateImpl.hasLease, LeaderLease) ---------------------------------
     def lease_start(self, slot: int, now_nanos: int, enabled: bool = True) -> None:
         """A new LeaderLease for ``slot`` (lease = now, enabled) with every follower stamped now."""
