@@ -26,6 +26,9 @@ def main():
     ap.add_argument("--sizes", default="2048,65536,250000,500000,1000000,2000000,4000000")
     ap.add_argument("--launches", type=int, default=200)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--no-bits", action="store_true", help="ablation: no valid / advanced bit columns")
+    ap.add_argument("--no-min", action="store_true", help="ablation: no min_out column")
+    ap.add_argument("--tiers", choices=["both", "stable", "joint"], default="both", help="ablation: one tier only")
     a = ap.parse_args()
     import torch
 
@@ -36,13 +39,19 @@ def main():
     pts = []
     for n in [int(x) for x in a.sizes.split(",")]:
         host = workload.commit_snapshot(n, joint_frac=0.10, peers=5, seed=workload.SEED + 1)
+        if a.tiers != "both":
+            host = [host[0 if a.tiers == "stable" else 1]]
         alg = sum(h.algorithmic_bytes() for h in host)
         R = max(8, math.ceil(615e6 / alg))
         batches = []
         for r in range(R):
             d = r << 44
-            batches.append([engine.TiledCommitTier.from_arrays(h.follower + d, h.flush + d, h.conf, h.commit + d,
-                                                               h.term_start + d) for h in host])
+            tiers = [engine.TiledCommitTier.from_arrays(h.follower + d, h.flush + d, h.conf, h.commit + d,
+                                                        h.term_start + d, bits=not a.no_bits) for h in host]
+            if a.no_min:
+                for t in tiers:
+                    t.min_out = False
+            batches.append(tiers)
         launches = [engine.prepare_commit(b) for b in batches]
         for i in range(2 * R):
             launches[i % R](ctx, stream)
