@@ -60,6 +60,8 @@ struct EvSet {
     rh_index_event* d_wall = nullptr;
     rh_index_event* hbm_adv = nullptr;   // the lists in HBM (RH_EVENTS_DEVICE, RH_EVENTS_AUTO's tile evaluations)
     rh_index_event* hbm_wall = nullptr;
+    uint32_t* bdesc = nullptr;           // REGION mode: the evaluation's per-workgroup counts
+    uint32_t nblocks = 0;                // REGION mode: its workgroups (0: the lists are contiguous)
     uint64_t* h_cnt = nullptr;       // host-mapped [2]: list lengths, written by the gather kernel
     uint64_t* d_cnt = nullptr;
     hipEvent_t done = nullptr;
@@ -67,6 +69,11 @@ struct EvSet {
     bool pending = false;
     bool hbm = false;   // this ticket's lists are in hbm_adv / hbm_wall (copied out by _wait)
 };
+
+// HBM list capacity: the table's capacity plus room for the REGION mode's per-workgroup regions
+// (every tier's last workgroup may be partial and the tiers round their rows up to 128).
+uint64_t hbm_records(uint64_t capacity) { return capacity + (uint64_t)(rh::kTableTiers + 1) * rh::kTableRecs; }
+uint64_t region_blocks(uint64_t capacity) { return hbm_records(capacity) / rh::kTableRecs + rh::kTableTiers + 1; }
 
 }  // namespace
 
@@ -119,6 +126,8 @@ struct rh_groups {
     rh_watch_event* watch = nullptr;          // host-mapped pinned [cap]: rh_watch_levels' list
     rh_watch_event* d_watch = nullptr;
     rh_watch_event* hbm_watch = nullptr;      // in HBM (as hbm_adv)
+    uint32_t* wbdesc = nullptr;               // REGION mode (as EvSet::bdesc)
+    uint32_t wnblocks = 0;
     uint64_t* h_wcnt = nullptr;               // host-mapped [2]: its length (the evaluation's last workgroup)
     uint64_t* d_wcnt = nullptr;
     hipEvent_t wdone = nullptr;
@@ -192,11 +201,13 @@ void free_groups(rh_groups* g) {
         if (g->ev[i].done) (void)hipEventDestroy(g->ev[i].done);
         (void)hipFree(g->ev[i].hbm_adv);
         (void)hipFree(g->ev[i].hbm_wall);
+        (void)hipFree(g->ev[i].bdesc);
     }
     (void)hipFree(g->d_lrows[0]);
     (void)hipFree(g->d_lrows[1]);
     (void)hipFree(g->d_lheads);
     (void)hipFree(g->hbm_watch);
+    (void)hipFree(g->wbdesc);
     (void)hipFree(g->d_evw);
     if (g->watch) (void)hipHostFree(g->watch);
     if (g->h_wcnt) (void)hipHostFree(g->h_wcnt);
@@ -363,14 +374,17 @@ struct EvTargets {
 };
 
 // Enqueues one evaluation (mode) of the dirty rows, its events written into the lists adv / wall
-// or watch of `t` (each `capacity` records; their lengths to counts_out, host-mapped).  The sink
-// picks the set: HOST_MAPPED [0], DEVICE [1], AUTO [1] for a tile evaluation (up to every row's
-// records: written at HBM speed, copied by DMA in _wait) and [0] for a list evaluation (few
-// records: written across PCIe by the kernel, no copy).  *hbm: whether [1] was used.
+// or watch of `t` (their lengths to counts_out, host-mapped).  The sink picks the set: HOST_MAPPED
+// [0], DEVICE [1], AUTO [1] for a tile evaluation (up to every row's records: written at HBM speed,
+// gathered into the pinned lists afterwards) and [0] for a list evaluation (few records: written
+// across PCIe by the kernel, no copy).  *hbm: whether [1] was used.  A tile evaluation into [1]
+// runs in REGION mode (rh_internal.h, TableEvents): per-workgroup regions and counts in `bdesc`, no
+// counter atomic, the lengths published by rh_table_gather; *nblocks = its workgroups (else 0).
 int evaluate(rh_groups* g, int mode, bool wall_on, const EvTargets& t, uint64_t* counts_out, uint64_t* h_counts,
-             bool* hbm) {
+             bool* hbm, uint32_t* bdesc, uint32_t* nblocks) {
     hipStream_t s = g->ctx->stream;
     *hbm = false;
+    *nblocks = 0;
     int rc = flush_ops(g);
     if (rc != RH_OK) return rc;
     const uint32_t blocks = rh::table_commit_blocks(g->dev);
@@ -410,6 +424,12 @@ int evaluate(rh_groups* g, int mode, bool wall_on, const EvTargets& t, uint64_t*
             const uint64_t hw = ((uint64_t)g->tiers[t].hw + rh::kTileRows - 1) / rh::kTileRows * rh::kTileRows;
             ed.tier[t].rows = (uint32_t)std::min<uint64_t>(ed.tier[t].rows, hw);
             rows += ed.tier[t].rows;
+        }
+        const uint32_t nb = rh::table_commit_blocks(ed);
+        if (k == 1 && nb <= region_blocks(g->capacity) && (uint64_t)nb * rh::kTableRecs <= hbm_records(g->capacity)) {
+            ev.bdesc = bdesc;
+            ev.cap = hbm_records(g->capacity);
+            *nblocks = nb;
         }
         // a quarter of the rows or more possibly dirty: the loads go out with the flag loads
         rc = rh_table_commit(ed, mode, ev, g->marks[m] * 4 >= rows, s, t0, t1);
@@ -587,14 +607,16 @@ RH_EXPORT int rh_groups_create(rh_ctx* ctx, uint64_t capacity, int64_t gap_thres
     for (int i = 0; i < kEvSets && rc == RH_OK; ++i) {
         if (rc == RH_OK) rc = halloc_mapped(&g->ev[i].adv, &g->ev[i].d_adv, capacity);
         if (rc == RH_OK) rc = halloc_mapped(&g->ev[i].wall, &g->ev[i].d_wall, capacity);
-        if (rc == RH_OK) rc = dalloc(&g->ev[i].hbm_adv, capacity);
-        if (rc == RH_OK) rc = dalloc(&g->ev[i].hbm_wall, capacity);
+        if (rc == RH_OK) rc = dalloc(&g->ev[i].hbm_adv, hbm_records(capacity));
+        if (rc == RH_OK) rc = dalloc(&g->ev[i].hbm_wall, hbm_records(capacity));
+        if (rc == RH_OK) rc = dalloc(&g->ev[i].bdesc, rh::kTableDesc * region_blocks(capacity));
         if (rc == RH_OK) rc = halloc_mapped(&g->ev[i].h_cnt, &g->ev[i].d_cnt, 2);
         if (rc == RH_OK && hipEventCreateWithFlags(&g->ev[i].done, hipEventDisableTiming) != hipSuccess)
             rc = rh::fail(RH_E_DEVICE, "hipEventCreate(commit batch)");
     }
     if (rc == RH_OK) rc = halloc_mapped(&g->watch, &g->d_watch, capacity);
-    if (rc == RH_OK) rc = dalloc(&g->hbm_watch, capacity);
+    if (rc == RH_OK) rc = dalloc(&g->hbm_watch, hbm_records(capacity));
+    if (rc == RH_OK) rc = dalloc(&g->wbdesc, rh::kTableDesc * region_blocks(capacity));
     if (rc == RH_OK) rc = halloc_mapped(&g->h_wcnt, &g->d_wcnt, 2);
     if (rc == RH_OK && hipEventCreateWithFlags(&g->wdone, hipEventDisableTiming) != hipSuccess)
         rc = rh::fail(RH_E_DEVICE, "hipEventCreate(watch levels)");
@@ -1000,13 +1022,15 @@ RH_EXPORT int rh_commit_batch_async(rh_groups* g, uint32_t flags, uint64_t* tick
     t.adv[0] = e.d_adv, t.adv[1] = e.hbm_adv;
     t.wall[0] = e.d_wall, t.wall[1] = e.hbm_wall;
     bool hbm = false;
-    rc = evaluate(g, RH_MODE_COMMIT, wall_on, t, e.d_cnt, e.h_cnt, &hbm);
+    rc = evaluate(g, RH_MODE_COMMIT, wall_on, t, e.d_cnt, e.h_cnt, &hbm, e.bdesc, &e.nblocks);
     if (rc != RH_OK) return rc;
-    if (hbm && g->event_sink == RH_EVENTS_AUTO) {   // drained into the pinned lists on the side stream
+    if (hbm && g->event_sink == RH_EVENTS_AUTO) {   // packed into the pinned lists on the side stream
         RH_HIP(hipEventRecord(g->evaluated, g->ctx->stream));
         RH_HIP(hipStreamWaitEvent(g->d2h_stream, g->evaluated, 0));
-        rc = rh_table_drain(e.d_cnt, e.hbm_adv, e.d_adv, wall_on ? e.hbm_wall : nullptr, e.d_wall, 16, g->capacity,
-                            g->d2h_stream);
+        rc = e.nblocks ? rh_table_gather(e.bdesc, e.nblocks, e.hbm_adv, e.d_adv, wall_on ? e.hbm_wall : nullptr,
+                                         e.d_wall, 16, e.d_cnt, g->d2h_stream)
+                       : rh_table_drain(e.d_cnt, e.hbm_adv, e.d_adv, wall_on ? e.hbm_wall : nullptr, e.d_wall, 16,
+                                        g->capacity, g->d2h_stream);
         if (rc != RH_OK) return rc;
         RH_HIP(hipEventRecord(e.done, g->d2h_stream));
         hbm = false;   // nothing left for _wait to copy
@@ -1034,19 +1058,26 @@ RH_EXPORT int rh_commit_batch_wait(rh_groups* g, uint64_t ticket, rh_commit_out*
     RH_HIP(hipEventSynchronize(done));
     std::unique_lock<std::mutex> lk(g->mu);
     if (e->ticket != ticket) return rh::fail(RH_E_STATE, "rh_commit_batch_wait: ticket superseded while waiting");
-    const uint64_t na = std::min<uint64_t>(e->h_cnt[0], g->capacity);
-    const uint64_t nw = std::min<uint64_t>(e->h_cnt[1], g->capacity);
-    if (e->hbm) {  // lists in HBM (DEVICE sink): the counted prefixes to the pinned result buffers
+    uint64_t na = std::min<uint64_t>(e->h_cnt[0], g->capacity);
+    uint64_t nw = std::min<uint64_t>(e->h_cnt[1], g->capacity);
+    if (e->hbm) {  // lists in HBM (DEVICE sink): into the pinned result buffers
         e->hbm = false;
         hipStream_t s = g->d2h_stream;
-        if (na) RH_HIP(hipMemcpyAsync(e->adv, e->hbm_adv, na * sizeof(rh_index_event), hipMemcpyDeviceToHost, s));
-        if (nw) RH_HIP(hipMemcpyAsync(e->wall, e->hbm_wall, nw * sizeof(rh_index_event), hipMemcpyDeviceToHost, s));
+        if (e->nblocks) {   // REGION mode: packed by the gather, which also publishes the lengths
+            int rc = rh_table_gather(e->bdesc, e->nblocks, e->hbm_adv, e->d_adv, e->hbm_wall, e->d_wall, 16, e->d_cnt, s);
+            if (rc != RH_OK) return rc;
+        } else {            // contiguous (a list evaluation): the counted prefixes
+            if (na) RH_HIP(hipMemcpyAsync(e->adv, e->hbm_adv, na * sizeof(rh_index_event), hipMemcpyDeviceToHost, s));
+            if (nw) RH_HIP(hipMemcpyAsync(e->wall, e->hbm_wall, nw * sizeof(rh_index_event), hipMemcpyDeviceToHost, s));
+        }
         RH_HIP(hipEventRecord(e->done, s));
         done = e->done;
         lk.unlock();   // the set stays this ticket's (pending) while the copy runs
         RH_HIP(hipEventSynchronize(done));
         lk.lock();
         if (e->ticket != ticket) return rh::fail(RH_E_STATE, "rh_commit_batch_wait: ticket superseded while waiting");
+        na = std::min<uint64_t>(e->h_cnt[0], g->capacity);
+        nw = std::min<uint64_t>(e->h_cnt[1], g->capacity);
     }
     e->pending = false;
     out->advanced = e->adv;
@@ -1078,12 +1109,15 @@ RH_EXPORT int rh_watch_levels_async(rh_groups* g) {
     EvTargets t;
     t.watch[0] = g->d_watch, t.watch[1] = g->hbm_watch;
     bool hbm = false;
-    rc = evaluate(g, RH_MODE_WATCH, false, t, g->d_wcnt, g->h_wcnt, &hbm);
+    rc = evaluate(g, RH_MODE_WATCH, false, t, g->d_wcnt, g->h_wcnt, &hbm, g->wbdesc, &g->wnblocks);
     if (rc != RH_OK) return rc;
-    if (hbm && g->event_sink == RH_EVENTS_AUTO) {   // drained into the pinned list on the side stream
+    if (hbm && g->event_sink == RH_EVENTS_AUTO) {   // packed into the pinned list on the side stream
         RH_HIP(hipEventRecord(g->evaluated, g->ctx->stream));
         RH_HIP(hipStreamWaitEvent(g->d2h_stream, g->evaluated, 0));
-        rc = rh_table_drain(g->d_wcnt, g->hbm_watch, g->d_watch, nullptr, nullptr, 32, g->capacity, g->d2h_stream);
+        rc = g->wnblocks ? rh_table_gather(g->wbdesc, g->wnblocks, g->hbm_watch, g->d_watch, nullptr, nullptr, 32,
+                                           g->d_wcnt, g->d2h_stream)
+                         : rh_table_drain(g->d_wcnt, g->hbm_watch, g->d_watch, nullptr, nullptr, 32, g->capacity,
+                                          g->d2h_stream);
         if (rc != RH_OK) return rc;
         RH_HIP(hipEventRecord(g->wdone, g->d2h_stream));
         hbm = false;
@@ -1107,16 +1141,23 @@ RH_EXPORT int rh_watch_levels_wait(rh_groups* g, const rh_watch_event** out_even
     RH_HIP(hipEventSynchronize(done));
     lk.lock();
     if (!g->wpending || g->wgen != gen) return rh::fail(RH_E_STATE, "rh_watch_levels_wait: superseded while waiting");
-    const uint64_t n = std::min<uint64_t>(g->h_wcnt[0], g->capacity);
-    if (g->whbm && n) {   // DEVICE sink: the counted prefix to the pinned list
+    uint64_t n = std::min<uint64_t>(g->h_wcnt[0], g->capacity);
+    if (g->whbm && (n || g->wnblocks)) {   // DEVICE sink: into the pinned list
         g->whbm = false;
-        RH_HIP(hipMemcpyAsync(g->watch, g->hbm_watch, n * sizeof(rh_watch_event), hipMemcpyDeviceToHost, g->d2h_stream));
+        if (g->wnblocks) {   // REGION mode: packed by the gather, which also publishes the length
+            int rc = rh_table_gather(g->wbdesc, g->wnblocks, g->hbm_watch, g->d_watch, nullptr, nullptr, 32, g->d_wcnt,
+                                     g->d2h_stream);
+            if (rc != RH_OK) return rc;
+        } else {
+            RH_HIP(hipMemcpyAsync(g->watch, g->hbm_watch, n * sizeof(rh_watch_event), hipMemcpyDeviceToHost, g->d2h_stream));
+        }
         RH_HIP(hipEventRecord(g->wdone, g->d2h_stream));
         done = g->wdone;
         lk.unlock();
         RH_HIP(hipEventSynchronize(done));
         lk.lock();
         if (!g->wpending || g->wgen != gen) return rh::fail(RH_E_STATE, "rh_watch_levels_wait: superseded while waiting");
+        n = std::min<uint64_t>(g->h_wcnt[0], g->capacity);
     }
     g->wpending = false;
     *out_events = g->watch;

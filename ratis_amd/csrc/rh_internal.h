@@ -168,7 +168,23 @@ struct TableEvents {
     int packed = 0;                    // tile kernels: the done count rides in `cnt` above the counts
     uint32_t done_target = 0;          // tile kernels: workgroups done that end the evaluation (0: not this launch)
     unsigned long long* lheads_next = nullptr;  // the other list-head set of the evaluated kind: cleared
+    // REGION mode (tile kernels writing HBM lists): no counter atomic, no LDS staging.  Workgroup gb
+    // (block_base + its block index: the evaluation's launches number their workgroups on) owns
+    // records [gb * kTableRecs, ...) of each list, its wave w the 128 from + 128 w, written there
+    // straight from registers; the workgroup stores its counts at bdesc[gb * kTableDesc]: the two
+    // totals, then each wave's two counts.  rh_table_gather then packs the regions into the result
+    // lists and publishes the lengths.  (One returning atomic per workgroup on one word, at every
+    // workgroup's end, cost the 1M-row evaluation 4.5 us.)
+    uint32_t* bdesc = nullptr;
+    uint32_t block_base = 0;
 };
+// Tile-kernel workgroup: RH_TABLE_BLOCK_WAVES waves, one 128-row tile each.  REGION mode: records
+// per workgroup region (its rows) and u32 counts per workgroup descriptor (2 totals + 2 per wave).
+#ifndef RH_TABLE_BLOCK_WAVES   // A/B builds (both table.hip and groups.cpp see it)
+#define RH_TABLE_BLOCK_WAVES 2
+#endif
+constexpr uint32_t kTableRecs = RH_TABLE_BLOCK_WAVES * 128;
+constexpr uint32_t kTableDesc = 2 + 2 * RH_TABLE_BLOCK_WAVES;
 // DIRTY-ROW LISTS (list mode).  While the host knows that few rows can be dirty (the deltas and
 // control ops since the last evaluation of a kind bound the rows they can mark), every 0 -> 1
 // transition of a row's dirty / wdirty flag (found with a 32-bit atomicOr on the flag's word) also
@@ -249,6 +265,11 @@ int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev, 
 // host mapping): list a (records of rec_bytes0 = 16 or 32 B, length counts[0]) and, if b is not
 // null, list b (16 B records, length counts[1]); counts = the host-mapped lengths the evaluation
 // published.  Enqueued on `stream` (ordered after the evaluation by the caller).
+// REGION mode: packs the per-workgroup regions of the HBM lists a (records of rec_bytes0 = 16 or 32 B)
+// and b (16 B, may be null) of an evaluation of n_blocks workgroups into the result lists a_out /
+// b_out (device pointers of the pinned lists) and writes the two lengths to counts_out (host-mapped).
+int rh_table_gather(const uint32_t* bdesc, uint32_t n_blocks, const void* a, void* a_out, const void* b, void* b_out,
+                    uint32_t rec_bytes0, uint64_t* counts_out, hipStream_t stream);
 int rh_table_drain(const uint64_t* counts, const void* a, void* a_out, const void* b, void* b_out, uint32_t rec_bytes0,
                    uint64_t cap, hipStream_t stream);
 // Initialises tiles [first_tile, n_tiles) of a tier as free rows (conf 0, row_slot kNoRow, clean).

@@ -260,18 +260,21 @@ __global__ __launch_bounds__(128) void table_init_tiles_kernel(TableTier tt, uin
 
 // ---- updateCommit / commitIndexChanged over the dirty rows ---------------------------------------
 // One workgroup = kTWaves waves, one 128-row tile per wave.  Every wave evaluates its rows' results
-// in registers, the block gathers its events in LDS in wave order, takes ONE range of each result
-// list with ONE device-scope atomic on the evaluation's counter word (rh_internal.h, TableEvents)
-// and copies the records out as contiguous 16-byte-per-lane stores.
+// in registers.  REGION mode (HBM lists: the DEVICE / AUTO sinks' tile evaluations): each wave
+// writes its records straight into its own 128-record part of the lists and the workgroup its
+// counts into its descriptor; rh_table_gather packs the parts afterwards.  Counter mode (the lists
+// in pinned memory): the block gathers its events in LDS in wave order, takes ONE range of each
+// result list with ONE device-scope atomic on the evaluation's counter word (rh_internal.h,
+// TableEvents) and copies the records out as contiguous 16-byte-per-lane stores.
+// Workgroup size (same box, 1M rows, profiles/r05/table_eval/): 12 waves 20.4 us all dirty, 6
+// waves 20.2, 4 waves 19.3, 2 waves 19.1, 1 wave 19.3 -- small workgroups leave no CU holding a
+// workgroup slot for its slowest wave at the tail.
 struct TierRange {
     uint32_t block_begin[rh::kTableTiers + 1];  // blocks of launch slot i: [block_begin[i], block_begin[i+1])
     int8_t tier[rh::kTableTiers];               // tier of launch slot i (widest first)
     int32_t n_slots;
 };
 
-#ifndef RH_TABLE_BLOCK_WAVES                 // A/B: waves per workgroup (one tile each)
-#define RH_TABLE_BLOCK_WAVES 12
-#endif
 #ifndef RH_TABLE_WPE                         // A/B: waves per SIMD the widths-2..6 kernel is pinned to
 #define RH_TABLE_WPE 6
 #endif
@@ -281,8 +284,18 @@ struct TierRange {
 constexpr int kTWaves = RH_TABLE_BLOCK_WAVES;
 constexpr int kTBlock = kTWaves * 64;
 constexpr uint32_t kTRows = kTWaves * 128;   // rows per workgroup
+static_assert(kTRows <= rh::kTableRecs && 2 * kTWaves + 2 == rh::kTableDesc,
+              "REGION mode: a workgroup's records fit its region, its counts its descriptor");
 #ifndef RH_TABLE_NT                          // A/B: non-temporal column loads (1) or plain (0)
 #define RH_TABLE_NT 0
+#endif
+
+#ifndef RH_TABLE_EV_NT   // A/B: REGION-mode event records stored non-temporally (1) or plain (0)
+#define RH_TABLE_EV_NT 0
+#endif
+
+#ifndef RH_TABLE_ABL   // ablation only (wrong results): 2 = no event records, 3 = no table stores, 4 = trivial arithmetic
+#define RH_TABLE_ABL 0
 #endif
 
 template <typename V>
@@ -297,7 +310,8 @@ __device__ __forceinline__ V tload(const uint8_t* p) {
 struct Stage {
     uint32_t cnt[2][kTWaves];
     uint32_t pre[2][kTWaves + 1];  // exclusive prefix of cnt over the waves
-    unsigned long long base;        // the block's range of the lists (both kinds packed)
+    unsigned long long base;        // the block's first record in list 0 (REGION mode: in both lists)
+    unsigned long long base1;       // counter mode: its first record in list 1
 };
 
 // SPEC (chosen per evaluation by the host, rh_table_commit): the evaluation follows deltas that
@@ -308,7 +322,7 @@ struct Stage {
 // lines loaded): hence the host's choice.
 template <int F, bool RANK, bool WATCH, bool SPEC>
 __device__ __forceinline__ void table_wave(const TableDev& T, const TableTier& tt, uint64_t tl, bool wall_on,
-                                           unsigned char* stage, Stage& sc) {
+                                           unsigned char* stage, Stage& sc, const TableEvents& ev, uint64_t gb) {
     constexpr int N = F + 1;
     constexpr uint64_t TB = tile::bytes(F);
     const int lane = threadIdx.x & 63;
@@ -379,7 +393,17 @@ __device__ __forceinline__ void table_wave(const TableDev& T, const TableTier& t
         vals[F] = self[g];
         bool v;
         int64_t mn, mj, mx;
+#if RH_TABLE_ABL == 4
+        (void)any_trans;
+        v = (w[g] & RH_CONF_ACTIVE) != 0;
+        mn = vals[0];
+#pragma unroll
+        for (int k = 1; k < N; ++k) mn ^= vals[k];
+        mj = mn + 1;
+        mx = mn + 2;
+#else
         rh_eval::eval_group<F, RANK>(vals, w[g], gap, any_trans, v, mn, mj, mx);
+#endif
         const bool dg = g ? d1 : d0;
         valid[g] = v ? 1u : 0u;
         if (WATCH) {
@@ -393,9 +417,14 @@ __device__ __forceinline__ void table_wave(const TableDev& T, const TableTier& t
         }
     }
     // table stores: only what changed, plus clearing this lane's dirty flags and the tile summary
+    const uint64_t a0 = __ballot(e0[0]), a1 = __ballot(e0[1]);
+#if RH_TABLE_ABL == 3
+    if (lane == 64) {
+#else
+    {
+#endif
     if (need) *reinterpret_cast<uint16_t*>(dflag) = 0;
     if (lane == 0) *sump = 0;
-    const uint64_t a0 = __ballot(e0[0]), a1 = __ballot(e0[1]);
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
         const uint32_t ro = 2u * lane + g;
@@ -414,11 +443,43 @@ __device__ __forceinline__ void table_wave(const TableDev& T, const TableTier& t
         }
     }
     if (!WATCH && (a0 | a1) && lane == 0) tt.sum[2 * tl + 1] = 1;
-    // events: compacted into this wave's LDS region, in row order
+    }
+#if RH_TABLE_ABL == 2
+    if (lane == 0) sc.cnt[0][threadIdx.x >> 6] = 0;
+    return;
+#endif
+    // events: compacted into this wave's LDS region, in row order -- or, in REGION mode, straight
+    // into this wave's 128 records of the block's region of the HBM lists (rh_table_gather packs them)
     const int wave = threadIdx.x >> 6;
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     uint32_t p = (uint32_t)(__popcll(a0 & lt) + __popcll(a1 & lt));
-    if (WATCH) {
+    const uint64_t rg = gb * rh::kTableRecs + (uint64_t)wave * 128;
+    if (ev.bdesc) {
+        if (WATCH) {
+#pragma unroll
+            for (int g = 0; g < 2; ++g)
+                if (e0[g]) ev.watch[rg + p++] = rh_watch_event{slot[g], valid[g], x0[g], x1[g], x2[g]};
+        } else {
+            const uint64_t c0 = __ballot(e1[0]), c1 = __ballot(e1[1]);
+            uint32_t q = (uint32_t)(__popcll(c0 & lt) + __popcll(c1 & lt));
+#pragma unroll
+            for (int g = 0; g < 2; ++g) {
+                if (RH_TABLE_EV_NT) {
+                    typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
+                    if (e0[g])
+                        __builtin_nontemporal_store(v4u32{slot[g], 0u, (uint32_t)x0[g], (uint32_t)((uint64_t)x0[g] >> 32)},
+                                                    reinterpret_cast<v4u32*>(ev.adv + rg + p++));
+                    if (e1[g])
+                        __builtin_nontemporal_store(v4u32{slot[g], 0u, (uint32_t)x1[g], (uint32_t)((uint64_t)x1[g] >> 32)},
+                                                    reinterpret_cast<v4u32*>(ev.wall + rg + q++));
+                } else {
+                    if (e0[g]) ev.adv[rg + p++] = rh_index_event{slot[g], 0u, x0[g]};
+                    if (e1[g]) ev.wall[rg + q++] = rh_index_event{slot[g], 0u, x1[g]};
+                }
+            }
+            if (lane == 0) sc.cnt[1][wave] = (uint32_t)(__popcll(c0) + __popcll(c1));
+        }
+    } else if (WATCH) {
         rh_watch_event* sw = reinterpret_cast<rh_watch_event*>(stage) + wave * 128;
 #pragma unroll
         for (int g = 0; g < 2; ++g)
@@ -440,11 +501,11 @@ __device__ __forceinline__ void table_wave(const TableDev& T, const TableTier& t
 
 template <int F, int FHI, bool RANK, bool WATCH, bool SPEC>
 __device__ __forceinline__ void table_dispatch(const TableDev& T, int t, uint64_t tl, bool wall_on,
-                                               unsigned char* stage, Stage& sc) {
+                                               unsigned char* stage, Stage& sc, const TableEvents& ev, uint64_t gb) {
     if ((int)rh::width_of_tier(t) == F)
-        table_wave<F, RANK, WATCH, SPEC>(T, T.tier[t], tl, wall_on, stage, sc);
+        table_wave<F, RANK, WATCH, SPEC>(T, T.tier[t], tl, wall_on, stage, sc, ev, gb);
     else if constexpr (F + 2 <= FHI)
-        table_dispatch<F + 2, FHI, RANK, WATCH, SPEC>(T, t, tl, wall_on, stage, sc);
+        table_dispatch<F + 2, FHI, RANK, WATCH, SPEC>(T, t, tl, wall_on, stage, sc, ev, gb);
 }
 
 // The evaluation's counter word (rh_internal.h, TableEvents): kind 0 in bits [0, cbits), kind 1 in
@@ -491,8 +552,28 @@ __device__ __forceinline__ void table_block_iter(const TableDev& T, const TierRa
     if (b == 0 && threadIdx.x < rh::kHeads && ev.lheads_next)
         ev.lheads_next[threadIdx.x * rh::kHeadStride] = 0ull;  // the next list set of this kind
     __syncthreads();
-    if (tl * rh::kTileRows < T.tier[t].rows) table_dispatch<FLO, FHI, FLO <= 6, WATCH, SPEC>(T, t, tl, wall_on, stage, sc);
+    const uint64_t gb = (uint64_t)ev.block_base + b;   // REGION mode: the evaluation's workgroup number
+    if (tl * rh::kTileRows < T.tier[t].rows)
+        table_dispatch<FLO, FHI, FLO <= 6, WATCH, SPEC>(T, t, tl, wall_on, stage, sc, ev, gb);
     __syncthreads();
+
+    if (ev.bdesc) {
+        // ---- REGION mode: the waves wrote their records into their own 128-record parts of the
+        // block's region; the block's counts (totals, then per wave) go to bdesc for the gather
+        if (threadIdx.x < 2 * kTWaves + 2) {
+            const uint32_t k = threadIdx.x;
+            uint32_t v;
+            if (k < 2) {
+                v = 0;
+#pragma unroll
+                for (int w = 0; w < kTWaves; ++w) v += sc.cnt[k][w];
+            } else {
+                v = sc.cnt[(k - 2) / kTWaves][(k - 2) % kTWaves];
+            }
+            ev.bdesc[gb * rh::kTableDesc + k] = v;
+        }
+        return;
+    }
 
     // ---- one range of each list per block (one device-scope atomic), then a contiguous copy
     if (threadIdx.x == 0) {
@@ -505,24 +586,27 @@ __device__ __forceinline__ void table_block_iter(const TableDev& T, const TierRa
         }
         sc.pre[0][kTWaves] = a0;
         sc.pre[1][kTWaves] = a1;
-        const uint32_t cb = ev.cbits;
-        const unsigned long long add = (unsigned long long)a0 | ((unsigned long long)a1 << cb) |
-                                       (ev.packed ? 1ull << (2 * cb) : 0ull);
-        const unsigned long long old = add ? atomicAdd(ev.cnt, add) : 0ull;
-        sc.base = old;
-        if (!ev.packed) {
-            block_done(ev, old);
-        } else if (ev.done_target && ((old + add) >> (2 * cb)) == ev.done_target) {   // the last workgroup
-            publish_counts(ev, old + add);
-            atomicExch(ev.cnt, 0ull);   // the next evaluation's counter
+        {   // counter mode (REGION mode returned above)
+            const uint32_t cb = ev.cbits;
+            const unsigned long long add = (unsigned long long)a0 | ((unsigned long long)a1 << cb) |
+                                           (ev.packed ? 1ull << (2 * cb) : 0ull);
+            const unsigned long long old = add ? atomicAdd(ev.cnt, add) : 0ull;
+            const unsigned long long cm = (1ull << cb) - 1;
+            sc.base = old & cm;
+            sc.base1 = (old >> cb) & cm;
+            if (!ev.packed) {
+                block_done(ev, old);
+            } else if (ev.done_target && ((old + add) >> (2 * cb)) == ev.done_target) {   // the last workgroup
+                publish_counts(ev, old + add);
+                atomicExch(ev.cnt, 0ull);   // the next evaluation's counter
+            }
         }
     }
     __syncthreads();
     const uint32_t tot0 = sc.pre[0][kTWaves], tot1 = sc.pre[1][kTWaves];
     if (!(tot0 | tot1)) return;
     const uint64_t R = ev.cap;   // a list holds one record per row at most: never reached
-    const unsigned long long cm = (1ull << ev.cbits) - 1;
-    const uint64_t b0 = sc.base & cm, b1 = (sc.base >> ev.cbits) & cm;
+    const uint64_t b0 = sc.base, b1 = sc.base1;
     const uint64_t lim0 = b0 >= R ? 0 : (b0 + tot0 <= R ? tot0 : R - b0);
     const uint64_t lim1 = b1 >= R ? 0 : (b1 + tot1 <= R ? tot1 : R - b1);
     // record e of the block lives in the region of wave k with pre[k] <= e < pre[k + 1]
@@ -567,8 +651,8 @@ __device__ __forceinline__ void table_commit_block(const TierRange& tr, const Ta
 }
 
 // Widths 2..6: rank-mask order statistics, 6 waves per SIMD (<= 84 VGPRs: the row pair's columns
-// are all in flight before the compute; at 64 VGPRs the compiler spilled 52 B per lane): two
-// 12-wave workgroups (2 x 48 KiB of event staging) per CU.  Widths 8..14: Batcher networks
+// are all in flight before the compute; at 64 VGPRs the compiler spilled 52 B per lane; pinned to
+// 8 waves per SIMD, 19.9 us vs 19.3 at 4-wave workgroups).  Widths 8..14: Batcher networks
 // (commit.hip's split) with the registers their 15-value networks need; these tiers are rare.
 template <bool WATCH, bool SPEC>
 __global__ __launch_bounds__(kTBlock) __attribute__((amdgpu_waves_per_eu(RH_TABLE_WPE, 8))) void table_commit_kernel_rank(
@@ -918,6 +1002,7 @@ int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev_i
         for (int s = tr.n_slots; s <= rh::kTableTiers; ++s) tr.block_begin[s] = blocks;
         if (blocks == 0) continue;
         ev.done_target = cls == last_cls ? total : 0u;   // workgroups of both launches count
+        ev.block_base = cls == 0 ? 0u : class_blocks(t, 0);   // REGION mode: workgroup numbering
         const dim3 g(blocks), b(kTBlock);
         const hipEvent_t a0 = cls == first_cls ? t0 : nullptr, a1 = cls == last_cls ? t1 : nullptr;
         hipError_t e;
@@ -974,6 +1059,96 @@ int rh_table_drain(const uint64_t* counts, const void* a, void* a_out, const voi
     hipLaunchKernelGGL(table_drain_kernel, dim3(512), dim3(256), 0, stream, counts, static_cast<const uint4*>(a),
                        static_cast<uint4*>(a_out), static_cast<const uint4*>(b), static_cast<uint4*>(b_out),
                        rec_bytes0 / 16u, cap);
+    RH_HIP(hipGetLastError());
+    return RH_OK;
+}
+
+// ---- REGION mode: the per-workgroup regions packed into the result lists --------------------------
+// One gather workgroup per kGatherWGs evaluation workgroups (kGatherChunks wave parts of 128
+// records).  Its offsets in the packed lists are the sums of the totals of the evaluation
+// workgroups before its first (read from bdesc, a few KiB: summed by the 256 threads, reduced in
+// LDS); its parts' counts are scanned in LDS, then every thread moves records (16-byte words; to
+// pinned memory: GPU writes across PCIe), finding each record's part by binary search of the scan.
+// Gather workgroup 0 also sums every total and publishes the two lengths.
+constexpr uint32_t kGatherWGs = kTWaves >= 32 ? 1u : 32u / kTWaves;
+constexpr uint32_t kGatherChunks = kGatherWGs * kTWaves;
+
+__device__ __forceinline__ uint32_t part_of(const uint32_t* pre, uint32_t e) {   // pre[c] <= e < pre[c + 1]
+    uint32_t lo = 0, hi = kGatherChunks;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (pre[mid] <= e) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(256) void table_gather_kernel(const uint32_t* __restrict__ bdesc, uint32_t n_blocks,
+                                                           const uint4* __restrict__ a, uint4* __restrict__ a_out,
+                                                           const uint4* __restrict__ b, uint4* __restrict__ b_out,
+                                                           uint32_t words0, uint64_t* counts_out) {
+    constexpr uint32_t D = rh::kTableDesc;   // per evaluation workgroup: totals, then per-wave counts
+    __shared__ unsigned long long red[2][256 / 64];
+    __shared__ uint32_t pre[2][kGatherChunks + 1];
+    const uint32_t first = blockIdx.x * kGatherWGs;      // first evaluation workgroup of this gather
+    const uint32_t upto = blockIdx.x == 0 ? n_blocks : first;   // gather workgroup 0 sums them all
+    unsigned long long s0 = 0, s1 = 0;
+    for (uint32_t j = threadIdx.x; j < upto; j += blockDim.x) {
+        s0 += bdesc[(uint64_t)j * D];
+        s1 += bdesc[(uint64_t)j * D + 1];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        s0 += __shfl_down(s0, o);
+        s1 += __shfl_down(s1, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = s0;
+        red[1][threadIdx.x >> 6] = s1;
+    }
+    for (uint32_t c = threadIdx.x; c < kGatherChunks; c += blockDim.x) {   // the parts' counts
+        const uint32_t gb = first + c / kTWaves, w = c % kTWaves;
+        pre[0][c + 1] = gb < n_blocks ? bdesc[(uint64_t)gb * D + 2 + w] : 0u;
+        pre[1][c + 1] = gb < n_blocks ? bdesc[(uint64_t)gb * D + 2 + kTWaves + w] : 0u;
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {   // inclusive scan of one kind's part counts
+        uint32_t* p = pre[threadIdx.x];
+        p[0] = 0;
+        for (uint32_t c = 1; c <= kGatherChunks; ++c) p[c] += p[c - 1];
+    }
+    s0 = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    s1 = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+    uint64_t p0 = s0, p1 = s1;
+    if (blockIdx.x == 0) {
+        if (threadIdx.x == 0) {
+            counts_out[0] = s0;
+            counts_out[1] = b ? s1 : 0;
+        }
+        p0 = p1 = 0;
+    }
+    __syncthreads();
+    const uint64_t part0 = (uint64_t)first * kTWaves;   // global index of this gather's first part
+    const uint32_t n0 = pre[0][kGatherChunks] * words0;
+    for (uint32_t j = threadIdx.x; j < n0; j += blockDim.x) {
+        const uint32_t e = j / words0, c = part_of(pre[0], e);
+        const uint64_t src = (part0 + c) * 128 + (e - pre[0][c]);
+        a_out[(p0 + e) * words0 + j % words0] = a[src * words0 + j % words0];
+    }
+    if (b) {
+        const uint32_t n1 = pre[1][kGatherChunks];
+        for (uint32_t e = threadIdx.x; e < n1; e += blockDim.x) {
+            const uint32_t c = part_of(pre[1], e);
+            b_out[p1 + e] = b[(part0 + c) * 128 + (e - pre[1][c])];
+        }
+    }
+}
+
+int rh_table_gather(const uint32_t* bdesc, uint32_t n_blocks, const void* a, void* a_out, const void* b, void* b_out,
+                    uint32_t rec_bytes0, uint64_t* counts_out, hipStream_t stream) {
+    if (n_blocks == 0) return rh::fail(RH_E_INVAL, "rh_table_gather: no workgroups");
+    hipLaunchKernelGGL(table_gather_kernel, dim3((n_blocks + kGatherWGs - 1) / kGatherWGs), dim3(256), 0, stream, bdesc,
+                       n_blocks, static_cast<const uint4*>(a), static_cast<uint4*>(a_out), static_cast<const uint4*>(b),
+                       static_cast<uint4*>(b_out), rec_bytes0 / 16u, counts_out);
     RH_HIP(hipGetLastError());
     return RH_OK;
 }
