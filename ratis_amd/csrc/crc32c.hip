@@ -1597,6 +1597,13 @@ int rh_crc_upload_tables(rh_ctx* ctx) {
     const std::vector<uint32_t> iff = rh::build_crc_init_terms(0xFFFFFFFFu);
     RH_HIP(hipMalloc(&ctx->d_initff, iff.size() * 4));
     RH_HIP(hipMemcpy(ctx->d_initff, iff.data(), iff.size() * 4, hipMemcpyHostToDevice));
+    ctx->h_initff = iff;
+    uint32_t s8[8][256];
+    for (int k = 0; k < 8; ++k)
+        for (int b = 0; b < 256; ++b)
+            s8[k][b] = k < 4 ? t.slice[k][b] : (s8[k - 1][b] >> 8) ^ t.slice[0][s8[k - 1][b] & 0xffu];
+    RH_HIP(hipMalloc(&ctx->d_slice8, sizeof(s8)));
+    RH_HIP(hipMemcpy(ctx->d_slice8, s8, sizeof(s8), hipMemcpyHostToDevice));
     return RH_OK;
 }
 
@@ -1735,4 +1742,145 @@ int rh_crc_verify_slots(rh_ctx* ctx, const rh_segments* g, const rh_segments_crc
     sp.total = g->total_frames;
     sp.n_seg = g->n_seg;
     return launch_frames(ctx, a, stream, dense_written, sp);
+}
+
+// ---- small flush batches from a registered buffer: zero-copy, one launch ---------------------------
+// (rh_internal.h, StampArgs.)  Every byte a workgroup needs -- its span across PCIe, its frame
+// records across PCIe, the slicing-by-8 table and the shift maps its frames need from HBM -- lands
+// in LDS by LDS-DMA (16 B per lane, no registers), all issued before the first barrier: one PCIe
+// round trip.  Thread t owns a run of frames for the window-count scan (wave scans + the wave
+// totals scanned by wave 0); windows are then dealt round robin: window w's frame by binary search
+// of the scan, j = its rank from the payload's end.  A window: 17 aligned LDS words funnel-shifted
+// to its byte position, the leading bytes outside the frame zeroed (a zero register absorbs
+// leading zeros), eight slicing-by-8 rounds (PJC:54-91) from a zero register, then advanced over
+// the 64 j bytes after it (j's set bits: the maps over 64 * 2^b zero bytes) and XOR-ed into its
+// frame's accumulator: a frame's register is A^len(init) ^ XOR of its windows' terms (the CRC is
+// affine in the register and linear in the bytes).
+namespace {
+constexpr uint32_t kStampWaves = kStampThreads / 64;
+constexpr uint32_t kStampFpt = kStampMaxFrames / kStampThreads;   // frames per thread in the scan
+constexpr uint32_t kStampLdsT = 8 * 1024 + kStampShifts * 4096;  // tables
+constexpr uint32_t kStampLdsF = kStampMaxFrames * 16;            // frame records
+constexpr uint32_t kStampLds = kStampLdsT + kStampLdsF + 16 * (kStampWaves + 1) + kStampFront + kStampSpan + 16;
+static_assert(kStampLds <= 160 * 1024, "LDS budget");
+static_assert(kStampMaxFrames % kStampThreads == 0, "frames per thread");
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_void_t;
+
+// pieces [0, n) of 16 B from global `src` to LDS `dst` (16-B aligned both), the workgroup's waves
+// each taking runs of 64 pieces (one LDS-DMA instruction: wave-uniform LDS base + lane * 16)
+__device__ __forceinline__ void dma16(const uint8_t* src, uint8_t* dst, uint32_t n, uint32_t wave, uint32_t lane) {
+    for (uint32_t p0 = 64u * wave; p0 < n; p0 += 64u * kStampWaves) {
+        const uint32_t i = p0 + lane;
+        if (i < n)
+            __builtin_amdgcn_global_load_lds((gbl_void_t*)(src + 16ull * i), (lds_void_t*)(dst + 16u * i), 16, 0, 0);
+    }
+}
+
+__global__ __launch_bounds__(kStampThreads) void crc_stamp_mapped_kernel(StampArgs arg) {
+    (void)arg;
+    const StampArgs& A = rh::kernarg_struct<StampArgs>();   // uniform index: scalar loads
+    extern __shared__ __attribute__((aligned(16))) uint8_t sb[];
+    const uint32_t* T = reinterpret_cast<const uint32_t*>(sb);   // [8][256]
+    const uint32_t* Z = T + 8 * 256;                            // [n_shift][4][256]
+    uint4* fr = reinterpret_cast<uint4*>(sb + kStampLdsT);      // [frame_n]: pos, payload, acc, prefix
+    uint32_t* wsum = reinterpret_cast<uint32_t*>(sb + kStampLdsT + kStampLdsF);   // [kStampWaves + 1]
+    uint8_t* img = sb + kStampLdsT + kStampLdsF + 16 * (kStampWaves + 1);         // kStampFront + span + 16
+    const StampGroup& g = A.g[blockIdx.x];
+    const uint32_t t = threadIdx.x, lane = t & 63u, wave = t >> 6;
+    const uint32_t nq = (g.bytes_n >> 12) / 16, F = g.bytes_n & 4095u;
+    dma16(reinterpret_cast<const uint8_t*>(g.src), img + kStampFront, nq, wave, lane);
+    dma16(reinterpret_cast<const uint8_t*>(A.frames + g.frame_first), reinterpret_cast<uint8_t*>(fr), F, wave, lane);
+    dma16(reinterpret_cast<const uint8_t*>(A.slice8), sb, 512, wave, lane);
+    dma16(reinterpret_cast<const uint8_t*>(A.shift64), sb + 8 * 1024, 256 * A.n_shift, wave, lane);
+    __syncthreads();   // (waits for the LDS-DMA)
+    // windows per frame, scanned: thread t's frames [kStampFpt t, + kStampFpt)
+    uint32_t own = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kStampFpt; ++k) {
+        const uint32_t f = kStampFpt * t + k;
+        if (f < F) own += (fr[f].y + 63u) / 64u;
+    }
+    uint32_t incl = own;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t v = (uint32_t)__shfl_up((int)incl, d);
+        if ((int)lane >= d) incl += v;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    if (wave == 0) {   // exclusive scan of the wave totals (lanes < kStampWaves)
+        const uint32_t v = lane < kStampWaves ? wsum[lane] : 0u;
+        uint32_t x = v;
+#pragma unroll
+        for (int d = 1; d < (int)kStampWaves; d <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)x, d);
+            if ((int)lane >= d) x += y;
+        }
+        if (lane < kStampWaves) wsum[lane] = x - v;
+        if (lane == kStampWaves - 1) wsum[kStampWaves] = x;
+    }
+    __syncthreads();
+    uint32_t run = wsum[wave] + incl - own;
+#pragma unroll
+    for (uint32_t k = 0; k < kStampFpt; ++k) {
+        const uint32_t f = kStampFpt * t + k;
+        if (f < F) {
+            fr[f].w = run;
+            run += (fr[f].y + 63u) / 64u;
+        }
+    }
+    const uint32_t n_win = wsum[kStampWaves];
+    __syncthreads();
+    for (uint32_t wi = t; wi < n_win; wi += kStampThreads) {
+        uint32_t lo = 0, hi = F;   // the frame f with prefix[f] <= wi < prefix[f] + its windows
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (fr[mid].w <= wi) lo = mid; else hi = mid;
+        }
+        const uint32_t f = lo, j = wi - fr[f].w, fp = fr[f].x;
+        const int32_t P = (int32_t)(fp + fr[f].y) - 64 * (int32_t)(j + 1);   // the window's first byte
+        const uint32_t pos = (uint32_t)P, lead = P < (int32_t)fp ? fp - (uint32_t)P : 0u;
+        const uint32_t* wp = reinterpret_cast<const uint32_t*>(img + (pos & ~3u));
+        uint32_t W[17];
+#pragma unroll
+        for (int i = 0; i < 17; ++i) W[i] = wp[i];
+        const uint32_t sh = pos & 3u;
+        uint32_t D[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const uint32_t x = __builtin_amdgcn_alignbyte(W[i + 1], W[i], sh);
+            const int32_t z = (int32_t)lead - 4 * i;   // bytes of this word before the frame
+            D[i] = z >= 4 ? 0u : (z <= 0 ? x : x & (~0u << (8 * z)));
+        }
+        uint32_t c = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const uint32_t lo8 = D[2 * k] ^ c, hi8 = D[2 * k + 1];
+            c = xor3(xor3(T[7 * 256 + (lo8 & 0xffu)], T[6 * 256 + ((lo8 >> 8) & 0xffu)], T[5 * 256 + ((lo8 >> 16) & 0xffu)]),
+                     xor3(T[4 * 256 + (lo8 >> 24)], T[3 * 256 + (hi8 & 0xffu)], T[2 * 256 + ((hi8 >> 8) & 0xffu)]),
+                     T[256 + ((hi8 >> 16) & 0xffu)] ^ T[hi8 >> 24]);
+        }
+#pragma unroll
+        for (uint32_t b = 0; b < kStampShifts; ++b)
+            if ((j >> b) & 1u) c = zshift(Z + b * 1024, c);
+        atomicXor(&fr[f].z, c);
+    }
+    __syncthreads();
+    for (uint32_t f = t; f < F; f += kStampThreads) A.crc_out[g.frame_first + f] = ~fr[f].z;   // getValue()
+    __threadfence_system();   // this wave's CRC stores performed (system scope) before the flag
+    __syncthreads();
+    if (t == 0) __hip_atomic_store(A.done + blockIdx.x, A.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+}  // namespace
+
+int rh_crc_stamp_mapped_launch(const StampArgs& a, uint32_t n_groups, hipStream_t stream) {
+    if (n_groups == 0 || n_groups > kStampMaxGroups) return rh::fail(RH_E_INVAL, "crc stamp (mapped): group count");
+    static const hipError_t attr = hipFuncSetAttribute(reinterpret_cast<const void*>(crc_stamp_mapped_kernel),
+                                                       hipFuncAttributeMaxDynamicSharedMemorySize, kStampLds);
+    RH_HIP(attr);
+    hipLaunchKernelGGL(crc_stamp_mapped_kernel, dim3(n_groups), dim3(kStampThreads), kStampLds, stream, a);
+    RH_HIP(hipGetLastError());
+    return RH_OK;
 }

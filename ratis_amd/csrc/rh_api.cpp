@@ -1,6 +1,8 @@
 // libratis_hip C ABI (include/ratis_hip.h): contexts, the resident group table, host-buffer
 // conveniences.  Kernels live in commit.hip and crc32c.hip.
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstring>
 #include <string>
 #include <new>
@@ -124,6 +126,7 @@ RH_EXPORT int rh_shutdown(rh_ctx* ctx) {
     (void)hipFree(ctx->d_lane16);
     (void)hipFree(ctx->d_inv32);
     (void)hipFree(ctx->d_initff);
+    (void)hipFree(ctx->d_slice8);
     if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
     if (ctx->pool) (void)hipMemPoolDestroy(ctx->pool);
     (void)hipStreamDestroy(ctx->stream);
@@ -335,6 +338,140 @@ RH_EXPORT int rh_host_unregister(rh_ctx* ctx, void* p) {
 // plan 0: frames up to this length go one lane per frame; longer ones to the streaming plans
 constexpr uint64_t kSerialMaxFrame = 64 << 10;
 
+#ifndef RH_STAMP_ZERO_COPY   // A/B: the zero-copy plan for registered buffers (1) or never (0)
+#define RH_STAMP_ZERO_COPY 1
+#endif
+#ifndef RH_STAMP_SPIN        // A/B: the zero-copy plan's completion by a polled flag (1) or the stream (0)
+#define RH_STAMP_SPIN 1
+#endif
+
+namespace {
+// Grows the context's pinned staging to `bytes` (under stage_mu).
+int stage_reserve(rh_ctx* ctx, uint64_t bytes) {
+    if (ctx->pinned_bytes >= bytes) return RH_OK;
+    if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
+    ctx->h_pinned = nullptr;
+    ctx->pinned_bytes = 0;
+    const size_t want = std::max<size_t>(bytes, (size_t)1 << 20);
+    if (hipHostMalloc(&ctx->h_pinned, want, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess)
+        return rh::fail(RH_E_NOMEM, "rh_crc32c_stamp_host: pinned staging");
+    ctx->pinned_bytes = want;
+    return RH_OK;
+}
+
+constexpr int kNotPlanned = 1;   // stamp_zero_copy: the batch does not fit the plan (nothing done)
+
+// rh_crc32c_stamp_host's zero-copy plan (rh_internal.h, StampArgs): the frames dealt in their order
+// to workgroups of at most `cap` bytes of span (cap: the batch over 3/4 of kStampMaxGroups
+// workgroups, at least kStampThreads windows' worth), kStampMaxWin windows and kStampMaxFrames
+// frames; the frame records and CRCs in the pinned staging.  Needs the batch's span inside a
+// mapped registration of `buf` (rh_host_register), every payload under 64 * 2^kStampShifts bytes
+// and at most kStampMaxGroups workgroups.  Caller holds stage_mu.
+int stamp_zero_copy(rh_ctx* ctx, uint8_t* buf, uint64_t lo, uint64_t hi, const uint64_t* frame_off,
+                    const uint32_t* frame_len, uint64_t n, uint64_t max_len) {
+    // groups of `cap` span bytes: 3/4 of the workgroup limit, the rest slack for frames that do not
+    // pack to the cap (a 1 MiB batch of <= 2 KiB entries: ~100 workgroups)
+    const uint64_t cap = std::min<uint64_t>(kStampSpan, std::max<uint64_t>(64ull * kStampThreads,
+                                                                            ((hi - lo) / (kStampMaxGroups * 3 / 4) + 15) & ~15ull));
+    if (!RH_STAMP_ZERO_COPY || max_len - 4 >= (64ull << kStampShifts) || ctx->h_initff.empty() ||
+        hi - lo > (uint64_t)kStampMaxGroups * 3 / 4 * kStampSpan)   // would not fit the workgroups
+        return kNotPlanned;
+    uint8_t *d_lo = nullptr, *d_hi = nullptr;
+    if (hipHostGetDevicePointer(reinterpret_cast<void**>(&d_lo), buf + lo, 0) != hipSuccess ||
+        hipHostGetDevicePointer(reinterpret_cast<void**>(&d_hi), buf + hi - 1, 0) != hipSuccess ||
+        (uint64_t)(d_hi - d_lo) != hi - 1 - lo) {
+        (void)hipGetLastError();   // not registered (mapped): the copying plan
+        return kNotPlanned;
+    }
+    StampArgs A{};
+    auto al = [](uint64_t x) { return (x + 255) / 256 * 256; };
+    const uint64_t o_fr = 0, o_crc = al(n * 16), o_done = o_crc + al(n * 4);
+    int rc = stage_reserve(ctx, o_done + al(kStampMaxGroups * 4));
+    if (rc != RH_OK) return rc;
+    uint8_t* st = static_cast<uint8_t*>(ctx->h_pinned);
+    uint4* fr = reinterpret_cast<uint4*>(st + o_fr);
+    uint32_t ng = 0, g_win = 0, max_w = 1;
+    uint64_t g_lo = 0, g_hi = 0, g_first = 0;
+    StampGroup* g = nullptr;
+    auto close = [&](uint64_t end) {   // group g's frames [g_first, end): positions in its LDS image
+        const uint64_t base = g_lo & ~15ull;
+        g->src = reinterpret_cast<uint64_t>(d_lo) + base - lo;
+        g->bytes_n = (uint32_t)(((g_hi + 15) & ~15ull) - base) << 12 | (uint32_t)(end - g_first);
+        for (uint64_t k = g_first; k < end; ++k) fr[k].x = (uint32_t)(kStampFront + frame_off[k] - base);
+    };
+    for (uint64_t i = 0; i < n; ++i) {
+        const uint64_t o = frame_off[i], p = frame_len[i] - 4;
+        const uint32_t nw = (uint32_t)((p + 63) / 64);
+        max_w = std::max(max_w, nw);
+        const uint64_t nlo = std::min(g_lo, o), nhi = std::max(g_hi, o + p);
+        if (!g || o < g_lo || ((nhi + 15) & ~15ull) - (nlo & ~15ull) > cap || g_win + nw > kStampMaxWin ||
+            i - g_first == kStampMaxFrames) {   // a new workgroup (a frame before the group's start: a new base)
+            if (g) close(i);
+            if (ng == kStampMaxGroups) return kNotPlanned;
+            g = &A.g[ng++];
+            g->frame_first = (uint32_t)i;
+            g_first = i;
+            g_lo = o;
+            g_hi = o + p;
+            g_win = 0;
+        } else {
+            g_hi = nhi;
+        }
+        g_win += nw;
+        fr[i].y = (uint32_t)p;
+        fr[i].z = ctx->h_initff[p];
+        fr[i].w = 0;
+    }
+    close(n);
+    // the shift maps the frames need: j < max_w windows after a window
+    uint32_t n_shift = 0;
+    while ((1u << n_shift) < max_w) ++n_shift;
+    // completion: each workgroup stores the call's number to its flag word in the staging after
+    // its CRCs; the host polls them -- a few microseconds less than the stream's completion signal
+    // (hipStreamSynchronize follows when a flag is late, and reports any fault)
+    volatile unsigned int* done = reinterpret_cast<volatile unsigned int*>(st + o_done);
+    for (uint32_t k = 0; k < ng; ++k) done[k] = 0u;
+    uint8_t* dst = nullptr;
+    RH_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&dst), st, 0));
+    A.frames = reinterpret_cast<const uint4*>(dst + o_fr);
+    A.crc_out = reinterpret_cast<uint32_t*>(dst + o_crc);
+    A.done = reinterpret_cast<unsigned int*>(dst + o_done);
+    A.slice8 = ctx->d_slice8;
+    A.shift64 = ctx->d_shift + (size_t)6 * 1024;   // 2^6 = 64 bytes, then 128, ... (consecutive maps)
+    A.seq = ++ctx->stamp_seq;
+    if (A.seq == 0) A.seq = ctx->stamp_seq = 1;
+    A.n_shift = n_shift;
+    hipStream_t s = ctx->stream;
+    rc = rh_crc_stamp_mapped_launch(A, ng, s);
+    if (rc != RH_OK) return rc;
+    bool seen = false;
+    if (RH_STAMP_SPIN) {
+        const auto t0 = std::chrono::steady_clock::now();
+        uint32_t k = 0;
+        for (uint32_t it = 0;; ++it) {
+            while (k < ng && done[k] == A.seq) ++k;
+            if (k == ng) {
+                seen = true;
+                break;
+            }
+            if ((it & 255) == 255 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(2)) break;
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+    }
+    if (!seen) RH_HIP(hipStreamSynchronize(s));
+    const uint32_t* crc = reinterpret_cast<const uint32_t*>(st + o_crc);
+    for (uint64_t i = 0; i < n; ++i) {   // buf.putInt((int) checksum.getValue()): big-endian
+        uint8_t* t = buf + frame_off[i] + frame_len[i] - 4;
+        const uint32_t v = crc[i];
+        t[0] = (uint8_t)(v >> 24);
+        t[1] = (uint8_t)(v >> 16);
+        t[2] = (uint8_t)(v >> 8);
+        t[3] = (uint8_t)v;
+    }
+    return RH_OK;
+}
+}  // namespace
+
 RH_EXPORT int rh_crc32c_stamp_host(rh_ctx* ctx, uint8_t* buf, uint64_t buf_len, const uint64_t* frame_off,
                                    const uint32_t* frame_len, uint64_t n) {
     if (!ctx) return rh::fail(RH_E_INVAL, "rh_crc32c_stamp_host: ctx == NULL");
@@ -360,15 +497,10 @@ RH_EXPORT int rh_crc32c_stamp_host(rh_ctx* ctx, uint8_t* buf, uint64_t buf_len, 
     const uint64_t span = hi - lo;
     const uint64_t t_off = 0, t_len = al(n * 8), t_crc = t_len + al(n * 4), t_bytes = t_crc + al(n * 4);
     std::lock_guard<std::mutex> lk(ctx->stage_mu);
-    if (ctx->pinned_bytes < t_bytes) {
-        if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
-        ctx->h_pinned = nullptr;
-        ctx->pinned_bytes = 0;
-        const size_t want = std::max<size_t>(t_bytes, (size_t)1 << 20);
-        if (hipHostMalloc(&ctx->h_pinned, want, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess)
-            return rh::fail(RH_E_NOMEM, "rh_crc32c_stamp_host: pinned staging");
-        ctx->pinned_bytes = want;
-    }
+    const int zc = stamp_zero_copy(ctx, buf, lo, hi, frame_off, frame_len, n, max_len);
+    if (zc != kNotPlanned) return zc;
+    const int rs = stage_reserve(ctx, t_bytes);
+    if (rs != RH_OK) return rs;
     uint8_t* st = static_cast<uint8_t*>(ctx->h_pinned);
     // the device image has kPad bytes before the span and after it: no frame lies within the window
     // kernel's guard distances of the image ends (67 B before, 8 B after), so none takes its byte-wise

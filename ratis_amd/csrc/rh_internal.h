@@ -214,6 +214,9 @@ struct rh_ctx {
     uint32_t* d_lane16 = nullptr;  // lane-distance nibble tables (Q = 2, 4, 8, 16, 32 lanes x 64 B)
     uint32_t* d_inv32 = nullptr;   // [32][8][16] inverse lane maps of the packed CRC kernel
     uint32_t* d_initff = nullptr;  // [kCrcInitSpan + 1] advance of reset()'s 0xFFFFFFFF over k zero bytes
+    uint32_t* d_slice8 = nullptr;  // [8][256]: PureJavaCrc32C's slicing-by-8 tables (T[k] = T[k-1] + one zero byte)
+    std::vector<uint32_t> h_initff;  // host copy of d_initff (rh_crc32c_stamp_host's zero-copy plan)
+    unsigned int stamp_seq = 0;   // zero-copy plan: the last call's completion number
     std::mutex pool_mu;  // guards the pool's creation
     std::mutex stage_mu;  // guards the pinned staging below (rh_crc32c_stamp_host's frame table / CRCs)
     void* h_pinned = nullptr;
@@ -282,6 +285,46 @@ int rh_table_read(const rh::TableDev& t, uint32_t first, uint32_t n, uint8_t col
 int rh_crc_launch_impl(rh_ctx* ctx, const rh_frames* f, uint32_t flags, hipStream_t stream, bool window_only = false);
 // One lane per frame (crc_serial_kernel): small batches of well-formed frames (no bad bits / counts).
 int rh_crc_serial_launch(rh_ctx* ctx, const rh_frames* f, uint32_t flags, hipStream_t stream);
+
+// rh_crc32c_stamp_host's zero-copy plan (a buffer registered with rh_host_register): one launch,
+// no copies, no device scratch.  The batch's frames are dealt in order to workgroups of at most
+// kStampSpan bytes of span and kStampMaxWin 64-byte windows (the host sizes them so that the
+// batch spreads over up to kStampMaxGroups CUs).  Workgroup g moves its span straight from the
+// mapped host buffer, its frame records from the mapped staging and the CRC tables from HBM into
+// LDS (LDS-DMA, one round trip), cuts every payload into windows from its end (a scan of the
+// window counts; each window's frame found by binary search), folds the windows (the first one's
+// bytes before the frame masked), and XORs each window's register, advanced over the bytes after
+// it in its frame, into its frame's accumulator (seeded with reset()'s term for the frame's
+// length).  The CRCs go to mapped pinned memory, then the workgroup's done flag.
+#ifndef RH_STAMP_THREADS      // A/B: threads per workgroup
+#define RH_STAMP_THREADS 128
+#endif
+struct StampGroup {
+    uint64_t src;          // device address (host mapping) of the span's first byte, 16-B aligned
+    uint32_t frame_first;  // its frames: records / CRCs [frame_first, + frame_n)
+    uint32_t bytes_n;      // span bytes (a multiple of 16, <= kStampSpan) << 12 | frame_n
+};
+constexpr uint32_t kStampThreads = RH_STAMP_THREADS;
+constexpr uint32_t kStampSpan = 64 << 10;   // span bytes per workgroup at most (its LDS image)
+constexpr uint32_t kStampMaxWin = 1024;     // windows per workgroup at most
+constexpr uint32_t kStampMaxFrames = 1024;  // frames per workgroup at most
+constexpr uint32_t kStampShifts = 8;        // windows after a window in its frame: < 2^kStampShifts
+constexpr uint32_t kStampMaxGroups = 128;   // workgroups per launch (descriptors: kernel arguments)
+constexpr uint32_t kStampFront = 64;        // LDS image bytes before the span (a first window starts <= 63 B early)
+static_assert(kStampSpan < (1u << 20) && kStampMaxFrames < 4096 && kStampThreads % 64 == 0, "StampGroup.bytes_n");
+// frame record in the staging (16 B: one LDS-DMA piece): x = LDS byte position of the payload,
+// y = payload bytes, z = reset()'s term for them, w = 0 (the kernel's window prefix)
+struct StampArgs {
+    StampGroup g[kStampMaxGroups];
+    const uint4* frames;        // mapped pinned, per frame
+    uint32_t* crc_out;          // mapped pinned, per frame
+    unsigned int* done;         // mapped pinned, per workgroup: `seq` once its CRCs are stored
+    const uint32_t* slice8;     // device [8][256]
+    const uint32_t* shift64;    // device: the zero-advance maps over 64 * 2^b bytes, b = 0..7
+    unsigned int seq;
+    uint32_t n_shift;           // maps staged (the longest frame's windows - 1 < 2^n_shift)
+};
+int rh_crc_stamp_mapped_launch(const StampArgs& a, uint32_t n_groups, hipStream_t stream);
 int rh_crc_upload_tables(rh_ctx* ctx);
 int rh_segments_launch_impl(rh_ctx* ctx, const rh_segments* segs, hipStream_t stream);
 int rh_segments_read_impl(rh_ctx* ctx, const rh_segments* segs, const rh_segments_crc* crc, hipStream_t stream);

@@ -117,3 +117,52 @@ def test_stamp_plan_boundaries(ctx, orc, case):
         off, ln = off[p], ln[p]
     engine.stamp_host(ctx, buf, off, ln)
     assert np.array_equal(buf, want)
+
+
+@pytest.mark.parametrize("case", ["16k", "64k_unaligned", "1m_groups", "tiny_entries", "1024_frames", "1025_frames",
+                                  "shuffled_with_gaps", "long_frame_fallback", "8m_over_groups"])
+def test_stamp_zero_copy_registered(ctx, orc, case):
+    """The zero-copy plan (rh_api.cpp stamp_zero_copy, rh_internal.h StampArgs): a registered buffer,
+    payloads under 16 KiB, at most 96 workgroups of 64 KiB span / 1024 windows / 1024 frames.  Frames
+    at unaligned offsets (the span's 16-byte rounding), empty and 1..3-byte payloads (windows that
+    are all leading bytes), workgroup splits by frame count and by span, frames out of buffer order
+    (a new workgroup whenever a frame starts before its group), and batches the plan does not take
+    (a 20 KiB payload, an 8 MiB batch over 96 workgroups) -- every trailer equal to the oracle
+    writer's and every other byte untouched."""
+    from ratis_amd import engine
+    rng = np.random.default_rng(hash(case) & 0xFFFF)
+    gap = 0
+    if case == "16k":
+        sizes = rng.integers(64, 2048, 16)
+    elif case == "64k_unaligned":
+        sizes = rng.integers(1, 2048, 60)
+        gap = 13
+    elif case == "1m_groups":
+        sizes = rng.integers(64, 2048, 1000)
+    elif case == "tiny_entries":
+        sizes = np.concatenate([np.zeros(40, np.int64), rng.integers(0, 4, 200), rng.integers(60, 70, 50)])
+        rng.shuffle(sizes)
+    elif case == "1024_frames":
+        sizes = rng.integers(0, 100, 1024)
+    elif case == "1025_frames":
+        sizes = rng.integers(0, 100, 1025)
+    elif case == "shuffled_with_gaps":
+        sizes = rng.integers(0, 5000, 200)
+        gap = 40
+    elif case == "long_frame_fallback":
+        sizes = np.append(rng.integers(0, 700, 50), 20 << 10)
+    else:
+        sizes = rng.integers(64, 2048, 8000)
+    want, buf, off, ln = _frames(orc, rng, sizes, gap=gap)
+    lead = int(rng.integers(1, 16))   # the batch starts off a 16-byte boundary of the registration
+    want = np.concatenate([np.full(lead, 0xC3, np.uint8), want, np.full(21, 0x3C, np.uint8)])
+    buf = np.concatenate([np.full(lead, 0xC3, np.uint8), buf, np.full(21, 0x3C, np.uint8)])
+    off = off + np.uint64(lead)
+    if case == "shuffled_with_gaps":
+        p = rng.permutation(off.size)
+        off, ln = off[p], ln[p]
+    with engine.HostRegistration(ctx, buf):
+        engine.stamp_host(ctx, buf, off, ln)
+        assert np.array_equal(buf, want)
+        engine.stamp_host(ctx, buf, off, ln)   # restamping stamped frames: the same bytes
+        assert np.array_equal(buf, want)

@@ -295,7 +295,7 @@ def test_writer_seam_stamps_flush_batches():
     close = _method_body(worker, "void close()")
     assert close.index("IOUtils.cleanup(LOG, hipStamper)") < close.index("PlatformDependent.freeDirectBuffer(writeBuffer)")
     keys = _patched_java("server/RaftServerConfigKeys.java")
-    assert 'CHECKSUM_GPU_MIN_BYTES_DEFAULT = SizeInBytes.valueOf("256KB")' in keys
+    assert 'CHECKSUM_GPU_MIN_BYTES_DEFAULT = SizeInBytes.valueOf("64KB")' in keys
     stamper = open(os.path.join(JAVA, "java", "org", "apache", "ratis", "hip", "HipFrameStamper.java")).read()
     assert "DEFAULT_MIN_GPU_BYTES = 256 << 10" in stamper
     st = _method_body(stamper, "public boolean stamp(ByteBuffer buf, FrameChecksum cpu)")
