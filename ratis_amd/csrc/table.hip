@@ -294,7 +294,7 @@ static_assert(kTRows <= rh::kTableRecs && 2 * kTWaves + 2 == rh::kTableDesc,
 #define RH_TABLE_EV_NT 0
 #endif
 
-#ifndef RH_TABLE_ABL   // ablation only (wrong results): 2 = no event records, 3 = no table stores, 4 = trivial arithmetic
+#ifndef RH_TABLE_ABL   // ablation only (wrong results): 2 = no events, 3 = no table stores, 4 = trivial arithmetic, 5 = REGION-mode counts without the record stores
 #define RH_TABLE_ABL 0
 #endif
 
@@ -472,7 +472,7 @@ __device__ __forceinline__ void table_wave(const TableDev& T, const TableTier& t
                     if (e1[g])
                         __builtin_nontemporal_store(v4u32{slot[g], 0u, (uint32_t)x1[g], (uint32_t)((uint64_t)x1[g] >> 32)},
                                                     reinterpret_cast<v4u32*>(ev.wall + rg + q++));
-                } else {
+                } else if (RH_TABLE_ABL != 5) {
                     if (e0[g]) ev.adv[rg + p++] = rh_index_event{slot[g], 0u, x0[g]};
                     if (e1[g]) ev.wall[rg + q++] = rh_index_event{slot[g], 0u, x1[g]};
                 }
