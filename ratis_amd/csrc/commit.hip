@@ -22,7 +22,11 @@
 
 namespace {
 
-constexpr int kBlock = 256;            // 4 waves
+#ifndef RH_COMMIT_BLOCK   // A/B: threads per commit_kernel_rank / _net workgroup (the fused leader kernel keeps 256)
+#define RH_COMMIT_BLOCK 256
+#endif
+constexpr int kBlock = RH_COMMIT_BLOCK;
+constexpr int kLeaderBlock = 256;      // 4 waves
 #ifndef RH_COMMIT_WAVES  // A/B builds override (scripts/ab_build.sh): waves per SIMD the F <= 6 kernels are pinned to
 #define RH_COMMIT_WAVES 8
 #endif
@@ -248,13 +252,13 @@ __device__ __forceinline__ void compute_store_sub(const TierArgs& ta, uint64_t w
 
 // One wave = one 128-group sub-tile: all loads of the tile are issued before any compute.  The
 // block's bit words (8 per column) leave through LDS in one 64-byte store per column.
-template <int F, bool RANK, bool NT, bool NTS>
+template <int F, bool RANK, bool NT, bool NTS, int BLOCK>
 __device__ __forceinline__ void run_tile(const TierArgs& ta, uint64_t tile) {
     constexpr uint64_t kWaveGroups = 128;
     __shared__ uint64_t bits[2][8];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const uint64_t wchunk = tile * (kWaveGroups * (kBlock / 64)) + (uint64_t)wave * kWaveGroups;
+    const uint64_t wchunk = tile * (kWaveGroups * (BLOCK / 64)) + (uint64_t)wave * kWaveGroups;
     const bool commit_mode = ta.t.mode == RH_MODE_COMMIT;
     if (wchunk < ta.t.n) {
         const bool full = wchunk + kWaveGroups <= ta.t.n && ta.vec_ok;
@@ -267,7 +271,7 @@ __device__ __forceinline__ void run_tile(const TierArgs& ta, uint64_t tile) {
             compute_store_sub<F, false, RANK>(ta, wchunk, commit_mode, st, bits);
         }
     }
-    if (RH_COMMIT_BITS_DIRECT || (!ta.t.valid_bits && !ta.t.advanced_bits)) return;  // block-uniform
+    if (RH_COMMIT_BITS_DIRECT || BLOCK != 256 || (!ta.t.valid_bits && !ta.t.advanced_bits)) return;  // block-uniform
     __syncthreads();
     if (threadIdx.x < 16) {
         const int col = threadIdx.x >> 3, k = threadIdx.x & 7;
@@ -277,12 +281,12 @@ __device__ __forceinline__ void run_tile(const TierArgs& ta, uint64_t tile) {
     }
 }
 
-template <int F, int FHI, bool RANK, bool NT, bool NTS>
+template <int F, int FHI, bool RANK, bool NT, bool NTS, int BLOCK>
 __device__ __forceinline__ void dispatch_f(const TierArgs& ta, uint64_t tile) {
     if (ta.t.n_followers == F)
-        run_tile<F, RANK, NT, NTS>(ta, tile);
+        run_tile<F, RANK, NT, NTS, BLOCK>(ta, tile);
     else if constexpr (F < FHI)
-        dispatch_f<F + 1, FHI, RANK, NT, NTS>(ta, tile);
+        dispatch_f<F + 1, FHI, RANK, NT, NTS, BLOCK>(ta, tile);
 }
 
 __device__ __forceinline__ int tier_of_block(const LaunchArgs& args, uint32_t b) {
@@ -303,7 +307,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RH_COMMI
     const LaunchArgs& args = rh::kernarg_struct<LaunchArgs>();  // scalar loads, no scratch copy
     const int ti = tier_of_block(args, blockIdx.x);
     const TierArgs& ta = args.tier[ti];
-    dispatch_f<1, 6, true, true, RH_COMMIT_NTS>(ta, (uint64_t)(blockIdx.x - ta.block_begin));
+    dispatch_f<1, 6, true, true, RH_COMMIT_NTS, kBlock>(ta, (uint64_t)(blockIdx.x - ta.block_begin));
 }
 
 // Tiers with F = 7..14 (8..15 voters): a Batcher network per conf (rank masks of 8+ values do
@@ -312,7 +316,7 @@ __global__ __launch_bounds__(kBlock) void commit_kernel_net(const LaunchArgs a) 
     const LaunchArgs& args = rh::kernarg_struct<LaunchArgs>();
     const int ti = tier_of_block(args, blockIdx.x);
     const TierArgs& ta = args.tier[ti];
-    dispatch_f<7, 14, false, false, false>(ta, (uint64_t)(blockIdx.x - ta.block_begin));
+    dispatch_f<7, 14, false, false, false, kBlock>(ta, (uint64_t)(blockIdx.x - ta.block_begin));
 }
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
@@ -320,8 +324,9 @@ bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) ==
 // Kernel arguments for the tiers whose F lies in [flo, fhi].  Blocks go to the widest tiers first:
 // a joint-consensus tier (two confs, 7 voters) costs several times a stable tier's compute per
 // group, and its blocks dispatched last were the launch's tail (config 3: 17.2 -> 16.1 us).
-void build_args(const rh_commit_soa* tiers, int n_tiers, int flo, int fhi, LaunchArgs& args, uint64_t& blocks) {
-    constexpr uint64_t kTile = (uint64_t)kBlock * kGroupsPerLane;  // groups per workgroup
+void build_args(const rh_commit_soa* tiers, int n_tiers, int flo, int fhi, LaunchArgs& args, uint64_t& blocks,
+                int block = kBlock) {
+    const uint64_t kTile = (uint64_t)block * kGroupsPerLane;  // groups per workgroup
     args = LaunchArgs{};
     blocks = 0;
     int order[RH_MAX_TIERS];
@@ -380,13 +385,13 @@ struct LeaderArgs {
     uint32_t commit_blocks;
 };
 
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RH_COMMIT_WAVES, 8))) void leader_kernel(const LeaderArgs arg) {
+__global__ __launch_bounds__(kLeaderBlock) __attribute__((amdgpu_waves_per_eu(RH_COMMIT_WAVES, 8))) void leader_kernel(const LeaderArgs arg) {
     const LeaderArgs& a = rh::kernarg_struct<LeaderArgs>();
     const uint32_t b = blockIdx.x;
     if (b < a.commit_blocks) {
         const int ti = tier_of_block(a.commit, b);
         const TierArgs& ta = a.commit.tier[ti];
-        dispatch_f<1, 6, true, true, RH_COMMIT_NTS>(ta, (uint64_t)(b - ta.block_begin));
+        dispatch_f<1, 6, true, true, RH_COMMIT_NTS, kLeaderBlock>(ta, (uint64_t)(b - ta.block_begin));
     } else {
         rh_lease::lease_block(a.lease, (uint64_t)(b - a.commit_blocks));
     }
@@ -437,12 +442,12 @@ int rh_leader_launch_impl(rh_ctx* ctx, const rh_commit_soa* commit, int n_commit
     if (rc != RH_OK) return rc;
     LeaderArgs a;
     uint64_t cb = 0, lb = 0;
-    build_args(commit, n_commit, 1, 6, a.commit, cb);
+    build_args(commit, n_commit, 1, 6, a.commit, cb, kLeaderBlock);
     rh_lease::build_lease_args(lease, n_lease, 0, 7, a.lease, lb);
     if (cb + lb > 0x7FFFFFFFull) return rh::fail(RH_E_RANGE, "rh_leader_soa_launch: too many groups");
     a.commit_blocks = (uint32_t)cb;
     if (cb + lb) {
-        hipLaunchKernelGGL(leader_kernel, dim3((uint32_t)(cb + lb)), dim3(kBlock), 0, stream, a);
+        hipLaunchKernelGGL(leader_kernel, dim3((uint32_t)(cb + lb)), dim3(kLeaderBlock), 0, stream, a);
         RH_HIP(hipGetLastError());
     }
     // tiers outside the fused kernel's classes: their own launches (same stream, same results)
