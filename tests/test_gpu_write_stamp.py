@@ -120,7 +120,8 @@ def test_stamp_plan_boundaries(ctx, orc, case):
 
 
 @pytest.mark.parametrize("case", ["16k", "64k_unaligned", "1m_groups", "tiny_entries", "1024_frames", "1025_frames",
-                                  "shuffled_with_gaps", "long_frame_fallback", "8m_over_groups"])
+                                  "shuffled_with_gaps", "long_frame_fallback", "8m_over_groups", "max_payloads",
+                                  "ends_at_registration_end"])
 def test_stamp_zero_copy_registered(ctx, orc, case):
     """The zero-copy plan (rh_api.cpp stamp_zero_copy, rh_internal.h StampArgs): a registered buffer,
     payloads under 16 KiB, at most 96 workgroups of 64 KiB span / 1024 windows / 1024 frames.  Frames
@@ -151,12 +152,18 @@ def test_stamp_zero_copy_registered(ctx, orc, case):
         gap = 40
     elif case == "long_frame_fallback":
         sizes = np.append(rng.integers(0, 700, 50), 20 << 10)
+    elif case == "max_payloads":   # payloads just under 16 KiB: 256 windows, every shift map staged
+        sizes = np.append(rng.integers(16300, 16378, 12), rng.integers(0, 100, 30))
+        rng.shuffle(sizes)
+    elif case == "ends_at_registration_end":
+        sizes = rng.integers(1, 3000, 40)
     else:
         sizes = rng.integers(64, 2048, 8000)
     want, buf, off, ln = _frames(orc, rng, sizes, gap=gap)
     lead = int(rng.integers(1, 16))   # the batch starts off a 16-byte boundary of the registration
-    want = np.concatenate([np.full(lead, 0xC3, np.uint8), want, np.full(21, 0x3C, np.uint8)])
-    buf = np.concatenate([np.full(lead, 0xC3, np.uint8), buf, np.full(21, 0x3C, np.uint8)])
+    tail = 0 if case == "ends_at_registration_end" else 21   # (or ends exactly where it ends)
+    want = np.concatenate([np.full(lead, 0xC3, np.uint8), want, np.full(tail, 0x3C, np.uint8)])
+    buf = np.concatenate([np.full(lead, 0xC3, np.uint8), buf, np.full(tail, 0x3C, np.uint8)])
     off = off + np.uint64(lead)
     if case == "shuffled_with_gaps":
         p = rng.permutation(off.size)
