@@ -649,15 +649,21 @@ def table_commit_leg(ctx, host, reps: int = 8, fracs=(1.0, 0.1, 0.01), pmc=None)
             res["watch_all"] = int(a.watch_all_slots.size)
         med = {key: float(np.median(v)) for key, v in res.items() if isinstance(key, tuple)}
         eval_ms = float(np.median(res[(_lib.RH_EVENTS_AUTO, "eval")]))   # the module's sink
-        # algorithmic bytes: 1 dirty byte per row; per dirty row its columns (F matchIndex, conf,
-        # row slot, commit, flush, term start, previous watch-ALL level) and the flag clear; per
-        # event 16 B of record (+ 8 B commit / watch level and 1 B watch-dirty flag stored)
+        # algorithmic bytes of the evaluation kernel: 1 dirty byte per row; per dirty row its
+        # columns (F matchIndex, conf, row slot, commit, flush, term start, previous watch-ALL level)
+        # and the flag clear; per event the 8 B commit / watch level and (advanced) the 1 B
+        # watch-dirty flag it stores, and -- list mode only -- the 16 B record it writes (a tile
+        # evaluation into AUTO writes 1 bit per row instead: rh_table_gather_commit builds the
+        # records from the table on the side stream)
         n_f4 = host[0].n
         f_mean = (n_f4 * F[0] + (n_all - n_f4) * (F[1] if len(F) > 1 else F[0])) / n_all
         per_dirty = 8 * f_mean + 4 + 4 + 8 + 8 + 8 + 8 + 1
-        alg = n_all * 1 + k * per_dirty + res["advanced"] * (16 + 8 + 1) + res["watch_all"] * (16 + 8)
-        ach = alg / (eval_ms * 1e-3) / 1e9
         list_mode = bool(np.all(res[(_lib.RH_EVENTS_AUTO, "list")]))
+        rec = 16 if list_mode else 0
+        alg = n_all * 1 + k * per_dirty + res["advanced"] * (rec + 8 + 1) + res["watch_all"] * (rec + 8)
+        if not list_mode:
+            alg += n_all / 4   # the event masks: 2 bits per row
+        ach = alg / (eval_ms * 1e-3) / 1e9
         case = {"dirty_groups": k, "advanced": res["advanced"], "watch_all_changed": res["watch_all"],
                 "ms_evaluation": round(eval_ms, 4), "list_mode": list_mode,
                 "sinks_agree": res["sinks_agree"]}
@@ -668,7 +674,7 @@ def table_commit_leg(ctx, host, reps: int = 8, fracs=(1.0, 0.1, 0.01), pmc=None)
                             "frac": round(ach / HBM_PEAK_GBPS, 4), "algorithmic_bytes_per_launch": int(alg),
                             "kernel": ("table_list_kernel<false>" if list_mode else "table_commit_kernel_rank<false>")
                             + (" (RH_EVENTS_AUTO: records into the pinned lists)" if list_mode
-                               else " (RH_EVENTS_AUTO: records into the HBM lists)"),
+                               else " (RH_EVENTS_AUTO: event masks; records rebuilt from the table by the gather)"),
                             # PMC passes (scripts/prof_kernels.py table case) run the all-dirty step
                             "traffic": (round(pmc["table_bytes_per_unit"] * n_all)
                                         if frac >= 1.0 and pmc and "table_bytes_per_unit" in pmc else None),

@@ -121,6 +121,12 @@ struct rh_groups {
     hipStream_t d2h_stream = nullptr;        // the result lists' way to the host: RH_EVENTS_DEVICE's D2H in
                                              // _wait, RH_EVENTS_AUTO's drain kernel after the evaluation
     hipEvent_t evaluated = nullptr;          // recorded after an evaluation: orders the drain behind it
+    // REGION-mode updateCommit records are rebuilt from the table's row-slot / commit / watch-ALL
+    // columns by rh_table_gather_commit on d2h_stream: every later launch that writes those columns
+    // (an updateCommit evaluation, control ops, a delta batch, a load, a tier's move) is ordered
+    // after it (gather_fence)
+    hipEvent_t gathered = nullptr;
+    bool gather_pending = false;
     uint64_t* d_lbits = nullptr;  // rh_lease_batch: slot bitmap (device) and its pinned copy
     uint64_t* h_lbits = nullptr;
     // events (rh_internal.h, TableEvents): the evaluation counter words, result sets
@@ -223,8 +229,17 @@ void free_groups(rh_groups* g) {
     if (g->copy_stream) (void)hipStreamDestroy(g->copy_stream);
     if (g->d2h_stream) (void)hipStreamDestroy(g->d2h_stream);
     if (g->evaluated) (void)hipEventDestroy(g->evaluated);
+    if (g->gathered) (void)hipEventDestroy(g->gathered);
     (void)hipFree(g->d_lbits);
     if (g->h_lbits) (void)hipHostFree(g->h_lbits);
+}
+
+// Orders the table stream's next launch after the last updateCommit record gather (see `gathered`).
+int gather_fence(rh_groups* g) {
+    if (!g->gather_pending) return RH_OK;
+    RH_HIP(hipStreamWaitEvent(g->ctx->stream, g->gathered, 0));
+    g->gather_pending = false;
+    return RH_OK;
 }
 
 // (Re)allocates tier t with `rows` rows (a multiple of 128), keeping the old rows' contents: tiles
@@ -255,6 +270,7 @@ int grow_tier(rh_groups* g, int t, uint32_t rows) {
     if (e == hipSuccess) e = hipMemsetAsync(n.shadow, 0, (size_t)tiles * TB, s);
     if (e == hipSuccess) rc = rh_table_init_tiles(n, keep, tiles - keep, s);
     if (e == hipSuccess && rc == RH_OK) e = hipStreamSynchronize(s);
+    if (e == hipSuccess && rc == RH_OK) e = hipStreamSynchronize(g->d2h_stream);   // a gather may read the old tiles
     if (e != hipSuccess || rc != RH_OK) {
         free_tier(n);
         return rc != RH_OK ? rc : rh::hip_fail(e, "rh_groups: tier growth");
@@ -308,7 +324,9 @@ int flush_ops(rh_groups* g) {
         RH_HIP(hipMemcpyAsync(g->d_ops, g->h_ops, n * sizeof(CtrlOp), hipMemcpyHostToDevice, s));
         RH_HIP(hipEventRecord(g->ops_free, s));
         g->ops_used = true;
-        int rc = rh_table_control(g->dev, g->d_ops, n, s);
+        int rc = gather_fence(g);   // control ops write row slots and commit indices
+        if (rc != RH_OK) return rc;
+        rc = rh_table_control(g->dev, g->d_ops, n, s);
         if (rc != RH_OK) return rc;
         g->ops.clear();
         g->lvalid[0] = g->lvalid[1] = false;   // control ops mark rows with plain stores: no lists
@@ -385,11 +403,12 @@ struct EvTargets {
 // runs in REGION mode (rh_internal.h, TableEvents): per-workgroup regions and counts in `bdesc`, no
 // counter atomic, the lengths published by rh_table_gather; *nblocks = its workgroups (else 0).
 int evaluate(rh_groups* g, int mode, bool wall_on, const EvTargets& t, uint64_t* counts_out, uint64_t* h_counts,
-             bool* hbm, uint32_t* bdesc, uint32_t* nblocks) {
+             bool* hbm, uint32_t* bdesc, uint32_t* nblocks, rh::TableDev* ed_out = nullptr) {
     hipStream_t s = g->ctx->stream;
     *hbm = false;
     *nblocks = 0;
     int rc = flush_ops(g);
+    if (rc == RH_OK && mode != RH_MODE_WATCH) rc = gather_fence(g);   // it rewrites commit / watch-ALL values
     if (rc != RH_OK) return rc;
     const uint32_t blocks = rh::table_commit_blocks(g->dev);
     if (blocks == 0) {   // no tier has rows: nothing can be dirty
@@ -434,6 +453,7 @@ int evaluate(rh_groups* g, int mode, bool wall_on, const EvTargets& t, uint64_t*
             ev.bdesc = bdesc;
             ev.cap = hbm_records(g->capacity);
             *nblocks = nb;
+            if (ed_out) *ed_out = ed;
         }
         // a quarter of the rows or more possibly dirty: the loads go out with the flag loads
         rc = rh_table_commit(ed, mode, ev, g->marks[m] * 4 >= rows, s, t0, t1);
@@ -485,6 +505,8 @@ int ring_submit(rh_groups* g, int i, size_t n, bool has_set) {
     RH_HIP(hipMemcpyAsync(g->d_ring[i], g->h_ring[i], n * sizeof(rh_delta), hipMemcpyHostToDevice, cs));
     RH_HIP(hipEventRecord(g->ring_free[i], cs));
     RH_HIP(hipStreamWaitEvent(s, g->ring_free[i], 0));
+    rc = gather_fence(g);   // RH_COL_COMMITTED deltas write the commit column
+    if (rc != RH_OK) return rc;
     g->ring_used[i] = true;
     g->ring_next = i ^ 1;
     // every delta marks at most one row per kind
@@ -596,6 +618,8 @@ RH_EXPORT int rh_groups_create(rh_ctx* ctx, uint64_t capacity, int64_t gap_thres
         rc = rh::fail(RH_E_DEVICE, "rh_groups_create: result copy stream");
     if (rc == RH_OK && hipEventCreateWithFlags(&g->evaluated, hipEventDisableTiming) != hipSuccess)
         rc = rh::fail(RH_E_DEVICE, "rh_groups_create: evaluation event");
+    if (rc == RH_OK && hipEventCreateWithFlags(&g->gathered, hipEventDisableTiming) != hipSuccess)
+        rc = rh::fail(RH_E_DEVICE, "rh_groups_create: gather event");
     if (rc == RH_OK && hipStreamCreateWithFlags(&g->copy_stream, hipStreamNonBlocking) != hipSuccess)
         rc = rh::fail(RH_E_DEVICE, "rh_groups_create: copy stream");
     for (int i = 0; i < 2 && rc == RH_OK; ++i) {
@@ -890,7 +914,9 @@ RH_EXPORT int rh_groups_load(rh_groups* g, uint32_t first, uint32_t n, uint32_t 
             e = hipMemcpyAsync(d_rows, rows.data(), m * 4, hipMemcpyHostToDevice, s);
             if (e == hipSuccess) e = hipMemcpyAsync(d_slots, slots.data(), m * 4, hipMemcpyHostToDevice, s);
             if (e == hipSuccess) e = hipMemcpyAsync(d_cols, cols.data(), cols.size() * 8, hipMemcpyHostToDevice, s);
+            if (e == hipSuccess) e = g->gather_pending ? hipStreamWaitEvent(s, g->gathered, 0) : hipSuccess;
             if (e == hipSuccess) {
+                g->gather_pending = false;
                 hipLaunchKernelGGL(table_load_kernel, dim3((m + 255) / 256), dim3(256), 0, s, g->dev, t, d_rows, d_slots,
                                    d_cols, m);
                 e = hipGetLastError();
@@ -1049,15 +1075,24 @@ RH_EXPORT int rh_commit_batch_async(rh_groups* g, uint32_t flags, uint64_t* tick
     t.adv[0] = e.d_adv, t.adv[1] = e.hbm_adv;
     t.wall[0] = e.d_wall, t.wall[1] = e.hbm_wall;
     bool hbm = false;
-    rc = evaluate(g, RH_MODE_COMMIT, wall_on, t, e.d_cnt, e.h_cnt, &hbm, e.bdesc, &e.nblocks);
+    rh::TableDev ed;
+    rc = evaluate(g, RH_MODE_COMMIT, wall_on, t, e.d_cnt, e.h_cnt, &hbm, e.bdesc, &e.nblocks, &ed);
     if (rc != RH_OK) return rc;
-    if (hbm && g->event_sink == RH_EVENTS_AUTO) {   // packed into the pinned lists on the side stream
+    if (hbm && e.nblocks) {   // REGION mode (DEVICE and AUTO): the records rebuilt into the pinned lists
         RH_HIP(hipEventRecord(g->evaluated, g->ctx->stream));
         RH_HIP(hipStreamWaitEvent(g->d2h_stream, g->evaluated, 0));
-        rc = e.nblocks ? rh_table_gather(e.bdesc, e.nblocks, e.hbm_adv, e.d_adv, wall_on ? e.hbm_wall : nullptr,
-                                         e.d_wall, 16, e.d_cnt, g->d2h_stream)
-                       : rh_table_drain(e.d_cnt, e.hbm_adv, e.d_adv, wall_on ? e.hbm_wall : nullptr, e.d_wall, 16,
-                                        g->capacity, g->d2h_stream);
+        rc = rh_table_gather_commit(ed, e.bdesc, e.nblocks, e.d_adv, wall_on ? e.d_wall : nullptr, e.d_cnt,
+                                    g->d2h_stream);
+        if (rc != RH_OK) return rc;
+        RH_HIP(hipEventRecord(e.done, g->d2h_stream));
+        RH_HIP(hipEventRecord(g->gathered, g->d2h_stream));
+        g->gather_pending = true;
+        hbm = false;   // nothing left for _wait to copy
+    } else if (hbm && g->event_sink == RH_EVENTS_AUTO) {   // contiguous HBM lists: drained on the side stream
+        RH_HIP(hipEventRecord(g->evaluated, g->ctx->stream));
+        RH_HIP(hipStreamWaitEvent(g->d2h_stream, g->evaluated, 0));
+        rc = rh_table_drain(e.d_cnt, e.hbm_adv, e.d_adv, wall_on ? e.hbm_wall : nullptr, e.d_wall, 16, g->capacity,
+                            g->d2h_stream);
         if (rc != RH_OK) return rc;
         RH_HIP(hipEventRecord(e.done, g->d2h_stream));
         hbm = false;   // nothing left for _wait to copy
@@ -1090,13 +1125,9 @@ RH_EXPORT int rh_commit_batch_wait(rh_groups* g, uint64_t ticket, rh_commit_out*
     if (e->hbm) {  // lists in HBM (DEVICE sink): into the pinned result buffers
         e->hbm = false;
         hipStream_t s = g->d2h_stream;
-        if (e->nblocks) {   // REGION mode: packed by the gather, which also publishes the lengths
-            int rc = rh_table_gather(e->bdesc, e->nblocks, e->hbm_adv, e->d_adv, e->hbm_wall, e->d_wall, 16, e->d_cnt, s);
-            if (rc != RH_OK) return rc;
-        } else {            // contiguous (a list evaluation): the counted prefixes
-            if (na) RH_HIP(hipMemcpyAsync(e->adv, e->hbm_adv, na * sizeof(rh_index_event), hipMemcpyDeviceToHost, s));
-            if (nw) RH_HIP(hipMemcpyAsync(e->wall, e->hbm_wall, nw * sizeof(rh_index_event), hipMemcpyDeviceToHost, s));
-        }
+        // contiguous lists (counter mode into HBM; REGION mode was gathered at _async): the counted prefixes
+        if (na) RH_HIP(hipMemcpyAsync(e->adv, e->hbm_adv, na * sizeof(rh_index_event), hipMemcpyDeviceToHost, s));
+        if (nw) RH_HIP(hipMemcpyAsync(e->wall, e->hbm_wall, nw * sizeof(rh_index_event), hipMemcpyDeviceToHost, s));
         RH_HIP(hipEventRecord(e->done, s));
         done = e->done;
         lk.unlock();   // the set stays this ticket's (pending) while the copy runs

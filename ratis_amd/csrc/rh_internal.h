@@ -168,13 +168,18 @@ struct TableEvents {
     int packed = 0;                    // tile kernels: the done count rides in `cnt` above the counts
     uint32_t done_target = 0;          // tile kernels: workgroups done that end the evaluation (0: not this launch)
     unsigned long long* lheads_next = nullptr;  // the other list-head set of the evaluated kind: cleared
-    // REGION mode (tile kernels writing HBM lists): no counter atomic, no LDS staging.  Workgroup gb
-    // (block_base + its block index: the evaluation's launches number their workgroups on) owns
-    // records [gb * kTableRecs, ...) of each list, its wave w the 128 from + 128 w, written there
-    // straight from registers; the workgroup stores its counts at bdesc[gb * kTableDesc]: the two
-    // totals, then each wave's two counts.  rh_table_gather then packs the regions into the result
-    // lists and publishes the lengths.  (One returning atomic per workgroup on one word, at every
-    // workgroup's end, cost the 1M-row evaluation 4.5 us.)
+    // REGION mode (tile kernels into the DEVICE / AUTO sinks): no counter atomic, no LDS staging.
+    // Workgroup gb (block_base + its block index: the evaluation's launches number their workgroups
+    // on) has descriptor gb, kTableDesc u32 at bdesc + gb * kTableDesc.  COMMIT writes no records:
+    // its descriptor is the two totals (u64: advanced | watch-ALL << 32) and per wave four u64
+    // masks (advanced rows 2L / 2L + 1, changed watch-ALL rows 2L / 2L + 1, bit L); the evaluation
+    // has stored the new commit / watch-ALL values in the table, so rh_table_gather_commit rebuilds
+    // the records from the masks and the table's columns (the host orders every later writer of
+    // those columns after it).  WATCH writes its records: wave w of workgroup gb the 128 records from
+    // (gb * kTWaves + w) * 128 of the HBM list, straight from registers; its descriptor is the two
+    // totals, then each wave's two counts (u32); rh_table_gather packs them.  (One returning atomic
+    // per workgroup on one word, at every workgroup's end, cost the 1M-row evaluation 4.5 us; the
+    // COMMIT records themselves 1.6 us of the 19.3.)
     uint32_t* bdesc = nullptr;
     uint32_t block_base = 0;
 };
@@ -184,7 +189,7 @@ struct TableEvents {
 #define RH_TABLE_BLOCK_WAVES 2
 #endif
 constexpr uint32_t kTableRecs = RH_TABLE_BLOCK_WAVES * 128;
-constexpr uint32_t kTableDesc = 2 + 2 * RH_TABLE_BLOCK_WAVES;
+constexpr uint32_t kTableDesc = 2 + 8 * RH_TABLE_BLOCK_WAVES;   // u32: COMMIT's u64 totals + 4 u64 masks per wave
 // DIRTY-ROW LISTS (list mode).  While the host knows that few rows can be dirty (the deltas and
 // control ops since the last evaluation of a kind bound the rows they can mark), every 0 -> 1
 // transition of a row's dirty / wdirty flag (found with a 32-bit atomicOr on the flag's word) also
@@ -273,6 +278,13 @@ int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev, 
 // b_out (device pointers of the pinned lists) and writes the two lengths to counts_out (host-mapped).
 int rh_table_gather(const uint32_t* bdesc, uint32_t n_blocks, const void* a, void* a_out, const void* b, void* b_out,
                     uint32_t rec_bytes0, uint64_t* counts_out, hipStream_t stream);
+// REGION mode, COMMIT: the records of an evaluation (its clipped table `t`, as given to
+// rh_table_commit) rebuilt from the descriptors' masks and the table's row-slot, commit and
+// watch-ALL columns into the pinned lists adv_out / wall_out (device pointers; wall_out null: no
+// watch-ALL list), lengths to counts_out.  Nothing may write those columns between the evaluation
+// and this kernel (groups.cpp gather_fence).
+int rh_table_gather_commit(const rh::TableDev& t, const uint32_t* bdesc, uint32_t n_blocks, rh_index_event* adv_out,
+                           rh_index_event* wall_out, uint64_t* counts_out, hipStream_t stream);
 int rh_table_drain(const uint64_t* counts, const void* a, void* a_out, const void* b, void* b_out, uint32_t rec_bytes0,
                    uint64_t cap, hipStream_t stream);
 // Initialises tiles [first_tile, n_tiles) of a tier as free rows (conf 0, row_slot kNoRow, clean).

@@ -284,17 +284,13 @@ struct TierRange {
 constexpr int kTWaves = RH_TABLE_BLOCK_WAVES;
 constexpr int kTBlock = kTWaves * 64;
 constexpr uint32_t kTRows = kTWaves * 128;   // rows per workgroup
-static_assert(kTRows <= rh::kTableRecs && 2 * kTWaves + 2 == rh::kTableDesc,
+static_assert(kTRows <= rh::kTableRecs && 2 + 8 * kTWaves == rh::kTableDesc,
               "REGION mode: a workgroup's records fit its region, its counts its descriptor");
 #ifndef RH_TABLE_NT                          // A/B: non-temporal column loads (1) or plain (0)
 #define RH_TABLE_NT 0
 #endif
 
-#ifndef RH_TABLE_EV_NT   // A/B: REGION-mode event records stored non-temporally (1) or plain (0)
-#define RH_TABLE_EV_NT 0
-#endif
-
-#ifndef RH_TABLE_ABL   // ablation only (wrong results): 2 = no events, 3 = no table stores, 4 = trivial arithmetic, 5 = REGION-mode counts without the record stores
+#ifndef RH_TABLE_ABL   // ablation only (wrong results): 2 = no events, 3 = no table stores, 4 = trivial arithmetic
 #define RH_TABLE_ABL 0
 #endif
 
@@ -308,6 +304,7 @@ __device__ __forceinline__ V tload(const uint8_t* p) {
 // advanced commit (COMMIT) / changed levels (WATCH), kind 1 = changed watch-ALL level (COMMIT)), so
 // a wave writes its records as soon as it has them and keeps nothing live across the barrier.
 struct Stage {
+    unsigned long long mask[kTWaves][4];   // REGION mode, COMMIT: each wave's event masks (zero: none)
     uint32_t cnt[2][kTWaves];
     uint32_t pre[2][kTWaves + 1];  // exclusive prefix of cnt over the waves
     unsigned long long base;        // the block's first record in list 0 (REGION mode: in both lists)
@@ -460,24 +457,16 @@ __device__ __forceinline__ void table_wave(const TableDev& T, const TableTier& t
             for (int g = 0; g < 2; ++g)
                 if (e0[g]) ev.watch[rg + p++] = rh_watch_event{slot[g], valid[g], x0[g], x1[g], x2[g]};
         } else {
+            // no records: the wave's masks (the values are in the table, rh_table_gather_commit),
+            // staged in LDS: a wave that returned early (clean tile) leaves the block's zeros
             const uint64_t c0 = __ballot(e1[0]), c1 = __ballot(e1[1]);
-            uint32_t q = (uint32_t)(__popcll(c0 & lt) + __popcll(c1 & lt));
-#pragma unroll
-            for (int g = 0; g < 2; ++g) {
-                if (RH_TABLE_EV_NT) {
-                    typedef uint32_t v4u32 __attribute__((ext_vector_type(4)));
-                    if (e0[g])
-                        __builtin_nontemporal_store(v4u32{slot[g], 0u, (uint32_t)x0[g], (uint32_t)((uint64_t)x0[g] >> 32)},
-                                                    reinterpret_cast<v4u32*>(ev.adv + rg + p++));
-                    if (e1[g])
-                        __builtin_nontemporal_store(v4u32{slot[g], 0u, (uint32_t)x1[g], (uint32_t)((uint64_t)x1[g] >> 32)},
-                                                    reinterpret_cast<v4u32*>(ev.wall + rg + q++));
-                } else if (RH_TABLE_ABL != 5) {
-                    if (e0[g]) ev.adv[rg + p++] = rh_index_event{slot[g], 0u, x0[g]};
-                    if (e1[g]) ev.wall[rg + q++] = rh_index_event{slot[g], 0u, x1[g]};
-                }
+            if (lane == 0) {
+                sc.mask[wave][0] = a0;
+                sc.mask[wave][1] = a1;
+                sc.mask[wave][2] = c0;
+                sc.mask[wave][3] = c1;
+                sc.cnt[1][wave] = (uint32_t)(__popcll(c0) + __popcll(c1));
             }
-            if (lane == 0) sc.cnt[1][wave] = (uint32_t)(__popcll(c0) + __popcll(c1));
         }
     } else if (WATCH) {
         rh_watch_event* sw = reinterpret_cast<rh_watch_event*>(stage) + wave * 128;
@@ -549,6 +538,7 @@ __device__ __forceinline__ void table_block_iter(const TableDev& T, const TierRa
     const int t = tr.tier[i];
     const uint64_t tl = (uint64_t)(b - tr.block_begin[i]) * kTWaves + wave;   // tile of this wave
     if (threadIdx.x < 2 * kTWaves) (&sc.cnt[0][0])[threadIdx.x] = 0u;
+    if (threadIdx.x < 4 * kTWaves) (&sc.mask[0][0])[threadIdx.x] = 0ull;
     if (b == 0 && threadIdx.x < rh::kHeads && ev.lheads_next)
         ev.lheads_next[threadIdx.x * rh::kHeadStride] = 0ull;  // the next list set of this kind
     __syncthreads();
@@ -557,9 +547,21 @@ __device__ __forceinline__ void table_block_iter(const TableDev& T, const TierRa
         table_dispatch<FLO, FHI, FLO <= 6, WATCH, SPEC>(T, t, tl, wall_on, stage, sc, ev, gb);
     __syncthreads();
 
+    if (ev.bdesc && !WATCH) {   // ---- REGION mode, COMMIT: the descriptor: totals, the waves' masks
+        uint64_t* md = reinterpret_cast<uint64_t*>(ev.bdesc) + gb * (rh::kTableDesc / 2);
+        if (threadIdx.x == 0) {
+            uint64_t v0 = 0, v1 = 0;
+#pragma unroll
+            for (int w = 0; w < kTWaves; ++w) v0 += sc.cnt[0][w], v1 += sc.cnt[1][w];
+            md[0] = v0 | v1 << 32;
+        } else if (threadIdx.x <= 4 * kTWaves) {
+            md[threadIdx.x] = (&sc.mask[0][0])[threadIdx.x - 1];
+        }
+        return;
+    }
     if (ev.bdesc) {
-        // ---- REGION mode: the waves wrote their records into their own 128-record parts of the
-        // block's region; the block's counts (totals, then per wave) go to bdesc for the gather
+        // ---- REGION mode, WATCH: the waves wrote their records into their own 128-record parts of
+        // the block's region; the block's counts (totals, then per wave) go to bdesc for the gather
         if (threadIdx.x < 2 * kTWaves + 2) {
             const uint32_t k = threadIdx.x;
             uint32_t v;
@@ -968,6 +970,21 @@ static uint32_t class_blocks(const rh::TableDev& t, int cls) {
 
 uint32_t rh::table_commit_blocks(const rh::TableDev& t) { return class_blocks(t, 0) + class_blocks(t, 1); }
 
+// The block -> tier map of width class cls's evaluation launch (widest tier first); its blocks.
+static uint32_t tier_range(const rh::TableDev& t, int cls, TierRange& tr) {
+    tr = TierRange{};
+    uint32_t blocks = 0;
+    for (int i = rh::kTableTiers - 1; i >= 0; --i) {
+        const bool in_cls = cls == 0 ? i <= 2 : i >= 3;
+        if (!in_cls || !t.tier[i].rows) continue;
+        tr.block_begin[tr.n_slots] = blocks;
+        tr.tier[tr.n_slots++] = (int8_t)i;
+        blocks += (t.tier[i].rows + kTRows - 1) / kTRows;
+    }
+    for (int s = tr.n_slots; s <= rh::kTableTiers; ++s) tr.block_begin[s] = blocks;
+    return blocks;
+}
+
 // Evaluation launches.  With timing events (rh_groups_timing) hipExtLaunchKernel stamps them at
 // the dispatch's own start and completion (the kernel boundaries rocprof reports), not as separate
 // stream packets around it: t0 on the evaluation's first launch, t1 on its last.
@@ -991,15 +1008,7 @@ int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev_i
     ev.packed = 2 * ev.cbits < 64 && (uint64_t)total < (1ull << (64 - 2 * ev.cbits)) ? 1 : 0;
     for (int cls = 0; cls < 2; ++cls) {
         TierRange tr{};
-        uint32_t blocks = 0;
-        for (int i = rh::kTableTiers - 1; i >= 0; --i) {
-            const bool in_cls = cls == 0 ? i <= 2 : i >= 3;
-            if (!in_cls || !t.tier[i].rows) continue;
-            tr.block_begin[tr.n_slots] = blocks;
-            tr.tier[tr.n_slots++] = (int8_t)i;
-            blocks += (t.tier[i].rows + kTRows - 1) / kTRows;
-        }
-        for (int s = tr.n_slots; s <= rh::kTableTiers; ++s) tr.block_begin[s] = blocks;
+        const uint32_t blocks = tier_range(t, cls, tr);
         if (blocks == 0) continue;
         ev.done_target = cls == last_cls ? total : 0u;   // workgroups of both launches count
         ev.block_base = cls == 0 ? 0u : class_blocks(t, 0);   // REGION mode: workgroup numbering
@@ -1149,6 +1158,128 @@ int rh_table_gather(const uint32_t* bdesc, uint32_t n_blocks, const void* a, voi
     hipLaunchKernelGGL(table_gather_kernel, dim3((n_blocks + kGatherWGs - 1) / kGatherWGs), dim3(256), 0, stream, bdesc,
                        n_blocks, static_cast<const uint4*>(a), static_cast<uint4*>(a_out), static_cast<const uint4*>(b),
                        static_cast<uint4*>(b_out), rec_bytes0 / 16u, counts_out);
+    RH_HIP(hipGetLastError());
+    return RH_OK;
+}
+
+// ---- REGION mode, updateCommit: the records rebuilt from the masks and the table -----------------
+// As table_gather_kernel (offsets from the totals before the gather workgroup's first evaluation
+// workgroup, its parts' counts -- popcounts of the masks -- scanned in LDS), then each wave takes
+// parts round robin: the part's tile (its launch, tier slot and tile, as the evaluation's block
+// map), lane L the rows 2L, 2L + 1: their row slots and, per list, the commit or watch-ALL value
+// the evaluation stored -- one coalesced load per column per wave -- written in row order.
+struct GatherCommitArgs {
+    TableDev t;             // the evaluation's (clipped) table
+    TierRange tr[2];        // its launches' block -> tier maps
+    uint32_t cls1_base;     // the second launch's first workgroup number
+    uint32_t n_blocks;
+    const uint64_t* desc;   // per workgroup: totals (advanced | watch-ALL << 32), per wave a0 a1 c0 c1
+    rh_index_event* adv;
+    rh_index_event* wall;   // null: no watch-ALL list
+    uint64_t* counts_out;
+};
+
+__global__ __launch_bounds__(256) void table_gather_commit_kernel(GatherCommitArgs arg) {
+    (void)arg;
+    const GatherCommitArgs& A = rh::kernarg_struct<GatherCommitArgs>();
+    constexpr uint32_t S = rh::kTableDesc / 2;   // u64 per descriptor
+    __shared__ unsigned long long red[2][256 / 64];
+    __shared__ uint32_t pre[2][kGatherChunks + 1];
+    const uint32_t first = blockIdx.x * kGatherWGs;
+    const uint32_t upto = blockIdx.x == 0 ? A.n_blocks : first;   // gather workgroup 0 sums them all
+    unsigned long long s0 = 0, s1 = 0;
+    for (uint32_t j = threadIdx.x; j < upto; j += blockDim.x) {
+        const uint64_t v = A.desc[(uint64_t)j * S];
+        s0 += (uint32_t)v;
+        s1 += v >> 32;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        s0 += __shfl_down(s0, o);
+        s1 += __shfl_down(s1, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        red[0][threadIdx.x >> 6] = s0;
+        red[1][threadIdx.x >> 6] = s1;
+    }
+    for (uint32_t c = threadIdx.x; c < kGatherChunks; c += blockDim.x) {   // the parts' counts
+        const uint32_t gb = first + c / kTWaves, w = c % kTWaves;
+        uint32_t n0 = 0, n1 = 0;
+        if (gb < A.n_blocks) {
+            const uint64_t* m = A.desc + (uint64_t)gb * S + 1 + 4 * w;
+            n0 = (uint32_t)(__popcll(m[0]) + __popcll(m[1]));
+            n1 = A.wall ? (uint32_t)(__popcll(m[2]) + __popcll(m[3])) : 0u;
+        }
+        pre[0][c + 1] = n0;
+        pre[1][c + 1] = n1;
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {   // exclusive scan of one list's part counts
+        uint32_t* p = pre[threadIdx.x];
+        p[0] = 0;
+        for (uint32_t c = 1; c <= kGatherChunks; ++c) p[c] += p[c - 1];
+    }
+    s0 = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    s1 = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+    uint64_t p0 = s0, p1 = s1;
+    if (blockIdx.x == 0) {
+        if (threadIdx.x == 0) {
+            A.counts_out[0] = s0;
+            A.counts_out[1] = A.wall ? s1 : 0;
+        }
+        p0 = p1 = 0;
+    }
+    __syncthreads();
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    for (uint32_t c = wv; c < kGatherChunks; c += blockDim.x / 64) {
+        const uint32_t gb = first + c / kTWaves, w = c % kTWaves;
+        if (gb >= A.n_blocks) break;   // wave-uniform
+        const uint64_t* m = A.desc + (uint64_t)gb * S + 1 + 4 * w;
+        const uint64_t a0 = m[0], a1 = m[1], c0 = A.wall ? m[2] : 0ull, c1 = A.wall ? m[3] : 0ull;
+        if (!(a0 | a1 | c0 | c1)) continue;
+        const int cls = gb < A.cls1_base ? 0 : 1;
+        const uint32_t b = gb - (cls ? A.cls1_base : 0u);
+        const TierRange& tr = A.tr[cls];
+        int i = 0;
+#pragma unroll
+        for (int k = 1; k < rh::kTableTiers; ++k)
+            if (k < tr.n_slots && b >= tr.block_begin[k]) i = k;
+        const TableTier& tt = A.t.tier[tr.tier[i]];
+        const uint64_t tl = (uint64_t)(b - tr.block_begin[i]) * kTWaves + w;
+        const uint8_t* tb = tt.base + tl * rh::tile::bytes(tt.width);
+        const bool e00 = (a0 >> lane) & 1u, e01 = (a1 >> lane) & 1u, e10 = (c0 >> lane) & 1u, e11 = (c1 >> lane) & 1u;
+        if (!(e00 || e01 || e10 || e11)) continue;
+        const uint2 sl = *reinterpret_cast<const uint2*>(tb + rh::tile::kSlot + 8u * lane);
+        if (e00 || e01) {
+            const int64_t* cp = reinterpret_cast<const int64_t*>(tb + rh::tile::commit(tt.width)) + 2 * lane;
+            uint64_t p = p0 + pre[0][c] + (uint64_t)(__popcll(a0 & lt) + __popcll(a1 & lt));
+            if (e00) A.adv[p++] = rh_index_event{sl.x, 0u, cp[0]};
+            if (e01) A.adv[p] = rh_index_event{sl.y, 0u, cp[1]};
+        }
+        if (e10 || e11) {
+            const int64_t* wp = reinterpret_cast<const int64_t*>(tb + rh::tile::wall(tt.width)) + 2 * lane;
+            uint64_t q = p1 + pre[1][c] + (uint64_t)(__popcll(c0 & lt) + __popcll(c1 & lt));
+            if (e10) A.wall[q++] = rh_index_event{sl.x, 0u, wp[0]};
+            if (e11) A.wall[q] = rh_index_event{sl.y, 0u, wp[1]};
+        }
+    }
+}
+
+int rh_table_gather_commit(const rh::TableDev& t, const uint32_t* bdesc, uint32_t n_blocks, rh_index_event* adv_out,
+                           rh_index_event* wall_out, uint64_t* counts_out, hipStream_t stream) {
+    if (n_blocks == 0) return rh::fail(RH_E_INVAL, "rh_table_gather_commit: no workgroups");
+    GatherCommitArgs a{};
+    a.t = t;
+    const uint32_t b0 = tier_range(t, 0, a.tr[0]), b1 = tier_range(t, 1, a.tr[1]);
+    if (b0 + b1 != n_blocks) return rh::fail(RH_E_STATE, "rh_table_gather_commit: workgroups differ from the evaluation's");
+    a.cls1_base = b0;
+    a.n_blocks = n_blocks;
+    a.desc = reinterpret_cast<const uint64_t*>(bdesc);
+    a.adv = adv_out;
+    a.wall = wall_out;
+    a.counts_out = counts_out;
+    hipLaunchKernelGGL(table_gather_commit_kernel, dim3((n_blocks + kGatherWGs - 1) / kGatherWGs), dim3(256), 0, stream, a);
     RH_HIP(hipGetLastError());
     return RH_OK;
 }

@@ -87,8 +87,9 @@ def main():
         f_mean = (host[0].n * 4 + (n - host[0].n) * 6) / n
         na = sum(e[0] for e in ev) / len(ev)
         nw = sum(e[1] for e in ev) / len(ev)
-        # bench.table_commit_leg's algorithmic bytes of a 100 % step (mean over the iterations)
-        alg = n * 1 + n * (8 * f_mean + 4 + 4 + 8 + 8 + 8 + 8 + 1) + na * (16 + 8 + 1) + nw * (16 + 8)
+        # bench.table_commit_leg's algorithmic bytes of a 100 % step (a tile evaluation into AUTO:
+        # no records, 2 mask bits per row; mean over the iterations)
+        alg = n * 1 + n * (8 * f_mean + 4 + 4 + 8 + 8 + 8 + 8 + 1) + na * (8 + 1) + nw * 8 + n / 4
         print("alg_bytes", int(alg), "rows", n, "advanced", int(na), "watch_all", int(nw))
     elif a.what == "lease":
         import numpy as np
