@@ -279,16 +279,18 @@ int rh_commit_batch(rh_groups* g, uint32_t flags, rh_commit_out* out);
  * deltas during any _wait (or an _async waiting for an unread earlier result) proceed at once. */
 int rh_commit_batch_async(rh_groups* g, uint32_t flags, uint64_t* ticket);
 int rh_commit_batch_wait(rh_groups* g, uint64_t ticket, rh_commit_out* out);
-/* Where the result lists are assembled.  Every sink runs the same evaluation kernels, which write
- * their records straight into contiguous lists (one range per workgroup) and the list lengths into
- * pinned memory.  HOST_MAPPED: the lists are the pinned result buffers themselves (PCIe writes by
- * the GPU), visible when the ticket completes.  DEVICE: the lists are in HBM (112 B x capacity) and
- * rh_commit_batch_wait / rh_watch_levels_wait copy the counted prefix into the same pinned buffers
- * (a D2H on the table's copy stream).  AUTO (the default): an evaluation over every tile (up to one
- * record per row) writes HBM lists at HBM speed and a drain kernel on a side stream moves the
- * counted prefixes into the pinned buffers across PCIe while the table stream goes on (the ticket
- * completes after it; no host-issued copy); an evaluation over the dirty-row lists (few records)
- * writes the pinned buffers directly.  Results are identical.  Not while an evaluation is outstanding (RH_E_STATE). */
+/* Where the result lists are assembled.  HOST_MAPPED: the evaluation kernels write the records
+ * straight into the pinned result buffers (one range per workgroup, PCIe writes by the GPU),
+ * visible when the ticket completes.  AUTO (the default): an evaluation over every tile (up to one
+ * record per row) runs without writing records to the host -- updateCommit stores two event bits
+ * per row and a gather kernel on a side stream rebuilds the records from the table's columns,
+ * commitIndexChanged writes its records to HBM and a gather packs them -- into the pinned buffers
+ * while the table stream goes on (the ticket completes after the gather; no host-issued copy; the
+ * table's next writers of those columns are ordered after it); an evaluation over the dirty-row
+ * lists (few records) writes the pinned buffers directly.  DEVICE: as AUTO, except that lists
+ * assembled in HBM without a gather are copied into the pinned buffers by the _wait call (a D2H
+ * on the table's copy stream).  Results are identical.  Not while an evaluation is outstanding
+ * (RH_E_STATE). */
 #define RH_EVENTS_HOST_MAPPED 0
 #define RH_EVENTS_DEVICE      1
 #define RH_EVENTS_AUTO        2
