@@ -395,6 +395,13 @@ struct EvTargets {
     rh_watch_event* watch[2] = {nullptr, nullptr};
 };
 
+#ifndef RH_SPEC_DIV   // SPEC tile evaluations from marks >= rows / RH_SPEC_DIV (A/B)
+#define RH_SPEC_DIV 4
+#endif
+#ifndef RH_LIST_PINNED_MAX   // AUTO: list evaluations of fewer marked rows write the pinned lists directly (A/B)
+#define RH_LIST_PINNED_MAX 8192
+#endif
+
 // Enqueues one evaluation (mode) of the dirty rows, its events written into the lists adv / wall
 // or watch of `t` (their lengths to counts_out, host-mapped).  The sink picks the set: HOST_MAPPED
 // [0], DEVICE [1], AUTO [1] for a tile evaluation (up to every row's records: written at HBM speed,
@@ -417,7 +424,11 @@ int evaluate(rh_groups* g, int mode, bool wall_on, const EvTargets& t, uint64_t*
     }
     const int m = mode == RH_MODE_WATCH ? 1 : 0;
     const bool list = g->lvalid[m];   // every row marked since the last evaluation is listed
-    const int k = (g->event_sink == RH_EVENTS_DEVICE || (g->event_sink == RH_EVENTS_AUTO && !list)) ? 1 : 0;
+    // AUTO: HBM lists (gathered / drained on the side stream) unless a list evaluation of few rows,
+    // whose records the kernel writes across PCIe itself (at 3 % of 1M rows those writes cost the
+    // list kernel 2.7 us; at 1 % HBM measured the same or 0.3 us less: profiles/r05/table_eval/)
+    const bool few = list && g->marks[m] < RH_LIST_PINNED_MAX;
+    const int k = (g->event_sink == RH_EVENTS_DEVICE || (g->event_sink == RH_EVENTS_AUTO && !few)) ? 1 : 0;
     rh::TableEvents ev;
     ev.adv = t.adv[k];
     ev.wall = wall_on ? t.wall[k] : nullptr;
@@ -456,7 +467,7 @@ int evaluate(rh_groups* g, int mode, bool wall_on, const EvTargets& t, uint64_t*
             if (ed_out) *ed_out = ed;
         }
         // a quarter of the rows or more possibly dirty: the loads go out with the flag loads
-        rc = rh_table_commit(ed, mode, ev, g->marks[m] * 4 >= rows, s, t0, t1);
+        rc = rh_table_commit(ed, mode, ev, g->marks[m] * RH_SPEC_DIV >= rows, s, t0, t1);
     }
     if (rc == RH_OK && g->timing) g->timed = true;
     if (rc != RH_OK) {
