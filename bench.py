@@ -673,7 +673,8 @@ def table_commit_leg(ctx, host, reps: int = 8, fracs=(1.0, 0.1, 0.01), pmc=None)
         case["roofline"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                             "frac": round(ach / HBM_PEAK_GBPS, 4), "algorithmic_bytes_per_launch": int(alg),
                             "kernel": ("table_list_kernel<false>" if list_mode else "table_commit_kernel_rank<false>")
-                            + (" (RH_EVENTS_AUTO: records into the pinned lists)" if list_mode
+                            + (" (RH_EVENTS_AUTO: records into the lists -- pinned below 8192 marked rows, else HBM"
+                               " drained on the side stream)" if list_mode
                                else " (RH_EVENTS_AUTO: event masks; records rebuilt from the table by the gather)"),
                             # PMC passes (scripts/prof_kernels.py table case) run the all-dirty step
                             "traffic": (round(pmc["table_bytes_per_unit"] * n_all)
