@@ -34,7 +34,7 @@ public final class HipFrameStamper implements AutoCloseable {
   }
 
   /** Flush batches from this size on go to the GPU (bench.py write_stamp leg: crossover_bytes). */
-  public static final int DEFAULT_MIN_GPU_BYTES = 256 << 10;
+  public static final int DEFAULT_MIN_GPU_BYTES = 64 << 10;
   /** GPU failures after which the stamper stays on the CPU path. */
   static final int MAX_GPU_FAILURES = 3;
 

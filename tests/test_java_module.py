@@ -297,7 +297,7 @@ def test_writer_seam_stamps_flush_batches():
     keys = _patched_java("server/RaftServerConfigKeys.java")
     assert 'CHECKSUM_GPU_MIN_BYTES_DEFAULT = SizeInBytes.valueOf("64KB")' in keys
     stamper = open(os.path.join(JAVA, "java", "org", "apache", "ratis", "hip", "HipFrameStamper.java")).read()
-    assert "DEFAULT_MIN_GPU_BYTES = 256 << 10" in stamper
+    assert "DEFAULT_MIN_GPU_BYTES = 64 << 10" in stamper
     st = _method_body(stamper, "public boolean stamp(ByteBuffer buf, FrameChecksum cpu)")
     assert "bytes >= minGpuBytes" in st and "gpu.stampFrames(buf, buf.position(), off, len, n)" in st
     assert "cpu.crc(d)" in st
