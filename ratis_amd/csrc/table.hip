@@ -500,11 +500,16 @@ __device__ __forceinline__ void table_dispatch(const TableDev& T, int t, uint64_
 // The evaluation's counter word (rh_internal.h, TableEvents): kind 0 in bits [0, cbits), kind 1 in
 // [cbits, 2 cbits), workgroups done above when the count fits there (`packed`; the list kernel
 // always: at most kListMaxGrid workgroups < 2^8).
-#ifndef RH_LIST_WAVES   // A/B: waves per list-kernel workgroup (the grid keeps 960 waves)
-#define RH_LIST_WAVES 4
+#ifndef RH_LIST_WAVES   // A/B: waves per list-kernel workgroup
+#define RH_LIST_WAVES 2
 #endif
 constexpr uint32_t kListWaves = RH_LIST_WAVES;
-constexpr uint32_t kListMaxGrid = 960 / kListWaves;   // < 2^8 workgroups: the done count's byte
+#ifndef RH_LIST_TOTAL_WAVES   // A/B: waves of the list grid (960 before round 5: 0.1 % dirty 8.0 -> 7.5 us, 1 % unchanged)
+#define RH_LIST_TOTAL_WAVES 480
+#endif
+constexpr uint32_t kListMaxGrid = RH_LIST_TOTAL_WAVES / kListWaves;   // < 2^8 workgroups: the done count's byte
+static_assert(kListMaxGrid < 256, "the done count's byte");
+static_assert(kListWaves >= 2, "thread 64 (wave 1) stages the tier table while wave 0 does the bookkeeping");
 
 __device__ __forceinline__ void publish_counts(const TableEvents& ev, unsigned long long c) {
     const unsigned long long m = (1ull << ev.cbits) - 1;
