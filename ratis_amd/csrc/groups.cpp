@@ -235,8 +235,11 @@ void free_groups(rh_groups* g) {
 }
 
 // Orders the table stream's next launch after the last updateCommit record gather (see `gathered`).
+#ifndef RH_GATHER_FENCE   // test-sensitivity builds only (0: no fence -- wrong results)
+#define RH_GATHER_FENCE 1
+#endif
 int gather_fence(rh_groups* g) {
-    if (!g->gather_pending) return RH_OK;
+    if (!RH_GATHER_FENCE || !g->gather_pending) return RH_OK;
     RH_HIP(hipStreamWaitEvent(g->ctx->stream, g->gathered, 0));
     g->gather_pending = false;
     return RH_OK;

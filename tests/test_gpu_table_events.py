@@ -11,6 +11,8 @@ oracle's commit arithmetic):
   * evaluations whose ticket is superseded without a wait, and an evaluation after them;
   * the async forms of commitIndexChanged and hasLease (rh_watch_levels_async / _wait,
     rh_lease_batch_async / _wait), their misuse, and the node forms over 4 shards on one GPU."""
+import os
+
 import numpy as np
 import pytest
 
@@ -341,5 +343,67 @@ def test_separate_done_word_of_large_tables(ctx, orc, monkeypatch):
                 tab.push(d)
                 model.apply(d)
                 compare(tab, model, orc, columns=False)
+    finally:
+        tab.close()
+
+
+@pytest.mark.parametrize("sink", ["device", "auto"])
+def test_region_records_survive_later_writers(ctx, orc, sink):
+    """updateCommit in REGION mode writes no records: the gather rebuilds them on the side stream
+    from the table's row-slot, commit and watch-ALL columns (rh_internal.h, TableEvents), so every
+    later writer of those columns must wait for it (groups.cpp gather_fence).  A commitIndexChanged
+    evaluation with ~half a million changed levels goes first, so its record gather holds the side
+    stream (~16 MB across PCIe) and the updateCommit gather queues behind it; meanwhile the host
+    rewrites every column that gather reads -- COMMITTED deltas on the advanced rows, stops, restarts
+    with other commits, reconfigurations into another tier -- and starts a second evaluation.  Both
+    tickets' lists must be what their evaluations computed."""
+    from ratis_amd import _lib, groups
+    rng = np.random.default_rng(1234)
+    n = int(os.environ.get("RH_TEST_HAZARD_ROWS", 1_000_000))
+    model = TableModel(n)
+    tab, n = _loaded(ctx, model, n, seed=77)
+    try:
+        tab.set_event_sink({"device": _lib.RH_EVENTS_DEVICE, "auto": _lib.RH_EVENTS_AUTO}[sink])
+        compare(tab, model, orc, columns=False)
+        live = np.arange(n)
+        d = random_deltas(rng, model, live, n)   # matchIndex, flushIndex and follower commitIndex
+        tab.push(d)
+        model.apply(d)
+        expect_w = model.watch(orc)
+        expect = model.commit_batch(orc)
+        assert expect[0].size > 1000 and expect[2].size > 1000 and expect_w[0].size > 100_000
+        adv = expect[0]
+        w = groups.make_deltas(adv, np.full(adv.size, _lib.RH_COL_COMMITTED), np.full(adv.size, 1 << 50),
+                               np.full(adv.size, _lib.RH_OP_SET))
+        stable, joint = conf_word(0b1111), conf_word(0b110011, old_mask=0b1111)
+        victims = [int(s) for s in adv[:64]]
+        tab.watch_async()                        # its record gather holds the side stream
+        tk = tab.commit_async(watch_all=True)    # this one's gather queues behind it
+        tab.push(w)                              # every column that gather reads, rewritten now
+        for s in victims[:32]:
+            tab.stop(s)
+        for s in victims[:32]:
+            tab.start(s, stable, 5_000, 4_000, 3_000)
+        moved = [s for s in victims[32:] if model.conf[s] == stable]
+        for s in moved:
+            tab.reconf(s, joint, [0, 1, 2, 3, -1, -1])
+        tk2 = tab.commit_async(watch_all=True)
+        got = tab.commit_wait(tk)
+        assert np.array_equal(got.advanced_slots, expect[0]) and np.array_equal(got.advanced_commit, expect[1])
+        assert np.array_equal(got.watch_all_slots, expect[2]) and np.array_equal(got.watch_all_min, expect[3])
+        levels = tab.watch_wait()
+        assert np.array_equal(levels["slot"], expect_w[0])
+        # the model replays the same calls after the first evaluation
+        model.apply(w)
+        for s in victims[:32]:
+            model.stop(s)
+        for s in victims[:32]:
+            model.start(s, stable, 5_000, 4_000, 3_000)
+        for s in moved:
+            model.reconf(s, joint, [0, 1, 2, 3, -1, -1])
+        expect2 = model.commit_batch(orc)
+        got2 = tab.commit_wait(tk2)
+        assert np.array_equal(got2.advanced_slots, expect2[0]) and np.array_equal(got2.advanced_commit, expect2[1])
+        assert np.array_equal(got2.watch_all_slots, expect2[2]) and np.array_equal(got2.watch_all_min, expect2[3])
     finally:
         tab.close()
