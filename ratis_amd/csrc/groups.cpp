@@ -450,7 +450,7 @@ int evaluate(rh_groups* g, int mode, bool wall_on, const EvTargets& t, uint64_t*
         l.cap = g->lcap;
         // COMMIT marks the rows whose commit advanced for commitIndexChanged: at most the listed ones
         const rh::TableLists lw = m == 0 ? lists_for(g, 1, g->lmarks[0]) : rh::TableLists{};
-        rc = rh_table_commit_lists(g->dev, mode, l, lw, ev, s, t0, t1);
+        rc = rh_table_commit_lists(g->dev, mode, l, lw, ev, s, t0, t1, g->lmarks[m]);
     } else {
         if (m == 0) g->lvalid[1] = false;   // the tile kernel marks wdirty with plain stores
         // tiles at or past a tier's high-water mark hold no row ever handed out (clean): the

@@ -264,7 +264,7 @@ int rh_table_apply_deltas(const rh::TableDev& t, const rh_delta* d_deltas, uint6
 // advanced to the watch list `lw` (when it is maintained).  Events as rh_table_commit.
 // t0 / t1 (may be null): timing events stamped at the evaluation's kernel boundaries.
 int rh_table_commit_lists(const rh::TableDev& t, int mode, const rh::TableLists& l, const rh::TableLists& lw,
-                          const rh::TableEvents& ev, hipStream_t stream, hipEvent_t t0, hipEvent_t t1);
+                          const rh::TableEvents& ev, hipStream_t stream, hipEvent_t t0, hipEvent_t t1, uint64_t rows_hint);
 int rh_table_control(const rh::TableDev& t, const rh::CtrlOp* d_ops, uint64_t n, hipStream_t stream);
 // spec: issue every column load with the dirty-flag load (a large part of the table is dirty).
 int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev, bool spec, hipStream_t stream,

@@ -1036,12 +1036,24 @@ int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev_i
     return RH_OK;
 }
 
+// List grid by the marked rows (an upper bound of the listed ones): about kListRowsPerWave rows per
+// wave, between kListMinGrid and kListMaxGrid workgroups (same box, 1M rows: 240 waves 9.5-10.0 us
+// at 1 %, 7.9-8.0 at 0.3 %, but 17.5-18.5 at 3 %, where 480 waves take 14.0-15.1;
+// profiles/r05/table_eval/)
+#ifndef RH_LIST_ROWS_PER_WAVE
+#define RH_LIST_ROWS_PER_WAVE 48
+#endif
+constexpr uint32_t kListMinGrid = kListMaxGrid / 2;
+
 int rh_table_commit_lists(const rh::TableDev& t, int mode, const rh::TableLists& l, const rh::TableLists& lw,
-                          const rh::TableEvents& ev_in, hipStream_t stream, hipEvent_t t0, hipEvent_t t1) {
+                          const rh::TableEvents& ev_in, hipStream_t stream, hipEvent_t t0, hipEvent_t t1,
+                          uint64_t rows_hint) {
     // the listed rows are dealt lane-major over every wave of a near-chip-wide grid: a few rows per
     // wave on ~every CU (random rows: the chain of dependent loads is latency-bound per CU, so the
     // rows are spread, not packed into few waves)
-    const dim3 g(kListMaxGrid), b(kListWaves * 64);
+    const uint64_t want = (rows_hint + (uint64_t)RH_LIST_ROWS_PER_WAVE * kListWaves - 1) / ((uint64_t)RH_LIST_ROWS_PER_WAVE * kListWaves);
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(kListMaxGrid, std::max<uint64_t>(kListMinGrid, want));
+    const dim3 g(grid), b(kListWaves * 64);
     rh::TableEvents ev = ev_in;
     hipError_t e;
     if (mode == RH_MODE_WATCH)
