@@ -1043,7 +1043,11 @@ int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev_i
 #ifndef RH_LIST_ROWS_PER_WAVE
 #define RH_LIST_ROWS_PER_WAVE 48
 #endif
-constexpr uint32_t kListMinGrid = kListMaxGrid / 2;
+#ifndef RH_LIST_MIN_GRID
+#define RH_LIST_MIN_GRID (kListMaxGrid / 2)
+#endif
+constexpr uint32_t kListMinGrid = RH_LIST_MIN_GRID;
+static_assert(kListMinGrid >= rh::kHeads, "a workgroup per list region at least");
 
 int rh_table_commit_lists(const rh::TableDev& t, int mode, const rh::TableLists& l, const rh::TableLists& lw,
                           const rh::TableEvents& ev_in, hipStream_t stream, hipEvent_t t0, hipEvent_t t1,
