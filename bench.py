@@ -689,6 +689,89 @@ def table_commit_leg(ctx, host, reps: int = 8, fracs=(1.0, 0.1, 0.01), pmc=None)
     return out
 
 
+def table_watch_leg(ctx, host, reps: int = 8, fracs=(1.0, 0.1, 0.01)) -> dict:
+    """commitIndexChanged over the resident table (LeaderStateImpl.java:612-622, rh_watch_levels_async
+    / _wait), the other evaluation the Java pump runs every tick: the followers' commitIndex deltas
+    (FollowerInfo.updateCommitIndex, one per dirty group: follower 0..3, +512 over its current value)
+    mark `frac` of config 3's 1M groups, then one watch evaluation per step, timed at its kernel
+    boundaries (rh_groups_timing).  Two tables fed the same deltas -- AUTO (the module's sink: a
+    tile evaluation writes 2 bits per row -- changed, valid -- and rh_table_gather_watch rebuilds the
+    level records from the table on the side stream; a list evaluation writes its records) and
+    HOST_MAPPED (records across PCIe from the kernel) -- must report the same levels.  Algorithmic
+    bytes of the evaluation: 1 B watch-dirty flag per row; per dirty row 8F follower commitIndex, 8
+    commit (the self value), 24 previous levels, 4 conf, 4 row slot, 1 flag clear; per changed row
+    the 24 B of levels stored, plus the 32 B record in list mode or the masks (n / 4 B) in tile
+    mode."""
+    import torch
+
+    from ratis_amd import _lib, groups
+    rng = np.random.default_rng(11)
+    n_all = sum(h.n for h in host)
+    F = [h.follower.shape[0] for h in host]
+    tabs = {}
+    for sink in (_lib.RH_EVENTS_AUTO, _lib.RH_EVENTS_HOST_MAPPED):
+        tab = groups.RaftGroupTable(ctx, capacity=n_all)
+        first = 0
+        for h in host:
+            tab.load(first, h.conf, h.flush, h.commit, h.term_start, match=h.follower)
+            first += h.n
+        tab.set_event_sink(sink)
+        tab.set_timing(True)
+        tab.commit_wait_counts(tab.commit_async(watch_all=False))
+        tab.watch_async()
+        tab.watch_wait_count()
+        tabs[sink] = tab
+    commit = np.concatenate([h.commit for h in host])
+    cur = np.tile(commit - 2048, (4, 1))   # follower commitIndex, below the leader's (all -1 after the load)
+    stream = torch.cuda.ExternalStream(_lib.load().rh_ctx_stream(ctx.handle))
+    out = {}
+    for frac in fracs:
+        k = n_all if frac >= 1.0 else int(n_all * frac)
+        res = {"eval": [], "list": []}
+        agree, changed = True, 0
+        for r in range(reps + 1):
+            slot = rng.permutation(n_all)[:k] if k < n_all else rng.permutation(n_all)
+            col = rng.integers(0, 4, size=k)
+            val = cur[col, slot] + 512
+            cur[col, slot] = val
+            d = groups.make_deltas(slot, 16 + col, val)
+            got = {}
+            for sink, tab in tabs.items():
+                tab.push(d)
+                LEGS.push(f"twatch_{frac * 100:g}pct" if (r and sink == _lib.RH_EVENTS_AUTO) else "twatch_warmup")
+                queue_gate(stream)
+                tab.watch_async()
+                got[sink] = tab.watch_wait()
+                torch.cuda.synchronize()
+                LEGS.pop()
+                if r and sink == _lib.RH_EVENTS_AUTO:
+                    res["eval"].append(tab.last_timing())
+                    res["list"].append(tab.last_was_list())
+            a, b = got[_lib.RH_EVENTS_AUTO], got[_lib.RH_EVENTS_HOST_MAPPED]
+            agree &= bool(np.array_equal(a, b))
+            changed = int(a.size)
+        eval_ms = float(np.median(res["eval"]))
+        list_mode = bool(np.all(res["list"]))
+        n_f4 = host[0].n
+        f_mean = (n_f4 * F[0] + (n_all - n_f4) * (F[1] if len(F) > 1 else F[0])) / n_all
+        alg = n_all * 1 + k * (8 * f_mean + 8 + 24 + 4 + 4 + 1) + changed * ((32 if list_mode else 0) + 24)
+        if not list_mode:
+            alg += n_all / 4   # the event masks: 2 bits per row
+        ach = alg / (eval_ms * 1e-3) / 1e9
+        out[f"dirty_{frac * 100:g}pct"] = {
+            "dirty_groups": k, "levels_changed": changed, "ms_evaluation": round(eval_ms, 4), "list_mode": list_mode,
+            "sinks_agree": agree,
+            "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": round(ach / HBM_PEAK_GBPS, 4), "algorithmic_bytes_per_launch": int(alg),
+                         "kernel": ("table_list_kernel<true> (records into the lists)" if list_mode
+                                    else "table_commit_kernel_rank<true> (event masks; records rebuilt by the gather)")}}
+    for tab in tabs.values():
+        tab.close()
+    out["workload"] = (f"resident table of {n_all} config-3 groups; follower commitIndex deltas mark the dirty "
+                       f"fraction, then one rh_watch_levels_async / _wait per step (AUTO sink); median of {reps} steps")
+    return out
+
+
 def ragged_read_path(ctx, args, rank, stream, barrier, max_over_ranks, sum_over_ranks, pmc=None) -> dict:
     """Segments of differently sized frames (64-2048 B, seeded random payloads, 1 in 10^5 frames
     with a flipped payload bit): framing alone (the serial walk defers each segment after its first
@@ -1035,6 +1118,7 @@ def main():
         pcie["note"] = "full snapshot H2D (pinned) + kernel + commit D2H per batch"
         pcie["delta_streaming"] = delta_streaming(ctx, host, fill_threads=cpu_threads())
         pcie["delta_streaming"]["table_commit"] = table_commit_leg(ctx, host, pmc=pmc)
+        pcie["delta_streaming"]["table_watch"] = table_watch_leg(ctx, host)
         pcie["delta_streaming"]["reply_mix"] = reply_mix_leg(host, threads=cpu_threads())
         pcie["write_stamp"] = write_stamp_leg(ctx)
 

@@ -282,9 +282,9 @@ int rh_commit_batch_wait(rh_groups* g, uint64_t ticket, rh_commit_out* out);
 /* Where the result lists are assembled.  HOST_MAPPED: the evaluation kernels write the records
  * straight into the pinned result buffers (one range per workgroup, PCIe writes by the GPU),
  * visible when the ticket completes.  AUTO (the default): an evaluation over every tile (up to one
- * record per row) runs without writing records to the host -- updateCommit stores two event bits
- * per row and a gather kernel on a side stream rebuilds the records from the table's columns,
- * commitIndexChanged writes its records to HBM and a gather packs them -- into the pinned buffers
+ * record per row) runs without writing records at all -- it stores two event bits per row
+ * (updateCommit: advanced, watch-ALL changed; commitIndexChanged: changed, valid) and a gather
+ * kernel on a side stream rebuilds the records from the table's columns into the pinned buffers
  * while the table stream goes on (the ticket completes after the gather; no host-issued copy; the
  * table's next writers of those columns are ordered after it); an evaluation over the dirty-row
  * lists writes records -- into the pinned buffers directly when fewer than 8192 rows were marked,

@@ -127,6 +127,10 @@ struct rh_groups {
     // after it (gather_fence)
     hipEvent_t gathered = nullptr;
     bool gather_pending = false;
+    // the same for commitIndexChanged's records (row-slot, wmin / wmaj / wmax columns: written by a
+    // watch evaluation, control ops, a load)
+    hipEvent_t wgathered = nullptr;
+    bool wgather_pending = false;
     uint64_t* d_lbits = nullptr;  // rh_lease_batch: slot bitmap (device) and its pinned copy
     uint64_t* h_lbits = nullptr;
     // events (rh_internal.h, TableEvents): the evaluation counter words, result sets
@@ -230,6 +234,7 @@ void free_groups(rh_groups* g) {
     if (g->d2h_stream) (void)hipStreamDestroy(g->d2h_stream);
     if (g->evaluated) (void)hipEventDestroy(g->evaluated);
     if (g->gathered) (void)hipEventDestroy(g->gathered);
+    if (g->wgathered) (void)hipEventDestroy(g->wgathered);
     (void)hipFree(g->d_lbits);
     if (g->h_lbits) (void)hipHostFree(g->h_lbits);
 }
@@ -242,6 +247,14 @@ int gather_fence(rh_groups* g) {
     if (!RH_GATHER_FENCE || !g->gather_pending) return RH_OK;
     RH_HIP(hipStreamWaitEvent(g->ctx->stream, g->gathered, 0));
     g->gather_pending = false;
+    return RH_OK;
+}
+
+// The same for the last commitIndexChanged record gather (see `wgathered`).
+int wgather_fence(rh_groups* g) {
+    if (!RH_GATHER_FENCE || !g->wgather_pending) return RH_OK;
+    RH_HIP(hipStreamWaitEvent(g->ctx->stream, g->wgathered, 0));
+    g->wgather_pending = false;
     return RH_OK;
 }
 
@@ -327,7 +340,8 @@ int flush_ops(rh_groups* g) {
         RH_HIP(hipMemcpyAsync(g->d_ops, g->h_ops, n * sizeof(CtrlOp), hipMemcpyHostToDevice, s));
         RH_HIP(hipEventRecord(g->ops_free, s));
         g->ops_used = true;
-        int rc = gather_fence(g);   // control ops write row slots and commit indices
+        int rc = gather_fence(g);   // control ops write row slots, commit indices and levels
+        if (rc == RH_OK) rc = wgather_fence(g);
         if (rc != RH_OK) return rc;
         rc = rh_table_control(g->dev, g->d_ops, n, s);
         if (rc != RH_OK) return rc;
@@ -410,15 +424,16 @@ struct EvTargets {
 // [0], DEVICE [1], AUTO [1] for a tile evaluation (up to every row's records: written at HBM speed,
 // gathered into the pinned lists afterwards) and [0] for a list evaluation (few records: written
 // across PCIe by the kernel, no copy).  *hbm: whether [1] was used.  A tile evaluation into [1]
-// runs in REGION mode (rh_internal.h, TableEvents): per-workgroup regions and counts in `bdesc`, no
-// counter atomic, the lengths published by rh_table_gather; *nblocks = its workgroups (else 0).
+// runs in REGION mode (rh_internal.h, TableEvents): per-workgroup masks and totals in `bdesc`, no
+// counter atomic, no records: the caller's rh_table_gather_commit / _watch rebuilds them and
+// publishes the lengths; *nblocks = its workgroups (else 0), *ed_out its clipped table.
 int evaluate(rh_groups* g, int mode, bool wall_on, const EvTargets& t, uint64_t* counts_out, uint64_t* h_counts,
              bool* hbm, uint32_t* bdesc, uint32_t* nblocks, rh::TableDev* ed_out = nullptr) {
     hipStream_t s = g->ctx->stream;
     *hbm = false;
     *nblocks = 0;
     int rc = flush_ops(g);
-    if (rc == RH_OK && mode != RH_MODE_WATCH) rc = gather_fence(g);   // it rewrites commit / watch-ALL values
+    if (rc == RH_OK) rc = mode != RH_MODE_WATCH ? gather_fence(g) : wgather_fence(g);   // it rewrites the values a gather reads
     if (rc != RH_OK) return rc;
     const uint32_t blocks = rh::table_commit_blocks(g->dev);
     if (blocks == 0) {   // no tier has rows: nothing can be dirty
@@ -633,6 +648,8 @@ RH_EXPORT int rh_groups_create(rh_ctx* ctx, uint64_t capacity, int64_t gap_thres
     if (rc == RH_OK && hipEventCreateWithFlags(&g->evaluated, hipEventDisableTiming) != hipSuccess)
         rc = rh::fail(RH_E_DEVICE, "rh_groups_create: evaluation event");
     if (rc == RH_OK && hipEventCreateWithFlags(&g->gathered, hipEventDisableTiming) != hipSuccess)
+        rc = rh::fail(RH_E_DEVICE, "rh_groups_create: gather event");
+    if (rc == RH_OK && hipEventCreateWithFlags(&g->wgathered, hipEventDisableTiming) != hipSuccess)
         rc = rh::fail(RH_E_DEVICE, "rh_groups_create: gather event");
     if (rc == RH_OK && hipStreamCreateWithFlags(&g->copy_stream, hipStreamNonBlocking) != hipSuccess)
         rc = rh::fail(RH_E_DEVICE, "rh_groups_create: copy stream");
@@ -929,8 +946,9 @@ RH_EXPORT int rh_groups_load(rh_groups* g, uint32_t first, uint32_t n, uint32_t 
             if (e == hipSuccess) e = hipMemcpyAsync(d_slots, slots.data(), m * 4, hipMemcpyHostToDevice, s);
             if (e == hipSuccess) e = hipMemcpyAsync(d_cols, cols.data(), cols.size() * 8, hipMemcpyHostToDevice, s);
             if (e == hipSuccess) e = g->gather_pending ? hipStreamWaitEvent(s, g->gathered, 0) : hipSuccess;
+            if (e == hipSuccess) e = g->wgather_pending ? hipStreamWaitEvent(s, g->wgathered, 0) : hipSuccess;
             if (e == hipSuccess) {
-                g->gather_pending = false;
+                g->gather_pending = g->wgather_pending = false;
                 hipLaunchKernelGGL(table_load_kernel, dim3((m + 255) / 256), dim3(256), 0, s, g->dev, t, d_rows, d_slots,
                                    d_cols, m);
                 e = hipGetLastError();
@@ -1181,15 +1199,22 @@ RH_EXPORT int rh_watch_levels_async(rh_groups* g) {
     EvTargets t;
     t.watch[0] = g->d_watch, t.watch[1] = g->hbm_watch;
     bool hbm = false;
-    rc = evaluate(g, RH_MODE_WATCH, false, t, g->d_wcnt, g->h_wcnt, &hbm, g->wbdesc, &g->wnblocks);
+    rh::TableDev ed;
+    rc = evaluate(g, RH_MODE_WATCH, false, t, g->d_wcnt, g->h_wcnt, &hbm, g->wbdesc, &g->wnblocks, &ed);
     if (rc != RH_OK) return rc;
-    if (hbm && g->event_sink == RH_EVENTS_AUTO) {   // packed into the pinned list on the side stream
+    if (hbm && g->wnblocks) {   // REGION mode (DEVICE and AUTO): the records rebuilt into the pinned list
         RH_HIP(hipEventRecord(g->evaluated, g->ctx->stream));
         RH_HIP(hipStreamWaitEvent(g->d2h_stream, g->evaluated, 0));
-        rc = g->wnblocks ? rh_table_gather(g->wbdesc, g->wnblocks, g->hbm_watch, g->d_watch, nullptr, nullptr, 32,
-                                           g->d_wcnt, g->d2h_stream)
-                         : rh_table_drain(g->d_wcnt, g->hbm_watch, g->d_watch, nullptr, nullptr, 32, g->capacity,
-                                          g->d2h_stream);
+        rc = rh_table_gather_watch(ed, g->wbdesc, g->wnblocks, g->d_watch, g->d_wcnt, g->d2h_stream);
+        if (rc != RH_OK) return rc;
+        RH_HIP(hipEventRecord(g->wdone, g->d2h_stream));
+        RH_HIP(hipEventRecord(g->wgathered, g->d2h_stream));
+        g->wgather_pending = true;
+        hbm = false;
+    } else if (hbm && g->event_sink == RH_EVENTS_AUTO) {   // contiguous HBM list: drained on the side stream
+        RH_HIP(hipEventRecord(g->evaluated, g->ctx->stream));
+        RH_HIP(hipStreamWaitEvent(g->d2h_stream, g->evaluated, 0));
+        rc = rh_table_drain(g->d_wcnt, g->hbm_watch, g->d_watch, nullptr, nullptr, 32, g->capacity, g->d2h_stream);
         if (rc != RH_OK) return rc;
         RH_HIP(hipEventRecord(g->wdone, g->d2h_stream));
         hbm = false;
@@ -1214,15 +1239,9 @@ RH_EXPORT int rh_watch_levels_wait(rh_groups* g, const rh_watch_event** out_even
     lk.lock();
     if (!g->wpending || g->wgen != gen) return rh::fail(RH_E_STATE, "rh_watch_levels_wait: superseded while waiting");
     uint64_t n = std::min<uint64_t>(g->h_wcnt[0], g->capacity);
-    if (g->whbm && (n || g->wnblocks)) {   // DEVICE sink: into the pinned list
+    if (g->whbm && n) {   // DEVICE sink, contiguous HBM list (REGION mode was gathered at _async)
         g->whbm = false;
-        if (g->wnblocks) {   // REGION mode: packed by the gather, which also publishes the length
-            int rc = rh_table_gather(g->wbdesc, g->wnblocks, g->hbm_watch, g->d_watch, nullptr, nullptr, 32, g->d_wcnt,
-                                     g->d2h_stream);
-            if (rc != RH_OK) return rc;
-        } else {
-            RH_HIP(hipMemcpyAsync(g->watch, g->hbm_watch, n * sizeof(rh_watch_event), hipMemcpyDeviceToHost, g->d2h_stream));
-        }
+        RH_HIP(hipMemcpyAsync(g->watch, g->hbm_watch, n * sizeof(rh_watch_event), hipMemcpyDeviceToHost, g->d2h_stream));
         RH_HIP(hipEventRecord(g->wdone, g->d2h_stream));
         done = g->wdone;
         lk.unlock();

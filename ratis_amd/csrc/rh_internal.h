@@ -170,16 +170,14 @@ struct TableEvents {
     unsigned long long* lheads_next = nullptr;  // the other list-head set of the evaluated kind: cleared
     // REGION mode (tile kernels into the DEVICE / AUTO sinks): no counter atomic, no LDS staging.
     // Workgroup gb (block_base + its block index: the evaluation's launches number their workgroups
-    // on) has descriptor gb, kTableDesc u32 at bdesc + gb * kTableDesc.  COMMIT writes no records:
-    // its descriptor is the two totals (u64: advanced | watch-ALL << 32) and per wave four u64
-    // masks (advanced rows 2L / 2L + 1, changed watch-ALL rows 2L / 2L + 1, bit L); the evaluation
-    // has stored the new commit / watch-ALL values in the table, so rh_table_gather_commit rebuilds
-    // the records from the masks and the table's columns (the host orders every later writer of
-    // those columns after it).  WATCH writes its records: wave w of workgroup gb the 128 records from
-    // (gb * kTWaves + w) * 128 of the HBM list, straight from registers; its descriptor is the two
-    // totals, then each wave's two counts (u32); rh_table_gather packs them.  (One returning atomic
-    // per workgroup on one word, at every workgroup's end, cost the 1M-row evaluation 4.5 us; the
-    // COMMIT records themselves 1.6 us of the 19.3.)
+    // on) has descriptor gb, kTableDesc u32 at bdesc + gb * kTableDesc, and writes no records: the
+    // descriptor is the totals (u64: list a | list b << 32) and per wave four u64 masks, bit L for
+    // rows 2L / 2L + 1 -- COMMIT: advanced rows, then changed watch-ALL rows; WATCH: rows whose
+    // levels changed, then which of them are valid.  The evaluation has stored the new values in the
+    // table, so rh_table_gather_commit / _watch rebuild the records from the masks and the table's
+    // columns (the host orders every later writer of those columns after the gather).  (One
+    // returning atomic per workgroup on one word, at every workgroup's end, cost the 1M-row
+    // evaluation 4.5 us; the COMMIT records themselves 1.6 us of the 19.3.)
     uint32_t* bdesc = nullptr;
     uint32_t block_base = 0;
 };
@@ -273,11 +271,6 @@ int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev, 
 // host mapping): list a (records of rec_bytes0 = 16 or 32 B, length counts[0]) and, if b is not
 // null, list b (16 B records, length counts[1]); counts = the host-mapped lengths the evaluation
 // published.  Enqueued on `stream` (ordered after the evaluation by the caller).
-// REGION mode: packs the per-workgroup regions of the HBM lists a (records of rec_bytes0 = 16 or 32 B)
-// and b (16 B, may be null) of an evaluation of n_blocks workgroups into the result lists a_out /
-// b_out (device pointers of the pinned lists) and writes the two lengths to counts_out (host-mapped).
-int rh_table_gather(const uint32_t* bdesc, uint32_t n_blocks, const void* a, void* a_out, const void* b, void* b_out,
-                    uint32_t rec_bytes0, uint64_t* counts_out, hipStream_t stream);
 // REGION mode, COMMIT: the records of an evaluation (its clipped table `t`, as given to
 // rh_table_commit) rebuilt from the descriptors' masks and the table's row-slot, commit and
 // watch-ALL columns into the pinned lists adv_out / wall_out (device pointers; wall_out null: no
@@ -285,6 +278,11 @@ int rh_table_gather(const uint32_t* bdesc, uint32_t n_blocks, const void* a, voi
 // and this kernel (groups.cpp gather_fence).
 int rh_table_gather_commit(const rh::TableDev& t, const uint32_t* bdesc, uint32_t n_blocks, rh_index_event* adv_out,
                            rh_index_event* wall_out, uint64_t* counts_out, hipStream_t stream);
+// REGION mode, WATCH: the level records (slot, valid, min, majority, max) of an evaluation rebuilt
+// the same way from the masks (changed rows, valid flags) and the row-slot / wmin / wmaj / wmax
+// columns into the pinned list `out` (device pointer), its length to counts_out[0].
+int rh_table_gather_watch(const rh::TableDev& t, const uint32_t* bdesc, uint32_t n_blocks, rh_watch_event* out,
+                          uint64_t* counts_out, hipStream_t stream);
 int rh_table_drain(const uint64_t* counts, const void* a, void* a_out, const void* b, void* b_out, uint32_t rec_bytes0,
                    uint64_t cap, hipStream_t stream);
 // Initialises tiles [first_tile, n_tiles) of a tier as free rows (conf 0, row_slot kNoRow, clean).

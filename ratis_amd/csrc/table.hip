@@ -260,9 +260,9 @@ __global__ __launch_bounds__(128) void table_init_tiles_kernel(TableTier tt, uin
 
 // ---- updateCommit / commitIndexChanged over the dirty rows ---------------------------------------
 // One workgroup = kTWaves waves, one 128-row tile per wave.  Every wave evaluates its rows' results
-// in registers.  REGION mode (HBM lists: the DEVICE / AUTO sinks' tile evaluations): each wave
-// writes its records straight into its own 128-record part of the lists and the workgroup its
-// counts into its descriptor; rh_table_gather packs the parts afterwards.  Counter mode (the lists
+// in registers.  REGION mode (the DEVICE / AUTO sinks' tile evaluations): no records -- each wave's
+// event masks go through LDS into its workgroup's descriptor, and rh_table_gather_commit / _watch
+// rebuild the records from the masks and the values stored in the table.  Counter mode (the lists
 // in pinned memory): the block gathers its events in LDS in wave order, takes ONE range of each
 // result list with ONE device-scope atomic on the evaluation's counter word (rh_internal.h,
 // TableEvents) and copies the records out as contiguous 16-byte-per-lane stores.
@@ -445,17 +445,20 @@ __device__ __forceinline__ void table_wave(const TableDev& T, const TableTier& t
     if (lane == 0) sc.cnt[0][threadIdx.x >> 6] = 0;
     return;
 #endif
-    // events: compacted into this wave's LDS region, in row order -- or, in REGION mode, straight
-    // into this wave's 128 records of the block's region of the HBM lists (rh_table_gather packs them)
+    // events: in REGION mode the wave's masks (into the workgroup's descriptor); else compacted into
+    // this wave's LDS region, in row order, for the workgroup's copy-out
     const int wave = threadIdx.x >> 6;
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     uint32_t p = (uint32_t)(__popcll(a0 & lt) + __popcll(a1 & lt));
-    const uint64_t rg = gb * rh::kTableRecs + (uint64_t)wave * 128;
     if (ev.bdesc) {
-        if (WATCH) {
-#pragma unroll
-            for (int g = 0; g < 2; ++g)
-                if (e0[g]) ev.watch[rg + p++] = rh_watch_event{slot[g], valid[g], x0[g], x1[g], x2[g]};
+        if (WATCH) {   // no records: the changed rows and their valid flags (levels: in the table)
+            const uint64_t v0 = __ballot(e0[0] && valid[0]), v1 = __ballot(e0[1] && valid[1]);
+            if (lane == 0) {
+                sc.mask[wave][0] = a0;
+                sc.mask[wave][1] = a1;
+                sc.mask[wave][2] = v0;
+                sc.mask[wave][3] = v1;
+            }
         } else {
             // no records: the wave's masks (the values are in the table, rh_table_gather_commit),
             // staged in LDS: a wave that returned early (clean tile) leaves the block's zeros
@@ -552,7 +555,7 @@ __device__ __forceinline__ void table_block_iter(const TableDev& T, const TierRa
         table_dispatch<FLO, FHI, FLO <= 6, WATCH, SPEC>(T, t, tl, wall_on, stage, sc, ev, gb);
     __syncthreads();
 
-    if (ev.bdesc && !WATCH) {   // ---- REGION mode, COMMIT: the descriptor: totals, the waves' masks
+    if (ev.bdesc) {   // ---- REGION mode: the descriptor: totals, the waves' masks
         uint64_t* md = reinterpret_cast<uint64_t*>(ev.bdesc) + gb * (rh::kTableDesc / 2);
         if (threadIdx.x == 0) {
             uint64_t v0 = 0, v1 = 0;
@@ -564,24 +567,6 @@ __device__ __forceinline__ void table_block_iter(const TableDev& T, const TierRa
         }
         return;
     }
-    if (ev.bdesc) {
-        // ---- REGION mode, WATCH: the waves wrote their records into their own 128-record parts of
-        // the block's region; the block's counts (totals, then per wave) go to bdesc for the gather
-        if (threadIdx.x < 2 * kTWaves + 2) {
-            const uint32_t k = threadIdx.x;
-            uint32_t v;
-            if (k < 2) {
-                v = 0;
-#pragma unroll
-                for (int w = 0; w < kTWaves; ++w) v += sc.cnt[k][w];
-            } else {
-                v = sc.cnt[(k - 2) / kTWaves][(k - 2) % kTWaves];
-            }
-            ev.bdesc[gb * rh::kTableDesc + k] = v;
-        }
-        return;
-    }
-
     // ---- one range of each list per block (one device-scope atomic), then a contiguous copy
     if (threadIdx.x == 0) {
         uint32_t a0 = 0, a1 = 0;
@@ -1093,119 +1078,39 @@ int rh_table_drain(const uint64_t* counts, const void* a, void* a_out, const voi
     return RH_OK;
 }
 
-// ---- REGION mode: the per-workgroup regions packed into the result lists --------------------------
-// One gather workgroup per kGatherWGs evaluation workgroups (kGatherChunks wave parts of 128
-// records).  Its offsets in the packed lists are the sums of the totals of the evaluation
-// workgroups before its first (read from bdesc, a few KiB: summed by the 256 threads, reduced in
-// LDS); its parts' counts are scanned in LDS, then every thread moves records (16-byte words; to
-// pinned memory: GPU writes across PCIe), finding each record's part by binary search of the scan.
-// Gather workgroup 0 also sums every total and publishes the two lengths.
+// ---- REGION mode gathers: one gather workgroup per kGatherWGs evaluation workgroups ----------------
 constexpr uint32_t kGatherWGs = kTWaves >= 32 ? 1u : 32u / kTWaves;
 constexpr uint32_t kGatherChunks = kGatherWGs * kTWaves;
 
-__device__ __forceinline__ uint32_t part_of(const uint32_t* pre, uint32_t e) {   // pre[c] <= e < pre[c + 1]
-    uint32_t lo = 0, hi = kGatherChunks;
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (pre[mid] <= e) lo = mid; else hi = mid;
-    }
-    return lo;
-}
 
-__global__ __launch_bounds__(256) void table_gather_kernel(const uint32_t* __restrict__ bdesc, uint32_t n_blocks,
-                                                           const uint4* __restrict__ a, uint4* __restrict__ a_out,
-                                                           const uint4* __restrict__ b, uint4* __restrict__ b_out,
-                                                           uint32_t words0, uint64_t* counts_out) {
-    constexpr uint32_t D = rh::kTableDesc;   // per evaluation workgroup: totals, then per-wave counts
-    __shared__ unsigned long long red[2][256 / 64];
-    __shared__ uint32_t pre[2][kGatherChunks + 1];
-    const uint32_t first = blockIdx.x * kGatherWGs;      // first evaluation workgroup of this gather
-    const uint32_t upto = blockIdx.x == 0 ? n_blocks : first;   // gather workgroup 0 sums them all
-    unsigned long long s0 = 0, s1 = 0;
-    for (uint32_t j = threadIdx.x; j < upto; j += blockDim.x) {
-        s0 += bdesc[(uint64_t)j * D];
-        s1 += bdesc[(uint64_t)j * D + 1];
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        s0 += __shfl_down(s0, o);
-        s1 += __shfl_down(s1, o);
-    }
-    if ((threadIdx.x & 63) == 0) {
-        red[0][threadIdx.x >> 6] = s0;
-        red[1][threadIdx.x >> 6] = s1;
-    }
-    for (uint32_t c = threadIdx.x; c < kGatherChunks; c += blockDim.x) {   // the parts' counts
-        const uint32_t gb = first + c / kTWaves, w = c % kTWaves;
-        pre[0][c + 1] = gb < n_blocks ? bdesc[(uint64_t)gb * D + 2 + w] : 0u;
-        pre[1][c + 1] = gb < n_blocks ? bdesc[(uint64_t)gb * D + 2 + kTWaves + w] : 0u;
-    }
-    __syncthreads();
-    if (threadIdx.x < 2) {   // inclusive scan of one kind's part counts
-        uint32_t* p = pre[threadIdx.x];
-        p[0] = 0;
-        for (uint32_t c = 1; c <= kGatherChunks; ++c) p[c] += p[c - 1];
-    }
-    s0 = red[0][0] + red[0][1] + red[0][2] + red[0][3];
-    s1 = red[1][0] + red[1][1] + red[1][2] + red[1][3];
-    uint64_t p0 = s0, p1 = s1;
-    if (blockIdx.x == 0) {
-        if (threadIdx.x == 0) {
-            counts_out[0] = s0;
-            counts_out[1] = b ? s1 : 0;
-        }
-        p0 = p1 = 0;
-    }
-    __syncthreads();
-    const uint64_t part0 = (uint64_t)first * kTWaves;   // global index of this gather's first part
-    const uint32_t n0 = pre[0][kGatherChunks] * words0;
-    for (uint32_t j = threadIdx.x; j < n0; j += blockDim.x) {
-        const uint32_t e = j / words0, c = part_of(pre[0], e);
-        const uint64_t src = (part0 + c) * 128 + (e - pre[0][c]);
-        a_out[(p0 + e) * words0 + j % words0] = a[src * words0 + j % words0];
-    }
-    if (b) {
-        const uint32_t n1 = pre[1][kGatherChunks];
-        for (uint32_t e = threadIdx.x; e < n1; e += blockDim.x) {
-            const uint32_t c = part_of(pre[1], e);
-            b_out[p1 + e] = b[(part0 + c) * 128 + (e - pre[1][c])];
-        }
-    }
-}
-
-int rh_table_gather(const uint32_t* bdesc, uint32_t n_blocks, const void* a, void* a_out, const void* b, void* b_out,
-                    uint32_t rec_bytes0, uint64_t* counts_out, hipStream_t stream) {
-    if (n_blocks == 0) return rh::fail(RH_E_INVAL, "rh_table_gather: no workgroups");
-    hipLaunchKernelGGL(table_gather_kernel, dim3((n_blocks + kGatherWGs - 1) / kGatherWGs), dim3(256), 0, stream, bdesc,
-                       n_blocks, static_cast<const uint4*>(a), static_cast<uint4*>(a_out), static_cast<const uint4*>(b),
-                       static_cast<uint4*>(b_out), rec_bytes0 / 16u, counts_out);
-    RH_HIP(hipGetLastError());
-    return RH_OK;
-}
-
-// ---- REGION mode, updateCommit: the records rebuilt from the masks and the table -----------------
-// As table_gather_kernel (offsets from the totals before the gather workgroup's first evaluation
-// workgroup, its parts' counts -- popcounts of the masks -- scanned in LDS), then each wave takes
+// ---- REGION mode: the records rebuilt from the masks and the table ---------------------------------
+// One gather workgroup per kGatherWGs evaluation workgroups: its offsets in the packed lists are
+// the sums of the totals before its first evaluation workgroup (summed by the 256 threads, reduced
+// in LDS), its parts' counts -- popcounts of the masks -- scanned in LDS; then each wave takes
 // parts round robin: the part's tile (its launch, tier slot and tile, as the evaluation's block
-// map), lane L the rows 2L, 2L + 1: their row slots and, per list, the commit or watch-ALL value
-// the evaluation stored -- one coalesced load per column per wave -- written in row order.
-struct GatherCommitArgs {
+// map), lane L the rows 2L, 2L + 1: their row slots and the values the evaluation stored -- one
+// coalesced load per column per wave -- written in row order.  updateCommit: list a = advanced
+// (the commit column), list b = changed watch-ALL levels (the watch-ALL column).  commitIndexChanged:
+// list a = changed levels (wmin / wmaj / wmax) with the valid flag from the mask's second pair.
+struct GatherRowsArgs {
     TableDev t;             // the evaluation's (clipped) table
     TierRange tr[2];        // its launches' block -> tier maps
     uint32_t cls1_base;     // the second launch's first workgroup number
     uint32_t n_blocks;
-    const uint64_t* desc;   // per workgroup: totals (advanced | watch-ALL << 32), per wave a0 a1 c0 c1
-    rh_index_event* adv;
-    rh_index_event* wall;   // null: no watch-ALL list
+    const uint64_t* desc;   // per workgroup: totals (a | b << 32), per wave 4 masks
+    void* a;                // rh_index_event (updateCommit) / rh_watch_event (commitIndexChanged) list
+    rh_index_event* b;      // updateCommit's watch-ALL list (null: none)
     uint64_t* counts_out;
 };
 
-__global__ __launch_bounds__(256) void table_gather_commit_kernel(GatherCommitArgs arg) {
+template <bool WATCH>
+__global__ __launch_bounds__(256) void table_gather_rows_kernel(GatherRowsArgs arg) {
     (void)arg;
-    const GatherCommitArgs& A = rh::kernarg_struct<GatherCommitArgs>();
+    const GatherRowsArgs& A = rh::kernarg_struct<GatherRowsArgs>();
     constexpr uint32_t S = rh::kTableDesc / 2;   // u64 per descriptor
     __shared__ unsigned long long red[2][256 / 64];
     __shared__ uint32_t pre[2][kGatherChunks + 1];
+    const bool has_b = !WATCH && A.b != nullptr;
     const uint32_t first = blockIdx.x * kGatherWGs;
     const uint32_t upto = blockIdx.x == 0 ? A.n_blocks : first;   // gather workgroup 0 sums them all
     unsigned long long s0 = 0, s1 = 0;
@@ -1229,7 +1134,7 @@ __global__ __launch_bounds__(256) void table_gather_commit_kernel(GatherCommitAr
         if (gb < A.n_blocks) {
             const uint64_t* m = A.desc + (uint64_t)gb * S + 1 + 4 * w;
             n0 = (uint32_t)(__popcll(m[0]) + __popcll(m[1]));
-            n1 = A.wall ? (uint32_t)(__popcll(m[2]) + __popcll(m[3])) : 0u;
+            n1 = has_b ? (uint32_t)(__popcll(m[2]) + __popcll(m[3])) : 0u;
         }
         pre[0][c + 1] = n0;
         pre[1][c + 1] = n1;
@@ -1246,7 +1151,7 @@ __global__ __launch_bounds__(256) void table_gather_commit_kernel(GatherCommitAr
     if (blockIdx.x == 0) {
         if (threadIdx.x == 0) {
             A.counts_out[0] = s0;
-            A.counts_out[1] = A.wall ? s1 : 0;
+            A.counts_out[1] = has_b ? s1 : 0;
         }
         p0 = p1 = 0;
     }
@@ -1257,8 +1162,8 @@ __global__ __launch_bounds__(256) void table_gather_commit_kernel(GatherCommitAr
         const uint32_t gb = first + c / kTWaves, w = c % kTWaves;
         if (gb >= A.n_blocks) break;   // wave-uniform
         const uint64_t* m = A.desc + (uint64_t)gb * S + 1 + 4 * w;
-        const uint64_t a0 = m[0], a1 = m[1], c0 = A.wall ? m[2] : 0ull, c1 = A.wall ? m[3] : 0ull;
-        if (!(a0 | a1 | c0 | c1)) continue;
+        const uint64_t a0 = m[0], a1 = m[1], c0 = (WATCH || has_b) ? m[2] : 0ull, c1 = (WATCH || has_b) ? m[3] : 0ull;
+        if (!(a0 | a1 | (WATCH ? 0ull : (c0 | c1)))) continue;
         const int cls = gb < A.cls1_base ? 0 : 1;
         const uint32_t b = gb - (cls ? A.cls1_base : 0u);
         const TierRange& tr = A.tr[cls];
@@ -1269,40 +1174,67 @@ __global__ __launch_bounds__(256) void table_gather_commit_kernel(GatherCommitAr
         const TableTier& tt = A.t.tier[tr.tier[i]];
         const uint64_t tl = (uint64_t)(b - tr.block_begin[i]) * kTWaves + w;
         const uint8_t* tb = tt.base + tl * rh::tile::bytes(tt.width);
-        const bool e00 = (a0 >> lane) & 1u, e01 = (a1 >> lane) & 1u, e10 = (c0 >> lane) & 1u, e11 = (c1 >> lane) & 1u;
+        const uint32_t F = tt.width;
+        const bool e00 = (a0 >> lane) & 1u, e01 = (a1 >> lane) & 1u;
+        const bool e10 = !WATCH && ((c0 >> lane) & 1u), e11 = !WATCH && ((c1 >> lane) & 1u);
         if (!(e00 || e01 || e10 || e11)) continue;
         const uint2 sl = *reinterpret_cast<const uint2*>(tb + rh::tile::kSlot + 8u * lane);
-        if (e00 || e01) {
-            const int64_t* cp = reinterpret_cast<const int64_t*>(tb + rh::tile::commit(tt.width)) + 2 * lane;
+        if (WATCH) {
+            const int64_t* mn = reinterpret_cast<const int64_t*>(tb + rh::tile::wmin(F)) + 2 * lane;
+            const int64_t* mj = reinterpret_cast<const int64_t*>(tb + rh::tile::wmaj(F)) + 2 * lane;
+            const int64_t* mx = reinterpret_cast<const int64_t*>(tb + rh::tile::wmax(F)) + 2 * lane;
+            rh_watch_event* out = static_cast<rh_watch_event*>(A.a);
             uint64_t p = p0 + pre[0][c] + (uint64_t)(__popcll(a0 & lt) + __popcll(a1 & lt));
-            if (e00) A.adv[p++] = rh_index_event{sl.x, 0u, cp[0]};
-            if (e01) A.adv[p] = rh_index_event{sl.y, 0u, cp[1]};
-        }
-        if (e10 || e11) {
-            const int64_t* wp = reinterpret_cast<const int64_t*>(tb + rh::tile::wall(tt.width)) + 2 * lane;
-            uint64_t q = p1 + pre[1][c] + (uint64_t)(__popcll(c0 & lt) + __popcll(c1 & lt));
-            if (e10) A.wall[q++] = rh_index_event{sl.x, 0u, wp[0]};
-            if (e11) A.wall[q] = rh_index_event{sl.y, 0u, wp[1]};
+            if (e00) out[p++] = rh_watch_event{sl.x, (uint32_t)((c0 >> lane) & 1u), mn[0], mj[0], mx[0]};
+            if (e01) out[p] = rh_watch_event{sl.y, (uint32_t)((c1 >> lane) & 1u), mn[1], mj[1], mx[1]};
+        } else {
+            if (e00 || e01) {
+                const int64_t* cp = reinterpret_cast<const int64_t*>(tb + rh::tile::commit(F)) + 2 * lane;
+                rh_index_event* out = static_cast<rh_index_event*>(A.a);
+                uint64_t p = p0 + pre[0][c] + (uint64_t)(__popcll(a0 & lt) + __popcll(a1 & lt));
+                if (e00) out[p++] = rh_index_event{sl.x, 0u, cp[0]};
+                if (e01) out[p] = rh_index_event{sl.y, 0u, cp[1]};
+            }
+            if (e10 || e11) {
+                const int64_t* wp = reinterpret_cast<const int64_t*>(tb + rh::tile::wall(F)) + 2 * lane;
+                uint64_t q = p1 + pre[1][c] + (uint64_t)(__popcll(c0 & lt) + __popcll(c1 & lt));
+                if (e10) A.b[q++] = rh_index_event{sl.x, 0u, wp[0]};
+                if (e11) A.b[q] = rh_index_event{sl.y, 0u, wp[1]};
+            }
         }
     }
 }
 
-int rh_table_gather_commit(const rh::TableDev& t, const uint32_t* bdesc, uint32_t n_blocks, rh_index_event* adv_out,
-                           rh_index_event* wall_out, uint64_t* counts_out, hipStream_t stream) {
-    if (n_blocks == 0) return rh::fail(RH_E_INVAL, "rh_table_gather_commit: no workgroups");
-    GatherCommitArgs a{};
-    a.t = t;
-    const uint32_t b0 = tier_range(t, 0, a.tr[0]), b1 = tier_range(t, 1, a.tr[1]);
-    if (b0 + b1 != n_blocks) return rh::fail(RH_E_STATE, "rh_table_gather_commit: workgroups differ from the evaluation's");
-    a.cls1_base = b0;
-    a.n_blocks = n_blocks;
-    a.desc = reinterpret_cast<const uint64_t*>(bdesc);
-    a.adv = adv_out;
-    a.wall = wall_out;
-    a.counts_out = counts_out;
-    hipLaunchKernelGGL(table_gather_commit_kernel, dim3((n_blocks + kGatherWGs - 1) / kGatherWGs), dim3(256), 0, stream, a);
+static int gather_rows(bool watch, const rh::TableDev& t, const uint32_t* bdesc, uint32_t n_blocks, void* a,
+                       rh_index_event* b, uint64_t* counts_out, hipStream_t stream) {
+    if (n_blocks == 0) return rh::fail(RH_E_INVAL, "rh_table_gather_rows: no workgroups");
+    GatherRowsArgs g{};
+    g.t = t;
+    const uint32_t b0 = tier_range(t, 0, g.tr[0]), b1 = tier_range(t, 1, g.tr[1]);
+    if (b0 + b1 != n_blocks) return rh::fail(RH_E_STATE, "rh_table_gather_rows: workgroups differ from the evaluation's");
+    g.cls1_base = b0;
+    g.n_blocks = n_blocks;
+    g.desc = reinterpret_cast<const uint64_t*>(bdesc);
+    g.a = a;
+    g.b = b;
+    g.counts_out = counts_out;
+    const dim3 grid((n_blocks + kGatherWGs - 1) / kGatherWGs), blk(256);
+    if (watch)
+        hipLaunchKernelGGL(table_gather_rows_kernel<true>, grid, blk, 0, stream, g);
+    else
+        hipLaunchKernelGGL(table_gather_rows_kernel<false>, grid, blk, 0, stream, g);
     RH_HIP(hipGetLastError());
     return RH_OK;
+}
+
+int rh_table_gather_commit(const rh::TableDev& t, const uint32_t* bdesc, uint32_t n_blocks, rh_index_event* adv_out,
+                           rh_index_event* wall_out, uint64_t* counts_out, hipStream_t stream) {
+    return gather_rows(false, t, bdesc, n_blocks, adv_out, wall_out, counts_out, stream);
+}
+
+int rh_table_gather_watch(const rh::TableDev& t, const uint32_t* bdesc, uint32_t n_blocks, rh_watch_event* out,
+                          uint64_t* counts_out, hipStream_t stream) {
+    return gather_rows(true, t, bdesc, n_blocks, out, nullptr, counts_out, stream);
 }
 
 int rh_table_init_tiles(const rh::TableTier& t, uint32_t first_tile, uint32_t n_tiles, hipStream_t stream) {

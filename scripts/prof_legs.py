@@ -22,7 +22,8 @@ GATE = "spin_kernel"   # torch.cuda._sleep: the queue gate in front of each time
 
 # the kernel each roofline of the bench line prices (legs without an entry: every kernel of the step)
 ROOFLINE_KERNEL = [("commit", "commit_kernel_rank"), ("lease", "lease_kernel"), ("fused", "leader_kernel"),
-                   ("table_", "table_commit_kernel|table_list_kernel"), ("crc", "crc_frames_kernel")]
+                   ("table_", "table_commit_kernel|table_list_kernel"), ("twatch_", "table_commit_kernel|table_list_kernel"),
+                   ("crc", "crc_frames_kernel")]
 
 
 def rows(path):
@@ -66,6 +67,10 @@ def bench_figures(line):
         if isinstance(v, dict) and "auto" in v:
             leg = "table_" + k[len("dirty_"):] + "_auto"
             f[leg] = (v["auto"]["ms_evaluation"], f"pcie.delta_streaming.table_commit.{k}.auto.ms_evaluation")
+    tw = g("pcie", "delta_streaming", "table_watch") or {}
+    for k, v in tw.items():
+        if isinstance(v, dict) and "ms_evaluation" in v:
+            f["twatch_" + k[len("dirty_"):]] = (v["ms_evaluation"], f"pcie.delta_streaming.table_watch.{k}.ms_evaluation")
     f["crc"] = (g("crc32c", "roofline", "avg_launch_ms"), "crc32c.roofline.avg_launch_ms")
     f["framing"] = (g("crc32c", "read_path", "ms_framing"), "crc32c.read_path.ms_framing")
     f["framing_plus_verify"] = (g("crc32c", "read_path", "ms_framing_plus_verify"), "crc32c.read_path.ms_framing_plus_verify")

@@ -350,8 +350,9 @@ def test_separate_done_word_of_large_tables(ctx, orc, monkeypatch):
 @pytest.mark.parametrize("sink", ["device", "auto"])
 def test_region_records_survive_later_writers(ctx, orc, sink):
     """updateCommit in REGION mode writes no records: the gather rebuilds them on the side stream
-    from the table's row-slot, commit and watch-ALL columns (rh_internal.h, TableEvents), so every
-    later writer of those columns must wait for it (groups.cpp gather_fence).  A commitIndexChanged
+    from the table's row-slot, commit and watch-ALL columns, and commitIndexChanged's from the
+    row-slot and level columns (rh_internal.h, TableEvents), so every later writer of those columns
+    must wait for them (groups.cpp gather_fence / wgather_fence).  A commitIndexChanged
     evaluation with ~half a million changed levels goes first, so its record gather holds the side
     stream (~16 MB across PCIe) and the updateCommit gather queues behind it; meanwhile the host
     rewrites every column that gather reads -- COMMITTED deltas on the advanced rows, stops, restarts
@@ -391,8 +392,10 @@ def test_region_records_survive_later_writers(ctx, orc, sink):
         got = tab.commit_wait(tk)
         assert np.array_equal(got.advanced_slots, expect[0]) and np.array_equal(got.advanced_commit, expect[1])
         assert np.array_equal(got.watch_all_slots, expect[2]) and np.array_equal(got.watch_all_min, expect[3])
-        levels = tab.watch_wait()
+        levels = tab.watch_wait()   # its records are rebuilt from the level columns the restarts reset
         assert np.array_equal(levels["slot"], expect_w[0])
+        assert np.array_equal(levels["min"], expect_w[1][0]) and np.array_equal(levels["majority"], expect_w[1][1])
+        assert np.array_equal(levels["max"], expect_w[1][2]) and np.array_equal(levels["valid"] != 0, expect_w[2])
         # the model replays the same calls after the first evaluation
         model.apply(w)
         for s in victims[:32]:
