@@ -287,11 +287,10 @@ int rh_commit_batch_wait(rh_groups* g, uint64_t ticket, rh_commit_out* out);
  * kernel on a side stream rebuilds the records from the table's columns into the pinned buffers
  * while the table stream goes on (the ticket completes after the gather; no host-issued copy; the
  * table's next writers of those columns are ordered after it); an evaluation over the dirty-row
- * lists writes records -- into the pinned buffers directly when fewer than 8192 rows were marked,
- * else into HBM lists drained on the side stream.  DEVICE: as AUTO, except that lists
- * assembled in HBM without a gather are copied into the pinned buffers by the _wait call (a D2H
- * on the table's copy stream).  Results are identical.  Not while an evaluation is outstanding
- * (RH_E_STATE). */
+ * lists writes records into the pinned buffers directly when fewer than 8192 rows were marked,
+ * else event bits per listed row, rebuilt the same way from the list entries.  DEVICE: as AUTO,
+ * except that every list evaluation takes the event-bit form.  Results are identical.  Not while
+ * an evaluation is outstanding (RH_E_STATE). */
 #define RH_EVENTS_HOST_MAPPED 0
 #define RH_EVENTS_DEVICE      1
 #define RH_EVENTS_AUTO        2

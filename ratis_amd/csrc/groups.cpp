@@ -78,6 +78,12 @@ struct EvSet {
 // (every tier's last workgroup may be partial and the tiers round their rows up to 128).
 uint64_t hbm_records(uint64_t capacity) { return capacity + (uint64_t)(rh::kTableTiers + 1) * rh::kTableRecs; }
 uint64_t region_blocks(uint64_t capacity) { return hbm_records(capacity) / rh::kTableRecs + rh::kTableTiers + 1; }
+// list capacity: a list evaluation is chosen while at most capacity / RH_LIST_DIV rows can be dirty
+uint32_t list_cap(uint64_t capacity) { return (uint32_t)std::max<uint64_t>(1024, capacity / RH_LIST_DIV); }
+// REGION-mode descriptors per result set: a tile evaluation's workgroups or a list evaluation's
+uint64_t desc_blocks(uint64_t capacity) {
+    return std::max<uint64_t>(region_blocks(capacity), rh::table_list_desc_blocks(list_cap(capacity)));
+}
 
 }  // namespace
 
@@ -131,6 +137,7 @@ struct rh_groups {
     // watch evaluation, control ops, a load)
     hipEvent_t wgathered = nullptr;
     bool wgather_pending = false;
+    bool wgather_list = false;   // ... and it reads the commitIndexChanged list's entries (list_fence)
     uint64_t* d_lbits = nullptr;  // rh_lease_batch: slot bitmap (device) and its pinned copy
     uint64_t* h_lbits = nullptr;
     // events (rh_internal.h, TableEvents): the evaluation counter words, result sets
@@ -240,6 +247,8 @@ void free_groups(rh_groups* g) {
 }
 
 // Orders the table stream's next launch after the last updateCommit record gather (see `gathered`).
+// A gather of a list evaluation also reads that list's entries, which the next appends overwrite:
+// the delta apply (every kind) and an updateCommit list evaluation (the commitIndexChanged list).
 #ifndef RH_GATHER_FENCE   // test-sensitivity builds only (0: no fence -- wrong results)
 #define RH_GATHER_FENCE 1
 #endif
@@ -255,8 +264,13 @@ int wgather_fence(rh_groups* g) {
     if (!RH_GATHER_FENCE || !g->wgather_pending) return RH_OK;
     RH_HIP(hipStreamWaitEvent(g->ctx->stream, g->wgathered, 0));
     g->wgather_pending = false;
+    g->wgather_list = false;
     return RH_OK;
 }
+
+// Before a launch that appends to the commitIndexChanged list: the last watch gather, if it reads
+// that list's entries.
+int list_fence(rh_groups* g) { return g->wgather_list ? wgather_fence(g) : RH_OK; }
 
 // (Re)allocates tier t with `rows` rows (a multiple of 128), keeping the old rows' contents: tiles
 // keep their position, so the old tiles and summaries are one copy each and the new tiles start
@@ -415,6 +429,9 @@ struct EvTargets {
 #ifndef RH_SPEC_DIV   // SPEC tile evaluations from marks >= rows / RH_SPEC_DIV (A/B)
 #define RH_SPEC_DIV 4
 #endif
+#ifndef RH_LIST_REGION   // A/B: list evaluations into HBM in REGION mode (1) or with the counter atomic (0)
+#define RH_LIST_REGION 1
+#endif
 #ifndef RH_LIST_PINNED_MAX   // AUTO: list evaluations of fewer marked rows write the pinned lists directly (A/B)
 #define RH_LIST_PINNED_MAX 8192
 #endif
@@ -428,12 +445,15 @@ struct EvTargets {
 // counter atomic, no records: the caller's rh_table_gather_commit / _watch rebuilds them and
 // publishes the lengths; *nblocks = its workgroups (else 0), *ed_out its clipped table.
 int evaluate(rh_groups* g, int mode, bool wall_on, const EvTargets& t, uint64_t* counts_out, uint64_t* h_counts,
-             bool* hbm, uint32_t* bdesc, uint32_t* nblocks, rh::TableDev* ed_out = nullptr) {
+             bool* hbm, uint32_t* bdesc, uint32_t* nblocks, rh::TableDev* ed_out = nullptr, rh::ListRegion* lr_out = nullptr) {
     hipStream_t s = g->ctx->stream;
     *hbm = false;
     *nblocks = 0;
+    if (lr_out) *lr_out = rh::ListRegion{};
     int rc = flush_ops(g);
     if (rc == RH_OK) rc = mode != RH_MODE_WATCH ? gather_fence(g) : wgather_fence(g);   // it rewrites the values a gather reads
+    // an updateCommit list evaluation appends to the commitIndexChanged list a watch gather may read
+    if (rc == RH_OK && mode != RH_MODE_WATCH && g->lvalid[0]) rc = list_fence(g);
     if (rc != RH_OK) return rc;
     const uint32_t blocks = rh::table_commit_blocks(g->dev);
     if (blocks == 0) {   // no tier has rows: nothing can be dirty
@@ -465,6 +485,19 @@ int evaluate(rh_groups* g, int mode, bool wall_on, const EvTargets& t, uint64_t*
         l.cap = g->lcap;
         // COMMIT marks the rows whose commit advanced for commitIndexChanged: at most the listed ones
         const rh::TableLists lw = m == 0 ? lists_for(g, 1, g->lmarks[0]) : rh::TableLists{};
+        // REGION mode into [1] (masks per wave and pass, no counter atomic, no records): the
+        // caller's gather rebuilds the records from the list entries and the table
+        const uint32_t grid = rh::table_list_grid(g->lmarks[m]);
+        const uint32_t passes = rh::table_list_passes(grid, std::min<uint64_t>(g->lmarks[m], g->lcap));
+        if (RH_LIST_REGION && k == 1 && lr_out && ed_out && passes && (uint64_t)passes * grid <= desc_blocks(g->capacity)) {
+            ev.bdesc = bdesc;
+            ev.list_passes = passes;
+            *nblocks = passes * grid;
+            *ed_out = g->dev;
+            lr_out->rows = g->d_lrows[m];
+            lr_out->cap = g->lcap;
+            lr_out->grid = grid;
+        }
         rc = rh_table_commit_lists(g->dev, mode, l, lw, ev, s, t0, t1, g->lmarks[m]);
     } else {
         if (m == 0) g->lvalid[1] = false;   // the tile kernel marks wdirty with plain stores
@@ -534,7 +567,8 @@ int ring_submit(rh_groups* g, int i, size_t n, bool has_set) {
     RH_HIP(hipMemcpyAsync(g->d_ring[i], g->h_ring[i], n * sizeof(rh_delta), hipMemcpyHostToDevice, cs));
     RH_HIP(hipEventRecord(g->ring_free[i], cs));
     RH_HIP(hipStreamWaitEvent(s, g->ring_free[i], 0));
-    rc = gather_fence(g);   // RH_COL_COMMITTED deltas write the commit column
+    rc = gather_fence(g);   // RH_COL_COMMITTED deltas write the commit column; appends, the lists
+    if (rc == RH_OK) rc = list_fence(g);
     if (rc != RH_OK) return rc;
     g->ring_used[i] = true;
     g->ring_next = i ^ 1;
@@ -668,14 +702,14 @@ RH_EXPORT int rh_groups_create(rh_ctx* ctx, uint64_t capacity, int64_t gap_thres
         if (rc == RH_OK) rc = halloc_mapped(&g->ev[i].wall, &g->ev[i].d_wall, capacity);
         if (rc == RH_OK) rc = dalloc(&g->ev[i].hbm_adv, hbm_records(capacity));
         if (rc == RH_OK) rc = dalloc(&g->ev[i].hbm_wall, hbm_records(capacity));
-        if (rc == RH_OK) rc = dalloc(&g->ev[i].bdesc, rh::kTableDesc * region_blocks(capacity));
+        if (rc == RH_OK) rc = dalloc(&g->ev[i].bdesc, rh::kTableDesc * desc_blocks(capacity));
         if (rc == RH_OK) rc = halloc_mapped(&g->ev[i].h_cnt, &g->ev[i].d_cnt, 2);
         if (rc == RH_OK && hipEventCreateWithFlags(&g->ev[i].done, hipEventDisableTiming) != hipSuccess)
             rc = rh::fail(RH_E_DEVICE, "hipEventCreate(commit batch)");
     }
     if (rc == RH_OK) rc = halloc_mapped(&g->watch, &g->d_watch, capacity);
     if (rc == RH_OK) rc = dalloc(&g->hbm_watch, hbm_records(capacity));
-    if (rc == RH_OK) rc = dalloc(&g->wbdesc, rh::kTableDesc * region_blocks(capacity));
+    if (rc == RH_OK) rc = dalloc(&g->wbdesc, rh::kTableDesc * desc_blocks(capacity));
     if (rc == RH_OK) rc = halloc_mapped(&g->h_wcnt, &g->d_wcnt, 2);
     if (rc == RH_OK && hipEventCreateWithFlags(&g->wdone, hipEventDisableTiming) != hipSuccess)
         rc = rh::fail(RH_E_DEVICE, "hipEventCreate(watch levels)");
@@ -686,8 +720,7 @@ RH_EXPORT int rh_groups_create(rh_ctx* ctx, uint64_t capacity, int64_t gap_thres
     g->cbits = capacity < (1ull << 24) ? 24u : 28u;
     if (const char* e = std::getenv("RATIS_HIP_TABLE_CNT_BITS"))
         if (std::atoi(e) == 28) g->cbits = 28u;
-    // list capacity: a list evaluation is chosen while at most capacity / RH_LIST_DIV rows can be dirty
-    g->lcap = (uint32_t)std::max<uint64_t>(1024, capacity / RH_LIST_DIV);
+    g->lcap = list_cap(capacity);
     for (int k = 0; k < 2 && rc == RH_OK; ++k) rc = dalloc(&g->d_lrows[k], kListRegions * g->lcap);
     if (rc == RH_OK) rc = dalloc(&g->d_lheads, (size_t)4 * kListRegions * rh::kHeadStride);
     if (rc == RH_OK && hipMemsetAsync(g->d_lheads, 0, (size_t)4 * kListRegions * rh::kHeadStride * 8, s) != hipSuccess)
@@ -1108,13 +1141,14 @@ RH_EXPORT int rh_commit_batch_async(rh_groups* g, uint32_t flags, uint64_t* tick
     t.wall[0] = e.d_wall, t.wall[1] = e.hbm_wall;
     bool hbm = false;
     rh::TableDev ed;
-    rc = evaluate(g, RH_MODE_COMMIT, wall_on, t, e.d_cnt, e.h_cnt, &hbm, e.bdesc, &e.nblocks, &ed);
+    rh::ListRegion lr;
+    rc = evaluate(g, RH_MODE_COMMIT, wall_on, t, e.d_cnt, e.h_cnt, &hbm, e.bdesc, &e.nblocks, &ed, &lr);
     if (rc != RH_OK) return rc;
     if (hbm && e.nblocks) {   // REGION mode (DEVICE and AUTO): the records rebuilt into the pinned lists
         RH_HIP(hipEventRecord(g->evaluated, g->ctx->stream));
         RH_HIP(hipStreamWaitEvent(g->d2h_stream, g->evaluated, 0));
         rc = rh_table_gather_commit(ed, e.bdesc, e.nblocks, e.d_adv, wall_on ? e.d_wall : nullptr, e.d_cnt,
-                                    g->d2h_stream);
+                                    g->d2h_stream, lr);
         if (rc != RH_OK) return rc;
         RH_HIP(hipEventRecord(e.done, g->d2h_stream));
         RH_HIP(hipEventRecord(g->gathered, g->d2h_stream));
@@ -1200,16 +1234,18 @@ RH_EXPORT int rh_watch_levels_async(rh_groups* g) {
     t.watch[0] = g->d_watch, t.watch[1] = g->hbm_watch;
     bool hbm = false;
     rh::TableDev ed;
-    rc = evaluate(g, RH_MODE_WATCH, false, t, g->d_wcnt, g->h_wcnt, &hbm, g->wbdesc, &g->wnblocks, &ed);
+    rh::ListRegion lr;
+    rc = evaluate(g, RH_MODE_WATCH, false, t, g->d_wcnt, g->h_wcnt, &hbm, g->wbdesc, &g->wnblocks, &ed, &lr);
     if (rc != RH_OK) return rc;
     if (hbm && g->wnblocks) {   // REGION mode (DEVICE and AUTO): the records rebuilt into the pinned list
         RH_HIP(hipEventRecord(g->evaluated, g->ctx->stream));
         RH_HIP(hipStreamWaitEvent(g->d2h_stream, g->evaluated, 0));
-        rc = rh_table_gather_watch(ed, g->wbdesc, g->wnblocks, g->d_watch, g->d_wcnt, g->d2h_stream);
+        rc = rh_table_gather_watch(ed, g->wbdesc, g->wnblocks, g->d_watch, g->d_wcnt, g->d2h_stream, lr);
         if (rc != RH_OK) return rc;
         RH_HIP(hipEventRecord(g->wdone, g->d2h_stream));
         RH_HIP(hipEventRecord(g->wgathered, g->d2h_stream));
         g->wgather_pending = true;
+        g->wgather_list = lr.rows != nullptr;
         hbm = false;
     } else if (hbm && g->event_sink == RH_EVENTS_AUTO) {   // contiguous HBM list: drained on the side stream
         RH_HIP(hipEventRecord(g->evaluated, g->ctx->stream));

@@ -180,6 +180,11 @@ struct TableEvents {
     // evaluation 4.5 us; the COMMIT records themselves 1.6 us of the 19.3.)
     uint32_t* bdesc = nullptr;
     uint32_t block_base = 0;
+    // REGION mode of the list kernel: descriptor gb = pass * grid + workgroup, wave w's masks at
+    // [1 + 4 w] (bit j: the wave's lane j's listed row in that pass) and [3 + 4 w] (COMMIT: watch-ALL
+    // changed; WATCH: valid), [2 + 4 w] = [4 + 4 w] = 0.  list_passes: the host's bound on the passes
+    // (rh::table_list_passes); descriptors of passes the evaluation does not run are zeroed.
+    uint32_t list_passes = 0;
 };
 // Tile-kernel workgroup: RH_TABLE_BLOCK_WAVES waves, one 128-row tile each.  REGION mode: records
 // per workgroup region (its rows) and u32 counts per workgroup descriptor (2 totals + 2 per wave).
@@ -204,6 +209,18 @@ struct TableLists {
 
 // Workgroups the table evaluation launches for a table (both width classes).
 uint32_t table_commit_blocks(const TableDev& t);
+// The list kernel's grid for `rows_hint` marked rows, a bound on its passes over lists of at most
+// `rows` entries (each pass: one entry per lane of every wave), and the most descriptors a
+// REGION-mode list evaluation of lists of capacity `cap` per region can write.
+uint32_t table_list_grid(uint64_t rows_hint);
+uint32_t table_list_passes(uint32_t grid, uint64_t rows);
+uint64_t table_list_desc_blocks(uint64_t cap);
+// A REGION-mode list evaluation's rows, for its gather: the list (entries per region: cap) and grid.
+struct ListRegion {
+    const uint32_t* rows = nullptr;   // null: a tile evaluation
+    uint32_t cap = 0;
+    uint32_t grid = 0;
+};
 
 }  // namespace rh
 
@@ -276,13 +293,16 @@ int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev, 
 // watch-ALL columns into the pinned lists adv_out / wall_out (device pointers; wall_out null: no
 // watch-ALL list), lengths to counts_out.  Nothing may write those columns between the evaluation
 // and this kernel (groups.cpp gather_fence).
+// A list evaluation's records (lr.rows set): the same, its rows from the list entries of the masks'
+// lanes -- nothing may append to that list either until the gather has run.
 int rh_table_gather_commit(const rh::TableDev& t, const uint32_t* bdesc, uint32_t n_blocks, rh_index_event* adv_out,
-                           rh_index_event* wall_out, uint64_t* counts_out, hipStream_t stream);
+                           rh_index_event* wall_out, uint64_t* counts_out, hipStream_t stream,
+                           const rh::ListRegion& lr = rh::ListRegion{});
 // REGION mode, WATCH: the level records (slot, valid, min, majority, max) of an evaluation rebuilt
 // the same way from the masks (changed rows, valid flags) and the row-slot / wmin / wmaj / wmax
 // columns into the pinned list `out` (device pointer), its length to counts_out[0].
 int rh_table_gather_watch(const rh::TableDev& t, const uint32_t* bdesc, uint32_t n_blocks, rh_watch_event* out,
-                          uint64_t* counts_out, hipStream_t stream);
+                          uint64_t* counts_out, hipStream_t stream, const rh::ListRegion& lr = rh::ListRegion{});
 int rh_table_drain(const uint64_t* counts, const void* a, void* a_out, const void* b, void* b_out, uint32_t rec_bytes0,
                    uint64_t cap, hipStream_t stream);
 // Initialises tiles [first_tile, n_tiles) of a tier as free rows (conf 0, row_slot kNoRow, clean).

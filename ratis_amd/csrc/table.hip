@@ -291,7 +291,7 @@ static_assert(kTRows <= rh::kTableRecs && 2 + 8 * kTWaves == rh::kTableDesc,
 #endif
 
 #ifndef RH_TABLE_ABL   // ablation only (wrong results): 2 = no events, 3 = no table stores, 4 = trivial arithmetic
-#define RH_TABLE_ABL 0
+#define RH_TABLE_ABL 0   // list kernel: 6 / 7 = 5 / 3 lines per row, 8 = no counter atomic or records, 9 = 6 + 8
 #endif
 
 template <typename V>
@@ -677,14 +677,23 @@ __device__ __forceinline__ void list_row(const TableDev& T, const TableTier& tt,
                                          bool wlisted, bool& e0, bool& e1, bool& wtrans, int64_t& x0, int64_t& x1,
                                          int64_t& x2, uint32_t& valid, uint32_t& slot) {
     int64_t vals[F + 1];
-#pragma unroll
-    for (int k = 0; k < F; ++k) vals[k] = *tt.i64(WATCH ? tile::fcommit(F, k) : tile::match(k), r);
     const uint32_t w = *tt.u32(tile::kConf, r);
     slot = *tt.u32(tile::kSlot, r);
     const int64_t cm = *tt.i64(tile::commit(F), r);
+#if RH_TABLE_ABL == 6 || RH_TABLE_ABL == 7 || RH_TABLE_ABL == 9   // ablation (wrong results): a row's lines cut to conf, slot, commit (+ flags)
+#pragma unroll
+    for (int k = 0; k < F; ++k) vals[k] = cm + k;
+#else
+#pragma unroll
+    for (int k = 0; k < F; ++k) vals[k] = *tt.i64(WATCH ? tile::fcommit(F, k) : tile::match(k), r);
+#endif
     // the row's commitIndexChanged flag, read with its columns: a listed row is in this list once,
     // so its lane alone may set the flag here (plain store; no atomic to find the transition)
+#if RH_TABLE_ABL == 7
+    const uint8_t wd = 0;
+#else
     const uint8_t wd = WATCH ? 0 : *tt.u8(tile::kWdirty, r);
+#endif
     int64_t self, ts = 0, p0 = 0, p1 = 0, p2 = 0;
     if (WATCH) {
         self = cm;  // lastCommittedIndex is the self value (LSI:613)
@@ -692,9 +701,13 @@ __device__ __forceinline__ void list_row(const TableDev& T, const TableTier& tt,
         p1 = *tt.i64(tile::wmaj(F), r);
         p2 = *tt.i64(tile::wmax(F), r);
     } else {
+#if RH_TABLE_ABL == 6 || RH_TABLE_ABL == 7 || RH_TABLE_ABL == 9
+        self = cm + 7, ts = 0, p0 = cm;
+#else
         self = *tt.i64(tile::flush(F), r);
         ts = *tt.i64(tile::tstart(F), r);
         if (wall_on) p0 = *tt.i64(tile::wall(F), r);
+#endif
     }
     vals[F] = self;
     const bool trans = (w & RH_CONF_ACTIVE) && (w & RH_CONF_TRANSITIONAL);   // lane-local: always exact
@@ -716,7 +729,9 @@ __device__ __forceinline__ void list_row(const TableDev& T, const TableTier& tt,
         e0 = rh_eval::commit_decision(v, mj, cm, self, ts, nc);
         e1 = wall_on && mn != p0;  // watch-ALL level changed (LSI:1025)
         x0 = nc, x1 = mn, x2 = 0;
+#if RH_TABLE_ABL != 7
         *tt.u8(tile::kDirty, r) = 0;
+#endif
         if (e0) {
             *tt.i64(tile::commit(F), r) = nc;
             // the commit index changed: commitIndexChanged follows (listed if the flag was clear)
@@ -733,6 +748,17 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
     for (int d = 1; d < 64; d <<= 1) v = max(v, (uint32_t)__shfl_xor((int)v, d));
     return v;
 }
+
+// REGION mode: this workgroup's descriptors of passes [from, list_passes) -- passes the evaluation
+// does not run -- zeroed, so the gather (launched over the host's bound) finds no events there.
+__device__ __forceinline__ void zero_list_desc(const TableEvents& ev, uint32_t from) {
+    constexpr uint32_t S = rh::kTableDesc / 2;
+    uint64_t* d = reinterpret_cast<uint64_t*>(ev.bdesc);
+    const uint32_t n = ev.list_passes > from ? (ev.list_passes - from) * S : 0u;
+    for (uint32_t j = threadIdx.x; j < n; j += blockDim.x)
+        d[((uint64_t)(from + j / S) * gridDim.x + blockIdx.x) * S + j % S] = 0ull;
+}
+static_assert(kListWaves == kTWaves, "REGION mode: a list workgroup's masks fill a tile workgroup's descriptor");
 
 template <bool WATCH>
 __global__ __launch_bounds__(kListWaves * 64) void table_list_kernel(TableDev Targ, TableLists L, TableLists Lw, TableEvents ev) {
@@ -803,8 +829,10 @@ __global__ __launch_bounds__(kListWaves * 64) void table_list_kernel(TableDev Ta
     const uint64_t R = ev.cap;
     const bool wall_on = !WATCH && ev.wall != nullptr;
     const bool wl = Lw.rows != nullptr;
+    const bool region = ev.bdesc != nullptr;   // REGION mode (kernel argument: uniform)
     if (active == 0) {   // empty lists
-        if (blockIdx.x == 0 && threadIdx.x == 0) publish_counts(ev, 0ull);
+        if (region) zero_list_desc(ev, 0);
+        else if (blockIdx.x == 0 && threadIdx.x == 0) publish_counts(ev, 0ull);
         return;
     }
     for (uint32_t pass = 0; pass < np; ++pass) {
@@ -831,6 +859,29 @@ __global__ __launch_bounds__(kListWaves * 64) void table_list_kernel(TableDev Ta
         }
         // events: one range of the lists per workgroup and pass
         const uint64_t a = __ballot(e0), c = WATCH ? 0ull : __ballot(e1);
+        if (region) {
+            // no records, no counter atomic: the wave's masks (COMMIT: advanced, watch-ALL changed;
+            // WATCH: changed, valid) and the workgroup's totals into its descriptor of this pass --
+            // rh_table_gather_commit / _watch rebuild the records from the list entries and the table
+            const uint64_t cv = WATCH ? __ballot(e0 && valid != 0u) : c;
+            const bool rec = pass < ev.list_passes;   // the host's bound: never exceeded
+            uint64_t* md = reinterpret_cast<uint64_t*>(ev.bdesc) + ((uint64_t)pass * gridDim.x + blockIdx.x) * (rh::kTableDesc / 2);
+            if (rec && lane < 4) md[1 + 4 * wave + lane] = lane == 0 ? a : (lane == 2 ? cv : 0ull);
+            if (lane == 0) {
+                wcnt[0][wave] = (uint32_t)__popcll(a);
+                wcnt[1][wave] = (uint32_t)__popcll(c);
+            }
+            __syncthreads();
+            if (!WATCH && wl) list_append(Lw, wtrans, t, row, h);   // kernel argument: uniform
+            if (threadIdx.x == 0 && rec) {
+                unsigned long long s0 = 0, s1 = 0;
+#pragma unroll
+                for (uint32_t q = 0; q < kListWaves; ++q) s0 += wcnt[0][q], s1 += wcnt[1][q];
+                md[0] = s0 | (s1 << 32);
+            }
+            if (pass + 1 < np) __syncthreads();   // wcnt is the next pass's (np: uniform)
+            continue;
+        }
         if (lane == 0) {
             wcnt[0][wave] = (uint32_t)__popcll(a);
             wcnt[1][wave] = (uint32_t)__popcll(c);
@@ -845,9 +896,15 @@ __global__ __launch_bounds__(kListWaves * 64) void table_list_kernel(TableDev Ta
             for (uint32_t q = 0; q < kListWaves; ++q) s0 += wcnt[0][q], s1 += wcnt[1][q];
             const uint32_t cb = ev.cbits;
             const unsigned long long add = s0 | (s1 << cb) | (last ? 1ull << (2 * cb) : 0ull);
+#if RH_TABLE_ABL == 8 || RH_TABLE_ABL == 9   // ablation (wrong results): no counter atomic, no records
+            const unsigned long long old = 0ull;
+            if (blockIdx.x == 0) publish_counts(ev, 0ull);
+            if (false) {
+#else
             const unsigned long long old = add ? atomicAdd(ev.cnt, add) : 0ull;
             lbase = old;
             if (last && ((old + add) >> (2 * cb)) == active) {   // every workgroup holding entries has counted
+#endif
                 publish_counts(ev, old + add);
                 atomicExch(ev.cnt, 0ull);   // the next evaluation's counter
             }
@@ -857,6 +914,9 @@ __global__ __launch_bounds__(kListWaves * 64) void table_list_kernel(TableDev Ta
         uint32_t b0 = (uint32_t)(lbase & cm), b1 = (uint32_t)((lbase >> ev.cbits) & cm);
         for (int q = 0; q < wave; ++q) b0 += wcnt[0][q], b1 += wcnt[1][q];
         if (pass + 1 < np) __syncthreads();   // wcnt / lbase are the next pass's (np: uniform)
+#if RH_TABLE_ABL == 8 || RH_TABLE_ABL == 9
+        continue;
+#endif
         if (e0) {
             const uint64_t kk = b0 + (uint64_t)__popcll(a & lt);
             if (kk < R) {
@@ -871,6 +931,7 @@ __global__ __launch_bounds__(kListWaves * 64) void table_list_kernel(TableDev Ta
             if (kk < R) ev.wall[kk] = rh_index_event{slot, 0u, x1};
         }
     }
+    if (region) zero_list_desc(ev, np);
 }
 
 // ---- hasLease over every started row -------------------------------------------------------------
@@ -1034,15 +1095,30 @@ int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev_i
 constexpr uint32_t kListMinGrid = RH_LIST_MIN_GRID;
 static_assert(kListMinGrid >= rh::kHeads, "a workgroup per list region at least");
 
+uint32_t rh::table_list_grid(uint64_t rows_hint) {
+    const uint64_t want = (rows_hint + (uint64_t)RH_LIST_ROWS_PER_WAVE * kListWaves - 1) / ((uint64_t)RH_LIST_ROWS_PER_WAVE * kListWaves);
+    return (uint32_t)std::min<uint64_t>(kListMaxGrid, std::max<uint64_t>(kListMinGrid, want));
+}
+
+// A region r's entries are dealt over its Wr = (W - r + 7) / 8 >= W / 8 waves, 64 per wave and pass.
+uint32_t rh::table_list_passes(uint32_t grid, uint64_t rows) {
+    const uint64_t per_pass = 64ull * ((uint64_t)grid * kListWaves / rh::kHeads);
+    return (uint32_t)((rows + per_pass - 1) / per_pass);
+}
+
+uint64_t rh::table_list_desc_blocks(uint64_t cap) {
+    uint64_t most = 0;
+    for (uint32_t g = kListMinGrid; g <= kListMaxGrid; ++g) most = std::max<uint64_t>(most, (uint64_t)g * table_list_passes(g, cap));
+    return most;
+}
+
 int rh_table_commit_lists(const rh::TableDev& t, int mode, const rh::TableLists& l, const rh::TableLists& lw,
                           const rh::TableEvents& ev_in, hipStream_t stream, hipEvent_t t0, hipEvent_t t1,
                           uint64_t rows_hint) {
     // the listed rows are dealt lane-major over every wave of a near-chip-wide grid: a few rows per
     // wave on ~every CU (random rows: the chain of dependent loads is latency-bound per CU, so the
     // rows are spread, not packed into few waves)
-    const uint64_t want = (rows_hint + (uint64_t)RH_LIST_ROWS_PER_WAVE * kListWaves - 1) / ((uint64_t)RH_LIST_ROWS_PER_WAVE * kListWaves);
-    const uint32_t grid = (uint32_t)std::min<uint64_t>(kListMaxGrid, std::max<uint64_t>(kListMinGrid, want));
-    const dim3 g(grid), b(kListWaves * 64);
+    const dim3 g(rh::table_list_grid(rows_hint)), b(kListWaves * 64);
     rh::TableEvents ev = ev_in;
     hipError_t e;
     if (mode == RH_MODE_WATCH)
@@ -1101,6 +1177,7 @@ struct GatherRowsArgs {
     void* a;                // rh_index_event (updateCommit) / rh_watch_event (commitIndexChanged) list
     rh_index_event* b;      // updateCommit's watch-ALL list (null: none)
     uint64_t* counts_out;
+    rh::ListRegion lr;      // a list evaluation's (rows null: a tile evaluation)
 };
 
 template <bool WATCH>
@@ -1164,6 +1241,29 @@ __global__ __launch_bounds__(256) void table_gather_rows_kernel(GatherRowsArgs a
         const uint64_t* m = A.desc + (uint64_t)gb * S + 1 + 4 * w;
         const uint64_t a0 = m[0], a1 = m[1], c0 = (WATCH || has_b) ? m[2] : 0ull, c1 = (WATCH || has_b) ? m[3] : 0ull;
         if (!(a0 | a1 | (WATCH ? 0ull : (c0 | c1)))) continue;
+        if (A.lr.rows) {   // a list evaluation: lane j's listed row of that wave and pass (a1 = c1 = 0)
+            const bool e0 = (a0 >> lane) & 1u, e1 = !WATCH && ((c0 >> lane) & 1u);
+            if (!(e0 || e1)) continue;
+            const uint32_t pass = gb / A.lr.grid, wg = (gb % A.lr.grid) * kListWaves + w;
+            const uint32_t W = A.lr.grid * kListWaves, r = wg % rh::kHeads, k = wg / rh::kHeads;
+            const uint32_t Wr = (W - r + rh::kHeads - 1) / rh::kHeads;
+            const uint32_t ent = A.lr.rows[(uint64_t)r * A.lr.cap + (pass * 64u + lane) * Wr + k];
+            const TableTier& tt = A.t.tier[(ent >> 28) < (uint32_t)rh::kTableTiers ? (ent >> 28) : 0u];
+            const uint32_t row = ent & rh::kRowMask, F = tt.width;
+            const uint32_t sl = *tt.u32(rh::tile::kSlot, row);
+            if (WATCH) {
+                rh_watch_event* out = static_cast<rh_watch_event*>(A.a);
+                out[p0 + pre[0][c] + (uint64_t)__popcll(a0 & lt)] =
+                    rh_watch_event{sl, (uint32_t)((c0 >> lane) & 1u), *tt.i64(rh::tile::wmin(F), row),
+                                   *tt.i64(rh::tile::wmaj(F), row), *tt.i64(rh::tile::wmax(F), row)};
+            } else {
+                if (e0)
+                    static_cast<rh_index_event*>(A.a)[p0 + pre[0][c] + (uint64_t)__popcll(a0 & lt)] =
+                        rh_index_event{sl, 0u, *tt.i64(rh::tile::commit(F), row)};
+                if (e1) A.b[p1 + pre[1][c] + (uint64_t)__popcll(c0 & lt)] = rh_index_event{sl, 0u, *tt.i64(rh::tile::wall(F), row)};
+            }
+            continue;
+        }
         const int cls = gb < A.cls1_base ? 0 : 1;
         const uint32_t b = gb - (cls ? A.cls1_base : 0u);
         const TierRange& tr = A.tr[cls];
@@ -1206,13 +1306,18 @@ __global__ __launch_bounds__(256) void table_gather_rows_kernel(GatherRowsArgs a
 }
 
 static int gather_rows(bool watch, const rh::TableDev& t, const uint32_t* bdesc, uint32_t n_blocks, void* a,
-                       rh_index_event* b, uint64_t* counts_out, hipStream_t stream) {
+                       rh_index_event* b, uint64_t* counts_out, hipStream_t stream, const rh::ListRegion& lr) {
     if (n_blocks == 0) return rh::fail(RH_E_INVAL, "rh_table_gather_rows: no workgroups");
     GatherRowsArgs g{};
     g.t = t;
-    const uint32_t b0 = tier_range(t, 0, g.tr[0]), b1 = tier_range(t, 1, g.tr[1]);
-    if (b0 + b1 != n_blocks) return rh::fail(RH_E_STATE, "rh_table_gather_rows: workgroups differ from the evaluation's");
-    g.cls1_base = b0;
+    g.lr = lr;
+    if (lr.rows) {   // descriptors: passes x the list grid
+        if (lr.grid == 0 || n_blocks % lr.grid) return rh::fail(RH_E_STATE, "rh_table_gather_rows: descriptors differ from the list grid's");
+    } else {
+        const uint32_t b0 = tier_range(t, 0, g.tr[0]), b1 = tier_range(t, 1, g.tr[1]);
+        if (b0 + b1 != n_blocks) return rh::fail(RH_E_STATE, "rh_table_gather_rows: workgroups differ from the evaluation's");
+        g.cls1_base = b0;
+    }
     g.n_blocks = n_blocks;
     g.desc = reinterpret_cast<const uint64_t*>(bdesc);
     g.a = a;
@@ -1228,13 +1333,13 @@ static int gather_rows(bool watch, const rh::TableDev& t, const uint32_t* bdesc,
 }
 
 int rh_table_gather_commit(const rh::TableDev& t, const uint32_t* bdesc, uint32_t n_blocks, rh_index_event* adv_out,
-                           rh_index_event* wall_out, uint64_t* counts_out, hipStream_t stream) {
-    return gather_rows(false, t, bdesc, n_blocks, adv_out, wall_out, counts_out, stream);
+                           rh_index_event* wall_out, uint64_t* counts_out, hipStream_t stream, const rh::ListRegion& lr) {
+    return gather_rows(false, t, bdesc, n_blocks, adv_out, wall_out, counts_out, stream, lr);
 }
 
 int rh_table_gather_watch(const rh::TableDev& t, const uint32_t* bdesc, uint32_t n_blocks, rh_watch_event* out,
-                          uint64_t* counts_out, hipStream_t stream) {
-    return gather_rows(true, t, bdesc, n_blocks, out, nullptr, counts_out, stream);
+                          uint64_t* counts_out, hipStream_t stream, const rh::ListRegion& lr) {
+    return gather_rows(true, t, bdesc, n_blocks, out, nullptr, counts_out, stream, lr);
 }
 
 int rh_table_init_tiles(const rh::TableTier& t, uint32_t first_tile, uint32_t n_tiles, hipStream_t stream) {

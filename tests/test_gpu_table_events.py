@@ -206,19 +206,21 @@ def test_node_watch_levels_and_lease_over_four_shards(ctx, orc):
         assert bits.shape == (4 * cap,) and not bits.any()
 
 
-@pytest.mark.parametrize("seed", [3, 4])
-def test_list_and_tile_evaluations_interleaved(ctx, orc, seed):
+@pytest.mark.parametrize("seed,sink", [(3, "auto"), (4, "device")])
+def test_list_and_tile_evaluations_interleaved(ctx, orc, seed, sink):
     """Sparse pushes run over the dirty-row lists (list mode), dense ones over every tile: steps of
     either kind, follower-commit-only steps (commitIndexChanged from the watch list), control ops
     (which give the lists up until the next evaluation) and the zero-copy ring, all against the
-    model -- and both modes must actually run."""
-    from ratis_amd import groups
+    model -- and both modes must actually run.  DEVICE runs every list evaluation in REGION mode
+    (masks per wave and pass, records rebuilt from the list entries by the gather)."""
+    from ratis_amd import _lib, groups
     rng = np.random.default_rng(seed)
     n = 50_000
     model = TableModel(n)
     tab, n = _loaded(ctx, model, n, seed=seed + 10)
     modes = {"commit": set(), "watch": set()}
     try:
+        tab.set_event_sink({"device": _lib.RH_EVENTS_DEVICE, "auto": _lib.RH_EVENTS_AUTO}[sink])
         tab.set_timing(True)
         compare(tab, model, orc, columns=False)
         live = np.arange(n)
@@ -259,16 +261,18 @@ def test_list_and_tile_evaluations_interleaved(ctx, orc, seed):
         tab.close()
 
 
-def test_list_mode_over_every_width(ctx, orc):
+@pytest.mark.parametrize("sink", ["auto", "device"])
+def test_list_mode_over_every_width(ctx, orc, sink):
     """List entries carry their tier ((tier << 28) | row) and a wave's lanes may hold rows of
     different widths: a table started over every width (1..14 followers, some in joint consensus)
     gets sparse pushes that run in list mode -- commit and commitIndexChanged -- against the model,
     with a control op between two of them (lists given up once, then list mode again)."""
-    from ratis_amd import groups
+    from ratis_amd import _lib, groups
     rng = np.random.default_rng(77)
     n = 4000
     model = TableModel(n)
     with groups.RaftGroupTable(ctx, capacity=n) as tab:
+        tab.set_event_sink({"device": _lib.RH_EVENTS_DEVICE, "auto": _lib.RH_EVENTS_AUTO}[sink])
         tab.set_timing(True)
         for s in range(n):
             F = 1 + s % 14
@@ -308,6 +312,40 @@ def test_list_mode_over_every_width(ctx, orc):
         assert all(m == (True, True) for i, m in enumerate(modes) if i not in (3, 4)), modes
         for col in [0, 1, 7, 13, 16, 29, 32, 33]:
             assert np.array_equal(tab.read(col), model.column(col)), col
+
+
+def test_list_region_mode_many_marks(ctx, orc):
+    """AUTO list evaluations of at least 8192 marked rows run in REGION mode (groups.cpp evaluate):
+    masks per wave and pass, the records rebuilt by the gather from the list entries.  On 1.5M
+    rows (list capacity 46,875 per region) 45,000 deltas need two passes of the 480-wave list grid
+    (3,840 entries per region and pass, ~4,500 updateCommit marks per region); 9,000 one pass; 500
+    the pinned lists (counter mode).  Against the model, commit and commitIndexChanged."""
+    rng = np.random.default_rng(515)
+    n = 1_500_000
+    model = TableModel(n)
+    tab, n = _loaded(ctx, model, n, seed=51)
+    try:
+        tab.set_timing(True)
+        compare(tab, model, orc, columns=False)   # after the load: tile evaluations
+        live = np.arange(n)
+        for k in (45_000, 9_000, 500, 45_000):
+            d = random_deltas(rng, model, live, k)
+            tab.push(d)
+            model.apply(d)
+            got = tab.update_commit()
+            assert tab.last_was_list(), k
+            a_s, a_c, w_s, w_m = model.commit_batch(orc)
+            assert np.array_equal(got.advanced_slots, a_s) and np.array_equal(got.advanced_commit, a_c), k
+            assert np.array_equal(got.watch_all_slots, w_s) and np.array_equal(got.watch_all_min, w_m), k
+            ev = tab.commit_index_changed()
+            m_s, m_lev, m_valid = model.watch(orc)
+            assert np.array_equal(ev["slot"].astype(np.int64), m_s), k
+            assert np.array_equal(ev["min"], m_lev[0]) and np.array_equal(ev["majority"], m_lev[1]), k
+            assert np.array_equal(ev["max"], m_lev[2]) and np.array_equal(ev["valid"].astype(bool), m_valid), k
+        for col in [0, 1, 16, 32, 33]:
+            assert np.array_equal(tab.read(col), model.column(col)), col
+    finally:
+        tab.close()
 
 
 def test_separate_done_word_of_large_tables(ctx, orc, monkeypatch):
