@@ -61,8 +61,11 @@ __device__ __forceinline__ const T& kernarg_struct() {
 //   [256, 384)    lon      u8    LeaderLease.enabled
 //   [512, 1024)   conf     u32   membership word (0 on free rows)
 //   [1024, 1536)  row_slot u32   row -> slot (kNoRow on free rows)
-//   then int64 columns of 1 KiB each:
+//   then int64 columns of 1 KiB each, addressed by these offsets (tile::match(k) ...):
 //   match[F] flush tstart commit wall | fcommit[F] wmin wmaj wmax | fts[F] lease
+//   and stored (tile::pair_off) as the commit column, then three sections of records of
+//   kGroupRows rows: [match[F] flush tstart wall] [fcommit[F] wmin wmaj wmax] [fts[F] lease] --
+//   each section still one contiguous run per tile.
 //
 // COMMIT reads dirty + [conf .. wall] (one run), WATCH wdirty + conf, row_slot, commit, fcommit..wmax,
 // the lease pass conf + fts + lease.  slot_map: slot -> (tier << 28) | row, kNoRow = stopped.
@@ -90,6 +93,32 @@ __host__ __device__ constexpr uint32_t wmax(uint32_t F) { return wmin(F) + 2048u
 __host__ __device__ constexpr uint32_t fts(uint32_t F, uint32_t k) { return kMatch + 1024u * (2 * F + 7 + k); }
 __host__ __device__ constexpr uint32_t lease(uint32_t F) { return fts(F, F); }
 __host__ __device__ constexpr uint32_t bytes(uint32_t F) { return kMatch + 1024u * (3 * F + 8); }
+// Byte offset in a tile of the 16 bytes that hold rows 2p and 2p + 1 of the int64 column at tile
+// offset `off` (a match / flush / ... offset above; row 2p + 1 at + 8).  Round 5: the commit column
+// stays a column (both evaluations read it); the others are grouped in three sections --
+// [match[F] flush tstart wall] | [fcommit[F] wmin wmaj wmax] | [fts[F] lease] -- each stored as
+// records of kGroupRows rows (per record: each column's kGroupRows values in turn), so a row's
+// updateCommit inputs are F + 3 values kGroupRows x 8 bytes apart instead of 1 KiB apart (list
+// mode: fewer random lines per row), while a tile wave still reads each section as one contiguous
+// run.  kGroupRows = 128 is the plain column layout.
+#ifndef RH_TABLE_GROUP
+#define RH_TABLE_GROUP 128
+#endif
+constexpr uint32_t kGroupRows = RH_TABLE_GROUP;
+static_assert(kGroupRows >= 2 && kGroupRows <= 128 && (kGroupRows & (kGroupRows - 1)) == 0, "a power of two");
+__host__ __device__ constexpr uint32_t pair_off(uint32_t F, uint32_t off, uint32_t p) {
+    const uint32_t c = (off - kMatch) >> 10;   // int64 column index in the tile:: order
+    const uint32_t r = 2u * p;
+    if (c == F + 2) return kMatch + 16u * p;   // commit
+    const uint32_t base = c < F + 4 ? kMatch + 1024u : c < 2 * F + 7 ? kMatch + 1024u * (F + 4) : kMatch + 1024u * (2 * F + 7);
+    const uint32_t ns = c < 2 * F + 7 ? F + 3 : F + 1;
+    const uint32_t j = c < F + 2 ? c : c < F + 4 ? c - 1 : c < 2 * F + 7 ? c - (F + 4) : c - (2 * F + 7);
+    return base + (r / kGroupRows) * (kGroupRows * 8u * ns) + j * 8u * kGroupRows + 8u * (r % kGroupRows);
+}
+// Byte offset in a tile of element r (0..127) of the column at tile offset `off`, element size sz.
+__host__ __device__ constexpr uint32_t elem_off(uint32_t F, uint32_t off, uint32_t r, uint32_t sz) {
+    return off >= kMatch ? pair_off(F, off, r >> 1) + 8u * (r & 1u) : off + r * sz;
+}
 }  // namespace tile
 
 struct TableTier {
@@ -104,12 +133,14 @@ struct TableTier {
     // element `r` of the column at tile offset `off` (element size sizeof(T))
     template <typename T>
     __host__ __device__ T* at(uint32_t off, uint64_t r) const {
-        return reinterpret_cast<T*>(base + (r >> 7) * (uint64_t)tile::bytes(width) + off + (r & 127) * sizeof(T));
+        return reinterpret_cast<T*>(base + (r >> 7) * (uint64_t)tile::bytes(width) +
+                                    tile::elem_off(width, off, (uint32_t)(r & 127), (uint32_t)sizeof(T)));
     }
     // the order key of the delta target at tile offset `off` (int64 column, or tile::kLon)
     __host__ __device__ unsigned long long* key(uint32_t off, uint64_t r) const {
         const uint32_t o = off == tile::kLon ? tile::kConf : off;
-        return reinterpret_cast<unsigned long long*>(shadow + (r >> 7) * (uint64_t)tile::bytes(width) + o + (r & 127) * 8);
+        return reinterpret_cast<unsigned long long*>(shadow + (r >> 7) * (uint64_t)tile::bytes(width) +
+                                                     tile::elem_off(width, o, (uint32_t)(r & 127), 8u));
     }
     __host__ __device__ int64_t* i64(uint32_t off, uint64_t r) const { return at<int64_t>(off, r); }
     __host__ __device__ uint32_t* u32(uint32_t off, uint64_t r) const { return at<uint32_t>(off, r); }

@@ -294,6 +294,12 @@ static_assert(kTRows <= rh::kTableRecs && 2 + 8 * kTWaves == rh::kTableDesc,
 #define RH_TABLE_ABL 0   // list kernel: 6 / 7 = 5 / 3 lines per row, 8 = no counter atomic or records, 9 = 6 + 8
 #endif
 
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) const void gbl_void_t;
+#ifndef RH_TABLE_STAGE   // A/B: SPEC evaluations stage their section through LDS (1) or load per lane (0)
+#define RH_TABLE_STAGE 0
+#endif
+
 template <typename V>
 __device__ __forceinline__ V tload(const uint8_t* p) {
     if (RH_TABLE_NT) return __builtin_nontemporal_load(reinterpret_cast<const V*>(p));
@@ -319,7 +325,7 @@ struct Stage {
 // lines loaded): hence the host's choice.
 template <int F, bool RANK, bool WATCH, bool SPEC>
 __device__ __forceinline__ void table_wave(const TableDev& T, const TableTier& tt, uint64_t tl, bool wall_on,
-                                           unsigned char* stage, Stage& sc, const TableEvents& ev, uint64_t gb) {
+                                           unsigned char* ws, Stage& sc, const TableEvents& ev, uint64_t gb) {
     constexpr int N = F + 1;
     constexpr uint64_t TB = tile::bytes(F);
     const int lane = threadIdx.x & 63;
@@ -337,17 +343,42 @@ __device__ __forceinline__ void table_wave(const TableDev& T, const TableTier& t
     int64_t fv[2][F], self[2] = {0, 0}, cin[2] = {0, 0}, ts[2] = {0, 0};
     int64_t p0[2] = {0, 0}, p1[2] = {0, 0}, p2[2] = {0, 0};
     uint32_t w[2] = {0u, 0u}, slot[2] = {0u, 0u};
-    const uint32_t l16 = 16u * lane, l8 = 8u * lane;
+    const uint32_t l8 = 8u * lane;
     if (SPEC || need) {  // every load of the row pair is issued before any result is used
+        // the lane's row-pair record of its evaluation's section (rh_internal.h, tile::pair_off):
+        // [match[F] flush tstart wall] or [fcommit[F] wmin wmaj wmax], NS 16-byte pairs
+        constexpr uint32_t NS = F + 3;
+        constexpr uint32_t c0 = WATCH ? tile::fcommit(F, 0) : tile::match(0);
+        constexpr uint32_t s0 = tile::pair_off(F, c0, 0);
+        const uint8_t* sb = tb + s0;   // the section: in the tile, or staged in LDS
+#if RH_TABLE_STAGE
+        if constexpr (SPEC) {
+            // nearly every row pair is dirty: the section moves as one coalesced run into the wave's
+            // LDS region (LDS-DMA, 64 x 16 B per instruction), each lane then reads its record --
+            // NS odd: 16-byte reads at a stride of NS x 16 B hit every bank group once per 16 lanes
+#pragma unroll
+            for (uint32_t i = 0; i < NS; ++i)
+                __builtin_amdgcn_global_load_lds((gbl_void_t*)(tb + s0 + 1024u * i + 16u * lane), (lds_void_t*)(ws + 1024u * i), 16, 0, 0);
+        }
+#endif
+        const v2u32 c = tload<v2u32>(tb + tile::kConf + l8);
+        const v2u32 sl = tload<v2u32>(tb + tile::kSlot + l8);
+        const v2i64 cm = tload<v2i64>(tb + tile::pair_off(F, tile::commit(F), lane));
+#if RH_TABLE_STAGE
+        if constexpr (SPEC) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the wave's LDS-DMA has landed
+            sb = ws;
+        }
+#endif
+        auto sec = [&](uint32_t col) {   // the lane's row pair of column col
+            return *reinterpret_cast<const v2i64*>(sb + (tile::pair_off(F, col, lane) - s0));
+        };
 #pragma unroll
         for (int k = 0; k < F; ++k) {
-            const v2i64 x = tload<v2i64>(tb + (WATCH ? tile::fcommit(F, k) : tile::match(k)) + l16);
+            const v2i64 x = sec(WATCH ? tile::fcommit(F, k) : tile::match(k));
             fv[0][k] = x.x;
             fv[1][k] = x.y;
         }
-        const v2u32 c = tload<v2u32>(tb + tile::kConf + l8);
-        const v2u32 sl = tload<v2u32>(tb + tile::kSlot + l8);
-        const v2i64 cm = tload<v2i64>(tb + tile::commit(F) + l16);
         slot[0] = sl.x;
         slot[1] = sl.y;
         w[0] = d0 ? c.x : 0u;  // a clean row is evaluated as inactive and produces nothing
@@ -357,16 +388,16 @@ __device__ __forceinline__ void table_wave(const TableDev& T, const TableTier& t
         if (WATCH) {
             self[0] = cm.x;  // lastCommittedIndex is the self value (LSI:613)
             self[1] = cm.y;
-            const v2i64 a = tload<v2i64>(tb + tile::wmin(F) + l16);
-            const v2i64 b = tload<v2i64>(tb + tile::wmaj(F) + l16);
-            const v2i64 e = tload<v2i64>(tb + tile::wmax(F) + l16);
+            const v2i64 a = sec(tile::wmin(F));
+            const v2i64 b = sec(tile::wmaj(F));
+            const v2i64 e = sec(tile::wmax(F));
             p0[0] = a.x, p0[1] = a.y, p1[0] = b.x, p1[1] = b.y, p2[0] = e.x, p2[1] = e.y;
         } else {
-            const v2i64 fl = tload<v2i64>(tb + tile::flush(F) + l16);
-            const v2i64 st = tload<v2i64>(tb + tile::tstart(F) + l16);
+            const v2i64 fl = sec(tile::flush(F));
+            const v2i64 st = sec(tile::tstart(F));
             self[0] = fl.x, self[1] = fl.y, ts[0] = st.x, ts[1] = st.y;
             if (wall_on) {  // watch-ALL levels are compared only when reported (RH_COMMIT_WATCH_ALL)
-                const v2i64 wa = tload<v2i64>(tb + tile::wall(F) + l16);
+                const v2i64 wa = sec(tile::wall(F));
                 p0[0] = wa.x, p0[1] = wa.y;
             }
         }
@@ -427,16 +458,16 @@ __device__ __forceinline__ void table_wave(const TableDev& T, const TableTier& t
         const uint32_t ro = 2u * lane + g;
         if (WATCH) {
             if (e0[g]) {
-                reinterpret_cast<int64_t*>(tb + tile::wmin(F))[ro] = x0[g];
-                reinterpret_cast<int64_t*>(tb + tile::wmaj(F))[ro] = x1[g];
-                reinterpret_cast<int64_t*>(tb + tile::wmax(F))[ro] = x2[g];
+                *reinterpret_cast<int64_t*>(tb + tile::pair_off(F, tile::wmin(F), lane) + 8u * g) = x0[g];
+                *reinterpret_cast<int64_t*>(tb + tile::pair_off(F, tile::wmaj(F), lane) + 8u * g) = x1[g];
+                *reinterpret_cast<int64_t*>(tb + tile::pair_off(F, tile::wmax(F), lane) + 8u * g) = x2[g];
             }
         } else {
             if (e0[g]) {
-                reinterpret_cast<int64_t*>(tb + tile::commit(F))[ro] = x0[g];
+                *reinterpret_cast<int64_t*>(tb + tile::pair_off(F, tile::commit(F), lane) + 8u * g) = x0[g];
                 tb[tile::kWdirty + ro] = 1;  // the commit index changed: commitIndexChanged follows (LSI:1003)
             }
-            if (e1[g]) reinterpret_cast<int64_t*>(tb + tile::wall(F))[ro] = x1[g];
+            if (e1[g]) *reinterpret_cast<int64_t*>(tb + tile::pair_off(F, tile::wall(F), lane) + 8u * g) = x1[g];
         }
     }
     if (!WATCH && (a0 | a1) && lane == 0) tt.sum[2 * tl + 1] = 1;
@@ -472,13 +503,13 @@ __device__ __forceinline__ void table_wave(const TableDev& T, const TableTier& t
             }
         }
     } else if (WATCH) {
-        rh_watch_event* sw = reinterpret_cast<rh_watch_event*>(stage) + wave * 128;
+        rh_watch_event* sw = reinterpret_cast<rh_watch_event*>(ws);   // this wave's LDS region
 #pragma unroll
         for (int g = 0; g < 2; ++g)
             if (e0[g]) sw[p++] = rh_watch_event{slot[g], valid[g], x0[g], x1[g], x2[g]};
     } else {
-        rh_index_event* sa = reinterpret_cast<rh_index_event*>(stage) + wave * 128;
-        rh_index_event* sw = sa + kTRows;
+        rh_index_event* sa = reinterpret_cast<rh_index_event*>(ws);   // this wave's LDS region
+        rh_index_event* sw = sa + 128;
         const uint64_t c0 = __ballot(e1[0]), c1 = __ballot(e1[1]);
         uint32_t q = (uint32_t)(__popcll(c0 & lt) + __popcll(c1 & lt));
 #pragma unroll
@@ -493,12 +524,17 @@ __device__ __forceinline__ void table_wave(const TableDev& T, const TableTier& t
 
 template <int F, int FHI, bool RANK, bool WATCH, bool SPEC>
 __device__ __forceinline__ void table_dispatch(const TableDev& T, int t, uint64_t tl, bool wall_on,
-                                               unsigned char* stage, Stage& sc, const TableEvents& ev, uint64_t gb) {
+                                               unsigned char* ws, Stage& sc, const TableEvents& ev, uint64_t gb) {
     if ((int)rh::width_of_tier(t) == F)
-        table_wave<F, RANK, WATCH, SPEC>(T, T.tier[t], tl, wall_on, stage, sc, ev, gb);
+        table_wave<F, RANK, WATCH, SPEC>(T, T.tier[t], tl, wall_on, ws, sc, ev, gb);
     else if constexpr (F + 2 <= FHI)
-        table_dispatch<F + 2, FHI, RANK, WATCH, SPEC>(T, t, tl, wall_on, stage, sc, ev, gb);
+        table_dispatch<F + 2, FHI, RANK, WATCH, SPEC>(T, t, tl, wall_on, ws, sc, ev, gb);
 }
+
+// LDS per wave of a tile workgroup whose widths reach FHI: the staged section (SPEC) or, in counter
+// mode, the wave's records (128 of 32 B, or 2 x 128 of 16 B) -- one region, used in that order
+template <int FHI, bool SPEC>
+constexpr uint32_t wave_lds() { return SPEC && RH_TABLE_STAGE && 1024u * (FHI + 3) > 4096u ? 1024u * (FHI + 3) : 4096u; }
 
 // The evaluation's counter word (rh_internal.h, TableEvents): kind 0 in bits [0, cbits), kind 1 in
 // [cbits, 2 cbits), workgroups done above when the count fits there (`packed`; the list kernel
@@ -551,8 +587,9 @@ __device__ __forceinline__ void table_block_iter(const TableDev& T, const TierRa
         ev.lheads_next[threadIdx.x * rh::kHeadStride] = 0ull;  // the next list set of this kind
     __syncthreads();
     const uint64_t gb = (uint64_t)ev.block_base + b;   // REGION mode: the evaluation's workgroup number
+    constexpr uint32_t WL = wave_lds<FHI, SPEC>();
     if (tl * rh::kTileRows < T.tier[t].rows)
-        table_dispatch<FLO, FHI, FLO <= 6, WATCH, SPEC>(T, t, tl, wall_on, stage, sc, ev, gb);
+        table_dispatch<FLO, FHI, FLO <= 6, WATCH, SPEC>(T, t, tl, wall_on, stage + wave * WL, sc, ev, gb);
     __syncthreads();
 
     if (ev.bdesc) {   // ---- REGION mode: the descriptor: totals, the waves' masks
@@ -611,7 +648,7 @@ __device__ __forceinline__ void table_block_iter(const TableDev& T, const TierRa
             uint32_t k = 0;
 #pragma unroll
             for (int m = 1; m < kTWaves; ++m) k += e >= sc.pre[0][m] ? 1u : 0u;
-            dst[j] = src[2 * (k * 128 + (e - sc.pre[0][k])) + (j & 1)];
+            dst[j] = src[k * (WL / 16) + 2 * (e - sc.pre[0][k]) + (j & 1)];
         }
     } else {
         v4u32* da = reinterpret_cast<v4u32*>(ev.adv + b0);
@@ -619,7 +656,7 @@ __device__ __forceinline__ void table_block_iter(const TableDev& T, const TierRa
             uint32_t k = 0;
 #pragma unroll
             for (int m = 1; m < kTWaves; ++m) k += e >= sc.pre[0][m] ? 1u : 0u;
-            da[e] = src[k * 128 + (e - sc.pre[0][k])];
+            da[e] = src[k * (WL / 16) + (e - sc.pre[0][k])];
         }
         if (ev.wall) {
             v4u32* dw = reinterpret_cast<v4u32*>(ev.wall + b1);
@@ -627,7 +664,7 @@ __device__ __forceinline__ void table_block_iter(const TableDev& T, const TierRa
                 uint32_t k = 0;
 #pragma unroll
                 for (int m = 1; m < kTWaves; ++m) k += e >= sc.pre[1][m] ? 1u : 0u;
-                dw[e] = src[kTRows + k * 128 + (e - sc.pre[1][k])];
+                dw[e] = src[k * (WL / 16) + 128 + (e - sc.pre[1][k])];
             }
         }
     }
@@ -636,8 +673,8 @@ __device__ __forceinline__ void table_block_iter(const TableDev& T, const TierRa
 template <bool WATCH, int FLO, int FHI, bool SPEC>
 __device__ __forceinline__ void table_commit_block(const TierRange& tr, const TableEvents& ev) {
     const TableDev& T = rh::kernarg_struct<TableDev>();  // block-uniform tier index: scalar loads
-    // COMMIT: [0, 24 KiB) advanced records, [24, 48 KiB) watch-ALL records; WATCH: level records
-    __shared__ __attribute__((aligned(16))) unsigned char stage[kTRows * sizeof(rh_watch_event)];
+    // per wave (wave_lds): the staged section, then (counter mode) its records
+    __shared__ __attribute__((aligned(16))) unsigned char stage[kTWaves * wave_lds<FHI, SPEC>()];
     __shared__ Stage sc;
     table_block_iter<WATCH, FLO, FHI, SPEC>(T, tr, ev, blockIdx.x, stage, sc);
 }
@@ -1280,23 +1317,23 @@ __global__ __launch_bounds__(256) void table_gather_rows_kernel(GatherRowsArgs a
         if (!(e00 || e01 || e10 || e11)) continue;
         const uint2 sl = *reinterpret_cast<const uint2*>(tb + rh::tile::kSlot + 8u * lane);
         if (WATCH) {
-            const int64_t* mn = reinterpret_cast<const int64_t*>(tb + rh::tile::wmin(F)) + 2 * lane;
-            const int64_t* mj = reinterpret_cast<const int64_t*>(tb + rh::tile::wmaj(F)) + 2 * lane;
-            const int64_t* mx = reinterpret_cast<const int64_t*>(tb + rh::tile::wmax(F)) + 2 * lane;
+            const int64_t* mn = reinterpret_cast<const int64_t*>(tb + rh::tile::pair_off(F, rh::tile::wmin(F), lane));
+            const int64_t* mj = reinterpret_cast<const int64_t*>(tb + rh::tile::pair_off(F, rh::tile::wmaj(F), lane));
+            const int64_t* mx = reinterpret_cast<const int64_t*>(tb + rh::tile::pair_off(F, rh::tile::wmax(F), lane));
             rh_watch_event* out = static_cast<rh_watch_event*>(A.a);
             uint64_t p = p0 + pre[0][c] + (uint64_t)(__popcll(a0 & lt) + __popcll(a1 & lt));
             if (e00) out[p++] = rh_watch_event{sl.x, (uint32_t)((c0 >> lane) & 1u), mn[0], mj[0], mx[0]};
             if (e01) out[p] = rh_watch_event{sl.y, (uint32_t)((c1 >> lane) & 1u), mn[1], mj[1], mx[1]};
         } else {
             if (e00 || e01) {
-                const int64_t* cp = reinterpret_cast<const int64_t*>(tb + rh::tile::commit(F)) + 2 * lane;
+                const int64_t* cp = reinterpret_cast<const int64_t*>(tb + rh::tile::pair_off(F, rh::tile::commit(F), lane));
                 rh_index_event* out = static_cast<rh_index_event*>(A.a);
                 uint64_t p = p0 + pre[0][c] + (uint64_t)(__popcll(a0 & lt) + __popcll(a1 & lt));
                 if (e00) out[p++] = rh_index_event{sl.x, 0u, cp[0]};
                 if (e01) out[p] = rh_index_event{sl.y, 0u, cp[1]};
             }
             if (e10 || e11) {
-                const int64_t* wp = reinterpret_cast<const int64_t*>(tb + rh::tile::wall(F)) + 2 * lane;
+                const int64_t* wp = reinterpret_cast<const int64_t*>(tb + rh::tile::pair_off(F, rh::tile::wall(F), lane));
                 uint64_t q = p1 + pre[1][c] + (uint64_t)(__popcll(c0 & lt) + __popcll(c1 & lt));
                 if (e10) A.b[q++] = rh_index_event{sl.x, 0u, wp[0]};
                 if (e11) A.b[q] = rh_index_event{sl.y, 0u, wp[1]};
