@@ -652,14 +652,16 @@ def table_commit_leg(ctx, host, reps: int = 8, fracs=(1.0, 0.1, 0.01), pmc=None)
         # algorithmic bytes of the evaluation kernel: 1 dirty byte per row; per dirty row its
         # columns (F matchIndex, conf, row slot, commit, flush, term start, previous watch-ALL level)
         # and the flag clear; per event the 8 B commit / watch level and (advanced) the 1 B
-        # watch-dirty flag it stores, and -- list mode only -- the 16 B record it writes (a tile
-        # evaluation into AUTO writes 1 bit per row instead: rh_table_gather_commit builds the
-        # records from the table on the side stream)
+        # watch-dirty flag it stores, and -- a list evaluation of fewer than 8192 marked rows only --
+        # the 16 B record it writes (tile evaluations and larger list evaluations into AUTO write
+        # event bits instead: rh_table_gather_commit builds the records from the table on the side
+        # stream)
         n_f4 = host[0].n
         f_mean = (n_f4 * F[0] + (n_all - n_f4) * (F[1] if len(F) > 1 else F[0])) / n_all
         per_dirty = 8 * f_mean + 4 + 4 + 8 + 8 + 8 + 8 + 1
         list_mode = bool(np.all(res[(_lib.RH_EVENTS_AUTO, "list")]))
-        rec = 16 if list_mode else 0
+        pinned = list_mode and k < 8192   # groups.cpp RH_LIST_PINNED_MAX
+        rec = 16 if pinned else 0
         alg = n_all * 1 + k * per_dirty + res["advanced"] * (rec + 8 + 1) + res["watch_all"] * (rec + 8)
         if not list_mode:
             alg += n_all / 4   # the event masks: 2 bits per row
@@ -673,9 +675,8 @@ def table_commit_leg(ctx, host, reps: int = 8, fracs=(1.0, 0.1, 0.01), pmc=None)
         case["roofline"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                             "frac": round(ach / HBM_PEAK_GBPS, 4), "algorithmic_bytes_per_launch": int(alg),
                             "kernel": ("table_list_kernel<false>" if list_mode else "table_commit_kernel_rank<false>")
-                            + (" (RH_EVENTS_AUTO: records into the lists -- pinned below 8192 marked rows, else HBM"
-                               " drained on the side stream)" if list_mode
-                               else " (RH_EVENTS_AUTO: event masks; records rebuilt from the table by the gather)"),
+                            + (" (RH_EVENTS_AUTO: records into the pinned lists)" if pinned
+                               else " (RH_EVENTS_AUTO: event masks; records rebuilt by the gather)"),
                             # PMC passes (scripts/prof_kernels.py table case) run the all-dirty step
                             "traffic": (round(pmc["table_bytes_per_unit"] * n_all)
                                         if frac >= 1.0 and pmc and "table_bytes_per_unit" in pmc else None),
@@ -696,12 +697,12 @@ def table_watch_leg(ctx, host, reps: int = 8, fracs=(1.0, 0.1, 0.01)) -> dict:
     mark `frac` of config 3's 1M groups, then one watch evaluation per step, timed at its kernel
     boundaries (rh_groups_timing).  Two tables fed the same deltas -- AUTO (the module's sink: a
     tile evaluation writes 2 bits per row -- changed, valid -- and rh_table_gather_watch rebuilds the
-    level records from the table on the side stream; a list evaluation writes its records) and
-    HOST_MAPPED (records across PCIe from the kernel) -- must report the same levels.  Algorithmic
-    bytes of the evaluation: 1 B watch-dirty flag per row; per dirty row 8F follower commitIndex, 8
-    commit (the self value), 24 previous levels, 4 conf, 4 row slot, 1 flag clear; per changed row
-    the 24 B of levels stored, plus the 32 B record in list mode or the masks (n / 4 B) in tile
-    mode."""
+    level records from the table on the side stream; so does a list evaluation of 8192 rows or more,
+    smaller ones write their records) and HOST_MAPPED (records across PCIe from the kernel) -- must
+    report the same levels.  Algorithmic bytes of the evaluation: 1 B watch-dirty flag per row; per
+    dirty row 8F follower commitIndex, 8 commit (the self value), 24 previous levels, 4 conf, 4 row
+    slot, 1 flag clear; per changed row the 24 B of levels stored, plus the 32 B record when the
+    kernel writes records, or the masks (n / 4 B) in tile mode."""
     import torch
 
     from ratis_amd import _lib, groups
@@ -754,7 +755,8 @@ def table_watch_leg(ctx, host, reps: int = 8, fracs=(1.0, 0.1, 0.01)) -> dict:
         list_mode = bool(np.all(res["list"]))
         n_f4 = host[0].n
         f_mean = (n_f4 * F[0] + (n_all - n_f4) * (F[1] if len(F) > 1 else F[0])) / n_all
-        alg = n_all * 1 + k * (8 * f_mean + 8 + 24 + 4 + 4 + 1) + changed * ((32 if list_mode else 0) + 24)
+        pinned = list_mode and k < 8192   # groups.cpp RH_LIST_PINNED_MAX: records into the pinned list
+        alg = n_all * 1 + k * (8 * f_mean + 8 + 24 + 4 + 4 + 1) + changed * ((32 if pinned else 0) + 24)
         if not list_mode:
             alg += n_all / 4   # the event masks: 2 bits per row
         ach = alg / (eval_ms * 1e-3) / 1e9
@@ -763,8 +765,8 @@ def table_watch_leg(ctx, host, reps: int = 8, fracs=(1.0, 0.1, 0.01)) -> dict:
             "sinks_agree": agree,
             "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(ach / HBM_PEAK_GBPS, 4), "algorithmic_bytes_per_launch": int(alg),
-                         "kernel": ("table_list_kernel<true> (records into the lists)" if list_mode
-                                    else "table_commit_kernel_rank<true> (event masks; records rebuilt by the gather)")}}
+                         "kernel": ("table_list_kernel<true>" if list_mode else "table_commit_kernel_rank<true>")
+                         + (" (records into the pinned list)" if pinned else " (event masks; records rebuilt by the gather)")}}
     for tab in tabs.values():
         tab.close()
     out["workload"] = (f"resident table of {n_all} config-3 groups; follower commitIndex deltas mark the dirty "
