@@ -291,7 +291,7 @@ static_assert(kTRows <= rh::kTableRecs && 2 + 8 * kTWaves == rh::kTableDesc,
 #endif
 
 #ifndef RH_TABLE_ABL   // ablation only (wrong results): 2 = no events, 3 = no table stores, 4 = trivial arithmetic
-#define RH_TABLE_ABL 0   // list kernel: 6 / 7 = 5 / 3 lines per row, 8 = no counter atomic or records, 9 = 6 + 8
+#define RH_TABLE_ABL 0   // list kernel: 6 / 7 = 5 / 3 lines per row, 8 = no counter atomic or records, 9 = 6 + 8, 10 = no watch-list appends
 #endif
 
 typedef __attribute__((address_space(3))) void lds_void_t;
@@ -909,7 +909,9 @@ __global__ __launch_bounds__(kListWaves * 64) void table_list_kernel(TableDev Ta
                 wcnt[1][wave] = (uint32_t)__popcll(c);
             }
             __syncthreads();
+#if RH_TABLE_ABL != 10   // ablation (wrong results): no watch-list appends
             if (!WATCH && wl) list_append(Lw, wtrans, t, row, h);   // kernel argument: uniform
+#endif
             if (threadIdx.x == 0 && rec) {
                 unsigned long long s0 = 0, s1 = 0;
 #pragma unroll
