@@ -1045,10 +1045,16 @@ RH_EXPORT int rh_push_deltas(rh_groups* g, const rh_delta* deltas, size_t n) {
             std::shared_lock<std::shared_mutex> sl(g->smu);   // the slot map changes only under exclusive
             if (g->ring_acquired >= 0) return rh::fail(RH_E_STATE, "rh_push_deltas: a staging slot is acquired");
             if (!validated) {
+                // a producer's deltas come in runs per division (a reply's SET + MAXes): the slot
+                // map is read once per run
+                uint32_t last = kNoRow, m = kNoRow, w = 0;
                 for (size_t i = 0; i < n; ++i) {
                     const rh_delta& d = deltas[i];
-                    const uint32_t m = d.slot < g->capacity ? g->slot_map[d.slot] : kNoRow;
-                    const uint32_t w = m == kNoRow ? 0u : rh::width_of_tier((int)(m >> 28));
+                    if (d.slot != last || i == 0) {
+                        last = d.slot;
+                        m = d.slot < g->capacity ? g->slot_map[d.slot] : kNoRow;
+                        w = m == kNoRow ? 0u : rh::width_of_tier((int)(m >> 28));
+                    }
                     const uint32_t c = d.column;
                     const bool ok_col = c < w || (c >= 16 && c < 16 + w) || c == RH_COL_FLUSH || c == RH_COL_COMMITTED ||
                                         (c >= 48 && c < 48 + w) || c == RH_COL_LEASE || c == RH_COL_LEASE_ON;
@@ -1522,8 +1528,9 @@ RH_EXPORT int rh_node_group_stop(rh_node* nd, uint32_t node_slot) {
 RH_EXPORT int rh_node_push_deltas(rh_node* nd, const rh_delta* deltas, size_t n) {
     if (!nd || (n && !deltas)) return rh::fail(RH_E_INVAL, "rh_node_push_deltas: NULL argument");
     const size_t S = nd->tab.size();
+    const uint64_t limit = (uint64_t)nd->cap * S;   // node slots [0, cap x shards): no division per delta
     for (size_t i = 0; i < n; ++i)  // validate every delta before any shard receives one
-        if (deltas[i].slot / nd->cap >= S)
+        if (deltas[i].slot >= limit)
             return rh::fail(RH_E_INVAL, "rh_node_push_deltas: delta " + std::to_string(i) + " has a bad slot");
     if (S == 1) return rh_push_deltas(nd->tab[0], deltas, n);  // node slot == table slot
     // per-shard partitions in the calling thread's own buffers (producers share nothing here; the
