@@ -650,18 +650,18 @@ def table_commit_leg(ctx, host, reps: int = 8, fracs=(1.0, 0.1, 0.01), pmc=None)
         med = {key: float(np.median(v)) for key, v in res.items() if isinstance(key, tuple)}
         eval_ms = float(np.median(res[(_lib.RH_EVENTS_AUTO, "eval")]))   # the module's sink
         # algorithmic bytes of the evaluation kernel: 1 dirty byte per row; per dirty row its
-        # columns (F matchIndex, conf, row slot, commit, flush, term start, previous watch-ALL level)
-        # and the flag clear; per event the 8 B commit / watch level and (advanced) the 1 B
-        # watch-dirty flag it stores, and -- a list evaluation of fewer than 8192 marked rows only --
-        # the 16 B record it writes (tile evaluations and larger list evaluations into AUTO write
-        # event bits instead: rh_table_gather_commit builds the records from the table on the side
-        # stream)
+        # columns (F matchIndex, conf, commit, flush, term start, previous watch-ALL level; the row
+        # slot only where the kernel writes records) and the flag clear; per event the 8 B commit /
+        # watch level and (advanced) the 1 B watch-dirty flag it stores, and -- a list evaluation of
+        # fewer than 8192 marked rows only -- the 16 B record it writes (tile evaluations and larger
+        # list evaluations into AUTO write event bits instead: rh_table_gather_commit builds the
+        # records from the table on the side stream)
         n_f4 = host[0].n
         f_mean = (n_f4 * F[0] + (n_all - n_f4) * (F[1] if len(F) > 1 else F[0])) / n_all
-        per_dirty = 8 * f_mean + 4 + 4 + 8 + 8 + 8 + 8 + 1
         list_mode = bool(np.all(res[(_lib.RH_EVENTS_AUTO, "list")]))
         pinned = list_mode and k < 8192   # groups.cpp RH_LIST_PINNED_MAX
         rec = 16 if pinned else 0
+        per_dirty = 8 * f_mean + 4 + (4 if pinned else 0) + 8 + 8 + 8 + 8 + 1
         alg = n_all * 1 + k * per_dirty + res["advanced"] * (rec + 8 + 1) + res["watch_all"] * (rec + 8)
         if not list_mode:
             alg += n_all / 4   # the event masks: 2 bits per row
@@ -700,8 +700,8 @@ def table_watch_leg(ctx, host, reps: int = 8, fracs=(1.0, 0.1, 0.01)) -> dict:
     level records from the table on the side stream; so does a list evaluation of 8192 rows or more,
     smaller ones write their records) and HOST_MAPPED (records across PCIe from the kernel) -- must
     report the same levels.  Algorithmic bytes of the evaluation: 1 B watch-dirty flag per row; per
-    dirty row 8F follower commitIndex, 8 commit (the self value), 24 previous levels, 4 conf, 4 row
-    slot, 1 flag clear; per changed row the 24 B of levels stored, plus the 32 B record when the
+    dirty row 8F follower commitIndex, 8 commit (the self value), 24 previous levels, 4 conf, 1 flag
+    clear; per changed row the 24 B of levels stored, plus the 4 B row slot and 32 B record when the
     kernel writes records, or the masks (n / 4 B) in tile mode."""
     import torch
 
@@ -756,7 +756,7 @@ def table_watch_leg(ctx, host, reps: int = 8, fracs=(1.0, 0.1, 0.01)) -> dict:
         n_f4 = host[0].n
         f_mean = (n_f4 * F[0] + (n_all - n_f4) * (F[1] if len(F) > 1 else F[0])) / n_all
         pinned = list_mode and k < 8192   # groups.cpp RH_LIST_PINNED_MAX: records into the pinned list
-        alg = n_all * 1 + k * (8 * f_mean + 8 + 24 + 4 + 4 + 1) + changed * ((32 if pinned else 0) + 24)
+        alg = n_all * 1 + k * (8 * f_mean + 8 + 24 + 4 + (4 if pinned else 0) + 1) + changed * ((32 if pinned else 0) + 24)
         if not list_mode:
             alg += n_all / 4   # the event masks: 2 bits per row
         ach = alg / (eval_ms * 1e-3) / 1e9

@@ -362,7 +362,8 @@ __device__ __forceinline__ void table_wave(const TableDev& T, const TableTier& t
         }
 #endif
         const v2u32 c = tload<v2u32>(tb + tile::kConf + l8);
-        const v2u32 sl = tload<v2u32>(tb + tile::kSlot + l8);
+        // row slots only for records this kernel writes (REGION mode: the gather reads them)
+        const v2u32 sl = ev.bdesc ? v2u32{0u, 0u} : tload<v2u32>(tb + tile::kSlot + l8);
         const v2i64 cm = tload<v2i64>(tb + tile::pair_off(F, tile::commit(F), lane));
 #if RH_TABLE_STAGE
         if constexpr (SPEC) {
@@ -712,10 +713,10 @@ __global__ __launch_bounds__(kTBlock) void table_commit_kernel_net(TableDev Targ
 template <int F, bool WATCH>
 __device__ __forceinline__ void list_row(const TableDev& T, const TableTier& tt, uint32_t r, bool wall_on,
                                          bool wlisted, bool& e0, bool& e1, bool& wtrans, int64_t& x0, int64_t& x1,
-                                         int64_t& x2, uint32_t& valid, uint32_t& slot) {
+                                         int64_t& x2, uint32_t& valid, uint32_t& slot, bool need_slot) {
     int64_t vals[F + 1];
     const uint32_t w = *tt.u32(tile::kConf, r);
-    slot = *tt.u32(tile::kSlot, r);
+    slot = need_slot ? *tt.u32(tile::kSlot, r) : 0u;   // REGION mode: the gather reads it
     const int64_t cm = *tt.i64(tile::commit(F), r);
 #if RH_TABLE_ABL == 6 || RH_TABLE_ABL == 7 || RH_TABLE_ABL == 9   // ablation (wrong results): a row's lines cut to conf, slot, commit (+ flags)
 #pragma unroll
@@ -885,13 +886,13 @@ __global__ __launch_bounds__(kListWaves * 64) void table_list_kernel(TableDev Ta
             row = ent & rh::kRowMask;
             const TableTier tt = tiers[t < rh::kTableTiers ? t : 0];
             switch (tt.width) {
-                case 2: list_row<2, WATCH>(T, tt, row, wall_on, wl, e0, e1, wtrans, x0, x1, x2, valid, slot); break;
-                case 4: list_row<4, WATCH>(T, tt, row, wall_on, wl, e0, e1, wtrans, x0, x1, x2, valid, slot); break;
-                case 6: list_row<6, WATCH>(T, tt, row, wall_on, wl, e0, e1, wtrans, x0, x1, x2, valid, slot); break;
-                case 8: list_row<8, WATCH>(T, tt, row, wall_on, wl, e0, e1, wtrans, x0, x1, x2, valid, slot); break;
-                case 10: list_row<10, WATCH>(T, tt, row, wall_on, wl, e0, e1, wtrans, x0, x1, x2, valid, slot); break;
-                case 12: list_row<12, WATCH>(T, tt, row, wall_on, wl, e0, e1, wtrans, x0, x1, x2, valid, slot); break;
-                default: list_row<14, WATCH>(T, tt, row, wall_on, wl, e0, e1, wtrans, x0, x1, x2, valid, slot); break;
+                case 2: list_row<2, WATCH>(T, tt, row, wall_on, wl, e0, e1, wtrans, x0, x1, x2, valid, slot, !region); break;
+                case 4: list_row<4, WATCH>(T, tt, row, wall_on, wl, e0, e1, wtrans, x0, x1, x2, valid, slot, !region); break;
+                case 6: list_row<6, WATCH>(T, tt, row, wall_on, wl, e0, e1, wtrans, x0, x1, x2, valid, slot, !region); break;
+                case 8: list_row<8, WATCH>(T, tt, row, wall_on, wl, e0, e1, wtrans, x0, x1, x2, valid, slot, !region); break;
+                case 10: list_row<10, WATCH>(T, tt, row, wall_on, wl, e0, e1, wtrans, x0, x1, x2, valid, slot, !region); break;
+                case 12: list_row<12, WATCH>(T, tt, row, wall_on, wl, e0, e1, wtrans, x0, x1, x2, valid, slot, !region); break;
+                default: list_row<14, WATCH>(T, tt, row, wall_on, wl, e0, e1, wtrans, x0, x1, x2, valid, slot, !region); break;
             }
         }
         // events: one range of the lists per workgroup and pass

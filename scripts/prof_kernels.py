@@ -89,7 +89,7 @@ def main():
         nw = sum(e[1] for e in ev) / len(ev)
         # bench.table_commit_leg's algorithmic bytes of a 100 % step (a tile evaluation into AUTO:
         # no records, 2 mask bits per row; mean over the iterations)
-        alg = n * 1 + n * (8 * f_mean + 4 + 4 + 8 + 8 + 8 + 8 + 1) + na * (8 + 1) + nw * 8 + n / 4
+        alg = n * 1 + n * (8 * f_mean + 4 + 8 + 8 + 8 + 8 + 1) + na * (8 + 1) + nw * 8 + n / 4   # no row slots: REGION mode
         print("alg_bytes", int(alg), "rows", n, "advanced", int(na), "watch_all", int(nw))
     elif a.what == "lease":
         import numpy as np
