@@ -577,7 +577,7 @@ def queue_gate(stream, cycles: int = 400_000) -> None:
         pass
 
 
-def table_commit_leg(ctx, host, reps: int = 8, fracs=(1.0, 0.1, 0.01), pmc=None) -> dict:
+def table_commit_leg(ctx, host, reps: int = 16, fracs=(1.0, 0.1, 0.01), pmc=None) -> dict:
     """The kernel the Java module drives: rh_commit_batch over the resident table (config-3
     groups, stable F=4 and joint F=6 tiers, 128-row tiled layout), after deltas marked `frac` of the
     groups dirty (one matchIndex / flushIndex update per dirty group, as delta_streaming's steps).
@@ -690,7 +690,7 @@ def table_commit_leg(ctx, host, reps: int = 8, fracs=(1.0, 0.1, 0.01), pmc=None)
     return out
 
 
-def table_watch_leg(ctx, host, reps: int = 8, fracs=(1.0, 0.1, 0.01)) -> dict:
+def table_watch_leg(ctx, host, reps: int = 16, fracs=(1.0, 0.1, 0.01)) -> dict:
     """commitIndexChanged over the resident table (LeaderStateImpl.java:612-622, rh_watch_levels_async
     / _wait), the other evaluation the Java pump runs every tick: the followers' commitIndex deltas
     (FollowerInfo.updateCommitIndex, one per dirty group: follower 0..3, +512 over its current value)
