@@ -17,6 +17,13 @@
 #include "rh_internal.h"
 #include "lease_eval.h"
 
+#ifndef RH_LEASE_NT      // A/B: non-temporal column loads in the F <= 7 kernel
+#define RH_LEASE_NT 1
+#endif
+#ifndef RH_LEASE_WAVES   // A/B: waves per SIMD the F <= 7 kernel is pinned to
+#define RH_LEASE_WAVES 8
+#endif
+
 namespace {
 
 using namespace rh_lease;
@@ -49,7 +56,7 @@ int rh_lease_launch_class(const rh_lease_soa* tiers, int n_tiers, int flo, int f
     if (flo != 0)
         hipLaunchKernelGGL((lease_kernel<8, 14, false, 1>), g, b, 0, stream, a);
     else
-        hipLaunchKernelGGL((lease_kernel<0, 7, true, 8>), g, b, 0, stream, a);
+        hipLaunchKernelGGL((lease_kernel<0, 7, RH_LEASE_NT != 0, RH_LEASE_WAVES>), g, b, 0, stream, a);
     RH_HIP(hipGetLastError());
     return RH_OK;
 }
