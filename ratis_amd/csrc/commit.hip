@@ -22,6 +22,9 @@
 
 namespace {
 
+#ifndef RH_COMMIT_XCD
+#define RH_COMMIT_XCD 0
+#endif
 #ifndef RH_COMMIT_BLOCK   // A/B: threads per commit_kernel_rank / _net workgroup (the fused leader kernel keeps 256)
 #define RH_COMMIT_BLOCK 256
 #endif
@@ -307,7 +310,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(RH_COMMI
     const LaunchArgs& args = rh::kernarg_struct<LaunchArgs>();  // scalar loads, no scratch copy
     const int ti = tier_of_block(args, blockIdx.x);
     const TierArgs& ta = args.tier[ti];
-    dispatch_f<1, 6, true, true, RH_COMMIT_NTS, kBlock>(ta, (uint64_t)(blockIdx.x - ta.block_begin));
+    uint32_t j = blockIdx.x - ta.block_begin;
+#if RH_COMMIT_XCD   // A/B: each XCD (blocks dealt round robin) streams one contiguous eighth of the tier
+    {
+        const uint32_t n = ta.n_blocks, x = j % 8u, q = n / 8u, r = n % 8u;
+        j = x * q + (x < r ? x : r) + j / 8u;
+    }
+#endif
+    dispatch_f<1, 6, true, true, RH_COMMIT_NTS, kBlock>(ta, (uint64_t)j);
 }
 
 // Tiers with F = 7..14 (8..15 voters): a Batcher network per conf (rank masks of 8+ values do

@@ -13,7 +13,7 @@ for lib in $R/ratis_amd/lib/libratis_hip.so $(ls $R/ratis_amd/lib/ab/*.so 2>/dev
 import json, sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
 print(sys.argv[2], "commit", round(d["ms_per_step"] * 1e3, 2), "lease", round(d["lease"]["ms_per_pass"] * 1e3, 2),
-      "fused", round(d["lease"]["fused_with_commit"]["roofline"]["avg_launch_ms"] * 1e3, 2), d["lease"]["parity_ok"])
+      "fused", round(d["lease"]["fused_with_commit"]["roofline"]["avg_launch_ms"] * 1e3, 2), d["lease"]["parity_ok"], {k: v for k, v in d.items() if "parity" in k})
 PY
 done
 done
