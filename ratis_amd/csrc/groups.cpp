@@ -746,11 +746,19 @@ RH_EXPORT int rh_groups_create(rh_ctx* ctx, uint64_t capacity, int64_t gap_thres
 RH_EXPORT int rh_groups_destroy(rh_groups* g) {
     if (!g) return rh::fail(RH_E_INVAL, "rh_groups_destroy: NULL");
     DeviceGuard dg(g->ctx->device);
-    (void)hipStreamSynchronize(g->ctx->stream);
-    if (g->copy_stream) (void)hipStreamSynchronize(g->copy_stream);
-    if (g->d2h_stream) (void)hipStreamSynchronize(g->d2h_stream);
+    // a fault of the table's last work is reported here, not swallowed (the table is freed anyway)
+    hipError_t e = hipStreamSynchronize(g->ctx->stream);
+    if (g->copy_stream) {
+        const hipError_t e1 = hipStreamSynchronize(g->copy_stream);
+        if (e == hipSuccess) e = e1;
+    }
+    if (g->d2h_stream) {
+        const hipError_t e2 = hipStreamSynchronize(g->d2h_stream);
+        if (e == hipSuccess) e = e2;
+    }
     free_groups(g);
     delete g;
+    if (e != hipSuccess) return rh::hip_fail(e, "rh_groups_destroy: the table's last work failed");
     return RH_OK;
 }
 
@@ -1476,10 +1484,15 @@ RH_EXPORT int rh_node_create(uint32_t device_mask, uint64_t capacity_per_shard, 
 
 RH_EXPORT int rh_node_destroy(rh_node* nd) {
     if (!nd) return rh::fail(RH_E_INVAL, "rh_node_destroy: NULL");
-    for (rh_groups* t : nd->tab) (void)rh_groups_destroy(t);
+    int rc = RH_OK;
+    std::string msg;
+    for (rh_groups* t : nd->tab) {
+        const int r = rh_groups_destroy(t);
+        if (r != RH_OK && rc == RH_OK) rc = r, msg = rh_last_error();   // the first shard's failure
+    }
     for (rh_ctx* c : nd->ctx) (void)rh_shutdown(c);
     delete nd;
-    return RH_OK;
+    return rc == RH_OK ? RH_OK : rh::fail(rc, msg);
 }
 
 RH_EXPORT int rh_node_shards(rh_node* nd) { return nd ? (int)nd->tab.size() : rh::fail(RH_E_INVAL, "rh_node_shards: NULL"); }

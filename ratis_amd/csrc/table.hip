@@ -1290,6 +1290,7 @@ __global__ __launch_bounds__(256) void table_gather_rows_kernel(GatherRowsArgs a
             const uint32_t ent = A.lr.rows[(uint64_t)r * A.lr.cap + (pass * 64u + lane) * Wr + k];
             const TableTier& tt = A.t.tier[(ent >> 28) < (uint32_t)rh::kTableTiers ? (ent >> 28) : 0u];
             const uint32_t row = ent & rh::kRowMask, F = tt.width;
+            if (row >= tt.rows) continue;   // never: the entry was listed by this evaluation (no stray access)
             const uint32_t sl = *tt.u32(rh::tile::kSlot, row);
             if (WATCH) {
                 rh_watch_event* out = static_cast<rh_watch_event*>(A.a);

@@ -116,9 +116,9 @@ class RaftGroupTable:
 
     # -- lifecycle --------------------------------------------------------------------------
     def close(self) -> None:
-        if self._h is not None and getattr(self, "_owned", True):
-            check(self._lib.rh_groups_destroy(self._h))
-        self._h = None
+        h, self._h = self._h, None
+        if h is not None and getattr(self, "_owned", True):
+            check(self._lib.rh_groups_destroy(h))   # raises if the table's last work faulted
 
     def __enter__(self):
         return self
@@ -353,9 +353,9 @@ class RaftNode:
                        for s in range(self.n_shards)]
 
     def close(self) -> None:
-        if self._h is not None:
-            check(self._lib.rh_node_destroy(self._h))
-            self._h = None
+        h, self._h = self._h, None
+        if h is not None:
+            check(self._lib.rh_node_destroy(h))
 
     def __enter__(self):
         return self
