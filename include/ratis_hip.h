@@ -226,6 +226,7 @@ typedef struct rh_commit_out {
 
 /* Creates a table of `capacity` slots (< 2^28); every slot starts stopped. */
 int rh_groups_create(rh_ctx* ctx, uint64_t capacity, int64_t gap_threshold, rh_groups** out);
+/* Waits for the table's work and frees it; RH_E_DEVICE if that work faulted (freed anyway). */
 int rh_groups_destroy(rh_groups* g);
 /* Leader start for `slot` (a new LeaderStateImpl: every FollowerInfo is new, matchIndex =
  * commitIndex = -1, FII:42-43, LSI:421-430; StartupLogEntry's index is term_start, LSI:296-301).
@@ -363,6 +364,7 @@ int rh_node_create(uint32_t device_mask, uint64_t capacity_per_shard, int64_t ga
  * how a one-GPU box runs the routing, gathering and lease bitmap of an 8-GPU server). */
 int rh_node_create_devices(const int* devices, int n_shards, uint64_t capacity_per_shard, int64_t gap_threshold,
                            rh_node** out);
+/* Destroys every shard (rh_groups_destroy) and context; the first shard's failure is returned. */
 int rh_node_destroy(rh_node* node);
 int rh_node_shards(rh_node* node);
 /* The shard table (for per-shard calls such as the zero-copy ring) and its context. */
