@@ -311,6 +311,20 @@ int grow_tier(rh_groups* g, int t, uint32_t rows) {
     return RH_OK;
 }
 
+// The table with each tier cut at its high-water mark (rounded up to a tile): rows past it were
+// never handed out, so passes over every row skip them; *rows: the rows left.
+rh::TableDev clipped(const rh_groups* g, uint64_t* rows) {
+    rh::TableDev ed = g->dev;
+    uint64_t n = 0;
+    for (int t = 0; t < rh::kTableTiers; ++t) {
+        const uint64_t hw = ((uint64_t)g->tiers[t].hw + rh::kTileRows - 1) / rh::kTileRows * rh::kTileRows;
+        ed.tier[t].rows = (uint32_t)std::min<uint64_t>(ed.tier[t].rows, hw);
+        n += ed.tier[t].rows;
+    }
+    if (rows) *rows = n;
+    return ed;
+}
+
 // A row of tier t for a new occupant.
 int alloc_row(rh_groups* g, int t, uint32_t* row) {
     TierHost& h = g->tiers[t];
@@ -503,13 +517,8 @@ int evaluate(rh_groups* g, int mode, bool wall_on, const EvTargets& t, uint64_t*
         if (m == 0) g->lvalid[1] = false;   // the tile kernel marks wdirty with plain stores
         // tiles at or past a tier's high-water mark hold no row ever handed out (clean): the
         // evaluation covers the tiles below it only
-        rh::TableDev ed = g->dev;
         uint64_t rows = 0;
-        for (int t = 0; t < rh::kTableTiers; ++t) {
-            const uint64_t hw = ((uint64_t)g->tiers[t].hw + rh::kTileRows - 1) / rh::kTileRows * rh::kTileRows;
-            ed.tier[t].rows = (uint32_t)std::min<uint64_t>(ed.tier[t].rows, hw);
-            rows += ed.tier[t].rows;
-        }
+        const rh::TableDev ed = clipped(g, &rows);
         const uint32_t nb = rh::table_commit_blocks(ed);
         if (k == 1 && nb <= region_blocks(g->capacity) && (uint64_t)nb * rh::kTableRecs <= hbm_records(g->capacity)) {
             ev.bdesc = bdesc;
@@ -1381,7 +1390,7 @@ RH_EXPORT int rh_lease_batch_async(rh_groups* g, int64_t now_nanos, int64_t time
     if (rc != RH_OK) return rc;
     const uint64_t words = (g->capacity + 63) / 64;
     RH_HIP(hipMemsetAsync(g->d_lbits, 0, words * 8, s));
-    rc = rh_table_lease(g->dev, now_nanos, timeout_ms, g->d_lbits, s);
+    rc = rh_table_lease(clipped(g, nullptr), now_nanos, timeout_ms, g->d_lbits, s);   // rows below the high-water marks
     if (rc != RH_OK) return rc;
     RH_HIP(hipMemcpyAsync(g->h_lbits, g->d_lbits, words * 8, hipMemcpyDeviceToHost, s));
     RH_HIP(hipEventRecord(g->ldone, s));

@@ -975,32 +975,57 @@ __global__ __launch_bounds__(kListWaves * 64) void table_list_kernel(TableDev Ta
 }
 
 // ---- hasLease over every started row -------------------------------------------------------------
+#ifndef RH_LEASE_BITS_WAVE   // A/B: the hasLease bitmap set per wave (1) or per row (0)
+#define RH_LEASE_BITS_WAVE 1
+#endif
 template <int F>
 __global__ __launch_bounds__(256) void table_lease_kernel(TableTier tt, int64_t now, int64_t timeout_ms,
                                                           uint64_t* __restrict__ slot_bits) {
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= tt.rows) return;
-    const uint32_t w = *tt.u32(tile::kConf, r);
-    if (!(w & RH_CONF_ACTIVE)) return;  // free row
-    int64_t ts[F];
-    uint32_t never = 0;
+    bool has = false;
+    uint32_t slot = 0;
+    if (r < tt.rows) {   // no early return: the bitmap words are set wave-wide below
+        const uint32_t w = *tt.u32(tile::kConf, r);
+        if (w & RH_CONF_ACTIVE) {   // a started row
+            int64_t ts[F];
+            uint32_t never = 0;
 #pragma unroll
-    for (int k = 0; k < F; ++k) {
-        ts[k] = *tt.i64(tile::fts(F, k), r);
-        never |= (ts[k] == rh::kNoTimestamp ? 1u : 0u) << k;
+            for (int k = 0; k < F; ++k) {
+                ts[k] = *tt.i64(tile::fts(F, k), r);
+                never |= (ts[k] == rh::kNoTimestamp ? 1u : 0u) << k;
+            }
+            rh_lease_soa t{};
+            t.now_nanos = now;
+            t.timeout_ms = timeout_ms;
+            int64_t lout;
+            bool ext;
+            int64_t* lease = tt.i64(tile::lease(F), r);
+            rh_lease::lease_one<F>(t, ts, w, *lease, *tt.u8(tile::kLon, r) != 0, true, lout, has, ext, never);
+            if (ext) *lease = lout;
+            if (has) slot = *tt.u32(tile::kSlot, r);
+        }
     }
-    rh_lease_soa t{};
-    t.now_nanos = now;
-    t.timeout_ms = timeout_ms;
-    int64_t lout;
-    bool has, ext;
-    int64_t* lease = tt.i64(tile::lease(F), r);
-    rh_lease::lease_one<F>(t, ts, w, *lease, *tt.u8(tile::kLon, r) != 0, true, lout, has, ext, never);
-    if (ext) *lease = lout;
-    if (has) {
-        const uint32_t slot = *tt.u32(tile::kSlot, r);
+#if RH_LEASE_BITS_WAVE
+    // the wave's rows usually hold consecutive slots (a load or a start fills rows in slot order):
+    // lanes whose bit lands in the first pending lane's word OR their bits together and one lane
+    // sets the word -- one atomic per word instead of one per row (64 same-address atomics a wave)
+    const int lane = threadIdx.x & 63;
+    uint64_t pend = __ballot(has);
+    for (int round = 0; pend && round < 2; ++round) {
+        const int lead = __ffsll((long long)pend) - 1;
+        const uint32_t word = (uint32_t)__shfl((int)(slot >> 6), lead);
+        const bool mine = has && (slot >> 6) == word && ((pend >> lane) & 1ull);
+        uint64_t v = mine ? 1ull << (slot & 63) : 0ull;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) v |= __shfl_xor(v, d);
+        if (lane == lead) atomicOr(reinterpret_cast<unsigned long long*>(slot_bits + word), v);
+        pend &= ~__ballot(mine);
+    }
+    if (has && ((pend >> lane) & 1ull))   // slots spread wider: one atomic per row
         atomicOr(reinterpret_cast<unsigned long long*>(slot_bits + (slot >> 6)), 1ull << (slot & 63));
-    }
+#else
+    if (has) atomicOr(reinterpret_cast<unsigned long long*>(slot_bits + (slot >> 6)), 1ull << (slot & 63));
+#endif
 }
 
 template <int F>
