@@ -138,7 +138,8 @@ struct rh_groups {
     hipEvent_t wgathered = nullptr;
     bool wgather_pending = false;
     bool wgather_list = false;   // ... and it reads the commitIndexChanged list's entries (list_fence)
-    uint64_t* d_lbits = nullptr;  // rh_lease_batch: slot bitmap (device) and its pinned copy
+    uint64_t* d_lbits = nullptr;  // rh_lease_batch: two slot bitmaps (device; a pass clears the other) and the pinned copy
+    int lbuf = 0;                 // the bitmap the next pass sets (zero)
     uint64_t* h_lbits = nullptr;
     // events (rh_internal.h, TableEvents): the evaluation counter words, result sets
     EvSet ev[kEvSets];
@@ -737,7 +738,9 @@ RH_EXPORT int rh_groups_create(rh_ctx* ctx, uint64_t capacity, int64_t gap_thres
     if (rc == RH_OK) rc = dalloc(&g->d_evw, (size_t)2 * rh::kHeadStride);
     if (rc == RH_OK && hipMemsetAsync(g->d_evw, 0, (size_t)2 * rh::kHeadStride * 8, s) != hipSuccess)
         rc = rh::fail(RH_E_DEVICE, "rh_groups_create: counters");
-    if (rc == RH_OK) rc = dalloc(&g->d_lbits, (capacity + 63) / 64);
+    if (rc == RH_OK) rc = dalloc(&g->d_lbits, 2 * ((capacity + 63) / 64));
+    if (rc == RH_OK && hipMemsetAsync(g->d_lbits, 0, 2 * ((capacity + 63) / 64) * 8, s) != hipSuccess)
+        rc = rh::fail(RH_E_DEVICE, "rh_groups_create: lease bitmaps");
     if (rc == RH_OK && hipHostMalloc(reinterpret_cast<void**>(&g->h_lbits), (capacity + 63) / 64 * 8) != hipSuccess)
         rc = rh::fail(RH_E_NOMEM, "hipHostMalloc(lease bitmap)");
     if (rc == RH_OK && hipEventCreateWithFlags(&g->ops_free, hipEventDisableTiming) != hipSuccess)
@@ -1389,10 +1392,17 @@ RH_EXPORT int rh_lease_batch_async(rh_groups* g, int64_t now_nanos, int64_t time
     if (rc == RH_OK) rc = flush_ops(g);
     if (rc != RH_OK) return rc;
     const uint64_t words = (g->capacity + 63) / 64;
-    RH_HIP(hipMemsetAsync(g->d_lbits, 0, words * 8, s));
-    rc = rh_table_lease(clipped(g, nullptr), now_nanos, timeout_ms, g->d_lbits, s);   // rows below the high-water marks
-    if (rc != RH_OK) return rc;
-    RH_HIP(hipMemcpyAsync(g->h_lbits, g->d_lbits, words * 8, hipMemcpyDeviceToHost, s));
+    // this pass sets bitmap lbuf (zeroed by the previous pass, or at creation) and zeroes the other
+    uint64_t* bits = g->d_lbits + (size_t)g->lbuf * words;
+    uint64_t* other = g->d_lbits + (size_t)(g->lbuf ^ 1) * words;
+    rc = rh_table_lease(clipped(g, nullptr), now_nanos, timeout_ms, bits, other, (uint32_t)words, s);   // rows below the high-water marks
+    if (rc != RH_OK) {   // a launch failed: the bitmaps' state is unknown
+        (void)hipStreamSynchronize(s);
+        (void)hipMemsetAsync(g->d_lbits, 0, 2 * words * 8, s);
+        return rc;
+    }
+    g->lbuf ^= 1;
+    RH_HIP(hipMemcpyAsync(g->h_lbits, bits, words * 8, hipMemcpyDeviceToHost, s));
     RH_HIP(hipEventRecord(g->ldone, s));
     ++g->lgen;
     g->lpending = true;

@@ -338,8 +338,10 @@ int rh_table_drain(const uint64_t* counts, const void* a, void* a_out, const voi
                    uint64_t cap, hipStream_t stream);
 // Initialises tiles [first_tile, n_tiles) of a tier as free rows (conf 0, row_slot kNoRow, clean).
 int rh_table_init_tiles(const rh::TableTier& t, uint32_t first_tile, uint32_t n_tiles, hipStream_t stream);
+// hasLease over every row into the zeroed bitmap d_slot_bits; the launch also zeroes d_clear_bits
+// (clear_words words: the next pass's bitmap).
 int rh_table_lease(const rh::TableDev& t, int64_t now_nanos, int64_t timeout_ms, uint64_t* d_slot_bits,
-                   hipStream_t stream);
+                   uint64_t* d_clear_bits, uint32_t clear_words, hipStream_t stream);
 int rh_table_read(const rh::TableDev& t, uint32_t first, uint32_t n, uint8_t column, int64_t* d_out,
                   hipStream_t stream);
 // window_only: every frame on the window kernel (one launch, no packed pass): small batches

@@ -980,8 +980,11 @@ __global__ __launch_bounds__(kListWaves * 64) void table_list_kernel(TableDev Ta
 #endif
 template <int F>
 __global__ __launch_bounds__(256) void table_lease_kernel(TableTier tt, int64_t now, int64_t timeout_ms,
-                                                          uint64_t* __restrict__ slot_bits) {
+                                                          uint64_t* __restrict__ slot_bits,
+                                                          uint64_t* __restrict__ clear, uint32_t clear_words) {
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // the other bitmap, the next pass's, cleared here (no memset launch of its own)
+    for (uint64_t j = r; j < clear_words; j += (uint64_t)gridDim.x * blockDim.x) clear[j] = 0ull;
     bool has = false;
     uint32_t slot = 0;
     if (r < tt.rows) {   // no early return: the bitmap words are set wave-wide below
@@ -1029,8 +1032,10 @@ __global__ __launch_bounds__(256) void table_lease_kernel(TableTier tt, int64_t 
 }
 
 template <int F>
-void launch_lease_width(const TableTier& tt, int64_t now, int64_t timeout_ms, uint64_t* bits, hipStream_t s) {
-    hipLaunchKernelGGL((table_lease_kernel<F>), dim3((tt.rows + 255) / 256), dim3(256), 0, s, tt, now, timeout_ms, bits);
+void launch_lease_width(const TableTier& tt, int64_t now, int64_t timeout_ms, uint64_t* bits, uint64_t* clear,
+                        uint32_t clear_words, hipStream_t s) {
+    hipLaunchKernelGGL((table_lease_kernel<F>), dim3((tt.rows + 255) / 256), dim3(256), 0, s, tt, now, timeout_ms, bits,
+                       clear, clear_words);
 }
 
 // ---- read-back -------------------------------------------------------------------------------------
@@ -1416,22 +1421,27 @@ int rh_table_init_tiles(const rh::TableTier& t, uint32_t first_tile, uint32_t n_
 }
 
 int rh_table_lease(const rh::TableDev& t, int64_t now_nanos, int64_t timeout_ms, uint64_t* d_slot_bits,
-                   hipStream_t stream) {
+                   uint64_t* d_clear_bits, uint32_t clear_words, hipStream_t stream) {
+    bool cleared = false;
     for (int i = 0; i < rh::kTableTiers; ++i) {
         const TableTier& tt = t.tier[i];
         if (!tt.rows) continue;
+        uint64_t* clear = cleared ? nullptr : d_clear_bits;   // the first launch clears the other bitmap
+        const uint32_t cw = cleared ? 0u : clear_words;
+        cleared = true;
         switch (tt.width) {
-            case 2: launch_lease_width<2>(tt, now_nanos, timeout_ms, d_slot_bits, stream); break;
-            case 4: launch_lease_width<4>(tt, now_nanos, timeout_ms, d_slot_bits, stream); break;
-            case 6: launch_lease_width<6>(tt, now_nanos, timeout_ms, d_slot_bits, stream); break;
-            case 8: launch_lease_width<8>(tt, now_nanos, timeout_ms, d_slot_bits, stream); break;
-            case 10: launch_lease_width<10>(tt, now_nanos, timeout_ms, d_slot_bits, stream); break;
-            case 12: launch_lease_width<12>(tt, now_nanos, timeout_ms, d_slot_bits, stream); break;
-            case 14: launch_lease_width<14>(tt, now_nanos, timeout_ms, d_slot_bits, stream); break;
+            case 2: launch_lease_width<2>(tt, now_nanos, timeout_ms, d_slot_bits, clear, cw, stream); break;
+            case 4: launch_lease_width<4>(tt, now_nanos, timeout_ms, d_slot_bits, clear, cw, stream); break;
+            case 6: launch_lease_width<6>(tt, now_nanos, timeout_ms, d_slot_bits, clear, cw, stream); break;
+            case 8: launch_lease_width<8>(tt, now_nanos, timeout_ms, d_slot_bits, clear, cw, stream); break;
+            case 10: launch_lease_width<10>(tt, now_nanos, timeout_ms, d_slot_bits, clear, cw, stream); break;
+            case 12: launch_lease_width<12>(tt, now_nanos, timeout_ms, d_slot_bits, clear, cw, stream); break;
+            case 14: launch_lease_width<14>(tt, now_nanos, timeout_ms, d_slot_bits, clear, cw, stream); break;
             default: return rh::fail(RH_E_STATE, "rh_lease_batch: unexpected tier width");
         }
         RH_HIP(hipGetLastError());
     }
+    if (!cleared && d_clear_bits && clear_words) RH_HIP(hipMemsetAsync(d_clear_bits, 0, (size_t)clear_words * 8, stream));
     return RH_OK;
 }
 
