@@ -80,6 +80,8 @@ uint64_t hbm_records(uint64_t capacity) { return capacity + (uint64_t)(rh::kTabl
 uint64_t region_blocks(uint64_t capacity) { return hbm_records(capacity) / rh::kTableRecs + rh::kTableTiers + 1; }
 // list capacity: a list evaluation is chosen while at most capacity / RH_LIST_DIV rows can be dirty
 uint32_t list_cap(uint64_t capacity) { return (uint32_t)std::max<uint64_t>(1024, capacity / RH_LIST_DIV); }
+// words between the two hasLease bitmaps (an even number: both 16-byte aligned)
+uint64_t lbits_stride(uint64_t capacity) { return ((capacity + 63) / 64 + 1) / 2 * 2; }
 // REGION-mode descriptors per result set: a tile evaluation's workgroups or a list evaluation's
 uint64_t desc_blocks(uint64_t capacity) {
     return std::max<uint64_t>(region_blocks(capacity), rh::table_list_desc_blocks(list_cap(capacity)));
@@ -141,6 +143,7 @@ struct rh_groups {
     uint64_t* d_lbits = nullptr;  // rh_lease_batch: two slot bitmaps (device; a pass clears the other) and the pinned copy
     int lbuf = 0;                 // the bitmap the next pass sets (zero)
     uint64_t* h_lbits = nullptr;
+    uint64_t* d_hlbits = nullptr;  // device view of h_lbits (the pass's last kernel writes it across PCIe)
     // events (rh_internal.h, TableEvents): the evaluation counter words, result sets
     EvSet ev[kEvSets];
     uint64_t next_ticket = 1;
@@ -738,11 +741,11 @@ RH_EXPORT int rh_groups_create(rh_ctx* ctx, uint64_t capacity, int64_t gap_thres
     if (rc == RH_OK) rc = dalloc(&g->d_evw, (size_t)2 * rh::kHeadStride);
     if (rc == RH_OK && hipMemsetAsync(g->d_evw, 0, (size_t)2 * rh::kHeadStride * 8, s) != hipSuccess)
         rc = rh::fail(RH_E_DEVICE, "rh_groups_create: counters");
-    if (rc == RH_OK) rc = dalloc(&g->d_lbits, 2 * ((capacity + 63) / 64));
-    if (rc == RH_OK && hipMemsetAsync(g->d_lbits, 0, 2 * ((capacity + 63) / 64) * 8, s) != hipSuccess)
+    // two bitmaps, each at a 16-byte aligned stride (the copy to the host moves 16 bytes a step)
+    if (rc == RH_OK) rc = dalloc(&g->d_lbits, 2 * lbits_stride(capacity));
+    if (rc == RH_OK && hipMemsetAsync(g->d_lbits, 0, 2 * lbits_stride(capacity) * 8, s) != hipSuccess)
         rc = rh::fail(RH_E_DEVICE, "rh_groups_create: lease bitmaps");
-    if (rc == RH_OK && hipHostMalloc(reinterpret_cast<void**>(&g->h_lbits), (capacity + 63) / 64 * 8) != hipSuccess)
-        rc = rh::fail(RH_E_NOMEM, "hipHostMalloc(lease bitmap)");
+    if (rc == RH_OK) rc = halloc_mapped(&g->h_lbits, &g->d_hlbits, (capacity + 63) / 64);
     if (rc == RH_OK && hipEventCreateWithFlags(&g->ops_free, hipEventDisableTiming) != hipSuccess)
         rc = rh::fail(RH_E_DEVICE, "hipEventCreate(control ops)");
     if (rc == RH_OK && hipStreamSynchronize(s) != hipSuccess) rc = rh::fail(RH_E_DEVICE, "rh_groups_create: sync");
@@ -1393,16 +1396,18 @@ RH_EXPORT int rh_lease_batch_async(rh_groups* g, int64_t now_nanos, int64_t time
     if (rc != RH_OK) return rc;
     const uint64_t words = (g->capacity + 63) / 64;
     // this pass sets bitmap lbuf (zeroed by the previous pass, or at creation) and zeroes the other
-    uint64_t* bits = g->d_lbits + (size_t)g->lbuf * words;
-    uint64_t* other = g->d_lbits + (size_t)(g->lbuf ^ 1) * words;
+    uint64_t* bits = g->d_lbits + (size_t)g->lbuf * lbits_stride(g->capacity);
+    uint64_t* other = g->d_lbits + (size_t)(g->lbuf ^ 1) * lbits_stride(g->capacity);
     rc = rh_table_lease(clipped(g, nullptr), now_nanos, timeout_ms, bits, other, (uint32_t)words, s);   // rows below the high-water marks
     if (rc != RH_OK) {   // a launch failed: the bitmaps' state is unknown
         (void)hipStreamSynchronize(s);
-        (void)hipMemsetAsync(g->d_lbits, 0, 2 * words * 8, s);
+        (void)hipMemsetAsync(g->d_lbits, 0, 2 * lbits_stride(g->capacity) * 8, s);
         return rc;
     }
     g->lbuf ^= 1;
-    RH_HIP(hipMemcpyAsync(g->h_lbits, bits, words * 8, hipMemcpyDeviceToHost, s));
+    // the bitmap to the host by GPU writes into the mapped pinned copy (no DMA setup on the path)
+    rc = rh_table_copy_words(bits, g->d_hlbits, words, s);
+    if (rc != RH_OK) return rc;
     RH_HIP(hipEventRecord(g->ldone, s));
     ++g->lgen;
     g->lpending = true;

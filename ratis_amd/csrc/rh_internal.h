@@ -334,6 +334,8 @@ int rh_table_gather_commit(const rh::TableDev& t, const uint32_t* bdesc, uint32_
 // columns into the pinned list `out` (device pointer), its length to counts_out[0].
 int rh_table_gather_watch(const rh::TableDev& t, const uint32_t* bdesc, uint32_t n_blocks, rh_watch_event* out,
                           uint64_t* counts_out, hipStream_t stream, const rh::ListRegion& lr = rh::ListRegion{});
+// n 64-bit words from device memory to a host-mapped pinned buffer (device view), as GPU writes.
+int rh_table_copy_words(const uint64_t* src, uint64_t* dst, uint64_t n, hipStream_t stream);
 int rh_table_drain(const uint64_t* counts, const void* a, void* a_out, const void* b, void* b_out, uint32_t rec_bytes0,
                    uint64_t cap, hipStream_t stream);
 // Initialises tiles [first_tile, n_tiles) of a tier as free rows (conf 0, row_slot kNoRow, clean).

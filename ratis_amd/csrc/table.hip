@@ -1215,6 +1215,25 @@ __global__ __launch_bounds__(256) void table_drain_kernel(const uint64_t* __rest
     }
 }
 
+__global__ __launch_bounds__(256) void table_copy_words_kernel(const uint64_t* __restrict__ src, uint64_t* __restrict__ dst,
+                                                               uint64_t n) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t n2 = n / 2;   // 16 bytes per thread and step (both pointers 16-byte aligned)
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n2; j += stride)
+        reinterpret_cast<uint4*>(dst)[j] = reinterpret_cast<const uint4*>(src)[j];
+    if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) dst[n - 1] = src[n - 1];
+}
+
+int rh_table_copy_words(const uint64_t* src, uint64_t* dst, uint64_t n, hipStream_t stream) {
+    if (n == 0) return RH_OK;
+    if ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 15)
+        return rh::fail(RH_E_STATE, "rh_table_copy_words: buffers not 16-byte aligned");
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>(64, (n / 2 + 255) / 256 + 1);
+    hipLaunchKernelGGL(table_copy_words_kernel, dim3(blocks), dim3(256), 0, stream, src, dst, n);
+    RH_HIP(hipGetLastError());
+    return RH_OK;
+}
+
 int rh_table_drain(const uint64_t* counts, const void* a, void* a_out, const void* b, void* b_out, uint32_t rec_bytes0,
                    uint64_t cap, hipStream_t stream) {
     hipLaunchKernelGGL(table_drain_kernel, dim3(512), dim3(256), 0, stream, counts, static_cast<const uint4*>(a),
