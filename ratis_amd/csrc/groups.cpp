@@ -22,6 +22,9 @@
 
 #define RH_EXPORT extern "C" __attribute__((visibility("default")))
 
+#ifndef RH_DELTA_ZC_MAX   // batches of at most this many deltas are applied from the pinned slot in place (A/B)
+#define RH_DELTA_ZC_MAX 4096
+#endif
 #ifndef RH_LIST_DIV   // A/B: list mode while at most capacity / RH_LIST_DIV rows can be dirty
 #define RH_LIST_DIV 32
 #endif
@@ -116,6 +119,7 @@ struct rh_groups {
     // a copy stream, so the copy of batch s+1 overlaps the apply / evaluation of batch s
     rh_delta* h_ring[2] = {nullptr, nullptr};
     rh_delta* d_ring[2] = {nullptr, nullptr};
+    const rh_delta* d_hring[2] = {nullptr, nullptr};   // device views of h_ring (small batches: read in place)
     hipEvent_t ring_free[2] = {nullptr, nullptr};   // H2D of the slot done (host slot reusable)
     hipEvent_t ring_read[2] = {nullptr, nullptr};   // apply of the slot done (device slot reusable)
     bool ring_used[2] = {false, false};
@@ -576,10 +580,18 @@ int ring_submit(rh_groups* g, int i, size_t n, bool has_set) {
     hipStream_t s = g->ctx->stream, cs = g->copy_stream;
     int rc = flush_ops(g);
     if (rc != RH_OK) return rc;
-    if (g->ring_used[i]) RH_HIP(hipStreamWaitEvent(cs, g->ring_read[i], 0));
-    RH_HIP(hipMemcpyAsync(g->d_ring[i], g->h_ring[i], n * sizeof(rh_delta), hipMemcpyHostToDevice, cs));
-    RH_HIP(hipEventRecord(g->ring_free[i], cs));
-    RH_HIP(hipStreamWaitEvent(s, g->ring_free[i], 0));
+    // a small batch (a pump tick's replies) is read by the apply kernels straight from the pinned
+    // slot across PCIe: no DMA set-up and no cross-stream wait on the tick's path; the host slot is
+    // free again once they are done.  Large batches go by DMA on the copy stream (overlapping the
+    // previous batch's apply), read from HBM by the apply phases.
+    const bool zc = n <= (size_t)RH_DELTA_ZC_MAX && g->d_hring[i] != nullptr;
+    const rh_delta* src = zc ? g->d_hring[i] : g->d_ring[i];
+    if (!zc) {
+        if (g->ring_used[i]) RH_HIP(hipStreamWaitEvent(cs, g->ring_read[i], 0));
+        RH_HIP(hipMemcpyAsync(g->d_ring[i], g->h_ring[i], n * sizeof(rh_delta), hipMemcpyHostToDevice, cs));
+        RH_HIP(hipEventRecord(g->ring_free[i], cs));
+        RH_HIP(hipStreamWaitEvent(s, g->ring_free[i], 0));
+    }
     rc = gather_fence(g);   // RH_COL_COMMITTED deltas write the commit column; appends, the lists
     if (rc == RH_OK) rc = list_fence(g);
     if (rc != RH_OK) return rc;
@@ -597,13 +609,14 @@ int ring_submit(rh_groups* g, int i, size_t n, bool has_set) {
             g->apply_gen = 0;
         }
         gen = ++g->apply_gen;
-        rc = rh_table_apply_deltas(g->dev, g->d_ring[i], n, kApplyKeys, gen, lc, lw, s);
-        if (rc == RH_OK) rc = rh_table_apply_deltas(g->dev, g->d_ring[i], n, kApplySet, gen, lc, lw, s);
+        rc = rh_table_apply_deltas(g->dev, src, n, kApplyKeys, gen, lc, lw, s);
+        if (rc == RH_OK) rc = rh_table_apply_deltas(g->dev, src, n, kApplySet, gen, lc, lw, s);
         if (rc != RH_OK) return rc;
     }
-    rc = rh_table_apply_deltas(g->dev, g->d_ring[i], n, kApplyMax, gen, lc, lw, s);
+    rc = rh_table_apply_deltas(g->dev, src, n, kApplyMax, gen, lc, lw, s);
     if (rc != RH_OK) return rc;
     RH_HIP(hipEventRecord(g->ring_read[i], s));
+    if (zc) RH_HIP(hipEventRecord(g->ring_free[i], s));   // the host slot was read by the apply itself
     return RH_OK;
 }
 
@@ -707,6 +720,8 @@ RH_EXPORT int rh_groups_create(rh_ctx* ctx, uint64_t capacity, int64_t gap_thres
         if (rc != RH_OK) break;
         if (hipHostMalloc(reinterpret_cast<void**>(&g->h_ring[i]), (size_t)RH_DELTA_SLOT * sizeof(rh_delta)) != hipSuccess)
             rc = rh::fail(RH_E_NOMEM, "hipHostMalloc(delta staging)");
+        void* dv = nullptr;   // no device view: every batch goes by DMA
+        if (rc == RH_OK && hipHostGetDevicePointer(&dv, g->h_ring[i], 0) == hipSuccess) g->d_hring[i] = static_cast<const rh_delta*>(dv);
         if (rc == RH_OK && hipEventCreateWithFlags(&g->ring_free[i], hipEventDisableTiming) != hipSuccess)
             rc = rh::fail(RH_E_DEVICE, "hipEventCreate(delta staging)");
     }
