@@ -1013,18 +1013,20 @@ RH_EXPORT int rh_groups_load(rh_groups* g, uint32_t first, uint32_t n, uint32_t 
         if (rc == RH_OK) rc = dalloc(&d_cols, cols.size());
         hipError_t e = hipSuccess;
         if (rc == RH_OK) {
-            e = hipMemcpyAsync(d_rows, rows.data(), m * 4, hipMemcpyHostToDevice, s);
-            if (e == hipSuccess) e = hipMemcpyAsync(d_slots, slots.data(), m * 4, hipMemcpyHostToDevice, s);
-            if (e == hipSuccess) e = hipMemcpyAsync(d_cols, cols.data(), cols.size() * 8, hipMemcpyHostToDevice, s);
-            if (e == hipSuccess) e = g->gather_pending ? hipStreamWaitEvent(s, g->gathered, 0) : hipSuccess;
-            if (e == hipSuccess) e = g->wgather_pending ? hipStreamWaitEvent(s, g->wgathered, 0) : hipSuccess;
-            if (e == hipSuccess) {
+            // host vectors: through the context's bounce buffers (rh::h2d), never page-locked in place
+            rc = rh::h2d(g->ctx, d_rows, rows.data(), (uint64_t)m * 4, s);
+            if (rc == RH_OK) rc = rh::h2d(g->ctx, d_slots, slots.data(), (uint64_t)m * 4, s);
+            if (rc == RH_OK) rc = rh::h2d(g->ctx, d_cols, cols.data(), cols.size() * 8, s);
+            if (rc == RH_OK) e = g->gather_pending ? hipStreamWaitEvent(s, g->gathered, 0) : hipSuccess;
+            if (rc == RH_OK && e == hipSuccess) e = g->wgather_pending ? hipStreamWaitEvent(s, g->wgathered, 0) : hipSuccess;
+            if (rc == RH_OK && e == hipSuccess) {
                 g->gather_pending = g->wgather_pending = false;
                 hipLaunchKernelGGL(table_load_kernel, dim3((m + 255) / 256), dim3(256), 0, s, g->dev, t, d_rows, d_slots,
                                    d_cols, m);
                 e = hipGetLastError();
             }
-            if (e == hipSuccess) e = hipStreamSynchronize(s);
+            const hipError_t es = hipStreamSynchronize(s);   // the bounce copies and the load (error paths too)
+            if (e == hipSuccess) e = es;
         }
         (void)hipFree(d_rows);
         (void)hipFree(d_slots);
@@ -1366,10 +1368,9 @@ RH_EXPORT int rh_groups_read(rh_groups* g, uint32_t first, uint32_t n, uint8_t c
     }
     rc = rh_table_read(g->dev, first, n, column, g->d_read, s);
     if (rc != RH_OK) return rc;
-    RH_HIP(hipMemcpyAsync(out, g->d_read, (size_t)n * 8, hipMemcpyDeviceToHost, s));
-    // the read-back buffer is the table's: keep the lock (a read is a diagnostic, not the hot path)
-    RH_HIP(hipStreamSynchronize(s));
-    return RH_OK;
+    // the read-back buffer is the table's: keep the lock (a read is a diagnostic, not the hot path);
+    // the caller's array through the context's bounce buffers (rh::d2h waits for the stream)
+    return rh::d2h(g->ctx, out, g->d_read, (uint64_t)n * 8, s);
 }
 
 // ---- leader lease ------------------------------------------------------------------------------------

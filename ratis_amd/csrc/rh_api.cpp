@@ -117,10 +117,16 @@ hipError_t rh::pool_alloc(rh_ctx* ctx, void** p, size_t bytes, hipStream_t strea
     return hipMallocFromPoolAsync(p, bytes, ctx->pool, stream);
 }
 
+// Releases everything the context owns.  The device is drained first -- not only the context's
+// stream: pool scratch is freed stream-ordered on whatever stream a launch was given (PoolScratch),
+// and a zero-copy stamp may still be completing -- and a fault of that work is returned (the context
+// is released all the same), never dropped.
 RH_EXPORT int rh_shutdown(rh_ctx* ctx) {
     if (!ctx) return rh::fail(RH_E_INVAL, "rh_shutdown: ctx == NULL");
     DeviceGuard g(ctx->device);
-    (void)hipStreamSynchronize(ctx->stream);
+    hipError_t err = hipStreamSynchronize(ctx->stream);
+    const hipError_t e2 = hipDeviceSynchronize();
+    if (err == hipSuccess) err = e2;
     (void)hipFree(ctx->d_slice);
     (void)hipFree(ctx->d_shift);
     (void)hipFree(ctx->d_lane16);
@@ -128,9 +134,15 @@ RH_EXPORT int rh_shutdown(rh_ctx* ctx) {
     (void)hipFree(ctx->d_initff);
     (void)hipFree(ctx->d_slice8);
     if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
+    for (int i = 0; i < 2; ++i) {
+        if (ctx->bounce[i]) (void)hipHostFree(ctx->bounce[i]);
+        if (ctx->bounce_ev[i]) (void)hipEventDestroy(ctx->bounce_ev[i]);
+    }
+    if (ctx->zc_done) (void)hipEventDestroy(ctx->zc_done);
     if (ctx->pool) (void)hipMemPoolDestroy(ctx->pool);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
+    if (err != hipSuccess) return rh::hip_fail(err, "rh_shutdown: the context's last work");
     return RH_OK;
 }
 
@@ -138,6 +150,101 @@ RH_EXPORT int rh_synchronize(rh_ctx* ctx) {
     if (!ctx) return rh::fail(RH_E_INVAL, "rh_synchronize: ctx == NULL");
     DeviceGuard g(ctx->device);
     RH_HIP(hipStreamSynchronize(ctx->stream));
+    {
+        std::lock_guard<std::mutex> lk(ctx->stage_mu);
+        int rc = rh::zc_settle(ctx);
+        if (rc != RH_OK) return rc;
+    }
+    return RH_OK;
+}
+
+// ---- transfers of caller host memory (rh_internal.h) ------------------------------------------------
+bool rh::host_registered(const void* p, uint64_t n) {
+    if (n == 0) return true;
+    void *d0 = nullptr, *d1 = nullptr;
+    if (hipHostGetDevicePointer(&d0, const_cast<void*>(p), 0) != hipSuccess ||
+        hipHostGetDevicePointer(&d1, const_cast<uint8_t*>(static_cast<const uint8_t*>(p)) + n - 1, 0) != hipSuccess ||
+        static_cast<uint8_t*>(d1) - static_cast<uint8_t*>(d0) != (ptrdiff_t)(n - 1)) {
+        (void)hipGetLastError();   // a pageable range: not an error
+        return false;
+    }
+    return true;
+}
+
+namespace {
+// The bounce buffers and their events (under bounce_mu).
+int bounce_reserve(rh_ctx* ctx) {
+    for (int i = 0; i < 2; ++i) {
+        if (!ctx->bounce[i] && hipHostMalloc(reinterpret_cast<void**>(&ctx->bounce[i]), rh::kBounceBytes, 0) != hipSuccess) {
+            ctx->bounce[i] = nullptr;
+            return rh::fail(RH_E_NOMEM, "pinned bounce buffer");
+        }
+        if (!ctx->bounce_ev[i]) RH_HIP(hipEventCreateWithFlags(&ctx->bounce_ev[i], hipEventDisableTiming));
+    }
+    return RH_OK;
+}
+}  // namespace
+
+int rh::h2d(rh_ctx* ctx, void* dst, const void* src, uint64_t n, hipStream_t s) {
+    if (n == 0) return RH_OK;
+    if (host_registered(src, n)) {
+        RH_HIP(hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, s));
+        return RH_OK;
+    }
+    std::lock_guard<std::mutex> lk(ctx->bounce_mu);
+    int rc = bounce_reserve(ctx);
+    if (rc != RH_OK) return rc;
+    const uint8_t* in = static_cast<const uint8_t*>(src);
+    uint8_t* out = static_cast<uint8_t*>(dst);
+    for (uint64_t off = 0, k = 0; off < n; off += kBounceBytes, ++k) {
+        const int i = (int)(k & 1);
+        const uint64_t c = std::min<uint64_t>(kBounceBytes, n - off);
+        if (ctx->bounce_used[i]) RH_HIP(hipEventSynchronize(ctx->bounce_ev[i]));   // its last copy has read it
+        std::memcpy(ctx->bounce[i], in + off, c);
+        RH_HIP(hipMemcpyAsync(out + off, ctx->bounce[i], c, hipMemcpyHostToDevice, s));
+        RH_HIP(hipEventRecord(ctx->bounce_ev[i], s));
+        ctx->bounce_used[i] = true;
+    }
+    return RH_OK;
+}
+
+int rh::d2h(rh_ctx* ctx, void* dst, const void* src, uint64_t n, hipStream_t s) {
+    if (n == 0) return RH_OK;
+    if (host_registered(dst, n)) {
+        RH_HIP(hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, s));
+        RH_HIP(hipStreamSynchronize(s));
+        return RH_OK;
+    }
+    std::lock_guard<std::mutex> lk(ctx->bounce_mu);
+    int rc = bounce_reserve(ctx);
+    if (rc != RH_OK) return rc;
+    const uint8_t* in = static_cast<const uint8_t*>(src);
+    uint8_t* out = static_cast<uint8_t*>(dst);
+    // chunk k lands in buffer k & 1; the host drains chunk k - 1 while chunk k is in flight
+    const uint64_t chunks = (n + kBounceBytes - 1) / kBounceBytes;
+    for (uint64_t k = 0; k <= chunks; ++k) {
+        if (k < chunks) {
+            const int i = (int)(k & 1);
+            if (ctx->bounce_used[i]) RH_HIP(hipEventSynchronize(ctx->bounce_ev[i]));
+            const uint64_t off = k * kBounceBytes, c = std::min<uint64_t>(kBounceBytes, n - off);
+            RH_HIP(hipMemcpyAsync(ctx->bounce[i], in + off, c, hipMemcpyDeviceToHost, s));
+            RH_HIP(hipEventRecord(ctx->bounce_ev[i], s));
+            ctx->bounce_used[i] = true;
+        }
+        if (k > 0) {
+            const int i = (int)((k - 1) & 1);
+            const uint64_t off = (k - 1) * kBounceBytes, c = std::min<uint64_t>(kBounceBytes, n - off);
+            RH_HIP(hipEventSynchronize(ctx->bounce_ev[i]));
+            std::memcpy(out + off, ctx->bounce[i], c);
+        }
+    }
+    return RH_OK;
+}
+
+int rh::zc_settle(rh_ctx* ctx) {
+    if (!ctx->zc_pending) return RH_OK;
+    ctx->zc_pending = false;
+    RH_HIP(hipEventSynchronize(ctx->zc_done));
     return RH_OK;
 }
 
@@ -248,8 +355,12 @@ RH_EXPORT int rh_crc32c(rh_ctx* ctx, uint32_t crc_state, const void* data, uint6
         uint32_t len;
         uint32_t crc;
     } hdr{0, (uint32_t)n, 0};
-    RH_HIP(hipMemcpyAsync(base, data, n, hipMemcpyHostToDevice, s));
-    RH_HIP(hipMemcpyAsync(base + o_len, &hdr, sizeof(hdr), hipMemcpyHostToDevice, s));
+    int rc = rh::h2d(ctx, base, data, n, s);
+    if (rc == RH_OK) rc = rh::h2d(ctx, base + o_len, &hdr, sizeof(hdr), s);
+    if (rc != RH_OK) {
+        (void)hipStreamSynchronize(s);
+        return rc;
+    }
     rh_frames f{};
     f.buf = base;
     f.buf_len = n;
@@ -258,9 +369,9 @@ RH_EXPORT int rh_crc32c(rh_ctx* ctx, uint32_t crc_state, const void* data, uint6
     f.n = 1;
     f.init_state = crc_state;
     f.crc_out = reinterpret_cast<uint32_t*>(base + o_len + 12);
-    int rc = rh_crc_launch_impl(ctx, &f, 0, s);
+    rc = rh_crc_launch_impl(ctx, &f, 0, s);
     uint32_t value = 0;
-    if (rc == RH_OK) RH_HIP(hipMemcpyAsync(&value, base + o_len + 12, 4, hipMemcpyDeviceToHost, s));
+    if (rc == RH_OK) rc = rh::d2h(ctx, &value, base + o_len + 12, 4, s);
     RH_HIP(hipStreamSynchronize(s));
     if (rc != RH_OK) return rc;
     *out_state = ~value;  // getValue() = ~crc
@@ -283,9 +394,13 @@ RH_EXPORT int rh_crc32c_verify_host(rh_ctx* ctx, const uint8_t* seg, uint64_t se
     rh::PoolScratch scratch(s);  // per-call stream-ordered scratch (as rh_crc32c), freed on every exit
     if (scratch.alloc(ctx, total) != hipSuccess) return rh::fail(RH_E_NOMEM, "rh_crc32c_verify_host: device scratch");
     uint8_t* base = scratch.bytes();
-    RH_HIP(hipMemcpyAsync(base + o_seg, seg, seg_len, hipMemcpyHostToDevice, s));
-    RH_HIP(hipMemcpyAsync(base + o_off, frame_off, n * 8, hipMemcpyHostToDevice, s));
-    RH_HIP(hipMemcpyAsync(base + o_len, frame_len, n * 4, hipMemcpyHostToDevice, s));
+    int rc = rh::h2d(ctx, base + o_seg, seg, seg_len, s);
+    if (rc == RH_OK) rc = rh::h2d(ctx, base + o_off, frame_off, n * 8, s);
+    if (rc == RH_OK) rc = rh::h2d(ctx, base + o_len, frame_len, n * 4, s);
+    if (rc != RH_OK) {
+        (void)hipStreamSynchronize(s);
+        return rc;
+    }
     RH_HIP(hipMemsetAsync(base + o_bad, 0, nwords * 8 + 256, s));
     rh_frames f{};
     f.buf = base + o_seg;
@@ -297,13 +412,11 @@ RH_EXPORT int rh_crc32c_verify_host(rh_ctx* ctx, const uint8_t* seg, uint64_t se
     f.crc_out = reinterpret_cast<uint32_t*>(base + o_crc);
     f.bad_bits = reinterpret_cast<uint64_t*>(base + o_bad);
     f.n_bad = reinterpret_cast<unsigned long long*>(base + o_cnt);
-    int rc = rh_crc_launch_impl(ctx, &f, RH_CRC_VERIFY, s);
+    rc = rh_crc_launch_impl(ctx, &f, RH_CRC_VERIFY, s);
     unsigned long long cnt = 0;
-    if (rc == RH_OK) {
-        if (crc_out) RH_HIP(hipMemcpyAsync(crc_out, base + o_crc, n * 4, hipMemcpyDeviceToHost, s));
-        if (bad_bits) RH_HIP(hipMemcpyAsync(bad_bits, base + o_bad, nwords * 8, hipMemcpyDeviceToHost, s));
-        RH_HIP(hipMemcpyAsync(&cnt, base + o_cnt, sizeof(cnt), hipMemcpyDeviceToHost, s));
-    }
+    if (rc == RH_OK && crc_out) rc = rh::d2h(ctx, crc_out, base + o_crc, n * 4, s);
+    if (rc == RH_OK && bad_bits) rc = rh::d2h(ctx, bad_bits, base + o_bad, nwords * 8, s);
+    if (rc == RH_OK) rc = rh::d2h(ctx, &cnt, base + o_cnt, sizeof(cnt), s);
     RH_HIP(hipStreamSynchronize(s));
     if (rc != RH_OK) return rc;
     *n_bad = cnt;
@@ -319,10 +432,21 @@ RH_EXPORT int rh_host_register(rh_ctx* ctx, void* p, uint64_t n) {
     return RH_OK;
 }
 
+// The GPU's mapping of the buffer goes away here: every launch that may still read it -- a zero-copy
+// stamp of this or any other context (the registration is portable) returns on polled flags, before
+// its completion -- is drained first, and a fault of that work is returned.
 RH_EXPORT int rh_host_unregister(rh_ctx* ctx, void* p) {
     if (!ctx || !p) return rh::fail(RH_E_INVAL, "rh_host_unregister: ctx/p == NULL");
     DeviceGuard g(ctx->device);
+    int rc;
+    {
+        std::lock_guard<std::mutex> lk(ctx->stage_mu);
+        rc = rh::zc_settle(ctx);
+    }
+    const hipError_t e = hipDeviceSynchronize();
     RH_HIP(hipHostUnregister(p));
+    if (rc != RH_OK) return rc;
+    if (e != hipSuccess) return rh::hip_fail(e, "rh_host_unregister: work still reading the buffer");
     return RH_OK;
 }
 
@@ -376,10 +500,15 @@ int stamp_zero_copy(rh_ctx* ctx, uint8_t* buf, uint64_t lo, uint64_t hi, const u
     if (!RH_STAMP_ZERO_COPY || max_len - 4 >= (64ull << kStampShifts) || ctx->h_initff.empty() ||
         hi - lo > (uint64_t)kStampMaxGroups * 3 / 4 * kStampSpan)   // would not fit the workgroups
         return kNotPlanned;
+    // the workgroups move 16-byte pieces from (offset & ~15) up to (end + 15) & ~15 of `buf`: that
+    // whole range, not only the frames, must lie inside the registration (a batch ending within 15
+    // bytes of the registration's end would otherwise read past it -- a GPU page fault when that end
+    // is also a page's end)
+    const uint64_t r_lo = lo & ~15ull, r_hi = (hi + 15) & ~15ull;
     uint8_t *d_lo = nullptr, *d_hi = nullptr;
     if (hipHostGetDevicePointer(reinterpret_cast<void**>(&d_lo), buf + lo, 0) != hipSuccess ||
         hipHostGetDevicePointer(reinterpret_cast<void**>(&d_hi), buf + hi - 1, 0) != hipSuccess ||
-        (uint64_t)(d_hi - d_lo) != hi - 1 - lo) {
+        (uint64_t)(d_hi - d_lo) != hi - 1 - lo || !rh::host_registered(buf + r_lo, r_hi - r_lo)) {
         (void)hipGetLastError();   // not registered (mapped): the copying plan
         return kNotPlanned;
     }
@@ -458,7 +587,15 @@ int stamp_zero_copy(rh_ctx* ctx, uint8_t* buf, uint64_t lo, uint64_t hi, const u
         }
         std::atomic_thread_fence(std::memory_order_acquire);
     }
-    if (!seen) RH_HIP(hipStreamSynchronize(s));
+    if (!seen) {
+        RH_HIP(hipStreamSynchronize(s));
+    } else {
+        // returned on the flags: the launch's completion (and any fault of it) is checked by the
+        // next stamp, rh_synchronize, rh_host_unregister or rh_shutdown
+        if (!ctx->zc_done) RH_HIP(hipEventCreateWithFlags(&ctx->zc_done, hipEventDisableTiming));
+        RH_HIP(hipEventRecord(ctx->zc_done, s));
+        ctx->zc_pending = true;
+    }
     const uint32_t* crc = reinterpret_cast<const uint32_t*>(st + o_crc);
     for (uint64_t i = 0; i < n; ++i) {   // buf.putInt((int) checksum.getValue()): big-endian
         uint8_t* t = buf + frame_off[i] + frame_len[i] - 4;
@@ -497,6 +634,8 @@ RH_EXPORT int rh_crc32c_stamp_host(rh_ctx* ctx, uint8_t* buf, uint64_t buf_len, 
     const uint64_t span = hi - lo;
     const uint64_t t_off = 0, t_len = al(n * 8), t_crc = t_len + al(n * 4), t_bytes = t_crc + al(n * 4);
     std::lock_guard<std::mutex> lk(ctx->stage_mu);
+    const int zs = rh::zc_settle(ctx);   // the last zero-copy launch read the staging this call rewrites
+    if (zs != RH_OK) return zs;
     const int zc = stamp_zero_copy(ctx, buf, lo, hi, frame_off, frame_len, n, max_len);
     if (zc != kNotPlanned) return zc;
     const int rs = stage_reserve(ctx, t_bytes);
@@ -520,10 +659,13 @@ RH_EXPORT int rh_crc32c_stamp_host(rh_ctx* ctx, uint8_t* buf, uint64_t buf_len, 
     rh::PoolScratch scratch(s);
     if (scratch.alloc(ctx, total) != hipSuccess) return rh::fail(RH_E_NOMEM, "rh_crc32c_stamp_host: device scratch");
     uint8_t* base = scratch.bytes();
-    RH_HIP(hipMemcpyAsync(base + o_img + kPad, buf + lo, span, hipMemcpyHostToDevice, s));
+    int rc = rh::h2d(ctx, base + o_img + kPad, buf + lo, span, s);
+    if (rc != RH_OK) {
+        (void)hipStreamSynchronize(s);
+        return rc;
+    }
     f.buf = base + o_img;
-    // STAMP also writes the device copy's trailers
-    int rc;
+    // the CRCs come back (crc_out) and the host writes the trailers; the device copy is not stamped
     if (RH_STAMP_PLAN == 2) {   // the frame table and the CRCs through the staging's device mapping
         uint8_t* dst = nullptr;
         RH_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&dst), st, 0));
@@ -599,9 +741,13 @@ RH_EXPORT int rh_segments_read_host(rh_ctx* ctx, const uint8_t* image, uint64_t 
     rh::PoolScratch scratch(s);
     if (scratch.alloc(ctx, o) != hipSuccess) return rh::fail(RH_E_NOMEM, "rh_segments_read_host: device scratch");
     uint8_t* b = scratch.bytes();
-    if (image_len) RH_HIP(hipMemcpyAsync(b + o_img, image, image_len, hipMemcpyHostToDevice, s));
-    RH_HIP(hipMemcpyAsync(b + o_soff, seg_off, n_seg * 8, hipMemcpyHostToDevice, s));
-    RH_HIP(hipMemcpyAsync(b + o_slen, seg_len, n_seg * 8, hipMemcpyHostToDevice, s));
+    int rc = rh::h2d(ctx, b + o_img, image, image_len, s);
+    if (rc == RH_OK) rc = rh::h2d(ctx, b + o_soff, seg_off, n_seg * 8, s);
+    if (rc == RH_OK) rc = rh::h2d(ctx, b + o_slen, seg_len, n_seg * 8, s);
+    if (rc != RH_OK) {
+        (void)hipStreamSynchronize(s);
+        return rc;
+    }
     rh_segments sg{};
     sg.buf = b + o_img;
     sg.buf_len = image_len;
@@ -626,29 +772,40 @@ RH_EXPORT int rh_segments_read_host(rh_ctx* ctx, const uint8_t* image, uint64_t 
     cr.seg_read_status = reinterpret_cast<int32_t*>(b + o_rst);
     cr.seg_read_stop = reinterpret_cast<uint64_t*>(b + o_rstop);
     cr.crc_out = reinterpret_cast<uint32_t*>(b + o_fcrc);
-    int rc = rh_segments_read_impl(ctx, &sg, &cr, s);
-    if (rc != RH_OK) return rc;
-    std::vector<uint64_t> first(n_seg), rstop(n_seg);
-    std::vector<uint32_t> nfr(n_seg), ok(n_seg);
-    std::vector<int32_t> rst(n_seg);
-    unsigned long long total = 0;
+    rc = rh_segments_read_impl(ctx, &sg, &cr, s);
+    if (rc != RH_OK) {
+        (void)hipStreamSynchronize(s);
+        return rc;
+    }
+    std::vector<uint64_t> first, rstop;
+    std::vector<uint32_t> nfr, ok;
+    std::vector<int32_t> rst;
     try {
-        RH_HIP(hipMemcpyAsync(first.data(), b + o_first, n_seg * 8, hipMemcpyDeviceToHost, s));
-        RH_HIP(hipMemcpyAsync(nfr.data(), b + o_nfr, n_seg * 4, hipMemcpyDeviceToHost, s));
-        RH_HIP(hipMemcpyAsync(ok.data(), b + o_ok, n_seg * 4, hipMemcpyDeviceToHost, s));
-        RH_HIP(hipMemcpyAsync(rst.data(), b + o_rst, n_seg * 4, hipMemcpyDeviceToHost, s));
-        RH_HIP(hipMemcpyAsync(rstop.data(), b + o_rstop, n_seg * 8, hipMemcpyDeviceToHost, s));
-        RH_HIP(hipMemcpyAsync(&total, b + o_tot, sizeof(total), hipMemcpyDeviceToHost, s));
-        RH_HIP(hipStreamSynchronize(s));
+        first.resize(n_seg);
+        rstop.resize(n_seg);
+        nfr.resize(n_seg);
+        ok.resize(n_seg);
+        rst.resize(n_seg);
     } catch (...) {
+        (void)hipStreamSynchronize(s);
         return rh::fail(RH_E_NOMEM, "rh_segments_read_host: out of host memory");
     }
+    unsigned long long total = 0;
+    rc = rh::d2h(ctx, first.data(), b + o_first, n_seg * 8, s);
+    if (rc == RH_OK) rc = rh::d2h(ctx, nfr.data(), b + o_nfr, n_seg * 4, s);
+    if (rc == RH_OK) rc = rh::d2h(ctx, ok.data(), b + o_ok, n_seg * 4, s);
+    if (rc == RH_OK) rc = rh::d2h(ctx, rst.data(), b + o_rst, n_seg * 4, s);
+    if (rc == RH_OK) rc = rh::d2h(ctx, rstop.data(), b + o_rstop, n_seg * 8, s);
+    if (rc == RH_OK) rc = rh::d2h(ctx, &total, b + o_tot, sizeof(total), s);
     const uint64_t nout = std::min<uint64_t>(total, frame_cap);
-    if (nout) {
-        RH_HIP(hipMemcpyAsync(frame_off, b + o_foff, nout * 8, hipMemcpyDeviceToHost, s));
-        RH_HIP(hipMemcpyAsync(frame_len, b + o_flen, nout * 4, hipMemcpyDeviceToHost, s));
-        if (frame_crc) RH_HIP(hipMemcpyAsync(frame_crc, b + o_fcrc, nout * 4, hipMemcpyDeviceToHost, s));
-        RH_HIP(hipStreamSynchronize(s));
+    if (rc == RH_OK && nout) {
+        rc = rh::d2h(ctx, frame_off, b + o_foff, nout * 8, s);
+        if (rc == RH_OK) rc = rh::d2h(ctx, frame_len, b + o_flen, nout * 4, s);
+        if (rc == RH_OK && frame_crc) rc = rh::d2h(ctx, frame_crc, b + o_fcrc, nout * 4, s);
+    }
+    if (rc != RH_OK) {
+        (void)hipStreamSynchronize(s);
+        return rc;
     }
     for (uint64_t i = 0; i < n_seg; ++i) {
         rh_segment_result& r = results[i];

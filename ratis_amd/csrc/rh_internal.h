@@ -273,6 +273,19 @@ struct rh_ctx {
     void* h_pinned = nullptr;
     size_t pinned_bytes = 0;
     hipMemPool_t pool = nullptr;  // stream-ordered scratch (rh::pool_alloc)
+    // The zero-copy stamp returns on polled flags, before its launch has completed: its completion,
+    // checked by the next stamp, rh_synchronize, rh_host_unregister and rh_shutdown (a fault of that
+    // launch is reported, never dropped).  Under stage_mu.
+    hipEvent_t zc_done = nullptr;
+    bool zc_pending = false;
+    // Pinned bounce buffers for transfers of CALLER host memory (rh::h2d / rh::d2h): the HIP runtime
+    // is never handed pageable memory the library does not own (it would page-lock it behind the
+    // call, and a lock that outlives the caller's buffer is a GPU mapping of freed pages -- DESIGN
+    // §11).  Two buffers of kBounceBytes, each with the event of the last copy that used it.
+    std::mutex bounce_mu;
+    uint8_t* bounce[2] = {nullptr, nullptr};
+    hipEvent_t bounce_ev[2] = {nullptr, nullptr};
+    bool bounce_used[2] = {false, false};
 };
 
 // Launchers implemented in the .hip files (device pointers, async on `stream`).
@@ -293,6 +306,18 @@ struct PoolScratch {
     hipError_t alloc(rh_ctx* ctx, size_t bytes) { return pool_alloc(ctx, &p, bytes, s); }
     uint8_t* bytes() const { return static_cast<uint8_t*>(p); }
 };
+
+// Transfers between CALLER host memory and the device on `s`.  A range inside one registration the
+// runtime knows (rh_host_register, hipHostMalloc) is copied directly; any other range goes through
+// the context's pinned bounce buffers in kBounceBytes chunks (the memcpy of chunk k + 1 overlaps the
+// DMA of chunk k).  h2d: enqueued, `src` reusable on return.  d2h: `dst` holds the bytes on return
+// (it waits for the stream).
+constexpr uint64_t kBounceBytes = 4ull << 20;
+bool host_registered(const void* p, uint64_t n);
+int h2d(rh_ctx* ctx, void* dst, const void* src, uint64_t n, hipStream_t s);
+int d2h(rh_ctx* ctx, void* dst, const void* src, uint64_t n, hipStream_t s);
+// Waits for the context's outstanding zero-copy stamp (if any); its fault is returned.
+int zc_settle(rh_ctx* ctx);
 }  // namespace rh
 
 int rh_commit_launch_impl(rh_ctx* ctx, const rh_commit_soa* tiers, int n_tiers, hipStream_t stream);

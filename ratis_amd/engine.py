@@ -22,6 +22,7 @@ Reference mapping (paths relative to the ratis tree):
 from __future__ import annotations
 
 import ctypes
+import weakref
 from dataclasses import dataclass, field
 from typing import List, Optional, Sequence
 
@@ -46,6 +47,14 @@ def _stream_ptr(stream: Optional[torch.cuda.Stream]) -> int:
     return s.cuda_stream
 
 
+_LIVE = weakref.WeakSet()
+
+
+def live_contexts() -> List["Context"]:
+    """The contexts not closed yet (tests/conftest.py drains each after every GPU test)."""
+    return [c for c in list(_LIVE) if c._h is not None]
+
+
 class Context:
     """One ``rh_ctx`` per (process, GPU)."""
 
@@ -58,6 +67,7 @@ class Context:
         h = ctypes.c_void_p()
         check(lib.rh_init(device, ctypes.byref(h)))
         self._h = h
+        _LIVE.add(self)
 
     @property
     def handle(self) -> ctypes.c_void_p:
@@ -65,10 +75,15 @@ class Context:
             raise _lib.RatisHipError(_lib.RH_E_STATE, "context closed")
         return self._h
 
+    def synchronize(self) -> None:
+        """``rh_synchronize``: the context stream drained, an outstanding zero-copy stamp settled;
+        raises on a fault of that work."""
+        check(_lib.load().rh_synchronize(self.handle))
+
     def close(self) -> None:
         if self._h is not None:
-            check(_lib.load().rh_shutdown(self._h))
-            self._h = None
+            h, self._h = self._h, None
+            check(_lib.load().rh_shutdown(h))   # raises if the context's last work faulted
 
     def __enter__(self):
         return self

@@ -1,0 +1,174 @@
+"""Host-memory hand-offs between the library and its caller (VERDICT r05 What's weak #1):
+each test drives one hand-off whose teardown used to race the GPU, in the order a caller would, and
+then uses the same host memory the way the failing driver run did -- freed, reallocated at the same
+size (numpy hands the address back) and copied across PCIe by torch.  Every step must succeed and
+every result match the oracle; the autouse fault fixture (conftest.py) then drains every context.
+
+  * the zero-copy stamp returns on polled flags before its launch completes: an immediate
+    rh_host_unregister and an immediate rh_shutdown (the JNI stamper's tail: stampHost0,
+    hostUnregister0, ctxDestroy0) must wait for it and report its fault, not drop it;
+  * a batch ending where the registration ends: the stamp's 16-byte DMA pieces must never read
+    past the registration (the plan falls back to the copying path instead);
+  * the host APIs (rh_crc32c, rh_crc32c_verify_host, rh_segments_read_host, rh_groups_load /
+    rh_groups_read) with caller arrays freed and reallocated right after each call: the library
+    copies through its own pinned bounce buffers, so the runtime never page-locks caller memory;
+  * rh_shutdown right after launches that took pool scratch on a caller's side stream."""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _batch(orc, rng, n_frames, lo=1, hi=3000):
+    frames = [orc.frame_write(rng.integers(0, 256, int(rng.integers(lo, hi)), dtype=np.uint8).tobytes())
+              for _ in range(n_frames)]
+    want = np.frombuffer(b"".join(frames), dtype=np.uint8).copy()
+    off = np.cumsum([0] + [len(f) for f in frames[:-1]]).astype(np.uint64)
+    ln = np.array([len(f) for f in frames], np.uint32)
+    return want, off, ln
+
+
+def _torch_roundtrip(nbytes, seed):
+    """A fresh pageable array of `nbytes` (numpy reuses the address just freed), through the GPU and
+    back by torch's own pageable copies (the copies that reported the round-5 fault)."""
+    import torch
+    a = np.random.default_rng(seed).integers(0, 256, nbytes, dtype=np.uint8)
+    g = torch.from_numpy(a).cuda()
+    back = g.cpu().numpy()
+    assert np.array_equal(a, back)
+
+
+def test_unregister_and_destroy_right_after_zero_copy_stamp(orc):
+    from ratis_amd import engine
+    rng = np.random.default_rng(11)
+    for rep in range(6):
+        want, off, ln = _batch(orc, rng, 300)
+        wb = np.zeros(want.size + 4096, np.uint8)
+        wb[: want.size] = want
+        for o, l in zip(off.astype(np.int64), ln.astype(np.int64)):
+            wb[o + l - 4: o + l] = 0
+        c = engine.Context(0)
+        reg = engine.HostRegistration(c, wb)
+        engine.stamp_host(c, wb, off, ln)     # zero-copy: returns on the workgroups' flags
+        reg.close()                           # hostUnregister0 right away
+        c.close()                             # ctxDestroy0 right away (reports a fault of the stamp)
+        assert np.array_equal(wb[: want.size], want)
+        nbytes = wb.size
+        del wb
+        _torch_roundtrip(max(nbytes, 2 << 20), rep)
+
+
+def test_stamp_never_reads_past_the_registration(ctx, orc):
+    """Batches ending 0..15 bytes short of a 16-byte boundary at the registration's very end (a
+    page-aligned end, where a read past it would fault): every trailer right."""
+    from ratis_amd import engine
+    rng = np.random.default_rng(12)
+    page = 4096
+    for _ in range(16):
+        want, off, ln = _batch(orc, rng, 40, hi=1500)
+        store = np.zeros(want.size + 3 * page, np.uint8)
+        end = (store.ctypes.data + want.size + page) // page * page   # a page boundary inside `store`
+        s0 = end - want.size - store.ctypes.data
+        buf = store[s0: s0 + want.size]
+        assert (buf.ctypes.data + buf.size) % page == 0
+        buf[:] = want
+        for o, l in zip(off.astype(np.int64), ln.astype(np.int64)):
+            buf[o + l - 4: o + l] = 0
+        with engine.HostRegistration(ctx, buf):
+            engine.stamp_host(ctx, buf, off, ln)
+            assert np.array_equal(buf, want)
+
+
+def test_host_apis_with_caller_arrays_freed_and_reused(ctx, orc):
+    from ratis_amd import _lib, engine, segment
+    lib = _lib.load()
+    rng = np.random.default_rng(13)
+    vp = ctypes.c_void_p
+    for rep in range(3):
+        # rh_crc32c_verify_host over a 3 MiB image of 4 KiB frames
+        n_fr = 768
+        img = rng.integers(0, 256, n_fr * 4096, dtype=np.uint8)
+        off = np.arange(n_fr, dtype=np.uint64) * 4096
+        ln = np.full(n_fr, 4096, np.uint32)
+        crc = np.zeros(n_fr, np.uint32)
+        bad = np.zeros((n_fr + 63) // 64, np.uint64)
+        nb = ctypes.c_uint64()
+        _lib.check(lib.rh_crc32c_verify_host(ctx.handle, vp(img.ctypes.data), img.size, vp(off.ctypes.data),
+                                             vp(ln.ctypes.data), n_fr, vp(crc.ctypes.data), vp(bad.ctypes.data),
+                                             ctypes.byref(nb)))
+        want_crc, want_bad = orc.crc32c_frames(img, off, ln)
+        assert np.array_equal(crc, want_crc) and nb.value == want_bad
+        nbytes = img.size
+        del img, crc, bad
+        _torch_roundtrip(nbytes, 100 + rep)
+        # rh_crc32c over a 5 MiB span (two bounce chunks and a tail)
+        data = rng.integers(0, 256, (5 << 20) + 123, dtype=np.uint8).tobytes()
+        assert engine.crc32c_update(ctx, 0xFFFFFFFF, data) == orc.crc32c_update(0xFFFFFFFF, data)
+        nbytes = len(data)
+        del data
+        _torch_roundtrip(nbytes, 200 + rep)
+        # rh_segments_read_host over a 9 MiB image
+        protos = segment.simple_operation_entries(2000, term=1)
+        seg, fo, fl = segment.build_segment(protos)
+        c0, _ = orc.crc32c_frames(seg, fo, fl)
+        for o, l, c in zip(fo.astype(np.int64), fl.astype(np.int64), c0):
+            seg[o + l - 4: o + l] = np.frombuffer(int(c).to_bytes(4, "big"), np.uint8)
+        reps = max(1, (9 << 20) // max(seg.size, 1))
+        step = (seg.size + 4096 + 255) // 256 * 256
+        image = np.zeros(step * reps, np.uint8)
+        for k in range(reps):
+            image[k * step: k * step + seg.size] = seg
+        so = np.arange(reps, dtype=np.int64) * step
+        sl = np.full(reps, seg.size + 4096, np.int64)
+        r = engine.read_segments_host(ctx, image, so, sl, frames_per_seg_cap=fo.size + 8)
+        ro, _, _, rst, rstop = orc.segment_scan(np.concatenate([seg, np.zeros(4096, np.uint8)]))
+        assert (r["status"] == rst).all() and (r["n_ok"] == len(ro)).all() and (r["stop"] == rstop).all()
+        nbytes = image.size
+        del image
+        _torch_roundtrip(nbytes, 300 + rep)
+
+
+def test_table_load_and_read_through_bounce_buffers(ctx, orc):
+    """rh_groups_load with 1.2 M rows' columns (host vectors of ~60 MiB) and rh_groups_read of every
+    slot back into a caller array freed right after: the values loaded come back."""
+    from ratis_amd import _lib, groups
+    rng = np.random.default_rng(14)
+    n = 1_200_000
+    with groups.RaftGroupTable(ctx, capacity=n) as tab:
+        conf = np.full(n, 0b1111 | (1 << 14) | (1 << 31), np.uint32)
+        flush = rng.integers(1 << 20, 1 << 30, n, dtype=np.int64)
+        commit = flush - rng.integers(0, 1000, n)
+        tstart = commit - 5
+        match = (flush[None, :] - rng.integers(0, 2000, (4, n))).astype(np.int64)
+        tab.load(0, conf, flush, commit, tstart, match=match)
+        for col, want in ((_lib.RH_COL_FLUSH, flush), (_lib.RH_COL_COMMITTED, commit), (0, match[0]), (3, match[3])):
+            got = tab.read(col, 0, n)
+            assert np.array_equal(got, want)
+            nbytes = got.nbytes
+            del got
+            _torch_roundtrip(nbytes, col)
+
+
+def test_shutdown_right_after_pool_scratch_on_a_side_stream(orc):
+    """Launches whose scratch comes from the context's stream-ordered pool, on a torch side stream,
+    then rh_shutdown at once (no synchronisation by the caller): the pool outlives that work."""
+    import torch
+
+    from ratis_amd import engine, workload
+    side = torch.cuda.Stream()
+    for rep in range(3):
+        c = engine.Context(0)
+        ss = workload.synth_segments(c, n_segments=4, corrupt_rate=0.0, seed=21 + rep)
+        n = ss.n_segments
+        with torch.cuda.stream(side):
+            seg_off = torch.arange(n, dtype=torch.int64, device="cuda") * ss.segment_size
+            seg_len = torch.full((n,), ss.segment_size, dtype=torch.int64, device="cuda")
+            b = engine.SegmentBatch(buf=ss.batch.buf, seg_off=seg_off, seg_len=seg_len,
+                                    frames_per_seg_cap=ss.frames_per_segment + 16)
+            r = engine.read_segments(c, b, stream=side)
+        c.close()                 # drains the device before the pool goes
+        side.synchronize()
+        assert int(r["total_frames"].item()) == n * ss.frames_per_segment
+        _torch_roundtrip(32 << 20, 400 + rep)
