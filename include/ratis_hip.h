@@ -250,7 +250,10 @@ int rh_groups_load(rh_groups* g, uint32_t first, uint32_t n, uint32_t n_host_fol
                    const int64_t* term_start, const uint32_t* conf);
 /* Copies deltas into the pinned staging ring (RaftLogIndex semantics per op, see Ordering above).
  * Deltas of stopped slots or of follower columns the slot's tier does not have are rejected
- * (RH_E_INVAL, nothing applied).  Returns once the caller's buffer may be reused.  Multi-producer:
+ * (RH_E_INVAL, nothing applied).  A call with more deltas than the open slot's room is staged
+ * chunk by chunk; a control call may take effect between two chunks, and each later chunk is checked
+ * again against the slot states it finds -- a delta rejected then fails the call with the earlier
+ * chunks staged (the message names them).  Returns once the caller's buffer may be reused.  Multi-producer:
  * concurrent calls copy into ranges of the open slot reserved with one atomic each, never waiting
  * for an evaluation, a _wait call or another producer's copy; a call's deltas keep their order and
  * calls that do not overlap in time keep theirs.  Staged deltas reach the device when the slot is

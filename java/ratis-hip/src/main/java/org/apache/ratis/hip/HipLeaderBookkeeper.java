@@ -497,11 +497,7 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
       for (int s = 0; s < RatisHip.MAX_FOLLOWERS; s++) {
         if (!followerSlot.containsValue(s)) {
           followerSlot.put(peer, s);
-          // a new FollowerInfoImpl starts at matchIndex = commitIndex = -1 (FollowerInfoImpl.java:42-43);
-          // a recycled slot still holds its previous peer's indices
-          emit(s, RatisHip.colMatch(s), RatisHip.OP_SET, -1L);
-          emit(s, RatisHip.colFollowerCommit(s), RatisHip.OP_SET, -1L);
-          emit(s, RatisHip.colTs(s), RatisHip.OP_SET, System.nanoTime());  // lastRpcTime (FollowerInfoImpl.java:58)
+          resetFollowerSlot(s);
           return s;
         }
       }
@@ -509,9 +505,50 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
       return -1;
     }
 
-    /** stopAndRemoveSenders (LeaderStateImpl.java:694-702): the slot becomes reusable. */
+    /**
+     * A new FollowerInfoImpl starts at matchIndex = commitIndex = -1 (FollowerInfoImpl.java:42-43)
+     * and lastRpcTime = now (:58).  A recycled slot still holds its previous peer's values, and that
+     * peer's last deltas may still sit in any producer thread's buffer -- buffers are pushed in
+     * registration order, so a reset SET buffered by this thread could reach the library before a
+     * stale MAX buffered by another, and the new follower would inherit the old matchIndex.  So,
+     * under the write lock (no delta is emitted meanwhile): every buffer is pushed first, then the
+     * three SETs go straight to the library, after every delta of the previous occupant.
+     */
+    private void resetFollowerSlot(int s) {
+      order.writeLock().lock();
+      try {
+        if (!started || s >= width) {
+          return;   // not in the tier: a widening reconf starts the column at -1
+        }
+        flushAllDeltas();
+        final ByteBuffer bb =
+            ByteBuffer.allocateDirect(3 * RatisHip.DELTA_BYTES).order(ByteOrder.LITTLE_ENDIAN);
+        RatisHip.putDelta(bb, nodeSlot, RatisHip.colMatch(s), RatisHip.OP_SET, -1L);
+        RatisHip.putDelta(bb, nodeSlot, RatisHip.colFollowerCommit(s), RatisHip.OP_SET, -1L);
+        RatisHip.putDelta(bb, nodeSlot, RatisHip.colTs(s), RatisHip.OP_SET, System.nanoTime());
+        hip.pushDeltas(bb, 3);
+      } catch (IOException e) {
+        throw new IllegalStateException("ratis-hip: pushDeltas failed", e);
+      } finally {
+        order.writeLock().unlock();
+      }
+    }
+
+    /**
+     * stopAndRemoveSenders (LeaderStateImpl.java:694-702): the slot becomes reusable.  The peer's
+     * buffered deltas are pushed now, under the write lock, so none of them can follow the reset
+     * of the slot's next occupant.
+     */
     public synchronized void removeFollower(RaftPeerId peer) {
       followerSlot.remove(peer);
+      order.writeLock().lock();
+      try {
+        if (started) {
+          flushAllDeltas();
+        }
+      } finally {
+        order.writeLock().unlock();
+      }
     }
 
     /**

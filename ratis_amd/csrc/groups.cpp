@@ -633,18 +633,6 @@ int stage_submit(rh_groups* g) {
     return ring_submit(g, i, n, has_set);
 }
 
-// Opens the next host slot for rh_push_deltas (waiting until its previous H2D has completed).
-int stage_open(rh_groups* g) {
-    int rc = stage_submit(g);
-    if (rc != RH_OK) return rc;
-    const int i = g->ring_next;
-    rc = ring_wait(g, i);
-    if (rc != RH_OK) return rc;
-    g->open = i;
-    g->fill.store(0, std::memory_order_relaxed);
-    return RH_OK;
-}
-
 // The exclusive side of the staging: both locks, staged deltas submitted first.
 struct Exclusive {
     std::unique_lock<std::shared_mutex> x;
@@ -1078,32 +1066,43 @@ RH_EXPORT int rh_push_deltas(rh_groups* g, const rh_delta* deltas, size_t n) {
     if (!g) return rh::fail(RH_E_INVAL, "rh_push_deltas: groups == NULL");
     if (n == 0) return RH_OK;
     if (!deltas) return rh::fail(RH_E_INVAL, "rh_push_deltas: deltas == NULL");
-    bool validated = false, any_set = false;
+    // deltas [lo, hi) against the current slot map (caller holds smu); a producer's deltas come in
+    // runs per division (a reply's SET + MAXes): the slot map is read once per run
+    bool any_set = false;
     size_t done = 0;
+    auto validate = [&](size_t lo, size_t hi) -> int {
+        uint32_t last = kNoRow, m = kNoRow, w = 0;
+        for (size_t i = lo; i < hi; ++i) {
+            const rh_delta& d = deltas[i];
+            if (d.slot != last || i == lo) {
+                last = d.slot;
+                m = d.slot < g->capacity ? g->slot_map[d.slot] : kNoRow;
+                w = m == kNoRow ? 0u : rh::width_of_tier((int)(m >> 28));
+            }
+            const uint32_t c = d.column;
+            const bool ok_col = c < w || (c >= 16 && c < 16 + w) || c == RH_COL_FLUSH || c == RH_COL_COMMITTED ||
+                                (c >= 48 && c < 48 + w) || c == RH_COL_LEASE || c == RH_COL_LEASE_ON;
+            if (m == kNoRow || !ok_col || d.op > RH_OP_SET)
+                return rh::fail(RH_E_INVAL, "rh_push_deltas: delta " + std::to_string(i) +
+                                                " names a stopped slot, a column outside its tier or an unknown op" +
+                                                (done ? " (deltas [0, " + std::to_string(done) + ") were staged)" : ""));
+            any_set |= d.op == RH_OP_SET;
+        }
+        return RH_OK;
+    };
+    // The whole call is checked first: a rejected call stages nothing.  A call longer than the open
+    // slot's room is staged chunk by chunk, and between two chunks the exclusive side below runs
+    // (and so may a control call): the next chunk is checked again against the slot map it finds.
+    bool recheck = false, validated = false;
     while (done < n) {
         {
             std::shared_lock<std::shared_mutex> sl(g->smu);   // the slot map changes only under exclusive
             if (g->ring_acquired >= 0) return rh::fail(RH_E_STATE, "rh_push_deltas: a staging slot is acquired");
-            if (!validated) {
-                // a producer's deltas come in runs per division (a reply's SET + MAXes): the slot
-                // map is read once per run
-                uint32_t last = kNoRow, m = kNoRow, w = 0;
-                for (size_t i = 0; i < n; ++i) {
-                    const rh_delta& d = deltas[i];
-                    if (d.slot != last || i == 0) {
-                        last = d.slot;
-                        m = d.slot < g->capacity ? g->slot_map[d.slot] : kNoRow;
-                        w = m == kNoRow ? 0u : rh::width_of_tier((int)(m >> 28));
-                    }
-                    const uint32_t c = d.column;
-                    const bool ok_col = c < w || (c >= 16 && c < 16 + w) || c == RH_COL_FLUSH || c == RH_COL_COMMITTED ||
-                                        (c >= 48 && c < 48 + w) || c == RH_COL_LEASE || c == RH_COL_LEASE_ON;
-                    if (m == kNoRow || !ok_col || d.op > RH_OP_SET)
-                        return rh::fail(RH_E_INVAL, "rh_push_deltas: delta " + std::to_string(i) +
-                                                        " names a stopped slot, a column outside its tier or an unknown op");
-                    any_set |= d.op == RH_OP_SET;
-                }
+            if (!validated || recheck) {
+                const int rc = validate(done, validated ? std::min<size_t>(n, done + RH_DELTA_SLOT) : n);
+                if (rc != RH_OK) return rc;
                 validated = true;
+                recheck = false;
             }
             if (g->open >= 0) {
                 uint64_t r = g->fill.load(std::memory_order_relaxed), take = 0;
@@ -1122,13 +1121,27 @@ RH_EXPORT int rh_push_deltas(rh_groups* g, const rh_delta* deltas, size_t n) {
                 }
             }
         }
-        // no open slot, or it is full: submit it and open the next one
+        recheck = true;   // the staging lock is left below: the next chunk is checked again
+        // no open slot, or it is full: submit it and open the next one -- waiting for the next slot's
+        // previous H2D / in-place apply with both locks released (no producer blocks the
+        // others, nor the _async / _wait callers, on device work)
         DeviceGuard dg(g->ctx->device);
         Exclusive ex(g);
         if (g->ring_acquired >= 0) return rh::fail(RH_E_STATE, "rh_push_deltas: a staging slot is acquired");
         if (g->open < 0 || g->fill.load(std::memory_order_relaxed) >= RH_DELTA_SLOT) {
-            int rc = stage_open(g);
+            int rc = stage_submit(g);
             if (rc != RH_OK) return rc;
+            const int i = g->ring_next;
+            if (g->ring_used[i] && hipEventQuery(g->ring_free[i]) == hipErrorNotReady) {
+                rc = wait_unlocked(ex, g->ring_free[i]);
+                if (rc != RH_OK) return rc;
+                continue;   // re-checked from the top (another producer may have opened a slot)
+            }
+            (void)hipGetLastError();
+            rc = ring_wait(g, i);   // complete (or never used): returns at once, reports a fault
+            if (rc != RH_OK) return rc;
+            g->open = i;
+            g->fill.store(0, std::memory_order_relaxed);
         }
     }
     return RH_OK;
@@ -1530,7 +1543,10 @@ RH_EXPORT int rh_node_destroy(rh_node* nd) {
         const int r = rh_groups_destroy(t);
         if (r != RH_OK && rc == RH_OK) rc = r, msg = rh_last_error();   // the first shard's failure
     }
-    for (rh_ctx* c : nd->ctx) (void)rh_shutdown(c);
+    for (rh_ctx* c : nd->ctx) {   // rh_shutdown reports a fault of the shard's last work as well
+        const int r = rh_shutdown(c);
+        if (r != RH_OK && rc == RH_OK) rc = r, msg = rh_last_error();
+    }
     delete nd;
     return rc == RH_OK ? RH_OK : rh::fail(rc, msg);
 }

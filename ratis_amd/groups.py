@@ -563,14 +563,26 @@ class PumpDivision:
         for k in range(self.MAX_FOLLOWERS):
             if k not in used:
                 self.follower_slot[peer] = k
-                self._emit(k, _lib.rh_col_match(k), _lib.RH_OP_SET, -1)
-                self._emit(k, _lib.rh_col_fcommit(k), _lib.RH_OP_SET, -1)
+                self._reset_slot(k)
                 return k
         self.fall_back("FOLLOWER_SLOTS")
         return -1
 
+    def _reset_slot(self, k: int) -> None:
+        """A new FollowerInfo (-1, -1) on slot k, ordered after every delta of the slot's previous
+        occupant in any producer's buffer (HipLeaderBookkeeper.resetFollowerSlot): every buffer is
+        pushed first, then the SETs go straight to the node, not through this thread's buffer."""
+        if not self.started or self.fallback or k >= self.width:
+            return
+        self.pump.drain()
+        self.pump.node.push(make_deltas([self.node_slot] * 2, [_lib.rh_col_match(k), _lib.rh_col_fcommit(k)],
+                                        [-1, -1], _lib.RH_OP_SET))
+
     def remove_follower(self, peer) -> None:
+        """The peer's buffered deltas pushed now: none can follow the next occupant's reset."""
         self.follower_slot.pop(peer, None)
+        if self.started and not self.fallback:
+            self.pump.drain()
 
     def conf_word(self, conf, old=None, self_in_conf=True, self_in_old=True) -> int:
         n = sum(1 << self.follower_slot[p] for p in conf if p in self.follower_slot)

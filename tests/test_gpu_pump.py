@@ -167,3 +167,63 @@ def test_pump_replica_fallback_at_fifteen_followers(ctx, orc):
                                [(k, 30_000 + t) for k in range(8)])
             assert b_cb.commit == before_b                 # no event reaches the fallen-back division
         assert a_cb.commit >= 10_500
+
+
+def test_pump_replica_recycled_slot_after_stale_delta_in_another_buffer(ctx, orc):
+    """a stale MAX(matchIndex) of a removed peer sits in one producer thread's buffer
+    when another thread recycles the peer's slot for a new follower.  The new follower must start
+    at -1 (FollowerInfoImpl.java:42-43) whatever order the buffers are pushed in: the reset is
+    pushed after every buffer (PumpDivision._reset_slot / HipLeaderBookkeeper.resetFollowerSlot),
+    so the commit does not advance on the old peer's index."""
+    import threading
+
+    from ratis_amd import _lib, groups
+    cap = 16
+    with groups.RaftNode(0, cap, devices=[0]) as node:
+        pump = groups.LeaderPump(node)
+        cb = Division(0)
+        d = pump.division(2, cb)
+        peers = ["p0", "p1", "p2", "p3"]
+        for p in peers:
+            d.add_follower(p)
+        d.start(d.conf_word(peers), 5_000, 1_000, 1_000)
+        for k in range(4):                       # every follower at 1_500: commit 1_500
+            d.match_index(k, 1_500)
+        pump.tick()
+        assert cb.commit == 1_500
+        # thread B's buffer is registered (pushed) BEFORE thread A's; A buffers a stale high
+        # matchIndex for p3's slot, then B removes p3 and gives the slot to p4 -- the order in which
+        # a plain drain would push B's reset SETs ahead of A's stale MAX
+        import queue
+        jobs = queue.Queue()
+
+        def worker():
+            while True:
+                f = jobs.get()
+                if f is None:
+                    return
+                f()
+                jobs.task_done()
+        tb = threading.Thread(target=worker)
+        tb.start()
+        jobs.put(lambda: d.flush_index(5_000))      # B's first delta: B's buffer registered first
+        jobs.join()
+        t_old = threading.Thread(target=lambda: d.match_index(3, 4_000))   # A: the stale MAX
+        t_old.start()
+        t_old.join()
+
+        def recycle():
+            d.remove_follower("p3")
+            assert d.add_follower("p4") == 3
+        jobs.put(recycle)
+        jobs.join()
+        jobs.put(None)
+        tb.join()
+        for k in range(3):                       # the three old followers reach 4_000
+            d.match_index(k, 4_000)
+        pump.tick()
+        got = node.tables[0].read(_lib.rh_col_match(3), 2, 1)
+        assert int(got[0]) == -1                 # the new follower's matchIndex, not the stale 4_000
+        # conf {self, p0, p1, p2, p4}: the majority (3 of 5) is at 4_000 -- the commit moves there
+        # only because three OLD followers reached it, never by p4's inherited value
+        assert cb.commit == 4_000
