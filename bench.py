@@ -610,6 +610,9 @@ def table_commit_leg(ctx, host, reps: int = 16, fracs=(1.0, 0.1, 0.01), pmc=None
         tab.set_timing(True)
         tab.commit_wait_counts(tab.commit_async(watch_all=False))   # the load marked every row dirty
         tabs[sink] = tab
+    # the reference rate for the event records: GPU stores into mapped pinned memory (the same path)
+    from ratis_amd import engine
+    pcie_write_gbps = engine.pcie_write_probe(ctx, 32 << 20, 9)
     cur_f = np.concatenate([h.follower[:4] for h in host], axis=1)   # followers 0..3 exist in both tiers
     cur_s = np.concatenate([h.flush for h in host])
     out = {}
@@ -638,8 +641,11 @@ def table_commit_leg(ctx, host, reps: int = 16, fracs=(1.0, 0.1, 0.01), pmc=None
                 LEGS.pop()
                 if r:   # the first round is a warm-up
                     res.setdefault((sink, "call"), []).append(e0.elapsed_time(e1))
-                    res.setdefault((sink, "eval"), []).append(tab.last_timing())
-                    res.setdefault((sink, "list"), []).append(tab.last_was_list())
+                    sp = tab.last_timing_split()
+                    res.setdefault((sink, "eval"), []).append(sp["eval_ms"])
+                    res.setdefault((sink, "submit"), []).append(sp["submit_ms"])
+                    res.setdefault((sink, "events"), []).append(sp["events_ms"])
+                    res.setdefault((sink, "list"), []).append(sp["list"])
             a = got[_lib.RH_EVENTS_DEVICE]
             ok = all(np.array_equal(a.advanced_slots, b.advanced_slots) and np.array_equal(a.advanced_commit, b.advanced_commit)
                      and np.array_equal(a.watch_all_slots, b.watch_all_slots) and np.array_equal(a.watch_all_min, b.watch_all_min)
@@ -669,9 +675,22 @@ def table_commit_leg(ctx, host, reps: int = 16, fracs=(1.0, 0.1, 0.01), pmc=None
         case = {"dirty_groups": k, "advanced": res["advanced"], "watch_all_changed": res["watch_all"],
                 "ms_evaluation": round(eval_ms, 4), "list_mode": list_mode,
                 "sinks_agree": res["sinks_agree"]}
+        ev_bytes = 16 * (res["advanced"] + res["watch_all"])   # rh_index_event records into the pinned lists
         for sink, nm in names.items():
             case[nm] = {"ms_evaluation": round(med[(sink, "eval")], 4),
+                        "ms_submit": round(med[(sink, "submit")], 4),
+                        "ms_events": round(med[(sink, "events")], 4),
                         "ms_commit_batch_async_hip_events": round(med[(sink, "call")], 4)}
+        ev_ms = med[(_lib.RH_EVENTS_AUTO, "events")]
+        case["events"] = {"records": res["advanced"] + res["watch_all"], "bytes": ev_bytes,
+                          "ms_auto": round(ev_ms, 4),
+                          "GBps_auto": round(ev_bytes / (ev_ms * 1e-3) / 1e9, 2) if ev_ms > 0 else None,
+                          "note": ("AUTO: from the evaluation's end until the records are in the pinned lists "
+                                   "(the REGION gather on the side stream; 0 when the list kernel wrote them "
+                                   "itself); rh_groups_last_timing_split")}
+        if pcie_write_gbps and ev_ms > 0:
+            case["events"]["pcie_write_GBps"] = round(pcie_write_gbps, 2)
+            case["events"]["vs_pcie_bound"] = round(ev_ms / (ev_bytes / (pcie_write_gbps * 1e9) * 1e3), 3)
         case["roofline"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                             "frac": round(ach / HBM_PEAK_GBPS, 4), "algorithmic_bytes_per_launch": int(alg),
                             "kernel": ("table_list_kernel<false>" if list_mode else "table_commit_kernel_rank<false>")
@@ -684,6 +703,7 @@ def table_commit_leg(ctx, host, reps: int = 16, fracs=(1.0, 0.1, 0.01), pmc=None
         out[f"dirty_{frac * 100:g}pct"] = case
     for tab in tabs.values():
         tab.close()
+    out["pcie_write_GBps"] = round(pcie_write_gbps, 2)
     out["workload"] = (f"resident table of {n_all} config-3 groups (F=4 and F=6 tiers); deltas mark the dirty "
                        "fraction, then one rh_commit_batch (RH_COMMIT_WATCH_ALL) per step; median of "
                        f"{reps} steps per case; auto is the sink the Java module runs")
@@ -746,8 +766,11 @@ def table_watch_leg(ctx, host, reps: int = 16, fracs=(1.0, 0.1, 0.01)) -> dict:
                 torch.cuda.synchronize()
                 LEGS.pop()
                 if r and sink == _lib.RH_EVENTS_AUTO:
-                    res["eval"].append(tab.last_timing())
-                    res["list"].append(tab.last_was_list())
+                    sp = tab.last_timing_split()
+                    res["eval"].append(sp["eval_ms"])
+                    res.setdefault("events", []).append(sp["events_ms"])
+                    res.setdefault("submit", []).append(sp["submit_ms"])
+                    res["list"].append(sp["list"])
             a, b = got[_lib.RH_EVENTS_AUTO], got[_lib.RH_EVENTS_HOST_MAPPED]
             agree &= bool(np.array_equal(a, b))
             changed = int(a.size)
@@ -760,9 +783,12 @@ def table_watch_leg(ctx, host, reps: int = 16, fracs=(1.0, 0.1, 0.01)) -> dict:
         if not list_mode:
             alg += n_all / 4   # the event masks: 2 bits per row
         ach = alg / (eval_ms * 1e-3) / 1e9
+        ev_ms = float(np.median(res["events"]))
         out[f"dirty_{frac * 100:g}pct"] = {
             "dirty_groups": k, "levels_changed": changed, "ms_evaluation": round(eval_ms, 4), "list_mode": list_mode,
-            "sinks_agree": agree,
+            "sinks_agree": agree, "ms_submit": round(float(np.median(res["submit"])), 4),
+            "events": {"records": changed, "bytes": 32 * changed, "ms_auto": round(ev_ms, 4),
+                       "GBps_auto": round(32 * changed / (ev_ms * 1e-3) / 1e9, 2) if ev_ms > 0 else None},
             "roofline": {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(ach / HBM_PEAK_GBPS, 4), "algorithmic_bytes_per_launch": int(alg),
                          "kernel": ("table_list_kernel<true>" if list_mode else "table_commit_kernel_rank<true>")

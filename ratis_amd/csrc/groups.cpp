@@ -174,7 +174,10 @@ struct rh_groups {
     uint64_t lmarks[2] = {0, 0};     // bound on the rows marked since then
     uint64_t marks[2] = {0, 0};      // deltas of each kind since its last evaluation (lists or not)
     bool last_list = false;     // the last evaluation ran over the dirty-row lists (diagnostics)
-    hipEvent_t tev[2] = {nullptr, nullptr};  // rh_groups_timing: around the evaluation
+    // rh_groups_timing: [0] / [1] the evaluation's kernel boundaries, [2] before the staged deltas'
+    // submission (H2D + apply), [3] after the event records reached the pinned lists (gather / drain,
+    // or the evaluation itself when its kernel wrote them)
+    hipEvent_t tev[4] = {nullptr, nullptr, nullptr, nullptr};
     bool timing = false, timed = false;
     int event_sink = RH_EVENTS_AUTO;
     uint32_t cbits = 28;   // bits per list count in the evaluation's counter word (TableEvents)
@@ -804,6 +807,25 @@ RH_EXPORT int rh_groups_timing(rh_groups* g, int enable) {
     return RH_OK;
 }
 
+RH_EXPORT int rh_groups_last_timing_split(rh_groups* g, float* submit_ms, float* eval_ms, float* events_ms,
+                                          int* list_evaluated) {
+    if (!g || !submit_ms || !eval_ms || !events_ms) return rh::fail(RH_E_INVAL, "rh_groups_last_timing_split: NULL argument");
+    DeviceGuard dg(g->ctx->device);
+    std::unique_lock<std::mutex> lk(g->mu);
+    if (!g->timed) return rh::fail(RH_E_STATE, "rh_groups_last_timing_split: no timed evaluation");
+    hipEvent_t ev[4] = {g->tev[0], g->tev[1], g->tev[2], g->tev[3]};
+    const bool was_list = g->last_list;
+    lk.unlock();   // no table lock across a device wait
+    RH_HIP(hipEventSynchronize(ev[3]));
+    RH_HIP(hipEventSynchronize(ev[1]));
+    RH_HIP(hipEventElapsedTime(submit_ms, ev[2], ev[0]));
+    RH_HIP(hipEventElapsedTime(eval_ms, ev[0], ev[1]));
+    RH_HIP(hipEventElapsedTime(events_ms, ev[1], ev[3]));
+    if (*events_ms < 0) *events_ms = 0;   // the evaluation wrote the records itself
+    if (list_evaluated) *list_evaluated = was_list ? 1 : 0;
+    return RH_OK;
+}
+
 RH_EXPORT int rh_groups_last_timing(rh_groups* g, float* eval_ms, int* list_evaluated) {
     if (!g || !eval_ms) return rh::fail(RH_E_INVAL, "rh_groups_last_timing: NULL argument");
     DeviceGuard dg(g->ctx->device);
@@ -1192,6 +1214,7 @@ RH_EXPORT int rh_commit_batch_async(rh_groups* g, uint32_t flags, uint64_t* tick
         if (e.pending && e.ticket == was) e.pending = false;
     }
     e.ticket = 0;
+    if (g->timing) RH_HIP(hipEventRecord(g->tev[2], g->ctx->stream));
     int rc = stage_submit(g);   // the deltas pushed before this call
     if (rc != RH_OK) return rc;
     const bool wall_on = (flags & RH_COMMIT_WATCH_ALL) != 0;
@@ -1211,6 +1234,7 @@ RH_EXPORT int rh_commit_batch_async(rh_groups* g, uint32_t flags, uint64_t* tick
         if (rc != RH_OK) return rc;
         RH_HIP(hipEventRecord(e.done, g->d2h_stream));
         RH_HIP(hipEventRecord(g->gathered, g->d2h_stream));
+        if (g->timing) RH_HIP(hipEventRecord(g->tev[3], g->d2h_stream));
         g->gather_pending = true;
         hbm = false;   // nothing left for _wait to copy
     } else if (hbm && g->event_sink == RH_EVENTS_AUTO) {   // contiguous HBM lists: drained on the side stream
@@ -1220,9 +1244,11 @@ RH_EXPORT int rh_commit_batch_async(rh_groups* g, uint32_t flags, uint64_t* tick
                             g->d2h_stream);
         if (rc != RH_OK) return rc;
         RH_HIP(hipEventRecord(e.done, g->d2h_stream));
+        if (g->timing) RH_HIP(hipEventRecord(g->tev[3], g->d2h_stream));
         hbm = false;   // nothing left for _wait to copy
     } else {
         RH_HIP(hipEventRecord(e.done, g->ctx->stream));
+        if (g->timing) RH_HIP(hipEventRecord(g->tev[3], g->ctx->stream));   // (DEVICE sink: _wait's copy not included)
     }
     e.ticket = tk;
     e.hbm = hbm;
@@ -1287,6 +1313,7 @@ RH_EXPORT int rh_watch_levels_async(rh_groups* g) {
         if (rc != RH_OK) return rc;
         if (g->wpending && g->wgen == was) g->wpending = false;
     }
+    if (g->timing) RH_HIP(hipEventRecord(g->tev[2], g->ctx->stream));
     int rc = stage_submit(g);
     if (rc != RH_OK) return rc;
     EvTargets t;
@@ -1303,6 +1330,7 @@ RH_EXPORT int rh_watch_levels_async(rh_groups* g) {
         if (rc != RH_OK) return rc;
         RH_HIP(hipEventRecord(g->wdone, g->d2h_stream));
         RH_HIP(hipEventRecord(g->wgathered, g->d2h_stream));
+        if (g->timing) RH_HIP(hipEventRecord(g->tev[3], g->d2h_stream));
         g->wgather_pending = true;
         g->wgather_list = lr.rows != nullptr;
         hbm = false;
@@ -1312,9 +1340,11 @@ RH_EXPORT int rh_watch_levels_async(rh_groups* g) {
         rc = rh_table_drain(g->d_wcnt, g->hbm_watch, g->d_watch, nullptr, nullptr, 32, g->capacity, g->d2h_stream);
         if (rc != RH_OK) return rc;
         RH_HIP(hipEventRecord(g->wdone, g->d2h_stream));
+        if (g->timing) RH_HIP(hipEventRecord(g->tev[3], g->d2h_stream));
         hbm = false;
     } else {
         RH_HIP(hipEventRecord(g->wdone, g->ctx->stream));
+        if (g->timing) RH_HIP(hipEventRecord(g->tev[3], g->ctx->stream));
     }
     g->whbm = hbm;
     ++g->wgen;

@@ -158,6 +158,50 @@ RH_EXPORT int rh_synchronize(rh_ctx* ctx) {
     return RH_OK;
 }
 
+// ---- diagnostics: the rate of GPU stores into mapped pinned memory -------------------------------------
+// The reference rate for the kernels that write event records across PCIe (the table's gather / drain,
+// the hasLease bitmap copy): `bytes` copied from HBM into a mapped pinned buffer by the same 16-byte
+// store kernel (rh_table_copy_words), `reps` times on the context stream; *ms = the median launch.
+RH_EXPORT int rh_pcie_write_probe(rh_ctx* ctx, uint64_t bytes, int reps, float* ms) {
+    if (!ctx || !ms || reps < 1 || bytes < 16 || bytes > (1ull << 32))
+        return rh::fail(RH_E_INVAL, "rh_pcie_write_probe: ctx/ms NULL, reps < 1 or bytes outside [16, 4 GiB]");
+    DeviceGuard g(ctx->device);
+    const uint64_t words = bytes / 8;
+    uint64_t* d_src = nullptr;
+    void* h_dst = nullptr;
+    uint64_t* d_dst = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    std::vector<float> t;
+    int rc = RH_OK;
+    if (hipMalloc(reinterpret_cast<void**>(&d_src), words * 8) != hipSuccess ||
+        hipHostMalloc(&h_dst, words * 8, hipHostMallocMapped) != hipSuccess ||
+        hipHostGetDevicePointer(reinterpret_cast<void**>(&d_dst), h_dst, 0) != hipSuccess ||
+        hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) {
+        rc = rh::fail(RH_E_NOMEM, "rh_pcie_write_probe: buffers");
+    }
+    if (rc == RH_OK && hipMemsetAsync(d_src, 0x5A, words * 8, ctx->stream) != hipSuccess)
+        rc = rh::fail(RH_E_DEVICE, "rh_pcie_write_probe: memset");
+    for (int r = 0; r <= reps && rc == RH_OK; ++r) {   // r = 0: warm-up
+        if (hipEventRecord(e0, ctx->stream) != hipSuccess) rc = rh::fail(RH_E_DEVICE, "rh_pcie_write_probe: event");
+        if (rc == RH_OK) rc = rh_table_copy_words(d_src, d_dst, words, ctx->stream);
+        if (rc == RH_OK && (hipEventRecord(e1, ctx->stream) != hipSuccess || hipEventSynchronize(e1) != hipSuccess))
+            rc = rh::fail(RH_E_DEVICE, "rh_pcie_write_probe: launch");
+        float x = 0;
+        if (rc == RH_OK && r > 0 && hipEventElapsedTime(&x, e0, e1) == hipSuccess) t.push_back(x);
+    }
+    if (rc == RH_OK && t.empty()) rc = rh::fail(RH_E_DEVICE, "rh_pcie_write_probe: no timing");
+    if (rc == RH_OK) {
+        std::sort(t.begin(), t.end());
+        *ms = t[t.size() / 2];
+    }
+    (void)hipStreamSynchronize(ctx->stream);
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+    if (h_dst) (void)hipHostFree(h_dst);
+    (void)hipFree(d_src);
+    return rc;
+}
+
 // ---- transfers of caller host memory (rh_internal.h) ------------------------------------------------
 bool rh::host_registered(const void* p, uint64_t n) {
     if (n == 0) return true;

@@ -604,6 +604,14 @@ def stamp_host(ctx: Context, buf, frame_off, frame_len) -> None:
                                    vp(ln.ctypes.data), off.size))
 
 
+def pcie_write_probe(ctx: Context, nbytes: int = 64 << 20, reps: int = 9) -> float:
+    """``rh_pcie_write_probe``: GB/s of GPU stores into mapped pinned host memory (the path the
+    table's event records take), median of ``reps`` launches moving ``nbytes``."""
+    ms = ctypes.c_float()
+    check(_lib.load().rh_pcie_write_probe(ctx.handle, int(nbytes), int(reps), ctypes.byref(ms)))
+    return nbytes / (ms.value * 1e-3) / 1e9
+
+
 class HostRegistration:
     """``rh_host_register`` / ``rh_host_unregister`` of a numpy buffer (a context manager)."""
 
