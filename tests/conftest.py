@@ -34,12 +34,33 @@ def ctx():
     c.close()
 
 
+_PROBE = []
+
+
+def _install_fault_probe():
+    """tests/fault_probe: prints the address, reason and mapping of a GPU memory fault when it
+    happens (the HIP runtime only reports hipErrorIllegalAddress later).  Test infrastructure."""
+    import ctypes
+
+    import torch
+    if _PROBE or not torch.cuda.is_available():
+        return
+    torch.cuda.init()   # the HSA runtime is up before the handler registers
+    path = os.path.join(ROOT, "tests", "fault_probe", "_build", "libfault_probe.so")
+    if os.path.exists(path):
+        lib = ctypes.CDLL(path)
+        lib.fault_probe_install()
+        _PROBE.append(lib)
+
+
 @pytest.fixture(autouse=True)
 def _gpu_fault_attribution(request):
     """After every GPU test: the device drained, every live library context synchronised (its
     stream and an outstanding zero-copy stamp) and one small round trip on torch's stream -- so a
     fault of work a test left in flight fails THAT test's teardown instead of surfacing tests later
     at an unrelated copy (What's weak #1)."""
+    if request.node.get_closest_marker("gpu") is not None:
+        _install_fault_probe()
     yield
     if request.node.get_closest_marker("gpu") is None:
         return
