@@ -138,7 +138,6 @@ RH_EXPORT int rh_shutdown(rh_ctx* ctx) {
         if (ctx->bounce[i]) (void)hipHostFree(ctx->bounce[i]);
         if (ctx->bounce_ev[i]) (void)hipEventDestroy(ctx->bounce_ev[i]);
     }
-    if (ctx->zc_done) (void)hipEventDestroy(ctx->zc_done);
     if (ctx->pool) (void)hipMemPoolDestroy(ctx->pool);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -149,12 +148,7 @@ RH_EXPORT int rh_shutdown(rh_ctx* ctx) {
 RH_EXPORT int rh_synchronize(rh_ctx* ctx) {
     if (!ctx) return rh::fail(RH_E_INVAL, "rh_synchronize: ctx == NULL");
     DeviceGuard g(ctx->device);
-    RH_HIP(hipStreamSynchronize(ctx->stream));
-    {
-        std::lock_guard<std::mutex> lk(ctx->stage_mu);
-        int rc = rh::zc_settle(ctx);
-        if (rc != RH_OK) return rc;
-    }
+    RH_HIP(hipStreamSynchronize(ctx->stream));   // (a zero-copy stamp's launch included)
     return RH_OK;
 }
 
@@ -203,7 +197,7 @@ RH_EXPORT int rh_pcie_write_probe(rh_ctx* ctx, uint64_t bytes, int reps, float* 
 }
 
 // ---- transfers of caller host memory (rh_internal.h) ------------------------------------------------
-bool rh::host_registered(const void* p, uint64_t n) {
+bool rh::host_registered(const void* p, uint64_t n, void** dev) {
     if (n == 0) return true;
     void *d0 = nullptr, *d1 = nullptr;
     if (hipHostGetDevicePointer(&d0, const_cast<void*>(p), 0) != hipSuccess ||
@@ -212,6 +206,7 @@ bool rh::host_registered(const void* p, uint64_t n) {
         (void)hipGetLastError();   // a pageable range: not an error
         return false;
     }
+    if (dev) *dev = d0;
     return true;
 }
 
@@ -285,12 +280,7 @@ int rh::d2h(rh_ctx* ctx, void* dst, const void* src, uint64_t n, hipStream_t s) 
     return RH_OK;
 }
 
-int rh::zc_settle(rh_ctx* ctx) {
-    if (!ctx->zc_pending) return RH_OK;
-    ctx->zc_pending = false;
-    RH_HIP(hipEventSynchronize(ctx->zc_done));
-    return RH_OK;
-}
+
 
 RH_EXPORT void* rh_ctx_stream(rh_ctx* ctx) { return ctx ? reinterpret_cast<void*>(ctx->stream) : nullptr; }
 
@@ -482,14 +472,8 @@ RH_EXPORT int rh_host_register(rh_ctx* ctx, void* p, uint64_t n) {
 RH_EXPORT int rh_host_unregister(rh_ctx* ctx, void* p) {
     if (!ctx || !p) return rh::fail(RH_E_INVAL, "rh_host_unregister: ctx/p == NULL");
     DeviceGuard g(ctx->device);
-    int rc;
-    {
-        std::lock_guard<std::mutex> lk(ctx->stage_mu);
-        rc = rh::zc_settle(ctx);
-    }
     const hipError_t e = hipDeviceSynchronize();
     RH_HIP(hipHostUnregister(p));
-    if (rc != RH_OK) return rc;
     if (e != hipSuccess) return rh::hip_fail(e, "rh_host_unregister: work still reading the buffer");
     return RH_OK;
 }
@@ -517,6 +501,7 @@ namespace {
 // Grows the context's pinned staging to `bytes` (under stage_mu).
 int stage_reserve(rh_ctx* ctx, uint64_t bytes) {
     if (ctx->pinned_bytes >= bytes) return RH_OK;
+    RH_HIP(hipStreamSynchronize(ctx->stream));   // a zero-copy launch may still map the old staging
     if (ctx->h_pinned) (void)hipHostFree(ctx->h_pinned);
     ctx->h_pinned = nullptr;
     ctx->pinned_bytes = 0;
@@ -545,17 +530,17 @@ int stamp_zero_copy(rh_ctx* ctx, uint8_t* buf, uint64_t lo, uint64_t hi, const u
         hi - lo > (uint64_t)kStampMaxGroups * 3 / 4 * kStampSpan)   // would not fit the workgroups
         return kNotPlanned;
     // the workgroups move 16-byte pieces from (offset & ~15) up to (end + 15) & ~15 of `buf`: that
-    // whole range, not only the frames, must lie inside the registration (a batch ending within 15
-    // bytes of the registration's end would otherwise read past it -- a GPU page fault when that end
-    // is also a page's end)
+    // whole range, not only the frames, must be mapped for the GPU.  A registration maps whole pages,
+    // so the pieces' ends may pass the registered bytes within the pages the frames occupy; past
+    // them only if the registration goes on (a batch ending within 15 bytes of a registration that
+    // ends on a page boundary would otherwise read the next page -- a GPU page fault)
     const uint64_t r_lo = lo & ~15ull, r_hi = (hi + 15) & ~15ull;
-    uint8_t *d_lo = nullptr, *d_hi = nullptr;
-    if (hipHostGetDevicePointer(reinterpret_cast<void**>(&d_lo), buf + lo, 0) != hipSuccess ||
-        hipHostGetDevicePointer(reinterpret_cast<void**>(&d_hi), buf + hi - 1, 0) != hipSuccess ||
-        (uint64_t)(d_hi - d_lo) != hi - 1 - lo || !rh::host_registered(buf + r_lo, r_hi - r_lo)) {
-        (void)hipGetLastError();   // not registered (mapped): the copying plan
-        return kNotPlanned;
-    }
+    const auto page = [](const uint8_t* p) { return reinterpret_cast<uintptr_t>(p) >> 12; };
+    const uint64_t c_lo = page(buf + r_lo) == page(buf + lo) ? lo : r_lo;
+    const uint64_t c_hi = page(buf + r_hi - 1) == page(buf + hi - 1) ? hi : r_hi;
+    void* d_c = nullptr;
+    if (!rh::host_registered(buf + c_lo, c_hi - c_lo, &d_c)) return kNotPlanned;   // the copying plan
+    uint8_t* d_lo = static_cast<uint8_t*>(d_c) + (lo - c_lo);
     StampArgs A{};
     auto al = [](uint64_t x) { return (x + 255) / 256 * 256; };
     const uint64_t o_fr = 0, o_crc = al(n * 16), o_done = o_crc + al(n * 4);
@@ -631,15 +616,10 @@ int stamp_zero_copy(rh_ctx* ctx, uint8_t* buf, uint64_t lo, uint64_t hi, const u
         }
         std::atomic_thread_fence(std::memory_order_acquire);
     }
-    if (!seen) {
-        RH_HIP(hipStreamSynchronize(s));
-    } else {
-        // returned on the flags: the launch's completion (and any fault of it) is checked by the
-        // next stamp, rh_synchronize, rh_host_unregister or rh_shutdown
-        if (!ctx->zc_done) RH_HIP(hipEventCreateWithFlags(&ctx->zc_done, hipEventDisableTiming));
-        RH_HIP(hipEventRecord(ctx->zc_done, s));
-        ctx->zc_pending = true;
-    }
+    // returned on the flags: every workgroup has made its last access (the flag store); the launch's
+    // completion -- and a fault of it -- is met by the next synchronisation of the context stream
+    // (rh_synchronize, the staging's growth), rh_host_unregister and rh_shutdown (device drains)
+    if (!seen) RH_HIP(hipStreamSynchronize(s));
     const uint32_t* crc = reinterpret_cast<const uint32_t*>(st + o_crc);
     for (uint64_t i = 0; i < n; ++i) {   // buf.putInt((int) checksum.getValue()): big-endian
         uint8_t* t = buf + frame_off[i] + frame_len[i] - 4;
@@ -678,8 +658,6 @@ RH_EXPORT int rh_crc32c_stamp_host(rh_ctx* ctx, uint8_t* buf, uint64_t buf_len, 
     const uint64_t span = hi - lo;
     const uint64_t t_off = 0, t_len = al(n * 8), t_crc = t_len + al(n * 4), t_bytes = t_crc + al(n * 4);
     std::lock_guard<std::mutex> lk(ctx->stage_mu);
-    const int zs = rh::zc_settle(ctx);   // the last zero-copy launch read the staging this call rewrites
-    if (zs != RH_OK) return zs;
     const int zc = stamp_zero_copy(ctx, buf, lo, hi, frame_off, frame_len, n, max_len);
     if (zc != kNotPlanned) return zc;
     const int rs = stage_reserve(ctx, t_bytes);

@@ -273,11 +273,6 @@ struct rh_ctx {
     void* h_pinned = nullptr;
     size_t pinned_bytes = 0;
     hipMemPool_t pool = nullptr;  // stream-ordered scratch (rh::pool_alloc)
-    // The zero-copy stamp returns on polled flags, before its launch has completed: its completion,
-    // checked by the next stamp, rh_synchronize, rh_host_unregister and rh_shutdown (a fault of that
-    // launch is reported, never dropped).  Under stage_mu.
-    hipEvent_t zc_done = nullptr;
-    bool zc_pending = false;
     // Pinned bounce buffers for transfers of CALLER host memory (rh::h2d / rh::d2h): the HIP runtime
     // is never handed pageable memory the library does not own (it would page-lock it behind the
     // call, and a lock that outlives the caller's buffer is a GPU mapping of freed pages -- DESIGN
@@ -313,11 +308,10 @@ struct PoolScratch {
 // DMA of chunk k).  h2d: enqueued, `src` reusable on return.  d2h: `dst` holds the bytes on return
 // (it waits for the stream).
 constexpr uint64_t kBounceBytes = 4ull << 20;
-bool host_registered(const void* p, uint64_t n);
+// (*dev: the device address of p, when registered)
+bool host_registered(const void* p, uint64_t n, void** dev = nullptr);
 int h2d(rh_ctx* ctx, void* dst, const void* src, uint64_t n, hipStream_t s);
 int d2h(rh_ctx* ctx, void* dst, const void* src, uint64_t n, hipStream_t s);
-// Waits for the context's outstanding zero-copy stamp (if any); its fault is returned.
-int zc_settle(rh_ctx* ctx);
 }  // namespace rh
 
 int rh_commit_launch_impl(rh_ctx* ctx, const rh_commit_soa* tiers, int n_tiers, hipStream_t stream);
