@@ -710,6 +710,62 @@ def table_commit_leg(ctx, host, reps: int = 16, fracs=(1.0, 0.1, 0.01), pmc=None
     return out
 
 
+def tick_leg(ctx, host, ks=(256, 2048), reps: int = 50) -> dict:
+    """The Java pump's sparse tick end to end (HipLeaderBookkeeper.tick, groups.LeaderPump.tick): k
+    follower replies -- a matchIndex and a commitIndex MAX for k / 2 random divisions of config 3's
+    1M, as FollowerInfo.updateMatchIndex / updateCommitIndex emit them (FollowerInfoImpl.java:93-105)
+    -- pushed, then updateCommit and commitIndexChanged put in flight together and waited for, their
+    event records read (LeaderStateImpl.java:946-950, 612-622: the reference runs them per reply event
+    per division).  Host wall clock from the push to the last wait, median and p90 of `reps` ticks
+    (no timing events on the table: they would lengthen the tick); the event records stay in the
+    library's pinned lists (the JNI glue's copy into the Java arrays is not included)."""
+    import time
+
+    from ratis_amd import groups
+    n_all = sum(h.n for h in host)
+    tab = groups.RaftGroupTable(ctx, capacity=n_all)
+    first = 0
+    for h in host:
+        tab.load(first, h.conf, h.flush, h.commit, h.term_start, match=h.follower)
+        first += h.n
+    tab.commit_wait_counts(tab.commit_async(watch_all=True))
+    tab.watch_async()
+    tab.watch_wait_count()
+    match = np.concatenate([h.follower[:4] for h in host], axis=1)
+    rng = np.random.default_rng(5)
+    out = {}
+    for k in ks:
+        ms = []
+        n_adv = 0
+        for r in range(reps + 3):
+            slot = rng.choice(n_all, size=k // 2, replace=False)
+            col = rng.integers(0, 4, size=slot.size)
+            match[col, slot] += rng.integers(1, 300, size=slot.size)
+            d = groups.make_deltas(np.concatenate([slot, slot]), np.concatenate([col, 16 + col]),
+                                   np.concatenate([match[col, slot], match[col, slot] - 2]))
+            LEGS.push(f"tick_k{k}" if r >= 3 else "tick_warmup")
+            t0 = time.perf_counter()
+            tab.push(d)
+            tk = tab.commit_async(watch_all=True)   # the pump's order: every pass in flight, then the waits
+            tab.watch_async()
+            na, _ = tab.commit_wait_counts(tk)
+            tab.watch_wait_count()
+            t1 = time.perf_counter()
+            LEGS.pop()
+            if r >= 3:
+                ms.append((t1 - t0) * 1e3)
+                n_adv += na
+        out[f"replies_{k}"] = {
+            "ms_tick_median": round(float(np.median(ms)), 4), "ms_tick_p90": round(float(np.percentile(ms, 90)), 4),
+            "replies_per_s": round(k / (float(np.median(ms)) * 1e-3), 1),
+            "commits_advanced_per_tick": round(n_adv / reps, 1)}
+    tab.close()
+    out["workload"] = (f"resident table of {n_all} config-3 groups; per tick k deltas (k/2 replies x matchIndex + "
+                       f"commitIndex), push + commit_async + watch_async + both waits (the pump's order); host wall "
+                       f"clock, median of {reps} ticks")
+    return out
+
+
 def table_watch_leg(ctx, host, reps: int = 16, fracs=(1.0, 0.1, 0.01)) -> dict:
     """commitIndexChanged over the resident table (LeaderStateImpl.java:612-622, rh_watch_levels_async
     / _wait), the other evaluation the Java pump runs every tick: the followers' commitIndex deltas
@@ -1147,6 +1203,7 @@ def main():
         pcie["delta_streaming"] = delta_streaming(ctx, host, fill_threads=cpu_threads())
         pcie["delta_streaming"]["table_commit"] = table_commit_leg(ctx, host, pmc=pmc)
         pcie["delta_streaming"]["table_watch"] = table_watch_leg(ctx, host)
+        pcie["delta_streaming"]["tick"] = tick_leg(ctx, host)
         pcie["delta_streaming"]["reply_mix"] = reply_mix_leg(host, threads=cpu_threads())
         pcie["write_stamp"] = write_stamp_leg(ctx)
 
