@@ -590,6 +590,9 @@ def table_commit_leg(ctx, host, reps: int = 16, fracs=(1.0, 0.1, 0.01), pmc=None
     (the lists in HBM, _wait copies the counted prefix) and RH_EVENTS_AUTO (the default, what the
     Java module and rh_node run: DEVICE for tile evaluations, HOST_MAPPED for list evaluations).
     `roofline` = AUTO's evaluation, events included.  The tables' events must be identical."""
+    import ctypes
+    import time
+
     import torch
 
     from ratis_amd import _lib, groups
@@ -633,14 +636,20 @@ def table_commit_leg(ctx, host, reps: int = 16, fracs=(1.0, 0.1, 0.01), pmc=None
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 LEGS.push(f"table_{frac * 100:g}pct_{names[sink]}" if r else "table_warmup")
                 queue_gate(stream)   # the evaluation is enqueued before the GPU reaches e0
+                torch.cuda.synchronize()   # (the gate: the host clock below starts on an idle GPU)
+                t_h0 = time.perf_counter()
                 e0.record(stream)
                 tk = tab.commit_async(watch_all=True)
                 e1.record(stream)
-                got[sink] = tab.commit_wait(tk)
+                raw = _lib.RhCommitOut()
+                _lib.check(lib.rh_commit_batch_wait(tab.handle, tk, ctypes.byref(raw)))
+                t_h1 = time.perf_counter()   # the records are in the pinned lists: what the pump waits for
+                got[sink] = groups.CommitResult(raw)
                 torch.cuda.synchronize()
                 LEGS.pop()
                 if r:   # the first round is a warm-up
                     res.setdefault((sink, "call"), []).append(e0.elapsed_time(e1))
+                    res.setdefault((sink, "host"), []).append((t_h1 - t_h0) * 1e3)
                     sp = tab.last_timing_split()
                     res.setdefault((sink, "eval"), []).append(sp["eval_ms"])
                     res.setdefault((sink, "submit"), []).append(sp["submit_ms"])
@@ -659,13 +668,13 @@ def table_commit_leg(ctx, host, reps: int = 16, fracs=(1.0, 0.1, 0.01), pmc=None
         # columns (F matchIndex, conf, commit, flush, term start, previous watch-ALL level; the row
         # slot only where the kernel writes records) and the flag clear; per event the 8 B commit /
         # watch level and (advanced) the 1 B watch-dirty flag it stores, and -- a list evaluation of
-        # fewer than 8192 marked rows only -- the 16 B record it writes (tile evaluations and larger
+        # (AUTO) only -- the 16 B record it writes (tile evaluations and larger
         # list evaluations into AUTO write event bits instead: rh_table_gather_commit builds the
         # records from the table on the side stream)
         n_f4 = host[0].n
         f_mean = (n_f4 * F[0] + (n_all - n_f4) * (F[1] if len(F) > 1 else F[0])) / n_all
         list_mode = bool(np.all(res[(_lib.RH_EVENTS_AUTO, "list")]))
-        pinned = list_mode and k < 8192   # groups.cpp RH_LIST_PINNED_MAX
+        pinned = list_mode   # groups.cpp RH_LIST_PINNED_MAX: every AUTO list evaluation writes its records
         rec = 16 if pinned else 0
         per_dirty = 8 * f_mean + 4 + (4 if pinned else 0) + 8 + 8 + 8 + 8 + 1
         alg = n_all * 1 + k * per_dirty + res["advanced"] * (rec + 8 + 1) + res["watch_all"] * (rec + 8)
@@ -680,6 +689,7 @@ def table_commit_leg(ctx, host, reps: int = 16, fracs=(1.0, 0.1, 0.01), pmc=None
             case[nm] = {"ms_evaluation": round(med[(sink, "eval")], 4),
                         "ms_submit": round(med[(sink, "submit")], 4),
                         "ms_events": round(med[(sink, "events")], 4),
+                        "ms_async_to_records_host": round(med[(sink, "host")], 4),
                         "ms_commit_batch_async_hip_events": round(med[(sink, "call")], 4)}
         ev_ms = med[(_lib.RH_EVENTS_AUTO, "events")]
         case["events"] = {"records": res["advanced"] + res["watch_all"], "bytes": ev_bytes,
@@ -773,8 +783,8 @@ def table_watch_leg(ctx, host, reps: int = 16, fracs=(1.0, 0.1, 0.01)) -> dict:
     mark `frac` of config 3's 1M groups, then one watch evaluation per step, timed at its kernel
     boundaries (rh_groups_timing).  Two tables fed the same deltas -- AUTO (the module's sink: a
     tile evaluation writes 2 bits per row -- changed, valid -- and rh_table_gather_watch rebuilds the
-    level records from the table on the side stream; so does a list evaluation of 8192 rows or more,
-    smaller ones write their records) and HOST_MAPPED (records across PCIe from the kernel) -- must
+    level records from the table on the side stream; a list evaluation writes its records itself,
+    across PCIe) and HOST_MAPPED (records across PCIe from the kernel) -- must
     report the same levels.  Algorithmic bytes of the evaluation: 1 B watch-dirty flag per row; per
     dirty row 8F follower commitIndex, 8 commit (the self value), 24 previous levels, 4 conf, 1 flag
     clear; per changed row the 24 B of levels stored, plus the 4 B row slot and 32 B record when the
@@ -834,7 +844,7 @@ def table_watch_leg(ctx, host, reps: int = 16, fracs=(1.0, 0.1, 0.01)) -> dict:
         list_mode = bool(np.all(res["list"]))
         n_f4 = host[0].n
         f_mean = (n_f4 * F[0] + (n_all - n_f4) * (F[1] if len(F) > 1 else F[0])) / n_all
-        pinned = list_mode and k < 8192   # groups.cpp RH_LIST_PINNED_MAX: records into the pinned list
+        pinned = list_mode   # groups.cpp RH_LIST_PINNED_MAX: records into the pinned list
         alg = n_all * 1 + k * (8 * f_mean + 8 + 24 + 4 + (4 if pinned else 0) + 1) + changed * ((32 if pinned else 0) + 24)
         if not list_mode:
             alg += n_all / 4   # the event masks: 2 bits per row

@@ -291,9 +291,9 @@ int rh_commit_batch_wait(rh_groups* g, uint64_t ticket, rh_commit_out* out);
  * kernel on a side stream rebuilds the records from the table's columns into the pinned buffers
  * while the table stream goes on (the ticket completes after the gather; no host-issued copy; the
  * table's next writers of those columns are ordered after it); an evaluation over the dirty-row
- * lists writes records into the pinned buffers directly when fewer than 8192 rows were marked,
- * else event bits per listed row, rebuilt the same way from the list entries.  DEVICE: as AUTO,
- * except that every list evaluation takes the event-bit form.  Results are identical.  Not while
+ * lists (at most capacity / 32 marked rows) writes its records into the pinned buffers directly.
+ * DEVICE: as AUTO, except that a list evaluation writes event bits per listed row, rebuilt the same
+ * way from the list entries.  Results are identical.  Not while
  * an evaluation is outstanding (RH_E_STATE). */
 #define RH_EVENTS_HOST_MAPPED 0
 #define RH_EVENTS_DEVICE      1

@@ -457,8 +457,12 @@ struct EvTargets {
 #ifndef RH_LIST_REGION   // A/B: list evaluations into HBM in REGION mode (1) or with the counter atomic (0)
 #define RH_LIST_REGION 1
 #endif
-#ifndef RH_LIST_PINNED_MAX   // AUTO: list evaluations of fewer marked rows write the pinned lists directly (A/B)
-#define RH_LIST_PINNED_MAX 8192
+// AUTO: list evaluations of fewer marked rows write the pinned lists directly (A/B).  Round 6: every
+// list evaluation does -- what the host waits for, from _async to the records in the pinned lists,
+// at 1 % of 1M rows 67 us against 95 us by REGION masks + the gather (the kernel itself 10.1 against
+// 9.0 us), at 3 % 83 against 112 us (profiles/r06/pin_ab/)
+#ifndef RH_LIST_PINNED_MAX
+#define RH_LIST_PINNED_MAX (~0ull)
 #endif
 
 // Enqueues one evaluation (mode) of the dirty rows, its events written into the lists adv / wall
@@ -487,9 +491,8 @@ int evaluate(rh_groups* g, int mode, bool wall_on, const EvTargets& t, uint64_t*
     }
     const int m = mode == RH_MODE_WATCH ? 1 : 0;
     const bool list = g->lvalid[m];   // every row marked since the last evaluation is listed
-    // AUTO: HBM lists (gathered / drained on the side stream) unless a list evaluation of few rows,
-    // whose records the kernel writes across PCIe itself (at 3 % of 1M rows those writes cost the
-    // list kernel 2.7 us; at 1 % HBM measured the same or 0.3 us less: profiles/r05/table_eval/)
+    // AUTO: HBM lists (gathered / drained on the side stream) for a tile evaluation; a list
+    // evaluation writes its records across PCIe itself (RH_LIST_PINNED_MAX above)
     const bool few = list && g->marks[m] < RH_LIST_PINNED_MAX;
     const int k = (g->event_sink == RH_EVENTS_DEVICE || (g->event_sink == RH_EVENTS_AUTO && !few)) ? 1 : 0;
     rh::TableEvents ev;

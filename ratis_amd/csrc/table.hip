@@ -1244,7 +1244,11 @@ int rh_table_drain(const uint64_t* counts, const void* a, void* a_out, const voi
 }
 
 // ---- REGION mode gathers: one gather workgroup per kGatherWGs evaluation workgroups ----------------
-constexpr uint32_t kGatherWGs = kTWaves >= 32 ? 1u : 32u / kTWaves;
+#ifndef RH_GATHER_CHUNKS   // evaluation waves (chunks) per gather workgroup of 4 waves: one per wave (round 6:
+                           // 10 % dirty 34.7 -> 23.2 us, 100 % 128.4 -> 126.2 us; profiles/r06/gather_ab/)
+#define RH_GATHER_CHUNKS 4
+#endif
+constexpr uint32_t kGatherWGs = kTWaves >= RH_GATHER_CHUNKS ? 1u : RH_GATHER_CHUNKS / kTWaves;
 constexpr uint32_t kGatherChunks = kGatherWGs * kTWaves;
 
 
