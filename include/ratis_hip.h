@@ -307,13 +307,14 @@ int rh_groups_set_event_sink(rh_groups* g, int sink);
  * evaluation of its kind were visited; 0: every tile). */
 int rh_groups_timing(rh_groups* g, int enable);
 int rh_groups_last_timing(rh_groups* g, float* eval_ms, int* list_evaluated);
-/* The last timed rh_commit_batch_async / rh_watch_levels_async split in three (ms, device events):
- * submit = the deltas staged before it (H2D + apply), eval = the evaluation kernels (as above),
- * events = from the evaluation's end until its event records are in the pinned result lists (the
- * REGION gather or the drain on the side stream; 0 when the evaluation kernel wrote them itself;
- * the DEVICE sink's copy in _wait not included).  Blocks until they have completed. */
+/* The last timed rh_commit_batch_async / rh_watch_levels_async split (ms, device events): submit =
+ * the deltas staged before it (H2D + apply), eval = the evaluation kernels (as above), events = from
+ * the evaluation's end until its event records are in the pinned result lists (the REGION gather or
+ * the drain on the side stream, their launch and cross-stream wait included; ~0 when the evaluation
+ * kernel wrote them itself; the DEVICE sink's copy in _wait not included), gather = the REGION
+ * gather kernel alone, at its kernel boundaries (0: none ran).  Blocks until they have completed. */
 int rh_groups_last_timing_split(rh_groups* g, float* submit_ms, float* eval_ms, float* events_ms,
-                                int* list_evaluated);
+                                float* gather_ms, int* list_evaluated);
 /* Diagnostics: GPU stores into mapped pinned host memory -- the path the event records take --
  * `bytes` from HBM by the library's 16-byte copy kernel, `reps` launches; *ms = the median one. */
 int rh_pcie_write_probe(rh_ctx* ctx, uint64_t bytes, int reps, float* ms);

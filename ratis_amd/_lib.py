@@ -236,7 +236,7 @@ _SIGNATURES = {
     "rh_groups_timing": (c_int, [c_void_p, c_int]),
     "rh_groups_last_timing": (c_int, [c_void_p, POINTER(ctypes.c_float), POINTER(c_int)]),
     "rh_groups_last_timing_split": (c_int, [c_void_p, POINTER(ctypes.c_float), POINTER(ctypes.c_float),
-                                            POINTER(ctypes.c_float), POINTER(c_int)]),
+                                            POINTER(ctypes.c_float), POINTER(ctypes.c_float), POINTER(c_int)]),
     "rh_pcie_write_probe": (c_int, [c_void_p, c_uint64, c_int, POINTER(ctypes.c_float)]),
     "rh_watch_levels_wait": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_uint64)]),
     "rh_lease_batch_async": (c_int, [c_void_p, c_int64, c_int64]),

@@ -177,8 +177,9 @@ struct rh_groups {
     // rh_groups_timing: [0] / [1] the evaluation's kernel boundaries, [2] before the staged deltas'
     // submission (H2D + apply), [3] after the event records reached the pinned lists (gather / drain,
     // or the evaluation itself when its kernel wrote them)
-    hipEvent_t tev[4] = {nullptr, nullptr, nullptr, nullptr};
-    bool timing = false, timed = false;
+    // [4] / [5] the gather kernel's boundaries (gathered: whether the last timed _async ran one)
+    hipEvent_t tev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    bool timing = false, timed = false, gathered_timed = false;
     int event_sink = RH_EVENTS_AUTO;
     uint32_t cbits = 28;   // bits per list count in the evaluation's counter word (TableEvents)
     int64_t* d_read = nullptr;
@@ -811,13 +812,14 @@ RH_EXPORT int rh_groups_timing(rh_groups* g, int enable) {
 }
 
 RH_EXPORT int rh_groups_last_timing_split(rh_groups* g, float* submit_ms, float* eval_ms, float* events_ms,
-                                          int* list_evaluated) {
-    if (!g || !submit_ms || !eval_ms || !events_ms) return rh::fail(RH_E_INVAL, "rh_groups_last_timing_split: NULL argument");
+                                          float* gather_ms, int* list_evaluated) {
+    if (!g || !submit_ms || !eval_ms || !events_ms || !gather_ms)
+        return rh::fail(RH_E_INVAL, "rh_groups_last_timing_split: NULL argument");
     DeviceGuard dg(g->ctx->device);
     std::unique_lock<std::mutex> lk(g->mu);
     if (!g->timed) return rh::fail(RH_E_STATE, "rh_groups_last_timing_split: no timed evaluation");
-    hipEvent_t ev[4] = {g->tev[0], g->tev[1], g->tev[2], g->tev[3]};
-    const bool was_list = g->last_list;
+    hipEvent_t ev[6] = {g->tev[0], g->tev[1], g->tev[2], g->tev[3], g->tev[4], g->tev[5]};
+    const bool was_list = g->last_list, gathered = g->gathered_timed;
     lk.unlock();   // no table lock across a device wait
     RH_HIP(hipEventSynchronize(ev[3]));
     RH_HIP(hipEventSynchronize(ev[1]));
@@ -825,6 +827,11 @@ RH_EXPORT int rh_groups_last_timing_split(rh_groups* g, float* submit_ms, float*
     RH_HIP(hipEventElapsedTime(eval_ms, ev[0], ev[1]));
     RH_HIP(hipEventElapsedTime(events_ms, ev[1], ev[3]));
     if (*events_ms < 0) *events_ms = 0;   // the evaluation wrote the records itself
+    *gather_ms = 0;
+    if (gathered) {
+        RH_HIP(hipEventSynchronize(ev[5]));
+        RH_HIP(hipEventElapsedTime(gather_ms, ev[4], ev[5]));
+    }
     if (list_evaluated) *list_evaluated = was_list ? 1 : 0;
     return RH_OK;
 }
@@ -1218,6 +1225,7 @@ RH_EXPORT int rh_commit_batch_async(rh_groups* g, uint32_t flags, uint64_t* tick
     }
     e.ticket = 0;
     if (g->timing) RH_HIP(hipEventRecord(g->tev[2], g->ctx->stream));
+    g->gathered_timed = false;
     int rc = stage_submit(g);   // the deltas pushed before this call
     if (rc != RH_OK) return rc;
     const bool wall_on = (flags & RH_COMMIT_WATCH_ALL) != 0;
@@ -1233,7 +1241,8 @@ RH_EXPORT int rh_commit_batch_async(rh_groups* g, uint32_t flags, uint64_t* tick
         RH_HIP(hipEventRecord(g->evaluated, g->ctx->stream));
         RH_HIP(hipStreamWaitEvent(g->d2h_stream, g->evaluated, 0));
         rc = rh_table_gather_commit(ed, e.bdesc, e.nblocks, e.d_adv, wall_on ? e.d_wall : nullptr, e.d_cnt,
-                                    g->d2h_stream, lr);
+                                    g->d2h_stream, lr, g->timing ? g->tev[4] : nullptr, g->timing ? g->tev[5] : nullptr);
+        g->gathered_timed = g->timing;
         if (rc != RH_OK) return rc;
         RH_HIP(hipEventRecord(e.done, g->d2h_stream));
         RH_HIP(hipEventRecord(g->gathered, g->d2h_stream));
@@ -1317,6 +1326,7 @@ RH_EXPORT int rh_watch_levels_async(rh_groups* g) {
         if (g->wpending && g->wgen == was) g->wpending = false;
     }
     if (g->timing) RH_HIP(hipEventRecord(g->tev[2], g->ctx->stream));
+    g->gathered_timed = false;
     int rc = stage_submit(g);
     if (rc != RH_OK) return rc;
     EvTargets t;
@@ -1329,7 +1339,9 @@ RH_EXPORT int rh_watch_levels_async(rh_groups* g) {
     if (hbm && g->wnblocks) {   // REGION mode (DEVICE and AUTO): the records rebuilt into the pinned list
         RH_HIP(hipEventRecord(g->evaluated, g->ctx->stream));
         RH_HIP(hipStreamWaitEvent(g->d2h_stream, g->evaluated, 0));
-        rc = rh_table_gather_watch(ed, g->wbdesc, g->wnblocks, g->d_watch, g->d_wcnt, g->d2h_stream, lr);
+        rc = rh_table_gather_watch(ed, g->wbdesc, g->wnblocks, g->d_watch, g->d_wcnt, g->d2h_stream, lr,
+                                   g->timing ? g->tev[4] : nullptr, g->timing ? g->tev[5] : nullptr);
+        g->gathered_timed = g->timing;
         if (rc != RH_OK) return rc;
         RH_HIP(hipEventRecord(g->wdone, g->d2h_stream));
         RH_HIP(hipEventRecord(g->wgathered, g->d2h_stream));

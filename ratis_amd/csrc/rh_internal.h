@@ -345,14 +345,16 @@ int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev, 
 // and this kernel (groups.cpp gather_fence).
 // A list evaluation's records (lr.rows set): the same, its rows from the list entries of the masks'
 // lanes -- nothing may append to that list either until the gather has run.
+// t0 / t1 (may be null): timing events stamped at the gather kernel's boundaries.
 int rh_table_gather_commit(const rh::TableDev& t, const uint32_t* bdesc, uint32_t n_blocks, rh_index_event* adv_out,
                            rh_index_event* wall_out, uint64_t* counts_out, hipStream_t stream,
-                           const rh::ListRegion& lr = rh::ListRegion{});
+                           const rh::ListRegion& lr = rh::ListRegion{}, hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
 // REGION mode, WATCH: the level records (slot, valid, min, majority, max) of an evaluation rebuilt
 // the same way from the masks (changed rows, valid flags) and the row-slot / wmin / wmaj / wmax
 // columns into the pinned list `out` (device pointer), its length to counts_out[0].
 int rh_table_gather_watch(const rh::TableDev& t, const uint32_t* bdesc, uint32_t n_blocks, rh_watch_event* out,
-                          uint64_t* counts_out, hipStream_t stream, const rh::ListRegion& lr = rh::ListRegion{});
+                          uint64_t* counts_out, hipStream_t stream, const rh::ListRegion& lr = rh::ListRegion{},
+                          hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
 // n 64-bit words from device memory to a host-mapped pinned buffer (device view), as GPU writes.
 int rh_table_copy_words(const uint64_t* src, uint64_t* dst, uint64_t n, hipStream_t stream);
 int rh_table_drain(const uint64_t* counts, const void* a, void* a_out, const void* b, void* b_out, uint32_t rec_bytes0,

@@ -1400,7 +1400,8 @@ __global__ __launch_bounds__(256) void table_gather_rows_kernel(GatherRowsArgs a
 }
 
 static int gather_rows(bool watch, const rh::TableDev& t, const uint32_t* bdesc, uint32_t n_blocks, void* a,
-                       rh_index_event* b, uint64_t* counts_out, hipStream_t stream, const rh::ListRegion& lr) {
+                       rh_index_event* b, uint64_t* counts_out, hipStream_t stream, const rh::ListRegion& lr,
+                       hipEvent_t t0, hipEvent_t t1) {
     if (n_blocks == 0) return rh::fail(RH_E_INVAL, "rh_table_gather_rows: no workgroups");
     GatherRowsArgs g{};
     g.t = t;
@@ -1418,22 +1419,24 @@ static int gather_rows(bool watch, const rh::TableDev& t, const uint32_t* bdesc,
     g.b = b;
     g.counts_out = counts_out;
     const dim3 grid((n_blocks + kGatherWGs - 1) / kGatherWGs), blk(256);
+    hipError_t e;
     if (watch)
-        hipLaunchKernelGGL(table_gather_rows_kernel<true>, grid, blk, 0, stream, g);
+        e = eval_launch(table_gather_rows_kernel<true>, grid, blk, stream, t0, t1, g);
     else
-        hipLaunchKernelGGL(table_gather_rows_kernel<false>, grid, blk, 0, stream, g);
-    RH_HIP(hipGetLastError());
+        e = eval_launch(table_gather_rows_kernel<false>, grid, blk, stream, t0, t1, g);
+    RH_HIP(e);
     return RH_OK;
 }
 
 int rh_table_gather_commit(const rh::TableDev& t, const uint32_t* bdesc, uint32_t n_blocks, rh_index_event* adv_out,
-                           rh_index_event* wall_out, uint64_t* counts_out, hipStream_t stream, const rh::ListRegion& lr) {
-    return gather_rows(false, t, bdesc, n_blocks, adv_out, wall_out, counts_out, stream, lr);
+                           rh_index_event* wall_out, uint64_t* counts_out, hipStream_t stream, const rh::ListRegion& lr,
+                           hipEvent_t t0, hipEvent_t t1) {
+    return gather_rows(false, t, bdesc, n_blocks, adv_out, wall_out, counts_out, stream, lr, t0, t1);
 }
 
 int rh_table_gather_watch(const rh::TableDev& t, const uint32_t* bdesc, uint32_t n_blocks, rh_watch_event* out,
-                          uint64_t* counts_out, hipStream_t stream, const rh::ListRegion& lr) {
-    return gather_rows(true, t, bdesc, n_blocks, out, nullptr, counts_out, stream, lr);
+                          uint64_t* counts_out, hipStream_t stream, const rh::ListRegion& lr, hipEvent_t t0, hipEvent_t t1) {
+    return gather_rows(true, t, bdesc, n_blocks, out, nullptr, counts_out, stream, lr, t0, t1);
 }
 
 int rh_table_init_tiles(const rh::TableTier& t, uint32_t first_tile, uint32_t n_tiles, hipStream_t stream) {

@@ -257,13 +257,14 @@ class RaftGroupTable:
 
     def last_timing_split(self) -> dict:
         """``rh_groups_last_timing_split``: the last timed _async split in submit (staged deltas' H2D +
-        apply), eval (the evaluation kernels) and events (until the records are in the pinned lists),
-        device ms; ``list``: whether it ran over the dirty-row lists."""
-        a, b, c, m = ctypes.c_float(), ctypes.c_float(), ctypes.c_float(), ctypes.c_int()
+        apply), eval (the evaluation kernels), events (until the records are in the pinned lists) and
+        gather (the REGION gather kernel alone, 0 if none), device ms; ``list``: whether it ran over the
+        dirty-row lists."""
+        a, b, c, d, m = ctypes.c_float(), ctypes.c_float(), ctypes.c_float(), ctypes.c_float(), ctypes.c_int()
         check(self._lib.rh_groups_last_timing_split(self.handle, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c),
-                                                    ctypes.byref(m)))
+                                                    ctypes.byref(d), ctypes.byref(m)))
         return {"submit_ms": float(a.value), "eval_ms": float(b.value), "events_ms": float(c.value),
-                "list": bool(m.value)}
+                "gather_ms": float(d.value), "list": bool(m.value)}
 
     def last_was_list(self) -> bool:
         """Whether the last (timed) evaluation ran over the dirty-row lists (list mode)."""
