@@ -172,3 +172,29 @@ def test_shutdown_right_after_pool_scratch_on_a_side_stream(orc):
         side.synchronize()
         assert int(r["total_frames"].item()) == n * ss.frames_per_segment
         _torch_roundtrip(32 << 20, 400 + rep)
+
+
+def test_timing_split_and_pcie_probe(ctx):
+    """Diagnostics the bench reads: rh_groups_last_timing_split names the REGION gather of a tile
+    evaluation (gather > 0, inside the events interval) and reports none for a list evaluation that
+    wrote its records itself; rh_pcie_write_probe returns a PCIe-like rate."""
+    from ratis_amd import _lib, engine, groups
+    rng = np.random.default_rng(15)
+    n = 200_000
+    with groups.RaftGroupTable(ctx, capacity=n) as tab:
+        conf = np.full(n, 0b1111 | (1 << 14) | (1 << 31), np.uint32)
+        flush = np.full(n, 10_000, np.int64)
+        tab.load(0, conf, flush, flush - 500, flush - 900, match=np.full((4, n), 9_000, np.int64))
+        tab.set_timing(True)
+        tab.commit_wait_counts(tab.commit_async(watch_all=True))   # the load marked every row: tile mode
+        sp = tab.last_timing_split()
+        assert not sp["list"] and sp["eval_ms"] > 0 and sp["gather_ms"] > 0 and sp["events_ms"] >= sp["gather_ms"] * 0.5
+        slots = rng.choice(n, 500, replace=False)
+        tab.push(groups.make_deltas(slots, np.zeros(500, np.int64), np.full(500, 9_900)))
+        tab.commit_wait_counts(tab.commit_async(watch_all=True))   # 500 marked rows: a list evaluation
+        sp = tab.last_timing_split()
+        assert sp["list"] and sp["gather_ms"] == 0 and sp["eval_ms"] > 0
+    gbps = engine.pcie_write_probe(ctx, 8 << 20, 5)
+    assert 5 < gbps < 200, gbps
+    with pytest.raises(_lib.IllegalArgumentError):
+        engine.pcie_write_probe(ctx, 8, 1)
