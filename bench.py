@@ -749,34 +749,41 @@ def tick_leg(ctx, host, ks=(256, 2048), reps: int = 50) -> dict:
     rng = np.random.default_rng(5)
     out = {}
     for k in ks:
-        ms = []
+        ms = {"tick_async": [], "two_calls": []}
         n_adv = 0
-        for r in range(reps + 3):
+        for r in range(2 * reps + 6):   # the two forms alternate tick by tick
+            fused = r % 2 == 0
             slot = rng.choice(n_all, size=k // 2, replace=False)
             col = rng.integers(0, 4, size=slot.size)
             match[col, slot] += rng.integers(1, 300, size=slot.size)
             d = groups.make_deltas(np.concatenate([slot, slot]), np.concatenate([col, 16 + col]),
                                    np.concatenate([match[col, slot], match[col, slot] - 2]))
-            LEGS.push(f"tick_k{k}" if r >= 3 else "tick_warmup")
+            LEGS.push((f"tick_k{k}" if fused else f"tick2_k{k}") if r >= 6 else "tick_warmup")
             t0 = time.perf_counter()
             tab.push(d)
-            tk = tab.commit_async(watch_all=True)   # the pump's order: every pass in flight, then the waits
-            tab.watch_async()
+            if fused:   # rh_tick_async: both evaluations in one launch (the pump's call)
+                tk = tab.tick_async(watch_all=True)
+            else:       # the same as two calls: two launches
+                tk = tab.commit_async(watch_all=True)
+                tab.watch_async()
             na, _ = tab.commit_wait_counts(tk)
             tab.watch_wait_count()
             t1 = time.perf_counter()
             LEGS.pop()
-            if r >= 3:
-                ms.append((t1 - t0) * 1e3)
-                n_adv += na
+            if r >= 6:
+                ms["tick_async" if fused else "two_calls"].append((t1 - t0) * 1e3)
+                n_adv += na if fused else 0
+        med = float(np.median(ms["tick_async"]))
         out[f"replies_{k}"] = {
-            "ms_tick_median": round(float(np.median(ms)), 4), "ms_tick_p90": round(float(np.percentile(ms, 90)), 4),
-            "replies_per_s": round(k / (float(np.median(ms)) * 1e-3), 1),
+            "ms_tick_median": round(med, 4), "ms_tick_p90": round(float(np.percentile(ms["tick_async"], 90)), 4),
+            "replies_per_s": round(k / (med * 1e-3), 1),
+            "ms_two_calls_median": round(float(np.median(ms["two_calls"])), 4),
             "commits_advanced_per_tick": round(n_adv / reps, 1)}
     tab.close()
     out["workload"] = (f"resident table of {n_all} config-3 groups; per tick k deltas (k/2 replies x matchIndex + "
-                       f"commitIndex), push + commit_async + watch_async + both waits (the pump's order); host wall "
-                       f"clock, median of {reps} ticks")
+                       f"commitIndex), push + rh_tick_async (both evaluations, one launch) + both waits (the pump's "
+                       f"order); two_calls: commit_async + watch_async instead, ticks alternating; host wall clock, "
+                       f"median of {reps} ticks each")
     return out
 
 
@@ -999,6 +1006,8 @@ def _summary(line: dict) -> dict:
     tk = g(line, "pcie", "delta_streaming", "tick")
     if tk:
         out["pump_tick_us"] = {k: round(v["ms_tick_median"] * 1e3, 1) for k, v in tk.items() if isinstance(v, dict)}
+        out["pump_tick_two_calls_us"] = {k: round(v["ms_two_calls_median"] * 1e3, 1) for k, v in tk.items()
+                                         if isinstance(v, dict)}
     ws = g(line, "pcie", "write_stamp")
     if ws:
         out["write_stamp_16KiB_us"] = ws["gpu_us"][0]

@@ -304,7 +304,8 @@ int rh_groups_set_event_sink(rh_groups* g, int sink);
  * as a profiler reports them); rh_groups_last_timing returns the last evaluation's device time in ms
  * (blocks until it has completed; RH_E_STATE before any timed evaluation) and, if list_evaluated is
  * not NULL, whether it ran over the dirty-row lists (1: only the rows marked since the previous
- * evaluation of its kind were visited; 0: every tile). */
+ * evaluation of its kind were visited; 2: both kinds' lists in one launch, rh_tick_async; 0: every
+ * tile). */
 int rh_groups_timing(rh_groups* g, int enable);
 int rh_groups_last_timing(rh_groups* g, float* eval_ms, int* list_evaluated);
 /* The last timed rh_commit_batch_async / rh_watch_levels_async split (ms, device events): submit =
@@ -326,6 +327,16 @@ int rh_watch_levels(rh_groups* g, const rh_watch_event** out_events, uint64_t* o
  * first, whose list it then replaces).  _wait fails with RH_E_STATE when none is outstanding. */
 int rh_watch_levels_async(rh_groups* g);
 int rh_watch_levels_wait(rh_groups* g, const rh_watch_event** out_events, uint64_t* out_n);
+/* A pump tick's two evaluations in one call: rh_commit_batch_async(g, flags, ticket) followed by
+ * rh_watch_levels_async(g), collected with rh_commit_batch_wait(g, *ticket, ..) and
+ * rh_watch_levels_wait(g, ..) -- the same results (each list in its own order; the _wait calls sort
+ * nothing).  When every row marked since the last evaluation of either kind is listed (the sparse
+ * tick: the marks since then fit the dirty-row lists, no control op in between) and the sink is not
+ * DEVICE, both run in ONE kernel launch: each listed row's updateCommit, then its commitIndexChanged
+ * right after in the same lane (the row's levels depend on its new commit index only), then the watch
+ * list's other rows (LeaderStateImpl.java:946-950, 612-622 per division); otherwise as the two calls.
+ * Replaces the two JNI crossings of LeaderStateImpl's updateCommit + commitIndexChanged per tick. */
+int rh_tick_async(rh_groups* g, uint32_t flags, uint64_t* ticket);
 /* Reads back one column of slots [first, first + n) (debug / checkpoint / tests): column =
  * RH_COL_MATCH(k) / RH_COL_FCOMMIT(k) / RH_COL_FLUSH / RH_COL_COMMITTED, or RH_COL_CONF (the
  * membership word, as int64) and RH_COL_TERM_START.  Stopped slots read INT64_MIN; follower

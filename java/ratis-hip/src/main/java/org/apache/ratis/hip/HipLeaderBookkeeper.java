@@ -321,12 +321,11 @@ public final class HipLeaderBookkeeper implements AutoCloseable {
     final long timeout = leaseTimeoutMs;
     final long batch = timeout >= 0 ? ++leaseBatchCount : 0;
     final long now = System.nanoTime();
-    // every shard's updateCommit(), then commitIndexChanged() (stream order on the shard's GPU: the
-    // commits the first stores are the second's input) and hasLease(): all shards in flight before
-    // any wait
+    // every shard's updateCommit(), then commitIndexChanged() (one call: the commits the first stores
+    // are the second's input; one launch when both kinds' dirty divisions are listed) and hasLease():
+    // all shards in flight before any wait
     for (int s = 0; s < shards; s++) {
-      tickets[s] = hip.commitAsync(s, RatisHip.COMMIT_WATCH_ALL);
-      hip.watchAsync(s);
+      tickets[s] = hip.tickAsync(s, RatisHip.COMMIT_WATCH_ALL);
       if (timeout >= 0) {
         hip.leaseAsync(s, now + leaseMarginNanos, timeout);
       }

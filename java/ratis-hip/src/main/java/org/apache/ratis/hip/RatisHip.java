@@ -168,6 +168,16 @@ public final class RatisHip implements AutoCloseable {
   }
 
   /**
+   * rh_tick_async on one shard: {@link #commitAsync} then {@link #watchAsync} in one call (one kernel
+   * launch when both kinds' dirty divisions are listed).  Collect with {@link #commitWait} (the
+   * returned ticket) and {@link #watchWait}.
+   */
+  public long tickAsync(int shard, int flags) throws IOException {
+    checkShard(shard);
+    return tickAsync0(node, shard, flags);
+  }
+
+  /**
    * rh_commit_batch_wait on one shard: the shard's events (slots WITHIN the shard) copied into the
    * caller's arrays, which must hold the shard capacity.  Returns nAdvanced << 32 | nWatchAll.
    */
@@ -324,6 +334,7 @@ public final class RatisHip implements AutoCloseable {
   private static native long commitBatch0(long node, int[] advSlot, long[] advCommit, int[] wallSlot, long[] wallMin)
       throws IOException;
   private static native long commitAsync0(long node, int shard, int flags) throws IOException;
+  private static native long tickAsync0(long node, int shard, int flags) throws IOException;
   private static native long commitWait0(long node, int shard, long ticket, int[] advSlot, long[] advCommit,
       int[] wallSlot, long[] wallMin) throws IOException;
   private static native int watchLevels0(long node, int shard, int[] slot, long[] min, long[] majority, long[] max,

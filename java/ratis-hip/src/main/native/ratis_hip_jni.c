@@ -195,6 +195,17 @@ JNIEXPORT jlong JNICALL CLS(commitAsync0)(JNIEnv* env, jclass c, jlong node, jin
     return (jlong)tk;
 }
 
+/* rh_tick_async: the shard's updateCommit and commitIndexChanged in one call (one launch when both
+ * kinds' dirty rows are listed); collected with commitWait0 (the ticket) and watchWait0. */
+JNIEXPORT jlong JNICALL CLS(tickAsync0)(JNIEnv* env, jclass c, jlong node, jint shard, jint flags) {
+    (void)c;
+    rh_groups* g = shard_table(env, node, shard);
+    if (!g) return 0;
+    uint64_t tk = 0;
+    if (check(env, rh_tick_async(g, (uint32_t)flags, &tk)) < 0) return 0;
+    return (jlong)tk;
+}
+
 /* The shard's events straight from the library's pinned result buffers into the caller's arrays
  * (slots within the shard); the arrays hold at least the shard capacity (checked in RatisHip). */
 JNIEXPORT jlong JNICALL CLS(commitWait0)(JNIEnv* env, jclass c, jlong node, jint shard, jlong ticket,

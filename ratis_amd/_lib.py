@@ -233,6 +233,7 @@ _SIGNATURES = {
     "rh_commit_batch_wait": (c_int, [c_void_p, c_uint64, POINTER(RhCommitOut)]),
     "rh_watch_levels": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_uint64)]),
     "rh_watch_levels_async": (c_int, [c_void_p]),
+    "rh_tick_async": (c_int, [c_void_p, c_uint32, POINTER(c_uint64)]),
     "rh_groups_timing": (c_int, [c_void_p, c_int]),
     "rh_groups_last_timing": (c_int, [c_void_p, POINTER(ctypes.c_float), POINTER(c_int)]),
     "rh_groups_last_timing_split": (c_int, [c_void_p, POINTER(ctypes.c_float), POINTER(ctypes.c_float),

@@ -173,7 +173,7 @@ struct rh_groups {
     bool lvalid[2] = {true, true};   // every row marked since the kind's last evaluation is listed
     uint64_t lmarks[2] = {0, 0};     // bound on the rows marked since then
     uint64_t marks[2] = {0, 0};      // deltas of each kind since its last evaluation (lists or not)
-    bool last_list = false;     // the last evaluation ran over the dirty-row lists (diagnostics)
+    int last_list = 0;          // the last evaluation: 0 tiles, 1 the dirty-row lists, 2 both kinds' lists in one launch
     // rh_groups_timing: [0] / [1] the evaluation's kernel boundaries, [2] before the staged deltas'
     // submission (H2D + apply), [3] after the event records reached the pinned lists (gather / drain,
     // or the evaluation itself when its kernel wrote them)
@@ -184,6 +184,7 @@ struct rh_groups {
     uint32_t cbits = 28;   // bits per list count in the evaluation's counter word (TableEvents)
     int64_t* d_read = nullptr;
     size_t read_cap = 0;
+    unsigned long long* d_tick = nullptr;   // [3 * kHeadStride]: the fused tick's counters (rh::TickEvents)
 };
 
 namespace {
@@ -242,6 +243,7 @@ void free_groups(rh_groups* g) {
     (void)hipFree(g->hbm_watch);
     (void)hipFree(g->wbdesc);
     (void)hipFree(g->d_evw);
+    (void)hipFree(g->d_tick);
     if (g->watch) (void)hipHostFree(g->watch);
     if (g->h_wcnt) (void)hipHostFree(g->h_wcnt);
     if (g->wdone) (void)hipEventDestroy(g->wdone);
@@ -439,6 +441,7 @@ int reset_heads(rh_groups* g) {
     (void)hipStreamSynchronize(s);
     RH_HIP(hipMemsetAsync(g->d_evw, 0, (size_t)2 * rh::kHeadStride * 8, s));
     RH_HIP(hipMemsetAsync(g->d_lheads, 0, (size_t)4 * kListRegions * rh::kHeadStride * 8, s));
+    RH_HIP(hipMemsetAsync(g->d_tick, 0, (size_t)3 * rh::kHeadStride * 8, s));
     RH_HIP(hipStreamSynchronize(s));
     g->lvalid[0] = g->lvalid[1] = false;   // the next evaluations run the tile kernels
     return RH_OK;
@@ -556,7 +559,7 @@ int evaluate(rh_groups* g, int mode, bool wall_on, const EvTargets& t, uint64_t*
     if (m == 0) g->marks[1] += g->marks[0];   // rows whose commit advanced are marked for commitIndexChanged
     g->marks[m] = 0;
     g->lvalid[m] = true;
-    g->last_list = list;
+    g->last_list = list ? 1 : 0;
     return RH_OK;
 }
 
@@ -748,6 +751,9 @@ RH_EXPORT int rh_groups_create(rh_ctx* ctx, uint64_t capacity, int64_t gap_thres
     if (rc == RH_OK) rc = dalloc(&g->d_lheads, (size_t)4 * kListRegions * rh::kHeadStride);
     if (rc == RH_OK && hipMemsetAsync(g->d_lheads, 0, (size_t)4 * kListRegions * rh::kHeadStride * 8, s) != hipSuccess)
         rc = rh::fail(RH_E_DEVICE, "rh_groups_create: list counters");
+    if (rc == RH_OK) rc = dalloc(&g->d_tick, (size_t)3 * rh::kHeadStride);
+    if (rc == RH_OK && hipMemsetAsync(g->d_tick, 0, (size_t)3 * rh::kHeadStride * 8, s) != hipSuccess)
+        rc = rh::fail(RH_E_DEVICE, "rh_groups_create: tick counters");
     if (rc == RH_OK) rc = dalloc(&g->d_evw, (size_t)2 * rh::kHeadStride);
     if (rc == RH_OK && hipMemsetAsync(g->d_evw, 0, (size_t)2 * rh::kHeadStride * 8, s) != hipSuccess)
         rc = rh::fail(RH_E_DEVICE, "rh_groups_create: counters");
@@ -819,7 +825,8 @@ RH_EXPORT int rh_groups_last_timing_split(rh_groups* g, float* submit_ms, float*
     std::unique_lock<std::mutex> lk(g->mu);
     if (!g->timed) return rh::fail(RH_E_STATE, "rh_groups_last_timing_split: no timed evaluation");
     hipEvent_t ev[6] = {g->tev[0], g->tev[1], g->tev[2], g->tev[3], g->tev[4], g->tev[5]};
-    const bool was_list = g->last_list, gathered = g->gathered_timed;
+    const int was_list = g->last_list;
+    const bool gathered = g->gathered_timed;
     lk.unlock();   // no table lock across a device wait
     RH_HIP(hipEventSynchronize(ev[3]));
     RH_HIP(hipEventSynchronize(ev[1]));
@@ -832,7 +839,7 @@ RH_EXPORT int rh_groups_last_timing_split(rh_groups* g, float* submit_ms, float*
         RH_HIP(hipEventSynchronize(ev[5]));
         RH_HIP(hipEventElapsedTime(gather_ms, ev[4], ev[5]));
     }
-    if (list_evaluated) *list_evaluated = was_list ? 1 : 0;
+    if (list_evaluated) *list_evaluated = was_list;
     return RH_OK;
 }
 
@@ -842,11 +849,11 @@ RH_EXPORT int rh_groups_last_timing(rh_groups* g, float* eval_ms, int* list_eval
     std::unique_lock<std::mutex> lk(g->mu);
     if (!g->timed) return rh::fail(RH_E_STATE, "rh_groups_last_timing: no timed evaluation");
     const hipEvent_t t0 = g->tev[0], t1 = g->tev[1];
-    const bool was_list = g->last_list;
+    const int was_list = g->last_list;
     lk.unlock();   // no table lock across a device wait
     RH_HIP(hipEventSynchronize(t1));
     RH_HIP(hipEventElapsedTime(eval_ms, t0, t1));
-    if (list_evaluated) *list_evaluated = was_list ? 1 : 0;
+    if (list_evaluated) *list_evaluated = was_list;
     return RH_OK;
 }
 
@@ -1210,24 +1217,41 @@ RH_EXPORT int rh_deltas_submit(rh_groups* g, size_t n) {
 // ---- evaluation -------------------------------------------------------------------------------------
 // No table lock is held across a device wait: a wait for an earlier evaluation (its result buffers
 // are about to be rewritten) and the _wait calls release both locks first, then re-validate.
-RH_EXPORT int rh_commit_batch_async(rh_groups* g, uint32_t flags, uint64_t* ticket) {
-    if (!g || !ticket) return rh::fail(RH_E_INVAL, "rh_commit_batch_async: NULL argument");
-    if (flags & ~RH_COMMIT_WATCH_ALL) return rh::fail(RH_E_INVAL, "rh_commit_batch_async: unknown flags");
-    DeviceGuard dg(g->ctx->device);
-    Exclusive ex(g);
-    const uint64_t tk = g->next_ticket++;
-    EvSet& e = g->ev[tk % kEvSets];
-    while (e.pending) {   // an unread earlier result set: wait for it before rewriting its buffers
+namespace {
+// The staged deltas go first, every evaluation of this call after them.
+int submit_staged(rh_groups* g) {
+    if (g->timing) RH_HIP(hipEventRecord(g->tev[2], g->ctx->stream));
+    g->gathered_timed = false;
+    return stage_submit(g);   // the deltas pushed before this call
+}
+
+// Frees result set `e` (ticket `tk`) for a new evaluation: an unread earlier result set is waited for
+// before its buffers are rewritten (both locks released while waiting).
+int claim_set(rh_groups* g, Exclusive& ex, EvSet& e) {
+    while (e.pending) {
         const uint64_t was = e.ticket;
         int rc = wait_unlocked(ex, e.done);
         if (rc != RH_OK) return rc;
         if (e.pending && e.ticket == was) e.pending = false;
     }
     e.ticket = 0;
-    if (g->timing) RH_HIP(hipEventRecord(g->tev[2], g->ctx->stream));
-    g->gathered_timed = false;
-    int rc = stage_submit(g);   // the deltas pushed before this call
-    if (rc != RH_OK) return rc;
+    return RH_OK;
+}
+
+// The same for the commitIndexChanged list.
+int claim_watch(rh_groups* g, Exclusive& ex) {
+    while (g->wpending) {   // the previous list is about to be rewritten: wait for it, unlocked
+        const uint64_t was = g->wgen;
+        int rc = wait_unlocked(ex, g->wdone);
+        if (rc != RH_OK) return rc;
+        if (g->wpending && g->wgen == was) g->wpending = false;
+    }
+    return RH_OK;
+}
+
+// updateCommit of the dirty rows into result set e under ticket tk (locks held, set claimed, staged
+// deltas submitted).
+int commit_issue(rh_groups* g, uint32_t flags, uint64_t tk, EvSet& e) {
     const bool wall_on = (flags & RH_COMMIT_WATCH_ALL) != 0;
     EvTargets t;
     t.adv[0] = e.d_adv, t.adv[1] = e.hbm_adv;
@@ -1235,7 +1259,7 @@ RH_EXPORT int rh_commit_batch_async(rh_groups* g, uint32_t flags, uint64_t* tick
     bool hbm = false;
     rh::TableDev ed;
     rh::ListRegion lr;
-    rc = evaluate(g, RH_MODE_COMMIT, wall_on, t, e.d_cnt, e.h_cnt, &hbm, e.bdesc, &e.nblocks, &ed, &lr);
+    int rc = evaluate(g, RH_MODE_COMMIT, wall_on, t, e.d_cnt, e.h_cnt, &hbm, e.bdesc, &e.nblocks, &ed, &lr);
     if (rc != RH_OK) return rc;
     if (hbm && e.nblocks) {   // REGION mode (DEVICE and AUTO): the records rebuilt into the pinned lists
         RH_HIP(hipEventRecord(g->evaluated, g->ctx->stream));
@@ -1265,6 +1289,21 @@ RH_EXPORT int rh_commit_batch_async(rh_groups* g, uint32_t flags, uint64_t* tick
     e.ticket = tk;
     e.hbm = hbm;
     e.pending = true;
+    return RH_OK;
+}
+}  // namespace
+
+RH_EXPORT int rh_commit_batch_async(rh_groups* g, uint32_t flags, uint64_t* ticket) {
+    if (!g || !ticket) return rh::fail(RH_E_INVAL, "rh_commit_batch_async: NULL argument");
+    if (flags & ~RH_COMMIT_WATCH_ALL) return rh::fail(RH_E_INVAL, "rh_commit_batch_async: unknown flags");
+    DeviceGuard dg(g->ctx->device);
+    Exclusive ex(g);
+    const uint64_t tk = g->next_ticket++;
+    EvSet& e = g->ev[tk % kEvSets];
+    int rc = claim_set(g, ex, e);
+    if (rc == RH_OK) rc = submit_staged(g);
+    if (rc == RH_OK) rc = commit_issue(g, flags, tk, e);
+    if (rc != RH_OK) return rc;
     *ticket = tk;
     return RH_OK;
 }
@@ -1315,26 +1354,16 @@ RH_EXPORT int rh_commit_batch(rh_groups* g, uint32_t flags, rh_commit_out* out) 
     return rc != RH_OK ? rc : rh_commit_batch_wait(g, tk, out);
 }
 
-RH_EXPORT int rh_watch_levels_async(rh_groups* g) {
-    if (!g) return rh::fail(RH_E_INVAL, "rh_watch_levels_async: groups == NULL");
-    DeviceGuard dg(g->ctx->device);
-    Exclusive ex(g);
-    while (g->wpending) {   // the previous list is about to be rewritten: wait for it, unlocked
-        const uint64_t was = g->wgen;
-        int rc = wait_unlocked(ex, g->wdone);
-        if (rc != RH_OK) return rc;
-        if (g->wpending && g->wgen == was) g->wpending = false;
-    }
-    if (g->timing) RH_HIP(hipEventRecord(g->tev[2], g->ctx->stream));
-    g->gathered_timed = false;
-    int rc = stage_submit(g);
-    if (rc != RH_OK) return rc;
+namespace {
+// commitIndexChanged of the watch-dirty rows into the watch list (locks held, list claimed, staged
+// deltas submitted).
+int watch_issue(rh_groups* g) {
     EvTargets t;
     t.watch[0] = g->d_watch, t.watch[1] = g->hbm_watch;
     bool hbm = false;
     rh::TableDev ed;
     rh::ListRegion lr;
-    rc = evaluate(g, RH_MODE_WATCH, false, t, g->d_wcnt, g->h_wcnt, &hbm, g->wbdesc, &g->wnblocks, &ed, &lr);
+    int rc = evaluate(g, RH_MODE_WATCH, false, t, g->d_wcnt, g->h_wcnt, &hbm, g->wbdesc, &g->wnblocks, &ed, &lr);
     if (rc != RH_OK) return rc;
     if (hbm && g->wnblocks) {   // REGION mode (DEVICE and AUTO): the records rebuilt into the pinned list
         RH_HIP(hipEventRecord(g->evaluated, g->ctx->stream));
@@ -1364,6 +1393,96 @@ RH_EXPORT int rh_watch_levels_async(rh_groups* g) {
     g->whbm = hbm;
     ++g->wgen;
     g->wpending = true;
+    return RH_OK;
+}
+
+#ifndef RH_TICK_FUSE   // rh_tick_async: both evaluations in one launch when both kinds run over their lists
+#define RH_TICK_FUSE 1
+#endif
+
+// Both evaluations of a tick in one launch (table_tick_kernel): every row marked for updateCommit
+// since its last evaluation and every row marked for commitIndexChanged since its last evaluation is
+// listed, and the records go to the pinned lists (not the DEVICE sink).  Locks held, result set e and
+// the watch list claimed, staged deltas submitted.
+int tick_issue(rh_groups* g, uint32_t flags, uint64_t tk, EvSet& e) {
+    hipStream_t s = g->ctx->stream;
+    int rc = flush_ops(g);   // control ops before: they drop the lists (-> the two launches)
+    if (rc == RH_OK) rc = gather_fence(g);
+    if (rc == RH_OK) rc = wgather_fence(g);
+    if (rc != RH_OK) return rc;
+    if (!(RH_TICK_FUSE && g->event_sink != RH_EVENTS_DEVICE && g->lvalid[0] && g->lvalid[1] &&
+          rh::table_commit_blocks(g->dev) > 0)) {   // the two evaluations one after the other
+        rc = commit_issue(g, flags, tk, e);
+        return rc != RH_OK ? rc : watch_issue(g);
+    }
+    rh::TableLists lc, lw;
+    lc.rows = g->d_lrows[0], lc.heads = lheads_of(g, 0, g->lpar[0]), lc.cap = g->lcap;
+    lw.rows = g->d_lrows[1], lw.heads = lheads_of(g, 1, g->lpar[1]), lw.cap = g->lcap;
+    rh::TickEvents ev;
+    ev.adv = e.d_adv;
+    ev.wall = (flags & RH_COMMIT_WATCH_ALL) ? e.d_wall : nullptr;
+    ev.watch = g->d_watch;
+    ev.cap = g->capacity;
+    ev.cnt = g->d_tick;
+    ev.counts_c = e.d_cnt;
+    ev.counts_w = g->d_wcnt;
+    ev.lheads_next_c = lheads_of(g, 0, g->lpar[0] ^ 1);
+    ev.lheads_next_w = lheads_of(g, 1, g->lpar[1] ^ 1);
+    rc = rh_table_tick_lists(g->dev, lc, lw, ev, s, g->timing ? g->tev[0] : nullptr, g->timing ? g->tev[1] : nullptr,
+                             std::max(g->lmarks[0], g->lmarks[1]));
+    if (rc != RH_OK) {
+        const std::string msg = rh_last_error();
+        (void)reset_heads(g);
+        return rh::fail(rc, msg);
+    }
+    if (g->timing) {
+        g->timed = true;
+        RH_HIP(hipEventRecord(g->tev[3], s));
+    }
+    RH_HIP(hipEventRecord(e.done, s));
+    RH_HIP(hipEventRecord(g->wdone, s));
+    for (int m = 0; m < 2; ++m) {   // both kinds' lists consumed; the next marks go to the fresh sets
+        g->lpar[m] ^= 1;
+        g->lmarks[m] = 0;
+        g->marks[m] = 0;
+        g->lvalid[m] = true;
+    }
+    g->last_list = 2;
+    e.nblocks = 0;
+    e.ticket = tk;
+    e.hbm = false;
+    e.pending = true;
+    g->wnblocks = 0;
+    g->whbm = false;
+    ++g->wgen;
+    g->wpending = true;
+    return RH_OK;
+}
+}  // namespace
+
+RH_EXPORT int rh_watch_levels_async(rh_groups* g) {
+    if (!g) return rh::fail(RH_E_INVAL, "rh_watch_levels_async: groups == NULL");
+    DeviceGuard dg(g->ctx->device);
+    Exclusive ex(g);
+    int rc = claim_watch(g, ex);
+    if (rc == RH_OK) rc = submit_staged(g);
+    return rc != RH_OK ? rc : watch_issue(g);
+}
+
+RH_EXPORT int rh_tick_async(rh_groups* g, uint32_t flags, uint64_t* ticket) {
+    if (!g || !ticket) return rh::fail(RH_E_INVAL, "rh_tick_async: NULL argument");
+    if (flags & ~RH_COMMIT_WATCH_ALL) return rh::fail(RH_E_INVAL, "rh_tick_async: unknown flags");
+    DeviceGuard dg(g->ctx->device);
+    Exclusive ex(g);
+    const uint64_t tk = g->next_ticket++;
+    EvSet& e = g->ev[tk % kEvSets];
+    int rc = claim_set(g, ex, e);
+    if (rc == RH_OK) rc = claim_watch(g, ex);
+    if (rc == RH_OK && e.pending) rc = rh::fail(RH_E_STATE, "rh_tick_async: result set taken while waiting");
+    if (rc == RH_OK) rc = submit_staged(g);
+    if (rc == RH_OK) rc = tick_issue(g, flags, tk, e);
+    if (rc != RH_OK) return rc;
+    *ticket = tk;
     return RH_OK;
 }
 

@@ -217,6 +217,21 @@ struct TableEvents {
     // (rh::table_list_passes); descriptors of passes the evaluation does not run are zeroed.
     uint32_t list_passes = 0;
 };
+// The fused tick's events (rh_tick_async, table_tick_kernel): both evaluations' records straight
+// into the pinned lists.  cnt: three u64 words kHeadStride apart -- the commit lists' counter
+// (advanced | watch-ALL << 32), the level records' counter, the workgroups done (u32) -- zero between
+// launches (the last workgroup zeroes them).
+struct TickEvents {
+    rh_index_event* adv = nullptr;
+    rh_index_event* wall = nullptr;    // null: watch-ALL changes not reported
+    rh_watch_event* watch = nullptr;
+    uint64_t cap = 0;
+    unsigned long long* cnt = nullptr;
+    uint64_t* counts_c = nullptr;      // [2] host-mapped: advanced, watch-ALL
+    uint64_t* counts_w = nullptr;      // [2] host-mapped: level records, 0
+    unsigned long long* lheads_next_c = nullptr;   // the other list-head sets: cleared
+    unsigned long long* lheads_next_w = nullptr;
+};
 // Tile-kernel workgroup: RH_TABLE_BLOCK_WAVES waves, one 128-row tile each.  REGION mode: records
 // per workgroup region (its rows) and u32 counts per workgroup descriptor (2 totals + 2 per wave).
 #ifndef RH_TABLE_BLOCK_WAVES   // A/B builds (both table.hip and groups.cpp see it)
@@ -331,6 +346,10 @@ int rh_table_apply_deltas(const rh::TableDev& t, const rh_delta* d_deltas, uint6
 int rh_table_commit_lists(const rh::TableDev& t, int mode, const rh::TableLists& l, const rh::TableLists& lw,
                           const rh::TableEvents& ev, hipStream_t stream, hipEvent_t t0, hipEvent_t t1, uint64_t rows_hint);
 int rh_table_control(const rh::TableDev& t, const rh::CtrlOp* d_ops, uint64_t n, hipStream_t stream);
+// The pump's tick in one launch: updateCommit over the commit list lc, commitIndexChanged over the rows
+// of the watch list lw and the rows whose commit advanced (table.hip, table_tick_kernel).
+int rh_table_tick_lists(const rh::TableDev& t, const rh::TableLists& lc, const rh::TableLists& lw, const rh::TickEvents& ev,
+                        hipStream_t stream, hipEvent_t t0, hipEvent_t t1, uint64_t rows_hint);
 // spec: issue every column load with the dirty-flag load (a large part of the table is dirty).
 int rh_table_commit(const rh::TableDev& t, int mode, const rh::TableEvents& ev, bool spec, hipStream_t stream,
                     hipEvent_t t0, hipEvent_t t1);

@@ -710,7 +710,9 @@ __global__ __launch_bounds__(kTBlock) void table_commit_kernel_net(TableDev Targ
 // workgroup (its waves' counts summed in LDS), records written straight into the result lists;
 // the last pass's atomic also counts the workgroup done (the counter word's top bits), so the
 // workgroup that completes the count knows the list lengths from its own atomic's return.
-template <int F, bool WATCH>
+// TICK (the fused tick kernel): neither flag is stored -- the caller claims the row's commitIndexChanged
+// and clears its updateCommit flag with atomics (table_tick_kernel).
+template <int F, bool WATCH, bool TICK = false>
 __device__ __forceinline__ void list_row(const TableDev& T, const TableTier& tt, uint32_t r, bool wall_on,
                                          bool wlisted, bool& e0, bool& e1, bool& wtrans, int64_t& x0, int64_t& x1,
                                          int64_t& x2, uint32_t& valid, uint32_t& slot, bool need_slot) {
@@ -730,7 +732,7 @@ __device__ __forceinline__ void list_row(const TableDev& T, const TableTier& tt,
 #if RH_TABLE_ABL == 7
     const uint8_t wd = 0;
 #else
-    const uint8_t wd = WATCH ? 0 : *tt.u8(tile::kWdirty, r);
+    const uint8_t wd = (WATCH || TICK) ? 0 : *tt.u8(tile::kWdirty, r);
 #endif
     int64_t self, ts = 0, p0 = 0, p1 = 0, p2 = 0;
     if (WATCH) {
@@ -761,21 +763,22 @@ __device__ __forceinline__ void list_row(const TableDev& T, const TableTier& tt,
             *tt.i64(tile::wmaj(F), r) = mj;
             *tt.i64(tile::wmax(F), r) = mx;
         }
-        *tt.u8(tile::kWdirty, r) = 0;
+        if (!TICK) *tt.u8(tile::kWdirty, r) = 0;
     } else {
         int64_t nc;
         e0 = rh_eval::commit_decision(v, mj, cm, self, ts, nc);
         e1 = wall_on && mn != p0;  // watch-ALL level changed (LSI:1025)
         x0 = nc, x1 = mn, x2 = 0;
 #if RH_TABLE_ABL != 7
-        *tt.u8(tile::kDirty, r) = 0;
+        if (!TICK) *tt.u8(tile::kDirty, r) = 0;
 #endif
         if (e0) {
             *tt.i64(tile::commit(F), r) = nc;
-            // the commit index changed: commitIndexChanged follows (listed if the flag was clear)
-            *tt.u8(tile::kWdirty, r) = 1;
-            *tt.summary(r, 1) = 1;
-            wtrans = wlisted && wd == 0;
+            if (!TICK) {   // the commit index changed: commitIndexChanged follows (listed if the flag was clear)
+                *tt.u8(tile::kWdirty, r) = 1;
+                *tt.summary(r, 1) = 1;
+                wtrans = wlisted && wd == 0;
+            }
         }
         if (e1) *tt.i64(tile::wall(F), r) = mn;
     }
@@ -972,6 +975,176 @@ __global__ __launch_bounds__(kListWaves * 64) void table_list_kernel(TableDev Ta
         }
     }
     if (region) zero_list_desc(ev, np);
+}
+
+// ---- the pump's tick in one launch (rh_tick_async) --------------------------------------------------
+// updateCommit over the commit list, then commitIndexChanged of every row whose levels may have moved
+// -- the watch list's rows (a follower commitIndex delta) and the rows whose commit advanced -- in the
+// same launch: a row's commitIndexChanged reads only that row (its followers' commitIndex, its new
+// commit index, its levels), so the lane that evaluated its updateCommit evaluates it right after
+// (LeaderStateImpl.java:946-950, then 612-622, per division), and the watch list's other rows are
+// evaluated by the launch's second phase.  Each row's commitIndexChanged runs exactly once, after its
+// updateCommit.  The two flags are touched only by atomics here (performed at the device's coherence
+// point: no fence, no cross-XCD staleness): a phase-A lane claims the row by clearing its watch flag
+// (or by its commit having advanced), waits for that atomic to return, then clears the row's
+// updateCommit flag; a phase-B lane reads the updateCommit flag with an atomic and claims only a row
+// whose flag it finds clear -- so phase A has claimed it already (the claim fails) or the row is not in
+// the commit list (the claim succeeds once).  Phase B reads only rows whose commit index this launch
+// does not write.  Records go straight into the pinned lists (one counter atomic per list kind per
+// workgroup and pass); the last workgroup to finish publishes both lists' lengths and zeroes the
+// counters.
+template <bool WATCH>
+__device__ __forceinline__ void list_row_any(const TableDev& T, const TableTier& tt, uint32_t row, bool wall_on, bool& e0,
+                                             bool& e1, int64_t& x0, int64_t& x1, int64_t& x2, uint32_t& valid,
+                                             uint32_t& slot) {
+    bool wt = false;
+    switch (tt.width) {
+        case 2: list_row<2, WATCH, true>(T, tt, row, wall_on, false, e0, e1, wt, x0, x1, x2, valid, slot, true); break;
+        case 4: list_row<4, WATCH, true>(T, tt, row, wall_on, false, e0, e1, wt, x0, x1, x2, valid, slot, true); break;
+        case 6: list_row<6, WATCH, true>(T, tt, row, wall_on, false, e0, e1, wt, x0, x1, x2, valid, slot, true); break;
+        case 8: list_row<8, WATCH, true>(T, tt, row, wall_on, false, e0, e1, wt, x0, x1, x2, valid, slot, true); break;
+        case 10: list_row<10, WATCH, true>(T, tt, row, wall_on, false, e0, e1, wt, x0, x1, x2, valid, slot, true); break;
+        case 12: list_row<12, WATCH, true>(T, tt, row, wall_on, false, e0, e1, wt, x0, x1, x2, valid, slot, true); break;
+        default: list_row<14, WATCH, true>(T, tt, row, wall_on, false, e0, e1, wt, x0, x1, x2, valid, slot, true); break;
+    }
+}
+
+// Clears byte `f` of its 32-bit word with one atomic; whether it was set.
+__device__ __forceinline__ bool claim_flag(uint8_t* f) {
+    uint32_t* w = reinterpret_cast<uint32_t*>(reinterpret_cast<uintptr_t>(f) & ~(uintptr_t)3);
+    const uint32_t sh = 8u * (uint32_t)(reinterpret_cast<uintptr_t>(f) & 3);
+    return ((atomicAnd(w, ~(0xFFu << sh)) >> sh) & 0xFFu) != 0u;
+}
+
+// Byte `f` as the device's coherence point holds it (a returning atomic that changes nothing).
+__device__ __forceinline__ uint8_t fetch_flag(uint8_t* f) {
+    uint32_t* w = reinterpret_cast<uint32_t*>(reinterpret_cast<uintptr_t>(f) & ~(uintptr_t)3);
+    const uint32_t sh = 8u * (uint32_t)(reinterpret_cast<uintptr_t>(f) & 3);
+    return (uint8_t)(atomicOr(w, 0u) >> sh);
+}
+
+__global__ __launch_bounds__(kListWaves * 64) void table_tick_kernel(TableDev Targ, TableLists Lc, TableLists Lw,
+                                                                     rh::TickEvents ev) {
+    const TableDev& T = rh::kernarg_struct<TableDev>();
+    (void)Targ;
+    constexpr uint32_t NR = rh::kHeads;
+    __shared__ __attribute__((aligned(16))) unsigned char tiers_mem[sizeof(TableTier) * rh::kTableTiers];
+    TableTier* tiers = reinterpret_cast<TableTier*>(tiers_mem);
+    __shared__ uint32_t wcnt[3][kListWaves];   // per pass: the waves' advanced / watch-ALL / level records
+    __shared__ unsigned long long bc, bw;      // per pass: the workgroup's ranges of the lists
+    __shared__ uint32_t book[2];               // passes over the commit list, over the watch list
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const uint32_t W = gridDim.x * kListWaves, wg = blockIdx.x * kListWaves + (uint32_t)wave;
+    const uint32_t r = wg % NR, k = wg / NR, Wr = (W - r + NR - 1) / NR;
+    const unsigned long long hc = Lc.heads[(uint64_t)r * rh::kHeadStride], hw = Lw.heads[(uint64_t)r * rh::kHeadStride];
+    uint32_t cl = 0;
+    if (wave == 0 && lane < (int)(2 * NR)) {   // lanes 0..7: the commit list's regions, 8..15: the watch list's
+        const TableLists& L = lane < (int)NR ? Lc : Lw;
+        const unsigned long long x = L.heads[(uint64_t)(lane % NR) * rh::kHeadStride];
+        cl = (uint32_t)(x < L.cap ? x : L.cap);
+    }
+    if (threadIdx.x == 64) {
+#pragma unroll
+        for (int q = 0; q < rh::kTableTiers; ++q) tiers[q] = T.tier[q];   // uniform index: scalar loads
+    }
+    if (blockIdx.x == 0 && threadIdx.x < NR) {   // the next list sets of both kinds
+        ev.lheads_next_c[(uint64_t)threadIdx.x * rh::kHeadStride] = 0ull;
+        ev.lheads_next_w[(uint64_t)threadIdx.x * rh::kHeadStride] = 0ull;
+    }
+    const uint32_t cnt_c = (uint32_t)(hc < Lc.cap ? hc : Lc.cap), cnt_w = (uint32_t)(hw < Lw.cap ? hw : Lw.cap);
+    if (wave == 0) {
+        uint32_t np = 0;
+        if (lane < (int)(2 * NR)) {
+            const uint32_t rr = (uint32_t)lane % NR, wr = (W - rr + NR - 1) / NR;
+            np = (cl + wr * 64u - 1) / (wr * 64u);
+        }
+        const uint32_t npc = wave_max_u32(lane < (int)NR ? np : 0u), npw = wave_max_u32(lane >= (int)NR ? np : 0u);
+        if (lane == 0) {
+            book[0] = npc;
+            book[1] = npw;
+        }
+    }
+    __syncthreads();
+    const uint32_t np_c = book[0], np_w = book[1];
+    const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const bool wall_on = ev.wall != nullptr;
+    const uint64_t R = ev.cap;
+    for (uint32_t phase = 0; phase < 2; ++phase) {
+        const uint32_t np = phase == 0 ? np_c : np_w;
+        for (uint32_t pass = 0; pass < np; ++pass) {
+            const uint32_t idx = (pass * 64u + (uint32_t)lane) * Wr + k;
+            bool e0 = false, e1 = false, ew = false;
+            int64_t x0 = 0, x1 = 0, x2 = 0, y0 = 0, y1 = 0, y2 = 0;
+            uint32_t valid = 0, slot = 0, wvalid = 0;
+            if (phase == 0 && idx < cnt_c) {   // updateCommit, then this row's commitIndexChanged if claimed
+                const uint32_t ent = Lc.rows[(uint64_t)r * Lc.cap + idx];
+                const uint32_t t = ent >> 28, row = ent & rh::kRowMask;
+                const TableTier tt = tiers[t < (uint32_t)rh::kTableTiers ? t : 0u];
+                if (row < tt.rows) {
+                    list_row_any<false>(T, tt, row, wall_on, e0, e1, x0, x1, x2, valid, slot);
+                    const bool mine = claim_flag(tt.u8(tile::kWdirty, row)) || e0;   // e0: the commit advanced
+                    // the claim performed (returned) before the updateCommit flag clears: phase B reads it
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                    (void)claim_flag(tt.u8(tile::kDirty, row));
+                    if (mine) {
+                        bool dummy = false;
+                        list_row_any<true>(T, tt, row, false, ew, dummy, y0, y1, y2, wvalid, slot);
+                    }
+                }
+            } else if (phase == 1 && idx < cnt_w) {   // the watch list's rows no updateCommit lane claims
+                const uint32_t ent = Lw.rows[(uint64_t)r * Lw.cap + idx];
+                const uint32_t t = ent >> 28, row = ent & rh::kRowMask;
+                const TableTier tt = tiers[t < (uint32_t)rh::kTableTiers ? t : 0u];
+                if (row < tt.rows && fetch_flag(tt.u8(tile::kDirty, row)) == 0 && claim_flag(tt.u8(tile::kWdirty, row))) {
+                    bool dummy = false;
+                    list_row_any<true>(T, tt, row, false, ew, dummy, y0, y1, y2, wvalid, slot);
+                }
+            }
+            const uint64_t a = __ballot(e0), c = __ballot(e1), w = __ballot(ew);
+            if (lane == 0) {
+                wcnt[0][wave] = (uint32_t)__popcll(a);
+                wcnt[1][wave] = (uint32_t)__popcll(c);
+                wcnt[2][wave] = (uint32_t)__popcll(w);
+            }
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                unsigned long long s0 = 0, s1 = 0, s2 = 0;
+#pragma unroll
+                for (uint32_t q = 0; q < kListWaves; ++q) s0 += wcnt[0][q], s1 += wcnt[1][q], s2 += wcnt[2][q];
+                bc = (s0 | s1) ? atomicAdd(ev.cnt, s0 | (s1 << 32)) : 0ull;
+                bw = s2 ? atomicAdd(ev.cnt + rh::kHeadStride, s2) : 0ull;
+            }
+            __syncthreads();
+            uint64_t b0 = bc & 0xFFFFFFFFull, b1 = bc >> 32, b2 = bw;
+            for (int q = 0; q < wave; ++q) b0 += wcnt[0][q], b1 += wcnt[1][q], b2 += wcnt[2][q];
+            __syncthreads();   // wcnt / bc / bw are the next pass's
+            if (e0) {
+                const uint64_t kk = b0 + (uint64_t)__popcll(a & lt);
+                if (kk < R) ev.adv[kk] = rh_index_event{slot, 0u, x0};
+            }
+            if (e1) {
+                const uint64_t kk = b1 + (uint64_t)__popcll(c & lt);
+                if (kk < R) ev.wall[kk] = rh_index_event{slot, 0u, x1};
+            }
+            if (ew) {
+                const uint64_t kk = b2 + (uint64_t)__popcll(w & lt);
+                if (kk < R) ev.watch[kk] = rh_watch_event{slot, wvalid, y0, y1, y2};
+            }
+        }
+    }
+    // the last workgroup to finish publishes both lists' lengths and zeroes the counters (every other
+    // workgroup's counter atomics returned before its done atomic was issued)
+    if (threadIdx.x == 0) {
+        const unsigned int prev = atomicAdd(reinterpret_cast<unsigned int*>(ev.cnt + 2 * rh::kHeadStride), 1u);
+        if (prev + 1u == gridDim.x) {
+            const unsigned long long c = atomicExch(ev.cnt, 0ull), w = atomicExch(ev.cnt + rh::kHeadStride, 0ull);
+            atomicExch(reinterpret_cast<unsigned int*>(ev.cnt + 2 * rh::kHeadStride), 0u);
+            ev.counts_c[0] = c & 0xFFFFFFFFull;
+            ev.counts_c[1] = c >> 32;
+            ev.counts_w[0] = w;
+            ev.counts_w[1] = 0;
+        }
+    }
 }
 
 // ---- hasLease over every started row -------------------------------------------------------------
@@ -1196,6 +1369,13 @@ int rh_table_commit_lists(const rh::TableDev& t, int mode, const rh::TableLists&
     else
         e = eval_launch(table_list_kernel<false>, g, b, stream, t0, t1, t, l, lw, ev);
     RH_HIP(e);
+    return RH_OK;
+}
+
+int rh_table_tick_lists(const rh::TableDev& t, const rh::TableLists& lc, const rh::TableLists& lw, const rh::TickEvents& ev,
+                        hipStream_t stream, hipEvent_t t0, hipEvent_t t1, uint64_t rows_hint) {
+    const dim3 g(rh::table_list_grid(rows_hint)), b(kListWaves * 64);
+    RH_HIP(eval_launch(table_tick_kernel, g, b, stream, t0, t1, t, lc, lw, ev));
     return RH_OK;
 }
 

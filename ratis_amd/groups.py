@@ -259,12 +259,12 @@ class RaftGroupTable:
         """``rh_groups_last_timing_split``: the last timed _async split in submit (staged deltas' H2D +
         apply), eval (the evaluation kernels), events (until the records are in the pinned lists) and
         gather (the REGION gather kernel alone, 0 if none), device ms; ``list``: whether it ran over the
-        dirty-row lists."""
+        dirty-row lists; ``fused``: both kinds in one launch (:meth:`tick_async`)."""
         a, b, c, d, m = ctypes.c_float(), ctypes.c_float(), ctypes.c_float(), ctypes.c_float(), ctypes.c_int()
         check(self._lib.rh_groups_last_timing_split(self.handle, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c),
                                                     ctypes.byref(d), ctypes.byref(m)))
         return {"submit_ms": float(a.value), "eval_ms": float(b.value), "events_ms": float(c.value),
-                "gather_ms": float(d.value), "list": bool(m.value)}
+                "gather_ms": float(d.value), "list": bool(m.value), "fused": m.value == 2}
 
     def last_was_list(self) -> bool:
         """Whether the last (timed) evaluation ran over the dirty-row lists (list mode)."""
@@ -275,6 +275,14 @@ class RaftGroupTable:
     def watch_async(self) -> None:
         """``rh_watch_levels_async``: commitIndexChanged() of the dirty slots, in flight."""
         check(self._lib.rh_watch_levels_async(self.handle))
+
+    def tick_async(self, watch_all: bool = True) -> int:
+        """``rh_tick_async``: :meth:`commit_async` then :meth:`watch_async` in one call (one kernel
+        launch when both kinds run over their dirty-row lists); collect with :meth:`commit_wait` (the
+        returned ticket) and :meth:`watch_wait`."""
+        tk = ctypes.c_uint64()
+        check(self._lib.rh_tick_async(self.handle, _lib.RH_COMMIT_WATCH_ALL if watch_all else 0, ctypes.byref(tk)))
+        return tk.value
 
     def watch_wait(self) -> np.ndarray:
         """``rh_watch_levels_wait``: the outstanding evaluation's changed levels, sorted by slot."""
@@ -500,8 +508,7 @@ class LeaderPump:
         lease = self.lease_timeout_ms >= 0
         tickets = []
         for t in self.node.tables:   # every shard's passes in flight before any wait (stream order:
-            tickets.append(t.commit_async(watch_all=True))   # commit, then its commitIndexChanged)
-            t.watch_async()
+            tickets.append(t.tick_async(watch_all=True))   # commit, then its commitIndexChanged)
             if lease:
                 t.lease_async(now_nanos, self.lease_timeout_ms)
         n = {"commit": 0, "watch_all": 0, "watch_levels": 0}

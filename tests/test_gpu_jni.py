@@ -20,7 +20,7 @@ from tests.test_gpu_table import conf_word, random_deltas
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HARNESS = os.path.join(ROOT, "tests", "jni_harness", "_build", "libratis_hip_jni_test.so")
 NATIVES = ["nodeCreate0", "nodeDestroy0", "nodeShards0", "shardOf0", "groupStart0", "groupReconf0", "groupStop0",
-           "pushDeltas0", "acquire0", "submit0", "commitBatch0", "commitAsync0", "commitWait0", "watchLevels0",
+           "pushDeltas0", "acquire0", "submit0", "commitBatch0", "commitAsync0", "tickAsync0", "commitWait0", "watchLevels0",
            "watchAsync0", "watchWait0", "setEventSink0", "leaseStart0", "leaseBatch0", "leaseBatchShard0",
            "leaseAsync0", "leaseWait0", "verifyHost0", "ctxCreate0", "ctxDestroy0", "readSegments0", "stampHost0",
            "hostRegister0", "hostUnregister0"]
@@ -126,6 +126,7 @@ def test_pump_natives_against_direct_calls_and_model(jni, ctx, orc):
         jni.clean()
         push = jni.fn("pushDeltas0", None, L, P, I)
         commit_async = jni.fn("commitAsync0", L, L, I, I)
+        tick_async = jni.fn("tickAsync0", L, L, I, I)
         commit_wait = jni.fn("commitWait0", L, L, I, L, P, P, P, P)
         watch_async = jni.fn("watchAsync0", None, L, I)
         watch_wait = jni.fn("watchWait0", I, L, I, P, P, P, P, P)
@@ -143,9 +144,12 @@ def test_pump_natives_against_direct_calls_and_model(jni, ctx, orc):
             twin.push(d)
             model.apply(d)
             jni.clean()
-            tk = commit_async(node, 0, _lib.RH_COMMIT_WATCH_ALL)
+            if step == 2:   # the pump's call: both evaluations (rh_tick_async)
+                tk = tick_async(node, 0, _lib.RH_COMMIT_WATCH_ALL)
+            else:
+                tk = commit_async(node, 0, _lib.RH_COMMIT_WATCH_ALL)
             tk2 = twin.tables[0].commit_async(watch_all=True)
-            if step % 2 == 0:
+            if step == 0:
                 watch_async(node, 0)
             counts = commit_wait(node, 0, tk, jni.arr(a_slot), jni.arr(a_val), jni.arr(w_slot), jni.arr(w_val))
             jni.clean()

@@ -108,18 +108,18 @@ def _method_body(src: str, signature: str) -> str:
 def test_pump_runs_watch_levels_and_watch_all_without_allocating():
     """commitIndexChanged (LeaderStateImpl.java:606-622) and updateCommit's watch ALL (:1025) in HIP
     mode: every tick evaluates with RH_COMMIT_WATCH_ALL, puts every shard's commit, watch and lease
-    passes in flight before any wait (rh_*_async), waits them per shard, and allocates nothing
-    (result arrays sized once per shard capacity)."""
+    passes in flight before any wait (rh_tick_async: commit + watch in one call; rh_lease_batch_async),
+    waits them per shard, and allocates nothing (result arrays sized once per shard capacity)."""
     book = open(BOOKKEEPER_JAVA).read()
     tick = _method_body(book, "void tick()")
-    assert "hip.commitAsync(s, RatisHip.COMMIT_WATCH_ALL)" in tick
+    assert "hip.tickAsync(s, RatisHip.COMMIT_WATCH_ALL)" in tick
     assert "hip.commitWait(" in tick and "hip.watchWait(" in tick and "hip.leaseWait(" in tick
     assert "onWatchLevels(" in tick and "onWatchAll(" in tick and "onCommit(" in tick
     assert not re.search(r"\bnew\b", tick), "tick() allocates"
     assert "capacity * hip.getShards()" not in book and "capacity * shards" not in book
     # every shard's three passes are issued in the first loop, before the first wait
     first_wait = tick.index("hip.commitWait(")
-    for call in ("hip.commitAsync(", "hip.watchAsync(", "hip.leaseAsync("):
+    for call in ("hip.tickAsync(", "hip.leaseAsync("):
         assert tick.index(call) < first_wait, call
     assert "hip.watchLevels(" not in tick and "hip.leaseBatch(" not in tick
 
