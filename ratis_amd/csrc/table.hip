@@ -982,17 +982,18 @@ __global__ __launch_bounds__(kListWaves * 64) void table_list_kernel(TableDev Ta
 // -- the watch list's rows (a follower commitIndex delta) and the rows whose commit advanced -- in the
 // same launch: a row's commitIndexChanged reads only that row (its followers' commitIndex, its new
 // commit index, its levels), so the lane that evaluated its updateCommit evaluates it right after
-// (LeaderStateImpl.java:946-950, then 612-622, per division), and the watch list's other rows are
-// evaluated by the launch's second phase.  Each row's commitIndexChanged runs exactly once, after its
-// updateCommit.  The two flags are touched only by atomics here (performed at the device's coherence
-// point: no fence, no cross-XCD staleness): a phase-A lane claims the row by clearing its watch flag
-// (or by its commit having advanced), waits for that atomic to return, then clears the row's
-// updateCommit flag; a phase-B lane reads the updateCommit flag with an atomic and claims only a row
-// whose flag it finds clear -- so phase A has claimed it already (the claim fails) or the row is not in
-// the commit list (the claim succeeds once).  Phase B reads only rows whose commit index this launch
-// does not write.  Records go straight into the pinned lists (one counter atomic per list kind per
-// workgroup and pass); the last workgroup to finish publishes both lists' lengths and zeroes the
-// counters.
+// (LeaderStateImpl.java:946-950, then 612-622, per division); the watch list's other rows are
+// evaluated by the lanes holding their entries, in the same passes (a lane takes one entry of each
+// list per pass: both rows' loads and atomics in flight together).  Each row's commitIndexChanged runs
+// exactly once, after its updateCommit.  The two flags are touched only by atomics here (performed at
+// the device's coherence point: no fence, no cross-XCD staleness): a commit-list lane claims the row
+// by clearing its watch flag (or by its commit having advanced), waits for that atomic to return,
+// then clears the row's updateCommit flag; a watch-list lane reads the updateCommit flag with an
+// atomic and claims only a row whose flag it finds clear -- so a commit-list lane has claimed it
+// already (the claim fails) or the row is not in the commit list (the claim succeeds once).  A
+// watch-list lane evaluates only rows whose commit index this launch does not write.  Records go
+// straight into the pinned lists (one counter atomic per list kind per workgroup and pass); the last
+// workgroup to finish publishes both lists' lengths and zeroes the counters.
 template <bool WATCH>
 __device__ __forceinline__ void list_row_any(const TableDev& T, const TableTier& tt, uint32_t row, bool wall_on, bool& e0,
                                              bool& e1, int64_t& x0, int64_t& x1, int64_t& x2, uint32_t& valid,
@@ -1069,67 +1070,80 @@ __global__ __launch_bounds__(kListWaves * 64) void table_tick_kernel(TableDev Ta
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const bool wall_on = ev.wall != nullptr;
     const uint64_t R = ev.cap;
-    for (uint32_t phase = 0; phase < 2; ++phase) {
-        const uint32_t np = phase == 0 ? np_c : np_w;
-        for (uint32_t pass = 0; pass < np; ++pass) {
-            const uint32_t idx = (pass * 64u + (uint32_t)lane) * Wr + k;
-            bool e0 = false, e1 = false, ew = false;
-            int64_t x0 = 0, x1 = 0, x2 = 0, y0 = 0, y1 = 0, y2 = 0;
-            uint32_t valid = 0, slot = 0, wvalid = 0;
-            if (phase == 0 && idx < cnt_c) {   // updateCommit, then this row's commitIndexChanged if claimed
-                const uint32_t ent = Lc.rows[(uint64_t)r * Lc.cap + idx];
-                const uint32_t t = ent >> 28, row = ent & rh::kRowMask;
-                const TableTier tt = tiers[t < (uint32_t)rh::kTableTiers ? t : 0u];
-                if (row < tt.rows) {
-                    list_row_any<false>(T, tt, row, wall_on, e0, e1, x0, x1, x2, valid, slot);
-                    const bool mine = claim_flag(tt.u8(tile::kWdirty, row)) || e0;   // e0: the commit advanced
-                    // the claim performed (returned) before the updateCommit flag clears: phase B reads it
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                    (void)claim_flag(tt.u8(tile::kDirty, row));
-                    if (mine) {
-                        bool dummy = false;
-                        list_row_any<true>(T, tt, row, false, ew, dummy, y0, y1, y2, wvalid, slot);
-                    }
-                }
-            } else if (phase == 1 && idx < cnt_w) {   // the watch list's rows no updateCommit lane claims
-                const uint32_t ent = Lw.rows[(uint64_t)r * Lw.cap + idx];
-                const uint32_t t = ent >> 28, row = ent & rh::kRowMask;
-                const TableTier tt = tiers[t < (uint32_t)rh::kTableTiers ? t : 0u];
-                if (row < tt.rows && fetch_flag(tt.u8(tile::kDirty, row)) == 0 && claim_flag(tt.u8(tile::kWdirty, row))) {
+    // one pass takes a lane's entry of each list: the two rows' loads and atomics in flight together
+    const uint32_t np = np_c > np_w ? np_c : np_w;
+    for (uint32_t pass = 0; pass < np; ++pass) {
+        const uint32_t idx = (pass * 64u + (uint32_t)lane) * Wr + k;
+        bool e0 = false, e1 = false, ew = false, ev2 = false;
+        int64_t x0 = 0, x1 = 0, x2 = 0, y0 = 0, y1 = 0, y2 = 0, z0 = 0, z1 = 0, z2 = 0;
+        uint32_t valid = 0, slot = 0, wvalid = 0, slot2 = 0, wvalid2 = 0;
+        // the watch list's entry: its updateCommit flag fetched first (the answer is needed last)
+        TableTier tw{};
+        uint32_t roww = 0;
+        uint8_t dflag = 1;
+        if (idx < cnt_w) {
+            const uint32_t ent = Lw.rows[(uint64_t)r * Lw.cap + idx];
+            const uint32_t t = ent >> 28;
+            roww = ent & rh::kRowMask;
+            tw = tiers[t < (uint32_t)rh::kTableTiers ? t : 0u];
+            if (roww < tw.rows) dflag = fetch_flag(tw.u8(tile::kDirty, roww));
+        }
+        // the commit list's entry: claimed, updateCommit, then (claimed or advanced) commitIndexChanged
+        if (idx < cnt_c) {
+            const uint32_t ent = Lc.rows[(uint64_t)r * Lc.cap + idx];
+            const uint32_t t = ent >> 28, row = ent & rh::kRowMask;
+            const TableTier tt = tiers[t < (uint32_t)rh::kTableTiers ? t : 0u];
+            if (row < tt.rows) {
+                const bool claimed = claim_flag(tt.u8(tile::kWdirty, row));
+                list_row_any<false>(T, tt, row, wall_on, e0, e1, x0, x1, x2, valid, slot);
+                // the claim performed (returned) before the updateCommit flag clears: the watch side reads it
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                (void)claim_flag(tt.u8(tile::kDirty, row));
+                if (claimed || e0) {   // e0: the commit advanced
                     bool dummy = false;
                     list_row_any<true>(T, tt, row, false, ew, dummy, y0, y1, y2, wvalid, slot);
                 }
             }
-            const uint64_t a = __ballot(e0), c = __ballot(e1), w = __ballot(ew);
-            if (lane == 0) {
-                wcnt[0][wave] = (uint32_t)__popcll(a);
-                wcnt[1][wave] = (uint32_t)__popcll(c);
-                wcnt[2][wave] = (uint32_t)__popcll(w);
-            }
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                unsigned long long s0 = 0, s1 = 0, s2 = 0;
+        }
+        // the watch list's row, if no updateCommit lane holds it: its updateCommit flag clear (an
+        // updateCommit lane has claimed it already, or it is not in the commit list), then the claim
+        if (dflag == 0 && claim_flag(tw.u8(tile::kWdirty, roww))) {
+            bool dummy = false;
+            list_row_any<true>(T, tw, roww, false, ev2, dummy, z0, z1, z2, wvalid2, slot2);
+        }
+        const uint64_t a = __ballot(e0), c = __ballot(e1), w = __ballot(ew), w2 = __ballot(ev2);
+        if (lane == 0) {
+            wcnt[0][wave] = (uint32_t)__popcll(a);
+            wcnt[1][wave] = (uint32_t)__popcll(c);
+            wcnt[2][wave] = (uint32_t)(__popcll(w) + __popcll(w2));
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long s0 = 0, s1 = 0, s2 = 0;
 #pragma unroll
-                for (uint32_t q = 0; q < kListWaves; ++q) s0 += wcnt[0][q], s1 += wcnt[1][q], s2 += wcnt[2][q];
-                bc = (s0 | s1) ? atomicAdd(ev.cnt, s0 | (s1 << 32)) : 0ull;
-                bw = s2 ? atomicAdd(ev.cnt + rh::kHeadStride, s2) : 0ull;
-            }
-            __syncthreads();
-            uint64_t b0 = bc & 0xFFFFFFFFull, b1 = bc >> 32, b2 = bw;
-            for (int q = 0; q < wave; ++q) b0 += wcnt[0][q], b1 += wcnt[1][q], b2 += wcnt[2][q];
-            __syncthreads();   // wcnt / bc / bw are the next pass's
-            if (e0) {
-                const uint64_t kk = b0 + (uint64_t)__popcll(a & lt);
-                if (kk < R) ev.adv[kk] = rh_index_event{slot, 0u, x0};
-            }
-            if (e1) {
-                const uint64_t kk = b1 + (uint64_t)__popcll(c & lt);
-                if (kk < R) ev.wall[kk] = rh_index_event{slot, 0u, x1};
-            }
-            if (ew) {
-                const uint64_t kk = b2 + (uint64_t)__popcll(w & lt);
-                if (kk < R) ev.watch[kk] = rh_watch_event{slot, wvalid, y0, y1, y2};
-            }
+            for (uint32_t q = 0; q < kListWaves; ++q) s0 += wcnt[0][q], s1 += wcnt[1][q], s2 += wcnt[2][q];
+            bc = (s0 | s1) ? atomicAdd(ev.cnt, s0 | (s1 << 32)) : 0ull;
+            bw = s2 ? atomicAdd(ev.cnt + rh::kHeadStride, s2) : 0ull;
+        }
+        __syncthreads();
+        uint64_t b0 = bc & 0xFFFFFFFFull, b1 = bc >> 32, b2 = bw;
+        for (int q = 0; q < wave; ++q) b0 += wcnt[0][q], b1 += wcnt[1][q], b2 += wcnt[2][q];
+        __syncthreads();   // wcnt / bc / bw are the next pass's
+        if (e0) {
+            const uint64_t kk = b0 + (uint64_t)__popcll(a & lt);
+            if (kk < R) ev.adv[kk] = rh_index_event{slot, 0u, x0};
+        }
+        if (e1) {
+            const uint64_t kk = b1 + (uint64_t)__popcll(c & lt);
+            if (kk < R) ev.wall[kk] = rh_index_event{slot, 0u, x1};
+        }
+        if (ew) {
+            const uint64_t kk = b2 + (uint64_t)__popcll(w & lt);
+            if (kk < R) ev.watch[kk] = rh_watch_event{slot, wvalid, y0, y1, y2};
+        }
+        if (ev2) {
+            const uint64_t kk = b2 + (uint64_t)__popcll(w) + (uint64_t)__popcll(w2 & lt);
+            if (kk < R) ev.watch[kk] = rh_watch_event{slot2, wvalid2, z0, z1, z2};
         }
     }
     // the last workgroup to finish publishes both lists' lengths and zeroes the counters (every other
