@@ -225,7 +225,7 @@ _SIGNATURES = {
     "rh_node_lease_batch": (c_int, [c_void_p, c_int64, c_int64, c_void_p, c_uint64]),
     "rh_groups_load": (c_int, [c_void_p, c_uint32, c_uint32, c_uint32, c_void_p, c_void_p, c_void_p, c_void_p,
                                c_void_p, c_void_p]),
-    "rh_push_deltas": (c_int, [c_void_p, POINTER(RhDelta), c_size_t]),
+    "rh_push_deltas": (c_int, [c_void_p, c_void_p, c_size_t]),   # rh_delta*: groups._addr
     "rh_deltas_acquire": (c_int, [c_void_p, POINTER(c_void_p), POINTER(c_size_t)]),
     "rh_deltas_submit": (c_int, [c_void_p, c_size_t]),
     "rh_commit_batch": (c_int, [c_void_p, c_uint32, POINTER(RhCommitOut)]),
@@ -254,7 +254,7 @@ _SIGNATURES = {
     "rh_node_group_start": (c_int, [c_void_p, c_uint32, c_uint32, c_int64, c_int64, c_int64]),
     "rh_node_group_reconf": (c_int, [c_void_p, c_uint32, c_uint32, c_void_p]),
     "rh_node_group_stop": (c_int, [c_void_p, c_uint32]),
-    "rh_node_push_deltas": (c_int, [c_void_p, POINTER(RhDelta), c_size_t]),
+    "rh_node_push_deltas": (c_int, [c_void_p, c_void_p, c_size_t]),   # rh_delta*: groups._addr
     "rh_node_commit_batch": (c_int, [c_void_p, c_uint32, c_void_p, c_uint64, POINTER(c_uint64), c_void_p, c_uint64,
                                      POINTER(c_uint64)]),
     "rh_crc32c_frames_launch": (c_int, [c_void_p, POINTER(RhFrames), c_uint32, c_void_p]),

@@ -160,6 +160,10 @@ struct rh_groups {
     uint64_t* h_wcnt = nullptr;               // host-mapped [2]: its length (the evaluation's last workgroup)
     uint64_t* d_wcnt = nullptr;
     hipEvent_t wdone = nullptr;
+    // the watch list of a fused tick completes with that tick's result set: wtick = its ticket (0: the
+    // list has its own wdone), wseen = the commit wait of that ticket has seen it complete
+    uint64_t wtick = 0;
+    bool wseen = false;
     bool wpending = false, whbm = false;
     uint64_t wgen = 0;                        // watch evaluations started (a waiter re-validates it)
     hipEvent_t ldone = nullptr;               // rh_lease_batch_async's bitmap D2H
@@ -185,6 +189,7 @@ struct rh_groups {
     int64_t* d_read = nullptr;
     size_t read_cap = 0;
     unsigned long long* d_tick = nullptr;   // [3 * kHeadStride]: the fused tick's counters (rh::TickEvents)
+    uint64_t map_gen = 0;   // bumped by every slot_map change (exclusive side): a push's checks stay valid while it holds
 };
 
 namespace {
@@ -574,6 +579,7 @@ int do_stop(rh_groups* g, uint32_t slot) {
     if (rc != RH_OK) return rc;
     g->tiers[m >> 28].pending_free.push_back(m & rh::kRowMask);
     g->slot_map[slot] = kNoRow;
+    ++g->map_gen;
     g->slot_conf[slot] = 0;
     return RH_OK;
 }
@@ -885,6 +891,7 @@ RH_EXPORT int rh_group_start(rh_groups* g, uint32_t slot, uint32_t conf, int64_t
     rc = queue_op(g, op);
     if (rc != RH_OK) return rc;
     g->slot_map[slot] = op.dst;
+    ++g->map_gen;
     g->slot_conf[slot] = conf;
     return RH_OK;
 }
@@ -925,6 +932,7 @@ RH_EXPORT int rh_group_reconf(rh_groups* g, uint32_t slot, uint32_t conf, const 
     if (rc != RH_OK) return rc;
     if (op.kind == rh::kCtrlMove) g->tiers[t_old].pending_free.push_back(m & rh::kRowMask);
     g->slot_map[slot] = op.dst;
+    ++g->map_gen;
     g->slot_conf[slot] = conf;
     return RH_OK;
 }
@@ -1060,6 +1068,7 @@ RH_EXPORT int rh_groups_load(rh_groups* g, uint32_t first, uint32_t n, uint32_t 
         (void)hipFree(d_cols);
         if (rc != RH_OK) return rc;
         if (e != hipSuccess) return rh::hip_fail(e, "rh_groups_load");
+        ++g->map_gen;
         for (uint32_t j = 0; j < m; ++j) {
             g->slot_map[slots[j]] = enc(t, rows[j]);
             g->slot_conf[slots[j]] = conf[mem[j]];
@@ -1111,7 +1120,12 @@ RH_EXPORT int rh_push_deltas(rh_groups* g, const rh_delta* deltas, size_t n) {
     size_t done = 0;
     auto validate = [&](size_t lo, size_t hi) -> int {
         uint32_t last = kNoRow, m = kNoRow, w = 0;
+        constexpr size_t kAhead = 16;   // the slot map's lines requested ahead (random slots: ~L3 latency each)
+        for (size_t i = lo; i < std::min(hi, lo + kAhead); ++i)
+            if (deltas[i].slot < g->capacity) __builtin_prefetch(&g->slot_map[deltas[i].slot]);
         for (size_t i = lo; i < hi; ++i) {
+            if (i + kAhead < hi && deltas[i + kAhead].slot < g->capacity)
+                __builtin_prefetch(&g->slot_map[deltas[i + kAhead].slot]);
             const rh_delta& d = deltas[i];
             if (d.slot != last || i == lo) {
                 last = d.slot;
@@ -1131,17 +1145,19 @@ RH_EXPORT int rh_push_deltas(rh_groups* g, const rh_delta* deltas, size_t n) {
     };
     // The whole call is checked first: a rejected call stages nothing.  A call longer than the open
     // slot's room is staged chunk by chunk, and between two chunks the exclusive side below runs
-    // (and so may a control call): the next chunk is checked again against the slot map it finds.
-    bool recheck = false, validated = false;
+    // (and so may a control call): if the slot map changed meanwhile (map_gen), the deltas not staged
+    // yet are checked again against the map they will be applied with.
+    bool validated = false;
+    uint64_t gen = 0;   // the slot map the remaining deltas were checked against
     while (done < n) {
         {
             std::shared_lock<std::shared_mutex> sl(g->smu);   // the slot map changes only under exclusive
             if (g->ring_acquired >= 0) return rh::fail(RH_E_STATE, "rh_push_deltas: a staging slot is acquired");
-            if (!validated || recheck) {
-                const int rc = validate(done, validated ? std::min<size_t>(n, done + RH_DELTA_SLOT) : n);
+            if (!validated || gen != g->map_gen) {   // first, or a control call changed the map meanwhile
+                const int rc = validate(done, n);   // everything not staged yet, against this map
                 if (rc != RH_OK) return rc;
                 validated = true;
-                recheck = false;
+                gen = g->map_gen;
             }
             if (g->open >= 0) {
                 uint64_t r = g->fill.load(std::memory_order_relaxed), take = 0;
@@ -1160,7 +1176,6 @@ RH_EXPORT int rh_push_deltas(rh_groups* g, const rh_delta* deltas, size_t n) {
                 }
             }
         }
-        recheck = true;   // the staging lock is left below: the next chunk is checked again
         // no open slot, or it is full: submit it and open the next one -- waiting for the next slot's
         // previous H2D / in-place apply with both locks released (no producer blocks the
         // others, nor the _async / _wait callers, on device work)
@@ -1171,14 +1186,16 @@ RH_EXPORT int rh_push_deltas(rh_groups* g, const rh_delta* deltas, size_t n) {
             int rc = stage_submit(g);
             if (rc != RH_OK) return rc;
             const int i = g->ring_next;
-            if (g->ring_used[i] && hipEventQuery(g->ring_free[i]) == hipErrorNotReady) {
-                rc = wait_unlocked(ex, g->ring_free[i]);
-                if (rc != RH_OK) return rc;
-                continue;   // re-checked from the top (another producer may have opened a slot)
+            if (g->ring_used[i]) {
+                const hipError_t q = hipEventQuery(g->ring_free[i]);
+                if (q == hipErrorNotReady) {
+                    (void)hipGetLastError();
+                    rc = wait_unlocked(ex, g->ring_free[i]);
+                    if (rc != RH_OK) return rc;
+                    continue;   // re-checked from the top (another producer may have opened a slot)
+                }
+                if (q != hipSuccess) return rh::hip_fail(q, "rh_push_deltas: staging slot");   // a device fault
             }
-            (void)hipGetLastError();
-            rc = ring_wait(g, i);   // complete (or never used): returns at once, reports a fault
-            if (rc != RH_OK) return rc;
             g->open = i;
             g->fill.store(0, std::memory_order_relaxed);
         }
@@ -1238,11 +1255,14 @@ int claim_set(rh_groups* g, Exclusive& ex, EvSet& e) {
     return RH_OK;
 }
 
+// The event the outstanding commitIndexChanged list completes with.
+hipEvent_t watch_done(rh_groups* g) { return g->wtick ? g->ev[g->wtick % kEvSets].done : g->wdone; }
+
 // The same for the commitIndexChanged list.
 int claim_watch(rh_groups* g, Exclusive& ex) {
     while (g->wpending) {   // the previous list is about to be rewritten: wait for it, unlocked
         const uint64_t was = g->wgen;
-        int rc = wait_unlocked(ex, g->wdone);
+        int rc = wait_unlocked(ex, watch_done(g));
         if (rc != RH_OK) return rc;
         if (g->wpending && g->wgen == was) g->wpending = false;
     }
@@ -1322,6 +1342,7 @@ RH_EXPORT int rh_commit_batch_wait(rh_groups* g, uint64_t ticket, rh_commit_out*
     RH_HIP(hipEventSynchronize(done));
     std::unique_lock<std::mutex> lk(g->mu);
     if (e->ticket != ticket) return rh::fail(RH_E_STATE, "rh_commit_batch_wait: ticket superseded while waiting");
+    if (g->wpending && g->wtick == ticket) g->wseen = true;   // a fused tick's watch list is complete too
     uint64_t na = std::min<uint64_t>(e->h_cnt[0], g->capacity);
     uint64_t nw = std::min<uint64_t>(e->h_cnt[1], g->capacity);
     if (e->hbm) {  // lists in HBM (DEVICE sink): into the pinned result buffers
@@ -1391,6 +1412,8 @@ int watch_issue(rh_groups* g) {
         if (g->timing) RH_HIP(hipEventRecord(g->tev[3], g->ctx->stream));
     }
     g->whbm = hbm;
+    g->wtick = 0;
+    g->wseen = false;
     ++g->wgen;
     g->wpending = true;
     return RH_OK;
@@ -1439,8 +1462,7 @@ int tick_issue(rh_groups* g, uint32_t flags, uint64_t tk, EvSet& e) {
         g->timed = true;
         RH_HIP(hipEventRecord(g->tev[3], s));
     }
-    RH_HIP(hipEventRecord(e.done, s));
-    RH_HIP(hipEventRecord(g->wdone, s));
+    RH_HIP(hipEventRecord(e.done, s));   // both lists complete with it (watch_done)
     for (int m = 0; m < 2; ++m) {   // both kinds' lists consumed; the next marks go to the fresh sets
         g->lpar[m] ^= 1;
         g->lmarks[m] = 0;
@@ -1454,6 +1476,8 @@ int tick_issue(rh_groups* g, uint32_t flags, uint64_t tk, EvSet& e) {
     e.pending = true;
     g->wnblocks = 0;
     g->whbm = false;
+    g->wtick = tk;
+    g->wseen = false;
     ++g->wgen;
     g->wpending = true;
     return RH_OK;
@@ -1492,17 +1516,19 @@ RH_EXPORT int rh_watch_levels_wait(rh_groups* g, const rh_watch_event** out_even
     std::unique_lock<std::mutex> lk(g->mu);
     if (!g->wpending) return rh::fail(RH_E_STATE, "rh_watch_levels_wait: no watch evaluation in flight");
     const uint64_t gen = g->wgen;
-    hipEvent_t done = g->wdone;
-    lk.unlock();   // no table lock across a device wait
-    RH_HIP(hipEventSynchronize(done));
-    lk.lock();
-    if (!g->wpending || g->wgen != gen) return rh::fail(RH_E_STATE, "rh_watch_levels_wait: superseded while waiting");
+    if (!g->wseen) {   // (a fused tick's commit wait may have seen it complete already)
+        hipEvent_t done = watch_done(g);
+        lk.unlock();   // no table lock across a device wait
+        RH_HIP(hipEventSynchronize(done));
+        lk.lock();
+        if (!g->wpending || g->wgen != gen) return rh::fail(RH_E_STATE, "rh_watch_levels_wait: superseded while waiting");
+    }
     uint64_t n = std::min<uint64_t>(g->h_wcnt[0], g->capacity);
     if (g->whbm && n) {   // DEVICE sink, contiguous HBM list (REGION mode was gathered at _async)
         g->whbm = false;
         RH_HIP(hipMemcpyAsync(g->watch, g->hbm_watch, n * sizeof(rh_watch_event), hipMemcpyDeviceToHost, g->d2h_stream));
         RH_HIP(hipEventRecord(g->wdone, g->d2h_stream));
-        done = g->wdone;
+        hipEvent_t done = g->wdone;
         lk.unlock();
         RH_HIP(hipEventSynchronize(done));
         lk.lock();

@@ -40,7 +40,7 @@ from typing import List, Optional, Sequence, Tuple
 import numpy as np
 
 from . import _lib
-from ._lib import RhCommitOut, RhDelta, check
+from ._lib import RhCommitOut, check
 
 DELTA_DTYPE = np.dtype([("slot", "<u4"), ("column", "u1"), ("op", "u1"), ("reserved", "<u2"), ("value", "<i8")])
 INDEX_EVENT_DTYPE = np.dtype([("slot", "<u4"), ("reserved", "<u4"), ("value", "<i8")])
@@ -77,6 +77,16 @@ def _src_array(src: Optional[Sequence[int]]):
     s = np.asarray(src, dtype=np.int64)
     a[: s.size] = s
     return a
+
+
+def _addr(a: np.ndarray):
+    """The array's address for a ``void*`` argument: a ctypes reference to its buffer (a pump tick's
+    push is a few microseconds; ``ndarray.ctypes.data_as`` alone costs 2-4 of them), or, for a
+    read-only or empty array, ``ndarray.ctypes.data``."""
+    try:
+        return ctypes.byref(ctypes.c_char.from_buffer(a))
+    except (TypeError, ValueError):
+        return a.ctypes.data
 
 
 class CommitResult:
@@ -179,7 +189,7 @@ class RaftGroupTable:
     # -- delta producers --------------------------------------------------------------------
     def push(self, deltas: np.ndarray) -> None:
         deltas = np.ascontiguousarray(deltas, dtype=DELTA_DTYPE)
-        check(self._lib.rh_push_deltas(self.handle, deltas.ctypes.data_as(ctypes.POINTER(RhDelta)), deltas.size))
+        check(self._lib.rh_push_deltas(self.handle, _addr(deltas), deltas.size))
 
     def push_deltas(self, slots, columns, values, ops=_lib.RH_OP_MAX) -> None:
         self.push(make_deltas(slots, columns, values, ops))
@@ -398,7 +408,7 @@ class RaftNode:
 
     def push(self, deltas: np.ndarray) -> None:
         deltas = np.ascontiguousarray(deltas, dtype=DELTA_DTYPE)
-        check(self._lib.rh_node_push_deltas(self._h, deltas.ctypes.data_as(ctypes.POINTER(RhDelta)), deltas.size))
+        check(self._lib.rh_node_push_deltas(self._h, _addr(deltas), deltas.size))
 
     def update_commit(self, cap: int) -> Tuple[np.ndarray, np.ndarray]:
         """All shards' updateCommit events: (advanced, watch_all) structured arrays, node slots."""
