@@ -123,6 +123,11 @@ struct rh_groups {
     hipEvent_t ring_free[2] = {nullptr, nullptr};   // H2D of the slot done (host slot reusable)
     hipEvent_t ring_read[2] = {nullptr, nullptr};   // apply of the slot done (device slot reusable)
     bool ring_used[2] = {false, false};
+    // the host slot is free again when ring_done[i] completes: ring_free[i], or -- after an in-place
+    // apply, which records no event of its own (an event record is ~4.6 us on the stream's timeline) --
+    // the done event of the next evaluation issued behind it (ring_lazy[i] until then)
+    hipEvent_t ring_done[2] = {nullptr, nullptr};
+    bool ring_lazy[2] = {false, false};
     int ring_next = 0;
     int ring_acquired = -1;
     int open = -1;                            // host slot open for rh_push_deltas (-1: none)
@@ -584,9 +589,35 @@ int do_stop(rh_groups* g, uint32_t slot) {
     return RH_OK;
 }
 
-int ring_wait(rh_groups* g, int i) {
-    if (g->ring_used[i]) RH_HIP(hipEventSynchronize(g->ring_free[i]));
+// The event whose completion frees host slot i (nullptr: never used).  A slot applied in place with
+// no evaluation issued since gets ring_free[i] recorded now, behind that apply.
+int slot_event(rh_groups* g, int i, hipEvent_t* ev) {
+    *ev = nullptr;
+    if (!g->ring_used[i]) return RH_OK;
+    if (g->ring_lazy[i]) {
+        RH_HIP(hipEventRecord(g->ring_free[i], g->ctx->stream));
+        g->ring_done[i] = g->ring_free[i];
+        g->ring_lazy[i] = false;
+    }
+    *ev = g->ring_done[i];
     return RH_OK;
+}
+
+// An evaluation's done event `ev`, recorded behind every apply enqueued so far, frees the slots applied
+// in place (any later re-record of `ev` completes later still).
+void slots_freed_by(rh_groups* g, hipEvent_t ev) {
+    for (int i = 0; i < 2; ++i)
+        if (g->ring_lazy[i]) {
+            g->ring_done[i] = ev;
+            g->ring_lazy[i] = false;
+        }
+}
+
+int ring_wait(rh_groups* g, int i) {
+    hipEvent_t ev = nullptr;
+    int rc = slot_event(g, i, &ev);
+    if (rc == RH_OK && ev) RH_HIP(hipEventSynchronize(ev));
+    return rc;
 }
 
 // H2D of the first n deltas of ring slot i on the copy stream (after the previous apply that read
@@ -631,8 +662,14 @@ int ring_submit(rh_groups* g, int i, size_t n, bool has_set) {
     }
     rc = rh_table_apply_deltas(g->dev, src, n, kApplyMax, gen, lc, lw, s);
     if (rc != RH_OK) return rc;
-    RH_HIP(hipEventRecord(g->ring_read[i], s));
-    if (zc) RH_HIP(hipEventRecord(g->ring_free[i], s));   // the host slot was read by the apply itself
+    if (zc) {   // the host slot was read by the apply itself: freed by the next evaluation's event
+        g->ring_lazy[i] = true;   // (the device slot was not read: ring_read[i] stays the last DMA apply's)
+        g->ring_done[i] = nullptr;
+    } else {
+        RH_HIP(hipEventRecord(g->ring_read[i], s));
+        g->ring_lazy[i] = false;
+        g->ring_done[i] = g->ring_free[i];
+    }
     return RH_OK;
 }
 
@@ -1186,11 +1223,14 @@ RH_EXPORT int rh_push_deltas(rh_groups* g, const rh_delta* deltas, size_t n) {
             int rc = stage_submit(g);
             if (rc != RH_OK) return rc;
             const int i = g->ring_next;
-            if (g->ring_used[i]) {
-                const hipError_t q = hipEventQuery(g->ring_free[i]);
+            hipEvent_t fe = nullptr;
+            rc = slot_event(g, i, &fe);
+            if (rc != RH_OK) return rc;
+            if (fe) {
+                const hipError_t q = hipEventQuery(fe);
                 if (q == hipErrorNotReady) {
                     (void)hipGetLastError();
-                    rc = wait_unlocked(ex, g->ring_free[i]);
+                    rc = wait_unlocked(ex, fe);
                     if (rc != RH_OK) return rc;
                     continue;   // re-checked from the top (another producer may have opened a slot)
                 }
@@ -1306,6 +1346,7 @@ int commit_issue(rh_groups* g, uint32_t flags, uint64_t tk, EvSet& e) {
         RH_HIP(hipEventRecord(e.done, g->ctx->stream));
         if (g->timing) RH_HIP(hipEventRecord(g->tev[3], g->ctx->stream));   // (DEVICE sink: _wait's copy not included)
     }
+    slots_freed_by(g, e.done);
     e.ticket = tk;
     e.hbm = hbm;
     e.pending = true;
@@ -1411,6 +1452,7 @@ int watch_issue(rh_groups* g) {
         RH_HIP(hipEventRecord(g->wdone, g->ctx->stream));
         if (g->timing) RH_HIP(hipEventRecord(g->tev[3], g->ctx->stream));
     }
+    slots_freed_by(g, g->wdone);
     g->whbm = hbm;
     g->wtick = 0;
     g->wseen = false;
@@ -1463,6 +1505,7 @@ int tick_issue(rh_groups* g, uint32_t flags, uint64_t tk, EvSet& e) {
         RH_HIP(hipEventRecord(g->tev[3], s));
     }
     RH_HIP(hipEventRecord(e.done, s));   // both lists complete with it (watch_done)
+    slots_freed_by(g, e.done);
     for (int m = 0; m < 2; ++m) {   // both kinds' lists consumed; the next marks go to the fresh sets
         g->lpar[m] ^= 1;
         g->lmarks[m] = 0;
