@@ -1017,6 +1017,65 @@ __device__ __forceinline__ bool claim_flag(uint8_t* f) {
     return ((atomicAnd(w, ~(0xFFu << sh)) >> sh) & 0xFFu) != 0u;
 }
 
+// A commit-list row of the tick: every load of both evaluations and the claim of its watch flag
+// issued together, then updateCommit (list_row<F, false>'s arithmetic), then -- claimed, or its
+// commit advanced -- commitIndexChanged from the same registers with the new commit index as the
+// self value (list_row<F, true>'s), so the second evaluation costs no second trip to the row.
+template <int F>
+__device__ __forceinline__ void tick_row(const TableDev& T, const TableTier& tt, uint32_t r, bool wall_on, bool& e0,
+                                         bool& e1, int64_t& x0, int64_t& x1, bool& ew, int64_t& y0, int64_t& y1,
+                                         int64_t& y2, uint32_t& wvalid, uint32_t& slot) {
+    int64_t m[F + 1], c[F + 1];
+    const uint32_t w = *tt.u32(tile::kConf, r);
+    slot = *tt.u32(tile::kSlot, r);
+    const int64_t cm = *tt.i64(tile::commit(F), r);
+#pragma unroll
+    for (int k = 0; k < F; ++k) {
+        m[k] = *tt.i64(tile::match(k), r);
+        c[k] = *tt.i64(tile::fcommit(F, k), r);
+    }
+    const int64_t self = *tt.i64(tile::flush(F), r), ts = *tt.i64(tile::tstart(F), r);
+    const int64_t p0 = wall_on ? *tt.i64(tile::wall(F), r) : 0;
+    const int64_t q0 = *tt.i64(tile::wmin(F), r), q1 = *tt.i64(tile::wmaj(F), r), q2 = *tt.i64(tile::wmax(F), r);
+    const bool claimed = claim_flag(tt.u8(tile::kWdirty, r));
+    const bool trans = (w & RH_CONF_ACTIVE) && (w & RH_CONF_TRANSITIONAL);
+    bool v;
+    int64_t mn, mj, mx, nc;
+    m[F] = self;
+    rh_eval::eval_group<F, (F <= 6)>(m, w, T.gap, trans, v, mn, mj, mx);
+    e0 = rh_eval::commit_decision(v, mj, cm, self, ts, nc);
+    e1 = wall_on && mn != p0;  // watch-ALL level changed (LSI:1025)
+    x0 = nc, x1 = mn;
+    if (e0) *tt.i64(tile::commit(F), r) = nc;
+    if (e1) *tt.i64(tile::wall(F), r) = mn;
+    if (claimed || e0) {   // commitIndexChanged: lastCommittedIndex (now nc if it advanced) is the self value (LSI:613)
+        c[F] = e0 ? nc : cm;
+        rh_eval::eval_group<F, (F <= 6)>(c, w, -1, trans, v, mn, mj, mx);
+        wvalid = v ? 1u : 0u;
+        ew = mn != q0 || mj != q1 || mx != q2;
+        y0 = mn, y1 = mj, y2 = mx;
+        if (ew) {
+            *tt.i64(tile::wmin(F), r) = mn;
+            *tt.i64(tile::wmaj(F), r) = mj;
+            *tt.i64(tile::wmax(F), r) = mx;
+        }
+    }
+}
+
+__device__ __forceinline__ void tick_row_any(const TableDev& T, const TableTier& tt, uint32_t r, bool wall_on, bool& e0,
+                                             bool& e1, int64_t& x0, int64_t& x1, bool& ew, int64_t& y0, int64_t& y1,
+                                             int64_t& y2, uint32_t& wvalid, uint32_t& slot) {
+    switch (tt.width) {
+        case 2: tick_row<2>(T, tt, r, wall_on, e0, e1, x0, x1, ew, y0, y1, y2, wvalid, slot); break;
+        case 4: tick_row<4>(T, tt, r, wall_on, e0, e1, x0, x1, ew, y0, y1, y2, wvalid, slot); break;
+        case 6: tick_row<6>(T, tt, r, wall_on, e0, e1, x0, x1, ew, y0, y1, y2, wvalid, slot); break;
+        case 8: tick_row<8>(T, tt, r, wall_on, e0, e1, x0, x1, ew, y0, y1, y2, wvalid, slot); break;
+        case 10: tick_row<10>(T, tt, r, wall_on, e0, e1, x0, x1, ew, y0, y1, y2, wvalid, slot); break;
+        case 12: tick_row<12>(T, tt, r, wall_on, e0, e1, x0, x1, ew, y0, y1, y2, wvalid, slot); break;
+        default: tick_row<14>(T, tt, r, wall_on, e0, e1, x0, x1, ew, y0, y1, y2, wvalid, slot); break;
+    }
+}
+
 // Byte `f` as the device's coherence point holds it (a returning atomic that changes nothing).
 __device__ __forceinline__ uint8_t fetch_flag(uint8_t* f) {
     uint32_t* w = reinterpret_cast<uint32_t*>(reinterpret_cast<uintptr_t>(f) & ~(uintptr_t)3);
@@ -1094,15 +1153,10 @@ __global__ __launch_bounds__(kListWaves * 64) void table_tick_kernel(TableDev Ta
             const uint32_t t = ent >> 28, row = ent & rh::kRowMask;
             const TableTier tt = tiers[t < (uint32_t)rh::kTableTiers ? t : 0u];
             if (row < tt.rows) {
-                const bool claimed = claim_flag(tt.u8(tile::kWdirty, row));
-                list_row_any<false>(T, tt, row, wall_on, e0, e1, x0, x1, x2, valid, slot);
+                tick_row_any(T, tt, row, wall_on, e0, e1, x0, x1, ew, y0, y1, y2, wvalid, slot);
                 // the claim performed (returned) before the updateCommit flag clears: the watch side reads it
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 (void)claim_flag(tt.u8(tile::kDirty, row));
-                if (claimed || e0) {   // e0: the commit advanced
-                    bool dummy = false;
-                    list_row_any<true>(T, tt, row, false, ew, dummy, y0, y1, y2, wvalid, slot);
-                }
             }
         }
         // the watch list's row, if no updateCommit lane holds it: its updateCommit flag clear (an

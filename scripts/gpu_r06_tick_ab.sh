@@ -1,5 +1,5 @@
-# Round 6 A/B: the fused tick's result-set event completed by the launch itself (default) vs recorded
-# after it (rec: RH_TICK_STOP_EVENT=0), tick_breakdown.py twice each, alternating.
+# Round 6 A/B of the tick (RATIS_HIP_LIB: default vs ratis_amd/lib/ab/libratis_hip_rec.so, the build under test), e.g. the result-set event completed by the launch itself vs recorded
+# after it (rec: RH_TICK_STOP_EVENT=0); tick_breakdown.py twice each, alternating.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 O=$R/gpurun_out/${1:-r06tickab}
