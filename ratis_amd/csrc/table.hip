@@ -710,9 +710,7 @@ __global__ __launch_bounds__(kTBlock) void table_commit_kernel_net(TableDev Targ
 // workgroup (its waves' counts summed in LDS), records written straight into the result lists;
 // the last pass's atomic also counts the workgroup done (the counter word's top bits), so the
 // workgroup that completes the count knows the list lengths from its own atomic's return.
-// TICK (the fused tick kernel): neither flag is stored -- the caller claims the row's commitIndexChanged
-// and clears its updateCommit flag with atomics (table_tick_kernel).
-template <int F, bool WATCH, bool TICK = false>
+template <int F, bool WATCH>
 __device__ __forceinline__ void list_row(const TableDev& T, const TableTier& tt, uint32_t r, bool wall_on,
                                          bool wlisted, bool& e0, bool& e1, bool& wtrans, int64_t& x0, int64_t& x1,
                                          int64_t& x2, uint32_t& valid, uint32_t& slot, bool need_slot) {
@@ -732,7 +730,7 @@ __device__ __forceinline__ void list_row(const TableDev& T, const TableTier& tt,
 #if RH_TABLE_ABL == 7
     const uint8_t wd = 0;
 #else
-    const uint8_t wd = (WATCH || TICK) ? 0 : *tt.u8(tile::kWdirty, r);
+    const uint8_t wd = WATCH ? 0 : *tt.u8(tile::kWdirty, r);
 #endif
     int64_t self, ts = 0, p0 = 0, p1 = 0, p2 = 0;
     if (WATCH) {
@@ -763,22 +761,21 @@ __device__ __forceinline__ void list_row(const TableDev& T, const TableTier& tt,
             *tt.i64(tile::wmaj(F), r) = mj;
             *tt.i64(tile::wmax(F), r) = mx;
         }
-        if (!TICK) *tt.u8(tile::kWdirty, r) = 0;
+        *tt.u8(tile::kWdirty, r) = 0;
     } else {
         int64_t nc;
         e0 = rh_eval::commit_decision(v, mj, cm, self, ts, nc);
         e1 = wall_on && mn != p0;  // watch-ALL level changed (LSI:1025)
         x0 = nc, x1 = mn, x2 = 0;
 #if RH_TABLE_ABL != 7
-        if (!TICK) *tt.u8(tile::kDirty, r) = 0;
+        *tt.u8(tile::kDirty, r) = 0;
 #endif
         if (e0) {
             *tt.i64(tile::commit(F), r) = nc;
-            if (!TICK) {   // the commit index changed: commitIndexChanged follows (listed if the flag was clear)
-                *tt.u8(tile::kWdirty, r) = 1;
-                *tt.summary(r, 1) = 1;
-                wtrans = wlisted && wd == 0;
-            }
+            // the commit index changed: commitIndexChanged follows (listed if the flag was clear)
+            *tt.u8(tile::kWdirty, r) = 1;
+            *tt.summary(r, 1) = 1;
+            wtrans = wlisted && wd == 0;
         }
         if (e1) *tt.i64(tile::wall(F), r) = mn;
     }
@@ -981,34 +978,19 @@ __global__ __launch_bounds__(kListWaves * 64) void table_list_kernel(TableDev Ta
 // updateCommit over the commit list, then commitIndexChanged of every row whose levels may have moved
 // -- the watch list's rows (a follower commitIndex delta) and the rows whose commit advanced -- in the
 // same launch: a row's commitIndexChanged reads only that row (its followers' commitIndex, its new
-// commit index, its levels), so the lane that evaluated its updateCommit evaluates it right after
-// (LeaderStateImpl.java:946-950, then 612-622, per division); the watch list's other rows are
-// evaluated by the lanes holding their entries, in the same passes (a lane takes one entry of each
-// list per pass: both rows' loads and atomics in flight together).  Each row's commitIndexChanged runs
-// exactly once, after its updateCommit.  The two flags are touched only by atomics here (performed at
-// the device's coherence point: no fence, no cross-XCD staleness): a commit-list lane claims the row
-// by clearing its watch flag (or by its commit having advanced), waits for that atomic to return,
-// then clears the row's updateCommit flag; a watch-list lane reads the updateCommit flag with an
-// atomic and claims only a row whose flag it finds clear -- so a commit-list lane has claimed it
-// already (the claim fails) or the row is not in the commit list (the claim succeeds once).  A
-// watch-list lane evaluates only rows whose commit index this launch does not write.  Records go
-// straight into the pinned lists (one counter atomic per list kind per workgroup and pass); the last
-// workgroup to finish publishes both lists' lengths and zeroes the counters.
-template <bool WATCH>
-__device__ __forceinline__ void list_row_any(const TableDev& T, const TableTier& tt, uint32_t row, bool wall_on, bool& e0,
-                                             bool& e1, int64_t& x0, int64_t& x1, int64_t& x2, uint32_t& valid,
-                                             uint32_t& slot) {
-    bool wt = false;
-    switch (tt.width) {
-        case 2: list_row<2, WATCH, true>(T, tt, row, wall_on, false, e0, e1, wt, x0, x1, x2, valid, slot, true); break;
-        case 4: list_row<4, WATCH, true>(T, tt, row, wall_on, false, e0, e1, wt, x0, x1, x2, valid, slot, true); break;
-        case 6: list_row<6, WATCH, true>(T, tt, row, wall_on, false, e0, e1, wt, x0, x1, x2, valid, slot, true); break;
-        case 8: list_row<8, WATCH, true>(T, tt, row, wall_on, false, e0, e1, wt, x0, x1, x2, valid, slot, true); break;
-        case 10: list_row<10, WATCH, true>(T, tt, row, wall_on, false, e0, e1, wt, x0, x1, x2, valid, slot, true); break;
-        case 12: list_row<12, WATCH, true>(T, tt, row, wall_on, false, e0, e1, wt, x0, x1, x2, valid, slot, true); break;
-        default: list_row<14, WATCH, true>(T, tt, row, wall_on, false, e0, e1, wt, x0, x1, x2, valid, slot, true); break;
-    }
-}
+// commit index, its levels), so the lane that evaluated its updateCommit evaluates it right after,
+// from the same load batch (LeaderStateImpl.java:946-950, then 612-622, per division).  A wave serves
+// one list: the commit list's waves and the watch list's run side by side.  Each row's
+// commitIndexChanged runs exactly once, after its updateCommit.  The two flags are touched only by
+// atomics here (performed at the device's coherence point: no fence, no cross-XCD staleness): a
+// commit-list lane claims the row by clearing its watch flag (or by its commit having advanced), waits
+// for that atomic to return, then clears the row's updateCommit flag; a watch-list lane reads the
+// updateCommit flag with an atomic and claims only a row whose flag it finds clear -- so a commit-list
+// lane has claimed it already (the claim fails) or the row is not in the commit list (the claim
+// succeeds once).  A watch-list lane evaluates only rows whose commit index this launch does not write
+// (its loads go out with the flag fetch and are used only then).  Records go straight into the pinned
+// lists (one counter atomic per list kind per workgroup and pass); the last workgroup to finish
+// publishes both lists' lengths and zeroes the counters.
 
 // Clears byte `f` of its 32-bit word with one atomic; whether it was set.
 __device__ __forceinline__ bool claim_flag(uint8_t* f) {
@@ -1017,14 +999,21 @@ __device__ __forceinline__ bool claim_flag(uint8_t* f) {
     return ((atomicAnd(w, ~(0xFFu << sh)) >> sh) & 0xFFu) != 0u;
 }
 
+// Byte `f` as the device's coherence point holds it (a returning atomic that changes nothing).
+__device__ __forceinline__ uint8_t fetch_flag(uint8_t* f) {
+    uint32_t* w = reinterpret_cast<uint32_t*>(reinterpret_cast<uintptr_t>(f) & ~(uintptr_t)3);
+    const uint32_t sh = 8u * (uint32_t)(reinterpret_cast<uintptr_t>(f) & 3);
+    return (uint8_t)(atomicOr(w, 0u) >> sh);
+}
+
 // A commit-list row of the tick: every load of both evaluations and the claim of its watch flag
 // issued together, then updateCommit (list_row<F, false>'s arithmetic), then -- claimed, or its
 // commit advanced -- commitIndexChanged from the same registers with the new commit index as the
 // self value (list_row<F, true>'s), so the second evaluation costs no second trip to the row.
 template <int F>
-__device__ __forceinline__ void tick_row(const TableDev& T, const TableTier& tt, uint32_t r, bool wall_on, bool& e0,
-                                         bool& e1, int64_t& x0, int64_t& x1, bool& ew, int64_t& y0, int64_t& y1,
-                                         int64_t& y2, uint32_t& wvalid, uint32_t& slot) {
+__device__ __forceinline__ void tick_row(const TableDev& T, const TableTier& tt, uint32_t r, bool wall_on, bool& claimed,
+                                         bool& e0, bool& e1, int64_t& x0, int64_t& x1, bool& ew, int64_t& y0,
+                                         int64_t& y1, int64_t& y2, uint32_t& wvalid, uint32_t& slot) {
     int64_t m[F + 1], c[F + 1];
     const uint32_t w = *tt.u32(tile::kConf, r);
     slot = *tt.u32(tile::kSlot, r);
@@ -1037,7 +1026,7 @@ __device__ __forceinline__ void tick_row(const TableDev& T, const TableTier& tt,
     const int64_t self = *tt.i64(tile::flush(F), r), ts = *tt.i64(tile::tstart(F), r);
     const int64_t p0 = wall_on ? *tt.i64(tile::wall(F), r) : 0;
     const int64_t q0 = *tt.i64(tile::wmin(F), r), q1 = *tt.i64(tile::wmaj(F), r), q2 = *tt.i64(tile::wmax(F), r);
-    const bool claimed = claim_flag(tt.u8(tile::kWdirty, r));
+    claimed = claim_flag(tt.u8(tile::kWdirty, r));
     const bool trans = (w & RH_CONF_ACTIVE) && (w & RH_CONF_TRANSITIONAL);
     bool v;
     int64_t mn, mj, mx, nc;
@@ -1062,26 +1051,60 @@ __device__ __forceinline__ void tick_row(const TableDev& T, const TableTier& tt,
     }
 }
 
-__device__ __forceinline__ void tick_row_any(const TableDev& T, const TableTier& tt, uint32_t r, bool wall_on, bool& e0,
-                                             bool& e1, int64_t& x0, int64_t& x1, bool& ew, int64_t& y0, int64_t& y1,
-                                             int64_t& y2, uint32_t& wvalid, uint32_t& slot) {
-    switch (tt.width) {
-        case 2: tick_row<2>(T, tt, r, wall_on, e0, e1, x0, x1, ew, y0, y1, y2, wvalid, slot); break;
-        case 4: tick_row<4>(T, tt, r, wall_on, e0, e1, x0, x1, ew, y0, y1, y2, wvalid, slot); break;
-        case 6: tick_row<6>(T, tt, r, wall_on, e0, e1, x0, x1, ew, y0, y1, y2, wvalid, slot); break;
-        case 8: tick_row<8>(T, tt, r, wall_on, e0, e1, x0, x1, ew, y0, y1, y2, wvalid, slot); break;
-        case 10: tick_row<10>(T, tt, r, wall_on, e0, e1, x0, x1, ew, y0, y1, y2, wvalid, slot); break;
-        case 12: tick_row<12>(T, tt, r, wall_on, e0, e1, x0, x1, ew, y0, y1, y2, wvalid, slot); break;
-        default: tick_row<14>(T, tt, r, wall_on, e0, e1, x0, x1, ew, y0, y1, y2, wvalid, slot); break;
+// A watch-list row of the tick: its loads issued with the atomic fetch of its updateCommit flag, then
+// -- the flag clear and the watch flag claimed -- commitIndexChanged (list_row<F, true>'s arithmetic).
+template <int F>
+__device__ __forceinline__ void tick_watch_row(const TableTier& tt, uint32_t r, bool& ew, int64_t& y0, int64_t& y1,
+                                               int64_t& y2, uint32_t& wvalid, uint32_t& slot) {
+    int64_t c[F + 1];
+    const uint32_t w = *tt.u32(tile::kConf, r);
+    slot = *tt.u32(tile::kSlot, r);
+    c[F] = *tt.i64(tile::commit(F), r);   // lastCommittedIndex is the self value (LSI:613)
+#pragma unroll
+    for (int k = 0; k < F; ++k) c[k] = *tt.i64(tile::fcommit(F, k), r);
+    const int64_t q0 = *tt.i64(tile::wmin(F), r), q1 = *tt.i64(tile::wmaj(F), r), q2 = *tt.i64(tile::wmax(F), r);
+    if (fetch_flag(tt.u8(tile::kDirty, r)) != 0 || !claim_flag(tt.u8(tile::kWdirty, r))) return;
+    const bool trans = (w & RH_CONF_ACTIVE) && (w & RH_CONF_TRANSITIONAL);
+    bool v;
+    int64_t mn, mj, mx;
+    rh_eval::eval_group<F, (F <= 6)>(c, w, -1, trans, v, mn, mj, mx);
+    wvalid = v ? 1u : 0u;
+    ew = mn != q0 || mj != q1 || mx != q2;
+    y0 = mn, y1 = mj, y2 = mx;
+    if (ew) {
+        *tt.i64(tile::wmin(F), r) = mn;
+        *tt.i64(tile::wmaj(F), r) = mj;
+        *tt.i64(tile::wmax(F), r) = mx;
     }
 }
 
-// Byte `f` as the device's coherence point holds it (a returning atomic that changes nothing).
-__device__ __forceinline__ uint8_t fetch_flag(uint8_t* f) {
-    uint32_t* w = reinterpret_cast<uint32_t*>(reinterpret_cast<uintptr_t>(f) & ~(uintptr_t)3);
-    const uint32_t sh = 8u * (uint32_t)(reinterpret_cast<uintptr_t>(f) & 3);
-    return (uint8_t)(atomicOr(w, 0u) >> sh);
+__device__ __forceinline__ void tick_watch_row_any(const TableTier& tt, uint32_t r, bool& ew, int64_t& y0, int64_t& y1,
+                                                   int64_t& y2, uint32_t& wvalid, uint32_t& slot) {
+    switch (tt.width) {
+        case 2: tick_watch_row<2>(tt, r, ew, y0, y1, y2, wvalid, slot); break;
+        case 4: tick_watch_row<4>(tt, r, ew, y0, y1, y2, wvalid, slot); break;
+        case 6: tick_watch_row<6>(tt, r, ew, y0, y1, y2, wvalid, slot); break;
+        case 8: tick_watch_row<8>(tt, r, ew, y0, y1, y2, wvalid, slot); break;
+        case 10: tick_watch_row<10>(tt, r, ew, y0, y1, y2, wvalid, slot); break;
+        case 12: tick_watch_row<12>(tt, r, ew, y0, y1, y2, wvalid, slot); break;
+        default: tick_watch_row<14>(tt, r, ew, y0, y1, y2, wvalid, slot); break;
+    }
 }
+
+__device__ __forceinline__ void tick_row_any(const TableDev& T, const TableTier& tt, uint32_t r, bool wall_on,
+                                             bool& claimed, bool& e0, bool& e1, int64_t& x0, int64_t& x1, bool& ew,
+                                             int64_t& y0, int64_t& y1, int64_t& y2, uint32_t& wvalid, uint32_t& slot) {
+    switch (tt.width) {
+        case 2: tick_row<2>(T, tt, r, wall_on, claimed, e0, e1, x0, x1, ew, y0, y1, y2, wvalid, slot); break;
+        case 4: tick_row<4>(T, tt, r, wall_on, claimed, e0, e1, x0, x1, ew, y0, y1, y2, wvalid, slot); break;
+        case 6: tick_row<6>(T, tt, r, wall_on, claimed, e0, e1, x0, x1, ew, y0, y1, y2, wvalid, slot); break;
+        case 8: tick_row<8>(T, tt, r, wall_on, claimed, e0, e1, x0, x1, ew, y0, y1, y2, wvalid, slot); break;
+        case 10: tick_row<10>(T, tt, r, wall_on, claimed, e0, e1, x0, x1, ew, y0, y1, y2, wvalid, slot); break;
+        case 12: tick_row<12>(T, tt, r, wall_on, claimed, e0, e1, x0, x1, ew, y0, y1, y2, wvalid, slot); break;
+        default: tick_row<14>(T, tt, r, wall_on, claimed, e0, e1, x0, x1, ew, y0, y1, y2, wvalid, slot); break;
+    }
+}
+
 
 __global__ __launch_bounds__(kListWaves * 64) void table_tick_kernel(TableDev Targ, TableLists Lc, TableLists Lw,
                                                                      rh::TickEvents ev) {
@@ -1096,12 +1119,20 @@ __global__ __launch_bounds__(kListWaves * 64) void table_tick_kernel(TableDev Ta
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const uint32_t W = gridDim.x * kListWaves, wg = blockIdx.x * kListWaves + (uint32_t)wave;
     const uint32_t r = wg % NR, k = wg / NR, Wr = (W - r + NR - 1) / NR;
-    const unsigned long long hc = Lc.heads[(uint64_t)r * rh::kHeadStride], hw = Lw.heads[(uint64_t)r * rh::kHeadStride];
+    // a wave serves one list (wave-uniform: the two row chains run on different waves, side by side):
+    // the region's even ranks its commit list, the odd ranks its watch list (the host's grid gives
+    // every region at least two waves)
+    const uint32_t role = k & 1u, kr = k >> 1, Wrr = role ? Wr / 2 : (Wr + 1) / 2;
+    const TableLists& L = role ? Lw : Lc;
+    const unsigned long long hl = L.heads[(uint64_t)r * rh::kHeadStride];
+    // the first pass's entry loaded with the count (speculatively: below the capacity it is in bounds)
+    const uint32_t i0 = (uint32_t)lane * Wrr + kr;
+    const uint32_t ent0 = i0 < L.cap ? L.rows[(uint64_t)r * L.cap + i0] : 0u;
     uint32_t cl = 0;
     if (wave == 0 && lane < (int)(2 * NR)) {   // lanes 0..7: the commit list's regions, 8..15: the watch list's
-        const TableLists& L = lane < (int)NR ? Lc : Lw;
-        const unsigned long long x = L.heads[(uint64_t)(lane % NR) * rh::kHeadStride];
-        cl = (uint32_t)(x < L.cap ? x : L.cap);
+        const TableLists& Lq = lane < (int)NR ? Lc : Lw;
+        const unsigned long long x = Lq.heads[(uint64_t)(lane % NR) * rh::kHeadStride];
+        cl = (uint32_t)(x < Lq.cap ? x : Lq.cap);
     }
     if (threadIdx.x == 64) {
 #pragma unroll
@@ -1111,12 +1142,13 @@ __global__ __launch_bounds__(kListWaves * 64) void table_tick_kernel(TableDev Ta
         ev.lheads_next_c[(uint64_t)threadIdx.x * rh::kHeadStride] = 0ull;
         ev.lheads_next_w[(uint64_t)threadIdx.x * rh::kHeadStride] = 0ull;
     }
-    const uint32_t cnt_c = (uint32_t)(hc < Lc.cap ? hc : Lc.cap), cnt_w = (uint32_t)(hw < Lw.cap ? hw : Lw.cap);
+    const uint32_t cnt = (uint32_t)(hl < L.cap ? hl : L.cap);
     if (wave == 0) {
         uint32_t np = 0;
         if (lane < (int)(2 * NR)) {
             const uint32_t rr = (uint32_t)lane % NR, wr = (W - rr + NR - 1) / NR;
-            np = (cl + wr * 64u - 1) / (wr * 64u);
+            const uint32_t wrr = lane < (int)NR ? (wr + 1) / 2 : wr / 2;
+            np = (cl + wrr * 64u - 1) / (wrr * 64u);
         }
         const uint32_t npc = wave_max_u32(lane < (int)NR ? np : 0u), npw = wave_max_u32(lane >= (int)NR ? np : 0u);
         if (lane == 0) {
@@ -1129,47 +1161,34 @@ __global__ __launch_bounds__(kListWaves * 64) void table_tick_kernel(TableDev Ta
     const uint64_t lt = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const bool wall_on = ev.wall != nullptr;
     const uint64_t R = ev.cap;
-    // one pass takes a lane's entry of each list: the two rows' loads and atomics in flight together
-    const uint32_t np = np_c > np_w ? np_c : np_w;
+    const uint32_t np = np_c > np_w ? np_c : np_w;   // uniform over the workgroup (its barriers)
     for (uint32_t pass = 0; pass < np; ++pass) {
-        const uint32_t idx = (pass * 64u + (uint32_t)lane) * Wr + k;
-        bool e0 = false, e1 = false, ew = false, ev2 = false;
-        int64_t x0 = 0, x1 = 0, x2 = 0, y0 = 0, y1 = 0, y2 = 0, z0 = 0, z1 = 0, z2 = 0;
-        uint32_t valid = 0, slot = 0, wvalid = 0, slot2 = 0, wvalid2 = 0;
-        // the watch list's entry: its updateCommit flag fetched first (the answer is needed last)
-        TableTier tw{};
-        uint32_t roww = 0;
-        uint8_t dflag = 1;
-        if (idx < cnt_w) {
-            const uint32_t ent = Lw.rows[(uint64_t)r * Lw.cap + idx];
-            const uint32_t t = ent >> 28;
-            roww = ent & rh::kRowMask;
-            tw = tiers[t < (uint32_t)rh::kTableTiers ? t : 0u];
-            if (roww < tw.rows) dflag = fetch_flag(tw.u8(tile::kDirty, roww));
-        }
-        // the commit list's entry: claimed, updateCommit, then (claimed or advanced) commitIndexChanged
-        if (idx < cnt_c) {
-            const uint32_t ent = Lc.rows[(uint64_t)r * Lc.cap + idx];
+        const uint32_t idx = (pass * 64u + (uint32_t)lane) * Wrr + kr;
+        bool e0 = false, e1 = false, ew = false;
+        int64_t x0 = 0, x1 = 0, y0 = 0, y1 = 0, y2 = 0;
+        uint32_t slot = 0, wvalid = 0;
+        if (idx < cnt) {
+            const uint32_t ent = pass == 0 ? ent0 : L.rows[(uint64_t)r * L.cap + idx];
             const uint32_t t = ent >> 28, row = ent & rh::kRowMask;
             const TableTier tt = tiers[t < (uint32_t)rh::kTableTiers ? t : 0u];
             if (row < tt.rows) {
-                tick_row_any(T, tt, row, wall_on, e0, e1, x0, x1, ew, y0, y1, y2, wvalid, slot);
-                // the claim performed (returned) before the updateCommit flag clears: the watch side reads it
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                (void)claim_flag(tt.u8(tile::kDirty, row));
+                if (role == 0) {   // updateCommit, then (watch flag claimed, or advanced) commitIndexChanged
+                    bool claimed = false;
+                    tick_row_any(T, tt, row, wall_on, claimed, e0, e1, x0, x1, ew, y0, y1, y2, wvalid, slot);
+                    // the claim performed (returned: its value in a register) before the updateCommit flag
+                    // clears -- the watch side reads it; no memory access moves across
+                    asm volatile("" ::"v"((uint32_t)claimed) : "memory");
+                    (void)claim_flag(tt.u8(tile::kDirty, row));
+                } else {   // commitIndexChanged, if no commit-list lane holds the row
+                    tick_watch_row_any(tt, row, ew, y0, y1, y2, wvalid, slot);
+                }
             }
         }
-        // the watch list's row, if no updateCommit lane holds it: its updateCommit flag clear (an
-        // updateCommit lane has claimed it already, or it is not in the commit list), then the claim
-        if (dflag == 0 && claim_flag(tw.u8(tile::kWdirty, roww))) {
-            bool dummy = false;
-            list_row_any<true>(T, tw, roww, false, ev2, dummy, z0, z1, z2, wvalid2, slot2);
-        }
-        const uint64_t a = __ballot(e0), c = __ballot(e1), w = __ballot(ew), w2 = __ballot(ev2);
+        const uint64_t a = __ballot(e0), c = __ballot(e1), w = __ballot(ew);
         if (lane == 0) {
             wcnt[0][wave] = (uint32_t)__popcll(a);
             wcnt[1][wave] = (uint32_t)__popcll(c);
-            wcnt[2][wave] = (uint32_t)(__popcll(w) + __popcll(w2));
+            wcnt[2][wave] = (uint32_t)__popcll(w);
         }
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -1194,10 +1213,6 @@ __global__ __launch_bounds__(kListWaves * 64) void table_tick_kernel(TableDev Ta
         if (ew) {
             const uint64_t kk = b2 + (uint64_t)__popcll(w & lt);
             if (kk < R) ev.watch[kk] = rh_watch_event{slot, wvalid, y0, y1, y2};
-        }
-        if (ev2) {
-            const uint64_t kk = b2 + (uint64_t)__popcll(w) + (uint64_t)__popcll(w2 & lt);
-            if (kk < R) ev.watch[kk] = rh_watch_event{slot2, wvalid2, z0, z1, z2};
         }
     }
     // the last workgroup to finish publishes both lists' lengths and zeroes the counters (every other
@@ -1442,7 +1457,8 @@ int rh_table_commit_lists(const rh::TableDev& t, int mode, const rh::TableLists&
 
 int rh_table_tick_lists(const rh::TableDev& t, const rh::TableLists& lc, const rh::TableLists& lw, const rh::TickEvents& ev,
                         hipStream_t stream, hipEvent_t t0, hipEvent_t t1, uint64_t rows_hint) {
-    const dim3 g(rh::table_list_grid(rows_hint)), b(kListWaves * 64);
+    // every region at least two waves: one per list (table_tick_kernel's roles)
+    const dim3 g(std::max<uint32_t>(rh::table_list_grid(rows_hint), 2 * rh::kHeads / kListWaves)), b(kListWaves * 64);
     RH_HIP(eval_launch(table_tick_kernel, g, b, stream, t0, t1, t, lc, lw, ev));
     return RH_OK;
 }
