@@ -243,7 +243,10 @@ def test_zero_copy_ring_pipelined_with_async_commit(ctx, orc):
         live = np.arange(n)
         prev = None
         for step in range(6):
-            d = random_deltas(rng, model, live, int(rng.integers(1000, 60000)), fcommit=False)
+            # both staging paths: up to 65536 deltas the apply reads the pinned slot in place, past it
+            # the slot goes to HBM by DMA on the copy stream first
+            k = int(rng.integers(1000, 60000)) if step % 2 == 0 else int(rng.integers(70_000, 150_000))
+            d = random_deltas(rng, model, live, k, fcommit=False)
             ring = tab.acquire_deltas()
             assert ring.size == _lib.RH_DELTA_SLOT
             ring[: d.size] = d
