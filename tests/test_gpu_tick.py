@@ -212,3 +212,84 @@ def test_tick_ticket_rotation_and_misuse(ctx, orc):
         assert tab._lib.rh_tick_async(tab.handle, 0, None) != 0   # NULL ticket
         tk = ctypes.c_uint64()
         assert tab._lib.rh_tick_async(tab.handle, 8, ctypes.byref(tk)) != 0   # unknown flag
+
+
+def test_tick_with_concurrent_producers(ctx, orc):
+    """4 producer threads push reply deltas (matchIndex, follower commitIndex, flushIndex MAXes) in
+    small calls while the main thread ticks (rh_tick_async + both waits) as fast as it can: no tick
+    reports a slot twice in one list, and after the producers are done and a last tick, every slot's
+    last reported commit index and levels -- and the table's columns -- are the model's for the whole
+    delta set (MAX deltas commute; commit and levels only rise)."""
+    import threading
+    import time
+
+    from ratis_amd import groups, workload
+    rng = np.random.default_rng(808)
+    n = 50_000
+    model = TableModel(n)
+    tiers = workload.commit_snapshot(n, joint_frac=0.1, peers=5, seed=81)
+    tab = None
+    try:
+        tab = groups.RaftGroupTable(ctx, capacity=sum(t.n for t in tiers))
+        first = 0
+        for h in tiers:
+            tab.load(first, h.conf, h.flush, h.commit, h.term_start, match=h.follower)
+            model.load(first, h.conf, h.flush, h.commit, h.term_start, match=h.follower)
+            first += h.n
+        _expect(*_tick(tab), model, orc)
+        live = np.arange(first)
+        T = 4
+        work = []
+        for t in range(T):
+            chunks = []
+            for _ in range(60):
+                k = int(rng.integers(1, 300))
+                d = random_deltas(rng, model, live, k)   # MAX only: match, follower commitIndex, flush
+                chunks.append(d)
+            work.append(chunks)
+        errors = []
+
+        def producer(t):
+            try:
+                for d in work[t]:
+                    tab.push(d)
+                    time.sleep(1e-4)   # replies trickle in across many ticks
+            except Exception as e:  # noqa: BLE001
+                errors.append(e)
+
+        th = [threading.Thread(target=producer, args=(t,)) for t in range(T)]
+        for x in th:
+            x.start()
+        last_commit, last_levels, ticks = {}, {}, 0
+
+        def collect(got, ev):
+            assert np.unique(got.advanced_slots).size == got.advanced_slots.size
+            assert np.unique(ev["slot"]).size == ev.size
+            for s_, v in zip(got.advanced_slots.tolist(), got.advanced_commit.tolist()):
+                last_commit[s_] = v
+            for e in ev:
+                last_levels[int(e["slot"])] = (int(e["min"]), int(e["majority"]), int(e["max"]), bool(e["valid"]))
+
+        while any(x.is_alive() for x in th):
+            collect(*_tick(tab))
+            ticks += 1
+        for x in th:
+            x.join()
+        assert not errors, errors
+        collect(*_tick(tab))
+        for t in range(T):
+            for d in work[t]:
+                model.apply(d)
+        a_s, a_c, _, _ = model.commit_batch(orc)
+        m_s, m_lev, m_valid = model.watch(orc)
+        assert {s_: last_commit[s_] for s_ in a_s.tolist()} == dict(zip(a_s.tolist(), a_c.tolist()))
+        assert set(last_commit) == set(a_s.tolist())
+        want = {int(s_): (int(m_lev[0][i]), int(m_lev[1][i]), int(m_lev[2][i]), bool(m_valid[i]))
+                for i, s_ in enumerate(m_s.tolist())}
+        assert last_levels == want
+        for col in [0, 3, 16, 19, COL_FLUSH, COL_COMMITTED]:
+            assert np.array_equal(tab.read(col), model.column(col)), col
+        assert ticks >= 10 and len(last_commit) > 100 and len(last_levels) > 100, (ticks, len(last_commit))
+    finally:
+        if tab is not None:
+            tab.close()
