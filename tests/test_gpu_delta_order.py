@@ -289,3 +289,26 @@ def test_wait_does_not_block_producers(ctx, orc, what):
     assert np.array_equal(got.watch_all_slots, w_s) and np.array_equal(got.watch_all_min, w_m)
     assert np.array_equal(tab.read(0), model.column(0))
     tab.close()
+
+
+def test_staging_slots_reused_without_evaluations(ctx):
+    """Batches submitted by reads and zero-copy submits with no evaluation in between -- so no
+    evaluation's event frees a slot applied in place, and the next user of the slot must record and
+    wait for one itself (groups.cpp slot_event) -- with sizes on both sides of the in-place bound
+    (65536 deltas: the slot read in place, or first copied to HBM): every cell ends where the
+    one-by-one order puts it."""
+    rng = np.random.default_rng(65536)
+    tab, cells = started_table(ctx, 64)
+    slots = np.arange(64)
+    for i, k in enumerate([100, 3000, 70_000, 500, 65_536, 65_537, 20, 40_000, 7, 1]):
+        d = random_batch(rng, slots, k)
+        if i % 3 == 2:   # a producer-filled slot (rh_deltas_acquire / submit)
+            ring = tab.acquire_deltas()
+            ring[: d.size] = d
+            tab.submit_deltas(d.size)
+        else:
+            tab.push(d)
+            tab.read(0)   # submits the staged batch: no evaluation
+        cells.apply(d)
+    check(tab, cells, slots)
+    tab.close()
