@@ -128,6 +128,9 @@ struct rh_groups {
     // the done event of the next evaluation issued behind it (ring_lazy[i] until then)
     hipEvent_t ring_done[2] = {nullptr, nullptr};
     bool ring_lazy[2] = {false, false};
+    // the slot was filled by rh_push_deltas, which stores each delta's row code (tier << 28 | row, the
+    // host slot map's) in its slot field: the apply skips the device slot map (false: rh_deltas_acquire)
+    bool ring_resolved[2] = {false, false};
     int ring_next = 0;
     int ring_acquired = -1;
     int open = -1;                            // host slot open for rh_push_deltas (-1: none)
@@ -656,11 +659,11 @@ int ring_submit(rh_groups* g, int i, size_t n, bool has_set) {
             g->apply_gen = 0;
         }
         gen = ++g->apply_gen;
-        rc = rh_table_apply_deltas(g->dev, src, n, kApplyKeys, gen, lc, lw, s);
-        if (rc == RH_OK) rc = rh_table_apply_deltas(g->dev, src, n, kApplySet, gen, lc, lw, s);
+        rc = rh_table_apply_deltas(g->dev, src, n, kApplyKeys, gen, lc, lw, s, g->ring_resolved[i]);
+        if (rc == RH_OK) rc = rh_table_apply_deltas(g->dev, src, n, kApplySet, gen, lc, lw, s, g->ring_resolved[i]);
         if (rc != RH_OK) return rc;
     }
-    rc = rh_table_apply_deltas(g->dev, src, n, kApplyMax, gen, lc, lw, s);
+    rc = rh_table_apply_deltas(g->dev, src, n, kApplyMax, gen, lc, lw, s, g->ring_resolved[i]);
     if (rc != RH_OK) return rc;
     if (zc) {   // the host slot was read by the apply itself: freed by the next evaluation's event
         g->ring_lazy[i] = true;   // (the device slot was not read: ring_read[i] stays the last DMA apply's)
@@ -1125,17 +1128,27 @@ RH_EXPORT int rh_groups_load(rh_groups* g, uint32_t first, uint32_t n, uint32_t 
 // the cached copy saturated near 30 GB/s (scripts/push_probe.py).  The fence orders the streaming
 // stores before the staging lock is released (the submitter takes it exclusively before the H2D).
 static_assert(sizeof(rh_delta) == 16, "one 16-byte store per delta");
-static void stage_copy(rh_delta* dst, const rh_delta* src, size_t n) {
+// The deltas into the staging slot with each slot field replaced by its row code (`codes`, from the
+// validation against the host slot map).
+static void stage_copy(rh_delta* dst, const rh_delta* src, const uint32_t* codes, size_t n) {
 #if defined(__x86_64__)
     if (RH_PUSH_NT && (reinterpret_cast<uintptr_t>(dst) & 15) == 0) {
         __m128i* d = reinterpret_cast<__m128i*>(dst);
         const __m128i* s = reinterpret_cast<const __m128i*>(src);
-        for (size_t i = 0; i < n; ++i) _mm_stream_si128(d + i, _mm_loadu_si128(s + i));
+        for (size_t i = 0; i < n; ++i) {
+            __m128i v = _mm_loadu_si128(s + i);
+            v = _mm_insert_epi16(v, (int)(codes[i] & 0xFFFFu), 0);   // slot field: bytes 0..3
+            v = _mm_insert_epi16(v, (int)(codes[i] >> 16), 1);
+            _mm_stream_si128(d + i, v);
+        }
         _mm_sfence();
         return;
     }
 #endif
-    std::memcpy(dst, src, n * sizeof(rh_delta));
+    for (size_t i = 0; i < n; ++i) {
+        dst[i] = src[i];
+        dst[i].slot = codes[i];
+    }
 }
 
 // Multi-producer: each call validates its deltas and copies them into the open pinned slot at a range
@@ -1155,6 +1168,8 @@ RH_EXPORT int rh_push_deltas(rh_groups* g, const rh_delta* deltas, size_t n) {
     // runs per division (a reply's SET + MAXes): the slot map is read once per run
     bool any_set = false;
     size_t done = 0;
+    thread_local std::vector<uint32_t> codes;   // each delta's row code, as the check found it
+    if (codes.size() < n) codes.resize(n);
     auto validate = [&](size_t lo, size_t hi) -> int {
         uint32_t last = kNoRow, m = kNoRow, w = 0;
         constexpr size_t kAhead = 16;   // the slot map's lines requested ahead (random slots: ~L3 latency each)
@@ -1177,6 +1192,7 @@ RH_EXPORT int rh_push_deltas(rh_groups* g, const rh_delta* deltas, size_t n) {
                                                 " names a stopped slot, a column outside its tier or an unknown op" +
                                                 (done ? " (deltas [0, " + std::to_string(done) + ") were staged)" : ""));
             any_set |= d.op == RH_OP_SET;
+            codes[i] = m;
         }
         return RH_OK;
     };
@@ -1207,7 +1223,7 @@ RH_EXPORT int rh_push_deltas(rh_groups* g, const rh_delta* deltas, size_t n) {
                 } while (!g->fill.compare_exchange_weak(r, r + take, std::memory_order_relaxed));
                 if (take) {
                     if (any_set) g->staged_set.store(true, std::memory_order_relaxed);
-                    stage_copy(g->h_ring[g->open] + r, deltas + done, take);
+                    stage_copy(g->h_ring[g->open] + r, deltas + done, codes.data() + done, take);
                     done += take;
                     continue;
                 }
@@ -1237,6 +1253,7 @@ RH_EXPORT int rh_push_deltas(rh_groups* g, const rh_delta* deltas, size_t n) {
                 if (q != hipSuccess) return rh::hip_fail(q, "rh_push_deltas: staging slot");   // a device fault
             }
             g->open = i;
+            g->ring_resolved[i] = true;   // pushes store row codes
             g->fill.store(0, std::memory_order_relaxed);
         }
     }
@@ -1254,6 +1271,7 @@ RH_EXPORT int rh_deltas_acquire(rh_groups* g, rh_delta** out_buf, size_t* out_ca
     rc = ring_wait(g, i);
     if (rc != RH_OK) return rc;
     g->ring_acquired = i;
+    g->ring_resolved[i] = false;   // producers write slots, not row codes
     *out_buf = g->h_ring[i];
     *out_cap = RH_DELTA_SLOT;
     return RH_OK;

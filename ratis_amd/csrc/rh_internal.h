@@ -338,8 +338,9 @@ int rh_commit_launch_impl(rh_ctx* ctx, const rh_commit_soa* tiers, int n_tiers, 
 // SET (all of them when gen == 0: a batch without SETs).  gen: the batch generation (>= 1) of the
 // keys, 0 for a batch without SETs.
 enum ApplyPhase : int { kApplySet = 0, kApplyMax = 1, kApplyKeys = 2 };
+// resolved: the deltas' slot fields hold row codes (tier << 28 | row), resolved by rh_push_deltas.
 int rh_table_apply_deltas(const rh::TableDev& t, const rh_delta* d_deltas, uint64_t n, int phase, uint32_t gen,
-                          const rh::TableLists& lc, const rh::TableLists& lw, hipStream_t stream);
+                          const rh::TableLists& lc, const rh::TableLists& lw, hipStream_t stream, bool resolved);
 // List-mode evaluation of the listed rows of one kind (mode); COMMIT appends the rows whose commit
 // advanced to the watch list `lw` (when it is maintained).  Events as rh_table_commit.
 // t0 / t1 (may be null): timing events stamped at the evaluation's kernel boundaries.

@@ -99,8 +99,11 @@ __device__ __forceinline__ void list_append(const TableLists& l, bool want, int 
 // before them.  A batch without SETs (gen == 0) runs kApplyMax alone, unchecked.  Every delta of a
 // phase that applies (SET: kApplySet, MAX: kApplyMax) marks its row dirty -- the UPDATE_COMMIT event
 // of LSI:846-854 -- and with dirty-row lists (lc / lw .rows non-null) appends a row it newly marks.
+// resolved: the batch's slot fields already hold the row code (tier << 28 | row) the host's slot map
+// gave at push time (rh_push_deltas; the device map is that map in stream order) -- no slot-map trip.
 __global__ __launch_bounds__(256) void table_apply_kernel(TableDev Targ, const rh_delta* __restrict__ d, uint64_t n,
-                                                          int phase, uint32_t gen, TableLists lc, TableLists lw) {
+                                                          int phase, uint32_t gen, TableLists lc, TableLists lw,
+                                                          int resolved) {
     // the tier is picked per thread: index the argument in the kernarg segment (scalar loads), not
     // the by-value copy, which the compiler spilled whole into scratch (984 B per lane, 8x slower)
     const TableDev& T = rh::kernarg_struct<TableDev>();
@@ -115,8 +118,16 @@ __global__ __launch_bounds__(256) void table_apply_kernel(TableDev Targ, const r
         const rh_delta x = d[i];
         if (x.op != (phase == kApplyMax ? RH_OP_MAX : RH_OP_SET)) break;
         const TableTier* tt;
-        if (!locate(T, x.slot, tt, row)) break;  // stopped slot / out of range: ignored
-        t = (int)(T.slot_map[x.slot] >> 28);
+        if (resolved) {   // kernel argument: uniform
+            t = (int)(x.slot >> 28);
+            row = x.slot & rh::kRowMask;
+            if (t >= rh::kTableTiers) break;
+            tt = &T.tier[t];
+            if (row >= tt->rows) break;
+        } else {
+            if (!locate(T, x.slot, tt, row)) break;  // stopped slot / out of range: ignored
+            t = (int)(T.slot_map[x.slot] >> 28);
+        }
         uint32_t off = 0xFFFFFFFFu;
         bool commit_ev = false, watch_ev = false;
         const uint32_t c = x.column, F = tt->width;
@@ -1322,11 +1333,11 @@ __global__ __launch_bounds__(256) void table_read_kernel(TableDev Targ, uint32_t
 }  // namespace
 
 int rh_table_apply_deltas(const rh::TableDev& t, const rh_delta* d_deltas, uint64_t n, int phase, uint32_t gen,
-                          const rh::TableLists& lc, const rh::TableLists& lw, hipStream_t stream) {
+                          const rh::TableLists& lc, const rh::TableLists& lw, hipStream_t stream, bool resolved) {
     if (n == 0) return RH_OK;
     const uint64_t blocks = (n + 255) / 256;
     hipLaunchKernelGGL(table_apply_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream, t, d_deltas, n, phase, gen, lc,
-                       lw);
+                       lw, resolved ? 1 : 0);
     RH_HIP(hipGetLastError());
     return RH_OK;
 }
