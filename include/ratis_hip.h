@@ -288,9 +288,9 @@ int rh_commit_batch_wait(rh_groups* g, uint64_t ticket, rh_commit_out* out);
  * visible when the ticket completes.  AUTO (the default): an evaluation over every tile (up to one
  * record per row) runs without writing records at all -- it stores two event bits per row
  * (updateCommit: advanced, watch-ALL changed; commitIndexChanged: changed, valid) and a gather
- * kernel on a side stream rebuilds the records from the table's columns into the pinned buffers
- * while the table stream goes on (the ticket completes after the gather; no host-issued copy; the
- * table's next writers of those columns are ordered after it); an evaluation over the dirty-row
+ * kernel right behind it on the table's stream rebuilds the records from the table's columns into
+ * the pinned buffers (the ticket completes after the gather; no host-issued copy; the table's next
+ * writers of those columns come after it in stream order); an evaluation over the dirty-row
  * lists (at most capacity / 32 marked rows) writes its records into the pinned buffers directly.
  * DEVICE: as AUTO, except that a list evaluation writes event bits per listed row, rebuilt the same
  * way from the list entries.  Results are identical.  Not while

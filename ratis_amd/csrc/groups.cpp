@@ -276,6 +276,9 @@ void free_groups(rh_groups* g) {
 // Orders the table stream's next launch after the last updateCommit record gather (see `gathered`).
 // A gather of a list evaluation also reads that list's entries, which the next appends overwrite:
 // the delta apply (every kind) and an updateCommit list evaluation (the commitIndexChanged list).
+#ifndef RH_GATHER_SIDE   // A/B: a REGION gather on the side stream behind an event (1) or on the table stream (0)
+#define RH_GATHER_SIDE 0
+#endif
 #ifndef RH_GATHER_FENCE   // test-sensitivity builds only (0: no fence -- wrong results)
 #define RH_GATHER_FENCE 1
 #endif
@@ -1340,16 +1343,21 @@ int commit_issue(rh_groups* g, uint32_t flags, uint64_t tk, EvSet& e) {
     int rc = evaluate(g, RH_MODE_COMMIT, wall_on, t, e.d_cnt, e.h_cnt, &hbm, e.bdesc, &e.nblocks, &ed, &lr);
     if (rc != RH_OK) return rc;
     if (hbm && e.nblocks) {   // REGION mode (DEVICE and AUTO): the records rebuilt into the pinned lists
-        RH_HIP(hipEventRecord(g->evaluated, g->ctx->stream));
-        RH_HIP(hipStreamWaitEvent(g->d2h_stream, g->evaluated, 0));
-        rc = rh_table_gather_commit(ed, e.bdesc, e.nblocks, e.d_adv, wall_on ? e.d_wall : nullptr, e.d_cnt,
-                                    g->d2h_stream, lr, g->timing ? g->tev[4] : nullptr, g->timing ? g->tev[5] : nullptr);
+        hipStream_t gs = RH_GATHER_SIDE ? g->d2h_stream : g->ctx->stream;
+        if (RH_GATHER_SIDE) {
+            RH_HIP(hipEventRecord(g->evaluated, g->ctx->stream));
+            RH_HIP(hipStreamWaitEvent(gs, g->evaluated, 0));
+        }
+        rc = rh_table_gather_commit(ed, e.bdesc, e.nblocks, e.d_adv, wall_on ? e.d_wall : nullptr, e.d_cnt, gs, lr,
+                                    g->timing ? g->tev[4] : nullptr, g->timing ? g->tev[5] : nullptr);
         g->gathered_timed = g->timing;
         if (rc != RH_OK) return rc;
-        RH_HIP(hipEventRecord(e.done, g->d2h_stream));
-        RH_HIP(hipEventRecord(g->gathered, g->d2h_stream));
-        if (g->timing) RH_HIP(hipEventRecord(g->tev[3], g->d2h_stream));
-        g->gather_pending = true;
+        RH_HIP(hipEventRecord(e.done, gs));
+        if (RH_GATHER_SIDE) {
+            RH_HIP(hipEventRecord(g->gathered, gs));
+            g->gather_pending = true;
+        }
+        if (g->timing) RH_HIP(hipEventRecord(g->tev[3], gs));
         hbm = false;   // nothing left for _wait to copy
     } else if (hbm && g->event_sink == RH_EVENTS_AUTO) {   // contiguous HBM lists: drained on the side stream
         RH_HIP(hipEventRecord(g->evaluated, g->ctx->stream));
@@ -1446,17 +1454,22 @@ int watch_issue(rh_groups* g) {
     int rc = evaluate(g, RH_MODE_WATCH, false, t, g->d_wcnt, g->h_wcnt, &hbm, g->wbdesc, &g->wnblocks, &ed, &lr);
     if (rc != RH_OK) return rc;
     if (hbm && g->wnblocks) {   // REGION mode (DEVICE and AUTO): the records rebuilt into the pinned list
-        RH_HIP(hipEventRecord(g->evaluated, g->ctx->stream));
-        RH_HIP(hipStreamWaitEvent(g->d2h_stream, g->evaluated, 0));
-        rc = rh_table_gather_watch(ed, g->wbdesc, g->wnblocks, g->d_watch, g->d_wcnt, g->d2h_stream, lr,
+        hipStream_t gs = RH_GATHER_SIDE ? g->d2h_stream : g->ctx->stream;
+        if (RH_GATHER_SIDE) {
+            RH_HIP(hipEventRecord(g->evaluated, g->ctx->stream));
+            RH_HIP(hipStreamWaitEvent(gs, g->evaluated, 0));
+        }
+        rc = rh_table_gather_watch(ed, g->wbdesc, g->wnblocks, g->d_watch, g->d_wcnt, gs, lr,
                                    g->timing ? g->tev[4] : nullptr, g->timing ? g->tev[5] : nullptr);
         g->gathered_timed = g->timing;
         if (rc != RH_OK) return rc;
-        RH_HIP(hipEventRecord(g->wdone, g->d2h_stream));
-        RH_HIP(hipEventRecord(g->wgathered, g->d2h_stream));
-        if (g->timing) RH_HIP(hipEventRecord(g->tev[3], g->d2h_stream));
-        g->wgather_pending = true;
-        g->wgather_list = lr.rows != nullptr;
+        RH_HIP(hipEventRecord(g->wdone, gs));
+        if (RH_GATHER_SIDE) {
+            RH_HIP(hipEventRecord(g->wgathered, gs));
+            g->wgather_pending = true;
+            g->wgather_list = lr.rows != nullptr;
+        }
+        if (g->timing) RH_HIP(hipEventRecord(g->tev[3], gs));
         hbm = false;
     } else if (hbm && g->event_sink == RH_EVENTS_AUTO) {   // contiguous HBM list: drained on the side stream
         RH_HIP(hipEventRecord(g->evaluated, g->ctx->stream));
