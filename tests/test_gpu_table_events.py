@@ -387,12 +387,13 @@ def test_separate_done_word_of_large_tables(ctx, orc, monkeypatch):
 
 @pytest.mark.parametrize("sink", ["device", "auto"])
 def test_region_records_survive_later_writers(ctx, orc, sink):
-    """updateCommit in REGION mode writes no records: the gather rebuilds them on the side stream
+    """updateCommit in REGION mode writes no records: the gather rebuilds them behind the evaluation
     from the table's row-slot, commit and watch-ALL columns, and commitIndexChanged's from the
     row-slot and level columns (rh_internal.h, TableEvents), so every later writer of those columns
-    must wait for them (groups.cpp gather_fence / wgather_fence).  A commitIndexChanged
-    evaluation with ~half a million changed levels goes first, so its record gather holds the side
-    stream (~16 MB across PCIe) and the updateCommit gather queues behind it; meanwhile the host
+    must come after them (the table stream's order; with RH_GATHER_SIDE=1 the side stream's gathers
+    and groups.cpp gather_fence / wgather_fence).  A commitIndexChanged evaluation with ~half a
+    million changed levels goes first, so its record gather takes long (~16 MB across PCIe) and the
+    updateCommit gather queues behind it; meanwhile the host
     rewrites every column that gather reads -- COMMITTED deltas on the advanced rows, stops, restarts
     with other commits, reconfigurations into another tier -- and starts a second evaluation.  Both
     tickets' lists must be what their evaluations computed."""
