@@ -1172,6 +1172,12 @@ RH_EXPORT int rh_push_deltas(rh_groups* g, const rh_delta* deltas, size_t n) {
     bool any_set = false;
     size_t done = 0;
     thread_local std::vector<uint32_t> codes;   // each delta's row code, as the check found it
+    struct Trim {   // a thread keeps at most 1 MiB of codes between calls (one large push frees its own)
+        std::vector<uint32_t>& v;
+        ~Trim() {
+            if (v.capacity() > (1u << 18)) std::vector<uint32_t>().swap(v);
+        }
+    } trim{codes};
     if (codes.size() < n) codes.resize(n);
     auto validate = [&](size_t lo, size_t hi) -> int {
         uint32_t last = kNoRow, m = kNoRow, w = 0;
